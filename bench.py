@@ -1,0 +1,187 @@
+#!/usr/bin/env python
+"""Headline benchmark: whole-node docs/s of federated ProdLDA K=50, one client per GPU.
+
+BASELINE.json metric: "docs/sec (whole node) + NPMI, ProdLDA K=50 8-client fed on
+synthetic BoW".  Config (reference config/dft_params.cf defaults + the reference
+synthetic generator, src/utils/generate_synthetic.py): V=5000 generator vocabulary,
+K=50 topics, hidden (50, 50), softplus, dropout 0.2, Adam(lr 2e-3, betas (0.99, 0.99)),
+batch 64 per client, 1000 documents per client of 150-250 tokens, 5 frozen topics.
+
+One *step* = one federation round exactly as the reference defines it
+(federated_avitm.py:51-147 + server.py:436-521): every client does one local
+minibatch step (forward, backward, Adam) and the sample-weighted average of
+all shared tensors (the 20 AVITM state_dict tensors of grads_to_share) replaces
+every client's copy.  On MI355X: fused HIP step (hipGraph replay) + one RCCL
+all-reduce of the pre-scaled flat state over xGMI.
+
+Weak scaling: per-GPU work (one client, batch 64) is fixed as N grows.
+``value`` = N * 64 / round_time (all clients' training documents per second).
+Vocabulary consensus, init broadcast and the NPMI evaluation run outside the
+timed region.
+
+Launch: ``python bench.py`` (1 GPU) or
+``python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N``.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from gfedntm_amd.data.bow import BatchPlan, DeviceCSR  # noqa: E402
+from gfedntm_amd.data.synthetic import (generate_synthetic, node_vocabulary_terms,  # noqa: E402
+                                        remap_to_vocabulary)
+from gfedntm_amd.data.vocab import union_vocabulary, vocabulary_dict  # noqa: E402
+from gfedntm_amd.models import AVITM  # noqa: E402
+from gfedntm_amd.parallel.aggregator import CollectiveAggregator  # noqa: E402
+from gfedntm_amd.utils.config import DEFAULT_GRADS_TO_SHARE  # noqa: E402
+
+# Reference numbers (BASELINE.md part B, measured on the unmodified reference):
+# 8-client loopback gRPC federation with the built-in sleeps removed.
+BASELINE_FED_DOCS_PER_S = 111.0
+BASELINE_CPU_CENTRALIZED_DOCS_PER_S = 17300.0
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=2000)
+    p.add_argument("--warmup", type=int, default=200)
+    p.add_argument("--model", default="prodLDA", choices=["prodLDA", "LDA"])
+    p.add_argument("--vocab", type=int, default=5000)
+    p.add_argument("--topics", type=int, default=50)
+    p.add_argument("--hidden", default="50,50")
+    p.add_argument("--batch", type=int, default=64)
+    p.add_argument("--docs", type=int, default=1000)
+    p.add_argument("--backend", default="fused", choices=["fused", "torch"])
+    p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--no-npmi", action="store_true")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    device = torch.device("cuda", local_rank)
+    n_clients = world
+
+    # ---- data: reference synthetic generator, one node per client ----
+    corpus = generate_synthetic(vocab_size=args.vocab, n_topics=args.topics, n_docs=args.docs,
+                                n_nodes=max(n_clients, 1), frozen_topics=5, seed=args.seed)
+    # ---- stage 1: vocabulary consensus (sorted union of local vocabularies) ----
+    local_terms = node_vocabulary_terms(corpus, rank)
+    if world > 1:
+        gathered = [None] * world
+        dist.all_gather_object(gathered, local_terms)
+    else:
+        gathered = [local_terms]
+    terms = union_vocabulary(gathered)
+    vocab = vocabulary_dict(terms)
+    X = remap_to_vocabulary(corpus, rank, vocab)
+
+    hidden = tuple(int(h) for h in args.hidden.split(","))
+    torch.manual_seed(args.seed)
+    tm = AVITM(input_size=len(terms), n_components=args.topics, model_type=args.model,
+               hidden_sizes=hidden, batch_size=args.batch, verbose=False, backend=args.backend,
+               device=device, shared_keys=DEFAULT_GRADS_TO_SHARE, seed=args.seed)
+    eng = tm.engine
+    agg = None
+    if world > 1:
+        dist.broadcast(tm.flat.buffer, src=0)        # identical W0 on every client
+        agg = CollectiveAggregator()
+        w = agg.weights(X.shape[0], device)
+        if args.backend == "fused":
+            eng.set_fedavg_scale(w[rank])
+    data = DeviceCSR(X, device)
+    n_steps = args.warmup + args.steps
+    plan = BatchPlan.build(data.n_docs, args.batch, n_steps, seed=args.seed + rank)
+    eng.bind_data(data, plan)
+    if args.backend == "fused" and not args.no_graph:
+        eng.enable_graph(True)
+
+    shared = tm.flat.shared
+
+    def round_(s):
+        eng.step(s)
+        if agg is not None:
+            if args.backend != "fused":
+                shared.mul_(w[rank])
+            agg.allreduce_(shared)
+
+    for s in range(args.warmup):
+        round_(s)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for s in range(args.warmup, n_steps):
+        round_(s)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ms = dt / args.steps * 1e3
+    docs_per_s = n_clients * args.batch * args.steps / dt
+    losses = eng.loss_hist.detach().cpu().numpy()
+
+    npmi = None
+    if rank == 0 and not args.no_npmi:
+        from gfedntm_amd.eval.metrics import npmi_coherence
+        from gfedntm_amd.data.synthetic import remap_to_vocabulary as remap
+        import scipy.sparse as sp
+        ref_corpus = sp.vstack([remap(corpus, i, vocab) for i in range(max(n_clients, 1))])
+        topics_idx = torch.topk(tm.model.beta.detach(), 10, dim=1).indices.cpu().numpy()
+        npmi = float(npmi_coherence(topics_idx, ref_corpus, device=device))
+
+    if rank == 0:
+        out = {
+            "metric": "docs/sec (whole node) + NPMI, ProdLDA K=50 8-client fed on synthetic BoW",
+            "value": round(docs_per_s, 1),
+            "unit": "docs/s",
+            "n_gpus": n_clients,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(docs_per_s / BASELINE_FED_DOCS_PER_S, 2),
+            "dtype": "fp32",
+            "data": "synthetic (reference LDA generator: V=5000, K=50, 1000 docs/client, "
+                    "150-250 tokens, 5 frozen topics), random init",
+            "config": {"model": f"{args.model} K={args.topics} H={hidden} V={len(terms)}",
+                       "global_batch": args.batch * n_clients, "seq_len": None,
+                       "per_client_batch": args.batch, "clients": n_clients,
+                       "parallelism": f"fedavg-dp{n_clients}",
+                       "backend": args.backend + ("" if args.no_graph else "+hipgraph"),
+                       "aggregation": "per-minibatch sample-weighted FedAvg of 20 shared tensors"
+                                      + (" (RCCL all-reduce)" if world > 1 else "")},
+            "npmi": None if npmi is None else round(npmi, 4),
+            "final_loss": float(np.mean(losses[-20:])),
+            "baseline": {"fed_grpc_8clients_docs_per_s": BASELINE_FED_DOCS_PER_S,
+                         "cpu_centralized_docs_per_s": BASELINE_CPU_CENTRALIZED_DOCS_PER_S},
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,311 @@
+// gfedntm_amd -- common device helpers and the C ABI of the fused NTM step.
+//
+// Target: gfx950 (MI355X, CDNA4), wave64.  Everything here is written for
+// 64-lane wavefronts: row reductions use __shfl_xor over 64 lanes, block sizes
+// are multiples of 64, and kernels that own one document use one workgroup of
+// 4 waves (256 threads).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define GFK_MAX_LAYERS 8
+#define GFK_MAX_SEGS 32
+#define GFK_WAVE 64
+
+// ---------------------------------------------------------------------------
+// C ABI (mirrored by gfedntm_amd/ops/kernel_abi.py -- keep field order in sync)
+// ---------------------------------------------------------------------------
+extern "C" {
+
+// Activation codes (reference inference_network.py:45-60; rrelu is not fused).
+enum GfkAct { GFK_SOFTPLUS = 0, GFK_RELU = 1, GFK_SIGMOID = 2, GFK_TANH = 3,
+              GFK_LEAKYRELU = 4, GFK_ELU = 5, GFK_SELU = 6 };
+
+enum GfkModelKind { GFK_PRODLDA = 0, GFK_LDA = 1 };
+
+// Encoder input kinds: BoW only (AVITM), BoW + adapted contextual (CombinedTM),
+// contextual only (ZeroShotTM).
+enum GfkInput { GFK_IN_BOW = 0, GFK_IN_COMBINED = 1, GFK_IN_CONTEXTUAL = 2 };
+
+typedef struct GfkModel {
+  // ---- dimensions ----
+  int32_t bmax;          // max rows per minibatch (grid size of per-row kernels)
+  int32_t V, K;          // vocabulary, topics
+  int32_t n_hidden;      // len(hidden_sizes)
+  int32_t H[GFK_MAX_LAYERS];
+  int32_t act;           // GfkAct
+  int32_t kind;          // GfkModelKind
+  int32_t input;         // GfkInput
+  int32_t C;             // contextual size (CTM)
+  int32_t L;             // label size (CTM)
+  int32_t vb;            // decoder vocab-tile width
+  int32_t n_tiles;       // ceil(V / vb)
+  int32_t dec_grid;      // workgroups of the vocab-tiled decoder kernels
+  int32_t learn_priors;
+  int32_t stage_flags;   // bit0: encoder weights fit in LDS, bit1: posterior-bwd stash fits in LDS
+  float drop_enc, drop_theta;
+  float bn_momentum, bn_eps;
+  float kl_weight;       // CTM loss_weights["beta"], 1 for AVITM
+  float pad1;
+  uint64_t seed;
+
+  // ---- parameters (views into the flat fp32 buffer) and their gradients ----
+  float *prior_mean, *prior_var, *beta;
+  float *w_in;           // input_layer.weight stored TRANSPOSED: [n_in, H0]
+  float *b_in;
+  float *w_h[GFK_MAX_LAYERS], *b_h[GFK_MAX_LAYERS];   // hidden l: [H[l+1], H[l]]
+  float *w_mu, *b_mu, *w_s, *b_s;                      // [K, H_last]
+  float *mu_rm, *mu_rv, *s_rm, *s_rv, *beta_rm, *beta_rv;
+  int64_t *nbt_mu, *nbt_s, *nbt_beta;                  // num_batches_tracked
+  float *g_prior_mean, *g_prior_var, *g_beta, *g_w_in, *g_b_in;
+  float *g_w_h[GFK_MAX_LAYERS], *g_b_h[GFK_MAX_LAYERS];
+  float *g_w_mu, *g_b_mu, *g_w_s, *g_b_s;
+
+  // ---- data (device-resident CSR shard + batch plan) ----
+  const int32_t *indptr, *indices;
+  const float *values;
+  const float *ctx;      // [D, C] contextual embeddings (CTM) or null
+  const int32_t *plan_order, *plan_start, *plan_size;
+  int32_t *step;         // device step counter (index into the plan)
+  int32_t *adam_t;       // device Adam step count
+  float *loss_hist;      // [n_steps]
+
+  // ---- workspace (fp32 unless noted) ----
+  int32_t *ws_doc;       // [bmax] doc ids of the current batch
+  int32_t *ws_nb;        // [1]    rows of the current batch
+  float *ws_z[GFK_MAX_LAYERS];   // pre-activations per layer [bmax, H[l]]
+  float *ws_a[GFK_MAX_LAYERS];   // activations act(z) per layer [bmax, H[l]]
+  float *ws_hd;          // dropped-out last hidden [bmax, H_last]
+  float *ws_mask_h;      // encoder dropout scale   [bmax, H_last]
+  float *ws_mu_raw, *ws_ls_raw;  // [bmax, K] pre-BN heads
+  float *ws_mu, *ws_ls;          // [bmax, K] post-BN
+  float *ws_bn_rstd;             // [2K] rstd of the mu / log-sigma BN
+  float *ws_eps;                 // [bmax, K]
+  float *ws_theta, *ws_thetad, *ws_mask_t;   // [bmax, K]
+  float *ws_kl, *ws_rl, *ws_lse, *ws_s;      // [bmax]
+  float *ws_zn;                  // [bmax, V] BN'ed logits (ProdLDA) / BN'ed beta^T [V, K] (LDA)
+  float *ws_col_rstd;            // [V] (ProdLDA: over batch; LDA: over topics)
+  float *ws_row_part;            // [dec_grid, max(bmax,K), 2] online (max, sumexp) partials
+  float *ws_dthetad;             // [bmax, K] accumulated by the decoder backward (atomics)
+  float *ws_dz0;                 // [bmax, H0]
+  float *ws_dmu, *ws_dls;        // [bmax, K] dL/d(post-BN mu, log-sigma)
+  float *ws_colpart;             // [bmax/4, 9, K] per-workgroup column sums (posterior bwd)
+  float *ws_dbsm;                // LDA: d softmax(beta)^T accumulator [V, K]
+  float *ws_ck;                  // LDA: [K] sum_v beta_sm * d beta_sm
+  float *ws_hctx;                // CTM: dense contextual contribution to layer 0 [bmax, H0]
+  int32_t *ws_tstart;            // [bmax, n_tiles+1] CSR position of each row's first nz per vocab tile
+  uint64_t *dbg;                 // diagnostic s_memtime stamps (GFK_STAMPS builds only)
+} GfkModel;
+
+typedef struct GfkAdam {
+  float *p, *g, *m, *v;
+  int32_t n_seg;
+  int32_t pad;
+  int64_t seg_start[GFK_MAX_SEGS];   // in floats, multiples of 4
+  int64_t seg_end[GFK_MAX_SEGS];
+  int32_t seg_flags[GFK_MAX_SEGS];   // bit0: Adam update, bit1: FedAvg pre-scale
+  float lr, beta1, beta2, eps, weight_decay, scale;
+  const int32_t *t;                  // device Adam step count (already incremented)
+} GfkAdam;
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Device helpers
+// ---------------------------------------------------------------------------
+namespace gfk {
+
+// In-kernel phase timestamps for diagnostic builds (-DGFK_STAMPS): lane 0 of
+// workgroup 0 writes s_memtime into dbg[slot].  Compiled out otherwise.
+#ifdef GFK_STAMPS
+#define GFK_STAMP(m, slot)                                                        \
+  do {                                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                            \
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (m).dbg)                           \
+      (m).dbg[slot] = __builtin_amdgcn_s_memtime();                               \
+    __builtin_amdgcn_sched_barrier(0);                                            \
+  } while (0)
+#else
+#define GFK_STAMP(m, slot) do { } while (0)
+#endif
+
+// Philox4x32-10 counter-based RNG: stateless, so every kernel (and every graph
+// replay) derives its random numbers from (seed, step, stream, element).
+__device__ __forceinline__ uint4 philox(uint32_t k0, uint32_t k1, uint4 c) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+    c = make_uint4((uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1,
+                   (uint32_t)(p0 >> 32) ^ c.w ^ k1, (uint32_t)p0);
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// Stream tags keep the draws of different random tensors independent.
+enum : uint32_t { RNG_EPS = 1, RNG_DROP_ENC = 2, RNG_DROP_THETA = 3, RNG_INFER = 4 };
+
+__device__ __forceinline__ uint4 rng4(uint64_t seed, uint32_t step, uint32_t tag, uint32_t idx) {
+  return philox((uint32_t)seed, (uint32_t)(seed >> 32), make_uint4(idx, step, tag, 0x5eedu));
+}
+
+__device__ __forceinline__ float u01(uint32_t x) {        // [0, 1)
+  return (float)(x >> 8) * (1.0f / 16777216.0f);
+}
+
+__device__ __forceinline__ float randn(uint64_t seed, uint32_t step, uint32_t tag, uint32_t idx) {
+  const uint4 r = rng4(seed, step, tag, idx);
+  const float u1 = ((float)(r.x >> 8) + 1.0f) * (1.0f / 16777216.0f);   // (0, 1]
+  const float u2 = u01(r.y);
+  return sqrtf(-2.0f * logf(u1)) * cospif(2.0f * u2);
+}
+
+// Inverted-dropout scale: 0 with probability p, 1/(1-p) otherwise (torch semantics).
+__device__ __forceinline__ float drop_scale(uint64_t seed, uint32_t step, uint32_t tag,
+                                            uint32_t idx, float p) {
+  if (p <= 0.f) return 1.f;
+  if (p >= 1.f) return 0.f;
+  return u01(rng4(seed, step, tag, idx).x) >= p ? 1.f / (1.f - p) : 0.f;
+}
+
+__device__ __forceinline__ float act_f(int a, float z) {
+  switch (a) {
+    case GFK_SOFTPLUS: return z > 20.f ? z : log1pf(expf(z));
+    case GFK_RELU: return z > 0.f ? z : 0.f;
+    case GFK_SIGMOID: return 1.f / (1.f + expf(-z));
+    case GFK_TANH: return tanhf(z);
+    case GFK_LEAKYRELU: return z > 0.f ? z : 0.01f * z;
+    case GFK_ELU: return z > 0.f ? z : expm1f(z);
+    default: {  // SELU
+      const float s = 1.0507009873554804934f, al = 1.6732632423543772848f;
+      return z > 0.f ? s * z : s * al * expm1f(z);
+    }
+  }
+}
+
+// d act / d z evaluated at the pre-activation z.
+__device__ __forceinline__ float act_d(int a, float z) {
+  switch (a) {
+    case GFK_SOFTPLUS: return z > 20.f ? 1.f : 1.f / (1.f + expf(-z));
+    case GFK_RELU: return z > 0.f ? 1.f : 0.f;
+    case GFK_SIGMOID: { const float s = 1.f / (1.f + expf(-z)); return s * (1.f - s); }
+    case GFK_TANH: { const float t = tanhf(z); return 1.f - t * t; }
+    case GFK_LEAKYRELU: return z > 0.f ? 1.f : 0.01f;
+    case GFK_ELU: return z > 0.f ? 1.f : expf(z);
+    default: {
+      const float s = 1.0507009873554804934f, al = 1.6732632423543772848f;
+      return z > 0.f ? s : s * al * expf(z);
+    }
+  }
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Combine two online-softmax partials (m, s): s = sum exp(x - m).
+__device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2) {
+  if (m2 == -INFINITY) return;
+  if (m == -INFINITY) { m = m2; s = s2; return; }
+  const float mn = fmaxf(m, m2);
+  s = s * __expf(m - mn) + s2 * __expf(m2 - mn);
+  m = mn;
+}
+
+__device__ __forceinline__ void wave_lse(float& m, float& s) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);
+    lse_merge(m, s, m2, s2);
+  }
+}
+
+__device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+// global -> LDS copy of n floats with U independent loads in flight per thread
+// (indices are clamped, never predicated, so hipcc keeps the loads back to back).
+template <int U>
+__device__ __forceinline__ void stage_lin(float* __restrict__ dst, const float* __restrict__ src,
+                                          int n, int tid, int nt) {
+  if (n <= 0) return;
+  for (int base = tid; base < n; base += U * nt) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = src[min(base + u * nt, n - 1)];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (base + u * nt < n) dst[base + u * nt] = v[u];
+  }
+}
+
+// Asynchronous global -> LDS copy (LDS-DMA, global_load_lds_dwordx4): every lane
+// moves one 16-byte chunk straight into LDS, no VGPR round trip, so a whole
+// staging phase is issued back to back and drained by ONE barrier.  Copies
+// ceil(n/4) chunks: src and dst must be 16-byte aligned and the source must be
+// readable up to the next multiple of 4 floats.  The LDS destination of a wave
+// instruction is its wave-uniform base + lane*16, so each wave copies 64
+// consecutive chunks.
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+typedef const __attribute__((address_space(1))) void* gbl_void_ptr;
+
+__device__ __forceinline__ void glds_copy(float* dst, const float* src, int n, int tid, int nt) {
+  const int nchunk = (n + 3) >> 2;
+  const int lane = tid & 63, w = tid >> 6, nw = nt >> 6;
+  for (int c0 = w * 64; c0 < nchunk; c0 += nw * 64)
+    if (c0 + lane < nchunk)
+      __builtin_amdgcn_global_load_lds((gbl_void_ptr)(src + 4 * (c0 + lane)),
+                                       (lds_void_ptr)(dst + 4 * c0), 16, 0, 0);
+}
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// 16x16x4 fp32 MFMA: lane l supplies A[l&15][l>>4] and B[l>>4][l&15];
+// the result holds C[(l>>4)*4 + r][l&15] in element r.
+__device__ __forceinline__ f32x4 mfma16x16x4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// A strided, bounds-checked matrix view (LDS or global).  Out-of-range elements
+// read as 0 through a clamped address + select, so no load is predicated.
+struct MatView {
+  const float* p;
+  int si, sj, rows, cols;
+  __device__ __forceinline__ float at(int i, int j) const {
+    const float v = p[(size_t)min(i, rows - 1) * si + (size_t)min(j, cols - 1) * sj];
+    return (i < rows && j < cols) ? v : 0.f;
+  }
+};
+
+// C[M x N] = A[M x R] @ B[R x N] on the fp32 matrix cores; 16x16 output tiles are
+// dealt round-robin to the workgroup's waves; store(i, j, value) is called for
+// every element with i < M, j < N.
+template <class Store>
+__device__ __forceinline__ void mfma_gemm(int M, int N, int R, const MatView& A, const MatView& B,
+                                          int wave, int nwaves, Store store) {
+  const int lane = threadIdx.x & 63;
+  const int mt = (M + 15) >> 4, nt = (N + 15) >> 4;
+  for (int s = wave; s < mt * nt; s += nwaves) {
+    const int i0 = (s / nt) * 16, j0 = (s % nt) * 16;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int ai = i0 + (lane & 15), bj = j0 + (lane & 15), kk = lane >> 4;
+    for (int k0 = 0; k0 < R; k0 += 4) acc = mfma16x16x4(A.at(ai, k0 + kk), B.at(k0 + kk, bj), acc);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = i0 + (lane >> 4) * 4 + r;
+      if (i < M && bj < N) store(i, bj, acc[r]);
+    }
+  }
+}
+
+}  // namespace gfk

@@ -1,0 +1,119 @@
+// Host-side launcher of the fused local step.
+//
+// The Python engine passes one GfkModel (dims + raw device pointers) and one
+// GfkAdam descriptor, and a list of phase ids; every kernel of the step is
+// launched from here on the caller's HIP stream, so a whole minibatch step is
+// a single ctypes call (eager mode) or a single hipGraph replay (graph mode,
+// captured around this call).  No allocation, no synchronisation: the call is
+// capture-safe.
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "gfk_common.h"
+
+extern "C" {
+int gfk_launch_encoder_fwd(const GfkModel*, hipStream_t);
+int gfk_launch_encoder_bwd(const GfkModel*, hipStream_t);
+int gfk_launch_batch_docs(const GfkModel*, hipStream_t);
+int gfk_launch_posterior_fwd(const GfkModel*, hipStream_t);
+int gfk_launch_posterior_bwd(const GfkModel*, hipStream_t);
+int gfk_launch_prodlda_fwd(const GfkModel*, hipStream_t);
+int gfk_launch_prodlda_bwd(const GfkModel*, hipStream_t);
+int gfk_launch_prodlda_row_loss(const GfkModel*, hipStream_t);
+int gfk_launch_lda_beta_fwd(const GfkModel*, hipStream_t);
+int gfk_launch_lda_row(const GfkModel*, hipStream_t);
+int gfk_launch_lda_beta_bwd(const GfkModel*, hipStream_t);
+int gfk_launch_adam(const GfkAdam*, int, hipStream_t);
+int gfk_launch_scale(float*, int64_t, float, hipStream_t);
+size_t gfk_prodlda_fwd_smem(int, int);
+size_t gfk_prodlda_bwd_smem(int, int);
+size_t gfk_lda_fwd_smem(int);
+size_t gfk_lda_bwd_smem(int);
+size_t gfk_posterior_bwd_smem(const GfkModel*);
+size_t gfk_posterior_fwd_smem(const GfkModel*);
+size_t gfk_mlp_weight_bytes(const GfkModel*);
+size_t gfk_encoder_fwd_smem(const GfkModel*);
+int gfk_encoder_set_smem(size_t);
+int gfk_prodlda_set_smem(size_t);
+int gfk_lda_set_smem(size_t);
+int gfk_posterior_set_smem(size_t);
+
+// Phase ids (mirrored in gfedntm_amd/ops/kernel_abi.py).
+enum GfkPhase {
+  GFK_PH_BATCH_DOCS = 0,
+  GFK_PH_ENC_FWD = 1,
+  GFK_PH_POST_FWD = 2,
+  GFK_PH_PRODLDA_FWD = 3,
+  GFK_PH_PRODLDA_LOSS = 4,
+  GFK_PH_PRODLDA_BWD = 5,
+  GFK_PH_LDA_BETA_FWD = 6,
+  GFK_PH_LDA_ROW = 7,
+  GFK_PH_POST_BWD = 8,
+  GFK_PH_LDA_BETA_BWD = 9,
+  GFK_PH_ENC_BWD = 10,
+  GFK_PH_ADAM = 11,
+};
+
+
+
+// LDS each kernel family needs for this model; 0 means "does not fit".
+size_t gfk_smem_required(const GfkModel* m, int which) {
+  switch (which) {
+    case 0: return gfk_prodlda_fwd_smem(m->bmax, m->K);
+    case 1: return gfk_prodlda_bwd_smem(m->bmax, m->K);
+    case 2: return gfk_lda_fwd_smem(m->K);
+    case 3: return gfk_lda_bwd_smem(m->K);
+    case 4: return gfk_posterior_bwd_smem(m);
+    case 5: return gfk_posterior_fwd_smem(m);
+    case 6: return gfk_mlp_weight_bytes(m);
+    case 7: return gfk_encoder_fwd_smem(m);
+    default: return 0;
+  }
+}
+
+// One-time per model shape: raise the dynamic-LDS limit of the kernels that use
+// more than the 64 KiB default (MI355X has 160 KiB per CU).
+int gfk_setup(const GfkModel* m) {
+  int e = 0;
+  size_t p = gfk_prodlda_fwd_smem(m->bmax, m->K), q = gfk_prodlda_bwd_smem(m->bmax, m->K);
+  if ((e = gfk_prodlda_set_smem(p > q ? p : q))) return e;
+  p = gfk_lda_fwd_smem(m->K);
+  q = gfk_lda_bwd_smem(m->K);
+  if ((e = gfk_lda_set_smem(p > q ? p : q))) return e;
+  if ((e = gfk_encoder_set_smem(gfk_encoder_fwd_smem(m)))) return e;
+  p = gfk_posterior_fwd_smem(m);
+  q = gfk_posterior_bwd_smem(m);
+  return gfk_posterior_set_smem(p > q ? p : q);
+}
+
+int gfk_run(const GfkModel* m, const GfkAdam* a, int adam_grid, hipStream_t s,
+            const int32_t* phases, int n_phases) {
+  for (int i = 0; i < n_phases; ++i) {
+    int e = 0;
+    switch (phases[i]) {
+      case GFK_PH_BATCH_DOCS: e = gfk_launch_batch_docs(m, s); break;
+      case GFK_PH_ENC_FWD: e = gfk_launch_encoder_fwd(m, s); break;
+      case GFK_PH_POST_FWD: e = gfk_launch_posterior_fwd(m, s); break;
+      case GFK_PH_PRODLDA_FWD: e = gfk_launch_prodlda_fwd(m, s); break;
+      case GFK_PH_PRODLDA_LOSS: e = gfk_launch_prodlda_row_loss(m, s); break;
+      case GFK_PH_PRODLDA_BWD: e = gfk_launch_prodlda_bwd(m, s); break;
+      case GFK_PH_LDA_BETA_FWD: e = gfk_launch_lda_beta_fwd(m, s); break;
+      case GFK_PH_LDA_ROW: e = gfk_launch_lda_row(m, s); break;
+      case GFK_PH_POST_BWD: e = gfk_launch_posterior_bwd(m, s); break;
+      case GFK_PH_LDA_BETA_BWD: e = gfk_launch_lda_beta_bwd(m, s); break;
+      case GFK_PH_ENC_BWD: e = gfk_launch_encoder_bwd(m, s); break;
+      case GFK_PH_ADAM: e = gfk_launch_adam(a, adam_grid, s); break;
+      default: e = -2;
+    }
+    if (e) return e * 100 + phases[i];
+  }
+  return 0;
+}
+
+int gfk_scale(float* p, int64_t n, float sc, hipStream_t s) { return gfk_launch_scale(p, n, sc, s); }
+
+size_t gfk_model_struct_size() { return sizeof(GfkModel); }
+size_t gfk_adam_struct_size() { return sizeof(GfkAdam); }
+
+}  // extern "C"

@@ -1,0 +1,120 @@
+"""Local-step engines.
+
+An engine owns one client's model state (flat buffer + optimizer state) and
+runs *one local minibatch step* = zero_grad -> forward -> loss -> backward ->
+optimizer step (reference federated_avitm.py:51-83, federated_ctm.py:50-114).
+
+* :class:`TorchEngine` -- stock PyTorch ops; the numerical oracle and the CPU
+  path (tests, gloo federation, any solver / activation / model variant).
+* :class:`gfedntm_amd.ops.engine.FusedEngine` -- hand-written CDNA4 HIP
+  kernels + fused multi-tensor Adam + hipGraph replay (MI355X training path).
+
+Both read minibatches from a device-resident CSR shard through a
+:class:`~gfedntm_amd.data.bow.BatchPlan`, and both record the loss of step s
+into ``loss_hist[s]`` on device, so the host only synchronizes when it logs.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+import torch
+from torch import optim
+
+from ..data.bow import BatchPlan, DeviceCSR
+from ..utils.flat import FlatState
+from .networks import kl_terms, reconstruction_terms
+
+
+def make_optimizer(params, solver: str, lr: float, momentum: float):
+    """Reference optimizer table (avitm.py:141-153, ctm.py:158-168)."""
+    if solver == "adam":
+        return optim.Adam(params, lr=lr, betas=(momentum, 0.99))
+    if solver == "sgd":
+        return optim.SGD(params, lr=lr, momentum=momentum)
+    if solver == "adagrad":
+        return optim.Adagrad(params, lr=lr)
+    if solver == "adadelta":
+        return optim.Adadelta(params, lr=lr)
+    if solver == "rmsprop":
+        return optim.RMSprop(params, lr=lr, momentum=momentum)
+    raise ValueError("solver must be 'adam', 'adadelta', 'sgd', 'rmsprop' or 'adagrad'")
+
+
+class EngineBase:
+    kind = "avitm"   # or "ctm"
+
+    def __init__(self, model, flat: FlatState, loss_weight_beta: float = 1.0):
+        self.model = model
+        self.flat = flat
+        self.beta_weight = float(loss_weight_beta)
+        self.data: Optional[DeviceCSR] = None
+        self.plan: Optional[BatchPlan] = None
+        self.loss_hist: Optional[torch.Tensor] = None
+        self.kl_hist: Optional[torch.Tensor] = None
+
+    @property
+    def device(self):
+        return self.flat.buffer.device
+
+    def bind_data(self, data: DeviceCSR, plan: BatchPlan):
+        self.data, self.plan = data, plan
+        self.loss_hist = torch.zeros(plan.n_steps, dtype=torch.float32, device=self.device)
+
+    def step(self, s: int) -> torch.Tensor:
+        raise NotImplementedError
+
+    def optimizer_state_dict(self):
+        return self.optimizer.state_dict()
+
+    def load_optimizer_state_dict(self, sd):
+        self.optimizer.load_state_dict(sd)
+
+    # the part of the state that is averaged every round
+    @property
+    def shared(self) -> torch.Tensor:
+        return self.flat.shared
+
+
+class TorchEngine(EngineBase):
+    """Reference-exact local step on stock PyTorch ops."""
+
+    def __init__(self, model, flat: FlatState, solver="adam", lr=2e-3, momentum=0.99,
+                 reduce_on_plateau=False, loss_weight_beta: float = 1.0, kind: str = "avitm"):
+        super().__init__(model, flat, loss_weight_beta)
+        self.kind = kind
+        self.optimizer = make_optimizer(model.parameters(), solver, lr, momentum)
+        self.scheduler = (optim.lr_scheduler.ReduceLROnPlateau(self.optimizer, patience=10)
+                          if reduce_on_plateau else None)
+
+    def _batch(self, s: int):
+        ids = torch.from_numpy(self.plan.batch(s).astype(np.int64)).to(self.device)
+        x = self.data.dense_rows(ids)
+        ctx = self.data.contextual[ids] if self.data.contextual is not None else None
+        lab = self.data.labels[ids] if self.data.labels is not None else None
+        return x, ctx, lab
+
+    def loss_on(self, x, ctx=None, labels=None):
+        """Forward + loss of one minibatch (reference avitm.py:168-229 / ctm.py:182-296)."""
+        m = self.model
+        if self.kind == "ctm":
+            pm, pv, mu, var, logvar, wd, est = m(x, ctx, labels)
+        else:
+            pm, pv, mu, var, logvar, wd = m(x)
+            est = None
+        kl = kl_terms(pm, pv, mu, var, logvar, m.n_components)
+        rl = reconstruction_terms(x, wd)
+        loss = (self.beta_weight * kl + rl).sum()
+        if labels is not None and est is not None:
+            loss = loss + torch.nn.functional.cross_entropy(est, torch.argmax(labels, 1))
+        return loss
+
+    def step(self, s: int) -> torch.Tensor:
+        self.model.train()
+        x, ctx, lab = self._batch(s)
+        self.model.zero_grad()
+        loss = self.loss_on(x, ctx, lab)
+        loss.backward()
+        self.optimizer.step()
+        self.loss_hist[s] = loss.detach()
+        return loss.detach()

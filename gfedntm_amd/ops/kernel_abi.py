@@ -1,0 +1,120 @@
+"""ctypes mirror of the C ABI in csrc/gfk_common.h and csrc/step.cpp.
+
+Field order and types MUST match the C structs; :func:`declare` checks the
+struct sizes against the library's own ``sizeof`` at load time.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+MAX_LAYERS = 8
+MAX_SEGS = 32
+P = C.c_void_p
+
+# activation / model / input codes
+ACT_CODES = {"softplus": 0, "relu": 1, "sigmoid": 2, "tanh": 3, "leakyrelu": 4, "elu": 5,
+             "selu": 6}
+KIND_PRODLDA, KIND_LDA = 0, 1
+IN_BOW, IN_COMBINED, IN_CONTEXTUAL = 0, 1, 2
+
+# phase ids (csrc/step.cpp GfkPhase)
+PH_BATCH_DOCS = 0
+PH_ENC_FWD = 1
+PH_POST_FWD = 2
+PH_PRODLDA_FWD = 3
+PH_PRODLDA_LOSS = 4
+PH_PRODLDA_BWD = 5
+PH_LDA_BETA_FWD = 6
+PH_LDA_ROW = 7
+PH_POST_BWD = 8
+PH_LDA_BETA_BWD = 9
+PH_ENC_BWD = 10
+PH_ADAM = 11
+
+# PH_POST_BWD = posterior_bwd_rows + posterior_bwd_mlp (which also scatters the
+# sparse input-layer gradient, so PH_ENC_BWD is not part of the fused step)
+PRODLDA_STEP = [PH_ENC_FWD, PH_POST_FWD, PH_PRODLDA_FWD, PH_PRODLDA_LOSS, PH_PRODLDA_BWD,
+                PH_POST_BWD, PH_ADAM]
+LDA_STEP = [PH_LDA_BETA_FWD, PH_ENC_FWD, PH_POST_FWD, PH_LDA_ROW, PH_POST_BWD, PH_LDA_BETA_BWD,
+            PH_ADAM]
+
+SEG_ADAM, SEG_SCALE = 1, 2
+
+
+class GfkModel(C.Structure):
+    _fields_ = [
+        ("bmax", C.c_int32), ("V", C.c_int32), ("K", C.c_int32), ("n_hidden", C.c_int32),
+        ("H", C.c_int32 * MAX_LAYERS),
+        ("act", C.c_int32), ("kind", C.c_int32), ("input", C.c_int32), ("C", C.c_int32),
+        ("L", C.c_int32), ("vb", C.c_int32), ("n_tiles", C.c_int32), ("dec_grid", C.c_int32),
+        ("learn_priors", C.c_int32), ("stage_flags", C.c_int32),
+        ("drop_enc", C.c_float), ("drop_theta", C.c_float), ("bn_momentum", C.c_float),
+        ("bn_eps", C.c_float), ("kl_weight", C.c_float), ("pad1", C.c_float),
+        ("seed", C.c_uint64),
+        ("prior_mean", P), ("prior_var", P), ("beta", P), ("w_in", P), ("b_in", P),
+        ("w_h", P * MAX_LAYERS), ("b_h", P * MAX_LAYERS),
+        ("w_mu", P), ("b_mu", P), ("w_s", P), ("b_s", P),
+        ("mu_rm", P), ("mu_rv", P), ("s_rm", P), ("s_rv", P), ("beta_rm", P), ("beta_rv", P),
+        ("nbt_mu", P), ("nbt_s", P), ("nbt_beta", P),
+        ("g_prior_mean", P), ("g_prior_var", P), ("g_beta", P), ("g_w_in", P), ("g_b_in", P),
+        ("g_w_h", P * MAX_LAYERS), ("g_b_h", P * MAX_LAYERS),
+        ("g_w_mu", P), ("g_b_mu", P), ("g_w_s", P), ("g_b_s", P),
+        ("indptr", P), ("indices", P), ("values", P), ("ctx", P),
+        ("plan_order", P), ("plan_start", P), ("plan_size", P),
+        ("step", P), ("adam_t", P), ("loss_hist", P),
+        ("ws_doc", P), ("ws_nb", P), ("ws_z", P * MAX_LAYERS), ("ws_a", P * MAX_LAYERS), ("ws_hd", P), ("ws_mask_h", P),
+        ("ws_mu_raw", P), ("ws_ls_raw", P), ("ws_mu", P), ("ws_ls", P), ("ws_bn_rstd", P),
+        ("ws_eps", P), ("ws_theta", P), ("ws_thetad", P), ("ws_mask_t", P),
+        ("ws_kl", P), ("ws_rl", P), ("ws_lse", P), ("ws_s", P),
+        ("ws_zn", P), ("ws_col_rstd", P), ("ws_row_part", P), ("ws_dthetad", P), ("ws_dz0", P),
+        ("ws_dmu", P), ("ws_dls", P), ("ws_colpart", P),
+        ("ws_dbsm", P), ("ws_ck", P), ("ws_hctx", P), ("ws_tstart", P), ("dbg", P),
+    ]
+
+
+class GfkAdam(C.Structure):
+    _fields_ = [
+        ("p", P), ("g", P), ("m", P), ("v", P),
+        ("n_seg", C.c_int32), ("pad", C.c_int32),
+        ("seg_start", C.c_int64 * MAX_SEGS), ("seg_end", C.c_int64 * MAX_SEGS),
+        ("seg_flags", C.c_int32 * MAX_SEGS),
+        ("lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float),
+        ("weight_decay", C.c_float), ("scale", C.c_float),
+        ("t", P),
+    ]
+
+
+# optional entry points: name -> (argtypes, restype)
+_EXTRA = {
+    "gfk_theta_infer": ([C.POINTER(GfkModel), C.c_void_p, C.c_void_p, C.c_int, C.c_int,
+                         C.c_uint64, C.c_void_p], C.c_int),
+}
+
+
+def declare(lib: C.CDLL) -> None:
+    lib.gfk_model_struct_size.restype = C.c_size_t
+    lib.gfk_adam_struct_size.restype = C.c_size_t
+    if lib.gfk_model_struct_size() != C.sizeof(GfkModel):
+        raise RuntimeError(f"GfkModel ABI mismatch: C {lib.gfk_model_struct_size()} vs "
+                           f"ctypes {C.sizeof(GfkModel)}")
+    if lib.gfk_adam_struct_size() != C.sizeof(GfkAdam):
+        raise RuntimeError(f"GfkAdam ABI mismatch: C {lib.gfk_adam_struct_size()} vs "
+                           f"ctypes {C.sizeof(GfkAdam)}")
+    lib.gfk_setup.argtypes = [C.POINTER(GfkModel)]
+    lib.gfk_setup.restype = C.c_int
+    lib.gfk_run.argtypes = [C.POINTER(GfkModel), C.POINTER(GfkAdam), C.c_int, C.c_void_p,
+                            C.POINTER(C.c_int32), C.c_int]
+    lib.gfk_run.restype = C.c_int
+    lib.gfk_smem_required.argtypes = [C.POINTER(GfkModel), C.c_int]
+    lib.gfk_smem_required.restype = C.c_size_t
+    lib.gfk_scale.argtypes = [C.c_void_p, C.c_int64, C.c_float, C.c_void_p]
+    lib.gfk_scale.restype = C.c_int
+    for name, args in _EXTRA.items():
+        if hasattr(lib, name):
+            f = getattr(lib, name)
+            f.argtypes, f.restype = args
+
+
+def phase_array(phases):
+    arr = (C.c_int32 * len(phases))(*phases)
+    return arr, len(phases)

@@ -1,0 +1,68 @@
+"""Loader for the in-tree native libraries (built by __graft_entry__.build()).
+
+* ``libgfedntm_kernels.so`` -- CDNA4 (gfx950) HIP kernels + the C++ step
+  launcher; called through ctypes with raw device pointers and the current
+  HIP stream, so every launch of a training step is made from C++.
+* ``libgfedntm_runtime.so`` -- host-side C++ runtime: CountVectorizer-
+  compatible tokenizer / CSR builder, batch-plan builder.
+
+On a GPU box the kernels library is REQUIRED: :func:`kernels` raises if it is
+missing instead of silently falling back to PyTorch.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Dict, Optional, Sequence
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_DIR = os.path.join(ROOT, "_lib")
+KERNELS_SO = os.path.join(LIB_DIR, "libgfedntm_kernels.so")
+RUNTIME_SO = os.path.join(LIB_DIR, "libgfedntm_runtime.so")
+
+_kernels: Optional[ctypes.CDLL] = None
+_runtime: Optional[ctypes.CDLL] = None
+_runtime_tried = False
+
+
+def kernels_available() -> bool:
+    return os.path.exists(KERNELS_SO)
+
+
+def kernels() -> ctypes.CDLL:
+    global _kernels
+    if _kernels is None:
+        if not kernels_available():
+            raise RuntimeError(
+                f"{KERNELS_SO} is missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        _kernels = ctypes.CDLL(KERNELS_SO, mode=ctypes.RTLD_GLOBAL)
+        from . import kernel_abi
+        kernel_abi.declare(_kernels)
+    return _kernels
+
+
+def runtime() -> Optional[ctypes.CDLL]:
+    global _runtime, _runtime_tried
+    if not _runtime_tried:
+        _runtime_tried = True
+        if os.path.exists(RUNTIME_SO):
+            _runtime = ctypes.CDLL(RUNTIME_SO)
+            from . import runtime_abi
+            runtime_abi.declare(_runtime)
+    return _runtime
+
+
+def tokenizer_available() -> bool:
+    return runtime() is not None
+
+
+def local_vocabulary(texts: Sequence[str]) -> Dict[str, int]:
+    from . import runtime_abi
+    return runtime_abi.local_vocabulary(runtime(), texts)
+
+
+def vectorize(texts: Sequence[str], vocabulary: Dict[str, int]):
+    from . import runtime_abi
+    return runtime_abi.vectorize(runtime(), texts, vocabulary)

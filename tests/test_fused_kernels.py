@@ -1,0 +1,164 @@
+"""Fused HIP step vs the PyTorch fp32 oracle (same weights, same noise).
+
+The kernels draw their dropout masks / Gaussian noise from Philox; the test
+reads them back from the engine workspace and feeds them to the functional
+oracle (gfedntm_amd/models/functional.py), then compares loss, every
+gradient, BN running statistics and the post-Adam parameters.
+"""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+from gfedntm_amd.data.bow import BatchPlan, DeviceCSR
+from gfedntm_amd.models import AVITM
+from gfedntm_amd.models.functional import avitm_loss_explicit
+from gfedntm_amd.ops import kernel_abi as abi
+from tests.helpers import random_csr
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(model_type="prodLDA", V=700, K=20, H=(32, 24), B=64, activation="softplus", seed=0):
+    torch.manual_seed(seed)
+    kw = dict(input_size=V, n_components=K, model_type=model_type, hidden_sizes=H,
+              batch_size=B, activation=activation, verbose=False, device="cuda")
+    fused = AVITM(backend="fused", **kw)
+    ref = AVITM(backend="torch", **kw)
+    ref.model.load_state_dict(fused.model.state_dict())
+    return fused, ref
+
+
+def _bind(tm, X, n_steps=3, seed=0, B=64):
+    data = DeviceCSR(X, "cuda")
+    plan = BatchPlan.build(data.n_docs, B, n_steps, seed=seed)
+    tm.engine.bind_data(data, plan)
+    return data, plan
+
+
+# Gradients that are zero in exact arithmetic (batch-norm removes the bias of the
+# layer before it; the prior mean sees sum_b mu_b = 0 after BN): both sides hold
+# rounding noise, so they are compared against the scale of their layer instead.
+_NOISE_KEYS = ("inf_net.f_mu.bias", "inf_net.f_sigma.bias", "prior_mean")
+
+
+def _check_grads(g, ref):
+    for k, p in ref.model.named_parameters():
+        scale = p.grad.abs().max().item() + 1e-6
+        atol = 2e-4 * scale + 1e-4
+        if k in _NOISE_KEYS:
+            atol = 1e-3 * max(q.grad.abs().max().item() for q in ref.model.parameters())
+        torch.testing.assert_close(g[k], p.grad, rtol=2e-3, atol=atol,
+                                   msg=lambda m: f"{k}: {m}")
+
+
+def _grads_of(tm_fused):
+    e = tm_fused.engine
+    return {k: e.view_like(e.grad, k).detach().clone() for k, _ in e.param_order}
+
+
+@pytest.mark.parametrize("model_type", ["prodLDA", "LDA"])
+@pytest.mark.parametrize("B,n_docs,K,H", [(64, 150, 20, (32, 24)), (32, 45, 20, (32, 24)),
+                                          (64, 100, 100, (40,)), (128, 200, 50, (50, 50))])
+def test_step_matches_oracle(model_type, B, n_docs, K, H):
+    V = 700
+    fused, ref = _pair(model_type, V=V, K=K, H=H, B=B)
+    X = random_csr(n_docs, V, 40, seed=1)
+    data, plan = _bind(fused, X, B=B)
+    e = fused.engine
+    phases = e.phases()
+    e.run_phases(phases[:-1])            # everything but Adam
+    torch.cuda.synchronize()
+    nb = int(plan.size[0])
+    ids = torch.from_numpy(plan.batch(0).astype(np.int64)).cuda()
+    x = data.dense_rows(ids)
+    eps = e.ws["eps"][:nb].clone()
+    mask_h = e.ws["mask_h"][:nb].clone()
+    mask_t = e.ws["mask_t"][:nb].clone()
+    ref.model.train()
+    ref.model.zero_grad()
+    loss, kl, rl = avitm_loss_explicit(ref.model, x, eps, mask_h, mask_t)
+    loss.backward()
+    torch.testing.assert_close(e.ws["kl"][:nb], kl.detach(), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(e.ws["rl"][:nb], rl.detach(), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(e.loss_hist[0], loss.detach(), rtol=1e-4, atol=1e-2)
+    g = _grads_of(fused)
+    _check_grads(g, ref)
+    sd_f, sd_r = fused.model.state_dict(), ref.model.state_dict()
+    for k in sd_r:
+        if "running" in k or "num_batches" in k:
+            torch.testing.assert_close(sd_f[k].float(), sd_r[k].float(), rtol=1e-4, atol=1e-5,
+                                       msg=lambda m: f"{k}: {m}")
+    # Adam, on identical gradients (a near-zero gradient's sign is rounding noise and
+    # Adam's first step normalises it to +-lr, so compare the optimizer in isolation)
+    for k, p in ref.model.named_parameters():
+        p.grad.copy_(g[k])
+    ref.optimizer.step()
+    e.run_phases([abi.PH_ADAM])
+    torch.cuda.synchronize()
+    sd_f = fused.model.state_dict()
+    for k, p in ref.model.named_parameters():
+        torch.testing.assert_close(sd_f[k], p.detach(), rtol=1e-4, atol=1e-5,
+                                   msg=lambda m: f"{k}: {m}")
+    assert int(e.d_step.item()) == 1 and int(e.adam_t.item()) == 1
+    assert float(e.grad.abs().max().item()) == 0.0   # consumed and cleared
+
+
+@pytest.mark.parametrize("activation", ["relu", "tanh", "elu", "selu", "sigmoid", "leakyrelu"])
+def test_activations(activation):
+    fused, ref = _pair("prodLDA", V=300, K=10, H=(16, 16, 8), B=32, activation=activation)
+    X = random_csr(40, 300, 20, seed=3)
+    data, plan = _bind(fused, X, B=32)
+    e = fused.engine
+    e.run_phases(e.phases()[:-1])
+    torch.cuda.synchronize()
+    nb = int(plan.size[0])
+    ids = torch.from_numpy(plan.batch(0).astype(np.int64)).cuda()
+    x = data.dense_rows(ids)
+    loss, _, _ = avitm_loss_explicit(ref.model, x, e.ws["eps"][:nb], e.ws["mask_h"][:nb],
+                                     e.ws["mask_t"][:nb])
+    ref.model.zero_grad()
+    loss.backward()
+    torch.testing.assert_close(e.loss_hist[0], loss.detach(), rtol=1e-4, atol=1e-2)
+    g = _grads_of(fused)
+    _check_grads(g, ref)
+
+
+def test_graph_replay_matches_eager():
+    torch.manual_seed(0)
+    kw = dict(input_size=500, n_components=16, hidden_sizes=(32, 32), batch_size=64,
+              verbose=False, device="cuda")
+    a = AVITM(backend="fused", **kw)
+    b = AVITM(backend="fused", **kw)
+    b.model.load_state_dict(a.model.state_dict())
+    b.engine.seed = a.engine.seed
+    b.engine._m.seed = a.engine.seed
+    X = random_csr(300, 500, 30, seed=5)
+    _bind(a, X, n_steps=12)
+    _bind(b, X, n_steps=12)
+    b.engine.enable_graph(True)
+    for s in range(12):
+        a.engine.step(s)
+        b.engine.step(s)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(a.engine.loss_hist, b.engine.loss_hist, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(a.flat.buffer, b.flat.buffer, rtol=1e-5, atol=1e-6)
+
+
+def test_training_decreases_loss():
+    torch.manual_seed(0)
+    from tests.helpers import tiny_corpus
+    from gfedntm_amd.data.bow import BOWDataset
+    c, terms, shards = tiny_corpus(V=800, K=10, n_docs=600, n_nodes=1, nwords=(80, 120))
+    ds = BOWDataset(shards[0], {i: t for i, t in enumerate(terms)})
+    m = AVITM(input_size=len(terms), n_components=10, hidden_sizes=(50, 50), num_epochs=15,
+              verbose=False, backend="fused", device="cuda")
+    data = m.device_data(ds)
+    plan = BatchPlan.build(data.n_docs, 64, 10 * 15, seed=0)
+    m.engine.bind_data(data, plan)
+    for s in range(plan.n_steps):
+        m.engine.step(s)
+    h = m.engine.loss_hist.cpu().numpy()
+    assert np.isfinite(h).all()
+    assert h[-10:].mean() < 0.9 * h[:10].mean()
