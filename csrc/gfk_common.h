@@ -10,7 +10,7 @@
 #include <stdint.h>
 
 #define GFK_MAX_LAYERS 8
-#define GFK_MAX_SEGS 32
+#define GFK_MAX_SEGS 48
 #define GFK_WAVE 64
 
 // ---------------------------------------------------------------------------
@@ -44,6 +44,10 @@ typedef struct GfkModel {
   int32_t dec_grid;      // workgroups of the vocab-tiled decoder kernels
   int32_t learn_priors;
   int32_t stage_flags;   // bit0: encoder weights fit in LDS, bit1: posterior-bwd stash fits in LDS
+  int32_t kt;            // row stride of ws_thetad: K padded to 4 x odd (conflict-free MFMA reads)
+  int32_t scatter_chunks;   // grid.y of the input-layer scatter (64 non-zeros per chunk)
+  int32_t n_dpart;       // partial slabs of d theta_d ([n_dpart, bmax, K]): n_tiles (ProdLDA), 1 (LDA)
+  int32_t n_steps;       // length of the batch plan
   float drop_enc, drop_theta;
   float bn_momentum, bn_eps;
   float kl_weight;       // CTM loss_weights["beta"], 1 for AVITM
@@ -61,6 +65,12 @@ typedef struct GfkModel {
   float *g_prior_mean, *g_prior_var, *g_beta, *g_w_in, *g_b_in;
   float *g_w_h[GFK_MAX_LAYERS], *g_b_h[GFK_MAX_LAYERS];
   float *g_w_mu, *g_b_mu, *g_w_s, *g_b_s;
+  // Gradient slabs: posterior_bwd_mlp workgroup g writes its partial gradient of
+  // the small MLP tensors with plain stores at s_* + g * slab_stride; the fused
+  // Adam reduces the slabs in a fixed order (deterministic, no atomics).
+  float *s_b_in, *s_w_h[GFK_MAX_LAYERS], *s_b_h[GFK_MAX_LAYERS];
+  float *s_w_mu, *s_b_mu, *s_w_s, *s_b_s;
+  int64_t slab_stride;
 
   // ---- data (device-resident CSR shard + batch plan) ----
   const int32_t *indptr, *indices;
@@ -82,12 +92,13 @@ typedef struct GfkModel {
   float *ws_mu, *ws_ls;          // [bmax, K] post-BN
   float *ws_bn_rstd;             // [2K] rstd of the mu / log-sigma BN
   float *ws_eps;                 // [bmax, K]
-  float *ws_theta, *ws_thetad, *ws_mask_t;   // [bmax, K]
+  float *ws_theta, *ws_mask_t;   // [bmax, K]
+  float *ws_thetad;              // [bmax, kt] dropped-out theta (zero padding columns)
   float *ws_kl, *ws_rl, *ws_lse, *ws_s;      // [bmax]
-  float *ws_zn;                  // [bmax, V] BN'ed logits (ProdLDA) / BN'ed beta^T [V, K] (LDA)
-  float *ws_col_rstd;            // [V] (ProdLDA: over batch; LDA: over topics)
-  float *ws_row_part;            // [dec_grid, max(bmax,K), 2] online (max, sumexp) partials
-  float *ws_dthetad;             // [bmax, K] accumulated by the decoder backward (atomics)
+  float *ws_zn;                  // ProdLDA: BN'ed logits tiled [n_tiles, bmax, 64]; LDA: BN'ed beta^T [V, K]
+  float *ws_col_rstd;            // [n_tiles * 64] (ProdLDA: over batch; LDA: over topics)
+  float *ws_row_part;            // online (max, sumexp) partials: ProdLDA [n_tiles*4, bmax, 2], LDA [dec_grid, K, 2]
+  float *ws_dthetad;             // [n_dpart, bmax, K] d theta_d partials (plain stores, reduced in order)
   float *ws_dz0;                 // [bmax, H0]
   float *ws_dmu, *ws_dls;        // [bmax, K] dL/d(post-BN mu, log-sigma)
   float *ws_colpart;             // [bmax/4, 9, K] per-workgroup column sums (posterior bwd)
@@ -95,6 +106,9 @@ typedef struct GfkModel {
   float *ws_ck;                  // LDA: [K] sum_v beta_sm * d beta_sm
   float *ws_hctx;                // CTM: dense contextual contribution to layer 0 [bmax, H0]
   int32_t *ws_tstart;            // [bmax, n_tiles+1] CSR position of each row's first nz per vocab tile
+  int32_t *ws_erange;            // [bmax, 2] CSR extent (e0, e1) of each row of the current batch
+  int32_t *ws_next;              // [1 + 3*bmax] next batch, prepared during the previous step:
+                                 //   nb, doc[bmax], (e0, e1)[bmax]
   uint64_t *dbg;                 // diagnostic s_memtime stamps (GFK_STAMPS builds only)
 } GfkModel;
 
@@ -107,6 +121,14 @@ typedef struct GfkAdam {
   int32_t seg_flags[GFK_MAX_SEGS];   // bit0: Adam update, bit1: FedAvg pre-scale
   float lr, beta1, beta2, eps, weight_decay, scale;
   const int32_t *t;                  // device Adam step count (already incremented)
+  // segment s takes its gradient from n_slab slabs (seg_slab[s] + j * slab_stride)
+  // instead of g when seg_slab[s] is non-null
+  const float* seg_slab[GFK_MAX_SEGS];
+  int32_t seg_first_block[GFK_MAX_SEGS];   // first workgroup of each segment (1024 float4 per block)
+  int64_t slab_stride;
+  int32_t n_slab;
+  int32_t pad2;
+  uint64_t* dbg;                     // diagnostic stamps (GFK_STAMPS builds)
 } GfkAdam;
 
 }  // extern "C"
@@ -232,6 +254,36 @@ __device__ __forceinline__ void wave_lse(float& m, float& s) {
 }
 
 __device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+// Pin a kernel-argument field in SGPRs at the point of the call: the empty asm
+// "modifies" the value, so the compiler can neither sink the scalar load to its
+// first use nor re-load it later.  Used in kernel prologues so that all
+// argument loads are issued back to back and waited on once, instead of one
+// dependent scalar-cache round trip per field in the middle of the kernel.
+template <class T>
+__device__ __forceinline__ void keep1(T& v) { asm volatile("" : "+s"(v)); }
+template <class... T>
+__device__ __forceinline__ void keep(T&... v) { (keep1(v), ...); }
+
+// DPP lane permutations inside each 16-lane row (VALU-rate, no LDS round trip):
+// quad_perm xor1 / xor2, row_half_mirror, row_mirror.  Applying all four with a
+// commutative op reduces over the 16 lanes and leaves the result in every lane.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x141>(v));
+  return fmaxf(v, dpp_f<0x140>(v));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0x141>(v);
+  return v + dpp_f<0x140>(v);
+}
 
 // global -> LDS copy of n floats with U independent loads in flight per thread
 // (indices are clamped, never predicated, so hipcc keeps the loads back to back).

@@ -112,10 +112,9 @@ extern "C" __global__ void __launch_bounds__(LDA_THREADS) gfk_lda_row_loss_bwd(G
   float* dth = smem;
   float* th = dth + 4 * K;
   float* rls = th + K;
-  for (int k = tid; k < K; k += LDA_THREADS) th[k] = m.ws_thetad[(size_t)b * K + k];
+  for (int k = tid; k < K; k += LDA_THREADS) th[k] = m.ws_thetad[(size_t)b * m.kt + k];
   __syncthreads();
-  const int doc = m.ws_doc[b];
-  const int e0 = m.indptr[doc], e1 = m.indptr[doc + 1];
+  const int e0 = m.ws_erange[2 * b], e1 = m.ws_erange[2 * b + 1];
   constexpr int KQ = 4;   // K <= 256
   float acc[KQ] = {0.f, 0.f, 0.f, 0.f};
   float rl = 0.f;

@@ -3,25 +3,39 @@
 //
 // Reference math: decoder_network.py:121-126, avitm.py:225.
 //
-// Tiling (MI355X-first): a workgroup (4 waves) owns a vocabulary tile of VB=64
-// columns x ALL batch rows (B <= 128), so the per-column batch-norm statistics
-// (a reduction over B) stay inside the tile; the softmax over V is an online
-// (max, sum-exp) per row across tiles.  The three GEMM-shaped products run on
-// the fp32 matrix cores (v_mfma_f32_16x16x4_f32, exact fp32 -- the reference is
-// fp32, so no bf16 here):
+// Tiling (MI355X-first): one workgroup (4 waves) owns one vocabulary tile of
+// VB=64 columns x ALL batch rows (B <= 128), so the per-column batch-norm
+// statistics (a reduction over B) never leave the workgroup, and the softmax
+// over V is an online (max, sum-exp) per row whose partials are merged by
+// row_loss.  The three GEMM-shaped products run on the fp32 matrix cores
+// (v_mfma_f32_16x16x4_f32, exact fp32 -- the reference is fp32):
 //     logits[B, VB]  = theta_d[B, K] @ beta[K, VB]           (forward)
 //     dbeta[K, VB]   = theta_d^T[K, B] @ dlogit[B, VB]       (backward, per tile)
-//     dtheta_d[B, K] += dlogit[B, VB] @ beta^T[VB, K]        (backward, across tiles)
-// with 16x16 output sub-tiles distributed over the 4 waves.  LDS row strides are
-// padded by one word so the MFMA operand reads are bank-conflict free.
+//     dtheta_d[B, K] = sum_tiles dlogit[B, VB] @ beta^T[VB, K] (per-tile partials)
+//
+// Latency discipline (the kernels are tiny, so round trips dominate):
+//  * every global read of a kernel is issued in ONE staging round before the
+//    first barrier: theta_d and the BN'ed logit tile go through LDS-DMA
+//    (global_load_lds_dwordx4), the beta tile through registers;
+//  * forward: wave w owns columns [16w, 16w+16) for all rows, so the column
+//    batch-norm statistics, the normalisation, the running-stat update and the
+//    per-row (max, sum-exp) partials are computed straight from the MFMA
+//    accumulators (cross-lane shuffles, no LDS pass, no second barrier);
+//  * backward: the x tile is never materialised -- the sparse -x p/(p+1e-10)
+//    terms are written into a pre-zeroed dlogit tile, then one register pass
+//    adds p*S and applies the BN backward.
 //
 // The loss never needs the dense [B, V] word distribution: only the CSR
 // non-zeros are gathered (row_loss), and the backward needs per row
 //   dL/dz_bj = p_bj * S_b - x_bj * p_bj / (p_bj + 1e-10),
 //   S_b = sum_{v in nz(b)} x_bv p_bv / (p_bv + 1e-10),
 // with p recomputed from the stored BN'ed logits.  row_loss also records where
-// each row's non-zeros of every vocab tile start (ws_tstart), so the backward
-// fills its x tile with two loads per row instead of a binary search.
+// each row's non-zeros of every vocab tile start (ws_tstart).
+//
+// Layouts: ws_thetad is [bmax, kt] (kt = K padded to 4 x odd, zero padding, so
+// the MFMA A-operand reads are bank-conflict free); ws_zn is tiled
+// [n_tiles][bmax][VB] so a tile is one contiguous LDS-DMA copy; ws_row_part is
+// [n_tiles * 4][bmax][2] (one partial per wave).
 #include "gfk_common.h"
 
 using namespace gfk;
@@ -29,21 +43,24 @@ using namespace gfk;
 namespace {
 constexpr int DEC_THREADS = 256;
 constexpr int VB = 64;
-constexpr int LDB = VB + 1;        // padded row stride of the beta / dlogit / logit tiles
+constexpr int LDB_F = 80;   // fwd beta tile stride: B-role reads (lane -> column) conflict free
+constexpr int LDB_B = 68;   // bwd beta tile stride: transposed B-role reads (lane -> k row)
+constexpr int LDD = 72;     // bwd dlogit stride: used as A (lane -> row) and B (lane -> column)
 constexpr float RL_EPS = 1e-10f;
 
 __host__ __device__ __forceinline__ int round_up(int x, int m) { return (x + m - 1) / m * m; }
 
-// Stage beta[:, c0:c0+VB] (rows < K, columns < V; zero elsewhere) into bt[KP x LDB].
-__device__ __forceinline__ void stage_beta_tile(float* bt, const float* __restrict__ beta, int K,
-                                                int KP, int V, int c0, int tid) {
-  constexpr int U = 8;
+// beta[0:KP, c0:c0+VB] -> bt[KP x ld] (zero for k >= K or column >= V); one
+// round of independent loads per 16 elements per thread.
+__device__ __forceinline__ void stage_beta_tile(float* bt, int ld, const float* __restrict__ beta,
+                                                int K, int KP, int V, int c0, int tid) {
+  constexpr int U = 16;
   const int n = KP * VB;
   for (int base = tid; base < n; base += U * DEC_THREADS) {
     float v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int i = base + u * DEC_THREADS;
+      const int i = min(base + u * DEC_THREADS, n - 1);
       const int k = min(i / VB, K - 1), c = min(c0 + i % VB, V - 1);
       v[u] = beta[(size_t)k * V + c];
     }
@@ -51,170 +68,161 @@ __device__ __forceinline__ void stage_beta_tile(float* bt, const float* __restri
     for (int u = 0; u < U; ++u) {
       const int i = base + u * DEC_THREADS;
       const int k = i / VB, c = i % VB;
-      if (i < n) bt[k * LDB + c] = (k < K && c0 + c < V) ? v[u] : 0.f;
+      if (i < n) bt[k * ld + c] = (k < K && c0 + c < V) ? v[u] : 0.f;
     }
   }
 }
 
-// Stage theta_d[nb, K] into th[BM x LDT] (zero rows >= nb, zero columns >= K).
-__device__ __forceinline__ void stage_theta(float* th, const float* __restrict__ thetad, int nb,
-                                            int K, int BM, int KP, int LDT, int tid) {
-  constexpr int U = 8;
-  const int n = BM * KP;
-  for (int base = tid; base < n; base += U * DEC_THREADS) {
-    float v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i = base + u * DEC_THREADS;
-      const int b = min(i / KP, max(nb - 1, 0)), k = min(i % KP, K - 1);
-      v[u] = thetad[(size_t)b * K + k];
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i = base + u * DEC_THREADS;
-      const int b = i / KP, k = i % KP;
-      if (i < n) th[b * LDT + k] = (b < nb && k < K) ? v[u] : 0.f;
-    }
-  }
+// sum over the 4 lane groups (lanes l, l^16, l^32, l^48): a column reduction
+__device__ __forceinline__ float sum_groups(float v) {
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
 }
 }  // namespace
 
-// grid: dec_grid workgroups, grid-stride over the n_tiles vocab tiles.
-// dynamic LDS: th[BM*LDT] + bt[KP*LDB] + lt[BM*LDB] + rowm[BM] + rows[BM]
+// grid: n_tiles workgroups (one vocab tile each).
+// dynamic LDS: th[BM*kt] + bt[KP*LDB_F]
 template <int BM>
 __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int K = m.K, V = m.V, nb = *m.ws_nb, tid = threadIdx.x;
+  const int K = m.K, V = m.V, KT = m.kt, tid = threadIdx.x;
   const int lane = tid & 63, wave = uniform(tid >> 6);
-  const int KP = round_up(K, 4), LDT = KP + 1;
+  const int KP = round_up(K, 4);
+  const int tile = blockIdx.x, c0 = tile * VB;
   float* th = smem;
-  float* bt = th + BM * LDT;
-  float* lt = bt + KP * LDB;
-  float* rowm = lt + BM * LDB;
-  float* rows = rowm + BM;
+  float* bt = th + BM * KT;
 
   GFK_STAMP(m, 16);
-  stage_theta(th, m.ws_thetad, nb, K, BM, KP, LDT, tid);
-  for (int b = tid; b < BM; b += DEC_THREADS) { rowm[b] = -INFINITY; rows[b] = 0.f; }
-  if (blockIdx.x == 0 && tid == 0) *m.nbt_beta += 1;
-
-  constexpr int NSUB = (BM / 16) * (VB / 16);   // 16x16 output sub-tiles per vocab tile
-  for (int tile = blockIdx.x; tile < m.n_tiles; tile += gridDim.x) {
-    const int c0 = tile * VB;
-    __syncthreads();
-    GFK_STAMP(m, 17);
-    stage_beta_tile(bt, m.beta, K, KP, V, c0, tid);
-    __syncthreads();
-    GFK_STAMP(m, 18);
-    // ---- logits = theta_d @ beta_tile on the matrix cores ----
-    for (int s = wave; s < NSUB; s += 4) {
-      const int rs = s / (VB / 16), cs = s % (VB / 16);
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      const float* ap = th + (rs * 16 + (lane & 15)) * LDT + (lane >> 4);
-      const float* bp = bt + (lane >> 4) * LDB + cs * 16 + (lane & 15);
-      for (int k0 = 0; k0 < KP; k0 += 4) acc = mfma16x16x4(ap[k0], bp[k0 * LDB], acc);
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        lt[(rs * 16 + (lane >> 4) * 4 + r) * LDB + cs * 16 + (lane & 15)] = acc[r];
-    }
-    __syncthreads();
-    GFK_STAMP(m, 19);
-    // ---- column batch-norm: 4 threads per column ----
-    {
-      const int c = tid >> 2, sub = tid & 3;
-      const bool valid = c0 + c < V;
-      float s = 0.f;
-      for (int b = sub; b < nb; b += 4) s += lt[b * LDB + c];
-      s += __shfl_xor(s, 1, 64);
-      s += __shfl_xor(s, 2, 64);
-      const float mean = s / (float)nb;
-      float q = 0.f;
-      for (int b = sub; b < nb; b += 4) {
-        const float d = lt[b * LDB + c] - mean;
-        q += d * d;
-      }
-      q += __shfl_xor(q, 1, 64);
-      q += __shfl_xor(q, 2, 64);
-      const float var = q / (float)nb;
-      const float rstd = rsqrtf(var + m.bn_eps);
-      for (int b = sub; b < nb; b += 4) {
-        const int i = b * LDB + c;
-        lt[i] = valid ? (lt[i] - mean) * rstd : -INFINITY;
-      }
-      if (sub == 0 && valid) {
-        const int v = c0 + c;
-        const float mom = m.bn_momentum;
-        const float unb = nb > 1 ? var * (float)nb / (float)(nb - 1) : var;
-        m.beta_rm[v] = (1.f - mom) * m.beta_rm[v] + mom * mean;
-        m.beta_rv[v] = (1.f - mom) * m.beta_rv[v] + mom * unb;
-        m.ws_col_rstd[v] = rstd;
-      }
-    }
-    __syncthreads();
-    GFK_STAMP(m, 20);
-    // ---- coalesced store of the BN'ed logits ----
-    for (int i = tid; i < nb * VB; i += DEC_THREADS) {
-      const int b = i / VB, c = i % VB;
-      if (c0 + c < V) m.ws_zn[(size_t)b * V + c0 + c] = lt[b * LDB + c];
-    }
-    // ---- online (max, sum exp) per row: 4 threads per row, 16 columns each ----
-    for (int b = tid >> 2; b < nb; b += DEC_THREADS / 4) {
-      const int sub = tid & 3;
-      const float* row = lt + b * LDB + 16 * sub;
-      float mx = -INFINITY;
-#pragma unroll
-      for (int c = 0; c < 16; ++c) mx = fmaxf(mx, row[c]);
-      mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
-      float se = 0.f;
-#pragma unroll
-      for (int c = 0; c < 16; ++c) se += __expf(row[c] - mx);
-      se += __shfl_xor(se, 1, 64);
-      se += __shfl_xor(se, 2, 64);
-      if (sub == 0) {
-        float rm = rowm[b], rs_ = rows[b];
-        lse_merge(rm, rs_, mx, se);
-        rowm[b] = rm;
-        rows[b] = rs_;
-      }
-    }
-  }
-  __syncthreads();
+  // ---- one staging round: theta_d (LDS-DMA), beta tile, running stats, nb ----
+  glds_copy(th, m.ws_thetad, BM * KT, tid, DEC_THREADS);
   GFK_STAMP(m, 21);
-  for (int b = tid; b < nb; b += DEC_THREADS) {
-    float* p = m.ws_row_part + ((size_t)blockIdx.x * m.bmax + b) * 2;
-    p[0] = rowm[b];
-    p[1] = rows[b];
-  }
+  const int col = 16 * wave + (lane & 15);      // this lane's column within the tile
+  const int v = c0 + col;
+  const bool valid = v < V;
+  const float rm0 = m.beta_rm[min(v, V - 1)], rv0 = m.beta_rv[min(v, V - 1)];
+  const int nb = *m.ws_nb;
   GFK_STAMP(m, 22);
+  stage_beta_tile(bt, LDB_F, m.beta, K, KP, V, c0, tid);
+  GFK_STAMP(m, 23);
+  if (tile == 0 && tid == 0) *m.nbt_beta += 1;
+  __syncthreads();
+  GFK_STAMP(m, 17);
+
+  // ---- logits for rows [0, BM) x this wave's 16 columns ----
+  constexpr int RT = BM / 16;
+  f32x4 acc[RT];
+#pragma unroll
+  for (int r = 0; r < RT; ++r) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+  {
+    const float* bp = bt + (lane >> 4) * LDB_F + col;
+    const float* ap = th + (lane & 15) * KT + (lane >> 4);
+    for (int k0 = 0; k0 < KP; k0 += 4) {
+      const float b = bp[k0 * LDB_F];
+#pragma unroll
+      for (int r = 0; r < RT; ++r) acc[r] = mfma16x16x4(ap[r * 16 * KT + k0], b, acc[r]);
+    }
+  }
+  GFK_STAMP(m, 18);
+
+  // ---- column batch-norm straight from the accumulators ----
+  // lane holds rows rt*16 + (lane>>4)*4 + e of column col
+  const float inv_nb = 1.f / (float)nb;
+  float s = 0.f;
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = r * 16 + (lane >> 4) * 4 + e;
+      s += row < nb ? acc[r][e] : 0.f;
+    }
+  const float mean = sum_groups(s) * inv_nb;
+  float q = 0.f;
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = r * 16 + (lane >> 4) * 4 + e;
+      const float d = acc[r][e] - mean;
+      q += row < nb ? d * d : 0.f;
+    }
+  const float var = sum_groups(q) * inv_nb;
+  const float rstd = rsqrtf(var + m.bn_eps);
+  if (lane < 16 && valid) {
+    const float mom = m.bn_momentum;
+    const float unb = nb > 1 ? var * (float)nb / (float)(nb - 1) : var;
+    m.beta_rm[v] = (1.f - mom) * rm0 + mom * mean;
+    m.beta_rv[v] = (1.f - mom) * rv0 + mom * unb;
+    m.ws_col_rstd[v] = rstd;
+  }
+  GFK_STAMP(m, 19);
+
+  // ---- normalise, store the BN'ed tile, per-row (max, sum-exp) partials ----
+  float* zt = m.ws_zn + (size_t)tile * BM * VB;
+  float* part = m.ws_row_part + (size_t)(tile * 4 + wave) * m.bmax * 2;
+#pragma unroll
+  for (int r = 0; r < RT; ++r) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = r * 16 + (lane >> 4) * 4 + e;
+      const float z = (acc[r][e] - mean) * rstd;
+      if (row < nb) zt[row * VB + col] = z;
+      const float zv = valid ? z : -INFINITY;
+      const float mx = row16_max(zv);
+      const float se = row16_sum(valid ? __expf(zv - mx) : 0.f);
+      if ((lane & 15) == 0 && row < nb) {
+        part[2 * row] = mx;
+        part[2 * row + 1] = se;
+      }
+    }
+  }
+  GFK_STAMP(m, 20);
 }
 
-// One wave per batch row: log-sum-exp from the per-workgroup partials, the
-// sparse reconstruction loss, S_b, and the per-tile CSR start table.
+// One wave per batch row: log-sum-exp from the per-wave partials, the sparse
+// reconstruction loss, S_b, and the per-tile CSR start table.
 extern "C" __global__ void __launch_bounds__(64) gfk_prodlda_row_loss(GfkModel m) {
+  int n_tiles = m.n_tiles, bmax = m.bmax;
+  const int32_t *nbp = m.ws_nb, *erange = m.ws_erange, *indices = m.indices;
+  const float *row_part = m.ws_row_part, *zn = m.ws_zn, *values = m.values;
+  keep(n_tiles, bmax, nbp, erange, indices, row_part, zn, values);
   const int b = blockIdx.x, lane = threadIdx.x;
-  const int nb = *m.ws_nb;
+  const int nb = *nbp;
   if (b >= nb) return;
+  const int np = n_tiles * 4;
+  const int e0 = erange[2 * b], e1 = erange[2 * b + 1];
+  constexpr int PU = 8;
+  float pm[PU], ps[PU];
+  // issue the partial loads for the first 64*PU partials at once
+#pragma unroll
+  for (int u = 0; u < PU; ++u) {
+    const int g = min(lane + 64 * u, np - 1);
+    const float2 p = *reinterpret_cast<const float2*>(row_part + ((size_t)g * bmax + b) * 2);
+    pm[u] = p.x;
+    ps[u] = p.y;
+  }
   float mx = -INFINITY, se = 0.f;
-  for (int g = lane; g < m.dec_grid; g += 64) {
-    const float2 p = *reinterpret_cast<const float2*>(m.ws_row_part + ((size_t)g * m.bmax + b) * 2);
+#pragma unroll
+  for (int u = 0; u < PU; ++u)
+    if (lane + 64 * u < np) lse_merge(mx, se, pm[u], ps[u]);
+  for (int g = lane + 64 * PU; g < np; g += 64) {
+    const float2 p = *reinterpret_cast<const float2*>(row_part + ((size_t)g * bmax + b) * 2);
     lse_merge(mx, se, p.x, p.y);
   }
   wave_lse(mx, se);
   const float lse = mx + logf(se);
-  const int doc = m.ws_doc[b];
-  const int e0 = m.indptr[doc], e1 = m.indptr[doc + 1];
-  const float* zn = m.ws_zn + (size_t)b * m.V;
-  int32_t* ts = m.ws_tstart + (size_t)b * (m.n_tiles + 1);
+  const size_t tstride = (size_t)bmax * VB;
+  int32_t* ts = m.ws_tstart + (size_t)b * (n_tiles + 1);
   float rl = 0.f, S = 0.f;
   for (int e = e0 + lane; e < e1; e += 64) {
-    const int col = m.indices[e];
-    const int prev = e > e0 ? m.indices[e - 1] / VB : -1;
-    const float x = m.values[e];
-    const float p = expf(zn[col] - lse);
+    const int c = indices[e];
+    const int prev = e > e0 ? indices[e - 1] / VB : -1;
+    const float x = values[e];
+    const float z = zn[(size_t)(c / VB) * tstride + (size_t)b * VB + (c % VB)];
+    const float p = expf(z - lse);
     rl += x * logf(p + RL_EPS);
     S += x * p / (p + RL_EPS);
-    for (int t = prev + 1; t <= col / VB; ++t) ts[t] = e;
+    for (int t = prev + 1; t <= c / VB; ++t) ts[t] = e;
   }
   {  // tiles after the last non-zero start at e1
     const int last = e1 > e0 ? m.indices[e1 - 1] / VB : -1;
@@ -229,140 +237,170 @@ extern "C" __global__ void __launch_bounds__(64) gfk_prodlda_row_loss(GfkModel m
   }
 }
 
-// Backward.  dynamic LDS: th[BM*LDT] + bt[KP*LDB] + dt[BM*LDB] + zt[BM*LDB] + xt[BM*VB]
-//                         + dacc[BM*LDT]   (KP = K rounded up to 16, LDT = KP + 1)
+// Backward.  grid: n_tiles workgroups.
+// dynamic LDS: th[BM*kt] + bt[KP16*LDB_B] + zt[BM*VB] + dt[BM*LDD] + lse[BM] + S[BM] + rstd[VB]
 template <int BM>
 __global__ void __launch_bounds__(DEC_THREADS) prodlda_bwd_kernel(GfkModel m) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int K = m.K, V = m.V, nb = *m.ws_nb, tid = threadIdx.x;
+  const int K = m.K, V = m.V, KT = m.kt, tid = threadIdx.x;
   const int lane = tid & 63, wave = uniform(tid >> 6);
-  const int KP = round_up(K, 16), LDT = KP + 1;
+  const int KP16 = round_up(K, 16);
+  const int tile = blockIdx.x, c0 = tile * VB;
   float* th = smem;
-  float* bt = th + BM * LDT;
-  float* dt = bt + KP * LDB;
-  float* zt = dt + BM * LDB;
-  float* xt = zt + BM * LDB;
-  float* dacc = xt + BM * VB;
+  float* bt = th + BM * KT;
+  float* zt = bt + KP16 * LDB_B;
+  float* dt = zt + BM * VB;
+  float* lse = dt + BM * LDD;
+  float* Sb = lse + BM;
+  float* rs = Sb + BM;
 
   GFK_STAMP(m, 24);
-  stage_theta(th, m.ws_thetad, nb, K, BM, KP, LDT, tid);
-  for (int i = tid; i < BM * LDT; i += DEC_THREADS) dacc[i] = 0.f;
-  const int ksub = KP / 16;
-  for (int tile = blockIdx.x; tile < m.n_tiles; tile += gridDim.x) {
-    const int c0 = tile * VB;
-    __syncthreads();
-    stage_beta_tile(bt, m.beta, K, KP, V, c0, tid);
-    for (int i = tid; i < BM * VB; i += DEC_THREADS) xt[i] = 0.f;
-    // zn tile (rows >= nb and columns >= V are zero so they drop out of every product)
-    {
-      constexpr int U = 8;
-      for (int base = tid; base < BM * VB; base += U * DEC_THREADS) {
-        float z[U];
+  // ---- one staging round ----
+  glds_copy(th, m.ws_thetad, BM * KT, tid, DEC_THREADS);
+  glds_copy(zt, m.ws_zn + (size_t)tile * BM * VB, BM * VB, tid, DEC_THREADS);
+  glds_copy(lse, m.ws_lse, BM, tid, DEC_THREADS);
+  glds_copy(Sb, m.ws_s, BM, tid, DEC_THREADS);
+  glds_copy(rs, m.ws_col_rstd + c0, VB, tid, DEC_THREADS);
+  const int nb = *m.ws_nb;
+  // sparse x of this tile: 4 threads per row, first NPRE non-zeros prefetched
+  constexpr int NPRE = 2;
+  const int sub = tid & 3;
+  constexpr int NH = (BM + 63) / 64;   // rows per thread quad
+  int xe0[NH], xe1[NH], xc[NH][NPRE];
+  float xv[NH][NPRE];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int i = base + u * DEC_THREADS;
-          const int b = min(i / VB, max(nb - 1, 0)), c = min(c0 + i % VB, V - 1);
-          z[u] = m.ws_zn[(size_t)b * V + c];
+  for (int h = 0; h < NH; ++h) {
+    const int row = min((tid >> 2) + 64 * h, BM - 1);
+    const int32_t* ts = m.ws_tstart + (size_t)row * (m.n_tiles + 1) + tile;
+    xe0[h] = ts[0];
+    xe1[h] = ts[1];
+  }
+#pragma unroll
+  for (int h = 0; h < NH; ++h)
+#pragma unroll
+    for (int i = 0; i < NPRE; ++i) {
+      const int e = min(xe0[h] + sub + 4 * i, max(xe1[h] - 1, 0));
+      xc[h][i] = m.indices[e];
+      xv[h][i] = m.values[e];
+    }
+  stage_beta_tile(bt, LDB_B, m.beta, K, KP16, V, c0, tid);
+  // zero the dlogit tile (register-pass layout: column col, rows g, g+4, ...)
+  const int col = 16 * wave + (lane & 15), g = lane >> 4;
+  for (int row = g; row < BM; row += 4) dt[row * LDD + col] = 0.f;
+  __syncthreads();
+  GFK_STAMP(m, 25);
+
+  // ---- sparse term: dt[b, c] = -x p / (p + 1e-10) at this tile's non-zeros ----
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+    const int row = (tid >> 2) + 64 * h;
+    if (row < nb && row < BM) {
+      const float l = lse[row];
+      for (int i = 0, e = xe0[h] + sub; e < xe1[h]; ++i, e += 4) {
+        int c;
+        float x;
+        if (i < NPRE) {
+          c = xc[h][min(i, NPRE - 1)];
+          x = xv[h][min(i, NPRE - 1)];
+        } else {
+          c = m.indices[e];
+          x = m.values[e];
         }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int i = base + u * DEC_THREADS;
-          const int b = i / VB, c = i % VB;
-          if (i < BM * VB) zt[b * LDB + c] = (b < nb && c0 + c < V) ? z[u] : 0.f;
-        }
+        c -= c0;
+        const float p = __expf(zt[row * VB + c] - l);
+        dt[row * LDD + c] = -x * p / (p + RL_EPS);
       }
-    }
-    __syncthreads();
-    GFK_STAMP(m, 25);
-    // x tile from the per-tile CSR start table
-    for (int b = tid; b < nb; b += DEC_THREADS) {
-      const int32_t* ts = m.ws_tstart + (size_t)b * (m.n_tiles + 1) + tile;
-      const int e0 = ts[0], e1 = ts[1];
-      for (int e = e0; e < e1; ++e) xt[b * VB + m.indices[e] - c0] = m.values[e];
-    }
-    __syncthreads();
-    GFK_STAMP(m, 26);
-    // dL/dzn
-    for (int i = tid; i < BM * VB; i += DEC_THREADS) {
-      const int b = i / VB, c = i % VB;
-      float d = 0.f;
-      if (b < nb && c0 + c < V) {
-        const float p = __expf(zt[b * LDB + c] - m.ws_lse[b]);
-        d = p * m.ws_s[b] - xt[b * VB + c] * p / (p + RL_EPS);
-      }
-      dt[b * LDB + c] = d;
-    }
-    __syncthreads();
-    GFK_STAMP(m, 27);
-    // column BN backward (batch statistics)
-    {
-      const int c = tid >> 2, sub = tid & 3;
-      float s1 = 0.f, s2 = 0.f;
-      for (int b = sub; b < nb; b += 4) {
-        const float g = dt[b * LDB + c];
-        s1 += g;
-        s2 += g * zt[b * LDB + c];
-      }
-      s1 += __shfl_xor(s1, 1, 64); s1 += __shfl_xor(s1, 2, 64);
-      s2 += __shfl_xor(s2, 1, 64); s2 += __shfl_xor(s2, 2, 64);
-      const float inv = 1.f / (float)nb;
-      const float rstd = (c0 + c < V) ? m.ws_col_rstd[c0 + c] : 0.f;
-      for (int b = sub; b < nb; b += 4) {
-        const int i = b * LDB + c;
-        dt[i] = rstd * (dt[i] - s1 * inv - zt[i] * s2 * inv);
-      }
-    }
-    __syncthreads();
-    GFK_STAMP(m, 28);
-    // dbeta[k, c] = sum_b th[b, k] dlogit[b, c]: sub-tiles (KP/16) x (VB/16)
-    for (int s = wave; s < ksub * (VB / 16); s += 4) {
-      const int ks = s / (VB / 16), cs = s % (VB / 16);
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      const float* ap = th + (lane >> 4) * LDT + ks * 16 + (lane & 15);
-      const float* bp = dt + (lane >> 4) * LDB + cs * 16 + (lane & 15);
-      for (int b0 = 0; b0 < BM; b0 += 4) acc = mfma16x16x4(ap[b0 * LDT], bp[b0 * LDB], acc);
-      const int c = c0 + cs * 16 + (lane & 15);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int k = ks * 16 + (lane >> 4) * 4 + r;
-        if (k < K && c < V) m.g_beta[(size_t)k * V + c] = acc[r];
-      }
-    }
-    // dtheta_d[b, k] += sum_c dlogit[b, c] beta[k, c]: sub-tiles (BM/16) x (KP/16)
-    for (int s = wave; s < (BM / 16) * ksub; s += 4) {
-      const int rs = s / ksub, ks = s % ksub;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      const float* ap = dt + (rs * 16 + (lane & 15)) * LDB + (lane >> 4);
-      const float* bp = bt + (ks * 16 + (lane & 15)) * LDB + (lane >> 4);
-      for (int c = 0; c < VB; c += 4) acc = mfma16x16x4(ap[c], bp[c], acc);
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        dacc[(rs * 16 + (lane >> 4) * 4 + r) * LDT + ks * 16 + (lane & 15)] += acc[r];
     }
   }
   __syncthreads();
-  GFK_STAMP(m, 29);
-  for (int i = tid; i < nb * K; i += DEC_THREADS) {
-    const int b = i / K, k = i % K;
-    atomicAdd(m.ws_dthetad + i, dacc[b * LDT + k]);
+  GFK_STAMP(m, 26);
+
+  // ---- dense term p*S and the column BN backward, in registers ----
+  {
+    const bool valid = c0 + col < V;
+    constexpr int NR = BM / 4;
+    float d[NR], z[NR];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int row = g + 4 * i;
+      z[i] = zt[row * VB + col];
+      const float p = __expf(z[i] - lse[row]);
+      d[i] = (row < nb && valid) ? p * Sb[row] + dt[row * LDD + col] : 0.f;
+      s1 += d[i];
+      s2 += d[i] * z[i];
+    }
+    s1 = sum_groups(s1) / (float)nb;
+    s2 = sum_groups(s2) / (float)nb;
+    const float r = valid ? rs[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int row = g + 4 * i;
+      dt[row * LDD + col] = row < nb ? r * (d[i] - s1 - z[i] * s2) : 0.f;
+    }
   }
-  GFK_STAMP(m, 30);
+  __syncthreads();
+  GFK_STAMP(m, 27);
+
+  // ---- dbeta[k, c] = sum_b th[b, k] dlogit[b, c]: wave w owns columns [16w, 16w+16) ----
+  {
+    const int ksub = KP16 / 16;
+    const float* bp = dt + (lane >> 4) * LDD + 16 * wave + (lane & 15);
+    const int c = c0 + 16 * wave + (lane & 15);
+    for (int ks = 0; ks < ksub; ++ks) {
+      const float* ap = th + (lane >> 4) * KT + ks * 16 + (lane & 15);
+      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int b0 = 0; b0 < BM; b0 += 8) {
+        a0 = mfma16x16x4(ap[b0 * KT], bp[b0 * LDD], a0);
+        a1 = mfma16x16x4(ap[(b0 + 4) * KT], bp[(b0 + 4) * LDD], a1);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = ks * 16 + (lane >> 4) * 4 + e;
+        if (k < K && c < V) m.g_beta[(size_t)k * V + c] = a0[e] + a1[e];
+      }
+    }
+  }
+  // ---- this tile's partial dtheta_d[b, k] = sum_c dlogit[b, c] beta[k, c] (plain stores;
+  //      posterior_bwd_rows sums the n_tiles partials in a fixed order) ----
+  {
+    float* dpart = m.ws_dthetad + (size_t)tile * m.bmax * K;
+    const int ksub = KP16 / 16;
+    for (int s = wave; s < (BM / 16) * ksub; s += 4) {
+      const int rt = s / ksub, ks = s % ksub;
+      const float* ap = dt + (rt * 16 + (lane & 15)) * LDD + (lane >> 4);
+      const float* bp = bt + (ks * 16 + (lane & 15)) * LDB_B + (lane >> 4);
+      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < VB; c += 8) {
+        a0 = mfma16x16x4(ap[c], bp[c], a0);
+        a1 = mfma16x16x4(ap[c + 4], bp[c + 4], a1);
+      }
+      const int k = ks * 16 + (lane & 15);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = rt * 16 + (lane >> 4) * 4 + e;
+        if (row < nb && k < K) dpart[(size_t)row * K + k] = a0[e] + a1[e];
+      }
+    }
+  }
+  GFK_STAMP(m, 28);
 }
 
-extern "C" size_t gfk_prodlda_fwd_smem(int bmax, int K) {
-  const int KP = round_up(K, 4), LDT = KP + 1;
-  return sizeof(float) * ((size_t)bmax * LDT + (size_t)KP * LDB + (size_t)bmax * LDB + 2 * bmax);
+extern "C" size_t gfk_prodlda_fwd_smem(const GfkModel* m) {
+  const size_t KP = round_up(m->K, 4);
+  return sizeof(float) * ((size_t)m->bmax * m->kt + KP * LDB_F);
 }
 
-extern "C" size_t gfk_prodlda_bwd_smem(int bmax, int K) {
-  const int KP = round_up(K, 16), LDT = KP + 1;
-  return sizeof(float) * ((size_t)bmax * LDT * 2 + (size_t)KP * LDB + 2 * (size_t)bmax * LDB +
-                          (size_t)bmax * VB);
+extern "C" size_t gfk_prodlda_bwd_smem(const GfkModel* m) {
+  const size_t KP16 = round_up(m->K, 16), B = m->bmax;
+  return sizeof(float) * (B * m->kt + KP16 * LDB_B + B * VB + B * LDD + 2 * B + VB);
 }
 
 extern "C" int gfk_launch_prodlda_fwd(const GfkModel* m, hipStream_t s) {
-  const size_t sm = gfk_prodlda_fwd_smem(m->bmax, m->K);
-  dim3 g(m->dec_grid), blk(DEC_THREADS);
+  const size_t sm = gfk_prodlda_fwd_smem(m);
+  dim3 g(m->n_tiles), blk(DEC_THREADS);
   switch (m->bmax) {
     case 16: hipLaunchKernelGGL(prodlda_fwd_kernel<16>, g, blk, sm, s, *m); break;
     case 32: hipLaunchKernelGGL(prodlda_fwd_kernel<32>, g, blk, sm, s, *m); break;
@@ -374,8 +412,8 @@ extern "C" int gfk_launch_prodlda_fwd(const GfkModel* m, hipStream_t s) {
 }
 
 extern "C" int gfk_launch_prodlda_bwd(const GfkModel* m, hipStream_t s) {
-  const size_t sm = gfk_prodlda_bwd_smem(m->bmax, m->K);
-  dim3 g(m->dec_grid), blk(DEC_THREADS);
+  const size_t sm = gfk_prodlda_bwd_smem(m);
+  dim3 g(m->n_tiles), blk(DEC_THREADS);
   switch (m->bmax) {
     case 16: hipLaunchKernelGGL(prodlda_bwd_kernel<16>, g, blk, sm, s, *m); break;
     case 32: hipLaunchKernelGGL(prodlda_bwd_kernel<32>, g, blk, sm, s, *m); break;

@@ -16,6 +16,7 @@ extern "C" {
 int gfk_launch_encoder_fwd(const GfkModel*, hipStream_t);
 int gfk_launch_encoder_bwd(const GfkModel*, hipStream_t);
 int gfk_launch_batch_docs(const GfkModel*, hipStream_t);
+int gfk_launch_batch_prep(const GfkModel*, hipStream_t);
 int gfk_launch_posterior_fwd(const GfkModel*, hipStream_t);
 int gfk_launch_posterior_bwd(const GfkModel*, hipStream_t);
 int gfk_launch_prodlda_fwd(const GfkModel*, hipStream_t);
@@ -26,8 +27,8 @@ int gfk_launch_lda_row(const GfkModel*, hipStream_t);
 int gfk_launch_lda_beta_bwd(const GfkModel*, hipStream_t);
 int gfk_launch_adam(const GfkAdam*, int, hipStream_t);
 int gfk_launch_scale(float*, int64_t, float, hipStream_t);
-size_t gfk_prodlda_fwd_smem(int, int);
-size_t gfk_prodlda_bwd_smem(int, int);
+size_t gfk_prodlda_fwd_smem(const GfkModel*);
+size_t gfk_prodlda_bwd_smem(const GfkModel*);
 size_t gfk_lda_fwd_smem(int);
 size_t gfk_lda_bwd_smem(int);
 size_t gfk_posterior_bwd_smem(const GfkModel*);
@@ -53,6 +54,7 @@ enum GfkPhase {
   GFK_PH_LDA_BETA_BWD = 9,
   GFK_PH_ENC_BWD = 10,
   GFK_PH_ADAM = 11,
+  GFK_PH_BATCH_PREP = 12,
 };
 
 
@@ -60,8 +62,8 @@ enum GfkPhase {
 // LDS each kernel family needs for this model; 0 means "does not fit".
 size_t gfk_smem_required(const GfkModel* m, int which) {
   switch (which) {
-    case 0: return gfk_prodlda_fwd_smem(m->bmax, m->K);
-    case 1: return gfk_prodlda_bwd_smem(m->bmax, m->K);
+    case 0: return gfk_prodlda_fwd_smem(m);
+    case 1: return gfk_prodlda_bwd_smem(m);
     case 2: return gfk_lda_fwd_smem(m->K);
     case 3: return gfk_lda_bwd_smem(m->K);
     case 4: return gfk_posterior_bwd_smem(m);
@@ -76,7 +78,7 @@ size_t gfk_smem_required(const GfkModel* m, int which) {
 // more than the 64 KiB default (MI355X has 160 KiB per CU).
 int gfk_setup(const GfkModel* m) {
   int e = 0;
-  size_t p = gfk_prodlda_fwd_smem(m->bmax, m->K), q = gfk_prodlda_bwd_smem(m->bmax, m->K);
+  size_t p = gfk_prodlda_fwd_smem(m), q = gfk_prodlda_bwd_smem(m);
   if ((e = gfk_prodlda_set_smem(p > q ? p : q))) return e;
   p = gfk_lda_fwd_smem(m->K);
   q = gfk_lda_bwd_smem(m->K);
@@ -104,6 +106,7 @@ int gfk_run(const GfkModel* m, const GfkAdam* a, int adam_grid, hipStream_t s,
       case GFK_PH_LDA_BETA_BWD: e = gfk_launch_lda_beta_bwd(m, s); break;
       case GFK_PH_ENC_BWD: e = gfk_launch_encoder_bwd(m, s); break;
       case GFK_PH_ADAM: e = gfk_launch_adam(a, adam_grid, s); break;
+      case GFK_PH_BATCH_PREP: e = gfk_launch_batch_prep(m, s); break;
       default: e = -2;
     }
     if (e) return e * 100 + phases[i];

@@ -65,13 +65,33 @@ def supports(tm, explain: bool = False) -> bool:
         if not _explain(ok, why, explain):
             return False
     bmax = next(b for b in BMAX_CHOICES if b >= tm.batch_size)
-    K = tm.n_components
-    hmax = max(tm.hidden_sizes)
-    kp = -(-K // 16) * 16
-    need = [4 * (2 * bmax * (kp + 1) + kp * (VB + 1) + 2 * bmax * (VB + 1) + bmax * VB),  # dec bwd
-            4 * (2 * bmax * K + 4 * K),                                                # post fwd
-            4 * (9 * K + 8 * K + 12 * hmax)]                                           # post bwd
-    return _explain(max(need) <= LDS_LIMIT, "LDS budget exceeded", explain)
+    need = lds_required(tm, bmax)
+    return _explain(need <= LDS_LIMIT, f"LDS budget exceeded ({need} B)", explain)
+
+
+def theta_stride(K: int) -> int:
+    """Row stride of the dropped-out theta workspace: K rounded up to 4 x odd, so
+    16 consecutive rows land on distinct LDS bank groups in the decoder MFMAs."""
+    kt = -(-K // 4) * 4
+    return kt + 4 if (kt // 4) % 2 == 0 else kt
+
+
+def lds_required(tm, bmax: int) -> int:
+    """Largest dynamic LDS any fused kernel needs for this model (weights unstaged),
+    as computed by the kernel library itself."""
+    m = abi.GfkModel()
+    hs = list(tm.hidden_sizes)
+    m.bmax, m.V, m.K, m.n_hidden = bmax, tm.input_size, tm.n_components, len(hs)
+    for i, h in enumerate(hs):
+        m.H[i] = h
+    m.kind = abi.KIND_PRODLDA if tm.model_type.lower() == "prodlda" else abi.KIND_LDA
+    m.kt = theta_stride(m.K)
+    m.vb, m.n_tiles = VB, -(-m.V // VB)
+    m.n_dpart = m.n_tiles if m.kind == abi.KIND_PRODLDA else 1
+    m.stage_flags = 0
+    lib = native.kernels()
+    which = (0, 1) if m.kind == abi.KIND_PRODLDA else (2, 3)
+    return int(max(lib.gfk_smem_required(C.byref(m), w) for w in which + (4, 5)))
 
 
 class FusedAdamState:
@@ -167,6 +187,18 @@ class FusedEngine(EngineBase):
             return flat.view(s.shape[1], s.shape[0]).t()
         return flat.view(s.shape)
 
+    def gradient(self, key: str) -> torch.Tensor:
+        """The pending gradient of parameter ``key`` (before Adam consumes it): slab
+        tensors are reduced here exactly as the fused Adam reduces them."""
+        if key in getattr(self, "slab_off", {}):
+            n = self.flat.slots[key].numel
+            o = self.slab_off[key]
+            slabs = self.slab.view(self.n_slab, self.slab_stride)[:, o:o + n]
+            g = slabs.sum(0)
+            s = self.flat.slots[key]
+            return g.view(s.shape[1], s.shape[0]).t() if s.transposed else g.view(s.shape)
+        return self.view_like(self.grad, key)
+
     def _ptr(self, buf, key):
         if key not in self.flat.slots:
             return None
@@ -191,6 +223,9 @@ class FusedEngine(EngineBase):
         props = torch.cuda.get_device_properties(self.device)
         m.dec_grid = int(min(m.n_tiles, 2 * props.multi_processor_count))
         m.learn_priors = int(tm.learn_priors)
+        m.kt = theta_stride(m.K)
+        m.scatter_chunks = 4
+        m.n_dpart = m.n_tiles if m.kind == abi.KIND_PRODLDA else 1
         m.drop_enc = float(net.dropout_enc.p)
         m.drop_theta = float(model.drop_theta.p)
         m.bn_momentum = float(model.beta_batchnorm.momentum)
@@ -246,24 +281,57 @@ class FusedEngine(EngineBase):
         m, dev = self._m, self.device
         B, K, V = self.bmax, m.K, m.V
         hs = [m.H[i] for i in range(m.n_hidden)]
-        f = lambda *s: torch.zeros(*s, dtype=torch.float32, device=dev)  # noqa: E731
+        def f(*shape):
+            # 16 floats of zeroed slack: LDS-DMA copies whole 16-byte chunks
+            n = int(np.prod(shape))
+            return torch.zeros(n + 16, dtype=torch.float32, device=dev)[:n].view(*shape)
+
         ws: Dict[str, torch.Tensor] = {
             "doc": torch.zeros(B, dtype=torch.int32, device=dev),
             "nb": torch.zeros(1, dtype=torch.int32, device=dev),
             "hd": f(B, hs[-1]), "mask_h": f(B, hs[-1]),
             "mu_raw": f(B, K), "ls_raw": f(B, K), "mu": f(B, K), "ls": f(B, K),
-            "bn_rstd": f(2 * K), "eps": f(B, K), "theta": f(B, K), "thetad": f(B, K),
+            "bn_rstd": f(2 * K), "eps": f(B, K), "theta": f(B, K), "thetad": f(B, m.kt),
             "mask_t": f(B, K), "kl": f(B), "rl": f(B), "lse": f(max(B, K)), "s": f(B),
-            "zn": f(B * V if m.kind == abi.KIND_PRODLDA else V * K), "col_rstd": f(V),
-            "row_part": f(m.dec_grid * max(B, K) * 2), "dthetad": f(B, K), "dz0": f(B, hs[0]),
+            "zn": f(m.n_tiles * B * VB if m.kind == abi.KIND_PRODLDA else V * K),
+            "col_rstd": f(m.n_tiles * VB),
+            "row_part": f(max(m.n_tiles * 4 * B, m.dec_grid * K) * 2),
+            "dthetad": f(m.n_dpart * B * K),
+            "dz0": f(B, hs[0]),
             "dmu": f(B, K), "dls": f(B, K), "colpart": f((B // 4) * 9 * K),
             "dbsm": f(V * K if m.kind == abi.KIND_LDA else 1), "ck": f(K),
             "hctx": f(B, hs[0]),
             "tstart": torch.zeros(B * (m.n_tiles + 1), dtype=torch.int32, device=dev),
+            "erange": torch.zeros(2 * B, dtype=torch.int32, device=dev),
+            "next": torch.zeros(1 + 3 * B, dtype=torch.int32, device=dev),
         }
         for i, h in enumerate(hs):
             ws[f"z{i}"] = f(B, h)
             ws[f"a{i}"] = f(B, h)
+        # per-workgroup gradient slabs of the small MLP tensors (posterior_bwd_mlp
+        # writes, Adam reduces): 16-float aligned, one slab per workgroup
+        self.slab_keys = ["inf_net.input_layer.bias"]
+        for l in range(len(hs) - 1):
+            self.slab_keys += [f"inf_net.hiddens.l_{l}.0.weight", f"inf_net.hiddens.l_{l}.0.bias"]
+        self.slab_keys += ["inf_net.f_mu.weight", "inf_net.f_mu.bias", "inf_net.f_sigma.weight",
+                           "inf_net.f_sigma.bias"]
+        up = lambda x: -(-x // ALIGN) * ALIGN  # noqa: E731
+        self.slab_off: Dict[str, int] = {}
+        off = 0
+        for k in self.slab_keys:
+            self.slab_off[k] = off
+            off += up(self.flat.slots[k].numel)
+        self.n_slab = B // 4                       # posterior_bwd_mlp workgroups (RPB = 4)
+        self.slab_stride = off
+        self.slab = f(self.n_slab * off)
+        sp = lambda k: self.slab.data_ptr() + 4 * self.slab_off[k]  # noqa: E731
+        m.s_b_in = sp("inf_net.input_layer.bias")
+        for l in range(len(hs) - 1):
+            m.s_w_h[l] = sp(f"inf_net.hiddens.l_{l}.0.weight")
+            m.s_b_h[l] = sp(f"inf_net.hiddens.l_{l}.0.bias")
+        m.s_w_mu, m.s_b_mu = sp("inf_net.f_mu.weight"), sp("inf_net.f_mu.bias")
+        m.s_w_s, m.s_b_s = sp("inf_net.f_sigma.weight"), sp("inf_net.f_sigma.bias")
+        m.slab_stride = off
         self.ws = ws
         for k, t in ws.items():
             if k[0] in "za" and k[1:].isdigit():
@@ -284,7 +352,12 @@ class FusedEngine(EngineBase):
         n_total = self.flat.n_total
         shared_end = up(self.flat.n_shared) if self.fedavg_scale is not None else 0
         pr = [(s0, up(s1)) for s0, s1 in self.flat.param_ranges()]
-        cuts = sorted({0, n_total, shared_end} | {x for r in pr for x in r})
+        slab_rng = {}
+        for k in self.slab_keys:
+            sl = self.flat.slots[k]
+            slab_rng[k] = (sl.offset, sl.offset + up(sl.numel))
+        cuts = sorted({0, n_total, shared_end} | {x for r in pr for x in r}
+                      | {x for r in slab_rng.values() for x in r})
         segs: List[List[int]] = []
         for x0, x1 in zip(cuts[:-1], cuts[1:]):
             if x1 <= x0:
@@ -296,17 +369,28 @@ class FusedEngine(EngineBase):
                 flags |= abi.SEG_SCALE
             if flags == 0:
                 continue
-            if segs and segs[-1][1] == x0 and segs[-1][2] == flags:
+            slab = None
+            for k, (r0, r1) in slab_rng.items():
+                if r0 <= x0 and x1 <= r1 and flags & abi.SEG_ADAM:
+                    slab = self.slab.data_ptr() + 4 * (self.slab_off[k] + x0 - r0)
+            if segs and segs[-1][1] == x0 and segs[-1][2] == flags and slab is None \
+                    and segs[-1][3] is None:
                 segs[-1][1] = x1
             else:
-                segs.append([x0, x1, flags])
+                segs.append([x0, x1, flags, slab])
         if len(segs) > abi.MAX_SEGS:
             raise RuntimeError("too many Adam segments")
         a.n_seg = len(segs)
-        for i, (s0, s1, fl) in enumerate(segs):
+        for i, (s0, s1, fl, slab) in enumerate(segs):
             a.seg_start[i], a.seg_end[i], a.seg_flags[i] = s0, s1, fl
-        n = sum(s1 - s0 for s0, s1, _ in segs) // 4
-        self.adam_grid = int(max(1, min(2048, -(-n // 256))))
+            a.seg_slab[i] = slab
+        a.slab_stride, a.n_slab = self.slab_stride, self.n_slab
+        # one workgroup per 1024 float4s of each segment (csrc/adam.hip block mapping)
+        nblk = 0
+        for i, sg in enumerate(segs):
+            a.seg_first_block[i] = nblk
+            nblk += -(-((sg[1] - sg[0]) // 4) // 1024)
+        self.adam_grid = int(max(1, nblk))
         self._invalidate_graph()
 
     def set_fedavg_scale(self, w: Optional[float]):
@@ -331,9 +415,16 @@ class FusedEngine(EngineBase):
         m.plan_start = self._plan_dev["start"].data_ptr()
         m.plan_size = self._plan_dev["size"].data_ptr()
         m.loss_hist = self.loss_hist.data_ptr()
+        m.n_steps = plan.n_steps
+        # wide scatter grid: 64 non-zeros per workgroup chunk, enough chunks for the
+        # longest document (rows loop over chunks beyond that)
+        lens = (data.indptr[1:] - data.indptr[:-1]).cpu().numpy()
+        maxlen = int(lens.max()) if len(lens) else 1
+        m.scatter_chunks = int(min(16, max(1, -(-maxlen // 64))))
         self.d_step.zero_()
         self._host_step = 0
         self._invalidate_graph()
+        self._launch([abi.PH_BATCH_PREP])
 
     def phases(self) -> List[int]:
         return abi.PRODLDA_STEP if self._m.kind == abi.KIND_PRODLDA else abi.LDA_STEP
@@ -380,6 +471,7 @@ class FusedEngine(EngineBase):
         if s != self._host_step:
             self.d_step.fill_(s)
             self._host_step = s
+            self._launch([abi.PH_BATCH_PREP])   # the step's batch is prepared by the previous one
 
     def step(self, s: int) -> torch.Tensor:
         if self.plan is None:

@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 
 MAX_LAYERS = 8
-MAX_SEGS = 32
+MAX_SEGS = 48
 P = C.c_void_p
 
 # activation / model / input codes
@@ -30,13 +30,14 @@ PH_POST_BWD = 8
 PH_LDA_BETA_BWD = 9
 PH_ENC_BWD = 10
 PH_ADAM = 11
+PH_BATCH_PREP = 12
 
-# PH_POST_BWD = posterior_bwd_rows + posterior_bwd_mlp (which also scatters the
-# sparse input-layer gradient, so PH_ENC_BWD is not part of the fused step)
+# PH_POST_BWD = posterior_bwd_rows + posterior_bwd_mlp; PH_ENC_BWD = the wide
+# sparse scatter of the input-layer gradient
 PRODLDA_STEP = [PH_ENC_FWD, PH_POST_FWD, PH_PRODLDA_FWD, PH_PRODLDA_LOSS, PH_PRODLDA_BWD,
-                PH_POST_BWD, PH_ADAM]
+                PH_POST_BWD, PH_ENC_BWD, PH_ADAM]
 LDA_STEP = [PH_LDA_BETA_FWD, PH_ENC_FWD, PH_POST_FWD, PH_LDA_ROW, PH_POST_BWD, PH_LDA_BETA_BWD,
-            PH_ADAM]
+            PH_ENC_BWD, PH_ADAM]
 
 SEG_ADAM, SEG_SCALE = 1, 2
 
@@ -47,7 +48,8 @@ class GfkModel(C.Structure):
         ("H", C.c_int32 * MAX_LAYERS),
         ("act", C.c_int32), ("kind", C.c_int32), ("input", C.c_int32), ("C", C.c_int32),
         ("L", C.c_int32), ("vb", C.c_int32), ("n_tiles", C.c_int32), ("dec_grid", C.c_int32),
-        ("learn_priors", C.c_int32), ("stage_flags", C.c_int32),
+        ("learn_priors", C.c_int32), ("stage_flags", C.c_int32), ("kt", C.c_int32),
+        ("scatter_chunks", C.c_int32), ("n_dpart", C.c_int32), ("n_steps", C.c_int32),
         ("drop_enc", C.c_float), ("drop_theta", C.c_float), ("bn_momentum", C.c_float),
         ("bn_eps", C.c_float), ("kl_weight", C.c_float), ("pad1", C.c_float),
         ("seed", C.c_uint64),
@@ -59,16 +61,19 @@ class GfkModel(C.Structure):
         ("g_prior_mean", P), ("g_prior_var", P), ("g_beta", P), ("g_w_in", P), ("g_b_in", P),
         ("g_w_h", P * MAX_LAYERS), ("g_b_h", P * MAX_LAYERS),
         ("g_w_mu", P), ("g_b_mu", P), ("g_w_s", P), ("g_b_s", P),
+        ("s_b_in", P), ("s_w_h", P * MAX_LAYERS), ("s_b_h", P * MAX_LAYERS),
+        ("s_w_mu", P), ("s_b_mu", P), ("s_w_s", P), ("s_b_s", P), ("slab_stride", C.c_int64),
         ("indptr", P), ("indices", P), ("values", P), ("ctx", P),
         ("plan_order", P), ("plan_start", P), ("plan_size", P),
         ("step", P), ("adam_t", P), ("loss_hist", P),
         ("ws_doc", P), ("ws_nb", P), ("ws_z", P * MAX_LAYERS), ("ws_a", P * MAX_LAYERS), ("ws_hd", P), ("ws_mask_h", P),
         ("ws_mu_raw", P), ("ws_ls_raw", P), ("ws_mu", P), ("ws_ls", P), ("ws_bn_rstd", P),
-        ("ws_eps", P), ("ws_theta", P), ("ws_thetad", P), ("ws_mask_t", P),
+        ("ws_eps", P), ("ws_theta", P), ("ws_mask_t", P), ("ws_thetad", P),
         ("ws_kl", P), ("ws_rl", P), ("ws_lse", P), ("ws_s", P),
         ("ws_zn", P), ("ws_col_rstd", P), ("ws_row_part", P), ("ws_dthetad", P), ("ws_dz0", P),
         ("ws_dmu", P), ("ws_dls", P), ("ws_colpart", P),
-        ("ws_dbsm", P), ("ws_ck", P), ("ws_hctx", P), ("ws_tstart", P), ("dbg", P),
+        ("ws_dbsm", P), ("ws_ck", P), ("ws_hctx", P), ("ws_tstart", P), ("ws_erange", P),
+        ("ws_next", P), ("dbg", P),
     ]
 
 
@@ -81,6 +86,9 @@ class GfkAdam(C.Structure):
         ("lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float),
         ("weight_decay", C.c_float), ("scale", C.c_float),
         ("t", P),
+        ("seg_slab", P * MAX_SEGS), ("seg_first_block", C.c_int32 * MAX_SEGS),
+        ("slab_stride", C.c_int64), ("n_slab", C.c_int32),
+        ("pad2", C.c_int32), ("dbg", P),
     ]
 
 

@@ -55,7 +55,7 @@ def _check_grads(g, ref):
 
 def _grads_of(tm_fused):
     e = tm_fused.engine
-    return {k: e.view_like(e.grad, k).detach().clone() for k, _ in e.param_order}
+    return {k: e.gradient(k).detach().clone() for k, _ in e.param_order}
 
 
 @pytest.mark.parametrize("model_type", ["prodLDA", "LDA"])

@@ -32,14 +32,19 @@ data = DeviceCSR(X, "cuda")
 tm.engine.bind_data(data, BatchPlan.build(1000, 64, 50))
 dbg = torch.zeros(64, dtype=torch.int64, device="cuda")
 tm.engine._m.dbg = dbg.data_ptr()
+tm.engine._a.dbg = dbg.data_ptr()
 for s in range(20):
     tm.engine.step(s)
 torch.cuda.synchronize()
 d = dbg.cpu().numpy()
 print("posterior_fwd cycles:", {n: int(d[i + 1] - d[i]) for i, n in enumerate(["stage", "colstats", "rows"])})
 print("posterior_bwd_rows cycles:", int(d[9] - d[8]))
-print("posterior_bwd_mlp cycles:", {n: int(d[11 + i] - d[10 + i]) for i, n in enumerate(["loads", "bn_bwd", "heads", "layers+dz0", "scatter"])})
-nf = ["nb+theta", "beta_tile", "mfma", "bn", "store+rowlse", "partial_store"]
-print("prodlda_fwd cycles:", {nf[i]: int(d[17 + i] - d[16 + i]) for i in range(6)})
-nbw = ["theta+zn", "x_tile", "dzn", "bn_bwd", "mfma x2", "atomics"]
-print("prodlda_bwd cycles:", {nbw[i]: int(d[25 + i] - d[24 + i]) for i in range(6)})
+print("posterior_bwd_mlp cycles:", {n: int(d[11 + i] - d[10 + i]) for i, n in enumerate(["loads", "bn_bwd", "heads", "layers+dz0"])})
+nf = ["stage", "mfma", "bn", "store+rowlse"]
+print("prodlda_fwd cycles:", {nf[i]: int(d[17 + i] - d[16 + i]) for i in range(4)})
+nbw = ["stage", "sparse", "dense+bn_bwd", "mfma+atomics"]
+print("prodlda_bwd cycles:", {nbw[i]: int(d[25 + i] - d[24 + i]) for i in range(4)})
+d16 = int(d[16])
+print("prodlda_fwd staging detail (cycles from kernel start): glds issued", int(d[21]) - d16,
+      "| scalars+nb", int(d[22]) - d16, "| beta staged", int(d[23]) - d16, "| barrier", int(d[17]) - d16)
+print("adam cycles: prologue+segment", int(d[33] - d[32]), "| body", int(d[34] - d[33]))
