@@ -1,37 +1,42 @@
-// Per-document encoder forward: sparse gather of the input layer, hidden MLP,
-// encoder dropout and the (pre-batch-norm) mu / log-sigma^2 heads; and the
-// standalone backward scatter into the transposed input-layer weight.
+// Encoder forward, one workgroup per document row: the sparse BoW gather
+// z0 = x W_in^T + b_in, the hidden MLP, the encoder dropout and the (pre
+// batch-norm) mu / log-sigma^2 heads -- plus all random draws of the row.
 //
-// Reference math: inference_network.py:76-85 (AVITM), ctm inference_network.py:176-193.
+// Reference math: inference_network.py:76-85 (AVITM), ctm inference_network.py:176-193
+// (the dense contextual part of CombinedTM / ZeroShotTM arrives precomputed in
+// ws_hctx); the draws are avitm decoder_network.py:102-118 (reparameterisation
+// noise, theta dropout) and inference_network.py:82 (encoder dropout).
 //
-// One 256-thread workgroup (4 waves) owns one document, so the bmax rows of a
-// minibatch run on bmax CUs in parallel.  The input layer is stored transposed
-// ([V, H0] row-major): every non-zero token gathers ONE contiguous 4*H0-byte
-// row.  Each wave takes the document's non-zeros 16 at a time: lanes 0-15 load
-// 16 (index, count) pairs with one instruction, the pairs are broadcast with
-// __shfl and the 16 row loads are issued back to back (16 loads in flight per
-// lane instead of a dependent index->row chain per token).  The MLP weights are
-// staged into LDS with 16 independent loads per thread, issued BEFORE the
-// gather so both round trips overlap.
+// One workgroup of 16 waves owns one document, so a minibatch of B rows runs on
+// B CUs with 16 * B waves.  The input layer is stored TRANSPOSED ([V, H0]
+// row-major): every non-zero token gathers one contiguous 4*H0-byte row.  Wave w
+// takes non-zeros [e0 + 64w + 1024r, +64): one lane-parallel load of the 64
+// (index, count) pairs, then the W rows CH at a time, all in flight (the pair is
+// broadcast with v_readlane into SGPRs, so the row address is scalar).  The
+// per-wave partial rows are summed through LDS.
+//
+// The batch itself (nb, doc ids, CSR extents) was prepared by the previous step
+// (prepare_next_batch), so the row's CSR extent is one round trip away.  The
+// random draws (Philox, keyed by seed/step/element) are produced here, where the
+// VALU is otherwise idle waiting on the gather.  Everything up to the heads is
+// row-local; the batch coupling (batch-norm) starts in post_fwd.
 #include "gfk_common.h"
 
 using namespace gfk;
 
 namespace {
 
-constexpr int ENC_THREADS = 256;
-constexpr int CH = 16;        // non-zeros per wave batch
+constexpr int ENC_THREADS = 1024;
+constexpr int ENC_WAVES = ENC_THREADS / 64;
 
 // acc[q] (output j = lane + 64*q) += sum over this wave's non-zeros of x * W[v, j].
-// Wave w takes non-zeros [e0 + 64w + 256r, +64): ONE lane-parallel load of the 64
-// (index, count) pairs, then the W rows are loaded CH at a time, all in flight.
 template <int NQ>
 __device__ __forceinline__ void gather_rows(const int32_t* __restrict__ idx,
                                             const float* __restrict__ val, int e0, int e1,
                                             int wave, const float* __restrict__ w, int H,
                                             int lane, float* acc) {
-  constexpr int CH = NQ == 1 ? 32 : (NQ == 2 ? 16 : 8);
-  for (int base = e0 + wave * 64; base < e1; base += 256) {
+  constexpr int CH = NQ == 1 ? 16 : (NQ == 2 ? 8 : 4);
+  for (int base = e0 + wave * 64; base < e1; base += ENC_WAVES * 64) {
     const int e = min(base + lane, e1 - 1);
     const int my_v = idx[e];
     const float my_x = (base + lane < e1) ? val[e] : 0.f;
@@ -40,35 +45,28 @@ __device__ __forceinline__ void gather_rows(const int32_t* __restrict__ idx,
       float wv[CH][NQ];
 #pragma unroll
       for (int i = 0; i < CH; ++i) {
-        const int v = __shfl(my_v, g + i, 64);
+        const int v = __builtin_amdgcn_readlane(my_v, min(g + i, 63));
+        const float* wr = w + (size_t)v * H;
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) wv[i][q] = w[(size_t)v * H + min(lane + 64 * q, H - 1)];
+        for (int q = 0; q < NQ; ++q) wv[i][q] = wr[min(lane + 64 * q, H - 1)];
       }
 #pragma unroll
       for (int i = 0; i < CH; ++i) {
-        const float x = __shfl(my_x, g + i, 64);
+        const float x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_x), min(g + i, 63)));
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) acc[q] += x * wv[i][q];
+        for (int q = 0; q < NQ; ++q) acc[q] += (g + i < cnt ? x : 0.f) * wv[i][q];
       }
     }
   }
 }
 
-__host__ __device__ inline int pad4(int x) { return (x + 3) & ~3; }
-
-__host__ __device__ inline int hmax_of(const GfkModel& m) {
-  int h = 0;
-#pragma unroll
-  for (int l = 0; l < GFK_MAX_LAYERS; ++l)
-    if (l < m.n_hidden) h = h > m.H[l] ? h : m.H[l];
-  return h;
-}
-
 }  // namespace
 
-// Floats of the staged encoder weights: hidden layers (W, b), then heads (W_mu,
-// b_mu, W_s, b_s), each padded to a multiple of 4.
-__host__ __device__ inline int enc_weights_floats(const GfkModel& m) {
+__host__ __device__ inline int pad4(int x) { return (x + 3) & ~3; }
+
+// Floats of the staged MLP weights: per hidden layer [W (pad4) | b (pad4)], then
+// W_mu, b_mu, W_s, b_s (pad4 each) -- the LDS-DMA destination layout.
+__host__ __device__ inline int enc_weight_floats(const GfkModel& m) {
   int n = 0;
 #pragma unroll
   for (int l = 0; l + 1 < GFK_MAX_LAYERS; ++l)
@@ -77,69 +75,85 @@ __host__ __device__ inline int enc_weights_floats(const GfkModel& m) {
   return n + 2 * (pad4(m.K * Hl) + pad4(m.K));
 }
 
-extern "C" size_t gfk_encoder_fwd_smem(const GfkModel* m) {
-  size_t n = 4 * (size_t)m->H[0] + 2 * (size_t)hmax_of(*m);
-  if (m->stage_flags & 1) n += enc_weights_floats(*m);
+__host__ __device__ inline int enc_hmax(const GfkModel& m) {
+  int h = 0;
+#pragma unroll
+  for (int l = 0; l < GFK_MAX_LAYERS; ++l)
+    if (l < m.n_hidden) h = h > m.H[l] ? h : m.H[l];
+  return h;
+}
+
+// dynamic LDS: red[16][H0] + act[2][hmax] + mask[Hl] (+ staged weights)
+extern "C" size_t gfk_enc_in_smem(const GfkModel* m) {
+  size_t n = (size_t)ENC_WAVES * m->H[0] + 2 * (size_t)pad4(enc_hmax(*m)) + pad4(m->H[m->n_hidden - 1]);
+  if (m->stage_flags & 1) n += enc_weight_floats(*m);
   return sizeof(float) * n;
 }
 
+// out[j] = sum_i W[j][i] x[i] (+ bias) for j < n_out: 16 lanes (one DPP row) per
+// output split the inputs, 64 outputs per pass of the workgroup.
+template <class Epi>
+__device__ __forceinline__ void rowvec_gemv(const float* W, const float* x, int n_out, int n_in, int tid,
+                                            Epi epi) {
+  const int s = tid & 15;
+  for (int j0 = 0; j0 < n_out; j0 += ENC_THREADS / 16) {
+    const int j = j0 + (tid >> 4);
+    float acc = 0.f;
+    if (j < n_out) {
+      const float* wr = W + (size_t)j * n_in;
+      for (int i = s; i < n_in; i += 16) acc += wr[i] * x[i];
+    }
+    acc = row16_sum(acc);
+    if (s == 0 && j < n_out) epi(j, acc);
+  }
+}
+
 // grid: bmax workgroups (one per batch row); rows >= nb exit.
-// dynamic LDS: red[4*H0] + a_cur[hmax] + a_nxt[hmax] (+ staged weights)
 //
-// Round trips: (1) kernel arguments (pinned in SGPRs up front), (2) the batch
-// prepared by the previous step (nb, doc, CSR extent) + the step counter, with
-// the weight staging (LDS-DMA) in flight, (3) the row's (index, count) pairs,
-// (4) the W_in rows.  Everything after that is LDS.
-extern "C" __global__ void __launch_bounds__(ENC_THREADS)
-gfk_encoder_fwd(GfkModel m) {
+// Round trips: the kernel arguments, then ONE round for the prepared batch row
+// (nb, doc, CSR extent), the step, the biases and the LDS-DMA staging of every MLP
+// weight; then the row's (index, count) pairs and the W_in rows.  After the
+// gather the whole MLP (hidden layers, dropout, mu / log-sigma heads) runs out of
+// LDS with LDS-only barriers: its global stores are never waited on.
+extern "C" __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in(GfkModel m) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int b = blockIdx.x, tid = threadIdx.x;
   const int lane = tid & 63, wave = uniform(tid >> 6);
-  // ---- prologue: every argument field used before the first barrier ----
-  int H0 = m.H[0], H1 = m.H[1], H2 = m.H[2], nh = m.n_hidden, K = m.K, sflags = m.stage_flags;
-  int bmax = m.bmax;
-  const int32_t* nxt = m.ws_next;
-  const int32_t* indices = m.indices;
-  const float* values = m.values;
-  const float* w_in = m.w_in;
-  const int32_t* stepp = m.step;
-  const float *w_h0 = m.w_h[0], *b_h0 = m.b_h[0], *w_h1 = m.w_h[1], *b_h1 = m.b_h[1];
-  const float *w_mu = m.w_mu, *b_mu = m.b_mu, *w_s = m.w_s, *b_s = m.b_s;
-  keep(H0, H1, H2, nh, K, sflags, bmax, nxt, indices, values, w_in, stepp, w_h0, b_h0, w_h1, b_h1,
-       w_mu, b_mu, w_s, b_s);
-  const int Hl = m.H[nh - 1], hm = hmax_of(m);
+  int H0 = m.H[0], K = m.K, bmax = m.bmax, nh = m.n_hidden, input = m.input, sflags = m.stage_flags;
+  const int32_t *nxt = m.ws_next, *indices = m.indices, *stepp = m.step;
+  const float *values = m.values, *w_in = m.w_in, *b_in = m.b_in;
+  keep(H0, K, bmax, nh, input, sflags, nxt, indices, stepp, values, w_in, b_in);
+  const int Hl = m.H[nh - 1], hm = enc_hmax(m);
   float* red = smem;
-  float* a_cur = red + 4 * H0;
-  float* a_nxt = a_cur + hm;
+  float* act0 = red + ENC_WAVES * H0;
+  float* act1 = act0 + pad4(hm);
+  float* maskh = act1 + pad4(hm);
+  float* wst = maskh + pad4(Hl);
   const bool staged = sflags & 1;
 
-  // ---- the batch row (prepared by the previous step) and the weight staging ----
-  const int nb = nxt[0];
-  const int doc = nxt[1 + min(b, bmax - 1)];
-  const int e0 = nxt[1 + bmax + 2 * b], e1 = nxt[2 + bmax + 2 * b];
-  const int step = *stepp;
-  // layout: per hidden layer [W (pad4) | b (pad4)], then W_mu, b_mu, W_s, b_s
-  float* wst = a_nxt + hm;
-  if (staged) {   // LDS-DMA: all copies in flight at once, drained by the first barrier
+  // ---- one round: the row, the step, the weights (LDS-DMA), the biases ----
+  if (staged) {
     float* p = wst;
 #pragma unroll
     for (int l = 0; l + 1 < GFK_MAX_LAYERS; ++l) {
       if (l + 1 < nh) {
-        const int hi = l == 0 ? H0 : (l == 1 ? H1 : m.H[l]);
-        const int ho = l == 0 ? H1 : (l == 1 ? H2 : m.H[l + 1]);
-        const float* W = l == 0 ? w_h0 : (l == 1 ? w_h1 : m.w_h[l]);
-        const float* Bv = l == 0 ? b_h0 : (l == 1 ? b_h1 : m.b_h[l]);
-        glds_copy(p, W, ho * hi, tid, ENC_THREADS); p += pad4(ho * hi);
-        glds_copy(p, Bv, ho, tid, ENC_THREADS); p += pad4(ho);
+        const int nw = m.H[l + 1] * m.H[l], nbias = m.H[l + 1];
+        glds_copy(p, m.w_h[l], nw, tid, ENC_THREADS); p += pad4(nw);
+        glds_copy(p, m.b_h[l], nbias, tid, ENC_THREADS); p += pad4(nbias);
       }
     }
-    glds_copy(p, w_mu, K * Hl, tid, ENC_THREADS); p += pad4(K * Hl);
-    glds_copy(p, b_mu, K, tid, ENC_THREADS); p += pad4(K);
-    glds_copy(p, w_s, K * Hl, tid, ENC_THREADS); p += pad4(K * Hl);
-    glds_copy(p, b_s, K, tid, ENC_THREADS);
+    glds_copy(p, m.w_mu, K * Hl, tid, ENC_THREADS); p += pad4(K * Hl);
+    glds_copy(p, m.b_mu, K, tid, ENC_THREADS); p += pad4(K);
+    glds_copy(p, m.w_s, K * Hl, tid, ENC_THREADS); p += pad4(K * Hl);
+    glds_copy(p, m.b_s, K, tid, ENC_THREADS);
   }
+  const int nb = nxt[0];
+  const int doc = nxt[1 + min(b, bmax - 1)];
+  const int e0 = nxt[1 + bmax + 2 * b], e1 = nxt[2 + bmax + 2 * b];
+  const int step = *stepp;
+  const float bias = b_in[min(tid, H0 - 1)];
   if (b >= nb) {            // drain the LDS-DMA before the workgroup retires
-    __syncthreads();
+    vm_barrier();
     return;
   }
   if (tid == 0) {           // publish the batch for the rest of the step
@@ -149,9 +163,8 @@ gfk_encoder_fwd(GfkModel m) {
     if (b == 0) *m.ws_nb = nb;
   }
 
-  // ---- input layer: BoW gather (+ dense contextual part precomputed in ws_hctx) ----
-  const bool has_bow = m.input != GFK_IN_CONTEXTUAL;
-  if (has_bow) {
+  // ---- sparse gather ----
+  if (input != GFK_IN_CONTEXTUAL) {
     float acc[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) acc[q] = 0.f;
@@ -165,115 +178,107 @@ gfk_encoder_fwd(GfkModel m) {
       if (j < H0) red[wave * H0 + j] = acc[q];
     }
   }
-  __syncthreads();
-  for (int j = tid; j < H0; j += ENC_THREADS) {
-    float z = m.b_in[j];
-    if (has_bow) z += red[j] + red[H0 + j] + red[2 * H0 + j] + red[3 * H0 + j];
-    if (m.input != GFK_IN_BOW) z += m.ws_hctx[(size_t)b * H0 + j];
-    const float a = act_f(m.act, z);
-    m.ws_z[0][(size_t)b * H0 + j] = z;
-    m.ws_a[0][(size_t)b * H0 + j] = a;
-    a_cur[j] = a;
-  }
-  __syncthreads();
 
-  // ---- hidden layers: z_{l+1} = W_l a_l + b_l ----
-  float* ain = a_cur;
-  float* aout = a_nxt;
+  // ---- per vocab tile (64 words): the CSR position of the row's first non-zero ----
+  {
+    int32_t* ts = m.ws_tstart + (size_t)b * (m.n_tiles + 1);
+    for (int e = e0 + tid; e < e1; e += ENC_THREADS) {
+      const int t = indices[e] >> 6;
+      const int tp = e > e0 ? (indices[e - 1] >> 6) : -1;
+      for (int u = tp + 1; u <= t; ++u) ts[u] = e;
+    }
+    const int last = e1 > e0 ? (indices[e1 - 1] >> 6) : -1;
+    for (int u = last + 1 + tid; u <= m.n_tiles; u += ENC_THREADS) ts[u] = e1;
+  }
+
+  // ---- the row's random draws for this step ----
+  for (int t = tid; t < 2 * K + Hl; t += ENC_THREADS) {
+    if (t < K) {
+      const uint32_t i = (uint32_t)(b * K + t);
+      m.ws_eps[i] = randn(m.seed, (uint32_t)step, RNG_EPS, i);
+    } else if (t < 2 * K) {
+      const uint32_t i = (uint32_t)(b * K + t - K);
+      m.ws_mask_t[i] = drop_scale(m.seed, (uint32_t)step, RNG_DROP_THETA, i, m.drop_theta);
+    } else {
+      const uint32_t i = (uint32_t)(b * Hl + t - 2 * K);
+      const float s = drop_scale(m.seed, (uint32_t)step, RNG_DROP_ENC, i, m.drop_enc);
+      m.ws_mask_h[i] = s;
+      maskh[t - 2 * K] = s;
+    }
+  }
+  vm_barrier();             // gather partials + staged weights
+
+  // ---- input layer: z0 = sum of the wave partials + bias (+ dense contextual part) ----
+  const int act = m.act;
+  if (tid < H0) {
+    float z = bias;
+    if (input != GFK_IN_CONTEXTUAL) {
+#pragma unroll
+      for (int w = 0; w < ENC_WAVES; ++w) z += red[w * H0 + tid];
+    }
+    if (input != GFK_IN_BOW) z += m.ws_hctx[(size_t)b * H0 + tid];
+    float a = act_f(act, z);
+    m.ws_z[0][(size_t)b * H0 + tid] = z;
+    m.ws_a[0][(size_t)b * H0 + tid] = a;
+    if (nh == 1) {
+      a *= maskh[tid];
+      m.ws_hd[(size_t)b * H0 + tid] = a;
+    }
+    act0[tid] = a;
+  }
+  lds_barrier();
+
+  // ---- hidden layers ----
+  float* ain = act0;
+  float* aout = act1;
   const float* wcur = wst;
-  for (int l = 0; l + 1 < nh; ++l) {
+#pragma unroll
+  for (int l = 0; l + 1 < GFK_MAX_LAYERS; ++l) {
+    if (l + 1 >= nh) break;
     const int Hi = m.H[l], Ho = m.H[l + 1];
     const float* W = staged ? wcur : m.w_h[l];
     const float* Bv = staged ? wcur + pad4(Ho * Hi) : m.b_h[l];
     wcur += pad4(Ho * Hi) + pad4(Ho);
-    for (int j = tid; j < Ho; j += ENC_THREADS) {
-      float z = Bv[j];
-      const float* wr = W + (size_t)j * Hi;
-#pragma unroll 8
-      for (int i = 0; i < Hi; ++i) z += wr[i] * ain[i];
-      const float a = act_f(m.act, z);
-      m.ws_z[l + 1][(size_t)b * Ho + j] = z;
-      m.ws_a[l + 1][(size_t)b * Ho + j] = a;
+    const bool last = l + 2 == nh;
+    float* zo = m.ws_z[l + 1] + (size_t)b * Ho;
+    float* ao = m.ws_a[l + 1] + (size_t)b * Ho;
+    float* hdo = m.ws_hd + (size_t)b * Ho;
+    rowvec_gemv(W, ain, Ho, Hi, tid, [&](int j, float acc) {
+      const float z = acc + Bv[j];
+      float a = act_f(act, z);
+      zo[j] = z;
+      ao[j] = a;
+      if (last) {
+        a *= maskh[j];
+        hdo[j] = a;
+      }
       aout[j] = a;
-    }
-    __syncthreads();
+    });
+    lds_barrier();
     float* t = ain; ain = aout; aout = t;
   }
 
-  // ---- encoder dropout (p fixed at 0.2 in the reference) ----
-  for (int j = tid; j < Hl; j += ENC_THREADS) {
-    const float s = drop_scale(m.seed, (uint32_t)step, RNG_DROP_ENC, (uint32_t)(b * Hl + j),
-                               m.drop_enc);
-    const float hd = ain[j] * s;
-    m.ws_mask_h[(size_t)b * Hl + j] = s;
-    m.ws_hd[(size_t)b * Hl + j] = hd;
-    aout[j] = hd;
-  }
-  __syncthreads();
-
-  // ---- mu / log-sigma heads (pre-BN) ----
-  const float* Wmu = staged ? wcur : w_mu;
-  const float* Bmu = staged ? wcur + pad4(K * Hl) : b_mu;
-  const float* Ws = staged ? wcur + pad4(K * Hl) + pad4(K) : w_s;
-  const float* Bs = staged ? wcur + 2 * pad4(K * Hl) + pad4(K) : b_s;
-  for (int t = tid; t < 2 * K; t += ENC_THREADS) {
-    const bool is_mu = t < K;
-    const int k = is_mu ? t : t - K;
-    const float* wr = (is_mu ? Wmu : Ws) + (size_t)k * Hl;
-    float z = is_mu ? Bmu[k] : Bs[k];
-#pragma unroll 8
-    for (int j = 0; j < Hl; ++j) z += wr[j] * aout[j];
-    (is_mu ? m.ws_mu_raw : m.ws_ls_raw)[(size_t)b * K + k] = z;
-  }
+  // ---- mu / log-sigma heads (pre batch-norm) ----
+  const float* Wmu = staged ? wcur : m.w_mu;
+  const float* Bmu = staged ? wcur + pad4(K * Hl) : m.b_mu;
+  const float* Ws = staged ? wcur + pad4(K * Hl) + pad4(K) : m.w_s;
+  const float* Bs = staged ? wcur + 2 * pad4(K * Hl) + pad4(K) : m.b_s;
+  float* mr = m.ws_mu_raw + (size_t)b * K;
+  float* lr = m.ws_ls_raw + (size_t)b * K;
+  rowvec_gemv(Wmu, ain, K, Hl, tid, [&](int k, float acc) { mr[k] = acc + Bmu[k]; });
+  rowvec_gemv(Ws, ain, K, Hl, tid, [&](int k, float acc) { lr[k] = acc + Bs[k]; });
 }
 
-// Standalone backward of the sparse input layer (the fused step does this
-// inside gfk_posterior_bwd): g_w_in[v, :] += x_bv * dz0[b, :].  Float atomics
-// (a word shared by several documents of the batch hits the same row); each
-// wave instruction adds one contiguous 4*H0-byte row.  grid: bmax workgroups.
-extern "C" __global__ void __launch_bounds__(ENC_THREADS)
-gfk_encoder_bwd_scatter(GfkModel m) {
-  // grid (bmax, scatter_chunks): workgroup (b, y) takes chunks y, y + gridDim.y, ...
-  // of 64 non-zeros of row b; each wave owns 16 of them, so every wave has at
-  // most 16 * ceil(H0/64) atomics in flight and the whole scatter is one round.
-  const int b = blockIdx.x;
-  const int nb = *m.ws_nb;
-  if (b >= nb) return;
-  const int H0 = m.H[0];
-  const int lane = threadIdx.x & 63, wave = uniform(threadIdx.x >> 6);
-  const float* dz = m.ws_dz0 + (size_t)b * H0;
-  const int e0 = m.ws_erange[2 * b], e1 = m.ws_erange[2 * b + 1];
-  for (int base = e0 + (blockIdx.y * 4 + wave) * CH; base < e1; base += gridDim.y * 4 * CH) {
-    const int e = min(base + (lane & (CH - 1)), e1 - 1);
-    const int my_v = m.indices[e];
-    const float my_x = m.values[e];
-    const int cnt = min(CH, e1 - base);
-    for (int j0 = 0; j0 < H0; j0 += 64) {
-      const int j = j0 + lane;
-      const float d = dz[min(j, H0 - 1)];
-#pragma unroll
-      for (int i = 0; i < CH; ++i) {
-        const int v = __shfl(my_v, i, 64);
-        const float x = __shfl(my_x, i, 64);
-        if (i < cnt && j < H0) atomicAdd(m.g_w_in + (size_t)v * H0 + j, x * d);
-      }
-    }
-  }
-}
-
-extern "C" int gfk_launch_encoder_fwd(const GfkModel* m, hipStream_t s) {
-  hipLaunchKernelGGL(gfk_encoder_fwd, dim3(m->bmax), dim3(ENC_THREADS), gfk_encoder_fwd_smem(m), s,
-                     *m);
+extern "C" int gfk_launch_enc_in(const GfkModel* m, hipStream_t s) {
+  hipLaunchKernelGGL(gfk_enc_in, dim3(m->bmax), dim3(ENC_THREADS), gfk_enc_in_smem(m), s, *m);
   return (int)hipGetLastError();
 }
 
-extern "C" int gfk_launch_encoder_bwd(const GfkModel* m, hipStream_t s) {
-  const int gy = m->scatter_chunks > 0 ? m->scatter_chunks : 1;
-  hipLaunchKernelGGL(gfk_encoder_bwd_scatter, dim3(m->bmax, gy), dim3(ENC_THREADS), 0, s, *m);
-  return (int)hipGetLastError();
+extern "C" int gfk_enc_in_set_smem(size_t bytes) {
+  return (int)hipFuncSetAttribute((const void*)gfk_enc_in, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)bytes);
 }
 
-extern "C" int gfk_encoder_set_smem(size_t bytes) {
-  return (int)hipFuncSetAttribute((const void*)gfk_encoder_fwd,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+extern "C" size_t gfk_enc_weight_bytes(const GfkModel* m) {
+  return sizeof(float) * (size_t)enc_weight_floats(*m);
 }

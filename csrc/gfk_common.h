@@ -65,12 +65,6 @@ typedef struct GfkModel {
   float *g_prior_mean, *g_prior_var, *g_beta, *g_w_in, *g_b_in;
   float *g_w_h[GFK_MAX_LAYERS], *g_b_h[GFK_MAX_LAYERS];
   float *g_w_mu, *g_b_mu, *g_w_s, *g_b_s;
-  // Gradient slabs: posterior_bwd_mlp workgroup g writes its partial gradient of
-  // the small MLP tensors with plain stores at s_* + g * slab_stride; the fused
-  // Adam reduces the slabs in a fixed order (deterministic, no atomics).
-  float *s_b_in, *s_w_h[GFK_MAX_LAYERS], *s_b_h[GFK_MAX_LAYERS];
-  float *s_w_mu, *s_b_mu, *s_w_s, *s_b_s;
-  int64_t slab_stride;
 
   // ---- data (device-resident CSR shard + batch plan) ----
   const int32_t *indptr, *indices;
@@ -99,9 +93,9 @@ typedef struct GfkModel {
   float *ws_col_rstd;            // [n_tiles * 64] (ProdLDA: over batch; LDA: over topics)
   float *ws_row_part;            // online (max, sumexp) partials: ProdLDA [n_tiles*4, bmax, 2], LDA [dec_grid, K, 2]
   float *ws_dthetad;             // [n_dpart, bmax, K] d theta_d partials (plain stores, reduced in order)
-  float *ws_dz0;                 // [bmax, H0]
+  float *ws_dz[GFK_MAX_LAYERS];  // d pre-activation of each hidden layer [bmax, H[l]] (l = 0: input layer)
+  float *ws_dmr, *ws_dlr;        // [bmax, K] d mu_raw / d log-sigma_raw (BN backward of the heads)
   float *ws_dmu, *ws_dls;        // [bmax, K] dL/d(post-BN mu, log-sigma)
-  float *ws_colpart;             // [bmax/4, 9, K] per-workgroup column sums (posterior bwd)
   float *ws_dbsm;                // LDA: d softmax(beta)^T accumulator [V, K]
   float *ws_ck;                  // LDA: [K] sum_v beta_sm * d beta_sm
   float *ws_hctx;                // CTM: dense contextual contribution to layer 0 [bmax, H0]
@@ -110,7 +104,44 @@ typedef struct GfkModel {
   int32_t *ws_next;              // [1 + 3*bmax] next batch, prepared during the previous step:
                                  //   nb, doc[bmax], (e0, e1)[bmax]
   uint64_t *dbg;                 // diagnostic s_memtime stamps (GFK_STAMPS builds only)
+
+  // ---- update (fused Adam epilogues) ----
+  float lr, beta1, beta2, adam_eps, weight_decay, fed_scale;
+  int32_t update_mode;           // 0: kernels write gradients (generic Adam follows); 1: fused Adam
+  int32_t fed_scale_on;          // multiply shared tensors (flat offset < n_shared) by fed_scale
+  float *flat_base;              // the parameter flat buffer
+  int64_t n_shared;              // floats of the shared (FedAvg) prefix
+  int64_t off_m, off_v, off_g;   // exp_avg / exp_avg_sq / grad slot = parameter pointer + off_*
+  double *adam_pow;              // [2] beta1^t, beta2^t (advanced on device with t)
+  float *adam_coef;              // [2] lr / (1 - beta1^t), 1 / sqrt(1 - beta2^t)
+  float *ws_dtheta;              // [bmax, K] reduced d theta_d
 } GfkModel;
+
+// Gradient + update jobs of the small tensors, run by the update kernel next to
+// the W_in tiles (csrc/update.hip).  Weight job: G[j][i] = sum_{b < nb} dz[b][j]
+// a[b][i] for the 64 x 64 output tile at (j0, i0) of param [rows][cols].  Vector
+// job: g[c] = sum_{b < nb} src[b][c] (src [bmax][n]), or the gradient already in
+// the grad slot when src is null (priors, written by post_bwd).
+typedef struct GfkWJob {
+  float* param;
+  const float* dz;
+  const float* a;
+  int32_t rows, cols, j0, i0;
+} GfkWJob;
+
+typedef struct GfkVJob {
+  float* param;
+  const float* src;
+  int32_t n, pad;
+} GfkVJob;
+
+#define GFK_MAX_WJOBS 24
+#define GFK_MAX_VJOBS 16
+typedef struct GfkUpdate {
+  int32_t n_w, n_v;
+  GfkWJob w[GFK_MAX_WJOBS];
+  GfkVJob v[GFK_MAX_VJOBS];
+} GfkUpdate;
 
 typedef struct GfkAdam {
   float *p, *g, *m, *v;
@@ -121,13 +152,8 @@ typedef struct GfkAdam {
   int32_t seg_flags[GFK_MAX_SEGS];   // bit0: Adam update, bit1: FedAvg pre-scale
   float lr, beta1, beta2, eps, weight_decay, scale;
   const int32_t *t;                  // device Adam step count (already incremented)
-  // segment s takes its gradient from n_slab slabs (seg_slab[s] + j * slab_stride)
-  // instead of g when seg_slab[s] is non-null
-  const float* seg_slab[GFK_MAX_SEGS];
+  const float *coef;                 // [2] step size, 1/sqrt(bias correction 2) (see GfkModel)
   int32_t seg_first_block[GFK_MAX_SEGS];   // first workgroup of each segment (1024 float4 per block)
-  int64_t slab_stride;
-  int32_t n_slab;
-  int32_t pad2;
   uint64_t* dbg;                     // diagnostic stamps (GFK_STAMPS builds)
 } GfkAdam;
 
@@ -255,6 +281,19 @@ __device__ __forceinline__ void wave_lse(float& m, float& s) {
 
 __device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
+// Workgroup barrier for LDS-only data exchange.  __syncthreads() is a
+// workgroup-scope fence + s_barrier, and on gfx9 the fence waits for EVERY
+// outstanding vector-memory operation (vmcnt(0)) -- including global stores,
+// whose acknowledgements take a full round trip.  Phases that only hand data
+// over through LDS use this instead: LDS ops drained, global stores left in
+// flight.  (LDS-DMA staging still needs __syncthreads() / vm_barrier().)
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+__device__ __forceinline__ void vm_barrier() {
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // Pin a kernel-argument field in SGPRs at the point of the call: the empty asm
 // "modifies" the value, so the compiler can neither sink the scalar load to its
 // first use nor re-load it later.  Used in kernel prologues so that all
@@ -262,6 +301,50 @@ __device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirs
 // dependent scalar-cache round trip per field in the middle of the kernel.
 template <class T>
 __device__ __forceinline__ void keep1(T& v) { asm volatile("" : "+s"(v)); }
+
+// torch.optim.Adam element update with the bias corrections precomputed on the
+// device (coef = {lr / (1 - b1^t), 1 / sqrt(1 - b2^t)}, from double-precision
+// running powers):  m += (1-b1)(g-m);  v = b2 v + (1-b2) g^2;
+//                   p -= step * m / (sqrt(v) / sqrt(bc2) + eps)
+struct AdamCoef {
+  float b1, b2, eps, wd, step, ibc2;
+};
+
+__device__ __forceinline__ AdamCoef adam_coef(const GfkModel& m) {
+  AdamCoef c;
+  c.b1 = m.beta1; c.b2 = m.beta2; c.eps = m.adam_eps; c.wd = m.weight_decay;
+  c.step = m.adam_coef[0];
+  c.ibc2 = m.adam_coef[1];
+  return c;
+}
+
+__device__ __forceinline__ float adam_update(float p, float g, float& mo, float& vo, const AdamCoef& c) {
+  if (c.wd != 0.f) g += c.wd * p;
+  mo += (1.f - c.b1) * (g - mo);
+  vo = c.b2 * vo + (1.f - c.b2) * g * g;
+  return p - c.step * mo / (sqrtf(vo) * c.ibc2 + c.eps);
+}
+
+// Final value of a parameter element: fused mode applies Adam (and the FedAvg
+// pre-scale for shared tensors) in place; gradient mode stores g into the grad
+// slot for the generic Adam kernel.  ptr points into the parameter flat buffer.
+__device__ __forceinline__ void param_update(const GfkModel& m, float* ptr, float g, const AdamCoef& c,
+                                             bool shared) {
+  if (m.update_mode == 0) {
+    ptr[m.off_g] = g;
+    return;
+  }
+  float mo = ptr[m.off_m], vo = ptr[m.off_v];
+  float p = adam_update(*ptr, g, mo, vo, c);
+  if (shared && m.fed_scale_on) p *= m.fed_scale;
+  ptr[m.off_m] = mo;
+  ptr[m.off_v] = vo;
+  *ptr = p;
+}
+
+__device__ __forceinline__ bool is_shared(const GfkModel& m, const float* ptr) {
+  return (ptr - m.flat_base) < m.n_shared;
+}
 template <class... T>
 __device__ __forceinline__ void keep(T&... v) { (keep1(v), ...); }
 
@@ -358,6 +441,83 @@ __device__ __forceinline__ void mfma_gemm(int M, int N, int R, const MatView& A,
       if (i < M && bj < N) store(i, bj, acc[r]);
     }
   }
+}
+
+// Prepares the NEXT minibatch (the step counter has already been advanced):
+// nb, the doc ids, and each row's CSR extent into ws_next -- a chain of four
+// dependent reads (step -> plan -> doc -> indptr) that runs in an extra
+// workgroup of win_update, off the critical path, so the next enc_in starts one
+// round trip from its data.  Rows past the batch repeat its first doc.
+__device__ __forceinline__ void prepare_next_batch(const GfkModel& m) {
+  const int step = *m.step;
+  int32_t* nxt = m.ws_next;
+  if (step >= m.n_steps) {
+    if (threadIdx.x == 0) nxt[0] = 0;
+    return;
+  }
+  const int nb = m.plan_size[step];
+  const int base = m.plan_start[step];
+  for (int b = threadIdx.x; b < m.bmax; b += blockDim.x) {
+    const int doc = m.plan_order[base + (b < nb ? b : 0)];
+    const int e0 = m.indptr[doc], e1 = m.indptr[doc + 1];
+    nxt[1 + b] = doc;
+    nxt[1 + m.bmax + 2 * b] = e0;
+    nxt[2 + m.bmax + 2 * b] = e1;
+  }
+  if (threadIdx.x == 0) nxt[0] = nb;
+}
+
+
+// One workgroup's share of the multi-segment Adam: workgroups are dealt to
+// segments in proportion to their size (1024 float4 per workgroup, segment s
+// starts at workgroup seg_first_block[s]).  A ballot over the segment table
+// finds the segment in one round trip.  Used by the generic Adam kernel and by
+// the extra workgroups of win_update (small tensors in fused mode).
+__device__ __forceinline__ void adam_block(const GfkAdam& a, int blk, int tid, int nthreads) {
+  AdamCoef c;                 // bias corrections advanced on the device (enc_head_fwd)
+  c.b1 = a.beta1; c.b2 = a.beta2; c.eps = a.eps; c.wd = a.weight_decay;
+  c.step = a.coef[0];
+  c.ibc2 = a.coef[1];
+  const int lane = tid & 63;
+  const int nseg = a.n_seg;
+  const int fb = lane < nseg ? a.seg_first_block[lane] : 0x7fffffff;
+  const uint64_t le = __ballot(fb <= blk);
+  const int s = __popcll(le) - 1;
+  if (s < 0 || s >= nseg) return;
+  const int first = a.seg_first_block[s];
+  const int64_t s0 = a.seg_start[s], n4 = (a.seg_end[s] - s0) >> 2;
+  const int flags = a.seg_flags[s];
+  const bool do_adam = flags & 1, do_scale = flags & 2;
+  const int64_t lo = (int64_t)(blk - first) * 1024, hi = lo + 1024 < n4 ? lo + 1024 : n4;
+  for (int64_t i = lo + tid; i < hi; i += nthreads) {
+    const int64_t o = s0 + 4 * i;
+    float4 p = *reinterpret_cast<float4*>(a.p + o);
+    if (do_adam) {
+      const float4 g = *reinterpret_cast<float4*>(a.g + o);
+      float4 m = *reinterpret_cast<float4*>(a.m + o);
+      float4 v = *reinterpret_cast<float4*>(a.v + o);
+      float* pp = &p.x; const float* gg = &g.x; float* mm = &m.x; float* vv = &v.x;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pp[j] = adam_update(pp[j], gg[j], mm[j], vv[j], c);
+      *reinterpret_cast<float4*>(a.m + o) = m;
+      *reinterpret_cast<float4*>(a.v + o) = v;
+      *reinterpret_cast<float4*>(a.g + o) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (do_scale) { p.x *= a.scale; p.y *= a.scale; p.z *= a.scale; p.w *= a.scale; }
+    if (do_adam || do_scale) *reinterpret_cast<float4*>(a.p + o) = p;
+  }
+}
+
+// Sum of one value per thread over the workgroup, computed by wave 0 from the
+// per-wave sums in `scratch` (one float per wave).  Result valid in wave 0.
+__device__ __forceinline__ float block_sum_wave0(float v, float* scratch) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  if (lane == 0) scratch[wave] = v;
+  __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+  float t = lane < nw ? scratch[lane] : 0.f;
+  return wave_sum(t);
 }
 
 }  // namespace gfk

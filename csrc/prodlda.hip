@@ -41,7 +41,7 @@
 using namespace gfk;
 
 namespace {
-constexpr int DEC_THREADS = 256;
+constexpr int DEC_THREADS = 1024;
 constexpr int VB = 64;
 constexpr int LDB_F = 80;   // fwd beta tile stride: B-role reads (lane -> column) conflict free
 constexpr int LDB_B = 68;   // bwd beta tile stride: transposed B-role reads (lane -> k row)
@@ -81,8 +81,9 @@ __device__ __forceinline__ float sum_groups(float v) {
 }
 }  // namespace
 
-// grid: n_tiles workgroups (one vocab tile each).
-// dynamic LDS: th[BM*kt] + bt[KP*LDB_F]
+// grid: n_tiles workgroups (one vocab tile each) of 16 waves.  Wave w owns column
+// strip cs = w & 3 (16 columns) and row tiles rt = (w >> 2) + 4 i.
+// dynamic LDS: th[BM*kt] + bt[KP*LDB_F] + colp[4][64] + colq[4][64] + stat[2][64]
 template <int BM>
 __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -92,80 +93,92 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
   const int tile = blockIdx.x, c0 = tile * VB;
   float* th = smem;
   float* bt = th + BM * KT;
+  float* colp = bt + KP * LDB_F;
+  float* colq = colp + 4 * VB;
+  constexpr int RT = BM / 16;                 // row tiles
+  constexpr int NRT = (RT + 3) / 4;           // row tiles per wave
+  const int cs = wave & 3, rt0 = wave >> 2;
 
   GFK_STAMP(m, 16);
   // ---- one staging round: theta_d (LDS-DMA), beta tile, running stats, nb ----
   glds_copy(th, m.ws_thetad, BM * KT, tid, DEC_THREADS);
-  GFK_STAMP(m, 21);
-  const int col = 16 * wave + (lane & 15);      // this lane's column within the tile
+  const int col = 16 * cs + (lane & 15);      // this lane's column within the tile
   const int v = c0 + col;
   const bool valid = v < V;
   const float rm0 = m.beta_rm[min(v, V - 1)], rv0 = m.beta_rv[min(v, V - 1)];
   const int nb = *m.ws_nb;
-  GFK_STAMP(m, 22);
   stage_beta_tile(bt, LDB_F, m.beta, K, KP, V, c0, tid);
-  GFK_STAMP(m, 23);
   if (tile == 0 && tid == 0) *m.nbt_beta += 1;
   __syncthreads();
   GFK_STAMP(m, 17);
 
-  // ---- logits for rows [0, BM) x this wave's 16 columns ----
-  constexpr int RT = BM / 16;
-  f32x4 acc[RT];
+  // ---- logits for this wave's row tiles x 16 columns ----
+  f32x4 acc[NRT];
 #pragma unroll
-  for (int r = 0; r < RT; ++r) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < NRT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   {
     const float* bp = bt + (lane >> 4) * LDB_F + col;
-    const float* ap = th + (lane & 15) * KT + (lane >> 4);
-    for (int k0 = 0; k0 < KP; k0 += 4) {
-      const float b = bp[k0 * LDB_F];
+    const float* ap = th + (rt0 * 16 + (lane & 15)) * KT + (lane >> 4);
+    if (rt0 < RT) {
+      for (int k0 = 0; k0 < KP; k0 += 4) {
+        const float b = bp[k0 * LDB_F];
 #pragma unroll
-      for (int r = 0; r < RT; ++r) acc[r] = mfma16x16x4(ap[r * 16 * KT + k0], b, acc[r]);
+        for (int i = 0; i < NRT; ++i)
+          if (rt0 + 4 * i < RT) acc[i] = mfma16x16x4(ap[i * 64 * KT + k0], b, acc[i]);
+      }
     }
   }
   GFK_STAMP(m, 18);
 
-  // ---- column batch-norm straight from the accumulators ----
-  // lane holds rows rt*16 + (lane>>4)*4 + e of column col
+  // ---- column batch-norm: wave partials over its rows, combined through LDS ----
   const float inv_nb = 1.f / (float)nb;
   float s = 0.f;
 #pragma unroll
-  for (int r = 0; r < RT; ++r)
+  for (int i = 0; i < NRT; ++i)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int row = r * 16 + (lane >> 4) * 4 + e;
-      s += row < nb ? acc[r][e] : 0.f;
+      const int row = (rt0 + 4 * i) * 16 + (lane >> 4) * 4 + e;
+      s += (row < nb && rt0 + 4 * i < RT) ? acc[i][e] : 0.f;
     }
-  const float mean = sum_groups(s) * inv_nb;
+  s = sum_groups(s);
+  if (lane < 16) colp[rt0 * VB + col] = s;
+  __syncthreads();
+  const float mean = (colp[col] + colp[VB + col] + colp[2 * VB + col] + colp[3 * VB + col]) * inv_nb;
   float q = 0.f;
 #pragma unroll
-  for (int r = 0; r < RT; ++r)
+  for (int i = 0; i < NRT; ++i)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int row = r * 16 + (lane >> 4) * 4 + e;
-      const float d = acc[r][e] - mean;
-      q += row < nb ? d * d : 0.f;
+      const int row = (rt0 + 4 * i) * 16 + (lane >> 4) * 4 + e;
+      const float d = acc[i][e] - mean;
+      q += (row < nb && rt0 + 4 * i < RT) ? d * d : 0.f;
     }
-  const float var = sum_groups(q) * inv_nb;
+  q = sum_groups(q);
+  if (lane < 16) colq[rt0 * VB + col] = q;
+  __syncthreads();
+  const float var = (colq[col] + colq[VB + col] + colq[2 * VB + col] + colq[3 * VB + col]) * inv_nb;
   const float rstd = rsqrtf(var + m.bn_eps);
-  if (lane < 16 && valid) {
+  if (rt0 == 0 && lane < 16 && valid) {
     const float mom = m.bn_momentum;
     const float unb = nb > 1 ? var * (float)nb / (float)(nb - 1) : var;
-    m.beta_rm[v] = (1.f - mom) * rm0 + mom * mean;
-    m.beta_rv[v] = (1.f - mom) * rv0 + mom * unb;
+    float nm = (1.f - mom) * rm0 + mom * mean, nv = (1.f - mom) * rv0 + mom * unb;
+    if (m.fed_scale_on && is_shared(m, m.beta_rm)) { nm *= m.fed_scale; nv *= m.fed_scale; }
+    m.beta_rm[v] = nm;
+    m.beta_rv[v] = nv;
     m.ws_col_rstd[v] = rstd;
   }
   GFK_STAMP(m, 19);
 
   // ---- normalise, store the BN'ed tile, per-row (max, sum-exp) partials ----
   float* zt = m.ws_zn + (size_t)tile * BM * VB;
-  float* part = m.ws_row_part + (size_t)(tile * 4 + wave) * m.bmax * 2;
+  float* part = m.ws_row_part + (size_t)(tile * 4 + cs) * m.bmax * 2;
 #pragma unroll
-  for (int r = 0; r < RT; ++r) {
+  for (int i = 0; i < NRT; ++i) {
+    if (rt0 + 4 * i >= RT) continue;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int row = r * 16 + (lane >> 4) * 4 + e;
-      const float z = (acc[r][e] - mean) * rstd;
+      const int row = (rt0 + 4 * i) * 16 + (lane >> 4) * 4 + e;
+      const float z = (acc[i][e] - mean) * rstd;
       if (row < nb) zt[row * VB + col] = z;
       const float zv = valid ? z : -INFINITY;
       const float mx = row16_max(zv);
@@ -212,21 +225,14 @@ extern "C" __global__ void __launch_bounds__(64) gfk_prodlda_row_loss(GfkModel m
   wave_lse(mx, se);
   const float lse = mx + logf(se);
   const size_t tstride = (size_t)bmax * VB;
-  int32_t* ts = m.ws_tstart + (size_t)b * (n_tiles + 1);
   float rl = 0.f, S = 0.f;
   for (int e = e0 + lane; e < e1; e += 64) {
     const int c = indices[e];
-    const int prev = e > e0 ? indices[e - 1] / VB : -1;
     const float x = values[e];
     const float z = zn[(size_t)(c / VB) * tstride + (size_t)b * VB + (c % VB)];
     const float p = expf(z - lse);
     rl += x * logf(p + RL_EPS);
     S += x * p / (p + RL_EPS);
-    for (int t = prev + 1; t <= c / VB; ++t) ts[t] = e;
-  }
-  {  // tiles after the last non-zero start at e1
-    const int last = e1 > e0 ? m.indices[e1 - 1] / VB : -1;
-    for (int t = last + 1 + lane; t <= m.n_tiles; t += 64) ts[t] = e1;
   }
   rl = wave_sum(rl);
   S = wave_sum(S);
@@ -237,7 +243,7 @@ extern "C" __global__ void __launch_bounds__(64) gfk_prodlda_row_loss(GfkModel m
   }
 }
 
-// Backward.  grid: n_tiles workgroups.
+// Backward.  grid: n_tiles workgroups of 16 waves.
 // dynamic LDS: th[BM*kt] + bt[KP16*LDB_B] + zt[BM*VB] + dt[BM*LDD] + lse[BM] + S[BM] + rstd[VB]
 template <int BM>
 __global__ void __launch_bounds__(DEC_THREADS) prodlda_bwd_kernel(GfkModel m) {
@@ -253,6 +259,7 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_bwd_kernel(GfkModel m) {
   float* lse = dt + BM * LDD;
   float* Sb = lse + BM;
   float* rs = Sb + BM;
+  constexpr int TPR = DEC_THREADS / BM < 16 ? DEC_THREADS / BM : 16;   // threads per row (sparse x)
 
   GFK_STAMP(m, 24);
   // ---- one staging round ----
@@ -262,113 +269,130 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_bwd_kernel(GfkModel m) {
   glds_copy(Sb, m.ws_s, BM, tid, DEC_THREADS);
   glds_copy(rs, m.ws_col_rstd + c0, VB, tid, DEC_THREADS);
   const int nb = *m.ws_nb;
-  // sparse x of this tile: 4 threads per row, first NPRE non-zeros prefetched
-  constexpr int NPRE = 2;
-  const int sub = tid & 3;
-  constexpr int NH = (BM + 63) / 64;   // rows per thread quad
-  int xe0[NH], xe1[NH], xc[NH][NPRE];
-  float xv[NH][NPRE];
-#pragma unroll
-  for (int h = 0; h < NH; ++h) {
-    const int row = min((tid >> 2) + 64 * h, BM - 1);
-    const int32_t* ts = m.ws_tstart + (size_t)row * (m.n_tiles + 1) + tile;
-    xe0[h] = ts[0];
-    xe1[h] = ts[1];
+  // sparse x of this tile: TPR threads per row, the first non-zero prefetched
+  const int xrow = tid / TPR, xsub = tid % TPR;
+  int xe0 = 0, xe1 = 0;
+  if (xrow < BM) {
+    const int32_t* ts = m.ws_tstart + (size_t)xrow * (m.n_tiles + 1) + tile;
+    xe0 = ts[0];
+    xe1 = ts[1];
   }
+  const int xe = min(xe0 + xsub, max(xe1 - 1, 0));
+  const int xc0 = m.indices[xe];
+  const float xv0 = m.values[xe];
+  // optimizer state of this lane's dbeta outputs (fused mode): wave -> (k tile, column strip)
+  const int ksub = KP16 / 16;
+  const int NB_T = ksub * 4;
+  constexpr int MAXU = 4;                         // K <= 256
+  const bool fused = m.update_mode == 1;
+  float bp_[MAXU][4], bm_[MAXU][4], bv_[MAXU][4];
 #pragma unroll
-  for (int h = 0; h < NH; ++h)
+  for (int u = 0; u < MAXU; ++u) {
+    const int t = wave + 16 * u;
+    const int ks = t >> 2, cst = t & 3;
+    const int c = min(c0 + cst * 16 + (lane & 15), V - 1);
 #pragma unroll
-    for (int i = 0; i < NPRE; ++i) {
-      const int e = min(xe0[h] + sub + 4 * i, max(xe1[h] - 1, 0));
-      xc[h][i] = m.indices[e];
-      xv[h][i] = m.values[e];
+    for (int r = 0; r < 4; ++r) {
+      const int k = min(ks * 16 + (lane >> 4) * 4 + r, K - 1);
+      bp_[u][r] = bm_[u][r] = bv_[u][r] = 0.f;
+      if (fused && t < NB_T) {
+        const float* p = m.beta + (size_t)k * V + c;
+        bp_[u][r] = *p;
+        bm_[u][r] = p[m.off_m];
+        bv_[u][r] = p[m.off_v];
+      }
     }
+  }
   stage_beta_tile(bt, LDB_B, m.beta, K, KP16, V, c0, tid);
-  // zero the dlogit tile (register-pass layout: column col, rows g, g+4, ...)
-  const int col = 16 * wave + (lane & 15), g = lane >> 4;
-  for (int row = g; row < BM; row += 4) dt[row * LDD + col] = 0.f;
+  // zero the dlogit tile (dense-pass layout: column tid>>4, rows (tid&15) + 16 i)
+  const int dcol = tid >> 4, dg = tid & 15;
+  for (int row = dg; row < BM; row += 16) dt[row * LDD + dcol] = 0.f;
   __syncthreads();
   GFK_STAMP(m, 25);
 
   // ---- sparse term: dt[b, c] = -x p / (p + 1e-10) at this tile's non-zeros ----
-#pragma unroll
-  for (int h = 0; h < NH; ++h) {
-    const int row = (tid >> 2) + 64 * h;
-    if (row < nb && row < BM) {
-      const float l = lse[row];
-      for (int i = 0, e = xe0[h] + sub; e < xe1[h]; ++i, e += 4) {
-        int c;
-        float x;
-        if (i < NPRE) {
-          c = xc[h][min(i, NPRE - 1)];
-          x = xv[h][min(i, NPRE - 1)];
-        } else {
-          c = m.indices[e];
-          x = m.values[e];
-        }
-        c -= c0;
-        const float p = __expf(zt[row * VB + c] - l);
-        dt[row * LDD + c] = -x * p / (p + RL_EPS);
-      }
+  if (xrow < nb && xrow < BM) {
+    const float l = lse[xrow];
+    for (int i = 0, e = xe0 + xsub; e < xe1; ++i, e += TPR) {
+      const int c = (i == 0 ? xc0 : m.indices[e]) - c0;
+      const float x = i == 0 ? xv0 : m.values[e];
+      const float p = __expf(zt[xrow * VB + c] - l);
+      dt[xrow * LDD + c] = -x * p / (p + RL_EPS);
     }
   }
   __syncthreads();
   GFK_STAMP(m, 26);
 
-  // ---- dense term p*S and the column BN backward, in registers ----
+  // ---- dense term p*S and the column BN backward: 16 lanes per column ----
   {
-    const bool valid = c0 + col < V;
-    constexpr int NR = BM / 4;
+    const bool valid = c0 + dcol < V;
+    constexpr int NR = BM / 16;
     float d[NR], z[NR];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
-      const int row = g + 4 * i;
-      z[i] = zt[row * VB + col];
+      const int row = dg + 16 * i;
+      z[i] = zt[row * VB + dcol];
       const float p = __expf(z[i] - lse[row]);
-      d[i] = (row < nb && valid) ? p * Sb[row] + dt[row * LDD + col] : 0.f;
+      d[i] = (row < nb && valid) ? p * Sb[row] + dt[row * LDD + dcol] : 0.f;
       s1 += d[i];
       s2 += d[i] * z[i];
     }
-    s1 = sum_groups(s1) / (float)nb;
-    s2 = sum_groups(s2) / (float)nb;
-    const float r = valid ? rs[col] : 0.f;
+    s1 = row16_sum(s1) / (float)nb;
+    s2 = row16_sum(s2) / (float)nb;
+    const float r = valid ? rs[dcol] : 0.f;
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
-      const int row = g + 4 * i;
-      dt[row * LDD + col] = row < nb ? r * (d[i] - s1 - z[i] * s2) : 0.f;
+      const int row = dg + 16 * i;
+      dt[row * LDD + dcol] = row < nb ? r * (d[i] - s1 - z[i] * s2) : 0.f;
     }
   }
   __syncthreads();
   GFK_STAMP(m, 27);
 
-  // ---- dbeta[k, c] = sum_b th[b, k] dlogit[b, c]: wave w owns columns [16w, 16w+16) ----
+  // ---- dbeta[k, c] = sum_b th[b, k] dlogit[b, c]  -> update (fused) or gradient ----
   {
-    const int ksub = KP16 / 16;
-    const float* bp = dt + (lane >> 4) * LDD + 16 * wave + (lane & 15);
-    const int c = c0 + 16 * wave + (lane & 15);
-    for (int ks = 0; ks < ksub; ++ks) {
+    const AdamCoef ac = adam_coef(m);
+    const bool sh = is_shared(m, m.beta);
+#pragma unroll
+    for (int u = 0; u < MAXU; ++u) {
+      const int t = wave + 16 * u;
+      if (t >= NB_T) break;
+      const int ks = t >> 2, cst = t & 3;
       const float* ap = th + (lane >> 4) * KT + ks * 16 + (lane & 15);
+      const float* bp = dt + (lane >> 4) * LDD + cst * 16 + (lane & 15);
       f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int b0 = 0; b0 < BM; b0 += 8) {
         a0 = mfma16x16x4(ap[b0 * KT], bp[b0 * LDD], a0);
         a1 = mfma16x16x4(ap[(b0 + 4) * KT], bp[(b0 + 4) * LDD], a1);
       }
+      const int c = c0 + cst * 16 + (lane & 15);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int k = ks * 16 + (lane >> 4) * 4 + e;
-        if (k < K && c < V) m.g_beta[(size_t)k * V + c] = a0[e] + a1[e];
+        if (k >= K || c >= V) continue;
+        float* p = m.beta + (size_t)k * V + c;
+        const float g = a0[e] + a1[e];
+        if (!fused) {
+          p[m.off_g] = g;
+        } else {
+          float mo = bm_[u][e], vo = bv_[u][e];
+          float np = adam_update(bp_[u][e], g, mo, vo, ac);
+          if (sh && m.fed_scale_on) np *= m.fed_scale;
+          p[m.off_m] = mo;
+          p[m.off_v] = vo;
+          *p = np;
+        }
       }
     }
   }
   // ---- this tile's partial dtheta_d[b, k] = sum_c dlogit[b, c] beta[k, c] (plain stores;
-  //      posterior_bwd_rows sums the n_tiles partials in a fixed order) ----
+  //      dtheta_reduce sums the n_tiles partials in a fixed order) ----
   {
     float* dpart = m.ws_dthetad + (size_t)tile * m.bmax * K;
-    const int ksub = KP16 / 16;
-    for (int s = wave; s < (BM / 16) * ksub; s += 4) {
-      const int rt = s / ksub, ks = s % ksub;
+    for (int t = wave; t < (BM / 16) * ksub; t += 16) {
+      const int rt = t / ksub, ks = t % ksub;
       const float* ap = dt + (rt * 16 + (lane & 15)) * LDD + (lane >> 4);
       const float* bp = bt + (ks * 16 + (lane & 15)) * LDB_B + (lane >> 4);
       f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
@@ -390,7 +414,7 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_bwd_kernel(GfkModel m) {
 
 extern "C" size_t gfk_prodlda_fwd_smem(const GfkModel* m) {
   const size_t KP = round_up(m->K, 4);
-  return sizeof(float) * ((size_t)m->bmax * m->kt + KP * LDB_F);
+  return sizeof(float) * ((size_t)m->bmax * m->kt + KP * LDB_F + 8 * VB);
 }
 
 extern "C" size_t gfk_prodlda_bwd_smem(const GfkModel* m) {

@@ -13,12 +13,12 @@
 #include "gfk_common.h"
 
 extern "C" {
-int gfk_launch_encoder_fwd(const GfkModel*, hipStream_t);
-int gfk_launch_encoder_bwd(const GfkModel*, hipStream_t);
+int gfk_launch_enc_in(const GfkModel*, hipStream_t);
+int gfk_launch_post_fwd(const GfkModel*, hipStream_t);
+int gfk_launch_post_bwd(const GfkModel*, hipStream_t);
+int gfk_launch_win_update(const GfkModel*, const GfkUpdate*, hipStream_t);
 int gfk_launch_batch_docs(const GfkModel*, hipStream_t);
 int gfk_launch_batch_prep(const GfkModel*, hipStream_t);
-int gfk_launch_posterior_fwd(const GfkModel*, hipStream_t);
-int gfk_launch_posterior_bwd(const GfkModel*, hipStream_t);
 int gfk_launch_prodlda_fwd(const GfkModel*, hipStream_t);
 int gfk_launch_prodlda_bwd(const GfkModel*, hipStream_t);
 int gfk_launch_prodlda_row_loss(const GfkModel*, hipStream_t);
@@ -31,14 +31,14 @@ size_t gfk_prodlda_fwd_smem(const GfkModel*);
 size_t gfk_prodlda_bwd_smem(const GfkModel*);
 size_t gfk_lda_fwd_smem(int);
 size_t gfk_lda_bwd_smem(int);
-size_t gfk_posterior_bwd_smem(const GfkModel*);
-size_t gfk_posterior_fwd_smem(const GfkModel*);
-size_t gfk_mlp_weight_bytes(const GfkModel*);
-size_t gfk_encoder_fwd_smem(const GfkModel*);
-int gfk_encoder_set_smem(size_t);
+size_t gfk_post_smem(const GfkModel*);
+size_t gfk_win_update_smem(const GfkModel*);
+size_t gfk_enc_in_smem(const GfkModel*);
+int gfk_enc_in_set_smem(size_t);
+int gfk_post_set_smem(size_t);
+int gfk_win_update_set_smem(size_t);
 int gfk_prodlda_set_smem(size_t);
 int gfk_lda_set_smem(size_t);
-int gfk_posterior_set_smem(size_t);
 
 // Phase ids (mirrored in gfedntm_amd/ops/kernel_abi.py).
 enum GfkPhase {
@@ -59,17 +59,16 @@ enum GfkPhase {
 
 
 
-// LDS each kernel family needs for this model; 0 means "does not fit".
+// LDS each kernel family needs for this model.
 size_t gfk_smem_required(const GfkModel* m, int which) {
   switch (which) {
     case 0: return gfk_prodlda_fwd_smem(m);
     case 1: return gfk_prodlda_bwd_smem(m);
     case 2: return gfk_lda_fwd_smem(m->K);
     case 3: return gfk_lda_bwd_smem(m->K);
-    case 4: return gfk_posterior_bwd_smem(m);
-    case 5: return gfk_posterior_fwd_smem(m);
-    case 6: return gfk_mlp_weight_bytes(m);
-    case 7: return gfk_encoder_fwd_smem(m);
+    case 4: return gfk_post_smem(m);
+    case 5: return gfk_win_update_smem(m);
+    case 7: return gfk_enc_in_smem(m);
     default: return 0;
   }
 }
@@ -83,28 +82,29 @@ int gfk_setup(const GfkModel* m) {
   p = gfk_lda_fwd_smem(m->K);
   q = gfk_lda_bwd_smem(m->K);
   if ((e = gfk_lda_set_smem(p > q ? p : q))) return e;
-  if ((e = gfk_encoder_set_smem(gfk_encoder_fwd_smem(m)))) return e;
-  p = gfk_posterior_fwd_smem(m);
-  q = gfk_posterior_bwd_smem(m);
-  return gfk_posterior_set_smem(p > q ? p : q);
+  if ((e = gfk_enc_in_set_smem(gfk_enc_in_smem(m)))) return e;
+  if ((e = gfk_post_set_smem(gfk_post_smem(m)))) return e;
+  return gfk_win_update_set_smem(gfk_win_update_smem(m));
 }
 
-int gfk_run(const GfkModel* m, const GfkAdam* a, int adam_grid, hipStream_t s,
+// a / adam_grid: the generic Adam (PH_ADAM, gradient mode); u: the small-tensor
+// gradient / update jobs of win_update.
+int gfk_run(const GfkModel* m, const GfkAdam* a, int adam_grid, const GfkUpdate* u, hipStream_t s,
             const int32_t* phases, int n_phases) {
   for (int i = 0; i < n_phases; ++i) {
     int e = 0;
     switch (phases[i]) {
       case GFK_PH_BATCH_DOCS: e = gfk_launch_batch_docs(m, s); break;
-      case GFK_PH_ENC_FWD: e = gfk_launch_encoder_fwd(m, s); break;
-      case GFK_PH_POST_FWD: e = gfk_launch_posterior_fwd(m, s); break;
+      case GFK_PH_ENC_FWD: e = gfk_launch_enc_in(m, s); break;
+      case GFK_PH_POST_FWD: e = gfk_launch_post_fwd(m, s); break;
       case GFK_PH_PRODLDA_FWD: e = gfk_launch_prodlda_fwd(m, s); break;
       case GFK_PH_PRODLDA_LOSS: e = gfk_launch_prodlda_row_loss(m, s); break;
       case GFK_PH_PRODLDA_BWD: e = gfk_launch_prodlda_bwd(m, s); break;
       case GFK_PH_LDA_BETA_FWD: e = gfk_launch_lda_beta_fwd(m, s); break;
       case GFK_PH_LDA_ROW: e = gfk_launch_lda_row(m, s); break;
-      case GFK_PH_POST_BWD: e = gfk_launch_posterior_bwd(m, s); break;
+      case GFK_PH_POST_BWD: e = gfk_launch_post_bwd(m, s); break;
       case GFK_PH_LDA_BETA_BWD: e = gfk_launch_lda_beta_bwd(m, s); break;
-      case GFK_PH_ENC_BWD: e = gfk_launch_encoder_bwd(m, s); break;
+      case GFK_PH_ENC_BWD: e = gfk_launch_win_update(m, u, s); break;
       case GFK_PH_ADAM: e = gfk_launch_adam(a, adam_grid, s); break;
       case GFK_PH_BATCH_PREP: e = gfk_launch_batch_prep(m, s); break;
       default: e = -2;
@@ -118,5 +118,6 @@ int gfk_scale(float* p, int64_t n, float sc, hipStream_t s) { return gfk_launch_
 
 size_t gfk_model_struct_size() { return sizeof(GfkModel); }
 size_t gfk_adam_struct_size() { return sizeof(GfkAdam); }
+size_t gfk_update_struct_size() { return sizeof(GfkUpdate); }
 
 }  // extern "C"

@@ -1,0 +1,255 @@
+// The optimizer step of every encoder tensor, each fused with the kernel that
+// completes its gradient, plus the next-batch prep.  Workgroup roles:
+//   [0, n_tiles)         W_in tiles (below)
+//   [n_tiles, +n_w)      small weight tiles: G[j][i] = sum_b dz[b][j] a[b][i] for a
+//                        64 x 64 output tile of W_h[l] / W_mu / W_s (MFMA, fused Adam)
+//   [.., +n_v)           bias / prior vectors: column sums over the batch (16 lanes
+//                        per column, DPP reduction) or the prior gradient, fused Adam
+//   last                 prepare_next_batch
+// (beta is updated in prodlda_bwd's epilogue.)
+//
+// dW_in^T[v, :] = sum_b x[b, v] dz0[b, :]  (reference: autograd of
+// inference_network.py:76 input_layer).  W_in is stored transposed ([V, H0]), so
+// a vocabulary tile of 64 words is a contiguous [64, H0] block.  Instead of
+// scattering B * nnz rows with float atomics (order-dependent, and each wave
+// serialises on its outstanding-atomic budget), every workgroup owns one tile:
+//   * builds the dense x^T tile [64, B] in LDS from the per-row tile start table
+//     (ws_tstart, written by enc_in) -- the CSR non-zeros of the tile;
+//   * multiplies it with dz0 [B, H0] on the fp32 matrix cores (16 waves, one
+//     16x16 output tile each at H0 <= 64);
+//   * applies Adam (and the FedAvg pre-scale) to its W_in block in the epilogue,
+//     with p / m / v prefetched before the MFMA (fused mode), or stores the
+//     gradient (gradient mode).
+// Deterministic, no atomics, W_in's gradient is never materialised in fused mode.
+// One extra workgroup prepares the next minibatch (gfk_common.h).
+#include "gfk_common.h"
+
+using namespace gfk;
+
+namespace {
+constexpr int UT = 1024;
+constexpr int UW = UT / 64;
+__host__ __device__ inline int rup(int x, int m) { return (x + m - 1) / m * m; }
+__host__ __device__ inline int lds_stride(int w) {
+  int s = rup(w, 4);
+  if ((s / 4) % 2 == 0) s += 4;
+  return s;
+}
+}  // namespace
+
+extern "C" size_t gfk_win_update_smem(const GfkModel* m) {
+  const int B = m->bmax, H0P = rup(m->H[0], 16);
+  const size_t a = (size_t)64 * lds_stride(B) + (size_t)B * lds_stride(H0P), b = 2 * (size_t)B * 68;
+  return sizeof(float) * (a > b ? a : b);
+}
+
+// Small weight tile job (see GfkWJob).  LDS: dz[B][LDJ] + a[B][LDJ]
+__device__ __forceinline__ void weight_job(const GfkModel& m, const GfkWJob& J, float* smem) {
+  constexpr int LDJ = 68;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int B = m.bmax, nb = *m.ws_nb;
+  float* dzs = smem;
+  float* as = smem + B * LDJ;
+  const bool fused = m.update_mode == 1;
+  // prefetch: the lane's 4 outputs of subtile (jt, it) = (wave >> 2, wave & 3)
+  const int jt = wave >> 2, it = wave & 3;
+  const int i = J.i0 + it * 16 + (lane & 15);
+  float pp[4], pm[4], pv[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int j = J.j0 + jt * 16 + (lane >> 4) * 4 + r;
+    const float* p = J.param + (size_t)min(j, J.rows - 1) * J.cols + min(i, J.cols - 1);
+    pp[r] = pm[r] = pv[r] = 0.f;
+    if (fused) { pp[r] = *p; pm[r] = p[m.off_m]; pv[r] = p[m.off_v]; }
+  }
+  // stage the two [B x 64] column slices (rows >= nb zero)
+  for (int e0 = 0; e0 < B * 64; e0 += 4 * UT) {
+    float vz[4], va[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * UT + tid, b = min(e >> 6, B - 1), c = e & 63;
+      vz[u] = J.dz[(size_t)b * J.rows + min(J.j0 + c, J.rows - 1)];
+      va[u] = J.a[(size_t)b * J.cols + min(J.i0 + c, J.cols - 1)];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = e0 + u * UT + tid, b = e >> 6, c = e & 63;
+      if (b < B) {
+        dzs[b * LDJ + c] = (b < nb && J.j0 + c < J.rows) ? vz[u] : 0.f;
+        as[b * LDJ + c] = (b < nb && J.i0 + c < J.cols) ? va[u] : 0.f;
+      }
+    }
+  }
+  lds_barrier();
+  const float* ap = dzs + (lane >> 4) * LDJ + jt * 16 + (lane & 15);
+  const float* bp = as + (lane >> 4) * LDJ + it * 16 + (lane & 15);
+  f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < B; k += 8) {
+    c0 = mfma16x16x4(ap[k * LDJ], bp[k * LDJ], c0);
+    c1 = mfma16x16x4(ap[(k + 4) * LDJ], bp[(k + 4) * LDJ], c1);
+  }
+  const f32x4 g = c0 + c1;
+  const AdamCoef ac = adam_coef(m);
+  const bool sh = is_shared(m, J.param);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int j = J.j0 + jt * 16 + (lane >> 4) * 4 + r;
+    if (j >= J.rows || i >= J.cols) continue;
+    float* p = J.param + (size_t)j * J.cols + i;
+    if (!fused) {
+      p[m.off_g] = g[r];
+    } else {
+      float mo = pm[r], vo = pv[r];
+      float np = adam_update(pp[r], g[r], mo, vo, ac);
+      if (sh && m.fed_scale_on) np *= m.fed_scale;
+      p[m.off_m] = mo;
+      p[m.off_v] = vo;
+      *p = np;
+    }
+  }
+}
+
+// Vector job (see GfkVJob): 16 lanes per element split the batch rows.
+__device__ __forceinline__ void vector_job(const GfkModel& m, const GfkVJob& J) {
+  const int tid = threadIdx.x, s = tid & 15;
+  const int B = m.bmax, nb = *m.ws_nb;
+  const bool fused = m.update_mode == 1;
+  const AdamCoef ac = adam_coef(m);
+  const bool sh = is_shared(m, J.param);
+  for (int c0 = 0; c0 < J.n; c0 += UT / 16) {
+    const int c = c0 + (tid >> 4), cc = min(c, J.n - 1);
+    float* p = J.param + cc;
+    float pp = 0.f, pm = 0.f, pv = 0.f, g = 0.f;
+    if (fused) { pp = *p; pm = p[m.off_m]; pv = p[m.off_v]; }
+    if (J.src) {
+      constexpr int RU = 8;                  // B <= 128: 8 rows per lane
+      float v[RU];
+#pragma unroll
+      for (int u = 0; u < RU; ++u) v[u] = J.src[(size_t)min(s + 16 * u, B - 1) * J.n + cc];
+#pragma unroll
+      for (int u = 0; u < RU; ++u) g += s + 16 * u < nb ? v[u] : 0.f;
+      g = row16_sum(g);
+    } else {
+      g = p[m.off_g];
+    }
+    if (s != 0 || c >= J.n) continue;
+    if (!fused) {
+      if (J.src) p[m.off_g] = g;
+    } else {
+      float np = adam_update(pp, g, pm, pv, ac);
+      if (sh && m.fed_scale_on) np *= m.fed_scale;
+      p[m.off_m] = pm;
+      p[m.off_v] = pv;
+      *p = np;
+    }
+  }
+}
+
+// grid: n_tiles + n_w + n_v + 1 workgroups of 1024 threads.
+// dynamic LDS: max(W_in tile: xt[64][lds_stride(B)] + dz[B][lds_stride(H0P)], weight job: 2 B 68)
+extern "C" __global__ void __launch_bounds__(UT) gfk_win_update(GfkModel m, GfkUpdate U) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  {
+    const int r = (int)blockIdx.x - m.n_tiles;
+    if (r >= 0 && r < U.n_w) { weight_job(m, U.w[r], smem); return; }
+    if (r >= U.n_w && r < U.n_w + U.n_v) { vector_job(m, U.v[r - U.n_w]); return; }
+    if (r == U.n_w + U.n_v) { prepare_next_batch(m); return; }
+  }
+  const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
+  int B = m.bmax, H0 = m.H[0], V = m.V, n_tiles = m.n_tiles;
+  const int32_t *tstart = m.ws_tstart, *indices = m.indices, *nbp = m.ws_nb;
+  const float *values = m.values, *dz0 = m.ws_dz[0];
+  float* w_in = m.w_in;
+  keep(B, H0, V, n_tiles, tstart, indices, nbp, values, dz0, w_in);
+  const int H0P = rup(H0, 16);
+  const int XS = lds_stride(B), ZS = lds_stride(H0P);
+  float* xt = smem;
+  float* dz = smem + 64 * XS;
+  const int tile = blockIdx.x, c0 = tile * 64;
+
+  // ---- staging: dz0 rows (zero padding), zero x^T tile, the tile's CSR extents ----
+  const int nb = *nbp;
+  for (int i = tid; i < B * H0P; i += UT) {
+    const int r = i / H0P, c = i % H0P;
+    dz[r * ZS + c] = (c < H0 && r < nb) ? dz0[r * H0 + c] : 0.f;
+  }
+  for (int i = tid; i < 64 * XS; i += UT) xt[i] = 0.f;
+  // 16 threads per row: the row's non-zeros inside this tile
+  const int row = tid >> 4, sub = tid & 15;
+  int e0 = 0, e1 = 0;
+  if (row < nb && row < B) {
+    const int32_t* ts = tstart + (size_t)row * (n_tiles + 1) + tile;
+    e0 = ts[0];
+    e1 = ts[1];
+  }
+  // prefetch the optimizer state of this lane's 4 outputs (16x16 tile per wave)
+  const int MT = 4, NT = H0P / 16;
+  float pp[4][4], pm[4][4], pv[4][4];
+  const bool fused = m.update_mode == 1;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int t = wave + UW * u;
+    const int i0 = (t / NT) * 16, j0 = (t % NT) * 16;
+    const int j = min(j0 + (lane & 15), H0 - 1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int v = min(c0 + i0 + (lane >> 4) * 4 + r, V - 1);
+      float* p = w_in + (size_t)v * H0 + j;
+      pp[u][r] = pm[u][r] = pv[u][r] = 0.f;
+      if (t < MT * NT && fused) {
+        pp[u][r] = *p;
+        pm[u][r] = p[m.off_m];
+        pv[u][r] = p[m.off_v];
+      }
+    }
+  }
+  __syncthreads();
+  for (int e = e0 + sub; e < e1; e += 16) xt[(indices[e] - c0) * XS + row] = values[e];
+  __syncthreads();
+
+  // ---- G[v, j] = sum_b xt[v, b] dz[b, j] and the update ----
+  const AdamCoef ac = adam_coef(m);
+  const bool sh = is_shared(m, w_in);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int t = wave + UW * u;
+    if (t >= MT * NT) break;
+    const int i0 = (t / NT) * 16, j0 = (t % NT) * 16;
+    const float* ap = xt + (i0 + (lane & 15)) * XS + (lane >> 4);
+    const float* bp = dz + (lane >> 4) * ZS + j0 + (lane & 15);
+    f32x4 c0v = {0.f, 0.f, 0.f, 0.f}, c1v = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < B; k += 8) {
+      c0v = mfma16x16x4(ap[k], bp[k * ZS], c0v);
+      c1v = mfma16x16x4(ap[k + 4], bp[(k + 4) * ZS], c1v);
+    }
+    const f32x4 g = c0v + c1v;
+    const int j = j0 + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int v = c0 + i0 + (lane >> 4) * 4 + r;
+      if (v >= V || j >= H0) continue;
+      float* p = w_in + (size_t)v * H0 + j;
+      if (!fused) {
+        p[m.off_g] = g[r];
+      } else {
+        float mo = pm[u][r], vo = pv[u][r];
+        float np = adam_update(pp[u][r], g[r], mo, vo, ac);
+        if (sh && m.fed_scale_on) np *= m.fed_scale;
+        p[m.off_m] = mo;
+        p[m.off_v] = vo;
+        *p = np;
+      }
+    }
+  }
+}
+
+extern "C" int gfk_launch_win_update(const GfkModel* m, const GfkUpdate* u, hipStream_t s) {
+  hipLaunchKernelGGL(gfk_win_update, dim3(m->n_tiles + u->n_w + u->n_v + 1), dim3(UT),
+                     gfk_win_update_smem(m), s, *m, *u);
+  return (int)hipGetLastError();
+}
+
+extern "C" int gfk_win_update_set_smem(size_t bytes) {
+  return (int)hipFuncSetAttribute((const void*)gfk_win_update,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}

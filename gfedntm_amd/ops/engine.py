@@ -1,23 +1,32 @@
 """Fused HIP engine: the MI355X local step.
 
 One local step (reference federated_avitm.py:51-83: zero_grad -> forward ->
-loss -> backward -> Adam) runs as 8 hand-written CDNA4 kernels launched from
-C++ (csrc/step.cpp) on the current HIP stream:
+loss -> backward -> Adam) runs as a short chain of hand-written CDNA4 kernels
+launched from C++ (csrc/step.cpp) on the current HIP stream:
 
-  ProdLDA: encoder_fwd -> posterior_fwd -> prodlda_fwd -> row_loss -> prodlda_bwd
-           -> posterior_bwd -> encoder_bwd_scatter -> adam(+FedAvg pre-scale)
-  NeuralLDA: lda_beta_fwd -> encoder_fwd -> posterior_fwd -> lda_row_loss_bwd
-           -> posterior_bwd -> lda_beta_bwd -> encoder_bwd_scatter -> adam
+  ProdLDA:   enc_in -> post_fwd -> prodlda_fwd -> row_loss -> prodlda_bwd
+             -> row_bwd -> post_bwd -> win_update
+  NeuralLDA: lda_beta_fwd -> enc_in -> post_fwd -> lda_row_loss_bwd -> row_bwd
+             -> post_bwd -> lda_beta_bwd -> win_update -> adam
+
+In the fused update mode (ProdLDA default) there is no optimizer kernel: every
+tensor's Adam update (and the FedAvg pre-scale w_i = n_i / sum n of the shared
+tensors) is applied in the epilogue of the kernel that completes its gradient
+(beta in prodlda_bwd; W_in and the small MLP tensors -- as batch-reduction
+GEMM tiles and column sums -- in win_update).  The gradient mode writes gradients into a flat buffer instead and
+appends the generic multi-segment Adam kernel (used by NeuralLDA, by the tests
+as the oracle of the fused epilogues, and by gradient-sharing variants).
 
 Everything the step reads or writes is device resident: the CSR shard, the
-batch plan, the step / Adam counters (advanced by the kernels themselves), the
-Philox RNG (keyed by seed and step), the loss history.  That makes the whole
-step capturable once into a hipGraph and replayed with no host work at all.
+batch plan, the step / Adam counters and bias-correction powers (advanced by
+the kernels themselves), the Philox RNG (keyed by seed and step), the loss
+history.  That makes the whole step capturable once into a hipGraph and
+replayed with no host work at all.
 
 Parameters live in the model's :class:`FlatState` buffer (views back to the
-reference-keyed nn.Module); gradients, Adam moments use the same layout, so
-Adam is one multi-segment launch and the FedAvg collective is one contiguous
-all-reduce of ``flat.shared``.
+reference-keyed nn.Module); gradients and Adam moments use the same layout, so
+kernels reach a parameter's moments at a fixed offset and the FedAvg
+collective is one contiguous all-reduce of ``flat.shared``.
 """
 from __future__ import annotations
 
@@ -69,11 +78,27 @@ def supports(tm, explain: bool = False) -> bool:
     return _explain(need <= LDS_LIMIT, f"LDS budget exceeded ({need} B)", explain)
 
 
+UPDATE_GRAD, UPDATE_FUSED = 0, 1
+
+
 def theta_stride(K: int) -> int:
     """Row stride of the dropped-out theta workspace: K rounded up to 4 x odd, so
     16 consecutive rows land on distinct LDS bank groups in the decoder MFMAs."""
     kt = -(-K // 4) * 4
     return kt + 4 if (kt // 4) % 2 == 0 else kt
+
+
+def _shape_model(tm, bmax: int) -> "abi.GfkModel":
+    m = abi.GfkModel()
+    hs = list(tm.hidden_sizes)
+    m.bmax, m.V, m.K, m.n_hidden = bmax, tm.input_size, tm.n_components, len(hs)
+    for i, h in enumerate(hs):
+        m.H[i] = h
+    m.kind = abi.KIND_PRODLDA if tm.model_type.lower() == "prodlda" else abi.KIND_LDA
+    m.kt = theta_stride(m.K)
+    m.vb, m.n_tiles = VB, -(-m.V // VB)
+    m.n_dpart = m.n_tiles if m.kind == abi.KIND_PRODLDA else 1
+    return m
 
 
 def lds_required(tm, bmax: int) -> int:
@@ -91,7 +116,7 @@ def lds_required(tm, bmax: int) -> int:
     m.stage_flags = 0
     lib = native.kernels()
     which = (0, 1) if m.kind == abi.KIND_PRODLDA else (2, 3)
-    return int(max(lib.gfk_smem_required(C.byref(m), w) for w in which + (4, 5)))
+    return int(max(lib.gfk_smem_required(C.byref(m), w) for w in which + (4, 5, 7)))
 
 
 class FusedAdamState:
@@ -139,7 +164,7 @@ class FusedAdamState:
             e.view_like(e.exp_avg_sq, name).copy_(torch.as_tensor(st["exp_avg_sq"]))
             step = st["step"]
             t = int(step.item() if isinstance(step, torch.Tensor) else step)
-        e.adam_t.fill_(t)
+        e.set_adam_t(t)
         e._rebuild_adam()
 
     def zero_grad(self, set_to_none: bool = False):
@@ -160,6 +185,9 @@ class FusedEngine(EngineBase):
         self.exp_avg_sq = torch.zeros_like(self.flat.buffer)
         self.d_step = torch.zeros(1, dtype=torch.int32, device=dev)
         self.adam_t = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.adam_pow = torch.ones(2, dtype=torch.float64, device=dev)     # beta1^t, beta2^t
+        self.adam_coef = torch.zeros(2, dtype=torch.float32, device=dev)   # see csrc/gfk_common.h
+        self.update_mode = UPDATE_FUSED if tm.model.is_prodlda else UPDATE_GRAD
         self.lr, self.beta1, self.beta2 = float(tm.lr), float(tm.momentum), 0.99
         self.eps, self.weight_decay = 1e-8, 0.0
         self.fedavg_scale: Optional[float] = None
@@ -173,6 +201,7 @@ class FusedEngine(EngineBase):
         self._graph_key = None
         self._m = abi.GfkModel()
         self._a = abi.GfkAdam()
+        self._u = abi.GfkUpdate()
         self._phases = None
         self._nb_int = {}
         self._fill_static()
@@ -188,16 +217,29 @@ class FusedEngine(EngineBase):
         return flat.view(s.shape)
 
     def gradient(self, key: str) -> torch.Tensor:
-        """The pending gradient of parameter ``key`` (before Adam consumes it): slab
-        tensors are reduced here exactly as the fused Adam reduces them."""
-        if key in getattr(self, "slab_off", {}):
-            n = self.flat.slots[key].numel
-            o = self.slab_off[key]
-            slabs = self.slab.view(self.n_slab, self.slab_stride)[:, o:o + n]
-            g = slabs.sum(0)
-            s = self.flat.slots[key]
-            return g.view(s.shape[1], s.shape[0]).t() if s.transposed else g.view(s.shape)
+        """The pending gradient of parameter ``key`` (gradient mode, before Adam
+        consumes it)."""
+        if self.update_mode != UPDATE_GRAD:
+            raise RuntimeError("gradients are only materialised in gradient mode")
         return self.view_like(self.grad, key)
+
+    def set_update_mode(self, mode: int):
+        """UPDATE_FUSED: optimizer in the kernel epilogues; UPDATE_GRAD: kernels write
+        gradients and the generic Adam kernel follows."""
+        if mode == UPDATE_FUSED and not self.model.is_prodlda:
+            raise ValueError("the fused update mode covers ProdLDA only")
+        self.update_mode = mode
+        self._m.update_mode = mode
+        self._rebuild_adam()
+
+    def set_adam_t(self, t: int):
+        """Set the optimizer step count and the device bias-correction state."""
+        self.adam_t.fill_(t)
+        p1, p2 = float(self.beta1) ** t, float(self.beta2) ** t
+        self.adam_pow.copy_(torch.tensor([p1, p2], dtype=torch.float64))
+        if t > 0:
+            self.adam_coef.copy_(torch.tensor([self.lr / (1.0 - p1), 1.0 / np.sqrt(1.0 - p2)],
+                                              dtype=torch.float32))
 
     def _ptr(self, buf, key):
         if key not in self.flat.slots:
@@ -224,7 +266,6 @@ class FusedEngine(EngineBase):
         m.dec_grid = int(min(m.n_tiles, 2 * props.multi_processor_count))
         m.learn_priors = int(tm.learn_priors)
         m.kt = theta_stride(m.K)
-        m.scatter_chunks = 4
         m.n_dpart = m.n_tiles if m.kind == abi.KIND_PRODLDA else 1
         m.drop_enc = float(net.dropout_enc.p)
         m.drop_theta = float(model.drop_theta.p)
@@ -264,10 +305,19 @@ class FusedEngine(EngineBase):
         m.nbt_s = net.f_sigma_batchnorm.num_batches_tracked.data_ptr()
         m.nbt_beta = model.beta_batchnorm.num_batches_tracked.data_ptr()
         m.step, m.adam_t = self.d_step.data_ptr(), self.adam_t.data_ptr()
-        # stage the MLP weights into LDS when the posterior kernels still fit
-        m.stage_flags = 1
+        # optimizer (fused epilogues + generic Adam)
+        m.update_mode = self.update_mode
+        m.flat_base = P.data_ptr()
+        m.n_shared = self.flat.n_shared
+        m.off_m = (self.exp_avg.data_ptr() - P.data_ptr()) // 4
+        m.off_v = (self.exp_avg_sq.data_ptr() - P.data_ptr()) // 4
+        m.off_g = (self.grad.data_ptr() - P.data_ptr()) // 4
+        m.adam_pow, m.adam_coef = self.adam_pow.data_ptr(), self.adam_coef.data_ptr()
+        self._sync_opt_fields()
+        which = (0, 1) if m.kind == abi.KIND_PRODLDA else (2, 3)
         need = lambda: max(self.lib.gfk_smem_required(C.byref(m), w)  # noqa: E731
-                           for w in (0, 1, 2, 3, 4, 5, 7))
+                           for w in which + (4, 5, 7))
+        m.stage_flags = 1                 # MLP weights staged in LDS by enc_in / post_bwd
         if need() > LDS_LIMIT:
             m.stage_flags = 0
         if need() > LDS_LIMIT:
@@ -297,8 +347,7 @@ class FusedEngine(EngineBase):
             "col_rstd": f(m.n_tiles * VB),
             "row_part": f(max(m.n_tiles * 4 * B, m.dec_grid * K) * 2),
             "dthetad": f(m.n_dpart * B * K),
-            "dz0": f(B, hs[0]),
-            "dmu": f(B, K), "dls": f(B, K), "colpart": f((B // 4) * 9 * K),
+            "dmr": f(B, K), "dlr": f(B, K), "dmu": f(B, K), "dls": f(B, K),
             "dbsm": f(V * K if m.kind == abi.KIND_LDA else 1), "ck": f(K),
             "hctx": f(B, hs[0]),
             "tstart": torch.zeros(B * (m.n_tiles + 1), dtype=torch.int32, device=dev),
@@ -308,96 +357,115 @@ class FusedEngine(EngineBase):
         for i, h in enumerate(hs):
             ws[f"z{i}"] = f(B, h)
             ws[f"a{i}"] = f(B, h)
-        # per-workgroup gradient slabs of the small MLP tensors (posterior_bwd_mlp
-        # writes, Adam reduces): 16-float aligned, one slab per workgroup
-        self.slab_keys = ["inf_net.input_layer.bias"]
-        for l in range(len(hs) - 1):
-            self.slab_keys += [f"inf_net.hiddens.l_{l}.0.weight", f"inf_net.hiddens.l_{l}.0.bias"]
-        self.slab_keys += ["inf_net.f_mu.weight", "inf_net.f_mu.bias", "inf_net.f_sigma.weight",
-                           "inf_net.f_sigma.bias"]
-        up = lambda x: -(-x // ALIGN) * ALIGN  # noqa: E731
-        self.slab_off: Dict[str, int] = {}
-        off = 0
-        for k in self.slab_keys:
-            self.slab_off[k] = off
-            off += up(self.flat.slots[k].numel)
-        self.n_slab = B // 4                       # posterior_bwd_mlp workgroups (RPB = 4)
-        self.slab_stride = off
-        self.slab = f(self.n_slab * off)
-        sp = lambda k: self.slab.data_ptr() + 4 * self.slab_off[k]  # noqa: E731
-        m.s_b_in = sp("inf_net.input_layer.bias")
-        for l in range(len(hs) - 1):
-            m.s_w_h[l] = sp(f"inf_net.hiddens.l_{l}.0.weight")
-            m.s_b_h[l] = sp(f"inf_net.hiddens.l_{l}.0.bias")
-        m.s_w_mu, m.s_b_mu = sp("inf_net.f_mu.weight"), sp("inf_net.f_mu.bias")
-        m.s_w_s, m.s_b_s = sp("inf_net.f_sigma.weight"), sp("inf_net.f_sigma.bias")
-        m.slab_stride = off
+        ws["dtheta"] = f(B, K)            # the reduced d theta_d (row_bwd)
+        for i, h in enumerate(hs):
+            ws[f"dz{i}"] = f(B, h)
         self.ws = ws
         for k, t in ws.items():
             if k[0] in "za" and k[1:].isdigit():
                 getattr(m, "ws_" + k[0])[int(k[1:])] = t.data_ptr()
+            elif k.startswith("dz") and k[2:].isdigit():
+                m.ws_dz[int(k[2:])] = t.data_ptr()
             else:
                 setattr(m, "ws_" + k, t.data_ptr())
+        self._build_update_jobs()
 
-    def _rebuild_adam(self):
-        """Segment table: [start, end) float ranges with ADAM and/or SCALE flags."""
-        a = self._a
+    def _build_update_jobs(self):
+        """The small-tensor gradient / update jobs of win_update (csrc/update.hip):
+        64 x 64 GEMM tiles for the hidden / head weights, batch column sums for the
+        biases, the priors' gradient (from post_bwd)."""
+        u, ws, P = self._u, self.ws, self.flat.buffer
+        hs = list(self.tm.hidden_sizes)
+        K = self._m.K
+        wj = []
+        for l in range(len(hs) - 1):
+            wj.append((f"inf_net.hiddens.l_{l}.0.weight", ws[f"dz{l + 1}"], ws[f"a{l}"], hs[l + 1], hs[l]))
+        wj.append(("inf_net.f_mu.weight", ws["dmr"], ws["hd"], K, hs[-1]))
+        wj.append(("inf_net.f_sigma.weight", ws["dlr"], ws["hd"], K, hs[-1]))
+        n = 0
+        for key, dz, a, rows, cols in wj:
+            for j0 in range(0, rows, 64):
+                for i0 in range(0, cols, 64):
+                    if n >= abi.MAX_WJOBS:
+                        raise RuntimeError("too many weight tiles for the fused update")
+                    J = u.w[n]
+                    J.param, J.dz, J.a = self._ptr(P, key), dz.data_ptr(), a.data_ptr()
+                    J.rows, J.cols, J.j0, J.i0 = rows, cols, j0, i0
+                    n += 1
+        u.n_w = n
+        vj = [("inf_net.input_layer.bias", ws["dz0"], hs[0])]
+        for l in range(len(hs) - 1):
+            vj.append((f"inf_net.hiddens.l_{l}.0.bias", ws[f"dz{l + 1}"], hs[l + 1]))
+        vj += [("inf_net.f_mu.bias", ws["dmr"], K), ("inf_net.f_sigma.bias", ws["dlr"], K)]
+        if self.tm.learn_priors:
+            vj += [("prior_mean", None, K), ("prior_variance", None, K)]
+        for i, (key, src, nn_) in enumerate(vj):
+            V = u.v[i]
+            V.param, V.src, V.n = self._ptr(P, key), (src.data_ptr() if src is not None else None), nn_
+        u.n_v = len(vj)
+
+    def _sync_opt_fields(self):
+        m = self._m
+        m.lr, m.beta1, m.beta2 = self.lr, self.beta1, self.beta2
+        m.adam_eps, m.weight_decay = self.eps, self.weight_decay
+        m.fed_scale_on = int(self.fedavg_scale is not None)
+        m.fed_scale = 1.0 if self.fedavg_scale is None else float(self.fedavg_scale)
+
+    def _fill_adam(self, a, keys=None):
+        """Segment table of a GfkAdam: [start, end) float ranges of parameters (all,
+        or the slots of ``keys``) with ADAM, plus SCALE on the shared prefix.
+        Batch-norm running statistics are scaled by the kernels that update them.
+        Returns the number of workgroups (1024 float4 each)."""
         a.p, a.g = self.flat.buffer.data_ptr(), self.grad.data_ptr()
         a.m, a.v = self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr()
         a.lr, a.beta1, a.beta2 = self.lr, self.beta1, self.beta2
         a.eps, a.weight_decay = self.eps, self.weight_decay
         a.scale = 1.0 if self.fedavg_scale is None else float(self.fedavg_scale)
         a.t = self.adam_t.data_ptr()
+        a.coef = self.adam_coef.data_ptr()
         up = lambda x: -(-x // ALIGN) * ALIGN  # noqa: E731
         n_total = self.flat.n_total
         shared_end = up(self.flat.n_shared) if self.fedavg_scale is not None else 0
-        pr = [(s0, up(s1)) for s0, s1 in self.flat.param_ranges()]
-        slab_rng = {}
-        for k in self.slab_keys:
-            sl = self.flat.slots[k]
-            slab_rng[k] = (sl.offset, sl.offset + up(sl.numel))
-        cuts = sorted({0, n_total, shared_end} | {x for r in pr for x in r}
-                      | {x for r in slab_rng.values() for x in r})
+        if keys is None:
+            pr = [(s0, up(s1)) for s0, s1 in self.flat.param_ranges()]
+        else:
+            pr = [(self.flat.slots[k].offset, up(self.flat.slots[k].offset + self.flat.slots[k].numel))
+                  for k in keys]
+        cuts = sorted({0, n_total, shared_end} | {x for r in pr for x in r})
         segs: List[List[int]] = []
         for x0, x1 in zip(cuts[:-1], cuts[1:]):
-            if x1 <= x0:
+            if x1 <= x0 or not any(s0 <= x0 and x1 <= s1 for s0, s1 in pr):
                 continue
-            flags = 0
-            if any(s0 <= x0 and x1 <= s1 for s0, s1 in pr):
-                flags |= abi.SEG_ADAM
-            if x1 <= shared_end:
-                flags |= abi.SEG_SCALE
-            if flags == 0:
-                continue
-            slab = None
-            for k, (r0, r1) in slab_rng.items():
-                if r0 <= x0 and x1 <= r1 and flags & abi.SEG_ADAM:
-                    slab = self.slab.data_ptr() + 4 * (self.slab_off[k] + x0 - r0)
-            if segs and segs[-1][1] == x0 and segs[-1][2] == flags and slab is None \
-                    and segs[-1][3] is None:
+            flags = abi.SEG_ADAM | (abi.SEG_SCALE if x1 <= shared_end else 0)
+            if segs and segs[-1][1] == x0 and segs[-1][2] == flags:
                 segs[-1][1] = x1
             else:
-                segs.append([x0, x1, flags, slab])
+                segs.append([x0, x1, flags])
         if len(segs) > abi.MAX_SEGS:
             raise RuntimeError("too many Adam segments")
         a.n_seg = len(segs)
-        for i, (s0, s1, fl, slab) in enumerate(segs):
-            a.seg_start[i], a.seg_end[i], a.seg_flags[i] = s0, s1, fl
-            a.seg_slab[i] = slab
-        a.slab_stride, a.n_slab = self.slab_stride, self.n_slab
-        # one workgroup per 1024 float4s of each segment (csrc/adam.hip block mapping)
         nblk = 0
-        for i, sg in enumerate(segs):
+        for i, (s0, s1, fl) in enumerate(segs):
+            a.seg_start[i], a.seg_end[i], a.seg_flags[i] = s0, s1, fl
             a.seg_first_block[i] = nblk
-            nblk += -(-((sg[1] - sg[0]) // 4) // 1024)
-        self.adam_grid = int(max(1, nblk))
+            nblk += -(-((s1 - s0) // 4) // 1024)
+        return nblk
+
+    def _rebuild_adam(self):
+        self._sync_opt_fields()
+        self.adam_grid = int(max(1, self._fill_adam(self._a)))
         self._invalidate_graph()
 
     def set_fedavg_scale(self, w: Optional[float]):
-        """Pre-scale the shared state by w after Adam (None disables)."""
+        """Pre-scale the shared state by w after the update (None disables)."""
         if w != self.fedavg_scale:
             self.fedavg_scale = w
             self._rebuild_adam()
+
+    def set_lr(self, lr: float):
+        self.lr = float(lr)
+        self.optimizer.param_groups[0]["lr"] = self.lr
+        self._rebuild_adam()
 
     # ------------------------------------------------------------------ data
     def bind_data(self, data: DeviceCSR, plan: BatchPlan):
@@ -416,24 +484,22 @@ class FusedEngine(EngineBase):
         m.plan_size = self._plan_dev["size"].data_ptr()
         m.loss_hist = self.loss_hist.data_ptr()
         m.n_steps = plan.n_steps
-        # wide scatter grid: 64 non-zeros per workgroup chunk, enough chunks for the
-        # longest document (rows loop over chunks beyond that)
-        lens = (data.indptr[1:] - data.indptr[:-1]).cpu().numpy()
-        maxlen = int(lens.max()) if len(lens) else 1
-        m.scatter_chunks = int(min(16, max(1, -(-maxlen // 64))))
         self.d_step.zero_()
         self._host_step = 0
         self._invalidate_graph()
         self._launch([abi.PH_BATCH_PREP])
 
     def phases(self) -> List[int]:
-        return abi.PRODLDA_STEP if self._m.kind == abi.KIND_PRODLDA else abi.LDA_STEP
+        if self._m.kind == abi.KIND_LDA:
+            return abi.LDA_STEP
+        return abi.PRODLDA_STEP + ([abi.PH_ADAM] if self.update_mode == UPDATE_GRAD else [])
 
     # ------------------------------------------------------------------ step
     def _launch(self, phases):
         arr, n = abi.phase_array(phases)
         stream = torch.cuda.current_stream(self.device).cuda_stream
-        rc = self.lib.gfk_run(C.byref(self._m), C.byref(self._a), self.adam_grid, stream, arr, n)
+        rc = self.lib.gfk_run(C.byref(self._m), C.byref(self._a), self.adam_grid,
+                              C.byref(self._u), stream, arr, n)
         if rc:
             raise RuntimeError(f"gfk_run failed: code {rc}")
 
@@ -451,7 +517,8 @@ class FusedEngine(EngineBase):
     def _capture(self):
         # warm-up on a side stream is not needed: no lazy allocation in gfk_run
         g = torch.cuda.CUDAGraph()
-        saved = (self.d_step.clone(), self.adam_t.clone())
+        saved = (self.d_step.clone(), self.adam_t.clone(), self.adam_pow.clone(),
+                 self.adam_coef.clone())
         snap = self._snapshot()
         with torch.cuda.graph(g):
             self._launch(self.phases())
@@ -459,6 +526,8 @@ class FusedEngine(EngineBase):
         self._restore(snap)
         self.d_step.copy_(saved[0])
         self.adam_t.copy_(saved[1])
+        self.adam_pow.copy_(saved[2])
+        self.adam_coef.copy_(saved[3])
         self._graph = g
 
     def _snapshot(self):

@@ -32,10 +32,13 @@ PH_ENC_BWD = 10
 PH_ADAM = 11
 PH_BATCH_PREP = 12
 
-# PH_POST_BWD = posterior_bwd_rows + posterior_bwd_mlp; PH_ENC_BWD = the wide
-# sparse scatter of the input-layer gradient
+# PH_ENC_FWD = enc_in (sparse gather, MLP, heads, random draws), PH_POST_FWD =
+# post_fwd (batch-norm, reparameterisation, softmax, KL), PH_POST_BWD = row_bwd +
+# post_bwd, PH_ENC_BWD = win_update (W_in tiles, small-tensor gradient tiles,
+# fused updates, next-batch prep).  In fused-update mode the optimizer step lives
+# in the kernel epilogues; gradient mode appends the generic Adam.
 PRODLDA_STEP = [PH_ENC_FWD, PH_POST_FWD, PH_PRODLDA_FWD, PH_PRODLDA_LOSS, PH_PRODLDA_BWD,
-                PH_POST_BWD, PH_ENC_BWD, PH_ADAM]
+                PH_POST_BWD, PH_ENC_BWD]
 LDA_STEP = [PH_LDA_BETA_FWD, PH_ENC_FWD, PH_POST_FWD, PH_LDA_ROW, PH_POST_BWD, PH_LDA_BETA_BWD,
             PH_ENC_BWD, PH_ADAM]
 
@@ -61,8 +64,6 @@ class GfkModel(C.Structure):
         ("g_prior_mean", P), ("g_prior_var", P), ("g_beta", P), ("g_w_in", P), ("g_b_in", P),
         ("g_w_h", P * MAX_LAYERS), ("g_b_h", P * MAX_LAYERS),
         ("g_w_mu", P), ("g_b_mu", P), ("g_w_s", P), ("g_b_s", P),
-        ("s_b_in", P), ("s_w_h", P * MAX_LAYERS), ("s_b_h", P * MAX_LAYERS),
-        ("s_w_mu", P), ("s_b_mu", P), ("s_w_s", P), ("s_b_s", P), ("slab_stride", C.c_int64),
         ("indptr", P), ("indices", P), ("values", P), ("ctx", P),
         ("plan_order", P), ("plan_start", P), ("plan_size", P),
         ("step", P), ("adam_t", P), ("loss_hist", P),
@@ -70,11 +71,34 @@ class GfkModel(C.Structure):
         ("ws_mu_raw", P), ("ws_ls_raw", P), ("ws_mu", P), ("ws_ls", P), ("ws_bn_rstd", P),
         ("ws_eps", P), ("ws_theta", P), ("ws_mask_t", P), ("ws_thetad", P),
         ("ws_kl", P), ("ws_rl", P), ("ws_lse", P), ("ws_s", P),
-        ("ws_zn", P), ("ws_col_rstd", P), ("ws_row_part", P), ("ws_dthetad", P), ("ws_dz0", P),
-        ("ws_dmu", P), ("ws_dls", P), ("ws_colpart", P),
+        ("ws_zn", P), ("ws_col_rstd", P), ("ws_row_part", P), ("ws_dthetad", P),
+        ("ws_dz", P * MAX_LAYERS), ("ws_dmr", P), ("ws_dlr", P),
+        ("ws_dmu", P), ("ws_dls", P),
         ("ws_dbsm", P), ("ws_ck", P), ("ws_hctx", P), ("ws_tstart", P), ("ws_erange", P),
         ("ws_next", P), ("dbg", P),
+        ("lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float), ("adam_eps", C.c_float),
+        ("weight_decay", C.c_float), ("fed_scale", C.c_float), ("update_mode", C.c_int32),
+        ("fed_scale_on", C.c_int32), ("flat_base", P), ("n_shared", C.c_int64),
+        ("off_m", C.c_int64), ("off_v", C.c_int64), ("off_g", C.c_int64),
+        ("adam_pow", P), ("adam_coef", P), ("ws_dtheta", P),
     ]
+
+
+class GfkWJob(C.Structure):
+    _fields_ = [("param", P), ("dz", P), ("a", P), ("rows", C.c_int32), ("cols", C.c_int32),
+                ("j0", C.c_int32), ("i0", C.c_int32)]
+
+
+class GfkVJob(C.Structure):
+    _fields_ = [("param", P), ("src", P), ("n", C.c_int32), ("pad", C.c_int32)]
+
+
+MAX_WJOBS, MAX_VJOBS = 24, 16
+
+
+class GfkUpdate(C.Structure):
+    _fields_ = [("n_w", C.c_int32), ("n_v", C.c_int32), ("w", GfkWJob * MAX_WJOBS),
+                ("v", GfkVJob * MAX_VJOBS)]
 
 
 class GfkAdam(C.Structure):
@@ -85,10 +109,8 @@ class GfkAdam(C.Structure):
         ("seg_flags", C.c_int32 * MAX_SEGS),
         ("lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float),
         ("weight_decay", C.c_float), ("scale", C.c_float),
-        ("t", P),
-        ("seg_slab", P * MAX_SEGS), ("seg_first_block", C.c_int32 * MAX_SEGS),
-        ("slab_stride", C.c_int64), ("n_slab", C.c_int32),
-        ("pad2", C.c_int32), ("dbg", P),
+        ("t", P), ("coef", P),
+        ("seg_first_block", C.c_int32 * MAX_SEGS), ("dbg", P),
     ]
 
 
@@ -108,10 +130,13 @@ def declare(lib: C.CDLL) -> None:
     if lib.gfk_adam_struct_size() != C.sizeof(GfkAdam):
         raise RuntimeError(f"GfkAdam ABI mismatch: C {lib.gfk_adam_struct_size()} vs "
                            f"ctypes {C.sizeof(GfkAdam)}")
+    lib.gfk_update_struct_size.restype = C.c_size_t
+    if lib.gfk_update_struct_size() != C.sizeof(GfkUpdate):
+        raise RuntimeError("GfkUpdate ABI mismatch")
     lib.gfk_setup.argtypes = [C.POINTER(GfkModel)]
     lib.gfk_setup.restype = C.c_int
-    lib.gfk_run.argtypes = [C.POINTER(GfkModel), C.POINTER(GfkAdam), C.c_int, C.c_void_p,
-                            C.POINTER(C.c_int32), C.c_int]
+    lib.gfk_run.argtypes = [C.POINTER(GfkModel), C.POINTER(GfkAdam), C.c_int, C.POINTER(GfkUpdate),
+                            C.c_void_p, C.POINTER(C.c_int32), C.c_int]
     lib.gfk_run.restype = C.c_int
     lib.gfk_smem_required.argtypes = [C.POINTER(GfkModel), C.c_int]
     lib.gfk_smem_required.restype = C.c_size_t

@@ -1,4 +1,4 @@
-"""Diagnostic: per-phase cycle shares of the single-workgroup posterior kernels.
+"""Diagnostic: per-phase cycle counts inside the fused-step kernels (s_memtime stamps).
 
 Builds a -DGFK_STAMPS copy of the kernel library into build/stamps/, runs a few
 eager steps and prints the s_memtime deltas between phase stamps (lane 0 of
@@ -9,7 +9,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 out = os.path.join(ROOT, "build", "stamps")
 os.makedirs(out, exist_ok=True)
-srcs = ["encoder.hip", "posterior.hip", "prodlda.hip", "neurallda.hip", "adam.hip", "step.cpp"]
+from tools.build_native import KERNEL_SRCS
+srcs = [x for x in KERNEL_SRCS if os.path.exists(os.path.join(ROOT, "csrc", x))]
 objs = []
 for s in srcs:
     o = os.path.join(out, s + ".o")
@@ -37,14 +38,10 @@ for s in range(20):
     tm.engine.step(s)
 torch.cuda.synchronize()
 d = dbg.cpu().numpy()
-print("posterior_fwd cycles:", {n: int(d[i + 1] - d[i]) for i, n in enumerate(["stage", "colstats", "rows"])})
-print("posterior_bwd_rows cycles:", int(d[9] - d[8]))
-print("posterior_bwd_mlp cycles:", {n: int(d[11 + i] - d[10 + i]) for i, n in enumerate(["loads", "bn_bwd", "heads", "layers+dz0"])})
 nf = ["stage", "mfma", "bn", "store+rowlse"]
 print("prodlda_fwd cycles:", {nf[i]: int(d[17 + i] - d[16 + i]) for i in range(4)})
-nbw = ["stage", "sparse", "dense+bn_bwd", "mfma+atomics"]
+nbw = ["stage", "sparse", "dense+bn_bwd", "mfma+update"]
 print("prodlda_bwd cycles:", {nbw[i]: int(d[25 + i] - d[24 + i]) for i in range(4)})
-d16 = int(d[16])
-print("prodlda_fwd staging detail (cycles from kernel start): glds issued", int(d[21]) - d16,
-      "| scalars+nb", int(d[22]) - d16, "| beta staged", int(d[23]) - d16, "| barrier", int(d[17]) - d16)
-print("adam cycles: prologue+segment", int(d[33] - d[32]), "| body", int(d[34] - d[33]))
+print("post_fwd cycles: stage", int(d[1] - d[0]), "| colstats", int(d[2] - d[1]), "| row", int(d[3] - d[2]))
+print("row_bwd cycles:", int(d[9] - d[8]))
+print("post_bwd cycles: stage", int(d[11] - d[10]), "| colsums", int(d[12] - d[11]), "| rest", int(d[13] - d[12]))
