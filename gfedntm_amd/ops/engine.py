@@ -68,8 +68,9 @@ def supports(tm, explain: bool = False) -> bool:
          "hidden layers too wide / too many"),
         (getattr(tm, "label_size", 0) == 0, "CTM labels not fused"),
     ]
-    if getattr(tm, "kind", "avitm") == "ctm":
-        checks.append((tm.inference_type in ("combined", "zeroshot"), "unknown CTM encoder"))
+    # CTM encoders need the dense contextual GEMM (ws_hctx) before enc_in; until that
+    # is wired into the fused step they run on the PyTorch backend.
+    checks.append((getattr(tm, "kind", "avitm") != "ctm", "CTM encoders run on the torch backend"))
     for ok, why in checks:
         if not _explain(ok, why, explain):
             return False
