@@ -41,7 +41,7 @@ class ClientCorpus:
 
     def local_terms(self) -> List[str]:
         if self.synthetic is not None:
-            return node_vocabulary_terms(self.synthetic, self.node)
+            return sorted(node_vocabulary_terms(self.synthetic, self.node))
         return sorted(local_vocabulary(self.texts))
 
     def bow(self, vocab: Dict[str, int]) -> sp.csr_matrix:

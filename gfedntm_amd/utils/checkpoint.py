@@ -37,6 +37,10 @@ def save_client_checkpoint(ckpt_dir: str, client, round_: int) -> str:
         "book": {k: getattr(client, k) for k in _BOOK},
         "best_loss_train": float(tm.best_loss_train),
         "seed": int(getattr(eng, "seed", 0)),
+        # the torch engine draws dropout / reparameterisation noise from the global RNG
+        "rng_cpu": torch.get_rng_state(),
+        "rng_cuda": (torch.cuda.get_rng_state(eng.device) if eng.device.type == "cuda"
+                     else torch.zeros(0, dtype=torch.uint8)),
     }
     path = checkpoint_path(ckpt_dir, client.id, round_)
     tmp = path + ".tmp"
@@ -69,6 +73,9 @@ def load_client_checkpoint(ckpt_dir: str, client, round_: Optional[int] = None) 
     for k, v in st["book"].items():
         setattr(client, k, v)
     tm.best_loss_train = st["best_loss_train"]
+    torch.set_rng_state(st["rng_cpu"])
+    if eng.device.type == "cuda" and st["rng_cuda"].numel():
+        torch.cuda.set_rng_state(st["rng_cuda"], eng.device)
     if hasattr(eng, "seed") and hasattr(eng, "_m"):
         eng.seed = st["seed"]
         eng._m.seed = st["seed"]

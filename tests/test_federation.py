@@ -1,0 +1,174 @@
+"""Federation protocol on CPU: reference round semantics (golden simulation),
+checkpoint / resume, gloo multi-process, CLI."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from gfedntm_amd.data.synthetic import generate_synthetic
+from gfedntm_amd.eval.export import load_model_npz
+from gfedntm_amd.federation.data import ClientCorpus, load_client_corpus
+from gfedntm_amd.federation.runner import LocalFederation
+from gfedntm_amd.models.engine import make_optimizer
+from gfedntm_amd.models.networks import kl_terms, reconstruction_terms
+from gfedntm_amd.utils.config import load_config
+
+
+def _params(**kw):
+    p = dict(load_config().training_params)
+    p.update(num_epochs=2, batch_size=16, hidden_sizes=(16, 16), n_components=5)
+    p.update(kw)
+    return p
+
+
+def _corpora(n=3, seed=1):
+    sc = generate_synthetic(vocab_size=120, n_topics=5, n_docs=40, n_nodes=n, frozen_topics=2,
+                            nwords=(15, 30), seed=seed)
+    return [ClientCorpus(synthetic=sc, node=i) for i in range(n)]
+
+
+def test_rounds_match_reference_semantics():
+    """Every round: each client one local Adam step on its own minibatch, then the
+    sample-weighted average of the shared state (server.py:477-487) -- re-stated
+    with plain torch modules and compared tensor by tensor."""
+    fed = LocalFederation(_corpora(), _params(), max_iters=6, device="cpu", backend="torch", seed=2)
+    sds = [{k: v.clone() for k, v in c.tm.model.state_dict().items()} for c in fed.clients]
+    # golden simulation
+    from gfedntm_amd.models.networks import DecoderNetwork
+    models = []
+    for c, sd in zip(fed.clients, sds):
+        m = DecoderNetwork(c.tm.input_size, 5, "prodLDA", (16, 16), "softplus", 0.2, True)
+        m.load_state_dict(sd)
+        models.append((m, make_optimizer(m.parameters(), "adam", 2e-3, 0.99)))
+    n = np.array([c.n_docs for c in fed.clients], dtype=np.float64)
+    w = n / n.sum()
+    torch.manual_seed(7)
+    fed.run()
+    torch.manual_seed(7)
+    for it in range(6):
+        for (m, opt), c in zip(models, fed.clients):
+            ids = torch.from_numpy(c.plan.batch(it).astype(np.int64))
+            x = c.data.dense_rows(ids)
+            m.train()
+            opt.zero_grad()
+            pm, pv, mu, var, lv, wd = m(x)
+            loss = (kl_terms(pm, pv, mu, var, lv, 5) + reconstruction_terms(x, wd)).sum()
+            loss.backward()
+            opt.step()
+        avg = {}
+        for k, v in models[0][0].state_dict().items():
+            if v.is_floating_point():
+                avg[k] = sum(wi * mm.state_dict()[k] for wi, (mm, _) in zip(w, models))
+        for m, _ in models:
+            sd = m.state_dict()
+            for k, v in avg.items():
+                sd[k].copy_(v)
+    for (m, _), c in zip(models, fed.clients):
+        for k, v in m.state_dict().items():
+            torch.testing.assert_close(c.tm.model.state_dict()[k].to(v.dtype), v, rtol=1e-5,
+                                       atol=1e-6, msg=lambda s: f"{k}: {s}")
+
+
+def test_outputs_and_bookkeeping(tmp_path):
+    fed = LocalFederation(_corpora(2), _params(num_epochs=1), max_iters=5, device="cpu",
+                          backend="torch", save_client=str(tmp_path / "client"),
+                          save_server=str(tmp_path / "server"), seed=0, stamp="20240101")
+    fed.run()
+    c = fed.clients[0]
+    assert c.current_epoch >= 1 and c.samples_processed == sum(c.plan.size[:5])
+    z = load_model_npz(str(tmp_path / "client1" / "model_1_20240101.npz"))
+    assert z["betas"].shape == (5, len(fed.terms)) and z["thetas"].shape == (40, 5)
+    assert np.allclose(z["thetas"].sum(1), 1) and z["topics"].shape == (5, 10)
+    g = load_model_npz(str(tmp_path / "server" / "global_model_20240101.npz"))
+    assert set(g) == {"betas", "ntopics"}
+    # all clients hold the same (averaged) state
+    for o in fed.clients[1:]:
+        assert torch.equal(o.shared, c.shared)
+
+
+def test_checkpoint_resume_is_exact(tmp_path):
+    kw = dict(max_iters=6, device="cpu", backend="torch", seed=4)
+    torch.manual_seed(11)
+    full = LocalFederation(_corpora(), _params(), **kw)
+    full.run()
+    torch.manual_seed(11)
+    a = LocalFederation(_corpora(), _params(), checkpoint_dir=str(tmp_path), checkpoint_every=3,
+                        **dict(kw, max_iters=3))
+    a.run()
+    b = LocalFederation(_corpora(), _params(), checkpoint_dir=str(tmp_path), checkpoint_every=3,
+                        **kw)
+    assert b.round == 3
+    b.run()
+    for cf, cb in zip(full.clients, b.clients):
+        torch.testing.assert_close(cb.shared, cf.shared, rtol=0, atol=0)
+        assert cb.current_epoch == cf.current_epoch and cb.samples_processed == cf.samples_processed
+
+
+def _dist_worker(rank, world, port, tmp, q):
+    import torch.distributed as dist
+    from gfedntm_amd.federation.runner import run_distributed
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        corpus = _corpora(world)[rank]
+        out = run_distributed(corpus, _params(), max_iters=5, backend="torch", seed=0,
+                              save_client=os.path.join(tmp, "client"),
+                              save_server=os.path.join(tmp, "server"), stamp="20240101")
+        q.put((rank, out["client"].shared.numpy().copy(), out["rounds"]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_two_ranks(tmp_path):
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dist_worker, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][2] == res[1][2] == 5
+    np.testing.assert_array_equal(res[0][1], res[1][1])      # identical averaged state
+    assert os.path.exists(tmp_path / "client2" / "model_2_20240101.npz")
+    assert os.path.exists(tmp_path / "server" / "global_model_20240101.npz")
+
+
+def test_cli_local(tmp_path):
+    from gfedntm_amd.cli import main
+    out = main(["--workdir", str(tmp_path), "--min_clients_federation", "2", "--max_iters", "4",
+                "--engine", "torch", "--device", "cpu",
+                "--generate_synthetic", str(tmp_path / "syn.npz")])
+    assert out["rounds"] == 4
+    found = [f for _, _, fs in os.walk(tmp_path) for f in fs]
+    assert any(f.startswith("global_model_") for f in found)
+    assert any(f.startswith("logs_") for f in found)
+
+
+def test_load_client_corpus(tmp_path):
+    sc = generate_synthetic(vocab_size=50, n_topics=3, n_docs=10, n_nodes=2, frozen_topics=1,
+                            nwords=(5, 9), seed=0)
+    p = str(tmp_path / "c.npz")
+    sc.save_counts_npz(p)
+    c = load_client_corpus("synthetic", p, 2)
+    assert c.n_docs == 10 and c.ground_truth_thetas.shape == (10, 3)
+    ref = str(tmp_path / "ref.npz")
+    sc.save_npz(ref)                                   # reference schema (object arrays)
+    with pytest.raises(ValueError):
+        load_client_corpus("synthetic", ref, 1)
+    c2 = load_client_corpus("synthetic", ref, 1, allow_pickle=True)
+    assert c2.n_docs == 10 and c2.local_terms() == ClientCorpus(synthetic=sc, node=0).local_terms()
+    import pandas as pd
+    df = pd.DataFrame({"bow_text": ["alpha beta gamma", "beta delta", "zeta eta"],
+                       "fos": ["cs", "cs", "bio"], "embeddings": ["0.1 0.2", "0.3 0.4", "1 2"]})
+    pq = str(tmp_path / "r.parquet")
+    df.to_parquet(pq)
+    r = load_client_corpus("real", pq, 1, fos="cs")
+    assert r.n_docs == 2 and r.embeddings.shape == (2, 2) and "gamma" in r.local_terms()

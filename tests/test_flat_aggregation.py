@@ -1,0 +1,61 @@
+"""Flat state layout and the FedAvg aggregation (golden test against a numpy
+re-statement of the reference server average, server.py:477-487)."""
+import numpy as np
+import torch
+
+from gfedntm_amd.models.networks import DecoderNetwork
+from gfedntm_amd.parallel.aggregator import LocalAggregator, fedavg_weights
+from gfedntm_amd.utils.config import DEFAULT_GRADS_TO_SHARE
+from gfedntm_amd.utils.flat import ALIGN, FlatState
+
+
+def _net():
+    torch.manual_seed(0)
+    return DecoderNetwork(60, 5, "prodLDA", (8, 6), "softplus", 0.2, True)
+
+
+def test_flat_views_and_shared_prefix():
+    m = _net()
+    before = {k: v.clone() for k, v in m.state_dict().items()}
+    fs = FlatState(m, ["beta", "prior_mean", "inf_net.f_mu.weight", "not_a_key"],
+                   transposed=("inf_net.input_layer.weight",))
+    # values preserved, parameters are views of the buffer
+    for k, v in m.state_dict().items():
+        assert torch.equal(v, before[k]), k
+    assert m.beta.data_ptr() == fs.view("beta").data_ptr()
+    # shared keys come first (state_dict order), unknown keys ignored (B2)
+    offs = {k: s.offset for k, s in fs.slots.items()}
+    shared = [k for k in ("prior_mean", "beta", "inf_net.f_mu.weight")]
+    assert max(offs[k] for k in shared) < min(o for k, o in offs.items() if k not in shared)
+    assert fs.shared.numel() >= sum(fs.slots[k].numel for k in shared)
+    assert all(s.offset % ALIGN == 0 for s in fs.slots.values())
+    # transposed storage: logical [h0, V] view, physical [V, h0]
+    w = m.inf_net.input_layer.weight
+    assert w.shape == (8, 60) and fs.raw("inf_net.input_layer.weight").shape == (60, 8)
+    fs.buffer.mul_(2)
+    assert torch.equal(m.beta, 2 * before["beta"])
+
+
+def test_fedavg_golden():
+    rng = np.random.default_rng(0)
+    n = [120, 80, 200]
+    states = [rng.normal(size=1000).astype(np.float32) for _ in n]
+    # reference: average of each tensor weighted by nr_samples / total
+    ref = sum(s * (ni / sum(n)) for s, ni in zip(states, n))
+    flats = [torch.from_numpy(s.copy()) for s in states]
+    LocalAggregator(n).average_(flats)
+    for f in flats:
+        np.testing.assert_allclose(f.numpy(), ref, rtol=1e-6, atol=1e-6)
+    # pre-scaled path (what the fused engine feeds): plain sum
+    w = fedavg_weights(n)
+    flats = [torch.from_numpy(s * wi) for s, wi in zip(states, w)]
+    LocalAggregator(n).average_(flats, prescaled=True)
+    np.testing.assert_allclose(flats[0].numpy(), ref, rtol=1e-5, atol=1e-6)
+
+
+def test_default_shared_keys_on_avitm():
+    m = _net()
+    fs = FlatState(m, DEFAULT_GRADS_TO_SHARE)
+    # every float tensor of the AVITM state is shared (adapt_bert keys are absent: B2)
+    float_keys = [k for k, v in m.state_dict().items() if v.is_floating_point()]
+    assert fs.n_shared >= sum(fs.slots[k].numel for k in float_keys)
