@@ -59,6 +59,15 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--stop_at_num_epochs", action="store_true")
     p.add_argument("--allow-pickle", dest="allow_pickle", action="store_true",
                    help="load reference synthetic npz files with object arrays (trusted files only)")
+    p.add_argument("--server_address", type=str, default=None,
+                   help="grpc: server host:port (default [addresses] local of the config)")
+    p.add_argument("--client_host", type=str, default="127.0.0.1",
+                   help="grpc: host of client i's client-server, '{id}' is replaced by i "
+                        "(e.g. gfedntm-client{id})")
+    p.add_argument("--server_port", type=int, default=None,
+                   help="grpc: server listen port (default [federation] server_port)")
+    p.add_argument("--base_port", type=int, default=None,
+                   help="grpc: client i's client-server listens on base_port + i")
     p.add_argument("--generate_synthetic", type=str, default=None,
                    help="write a synthetic corpus (reference generator) to this path and use it")
     return p

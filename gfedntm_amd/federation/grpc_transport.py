@@ -1,0 +1,405 @@
+"""gRPC transport speaking the reference wire protocol (``federated.proto``).
+
+Reference: src/federation/server.py (Federation service + the training loop),
+src/federation/client.py (Client and the per-client FederationServer),
+src/federation/federation{,_client}.py (client registry).
+
+Protocol, unchanged on the wire so mixed deployments interoperate:
+
+  client  -> server  Federation.sendLocalDic(DictRequest{vocab, client_id, nr_samples})
+  client  -> server  Federation.sendGlobalDicAndInitialNN(Empty) -> FeatureUnion
+                     {dic=[global vocab], initialNN=NNUpdate{W0, Adam state},
+                      model_params, model_type}; blocks until min_clients registered
+  client  -> server  Federation.trainFederatedModel(ClientTensorRequest{READY})
+  server  -> client  FederationServer.getGradient(iter) -> ClientTensorRequest with the
+                     client's shared state after one local minibatch step
+  server  -> client  FederationServer.sendAggregatedTensor(nndata = sum_i n_i W_i / sum n)
+  server  -> client  FederationServer.sendAggregatedTensor(SERVER_STOP_TRAINING_REQUEST)
+
+Client-servers listen on ``base_port + id``; the server reaches client ``i`` at
+``client_host.format(id=i)`` (``127.0.0.1`` locally, e.g. ``gfedntm-client{id}`` in
+docker).
+
+Changes vs the reference (SURVEY 3.1 defects): clients are identified by their
+``client_id`` / ``id_machine`` rather than the connection peer (B6/B7); each
+round the gradient requests and the aggregated pushes go to all clients
+concurrently over persistent channels (no per-request channel, no sleeps: B13);
+the global model is the averaged state and is saved at the end (B4/B5); the
+server builds its W0 model properly (B1); ``stop_at_num_epochs`` ends the rounds
+early once every client reports ``current_epoch >= num_max_epochs``.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import datetime
+import logging
+import threading
+import time
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ..data.vocab import union_vocabulary, vocabulary_dict
+from ..eval.export import client_model_path, save_model_as_npz, server_model_path
+from ..utils.config import DEFAULT_GRADS_TO_SHARE
+from . import wire
+from .client import FederatedClient
+from .runner import build_dataset, make_topic_model
+from .wire import MessageType, pb
+
+
+def _grpc():
+    import grpc
+    return grpc
+
+
+def _unary(channel, service: str, method: str):
+    req, resp = wire.SERVICES[service][method]
+    return channel.unary_unary(f"/{wire.PACKAGE}.{service}/{method}",
+                               request_serializer=getattr(pb, req).SerializeToString,
+                               response_deserializer=getattr(pb, resp).FromString)
+
+
+def _handlers(service: str, impl) -> object:
+    grpc = _grpc()
+    table = {}
+    for method, (req, resp) in wire.SERVICES[service].items():
+        table[method] = grpc.unary_unary_rpc_method_handler(
+            getattr(impl, method), request_deserializer=getattr(pb, req).FromString,
+            response_serializer=getattr(pb, resp).SerializeToString)
+    return grpc.method_handlers_generic_handler(f"{wire.PACKAGE}.{service}", table)
+
+
+def weighted_average(states: List[Dict[str, np.ndarray]], n: List[int]) -> Dict[str, np.ndarray]:
+    """sum_i n_i W_i / sum n, per tensor; integer tensors are rounded back (reference
+    server.py:478-490 averages num_batches_tracked the same way)."""
+    total = float(sum(n))
+    out = {}
+    for k in states[0]:
+        acc = sum(s[k].astype(np.float64) * (ni / total) for s, ni in zip(states, n))
+        dt = states[0][k].dtype
+        out[k] = (np.rint(acc) if np.issubdtype(dt, np.integer) else acc).astype(dt)
+    return out
+
+
+# ---------------------------------------------------------------------------
+# server
+# ---------------------------------------------------------------------------
+class FederationServicer:
+    """The coordinator: vocabulary consensus, W0, and the round loop."""
+
+    def __init__(self, params: Dict, model_type: str, min_clients: int, max_iters: int,
+                 client_host: str = "127.0.0.1", base_port: int = 50051,
+                 grads_to_share=DEFAULT_GRADS_TO_SHARE, seed: int = 0,
+                 save_server: Optional[str] = None, stamp: Optional[str] = None,
+                 channel_options=(), logger=None, wait_timeout: float = 600.0,
+                 stop_at_num_epochs: bool = False):
+        self.params, self.model_type = dict(params), model_type
+        self.min_clients, self.max_iters = min_clients, max_iters
+        self.client_host, self.base_port = client_host, base_port
+        self.grads_to_share, self.seed = grads_to_share, seed
+        self.save_server = save_server
+        self.stamp = stamp or datetime.datetime.now().strftime("%Y%m%d")
+        self.channel_options = list(channel_options)
+        self.logger = logger or logging.getLogger("gfedntm_amd.server")
+        self.wait_timeout = wait_timeout
+        self.stop_at_num_epochs = stop_at_num_epochs
+        self.cond = threading.Condition()
+        self.dicts: Dict[int, Dict[str, int]] = {}
+        self.n_samples: Dict[int, int] = {}
+        self.ready: set = set()
+        self.feature_union = None
+        self.global_tm = None
+        self.aggregated = None
+        self.training: Optional[threading.Thread] = None
+        self.done = threading.Event()
+        self.error: Optional[BaseException] = None
+        self.rounds = 0
+
+    def _wait(self, pred, what: str):
+        if not self.cond.wait_for(pred, timeout=self.wait_timeout):
+            raise TimeoutError(f"timed out waiting for {what}")
+
+    # ---- Federation service ------------------------------------------------
+    def sendLocalDic(self, request, context):
+        vocab = wire.vocab_from_dictionary(request.vocab)
+        with self.cond:
+            self.dicts[int(request.client_id)] = vocab
+            self.n_samples[int(request.client_id)] = int(request.nr_samples)
+            self.cond.notify_all()
+        self.logger.info("-- -- Received vocabulary of %d terms from client %d (%d documents)",
+                         len(vocab), request.client_id, request.nr_samples)
+        return pb.Reply(length=len(vocab))
+
+    def _build_feature_union(self):
+        terms = union_vocabulary([sorted(d) for _, d in sorted(self.dicts.items())])
+        vocab = vocabulary_dict(terms)
+        self.terms = terms
+        self.logger.info("-- -- Server initializing global model (%d terms)", len(terms))
+        self.global_tm = make_topic_model(self.model_type, self.params, len(terms),
+                                          torch.device("cpu"), "torch", self.grads_to_share,
+                                          seed=self.seed, logger=self.logger)
+        sd = self.global_tm.model.state_dict()
+        nn_update = pb.NNUpdate(
+            modelUpdate=wire.model_update_from_state(sd, -1),
+            optUpdate=wire.adam_update_from_state_dict(self.global_tm.engine.optimizer_state_dict()))
+        fu = pb.FeatureUnion(initialNN=nn_update, model_params=wire.dictionary_from_params(self.params),
+                             model_type=self.model_type)
+        fu.dic.append(wire.dictionary_from_vocab(vocab))
+        self.shared_keys = [k for k in sd if k in set(self.grads_to_share)]
+        return fu
+
+    def sendGlobalDicAndInitialNN(self, request, context):
+        with self.cond:
+            self._wait(lambda: len(self.dicts) >= self.min_clients, "the vocabulary consensus")
+            if self.feature_union is None:
+                self.feature_union = self._build_feature_union()
+            return self.feature_union
+
+    def trainFederatedModel(self, request, context):
+        cid = int(request.metadata.id_machine)
+        with self.cond:
+            self.ready.add(cid)
+            self.cond.notify_all()
+            self.logger.info("-- -- Client %d ready for training", cid)
+            if len(self.ready) >= self.min_clients and self.training is None:
+                self.training = threading.Thread(target=self._train_guarded, daemon=True)
+                self.training.start()
+            self._wait(lambda: self.training is not None, "the training to start")
+        return pb.Empty()
+
+    def sendAggregatedTensor(self, request, context):
+        """Last aggregated state (pull-style access, same message as the push)."""
+        hdr = pb.MessageHeader(message_type=MessageType["SERVER_AGGREGATED_TENSOR_SEND"])
+        msg = pb.ServerAggregatedTensorRequest(header=hdr)
+        if self.aggregated is not None:
+            msg.nndata.modelUpdate.CopyFrom(wire.model_update_from_state(self.aggregated,
+                                                                         self.rounds))
+        return msg
+
+    # ---- round loop ----------------------------------------------------------
+    def client_address(self, cid: int) -> str:
+        return f"{self.client_host.format(id=cid)}:{self.base_port + cid}"
+
+    def _train_guarded(self):
+        try:
+            self.train()
+        except BaseException as e:   # surfaced by serve()
+            self.error = e
+            self.logger.exception("federated training failed")
+        finally:
+            self.done.set()
+
+    def train(self):
+        grpc = _grpc()
+        cids = sorted(self.ready)
+        n = [self.n_samples[c] for c in cids]
+        chans = {c: grpc.insecure_channel(self.client_address(c), options=self.channel_options)
+                 for c in cids}
+        get = {c: _unary(chans[c], "FederationServer", "getGradient") for c in cids}
+        push = {c: _unary(chans[c], "FederationServer", "sendAggregatedTensor") for c in cids}
+        pool = cf.ThreadPoolExecutor(max_workers=len(cids))
+        t0 = time.perf_counter()
+        try:
+            for it in range(self.max_iters):
+                req = pb.ServerGetGradientRequest(iter=it)
+                replies = list(pool.map(lambda c: get[c](req), cids))
+                states = [{u.tensor_name: wire.proto_to_numpy(u.tensor) for u in r.updates}
+                          for r in replies]
+                self.aggregated = weighted_average(states, n)
+                hdr = pb.MessageHeader(id_request=str(it),
+                                       message_type=MessageType["SERVER_AGGREGATED_TENSOR_SEND"])
+                msg = pb.ServerAggregatedTensorRequest(header=hdr)
+                msg.metadata.current_epoch = max(r.metadata.current_epoch for r in replies)
+                msg.nndata.modelUpdate.CopyFrom(wire.model_update_from_state(self.aggregated, it))
+                list(pool.map(lambda c: push[c](msg), cids))
+                self.rounds = it + 1
+                if self.stop_at_num_epochs and all(
+                        r.metadata.current_epoch >= r.metadata.num_max_epochs for r in replies):
+                    self.logger.info("-- -- All clients reached num_epochs; stopping at round %d",
+                                     self.rounds)
+                    break
+            wall = time.perf_counter() - t0
+            self.logger.info("-- -- Federated training finished: %d rounds in %.2f s", self.rounds,
+                             wall)
+            if self.aggregated is not None and self.global_tm is not None:
+                sd = self.global_tm.model.state_dict()
+                for k, v in self.aggregated.items():
+                    sd[k].copy_(torch.from_numpy(v))
+            if self.save_server and self.global_tm is not None:
+                self.logger.info("-- -- Saving global model...")
+                save_model_as_npz(server_model_path(self.save_server, self.stamp),
+                                  self.global_tm.get_topic_word_distribution(), None,
+                                  self.global_tm.n_components, None)
+            stop = pb.ServerAggregatedTensorRequest(header=pb.MessageHeader(
+                message_type=MessageType["SERVER_STOP_TRAINING_REQUEST"]))
+            list(pool.map(lambda c: push[c](stop), cids))
+        finally:
+            pool.shutdown()
+            for ch in chans.values():
+                ch.close()
+
+
+def serve(servicer: FederationServicer, port: int, options=(), max_workers: int = 32):
+    """Start the Federation service; returns the grpc server (already started)."""
+    grpc = _grpc()
+    server = grpc.server(cf.ThreadPoolExecutor(max_workers=max_workers), options=list(options))
+    server.add_generic_rpc_handlers((_handlers("Federation", servicer),))
+    bound = server.add_insecure_port(f"[::]:{port}")
+    server.start()
+    servicer.port = bound
+    return server
+
+
+# ---------------------------------------------------------------------------
+# client
+# ---------------------------------------------------------------------------
+class ClientServicer:
+    """FederationServer service of one client: one local step per getGradient."""
+
+    def __init__(self, client: FederatedClient, logger=None):
+        self.client = client
+        self.logger = logger or client.logger
+        self.sd = client.tm.model.state_dict()      # views into the flat buffer
+        self.keys = list(client.tm.flat.shared_keys)
+        self.stopped = threading.Event()
+        self.it = 0
+
+    def getGradient(self, request, context):
+        c = self.client
+        self.it = int(request.iter)
+        c.local_step(self.it)
+        hdr = pb.MessageHeader(id_request=f"ID{c.id}_{round(time.time())}",
+                               message_type=MessageType["CLIENT_TENSOR_SEND"])
+        md = pb.MessageAdditionalData(current_mb=c.current_mb, current_epoch=c.current_epoch,
+                                      num_max_epochs=c.tm.num_epochs, id_machine=c.id)
+        state = {k: self.sd[k] for k in self.keys}
+        return pb.ClientTensorRequest(header=hdr, metadata=md, updates=wire.updates_from_state(state))
+
+    def sendAggregatedTensor(self, request, context):
+        mt = request.header.message_type
+        if mt == MessageType["SERVER_AGGREGATED_TENSOR_SEND"]:
+            agg = wire.state_from_model_update(request.nndata.modelUpdate)
+            for k, v in agg.items():
+                if k in self.sd:
+                    self.sd[k].copy_(v.to(self.sd[k].device, self.sd[k].dtype))
+            self.client.end_round(self.it)
+            hdr = pb.MessageHeader(id_request=str(self.it),
+                                   message_type=MessageType["CLIENT_CONFIRM_RECEIVED"])
+        elif mt == MessageType["SERVER_STOP_TRAINING_REQUEST"]:
+            self.logger.info("-- -- Client-server %d received the stop request", self.client.id)
+            c = self.client
+            if c.save_path and not c.results_saved:
+                c.save_results(c.save_path)
+                c.results_saved = True
+            hdr = pb.MessageHeader(message_type=MessageType["CLIENT_CONFIRM_RECEIVED"])
+            self.stopped.set()
+        else:
+            raise ValueError(f"unexpected message type {mt}")
+        return pb.ClientReceivedResponse(header=hdr)
+
+
+def run_client(corpus, client_id: int, server_address: str, port: int, backend: str = "auto",
+               device=None, grads_to_share=DEFAULT_GRADS_TO_SHARE, seed: int = 0,
+               save_client: Optional[str] = None, stamp: Optional[str] = None,
+               client_options=(), server_options=(), logger=None, graph: bool = True,
+               log_every: int = 0, timeout: Optional[float] = None,
+               max_iters: int = 25000) -> FederatedClient:
+    """Runs one gRPC client to completion (STOP received); returns the client."""
+    grpc = _grpc()
+    logger = logger or logging.getLogger(f"gfedntm_amd.client{client_id}")
+    stamp = stamp or datetime.datetime.now().strftime("%Y%m%d")
+    device = torch.device(device) if device is not None else \
+        torch.device("cuda" if torch.cuda.is_available() else "cpu")
+    channel = grpc.insecure_channel(server_address, options=list(client_options))
+    try:
+        local = vocabulary_dict(corpus.local_terms())
+        reply = _unary(channel, "Federation", "sendLocalDic")(pb.DictRequest(
+            vocab=wire.dictionary_from_vocab(local), client_id=client_id, nr_samples=corpus.n_docs),
+            wait_for_ready=True, timeout=timeout)
+        logger.info("-- -- Client %d sent its vocabulary (%d terms)", client_id, reply.length)
+        fu = _unary(channel, "Federation", "sendGlobalDicAndInitialNN")(pb.Empty(), timeout=timeout)
+        vocab = wire.vocab_from_dictionary(fu.dic[0])
+        terms = [t for t, _ in sorted(vocab.items(), key=lambda kv: kv[1])]
+        params = wire.params_from_dictionary(fu.model_params)
+        ds = build_dataset(fu.model_type, corpus, vocab, terms)
+        tm = make_topic_model(fu.model_type, params, len(terms), device, backend, grads_to_share,
+                              seed=seed, logger=logger)
+        sd = tm.model.state_dict()
+        for k, v in wire.state_from_model_update(fu.initialNN.modelUpdate).items():
+            sd[k].copy_(v.to(sd[k].device, sd[k].dtype))
+        opt = wire.adam_state_dict_from_update(fu.initialNN.optUpdate)
+        if opt["state"]:
+            tm.engine.load_optimizer_state_dict(opt)
+        path = client_model_path(save_client, client_id, stamp) if save_client else None
+        client = FederatedClient(client_id, tm, ds, max_iters=max_iters,
+                                 logger=logger, seed=seed + client_id, save_path=path,
+                                 log_every=log_every, epoch_snapshots=(fu.model_type == "ctm"))
+        client.enable_graph(graph)
+        impl = ClientServicer(client, logger)
+        server = grpc.server(cf.ThreadPoolExecutor(max_workers=2), options=list(server_options))
+        server.add_generic_rpc_handlers((_handlers("FederationServer", impl),))
+        server.add_insecure_port(f"[::]:{port}")
+        server.start()
+        logger.info("-- -- Client-server %d listening on %d", client_id, port)
+        ready = pb.ClientTensorRequest(
+            header=pb.MessageHeader(message_type=MessageType["CLIENT_READY_FOR_TRAINING"]),
+            metadata=pb.MessageAdditionalData(id_machine=client_id))
+        _unary(channel, "Federation", "trainFederatedModel")(ready, timeout=timeout)
+        if not impl.stopped.wait(timeout):
+            raise TimeoutError(f"client {client_id}: no stop request received")
+        server.stop(grace=1.0).wait()
+        return client
+    finally:
+        channel.close()
+
+
+# ---------------------------------------------------------------------------
+# CLI entry points (``--backend grpc``)
+# ---------------------------------------------------------------------------
+def _base_port(args, cfg) -> int:
+    return args.base_port if args.base_port is not None else cfg.base_port
+
+
+def start_server(args, cfg):
+    from ..cli import _ensure_source, _paths
+    from ..utils.logging import setup_logger
+    stamp, _, save_server, _, logs_server = _paths(args, cfg)
+    logger = setup_logger("gfedntm_amd.server", logs_server, stamp)
+    if args.data_type == "synthetic":
+        _ensure_source(args, cfg, args.min_clients_federation)
+    svc = FederationServicer(
+        cfg.training_params, args.model_type, args.min_clients_federation, args.max_iters,
+        client_host=args.client_host, base_port=_base_port(args, cfg), grads_to_share=cfg.grads_to_share,
+        seed=args.seed, save_server=save_server, stamp=stamp,
+        channel_options=cfg.grpc_client_options(), logger=logger,
+        stop_at_num_epochs=args.stop_at_num_epochs or cfg.stop_at_num_epochs)
+    port = args.server_port if args.server_port is not None else cfg.server_port
+    server = serve(svc, port, cfg.grpc_server_options())
+    logger.info("-- -- Federation server listening on %d", svc.port)
+    svc.done.wait()
+    server.stop(grace=2.0).wait()
+    if svc.error is not None:
+        raise svc.error
+    return {"rounds": svc.rounds}
+
+
+def start_client(args, cfg):
+    from ..cli import _client_fos, _ensure_source, _paths
+    from ..utils.logging import setup_logger
+    from .data import load_client_corpus
+    stamp, save_client, _, logs_client, _ = _paths(args, cfg)
+    logger = setup_logger(f"gfedntm_amd.client{args.id}", f"{logs_client}{args.id}", stamp)
+    source = _ensure_source(args, cfg, args.min_clients_federation)
+    corpus = load_client_corpus(args.data_type, source, args.id, _client_fos(args, args.id),
+                                args.allow_pickle)
+    address = args.server_address or cfg.local_address
+    client = run_client(corpus, args.id, address, _base_port(args, cfg) + args.id,
+                        backend=args.engine or cfg.backend, device=args.device,
+                        grads_to_share=cfg.grads_to_share, seed=args.seed, save_client=save_client,
+                        stamp=stamp, client_options=cfg.grpc_client_options(),
+                        server_options=cfg.grpc_server_options(), logger=logger,
+                        graph=cfg.graph and not args.no_graph, log_every=args.log_every,
+                        max_iters=args.max_iters)
+    return {"client": client}
