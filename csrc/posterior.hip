@@ -61,11 +61,18 @@ __host__ __device__ inline int post_weight_floats(const GfkModel& m) {
 // ---------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------
+// stage_flags bit 1 (GFK_STAGE_BATCH_L2): the [B][K] batch matrices are read from
+// global memory (L2-resident) instead of being staged in LDS -- large K, where
+// four of them would not fit the 160 KiB.
+__host__ __device__ inline bool batch_in_lds(const GfkModel& m) { return !(m.stage_flags & 2); }
+
 extern "C" size_t gfk_post_fwd_smem(const GfkModel* m) {
-  return sizeof(float) * (2 * (size_t)m->bmax * m->K + 4 * (size_t)pad4(m->K));
+  const size_t mats = batch_in_lds(*m) ? 2 * (size_t)m->bmax * m->K : 0;
+  return sizeof(float) * (mats + 4 * (size_t)pad4(m->K));
 }
 
-// grid: bmax workgroups (row = blockIdx.x).  dynamic LDS: mr[B*K] + lr[B*K] + mean[2K] + rstd[2K]
+// grid: bmax workgroups (row = blockIdx.x).  dynamic LDS: mr[B*K] + lr[B*K] (unless
+// read from L2) + mean[2K] + rstd[2K]
 extern "C" __global__ void __launch_bounds__(PT) gfk_post_fwd(GfkModel m) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   int K = m.K, B = m.bmax;
@@ -74,15 +81,18 @@ extern "C" __global__ void __launch_bounds__(PT) gfk_post_fwd(GfkModel m) {
   keep(K, B, mu_raw, ls_raw, nbp);
   const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
   const int row = blockIdx.x;
-  float* mr = smem;
-  float* lr = mr + B * K;
-  float* cmean = lr + B * K;
+  const bool in_lds = batch_in_lds(m);
+  const float* mr = in_lds ? smem : mu_raw;
+  const float* lr = in_lds ? smem + B * K : ls_raw;
+  float* cmean = smem + (in_lds ? 2 * B * K : 0);
   float* crstd = cmean + 2 * pad4(K);
   GFK_STAMP(m, 0);
 
   // ---- one round: the raw heads of every row (LDS-DMA) + the own row + stats ----
-  glds_copy(mr, mu_raw, B * K, tid, PT);
-  glds_copy(lr, ls_raw, B * K, tid, PT);
+  if (in_lds) {
+    glds_copy(smem, mu_raw, B * K, tid, PT);
+    glds_copy(smem + B * K, ls_raw, B * K, tid, PT);
+  }
   const int nb = *nbp;
   constexpr int KQ = 4;                    // K <= 256
   float ep[KQ], mt[KQ], pm[KQ], pv[KQ];
@@ -308,11 +318,12 @@ struct PostLds {
 __host__ __device__ inline PostLds post_lds(const GfkModel& m) {
   PostLds L;
   const int B = m.bmax, K = m.K, hm = pad4(post_hmax(m));
+  const int mat = batch_in_lds(m) ? B * K : 0;
   int o = 0;
-  L.dmu = o; o += B * K;
-  L.dls = o; o += B * K;
-  L.mu = o; o += B * K;
-  L.ls = o; o += B * K;
+  L.dmu = o; o += mat;
+  L.dls = o; o += mat;
+  L.mu = o; o += mat;
+  L.ls = o; o += mat;
   L.sums = o; o += 4 * pad4(2 * K);
   L.dr = o; o += 2 * pad4(K);
   L.v0 = o; o += hm;
@@ -360,11 +371,14 @@ extern "C" __global__ void __launch_bounds__(PT) gfk_post_bwd(GfkModel m) {
   const bool staged = sflags & 1;
   GFK_STAMP(m, 10);
 
+  const bool in_lds = batch_in_lds(m);
   // ---- one round: the four [B][K] matrices, the own row, the weights, stats ----
-  glds_copy(smem + L.dmu, dmu_g, B * K, tid, PT);
-  glds_copy(smem + L.dls, dls_g, B * K, tid, PT);
-  glds_copy(smem + L.mu, mu_g, B * K, tid, PT);
-  glds_copy(smem + L.ls, ls_g, B * K, tid, PT);
+  if (in_lds) {
+    glds_copy(smem + L.dmu, dmu_g, B * K, tid, PT);
+    glds_copy(smem + L.dls, dls_g, B * K, tid, PT);
+    glds_copy(smem + L.mu, mu_g, B * K, tid, PT);
+    glds_copy(smem + L.ls, ls_g, B * K, tid, PT);
+  }
   {
     int o = L.zrow;
 #pragma unroll
@@ -385,8 +399,10 @@ extern "C" __global__ void __launch_bounds__(PT) gfk_post_bwd(GfkModel m) {
       if (l + 1 < nh) { glds_copy(p, m.w_h[l], m.H[l + 1] * m.H[l], tid, PT); p += pad4(m.H[l + 1] * m.H[l]); }
   }
   const int nb = *nbp;
-  float rs = 0.f;                       // rstd of column tid (< 2K)
-  if (tid < 2 * K) rs = m.ws_bn_rstd[tid];
+  constexpr int CQ = 2;                 // columns tid, tid + PT of the 2K (K <= 256)
+  float rs[CQ];                         // rstd of those columns
+#pragma unroll
+  for (int q = 0; q < CQ; ++q) rs[q] = m.ws_bn_rstd[min(tid + q * PT, 2 * K - 1)];
   // workgroup 0 extras: the loss terms, priors, NeuralLDA theta_d * d theta_d
   float lterm = 0.f, pmk = 0.f, pvk = 1.f;
   if (row == 0) {
@@ -401,10 +417,10 @@ extern "C" __global__ void __launch_bounds__(PT) gfk_post_bwd(GfkModel m) {
   GFK_STAMP(m, 11);
 
   // ---- column sums over the batch: 4 threads per column ----
-  const float* dmu = smem + L.dmu;
-  const float* dls = smem + L.dls;
-  const float* mu = smem + L.mu;
-  const float* ls = smem + L.ls;
+  const float* dmu = in_lds ? smem + L.dmu : dmu_g;
+  const float* dls = in_lds ? smem + L.dls : dls_g;
+  const float* mu = in_lds ? smem + L.mu : mu_g;
+  const float* ls = in_lds ? smem + L.ls : ls_g;
   float* S = smem + L.sums;             // [4][pad4(2K)]: sum dy, sum dy * xh, (wg 0:) sum xh / extra
   const int P2 = pad4(2 * K);
   for (int cb = 0; cb < 2 * K; cb += PT / 4) {
@@ -466,13 +482,18 @@ extern "C" __global__ void __launch_bounds__(PT) gfk_post_bwd(GfkModel m) {
 
   // ---- own row: BN backward -> d mu_raw | d ls_raw ----
   float* dr = smem + L.dr;              // [2K]: dmr then dlr
-  if (tid < 2 * K) {
-    const int k = tid < K ? tid : tid - K;
-    const float* dy = tid < K ? dmu : dls;
-    const float* xh = tid < K ? mu : ls;
-    const float v = rs * (dy[row * K + k] - S[tid] * inv_nb - xh[row * K + k] * S[P2 + tid] * inv_nb);
-    dr[tid] = v;
-    (tid < K ? m.ws_dmr : m.ws_dlr)[row * K + k] = v;
+#pragma unroll
+  for (int q = 0; q < CQ; ++q) {
+    const int c2 = tid + q * PT;
+    if (c2 < 2 * K) {
+      const int k = c2 < K ? c2 : c2 - K;
+      const float* dy = c2 < K ? dmu : dls;
+      const float* xh = c2 < K ? mu : ls;
+      const float v =
+          rs[q] * (dy[row * K + k] - S[c2] * inv_nb - xh[row * K + k] * S[P2 + c2] * inv_nb);
+      dr[c2] = v;
+      (c2 < K ? m.ws_dmr : m.ws_dlr)[row * K + k] = v;
+    }
   }
   lds_barrier();
 

@@ -45,6 +45,10 @@ from . import native
 BMAX_CHOICES = (16, 32, 64, 128)
 LDS_LIMIT = 160 * 1024
 VB = 64
+# stage_flags plans, fastest first: bit 0 = MLP weights staged in LDS (enc_in,
+# post_bwd); bit 1 = the posterior kernels read the [B, K] batch matrices from L2
+# instead of staging them (large K)
+STAGE_PLANS = (1, 0, 2)
 
 
 def _explain(ok: bool, why: str, explain: bool) -> bool:
@@ -114,10 +118,15 @@ def lds_required(tm, bmax: int) -> int:
     m.kt = theta_stride(m.K)
     m.vb, m.n_tiles = VB, -(-m.V // VB)
     m.n_dpart = m.n_tiles if m.kind == abi.KIND_PRODLDA else 1
-    m.stage_flags = 0
     lib = native.kernels()
     which = (0, 1) if m.kind == abi.KIND_PRODLDA else (2, 3)
-    return int(max(lib.gfk_smem_required(C.byref(m), w) for w in which + (4, 5, 7)))
+    need = 0
+    for flags in STAGE_PLANS[1:]:        # weights unstaged; batch matrices in LDS, then in L2
+        m.stage_flags = flags
+        need = int(max(lib.gfk_smem_required(C.byref(m), w) for w in which + (4, 5, 7)))
+        if need <= LDS_LIMIT:
+            break
+    return need
 
 
 class FusedAdamState:
@@ -318,10 +327,11 @@ class FusedEngine(EngineBase):
         which = (0, 1) if m.kind == abi.KIND_PRODLDA else (2, 3)
         need = lambda: max(self.lib.gfk_smem_required(C.byref(m), w)  # noqa: E731
                            for w in which + (4, 5, 7))
-        m.stage_flags = 1                 # MLP weights staged in LDS by enc_in / post_bwd
-        if need() > LDS_LIMIT:
-            m.stage_flags = 0
-        if need() > LDS_LIMIT:
+        for flags in STAGE_PLANS:         # first plan that fits the 160 KiB of LDS
+            m.stage_flags = flags
+            if need() <= LDS_LIMIT:
+                break
+        else:
             raise RuntimeError(f"fused step needs {need()} B of LDS (> {LDS_LIMIT})")
         self._alloc_workspace()
         rc = self.lib.gfk_setup(C.byref(m))

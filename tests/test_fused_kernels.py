@@ -61,11 +61,15 @@ def _grads_of(tm_fused):
 
 
 @pytest.mark.parametrize("model_type", ["prodLDA", "LDA"])
-@pytest.mark.parametrize("B,n_docs,K,H", [(64, 150, 20, (32, 24)), (32, 45, 20, (32, 24)),
-                                          (64, 100, 100, (40,)), (64, 200, 50, (50, 50, 50))])
-def test_step_matches_oracle(model_type, B, n_docs, K, H):
-    V = 700
+@pytest.mark.parametrize("B,n_docs,K,H,V", [(64, 150, 20, (32, 24), 700), (32, 45, 20, (32, 24), 700),
+                                            (64, 100, 100, (40,), 700),
+                                            (64, 200, 50, (50, 50, 50), 700),
+                                            (64, 100, 200, (50, 50), 700),       # K > 128, L2 mode
+                                            (64, 80, 50, (50, 50), 30000)])      # many V tiles
+def test_step_matches_oracle(model_type, B, n_docs, K, H, V):
     fused, ref = _pair(model_type, V=V, K=K, H=H, B=B)
+    if K == 200 and model_type == "prodLDA":
+        assert fused.engine._m.stage_flags & 2     # batch matrices read from L2
     X = random_csr(n_docs, V, 40, seed=1)
     data, plan = _bind(fused, X, B=B)
     e = fused.engine
