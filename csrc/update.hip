@@ -155,6 +155,7 @@ extern "C" __global__ void __launch_bounds__(UT) gfk_win_update(GfkModel m, GfkU
     if (r >= U.n_w && r < U.n_w + U.n_v) { vector_job(m, U.v[r - U.n_w]); return; }
     if (r == U.n_w + U.n_v) { prepare_next_batch(m); return; }
   }
+  if (m.input == GFK_IN_CONTEXTUAL) return;   // ZeroShotTM: W_in is the dense [C, H0] layer (host GEMM)
   const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
   int B = m.bmax, H0 = m.H[0], V = m.V, n_tiles = m.n_tiles;
   const int32_t *tstart = m.ws_tstart, *indices = m.indices, *nbp = m.ws_nb;

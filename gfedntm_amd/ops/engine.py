@@ -72,9 +72,6 @@ def supports(tm, explain: bool = False) -> bool:
          "hidden layers too wide / too many"),
         (getattr(tm, "label_size", 0) == 0, "CTM labels not fused"),
     ]
-    # CTM encoders need the dense contextual GEMM (ws_hctx) before enc_in; until that
-    # is wired into the fused step they run on the PyTorch backend.
-    checks.append((getattr(tm, "kind", "avitm") != "ctm", "CTM encoders run on the torch backend"))
     for ok, why in checks:
         if not _explain(ok, why, explain):
             return False
@@ -197,7 +194,9 @@ class FusedEngine(EngineBase):
         self.adam_t = torch.zeros(1, dtype=torch.int32, device=dev)
         self.adam_pow = torch.ones(2, dtype=torch.float64, device=dev)     # beta1^t, beta2^t
         self.adam_coef = torch.zeros(2, dtype=torch.float32, device=dev)   # see csrc/gfk_common.h
-        self.update_mode = UPDATE_FUSED if tm.model.is_prodlda else UPDATE_GRAD
+        # fused epilogue updates: ProdLDA AVITM; NeuralLDA and CTM (whose contextual
+        # tensors get their gradients from host-issued GEMMs) run the generic Adam
+        self.update_mode = UPDATE_FUSED if tm.model.is_prodlda and tm.kind != "ctm" else UPDATE_GRAD
         self.lr, self.beta1, self.beta2 = float(tm.lr), float(tm.momentum), 0.99
         self.eps, self.weight_decay = 1e-8, 0.0
         self.fedavg_scale: Optional[float] = None
@@ -236,8 +235,8 @@ class FusedEngine(EngineBase):
     def set_update_mode(self, mode: int):
         """UPDATE_FUSED: optimizer in the kernel epilogues; UPDATE_GRAD: kernels write
         gradients and the generic Adam kernel follows."""
-        if mode == UPDATE_FUSED and not self.model.is_prodlda:
-            raise ValueError("the fused update mode covers ProdLDA only")
+        if mode == UPDATE_FUSED and (not self.model.is_prodlda or self.kind == "ctm"):
+            raise ValueError("the fused update mode covers AVITM ProdLDA only")
         self.update_mode = mode
         self._m.update_mode = mode
         self._rebuild_adam()
@@ -372,6 +371,7 @@ class FusedEngine(EngineBase):
         for i, h in enumerate(hs):
             ws[f"dz{i}"] = f(B, h)
         self.ws = ws
+        self._alloc_ctx()
         for k, t in ws.items():
             if k[0] in "za" and k[1:].isdigit():
                 getattr(m, "ws_" + k[0])[int(k[1:])] = t.data_ptr()
@@ -502,11 +502,95 @@ class FusedEngine(EngineBase):
 
     def phases(self) -> List[int]:
         if self._m.kind == abi.KIND_LDA:
-            return abi.LDA_STEP
-        return abi.PRODLDA_STEP + ([abi.PH_ADAM] if self.update_mode == UPDATE_GRAD else [])
+            ph = list(abi.LDA_STEP)
+        else:
+            ph = abi.PRODLDA_STEP + ([abi.PH_ADAM] if self.update_mode == UPDATE_GRAD else [])
+        if self.kind == "ctm":
+            ph.insert(ph.index(abi.PH_ENC_FWD), abi.PH_CTX_FWD)
+            ph.insert(ph.index(abi.PH_ENC_BWD) + 1, abi.PH_CTX_BWD)
+        return ph
+
+    # ------------------------------------------------------------------ CTM
+    def _alloc_ctx(self):
+        """CTM contextual path (reference ctm inference_network.py:97-193).  The
+        dense GEMMs -- adapt_bert [B,C]x[C,V], the contextual half of input_layer
+        [B,V]x[V,H0] and their weight gradients -- are plain library GEMMs
+        (hipBLASLt through torch, fp32), issued on the step's stream between the
+        fused kernels: CTX_FWD fills ws_hctx (added to the input layer's
+        pre-activation by enc_in), CTX_BWD turns enc's d z0 into the gradients of
+        the contextual tensors (generic Adam follows).  The BoW half of input_layer
+        stays on the sparse enc_in / win_update path."""
+        self._ctx = None
+        if self.kind != "ctm":
+            return
+        m, dev = self._m, self.device
+        B, V, C, H0 = self.bmax, m.V, int(m.C), int(m.H[0])
+        z = lambda *sh: torch.zeros(*sh, dtype=torch.float32, device=dev)  # noqa: E731
+        c = {"docs": torch.zeros(B, dtype=torch.int64, device=dev),
+             "rows": torch.arange(B, dtype=torch.int32, device=dev),
+             "valid": torch.zeros(B, dtype=torch.bool, device=dev),
+             "xc": z(B, C), "dzm": z(B, H0)}
+        kw = "inf_net.input_layer.weight"
+        w_in, g_in = self.flat.raw(kw), self.raw_like(self.grad, kw)     # [n_in, H0]
+        if m.input == abi.IN_COMBINED:
+            c.update(a=z(B, V), da=z(B, V),
+                     Wa=self.flat.view("inf_net.adapt_bert.weight"),          # [V, C]
+                     ba=self.flat.view("inf_net.adapt_bert.bias"),
+                     gWa=self.view_like(self.grad, "inf_net.adapt_bert.weight"),
+                     gba=self.view_like(self.grad, "inf_net.adapt_bert.bias"),
+                     Wc=w_in[V:2 * V], gWc=g_in[V:2 * V])
+        else:
+            c.update(W=w_in, gW=g_in)                                           # [C, H0]
+        self._ctx = c
+
+    def raw_like(self, buf: torch.Tensor, key: str) -> torch.Tensor:
+        s = self.flat.slots[key]
+        flat = buf[s.offset: s.offset + s.numel]
+        return flat.view(s.shape[1], s.shape[0]) if s.transposed else flat.view(s.shape)
+
+    def _ctx_fwd(self):
+        c, ws = self._ctx, self.ws
+        if self.data is None or self.data.contextual is None:
+            raise RuntimeError("CTM needs contextual embeddings in the bound data")
+        c["docs"].copy_(ws["next"][1: 1 + self.bmax])        # this step's rows (batch prep)
+        torch.index_select(self.data.contextual, 0, c["docs"], out=c["xc"])
+        if "Wa" in c:
+            torch.addmm(c["ba"], c["xc"], c["Wa"].t(), out=c["a"])
+            torch.mm(c["a"], c["Wc"], out=ws["hctx"])
+        else:
+            torch.mm(c["xc"], c["W"], out=ws["hctx"])
+
+    def _ctx_bwd(self):
+        c, ws = self._ctx, self.ws
+        torch.lt(c["rows"], ws["nb"], out=c["valid"])         # rows >= nb hold stale d z0
+        torch.mul(ws["dz0"], c["valid"].unsqueeze(1), out=c["dzm"])
+        if "Wa" in c:
+            torch.mm(c["a"].t(), c["dzm"], out=c["gWc"])
+            torch.mm(c["dzm"], c["Wc"].t(), out=c["da"])
+            torch.mm(c["da"].t(), c["xc"], out=c["gWa"])
+            torch.sum(c["da"], 0, out=c["gba"])
+        else:
+            torch.mm(c["xc"].t(), c["dzm"], out=c["gW"])
 
     # ------------------------------------------------------------------ step
     def _launch(self, phases):
+        if any(p in abi.HOST_PHASES for p in phases):
+            run: List[int] = []
+            for p in list(phases) + [None]:
+                if p is None or p in abi.HOST_PHASES:
+                    if run:
+                        self._launch_native(run)
+                        run = []
+                    if p == abi.PH_CTX_FWD:
+                        self._ctx_fwd()
+                    elif p == abi.PH_CTX_BWD:
+                        self._ctx_bwd()
+                else:
+                    run.append(p)
+            return
+        self._launch_native(phases)
+
+    def _launch_native(self, phases):
         arr, n = abi.phase_array(phases)
         stream = torch.cuda.current_stream(self.device).cuda_stream
         rc = self.lib.gfk_run(C.byref(self._m), C.byref(self._a), self.adam_grid,
@@ -527,8 +611,15 @@ class FusedEngine(EngineBase):
 
     def _capture(self):
         # warm-up on a side stream is not needed: no lazy allocation in gfk_run
+        if self._ctx is not None:
+            # hipBLASLt picks algorithms / workspaces on a shape's first call, which is
+            # not allowed while capturing: run the host GEMMs once eagerly (their
+            # outputs are fully rewritten by the next step before anything reads them)
+            self._ctx_fwd()
+            self._ctx_bwd()
+            torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph()
-        saved = (self.d_step.clone(), self.adam_t.clone(), self.adam_pow.clone(),
+        saved =(self.d_step.clone(), self.adam_t.clone(), self.adam_pow.clone(),
                  self.adam_coef.clone())
         snap = self._snapshot()
         with torch.cuda.graph(g):

@@ -37,6 +37,12 @@ PH_BATCH_PREP = 12
 # post_bwd, PH_ENC_BWD = win_update (W_in tiles, small-tensor gradient tiles,
 # fused updates, next-batch prep).  In fused-update mode the optimizer step lives
 # in the kernel epilogues; gradient mode appends the generic Adam.
+# host-side phases (CTM): the dense contextual GEMMs around the fused kernels,
+# issued on the same stream (hipBLASLt through torch) and captured in the same graph
+PH_CTX_FWD = 100
+PH_CTX_BWD = 101
+HOST_PHASES = (PH_CTX_FWD, PH_CTX_BWD)
+
 PRODLDA_STEP = [PH_ENC_FWD, PH_POST_FWD, PH_PRODLDA_FWD, PH_PRODLDA_LOSS, PH_PRODLDA_BWD,
                 PH_POST_BWD, PH_ENC_BWD]
 LDA_STEP = [PH_LDA_BETA_FWD, PH_ENC_FWD, PH_POST_FWD, PH_LDA_ROW, PH_POST_BWD, PH_LDA_BETA_BWD,

@@ -208,3 +208,69 @@ def test_training_decreases_loss():
     h = m.engine.loss_hist.cpu().numpy()
     assert np.isfinite(h).all()
     assert h[-10:].mean() < 0.9 * h[:10].mean()
+
+
+@pytest.mark.parametrize("inference_type", ["combined", "zeroshot"])
+@pytest.mark.parametrize("model_type", ["prodLDA", "LDA"])
+def test_ctm_step_matches_oracle(inference_type, model_type):
+    """CTM on the fused engine: host GEMMs for the contextual path around the HIP
+    kernels; compared with the explicit-noise oracle through the CTM encoder."""
+    from gfedntm_amd.models import CombinedTM, ZeroShotTM
+    cls = CombinedTM if inference_type == "combined" else ZeroShotTM
+    V, K, H, B, Cdim, n_docs = 600, 20, (32, 24), 64, 96, 150
+    torch.manual_seed(0)
+    kw = dict(input_size=V, contextual_size=Cdim, n_components=K, model_type=model_type,
+              hidden_sizes=H, batch_size=B, verbose=False, device="cuda")
+    fused = cls(backend="fused", **kw)
+    assert fused.backend == "fused"
+    ref = cls(backend="torch", **kw)
+    ref.model.load_state_dict(fused.model.state_dict())
+    X = random_csr(n_docs, V, 40, seed=1)
+    ctx = np.random.default_rng(2).standard_normal((n_docs, Cdim)).astype(np.float32)
+    data = DeviceCSR(X, "cuda", contextual=ctx)
+    plan = BatchPlan.build(data.n_docs, B, 3, seed=0)
+    e = fused.engine
+    e.bind_data(data, plan)
+    phases = e.phases()
+    assert phases[-1] == abi.PH_ADAM and abi.PH_CTX_FWD in phases and abi.PH_CTX_BWD in phases
+    e.run_phases(phases[:-1])
+    torch.cuda.synchronize()
+    nb = int(plan.size[0])
+    ids = torch.from_numpy(plan.batch(0).astype(np.int64)).cuda()
+    x, xc = data.dense_rows(ids), data.contextual[ids]
+    eps = e.ws["eps"][:nb].clone()
+    mask_h = e.ws["mask_h"][:nb].clone()
+    mask_t = e.ws["mask_t"][:nb].clone()
+    ref.model.train()
+    ref.model.zero_grad()
+    net = ref.model.inf_net
+    x_enc = torch.cat([x, net.adapt_bert(xc)], 1) if inference_type == "combined" else xc
+    kw_ = float(ref.weights.get("beta", 1.0))
+    loss, kl, rl = avitm_loss_explicit(ref.model, x, eps, mask_h, mask_t, kl_weight=kw_,
+                                       x_enc=x_enc)
+    loss.backward()
+    torch.testing.assert_close(e.ws["kl"][:nb], kl.detach(), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(e.ws["rl"][:nb], rl.detach(), rtol=1e-4, atol=1e-2)
+    _check_grads(_grads_of(fused), ref)
+    e.run_phases([abi.PH_ADAM])
+    torch.cuda.synchronize()
+    assert float(e.grad.abs().max().item()) == 0.0
+
+
+def test_ctm_graph_training():
+    from gfedntm_amd.models import CombinedTM
+    V, K, B, Cdim, n_docs = 500, 10, 64, 64, 400
+    torch.manual_seed(0)
+    tm = CombinedTM(input_size=V, contextual_size=Cdim, n_components=K, hidden_sizes=(50, 50),
+                    batch_size=B, verbose=False, device="cuda", backend="fused")
+    X = random_csr(n_docs, V, 40, seed=3)
+    ctx = np.random.default_rng(4).standard_normal((n_docs, Cdim)).astype(np.float32)
+    data = DeviceCSR(X, "cuda", contextual=ctx)
+    plan = BatchPlan.build(data.n_docs, B, 200, seed=0)
+    e = tm.engine
+    e.bind_data(data, plan)
+    e.enable_graph(True)
+    for s in range(200):
+        e.step(s)
+    h = e.loss_hist[:200].cpu().numpy()
+    assert np.isfinite(h).all() and h[-20:].mean() < h[:20].mean()
