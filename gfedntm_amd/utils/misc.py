@@ -1,0 +1,60 @@
+"""Experiment helpers: Mallet corpus files and the typed experiment-config reader.
+
+Reference: src/aux_modules/utils/misc.py:206-288.  A Mallet import file has one
+document per line, ``<id> 0 <text>``.
+"""
+from __future__ import annotations
+
+import configparser
+from typing import Any, Dict
+
+_INT_KEYS = {"ntopics", "num_iterations", "batch_size", "num_threads", "optimize_interval",
+             "num_epochs", "num_samples", "num_data_loader_workers", "contextual_size",
+             "max_features"}
+_FLOAT_KEYS = {"thetas_thr", "doc_topic_thr", "alpha", "dropout_in", "dropout_out", "lr",
+               "momentum", "topic_prior_mean"}
+
+
+def mallet_corpus_to_df(corpus_file: str):
+    import pandas as pd
+    ids, texts = [], []
+    with open(corpus_file, encoding="utf-8") as f:
+        for line in f:
+            head, sep, tail = line.rstrip("\n").partition(" 0 ")
+            if not sep:
+                continue
+            ids.append(head.strip())
+            texts.append(tail.strip())
+    return pd.DataFrame({"id": ids, "text": texts})
+
+
+def corpus_df_to_mallet(corpus_df, out_file: str, id_column: str = "id",
+                        text_column: str = "text") -> None:
+    with open(out_file, "w", encoding="utf-8") as f:
+        for i, t in zip(corpus_df[id_column].astype(str), corpus_df[text_column].astype(str)):
+            f.write(f"{i} 0 {t}\n")
+
+
+def read_config_experiments(file_path: str) -> Dict[str, Any]:
+    """Flat, typed dict of every option of an experiments INI file."""
+    cp = configparser.ConfigParser()
+    cp.read(file_path)
+    out: Dict[str, Any] = {}
+    for section in cp.sections():
+        for opt in cp.options(section):
+            v = cp.get(section, opt)
+            if opt in _INT_KEYS:
+                out[opt] = int(v)
+            elif opt in _FLOAT_KEYS:
+                out[opt] = float(v)
+            elif opt == "labels":
+                out[opt] = ""
+            elif opt == "topic_prior_variance":
+                out[opt] = None
+            elif opt in ("learn_priors", "reduce_on_plateau"):
+                out[opt] = v == "True"
+            elif opt == "hidden_sizes":
+                out[opt] = tuple(int(x) for x in v.strip()[1:-1].split(",") if x.strip())
+            else:
+                out[opt] = v
+    return out
