@@ -113,10 +113,11 @@ def main():
     else:
         tm = AVITM(**kw)
     eng = tm.engine
-    agg = None
+    agg, comm = None, None
     if world > 1:
         dist.broadcast(tm.flat.buffer, src=0)        # identical W0 on every client
         agg = CollectiveAggregator()
+        comm = agg.prepare(tm.flat.shared)          # custom xGMI all-reduce if it validates
         w = agg.weights(X.shape[0], device)
         if args.backend == "fused":
             eng.set_fedavg_scale(w[rank])
@@ -152,6 +153,11 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    comm_error = 0
+    if agg is not None and agg.xgmi is not None:
+        comm_error = agg.xgmi.error()          # a timed-out wait invalidates the run
+        if comm_error:
+            raise RuntimeError(f"xGMI all-reduce reported error {comm_error}")
     ms = dt / args.steps * 1e3
     docs_per_s = n_clients * args.batch * args.steps / dt
     losses = eng.loss_hist.detach().cpu().numpy()
@@ -188,7 +194,7 @@ def main():
                        "parallelism": f"fedavg-dp{n_clients}",
                        "backend": args.backend + ("" if args.no_graph else "+hipgraph"),
                        "aggregation": "per-minibatch sample-weighted FedAvg of 20 shared tensors"
-                                      + (" (RCCL all-reduce)" if world > 1 else "")},
+                                      + (f" ({comm} all-reduce)" if world > 1 else "")},
             "npmi": None if npmi is None else round(npmi, 4),
             "final_loss": float(np.mean(losses[-20:])),
             "baseline": {"fed_grpc_8clients_docs_per_s": BASELINE_FED_DOCS_PER_S,

@@ -1,0 +1,247 @@
+// Deterministic two-shot all-reduce (SUM) over xGMI peer memory, for the
+// per-round FedAvg of the pre-scaled shared state (reference server.py:477-487:
+// sum_i n_i W_i / sum n, here sum_i (w_i W_i) with w_i applied by the update
+// kernels).
+//
+// Every rank owns a double-buffered stage [2][world * chunk] floats and a flag
+// array [2 phases][nblk][8] (uncached), both IPC-mapped into every peer.  The
+// n floats are cut into `world` chunks; chunk c is cut into `nblk` slices, and
+// workgroup b of every rank handles slice b of each chunk, so every data
+// dependency is per (workgroup, slice) and no grid-wide barrier is needed:
+//   phase 0  copy slice b of all chunks into my stage (write-through, system
+//            scope), then tell every rank (flag[0][b][me] = epoch);
+//   phase 1  once all ranks published: chunk me, slice b = sum over ranks in
+//            RANK ORDER (bit-identical everywhere: each chunk is summed by
+//            exactly one rank), into my stage and my output; flag[1][b][me];
+//   phase 2  once all ranks reduced: copy the other chunks' slice b from their
+//            owners' stages into my output.
+// Round e uses stage buffer e & 1: a rank starts overwriting a buffer only
+// after every rank passed the next round's phase 0, i.e. finished reading it.
+// The per-workgroup epoch lives in device memory (so hipGraph replays advance
+// it); every wait is bounded: on timeout the workgroup records an error word and
+// finishes (the host checks it), it never hangs the device.
+//
+// Visibility across devices (MI355X_MICROARCH.md inter-workgroup rules, lifted
+// to system scope): payload stores sc0 sc1 (write-through) -> s_waitcnt
+// vmcnt(0) -> barrier -> system release -> one lane per rank stores the flag at
+// system scope; consumers poll relaxed at system scope, one system acquire, then
+// sc0 sc1 loads of the payload.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace {
+constexpr int CMAX = 8;          // ranks (one node)
+constexpr int CT = 256;          // threads per workgroup
+constexpr int AUX_SYS = 17;      // cache policy sc0 | sc1: system coherence
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+}  // namespace
+
+struct GfkComm {
+  float* stage[2][CMAX];         // every rank's stage buffers (own one included)
+  uint32_t* flags[CMAX];         // every rank's flag array [2][nblk][CMAX]
+  uint32_t* epoch;               // own per-workgroup round counter [nblk]
+  int32_t* err;                  // own error word (timeouts)
+  int32_t rank, world, nblk, spin_limit;
+  int64_t n, chunk, slice;       // floats; chunk, slice multiples of 4
+};
+
+namespace {
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ float4 ld_sys(__amdgpu_buffer_rsrc_t r, int64_t i) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(i * 4), 0, AUX_SYS);
+  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
+                     __uint_as_float(v.w));
+}
+
+__device__ __forceinline__ void st_sys(__amdgpu_buffer_rsrc_t r, int64_t i, float4 f) {
+  u32x4 v;
+  v.x = __float_as_uint(f.x); v.y = __float_as_uint(f.y);
+  v.z = __float_as_uint(f.z); v.w = __float_as_uint(f.w);
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(i * 4), 0, AUX_SYS);
+}
+
+__device__ __forceinline__ float ld_sys1(__amdgpu_buffer_rsrc_t r, int64_t i) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)(i * 4), 0, AUX_SYS));
+}
+
+__device__ __forceinline__ void st_sys1(__amdgpu_buffer_rsrc_t r, int64_t i, float f) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(f), r, (int)(i * 4), 0, AUX_SYS);
+}
+
+__device__ __forceinline__ float4 add4(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+// All storing waves drained, then one lane per destination rank raises the flag.
+__device__ __forceinline__ void publish(const GfkComm& c, int phase, int b, uint32_t e) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < c.world) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(c.flags[t] + ((size_t)phase * c.nblk + b) * CMAX + c.rank, e,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// Wave 0 polls this workgroup's flag row until every rank reached epoch e.
+__device__ __forceinline__ void await_all(const GfkComm& c, int phase, int b, uint32_t e) {
+  const int t = threadIdx.x;
+  if (t < 64) {
+    const uint32_t* f = c.flags[c.rank] + ((size_t)phase * c.nblk + b) * CMAX;
+    int spins = 0;
+    for (;;) {
+      uint32_t v = e;
+      if (t < c.world) v = __hip_atomic_load(f + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (__all((int32_t)(v - e) >= 0)) break;
+      if (++spins > c.spin_limit) {
+        if (t == 0) __hip_atomic_store(c.err, 1 + phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void slice_range(const GfkComm& c, int ch, int b, int64_t& s0, int64_t& s1) {
+  const int64_t c0 = (int64_t)ch * c.chunk, c1 = c0 + c.chunk < c.n ? c0 + c.chunk : c.n;
+  s0 = c0 + (int64_t)b * c.slice;
+  s1 = s0 + c.slice < c1 ? s0 + c.slice : c1;
+}
+}  // namespace
+
+extern "C" __global__ void __launch_bounds__(CT) gfk_xgmi_allreduce(GfkComm c, float* data) {
+  __shared__ uint32_t s_epoch;
+  const int b = blockIdx.x, t = threadIdx.x;
+  if (t == 0) {
+    const uint32_t e = c.epoch[b] + 1;
+    c.epoch[b] = e;
+    s_epoch = e;
+  }
+  __syncthreads();
+  const uint32_t e = s_epoch;
+  const int buf = e & 1, R = c.rank, W = c.world;
+  const int64_t sbytes = (int64_t)W * c.chunk * 4;
+  const __amdgpu_buffer_rsrc_t mine = rsrc(c.stage[buf][R], sbytes);
+
+  // (slices are float4-aligned; only the last one of the last chunk can end in a
+  // partial float4, handled element-wise: nothing past n is ever touched)
+  // ---- phase 0: publish slice b of every chunk ----
+  for (int ch = 0; ch < W; ++ch) {
+    int64_t s0, s1;
+    slice_range(c, ch, b, s0, s1);
+    const int64_t s4 = s0 + ((s1 - s0) & ~(int64_t)3);
+    for (int64_t i = s0 + 4 * t; i < s4; i += 4 * CT)
+      st_sys(mine, i, *reinterpret_cast<const float4*>(data + i));
+    if (s4 + t < s1) st_sys1(mine, s4 + t, data[s4 + t]);
+  }
+  publish(c, 0, b, e);
+  await_all(c, 0, b, e);
+
+  // ---- phase 1: my chunk, slice b: sum over ranks in rank order ----
+  {
+    int64_t s0, s1;
+    slice_range(c, R, b, s0, s1);
+    __amdgpu_buffer_rsrc_t src[CMAX];
+#pragma unroll
+    for (int j = 0; j < CMAX; ++j) src[j] = rsrc(c.stage[buf][j < W ? j : 0], sbytes);
+    const int64_t s4 = s0 + ((s1 - s0) & ~(int64_t)3);
+    if (s4 + t < s1) {
+      float acc = ld_sys1(src[0], s4 + t);
+      for (int j = 1; j < W; ++j) acc += ld_sys1(src[j], s4 + t);
+      st_sys1(mine, s4 + t, acc);
+      data[s4 + t] = acc;
+    }
+    for (int64_t i = s0 + 4 * t; i < s4; i += 4 * CT) {
+      float4 v[CMAX];
+#pragma unroll
+      for (int j = 0; j < CMAX; ++j)
+        if (j < W) v[j] = ld_sys(src[j], i);
+      float4 acc = v[0];
+#pragma unroll
+      for (int j = 1; j < CMAX; ++j)
+        if (j < W) acc = add4(acc, v[j]);
+      st_sys(mine, i, acc);
+      *reinterpret_cast<float4*>(data + i) = acc;
+    }
+  }
+  publish(c, 1, b, e);
+  await_all(c, 1, b, e);
+
+  // ---- phase 2: the other chunks' slice b from their owners ----
+  for (int ch = 0; ch < W; ++ch) {
+    if (ch == R) continue;
+    int64_t s0, s1;
+    slice_range(c, ch, b, s0, s1);
+    const __amdgpu_buffer_rsrc_t src = rsrc(c.stage[buf][ch], sbytes);
+    const int64_t s4 = s0 + ((s1 - s0) & ~(int64_t)3);
+    for (int64_t i = s0 + 4 * t; i < s4; i += 4 * CT)
+      *reinterpret_cast<float4*>(data + i) = ld_sys(src, i);
+    if (s4 + t < s1) data[s4 + t] = ld_sys1(src, s4 + t);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host API (ctypes)
+// ---------------------------------------------------------------------------
+extern "C" size_t gfk_comm_struct_size() { return sizeof(GfkComm); }
+
+// stage: 2 * stage_bytes (regular); flags: uncached, zeroed; state: epoch[nblk] + err, zeroed.
+extern "C" int gfk_comm_alloc(int64_t stage_bytes, int64_t flag_bytes, int64_t state_bytes,
+                              void** stage, void** flags, void** state) {
+  hipError_t e;
+  if ((e = hipMalloc(stage, 2 * stage_bytes))) return (int)e;
+  if ((e = hipMemset(*stage, 0, 2 * stage_bytes))) return (int)e;
+  if (hipExtMallocWithFlags(flags, flag_bytes, hipDeviceMallocUncached) != hipSuccess) {
+    (void)hipGetLastError();
+    if ((e = hipMalloc(flags, flag_bytes))) return (int)e;
+  }
+  if ((e = hipMemset(*flags, 0, flag_bytes))) return (int)e;
+  if ((e = hipMalloc(state, state_bytes))) return (int)e;
+  if ((e = hipMemset(*state, 0, state_bytes))) return (int)e;
+  return (int)hipDeviceSynchronize();
+}
+
+extern "C" int gfk_comm_free(void* stage, void* flags, void* state) {
+  hipFree(stage);
+  hipFree(flags);
+  hipFree(state);
+  return 0;
+}
+
+extern "C" int gfk_ipc_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
+
+extern "C" int gfk_ipc_get(void* ptr, void* handle) {
+  return (int)hipIpcGetMemHandle(reinterpret_cast<hipIpcMemHandle_t*>(handle), ptr);
+}
+
+extern "C" int gfk_ipc_open(const void* handle, void** ptr) {
+  hipIpcMemHandle_t h;
+  __builtin_memcpy(&h, handle, sizeof(h));
+  return (int)hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess);
+}
+
+extern "C" int gfk_ipc_close(void* ptr) { return (int)hipIpcCloseMemHandle(ptr); }
+
+// The error word (0 = fine, 1 / 2 = a phase-0 / phase-1 wait timed out); synchronous.
+extern "C" int gfk_comm_error(const GfkComm* c) {
+  int32_t v = 0;
+  if (hipMemcpy(&v, c->err, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return v;
+}
+
+extern "C" int gfk_comm_launch(const GfkComm* c, float* data, hipStream_t s) {
+  if (c->world < 1 || c->world > CMAX || c->nblk < 1 || (c->chunk & 3) || (c->slice & 3) ||
+      (int64_t)c->slice * c->nblk < c->chunk || (int64_t)c->chunk * c->world < c->n ||
+      ((uintptr_t)data & 15))
+    return -1;
+  hipLaunchKernelGGL(gfk_xgmi_allreduce, dim3(c->nblk), dim3(CT), 0, s, *c, data);
+  return (int)hipGetLastError();
+}

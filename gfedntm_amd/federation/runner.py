@@ -229,6 +229,8 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
     client.set_fedavg_weight(weights[rank])
     client.enable_graph(graph)
     agg = CollectiveAggregator(bucket_bytes=bucket_bytes)
+    if data_backend == "nccl":
+        logger.info("-- -- FedAvg all-reduce: %s", agg.prepare(client.shared))
     start = 0
     if checkpoint_dir:
         start = ckpt.load_client_checkpoint(checkpoint_dir, client)

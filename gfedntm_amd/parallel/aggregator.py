@@ -29,13 +29,55 @@ def fedavg_weights(n_samples: Sequence[int]) -> List[float]:
 
 
 class CollectiveAggregator:
-    """All-reduce of pre-scaled flat buffers across the ranks of a process group."""
+    """All-reduce of pre-scaled flat buffers across the ranks of a process group.
 
-    def __init__(self, group=None, bucket_bytes: int = 64 << 20):
+    ``method``: "rccl" (torch.distributed all_reduce: RCCL on GPUs, gloo on CPU),
+    "xgmi" (the custom two-shot peer-memory kernel, parallel/xgmi.py) or "auto":
+    xgmi when the group is one node of <= 8 GPU ranks and the kernel passes its
+    exactness check at :meth:`prepare`, RCCL otherwise.  The environment variable
+    ``GFEDNTM_ALLREDUCE`` (rccl|xgmi|auto) overrides the default."""
+
+    def __init__(self, group=None, bucket_bytes: int = 64 << 20, method: Optional[str] = None):
+        import os
         self.group = group
         self.bucket_elems = max(1, bucket_bytes // 4)
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
+        self.method = (method or os.environ.get("GFEDNTM_ALLREDUCE", "auto")).lower()
+        self.xgmi = None
+        self.active = "rccl"
+
+    def prepare(self, flat: torch.Tensor) -> str:
+        """Choose the all-reduce for buffers shaped like ``flat`` (call once, on every
+        rank, before the timed / captured region).  Returns the method in use."""
+        if self.world == 1 or self.method == "rccl" or flat.device.type != "cuda":
+            self.active = "rccl"
+            return self.active
+        import socket
+        hosts: List = [None] * self.world
+        dist.all_gather_object(hosts, socket.gethostname(), group=self.group)
+        ok = len(set(hosts)) == 1 and self.world <= 8
+        xg = None
+        if ok:
+            from .xgmi import XgmiAllReduce
+            try:
+                xg = XgmiAllReduce(flat.numel(), flat.device, group=self.group)
+            except Exception as e:   # every rank must reach the agreement below
+                import logging
+                logging.getLogger("gfedntm_amd.xgmi").warning("xGMI all-reduce setup failed: %s", e)
+                xg = None
+        flags: List = [None] * self.world
+        dist.all_gather_object(flags, xg is not None, group=self.group)
+        ok = ok and all(flags) and xg.validate()
+        if ok:
+            self.xgmi, self.active = xg, "xgmi"
+        else:
+            if xg is not None:
+                xg.close()
+            if self.method == "xgmi":
+                raise RuntimeError("xGMI all-reduce requested but unavailable / failed validation")
+            self.active = "rccl"
+        return self.active
 
     def weights(self, n_local: int, device) -> List[float]:
         t = torch.tensor([float(n_local)], dtype=torch.float64, device=device)
@@ -48,6 +90,9 @@ class CollectiveAggregator:
         if self.world == 1:
             return []
         n = flat.numel()
+        if self.xgmi is not None and n == self.xgmi.n and not async_op:
+            self.xgmi.allreduce_(flat)
+            return []
         works = []
         for a in range(0, n, self.bucket_elems):
             w = dist.all_reduce(flat[a: a + self.bucket_elems], op=dist.ReduceOp.SUM,

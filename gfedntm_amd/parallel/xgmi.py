@@ -1,0 +1,174 @@
+"""Custom xGMI all-reduce for the per-round FedAvg (csrc/comm.hip).
+
+Why: the federation round is one fused training step (~tens of µs) followed by
+the all-reduce of the pre-scaled shared state (~2 MB at the headline config).
+At that size a ring all-reduce is latency-bound: 2(N-1) dependent hops.  The
+two-shot kernel reads the peers' buffers directly over xGMI (every GPU of the
+node has a link to every other), so a round costs two hand-offs: a reduce-
+scatter where each rank sums its chunk in rank order, and an all-gather.  The
+result is bit-identical on every rank and independent of timing.
+
+Setup: each rank allocates its stage/flag buffers, exports IPC handles
+(hipIpcGetMemHandle, dmabuf on this stack: keep HSA_ENABLE_IPC_MODE_LEGACY=0),
+gathers the peers' handles over the process group and maps them.
+:meth:`validate` runs one all-reduce of rank-dependent data against an exact
+host reference and returns a verdict agreed by all ranks; callers fall back
+to RCCL when it fails (see :class:`~gfedntm_amd.parallel.aggregator.CollectiveAggregator`).
+The kernel is a plain stream launch, so it is captured into hipGraphs like any
+other kernel.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import logging
+from typing import List, Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..ops import native
+
+CMAX = 8
+P = C.c_void_p
+log = logging.getLogger("gfedntm_amd.xgmi")
+
+
+class GfkComm(C.Structure):
+    _fields_ = [("stage", (P * CMAX) * 2), ("flags", P * CMAX), ("epoch", P), ("err", P),
+                ("rank", C.c_int32), ("world", C.c_int32), ("nblk", C.c_int32),
+                ("spin_limit", C.c_int32), ("n", C.c_int64), ("chunk", C.c_int64),
+                ("slice", C.c_int64)]
+
+
+def _declare(lib):
+    if getattr(lib, "_gfk_comm_declared", False):
+        return
+    lib.gfk_comm_struct_size.restype = C.c_size_t
+    lib.gfk_comm_alloc.argtypes = [C.c_int64, C.c_int64, C.c_int64, C.POINTER(P), C.POINTER(P),
+                                   C.POINTER(P)]
+    lib.gfk_comm_free.argtypes = [P, P, P]
+    lib.gfk_ipc_get.argtypes = [P, P]
+    lib.gfk_ipc_open.argtypes = [P, C.POINTER(P)]
+    lib.gfk_ipc_close.argtypes = [P]
+    lib.gfk_comm_launch.argtypes = [C.POINTER(GfkComm), P, P]
+    lib.gfk_comm_error.argtypes = [C.POINTER(GfkComm)]
+    if lib.gfk_comm_struct_size() != C.sizeof(GfkComm):
+        raise RuntimeError("GfkComm ABI mismatch between csrc/comm.hip and xgmi.py")
+    lib._gfk_comm_declared = True
+
+
+def _up4(x: int) -> int:
+    return -(-x // 4) * 4
+
+
+class XgmiAllReduce:
+    """In-place SUM all-reduce of one fixed-size fp32 buffer across the ranks of a
+    single-node process group (≤ 8 ranks; several ranks may share one GPU)."""
+
+    def __init__(self, n: int, device, group=None, nblk: Optional[int] = None,
+                 spin_limit: int = 1 << 25):
+        self.lib = native.kernels()
+        _declare(self.lib)
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        if self.world > CMAX:
+            raise ValueError(f"xGMI all-reduce supports up to {CMAX} ranks")
+        self.device = torch.device(device)
+        self.n = int(n)
+        chunk = _up4(-(-self.n // self.world))
+        if nblk is None:   # >= 4 KB per slice, up to 64 workgroups
+            nblk = int(max(1, min(64, chunk // 1024)))
+        self.nblk = nblk
+        slice_ = _up4(-(-chunk // nblk))
+        self._handles: List[int] = []
+        with torch.cuda.device(self.device):
+            stage, flags, state = P(), P(), P()
+            stage_bytes = self.world * chunk * 4
+            flag_bytes = 2 * nblk * CMAX * 4
+            rc = self.lib.gfk_comm_alloc(stage_bytes, flag_bytes, nblk * 4 + 16,
+                                         C.byref(stage), C.byref(flags), C.byref(state))
+            if rc:
+                raise RuntimeError(f"gfk_comm_alloc failed ({rc})")
+            self._own = (stage.value, flags.value, state.value)
+            hs = self.lib.gfk_ipc_handle_size()
+            mine = []
+            for ptr in (stage.value, flags.value):
+                h = C.create_string_buffer(hs)
+                rc = self.lib.gfk_ipc_get(P(ptr), h)
+                if rc:
+                    raise RuntimeError(f"hipIpcGetMemHandle failed ({rc})")
+                mine.append(h.raw)
+            allh: List = [None] * self.world
+            dist.all_gather_object(allh, mine, group=group)
+            c = GfkComm()
+            for j in range(self.world):
+                if j == self.rank:
+                    sp, fp = stage.value, flags.value
+                else:
+                    sp, fp = self._open(allh[j][0]), self._open(allh[j][1])
+                c.stage[0][j] = sp
+                c.stage[1][j] = sp + stage_bytes
+                c.flags[j] = fp
+            c.epoch = state.value
+            c.err = state.value + nblk * 4
+            c.rank, c.world, c.nblk, c.spin_limit = self.rank, self.world, nblk, int(spin_limit)
+            c.n, c.chunk, c.slice = self.n, chunk, slice_
+            self.c = c
+            self._err_ptr = c.err
+
+    def _open(self, handle: bytes) -> int:
+        p = P()
+        rc = self.lib.gfk_ipc_open(C.create_string_buffer(handle, len(handle)), C.byref(p))
+        if rc:
+            raise RuntimeError(f"hipIpcOpenMemHandle failed ({rc})")
+        self._handles.append(p.value)
+        return p.value
+
+    def allreduce_(self, t: torch.Tensor) -> torch.Tensor:
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != self.n \
+                or t.device != self.device or t.data_ptr() % 16:
+            raise ValueError("xGMI all-reduce: fp32, contiguous, 16-B aligned, fixed size")
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        rc = self.lib.gfk_comm_launch(C.byref(self.c), P(t.data_ptr()), P(stream))
+        if rc:
+            raise RuntimeError(f"gfk_comm_launch failed ({rc})")
+        return t
+
+    def error(self) -> int:
+        """Non-zero once a bounded wait timed out (results since are invalid)."""
+        torch.cuda.synchronize(self.device)
+        return int(self.lib.gfk_comm_error(C.byref(self.c)))
+
+    def validate(self, rounds: int = 3) -> bool:
+        """All-reduce rank-dependent data ``rounds`` times and compare with the exact
+        rank-ordered fp32 sum; True only if every rank agrees."""
+        ok = True
+        try:
+            for r in range(rounds):
+                g = torch.Generator(device="cpu").manual_seed(1234 + 97 * self.rank + r)
+                x = torch.randn(self.n, generator=g, dtype=torch.float32)
+                allx: List = [None] * self.world
+                dist.all_gather_object(allx, x.numpy(), group=self.group)
+                exp = allx[0].copy()
+                for j in range(1, self.world):
+                    exp = (exp + allx[j]).astype(np.float32)
+                t = x.to(self.device)
+                self.allreduce_(t)
+                torch.cuda.synchronize(self.device)
+                ok &= bool(np.array_equal(t.cpu().numpy(), exp)) and self.error() == 0
+        except Exception as e:  # pragma: no cover - reported and agreed below
+            log.warning("xGMI all-reduce validation error: %s", e)
+            ok = False
+        flags: List = [None] * self.world
+        dist.all_gather_object(flags, ok, group=self.group)
+        return all(flags)
+
+    def close(self):
+        for p in self._handles:
+            self.lib.gfk_ipc_close(P(p))
+        self._handles = []
+        if getattr(self, "_own", None):
+            self.lib.gfk_comm_free(*[P(x) for x in self._own])
+            self._own = None
