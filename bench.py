@@ -75,9 +75,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # GFEDNTM_REHEARSE_1GPU=1: rehearse the multi-rank path on a one-GPU box -- every
+    # rank on cuda:0, gloo process group (timings are meaningless, the code path and
+    # the xGMI all-reduce protocol are the real ones)
+    rehearse = os.environ.get("GFEDNTM_REHEARSE_1GPU") == "1"
+    if rehearse:
+        local_rank = 0
     if world > 1:
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     device = torch.device("cuda", local_rank)
     n_clients = world
 
@@ -116,11 +125,16 @@ def main():
     agg, comm = None, None
     if world > 1:
         dist.broadcast(tm.flat.buffer, src=0)        # identical W0 on every client
-        agg = CollectiveAggregator()
-        comm = agg.prepare(tm.flat.shared)          # custom xGMI all-reduce if it validates
+        agg = CollectiveAggregator(method="rccl")
         w = agg.weights(X.shape[0], device)
         if args.backend == "fused":
             eng.set_fedavg_scale(w[rank])
+            # the all-reduce becomes part of the step (custom xGMI kernel captured in the
+            # step graph, beta's share overlapped with the encoder backward) or follows
+            # it (RCCL) -- see FusedEngine.attach_fedavg
+            comm = eng.attach_fedavg()
+        else:
+            comm = agg.prepare(tm.flat.shared)
     data = DeviceCSR(X, device, contextual=ctx)
     n_steps = args.warmup + args.steps
     plan = BatchPlan.build(data.n_docs, args.batch, n_steps, seed=args.seed + rank)
@@ -132,9 +146,8 @@ def main():
 
     def round_(s):
         eng.step(s)
-        if agg is not None:
-            if args.backend != "fused":
-                shared.mul_(w[rank])
+        if agg is not None and args.backend != "fused":
+            shared.mul_(w[rank])
             agg.allreduce_(shared)
 
     for s in range(args.warmup):
@@ -153,11 +166,9 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    comm_error = 0
-    if agg is not None and agg.xgmi is not None:
-        comm_error = agg.xgmi.error()          # a timed-out wait invalidates the run
-        if comm_error:
-            raise RuntimeError(f"xGMI all-reduce reported error {comm_error}")
+    comm_error = eng.fedavg_error() if args.backend == "fused" else 0
+    if comm_error:                              # a timed-out wait invalidates the run
+        raise RuntimeError(f"xGMI all-reduce reported error {comm_error}")
     ms = dt / args.steps * 1e3
     docs_per_s = n_clients * args.batch * args.steps / dt
     losses = eng.loss_hist.detach().cpu().numpy()

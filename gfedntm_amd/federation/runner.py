@@ -228,9 +228,13 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
                              epoch_snapshots=(model_type == "ctm"))
     client.set_fedavg_weight(weights[rank])
     client.enable_graph(graph)
-    agg = CollectiveAggregator(bucket_bytes=bucket_bytes)
-    if data_backend == "nccl":
-        logger.info("-- -- FedAvg all-reduce: %s", agg.prepare(client.shared))
+    agg = CollectiveAggregator(bucket_bytes=bucket_bytes, method="rccl")
+    in_step = False
+    if data_backend == "nccl" and client.fused:
+        # the FedAvg all-reduce runs inside the step (graph-captured xGMI kernel, beta
+        # overlapped with the encoder backward) or right after it (RCCL)
+        logger.info("-- -- FedAvg all-reduce: %s", tm.engine.attach_fedavg())
+        in_step = True
     start = 0
     if checkpoint_dir:
         start = ckpt.load_client_checkpoint(checkpoint_dir, client)
@@ -244,7 +248,8 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
     it = start
     for it in range(start, max_iters):
         client.local_step(it)
-        agg.allreduce_(shared)
+        if not in_step:
+            agg.allreduce_(shared)
         done = client.end_round(it)
         if checkpoint_dir and checkpoint_every and (it + 1) % checkpoint_every == 0:
             ckpt.save_client_checkpoint(checkpoint_dir, client, it + 1)

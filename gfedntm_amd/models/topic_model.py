@@ -167,7 +167,8 @@ class TopicModelBase:
     def _build_engine(self):
         transposed = TRANSPOSED_KEYS if self.backend == "fused" else ()
         self.flat = FlatState(self.model, self.shared_keys, transposed=transposed,
-                              device=self.device)
+                              device=self.device,
+                              shared_last=("beta",) if self.backend == "fused" else ())
         if self.backend == "fused":
             from ..ops.engine import FusedEngine
             self.engine = FusedEngine(self)

@@ -208,6 +208,7 @@ class FusedEngine(EngineBase):
         self.graph_enabled = False
         self._graph = None
         self._graph_key = None
+        self._comm = None
         self._m = abi.GfkModel()
         self._a = abi.GfkAdam()
         self._u = abi.GfkUpdate()
@@ -508,7 +509,79 @@ class FusedEngine(EngineBase):
         if self.kind == "ctm":
             ph.insert(ph.index(abi.PH_ENC_FWD), abi.PH_CTX_FWD)
             ph.insert(ph.index(abi.PH_ENC_BWD) + 1, abi.PH_CTX_BWD)
+        if self._comm is not None and self._comm["mode"] == "graph":
+            if "beta" in self._comm:
+                ph.insert(ph.index(abi.PH_PRODLDA_BWD) + 1, abi.PH_FEDAVG_BETA)
+            ph.append(abi.PH_FEDAVG_END)
         return ph
+
+    # ------------------------------------------------------------------ FedAvg
+    def attach_fedavg(self, group=None, method: Optional[str] = None) -> str:
+        """Make the round's FedAvg all-reduce part of :meth:`step` (collective: call on
+        every rank, after the shared state is pre-scaled).
+
+        With the custom xGMI all-reduce the collectives are kernels on the step's
+        streams and are captured in the step's graph; in fused ProdLDA mode beta is
+        final after prodlda_bwd (Adam + pre-scale in its epilogue), so its all-reduce
+        runs on a side stream while row_bwd / post_bwd / win_update proceed, and only
+        the encoder part stays on the critical path.  Otherwise (RCCL) the all-reduce
+        follows the step eagerly.  Returns the method in use."""
+        from ..parallel.aggregator import CollectiveAggregator
+        self._comm = None
+        shared, flat = self.flat.shared, self.flat
+        parts = {"rest": shared}
+        if (self.update_mode == UPDATE_FUSED and flat.shared_keys
+                and flat.shared_keys[-1] == "beta" and len(flat.shared_keys) > 1):
+            b0 = flat.slots["beta"].offset
+            parts = {"rest": shared[:b0], "beta": shared[b0:]}
+        aggs = {k: CollectiveAggregator(group, method=method) for k in parts}
+        methods = {k: aggs[k].prepare(v) for k, v in parts.items()}
+        if all(m == "xgmi" for m in methods.values()):
+            c = {"mode": "graph", "rest": (aggs["rest"], parts["rest"])}
+            if "beta" in parts:
+                c["beta"] = (aggs["beta"], parts["beta"])
+                c["stream"] = torch.cuda.Stream(self.device)
+                c["ev_fork"] = torch.cuda.Event()
+                c["ev_join"] = torch.cuda.Event()
+            self._comm = c
+            used = "xgmi" + ("+overlap" if "beta" in parts else "")
+        else:
+            for a in aggs.values():
+                if a.xgmi is not None:
+                    a.xgmi.close()
+            agg = CollectiveAggregator(group, method="rccl")
+            self._comm = {"mode": "eager", "rest": (agg, shared)}
+            used = agg.active
+        self._invalidate_graph()
+        return used
+
+    def fedavg_error(self) -> int:
+        """Non-zero if an xGMI all-reduce wait timed out (synchronises)."""
+        if self._comm is None:
+            return 0
+        err = 0
+        for k in ("rest", "beta"):
+            if k in self._comm and self._comm[k][0].xgmi is not None:
+                err = err or self._comm[k][0].xgmi.error()
+        return err
+
+    def _fedavg_beta(self):
+        c = self._comm
+        cur = torch.cuda.current_stream(self.device)
+        c["ev_fork"].record(cur)
+        side = c["stream"]
+        side.wait_event(c["ev_fork"])
+        with torch.cuda.stream(side):
+            agg, buf = c["beta"]
+            agg.allreduce_(buf)
+        c["ev_join"].record(side)
+
+    def _fedavg_end(self):
+        c = self._comm
+        agg, buf = c["rest"]
+        agg.allreduce_(buf)
+        if "beta" in c:
+            torch.cuda.current_stream(self.device).wait_event(c["ev_join"])
 
     # ------------------------------------------------------------------ CTM
     def _alloc_ctx(self):
@@ -585,6 +658,10 @@ class FusedEngine(EngineBase):
                         self._ctx_fwd()
                     elif p == abi.PH_CTX_BWD:
                         self._ctx_bwd()
+                    elif p == abi.PH_FEDAVG_BETA:
+                        self._fedavg_beta()
+                    elif p == abi.PH_FEDAVG_END:
+                        self._fedavg_end()
                 else:
                     run.append(p)
             return
@@ -654,6 +731,9 @@ class FusedEngine(EngineBase):
             self._graph.replay()
         else:
             self._launch(self.phases())
+        if self._comm is not None and self._comm["mode"] == "eager":
+            agg, buf = self._comm["rest"]
+            agg.allreduce_(buf)
         self._host_step = s + 1
         return self.loss_hist[s]
 

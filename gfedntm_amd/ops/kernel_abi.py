@@ -41,7 +41,11 @@ PH_BATCH_PREP = 12
 # issued on the same stream (hipBLASLt through torch) and captured in the same graph
 PH_CTX_FWD = 100
 PH_CTX_BWD = 101
-HOST_PHASES = (PH_CTX_FWD, PH_CTX_BWD)
+# host-side phases (multi-GPU): the FedAvg all-reduce of beta (on a side stream,
+# overlapping the encoder backward) and of the rest of the shared state
+PH_FEDAVG_BETA = 102
+PH_FEDAVG_END = 103
+HOST_PHASES = (PH_CTX_FWD, PH_CTX_BWD, PH_FEDAVG_BETA, PH_FEDAVG_END)
 
 PRODLDA_STEP = [PH_ENC_FWD, PH_POST_FWD, PH_PRODLDA_FWD, PH_PRODLDA_LOSS, PH_PRODLDA_BWD,
                 PH_POST_BWD, PH_ENC_BWD]

@@ -50,12 +50,15 @@ def _resolve(module: nn.Module, key: str):
 
 class FlatState:
     def __init__(self, model: nn.Module, shared_keys: Sequence[str] = (),
-                 transposed: Iterable[str] = (), device=None):
+                 transposed: Iterable[str] = (), device=None, shared_last: Sequence[str] = ()):
         self.model = model
         sd = model.state_dict(keep_vars=True)
         params = dict(model.named_parameters())
         float_keys = [k for k, v in sd.items() if v.is_floating_point()]
         shared = [k for k in float_keys if k in set(shared_keys)]
+        # ``shared_last`` keys close the shared prefix (the fused engine overlaps the
+        # all-reduce of a tail range that is final early in the step)
+        shared = [k for k in shared if k not in shared_last] + [k for k in shared_last if k in shared]
         rest = [k for k in float_keys if k not in set(shared)]
         self.transposed = set(transposed)
         self.slots: Dict[str, Slot] = {}

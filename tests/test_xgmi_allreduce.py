@@ -72,3 +72,56 @@ def test_xgmi_allreduce_exact(world, n):
         assert len(r) == 6, r
         _, ok, graph_ok, err, method, agg_ok = r
         assert ok and graph_ok and err == 0 and method == "xgmi" and agg_ok, r
+
+
+def _fused_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    try:
+        import numpy as np
+        from gfedntm_amd.data.bow import BatchPlan, DeviceCSR
+        from gfedntm_amd.models import AVITM
+        from tests.helpers import random_csr
+        out = {}
+        for method in ("auto", "rccl"):
+            torch.manual_seed(0)                     # same W0 and Philox seed on both ranks
+            tm = AVITM(input_size=900, n_components=20, hidden_sizes=(32, 32), batch_size=64,
+                       verbose=False, device="cuda", backend="fused")
+            X = random_csr(300 + 50 * rank, 900, 40, seed=10 + rank)
+            data = DeviceCSR(X, "cuda")
+            e = tm.engine
+            e.bind_data(data, BatchPlan.build(data.n_docs, 64, 30, seed=rank))
+            n = [300.0, 350.0]
+            e.set_fedavg_scale(n[rank] / sum(n))
+            used = e.attach_fedavg(method=method)
+            e.enable_graph(True)
+            for s in range(30):
+                e.step(s)
+            torch.cuda.synchronize()
+            out[method] = (used, tm.flat.shared.detach().cpu().numpy().copy(), e.fedavg_error())
+        same_rank = np.array_equal(out["auto"][1], out["rccl"][1])
+        q.put((rank, out["auto"][0], out["rccl"][0], same_rank, out["auto"][2],
+               out["auto"][1][:1000].tolist()))
+    except Exception as ex:  # pragma: no cover
+        q.put((rank, repr(ex)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_fused_fedavg_overlap_matches_eager():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_fused_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=600) for _ in range(2)], key=lambda r: r[0])
+    for p in ps:
+        p.join(60)
+    for r in res:
+        assert len(r) == 6, r
+        _, used_auto, used_rccl, same, err, _ = r
+        assert used_auto == "xgmi+overlap" and used_rccl == "rccl", r[:5]
+        assert same and err == 0, r[:5]
+    assert res[0][5] == res[1][5]                    # ranks hold the same averaged state
