@@ -115,7 +115,10 @@ __device__ __forceinline__ void rowvec_gemv(const float* W, const float* x, int 
 // weight; then the row's (index, count) pairs and the W_in rows.  After the
 // gather the whole MLP (hidden layers, dropout, mu / log-sigma heads) runs out of
 // LDS with LDS-only barriers: its global stores are never waited on.
-extern "C" __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in(GfkModel m) {
+// Staged (compile-time): the MLP weights are read from LDS (ds_read); a runtime
+// select between the LDS copy and global memory would make every read a flat load.
+template <bool Staged>
+__global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkModel m) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int b = blockIdx.x, tid = threadIdx.x;
   const int lane = tid & 63, wave = uniform(tid >> 6);
@@ -129,7 +132,7 @@ extern "C" __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in(GfkModel m)
   float* act1 = act0 + pad4(hm);
   float* maskh = act1 + pad4(hm);
   float* wst = maskh + pad4(Hl);
-  const bool staged = sflags & 1;
+  constexpr bool staged = Staged;
 
   // ---- one round: the row, the step, the weights (LDS-DMA), the biases ----
   if (staged) {
@@ -270,13 +273,20 @@ extern "C" __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in(GfkModel m)
 }
 
 extern "C" int gfk_launch_enc_in(const GfkModel* m, hipStream_t s) {
-  hipLaunchKernelGGL(gfk_enc_in, dim3(m->bmax), dim3(ENC_THREADS), gfk_enc_in_smem(m), s, *m);
+  if (m->stage_flags & 1)
+    hipLaunchKernelGGL(gfk_enc_in_k<true>, dim3(m->bmax), dim3(ENC_THREADS), gfk_enc_in_smem(m), s, *m);
+  else
+    hipLaunchKernelGGL(gfk_enc_in_k<false>, dim3(m->bmax), dim3(ENC_THREADS), gfk_enc_in_smem(m), s, *m);
   return (int)hipGetLastError();
 }
 
 extern "C" int gfk_enc_in_set_smem(size_t bytes) {
-  return (int)hipFuncSetAttribute((const void*)gfk_enc_in, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)bytes);
+  const void* ks[] = {(const void*)gfk_enc_in_k<true>, (const void*)gfk_enc_in_k<false>};
+  for (const void* k : ks) {
+    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e != hipSuccess) return (int)e;
+  }
+  return 0;
 }
 
 extern "C" size_t gfk_enc_weight_bytes(const GfkModel* m) {

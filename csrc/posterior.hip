@@ -71,9 +71,67 @@ extern "C" size_t gfk_post_fwd_smem(const GfkModel* m) {
   return sizeof(float) * (mats + 4 * (size_t)pad4(m->K));
 }
 
+// Column statistics of the raw heads (4 threads per column, RPT = rows per thread
+// held in registers across the mean and variance passes); workgroup 0 also
+// advances the running statistics (prefetched rmp / rvp, one per pass).
+template <int RPT>
+__device__ __forceinline__ void post_colstats(const GfkModel& m, const float* mr, const float* lr,
+                                              float* cmean, float* crstd, const float (&rmp)[8],
+                                              const float (&rvp)[8], int nb, float inv_nb, int row,
+                                              int tid) {
+  constexpr int CP = 8;
+  const int K = m.K;
+#pragma unroll
+  for (int pass = 0; pass < CP; ++pass) {
+    const int cb = pass * (PT / 4);
+    if (cb >= 2 * K) break;
+    const int c2 = cb + (tid >> 2), g = tid & 3;
+    const bool valid = c2 < 2 * K;
+    const float* x = (c2 < K ? mr + c2 : lr + (c2 - K));
+    float xv[RPT];
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int r = g + 4 * i;
+      xv[i] = (valid && r < nb) ? x[r * K] : 0.f;
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) s += xv[i];
+    const float mean = quad_sum(s) * inv_nb;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const float d = g + 4 * i < nb ? xv[i] - mean : 0.f;
+      q += d * d;
+    }
+    const float var = quad_sum(q) * inv_nb;
+    const float rstd = rsqrtf(var + m.bn_eps);
+    if (valid && g == 0) {
+      cmean[c2] = mean;
+      crstd[c2] = rstd;
+      if (row == 0) {
+        const int k = c2 < K ? c2 : c2 - K;
+        float* rm = c2 < K ? m.mu_rm + k : m.s_rm + k;
+        float* rv = c2 < K ? m.mu_rv + k : m.s_rv + k;
+        const float mom = m.bn_momentum;
+        const float unb = nb > 1 ? var * (float)nb / (float)(nb - 1) : var;
+        const float o_m = rmp[pass], o_v = rvp[pass];
+        float nm = (1.f - mom) * o_m + mom * mean, nv = (1.f - mom) * o_v + mom * unb;
+        if (m.fed_scale_on && is_shared(m, rm)) { nm *= m.fed_scale; nv *= m.fed_scale; }
+        *rm = nm;
+        *rv = nv;
+        m.ws_bn_rstd[c2] = rstd;
+      }
+    }
+  }
+}
+
 // grid: bmax workgroups (row = blockIdx.x).  dynamic LDS: mr[B*K] + lr[B*K] (unless
 // read from L2) + mean[2K] + rstd[2K]
-extern "C" __global__ void __launch_bounds__(PT) gfk_post_fwd(GfkModel m) {
+// InLds: the batch matrices are staged in LDS (compile-time, so every access is a
+// ds_read; a runtime select of the pointer would turn them into flat loads).
+template <bool InLds>
+__global__ void __launch_bounds__(PT) gfk_post_fwd_k(GfkModel m) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   int K = m.K, B = m.bmax;
   const float *mu_raw = m.ws_mu_raw, *ls_raw = m.ws_ls_raw;
@@ -81,7 +139,7 @@ extern "C" __global__ void __launch_bounds__(PT) gfk_post_fwd(GfkModel m) {
   keep(K, B, mu_raw, ls_raw, nbp);
   const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
   const int row = blockIdx.x;
-  const bool in_lds = batch_in_lds(m);
+  constexpr bool in_lds = InLds;
   const float* mr = in_lds ? smem : mu_raw;
   const float* lr = in_lds ? smem + B * K : ls_raw;
   float* cmean = smem + (in_lds ? 2 * B * K : 0);
@@ -105,11 +163,29 @@ extern "C" __global__ void __launch_bounds__(PT) gfk_post_fwd(GfkModel m) {
     pm[q] = m.prior_mean[k];
     pv[q] = m.prior_var[k];
   }
-  float rm0 = 0.f, rv0 = 0.f;              // running stats of column (tid >> 2) (workgroup 0)
-  if (row == 0) {
-    const int c2 = min(tid >> 2, 2 * K - 1);
-    rm0 = c2 < K ? m.mu_rm[c2] : m.s_rm[c2 - K];
-    rv0 = c2 < K ? m.mu_rv[c2] : m.s_rv[c2 - K];
+  // workgroup 0, thread 0: the counters it advances, prefetched
+  double pw0 = 0.0, pw1 = 0.0;
+  int64_t nbt0 = 0, nbt1 = 0;
+  int32_t at0 = 0;
+  if (row == 0 && tid == 0) {
+    pw0 = m.adam_pow[0];
+    pw1 = m.adam_pow[1];
+    nbt0 = *m.nbt_mu;
+    nbt1 = *m.nbt_s;
+    at0 = *m.adam_t;
+  }
+  // running stats of the columns this thread updates (workgroup 0), one per column
+  // pass, prefetched with the staging round (K <= 256: at most 8 passes)
+  constexpr int CP = 8;
+  float rmp[CP], rvp[CP];
+#pragma unroll
+  for (int q = 0; q < CP; ++q) {
+    rmp[q] = rvp[q] = 0.f;
+    if (row == 0 && q * (PT / 4) < 2 * K) {
+      const int c2 = min(q * (PT / 4) + (tid >> 2), 2 * K - 1);
+      rmp[q] = c2 < K ? m.mu_rm[c2] : m.s_rm[c2 - K];
+      rvp[q] = c2 < K ? m.mu_rv[c2] : m.s_rv[c2 - K];
+    }
   }
   // NeuralLDA: per-topic log-sum-exp over V from lda_beta_fwd's tile partials
   // (topics dealt to the workgroups' last wave)
@@ -131,46 +207,17 @@ extern "C" __global__ void __launch_bounds__(PT) gfk_post_fwd(GfkModel m) {
   vm_barrier();
   GFK_STAMP(m, 1);
 
-  // ---- column statistics over the batch: 4 threads per column ----
+  // ---- column statistics over the batch: 4 threads per column, the column's
+  // values held in registers across the mean and variance passes ----
   const float inv_nb = 1.f / (float)nb;
-  for (int cb = 0; cb < 2 * K; cb += PT / 4) {
-    const int c2 = cb + (tid >> 2), g = tid & 3;
-    const bool valid = c2 < 2 * K;
-    const float* x = (c2 < K ? mr + c2 : lr + (c2 - K));
-    float s = 0.f;
-    if (valid)
-      for (int r = g; r < nb; r += 4) s += x[r * K];
-    const float mean = quad_sum(s) * inv_nb;
-    float q = 0.f;
-    if (valid)
-      for (int r = g; r < nb; r += 4) { const float d = x[r * K] - mean; q += d * d; }
-    const float var = quad_sum(q) * inv_nb;
-    const float rstd = rsqrtf(var + m.bn_eps);
-    if (valid && g == 0) {
-      cmean[c2] = mean;
-      crstd[c2] = rstd;
-      if (row == 0) {
-        const int k = c2 < K ? c2 : c2 - K;
-        float* rm = c2 < K ? m.mu_rm + k : m.s_rm + k;
-        float* rv = c2 < K ? m.mu_rv + k : m.s_rv + k;
-        const float mom = m.bn_momentum;
-        const float unb = nb > 1 ? var * (float)nb / (float)(nb - 1) : var;
-        // (cb == 0 pass: the prefetched values; later passes read them here)
-        const float o_m = cb == 0 ? rm0 : *rm, o_v = cb == 0 ? rv0 : *rv;
-        float nm = (1.f - mom) * o_m + mom * mean, nv = (1.f - mom) * o_v + mom * unb;
-        if (m.fed_scale_on && is_shared(m, rm)) { nm *= m.fed_scale; nv *= m.fed_scale; }
-        *rm = nm;
-        *rv = nv;
-        m.ws_bn_rstd[c2] = rstd;
-      }
-    }
-  }
+  if (B <= 64) post_colstats<16>(m, mr, lr, cmean, crstd, rmp, rvp, nb, inv_nb, row, tid);
+  else post_colstats<32>(m, mr, lr, cmean, crstd, rmp, rvp, nb, inv_nb, row, tid);
   if (row == 0 && tid == 0) {
-    *m.nbt_mu += 1;
-    *m.nbt_s += 1;
+    *m.nbt_mu = nbt0 + 1;
+    *m.nbt_s = nbt1 + 1;
     // the optimizer step of this minibatch: t and the bias corrections
-    *m.adam_t += 1;
-    const double p1 = m.adam_pow[0] * (double)m.beta1, p2 = m.adam_pow[1] * (double)m.beta2;
+    *m.adam_t = at0 + 1;
+    const double p1 = pw0 * (double)m.beta1, p2 = pw1 * (double)m.beta2;
     m.adam_pow[0] = p1;
     m.adam_pow[1] = p2;
     m.adam_coef[0] = (float)((double)m.lr / (1.0 - p1));
@@ -236,7 +283,11 @@ extern "C" __global__ void __launch_bounds__(PT) gfk_post_fwd(GfkModel m) {
 // grid: bmax workgroups.  dynamic LDS: part[4][K]
 extern "C" size_t gfk_row_bwd_smem(const GfkModel* m) { return sizeof(float) * 4 * (size_t)pad4(m->K); }
 
-extern "C" __global__ void __launch_bounds__(PT) gfk_row_bwd(GfkModel m) {
+// KQ = ceil(K / 64) topics per lane: only live topics are loaded (K <= 64 -> one
+// load per partial), U partials per wave per round so a row's partials are in
+// flight at once.
+template <int KQ>
+__global__ void __launch_bounds__(PT) gfk_row_bwd_k(GfkModel m) {
   extern __shared__ __attribute__((aligned(16))) float part[];
   int K = m.K, B = m.bmax, np = m.n_dpart;
   const float* dpart = m.ws_dthetad;
@@ -248,8 +299,10 @@ extern "C" __global__ void __launch_bounds__(PT) gfk_row_bwd(GfkModel m) {
   if (row >= nb) return;
   GFK_STAMP(m, 8);
   // ---- wave w sums partials w, w + 4, ... of the row (lane = topic), all loads first ----
-  constexpr int KQ = 4, U = 8;
-  float acc[KQ] = {0.f, 0.f, 0.f, 0.f};
+  constexpr int U = 32 / KQ;
+  float acc[KQ];
+#pragma unroll
+  for (int q = 0; q < KQ; ++q) acc[q] = 0.f;
   for (int p0 = wave; p0 < np; p0 += 4 * U) {
     float v[U][KQ];
 #pragma unroll
@@ -312,7 +365,7 @@ extern "C" __global__ void __launch_bounds__(PT) gfk_row_bwd(GfkModel m) {
 // LDS plan (floats): dmu, dls, mu, ls [B][K] + s1..s4 [2K] + own-row vectors
 // (dmr|dlr [2K], dz ping-pong [2][hmax], z rows, mask) + staged weights.
 struct PostLds {
-  int dmu, dls, mu, ls, sums, dr, v0, v1, zrow, mask, w, total;
+  int dmu, dls, mu, ls, sums, pm, dr, v0, v1, zrow, mask, w, total;
 };
 
 __host__ __device__ inline PostLds post_lds(const GfkModel& m) {
@@ -325,6 +378,7 @@ __host__ __device__ inline PostLds post_lds(const GfkModel& m) {
   L.mu = o; o += mat;
   L.ls = o; o += mat;
   L.sums = o; o += 4 * pad4(2 * K);
+  L.pm = o; o += pad4(K);
   L.dr = o; o += 2 * pad4(K);
   L.v0 = o; o += hm;
   L.v1 = o; o += hm;
@@ -358,7 +412,8 @@ __device__ __forceinline__ void colvec_gemv(const float* W, int ldw, const float
 }
 
 // grid: bmax workgroups (row = blockIdx.x).
-extern "C" __global__ void __launch_bounds__(PT) gfk_post_bwd(GfkModel m) {
+template <bool InLds, bool Staged>
+__global__ void __launch_bounds__(PT) gfk_post_bwd_k(GfkModel m) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   int K = m.K, B = m.bmax, nh = m.n_hidden, sflags = m.stage_flags;
   const float *dmu_g = m.ws_dmu, *dls_g = m.ws_dls, *mu_g = m.ws_mu, *ls_g = m.ws_ls;
@@ -368,10 +423,10 @@ extern "C" __global__ void __launch_bounds__(PT) gfk_post_bwd(GfkModel m) {
   const int row = blockIdx.x;
   const PostLds L = post_lds(m);
   const int Hl = m.H[nh - 1];
-  const bool staged = sflags & 1;
+  constexpr bool staged = Staged;
   GFK_STAMP(m, 10);
 
-  const bool in_lds = batch_in_lds(m);
+  constexpr bool in_lds = InLds;
   // ---- one round: the four [B][K] matrices, the own row, the weights, stats ----
   if (in_lds) {
     glds_copy(smem + L.dmu, dmu_g, B * K, tid, PT);
@@ -390,6 +445,7 @@ extern "C" __global__ void __launch_bounds__(PT) gfk_post_bwd(GfkModel m) {
     }
   }
   glds_copy(smem + L.mask, m.ws_mask_h + (size_t)row * Hl, Hl, tid, PT);
+  glds_copy(smem + L.pm, m.prior_mean, K, tid, PT);
   if (staged) {
     float* p = smem + L.w;
     glds_copy(p, m.w_mu, K * Hl, tid, PT); p += pad4(K * Hl);
@@ -405,9 +461,11 @@ extern "C" __global__ void __launch_bounds__(PT) gfk_post_bwd(GfkModel m) {
   for (int q = 0; q < CQ; ++q) rs[q] = m.ws_bn_rstd[min(tid + q * PT, 2 * K - 1)];
   // workgroup 0 extras: the loss terms, priors, NeuralLDA theta_d * d theta_d
   float lterm = 0.f, pmk = 0.f, pvk = 1.f;
+  int step0 = 0;
   if (row == 0) {
     if (tid < nb) lterm = m.kl_weight * m.ws_kl[tid] + m.ws_rl[tid];
     if (tid < K) { pmk = m.prior_mean[tid]; pvk = m.prior_var[tid]; }
+    if (tid == 0) step0 = *m.step;
   }
   if (row >= nb) {
     vm_barrier();
@@ -423,21 +481,24 @@ extern "C" __global__ void __launch_bounds__(PT) gfk_post_bwd(GfkModel m) {
   const float* ls = in_lds ? smem + L.ls : ls_g;
   float* S = smem + L.sums;             // [4][pad4(2K)]: sum dy, sum dy * xh, (wg 0:) sum xh / extra
   const int P2 = pad4(2 * K);
+  const float* pmean = smem + L.pm;     // prior mean, staged
   for (int cb = 0; cb < 2 * K; cb += PT / 4) {
     const int c2 = cb + (tid >> 2), g = tid & 3;
     const bool valid = c2 < 2 * K;
     const int k = c2 < K ? c2 : c2 - K;
     const float* dy = c2 < K ? dmu : dls;
     const float* xh = c2 < K ? mu : ls;
+    const float pm = pmean[k];
     float s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f;
     if (valid)
       for (int r = g; r < nb; r += 4) {
         const float d = dy[r * K + k], x = xh[r * K + k];
         s1 += d;
         s2 += d * x;
-        if (row == 0) {                 // priors: sum mu, sum exp(ls), sum (pm - mu)^2
+        if (row == 0) {                 // priors: sum mu | sum exp(ls), sum (pm - mu)^2
           s3 += c2 < K ? x : expf(x);
-          s4 += x;
+          const float dm = pm - x;
+          s4 += c2 < K ? dm * dm : 0.f;
         }
       }
     s1 = quad_sum(s1);
@@ -459,9 +520,7 @@ extern "C" __global__ void __launch_bounds__(PT) gfk_post_bwd(GfkModel m) {
   if (row == 0) {
     const float wk = m.kl_weight;
     if (tid < K && m.learn_priors) {
-      // sum_b (pm - mu_b)^2 = nb pm^2 - 2 pm sum mu + sum mu^2: recomputed exactly below
-      float sdm2 = 0.f;
-      for (int r = 0; r < nb; ++r) { const float d = pmk - mu[r * K + tid]; sdm2 += d * d; }
+      const float sdm2 = S[3 * P2 + tid];                 // sum_b (pm - mu_b)^2
       const float smu = S[2 * P2 + tid], svar = S[2 * P2 + K + tid];
       m.prior_mean[tid + m.off_g] = wk * ((float)nb * pmk - smu) / pvk;
       m.prior_var[tid + m.off_g] =
@@ -469,16 +528,27 @@ extern "C" __global__ void __launch_bounds__(PT) gfk_post_bwd(GfkModel m) {
     }
     if (m.kind == GFK_LDA && tid < K) {
       float ck = 0.f;
-      for (int r = 0; r < nb; ++r) ck += m.ws_thetad[r * m.kt + tid] * m.ws_dtheta[r * K + tid];
+      int r = 0;
+      for (; r + 8 <= nb; r += 8) {     // 8 independent load pairs per round
+        float a[8], d[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          a[u] = m.ws_thetad[(r + u) * m.kt + tid];
+          d[u] = m.ws_dtheta[(r + u) * K + tid];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) ck += a[u] * d[u];
+      }
+      for (; r < nb; ++r) ck += m.ws_thetad[r * m.kt + tid] * m.ws_dtheta[r * K + tid];
       m.ws_ck[tid] = ck;
     }
     const float l = block_sum_wave0(lterm, smem + L.v1);   // (v1 is free until the hidden layers)
     if (tid == 0) {
-      const int step = *m.step;
-      m.loss_hist[step] = l;
-      *m.step = step + 1;
+      m.loss_hist[step0] = l;
+      *m.step = step0 + 1;
     }
   }
+  GFK_STAMP(m, 14);
 
   // ---- own row: BN backward -> d mu_raw | d ls_raw ----
   float* dr = smem + L.dr;              // [2K]: dmr then dlr
@@ -496,6 +566,7 @@ extern "C" __global__ void __launch_bounds__(PT) gfk_post_bwd(GfkModel m) {
     }
   }
   lds_barrier();
+  GFK_STAMP(m, 15);
 
   // ---- heads backward: d hd[j] = sum_k dmr[k] W_mu[k][j] + dlr[k] W_s[k][j] ----
   const float* wst = smem + L.w;
@@ -527,6 +598,7 @@ extern "C" __global__ void __launch_bounds__(PT) gfk_post_bwd(GfkModel m) {
     }
   }
   lds_barrier();
+  GFK_STAMP(m, 29);
 
   // ---- hidden layers, last to first: dz_{l} = (dz_{l+1} W_l) * act'(z_l) ----
   float* din = v0;
@@ -571,15 +643,33 @@ extern "C" __global__ void gfk_batch_docs(GfkModel m) {
 // launchers
 // ---------------------------------------------------------------------------
 extern "C" int gfk_launch_post_fwd(const GfkModel* m, hipStream_t s) {
-  hipLaunchKernelGGL(gfk_post_fwd, dim3(m->bmax), dim3(PT), gfk_post_fwd_smem(m), s, *m);
+  if (batch_in_lds(*m))
+    hipLaunchKernelGGL(gfk_post_fwd_k<true>, dim3(m->bmax), dim3(PT), gfk_post_fwd_smem(m), s, *m);
+  else
+    hipLaunchKernelGGL(gfk_post_fwd_k<false>, dim3(m->bmax), dim3(PT), gfk_post_fwd_smem(m), s, *m);
   return (int)hipGetLastError();
 }
 
 extern "C" int gfk_launch_post_bwd(const GfkModel* m, hipStream_t s) {
-  hipLaunchKernelGGL(gfk_row_bwd, dim3(m->bmax), dim3(PT), gfk_row_bwd_smem(m), s, *m);
+  const int kq = (m->K + 63) / 64;
+  const dim3 g(m->bmax), t(PT);
+  const size_t sm = gfk_row_bwd_smem(m);
+  if (kq <= 1) hipLaunchKernelGGL(gfk_row_bwd_k<1>, g, t, sm, s, *m);
+  else if (kq == 2) hipLaunchKernelGGL(gfk_row_bwd_k<2>, g, t, sm, s, *m);
+  else if (kq == 3) hipLaunchKernelGGL(gfk_row_bwd_k<3>, g, t, sm, s, *m);
+  else hipLaunchKernelGGL(gfk_row_bwd_k<4>, g, t, sm, s, *m);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(gfk_post_bwd, dim3(m->bmax), dim3(PT), gfk_post_bwd_smem(m), s, *m);
+  const dim3 gb(m->bmax), tb(PT);
+  const size_t sb = gfk_post_bwd_smem(m);
+  const bool st = m->stage_flags & 1;
+  if (batch_in_lds(*m)) {
+    if (st) hipLaunchKernelGGL((gfk_post_bwd_k<true, true>), gb, tb, sb, s, *m);
+    else hipLaunchKernelGGL((gfk_post_bwd_k<true, false>), gb, tb, sb, s, *m);
+  } else {
+    if (st) hipLaunchKernelGGL((gfk_post_bwd_k<false, true>), gb, tb, sb, s, *m);
+    else hipLaunchKernelGGL((gfk_post_bwd_k<false, false>), gb, tb, sb, s, *m);
+  }
   return (int)hipGetLastError();
 }
 
@@ -594,7 +684,11 @@ extern "C" int gfk_launch_batch_docs(const GfkModel* m, hipStream_t s) {
 }
 
 extern "C" int gfk_post_set_smem(size_t bytes) {
-  const void* ks[] = {(const void*)gfk_post_fwd, (const void*)gfk_row_bwd, (const void*)gfk_post_bwd};
+  const void* ks[] = {(const void*)gfk_post_fwd_k<true>, (const void*)gfk_post_fwd_k<false>,
+                      (const void*)gfk_row_bwd_k<1>, (const void*)gfk_row_bwd_k<2>,
+                      (const void*)gfk_row_bwd_k<3>, (const void*)gfk_row_bwd_k<4>,
+                      (const void*)gfk_post_bwd_k<true, true>, (const void*)gfk_post_bwd_k<true, false>,
+                      (const void*)gfk_post_bwd_k<false, true>, (const void*)gfk_post_bwd_k<false, false>};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return (int)e;

@@ -57,6 +57,13 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--checkpoint_dir", type=str, default=None)
     p.add_argument("--checkpoint_every", type=int, default=None)
     p.add_argument("--stop_at_num_epochs", action="store_true")
+    p.add_argument("--metrics_every", type=int, default=0,
+                   help="JSONL metrics window (rounds) in <logs>/metrics_<date>.jsonl; 0 = end only")
+    p.add_argument("--collective_timeout", type=float, default=1800.0,
+                   help="rccl/gloo: process-group timeout in seconds (failed collectives abort)")
+    p.add_argument("--heartbeat_timeout", type=float, default=120.0,
+                   help="rccl/gloo: seconds without a peer heartbeat before this rank aborts "
+                        "(0 = off); resume with --checkpoint_dir")
     p.add_argument("--allow-pickle", dest="allow_pickle", action="store_true",
                    help="load reference synthetic npz files with object arrays (trusted files only)")
     p.add_argument("--server_address", type=str, default=None,
@@ -119,6 +126,8 @@ def run_local(args, cfg) -> dict:
                for i in range(1, n + 1)]
     fed = LocalFederation(
         corpora, cfg.training_params, args.model_type, args.max_iters, device=args.device,
+        metrics_path=os.path.join(logs_server, f"metrics_{stamp}.jsonl"),
+        metrics_every=args.metrics_every,
         backend=args.engine or cfg.backend, grads_to_share=cfg.grads_to_share, seed=args.seed,
         save_client=save_client, save_server=save_server, logger=logger,
         graph=cfg.graph and not args.no_graph, log_every=args.log_every,
@@ -153,7 +162,9 @@ def _rank_main(args, cfg) -> dict:
         stop_at_num_epochs=args.stop_at_num_epochs or cfg.stop_at_num_epochs,
         checkpoint_dir=args.checkpoint_dir,
         checkpoint_every=args.checkpoint_every if args.checkpoint_every is not None
-        else cfg.checkpoint_every, stamp=stamp)
+        else cfg.checkpoint_every, stamp=stamp,
+        metrics_path=os.path.join(f"{logs_client}{cid}", f"metrics_{stamp}.jsonl"),
+        metrics_every=args.metrics_every, heartbeat_timeout=args.heartbeat_timeout)
 
 
 def _spawned(local_rank: int, world: int, port: int, argv: List[str]):
@@ -173,11 +184,12 @@ def run_collective(args, cfg, argv: List[str]) -> Optional[dict]:
     backend = "nccl" if args.backend == "rccl" else "gloo"
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    timeout = datetime.timedelta(seconds=args.collective_timeout)
     if backend == "nccl":
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank), timeout=timeout)
     else:
-        dist.init_process_group("gloo")
+        dist.init_process_group("gloo", timeout=timeout)
         if args.device is None:
             args.device = "cpu"
     try:

@@ -71,6 +71,21 @@ def _handlers(service: str, impl) -> object:
     return grpc.method_handlers_generic_handler(f"{wire.PACKAGE}.{service}", table)
 
 
+def call_with_retry(fn, request, timeout: Optional[float], retries: int = 3, backoff: float = 0.5):
+    """Unary call with a deadline, retried on UNAVAILABLE / DEADLINE_EXCEEDED (the
+    client-server handlers are idempotent per round, so a retry never re-trains)."""
+    grpc = _grpc()
+    for attempt in range(retries + 1):
+        try:
+            return fn(request, timeout=timeout)
+        except grpc.RpcError as e:
+            code = e.code() if hasattr(e, "code") else None
+            if attempt == retries or code not in (grpc.StatusCode.UNAVAILABLE,
+                                                  grpc.StatusCode.DEADLINE_EXCEEDED):
+                raise
+            time.sleep(backoff * (2 ** attempt))
+
+
 def weighted_average(states: List[Dict[str, np.ndarray]], n: List[int]) -> Dict[str, np.ndarray]:
     """sum_i n_i W_i / sum n, per tensor; integer tensors are rounded back (reference
     server.py:478-490 averages num_batches_tracked the same way)."""
@@ -94,7 +109,8 @@ class FederationServicer:
                  grads_to_share=DEFAULT_GRADS_TO_SHARE, seed: int = 0,
                  save_server: Optional[str] = None, stamp: Optional[str] = None,
                  channel_options=(), logger=None, wait_timeout: float = 600.0,
-                 stop_at_num_epochs: bool = False):
+                 stop_at_num_epochs: bool = False, rpc_timeout: Optional[float] = 600.0,
+                 rpc_retries: int = 3):
         self.params, self.model_type = dict(params), model_type
         self.min_clients, self.max_iters = min_clients, max_iters
         self.client_host, self.base_port = client_host, base_port
@@ -105,6 +121,7 @@ class FederationServicer:
         self.logger = logger or logging.getLogger("gfedntm_amd.server")
         self.wait_timeout = wait_timeout
         self.stop_at_num_epochs = stop_at_num_epochs
+        self.rpc_timeout, self.rpc_retries = rpc_timeout, rpc_retries
         self.cond = threading.Condition()
         self.dicts: Dict[int, Dict[str, int]] = {}
         self.n_samples: Dict[int, int] = {}
@@ -204,7 +221,8 @@ class FederationServicer:
         try:
             for it in range(self.max_iters):
                 req = pb.ServerGetGradientRequest(iter=it)
-                replies = list(pool.map(lambda c: get[c](req), cids))
+                call = lambda fn, r: call_with_retry(fn, r, self.rpc_timeout, self.rpc_retries)  # noqa: E731
+                replies = list(pool.map(lambda c: call(get[c], req), cids))
                 states = [{u.tensor_name: wire.proto_to_numpy(u.tensor) for u in r.updates}
                           for r in replies]
                 self.aggregated = weighted_average(states, n)
@@ -213,7 +231,7 @@ class FederationServicer:
                 msg = pb.ServerAggregatedTensorRequest(header=hdr)
                 msg.metadata.current_epoch = max(r.metadata.current_epoch for r in replies)
                 msg.nndata.modelUpdate.CopyFrom(wire.model_update_from_state(self.aggregated, it))
-                list(pool.map(lambda c: push[c](msg), cids))
+                list(pool.map(lambda c: call(push[c], msg), cids))
                 self.rounds = it + 1
                 if self.stop_at_num_epochs and all(
                         r.metadata.current_epoch >= r.metadata.num_max_epochs for r in replies):
@@ -234,7 +252,8 @@ class FederationServicer:
                                   self.global_tm.n_components, None)
             stop = pb.ServerAggregatedTensorRequest(header=pb.MessageHeader(
                 message_type=MessageType["SERVER_STOP_TRAINING_REQUEST"]))
-            list(pool.map(lambda c: push[c](stop), cids))
+            list(pool.map(lambda c: call_with_retry(push[c], stop, self.rpc_timeout,
+                                                    self.rpc_retries), cids))
         finally:
             pool.shutdown()
             for ch in chans.values():
@@ -264,27 +283,44 @@ class ClientServicer:
         self.sd = client.tm.model.state_dict()      # views into the flat buffer
         self.keys = list(client.tm.flat.shared_keys)
         self.stopped = threading.Event()
-        self.it = 0
+        self.it = -1
+        self.applied = -1
+        self._last = None          # (iter, response): a retried request gets it again
+        self.lock = threading.Lock()
 
     def getGradient(self, request, context):
+        with self.lock:
+            return self._get_gradient(int(request.iter))
+
+    def _get_gradient(self, it: int):
         c = self.client
-        self.it = int(request.iter)
+        if self._last is not None and self._last[0] == it:
+            return self._last[1]
+        self.it = it
         c.local_step(self.it)
         hdr = pb.MessageHeader(id_request=f"ID{c.id}_{round(time.time())}",
                                message_type=MessageType["CLIENT_TENSOR_SEND"])
         md = pb.MessageAdditionalData(current_mb=c.current_mb, current_epoch=c.current_epoch,
                                       num_max_epochs=c.tm.num_epochs, id_machine=c.id)
         state = {k: self.sd[k] for k in self.keys}
-        return pb.ClientTensorRequest(header=hdr, metadata=md, updates=wire.updates_from_state(state))
+        resp = pb.ClientTensorRequest(header=hdr, metadata=md, updates=wire.updates_from_state(state))
+        self._last = (it, resp)
+        return resp
 
     def sendAggregatedTensor(self, request, context):
+        with self.lock:
+            return self._send_aggregated(request)
+
+    def _send_aggregated(self, request):
         mt = request.header.message_type
         if mt == MessageType["SERVER_AGGREGATED_TENSOR_SEND"]:
-            agg = wire.state_from_model_update(request.nndata.modelUpdate)
-            for k, v in agg.items():
-                if k in self.sd:
-                    self.sd[k].copy_(v.to(self.sd[k].device, self.sd[k].dtype))
-            self.client.end_round(self.it)
+            if self.applied != self.it:            # a retried push is acknowledged only
+                agg = wire.state_from_model_update(request.nndata.modelUpdate)
+                for k, v in agg.items():
+                    if k in self.sd:
+                        self.sd[k].copy_(v.to(self.sd[k].device, self.sd[k].dtype))
+                self.client.end_round(self.it)
+                self.applied = self.it
             hdr = pb.MessageHeader(id_request=str(self.it),
                                    message_type=MessageType["CLIENT_CONFIRM_RECEIVED"])
         elif mt == MessageType["SERVER_STOP_TRAINING_REQUEST"]:

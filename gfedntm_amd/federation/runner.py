@@ -43,6 +43,8 @@ from ..eval.export import save_model_as_npz, server_model_path
 from ..parallel.aggregator import CollectiveAggregator, LocalAggregator, fedavg_weights
 from ..utils import checkpoint as ckpt
 from ..utils.config import DEFAULT_GRADS_TO_SHARE, model_kwargs_from_params
+from ..utils.logging import MetricsWriter
+from ..utils.trace import RoundWindow, trace_range
 from .client import FederatedClient
 from .data import ClientCorpus
 
@@ -97,8 +99,11 @@ class LocalFederation:
                  save_client: Optional[str] = None, save_server: Optional[str] = None,
                  logger=None, graph: bool = True, log_every: int = 0,
                  stop_at_num_epochs: bool = False, checkpoint_dir: Optional[str] = None,
-                 checkpoint_every: int = 0, stamp: Optional[str] = None):
+                 checkpoint_every: int = 0, stamp: Optional[str] = None,
+                 metrics_path: Optional[str] = None, metrics_every: int = 0):
         self.logger = logger or logging.getLogger("gfedntm_amd.federation")
+        self.metrics = MetricsWriter(metrics_path)
+        self.metrics_every = int(metrics_every)
         self.device = torch.device(device) if device is not None else \
             torch.device("cuda" if torch.cuda.is_available() else "cpu")
         self.max_iters, self.model_type = max_iters, model_type
@@ -106,7 +111,8 @@ class LocalFederation:
         self.checkpoint_dir, self.checkpoint_every = checkpoint_dir, checkpoint_every
         self.stamp = stamp or datetime.datetime.now().strftime("%Y%m%d")
         # ---- stage 1: vocabulary consensus ----
-        self.terms = union_vocabulary([c.local_terms() for c in corpora])
+        with trace_range("consensus"):
+            self.terms = union_vocabulary([c.local_terms() for c in corpora])
         self.vocab = vocabulary_dict(self.terms)
         self.logger.info("-- -- Global vocabulary agreed: %d terms from %d clients",
                          len(self.terms), len(corpora))
@@ -141,26 +147,49 @@ class LocalFederation:
             if self.round:
                 self.logger.info("-- -- Resuming the federation at round %d", self.round)
 
+    def _sync(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
     def run(self) -> Dict:
         t0 = time.perf_counter()
-        for it in range(self.round, self.max_iters):
-            for c in self.clients:
-                c.local_step(it)
-            self.agg.average_([c.shared for c in self.clients], prescaled=True)
-            done = [c.end_round(it) for c in self.clients]
-            self.round = it + 1
-            if self.checkpoint_dir and self.checkpoint_every and self.round % self.checkpoint_every == 0:
+        start = self.round
+        win = RoundWindow(self._sync)
+        with trace_range("rounds"):
+            for it in range(self.round, self.max_iters):
                 for c in self.clients:
-                    ckpt.save_client_checkpoint(self.checkpoint_dir, c, self.round)
-            if self.stop_at_num_epochs and all(done):
-                self.logger.info("-- -- All clients reached num_epochs; stopping at round %d",
-                                 self.round)
-                break
-        if self.device.type == "cuda":
-            torch.cuda.synchronize()
+                    c.local_step(it)
+                self.agg.average_([c.shared for c in self.clients], prescaled=True)
+                done = [c.end_round(it) for c in self.clients]
+                self.round = it + 1
+                win.add(sum(int(c.plan.size[it]) for c in self.clients))
+                if self.metrics_every and self.round % self.metrics_every == 0:
+                    self._window_metrics(win, it)
+                if self.checkpoint_dir and self.checkpoint_every and self.round % self.checkpoint_every == 0:
+                    with trace_range("checkpoint"):
+                        for c in self.clients:
+                            ckpt.save_client_checkpoint(self.checkpoint_dir, c, self.round)
+                if self.stop_at_num_epochs and all(done):
+                    self.logger.info("-- -- All clients reached num_epochs; stopping at round %d",
+                                     self.round)
+                    break
+        self._sync()
         wall = time.perf_counter() - t0
-        self.finish()
+        docs = sum(int(c.plan.size[start:self.round].sum()) for c in self.clients)
+        self.metrics.write(event="train_end", rounds=self.round - start, wall_s=wall,
+                           docs=docs, docs_per_s=docs / wall if wall else None,
+                           ms_per_round=1e3 * wall / max(self.round - start, 1))
+        with trace_range("finish"):
+            self.finish()
         return {"rounds": self.round, "wall_s": wall}
+
+    def _window_metrics(self, win: RoundWindow, it: int):
+        w = win.close()
+        if w is None:
+            return
+        loss = float(np.mean([float(c.tm.engine.loss_hist[max(0, it + 1 - w["rounds"]): it + 1]
+                                    .mean().item()) for c in self.clients]))
+        self.metrics.write(event="window", round=it + 1, loss=loss, **w)
 
     def finish(self):
         for c in self.clients:
@@ -188,7 +217,8 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
                     logger=None, graph: bool = True, log_every: int = 0,
                     stop_at_num_epochs: bool = False, checkpoint_dir: Optional[str] = None,
                     checkpoint_every: int = 0, stamp: Optional[str] = None,
-                    bucket_bytes: int = 64 << 20) -> Dict:
+                    bucket_bytes: int = 64 << 20, metrics_path: Optional[str] = None,
+                    metrics_every: int = 0, heartbeat_timeout: float = 0.0) -> Dict:
     """Runs this process's client; torch.distributed must be initialised (RANK /
     WORLD_SIZE).  Rank r is client r+1; rank 0 also plays the coordinator (global
     save).  ``data_backend`` is the process group's backend ('nccl' = RCCL or
@@ -204,9 +234,16 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
         device = torch.device("cpu")
     stamp = stamp or datetime.datetime.now().strftime("%Y%m%d")
     # ---- stage 1: vocabulary consensus + counts over the control plane ----
+    metrics = MetricsWriter(metrics_path)
+    hb = None
+    if heartbeat_timeout and world > 1:
+        from ..parallel.heartbeat import Heartbeat
+        hb = Heartbeat(rank, world, timeout=heartbeat_timeout,
+                       interval=max(0.5, min(5.0, heartbeat_timeout / 10))).start()
     local = corpus.local_terms()
     gathered = [None] * world
-    dist.all_gather_object(gathered, (local, corpus.n_docs), group=ctrl)
+    with trace_range("consensus"):
+        dist.all_gather_object(gathered, (local, corpus.n_docs), group=ctrl)
     terms = union_vocabulary([g[0] for g in gathered])
     vocab = vocabulary_dict(terms)
     n = [g[1] for g in gathered]
@@ -217,7 +254,8 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
     tm = make_topic_model(model_type, params, len(terms), device, backend, grads_to_share,
                           seed=seed, logger=logger)
     # identical W0 on every client: the flat buffer holds every float parameter and buffer
-    dist.broadcast(tm.flat.buffer, src=0)
+    with trace_range("w0_broadcast"):
+        dist.broadcast(tm.flat.buffer, src=0)
     cid = rank + 1
     path = None
     if save_client is not None:
@@ -244,23 +282,36 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
             raise RuntimeError(f"inconsistent client checkpoints: rounds {rounds}")
     shared = client.shared
     dist.barrier(group=ctrl)
+    sync = (lambda: torch.cuda.synchronize(device)) if device.type == "cuda" else None
+    win = RoundWindow(sync)
     t0 = time.perf_counter()
     it = start
-    for it in range(start, max_iters):
-        client.local_step(it)
-        if not in_step:
-            agg.allreduce_(shared)
-        done = client.end_round(it)
-        if checkpoint_dir and checkpoint_every and (it + 1) % checkpoint_every == 0:
-            ckpt.save_client_checkpoint(checkpoint_dir, client, it + 1)
-        if stop_at_num_epochs:
-            flag = torch.tensor([0 if done else 1], device=device)
-            dist.all_reduce(flag)
-            if int(flag.item()) == 0:
-                break
+    with trace_range("rounds"):
+        for it in range(start, max_iters):
+            client.local_step(it)
+            if not in_step:
+                agg.allreduce_(shared)
+            done = client.end_round(it)
+            win.add(int(client.plan.size[it]))
+            if metrics_every and (it + 1) % metrics_every == 0:
+                w = win.close()
+                metrics.write(event="window", rank=rank, round=it + 1, **w)
+            if checkpoint_dir and checkpoint_every and (it + 1) % checkpoint_every == 0:
+                with trace_range("checkpoint"):
+                    ckpt.save_client_checkpoint(checkpoint_dir, client, it + 1)
+            if stop_at_num_epochs:
+                flag = torch.tensor([0 if done else 1], device=device)
+                dist.all_reduce(flag)
+                if int(flag.item()) == 0:
+                    break
     if device.type == "cuda":
         torch.cuda.synchronize()
     wall = time.perf_counter() - t0
+    n_rounds = it + 1 - start
+    docs = int(client.plan.size[start: it + 1].sum())
+    metrics.write(event="train_end", rank=rank, rounds=n_rounds, wall_s=wall, docs=docs,
+                  docs_per_s=docs / wall if wall else None,
+                  ms_per_round=1e3 * wall / max(n_rounds, 1))
     if client.save_path and not client.results_saved:
         client.save_results(client.save_path)
     if rank == 0 and save_server:
@@ -268,4 +319,6 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
         save_model_as_npz(server_model_path(save_server, stamp), tm.get_topic_word_distribution(),
                           None, tm.n_components, None)
     dist.barrier(group=ctrl)
+    if hb is not None:
+        hb.stop()
     return {"rounds": it + 1, "wall_s": wall, "client": client}

@@ -185,3 +185,38 @@ def test_cli_grpc_processes(tmp_path):
     found = [f for _, _, fs in os.walk(tmp_path) for f in fs]
     assert any(f.startswith("global_model_") for f in found)
     assert sum(f.startswith("model_") for f in found) == 2
+
+
+def test_client_servicer_is_idempotent_per_round():
+    """A retried getGradient / sendAggregatedTensor (after a deadline) must not train
+    or apply twice."""
+    from gfedntm_amd.data.synthetic import generate_synthetic
+    from gfedntm_amd.data.vocab import vocabulary_dict
+    from gfedntm_amd.federation.client import FederatedClient
+    from gfedntm_amd.federation.data import ClientCorpus
+    from gfedntm_amd.federation.grpc_transport import ClientServicer
+    from gfedntm_amd.federation.runner import build_dataset, make_topic_model
+    from gfedntm_amd.utils.config import load_config
+    params = dict(load_config().training_params)
+    params.update(num_epochs=1, batch_size=16, hidden_sizes=(16, 16), n_components=5)
+    sc = generate_synthetic(vocab_size=80, n_topics=5, n_docs=40, n_nodes=1, frozen_topics=1,
+                            nwords=(10, 20), seed=1)
+    corpus = ClientCorpus(synthetic=sc, node=0)
+    terms = corpus.local_terms()
+    ds = build_dataset("avitm", corpus, vocabulary_dict(terms), terms)
+    tm = make_topic_model("avitm", params, len(terms), torch.device("cpu"), "torch", seed=0)
+    c = FederatedClient(1, tm, ds, max_iters=5)
+    svc = ClientServicer(c)
+    r1 = svc.getGradient(pb.ServerGetGradientRequest(iter=0), None)
+    state = {k: v.clone() for k, v in tm.model.state_dict().items()}
+    r2 = svc.getGradient(pb.ServerGetGradientRequest(iter=0), None)
+    assert r1 is r2
+    for k, v in tm.model.state_dict().items():
+        assert torch.equal(v, state[k]), k            # no second local step
+    hdr = pb.MessageHeader(message_type=wire.MessageType["SERVER_AGGREGATED_TENSOR_SEND"])
+    msg = pb.ServerAggregatedTensorRequest(header=hdr)
+    shared = {k: v for k, v in tm.model.state_dict().items() if k in set(tm.flat.shared_keys)}
+    msg.nndata.modelUpdate.CopyFrom(wire.model_update_from_state(shared, 0))
+    svc.sendAggregatedTensor(msg, None)
+    svc.sendAggregatedTensor(msg, None)
+    assert c.current_mb == 1 and c.samples_processed == int(c.plan.size[0])

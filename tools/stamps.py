@@ -45,3 +45,5 @@ print("prodlda_bwd cycles:", {nbw[i]: int(d[25 + i] - d[24 + i]) for i in range(
 print("post_fwd cycles: stage", int(d[1] - d[0]), "| colstats", int(d[2] - d[1]), "| row", int(d[3] - d[2]))
 print("row_bwd cycles:", int(d[9] - d[8]))
 print("post_bwd cycles: stage", int(d[11] - d[10]), "| colsums", int(d[12] - d[11]), "| rest", int(d[13] - d[12]))
+print("post_bwd rest: wg0 extras", int(d[14] - d[12]), "| bn_bwd", int(d[15] - d[14]),
+      "| heads", int(d[29] - d[15]), "| hidden", int(d[13] - d[29]))
