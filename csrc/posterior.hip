@@ -395,20 +395,42 @@ __host__ __device__ inline PostLds post_lds(const GfkModel& m) {
 
 extern "C" size_t gfk_post_bwd_smem(const GfkModel* m) { return sizeof(float) * (size_t)post_lds(*m).total; }
 
-// out[j] = sum_k x[k] W[k * ldw + j] for j < n_out (column of a row-major W): 16
-// lanes per output split k, DPP row reduction.
+// out[j] = sum_k term(k, j) for j < n_out: LPO lanes per output split k (DPP quad /
+// row reduction).  LPO = 4 covers 64 outputs per pass of the 256-thread workgroup,
+// so the usual hidden widths take one pass instead of four.
+template <int LPO, class Term, class Epi>
+__device__ __forceinline__ void gemv_lanes(int n_out, int n_in, int tid, Term term, Epi epi) {
+  const int s = tid & (LPO - 1);
+  for (int j0 = 0; j0 < n_out; j0 += PT / LPO) {
+    const int j = j0 + tid / LPO;
+    float acc = 0.f;
+    if (j < n_out) {
+      float a2 = 0.f;                  // two chains, unrolled: LDS reads of 4 k in flight
+      int k = s;
+#pragma unroll 2
+      for (; k + LPO < n_in; k += 2 * LPO) {
+        acc += term(k, j);
+        a2 += term(k + LPO, j);
+      }
+      if (k < n_in) acc += term(k, j);
+      acc += a2;
+    }
+    acc = LPO == 4 ? quad_sum(acc) : row16_sum(acc);
+    if (s == 0 && j < n_out) epi(j, acc);
+  }
+}
+
+template <class Term, class Epi>
+__device__ __forceinline__ void gemv_cols(int n_out, int n_in, int tid, Term term, Epi epi) {
+  if (n_out * 16 <= PT) gemv_lanes<16>(n_out, n_in, tid, term, epi);
+  else gemv_lanes<4>(n_out, n_in, tid, term, epi);
+}
+
+// out[j] = sum_k x[k] W[k * ldw + j] for j < n_out (column of a row-major W).
 template <class Epi>
 __device__ __forceinline__ void colvec_gemv(const float* W, int ldw, const float* x, int n_out, int n_in,
                                             int tid, Epi epi) {
-  const int s = tid & 15;
-  for (int j0 = 0; j0 < n_out; j0 += PT / 16) {
-    const int j = j0 + (tid >> 4);
-    float acc = 0.f;
-    if (j < n_out)
-      for (int k = s; k < n_in; k += 16) acc += x[k] * W[k * ldw + j];
-    acc = row16_sum(acc);
-    if (s == 0 && j < n_out) epi(j, acc);
-  }
+  gemv_cols(n_out, n_in, tid, [&](int k, int j) { return x[k] * W[k * ldw + j]; }, epi);
 }
 
 // grid: bmax workgroups (row = blockIdx.x).
@@ -491,6 +513,7 @@ __global__ void __launch_bounds__(PT) gfk_post_bwd_k(GfkModel m) {
     const float pm = pmean[k];
     float s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f;
     if (valid)
+#pragma unroll 4
       for (int r = g; r < nb; r += 4) {
         const float d = dy[r * K + k], x = xh[r * K + k];
         s1 += d;
@@ -583,19 +606,13 @@ __global__ void __launch_bounds__(PT) gfk_post_bwd_k(GfkModel m) {
     const float* mask = smem + L.mask;
     const float* zl = zrow + zoff_last;
     float* dzo = m.ws_dz[nh - 1] + (size_t)row * Hl;
-    const int s = tid & 15;
-    for (int j0 = 0; j0 < Hl; j0 += PT / 16) {
-      const int j = j0 + (tid >> 4);
-      float acc = 0.f;
-      if (j < Hl)
-        for (int k = s; k < K; k += 16) acc += dr[k] * Wmu[k * Hl + j] + dr[K + k] * Ws[k * Hl + j];
-      acc = row16_sum(acc);
-      if (s == 0 && j < Hl) {
-        const float g = acc * mask[j] * act_d(m.act, zl[j]);
-        v0[j] = g;
-        dzo[j] = g;
-      }
-    }
+    gemv_cols(Hl, K, tid,
+              [&](int k, int j) { return dr[k] * Wmu[k * Hl + j] + dr[K + k] * Ws[k * Hl + j]; },
+              [&](int j, float acc) {
+                const float g = acc * mask[j] * act_d(m.act, zl[j]);
+                v0[j] = g;
+                dzo[j] = g;
+              });
   }
   lds_barrier();
   GFK_STAMP(m, 29);
