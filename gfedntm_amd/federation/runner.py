@@ -288,7 +288,11 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
     it = start
     with trace_range("rounds"):
         for it in range(start, max_iters):
+            if hb is not None:
+                hb.mark(it, 0)
             client.local_step(it)
+            if hb is not None:
+                hb.mark(it, 1)
             if not in_step:
                 agg.allreduce_(shared)
             done = client.end_round(it)

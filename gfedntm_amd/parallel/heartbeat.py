@@ -2,9 +2,13 @@
 
 The reference has no failure detection: a client that dies leaves the server's
 training thread raising inside an RPC and the rest of the federation hanging.
-Here every rank publishes a heartbeat (a monotonic counter) in the process
-group's TCP store from a daemon thread and checks its peers' counters; a peer
-whose counter stops moving for ``timeout`` seconds is declared dead and the
+Here every rank publishes a heartbeat (a monotonic counter plus its round
+progress, which the training loop sets with :meth:`Heartbeat.mark` -- a plain
+attribute store, no I/O on the hot path) in the process group's TCP store from a
+daemon thread and checks its peers.  A peer is declared failed when its counter
+stops moving for ``timeout`` seconds (process dead or frozen), or when it is
+behind this rank's progress and has not progressed for ``timeout`` seconds (its
+main thread hangs while this rank waits for it in a collective); then the
 ``on_failure`` callback runs (default: log, then hard-exit the process, since
 the main thread is typically blocked inside a collective that will never
 complete; the last round checkpoint is the resume point).  A rank that finishes
@@ -43,6 +47,11 @@ class Heartbeat:
         self._thread: Optional[threading.Thread] = None
         self.failed: List[int] = []
         self._seen: Dict[int, tuple] = {}
+        self.progress = 0
+
+    def mark(self, rnd: int, phase: int = 0):
+        """Training-loop progress: 2 * round + phase (0 = local step, 1 = all-reduce)."""
+        self.progress = 2 * int(rnd) + int(phase)
 
     def _key(self, kind: str, r: int) -> str:
         return f"{self.prefix}/{kind}/{r}"
@@ -54,9 +63,10 @@ class Heartbeat:
         os._exit(3)
 
     def start(self) -> "Heartbeat":
-        self.store.set(self._key("beat", self.rank), "0")
+        self.store.set(self._key("beat", self.rank), f"0:{self.progress}")
         now = time.monotonic()
-        self._seen = {r: ("", now) for r in range(self.world) if r != self.rank}
+        # peer -> (last beat, time it changed, last progress, time progress changed)
+        self._seen = {r: ("", now, -1, now) for r in range(self.world) if r != self.rank}
         self._thread = threading.Thread(target=self._run, name="gfedntm-heartbeat", daemon=True)
         self._thread.start()
         return self
@@ -73,17 +83,24 @@ class Heartbeat:
         while not self._stop.wait(self.interval):
             n += 1
             try:
-                self.store.set(self._key("beat", self.rank), str(n))
+                mine = self.progress
+                self.store.set(self._key("beat", self.rank), f"{n}:{mine}")
                 now = time.monotonic()
                 dead = []
-                for r, (last, t) in list(self._seen.items()):
+                for r, (last, t, prog, tp) in list(self._seen.items()):
                     v = self._peer_state(r)
                     if v == "done":
                         self._seen.pop(r)
                         continue
+                    p = int(v.split(":")[1]) if ":" in v else prog
+                    if p != prog:
+                        prog, tp = p, now
                     if v != last:
-                        self._seen[r] = (v, now)
-                    elif now - t > self.timeout:
+                        last, t = v, now
+                    self._seen[r] = (last, t, prog, tp)
+                    if now - t > self.timeout:                       # no beats: dead / frozen
+                        dead.append(r)
+                    elif 0 <= prog < mine and now - tp > self.timeout:  # behind and stuck
                         dead.append(r)
                 if dead:
                     self.failed = dead

@@ -73,3 +73,52 @@ def test_cli_writes_jsonl_metrics(tmp_path):
     assert [w["round"] for w in windows] == [3, 6] and len(end) == 1
     assert end[0]["rounds"] == 6 and end[0]["docs_per_s"] > 0
     assert all(w["docs"] > 0 and w["loss"] > 0 for w in windows)
+
+
+def _hang_worker(rank, world, port, tmp):
+    import os as _os
+    import time as _time
+    _os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                       WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=600))
+    from gfedntm_amd.data.synthetic import generate_synthetic
+    from gfedntm_amd.federation import client as client_mod
+    from gfedntm_amd.federation.data import ClientCorpus
+    from gfedntm_amd.federation.runner import run_distributed
+    from gfedntm_amd.utils.config import load_config
+    orig = client_mod.FederatedClient.local_step
+
+    def local_step(self, it):
+        if rank == 1 and it == 3:
+            _time.sleep(600)                  # the main thread hangs; its heartbeat lives on
+        return orig(self, it)
+
+    client_mod.FederatedClient.local_step = local_step
+    params = dict(load_config().training_params)
+    params.update(num_epochs=2, batch_size=16, hidden_sizes=(16, 16), n_components=5)
+    sc = generate_synthetic(vocab_size=60, n_topics=5, n_docs=30, n_nodes=2, frozen_topics=1,
+                            nwords=(10, 20), seed=2)
+    run_distributed(ClientCorpus(synthetic=sc, node=rank), params, max_iters=50,
+                    backend="torch", heartbeat_timeout=3.0)
+
+
+def test_hung_peer_aborts_the_waiting_rank(tmp_path):
+    """A rank whose training loop hangs (process alive) is detected by the waiting
+    rank, which aborts (exit code 3) instead of blocking in the collective."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ps = [ctx.Process(target=_hang_worker, args=(r, 2, port, str(tmp_path))) for r in range(2)]
+    for p in ps:
+        p.start()
+    ps[0].join(120)
+    try:
+        assert ps[0].exitcode == 3, ps[0].exitcode
+    finally:
+        for p in ps:
+            if p.is_alive():
+                p.kill()
+            p.join(10)
