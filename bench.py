@@ -182,6 +182,30 @@ def main():
         topics_idx = torch.topk(tm.model.beta.detach(), 10, dim=1).indices.cpu().numpy()
         npmi = float(npmi_coherence(topics_idx, ref_corpus, device=device))
 
+    # round latency split (BASELINE: compute / all-reduce / host): the same number of
+    # steps again with the collective detached, after the timed region
+    split = None
+    if world > 1 and args.backend == "fused" and eng._comm is not None:
+        saved_comm = eng._comm
+        eng._comm = None
+        eng._invalidate_graph()
+        k2 = max(1, min(args.steps, 500))
+        for s in range(n_steps, n_steps + min(args.warmup, 50)):
+            eng.step(s % n_steps)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t1 = time.perf_counter()
+        for s in range(k2):
+            eng.step(s % n_steps)
+        torch.cuda.synchronize()
+        tc = torch.tensor([(time.perf_counter() - t1) / k2 * 1e3], dtype=torch.float64,
+                          device=device)
+        dist.all_reduce(tc, op=dist.ReduceOp.MAX)
+        eng._comm = saved_comm
+        split = {"compute_ms": round(float(tc.item()), 5)}
+    if split is not None:
+        split["allreduce_exposed_ms"] = round(max(ms - split["compute_ms"], 0.0), 5)
+
     if rank == 0:
         out = {
             "metric": "docs/sec (whole node) + NPMI, ProdLDA K=50 8-client fed on synthetic BoW",
@@ -207,6 +231,8 @@ def main():
                        "aggregation": "per-minibatch sample-weighted FedAvg of 20 shared tensors"
                                       + (f" ({comm} all-reduce)" if world > 1 else "")},
             "npmi": None if npmi is None else round(npmi, 4),
+            "round_split_ms": split if split is not None else {"compute_ms": round(ms, 5),
+                                                               "allreduce_exposed_ms": 0.0},
             "final_loss": float(np.mean(losses[-20:])),
             "baseline": {"fed_grpc_8clients_docs_per_s": BASELINE_FED_DOCS_PER_S,
                          "cpu_centralized_docs_per_s": BASELINE_CPU_CENTRALIZED_DOCS_PER_S},
