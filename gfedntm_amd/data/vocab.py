@@ -30,7 +30,9 @@ def local_vocabulary(texts: Sequence[str]) -> Dict[str, int]:
     """Term -> local column index, exactly as CountVectorizer.vocabulary_."""
     from ..ops import native
     if native.tokenizer_available():
-        return native.local_vocabulary(texts)
+        v = native.local_vocabulary(texts)      # None: non-ASCII corpus -> scikit-learn
+        if v is not None:
+            return v
     cv = _sklearn_cv(stop_words="english")
     cv.fit(texts)
     return {k: int(v) for k, v in cv.vocabulary_.items()}
@@ -52,7 +54,9 @@ def vectorize(texts: Sequence[str], vocabulary: Dict[str, int]) -> sp.csr_matrix
     """Doc-term counts of ``texts`` over a fixed vocabulary (float32 CSR)."""
     from ..ops import native
     if native.tokenizer_available():
-        return native.vectorize(texts, vocabulary)
+        m = native.vectorize(texts, vocabulary)
+        if m is not None:
+            return m
     cv = _sklearn_cv(vocabulary=vocabulary)
     m = cv.transform(texts).astype(np.float32)
     m.sort_indices()

@@ -60,7 +60,8 @@ def build(verbose=True, jobs=8):
         obj = os.path.join(OBJ, s + ".host.o")
         robjs.append(obj)
         if _newer(src, obj, headers):
-            jobs_list.append((["g++", "-O3", "-fPIC", "-std=c++17", "-c", src, "-o", obj], s))
+            jobs_list.append((["g++", "-O3", "-fPIC", "-std=c++17", "-pthread", "-Wall", "-c", src,
+                              "-o", obj], s))
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         for s in ex.map(_compile, jobs_list):
             if verbose:
@@ -77,7 +78,7 @@ def build(verbose=True, jobs=8):
     rso = os.path.join(LIB, "libgfedntm_runtime.so")
     if robjs and (not os.path.exists(rso) or any(os.path.getmtime(o) > os.path.getmtime(rso)
                                                  for o in robjs)):
-        r = subprocess.run(["g++", "-shared", "-fPIC", "-o", rso] + robjs, capture_output=True,
+        r = subprocess.run(["g++", "-shared", "-fPIC", "-pthread", "-o", rso] + robjs, capture_output=True,
                            text=True)
         if r.returncode:
             raise RuntimeError(r.stderr[-4000:])
