@@ -96,7 +96,7 @@ typedef struct GfkModel {
   float *ws_dz[GFK_MAX_LAYERS];  // d pre-activation of each hidden layer [bmax, H[l]] (l = 0: input layer)
   float *ws_dmr, *ws_dlr;        // [bmax, K] d mu_raw / d log-sigma_raw (BN backward of the heads)
   float *ws_dmu, *ws_dls;        // [bmax, K] dL/d(post-BN mu, log-sigma)
-  float *ws_dbsm;                // LDA: d softmax(beta)^T accumulator [V, K]
+  float *ws_dbsm;                // LDA: per CSR non-zero of the batch, g = -x / (wd + 1e-10) [nnz]
   float *ws_ck;                  // LDA: [K] sum_v beta_sm * d beta_sm
   float *ws_hctx;                // CTM: dense contextual contribution to layer 0 [bmax, H0]
   int32_t *ws_tstart;            // [bmax, n_tiles+1] CSR position of each row's first nz per vocab tile

@@ -11,7 +11,7 @@
 // tokens (stored transposed, [V, K], one contiguous 4K-byte row per token).
 // The softmax-over-V backward needs c_k = sum_v beta_sm[k,v] dbeta_sm[k,v],
 // which equals sum_b theta_d[b,k] dtheta_d[b,k] and is computed from the tiny
-// [B, K] tensors in the posterior backward instead of a V-wide reduction.
+// [B, K] tensors in lda_beta_bwd's prologue instead of a V-wide reduction.
 #include "gfk_common.h"
 
 using namespace gfk;
@@ -102,43 +102,67 @@ extern "C" __global__ void __launch_bounds__(LDA_THREADS) gfk_lda_beta_fwd(GfkMo
   }
 }
 
-// One workgroup per document: sparse loss + d theta_d + scatter of d beta_sm^T.
-// dynamic LDS: dth[4*K] + th[K] + rls[4]
-extern "C" __global__ void __launch_bounds__(LDA_THREADS) gfk_lda_row_loss_bwd(GfkModel m) {
+// One workgroup (16 waves) per document: the sparse loss, d theta_d, and the
+// coefficient g = -x / (wd + 1e-10) of every non-zero (ws_dbsm, indexed by CSR
+// position).  d beta_sm^T[v, k] = sum_b theta_d[b, k] g[b, v] is formed later by
+// lda_beta_bwd as an MFMA product per vocab tile -- deterministic, no atomics.
+// Each wave takes U non-zeros per round so their gathers are in flight together.
+// dynamic LDS: dth[16*K] + rls[16]
+constexpr int LDA_ROW_THREADS = 1024;
+constexpr int LDA_ROW_WAVES = LDA_ROW_THREADS / 64;
+
+template <int KQ>
+__global__ void __launch_bounds__(LDA_ROW_THREADS) gfk_lda_row_k(GfkModel m) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int b = blockIdx.x, nb = *m.ws_nb;
   if (b >= nb) return;
   const int K = m.K, tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
   float* dth = smem;
-  float* th = dth + 4 * K;
-  float* rls = th + K;
-  for (int k = tid; k < K; k += LDA_THREADS) th[k] = m.ws_thetad[(size_t)b * m.kt + k];
-  __syncthreads();
+  float* rls = dth + LDA_ROW_WAVES * K;
+  float th[KQ], ls[KQ];
+#pragma unroll
+  for (int q = 0; q < KQ; ++q) {
+    const int k = lane + 64 * q;
+    th[q] = k < K ? m.ws_thetad[(size_t)b * m.kt + k] : 0.f;
+    ls[q] = k < K ? m.ws_lse[k] : 0.f;
+  }
   const int e0 = m.ws_erange[2 * b], e1 = m.ws_erange[2 * b + 1];
-  constexpr int KQ = 4;   // K <= 256
-  float acc[KQ] = {0.f, 0.f, 0.f, 0.f};
+  constexpr int U = 4;
+  float acc[KQ];
+#pragma unroll
+  for (int q = 0; q < KQ; ++q) acc[q] = 0.f;
   float rl = 0.f;
-  for (int e = e0 + wave; e < e1; e += 4) {
-    const int v = m.indices[e];
-    const float x = m.values[e];
-    const float* bnr = m.ws_zn + (size_t)v * K;
-    float bs[KQ];
-    float wd = 0.f;
+  for (int e = e0 + wave; e < e1; e += LDA_ROW_WAVES * U) {
+    int v[U];
+    float x[U];
 #pragma unroll
-    for (int q = 0; q < KQ; ++q) {
-      const int k = lane + 64 * q;
-      bs[q] = k < K ? __expf(bnr[k] - m.ws_lse[k]) : 0.f;
-      wd += (k < K ? th[k] : 0.f) * bs[q];
+    for (int u = 0; u < U; ++u) {
+      const int ee = min(e + LDA_ROW_WAVES * u, e1 - 1);
+      v[u] = m.indices[ee];
+      x[u] = e + LDA_ROW_WAVES * u < e1 ? m.values[ee] : 0.f;
     }
-    wd = wave_sum(wd);
-    const float g = -x / (wd + RL_EPS);
-    rl += x * logf(wd + RL_EPS);
+    float z[U][KQ];
 #pragma unroll
-    for (int q = 0; q < KQ; ++q) {
-      const int k = lane + 64 * q;
-      if (k < K) {
-        acc[q] += g * bs[q];
-        atomicAdd(m.ws_dbsm + (size_t)v * K + k, th[k] * g);
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int q = 0; q < KQ; ++q)
+        z[u][q] = m.ws_zn[(size_t)v[u] * K + min(lane + 64 * q, K - 1)];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int ee = e + LDA_ROW_WAVES * u;
+      float bs[KQ], wd = 0.f;
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) {
+        bs[q] = lane + 64 * q < K ? __expf(z[u][q] - ls[q]) : 0.f;
+        wd += th[q] * bs[q];
+      }
+      wd = wave_sum(wd);
+      if (ee < e1) {                       // wave-uniform
+        const float g = -x[u] / (wd + RL_EPS);
+        rl += x[u] * logf(wd + RL_EPS);
+#pragma unroll
+        for (int q = 0; q < KQ; ++q) acc[q] += g * bs[q];
+        if (lane == 0) m.ws_dbsm[ee] = g;
       }
     }
   }
@@ -147,37 +171,104 @@ extern "C" __global__ void __launch_bounds__(LDA_THREADS) gfk_lda_row_loss_bwd(G
     const int k = lane + 64 * q;
     if (k < K) dth[wave * K + k] = acc[q];
   }
-  // x and wd are wave-uniform, so every lane of a wave holds the wave's loss partial
   if (lane == 0) rls[wave] = rl;
   __syncthreads();
-  for (int k = tid; k < K; k += LDA_THREADS)
-    m.ws_dthetad[(size_t)b * K + k] = dth[k] + dth[K + k] + dth[2 * K + k] + dth[3 * K + k];
-  if (tid == 0) m.ws_rl[b] = -(rls[0] + rls[1] + rls[2] + rls[3]);
+  for (int k = tid; k < K; k += LDA_ROW_THREADS) {
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < LDA_ROW_WAVES; ++w) s += dth[w * K + k];
+    m.ws_dthetad[(size_t)b * K + k] = s;
+  }
+  if (tid == 0) {
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < LDA_ROW_WAVES; ++w) s += rls[w];
+    m.ws_rl[b] = -s;
+  }
 }
 
-// grid: dec_grid workgroups over vocab tiles.  softmax-over-V backward and
-// BN-over-K backward; clears the consumed d beta_sm accumulator.
-// dynamic LDS: bn[K*LD] + d[K*LD]
-extern "C" __global__ void __launch_bounds__(LDA_THREADS) gfk_lda_beta_bwd(GfkModel m) {
+// grid: dec_grid workgroups over vocab tiles.  Per tile: d beta_sm^T = G^T theta_d
+// on the matrix cores (G = the tile's [64 x B] non-zero coefficients, built in LDS
+// from the per-row CSR tile table), then the softmax-over-V backward and the
+// BN-over-K backward.  ThLds: theta_d staged in LDS (K up to ~128), else read from L2.
+// dynamic LDS: bn[K*LD] + d[K*LD] + xt[64*XS] (+ thd[B*kt + 64]) + ck[pad4(K)] (+ dth[B*K])
+__host__ __device__ inline int lda_xs(int B) {
+  int s = (B + 3) & ~3;
+  if ((s / 4) % 2 == 0) s += 4;
+  return s;
+}
+
+template <bool ThLds>
+__global__ void __launch_bounds__(LDA_THREADS) gfk_lda_beta_bwd_k(GfkModel m) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int K = m.K, V = m.V, tid = threadIdx.x;
+  const int K = m.K, V = m.V, tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
+  const int B = m.bmax, kt = m.kt, XS = lda_xs(B), nb = *m.ws_nb;
   float* bn = smem;
   float* d = bn + K * LD;
+  float* xt = d + K * LD;
+  float* thd = xt + VB * XS;
+  float* ckl = thd + (ThLds ? B * kt + 64 : 0);
+  float* dtl = ckl + ((K + 3) & ~3);                 // staged d theta_d [B][K] (ThLds)
+  if (ThLds) {                                        // LDS-DMA: theta_d and d theta_d
+    glds_copy(thd, m.ws_thetad, B * kt, tid, LDA_THREADS);
+    glds_copy(dtl, m.ws_dtheta, B * K, tid, LDA_THREADS);
+    for (int i = tid; i < 64; i += LDA_THREADS) thd[B * kt + i] = 0.f;
+    vm_barrier();
+  }
+  const float* thv = ThLds ? thd : m.ws_thetad;
+  const float* dtv = ThLds ? dtl : m.ws_dtheta;
+  // c_k = sum_b theta_d[b, k] d theta_d[b, k] (softmax-over-V backward), 4 threads per topic
+  for (int k0 = 0; k0 < K; k0 += LDA_THREADS / 4) {
+    const int k = k0 + (tid >> 2), sub = tid & 3;
+    float s = 0.f;
+    if (k < K)
+#pragma unroll 4
+      for (int r = sub; r < nb; r += 4) s += thv[r * kt + k] * dtv[r * K + k];
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    if (sub == 0 && k < K) ckl[k] = s;
+  }
+  const int NT = (K + 15) / 16;
   for (int tile = blockIdx.x; tile < m.n_tiles; tile += gridDim.x) {
     const int c0 = tile * VB;
     __syncthreads();
+    for (int i = tid; i < VB * XS; i += LDA_THREADS) xt[i] = 0.f;
     for (int i = tid; i < K * VB; i += LDA_THREADS) {
       const int c = i / K, k = i % K;
-      float z = 0.f, g = 0.f;
+      float z = 0.f, bs = 0.f;
       if (c0 + c < V) {
-        const size_t o = (size_t)(c0 + c) * K + k;
-        z = m.ws_zn[o];
-        const float bs = __expf(z - m.ws_lse[k]);
-        g = bs * (m.ws_dbsm[o] - m.ws_ck[k]);
-        m.ws_dbsm[o] = 0.f;
+        z = m.ws_zn[(size_t)(c0 + c) * K + k];
+        bs = __expf(z - m.ws_lse[k]);
       }
       bn[k * LD + c] = z;
-      d[k * LD + c] = g;
+      d[k * LD + c] = bs;
+    }
+    __syncthreads();
+    {  // the tile's non-zero coefficients: 4 threads per batch row
+      const int row = tid >> 2, sub = tid & 3;
+      if (row < nb && row < B) {
+        const int32_t* ts = m.ws_tstart + (size_t)row * (m.n_tiles + 1) + tile;
+        const int es = ts[0], ee = ts[1];
+        for (int e = es + sub; e < ee; e += 4) xt[(m.indices[e] - c0) * XS + row] = m.ws_dbsm[e];
+      }
+    }
+    __syncthreads();
+    // G[c][k] = sum_b xt[c][b] theta_d[b][k]; then d <- bs * (G - c_k)
+    for (int t = wave; t < 4 * NT; t += LDA_THREADS / 64) {
+      const int i0 = (t / NT) * 16, j0 = (t % NT) * 16;
+      const float* ap = xt + (i0 + (lane & 15)) * XS + (lane >> 4);
+      const float* bp = thv + (lane >> 4) * kt + j0 + (lane & 15);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int kb = 0; kb < B; kb += 4) acc = mfma16x16x4(ap[kb], bp[kb * kt], acc);
+      const int k = j0 + (lane & 15);
+      if (k < K) {
+        const float ck = ckl[k];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = i0 + (lane >> 4) * 4 + r;
+          d[k * LD + c] = d[k * LD + c] * (acc[r] - ck);
+        }
+      }
     }
     __syncthreads();
     {
@@ -208,8 +299,18 @@ extern "C" __global__ void __launch_bounds__(LDA_THREADS) gfk_lda_beta_bwd(GfkMo
 }
 
 extern "C" size_t gfk_lda_fwd_smem(int K) { return sizeof(float) * ((size_t)K * LD + 2 * K); }
-extern "C" size_t gfk_lda_row_smem(int K) { return sizeof(float) * ((size_t)K * 5 + 4); }
-extern "C" size_t gfk_lda_bwd_smem(int K) { return sizeof(float) * ((size_t)K * LD * 2); }
+extern "C" size_t gfk_lda_row_smem(int K) {
+  return sizeof(float) * ((size_t)K * LDA_ROW_WAVES + LDA_ROW_WAVES);
+}
+static size_t lda_bwd_floats(const GfkModel* m, bool th_lds) {
+  size_t n = (size_t)m->K * LD * 2 + (size_t)VB * lda_xs(m->bmax) + (((size_t)m->K + 3) & ~(size_t)3);
+  if (th_lds) n += (size_t)m->bmax * m->kt + 64 + (size_t)m->bmax * m->K + 4;
+  return n;
+}
+static bool lda_bwd_th_lds(const GfkModel* m) { return sizeof(float) * lda_bwd_floats(m, true) <= 160 * 1024; }
+extern "C" size_t gfk_lda_bwd_smem(const GfkModel* m) {
+  return sizeof(float) * lda_bwd_floats(m, lda_bwd_th_lds(m));
+}
 
 extern "C" int gfk_launch_lda_beta_fwd(const GfkModel* m, hipStream_t s) {
   hipLaunchKernelGGL(gfk_lda_beta_fwd, dim3(m->dec_grid), dim3(LDA_THREADS), gfk_lda_fwd_smem(m->K),
@@ -218,22 +319,31 @@ extern "C" int gfk_launch_lda_beta_fwd(const GfkModel* m, hipStream_t s) {
 }
 
 extern "C" int gfk_launch_lda_row(const GfkModel* m, hipStream_t s) {
-  hipLaunchKernelGGL(gfk_lda_row_loss_bwd, dim3(m->bmax), dim3(LDA_THREADS), gfk_lda_row_smem(m->K),
-                     s, *m);
+  const dim3 g(m->bmax), t(LDA_ROW_THREADS);
+  const size_t sm = gfk_lda_row_smem(m->K);
+  const int kq = (m->K + 63) / 64;
+  if (kq <= 1) hipLaunchKernelGGL(gfk_lda_row_k<1>, g, t, sm, s, *m);
+  else if (kq == 2) hipLaunchKernelGGL(gfk_lda_row_k<2>, g, t, sm, s, *m);
+  else if (kq == 3) hipLaunchKernelGGL(gfk_lda_row_k<3>, g, t, sm, s, *m);
+  else hipLaunchKernelGGL(gfk_lda_row_k<4>, g, t, sm, s, *m);
   return (int)hipGetLastError();
 }
 
 extern "C" int gfk_launch_lda_beta_bwd(const GfkModel* m, hipStream_t s) {
-  hipLaunchKernelGGL(gfk_lda_beta_bwd, dim3(m->dec_grid), dim3(LDA_THREADS), gfk_lda_bwd_smem(m->K),
-                     s, *m);
+  const dim3 g(m->dec_grid), t(LDA_THREADS);
+  if (lda_bwd_th_lds(m))
+    hipLaunchKernelGGL(gfk_lda_beta_bwd_k<true>, g, t, gfk_lda_bwd_smem(m), s, *m);
+  else
+    hipLaunchKernelGGL(gfk_lda_beta_bwd_k<false>, g, t, gfk_lda_bwd_smem(m), s, *m);
   return (int)hipGetLastError();
 }
 
 extern "C" int gfk_lda_set_smem(size_t bytes) {
-  hipError_t e = hipFuncSetAttribute((const void*)gfk_lda_beta_fwd,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-  if (e == hipSuccess)
-    e = hipFuncSetAttribute((const void*)gfk_lda_beta_bwd,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-  return (int)e;
+  const void* ks[] = {(const void*)gfk_lda_beta_fwd, (const void*)gfk_lda_beta_bwd_k<true>,
+                      (const void*)gfk_lda_beta_bwd_k<false>};
+  for (const void* k : ks) {
+    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e != hipSuccess) return (int)e;
+  }
+  return 0;
 }

@@ -23,8 +23,7 @@
 //               partials, softmax / reparameterisation / KL backward -> dmu, dls.
 //   post_bwd  : column sums of dmu, dls (all rows), own row: BN backward ->
 //               d mu_raw, d ls_raw, heads and hidden-layer backward -> dz of every
-//               layer.  Workgroup 0: prior gradients, NeuralLDA c_k, the loss, the
-//               step counter.
+//               layer.  Workgroup 0: prior gradients, the loss, the step counter.
 #include "gfk_common.h"
 
 using namespace gfk;
@@ -538,7 +537,7 @@ __global__ void __launch_bounds__(PT) gfk_post_bwd_k(GfkModel m) {
   lds_barrier();
   GFK_STAMP(m, 12);
 
-  // ---- workgroup 0: prior gradients (-> grad slots), NeuralLDA c_k, loss, step ----
+  // ---- workgroup 0: prior gradients (-> grad slots), loss, step ----
   const float inv_nb = 1.f / (float)nb;
   if (row == 0) {
     const float wk = m.kl_weight;
@@ -548,22 +547,6 @@ __global__ void __launch_bounds__(PT) gfk_post_bwd_k(GfkModel m) {
       m.prior_mean[tid + m.off_g] = wk * ((float)nb * pmk - smu) / pvk;
       m.prior_var[tid + m.off_g] =
           wk * 0.5f * ((float)nb / pvk - svar / (pvk * pvk) - sdm2 / (pvk * pvk));
-    }
-    if (m.kind == GFK_LDA && tid < K) {
-      float ck = 0.f;
-      int r = 0;
-      for (; r + 8 <= nb; r += 8) {     // 8 independent load pairs per round
-        float a[8], d[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          a[u] = m.ws_thetad[(r + u) * m.kt + tid];
-          d[u] = m.ws_dtheta[(r + u) * K + tid];
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) ck += a[u] * d[u];
-      }
-      for (; r < nb; ++r) ck += m.ws_thetad[r * m.kt + tid] * m.ws_dtheta[r * K + tid];
-      m.ws_ck[tid] = ck;
     }
     const float l = block_sum_wave0(lterm, smem + L.v1);   // (v1 is free until the hidden layers)
     if (tid == 0) {

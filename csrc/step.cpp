@@ -30,7 +30,7 @@ int gfk_launch_scale(float*, int64_t, float, hipStream_t);
 size_t gfk_prodlda_fwd_smem(const GfkModel*);
 size_t gfk_prodlda_bwd_smem(const GfkModel*);
 size_t gfk_lda_fwd_smem(int);
-size_t gfk_lda_bwd_smem(int);
+size_t gfk_lda_bwd_smem(const GfkModel*);
 size_t gfk_post_smem(const GfkModel*);
 size_t gfk_win_update_smem(const GfkModel*);
 size_t gfk_enc_in_smem(const GfkModel*);
@@ -65,7 +65,7 @@ size_t gfk_smem_required(const GfkModel* m, int which) {
     case 0: return gfk_prodlda_fwd_smem(m);
     case 1: return gfk_prodlda_bwd_smem(m);
     case 2: return gfk_lda_fwd_smem(m->K);
-    case 3: return gfk_lda_bwd_smem(m->K);
+    case 3: return gfk_lda_bwd_smem(m);
     case 4: return gfk_post_smem(m);
     case 5: return gfk_win_update_smem(m);
     case 7: return gfk_enc_in_smem(m);
@@ -80,7 +80,7 @@ int gfk_setup(const GfkModel* m) {
   size_t p = gfk_prodlda_fwd_smem(m), q = gfk_prodlda_bwd_smem(m);
   if ((e = gfk_prodlda_set_smem(p > q ? p : q))) return e;
   p = gfk_lda_fwd_smem(m->K);
-  q = gfk_lda_bwd_smem(m->K);
+  q = gfk_lda_bwd_smem(m);
   if ((e = gfk_lda_set_smem(p > q ? p : q))) return e;
   if ((e = gfk_enc_in_set_smem(gfk_enc_in_smem(m)))) return e;
   if ((e = gfk_post_set_smem(gfk_post_smem(m)))) return e;

@@ -359,7 +359,7 @@ class FusedEngine(EngineBase):
             "row_part": f(max(m.n_tiles * 4 * B, m.dec_grid * K) * 2),
             "dthetad": f(m.n_dpart * B * K),
             "dmr": f(B, K), "dlr": f(B, K), "dmu": f(B, K), "dls": f(B, K),
-            "dbsm": f(V * K if m.kind == abi.KIND_LDA else 1), "ck": f(K),
+            "dbsm": f(1), "ck": f(K),        # LDA: per-non-zero coefficients, sized in bind_data
             "hctx": f(B, hs[0]),
             "tstart": torch.zeros(B * (m.n_tiles + 1), dtype=torch.int32, device=dev),
             "erange": torch.zeros(2 * B, dtype=torch.int32, device=dev),
@@ -490,6 +490,11 @@ class FusedEngine(EngineBase):
         }
         m.indptr, m.indices, m.values = (data.indptr.data_ptr(), data.indices.data_ptr(),
                                          data.values.data_ptr())
+        if m.kind == abi.KIND_LDA:      # g = -x / (wd + eps) per CSR non-zero (lda_row -> lda_beta_bwd)
+            nnz = int(data.indices.numel())
+            if self.ws["dbsm"].numel() < nnz:
+                self.ws["dbsm"] = torch.zeros(nnz + 16, dtype=torch.float32, device=dev)
+            m.ws_dbsm = self.ws["dbsm"].data_ptr()
         m.ctx = data.contextual.data_ptr() if data.contextual is not None else None
         m.plan_order = self._plan_dev["order"].data_ptr()
         m.plan_start = self._plan_dev["start"].data_ptr()

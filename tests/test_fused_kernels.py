@@ -274,3 +274,20 @@ def test_ctm_graph_training():
         e.step(s)
     h = e.loss_hist[:200].cpu().numpy()
     assert np.isfinite(h).all() and h[-20:].mean() < h[:20].mean()
+
+
+@pytest.mark.parametrize("model_type", ["prodLDA", "LDA"])
+def test_steps_are_bitwise_deterministic(model_type):
+    """No atomics anywhere: two runs from the same state give identical bits."""
+    X = random_csr(300, 900, 60, seed=5)
+    outs = []
+    for _ in range(2):
+        torch.manual_seed(3)
+        tm = AVITM(input_size=900, n_components=30, model_type=model_type, hidden_sizes=(40, 40),
+                   batch_size=64, verbose=False, device="cuda", backend="fused")
+        _bind(tm, X, n_steps=12)
+        for s in range(12):
+            tm.engine.step(s)
+        torch.cuda.synchronize()
+        outs.append((tm.flat.buffer.clone(), tm.engine.loss_hist[:12].clone()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
