@@ -36,11 +36,15 @@ __device__ __forceinline__ void gather_rows(const int32_t* __restrict__ idx,
                                             int wave, const float* __restrict__ w, int H,
                                             int lane, float* acc) {
   constexpr int CH = NQ == 1 ? 16 : (NQ == 2 ? 8 : 4);
-  for (int base = e0 + wave * 64; base < e1; base += ENC_WAVES * 64) {
-    const int e = min(base + lane, e1 - 1);
+  // non-zeros dealt round-robin over the waves (wave w: e0 + w + ENC_WAVES * i), so a
+  // typical row (~100-200 non-zeros) costs every wave one index load and one batch of
+  // CH row loads in flight
+  for (int base = e0 + wave; base < e1; base += ENC_WAVES * 64) {
+    const int le = base + ENC_WAVES * lane;
+    const int e = min(le, e1 - 1);
     const int my_v = idx[e];
-    const float my_x = (base + lane < e1) ? val[e] : 0.f;
-    const int cnt = min(64, e1 - base);
+    const float my_x = le < e1 ? val[e] : 0.f;
+    const int cnt = min(64, (e1 - base + ENC_WAVES - 1) / ENC_WAVES);
     for (int g = 0; g < cnt; g += CH) {
       float wv[CH][NQ];
 #pragma unroll
@@ -134,6 +138,7 @@ __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkModel m) {
   float* wst = maskh + pad4(Hl);
   constexpr bool staged = Staged;
 
+  GFK_STAMP(m, 4);
   // ---- one round: the row, the step, the weights (LDS-DMA), the biases ----
   if (staged) {
     float* p = wst;
@@ -166,6 +171,7 @@ __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkModel m) {
     if (b == 0) *m.ws_nb = nb;
   }
 
+  GFK_STAMP(m, 5);
   // ---- sparse gather ----
   if (input != GFK_IN_CONTEXTUAL) {
     float acc[8];
@@ -210,6 +216,7 @@ __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkModel m) {
     }
   }
   vm_barrier();             // gather partials + staged weights
+  GFK_STAMP(m, 6);
 
   // ---- input layer: z0 = sum of the wave partials + bias (+ dense contextual part) ----
   const int act = m.act;
@@ -261,6 +268,7 @@ __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkModel m) {
     float* t = ain; ain = aout; aout = t;
   }
 
+  GFK_STAMP(m, 7);
   // ---- mu / log-sigma heads (pre batch-norm) ----
   const float* Wmu = staged ? wcur : m.w_mu;
   const float* Bmu = staged ? wcur + pad4(K * Hl) : m.b_mu;

@@ -168,6 +168,7 @@ extern "C" __global__ void __launch_bounds__(UT) gfk_win_update(GfkModel m, GfkU
   float* dz = smem + 64 * XS;
   const int tile = blockIdx.x, c0 = tile * 64;
 
+  GFK_STAMP(m, 40);
   // ---- staging: dz0 rows (zero padding), zero x^T tile, the tile's CSR extents ----
   const int nb = *nbp;
   for (int i = tid; i < B * H0P; i += UT) {
@@ -208,6 +209,7 @@ extern "C" __global__ void __launch_bounds__(UT) gfk_win_update(GfkModel m, GfkU
   for (int e = e0 + sub; e < e1; e += 16) xt[(indices[e] - c0) * XS + row] = values[e];
   __syncthreads();
 
+  GFK_STAMP(m, 41);
   // ---- G[v, j] = sum_b xt[v, b] dz[b, j] and the update ----
   const AdamCoef ac = adam_coef(m);
   const bool sh = is_shared(m, w_in);
@@ -242,6 +244,7 @@ extern "C" __global__ void __launch_bounds__(UT) gfk_win_update(GfkModel m, GfkU
       }
     }
   }
+  GFK_STAMP(m, 42);
 }
 
 extern "C" int gfk_launch_win_update(const GfkModel* m, const GfkUpdate* u, hipStream_t s) {

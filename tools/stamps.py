@@ -47,3 +47,6 @@ print("row_bwd cycles:", int(d[9] - d[8]))
 print("post_bwd cycles: stage", int(d[11] - d[10]), "| colsums", int(d[12] - d[11]), "| rest", int(d[13] - d[12]))
 print("post_bwd rest: wg0 extras", int(d[14] - d[12]), "| bn_bwd", int(d[15] - d[14]),
       "| heads", int(d[29] - d[15]), "| hidden", int(d[13] - d[29]))
+print("enc_in cycles: row+weights issue", int(d[5] - d[4]), "| gather+draws", int(d[6] - d[5]),
+      "| input+hidden", int(d[7] - d[6]))
+print("win_update (W_in tile 0) cycles: staging", int(d[41] - d[40]), "| mfma+update", int(d[42] - d[41]))
