@@ -192,9 +192,11 @@ __global__ void __launch_bounds__(LDA_ROW_THREADS) gfk_lda_row_k(GfkModel m) {
 // from the per-row CSR tile table), then the softmax-over-V backward and the
 // BN-over-K backward.  ThLds: theta_d staged in LDS (K up to ~128), else read from L2.
 // dynamic LDS: bn[K*LD] + d[K*LD] + xt[64*XS] (+ thd[B*kt + 64]) + ck[pad4(K)] (+ dth[B*K])
+// x^T tile stride: 2 x odd, so the A-role MFMA reads (16 rows x 2 k per half-wave)
+// hit 32 distinct ds_read_b32 banks
 __host__ __device__ inline int lda_xs(int B) {
-  int s = (B + 3) & ~3;
-  if ((s / 4) % 2 == 0) s += 4;
+  int s = (B + 1) & ~1;
+  if ((s / 2) % 2 == 0) s += 2;
   return s;
 }
 
@@ -204,8 +206,8 @@ __global__ void __launch_bounds__(LDA_THREADS) gfk_lda_beta_bwd_k(GfkModel m) {
   const int K = m.K, V = m.V, tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
   const int B = m.bmax, kt = m.kt, XS = lda_xs(B), nb = *m.ws_nb;
   float* bn = smem;
-  float* d = bn + K * LD;
-  float* xt = d + K * LD;
+  float* d = bn + ((K * LD + 3) & ~3);
+  float* xt = d + ((K * LD + 3) & ~3);      // 16-B aligned: thd / dtl are LDS-DMA destinations
   float* thd = xt + VB * XS;
   float* ckl = thd + (ThLds ? B * kt + 64 : 0);
   float* dtl = ckl + ((K + 3) & ~3);                 // staged d theta_d [B][K] (ThLds)
@@ -303,7 +305,8 @@ extern "C" size_t gfk_lda_row_smem(int K) {
   return sizeof(float) * ((size_t)K * LDA_ROW_WAVES + LDA_ROW_WAVES);
 }
 static size_t lda_bwd_floats(const GfkModel* m, bool th_lds) {
-  size_t n = (size_t)m->K * LD * 2 + (size_t)VB * lda_xs(m->bmax) + (((size_t)m->K + 3) & ~(size_t)3);
+  size_t n = ((((size_t)m->K * LD) + 3) & ~(size_t)3) * 2 + (size_t)VB * lda_xs(m->bmax) +
+             (((size_t)m->K + 3) & ~(size_t)3);
   if (th_lds) n += (size_t)m->bmax * m->kt + 64 + (size_t)m->bmax * m->K + 4;
   return n;
 }

@@ -44,8 +44,17 @@ namespace {
 constexpr int DEC_THREADS = 1024;
 constexpr int VB = 64;
 constexpr int LDB_F = 80;   // fwd beta tile stride: B-role reads (lane -> column) conflict free
-constexpr int LDB_B = 68;   // bwd beta tile stride: transposed B-role reads (lane -> k row)
-constexpr int LDD = 72;     // bwd dlogit stride: used as A (lane -> row) and B (lane -> column)
+// bwd strides, 2 mod 32: the transposed B-role reads of the beta tile (lane -> k row) and
+// the A-role reads of dlogit (lane -> row) put 16 rows x 2 columns of a half-wave on 32
+// distinct ds_read_b32 banks; so do the dense pass's 16 rows x 2 columns of dlogit
+constexpr int LDB_B = 66;
+constexpr int LDD = 66;
+// BN'ed logit tiles (ws_zn) are stored XOR-swizzled: element (row, col) of a tile at
+// row * VB + (col ^ zswz(row)).  The bwd dense pass reads 16 rows x 2 columns per
+// half-wave; unswizzled (stride VB = 64) those 16 rows hit ONE bank (16-way conflict),
+// swizzled they cover 32 distinct banks.  The tile is LDS-DMA'd verbatim, so the
+// swizzle is applied by the writer (prodlda_fwd) and every reader.
+__host__ __device__ __forceinline__ int zswz(int row) { return (row & 15) << 1; }
 constexpr float RL_EPS = 1e-10f;
 
 __host__ __device__ __forceinline__ int round_up(int x, int m) { return (x + m - 1) / m * m; }
@@ -179,7 +188,7 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
     for (int e = 0; e < 4; ++e) {
       const int row = (rt0 + 4 * i) * 16 + (lane >> 4) * 4 + e;
       const float z = (acc[i][e] - mean) * rstd;
-      if (row < nb) zt[row * VB + col] = z;
+      if (row < nb) zt[row * VB + (col ^ zswz(row))] = z;
       const float zv = valid ? z : -INFINITY;
       const float mx = row16_max(zv);
       const float se = row16_sum(valid ? __expf(zv - mx) : 0.f);
@@ -229,7 +238,7 @@ extern "C" __global__ void __launch_bounds__(64) gfk_prodlda_row_loss(GfkModel m
   for (int e = e0 + lane; e < e1; e += 64) {
     const int c = indices[e];
     const float x = values[e];
-    const float z = zn[(size_t)(c / VB) * tstride + (size_t)b * VB + (c % VB)];
+    const float z = zn[(size_t)(c / VB) * tstride + (size_t)b * VB + ((c % VB) ^ zswz(b))];
     const float p = expf(z - lse);
     rl += x * logf(p + RL_EPS);
     S += x * p / (p + RL_EPS);
@@ -316,7 +325,7 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_bwd_kernel(GfkModel m) {
     for (int i = 0, e = xe0 + xsub; e < xe1; ++i, e += TPR) {
       const int c = (i == 0 ? xc0 : m.indices[e]) - c0;
       const float x = i == 0 ? xv0 : m.values[e];
-      const float p = __expf(zt[xrow * VB + c] - l);
+      const float p = __expf(zt[xrow * VB + (c ^ zswz(xrow))] - l);
       dt[xrow * LDD + c] = -x * p / (p + RL_EPS);
     }
   }
@@ -332,7 +341,7 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_bwd_kernel(GfkModel m) {
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
       const int row = dg + 16 * i;
-      z[i] = zt[row * VB + dcol];
+      z[i] = zt[row * VB + (dcol ^ zswz(row))];
       const float p = __expf(z[i] - lse[row]);
       d[i] = (row < nb && valid) ? p * Sb[row] + dt[row * LDD + dcol] : 0.f;
       s1 += d[i];

@@ -30,22 +30,29 @@ namespace {
 constexpr int UT = 1024;
 constexpr int UW = UT / 64;
 __host__ __device__ inline int rup(int x, int m) { return (x + m - 1) / m * m; }
-__host__ __device__ inline int lds_stride(int w) {
-  int s = rup(w, 4);
-  if ((s / 4) % 2 == 0) s += 4;
+// LDS strides for ds_read_b32 MFMA operands (bank = dword % 32 per half-wave):
+// A-role reads (lane & 15 -> row, lane >> 4 -> k) want stride = 2 x odd, so 16 rows x
+// 2 k land on 32 distinct banks; B-role reads (lane >> 4 -> row, lane & 15 -> column)
+// want stride = 16 mod 32, so a half-wave's 2 rows x 16 columns do.
+__host__ __device__ inline int stride_a(int w) {
+  int s = rup(w, 2);
+  if ((s / 2) % 2 == 0) s += 2;
   return s;
+}
+__host__ __device__ inline int stride_b(int w) {   // w: multiple of 16
+  return w % 32 == 16 ? w : w + 16;
 }
 }  // namespace
 
 extern "C" size_t gfk_win_update_smem(const GfkModel* m) {
   const int B = m->bmax, H0P = rup(m->H[0], 16);
-  const size_t a = (size_t)64 * lds_stride(B) + (size_t)B * lds_stride(H0P), b = 2 * (size_t)B * 68;
+  const size_t a = (size_t)64 * stride_a(B) + (size_t)B * stride_b(H0P), b = 2 * (size_t)B * 80;
   return sizeof(float) * (a > b ? a : b);
 }
 
 // Small weight tile job (see GfkWJob).  LDS: dz[B][LDJ] + a[B][LDJ]
 __device__ __forceinline__ void weight_job(const GfkModel& m, const GfkWJob& J, float* smem) {
-  constexpr int LDJ = 68;
+  constexpr int LDJ = 80;            // B-role stride (16 mod 32): conflict-free operand reads
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int B = m.bmax, nb = *m.ws_nb;
   float* dzs = smem;
@@ -146,7 +153,7 @@ __device__ __forceinline__ void vector_job(const GfkModel& m, const GfkVJob& J) 
 }
 
 // grid: n_tiles + n_w + n_v + 1 workgroups of 1024 threads.
-// dynamic LDS: max(W_in tile: xt[64][lds_stride(B)] + dz[B][lds_stride(H0P)], weight job: 2 B 68)
+// dynamic LDS: max(W_in tile: xt[64][stride_a(B)] + dz[B][stride_b(H0P)], weight job: 2 B 80)
 extern "C" __global__ void __launch_bounds__(UT) gfk_win_update(GfkModel m, GfkUpdate U) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   {
@@ -163,7 +170,7 @@ extern "C" __global__ void __launch_bounds__(UT) gfk_win_update(GfkModel m, GfkU
   float* w_in = m.w_in;
   keep(B, H0, V, n_tiles, tstart, indices, nbp, values, dz0, w_in);
   const int H0P = rup(H0, 16);
-  const int XS = lds_stride(B), ZS = lds_stride(H0P);
+  const int XS = stride_a(B), ZS = stride_b(H0P);
   float* xt = smem;
   float* dz = smem + 64 * XS;
   const int tile = blockIdx.x, c0 = tile * 64;

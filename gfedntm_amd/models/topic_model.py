@@ -285,12 +285,18 @@ class TopicModelBase:
     @torch.no_grad()
     def get_doc_topic_distribution(self, dataset, n_samples=20, seed: Optional[int] = None,
                                    chunk: int = 4096):
-        """Mean over ``n_samples`` reparameterised draws of softmax(theta), per doc."""
+        """Mean over ``n_samples`` reparameterised draws of softmax(theta), per doc.
+        Fused engine: one HIP launch per chunk (csrc/infer.hip), encoder evaluated once
+        per document; torch engine: encoder once per chunk, draws from torch."""
         data = self.device_data(dataset)
+        if seed is None:
+            seed = int(torch.initial_seed()) % (2**31)
+        if self.backend == "fused":
+            return self.engine.theta_infer(data, n_samples, seed=seed).cpu().numpy()
         was = self.model.training
         self.model.eval()
         gen = torch.Generator(device=self.device)
-        gen.manual_seed(seed if seed is not None else int(torch.initial_seed()) % (2**31))
+        gen.manual_seed(seed)
         out = []
         for a in range(0, data.n_docs, chunk):
             ids = torch.arange(a, min(a + chunk, data.n_docs), device=self.device)

@@ -84,10 +84,11 @@ UPDATE_GRAD, UPDATE_FUSED = 0, 1
 
 
 def theta_stride(K: int) -> int:
-    """Row stride of the dropped-out theta workspace: K rounded up to 4 x odd, so
-    16 consecutive rows land on distinct LDS bank groups in the decoder MFMAs."""
-    kt = -(-K // 4) * 4
-    return kt + 4 if (kt // 4) % 2 == 0 else kt
+    """Row stride of the dropped-out theta workspace: K rounded up to 2 x odd, so the
+    decoder MFMAs' A-role reads (16 rows x 2 k per half-wave, ds_read_b32: bank =
+    dword % 32) land on 32 distinct banks (B * kt stays a multiple of 4 for LDS-DMA)."""
+    kt = -(-K // 2) * 2
+    return kt + 2 if (kt // 2) % 2 == 0 else kt
 
 
 def _shape_model(tm, bmax: int) -> "abi.GfkModel":
@@ -649,6 +650,57 @@ class FusedEngine(EngineBase):
             torch.sum(c["da"], 0, out=c["gba"])
         else:
             torch.mm(c["xc"].t(), c["dzm"], out=c["gW"])
+
+    # ------------------------------------------------------------------ inference
+    def _ctx_dense(self, data: DeviceCSR, d0: int, d1: int) -> torch.Tensor:
+        """Dense contextual contribution to the input layer for documents [d0, d1):
+        adapt_bert + the contextual half of input_layer (CombinedTM) or the whole
+        input layer (ZeroShotTM) -- library GEMMs, as in the step's CTX_FWD."""
+        c = self._ctx
+        x = data.contextual[d0:d1]
+        if "Wa" in c:
+            return torch.addmm(c["ba"], x, c["Wa"].t()) @ c["Wc"]
+        return x @ c["W"]
+
+    @torch.no_grad()
+    def theta_infer(self, data: DeviceCSR, n_samples: int = 20, seed: int = 0,
+                    postprocess: bool = False, threshold: float = 3e-3, moments: bool = False,
+                    chunk: Optional[int] = None) -> torch.Tensor:
+        """Document-topic distribution of every document of ``data`` (csrc/infer.hip):
+        the mean over ``n_samples`` draws of softmax(mu + eps * sigma) with the encoder
+        in eval mode (running batch-norm statistics, no dropout), evaluated ONCE per
+        document with the draws made in registers (the reference re-runs the encoder
+        for every sample, avitm.py:470-523).  ``postprocess`` fuses the theta
+        threshold + L1 normalisation (federated_model.py:170-173); ``moments`` returns
+        the posterior [D, 2, K] = (mu, log sigma^2) instead.  The draws are keyed by
+        (seed, document index), so the chunking does not change the result."""
+        m, K, n = self._m, int(self._m.K), int(data.n_docs)
+        out = torch.empty(n, 2 * K if moments else K, dtype=torch.float32, device=self.device)
+        if n:
+            ctx = m.input != abi.IN_BOW
+            if ctx and data.contextual is None:
+                raise RuntimeError("CTM inference needs the contextual embeddings")
+            if chunk is None:       # the CombinedTM adapt_bert output is [chunk, V]: <= 1 GiB
+                chunk = (1 << 16) if not ctx else max(256, min(1 << 16, (1 << 28) // max(m.V, 1)))
+            cu = torch.cuda.get_device_properties(self.device).multi_processor_count
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            for d0 in range(0, n, chunk):
+                d1 = min(n, d0 + chunk)
+                hctx = self._ctx_dense(data, d0, d1).contiguous() if ctx else None
+                p = abi.GfkInfer()
+                p.indptr = data.indptr.data_ptr() + 4 * d0
+                p.indices, p.values = data.indices.data_ptr(), data.values.data_ptr()
+                p.hctx = hctx.data_ptr() if hctx is not None else None
+                p.out = out.data_ptr() + 4 * d0 * out.shape[1]
+                p.n_docs, p.n_samples = d1 - d0, int(n_samples)
+                p.flags = (abi.INFER_POSTPROCESS if postprocess else 0) | \
+                    (abi.INFER_MOMENTS if moments else 0)
+                p.thr, p.seed, p.doc0 = float(threshold), int(seed) % (1 << 64), d0
+                p.grid = int(max(1, min(-(-(d1 - d0) // 8), 4 * cu)))   # 8 waves (docs) per WG
+                rc = self.lib.gfk_theta_infer(C.byref(m), C.byref(p), stream)
+                if rc:
+                    raise RuntimeError(f"gfk_theta_infer failed ({rc})")
+        return out.view(n, 2, K) if moments else out
 
     # ------------------------------------------------------------------ step
     def _launch(self, phases):

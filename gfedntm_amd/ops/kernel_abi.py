@@ -124,10 +124,19 @@ class GfkAdam(C.Structure):
     ]
 
 
+class GfkInfer(C.Structure):
+    """theta-inference launch (csrc/infer.hip)."""
+    _fields_ = [("indptr", P), ("indices", P), ("values", P), ("hctx", P), ("out", P),
+                ("n_docs", C.c_int32), ("n_samples", C.c_int32), ("flags", C.c_int32),
+                ("thr", C.c_float), ("seed", C.c_uint64), ("grid", C.c_int32), ("doc0", C.c_int32)]
+
+
+INFER_POSTPROCESS, INFER_MOMENTS = 1, 2
+
 # optional entry points: name -> (argtypes, restype)
 _EXTRA = {
-    "gfk_theta_infer": ([C.POINTER(GfkModel), C.c_void_p, C.c_void_p, C.c_int, C.c_int,
-                         C.c_uint64, C.c_void_p], C.c_int),
+    "gfk_theta_infer": ([C.POINTER(GfkModel), C.POINTER(GfkInfer), C.c_void_p], C.c_int),
+    "gfk_theta_infer_smem": ([C.POINTER(GfkModel)], C.c_size_t),
 }
 
 
@@ -152,6 +161,9 @@ def declare(lib: C.CDLL) -> None:
     lib.gfk_smem_required.restype = C.c_size_t
     lib.gfk_scale.argtypes = [C.c_void_p, C.c_int64, C.c_float, C.c_void_p]
     lib.gfk_scale.restype = C.c_int
+    lib.gfk_infer_struct_size.restype = C.c_size_t
+    if lib.gfk_infer_struct_size() != C.sizeof(GfkInfer):
+        raise RuntimeError("GfkInfer ABI mismatch")
     for name, args in _EXTRA.items():
         if hasattr(lib, name):
             f = getattr(lib, name)
