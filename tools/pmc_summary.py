@@ -24,9 +24,11 @@ def load(dirs):
         for path in glob.glob(os.path.join(d, "*counter_collection.csv")):
             with open(path) as f:
                 for row in csv.DictReader(f):
-                    name = row["Kernel_Name"].split("(")[0]
-                    if name.startswith("void "):
-                        name = name[5:]
+                    name = row["Kernel_Name"]
+                    for pre in ("void ", "(anonymous namespace)::"):
+                        if name.startswith(pre):
+                            name = name[len(pre):]
+                    name = name.split("(")[0]
                     vals[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
     return vals
 
