@@ -29,6 +29,10 @@ import torch
 
 def build_parser() -> argparse.ArgumentParser:
     p = argparse.ArgumentParser(description="gfedntm_amd: federated neural topic models on MI355X")
+    # the reference README's invocation `main.py start_client --id i ...` (README.md:77; the
+    # reference argparse itself has no sub-command): accepted, the role still comes from --id
+    p.add_argument("command", nargs="?", default=None, choices=["start_client", "start_server"],
+                   help="optional role word (reference README syntax)")
     # reference flags
     p.add_argument("--id", type=int, default=0, help="0 = server / coordinator, i >= 1 = client i")
     p.add_argument("--source", type=str, default=None, help="synthetic npz or real parquet")
@@ -200,7 +204,12 @@ def run_collective(args, cfg, argv: List[str]) -> Optional[dict]:
 
 def main(argv: Optional[List[str]] = None):
     argv = list(sys.argv[1:] if argv is None else argv)
-    args = build_parser().parse_args(argv)
+    parser = build_parser()
+    args = parser.parse_args(argv)
+    if args.command == "start_client" and args.id == 0:
+        parser.error("start_client needs --id >= 1 (0 is the server)")
+    if args.command == "start_server" and args.id != 0:
+        parser.error("start_server runs with --id 0")
     from .utils.config import load_config
     cfg = load_config(args.config)
     if args.backend == "local":

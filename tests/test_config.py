@@ -51,3 +51,14 @@ def test_grpc_options():
     assert keys["grpc.max_send_message_length"] == 262144000
     srv = dict(cfg.grpc_server_options())
     assert srv["grpc.keepalive_time_ms"] == 10000 and srv["grpc.http2.max_ping_strikes"] == 0
+
+
+def test_cli_accepts_reference_readme_syntax():
+    """README.md:77 writes `main.py start_client --id <id> ...`; the role word is accepted."""
+    import pytest
+    from gfedntm_amd.cli import build_parser, main
+    a = build_parser().parse_args(["start_client", "--id", "2", "--data_type", "real", "--fos", "x"])
+    assert a.command == "start_client" and a.id == 2
+    assert build_parser().parse_args(["--id", "0"]).command is None
+    with pytest.raises(SystemExit):
+        main(["start_client", "--id", "0"])
