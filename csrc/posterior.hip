@@ -432,7 +432,9 @@ __device__ __forceinline__ void colvec_gemv(const float* W, int ldw, const float
   gemv_cols(n_out, n_in, tid, [&](int k, int j) { return x[k] * W[k * ldw + j]; }, epi);
 }
 
-// grid: bmax workgroups (row = blockIdx.x).
+// grid: bmax + 1 workgroups: row = blockIdx.x < bmax, plus one extra workgroup
+// (the last) for the batch-level work -- prior gradients, the loss, the step
+// counter -- so no row workgroup carries it on the critical path.
 template <bool InLds, bool Staged>
 __global__ void __launch_bounds__(PT) gfk_post_bwd_k(GfkModel m) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -442,6 +444,7 @@ __global__ void __launch_bounds__(PT) gfk_post_bwd_k(GfkModel m) {
   keep(K, B, nh, sflags, dmu_g, dls_g, mu_g, ls_g, nbp);
   const int tid = threadIdx.x, lane = tid & 63;
   const int row = blockIdx.x;
+  const bool extra = row == (int)gridDim.x - 1;
   const PostLds L = post_lds(m);
   const int Hl = m.H[nh - 1];
   constexpr bool staged = Staged;
@@ -455,7 +458,7 @@ __global__ void __launch_bounds__(PT) gfk_post_bwd_k(GfkModel m) {
     glds_copy(smem + L.mu, mu_g, B * K, tid, PT);
     glds_copy(smem + L.ls, ls_g, B * K, tid, PT);
   }
-  {
+  if (!extra) {                         // own row (the extra workgroup has none)
     int o = L.zrow;
 #pragma unroll
     for (int l = 0; l < GFK_MAX_LAYERS; ++l) {
@@ -464,10 +467,10 @@ __global__ void __launch_bounds__(PT) gfk_post_bwd_k(GfkModel m) {
         o += pad4(m.H[l]);
       }
     }
+    glds_copy(smem + L.mask, m.ws_mask_h + (size_t)row * Hl, Hl, tid, PT);
   }
-  glds_copy(smem + L.mask, m.ws_mask_h + (size_t)row * Hl, Hl, tid, PT);
   glds_copy(smem + L.pm, m.prior_mean, K, tid, PT);
-  if (staged) {
+  if (staged && !extra) {
     float* p = smem + L.w;
     glds_copy(p, m.w_mu, K * Hl, tid, PT); p += pad4(K * Hl);
     glds_copy(p, m.w_s, K * Hl, tid, PT); p += pad4(K * Hl);
@@ -480,15 +483,15 @@ __global__ void __launch_bounds__(PT) gfk_post_bwd_k(GfkModel m) {
   float rs[CQ];                         // rstd of those columns
 #pragma unroll
   for (int q = 0; q < CQ; ++q) rs[q] = m.ws_bn_rstd[min(tid + q * PT, 2 * K - 1)];
-  // workgroup 0 extras: the loss terms, priors, NeuralLDA theta_d * d theta_d
+  // extra workgroup: the loss terms, priors, step
   float lterm = 0.f, pmk = 0.f, pvk = 1.f;
   int step0 = 0;
-  if (row == 0) {
+  if (extra) {
     if (tid < nb) lterm = m.kl_weight * m.ws_kl[tid] + m.ws_rl[tid];
     if (tid < K) { pmk = m.prior_mean[tid]; pvk = m.prior_var[tid]; }
     if (tid == 0) step0 = *m.step;
   }
-  if (row >= nb) {
+  if (row >= nb && !extra) {
     vm_barrier();
     return;
   }
@@ -500,46 +503,35 @@ __global__ void __launch_bounds__(PT) gfk_post_bwd_k(GfkModel m) {
   const float* dls = in_lds ? smem + L.dls : dls_g;
   const float* mu = in_lds ? smem + L.mu : mu_g;
   const float* ls = in_lds ? smem + L.ls : ls_g;
-  float* S = smem + L.sums;             // [4][pad4(2K)]: sum dy, sum dy * xh, (wg 0:) sum xh / extra
+  float* S = smem + L.sums;             // [4][pad4(2K)]: sum dy, sum dy * xh | (extra:) priors
   const int P2 = pad4(2 * K);
-  const float* pmean = smem + L.pm;     // prior mean, staged
-  for (int cb = 0; cb < 2 * K; cb += PT / 4) {
-    const int c2 = cb + (tid >> 2), g = tid & 3;
-    const bool valid = c2 < 2 * K;
-    const int k = c2 < K ? c2 : c2 - K;
-    const float* dy = c2 < K ? dmu : dls;
-    const float* xh = c2 < K ? mu : ls;
-    const float pm = pmean[k];
-    float s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f;
-    if (valid)
+  const float inv_nb = 1.f / (float)nb;
+  if (extra) {
+    // ---- extra workgroup: prior gradients (-> grad slots), loss, step ----
+    const float* pmean = smem + L.pm;   // prior mean, staged
+    for (int cb = 0; cb < 2 * K; cb += PT / 4) {
+      const int c2 = cb + (tid >> 2), g = tid & 3;
+      const bool valid = c2 < 2 * K;
+      const int k = c2 < K ? c2 : c2 - K;
+      const float* xh = c2 < K ? mu : ls;
+      const float pm = pmean[k];
+      float s3 = 0.f, s4 = 0.f;         // sum mu | sum exp(ls), sum (pm - mu)^2
+      if (valid)
 #pragma unroll 4
-      for (int r = g; r < nb; r += 4) {
-        const float d = dy[r * K + k], x = xh[r * K + k];
-        s1 += d;
-        s2 += d * x;
-        if (row == 0) {                 // priors: sum mu | sum exp(ls), sum (pm - mu)^2
+        for (int r = g; r < nb; r += 4) {
+          const float x = xh[r * K + k];
           s3 += c2 < K ? x : expf(x);
           const float dm = pm - x;
           s4 += c2 < K ? dm * dm : 0.f;
         }
+      s3 = quad_sum(s3);
+      s4 = quad_sum(s4);
+      if (valid && g == 0) {
+        S[2 * P2 + c2] = s3;
+        S[3 * P2 + c2] = s4;
       }
-    s1 = quad_sum(s1);
-    s2 = quad_sum(s2);
-    s3 = quad_sum(s3);
-    s4 = quad_sum(s4);
-    if (valid && g == 0) {
-      S[c2] = s1;
-      S[P2 + c2] = s2;
-      S[2 * P2 + c2] = s3;
-      S[3 * P2 + c2] = s4;
     }
-  }
-  lds_barrier();
-  GFK_STAMP(m, 12);
-
-  // ---- workgroup 0: prior gradients (-> grad slots), loss, step ----
-  const float inv_nb = 1.f / (float)nb;
-  if (row == 0) {
+    lds_barrier();
     const float wk = m.kl_weight;
     if (tid < K && m.learn_priors) {
       const float sdm2 = S[3 * P2 + tid];                 // sum_b (pm - mu_b)^2
@@ -548,12 +540,36 @@ __global__ void __launch_bounds__(PT) gfk_post_bwd_k(GfkModel m) {
       m.prior_var[tid + m.off_g] =
           wk * 0.5f * ((float)nb / pvk - svar / (pvk * pvk) - sdm2 / (pvk * pvk));
     }
-    const float l = block_sum_wave0(lterm, smem + L.v1);   // (v1 is free until the hidden layers)
+    const float l = block_sum_wave0(lterm, smem + L.v1);
     if (tid == 0) {
       m.loss_hist[step0] = l;
       *m.step = step0 + 1;
     }
+    return;
   }
+  for (int cb = 0; cb < 2 * K; cb += PT / 4) {
+    const int c2 = cb + (tid >> 2), g = tid & 3;
+    const bool valid = c2 < 2 * K;
+    const int k = c2 < K ? c2 : c2 - K;
+    const float* dy = c2 < K ? dmu : dls;
+    const float* xh = c2 < K ? mu : ls;
+    float s1 = 0.f, s2 = 0.f;
+    if (valid)
+#pragma unroll 4
+      for (int r = g; r < nb; r += 4) {
+        const float d = dy[r * K + k], x = xh[r * K + k];
+        s1 += d;
+        s2 += d * x;
+      }
+    s1 = quad_sum(s1);
+    s2 = quad_sum(s2);
+    if (valid && g == 0) {
+      S[c2] = s1;
+      S[P2 + c2] = s2;
+    }
+  }
+  lds_barrier();
+  GFK_STAMP(m, 12);
   GFK_STAMP(m, 14);
 
   // ---- own row: BN backward -> d mu_raw | d ls_raw ----
@@ -660,7 +676,7 @@ extern "C" int gfk_launch_post_bwd(const GfkModel* m, hipStream_t s) {
   else hipLaunchKernelGGL(gfk_row_bwd_k<4>, g, t, sm, s, *m);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  const dim3 gb(m->bmax), tb(PT);
+  const dim3 gb(m->bmax + 1), tb(PT);     // + the prior / loss / step workgroup
   const size_t sb = gfk_post_bwd_smem(m);
   const bool st = m->stage_flags & 1;
   if (batch_in_lds(*m)) {
