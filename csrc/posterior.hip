@@ -29,7 +29,9 @@
 using namespace gfk;
 
 namespace {
-constexpr int PT = 256;                 // threads per workgroup
+constexpr int PT = 256;                 // threads per workgroup (row_bwd)
+constexpr int FT = 1024;                // threads per workgroup (post_fwd, post_bwd): 16 lanes
+                                        // per batch column in the column reductions
 __host__ __device__ inline int pad4(int x) { return (x + 3) & ~3; }
 
 // Sum over the 4 lanes of a DPP quad (xor 1, xor 2); result in every lane.
@@ -70,9 +72,10 @@ extern "C" size_t gfk_post_fwd_smem(const GfkModel* m) {
   return sizeof(float) * (mats + 4 * (size_t)pad4(m->K));
 }
 
-// Column statistics of the raw heads (4 threads per column, RPT = rows per thread
-// held in registers across the mean and variance passes); workgroup 0 also
-// advances the running statistics (prefetched rmp / rvp, one per pass).
+// Column statistics of the raw heads (16 lanes -- one DPP row -- per column, RPT =
+// rows per lane held in registers across the mean and variance passes, 64 columns
+// per pass); workgroup 0 also advances the running statistics (prefetched rmp /
+// rvp, one per pass).
 template <int RPT>
 __device__ __forceinline__ void post_colstats(const GfkModel& m, const float* mr, const float* lr,
                                               float* cmean, float* crstd, const float (&rmp)[8],
@@ -82,28 +85,28 @@ __device__ __forceinline__ void post_colstats(const GfkModel& m, const float* mr
   const int K = m.K;
 #pragma unroll
   for (int pass = 0; pass < CP; ++pass) {
-    const int cb = pass * (PT / 4);
+    const int cb = pass * (FT / 16);
     if (cb >= 2 * K) break;
-    const int c2 = cb + (tid >> 2), g = tid & 3;
+    const int c2 = cb + (tid >> 4), g = tid & 15;
     const bool valid = c2 < 2 * K;
     const float* x = (c2 < K ? mr + c2 : lr + (c2 - K));
     float xv[RPT];
 #pragma unroll
     for (int i = 0; i < RPT; ++i) {
-      const int r = g + 4 * i;
+      const int r = g + 16 * i;
       xv[i] = (valid && r < nb) ? x[r * K] : 0.f;
     }
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < RPT; ++i) s += xv[i];
-    const float mean = quad_sum(s) * inv_nb;
+    const float mean = row16_sum(s) * inv_nb;
     float q = 0.f;
 #pragma unroll
     for (int i = 0; i < RPT; ++i) {
-      const float d = g + 4 * i < nb ? xv[i] - mean : 0.f;
+      const float d = g + 16 * i < nb ? xv[i] - mean : 0.f;
       q += d * d;
     }
-    const float var = quad_sum(q) * inv_nb;
+    const float var = row16_sum(q) * inv_nb;
     const float rstd = rsqrtf(var + m.bn_eps);
     if (valid && g == 0) {
       cmean[c2] = mean;
@@ -130,7 +133,7 @@ __device__ __forceinline__ void post_colstats(const GfkModel& m, const float* mr
 // InLds: the batch matrices are staged in LDS (compile-time, so every access is a
 // ds_read; a runtime select of the pointer would turn them into flat loads).
 template <bool InLds>
-__global__ void __launch_bounds__(PT) gfk_post_fwd_k(GfkModel m) {
+__global__ void __launch_bounds__(FT) gfk_post_fwd_k(GfkModel m) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   int K = m.K, B = m.bmax;
   const float *mu_raw = m.ws_mu_raw, *ls_raw = m.ws_ls_raw;
@@ -147,8 +150,8 @@ __global__ void __launch_bounds__(PT) gfk_post_fwd_k(GfkModel m) {
 
   // ---- one round: the raw heads of every row (LDS-DMA) + the own row + stats ----
   if (in_lds) {
-    glds_copy(smem, mu_raw, B * K, tid, PT);
-    glds_copy(smem + B * K, ls_raw, B * K, tid, PT);
+    glds_copy(smem, mu_raw, B * K, tid, FT);
+    glds_copy(smem + B * K, ls_raw, B * K, tid, FT);
   }
   const int nb = *nbp;
   constexpr int KQ = 4;                    // K <= 256
@@ -180,8 +183,8 @@ __global__ void __launch_bounds__(PT) gfk_post_fwd_k(GfkModel m) {
 #pragma unroll
   for (int q = 0; q < CP; ++q) {
     rmp[q] = rvp[q] = 0.f;
-    if (row == 0 && q * (PT / 4) < 2 * K) {
-      const int c2 = min(q * (PT / 4) + (tid >> 2), 2 * K - 1);
+    if (row == 0 && q * (FT / 16) < 2 * K) {
+      const int c2 = min(q * (FT / 16) + (tid >> 4), 2 * K - 1);
       rmp[q] = c2 < K ? m.mu_rm[c2] : m.s_rm[c2 - K];
       rvp[q] = c2 < K ? m.mu_rv[c2] : m.s_rv[c2 - K];
     }
@@ -209,8 +212,8 @@ __global__ void __launch_bounds__(PT) gfk_post_fwd_k(GfkModel m) {
   // ---- column statistics over the batch: 4 threads per column, the column's
   // values held in registers across the mean and variance passes ----
   const float inv_nb = 1.f / (float)nb;
-  if (B <= 64) post_colstats<16>(m, mr, lr, cmean, crstd, rmp, rvp, nb, inv_nb, row, tid);
-  else post_colstats<32>(m, mr, lr, cmean, crstd, rmp, rvp, nb, inv_nb, row, tid);
+  if (B <= 64) post_colstats<4>(m, mr, lr, cmean, crstd, rmp, rvp, nb, inv_nb, row, tid);
+  else post_colstats<8>(m, mr, lr, cmean, crstd, rmp, rvp, nb, inv_nb, row, tid);
   if (row == 0 && tid == 0) {
     *m.nbt_mu = nbt0 + 1;
     *m.nbt_s = nbt1 + 1;
@@ -364,7 +367,7 @@ __global__ void __launch_bounds__(PT) gfk_row_bwd_k(GfkModel m) {
 // LDS plan (floats): dmu, dls, mu, ls [B][K] + s1..s4 [2K] + own-row vectors
 // (dmr|dlr [2K], dz ping-pong [2][hmax], z rows, mask) + staged weights.
 struct PostLds {
-  int dmu, dls, mu, ls, sums, pm, dr, v0, v1, zrow, mask, w, total;
+  int dmu, dls, mu, ls, sums, pm, dr, v0, v1, zrow, mask, red, w, total;
 };
 
 __host__ __device__ inline PostLds post_lds(const GfkModel& m) {
@@ -386,6 +389,7 @@ __host__ __device__ inline PostLds post_lds(const GfkModel& m) {
   for (int l = 0; l < GFK_MAX_LAYERS; ++l)
     if (l < m.n_hidden) o += pad4(m.H[l]);
   L.mask = o; o += pad4(m.H[m.n_hidden - 1]);
+  L.red = o; o += FT / 64;                // block_sum_wave0 scratch, one float per wave
   L.w = o;
   if (m.stage_flags & 1) o += post_weight_floats(m);
   L.total = o;
@@ -400,7 +404,7 @@ extern "C" size_t gfk_post_bwd_smem(const GfkModel* m) { return sizeof(float) * 
 template <int LPO, class Term, class Epi>
 __device__ __forceinline__ void gemv_lanes(int n_out, int n_in, int tid, Term term, Epi epi) {
   const int s = tid & (LPO - 1);
-  for (int j0 = 0; j0 < n_out; j0 += PT / LPO) {
+  for (int j0 = 0; j0 < n_out; j0 += FT / LPO) {
     const int j = j0 + tid / LPO;
     float acc = 0.f;
     if (j < n_out) {
@@ -421,7 +425,7 @@ __device__ __forceinline__ void gemv_lanes(int n_out, int n_in, int tid, Term te
 
 template <class Term, class Epi>
 __device__ __forceinline__ void gemv_cols(int n_out, int n_in, int tid, Term term, Epi epi) {
-  if (n_out * 16 <= PT) gemv_lanes<16>(n_out, n_in, tid, term, epi);
+  if (n_out * 16 <= FT) gemv_lanes<16>(n_out, n_in, tid, term, epi);
   else gemv_lanes<4>(n_out, n_in, tid, term, epi);
 }
 
@@ -436,7 +440,7 @@ __device__ __forceinline__ void colvec_gemv(const float* W, int ldw, const float
 // (the last) for the batch-level work -- prior gradients, the loss, the step
 // counter -- so no row workgroup carries it on the critical path.
 template <bool InLds, bool Staged>
-__global__ void __launch_bounds__(PT) gfk_post_bwd_k(GfkModel m) {
+__global__ void __launch_bounds__(FT) gfk_post_bwd_k(GfkModel m) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   int K = m.K, B = m.bmax, nh = m.n_hidden, sflags = m.stage_flags;
   const float *dmu_g = m.ws_dmu, *dls_g = m.ws_dls, *mu_g = m.ws_mu, *ls_g = m.ws_ls;
@@ -453,36 +457,36 @@ __global__ void __launch_bounds__(PT) gfk_post_bwd_k(GfkModel m) {
   constexpr bool in_lds = InLds;
   // ---- one round: the four [B][K] matrices, the own row, the weights, stats ----
   if (in_lds) {
-    glds_copy(smem + L.dmu, dmu_g, B * K, tid, PT);
-    glds_copy(smem + L.dls, dls_g, B * K, tid, PT);
-    glds_copy(smem + L.mu, mu_g, B * K, tid, PT);
-    glds_copy(smem + L.ls, ls_g, B * K, tid, PT);
+    glds_copy(smem + L.dmu, dmu_g, B * K, tid, FT);
+    glds_copy(smem + L.dls, dls_g, B * K, tid, FT);
+    glds_copy(smem + L.mu, mu_g, B * K, tid, FT);
+    glds_copy(smem + L.ls, ls_g, B * K, tid, FT);
   }
   if (!extra) {                         // own row (the extra workgroup has none)
     int o = L.zrow;
 #pragma unroll
     for (int l = 0; l < GFK_MAX_LAYERS; ++l) {
       if (l < nh) {
-        glds_copy(smem + o, m.ws_z[l] + (size_t)row * m.H[l], m.H[l], tid, PT);
+        glds_copy(smem + o, m.ws_z[l] + (size_t)row * m.H[l], m.H[l], tid, FT);
         o += pad4(m.H[l]);
       }
     }
-    glds_copy(smem + L.mask, m.ws_mask_h + (size_t)row * Hl, Hl, tid, PT);
+    glds_copy(smem + L.mask, m.ws_mask_h + (size_t)row * Hl, Hl, tid, FT);
   }
-  glds_copy(smem + L.pm, m.prior_mean, K, tid, PT);
+  glds_copy(smem + L.pm, m.prior_mean, K, tid, FT);
   if (staged && !extra) {
     float* p = smem + L.w;
-    glds_copy(p, m.w_mu, K * Hl, tid, PT); p += pad4(K * Hl);
-    glds_copy(p, m.w_s, K * Hl, tid, PT); p += pad4(K * Hl);
+    glds_copy(p, m.w_mu, K * Hl, tid, FT); p += pad4(K * Hl);
+    glds_copy(p, m.w_s, K * Hl, tid, FT); p += pad4(K * Hl);
 #pragma unroll
     for (int l = 0; l + 1 < GFK_MAX_LAYERS; ++l)
-      if (l + 1 < nh) { glds_copy(p, m.w_h[l], m.H[l + 1] * m.H[l], tid, PT); p += pad4(m.H[l + 1] * m.H[l]); }
+      if (l + 1 < nh) { glds_copy(p, m.w_h[l], m.H[l + 1] * m.H[l], tid, FT); p += pad4(m.H[l + 1] * m.H[l]); }
   }
   const int nb = *nbp;
-  constexpr int CQ = 2;                 // columns tid, tid + PT of the 2K (K <= 256)
+  constexpr int CQ = (512 + FT - 1) / FT;   // columns tid, tid + FT, ... of the 2K (K <= 256)
   float rs[CQ];                         // rstd of those columns
 #pragma unroll
-  for (int q = 0; q < CQ; ++q) rs[q] = m.ws_bn_rstd[min(tid + q * PT, 2 * K - 1)];
+  for (int q = 0; q < CQ; ++q) rs[q] = m.ws_bn_rstd[min(tid + q * FT, 2 * K - 1)];
   // extra workgroup: the loss terms, priors, step
   float lterm = 0.f, pmk = 0.f, pvk = 1.f;
   int step0 = 0;
@@ -509,8 +513,8 @@ __global__ void __launch_bounds__(PT) gfk_post_bwd_k(GfkModel m) {
   if (extra) {
     // ---- extra workgroup: prior gradients (-> grad slots), loss, step ----
     const float* pmean = smem + L.pm;   // prior mean, staged
-    for (int cb = 0; cb < 2 * K; cb += PT / 4) {
-      const int c2 = cb + (tid >> 2), g = tid & 3;
+    for (int cb = 0; cb < 2 * K; cb += FT / 16) {
+      const int c2 = cb + (tid >> 4), g = tid & 15;
       const bool valid = c2 < 2 * K;
       const int k = c2 < K ? c2 : c2 - K;
       const float* xh = c2 < K ? mu : ls;
@@ -518,14 +522,14 @@ __global__ void __launch_bounds__(PT) gfk_post_bwd_k(GfkModel m) {
       float s3 = 0.f, s4 = 0.f;         // sum mu | sum exp(ls), sum (pm - mu)^2
       if (valid)
 #pragma unroll 4
-        for (int r = g; r < nb; r += 4) {
+        for (int r = g; r < nb; r += 16) {
           const float x = xh[r * K + k];
           s3 += c2 < K ? x : expf(x);
           const float dm = pm - x;
           s4 += c2 < K ? dm * dm : 0.f;
         }
-      s3 = quad_sum(s3);
-      s4 = quad_sum(s4);
+      s3 = row16_sum(s3);
+      s4 = row16_sum(s4);
       if (valid && g == 0) {
         S[2 * P2 + c2] = s3;
         S[3 * P2 + c2] = s4;
@@ -540,15 +544,15 @@ __global__ void __launch_bounds__(PT) gfk_post_bwd_k(GfkModel m) {
       m.prior_var[tid + m.off_g] =
           wk * 0.5f * ((float)nb / pvk - svar / (pvk * pvk) - sdm2 / (pvk * pvk));
     }
-    const float l = block_sum_wave0(lterm, smem + L.v1);
+    const float l = block_sum_wave0(lterm, smem + L.red);
     if (tid == 0) {
       m.loss_hist[step0] = l;
       *m.step = step0 + 1;
     }
     return;
   }
-  for (int cb = 0; cb < 2 * K; cb += PT / 4) {
-    const int c2 = cb + (tid >> 2), g = tid & 3;
+  for (int cb = 0; cb < 2 * K; cb += FT / 16) {
+    const int c2 = cb + (tid >> 4), g = tid & 15;
     const bool valid = c2 < 2 * K;
     const int k = c2 < K ? c2 : c2 - K;
     const float* dy = c2 < K ? dmu : dls;
@@ -556,13 +560,13 @@ __global__ void __launch_bounds__(PT) gfk_post_bwd_k(GfkModel m) {
     float s1 = 0.f, s2 = 0.f;
     if (valid)
 #pragma unroll 4
-      for (int r = g; r < nb; r += 4) {
+      for (int r = g; r < nb; r += 16) {
         const float d = dy[r * K + k], x = xh[r * K + k];
         s1 += d;
         s2 += d * x;
       }
-    s1 = quad_sum(s1);
-    s2 = quad_sum(s2);
+    s1 = row16_sum(s1);
+    s2 = row16_sum(s2);
     if (valid && g == 0) {
       S[c2] = s1;
       S[P2 + c2] = s2;
@@ -576,7 +580,7 @@ __global__ void __launch_bounds__(PT) gfk_post_bwd_k(GfkModel m) {
   float* dr = smem + L.dr;              // [2K]: dmr then dlr
 #pragma unroll
   for (int q = 0; q < CQ; ++q) {
-    const int c2 = tid + q * PT;
+    const int c2 = tid + q * FT;
     if (c2 < 2 * K) {
       const int k = c2 < K ? c2 : c2 - K;
       const float* dy = c2 < K ? dmu : dls;
@@ -660,9 +664,9 @@ extern "C" __global__ void gfk_batch_docs(GfkModel m) {
 // ---------------------------------------------------------------------------
 extern "C" int gfk_launch_post_fwd(const GfkModel* m, hipStream_t s) {
   if (batch_in_lds(*m))
-    hipLaunchKernelGGL(gfk_post_fwd_k<true>, dim3(m->bmax), dim3(PT), gfk_post_fwd_smem(m), s, *m);
+    hipLaunchKernelGGL(gfk_post_fwd_k<true>, dim3(m->bmax), dim3(FT), gfk_post_fwd_smem(m), s, *m);
   else
-    hipLaunchKernelGGL(gfk_post_fwd_k<false>, dim3(m->bmax), dim3(PT), gfk_post_fwd_smem(m), s, *m);
+    hipLaunchKernelGGL(gfk_post_fwd_k<false>, dim3(m->bmax), dim3(FT), gfk_post_fwd_smem(m), s, *m);
   return (int)hipGetLastError();
 }
 
@@ -676,7 +680,7 @@ extern "C" int gfk_launch_post_bwd(const GfkModel* m, hipStream_t s) {
   else hipLaunchKernelGGL(gfk_row_bwd_k<4>, g, t, sm, s, *m);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  const dim3 gb(m->bmax + 1), tb(PT);     // + the prior / loss / step workgroup
+  const dim3 gb(m->bmax + 1), tb(FT);     // + the prior / loss / step workgroup
   const size_t sb = gfk_post_bwd_smem(m);
   const bool st = m->stage_flags & 1;
   if (batch_in_lds(*m)) {
