@@ -61,8 +61,10 @@ extern "C" __global__ void __launch_bounds__(LDA_THREADS) gfk_lda_beta_fwd(GfkMo
         const int v = c0 + c;
         const float mom = m.bn_momentum;
         const float unb = K > 1 ? var * (float)K / (float)(K - 1) : var;
-        m.beta_rm[v] = (1.f - mom) * m.beta_rm[v] + mom * mean;
-        m.beta_rv[v] = (1.f - mom) * m.beta_rv[v] + mom * unb;
+        float nm = (1.f - mom) * m.beta_rm[v] + mom * mean, nv = (1.f - mom) * m.beta_rv[v] + mom * unb;
+        if (m.fed_scale_on && is_shared(m, m.beta_rm)) { nm *= m.fed_scale; nv *= m.fed_scale; }
+        m.beta_rm[v] = nm;
+        m.beta_rv[v] = nv;
         m.ws_col_rstd[v] = rstd;
       }
     }
@@ -200,8 +202,18 @@ __host__ __device__ inline int lda_xs(int B) {
   return s;
 }
 
+// 16 waves; one vocab tile per workgroup per iteration.  Every global read of the
+// iteration is issued in ONE round before the first barrier: theta_d, d theta_d and
+// the tile's BN'ed beta^T rows [64][K] (LDS-DMA; the tile lands in d's storage and is
+// transposed LDS -> LDS), the rows' CSR extents in the tile, and the Adam state of the
+// outputs this thread updates (fused mode).  Second round: the tile's per-non-zero
+// coefficients (ws_dbsm).  Then c_k, the x^T theta_d MFMA, the BN backward over the
+// topics and the update, all out of LDS.
+constexpr int LBT = 1024;
+constexpr int LBW = LBT / 64;
+
 template <bool ThLds>
-__global__ void __launch_bounds__(LDA_THREADS) gfk_lda_beta_bwd_k(GfkModel m) {
+__global__ void __launch_bounds__(LBT) gfk_lda_beta_bwd_k(GfkModel m) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int K = m.K, V = m.V, tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
   const int B = m.bmax, kt = m.kt, XS = lda_xs(B), nb = *m.ws_nb;
@@ -211,52 +223,79 @@ __global__ void __launch_bounds__(LDA_THREADS) gfk_lda_beta_bwd_k(GfkModel m) {
   float* thd = xt + VB * XS;
   float* ckl = thd + (ThLds ? B * kt + 64 : 0);
   float* dtl = ckl + ((K + 3) & ~3);                 // staged d theta_d [B][K] (ThLds)
+  float* lsl = dtl + (ThLds ? ((B * K + 3) & ~3) : 0);   // per-topic log-sum-exp [K]
   if (ThLds) {                                        // LDS-DMA: theta_d and d theta_d
-    glds_copy(thd, m.ws_thetad, B * kt, tid, LDA_THREADS);
-    glds_copy(dtl, m.ws_dtheta, B * K, tid, LDA_THREADS);
-    for (int i = tid; i < 64; i += LDA_THREADS) thd[B * kt + i] = 0.f;
-    vm_barrier();
+    glds_copy(thd, m.ws_thetad, B * kt, tid, LBT);
+    glds_copy(dtl, m.ws_dtheta, B * K, tid, LBT);
+    for (int i = tid; i < 64; i += LBT) thd[B * kt + i] = 0.f;
   }
+  glds_copy(lsl, m.ws_lse, K, tid, LBT);
   const float* thv = ThLds ? thd : m.ws_thetad;
   const float* dtv = ThLds ? dtl : m.ws_dtheta;
-  // c_k = sum_b theta_d[b, k] d theta_d[b, k] (softmax-over-V backward), 4 threads per topic
-  for (int k0 = 0; k0 < K; k0 += LDA_THREADS / 4) {
-    const int k = k0 + (tid >> 2), sub = tid & 3;
-    float s = 0.f;
-    if (k < K)
-#pragma unroll 4
-      for (int r = sub; r < nb; r += 4) s += thv[r * kt + k] * dtv[r * K + k];
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
-    if (sub == 0 && k < K) ckl[k] = s;
-  }
   const int NT = (K + 15) / 16;
+  const bool fused = m.update_mode == 1;
+  constexpr int PU = 4;                               // prefetched updates per thread (K <= 64)
+  const int n_upd = (K * VB + LBT - 1) / LBT;
   for (int tile = blockIdx.x; tile < m.n_tiles; tile += gridDim.x) {
-    const int c0 = tile * VB;
+    const int c0 = tile * VB, nv = min(VB, V - c0);
     __syncthreads();
-    for (int i = tid; i < VB * XS; i += LDA_THREADS) xt[i] = 0.f;
-    for (int i = tid; i < K * VB; i += LDA_THREADS) {
-      const int c = i / K, k = i % K;
-      float z = 0.f, bs = 0.f;
-      if (c0 + c < V) {
-        z = m.ws_zn[(size_t)(c0 + c) * K + k];
-        bs = __expf(z - m.ws_lse[k]);
-      }
-      bn[k * LD + c] = z;
-      d[k * LD + c] = bs;
+    // ---- round 1 ----
+    glds_copy(d, m.ws_zn + (size_t)c0 * K, nv * K, tid, LBT);
+    const int xrow = tid >> 4, xsub = tid & 15;       // 16 threads per batch row
+    int es = 0, ee = 0;
+    if (xrow < nb && xrow < B) {
+      const int32_t* ts = m.ws_tstart + (size_t)xrow * (m.n_tiles + 1) + tile;
+      es = ts[0];
+      ee = ts[1];
     }
-    __syncthreads();
-    {  // the tile's non-zero coefficients: 4 threads per batch row
-      const int row = tid >> 2, sub = tid & 3;
-      if (row < nb && row < B) {
-        const int32_t* ts = m.ws_tstart + (size_t)row * (m.n_tiles + 1) + tile;
-        const int es = ts[0], ee = ts[1];
-        for (int e = es + sub; e < ee; e += 4) xt[(m.indices[e] - c0) * XS + row] = m.ws_dbsm[e];
+    float pp[PU], pm[PU], pv[PU];
+#pragma unroll
+    for (int u = 0; u < PU; ++u) {
+      pp[u] = pm[u] = pv[u] = 0.f;
+      const int i = tid + LBT * u, k = i / VB, c = i % VB;
+      if (fused && u < n_upd && k < K && c < nv) {
+        const float* p = m.beta + (size_t)k * V + c0 + c;
+        pp[u] = *p;
+        pm[u] = p[m.off_m];
+        pv[u] = p[m.off_v];
       }
     }
-    __syncthreads();
-    // G[c][k] = sum_b xt[c][b] theta_d[b][k]; then d <- bs * (G - c_k)
-    for (int t = wave; t < 4 * NT; t += LDA_THREADS / 64) {
+    for (int i = tid; i < VB * XS; i += LBT) xt[i] = 0.f;
+    vm_barrier();
+    // ---- round 2: the tile's non-zero coefficients g = -x / (wd + eps) -> x^T tile ----
+    for (int e = es + xsub; e < ee; e += 16) xt[(m.indices[e] - c0) * XS + xrow] = m.ws_dbsm[e];
+    // c_k = sum_b theta_d[b, k] d theta_d[b, k] (softmax-over-V backward), 16 lanes per topic
+    if (tile == (int)blockIdx.x) {
+      for (int k0 = 0; k0 < K; k0 += LBT / 16) {
+        const int k = k0 + (tid >> 4), sub = tid & 15;
+        float s = 0.f;
+        if (k < K)
+          for (int r = sub; r < nb; r += 16) s += thv[r * kt + k] * dtv[r * K + k];
+        s = row16_sum(s);
+        if (sub == 0 && k < K) ckl[k] = s;
+      }
+    }
+    // the BN'ed beta^T rows (in d's storage) -> bn [K][LD]
+    float zr[(VB * 256 + LBT - 1) / LBT];             // K <= 256
+    {
+      int u = 0;
+      for (int i = tid; i < K * VB; i += LBT, ++u) {
+        const int c = i / K, k = i % K;
+        zr[u] = c < nv ? d[c * K + k] : 0.f;
+      }
+    }
+    lds_barrier();
+    {
+      int u = 0;
+      for (int i = tid; i < K * VB; i += LBT, ++u) {
+        const int c = i / K, k = i % K;
+        bn[k * LD + c] = zr[u];
+        d[k * LD + c] = c < nv ? __expf(zr[u] - lsl[k]) : 0.f;   // beta_sm
+      }
+    }
+    lds_barrier();
+    // G[c][k] = sum_b xt[c][b] theta_d[b][k]; then d <- beta_sm * (G - c_k)
+    for (int t = wave; t < 4 * NT; t += LBW) {
       const int i0 = (t / NT) * 16, j0 = (t % NT) * 16;
       const float* ap = xt + (i0 + (lane & 15)) * XS + (lane >> 4);
       const float* bp = thv + (lane >> 4) * kt + j0 + (lane & 15);
@@ -272,30 +311,50 @@ __global__ void __launch_bounds__(LDA_THREADS) gfk_lda_beta_bwd_k(GfkModel m) {
         }
       }
     }
-    __syncthreads();
-    {
-      const int c = tid >> 2, sub = tid & 3;
+    lds_barrier();
+    {  // BN backward over the K topics of each column: 16 lanes per column
+      const int c = tid >> 4, sub = tid & 15;
       float s1 = 0.f, s2 = 0.f;
-      for (int k = sub; k < K; k += 4) {
+      for (int k = sub; k < K; k += 16) {
         const float g = d[k * LD + c];
         s1 += g;
         s2 += g * bn[k * LD + c];
       }
-      s1 += __shfl_xor(s1, 1, 64); s1 += __shfl_xor(s1, 2, 64);
-      s2 += __shfl_xor(s2, 1, 64); s2 += __shfl_xor(s2, 2, 64);
+      s1 = row16_sum(s1);
+      s2 = row16_sum(s2);
       const float inv = 1.f / (float)K;
-      if (c0 + c < V) {
+      if (c < nv) {
         const float rstd = m.ws_col_rstd[c0 + c];
-        for (int k = sub; k < K; k += 4) {
+        for (int k = sub; k < K; k += 16) {
           const int i = k * LD + c;
           d[i] = rstd * (d[i] - s1 * inv - bn[i] * s2 * inv);
         }
       }
     }
-    __syncthreads();
-    for (int i = tid; i < K * VB; i += LDA_THREADS) {
-      const int k = i / VB, c = i % VB;
-      if (c0 + c < V) m.g_beta[(size_t)k * V + c0 + c] = d[k * LD + c];
+    lds_barrier();
+    // gradient (gradient mode) or Adam + FedAvg pre-scale in place (fused mode)
+    const AdamCoef ac = adam_coef(m);
+    const bool sh = is_shared(m, m.beta);
+    {
+      int u = 0;
+      for (int i = tid; i < K * VB; i += LBT, ++u) {
+        const int k = i / VB, c = i % VB;
+        if (c >= nv) continue;
+        float* p = m.beta + (size_t)k * V + c0 + c;
+        const float g = d[k * LD + c];
+        if (!fused) {
+          p[m.off_g] = g;
+        } else if (u < PU) {
+          float mo = pm[u], vo = pv[u];
+          float np = adam_update(pp[u], g, mo, vo, ac);
+          if (sh && m.fed_scale_on) np *= m.fed_scale;
+          p[m.off_m] = mo;
+          p[m.off_v] = vo;
+          *p = np;
+        } else {
+          param_update(m, p, g, ac, sh);
+        }
+      }
     }
   }
 }
@@ -307,8 +366,8 @@ extern "C" size_t gfk_lda_row_smem(int K) {
 static size_t lda_bwd_floats(const GfkModel* m, bool th_lds) {
   size_t n = ((((size_t)m->K * LD) + 3) & ~(size_t)3) * 2 + (size_t)VB * lda_xs(m->bmax) +
              (((size_t)m->K + 3) & ~(size_t)3);
-  if (th_lds) n += (size_t)m->bmax * m->kt + 64 + (size_t)m->bmax * m->K + 4;
-  return n;
+  if (th_lds) n += (size_t)m->bmax * m->kt + 64 + (((size_t)m->bmax * m->K + 3) & ~(size_t)3);
+  return n + (((size_t)m->K + 3) & ~(size_t)3);     // per-topic log-sum-exp
 }
 static bool lda_bwd_th_lds(const GfkModel* m) { return sizeof(float) * lda_bwd_floats(m, true) <= 160 * 1024; }
 extern "C" size_t gfk_lda_bwd_smem(const GfkModel* m) {
@@ -333,7 +392,7 @@ extern "C" int gfk_launch_lda_row(const GfkModel* m, hipStream_t s) {
 }
 
 extern "C" int gfk_launch_lda_beta_bwd(const GfkModel* m, hipStream_t s) {
-  const dim3 g(m->dec_grid), t(LDA_THREADS);
+  const dim3 g(m->dec_grid), t(LBT);
   if (lda_bwd_th_lds(m))
     hipLaunchKernelGGL(gfk_lda_beta_bwd_k<true>, g, t, gfk_lda_bwd_smem(m), s, *m);
   else

@@ -7,12 +7,12 @@ launched from C++ (csrc/step.cpp) on the current HIP stream:
   ProdLDA:   enc_in -> post_fwd -> prodlda_fwd -> row_loss -> prodlda_bwd
              -> row_bwd -> post_bwd -> win_update
   NeuralLDA: lda_beta_fwd -> enc_in -> post_fwd -> lda_row_loss_bwd -> row_bwd
-             -> post_bwd -> lda_beta_bwd -> win_update -> adam
+             -> post_bwd -> lda_beta_bwd -> win_update
 
-In the fused update mode (ProdLDA default) there is no optimizer kernel: every
+In the fused update mode (AVITM default) there is no optimizer kernel: every
 tensor's Adam update (and the FedAvg pre-scale w_i = n_i / sum n of the shared
 tensors) is applied in the epilogue of the kernel that completes its gradient
-(beta in prodlda_bwd; W_in and the small MLP tensors -- as batch-reduction
+(beta in prodlda_bwd / lda_beta_bwd; W_in and the small MLP tensors -- as batch-reduction
 GEMM tiles and column sums -- in win_update).  The gradient mode writes gradients into a flat buffer instead and
 appends the generic multi-segment Adam kernel (used by NeuralLDA, by the tests
 as the oracle of the fused epilogues, and by gradient-sharing variants).
@@ -197,7 +197,7 @@ class FusedEngine(EngineBase):
         self.adam_coef = torch.zeros(2, dtype=torch.float32, device=dev)   # see csrc/gfk_common.h
         # fused epilogue updates: ProdLDA AVITM; NeuralLDA and CTM (whose contextual
         # tensors get their gradients from host-issued GEMMs) run the generic Adam
-        self.update_mode = UPDATE_FUSED if tm.model.is_prodlda and tm.kind != "ctm" else UPDATE_GRAD
+        self.update_mode = UPDATE_FUSED if tm.kind != "ctm" else UPDATE_GRAD
         self.lr, self.beta1, self.beta2 = float(tm.lr), float(tm.momentum), 0.99
         self.eps, self.weight_decay = 1e-8, 0.0
         self.fedavg_scale: Optional[float] = None
@@ -237,8 +237,8 @@ class FusedEngine(EngineBase):
     def set_update_mode(self, mode: int):
         """UPDATE_FUSED: optimizer in the kernel epilogues; UPDATE_GRAD: kernels write
         gradients and the generic Adam kernel follows."""
-        if mode == UPDATE_FUSED and (not self.model.is_prodlda or self.kind == "ctm"):
-            raise ValueError("the fused update mode covers AVITM ProdLDA only")
+        if mode == UPDATE_FUSED and self.kind == "ctm":
+            raise ValueError("the fused update mode covers the AVITM models only")
         self.update_mode = mode
         self._m.update_mode = mode
         self._rebuild_adam()
@@ -509,7 +509,8 @@ class FusedEngine(EngineBase):
 
     def phases(self) -> List[int]:
         if self._m.kind == abi.KIND_LDA:
-            ph = list(abi.LDA_STEP)
+            ph = [p for p in abi.LDA_STEP if p != abi.PH_ADAM] + \
+                ([abi.PH_ADAM] if self.update_mode == UPDATE_GRAD else [])
         else:
             ph = abi.PRODLDA_STEP + ([abi.PH_ADAM] if self.update_mode == UPDATE_GRAD else [])
         if self.kind == "ctm":
@@ -517,7 +518,8 @@ class FusedEngine(EngineBase):
             ph.insert(ph.index(abi.PH_ENC_BWD) + 1, abi.PH_CTX_BWD)
         if self._comm is not None and self._comm["mode"] == "graph":
             if "beta" in self._comm:
-                ph.insert(ph.index(abi.PH_PRODLDA_BWD) + 1, abi.PH_FEDAVG_BETA)
+                last = abi.PH_PRODLDA_BWD if abi.PH_PRODLDA_BWD in ph else abi.PH_LDA_BETA_BWD
+                ph.insert(ph.index(last) + 1, abi.PH_FEDAVG_BETA)
             ph.append(abi.PH_FEDAVG_END)
         return ph
 

@@ -153,14 +153,15 @@ def test_graph_replay_matches_eager():
     torch.testing.assert_close(a.flat.buffer, b.flat.buffer, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("model_type", ["prodLDA", "LDA"])
 @pytest.mark.parametrize("B,K,H", [(64, 50, (50, 50)), (32, 20, (32,)), (16, 100, (24, 100, 24))])
-def test_fused_update_matches_gradient_mode(B, K, H):
+def test_fused_update_matches_gradient_mode(B, K, H, model_type):
     """The Adam epilogues fused into prodlda_bwd / enc_head_bwd / win_update give the
     same parameters, moments and BN statistics as gradient mode + the generic Adam,
     over several steps, with the FedAvg pre-scale on."""
     torch.manual_seed(0)
     kw = dict(input_size=900, n_components=K, hidden_sizes=H, batch_size=B, verbose=False,
-              device="cuda")
+              device="cuda", model_type=model_type)
     a = AVITM(backend="fused", **kw)
     b = AVITM(backend="fused", **kw)
     b.model.load_state_dict(a.model.state_dict())
@@ -292,3 +293,31 @@ def test_steps_are_bitwise_deterministic(model_type):
         torch.cuda.synchronize()
         outs.append((tm.flat.buffer.clone(), tm.engine.loss_hist[:12].clone()))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("model_type", ["prodLDA", "LDA"])
+@pytest.mark.parametrize("mode", [UPDATE_FUSED, UPDATE_GRAD])
+def test_fedavg_prescale_covers_every_shared_tensor(model_type, mode):
+    """One step with the FedAvg pre-scale w must leave w x (the unscaled step) in EVERY
+    shared float tensor -- parameters and batch-norm running statistics alike -- or the
+    all-reduce would not be the sample-weighted average (server.py:477-487)."""
+    torch.manual_seed(0)
+    kw = dict(input_size=700, n_components=20, hidden_sizes=(32, 24), batch_size=64,
+              verbose=False, device="cuda", model_type=model_type)
+    a, b = AVITM(backend="fused", **kw), AVITM(backend="fused", **kw)
+    b.model.load_state_dict(a.model.state_dict())
+    b.engine.seed = b.engine._m.seed = a.engine.seed
+    for e in (a.engine, b.engine):
+        e.set_update_mode(mode)
+    a.engine.set_fedavg_scale(0.25)
+    X = random_csr(150, 700, 40, seed=1)
+    _bind(a, X, n_steps=1)
+    _bind(b, X, n_steps=1)
+    a.engine.step(0)
+    b.engine.step(0)
+    torch.cuda.synchronize()
+    sa, sb = a.model.state_dict(), b.model.state_dict()
+    for k in a.shared_keys:
+        if k in sb and sb[k].is_floating_point():
+            torch.testing.assert_close(sa[k], 0.25 * sb[k], rtol=1e-5, atol=1e-7,
+                                       msg=lambda m: f"{k}: {m}")
