@@ -17,43 +17,56 @@
 using namespace gfk;
 
 namespace {
-constexpr int LDA_THREADS = 256;
 constexpr int VB = 64;
 constexpr int LD = VB + 1;
 constexpr float RL_EPS = 1e-10f;
 }  // namespace
 
-// grid: dec_grid workgroups over the vocab tiles.
+// grid: dec_grid workgroups over the vocab tiles, 16 waves each.  Per tile: ONE round
+// of independent loads (the beta tile into registers, this lane's column running
+// statistics), then BN over the topics (16 lanes per column), the transposed store
+// beta_bn^T [V, K], and the per-topic online (max, sum-exp) over the tile's columns.
 // dynamic LDS: bn[K*LD] + rowm[K] + rows[K]
-extern "C" __global__ void __launch_bounds__(LDA_THREADS) gfk_lda_beta_fwd(GfkModel m) {
+constexpr int LBT = 1024;
+constexpr int LBW = LBT / 64;
+
+extern "C" __global__ void __launch_bounds__(LBT) gfk_lda_beta_fwd(GfkModel m) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int K = m.K, V = m.V, tid = threadIdx.x;
   float* bn = smem;
   float* rowm = bn + K * LD;
   float* rows = rowm + K;
-  for (int k = tid; k < K; k += LDA_THREADS) { rowm[k] = -INFINITY; rows[k] = 0.f; }
+  for (int k = tid; k < K; k += LBT) { rowm[k] = -INFINITY; rows[k] = 0.f; }
   if (blockIdx.x == 0 && tid == 0) *m.nbt_beta += 1;
+  constexpr int BU = (256 * VB + LBT - 1) / LBT;      // K <= 256
+  const int c = tid >> 4, sub = tid & 15;             // BN: 16 lanes per column
   for (int tile = blockIdx.x; tile < m.n_tiles; tile += gridDim.x) {
-    const int c0 = tile * VB;
+    const int c0 = tile * VB, nv = min(VB, V - c0);
+    const bool valid = c < nv;
     __syncthreads();
-    for (int i = tid; i < K * VB; i += LDA_THREADS) {
-      const int k = i / VB, c = i % VB;
-      bn[k * LD + c] = (c0 + c < V) ? m.beta[(size_t)k * V + c0 + c] : 0.f;
+    float bv[BU];
+#pragma unroll
+    for (int u = 0; u < BU; ++u) {
+      const int i = tid + LBT * u, k = i / VB, cc = i % VB;
+      bv[u] = (i < K * VB && cc < nv) ? m.beta[(size_t)k * V + c0 + cc] : 0.f;
     }
-    __syncthreads();
-    {  // BN over the K topics of each column: 4 threads per column
-      const int c = tid >> 2, sub = tid & 3;
-      const bool valid = c0 + c < V;
+    float rm0 = 0.f, rv0 = 0.f;
+    if (sub == 0 && valid) { rm0 = m.beta_rm[c0 + c]; rv0 = m.beta_rv[c0 + c]; }
+#pragma unroll
+    for (int u = 0; u < BU; ++u) {
+      const int i = tid + LBT * u;
+      if (i < K * VB) bn[(i / VB) * LD + i % VB] = bv[u];
+    }
+    lds_barrier();
+    {  // BN over the K topics of each column
       float s = 0.f;
-      for (int k = sub; k < K; k += 4) s += bn[k * LD + c];
-      s += __shfl_xor(s, 1, 64); s += __shfl_xor(s, 2, 64);
-      const float mean = s / (float)K;
+      for (int k = sub; k < K; k += 16) s += bn[k * LD + c];
+      const float mean = row16_sum(s) / (float)K;
       float q = 0.f;
-      for (int k = sub; k < K; k += 4) { const float d = bn[k * LD + c] - mean; q += d * d; }
-      q += __shfl_xor(q, 1, 64); q += __shfl_xor(q, 2, 64);
-      const float var = q / (float)K;
+      for (int k = sub; k < K; k += 16) { const float d = bn[k * LD + c] - mean; q += d * d; }
+      const float var = row16_sum(q) / (float)K;
       const float rstd = rsqrtf(var + m.bn_eps);
-      for (int k = sub; k < K; k += 4) {
+      for (int k = sub; k < K; k += 16) {
         const int i = k * LD + c;
         bn[i] = valid ? (bn[i] - mean) * rstd : -INFINITY;
       }
@@ -61,33 +74,28 @@ extern "C" __global__ void __launch_bounds__(LDA_THREADS) gfk_lda_beta_fwd(GfkMo
         const int v = c0 + c;
         const float mom = m.bn_momentum;
         const float unb = K > 1 ? var * (float)K / (float)(K - 1) : var;
-        float nm = (1.f - mom) * m.beta_rm[v] + mom * mean, nv = (1.f - mom) * m.beta_rv[v] + mom * unb;
-        if (m.fed_scale_on && is_shared(m, m.beta_rm)) { nm *= m.fed_scale; nv *= m.fed_scale; }
+        float nm = (1.f - mom) * rm0 + mom * mean, nv2 = (1.f - mom) * rv0 + mom * unb;
+        if (m.fed_scale_on && is_shared(m, m.beta_rm)) { nm *= m.fed_scale; nv2 *= m.fed_scale; }
         m.beta_rm[v] = nm;
-        m.beta_rv[v] = nv;
+        m.beta_rv[v] = nv2;
         m.ws_col_rstd[v] = rstd;
       }
     }
-    __syncthreads();
+    lds_barrier();
     // transposed store bn^T [V, K] (contiguous K-vector per token)
-    for (int i = tid; i < K * VB; i += LDA_THREADS) {
-      const int c = i / K, k = i % K;
-      if (c0 + c < V) m.ws_zn[(size_t)(c0 + c) * K + k] = bn[k * LD + c];
+    for (int i = tid; i < K * VB; i += LBT) {
+      const int cc = i / K, k = i % K;
+      if (cc < nv) m.ws_zn[(size_t)(c0 + cc) * K + k] = bn[k * LD + cc];
     }
-    // online (max, sum exp) over this tile for every topic row: 4 threads per row
-    for (int k = tid >> 2; k < K; k += LDA_THREADS / 4) {
-      const int sub = tid & 3;
-      const float* row = bn + k * LD + 16 * sub;
-      float mx = -INFINITY;
-#pragma unroll
-      for (int c = 0; c < 16; ++c) mx = fmaxf(mx, row[c]);
-      mx = fmaxf(mx, __shfl_xor(mx, 1, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
+    // online (max, sum exp) over this tile for every topic row: 16 lanes per row
+    for (int k = tid >> 4; k < K; k += LBT / 16) {
+      const float* row = bn + k * LD + 4 * sub;
+      float mx = fmaxf(fmaxf(row[0], row[1]), fmaxf(row[2], row[3]));
+      mx = row16_max(mx);
       float se = 0.f;
 #pragma unroll
-      for (int c = 0; c < 16; ++c) se += __expf(row[c] - mx);
-      se += __shfl_xor(se, 1, 64);
-      se += __shfl_xor(se, 2, 64);
+      for (int j = 0; j < 4; ++j) se += __expf(row[j] - mx);
+      se = row16_sum(se);
       if (sub == 0) {
         float rm = rowm[k], rs = rows[k];
         lse_merge(rm, rs, mx, se);
@@ -97,7 +105,7 @@ extern "C" __global__ void __launch_bounds__(LDA_THREADS) gfk_lda_beta_fwd(GfkMo
     }
   }
   __syncthreads();
-  for (int k = tid; k < K; k += LDA_THREADS) {
+  for (int k = tid; k < K; k += LBT) {
     float* p = m.ws_row_part + ((size_t)blockIdx.x * K + k) * 2;
     p[0] = rowm[k];
     p[1] = rows[k];
@@ -209,9 +217,6 @@ __host__ __device__ inline int lda_xs(int B) {
 // outputs this thread updates (fused mode).  Second round: the tile's per-non-zero
 // coefficients (ws_dbsm).  Then c_k, the x^T theta_d MFMA, the BN backward over the
 // topics and the update, all out of LDS.
-constexpr int LBT = 1024;
-constexpr int LBW = LBT / 64;
-
 template <bool ThLds>
 __global__ void __launch_bounds__(LBT) gfk_lda_beta_bwd_k(GfkModel m) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -375,7 +380,7 @@ extern "C" size_t gfk_lda_bwd_smem(const GfkModel* m) {
 }
 
 extern "C" int gfk_launch_lda_beta_fwd(const GfkModel* m, hipStream_t s) {
-  hipLaunchKernelGGL(gfk_lda_beta_fwd, dim3(m->dec_grid), dim3(LDA_THREADS), gfk_lda_fwd_smem(m->K),
+  hipLaunchKernelGGL(gfk_lda_beta_fwd, dim3(m->dec_grid), dim3(LBT), gfk_lda_fwd_smem(m->K),
                      s, *m);
   return (int)hipGetLastError();
 }
