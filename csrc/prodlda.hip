@@ -35,7 +35,7 @@
 // Layouts: ws_thetad is [bmax, kt] (kt = K padded to 4 x odd, zero padding, so
 // the MFMA A-operand reads are bank-conflict free); ws_zn is tiled
 // [n_tiles][bmax][VB] so a tile is one contiguous LDS-DMA copy; ws_row_part is
-// [n_tiles * 4][bmax][2] (one partial per wave).
+// [dec_grid * 4][bmax][2] (one partial per forward wave column strip).
 #include "gfk_common.h"
 
 using namespace gfk;
@@ -90,8 +90,12 @@ __device__ __forceinline__ float sum_groups(float v) {
 }
 }  // namespace
 
-// grid: n_tiles workgroups (one vocab tile each) of 16 waves.  Wave w owns column
-// strip cs = w & 3 (16 columns) and row tiles rt = (w >> 2) + 4 i.
+// grid: dec_grid workgroups of 16 waves (persistent: workgroup g owns vocab tiles
+// g, g + dec_grid, ...; the usual case is one tile each).  theta_d is staged once per
+// workgroup, so large vocabularies do not re-read it per tile, and the per-row
+// (max, sum-exp) partials are merged across the workgroup's tiles in registers
+// (ws_row_part holds dec_grid * 4 partials per row).  Wave w owns column strip
+// cs = w & 3 (16 columns) and row tiles rt = (w >> 2) + 4 i.
 // dynamic LDS: th[BM*kt] + bt[KP*LDB_F] + colp[4][64] + colq[4][64] + stat[2][64]
 template <int BM>
 __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
@@ -99,7 +103,6 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
   const int K = m.K, V = m.V, KT = m.kt, tid = threadIdx.x;
   const int lane = tid & 63, wave = uniform(tid >> 6);
   const int KP = round_up(K, 4);
-  const int tile = blockIdx.x, c0 = tile * VB;
   float* th = smem;
   float* bt = th + BM * KT;
   float* colp = bt + KP * LDB_F;
@@ -107,20 +110,28 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
   constexpr int RT = BM / 16;                 // row tiles
   constexpr int NRT = (RT + 3) / 4;           // row tiles per wave
   const int cs = wave & 3, rt0 = wave >> 2;
+  const int col = 16 * cs + (lane & 15);      // this lane's column within a tile
+  float rm_[NRT][4], rs_[NRT][4];             // running (max, sum-exp) of this lane's rows
+#pragma unroll
+  for (int i = 0; i < NRT; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { rm_[i][e] = -INFINITY; rs_[i][e] = 0.f; }
 
   GFK_STAMP(m, 16);
-  // ---- one staging round: theta_d (LDS-DMA), beta tile, running stats, nb ----
   glds_copy(th, m.ws_thetad, BM * KT, tid, DEC_THREADS);
-  const int col = 16 * cs + (lane & 15);      // this lane's column within the tile
+  const int nb = *m.ws_nb;
+  if (blockIdx.x == 0 && tid == 0) *m.nbt_beta += 1;
+#pragma unroll 1
+  for (int tile = blockIdx.x; tile < m.n_tiles; tile += gridDim.x) {
+  const int c0 = tile * VB;
+  // ---- one staging round: beta tile, running stats (theta_d: first iteration) ----
   const int v = c0 + col;
   const bool valid = v < V;
   const float rm0 = m.beta_rm[min(v, V - 1)], rv0 = m.beta_rv[min(v, V - 1)];
-  const int nb = *m.ws_nb;
+  if (tile != (int)blockIdx.x) __syncthreads();     // previous tile's bt / colp reads done
   stage_beta_tile(bt, LDB_F, m.beta, K, KP, V, c0, tid);
-  if (tile == 0 && tid == 0) *m.nbt_beta += 1;
   __syncthreads();
   GFK_STAMP(m, 17);
-
   // ---- logits for this wave's row tiles x 16 columns ----
   f32x4 acc[NRT];
 #pragma unroll
@@ -178,9 +189,8 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
   }
   GFK_STAMP(m, 19);
 
-  // ---- normalise, store the BN'ed tile, per-row (max, sum-exp) partials ----
+  // ---- normalise, store the BN'ed tile, merge the per-row (max, sum-exp) ----
   float* zt = m.ws_zn + (size_t)tile * BM * VB;
-  float* part = m.ws_row_part + (size_t)(tile * 4 + cs) * m.bmax * 2;
 #pragma unroll
   for (int i = 0; i < NRT; ++i) {
     if (rt0 + 4 * i >= RT) continue;
@@ -192,13 +202,25 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
       const float zv = valid ? z : -INFINITY;
       const float mx = row16_max(zv);
       const float se = row16_sum(valid ? __expf(zv - mx) : 0.f);
-      if ((lane & 15) == 0 && row < nb) {
-        part[2 * row] = mx;
-        part[2 * row + 1] = se;
-      }
+      lse_merge(rm_[i][e], rs_[i][e], mx, se);
     }
   }
   GFK_STAMP(m, 20);
+  }
+  // ---- this workgroup's per-row partials (one per wave column strip) ----
+  float* part = m.ws_row_part + (size_t)(blockIdx.x * 4 + cs) * m.bmax * 2;
+#pragma unroll
+  for (int i = 0; i < NRT; ++i) {
+    if (rt0 + 4 * i >= RT) continue;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = (rt0 + 4 * i) * 16 + (lane >> 4) * 4 + e;
+      if ((lane & 15) == 0 && row < nb) {
+        part[2 * row] = rm_[i][e];
+        part[2 * row + 1] = rs_[i][e];
+      }
+    }
+  }
 }
 
 // One wave per batch row: log-sum-exp from the per-wave partials, the sparse
@@ -211,7 +233,7 @@ extern "C" __global__ void __launch_bounds__(64) gfk_prodlda_row_loss(GfkModel m
   const int b = blockIdx.x, lane = threadIdx.x;
   const int nb = *nbp;
   if (b >= nb) return;
-  const int np = n_tiles * 4;
+  const int np = m.dec_grid * 4;                 // per-workgroup partials of prodlda_fwd
   const int e0 = erange[2 * b], e1 = erange[2 * b + 1];
   constexpr int PU = 8;
   float pm[PU], ps[PU];
@@ -254,7 +276,9 @@ extern "C" __global__ void __launch_bounds__(64) gfk_prodlda_row_loss(GfkModel m
 
 // Backward.  grid: n_tiles workgroups of 16 waves.
 // dynamic LDS: th[BM*kt] + bt[KP16*LDB_B] + zt[BM*VB] + dt[BM*LDD] + lse[BM] + S[BM] + rstd[VB]
-template <int BM>
+// MAXU: dbeta 16x16 output tiles per wave = ceil(K / 64) (Adam state prefetched for
+// each; a compile-time count keeps the prefetch in registers)
+template <int BM, int MAXU>
 __global__ void __launch_bounds__(DEC_THREADS) prodlda_bwd_kernel(GfkModel m) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int K = m.K, V = m.V, KT = m.kt, tid = threadIdx.x;
@@ -292,7 +316,6 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_bwd_kernel(GfkModel m) {
   // optimizer state of this lane's dbeta outputs (fused mode): wave -> (k tile, column strip)
   const int ksub = KP16 / 16;
   const int NB_T = ksub * 4;
-  constexpr int MAXU = 4;                         // K <= 256
   const bool fused = m.update_mode == 1;
   float bp_[MAXU][4], bm_[MAXU][4], bv_[MAXU][4];
 #pragma unroll
@@ -433,7 +456,7 @@ extern "C" size_t gfk_prodlda_bwd_smem(const GfkModel* m) {
 
 extern "C" int gfk_launch_prodlda_fwd(const GfkModel* m, hipStream_t s) {
   const size_t sm = gfk_prodlda_fwd_smem(m);
-  dim3 g(m->n_tiles), blk(DEC_THREADS);
+  dim3 g(m->dec_grid), blk(DEC_THREADS);
   switch (m->bmax) {
     case 16: hipLaunchKernelGGL(prodlda_fwd_kernel<16>, g, blk, sm, s, *m); break;
     case 32: hipLaunchKernelGGL(prodlda_fwd_kernel<32>, g, blk, sm, s, *m); break;
@@ -444,15 +467,25 @@ extern "C" int gfk_launch_prodlda_fwd(const GfkModel* m, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+template <int MAXU>
+static void launch_bwd(const GfkModel* m, dim3 g, dim3 blk, size_t sm, hipStream_t s) {
+  switch (m->bmax) {
+    case 16: hipLaunchKernelGGL((prodlda_bwd_kernel<16, MAXU>), g, blk, sm, s, *m); break;
+    case 32: hipLaunchKernelGGL((prodlda_bwd_kernel<32, MAXU>), g, blk, sm, s, *m); break;
+    case 64: hipLaunchKernelGGL((prodlda_bwd_kernel<64, MAXU>), g, blk, sm, s, *m); break;
+    default: hipLaunchKernelGGL((prodlda_bwd_kernel<128, MAXU>), g, blk, sm, s, *m); break;
+  }
+}
+
 extern "C" int gfk_launch_prodlda_bwd(const GfkModel* m, hipStream_t s) {
   const size_t sm = gfk_prodlda_bwd_smem(m);
-  dim3 g(m->n_tiles), blk(DEC_THREADS);
-  switch (m->bmax) {
-    case 16: hipLaunchKernelGGL(prodlda_bwd_kernel<16>, g, blk, sm, s, *m); break;
-    case 32: hipLaunchKernelGGL(prodlda_bwd_kernel<32>, g, blk, sm, s, *m); break;
-    case 64: hipLaunchKernelGGL(prodlda_bwd_kernel<64>, g, blk, sm, s, *m); break;
-    case 128: hipLaunchKernelGGL(prodlda_bwd_kernel<128>, g, blk, sm, s, *m); break;
-    default: return -1;
+  dim3 g(m->n_tiles), blk(DEC_THREADS);          // one vocab tile per workgroup
+  if (m->bmax != 16 && m->bmax != 32 && m->bmax != 64 && m->bmax != 128) return -1;
+  switch ((m->K + 63) / 64) {
+    case 1: launch_bwd<1>(m, g, blk, sm, s); break;
+    case 2: launch_bwd<2>(m, g, blk, sm, s); break;
+    case 3: launch_bwd<3>(m, g, blk, sm, s); break;
+    default: launch_bwd<4>(m, g, blk, sm, s); break;
   }
   return (int)hipGetLastError();
 }
@@ -465,8 +498,10 @@ extern "C" int gfk_launch_prodlda_row_loss(const GfkModel* m, hipStream_t s) {
 extern "C" int gfk_prodlda_set_smem(size_t bytes) {
   const void* ks[] = {(const void*)prodlda_fwd_kernel<16>, (const void*)prodlda_fwd_kernel<32>,
                       (const void*)prodlda_fwd_kernel<64>, (const void*)prodlda_fwd_kernel<128>,
-                      (const void*)prodlda_bwd_kernel<16>, (const void*)prodlda_bwd_kernel<32>,
-                      (const void*)prodlda_bwd_kernel<64>, (const void*)prodlda_bwd_kernel<128>};
+#define GFK_BWD_PTRS(U) (const void*)prodlda_bwd_kernel<16, U>, (const void*)prodlda_bwd_kernel<32, U>, \
+    (const void*)prodlda_bwd_kernel<64, U>, (const void*)prodlda_bwd_kernel<128, U>
+                      GFK_BWD_PTRS(1), GFK_BWD_PTRS(2), GFK_BWD_PTRS(3), GFK_BWD_PTRS(4)};
+#undef GFK_BWD_PTRS
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return (int)e;

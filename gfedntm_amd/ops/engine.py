@@ -334,6 +334,13 @@ class FusedEngine(EngineBase):
                 break
         else:
             raise RuntimeError(f"fused step needs {need()} B of LDS (> {LDS_LIMIT})")
+        if m.kind == abi.KIND_PRODLDA:
+            # persistent decoder forward: one workgroup per resident slot (16-wave
+            # workgroups: 2 per CU when the LDS allows), each looping over its vocab
+            # tiles with theta_d staged once and its row-LSE partials merged
+            sm = self.lib.gfk_smem_required(C.byref(m), 0)
+            per_cu = 2 if 2 * sm <= LDS_LIMIT else 1
+            m.dec_grid = int(min(m.n_tiles, per_cu * props.multi_processor_count))
         self._alloc_workspace()
         rc = self.lib.gfk_setup(C.byref(m))
         if rc:
