@@ -444,6 +444,190 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_bwd_kernel(GfkModel m) {
   GFK_STAMP(m, 28);
 }
 
+// Backward, persistent variant for large vocabularies (n_tiles > dec_grid): the same
+// per-tile work; theta_d, lse and S staged once per workgroup, and the workgroup's
+// dtheta_d partial sums its tiles (first tile stores, later tiles add to the same slab,
+// each element owned by one lane -- deterministic), so row_bwd reduces dec_grid
+// partials instead of n_tiles.
+// dynamic LDS: th[BM*kt] + bt[KP16*LDB_B] + zt[BM*VB] + dt[BM*LDD] + lse[BM] + S[BM] + rstd[VB]
+// MAXU: dbeta 16x16 output tiles per wave = ceil(K / 64) (Adam state prefetched for
+// each; a compile-time count keeps the prefetch in registers)
+template <int BM, int MAXU>
+__global__ void __launch_bounds__(DEC_THREADS) prodlda_bwd_persist_kernel(GfkModel m) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int K = m.K, V = m.V, KT = m.kt, tid0 = threadIdx.x;
+  const int KP16 = round_up(K, 16);
+  float* th = smem;
+  float* bt = th + BM * KT;
+  float* zt = bt + KP16 * LDB_B;
+  float* dt = zt + BM * VB;
+  float* lse = dt + BM * LDD;
+  float* Sb = lse + BM;
+  float* rs = Sb + BM;
+  constexpr int TPR = DEC_THREADS / BM < 16 ? DEC_THREADS / BM : 16;   // threads per row (sparse x)
+
+  glds_copy(th, m.ws_thetad, BM * KT, tid0, DEC_THREADS);
+  glds_copy(lse, m.ws_lse, BM, tid0, DEC_THREADS);
+  glds_copy(Sb, m.ws_s, BM, tid0, DEC_THREADS);
+#pragma unroll 1
+  for (int tile = blockIdx.x; tile < m.n_tiles; tile += gridDim.x) {
+  // the thread index is made opaque per iteration so the compiler rebuilds the
+  // lane-dependent LDS / global addresses inside the loop instead of hoisting them
+  // all out of it (which costs ~60 VGPRs and spills)
+  int tid = tid0;
+  asm volatile("" : "+v"(tid));
+  const int lane = tid & 63, wave = uniform(tid >> 6);
+  const int c0 = tile * VB;
+  if (tile != (int)blockIdx.x) vm_barrier();   // previous tile: LDS reads and slab stores done
+  glds_copy(zt, m.ws_zn + (size_t)tile * BM * VB, BM * VB, tid, DEC_THREADS);
+  glds_copy(rs, m.ws_col_rstd + c0, VB, tid, DEC_THREADS);
+  const int nb = *m.ws_nb;
+  // sparse x of this tile: TPR threads per row, the first non-zero prefetched
+  const int xrow = tid / TPR, xsub = tid % TPR;
+  int xe0 = 0, xe1 = 0;
+  if (xrow < BM) {
+    const int32_t* ts = m.ws_tstart + (size_t)xrow * (m.n_tiles + 1) + tile;
+    xe0 = ts[0];
+    xe1 = ts[1];
+  }
+  const int xe = min(xe0 + xsub, max(xe1 - 1, 0));
+  const int xc0 = m.indices[xe];
+  const float xv0 = m.values[xe];
+  // optimizer state of this lane's dbeta outputs (fused mode): wave -> (k tile, column strip)
+  const int ksub = KP16 / 16;
+  const int NB_T = ksub * 4;
+  const bool fused = m.update_mode == 1;
+  float bp_[MAXU][4], bm_[MAXU][4], bv_[MAXU][4];
+#pragma unroll
+  for (int u = 0; u < MAXU; ++u) {
+    const int t = wave + 16 * u;
+    const int ks = t >> 2, cst = t & 3;
+    const int c = min(c0 + cst * 16 + (lane & 15), V - 1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int k = min(ks * 16 + (lane >> 4) * 4 + r, K - 1);
+      bp_[u][r] = bm_[u][r] = bv_[u][r] = 0.f;
+      if (fused && t < NB_T) {
+        const float* p = m.beta + (size_t)k * V + c;
+        bp_[u][r] = *p;
+        bm_[u][r] = p[m.off_m];
+        bv_[u][r] = p[m.off_v];
+      }
+    }
+  }
+  stage_beta_tile(bt, LDB_B, m.beta, K, KP16, V, c0, tid);
+  // zero the dlogit tile (dense-pass layout: column tid>>4, rows (tid&15) + 16 i)
+  const int dcol = tid >> 4, dg = tid & 15;
+  for (int row = dg; row < BM; row += 16) dt[row * LDD + dcol] = 0.f;
+  __syncthreads();
+  GFK_STAMP(m, 25);
+
+  // ---- sparse term: dt[b, c] = -x p / (p + 1e-10) at this tile's non-zeros ----
+  if (xrow < nb && xrow < BM) {
+    const float l = lse[xrow];
+    for (int i = 0, e = xe0 + xsub; e < xe1; ++i, e += TPR) {
+      const int c = (i == 0 ? xc0 : m.indices[e]) - c0;
+      const float x = i == 0 ? xv0 : m.values[e];
+      const float p = __expf(zt[xrow * VB + (c ^ zswz(xrow))] - l);
+      dt[xrow * LDD + c] = -x * p / (p + RL_EPS);
+    }
+  }
+  __syncthreads();
+  GFK_STAMP(m, 26);
+
+  // ---- dense term p*S and the column BN backward: 16 lanes per column ----
+  {
+    const bool valid = c0 + dcol < V;
+    constexpr int NR = BM / 16;
+    float d[NR], z[NR];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int row = dg + 16 * i;
+      z[i] = zt[row * VB + (dcol ^ zswz(row))];
+      const float p = __expf(z[i] - lse[row]);
+      d[i] = (row < nb && valid) ? p * Sb[row] + dt[row * LDD + dcol] : 0.f;
+      s1 += d[i];
+      s2 += d[i] * z[i];
+    }
+    s1 = row16_sum(s1) / (float)nb;
+    s2 = row16_sum(s2) / (float)nb;
+    const float r = valid ? rs[dcol] : 0.f;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int row = dg + 16 * i;
+      dt[row * LDD + dcol] = row < nb ? r * (d[i] - s1 - z[i] * s2) : 0.f;
+    }
+  }
+  __syncthreads();
+  GFK_STAMP(m, 27);
+
+  // ---- dbeta[k, c] = sum_b th[b, k] dlogit[b, c]  -> update (fused) or gradient ----
+  {
+    const AdamCoef ac = adam_coef(m);
+    const bool sh = is_shared(m, m.beta);
+#pragma unroll
+    for (int u = 0; u < MAXU; ++u) {
+      const int t = wave + 16 * u;
+      if (t >= NB_T) break;
+      const int ks = t >> 2, cst = t & 3;
+      const float* ap = th + (lane >> 4) * KT + ks * 16 + (lane & 15);
+      const float* bp = dt + (lane >> 4) * LDD + cst * 16 + (lane & 15);
+      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int b0 = 0; b0 < BM; b0 += 8) {
+        a0 = mfma16x16x4(ap[b0 * KT], bp[b0 * LDD], a0);
+        a1 = mfma16x16x4(ap[(b0 + 4) * KT], bp[(b0 + 4) * LDD], a1);
+      }
+      const int c = c0 + cst * 16 + (lane & 15);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = ks * 16 + (lane >> 4) * 4 + e;
+        if (k >= K || c >= V) continue;
+        float* p = m.beta + (size_t)k * V + c;
+        const float g = a0[e] + a1[e];
+        if (!fused) {
+          p[m.off_g] = g;
+        } else {
+          float mo = bm_[u][e], vo = bv_[u][e];
+          float np = adam_update(bp_[u][e], g, mo, vo, ac);
+          if (sh && m.fed_scale_on) np *= m.fed_scale;
+          p[m.off_m] = mo;
+          p[m.off_v] = vo;
+          *p = np;
+        }
+      }
+    }
+  }
+  // ---- this tile's partial dtheta_d[b, k] = sum_c dlogit[b, c] beta[k, c] (plain stores;
+  //      dtheta_reduce sums the n_tiles partials in a fixed order) ----
+  {
+    const bool first = tile == (int)blockIdx.x;
+    float* dpart = m.ws_dthetad + (size_t)blockIdx.x * m.bmax * K;
+    for (int t = wave; t < (BM / 16) * ksub; t += 16) {
+      const int rt = t / ksub, ks = t % ksub;
+      const float* ap = dt + (rt * 16 + (lane & 15)) * LDD + (lane >> 4);
+      const float* bp = bt + (ks * 16 + (lane & 15)) * LDB_B + (lane >> 4);
+      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < VB; c += 8) {
+        a0 = mfma16x16x4(ap[c], bp[c], a0);
+        a1 = mfma16x16x4(ap[c + 4], bp[c + 4], a1);
+      }
+      const int k = ks * 16 + (lane & 15);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = rt * 16 + (lane >> 4) * 4 + e;
+        if (row < nb && k < K) {
+          float* q = dpart + (size_t)row * K + k;
+          *q = first ? a0[e] + a1[e] : *q + (a0[e] + a1[e]);
+        }
+      }
+    }
+  }
+  }
+}
+
 extern "C" size_t gfk_prodlda_fwd_smem(const GfkModel* m) {
   const size_t KP = round_up(m->K, 4);
   return sizeof(float) * ((size_t)m->bmax * m->kt + KP * LDB_F + 8 * VB);
@@ -469,6 +653,16 @@ extern "C" int gfk_launch_prodlda_fwd(const GfkModel* m, hipStream_t s) {
 
 template <int MAXU>
 static void launch_bwd(const GfkModel* m, dim3 g, dim3 blk, size_t sm, hipStream_t s) {
+  if (m->n_dpart < m->n_tiles) {         // persistent: dec_grid workgroups, dec_grid partials
+    g = dim3(m->n_dpart);
+    switch (m->bmax) {
+      case 16: hipLaunchKernelGGL((prodlda_bwd_persist_kernel<16, MAXU>), g, blk, sm, s, *m); break;
+      case 32: hipLaunchKernelGGL((prodlda_bwd_persist_kernel<32, MAXU>), g, blk, sm, s, *m); break;
+      case 64: hipLaunchKernelGGL((prodlda_bwd_persist_kernel<64, MAXU>), g, blk, sm, s, *m); break;
+      default: hipLaunchKernelGGL((prodlda_bwd_persist_kernel<128, MAXU>), g, blk, sm, s, *m); break;
+    }
+    return;
+  }
   switch (m->bmax) {
     case 16: hipLaunchKernelGGL((prodlda_bwd_kernel<16, MAXU>), g, blk, sm, s, *m); break;
     case 32: hipLaunchKernelGGL((prodlda_bwd_kernel<32, MAXU>), g, blk, sm, s, *m); break;
@@ -499,7 +693,9 @@ extern "C" int gfk_prodlda_set_smem(size_t bytes) {
   const void* ks[] = {(const void*)prodlda_fwd_kernel<16>, (const void*)prodlda_fwd_kernel<32>,
                       (const void*)prodlda_fwd_kernel<64>, (const void*)prodlda_fwd_kernel<128>,
 #define GFK_BWD_PTRS(U) (const void*)prodlda_bwd_kernel<16, U>, (const void*)prodlda_bwd_kernel<32, U>, \
-    (const void*)prodlda_bwd_kernel<64, U>, (const void*)prodlda_bwd_kernel<128, U>
+    (const void*)prodlda_bwd_kernel<64, U>, (const void*)prodlda_bwd_kernel<128, U>, \
+    (const void*)prodlda_bwd_persist_kernel<16, U>, (const void*)prodlda_bwd_persist_kernel<32, U>, \
+    (const void*)prodlda_bwd_persist_kernel<64, U>, (const void*)prodlda_bwd_persist_kernel<128, U>
                       GFK_BWD_PTRS(1), GFK_BWD_PTRS(2), GFK_BWD_PTRS(3), GFK_BWD_PTRS(4)};
 #undef GFK_BWD_PTRS
   for (const void* k : ks) {

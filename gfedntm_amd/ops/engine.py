@@ -338,9 +338,13 @@ class FusedEngine(EngineBase):
             # persistent decoder forward: one workgroup per resident slot (16-wave
             # workgroups: 2 per CU when the LDS allows), each looping over its vocab
             # tiles with theta_d staged once and its row-LSE partials merged
+            cu = props.multi_processor_count
             sm = self.lib.gfk_smem_required(C.byref(m), 0)
-            per_cu = 2 if 2 * sm <= LDS_LIMIT else 1
-            m.dec_grid = int(min(m.n_tiles, per_cu * props.multi_processor_count))
+            m.dec_grid = int(min(m.n_tiles, (2 if 2 * sm <= LDS_LIMIT else 1) * cu))
+            # backward: one workgroup per tile while the tiles fit the resident slots,
+            # else persistent (n_dpart workgroups, n_dpart dtheta partials)
+            sb = self.lib.gfk_smem_required(C.byref(m), 1)
+            m.n_dpart = int(min(m.n_tiles, (2 if 2 * sb <= LDS_LIMIT else 1) * cu))
         self._alloc_workspace()
         rc = self.lib.gfk_setup(C.byref(m))
         if rc:

@@ -66,7 +66,9 @@ def _grads_of(tm_fused):
                                             (64, 200, 50, (50, 50, 50), 700),
                                             (64, 100, 200, (50, 50), 700),       # K > 128, L2 mode
                                             (64, 120, 25, (30, 20), 700),        # odd K, odd strides
-                                            (64, 80, 50, (50, 50), 30000)])      # many V tiles
+                                            (64, 80, 50, (50, 50), 30000),       # many V tiles
+                                            (64, 80, 50, (50, 50), 40000),       # persistent decoder
+                                            (64, 80, 200, (50, 50), 40000)])     # persistent, 3 tiles/WG
 def test_step_matches_oracle(model_type, B, n_docs, K, H, V):
     fused, ref = _pair(model_type, V=V, K=K, H=H, B=B)
     if K == 200 and model_type == "prodLDA":
