@@ -1,0 +1,387 @@
+// CombinedTM contextual path on the fused kernels: adapt_bert and the contextual
+// half of the input layer, forward and backward, with the adapt_bert Adam updates
+// in the epilogue (reference ctm inference_network.py:160-185:
+// z0 = [x_bow | adapt_bert(x_ctx)] W_in^T + b, adapt_bert(x) = x Wa^T + ba).
+//
+// Shapes: B (bmax) batch rows, V vocabulary, C contextual size, H0 first hidden
+// width.  Wa [V, C], ba [V], Wc = rows V..2V-1 of the transposed input layer [2V, H0].
+//
+//   ctx_fwd (before enc_in), one workgroup per (vocab tile t, 16-row block r):
+//       A_rt  = x_ctx[rows r] Wa[tile t]^T + ba[tile t]                      [16, 64]
+//       P_rt  = A_rt Wc[tile t]                                              [16, H0]
+//     the MFMA operands come straight from global memory as float4 (lane group g
+//     holds k = 16 s + 4 g + j for MFMA step j: A and B agree on the k permutation),
+//     the four waves of a 16x16 output tile split the C reduction, and the row
+//     blocks of one tile are dealt to the same XCD so Wa[tile t] is read once per L2.
+//     A is kept for the backward (ws_actx); enc_in adds sum_t P_t to its row's
+//     pre-activation (fixed order: deterministic).
+//   ctx_bwd (after post_bwd, before win_update), grid n_tiles x kb, (tile t, chunk k):
+//       dA_t  = dz0 Wc[tile t]^T                                             [B, 64]
+//       g_ba  = sum_b dA_t                              (chunk 0; Adam on ba)
+//       g_Wa  = dA_t^T x_ctx[:, chunk k]                (Adam on Wa[tile t, chunk k])
+//     Wc's own gradient A^T dz0 is a dense tile of win_update (same MFMA + Adam
+//     epilogue as the bag-of-words half), which runs after ctx_bwd has read Wc.
+//
+// All products are fp32 MFMA (v_mfma_f32_16x16x4_f32); operand tiles are staged in
+// LDS with strides 2 mod 4 (A-role reads: 16 rows x 2 k per half-wave) or 16 mod 32
+// (B-role reads: 2 rows x 16 columns), so every ds_read_b32 hits 32 distinct banks.
+// In the backward the C dimension is split across workgroups so the grid covers the
+// chip even for a small vocabulary; that split also spreads the Wa Adam traffic
+// (p / m / v of V x C floats), which is what bounds it.
+#include "gfk_common.h"
+
+using namespace gfk;
+
+namespace {
+constexpr int CT = 1024;
+constexpr int CW = CT / 64;
+__host__ __device__ inline int rup(int x, int m) { return (x + m - 1) / m * m; }
+__host__ __device__ inline int stride_a(int w) {     // 2 x odd
+  int s = rup(w, 2);
+  return (s / 2) % 2 == 0 ? s + 2 : s;
+}
+__host__ __device__ inline int stride_b(int w) {     // 16 mod 32 (w: multiple of 16)
+  return w % 32 == 16 ? w : w + 16;
+}
+
+// forward LDS: the 2 C-half partials of A [2][16][68], A [16][66], Wc tile [64][ldc]
+__host__ __device__ inline int fwd_ldc(const GfkModel& m) { return stride_b(rup(m.H[0], 16)); }
+__host__ __device__ inline int fwd_lds_floats(const GfkModel& m) {
+  return 2 * 16 * 68 + 16 * 66 + 64 * fwd_ldc(m);
+}
+
+struct BwdLds {
+  int ldz, ldxb, dz, wc, da, xc, total;
+};
+__host__ __device__ inline BwdLds bwd_lds(const GfkModel& m) {
+  BwdLds L;
+  const int B = m.bmax;
+  L.ldz = stride_a(rup(m.H[0], 4));
+  L.ldxb = stride_b(m.ctx_ckb);
+  int o = 0;
+  L.dz = o; o += B * L.ldz;
+  L.wc = o; o += 64 * L.ldz;
+  L.da = o; o += B * 80;
+  L.xc = o; o += B * L.ldxb;
+  L.total = o;
+  return L;
+}
+// Global -> LDS copy of elements [i0, n) with NR loads in flight per thread: the
+// loads of a group are all issued before the first LDS store (a plain strided loop
+// would wait out one memory latency per element).
+template <int NR, int NT = CT, typename Ld, typename St>
+__device__ __forceinline__ void staged_copy(int i0, int n, Ld ld, St st) {
+  for (int base = i0 + (int)threadIdx.x; base < n; base += NR * NT) {
+    float r[NR];
+#pragma unroll
+    for (int u = 0; u < NR; ++u) {
+      const int i = base + u * NT;
+      r[u] = i < n ? ld(i) : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < NR; ++u) {
+      const int i = base + u * NT;
+      if (i < n) st(i, r[u]);
+    }
+  }
+}
+
+// Split staging: reg_load issues the first NR * NT elements' loads into registers,
+// reg_store writes them to LDS later (other loads can be issued in between) and
+// copies any remainder (wide shapes) with staged_copy.
+template <int NR, int NT = CT, typename Ld>
+__device__ __forceinline__ void reg_load(float (&r)[NR], int n, Ld ld) {
+#pragma unroll
+  for (int u = 0; u < NR; ++u) {
+    const int i = (int)threadIdx.x + u * NT;
+    r[u] = i < n ? ld(i) : 0.f;
+  }
+}
+template <int NR, int NT = CT, typename Ld, typename St>
+__device__ __forceinline__ void reg_store(const float (&r)[NR], int n, Ld ld, St st) {
+#pragma unroll
+  for (int u = 0; u < NR; ++u) {
+    const int i = (int)threadIdx.x + u * NT;
+    if (i < n) st(i, r[u]);
+  }
+  if (n > NR * NT) staged_copy<NR, NT>(NR * NT, n, ld, st);
+}
+
+}  // namespace
+
+// grid: 8 * ceil(n_tiles / 8) * (BM / 16) workgroups of 8 waves; workgroup x runs on
+// XCD x % 8 and handles tile 8 (x / 8 / RB) + x % 8, row block (x / 8) % RB.
+// Wave (vt, kh) = (wave & 3, wave >> 2): 16x16 output tile vt over the C half kh,
+// FB float4 steps of both operands per buffer, two buffers in flight.
+constexpr int FT = 512;
+template <int BM>
+__global__ void __launch_bounds__(FT) gfk_ctx_fwd_k(GfkModel m) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int RB = BM / 16, FB = 4;
+  const int x = blockIdx.x, jx = x >> 3, rb = jx % RB, tile = (jx / RB) * 8 + (x & 7);
+  if (tile >= m.n_tiles) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
+  const int vt = wave & 3, kh = wave >> 2, r = lane & 15, g = lane >> 4;
+  const int V = m.V, C = m.C, H0 = m.H[0];
+  const int c0 = tile * 64, nvv = min(64, V - c0), H0P = rup(H0, 16), LDC = fwd_ldc(m);
+  float* red = smem;                     // [2][16][68]
+  float* as = smem + 2 * 16 * 68;        // [16][66]
+  float* wc = as + 16 * 66;              // [64][LDC]
+  const float* wcg = m.w_in + (size_t)V * H0;
+
+  // ---- loads that do not depend on the batch: Wa rows, Wc tile, bias ----
+  const int v = vt * 16 + r;
+  const float* wp = m.w_a + (size_t)(c0 + min(v, nvv - 1)) * C + 4 * g;
+  const float vmask = v < nvv ? 1.f : 0.f;
+  const int NS = (C + 15) / 16, s0 = kh * NS / 2, s1 = (kh + 1) * NS / 2;
+  auto ld_wc = [&](int i) {
+    const int vv = i / H0P, j = i - vv * H0P;
+    return (vv < nvv && j < H0) ? wcg[(size_t)(c0 + vv) * H0 + j] : 0.f;
+  };
+  auto st_wc = [&](int i, float xv) { const int vv = i / H0P; wc[vv * LDC + i - vv * H0P] = xv; };
+  float wcr[8];
+  reg_load<8, FT>(wcr, 64 * H0P, ld_wc);
+  const int bv = tid & 63;
+  const float bias = bv < nvv ? m.b_a[c0 + bv] : 0.f;
+  const int doc = m.ws_next[1 + rb * 16 + r];   // the batch prepared by the previous step
+  const float* xp = m.ctx + (size_t)doc * C + 4 * g;
+
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  const f32x4* wp4 = reinterpret_cast<const f32x4*>(wp);
+  const f32x4* xp4 = reinterpret_cast<const f32x4*>(xp);
+  auto ld = [&](int s, f32x4 (&xa)[FB], f32x4 (&wb)[FB]) {
+#pragma unroll
+    for (int u = 0; u < FB; ++u) {
+      const bool ok = s + u < s1 && 16 * (s + u) + 4 * g < C;
+      const int o = ok ? 4 * (s + u) : 0;        // in-bounds address; zeroed below
+      wb[u] = wp4[o];
+      xa[u] = xp4[o];
+      if (!ok) wb[u] = xa[u] = z4;
+    }
+  };
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  auto mm = [&](const f32x4 (&xa)[FB], const f32x4 (&wb)[FB]) {
+#pragma unroll
+    for (int u = 0; u < FB; ++u)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc = mfma16x16x4(xa[u][c], wb[u][c] * vmask, acc);
+  };
+  f32x4 xa0[FB], wb0[FB], xa1[FB], wb1[FB];
+  ld(s0, xa0, wb0);
+  for (int s = s0; s < s1; s += 2 * FB) {
+    ld(s + FB, xa1, wb1);
+    mm(xa0, wb0);
+    if (s + 2 * FB < s1) ld(s + 2 * FB, xa0, wb0);
+    if (s + FB < s1) mm(xa1, wb1);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) red[(kh * 16 + g * 4 + i) * 68 + v] = acc[i];
+  reg_store<8, FT>(wcr, 64 * H0P, ld_wc, st_wc);
+  __syncthreads();
+
+  // ---- A = sum of the halves + bias: two elements per thread (16 x 64 = 2 FT) ----
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int rr = (tid >> 6) + 8 * h;
+    float a = red[rr * 68 + bv] + red[(16 + rr) * 68 + bv];
+    a = bv < nvv ? a + bias : 0.f;
+    as[rr * 66 + bv] = a;
+    m.ws_actx[((size_t)tile * m.bmax + rb * 16 + rr) * 64 + bv] = a;
+  }
+  __syncthreads();
+
+  // ---- P [16, H0] = A Wc_tile ----
+  float* hg = m.ws_hpart + ((size_t)tile * m.bmax + rb * 16) * H0;
+  for (int jt = wave; jt < H0P / 16; jt += FT / 64) {
+    f32x4 p = {0.f, 0.f, 0.f, 0.f};
+    const float* ap = as + r * 66 + g;
+    const float* bp = wc + g * LDC + jt * 16 + r;
+#pragma unroll 4
+    for (int k = 0; k < 64; k += 4) p = mfma16x16x4(ap[k], bp[k * LDC], p);
+    const int j = jt * 16 + r;
+    if (j < H0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) hg[(g * 4 + i) * H0 + j] = p[i];
+    }
+  }
+}
+
+// grid: n_tiles * ctx_kb workgroups of 16 waves.
+// one workgroup per CU (the grid is sized to one round of CU workgroups)
+template <int BM>
+__global__ void __launch_bounds__(CT) gfk_ctx_bwd_k(GfkModel m) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ int docs_s[BM];
+  const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
+  const int n_tiles = m.n_tiles, tile = blockIdx.x % n_tiles, kc = blockIdx.x / n_tiles;
+  const int V = m.V, C = m.C, H0 = m.H[0], ckb = m.ctx_ckb;
+  if (tid < BM) docs_s[tid] = m.ws_doc[tid];
+  const int c0 = tile * 64, nvv = min(64, V - c0), k0 = kc * ckb, kn = min(ckb, C - k0);
+  const int H0Q = rup(H0, 4);
+  const BwdLds L = bwd_lds(m);
+  float* dzs = smem + L.dz;
+  float* wcs = smem + L.wc;
+  float* das = smem + L.da;
+  float* xcs = smem + L.xc;
+  const float* wcg = m.w_in + (size_t)V * H0;
+  const int nb = *m.ws_nb;
+  const bool fused = m.update_mode == 1;
+
+  // ---- g_Wa^T output tiles of this wave: (vt, ct) = (t & 3, t >> 2), t = wave + 16 u.
+  //      The product is formed transposed (C chunk x vocab) so each lane owns 4
+  //      consecutive C positions of one Wa row: p / m / v move as float4 ----
+  const int NCT = ckb / 16;
+  constexpr int MAXU = 4;               // ckb <= 256
+  f32x4 pp[MAXU], pm[MAXU], pv[MAXU];
+  const int li = lane & 15, lj = (lane >> 4) * 4;
+#pragma unroll
+  for (int u = 0; u < MAXU; ++u) {
+    const int t = wave + CW * u, vt = t & 3, ct = t >> 2;
+    const int i = vt * 16 + li, j = ct * 16 + lj;
+    pp[u] = pm[u] = pv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (fused && ct < NCT && i < nvv && j < kn) {     // kn % 4 == 0: whole float4 in range
+      const f32x4* p = reinterpret_cast<const f32x4*>(m.w_a + (size_t)(c0 + i) * C + k0 + j);
+      pp[u] = p[0];
+      pm[u] = p[m.off_m / 4];
+      pv[u] = p[m.off_v / 4];
+    }
+  }
+  // ---- one staging round: dz0 (rows >= nb zero), Wc tile, x_ctx chunk; the
+  //      dz0 / Wc loads are in flight while the doc ids reach LDS ----
+  const float* dz0 = m.ws_dz[0];
+  const float* ctx = m.ctx;
+  auto ld_dz = [&](int i) {
+    const int b = i / H0Q, j = i - b * H0Q;
+    return (b < nb && j < H0) ? dz0[b * H0 + j] : 0.f;
+  };
+  auto st_dz = [&](int i, float x) { const int b = i / H0Q; dzs[b * L.ldz + i - b * H0Q] = x; };
+  auto ld_wc = [&](int i) {
+    const int v = i / H0Q, j = i - v * H0Q;
+    return (v < nvv && j < H0) ? wcg[(size_t)(c0 + v) * H0 + j] : 0.f;
+  };
+  auto st_wc = [&](int i, float x) { const int v = i / H0Q; wcs[v * L.ldz + i - v * H0Q] = x; };
+  float rdz[4], rwc[4];
+  reg_load<4>(rdz, BM * H0Q, ld_dz);
+  reg_load<4>(rwc, 64 * H0Q, ld_wc);
+  __syncthreads();          // docs_s
+  auto ld_xc = [&](int i) {
+    const int b = i / ckb, k = i - b * ckb;
+    return (b < nb && k < kn) ? ctx[(size_t)docs_s[b] * C + k0 + k] : 0.f;
+  };
+  auto st_xc = [&](int i, float x) { const int b = i / ckb; xcs[b * L.ldxb + i - b * ckb] = x; };
+  float rxc[8];
+  reg_load<8>(rxc, BM * ckb, ld_xc);
+  reg_store<4>(rdz, BM * H0Q, ld_dz, st_dz);
+  reg_store<4>(rwc, 64 * H0Q, ld_wc, st_wc);
+  reg_store<8>(rxc, BM * ckb, ld_xc, st_xc);
+  __syncthreads();
+
+  // ---- dA [BM, 64] = dz0 Wc_tile^T ----
+  constexpr int RT = BM / 16;
+  for (int t = wave; t < RT * 4; t += CW) {
+    const int rt = t >> 2, vt = t & 3;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const float* ap = dzs + (rt * 16 + (lane & 15)) * L.ldz + (lane >> 4);
+    const float* bp = wcs + (vt * 16 + (lane & 15)) * L.ldz + (lane >> 4);
+    for (int k = 0; k < H0Q; k += 4) acc = mfma16x16x4(ap[k], bp[k], acc);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) das[(rt * 16 + (lane >> 4) * 4 + r) * 80 + vt * 16 + (lane & 15)] = acc[r];
+  }
+  lds_barrier();
+
+  const AdamCoef ac = adam_coef(m);
+  // ---- g_ba = column sums of dA (chunk 0): 16 lanes per column ----
+  if (kc == 0) {
+    const int v = tid >> 4, sub = tid & 15;
+    float s = 0.f;
+    for (int b = sub; b < BM; b += 16) s += das[b * 80 + v];
+    s = row16_sum(s);
+    if (sub == 0 && v < nvv) param_update(m, m.b_a + c0 + v, s, ac, is_shared(m, m.b_a));
+  }
+  // ---- g_Wa^T [chunk, 64] = x_ctx^T dA and the update ----
+  const bool sh = is_shared(m, m.w_a);
+#pragma unroll
+  for (int u = 0; u < MAXU; ++u) {
+    const int t = wave + CW * u, vt = t & 3, ct = t >> 2;
+    if (ct >= NCT) break;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const float* ap = xcs + (lane >> 4) * L.ldxb + ct * 16 + li;
+    const float* bp = das + (lane >> 4) * 80 + vt * 16 + li;
+    for (int b = 0; b < BM; b += 4) acc = mfma16x16x4(ap[b * L.ldxb], bp[b * 80], acc);
+    const int i = vt * 16 + li, j = ct * 16 + lj;
+    if (i >= nvv || j >= kn) continue;
+    f32x4* p = reinterpret_cast<f32x4*>(m.w_a + (size_t)(c0 + i) * C + k0 + j);
+    if (!fused) {
+      p[m.off_g / 4] = acc;
+    } else {
+      f32x4 np, mo = pm[u], vo = pv[u];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float a = mo[r], b2 = vo[r];
+        float x = adam_update(pp[u][r], acc[r], a, b2, ac);
+        if (sh && m.fed_scale_on) x *= m.fed_scale;
+        mo[r] = a;
+        vo[r] = b2;
+        np[r] = x;
+      }
+      p[m.off_m / 4] = mo;
+      p[m.off_v / 4] = vo;
+      p[0] = np;
+    }
+  }
+}
+
+extern "C" size_t gfk_ctx_smem(const GfkModel* m) {
+  const size_t a = fwd_lds_floats(*m), b = bwd_lds(*m).total;
+  return sizeof(float) * (a > b ? a : b);
+}
+
+extern "C" int gfk_ctx_set_smem(size_t bytes) {
+  const void* ks[] = {(const void*)gfk_ctx_fwd_k<16>, (const void*)gfk_ctx_fwd_k<32>,
+                      (const void*)gfk_ctx_fwd_k<64>, (const void*)gfk_ctx_fwd_k<128>,
+                      (const void*)gfk_ctx_bwd_k<16>, (const void*)gfk_ctx_bwd_k<32>,
+                      (const void*)gfk_ctx_bwd_k<64>, (const void*)gfk_ctx_bwd_k<128>};
+  for (const void* k : ks) {
+    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e != hipSuccess) return (int)e;
+  }
+  return 0;
+}
+
+// Host checks mirror the kernels' assumptions: the backward chunk a multiple of 16
+// and <= 256 (prefetch slots), H0 <= 512, float4-aligned contextual rows / Wa.
+static bool ctx_ok(const GfkModel* m) {
+  return m->ctx_fused && m->ctx && m->ws_actx && m->ws_hpart && m->ctx_ckb > 0 &&
+         m->ctx_ckb % 16 == 0 && m->ctx_ckb <= 256 && m->H[0] <= 512 && m->C % 4 == 0 &&
+         (uintptr_t)m->ctx % 16 == 0 && (uintptr_t)m->w_a % 16 == 0 && m->off_m % 4 == 0 &&
+         m->off_v % 4 == 0 && m->off_g % 4 == 0 &&
+         (int64_t)m->ctx_kb * m->ctx_ckb >= m->C;
+}
+
+extern "C" int gfk_launch_ctx_fwd(const GfkModel* m, hipStream_t s) {
+  if (!ctx_ok(m)) return -9;
+  const dim3 g(8 * ((m->n_tiles + 7) / 8) * (m->bmax / 16)), t(FT);
+  const size_t sm = sizeof(float) * fwd_lds_floats(*m);
+  switch (m->bmax) {
+    case 16: hipLaunchKernelGGL(gfk_ctx_fwd_k<16>, g, t, sm, s, *m); break;
+    case 32: hipLaunchKernelGGL(gfk_ctx_fwd_k<32>, g, t, sm, s, *m); break;
+    case 64: hipLaunchKernelGGL(gfk_ctx_fwd_k<64>, g, t, sm, s, *m); break;
+    case 128: hipLaunchKernelGGL(gfk_ctx_fwd_k<128>, g, t, sm, s, *m); break;
+    default: return -1;
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int gfk_launch_ctx_bwd(const GfkModel* m, hipStream_t s) {
+  if (!ctx_ok(m)) return -9;
+  const dim3 g(m->n_tiles * m->ctx_kb), t(CT);
+  const size_t sm = sizeof(float) * bwd_lds(*m).total;
+  switch (m->bmax) {
+    case 16: hipLaunchKernelGGL(gfk_ctx_bwd_k<16>, g, t, sm, s, *m); break;
+    case 32: hipLaunchKernelGGL(gfk_ctx_bwd_k<32>, g, t, sm, s, *m); break;
+    case 64: hipLaunchKernelGGL(gfk_ctx_bwd_k<64>, g, t, sm, s, *m); break;
+    case 128: hipLaunchKernelGGL(gfk_ctx_bwd_k<128>, g, t, sm, s, *m); break;
+    default: return -1;
+  }
+  return (int)hipGetLastError();
+}

@@ -181,6 +181,25 @@ __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkModel m) {
     else if (H0 <= 128) gather_rows<2>(indices, values, e0, e1, wave, w_in, H0, lane, acc);
     else if (H0 <= 256) gather_rows<4>(indices, values, e0, e1, wave, w_in, H0, lane, acc);
     else gather_rows<8>(indices, values, e0, e1, wave, w_in, H0, lane, acc);
+    if (m.ctx_fused) {      // CombinedTM: the row's contextual partials from ctx_fwd (fixed order)
+      const int P = m.n_tiles;
+      const size_t ps = (size_t)bmax * H0;
+      const float* hp = m.ws_hpart + (size_t)b * H0;
+      for (int p0 = wave; p0 < P; p0 += 4 * ENC_WAVES) {
+        float hv[4][8];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int p = min(p0 + u * ENC_WAVES, P - 1);
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            hv[u][q] = 64 * q < H0 ? hp[(size_t)p * ps + min(lane + 64 * q, H0 - 1)] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int q = 0; q < 8; ++q) acc[q] += p0 + u * ENC_WAVES < P ? hv[u][q] : 0.f;
+      }
+    }
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int j = lane + 64 * q;
@@ -226,7 +245,7 @@ __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkModel m) {
 #pragma unroll
       for (int w = 0; w < ENC_WAVES; ++w) z += red[w * H0 + tid];
     }
-    if (input != GFK_IN_BOW) z += m.ws_hctx[(size_t)b * H0 + tid];
+    if (input != GFK_IN_BOW && !m.ctx_fused) z += m.ws_hctx[(size_t)b * H0 + tid];
     float a = act_f(act, z);
     m.ws_z[0][(size_t)b * H0 + tid] = z;
     m.ws_a[0][(size_t)b * H0 + tid] = a;

@@ -115,6 +115,15 @@ typedef struct GfkModel {
   double *adam_pow;              // [2] beta1^t, beta2^t (advanced on device with t)
   float *adam_coef;              // [2] lr / (1 - beta1^t), 1 / sqrt(1 - beta2^t)
   float *ws_dtheta;              // [bmax, K] reduced d theta_d
+
+  // ---- CombinedTM contextual path on the fused kernels (csrc/ctx.hip) ----
+  float *w_a, *b_a;              // adapt_bert.weight [V, C], adapt_bert.bias [V]
+  float *ws_actx;                // [n_tiles][bmax][64] adapted rows A (ctx_fwd)
+  float *ws_hpart;               // [n_tiles][bmax][H0] per-tile contextual z0 terms
+  int32_t ctx_fused;             // 1: adapt_bert + contextual input layer in ctx_fwd / ctx_bwd /
+                                 //    win_update (no host GEMMs)
+  int32_t ctx_kb, ctx_ckb;       // backward: C split into ctx_kb chunks of ctx_ckb
+  int32_t pad2;
 } GfkModel;
 
 // Gradient + update jobs of the small tensors, run by the update kernel next to

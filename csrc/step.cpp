@@ -27,6 +27,10 @@ int gfk_launch_lda_row(const GfkModel*, hipStream_t);
 int gfk_launch_lda_beta_bwd(const GfkModel*, hipStream_t);
 int gfk_launch_adam(const GfkAdam*, int, hipStream_t);
 int gfk_launch_scale(float*, int64_t, float, hipStream_t);
+int gfk_launch_ctx_fwd(const GfkModel*, hipStream_t);
+int gfk_launch_ctx_bwd(const GfkModel*, hipStream_t);
+size_t gfk_ctx_smem(const GfkModel*);
+int gfk_ctx_set_smem(size_t);
 size_t gfk_prodlda_fwd_smem(const GfkModel*);
 size_t gfk_prodlda_bwd_smem(const GfkModel*);
 size_t gfk_lda_fwd_smem(int);
@@ -55,6 +59,8 @@ enum GfkPhase {
   GFK_PH_ENC_BWD = 10,
   GFK_PH_ADAM = 11,
   GFK_PH_BATCH_PREP = 12,
+  GFK_PH_CTXF_FWD = 13,
+  GFK_PH_CTXF_BWD = 14,
 };
 
 
@@ -69,6 +75,7 @@ size_t gfk_smem_required(const GfkModel* m, int which) {
     case 4: return gfk_post_smem(m);
     case 5: return gfk_win_update_smem(m);
     case 7: return gfk_enc_in_smem(m);
+    case 8: return m->ctx_fused ? gfk_ctx_smem(m) : 0;
     default: return 0;
   }
 }
@@ -84,6 +91,7 @@ int gfk_setup(const GfkModel* m) {
   if ((e = gfk_lda_set_smem(p > q ? p : q))) return e;
   if ((e = gfk_enc_in_set_smem(gfk_enc_in_smem(m)))) return e;
   if ((e = gfk_post_set_smem(gfk_post_smem(m)))) return e;
+  if (m->ctx_fused && (e = gfk_ctx_set_smem(gfk_ctx_smem(m)))) return e;
   return gfk_win_update_set_smem(gfk_win_update_smem(m));
 }
 
@@ -107,6 +115,8 @@ int gfk_run(const GfkModel* m, const GfkAdam* a, int adam_grid, const GfkUpdate*
       case GFK_PH_ENC_BWD: e = gfk_launch_win_update(m, u, s); break;
       case GFK_PH_ADAM: e = gfk_launch_adam(a, adam_grid, s); break;
       case GFK_PH_BATCH_PREP: e = gfk_launch_batch_prep(m, s); break;
+      case GFK_PH_CTXF_FWD: e = gfk_launch_ctx_fwd(m, s); break;
+      case GFK_PH_CTXF_BWD: e = gfk_launch_ctx_bwd(m, s); break;
       default: e = -2;
     }
     if (e) return e * 100 + phases[i];

@@ -195,9 +195,11 @@ class FusedEngine(EngineBase):
         self.adam_t = torch.zeros(1, dtype=torch.int32, device=dev)
         self.adam_pow = torch.ones(2, dtype=torch.float64, device=dev)     # beta1^t, beta2^t
         self.adam_coef = torch.zeros(2, dtype=torch.float32, device=dev)   # see csrc/gfk_common.h
-        # fused epilogue updates: ProdLDA AVITM; NeuralLDA and CTM (whose contextual
-        # tensors get their gradients from host-issued GEMMs) run the generic Adam
-        self.update_mode = UPDATE_FUSED if tm.kind != "ctm" else UPDATE_GRAD
+        # fused epilogue updates: AVITM and CombinedTM (contextual path on ctx_fwd /
+        # ctx_bwd); ZeroShotTM, whose dense input layer comes from host-issued GEMMs,
+        # runs the generic Adam
+        self.ctx_fused = tm.kind == "ctm" and tm.inference_type == "combined"
+        self.update_mode = UPDATE_FUSED if (tm.kind != "ctm" or self.ctx_fused) else UPDATE_GRAD
         self.lr, self.beta1, self.beta2 = float(tm.lr), float(tm.momentum), 0.99
         self.eps, self.weight_decay = 1e-8, 0.0
         self.fedavg_scale: Optional[float] = None
@@ -237,8 +239,8 @@ class FusedEngine(EngineBase):
     def set_update_mode(self, mode: int):
         """UPDATE_FUSED: optimizer in the kernel epilogues; UPDATE_GRAD: kernels write
         gradients and the generic Adam kernel follows."""
-        if mode == UPDATE_FUSED and self.kind == "ctm":
-            raise ValueError("the fused update mode covers the AVITM models only")
+        if mode == UPDATE_FUSED and self.kind == "ctm" and not self.ctx_fused:
+            raise ValueError("the fused update mode covers AVITM and CombinedTM only")
         self.update_mode = mode
         self._m.update_mode = mode
         self._rebuild_adam()
@@ -271,9 +273,11 @@ class FusedEngine(EngineBase):
             m.C = tm.contextual_size
         else:
             m.input = abi.IN_BOW
+        props = torch.cuda.get_device_properties(self.device)
+        if self.ctx_fused:
+            self._plan_ctx(props.multi_processor_count)
         m.vb = VB
         m.n_tiles = -(-m.V // VB)
-        props = torch.cuda.get_device_properties(self.device)
         m.dec_grid = int(min(m.n_tiles, 2 * props.multi_processor_count))
         m.learn_priors = int(tm.learn_priors)
         m.kt = theta_stride(m.K)
@@ -316,6 +320,8 @@ class FusedEngine(EngineBase):
         m.nbt_s = net.f_sigma_batchnorm.num_batches_tracked.data_ptr()
         m.nbt_beta = model.beta_batchnorm.num_batches_tracked.data_ptr()
         m.step, m.adam_t = self.d_step.data_ptr(), self.adam_t.data_ptr()
+        if self.ctx_fused:
+            m.w_a, m.b_a = self._ptr(P, "inf_net.adapt_bert.weight"), self._ptr(P, "inf_net.adapt_bert.bias")
         # optimizer (fused epilogues + generic Adam)
         m.update_mode = self.update_mode
         m.flat_base = P.data_ptr()
@@ -327,7 +333,7 @@ class FusedEngine(EngineBase):
         self._sync_opt_fields()
         which = (0, 1) if m.kind == abi.KIND_PRODLDA else (2, 3)
         need = lambda: max(self.lib.gfk_smem_required(C.byref(m), w)  # noqa: E731
-                           for w in which + (4, 5, 7))
+                           for w in which + (4, 5, 7, 8))
         for flags in STAGE_PLANS:         # first plan that fits the 160 KiB of LDS
             m.stage_flags = flags
             if need() <= LDS_LIMIT:
@@ -349,6 +355,25 @@ class FusedEngine(EngineBase):
         rc = self.lib.gfk_setup(C.byref(m))
         if rc:
             raise RuntimeError(f"gfk_setup failed ({rc})")
+
+    def _plan_ctx(self, cu: int):
+        """Fused CombinedTM contextual kernels (csrc/ctx.hip).  The forward runs one
+        workgroup per (vocab tile, 16-row block); the backward splits C into chunks
+        of 16k <= 256 floats, enough of them that n_tiles x chunks covers the CUs
+        once (one 16-wave workgroup per CU).  Falls back to the host GEMMs when a shape is outside
+        the kernels' assumptions (C % 4, H0 <= 512, LDS)."""
+        m = self._m
+        n_tiles, Cs = -(-int(m.V) // VB), int(m.C)
+        k = max(1, min(cu // n_tiles, -(-Cs // 16)))      # one round, one workgroup per CU
+        m.ctx_ckb = min(256, -(-(-(-Cs // k)) // 16) * 16)
+        m.ctx_kb = -(-Cs // m.ctx_ckb)
+        m.ctx_fused = 1
+        aligned = self.flat.slots["inf_net.adapt_bert.weight"].offset % 4 == 0
+        if (self.lib.gfk_smem_required(C.byref(m), 8) > LDS_LIMIT or int(m.H[0]) > 512
+                or Cs % 4 or not aligned):
+            m.ctx_fused, m.ctx_kb = 0, 0
+            self.ctx_fused = False
+            self.update_mode = UPDATE_GRAD
 
     def _alloc_workspace(self):
         m, dev = self._m, self.device
@@ -376,6 +401,10 @@ class FusedEngine(EngineBase):
             "tstart": torch.zeros(B * (m.n_tiles + 1), dtype=torch.int32, device=dev),
             "erange": torch.zeros(2 * B, dtype=torch.int32, device=dev),
             "next": torch.zeros(1 + 3 * B, dtype=torch.int32, device=dev),
+            # fused CombinedTM: the adapted rows per vocab tile and their contextual
+            # pre-activation partials (csrc/ctx.hip)
+            "actx": f(m.n_tiles * B * 64 if m.ctx_fused else 1),
+            "hpart": f(m.n_tiles * B * hs[0] if m.ctx_fused else 1),
         }
         for i, h in enumerate(hs):
             ws[f"z{i}"] = f(B, h)
@@ -524,7 +553,10 @@ class FusedEngine(EngineBase):
                 ([abi.PH_ADAM] if self.update_mode == UPDATE_GRAD else [])
         else:
             ph = abi.PRODLDA_STEP + ([abi.PH_ADAM] if self.update_mode == UPDATE_GRAD else [])
-        if self.kind == "ctm":
+        if self.ctx_fused:
+            ph.insert(ph.index(abi.PH_ENC_FWD), abi.PH_CTXF_FWD)
+            ph.insert(ph.index(abi.PH_ENC_BWD), abi.PH_CTXF_BWD)
+        elif self.kind == "ctm":
             ph.insert(ph.index(abi.PH_ENC_FWD), abi.PH_CTX_FWD)
             ph.insert(ph.index(abi.PH_ENC_BWD) + 1, abi.PH_CTX_BWD)
         if self._comm is not None and self._comm["mode"] == "graph":
@@ -758,7 +790,7 @@ class FusedEngine(EngineBase):
 
     def _capture(self):
         # warm-up on a side stream is not needed: no lazy allocation in gfk_run
-        if self._ctx is not None:
+        if self._ctx is not None and not self.ctx_fused:
             # hipBLASLt picks algorithms / workspaces on a shape's first call, which is
             # not allowed while capturing: run the host GEMMs once eagerly (their
             # outputs are fully rewritten by the next step before anything reads them)

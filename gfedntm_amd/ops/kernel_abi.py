@@ -31,6 +31,8 @@ PH_LDA_BETA_BWD = 9
 PH_ENC_BWD = 10
 PH_ADAM = 11
 PH_BATCH_PREP = 12
+PH_CTXF_FWD = 13      # CombinedTM contextual forward on the fused kernels (ctx_fwd)
+PH_CTXF_BWD = 14      # ... and its backward + adapt_bert updates (ctx_bwd)
 
 # PH_ENC_FWD = enc_in (sparse gather, MLP, heads, random draws), PH_POST_FWD =
 # post_fwd (batch-norm, reparameterisation, softmax, KL), PH_POST_BWD = row_bwd +
@@ -91,6 +93,9 @@ class GfkModel(C.Structure):
         ("fed_scale_on", C.c_int32), ("flat_base", P), ("n_shared", C.c_int64),
         ("off_m", C.c_int64), ("off_v", C.c_int64), ("off_g", C.c_int64),
         ("adam_pow", P), ("adam_coef", P), ("ws_dtheta", P),
+        ("w_a", P), ("b_a", P), ("ws_actx", P), ("ws_hpart", P),
+        ("ctx_fused", C.c_int32), ("ctx_kb", C.c_int32), ("ctx_ckb", C.c_int32),
+        ("pad2", C.c_int32),
     ]
 
 

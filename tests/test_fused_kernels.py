@@ -214,14 +214,16 @@ def test_training_decreases_loss():
     assert h[-10:].mean() < 0.9 * h[:10].mean()
 
 
-@pytest.mark.parametrize("inference_type", ["combined", "zeroshot"])
+@pytest.mark.parametrize("inference_type,Cdim", [("combined", 96), ("combined", 100),
+                                                 ("combined", 16), ("zeroshot", 96)])
 @pytest.mark.parametrize("model_type", ["prodLDA", "LDA"])
-def test_ctm_step_matches_oracle(inference_type, model_type):
-    """CTM on the fused engine: host GEMMs for the contextual path around the HIP
-    kernels; compared with the explicit-noise oracle through the CTM encoder."""
+def test_ctm_step_matches_oracle(inference_type, Cdim, model_type):
+    """CTM on the fused engine: CombinedTM's contextual path on ctx_fwd / ctx_bwd
+    (csrc/ctx.hip, C split into chunks), ZeroShotTM's dense input layer on host GEMMs;
+    compared with the explicit-noise oracle through the CTM encoder (gradient mode)."""
     from gfedntm_amd.models import CombinedTM, ZeroShotTM
     cls = CombinedTM if inference_type == "combined" else ZeroShotTM
-    V, K, H, B, Cdim, n_docs = 600, 20, (32, 24), 64, 96, 150
+    V, K, H, B, n_docs = 600, 20, (32, 24), 64, 150
     torch.manual_seed(0)
     kw = dict(input_size=V, contextual_size=Cdim, n_components=K, model_type=model_type,
               hidden_sizes=H, batch_size=B, verbose=False, device="cuda")
@@ -234,9 +236,14 @@ def test_ctm_step_matches_oracle(inference_type, model_type):
     data = DeviceCSR(X, "cuda", contextual=ctx)
     plan = BatchPlan.build(data.n_docs, B, 3, seed=0)
     e = fused.engine
+    if inference_type == "combined":
+        assert e.update_mode == UPDATE_FUSED and (e._m.ctx_kb > 1) == (Cdim > 16)
+        e.set_update_mode(UPDATE_GRAD)
     e.bind_data(data, plan)
     phases = e.phases()
-    assert phases[-1] == abi.PH_ADAM and abi.PH_CTX_FWD in phases and abi.PH_CTX_BWD in phases
+    ctx_ph = (abi.PH_CTXF_FWD, abi.PH_CTXF_BWD) if inference_type == "combined" else \
+        (abi.PH_CTX_FWD, abi.PH_CTX_BWD)
+    assert phases[-1] == abi.PH_ADAM and all(p in phases for p in ctx_ph)
     e.run_phases(phases[:-1])
     torch.cuda.synchronize()
     nb = int(plan.size[0])
@@ -259,6 +266,41 @@ def test_ctm_step_matches_oracle(inference_type, model_type):
     e.run_phases([abi.PH_ADAM])
     torch.cuda.synchronize()
     assert float(e.grad.abs().max().item()) == 0.0
+
+
+@pytest.mark.parametrize("model_type", ["prodLDA", "LDA"])
+def test_ctm_fused_update_matches_gradient_mode(model_type):
+    """CombinedTM: Adam fused into ctx_bwd (adapt_bert) and win_update's contextual
+    tiles (input layer) == gradient mode + the generic Adam, with the FedAvg pre-scale."""
+    from gfedntm_amd.models import CombinedTM
+    V, K, B, Cdim, n_docs = 700, 30, 64, 136, 200
+    torch.manual_seed(0)
+    kw = dict(input_size=V, contextual_size=Cdim, n_components=K, hidden_sizes=(48, 40),
+              batch_size=B, verbose=False, device="cuda", backend="fused", model_type=model_type)
+    a, b = CombinedTM(**kw), CombinedTM(**kw)
+    b.model.load_state_dict(a.model.state_dict())
+    b.engine.seed = b.engine._m.seed = a.engine.seed
+    b.engine.set_update_mode(UPDATE_GRAD)
+    X = random_csr(n_docs, V, 40, seed=3)
+    ctx = np.random.default_rng(4).standard_normal((n_docs, Cdim)).astype(np.float32)
+    for t in (a, b):
+        t.engine.set_fedavg_scale(0.75)
+        t.engine.bind_data(DeviceCSR(X, "cuda", contextual=ctx), BatchPlan.build(n_docs, B, 5, seed=0))
+    for s in range(5):
+        a.engine.step(s)
+        b.engine.step(s)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(a.engine.loss_hist, b.engine.loss_hist, rtol=1e-4, atol=1e-2)
+    sa, sb = a.model.state_dict(), b.model.state_dict()
+    lr_steps = 2 * a.engine.lr * 5
+    for k in sb:
+        if not sb[k].is_floating_point():
+            assert torch.equal(sa[k], sb[k]), k
+            continue
+        noisy = k in _NOISE_KEYS or k.startswith(("inf_net.f_mu_batchnorm.running_mean",
+                                                   "inf_net.f_sigma_batchnorm.running_mean"))
+        torch.testing.assert_close(sa[k], sb[k], rtol=1e-3, atol=lr_steps if noisy else 5e-5,
+                                   msg=lambda m: f"{k}: {m}")
 
 
 def test_ctm_graph_training():
@@ -297,7 +339,7 @@ def test_steps_are_bitwise_deterministic(model_type):
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
 
-@pytest.mark.parametrize("model_type", ["prodLDA", "LDA"])
+@pytest.mark.parametrize("model_type", ["prodLDA", "LDA", "ctm"])
 @pytest.mark.parametrize("mode", [UPDATE_FUSED, UPDATE_GRAD])
 def test_fedavg_prescale_covers_every_shared_tensor(model_type, mode):
     """One step with the FedAvg pre-scale w must leave w x (the unscaled step) in EVERY
@@ -306,15 +348,24 @@ def test_fedavg_prescale_covers_every_shared_tensor(model_type, mode):
     torch.manual_seed(0)
     kw = dict(input_size=700, n_components=20, hidden_sizes=(32, 24), batch_size=64,
               verbose=False, device="cuda", model_type=model_type)
-    a, b = AVITM(backend="fused", **kw), AVITM(backend="fused", **kw)
+    X = random_csr(150, 700, 40, seed=1)
+    if model_type == "ctm":           # CombinedTM (adapt_bert + contextual input half)
+        from gfedntm_amd.models import CombinedTM
+        kw.update(model_type="prodLDA", contextual_size=80)
+        a, b = CombinedTM(backend="fused", **kw), CombinedTM(backend="fused", **kw)
+        ctx = np.random.default_rng(4).standard_normal((150, 80)).astype(np.float32)
+        bind = lambda t: t.engine.bind_data(DeviceCSR(X, "cuda", contextual=ctx),  # noqa: E731
+                                            BatchPlan.build(150, 64, 1, seed=0))
+    else:
+        a, b = AVITM(backend="fused", **kw), AVITM(backend="fused", **kw)
+        bind = lambda t: _bind(t, X, n_steps=1)  # noqa: E731
     b.model.load_state_dict(a.model.state_dict())
     b.engine.seed = b.engine._m.seed = a.engine.seed
     for e in (a.engine, b.engine):
         e.set_update_mode(mode)
     a.engine.set_fedavg_scale(0.25)
-    X = random_csr(150, 700, 40, seed=1)
-    _bind(a, X, n_steps=1)
-    _bind(b, X, n_steps=1)
+    bind(a)
+    bind(b)
     a.engine.step(0)
     b.engine.step(0)
     torch.cuda.synchronize()

@@ -100,7 +100,7 @@ def _hang_worker(rank, world, port, tmp):
     sc = generate_synthetic(vocab_size=60, n_topics=5, n_docs=30, n_nodes=2, frozen_topics=1,
                             nwords=(10, 20), seed=2)
     run_distributed(ClientCorpus(synthetic=sc, node=rank), params, max_iters=50,
-                    backend="torch", heartbeat_timeout=3.0)
+                    backend="torch", heartbeat_timeout=10.0)
 
 
 def test_hung_peer_aborts_the_waiting_rank(tmp_path):

@@ -17,7 +17,7 @@ LIB = os.path.join(ROOT, "gfedntm_amd", "_lib")
 OBJ = os.path.join(ROOT, "build", "obj")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-KERNEL_SRCS = ["encoder.hip", "posterior.hip", "prodlda.hip", "neurallda.hip", "update.hip",
+KERNEL_SRCS = ["ctx.hip", "encoder.hip", "posterior.hip", "prodlda.hip", "neurallda.hip", "update.hip",
                "adam.hip", "comm.hip", "infer.hip", "step.cpp"]
 RUNTIME_SRCS = ["runtime.cpp"]
 
