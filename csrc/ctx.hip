@@ -9,18 +9,20 @@
 //   ctx_fwd (before enc_in), one workgroup per (vocab tile t, 16-row block r):
 //       A_rt  = x_ctx[rows r] Wa[tile t]^T + ba[tile t]                      [16, 64]
 //       P_rt  = A_rt Wc[tile t]                                              [16, H0]
-//     the MFMA operands come straight from global memory as float4 (lane group g
-//     holds k = 16 s + 4 g + j for MFMA step j: A and B agree on the k permutation),
-//     the four waves of a 16x16 output tile split the C reduction, and the row
-//     blocks of one tile are dealt to the same XCD so Wa[tile t] is read once per L2.
-//     A is kept for the backward (ws_actx); enc_in adds sum_t P_t to its row's
-//     pre-activation (fixed order: deterministic).
+//     C is walked in chunks of 128: the x_ctx rows and the Wa tile of a chunk are
+//     loaded as coalesced float4 rows (two chunks in flight in registers) and
+//     staged in LDS for the MFMA; the row blocks of one tile are dealt to the same
+//     XCD so Wa[tile t] comes from HBM once per L2.  A is kept for the backward
+//     (ws_actx); enc_in adds sum_t P_t to its row's pre-activation (fixed order:
+//     deterministic).
 //   ctx_bwd (after post_bwd, before win_update), grid n_tiles x kb, (tile t, chunk k):
 //       dA_t  = dz0 Wc[tile t]^T                                             [B, 64]
 //       g_ba  = sum_b dA_t                              (chunk 0; Adam on ba)
 //       g_Wa  = dA_t^T x_ctx[:, chunk k]                (Adam on Wa[tile t, chunk k])
-//     Wc's own gradient A^T dz0 is a dense tile of win_update (same MFMA + Adam
-//     epilogue as the bag-of-words half), which runs after ctx_bwd has read Wc.
+//     the g_Wa tile goes through LDS so the Adam epilogue moves p / m / v as
+//     coalesced float4 rows (prefetched before the products).  Wc's own gradient
+//     A^T dz0 is a dense tile of win_update (same MFMA + Adam epilogue as the
+//     bag-of-words half), which runs after ctx_bwd has read Wc.
 //
 // All products are fp32 MFMA (v_mfma_f32_16x16x4_f32); operand tiles are staged in
 // LDS with strides 2 mod 4 (A-role reads: 16 rows x 2 k per half-wave) or 16 mod 32
@@ -35,6 +37,8 @@ using namespace gfk;
 namespace {
 constexpr int CT = 1024;
 constexpr int CW = CT / 64;
+constexpr int FT = 512;                 // forward workgroup
+constexpr int FK = 128, LDK = 130;      // forward C chunk, its LDS stride (2 x odd)
 __host__ __device__ inline int rup(int x, int m) { return (x + m - 1) / m * m; }
 __host__ __device__ inline int stride_a(int w) {     // 2 x odd
   int s = rup(w, 2);
@@ -44,51 +48,35 @@ __host__ __device__ inline int stride_b(int w) {     // 16 mod 32 (w: multiple o
   return w % 32 == 16 ? w : w + 16;
 }
 
-// forward LDS: the 2 C-half partials of A [2][16][68], A [16][66], Wc tile [64][ldc]
+// forward LDS: x_ctx chunk [16][LDK] + Wa chunk [64][LDK], the 2 C-half partials of
+// A [2][16][68], A [16][66], Wc tile [64][ldc]
 __host__ __device__ inline int fwd_ldc(const GfkModel& m) { return stride_b(rup(m.H[0], 16)); }
 __host__ __device__ inline int fwd_lds_floats(const GfkModel& m) {
-  return 2 * 16 * 68 + 16 * 66 + 64 * fwd_ldc(m);
+  return 80 * LDK + 2 * 16 * 68 + 16 * 66 + 64 * fwd_ldc(m);
 }
 
 struct BwdLds {
-  int ldz, ldxb, dz, wc, da, xc, total;
+  int ldz, ldxb, gs, dz, wc, da, xc, g, total;
 };
 __host__ __device__ inline BwdLds bwd_lds(const GfkModel& m) {
   BwdLds L;
   const int B = m.bmax;
   L.ldz = stride_a(rup(m.H[0], 4));
   L.ldxb = stride_b(m.ctx_ckb);
+  L.gs = m.ctx_ckb + 4;                 // g_Wa tile rows: 4 x stride = 16 mod 32
   int o = 0;
   L.dz = o; o += B * L.ldz;
   L.wc = o; o += 64 * L.ldz;
   L.da = o; o += B * 80;
   L.xc = o; o += B * L.ldxb;
-  L.total = o;
+  L.g = L.da;                           // reuses dA / x_ctx once the products are done
+  L.total = o > L.g + 64 * L.gs ? o : L.g + 64 * L.gs;
   return L;
-}
-// Global -> LDS copy of elements [i0, n) with NR loads in flight per thread: the
-// loads of a group are all issued before the first LDS store (a plain strided loop
-// would wait out one memory latency per element).
-template <int NR, int NT = CT, typename Ld, typename St>
-__device__ __forceinline__ void staged_copy(int i0, int n, Ld ld, St st) {
-  for (int base = i0 + (int)threadIdx.x; base < n; base += NR * NT) {
-    float r[NR];
-#pragma unroll
-    for (int u = 0; u < NR; ++u) {
-      const int i = base + u * NT;
-      r[u] = i < n ? ld(i) : 0.f;
-    }
-#pragma unroll
-    for (int u = 0; u < NR; ++u) {
-      const int i = base + u * NT;
-      if (i < n) st(i, r[u]);
-    }
-  }
 }
 
 // Split staging: reg_load issues the first NR * NT elements' loads into registers,
 // reg_store writes them to LDS later (other loads can be issued in between) and
-// copies any remainder (wide shapes) with staged_copy.
+// copies any remainder (wide shapes) in further groups of NR loads per thread.
 template <int NR, int NT = CT, typename Ld>
 __device__ __forceinline__ void reg_load(float (&r)[NR], int n, Ld ld) {
 #pragma unroll
@@ -104,36 +92,45 @@ __device__ __forceinline__ void reg_store(const float (&r)[NR], int n, Ld ld, St
     const int i = (int)threadIdx.x + u * NT;
     if (i < n) st(i, r[u]);
   }
-  if (n > NR * NT) staged_copy<NR, NT>(NR * NT, n, ld, st);
+  for (int base = NR * NT + (int)threadIdx.x; base < n; base += NR * NT) {
+    float q[NR];
+#pragma unroll
+    for (int u = 0; u < NR; ++u) q[u] = base + u * NT < n ? ld(base + u * NT) : 0.f;
+#pragma unroll
+    for (int u = 0; u < NR; ++u)
+      if (base + u * NT < n) st(base + u * NT, q[u]);
+  }
 }
 
+__device__ __forceinline__ void st_f4_as_f2(float* p, const f32x4& x) {   // 8-byte aligned LDS
+  reinterpret_cast<float2*>(p)[0] = make_float2(x[0], x[1]);
+  reinterpret_cast<float2*>(p)[1] = make_float2(x[2], x[3]);
+}
 }  // namespace
 
 // grid: 8 * ceil(n_tiles / 8) * (BM / 16) workgroups of 8 waves; workgroup x runs on
 // XCD x % 8 and handles tile 8 (x / 8 / RB) + x % 8, row block (x / 8) % RB.
-// Wave (vt, kh) = (wave & 3, wave >> 2): 16x16 output tile vt over the C half kh,
-// FB float4 steps of both operands per buffer, two buffers in flight.
-constexpr int FT = 512;
+// Wave (vt, kh) = (wave & 3, wave >> 2): 16x16 output tile vt over half kh of each
+// chunk.  Staging: thread element u (< 5) of a chunk is float4 (row, q) =
+// ((tid + 512 u) / 32, (tid + 512 u) % 32): u = 0 covers the 16 x_ctx rows, u >= 1
+// the 64 Wa rows, 32 consecutive lanes per 512-byte row segment.
 template <int BM>
 __global__ void __launch_bounds__(FT) gfk_ctx_fwd_k(GfkModel m) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  constexpr int RB = BM / 16, FB = 4;
+  constexpr int RB = BM / 16, SU = 5;
   const int x = blockIdx.x, jx = x >> 3, rb = jx % RB, tile = (jx / RB) * 8 + (x & 7);
   if (tile >= m.n_tiles) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
   const int vt = wave & 3, kh = wave >> 2, r = lane & 15, g = lane >> 4;
   const int V = m.V, C = m.C, H0 = m.H[0];
   const int c0 = tile * 64, nvv = min(64, V - c0), H0P = rup(H0, 16), LDC = fwd_ldc(m);
-  float* red = smem;                     // [2][16][68]
-  float* as = smem + 2 * 16 * 68;        // [16][66]
+  float* xs = smem;                      // [16][LDK], then Wa chunk [64][LDK]
+  float* red = smem + 80 * LDK;          // [2][16][68]
+  float* as = red + 2 * 16 * 68;         // [16][66]
   float* wc = as + 16 * 66;              // [64][LDC]
   const float* wcg = m.w_in + (size_t)V * H0;
 
-  // ---- loads that do not depend on the batch: Wa rows, Wc tile, bias ----
-  const int v = vt * 16 + r;
-  const float* wp = m.w_a + (size_t)(c0 + min(v, nvv - 1)) * C + 4 * g;
-  const float vmask = v < nvv ? 1.f : 0.f;
-  const int NS = (C + 15) / 16, s0 = kh * NS / 2, s1 = (kh + 1) * NS / 2;
+  // ---- loads that do not depend on the chunk loop: Wc tile, bias, doc ids ----
   auto ld_wc = [&](int i) {
     const int vv = i / H0P, j = i - vv * H0P;
     return (vv < nvv && j < H0) ? wcg[(size_t)(c0 + vv) * H0 + j] : 0.f;
@@ -143,40 +140,63 @@ __global__ void __launch_bounds__(FT) gfk_ctx_fwd_k(GfkModel m) {
   reg_load<8, FT>(wcr, 64 * H0P, ld_wc);
   const int bv = tid & 63;
   const float bias = bv < nvv ? m.b_a[c0 + bv] : 0.f;
-  const int doc = m.ws_next[1 + rb * 16 + r];   // the batch prepared by the previous step
-  const float* xp = m.ctx + (size_t)doc * C + 4 * g;
-
-  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
-  const f32x4* wp4 = reinterpret_cast<const f32x4*>(wp);
-  const f32x4* xp4 = reinterpret_cast<const f32x4*>(xp);
-  auto ld = [&](int s, f32x4 (&xa)[FB], f32x4 (&wb)[FB]) {
+  const int q4 = (tid & 31) * 4;
+  const int doc = m.ws_next[1 + rb * 16 + (tid >> 5)];   // the batch prepared by the previous step
+  const float* xrow = m.ctx + (size_t)doc * C + q4;
+  const float* wrow[SU - 1];
+  bool wok[SU - 1];
 #pragma unroll
-    for (int u = 0; u < FB; ++u) {
-      const bool ok = s + u < s1 && 16 * (s + u) + 4 * g < C;
-      const int o = ok ? 4 * (s + u) : 0;        // in-bounds address; zeroed below
-      wb[u] = wp4[o];
-      xa[u] = xp4[o];
-      if (!ok) wb[u] = xa[u] = z4;
-    }
+  for (int u = 1; u < SU; ++u) {
+    const int vv = ((tid + FT * u) >> 5) - 16;
+    wok[u - 1] = vv < nvv;
+    wrow[u - 1] = m.w_a + (size_t)(c0 + min(vv, nvv - 1)) * C + q4;
+  }
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  auto ld = [&](int c, f32x4 (&rg)[SU]) {
+    const int k = c * FK;
+    const bool kin = k + q4 < C;          // C % 4 == 0: whole float4 in or out
+    rg[0] = kin ? *reinterpret_cast<const f32x4*>(xrow + k) : z4;
+#pragma unroll
+    for (int u = 1; u < SU; ++u)
+      rg[u] = (kin && wok[u - 1]) ? *reinterpret_cast<const f32x4*>(wrow[u - 1] + k) : z4;
+  };
+  auto st = [&](const f32x4 (&rg)[SU]) {
+#pragma unroll
+    for (int u = 0; u < SU; ++u) st_f4_as_f2(xs + ((tid + FT * u) >> 5) * LDK + q4, rg[u]);
   };
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  auto mm = [&](const f32x4 (&xa)[FB], const f32x4 (&wb)[FB]) {
+  const float* ap = xs + r * LDK + kh * 64 + g;
+  const float* bp = xs + (16 + vt * 16 + r) * LDK + kh * 64 + g;
+  auto mma = [&]() {
 #pragma unroll
-    for (int u = 0; u < FB; ++u)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) acc = mfma16x16x4(xa[u][c], wb[u][c] * vmask, acc);
+    for (int k = 0; k < 64; k += 4) acc = mfma16x16x4(ap[k], bp[k], acc);
   };
-  f32x4 xa0[FB], wb0[FB], xa1[FB], wb1[FB];
-  ld(s0, xa0, wb0);
-  for (int s = s0; s < s1; s += 2 * FB) {
-    ld(s + FB, xa1, wb1);
-    mm(xa0, wb0);
-    if (s + 2 * FB < s1) ld(s + 2 * FB, xa0, wb0);
-    if (s + FB < s1) mm(xa1, wb1);
+
+  // ---- the C loop: chunk c in LDS, c + 1 and c + 2 in flight ----
+  const int NC = (C + FK - 1) / FK;
+  f32x4 ra[SU], rb2[SU];
+  ld(0, ra);
+  if (NC > 1) ld(1, rb2);
+  reg_store<8, FT>(wcr, 64 * H0P, ld_wc, st_wc);
+  st(ra);
+  if (NC > 2) ld(2, ra);
+  __syncthreads();
+  for (int c = 0; c < NC; c += 2) {
+    mma();
+    if (c + 1 >= NC) break;
+    __syncthreads();
+    st(rb2);
+    if (c + 3 < NC) ld(c + 3, rb2);
+    __syncthreads();
+    mma();
+    if (c + 2 >= NC) break;
+    __syncthreads();
+    st(ra);
+    if (c + 4 < NC) ld(c + 4, ra);
+    __syncthreads();
   }
 #pragma unroll
-  for (int i = 0; i < 4; ++i) red[(kh * 16 + g * 4 + i) * 68 + v] = acc[i];
-  reg_store<8, FT>(wcr, 64 * H0P, ld_wc, st_wc);
+  for (int i = 0; i < 4; ++i) red[(kh * 16 + g * 4 + i) * 68 + vt * 16 + r] = acc[i];
   __syncthreads();
 
   // ---- A = sum of the halves + bias: two elements per thread (16 x 64 = 2 FT) ----
@@ -194,10 +214,10 @@ __global__ void __launch_bounds__(FT) gfk_ctx_fwd_k(GfkModel m) {
   float* hg = m.ws_hpart + ((size_t)tile * m.bmax + rb * 16) * H0;
   for (int jt = wave; jt < H0P / 16; jt += FT / 64) {
     f32x4 p = {0.f, 0.f, 0.f, 0.f};
-    const float* ap = as + r * 66 + g;
-    const float* bp = wc + g * LDC + jt * 16 + r;
+    const float* pa = as + r * 66 + g;
+    const float* pb = wc + g * LDC + jt * 16 + r;
 #pragma unroll 4
-    for (int k = 0; k < 64; k += 4) p = mfma16x16x4(ap[k], bp[k * LDC], p);
+    for (int k = 0; k < 64; k += 4) p = mfma16x16x4(pa[k], pb[k * LDC], p);
     const int j = jt * 16 + r;
     if (j < H0) {
 #pragma unroll
@@ -206,8 +226,7 @@ __global__ void __launch_bounds__(FT) gfk_ctx_fwd_k(GfkModel m) {
   }
 }
 
-// grid: n_tiles * ctx_kb workgroups of 16 waves.
-// one workgroup per CU (the grid is sized to one round of CU workgroups)
+// grid: n_tiles * ctx_kb workgroups of 16 waves (one per CU).
 template <int BM>
 __global__ void __launch_bounds__(CT) gfk_ctx_bwd_k(GfkModel m) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -223,24 +242,25 @@ __global__ void __launch_bounds__(CT) gfk_ctx_bwd_k(GfkModel m) {
   float* wcs = smem + L.wc;
   float* das = smem + L.da;
   float* xcs = smem + L.xc;
+  float* gs = smem + L.g;
   const float* wcg = m.w_in + (size_t)V * H0;
   const int nb = *m.ws_nb;
   const bool fused = m.update_mode == 1;
 
-  // ---- g_Wa^T output tiles of this wave: (vt, ct) = (t & 3, t >> 2), t = wave + 16 u.
-  //      The product is formed transposed (C chunk x vocab) so each lane owns 4
-  //      consecutive C positions of one Wa row: p / m / v move as float4 ----
-  const int NCT = ckb / 16;
-  constexpr int MAXU = 4;               // ckb <= 256
-  f32x4 pp[MAXU], pm[MAXU], pv[MAXU];
-  const int li = lane & 15, lj = (lane >> 4) * 4;
+  // ---- prefetch p / m / v of the Wa block [64, chunk] as coalesced float4 rows:
+  //      element u of a thread is (row, q) = (e / NQ, e % NQ), e = tid + 1024 u ----
+  constexpr int MAXQ = 4;               // 64 x 256 / 4 / 1024
+  const int NQ = ckb / 4;
+  f32x4 pp[MAXQ], pm[MAXQ], pv[MAXQ];
+  int prow[MAXQ], pq[MAXQ];
 #pragma unroll
-  for (int u = 0; u < MAXU; ++u) {
-    const int t = wave + CW * u, vt = t & 3, ct = t >> 2;
-    const int i = vt * 16 + li, j = ct * 16 + lj;
+  for (int u = 0; u < MAXQ; ++u) {
+    const int e = tid + CT * u;
+    prow[u] = e / NQ;
+    pq[u] = e - prow[u] * NQ;
     pp[u] = pm[u] = pv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (fused && ct < NCT && i < nvv && j < kn) {     // kn % 4 == 0: whole float4 in range
-      const f32x4* p = reinterpret_cast<const f32x4*>(m.w_a + (size_t)(c0 + i) * C + k0 + j);
+    if (fused && prow[u] < nvv && 4 * pq[u] < kn) {
+      const f32x4* p = reinterpret_cast<const f32x4*>(m.w_a + (size_t)(c0 + prow[u]) * C + k0 + 4 * pq[u]);
       pp[u] = p[0];
       pm[u] = p[m.off_m / 4];
       pv[u] = p[m.off_v / 4];
@@ -249,7 +269,6 @@ __global__ void __launch_bounds__(CT) gfk_ctx_bwd_k(GfkModel m) {
   // ---- one staging round: dz0 (rows >= nb zero), Wc tile, x_ctx chunk; the
   //      dz0 / Wc loads are in flight while the doc ids reach LDS ----
   const float* dz0 = m.ws_dz[0];
-  const float* ctx = m.ctx;
   auto ld_dz = [&](int i) {
     const int b = i / H0Q, j = i - b * H0Q;
     return (b < nb && j < H0) ? dz0[b * H0 + j] : 0.f;
@@ -264,16 +283,22 @@ __global__ void __launch_bounds__(CT) gfk_ctx_bwd_k(GfkModel m) {
   reg_load<4>(rdz, BM * H0Q, ld_dz);
   reg_load<4>(rwc, 64 * H0Q, ld_wc);
   __syncthreads();          // docs_s
-  auto ld_xc = [&](int i) {
-    const int b = i / ckb, k = i - b * ckb;
-    return (b < nb && k < kn) ? ctx[(size_t)docs_s[b] * C + k0 + k] : 0.f;
-  };
-  auto st_xc = [&](int i, float x) { const int b = i / ckb; xcs[b * L.ldxb + i - b * ckb] = x; };
-  float rxc[8];
-  reg_load<8>(rxc, BM * ckb, ld_xc);
+  constexpr int XU = (BM * 64 + CT - 1) / CT;   // float4 of the x_ctx chunk per thread
+  f32x4 rxc[XU];
+#pragma unroll
+  for (int u = 0; u < XU; ++u) {
+    const int e = tid + CT * u, b = e / NQ, q = e - b * NQ;
+    rxc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (b < nb && b < BM && 4 * q < kn)
+      rxc[u] = *reinterpret_cast<const f32x4*>(m.ctx + (size_t)docs_s[b] * C + k0 + 4 * q);
+  }
   reg_store<4>(rdz, BM * H0Q, ld_dz, st_dz);
   reg_store<4>(rwc, 64 * H0Q, ld_wc, st_wc);
-  reg_store<8>(rxc, BM * ckb, ld_xc, st_xc);
+#pragma unroll
+  for (int u = 0; u < XU; ++u) {
+    const int e = tid + CT * u, b = e / NQ, q = e - b * NQ;
+    if (b < BM) *reinterpret_cast<f32x4*>(xcs + b * L.ldxb + 4 * q) = rxc[u];
+  }
   __syncthreads();
 
   // ---- dA [BM, 64] = dz0 Wc_tile^T ----
@@ -298,31 +323,50 @@ __global__ void __launch_bounds__(CT) gfk_ctx_bwd_k(GfkModel m) {
     s = row16_sum(s);
     if (sub == 0 && v < nvv) param_update(m, m.b_a + c0 + v, s, ac, is_shared(m, m.b_a));
   }
-  // ---- g_Wa^T [chunk, 64] = x_ctx^T dA and the update ----
-  const bool sh = is_shared(m, m.w_a);
+  // ---- g_Wa [64, chunk] = dA^T x_ctx: wave tiles (vt, ct) = (t & 3, t >> 2),
+  //      t = wave + 16 u, parked in registers until every wave has read dA / x_ctx ----
+  const int NCT = ckb / 16;
+  constexpr int MAXU = 4;               // ckb <= 256
+  f32x4 gacc[MAXU];
 #pragma unroll
   for (int u = 0; u < MAXU; ++u) {
     const int t = wave + CW * u, vt = t & 3, ct = t >> 2;
-    if (ct >= NCT) break;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    const float* ap = xcs + (lane >> 4) * L.ldxb + ct * 16 + li;
-    const float* bp = das + (lane >> 4) * 80 + vt * 16 + li;
-    for (int b = 0; b < BM; b += 4) acc = mfma16x16x4(ap[b * L.ldxb], bp[b * 80], acc);
-    const int i = vt * 16 + li, j = ct * 16 + lj;
-    if (i >= nvv || j >= kn) continue;
-    f32x4* p = reinterpret_cast<f32x4*>(m.w_a + (size_t)(c0 + i) * C + k0 + j);
+    gacc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (ct >= NCT) continue;
+    const float* ap = das + (lane >> 4) * 80 + vt * 16 + (lane & 15);
+    const float* bp = xcs + (lane >> 4) * L.ldxb + ct * 16 + (lane & 15);
+    for (int b = 0; b < BM; b += 4) gacc[u] = mfma16x16x4(ap[b * 80], bp[b * L.ldxb], gacc[u]);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < MAXU; ++u) {
+    const int t = wave + CW * u, vt = t & 3, ct = t >> 2;
+    if (ct >= NCT) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      gs[(vt * 16 + (lane >> 4) * 4 + r) * L.gs + ct * 16 + (lane & 15)] = gacc[u][r];
+  }
+  __syncthreads();
+
+  // ---- the update on coalesced float4 rows ----
+  const bool sh = is_shared(m, m.w_a);
+#pragma unroll
+  for (int u = 0; u < MAXQ; ++u) {
+    if (prow[u] >= nvv || 4 * pq[u] >= kn) continue;
+    const f32x4 gr = *reinterpret_cast<const f32x4*>(gs + prow[u] * L.gs + 4 * pq[u]);
+    f32x4* p = reinterpret_cast<f32x4*>(m.w_a + (size_t)(c0 + prow[u]) * C + k0 + 4 * pq[u]);
     if (!fused) {
-      p[m.off_g / 4] = acc;
+      p[m.off_g / 4] = gr;
     } else {
       f32x4 np, mo = pm[u], vo = pv[u];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float a = mo[r], b2 = vo[r];
-        float x = adam_update(pp[u][r], acc[r], a, b2, ac);
-        if (sh && m.fed_scale_on) x *= m.fed_scale;
+        float xv = adam_update(pp[u][r], gr[r], a, b2, ac);
+        if (sh && m.fed_scale_on) xv *= m.fed_scale;
         mo[r] = a;
         vo[r] = b2;
-        np[r] = x;
+        np[r] = xv;
       }
       p[m.off_m / 4] = mo;
       p[m.off_v / 4] = vo;
