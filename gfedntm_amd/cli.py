@@ -58,6 +58,10 @@ def build_parser() -> argparse.ArgumentParser:
                    help="comma list: client i trains on category i (local / rccl / gloo)")
     p.add_argument("--log_every", type=int, default=0, help="minibatch loss line every N rounds")
     p.add_argument("--no_graph", action="store_true", help="disable hipGraph replay")
+    p.add_argument("--agg", type=str, default="params", choices=["params", "grads"],
+                   help="params: FedAvg of the shared state after every local step (reference); "
+                        "grads: all-reduce of the sample-weighted gradients before one optimizer "
+                        "step on every client (classic synchronous data parallelism)")
     p.add_argument("--checkpoint_dir", type=str, default=None)
     p.add_argument("--checkpoint_every", type=int, default=None)
     p.add_argument("--stop_at_num_epochs", action="store_true")
@@ -138,7 +142,7 @@ def run_local(args, cfg) -> dict:
         stop_at_num_epochs=args.stop_at_num_epochs or cfg.stop_at_num_epochs,
         checkpoint_dir=args.checkpoint_dir,
         checkpoint_every=args.checkpoint_every if args.checkpoint_every is not None
-        else cfg.checkpoint_every, stamp=stamp)
+        else cfg.checkpoint_every, stamp=stamp, agg=args.agg)
     return fed.run()
 
 
@@ -168,7 +172,8 @@ def _rank_main(args, cfg) -> dict:
         checkpoint_every=args.checkpoint_every if args.checkpoint_every is not None
         else cfg.checkpoint_every, stamp=stamp,
         metrics_path=os.path.join(f"{logs_client}{cid}", f"metrics_{stamp}.jsonl"),
-        metrics_every=args.metrics_every, heartbeat_timeout=args.heartbeat_timeout)
+        metrics_every=args.metrics_every, heartbeat_timeout=args.heartbeat_timeout,
+        agg_mode=args.agg)
 
 
 def _spawned(local_rank: int, world: int, port: int, argv: List[str]):
@@ -216,6 +221,9 @@ def main(argv: Optional[List[str]] = None):
         return run_local(args, cfg)
     if args.backend in ("rccl", "gloo"):
         return run_collective(args, cfg, argv)
+    if args.agg != "params":
+        raise SystemExit("--agg grads needs a collective backend (local / rccl / gloo): the "
+                         "reference wire protocol carries parameters, not gradients")
     from .federation import grpc_transport
     if args.id == 0:
         return grpc_transport.start_server(args, cfg)

@@ -12,6 +12,13 @@ Per round (``local_step`` then, after the aggregation, ``end_round``):
     processed, the epoch summary line, best components, and the results save
     once ``num_epochs`` is reached.
 
+``agg="grads"`` (classic synchronous data parallelism, not the reference
+semantics): ``local_step`` leaves the step's gradients in the engine's flat
+gradient buffer pre-scaled by w_i, the transport sums their shared prefix,
+``apply_step`` runs the optimizer on the averaged gradients -- the replicas stay
+identical -- and the batch-norm running statistics are averaged separately
+(``pack_buffers`` / ``unpack_buffers``).
+
 Differences by design: the per-minibatch loss line needs the loss on the host,
 which would force a device sync every round, so it is logged every
 ``log_every`` rounds (0 = never); the epoch summary reads the whole epoch's
@@ -35,7 +42,10 @@ from ..eval.export import postprocess_thetas, save_model_as_npz
 class FederatedClient:
     def __init__(self, client_id: int, tm, dataset, max_iters: int, logger=None, seed: int = 0,
                  save_path: Optional[str] = None, log_every: int = 0, n_samples: int = 20,
-                 epoch_snapshots: bool = False):
+                 epoch_snapshots: bool = False, agg: str = "params"):
+        if agg not in ("params", "grads"):
+            raise ValueError("agg must be 'params' (FedAvg) or 'grads' (gradient all-reduce)")
+        self.agg = agg
         self.id = client_id
         self.tm = tm
         self.dataset = dataset
@@ -49,6 +59,9 @@ class FederatedClient:
         self.n_docs = self.data.n_docs
         self.max_iters = max_iters
         self.plan = BatchPlan.build(self.n_docs, tm.batch_size, max_iters, seed=seed)
+        if agg == "grads" and tm.backend == "fused":
+            from ..ops.engine import UPDATE_GRAD
+            tm.engine.set_update_mode(UPDATE_GRAD)
         tm.engine.bind_data(self.data, self.plan)
         tm.model.train()
         self.weight: Optional[float] = None
@@ -74,7 +87,7 @@ class FederatedClient:
         """Pre-scale the shared state by w_i = n_i / sum n after every local step, so the
         aggregation is a plain sum (fused engine: inside the update kernels)."""
         self.weight = float(w)
-        if self.fused:
+        if self.fused and self.agg == "params":
             self.tm.engine.set_fedavg_scale(self.weight)
 
     def enable_graph(self, on: bool = True):
@@ -83,9 +96,41 @@ class FederatedClient:
 
     # ------------------------------------------------------------------ round
     def local_step(self, it: int):
+        if self.agg == "grads":
+            self.tm.engine.compute_grads(it)
+            if self.weight is not None:
+                self.shared_grads.mul_(self.weight)
+            return
         self.tm.engine.step(it)
         if self.weight is not None and not self.fused:
             self.shared.mul_(self.weight)
+
+    # ---- gradient aggregation (agg="grads") ----
+    @property
+    def shared_grads(self) -> torch.Tensor:
+        return self.tm.engine.grad_shared
+
+    def apply_step(self, it: int):
+        """Optimizer step on the aggregated gradients."""
+        self.tm.engine.apply_grads(it)
+
+    def pack_buffers(self) -> torch.Tensor:
+        """The shared batch-norm running statistics, pre-scaled by w_i, in one buffer."""
+        flat = self.tm.flat
+        parts = [flat.buffer[s.offset: s.offset + s.numel] for s in flat.shared_buffer_slots()]
+        if not parts:
+            return torch.zeros(0, device=flat.buffer.device)
+        out = torch.cat(parts)
+        if self.weight is not None:
+            out.mul_(self.weight)
+        return out
+
+    def unpack_buffers(self, packed: torch.Tensor):
+        o = 0
+        flat = self.tm.flat
+        for s in flat.shared_buffer_slots():
+            flat.buffer[s.offset: s.offset + s.numel].copy_(packed[o: o + s.numel])
+            o += s.numel
 
     def end_round(self, it: int) -> bool:
         """Bookkeeping after the aggregated state was loaded; True when this client has

@@ -100,8 +100,9 @@ class LocalFederation:
                  logger=None, graph: bool = True, log_every: int = 0,
                  stop_at_num_epochs: bool = False, checkpoint_dir: Optional[str] = None,
                  checkpoint_every: int = 0, stamp: Optional[str] = None,
-                 metrics_path: Optional[str] = None, metrics_every: int = 0):
+                 metrics_path: Optional[str] = None, metrics_every: int = 0, agg: str = "params"):
         self.logger = logger or logging.getLogger("gfedntm_amd.federation")
+        self.agg_mode = agg
         self.metrics = MetricsWriter(metrics_path)
         self.metrics_every = int(metrics_every)
         self.device = torch.device(device) if device is not None else \
@@ -133,9 +134,9 @@ class LocalFederation:
                 path = client_model_path(save_client, cid, self.stamp)
             c = FederatedClient(cid, tm, ds, max_iters, logger=self.logger, seed=seed + cid,
                                 save_path=path, log_every=log_every,
-                                epoch_snapshots=(model_type == "ctm"))
+                                epoch_snapshots=(model_type == "ctm"), agg=agg)
             c.set_fedavg_weight(self.weights[i])
-            c.enable_graph(graph)
+            c.enable_graph(graph and agg == "params")
             self.clients.append(c)
         self.agg = LocalAggregator(n)
         self.round = 0
@@ -159,7 +160,16 @@ class LocalFederation:
             for it in range(self.round, self.max_iters):
                 for c in self.clients:
                     c.local_step(it)
-                self.agg.average_([c.shared for c in self.clients], prescaled=True)
+                if self.agg_mode == "grads":
+                    self.agg.average_([c.shared_grads for c in self.clients], prescaled=True)
+                    for c in self.clients:
+                        c.apply_step(it)
+                    packs = [c.pack_buffers() for c in self.clients]
+                    self.agg.average_(packs, prescaled=True)
+                    for c, p in zip(self.clients, packs):
+                        c.unpack_buffers(p)
+                else:
+                    self.agg.average_([c.shared for c in self.clients], prescaled=True)
                 done = [c.end_round(it) for c in self.clients]
                 self.round = it + 1
                 win.add(sum(int(c.plan.size[it]) for c in self.clients))
@@ -218,11 +228,15 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
                     stop_at_num_epochs: bool = False, checkpoint_dir: Optional[str] = None,
                     checkpoint_every: int = 0, stamp: Optional[str] = None,
                     bucket_bytes: int = 64 << 20, metrics_path: Optional[str] = None,
-                    metrics_every: int = 0, heartbeat_timeout: float = 0.0) -> Dict:
+                    metrics_every: int = 0, heartbeat_timeout: float = 0.0,
+                    agg_mode: str = "params") -> Dict:
     """Runs this process's client; torch.distributed must be initialised (RANK /
     WORLD_SIZE).  Rank r is client r+1; rank 0 also plays the coordinator (global
     save).  ``data_backend`` is the process group's backend ('nccl' = RCCL or
-    'gloo'); a separate gloo group carries the control plane."""
+    'gloo'); a separate gloo group carries the control plane.  ``agg_mode``
+    "params" is the reference FedAvg of the shared state after every local step;
+    "grads" all-reduces the pre-scaled gradients before one optimizer step on
+    every rank (classic synchronous data parallelism; BN statistics averaged)."""
     import torch.distributed as dist
     logger = logger or logging.getLogger("gfedntm_amd.federation")
     rank, world = dist.get_rank(), dist.get_world_size()
@@ -263,12 +277,12 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
         path = client_model_path(save_client, cid, stamp)
     client = FederatedClient(cid, tm, ds, max_iters, logger=logger, seed=seed + cid,
                              save_path=path, log_every=log_every,
-                             epoch_snapshots=(model_type == "ctm"))
+                             epoch_snapshots=(model_type == "ctm"), agg=agg_mode)
     client.set_fedavg_weight(weights[rank])
-    client.enable_graph(graph)
+    client.enable_graph(graph and agg_mode == "params")
     agg = CollectiveAggregator(bucket_bytes=bucket_bytes, method="rccl")
     in_step = False
-    if data_backend == "nccl" and client.fused:
+    if data_backend == "nccl" and client.fused and agg_mode == "params":
         # the FedAvg all-reduce runs inside the step (graph-captured xGMI kernel, beta
         # overlapped with the encoder backward) or right after it (RCCL)
         logger.info("-- -- FedAvg all-reduce: %s", tm.engine.attach_fedavg())
@@ -293,7 +307,13 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
             client.local_step(it)
             if hb is not None:
                 hb.mark(it, 1)
-            if not in_step:
+            if agg_mode == "grads":
+                agg.allreduce_(client.shared_grads)
+                client.apply_step(it)
+                packed = client.pack_buffers()
+                agg.allreduce_(packed)
+                client.unpack_buffers(packed)
+            elif not in_step:
                 agg.allreduce_(shared)
             done = client.end_round(it)
             win.add(int(client.plan.size[it]))

@@ -64,6 +64,20 @@ class EngineBase:
     def step(self, s: int) -> torch.Tensor:
         raise NotImplementedError
 
+    # ---- split step for gradient aggregation (classic synchronous data parallelism):
+    # compute_grads leaves this step's gradients in a flat buffer with the parameter
+    # layout (grad_buffer), the transport averages its shared prefix, apply_grads runs
+    # the optimizer on the averaged gradients.
+    def compute_grads(self, s: int) -> torch.Tensor:
+        raise NotImplementedError
+
+    def apply_grads(self, s: int):
+        raise NotImplementedError
+
+    @property
+    def grad_shared(self) -> torch.Tensor:
+        return self.grad_buffer[: self.flat.n_shared]
+
     def optimizer_state_dict(self):
         return self.optimizer.state_dict()
 
@@ -118,3 +132,30 @@ class TorchEngine(EngineBase):
         self.optimizer.step()
         self.loss_hist[s] = loss.detach()
         return loss.detach()
+
+    @property
+    def grad_buffer(self) -> torch.Tensor:
+        if getattr(self, "_grad_buf", None) is None:
+            self._grad_buf = torch.zeros_like(self.flat.buffer)
+        return self._grad_buf
+
+    def compute_grads(self, s: int) -> torch.Tensor:
+        self.model.train()
+        x, ctx, lab = self._batch(s)
+        self.model.zero_grad()
+        loss = self.loss_on(x, ctx, lab)
+        loss.backward()
+        g = self.grad_buffer
+        g.zero_()
+        for k, p in self.model.named_parameters():
+            if p.grad is not None:
+                self.flat.view_like(g, k).copy_(p.grad)
+        self.loss_hist[s] = loss.detach()
+        return loss.detach()
+
+    def apply_grads(self, s: int):
+        g = self.grad_buffer
+        for k, p in self.model.named_parameters():
+            if p.grad is not None:
+                p.grad.copy_(self.flat.view_like(g, k))
+        self.optimizer.step()

@@ -823,6 +823,26 @@ class FusedEngine(EngineBase):
             self._host_step = s
             self._launch([abi.PH_BATCH_PREP])   # the step's batch is prepared by the previous one
 
+    @property
+    def grad_buffer(self) -> torch.Tensor:
+        return self.grad
+
+    def compute_grads(self, s: int) -> torch.Tensor:
+        """The step's kernels without the optimizer (gradient mode): the gradients are
+        left in ``grad`` for an all-reduce before :meth:`apply_grads`."""
+        if self.update_mode != UPDATE_GRAD or self.fedavg_scale is not None:
+            raise RuntimeError("gradient aggregation needs gradient mode without the FedAvg pre-scale")
+        if self.plan is None:
+            raise RuntimeError("bind_data() first")
+        self.sync_step_counter(s)
+        self._launch([p for p in self.phases() if p not in (abi.PH_ADAM, abi.PH_FEDAVG_BETA,
+                                                           abi.PH_FEDAVG_END)])
+        self._host_step = s + 1
+        return self.loss_hist[s]
+
+    def apply_grads(self, s: int):
+        self._launch([abi.PH_ADAM])
+
     def step(self, s: int) -> torch.Tensor:
         if self.plan is None:
             raise RuntimeError("bind_data() first")

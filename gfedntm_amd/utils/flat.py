@@ -94,6 +94,18 @@ class FlatState:
             return flat.view(s.shape[1], s.shape[0]).t()
         return flat.view(s.shape)
 
+    def view_like(self, buf: torch.Tensor, key: str) -> torch.Tensor:
+        """The slot of ``key`` inside another buffer with this layout (gradients)."""
+        s = self.slots[key]
+        flat = buf[s.offset: s.offset + s.numel]
+        if s.transposed:
+            return flat.view(s.shape[1], s.shape[0]).t()
+        return flat.view(s.shape)
+
+    def shared_buffer_slots(self) -> List[Slot]:
+        """Shared float tensors that are not parameters (batch-norm running stats)."""
+        return [self.slots[k] for k in self.shared_keys if not self.slots[k].is_param]
+
     def raw(self, key: str) -> torch.Tensor:
         """Storage-order (contiguous) view: [in, out] for transposed weights."""
         s = self.slots[key]
