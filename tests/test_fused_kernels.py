@@ -70,10 +70,21 @@ def _grads_of(tm_fused):
                                             (64, 80, 50, (50, 50), 40000),       # persistent decoder
                                             (64, 80, 200, (50, 50), 40000)])     # persistent, 3 tiles/WG
 def test_step_matches_oracle(model_type, B, n_docs, K, H, V):
+    _oracle_step(model_type, B, n_docs, K, H, V)
+
+
+@pytest.mark.parametrize("model_type", ["prodLDA", "LDA"])
+@pytest.mark.parametrize("B,K", [(64, 50), (128, 50)])
+def test_long_rows_match_oracle(model_type, B, K):
+    """Rows of up to 400 non-zeros (several per lane in the row-wise loops)."""
+    _oracle_step(model_type, B, 2 * B, K, (50, 50), 3000, nnz=400)
+
+
+def _oracle_step(model_type, B, n_docs, K, H, V, nnz=40):
     fused, ref = _pair(model_type, V=V, K=K, H=H, B=B)
-    if K == 200 and model_type == "prodLDA":
+    if K == 200 and model_type == "prodLDA" and B == 64:
         assert fused.engine._m.stage_flags & 2     # batch matrices read from L2
-    X = random_csr(n_docs, V, 40, seed=1)
+    X = random_csr(n_docs, V, nnz, seed=1)
     data, plan = _bind(fused, X, B=B)
     e = fused.engine
     phases = e.phases()
