@@ -64,6 +64,44 @@ __device__ __forceinline__ void gather_rows(const int32_t* __restrict__ idx,
   }
 }
 
+// The same gather over the row's slot copy (prepare_next_batch): non-zeros
+// j in [0, n); the first batch's (index, value) of this lane (j = wave + 16 lane)
+// was loaded by the caller together with the row's extent, so the W_in row loads
+// are the kernel's second round trip instead of its third.
+template <int NQ>
+__device__ __forceinline__ void gather_slots(const int32_t* __restrict__ sidx,
+                                             const float* __restrict__ sval, int n, int v0,
+                                             float x0, int wave, const float* __restrict__ w,
+                                             int H, int lane, float* acc) {
+  constexpr int CH = NQ == 1 ? 16 : (NQ == 2 ? 8 : 4);
+  for (int base = wave; base < n; base += ENC_WAVES * 64) {
+    const int le = base + ENC_WAVES * lane;
+    int my_v = v0;
+    float my_x = le < n ? x0 : 0.f;
+    if (base != wave) {                  // rows of more than 1024 non-zeros
+      my_v = sidx[min(le, n - 1)];
+      my_x = le < n ? sval[min(le, n - 1)] : 0.f;
+    }
+    const int cnt = min(64, (n - base + ENC_WAVES - 1) / ENC_WAVES);
+    for (int g = 0; g < cnt; g += CH) {
+      float wv[CH][NQ];
+#pragma unroll
+      for (int i = 0; i < CH; ++i) {
+        const int v = __builtin_amdgcn_readlane(my_v, min(g + i, 63));
+        const float* wr = w + (size_t)v * H;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) wv[i][q] = wr[min(lane + 64 * q, H - 1)];
+      }
+#pragma unroll
+      for (int i = 0; i < CH; ++i) {
+        const float x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_x), min(g + i, 63)));
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) acc[q] += (g + i < cnt ? x : 0.f) * wv[i][q];
+      }
+    }
+  }
+}
+
 }  // namespace
 
 __host__ __device__ inline int pad4(int x) { return (x + 3) & ~3; }
@@ -160,6 +198,16 @@ __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkModel m) {
   const int e0 = nxt[1 + bmax + 2 * b], e1 = nxt[2 + bmax + 2 * b];
   const int step = *stepp;
   const float bias = b_in[min(tid, H0 - 1)];
+  // the row's non-zeros from its slots, in the same round: this lane's first gather
+  // pair and the (tid, tid - 1) pair of the tile-start table
+  const int cap = m.slot_cap;
+  const int32_t* sidx = m.ws_sidx + (size_t)min(b, bmax - 1) * cap;
+  const float* sval = m.ws_sval + (size_t)min(b, bmax - 1) * cap;
+  const int gj = min(wave + ENC_WAVES * lane, cap - 1), tj = min(tid, cap - 1);
+  const int gv = sidx[gj];
+  const float gx = sval[gj];
+  const int tv = sidx[tj], tvp = sidx[max(tj - 1, 0)];
+  __shared__ int last_tile;
   if (b >= nb) {            // drain the LDS-DMA before the workgroup retires
     vm_barrier();
     return;
@@ -177,10 +225,11 @@ __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkModel m) {
     float acc[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) acc[q] = 0.f;
-    if (H0 <= 64) gather_rows<1>(indices, values, e0, e1, wave, w_in, H0, lane, acc);
-    else if (H0 <= 128) gather_rows<2>(indices, values, e0, e1, wave, w_in, H0, lane, acc);
-    else if (H0 <= 256) gather_rows<4>(indices, values, e0, e1, wave, w_in, H0, lane, acc);
-    else gather_rows<8>(indices, values, e0, e1, wave, w_in, H0, lane, acc);
+    const int n = e1 - e0;
+    if (H0 <= 64) gather_slots<1>(sidx, sval, n, gv, gx, wave, w_in, H0, lane, acc);
+    else if (H0 <= 128) gather_slots<2>(sidx, sval, n, gv, gx, wave, w_in, H0, lane, acc);
+    else if (H0 <= 256) gather_slots<4>(sidx, sval, n, gv, gx, wave, w_in, H0, lane, acc);
+    else gather_slots<8>(sidx, sval, n, gv, gx, wave, w_in, H0, lane, acc);
     if (m.ctx_fused) {      // CombinedTM: the row's contextual partials from ctx_fwd (fixed order)
       const int P = m.n_tiles;
       const size_t ps = (size_t)bmax * H0;
@@ -207,16 +256,18 @@ __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkModel m) {
     }
   }
 
-  // ---- per vocab tile (64 words): the CSR position of the row's first non-zero ----
+  // ---- per vocab tile (64 words): the CSR position of the row's first non-zero
+  //      (the tail past the row's last tile is filled after the next barrier) ----
   {
     int32_t* ts = m.ws_tstart + (size_t)b * (m.n_tiles + 1);
-    for (int e = e0 + tid; e < e1; e += ENC_THREADS) {
-      const int t = indices[e] >> 6;
-      const int tp = e > e0 ? (indices[e - 1] >> 6) : -1;
-      for (int u = tp + 1; u <= t; ++u) ts[u] = e;
+    const int n = e1 - e0;
+    if (tid == 0 && n == 0) last_tile = -1;
+    for (int j = tid; j < n; j += ENC_THREADS) {
+      const int t = (j == tid ? tv : sidx[j]) >> 6;
+      const int tp = j > 0 ? (j == tid ? tvp : sidx[j - 1]) >> 6 : -1;
+      for (int u = tp + 1; u <= t; ++u) ts[u] = e0 + j;
+      if (j == n - 1) last_tile = t;
     }
-    const int last = e1 > e0 ? (indices[e1 - 1] >> 6) : -1;
-    for (int u = last + 1 + tid; u <= m.n_tiles; u += ENC_THREADS) ts[u] = e1;
   }
 
   // ---- the row's random draws for this step ----
@@ -236,6 +287,10 @@ __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkModel m) {
   }
   vm_barrier();             // gather partials + staged weights
   GFK_STAMP(m, 6);
+  {
+    int32_t* ts = m.ws_tstart + (size_t)b * (m.n_tiles + 1);
+    for (int u = last_tile + 1 + tid; u <= m.n_tiles; u += ENC_THREADS) ts[u] = e1;
+  }
 
   // ---- input layer: z0 = sum of the wave partials + bias (+ dense contextual part) ----
   const int act = m.act;

@@ -123,7 +123,12 @@ typedef struct GfkModel {
   int32_t ctx_fused;             // 1: adapt_bert + contextual input layer in ctx_fwd / ctx_bwd /
                                  //    win_update (no host GEMMs)
   int32_t ctx_kb, ctx_ckb;       // backward: C split into ctx_kb chunks of ctx_ckb
-  int32_t pad2;
+  int32_t slot_cap;              // non-zero slots per row of ws_sidx / ws_sval (0: not bound)
+  // the next batch's CSR rows copied into fixed slots [bmax][slot_cap] by
+  // prepare_next_batch, so a row's non-zeros are one round trip away (no CSR extent
+  // first); valid entries j < e1 - e0 of the row
+  int32_t* ws_sidx;
+  float* ws_sval;
 } GfkModel;
 
 // Gradient + update jobs of the small tensors, run by the update kernel next to
@@ -458,6 +463,7 @@ __device__ __forceinline__ void mfma_gemm(int M, int N, int R, const MatView& A,
 // workgroup of win_update, off the critical path, so the next enc_in starts one
 // round trip from its data.  Rows past the batch repeat its first doc.
 __device__ __forceinline__ void prepare_next_batch(const GfkModel& m) {
+  __shared__ int pnb_e[2 * 128];       // (e0, e1) of the next batch's rows (bmax <= 128)
   const int step = *m.step;
   int32_t* nxt = m.ws_next;
   if (step >= m.n_steps) {
@@ -466,14 +472,46 @@ __device__ __forceinline__ void prepare_next_batch(const GfkModel& m) {
   }
   const int nb = m.plan_size[step];
   const int base = m.plan_start[step];
-  for (int b = threadIdx.x; b < m.bmax; b += blockDim.x) {
+  const int bmax = m.bmax;
+  for (int b = threadIdx.x; b < bmax; b += blockDim.x) {
     const int doc = m.plan_order[base + (b < nb ? b : 0)];
     const int e0 = m.indptr[doc], e1 = m.indptr[doc + 1];
     nxt[1 + b] = doc;
-    nxt[1 + m.bmax + 2 * b] = e0;
-    nxt[2 + m.bmax + 2 * b] = e1;
+    nxt[1 + bmax + 2 * b] = e0;
+    nxt[2 + bmax + 2 * b] = e1;
+    pnb_e[2 * b] = e0;
+    pnb_e[2 * b + 1] = e1;
   }
   if (threadIdx.x == 0) nxt[0] = nb;
+  const int cap = m.slot_cap;
+  if (cap <= 0) return;
+  __syncthreads();
+  // the rows' non-zeros into their slots: G threads per row, U loads in flight each
+  constexpr int U = 8;
+  const int G = max(1, (int)blockDim.x / bmax);
+  for (int b = threadIdx.x / G; b < bmax; b += blockDim.x / G) {
+    const int e0 = pnb_e[2 * b], n = pnb_e[2 * b + 1] - e0;
+    int32_t* si = m.ws_sidx + (size_t)b * cap;
+    float* sv = m.ws_sval + (size_t)b * cap;
+    for (int j0 = (int)threadIdx.x % G; j0 < n; j0 += G * U) {
+      int ci[U];
+      float xv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int j = min(j0 + G * u, n - 1);
+        ci[u] = m.indices[e0 + j];
+        xv[u] = m.values[e0 + j];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int j = j0 + G * u;
+        if (j < n) {
+          si[j] = ci[u];
+          sv[j] = xv[u];
+        }
+      }
+    }
+  }
 }
 
 

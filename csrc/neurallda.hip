@@ -246,12 +246,18 @@ __global__ void __launch_bounds__(LBT) gfk_lda_beta_bwd_k(GfkModel m) {
     __syncthreads();
     // ---- round 1 ----
     glds_copy(d, m.ws_zn + (size_t)c0 * K, nv * K, tid, LBT);
-    const int xrow = tid >> 4, xsub = tid & 15;       // 16 threads per batch row
-    int es = 0, ee = 0;
+    // 16 threads per batch row: rows tid/16 and, at bmax = 128, tid/16 + 64
+    const int xrow = tid >> 4, xsub = tid & 15, xrow2 = xrow + LBT / 16;
+    int es = 0, ee = 0, fs = 0, fe = 0;
     if (xrow < nb && xrow < B) {
       const int32_t* ts = m.ws_tstart + (size_t)xrow * (m.n_tiles + 1) + tile;
       es = ts[0];
       ee = ts[1];
+    }
+    if (xrow2 < nb && xrow2 < B) {
+      const int32_t* ts = m.ws_tstart + (size_t)xrow2 * (m.n_tiles + 1) + tile;
+      fs = ts[0];
+      fe = ts[1];
     }
     float pp[PU], pm[PU], pv[PU];
 #pragma unroll
@@ -269,6 +275,7 @@ __global__ void __launch_bounds__(LBT) gfk_lda_beta_bwd_k(GfkModel m) {
     vm_barrier();
     // ---- round 2: the tile's non-zero coefficients g = -x / (wd + eps) -> x^T tile ----
     for (int e = es + xsub; e < ee; e += 16) xt[(m.indices[e] - c0) * XS + xrow] = m.ws_dbsm[e];
+    for (int e = fs + xsub; e < fe; e += 16) xt[(m.indices[e] - c0) * XS + xrow2] = m.ws_dbsm[e];
     // c_k = sum_b theta_d[b, k] d theta_d[b, k] (softmax-over-V backward), 16 lanes per topic
     if (tile == (int)blockIdx.x) {
       for (int k0 = 0; k0 < K; k0 += LBT / 16) {

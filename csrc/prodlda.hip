@@ -224,26 +224,48 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
 }
 
 // One wave per batch row: log-sum-exp from the per-wave partials, the sparse
-// reconstruction loss, S_b, and the per-tile CSR start table.
+// reconstruction loss and S_b over the row's non-zeros (read from the row slots
+// prepared with the batch, so the logit gathers are the second round trip).
 extern "C" __global__ void __launch_bounds__(64) gfk_prodlda_row_loss(GfkModel m) {
   int n_tiles = m.n_tiles, bmax = m.bmax;
-  const int32_t *nbp = m.ws_nb, *erange = m.ws_erange, *indices = m.indices;
-  const float *row_part = m.ws_row_part, *zn = m.ws_zn, *values = m.values;
-  keep(n_tiles, bmax, nbp, erange, indices, row_part, zn, values);
+  const int32_t *nbp = m.ws_nb, *erange = m.ws_erange;
+  const float *row_part = m.ws_row_part, *zn = m.ws_zn;
+  keep(n_tiles, bmax, nbp, erange, row_part, zn);
   const int b = blockIdx.x, lane = threadIdx.x;
+  // ---- round 1: batch size, the row's extent, LSE partials, its non-zeros (slots) ----
   const int nb = *nbp;
-  if (b >= nb) return;
   const int np = m.dec_grid * 4;                 // per-workgroup partials of prodlda_fwd
   const int e0 = erange[2 * b], e1 = erange[2 * b + 1];
-  constexpr int PU = 8;
+  constexpr int PU = 8, SU = 4;
   float pm[PU], ps[PU];
-  // issue the partial loads for the first 64*PU partials at once
 #pragma unroll
   for (int u = 0; u < PU; ++u) {
     const int g = min(lane + 64 * u, np - 1);
     const float2 p = *reinterpret_cast<const float2*>(row_part + ((size_t)g * bmax + b) * 2);
     pm[u] = p.x;
     ps[u] = p.y;
+  }
+  const int cap = m.slot_cap;
+  const int32_t* sidx = m.ws_sidx + (size_t)b * cap;
+  const float* sval = m.ws_sval + (size_t)b * cap;
+  int ci[SU];
+  float xv[SU];
+#pragma unroll
+  for (int u = 0; u < SU; ++u) {
+    const int j = min(lane + 64 * u, cap - 1);
+    ci[u] = sidx[j];
+    xv[u] = sval[j];
+  }
+  if (b >= nb) return;
+  const int n = e1 - e0;
+  // ---- round 2: the BN'ed logits at the non-zeros ----
+  const size_t tstride = (size_t)bmax * VB;
+  const float* zr = zn + (size_t)b * VB;
+  float zv[SU];
+#pragma unroll
+  for (int u = 0; u < SU; ++u) {
+    const int c = ci[u];
+    zv[u] = lane + 64 * u < n ? zr[(size_t)(c / VB) * tstride + ((c % VB) ^ zswz(b))] : 0.f;
   }
   float mx = -INFINITY, se = 0.f;
 #pragma unroll
@@ -255,13 +277,18 @@ extern "C" __global__ void __launch_bounds__(64) gfk_prodlda_row_loss(GfkModel m
   }
   wave_lse(mx, se);
   const float lse = mx + logf(se);
-  const size_t tstride = (size_t)bmax * VB;
   float rl = 0.f, S = 0.f;
-  for (int e = e0 + lane; e < e1; e += 64) {
-    const int c = indices[e];
-    const float x = values[e];
-    const float z = zn[(size_t)(c / VB) * tstride + (size_t)b * VB + ((c % VB) ^ zswz(b))];
-    const float p = expf(z - lse);
+#pragma unroll
+  for (int u = 0; u < SU; ++u) {
+    if (lane + 64 * u >= n) continue;
+    const float p = expf(zv[u] - lse);
+    rl += xv[u] * logf(p + RL_EPS);
+    S += xv[u] * p / (p + RL_EPS);
+  }
+  for (int j = lane + 64 * SU; j < n; j += 64) {    // rows of more than 256 non-zeros
+    const int c = sidx[j];
+    const float x = sval[j];
+    const float p = expf(zr[(size_t)(c / VB) * tstride + ((c % VB) ^ zswz(b))] - lse);
     rl += x * logf(p + RL_EPS);
     S += x * p / (p + RL_EPS);
   }

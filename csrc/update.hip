@@ -196,13 +196,19 @@ extern "C" __global__ void __launch_bounds__(UT) gfk_win_update(GfkModel m, GfkU
   } else {
     for (int i = tid; i < 64 * XS; i += UT) xt[i] = 0.f;
   }
-  // 16 threads per row: the row's non-zeros inside this tile
-  const int row = tid >> 4, sub = tid & 15;
-  int e0 = 0, e1 = 0;
+  // 16 threads per row: the row's non-zeros inside this tile (rows tid/16 and, at
+  // bmax = 128, tid/16 + 64)
+  const int row = tid >> 4, sub = tid & 15, row2 = row + UT / 16;
+  int e0 = 0, e1 = 0, f0 = 0, f1 = 0;
   if (!ctxt && row < nb && row < B) {
     const int32_t* ts = tstart + (size_t)row * (n_tiles + 1) + tile;
     e0 = ts[0];
     e1 = ts[1];
+  }
+  if (!ctxt && row2 < nb && row2 < B) {
+    const int32_t* ts = tstart + (size_t)row2 * (n_tiles + 1) + tile;
+    f0 = ts[0];
+    f1 = ts[1];
   }
   // prefetch the optimizer state of this lane's 4 outputs (16x16 tile per wave)
   const int MT = 4, NT = H0P / 16;
@@ -227,6 +233,7 @@ extern "C" __global__ void __launch_bounds__(UT) gfk_win_update(GfkModel m, GfkU
   }
   __syncthreads();
   for (int e = e0 + sub; e < e1; e += 16) xt[(indices[e] - c0) * XS + row] = values[e];
+  for (int e = f0 + sub; e < f1; e += 16) xt[(indices[e] - c0) * XS + row2] = values[e];
   __syncthreads();
 
   GFK_STAMP(m, 41);

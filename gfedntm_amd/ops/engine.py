@@ -537,6 +537,13 @@ class FusedEngine(EngineBase):
                 self.ws["dbsm"] = torch.zeros(nnz + 16, dtype=torch.float32, device=dev)
             m.ws_dbsm = self.ws["dbsm"].data_ptr()
         m.ctx = data.contextual.data_ptr() if data.contextual is not None else None
+        # the next batch's rows in fixed slots (prepare_next_batch -> enc_in / row_loss)
+        cap = max(16, -(-int(data.row_len_max) // 16) * 16)
+        if self.ws.get("sidx") is None or self.ws["sidx"].numel() < self.bmax * cap:
+            self.ws["sidx"] = torch.zeros(self.bmax * cap + 16, dtype=torch.int32, device=dev)
+            self.ws["sval"] = torch.zeros(self.bmax * cap + 16, dtype=torch.float32, device=dev)
+        m.slot_cap = cap
+        m.ws_sidx, m.ws_sval = self.ws["sidx"].data_ptr(), self.ws["sval"].data_ptr()
         m.plan_order = self._plan_dev["order"].data_ptr()
         m.plan_start = self._plan_dev["start"].data_ptr()
         m.plan_size = self._plan_dev["size"].data_ptr()

@@ -95,7 +95,7 @@ class GfkModel(C.Structure):
         ("adam_pow", P), ("adam_coef", P), ("ws_dtheta", P),
         ("w_a", P), ("b_a", P), ("ws_actx", P), ("ws_hpart", P),
         ("ctx_fused", C.c_int32), ("ctx_kb", C.c_int32), ("ctx_ckb", C.c_int32),
-        ("pad2", C.c_int32),
+        ("slot_cap", C.c_int32), ("ws_sidx", P), ("ws_sval", P),
     ]
 
 

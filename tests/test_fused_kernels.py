@@ -62,6 +62,7 @@ def _grads_of(tm_fused):
 
 @pytest.mark.parametrize("model_type", ["prodLDA", "LDA"])
 @pytest.mark.parametrize("B,n_docs,K,H,V", [(64, 150, 20, (32, 24), 700), (32, 45, 20, (32, 24), 700),
+                                            (128, 300, 50, (50, 50), 2000),     # 128-row batches
                                             (64, 100, 100, (40,), 700),
                                             (64, 200, 50, (50, 50, 50), 700),
                                             (64, 100, 200, (50, 50), 700),       # K > 128, L2 mode
