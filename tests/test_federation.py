@@ -120,7 +120,8 @@ def _dist_worker(rank, world, port, tmp, q):
         dist.destroy_process_group()
 
 
-def test_gloo_two_ranks(tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_ranks(tmp_path, world):
     import socket
     import torch.multiprocessing as mp
     with socket.socket() as s:
@@ -128,16 +129,18 @@ def test_gloo_two_ranks(tmp_path):
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_dist_worker, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    procs = [ctx.Process(target=_dist_worker, args=(r, world, port, str(tmp_path), q))
+             for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted(q.get(timeout=240) for _ in procs)
+    res = sorted((q.get(timeout=240) for _ in procs), key=lambda t: t[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert res[0][2] == res[1][2] == 5
-    np.testing.assert_array_equal(res[0][1], res[1][1])      # identical averaged state
-    assert os.path.exists(tmp_path / "client2" / "model_2_20240101.npz")
+    assert all(r[2] == 5 for r in res)
+    for r in res[1:]:
+        np.testing.assert_array_equal(res[0][1], r[1])        # identical averaged state
+    assert os.path.exists(tmp_path / f"client{world}" / f"model_{world}_20240101.npz")
     assert os.path.exists(tmp_path / "server" / "global_model_20240101.npz")
 
 

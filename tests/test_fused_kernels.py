@@ -63,6 +63,8 @@ def _grads_of(tm_fused):
 @pytest.mark.parametrize("model_type", ["prodLDA", "LDA"])
 @pytest.mark.parametrize("B,n_docs,K,H,V", [(64, 150, 20, (32, 24), 700), (32, 45, 20, (32, 24), 700),
                                             (128, 300, 50, (50, 50), 2000),     # 128-row batches
+                                            (64, 150, 10, (50, 50), 5000),      # K = 10, V = 5 k
+                                            (64, 80, 50, (50, 50), 100000),     # V = 100 k
                                             (64, 100, 100, (40,), 700),
                                             (64, 200, 50, (50, 50, 50), 700),
                                             (64, 100, 200, (50, 50), 700),       # K > 128, L2 mode

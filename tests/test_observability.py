@@ -122,3 +122,53 @@ def test_hung_peer_aborts_the_waiting_rank(tmp_path):
             if p.is_alive():
                 p.kill()
             p.join(10)
+
+
+def _kill_worker(rank, world, port):
+    import os as _os
+    _os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                       WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=600))
+    from gfedntm_amd.data.synthetic import generate_synthetic
+    from gfedntm_amd.federation import client as client_mod
+    from gfedntm_amd.federation.data import ClientCorpus
+    from gfedntm_amd.federation.runner import run_distributed
+    from gfedntm_amd.utils.config import load_config
+    orig = client_mod.FederatedClient.local_step
+
+    def local_step(self, it):
+        if rank == 1 and it == 3:
+            _os._exit(9)                      # the process dies mid-round
+        return orig(self, it)
+
+    client_mod.FederatedClient.local_step = local_step
+    params = dict(load_config().training_params)
+    params.update(num_epochs=2, batch_size=16, hidden_sizes=(16, 16), n_components=5)
+    sc = generate_synthetic(vocab_size=60, n_topics=5, n_docs=30, n_nodes=world, frozen_topics=1,
+                            nwords=(10, 20), seed=2)
+    run_distributed(ClientCorpus(synthetic=sc, node=rank), params, max_iters=50,
+                    backend="torch", heartbeat_timeout=10.0)
+
+
+def test_killed_peer_ends_the_surviving_rank():
+    """a rank killed mid-round makes the surviving rank stop with an error
+    (peer connection closed or liveness timeout) instead of hanging."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ps = [ctx.Process(target=_kill_worker, args=(r, 2, port)) for r in range(2)]
+    for p in ps:
+        p.start()
+    ps[1].join(120)
+    ps[0].join(120)
+    try:
+        assert ps[1].exitcode == 9, ps[1].exitcode
+        assert ps[0].exitcode not in (None, 0), ps[0].exitcode    # ended, with an error
+    finally:
+        for p in ps:
+            if p.is_alive():
+                p.kill()
+            p.join(10)
