@@ -381,6 +381,11 @@ extern "C" size_t gfk_ctx_smem(const GfkModel* m) {
 }
 
 extern "C" int gfk_ctx_set_smem(size_t bytes) {
+  // the attribute is per function and process-wide: only ever raise it, so an engine
+  // built earlier with a larger footprint keeps launching after a smaller one is set up
+  static size_t cur = 0;
+  if (bytes <= cur) return 0;
+  cur = bytes;
   const void* ks[] = {(const void*)gfk_ctx_fwd_k<16>, (const void*)gfk_ctx_fwd_k<32>,
                       (const void*)gfk_ctx_fwd_k<64>, (const void*)gfk_ctx_fwd_k<128>,
                       (const void*)gfk_ctx_bwd_k<16>, (const void*)gfk_ctx_bwd_k<32>,

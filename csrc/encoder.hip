@@ -363,6 +363,11 @@ extern "C" int gfk_launch_enc_in(const GfkModel* m, hipStream_t s) {
 }
 
 extern "C" int gfk_enc_in_set_smem(size_t bytes) {
+  // the attribute is per function and process-wide: only ever raise it, so an engine
+  // built earlier with a larger footprint keeps launching after a smaller one is set up
+  static size_t cur = 0;
+  if (bytes <= cur) return 0;
+  cur = bytes;
   const void* ks[] = {(const void*)gfk_enc_in_k<true>, (const void*)gfk_enc_in_k<false>};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);

@@ -704,6 +704,11 @@ extern "C" int gfk_launch_batch_docs(const GfkModel* m, hipStream_t s) {
 }
 
 extern "C" int gfk_post_set_smem(size_t bytes) {
+  // the attribute is per function and process-wide: only ever raise it, so an engine
+  // built earlier with a larger footprint keeps launching after a smaller one is set up
+  static size_t cur = 0;
+  if (bytes <= cur) return 0;
+  cur = bytes;
   const void* ks[] = {(const void*)gfk_post_fwd_k<true>, (const void*)gfk_post_fwd_k<false>,
                       (const void*)gfk_row_bwd_k<1>, (const void*)gfk_row_bwd_k<2>,
                       (const void*)gfk_row_bwd_k<3>, (const void*)gfk_row_bwd_k<4>,

@@ -717,6 +717,11 @@ extern "C" int gfk_launch_prodlda_row_loss(const GfkModel* m, hipStream_t s) {
 }
 
 extern "C" int gfk_prodlda_set_smem(size_t bytes) {
+  // the attribute is per function and process-wide: only ever raise it, so an engine
+  // built earlier with a larger footprint keeps launching after a smaller one is set up
+  static size_t cur = 0;
+  if (bytes <= cur) return 0;
+  cur = bytes;
   const void* ks[] = {(const void*)prodlda_fwd_kernel<16>, (const void*)prodlda_fwd_kernel<32>,
                       (const void*)prodlda_fwd_kernel<64>, (const void*)prodlda_fwd_kernel<128>,
 #define GFK_BWD_PTRS(U) (const void*)prodlda_bwd_kernel<16, U>, (const void*)prodlda_bwd_kernel<32, U>, \

@@ -281,6 +281,11 @@ extern "C" int gfk_launch_win_update(const GfkModel* m, const GfkUpdate* u, hipS
 }
 
 extern "C" int gfk_win_update_set_smem(size_t bytes) {
+  // the attribute is per function and process-wide: only ever raise it, so an engine
+  // built earlier with a larger footprint keeps launching after a smaller one is set up
+  static size_t cur = 0;
+  if (bytes <= cur) return 0;
+  cur = bytes;
   return (int)hipFuncSetAttribute((const void*)gfk_win_update,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
