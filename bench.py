@@ -141,6 +141,10 @@ def main():
     eng.bind_data(data, plan)
     if args.backend == "fused" and not args.no_graph:
         eng.enable_graph(True)
+        eng.warm_graph()
+    if world > 1:                 # ranks enter the first (collective) step together
+        torch.cuda.synchronize()
+        dist.barrier()
 
     shared = tm.flat.shared
 

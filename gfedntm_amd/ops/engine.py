@@ -818,6 +818,12 @@ class FusedEngine(EngineBase):
         self.adam_coef.copy_(saved[3])
         self._graph = g
 
+    def warm_graph(self):
+        """Capture the step graph now (no execution), so the first timed / collective
+        step is a plain replay on every rank."""
+        if self.graph_enabled and self._graph is None:
+            self._capture()
+
     def _snapshot(self):
         return None
 

@@ -67,7 +67,7 @@ class XgmiAllReduce:
     single-node process group (≤ 8 ranks; several ranks may share one GPU)."""
 
     def __init__(self, n: int, device, group=None, nblk: Optional[int] = None,
-                 spin_limit: int = 1 << 25):
+                 spin_limit: int = 1 << 28):
         self.lib = native.kernels()
         _declare(self.lib)
         self.group = group
