@@ -102,6 +102,37 @@ __device__ __forceinline__ void gather_slots(const int32_t* __restrict__ sidx,
   }
 }
 
+// ZeroShotTM's dense input layer inside the gather: acc[q] += sum over this wave's
+// contextual features c (c = wave + 16 i) of x[c] * W[c, j], W = the transposed
+// [C, H0] input layer; the same batches of CH row loads in flight as gather_rows.
+template <int NQ>
+__device__ __forceinline__ void gather_dense(const float* __restrict__ x, int C, int wave,
+                                             const float* __restrict__ w, int H, int lane,
+                                             float* acc) {
+  constexpr int CH = NQ == 1 ? 16 : (NQ == 2 ? 8 : 4);
+  for (int base = wave; base < C; base += ENC_WAVES * 64) {
+    const int le = base + ENC_WAVES * lane;
+    const float my_x = le < C ? x[le] : 0.f;
+    const int cnt = min(64, (C - base + ENC_WAVES - 1) / ENC_WAVES);
+    for (int g = 0; g < cnt; g += CH) {
+      float wv[CH][NQ];
+#pragma unroll
+      for (int i = 0; i < CH; ++i) {
+        const int v = min(base + ENC_WAVES * min(g + i, cnt - 1), C - 1);
+        const float* wr = w + (size_t)v * H;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) wv[i][q] = wr[min(lane + 64 * q, H - 1)];
+      }
+#pragma unroll
+      for (int i = 0; i < CH; ++i) {
+        const float xg = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_x), min(g + i, 63)));
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) acc[q] += (g + i < cnt ? xg : 0.f) * wv[i][q];
+      }
+    }
+  }
+}
+
 }  // namespace
 
 __host__ __device__ inline int pad4(int x) { return (x + 3) & ~3; }
@@ -168,6 +199,7 @@ __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkModel m) {
   const int32_t *nxt = m.ws_next, *indices = m.indices, *stepp = m.step;
   const float *values = m.values, *w_in = m.w_in, *b_in = m.b_in;
   keep(H0, K, bmax, nh, input, sflags, nxt, indices, stepp, values, w_in, b_in);
+  const bool zs = m.ctx_fused == 2;       // ZeroShotTM: dense input layer fused here
   const int Hl = m.H[nh - 1], hm = enc_hmax(m);
   float* red = smem;
   float* act0 = red + ENC_WAVES * H0;
@@ -220,7 +252,22 @@ __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkModel m) {
   }
 
   GFK_STAMP(m, 5);
-  // ---- sparse gather ----
+  // ---- sparse gather (ZeroShotTM fused: the dense contextual input layer) ----
+  if (zs) {
+    float acc[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+    const float* xr = m.ctx + (size_t)doc * m.C;
+    if (H0 <= 64) gather_dense<1>(xr, m.C, wave, w_in, H0, lane, acc);
+    else if (H0 <= 128) gather_dense<2>(xr, m.C, wave, w_in, H0, lane, acc);
+    else if (H0 <= 256) gather_dense<4>(xr, m.C, wave, w_in, H0, lane, acc);
+    else gather_dense<8>(xr, m.C, wave, w_in, H0, lane, acc);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int j = lane + 64 * q;
+      if (j < H0) red[wave * H0 + j] = acc[q];
+    }
+  }
   if (input != GFK_IN_CONTEXTUAL) {
     float acc[8];
 #pragma unroll
@@ -296,7 +343,7 @@ __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkModel m) {
   const int act = m.act;
   if (tid < H0) {
     float z = bias;
-    if (input != GFK_IN_CONTEXTUAL) {
+    if (input != GFK_IN_CONTEXTUAL || zs) {
 #pragma unroll
       for (int w = 0; w < ENC_WAVES; ++w) z += red[w * H0 + tid];
     }

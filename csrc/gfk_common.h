@@ -120,8 +120,9 @@ typedef struct GfkModel {
   float *w_a, *b_a;              // adapt_bert.weight [V, C], adapt_bert.bias [V]
   float *ws_actx;                // [n_tiles][bmax][64] adapted rows A (ctx_fwd)
   float *ws_hpart;               // [n_tiles][bmax][H0] per-tile contextual z0 terms
-  int32_t ctx_fused;             // 1: adapt_bert + contextual input layer in ctx_fwd / ctx_bwd /
-                                 //    win_update (no host GEMMs)
+  int32_t ctx_fused;             // 1 (CombinedTM): adapt_bert + contextual input layer in
+                                 //    ctx_fwd / ctx_bwd / win_update; 2 (ZeroShotTM): the dense
+                                 //    [C, H0] input layer in enc_in / win_update (no host GEMMs)
   int32_t ctx_kb, ctx_ckb;       // backward: C split into ctx_kb chunks of ctx_ckb
   int32_t slot_cap;              // non-zero slots per row of ws_sidx / ws_sval (0: not bound)
   // the next batch's CSR rows copied into fixed slots [bmax][slot_cap] by

@@ -75,7 +75,7 @@ size_t gfk_smem_required(const GfkModel* m, int which) {
     case 4: return gfk_post_smem(m);
     case 5: return gfk_win_update_smem(m);
     case 7: return gfk_enc_in_smem(m);
-    case 8: return m->ctx_fused ? gfk_ctx_smem(m) : 0;
+    case 8: return m->ctx_fused == 1 ? gfk_ctx_smem(m) : 0;
     default: return 0;
   }
 }
@@ -91,7 +91,7 @@ int gfk_setup(const GfkModel* m) {
   if ((e = gfk_lda_set_smem(p > q ? p : q))) return e;
   if ((e = gfk_enc_in_set_smem(gfk_enc_in_smem(m)))) return e;
   if ((e = gfk_post_set_smem(gfk_post_smem(m)))) return e;
-  if (m->ctx_fused && (e = gfk_ctx_set_smem(gfk_ctx_smem(m)))) return e;
+  if (m->ctx_fused == 1 && (e = gfk_ctx_set_smem(gfk_ctx_smem(m)))) return e;
   return gfk_win_update_set_smem(gfk_win_update_smem(m));
 }
 

@@ -152,10 +152,11 @@ __device__ __forceinline__ void vector_job(const GfkModel& m, const GfkVJob& J) 
   }
 }
 
-// grid: n_tiles + n_w + n_v + 1 (+ n_tiles for fused CombinedTM) workgroups of 1024
-// threads.  The trailing n_tiles (CombinedTM) are the contextual half of the input
-// layer, Wc = rows V..2V-1 of the transposed W_in: the same tile GEMM + Adam with the
-// dense adapted rows A^T (ctx_fwd's summed slab) in place of x^T.
+// grid: n_tiles + n_w + n_v + 1 (+ n_tiles for fused CombinedTM, + ceil(C / 64) for fused
+// ZeroShotTM) workgroups of 1024 threads.  The trailing tiles are the contextual input
+// layer: CombinedTM's Wc = rows V..2V-1 of the transposed W_in with the dense adapted
+// rows A^T (ctx_fwd's output) in place of x^T, or ZeroShotTM's whole [C, H0] layer with
+// the batch's contextual rows x_ctx^T -- the same tile GEMM + Adam epilogue.
 // dynamic LDS: max(W_in tile: xt[64][stride_a(B)] + dz[B][stride_b(H0P)], weight job: 2 B 80)
 extern "C" __global__ void __launch_bounds__(UT) gfk_win_update(GfkModel m, GfkUpdate U) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -165,14 +166,16 @@ extern "C" __global__ void __launch_bounds__(UT) gfk_win_update(GfkModel m, GfkU
     if (r >= U.n_w && r < U.n_w + U.n_v) { vector_job(m, U.v[r - U.n_w]); return; }
     if (r == U.n_w + U.n_v) { prepare_next_batch(m); return; }
   }
-  if (m.input == GFK_IN_CONTEXTUAL) return;   // ZeroShotTM: W_in is the dense [C, H0] layer (host GEMM)
+  const bool zs = m.ctx_fused == 2;            // ZeroShotTM: W_in is the dense [C, H0] layer
+  if (m.input == GFK_IN_CONTEXTUAL && !zs) return;   // (host GEMMs when not fused)
   const int rr = (int)blockIdx.x - (m.n_tiles + U.n_w + U.n_v + 1);
-  const bool ctxt = rr >= 0;                   // a Wc tile (fused CombinedTM)
+  const bool ctxt = rr >= 0;                   // a Wc tile (CombinedTM) / W tile (ZeroShotTM)
+  if (zs && !ctxt) return;                     // ZeroShotTM has no bag-of-words half
   const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
-  int B = m.bmax, H0 = m.H[0], V = m.V, n_tiles = m.n_tiles;
+  int B = m.bmax, H0 = m.H[0], V = zs ? m.C : m.V, n_tiles = m.n_tiles;
   const int32_t *tstart = m.ws_tstart, *indices = m.indices, *nbp = m.ws_nb;
   const float *values = m.values, *dz0 = m.ws_dz[0];
-  float* w_in = m.w_in + (ctxt ? (size_t)m.V * m.H[0] : 0);
+  float* w_in = m.w_in + (ctxt && !zs ? (size_t)m.V * m.H[0] : 0);
   keep(B, H0, V, n_tiles, tstart, indices, nbp, values, dz0, w_in);
   const int H0P = rup(H0, 16);
   const int XS = stride_a(B), ZS = stride_b(H0P);
@@ -187,7 +190,12 @@ extern "C" __global__ void __launch_bounds__(UT) gfk_win_update(GfkModel m, GfkU
     const int r = i / H0P, c = i % H0P;
     dz[r * ZS + c] = (c < H0 && r < nb) ? dz0[r * H0 + c] : 0.f;
   }
-  if (ctxt) {                 // A^T tile: the adapted rows (slab 0 of ctx_fwd's output)
+  if (zs) {                   // x_ctx^T tile: the batch rows' contextual features
+    for (int i = tid; i < B * 64; i += UT) {
+      const int b = i >> 6, v = i & 63;
+      xt[v * XS + b] = (b < nb && c0 + v < V) ? m.ctx[(size_t)m.ws_doc[b] * V + c0 + v] : 0.f;
+    }
+  } else if (ctxt) {          // A^T tile: the adapted rows (slab 0 of ctx_fwd's output)
     const float* ag = m.ws_actx + (size_t)tile * B * 64;
     for (int i = tid; i < B * 64; i += UT) {
       const int b = i >> 6, v = i & 63;
@@ -275,7 +283,8 @@ extern "C" __global__ void __launch_bounds__(UT) gfk_win_update(GfkModel m, GfkU
 }
 
 extern "C" int gfk_launch_win_update(const GfkModel* m, const GfkUpdate* u, hipStream_t s) {
-  hipLaunchKernelGGL(gfk_win_update, dim3(m->n_tiles + u->n_w + u->n_v + 1 + (m->ctx_fused ? m->n_tiles : 0)), dim3(UT),
+  const int extra = m->ctx_fused == 1 ? m->n_tiles : (m->ctx_fused == 2 ? (m->C + 63) / 64 : 0);
+  hipLaunchKernelGGL(gfk_win_update, dim3(m->n_tiles + u->n_w + u->n_v + 1 + extra), dim3(UT),
                      gfk_win_update_smem(m), s, *m, *u);
   return (int)hipGetLastError();
 }

@@ -198,7 +198,9 @@ class FusedEngine(EngineBase):
         # fused epilogue updates: AVITM and CombinedTM (contextual path on ctx_fwd /
         # ctx_bwd); ZeroShotTM, whose dense input layer comes from host-issued GEMMs,
         # runs the generic Adam
-        self.ctx_fused = tm.kind == "ctm" and tm.inference_type == "combined"
+        # CTM contextual path on the fused kernels: CombinedTM (ctx_fwd / ctx_bwd) and
+        # ZeroShotTM (dense input layer in enc_in / win_update); _plan_ctx may fall back
+        self.ctx_fused = tm.kind == "ctm"
         self.update_mode = UPDATE_FUSED if (tm.kind != "ctm" or self.ctx_fused) else UPDATE_GRAD
         self.lr, self.beta1, self.beta2 = float(tm.lr), float(tm.momentum), 0.99
         self.eps, self.weight_decay = 1e-8, 0.0
@@ -240,7 +242,7 @@ class FusedEngine(EngineBase):
         """UPDATE_FUSED: optimizer in the kernel epilogues; UPDATE_GRAD: kernels write
         gradients and the generic Adam kernel follows."""
         if mode == UPDATE_FUSED and self.kind == "ctm" and not self.ctx_fused:
-            raise ValueError("the fused update mode covers AVITM and CombinedTM only")
+            raise ValueError("the fused update mode needs the fused contextual path")
         self.update_mode = mode
         self._m.update_mode = mode
         self._rebuild_adam()
@@ -320,7 +322,7 @@ class FusedEngine(EngineBase):
         m.nbt_s = net.f_sigma_batchnorm.num_batches_tracked.data_ptr()
         m.nbt_beta = model.beta_batchnorm.num_batches_tracked.data_ptr()
         m.step, m.adam_t = self.d_step.data_ptr(), self.adam_t.data_ptr()
-        if self.ctx_fused:
+        if m.ctx_fused == 1:
             m.w_a, m.b_a = self._ptr(P, "inf_net.adapt_bert.weight"), self._ptr(P, "inf_net.adapt_bert.bias")
         # optimizer (fused epilogues + generic Adam)
         m.update_mode = self.update_mode
@@ -363,6 +365,14 @@ class FusedEngine(EngineBase):
         once (one 16-wave workgroup per CU).  Falls back to the host GEMMs when a shape is outside
         the kernels' assumptions (C % 4, H0 <= 512, LDS)."""
         m = self._m
+        if m.input == abi.IN_CONTEXTUAL:
+            # ZeroShotTM: the [C, H0] input layer is gathered densely by enc_in and its
+            # gradient + Adam are ceil(C / 64) extra win_update tiles
+            m.ctx_fused = 2 if int(m.H[0]) <= 512 else 0
+            if not m.ctx_fused:
+                self.ctx_fused = False
+                self.update_mode = UPDATE_GRAD
+            return
         n_tiles, Cs = -(-int(m.V) // VB), int(m.C)
         k = max(1, min(cu // n_tiles, -(-Cs // 16)))      # one round, one workgroup per CU
         m.ctx_ckb = min(256, -(-(-(-Cs // k)) // 16) * 16)
@@ -403,8 +413,8 @@ class FusedEngine(EngineBase):
             "next": torch.zeros(1 + 3 * B, dtype=torch.int32, device=dev),
             # fused CombinedTM: the adapted rows per vocab tile and their contextual
             # pre-activation partials (csrc/ctx.hip)
-            "actx": f(m.n_tiles * B * 64 if m.ctx_fused else 1),
-            "hpart": f(m.n_tiles * B * hs[0] if m.ctx_fused else 1),
+            "actx": f(m.n_tiles * B * 64 if m.ctx_fused == 1 else 1),
+            "hpart": f(m.n_tiles * B * hs[0] if m.ctx_fused == 1 else 1),
         }
         for i, h in enumerate(hs):
             ws[f"z{i}"] = f(B, h)
@@ -561,8 +571,9 @@ class FusedEngine(EngineBase):
         else:
             ph = abi.PRODLDA_STEP + ([abi.PH_ADAM] if self.update_mode == UPDATE_GRAD else [])
         if self.ctx_fused:
-            ph.insert(ph.index(abi.PH_ENC_FWD), abi.PH_CTXF_FWD)
-            ph.insert(ph.index(abi.PH_ENC_BWD), abi.PH_CTXF_BWD)
+            if self._m.ctx_fused == 1:
+                ph.insert(ph.index(abi.PH_ENC_FWD), abi.PH_CTXF_FWD)
+                ph.insert(ph.index(abi.PH_ENC_BWD), abi.PH_CTXF_BWD)
         elif self.kind == "ctm":
             ph.insert(ph.index(abi.PH_ENC_FWD), abi.PH_CTX_FWD)
             ph.insert(ph.index(abi.PH_ENC_BWD) + 1, abi.PH_CTX_BWD)

@@ -250,14 +250,17 @@ def test_ctm_step_matches_oracle(inference_type, Cdim, model_type):
     data = DeviceCSR(X, "cuda", contextual=ctx)
     plan = BatchPlan.build(data.n_docs, B, 3, seed=0)
     e = fused.engine
+    assert e.update_mode == UPDATE_FUSED
     if inference_type == "combined":
-        assert e.update_mode == UPDATE_FUSED and (e._m.ctx_kb > 1) == (Cdim > 16)
-        e.set_update_mode(UPDATE_GRAD)
+        assert e._m.ctx_fused == 1 and (e._m.ctx_kb > 1) == (Cdim > 16)
+    else:
+        assert e._m.ctx_fused == 2           # dense input layer in enc_in / win_update
+    e.set_update_mode(UPDATE_GRAD)
     e.bind_data(data, plan)
     phases = e.phases()
-    ctx_ph = (abi.PH_CTXF_FWD, abi.PH_CTXF_BWD) if inference_type == "combined" else \
-        (abi.PH_CTX_FWD, abi.PH_CTX_BWD)
+    ctx_ph = (abi.PH_CTXF_FWD, abi.PH_CTXF_BWD) if inference_type == "combined" else ()
     assert phases[-1] == abi.PH_ADAM and all(p in phases for p in ctx_ph)
+    assert not any(p in abi.HOST_PHASES for p in phases)
     e.run_phases(phases[:-1])
     torch.cuda.synchronize()
     nb = int(plan.size[0])
@@ -282,16 +285,19 @@ def test_ctm_step_matches_oracle(inference_type, Cdim, model_type):
     assert float(e.grad.abs().max().item()) == 0.0
 
 
+@pytest.mark.parametrize("inference_type", ["combined", "zeroshot"])
 @pytest.mark.parametrize("model_type", ["prodLDA", "LDA"])
-def test_ctm_fused_update_matches_gradient_mode(model_type):
-    """CombinedTM: Adam fused into ctx_bwd (adapt_bert) and win_update's contextual
-    tiles (input layer) == gradient mode + the generic Adam, with the FedAvg pre-scale."""
-    from gfedntm_amd.models import CombinedTM
+def test_ctm_fused_update_matches_gradient_mode(model_type, inference_type):
+    """CTM: Adam fused into ctx_bwd (adapt_bert) and win_update's contextual tiles (the
+    input layer; ZeroShotTM: the whole dense layer) == gradient mode + the generic Adam,
+    with the FedAvg pre-scale."""
+    from gfedntm_amd.models import CombinedTM, ZeroShotTM
+    cls = CombinedTM if inference_type == "combined" else ZeroShotTM
     V, K, B, Cdim, n_docs = 700, 30, 64, 136, 200
     torch.manual_seed(0)
     kw = dict(input_size=V, contextual_size=Cdim, n_components=K, hidden_sizes=(48, 40),
               batch_size=B, verbose=False, device="cuda", backend="fused", model_type=model_type)
-    a, b = CombinedTM(**kw), CombinedTM(**kw)
+    a, b = cls(**kw), cls(**kw)
     b.model.load_state_dict(a.model.state_dict())
     b.engine.seed = b.engine._m.seed = a.engine.seed
     b.engine.set_update_mode(UPDATE_GRAD)
