@@ -39,7 +39,7 @@ from gfedntm_amd.data.bow import BatchPlan, DeviceCSR  # noqa: E402
 from gfedntm_amd.data.synthetic import (generate_synthetic, node_vocabulary_terms,  # noqa: E402
                                         remap_to_vocabulary)
 from gfedntm_amd.data.vocab import union_vocabulary, vocabulary_dict  # noqa: E402
-from gfedntm_amd.models import AVITM, CombinedTM  # noqa: E402
+from gfedntm_amd.models import AVITM, CombinedTM, ZeroShotTM  # noqa: E402
 from gfedntm_amd.parallel.aggregator import CollectiveAggregator  # noqa: E402
 from gfedntm_amd.utils.config import DEFAULT_GRADS_TO_SHARE  # noqa: E402
 
@@ -55,8 +55,9 @@ def parse():
     p.add_argument("--steps", type=int, default=2000)
     p.add_argument("--warmup", type=int, default=200)
     p.add_argument("--model", default="prodLDA", choices=["prodLDA", "LDA"])
-    p.add_argument("--family", default="avitm", choices=["avitm", "ctm"],
-                   help="ctm = CombinedTM with --contextual-size synthetic embeddings")
+    p.add_argument("--family", default="avitm", choices=["avitm", "ctm", "zeroshot"],
+                   help="ctm = CombinedTM, zeroshot = ZeroShotTM, with --contextual-size "
+                        "synthetic embeddings")
     p.add_argument("--contextual-size", type=int, default=768)
     p.add_argument("--vocab", type=int, default=5000)
     p.add_argument("--topics", type=int, default=50)
@@ -110,7 +111,7 @@ def main():
               hidden_sizes=hidden, batch_size=args.batch, verbose=False, backend=args.backend,
               device=device, shared_keys=DEFAULT_GRADS_TO_SHARE, seed=args.seed)
     ctx = None
-    if args.family == "ctm":
+    if args.family in ("ctm", "zeroshot"):
         # SBERT is not available offline: per-document embeddings are synthetic
         # (a fixed random projection of the document's topic mixture plus noise)
         rng = np.random.default_rng(args.seed + 17 * rank)
@@ -118,7 +119,8 @@ def main():
             (args.topics, args.contextual_size)).astype(np.float32)
         ctx = (np.asarray(corpus.doc_topics[rank], dtype=np.float32) @ proj
                + 0.1 * rng.standard_normal((X.shape[0], args.contextual_size)).astype(np.float32))
-        tm = CombinedTM(contextual_size=args.contextual_size, **kw)
+        cls = CombinedTM if args.family == "ctm" else ZeroShotTM
+        tm = cls(contextual_size=args.contextual_size, **kw)
     else:
         tm = AVITM(**kw)
     eng = tm.engine
@@ -225,8 +227,10 @@ def main():
             "dtype": "fp32",
             "data": "synthetic (reference LDA generator: V=5000, K=50, 1000 docs/client, "
                     "150-250 tokens, 5 frozen topics), random init",
-            "config": {"model": (f"CombinedTM-{args.model} C={args.contextual_size}"
-                                 if args.family == "ctm" else args.model)
+            "config": {"model": ((f"CombinedTM-{args.model} C={args.contextual_size}"
+                                  if args.family == "ctm" else
+                                  f"ZeroShotTM-{args.model} C={args.contextual_size}")
+                                 if args.family in ("ctm", "zeroshot") else args.model)
                                 + f" K={args.topics} H={hidden} V={len(terms)}",
                        "global_batch": args.batch * n_clients, "seq_len": None,
                        "per_client_batch": args.batch, "clients": n_clients,
