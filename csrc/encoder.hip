@@ -29,45 +29,12 @@ namespace {
 constexpr int ENC_THREADS = 1024;
 constexpr int ENC_WAVES = ENC_THREADS / 64;
 
-// acc[q] (output j = lane + 64*q) += sum over this wave's non-zeros of x * W[v, j].
-template <int NQ>
-__device__ __forceinline__ void gather_rows(const int32_t* __restrict__ idx,
-                                            const float* __restrict__ val, int e0, int e1,
-                                            int wave, const float* __restrict__ w, int H,
-                                            int lane, float* acc) {
-  constexpr int CH = NQ == 1 ? 16 : (NQ == 2 ? 8 : 4);
-  // non-zeros dealt round-robin over the waves (wave w: e0 + w + ENC_WAVES * i), so a
-  // typical row (~100-200 non-zeros) costs every wave one index load and one batch of
-  // CH row loads in flight
-  for (int base = e0 + wave; base < e1; base += ENC_WAVES * 64) {
-    const int le = base + ENC_WAVES * lane;
-    const int e = min(le, e1 - 1);
-    const int my_v = idx[e];
-    const float my_x = le < e1 ? val[e] : 0.f;
-    const int cnt = min(64, (e1 - base + ENC_WAVES - 1) / ENC_WAVES);
-    for (int g = 0; g < cnt; g += CH) {
-      float wv[CH][NQ];
-#pragma unroll
-      for (int i = 0; i < CH; ++i) {
-        const int v = __builtin_amdgcn_readlane(my_v, min(g + i, 63));
-        const float* wr = w + (size_t)v * H;
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) wv[i][q] = wr[min(lane + 64 * q, H - 1)];
-      }
-#pragma unroll
-      for (int i = 0; i < CH; ++i) {
-        const float x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_x), min(g + i, 63)));
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) acc[q] += (g + i < cnt ? x : 0.f) * wv[i][q];
-      }
-    }
-  }
-}
-
-// The same gather over the row's slot copy (prepare_next_batch): non-zeros
-// j in [0, n); the first batch's (index, value) of this lane (j = wave + 16 lane)
-// was loaded by the caller together with the row's extent, so the W_in row loads
-// are the kernel's second round trip instead of its third.
+// acc[q] (output j = lane + 64*q) += sum over this wave's non-zeros of x * W[v, j], for
+// the row's non-zeros j in [0, n) of its slot copy (prepare_next_batch).  Non-zeros
+// are dealt round-robin over the waves (wave w: j = w + ENC_WAVES * i), so a typical
+// row (~100-200 non-zeros) costs every wave one batch of CH W_in row loads in flight;
+// this lane's first (index, value) (j = wave + 16 lane) was loaded by the caller with
+// the row's extent, so the W_in row loads are the kernel's second round trip.
 template <int NQ>
 __device__ __forceinline__ void gather_slots(const int32_t* __restrict__ sidx,
                                              const float* __restrict__ sval, int n, int v0,
@@ -104,7 +71,7 @@ __device__ __forceinline__ void gather_slots(const int32_t* __restrict__ sidx,
 
 // ZeroShotTM's dense input layer inside the gather: acc[q] += sum over this wave's
 // contextual features c (c = wave + 16 i) of x[c] * W[c, j], W = the transposed
-// [C, H0] input layer; the same batches of CH row loads in flight as gather_rows.
+// [C, H0] input layer; the same batches of CH row loads in flight as gather_slots.
 template <int NQ>
 __device__ __forceinline__ void gather_dense(const float* __restrict__ x, int C, int wave,
                                              const float* __restrict__ w, int H, int lane,
