@@ -158,10 +158,22 @@ typedef struct GfkUpdate {
   GfkVJob v[GFK_MAX_VJOBS];
 } GfkUpdate;
 
+// Update rules of the generic optimizer kernel (gradient mode), torch.optim
+// semantics as the reference constructs them (avitm.py:141-153):
+//   ADAM      see adam_update (m = exp_avg, v = exp_avg_sq)
+//   SGD       buf = b1 buf + g; p -= lr buf                       (m = momentum_buffer)
+//   ADAGRAD   sum += g^2; p -= lr g / (sqrt(sum) + eps)           (v = sum)
+//   ADADELTA  sq = b2 sq + (1-b2) g^2; d = sqrt(acc + eps) / sqrt(sq + eps) g;
+//             acc = b2 acc + (1-b2) d^2; p -= lr d                (v = square_avg, m = acc_delta)
+//   RMSPROP   sq = b2 sq + (1-b2) g^2; buf = b1 buf + g / (sqrt(sq) + eps); p -= lr buf
+//                                                                 (v = square_avg, m = momentum_buffer)
+enum { GFK_SOLVER_ADAM = 0, GFK_SOLVER_SGD = 1, GFK_SOLVER_ADAGRAD = 2, GFK_SOLVER_ADADELTA = 3,
+       GFK_SOLVER_RMSPROP = 4 };
+
 typedef struct GfkAdam {
   float *p, *g, *m, *v;
   int32_t n_seg;
-  int32_t pad;
+  int32_t solver;                    // GFK_SOLVER_*: update rule of the optimizer segments
   int64_t seg_start[GFK_MAX_SEGS];   // in floats, multiples of 4
   int64_t seg_end[GFK_MAX_SEGS];
   int32_t seg_flags[GFK_MAX_SEGS];   // bit0: Adam update, bit1: FedAvg pre-scale
@@ -545,8 +557,48 @@ __device__ __forceinline__ void adam_block(const GfkAdam& a, int blk, int tid, i
       float4 m = *reinterpret_cast<float4*>(a.m + o);
       float4 v = *reinterpret_cast<float4*>(a.v + o);
       float* pp = &p.x; const float* gg = &g.x; float* mm = &m.x; float* vv = &v.x;
+      switch (a.solver) {
+        case GFK_SOLVER_ADAM:
 #pragma unroll
-      for (int j = 0; j < 4; ++j) pp[j] = adam_update(pp[j], gg[j], mm[j], vv[j], c);
+          for (int j = 0; j < 4; ++j) pp[j] = adam_update(pp[j], gg[j], mm[j], vv[j], c);
+          break;
+        case GFK_SOLVER_SGD:
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float g1 = c.wd != 0.f ? gg[j] + c.wd * pp[j] : gg[j];
+            mm[j] = c.b1 * mm[j] + g1;
+            pp[j] -= a.lr * (c.b1 != 0.f ? mm[j] : g1);
+          }
+          break;
+        case GFK_SOLVER_ADAGRAD:
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float g1 = c.wd != 0.f ? gg[j] + c.wd * pp[j] : gg[j];
+            vv[j] += g1 * g1;
+            pp[j] -= a.lr * g1 / (sqrtf(vv[j]) + c.eps);
+          }
+          break;
+        case GFK_SOLVER_ADADELTA:
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float g1 = c.wd != 0.f ? gg[j] + c.wd * pp[j] : gg[j];
+            vv[j] = c.b2 * vv[j] + (1.f - c.b2) * g1 * g1;
+            const float d = sqrtf(mm[j] + c.eps) / sqrtf(vv[j] + c.eps) * g1;
+            mm[j] = c.b2 * mm[j] + (1.f - c.b2) * d * d;
+            pp[j] -= a.lr * d;
+          }
+          break;
+        default:   // GFK_SOLVER_RMSPROP
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float g1 = c.wd != 0.f ? gg[j] + c.wd * pp[j] : gg[j];
+            vv[j] = c.b2 * vv[j] + (1.f - c.b2) * g1 * g1;
+            const float q = g1 / (sqrtf(vv[j]) + c.eps);
+            mm[j] = c.b1 * mm[j] + q;
+            pp[j] -= a.lr * (c.b1 != 0.f ? mm[j] : q);
+          }
+          break;
+      }
       *reinterpret_cast<float4*>(a.m + o) = m;
       *reinterpret_cast<float4*>(a.v + o) = v;
       *reinterpret_cast<float4*>(a.g + o) = make_float4(0.f, 0.f, 0.f, 0.f);

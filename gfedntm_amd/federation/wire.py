@@ -279,7 +279,11 @@ def state_from_updates(updates) -> Dict[str, torch.Tensor]:
 # ---------------------------------------------------------------------------
 def adam_update_from_state_dict(sd: Dict) -> Any:
     au = pb.AdamUpdate()
+    # the message is Adam's (federated.proto AdamUpdate); other solvers' states have
+    # no exp_avg / exp_avg_sq pair and travel as the param group only
     for sid, st in sd.get("state", {}).items():
+        if "exp_avg" not in st or "exp_avg_sq" not in st:
+            continue
         cs = au.state.contentState.add(state_id=int(sid))
         cs.step.CopyFrom(tensor_to_proto(torch.as_tensor(st["step"], dtype=torch.float32)))
         cs.exp_avg.CopyFrom(tensor_to_proto(st["exp_avg"]))
@@ -287,8 +291,9 @@ def adam_update_from_state_dict(sd: Dict) -> Any:
     pg = sd["param_groups"][0]
     g = au.paramGroups
     g.lr = float(pg["lr"])
-    g.betas.beta1, g.betas.beta2 = float(pg["betas"][0]), float(pg["betas"][1])
-    g.eps, g.weight_decay = float(pg["eps"]), float(pg["weight_decay"])
+    betas = pg.get("betas", (pg.get("momentum", 0.0), pg.get("alpha", pg.get("rho", 0.0))))
+    g.betas.beta1, g.betas.beta2 = float(betas[0]), float(betas[1])
+    g.eps, g.weight_decay = float(pg.get("eps", 0.0)), float(pg.get("weight_decay", 0.0))
     g.amsgrad = bool(pg.get("amsgrad", False))
     g.params.extend(int(p) for p in pg["params"])
     return pb.OptUpdate(adamUpdate=au)

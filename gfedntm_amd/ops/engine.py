@@ -63,15 +63,16 @@ def supports(tm, explain: bool = False) -> bool:
     checks = [
         (dev.type == "cuda", "needs a GPU device"),
         (native.kernels_available(), "kernel library not built"),
-        (tm.solver == "adam", "only the adam solver is fused"),
+        (tm.solver in abi.SOLVER_CODES, f"solver {tm.solver} not fused"),
         (tm.activation in abi.ACT_CODES, f"activation {tm.activation} not fused"),
-        (not tm.reduce_on_plateau, "ReduceLROnPlateau not fused"),
         (tm.batch_size <= BMAX_CHOICES[-1], "batch_size > 128"),
         (tm.n_components <= 256, "n_components > 256"),
         (max(tm.hidden_sizes) <= 512 and len(tm.hidden_sizes) <= abi.MAX_LAYERS,
          "hidden layers too wide / too many"),
         (getattr(tm, "label_size", 0) == 0, "CTM labels not fused"),
     ]
+    # reduce_on_plateau needs nothing here: the reference builds ReduceLROnPlateau
+    # (avitm.py:156-157) but never calls scheduler.step(), so the lr never changes
     for ok, why in checks:
         if not _explain(ok, why, explain):
             return False
@@ -127,16 +128,55 @@ def lds_required(tm, bmax: int) -> int:
     return need
 
 
+# Per solver: hyperparameters as the reference constructs the torch optimizer
+# (avitm.py:141-153: Adam betas=(momentum, 0.99), SGD / RMSprop momentum=momentum,
+# torch defaults otherwise), and the torch state names of the two flat state buffers.
+SOLVER_STATE = {
+    "adam": (("exp_avg", "exp_avg"), ("exp_avg_sq", "exp_avg_sq")),
+    "sgd": (("momentum_buffer", "exp_avg"),),
+    "adagrad": (("sum", "exp_avg_sq"),),
+    "adadelta": (("square_avg", "exp_avg_sq"), ("acc_delta", "exp_avg")),
+    "rmsprop": (("square_avg", "exp_avg_sq"), ("momentum_buffer", "exp_avg")),
+}
+
+
+def solver_hparams(solver: str, momentum: float) -> Dict[str, float]:
+    """beta1 / beta2 / eps of the generic optimizer kernel for ``solver``."""
+    return {"adam": dict(beta1=momentum, beta2=0.99, eps=1e-8),
+            "sgd": dict(beta1=momentum, beta2=0.0, eps=0.0),
+            "adagrad": dict(beta1=0.0, beta2=0.0, eps=1e-10),
+            "adadelta": dict(beta1=0.0, beta2=0.9, eps=1e-6),
+            "rmsprop": dict(beta1=momentum, beta2=0.99, eps=1e-8)}[solver]
+
+
 class FusedAdamState:
-    """torch.optim.Adam-compatible view of the flat Adam state (for checkpoints and
-    the reference OptUpdate wire message)."""
+    """torch.optim-compatible view of the flat optimizer state (for checkpoints and
+    the reference OptUpdate wire message): the state_dict has the keys and
+    param_group fields of the torch optimizer of the same solver."""
 
     def __init__(self, engine: "FusedEngine"):
         self.e = engine
-        self.param_groups = [{"lr": engine.lr, "betas": (engine.beta1, engine.beta2),
-                              "eps": engine.eps, "weight_decay": engine.weight_decay,
-                              "amsgrad": False, "maximize": False, "foreach": None,
-                              "capturable": False, "differentiable": False, "fused": None}]
+        self.param_groups = [self._group()]
+
+    def _group(self):
+        e = self.e
+        # the installed torch optimizer's defaults give the exact key set of its
+        # param groups (it changes across torch versions); our values override
+        from ..models.engine import make_optimizer
+        dummy = torch.nn.Parameter(torch.zeros(1))
+        base = dict(make_optimizer([dummy], e.solver, e.lr, e.beta1 or 0.0).defaults)
+        common = {"lr": e.lr, "weight_decay": e.weight_decay}
+        extra = {
+            "adam": {"betas": (e.beta1, e.beta2), "eps": e.eps, "amsgrad": False,
+                     "capturable": False, "fused": None},
+            "sgd": {"momentum": e.beta1, "dampening": 0, "nesterov": False, "fused": None},
+            "adagrad": {"lr_decay": 0, "initial_accumulator_value": 0, "eps": e.eps,
+                        "fused": None},
+            "adadelta": {"rho": e.beta2, "eps": e.eps, "capturable": False},
+            "rmsprop": {"alpha": e.beta2, "eps": e.eps, "momentum": e.beta1,
+                        "centered": False, "capturable": False},
+        }[e.solver]
+        return {**base, **common, **{k: v for k, v in extra.items() if k in base}}
 
     def state_dict(self):
         e = self.e
@@ -144,9 +184,10 @@ class FusedAdamState:
         state = {}
         if t > 0:
             for i, (name, _) in enumerate(e.param_order):
-                state[i] = {"step": torch.tensor(float(t)),
-                            "exp_avg": e.view_like(e.exp_avg, name).detach().clone(),
-                            "exp_avg_sq": e.view_like(e.exp_avg_sq, name).detach().clone()}
+                st = {} if e.solver == "sgd" else {"step": torch.tensor(float(t))}
+                for key, buf in SOLVER_STATE[e.solver]:
+                    st[key] = e.view_like(getattr(e, buf), name).detach().clone()
+                state[i] = st
         pg = dict(self.param_groups[0])
         pg["params"] = list(range(len(e.param_order)))
         return {"state": state, "param_groups": [pg]}
@@ -155,23 +196,26 @@ class FusedAdamState:
         e = self.e
         pg = sd["param_groups"][0]
         e.lr = float(pg.get("lr", e.lr))
-        b = pg.get("betas", (e.beta1, e.beta2))
-        e.beta1, e.beta2 = float(b[0]), float(b[1])
+        if e.solver == "adam":
+            e.beta1, e.beta2 = (float(x) for x in pg.get("betas", (e.beta1, e.beta2)))
+        e.beta1 = float(pg.get("momentum", e.beta1))
+        e.beta2 = float(pg.get("rho", pg.get("alpha", e.beta2)))
         e.eps = float(pg.get("eps", e.eps))
         e.weight_decay = float(pg.get("weight_decay", e.weight_decay))
-        self.param_groups[0].update(lr=e.lr, betas=(e.beta1, e.beta2), eps=e.eps,
-                                    weight_decay=e.weight_decay)
+        self.param_groups = [self._group()]
         e.exp_avg.zero_()
         e.exp_avg_sq.zero_()
-        t = 0
+        t = int(e.adam_t.item()) if e.solver == "sgd" else 0
         for i, (name, _) in enumerate(e.param_order):
             st = sd["state"].get(i, sd["state"].get(str(i)))
             if not st:
                 continue
-            e.view_like(e.exp_avg, name).copy_(torch.as_tensor(st["exp_avg"]))
-            e.view_like(e.exp_avg_sq, name).copy_(torch.as_tensor(st["exp_avg_sq"]))
-            step = st["step"]
-            t = int(step.item() if isinstance(step, torch.Tensor) else step)
+            for key, buf in SOLVER_STATE[e.solver]:
+                if st.get(key) is not None:
+                    e.view_like(getattr(e, buf), name).copy_(torch.as_tensor(st[key]))
+            if "step" in st:
+                step = st["step"]
+                t = int(step.item() if isinstance(step, torch.Tensor) else step)
         e.set_adam_t(t)
         e._rebuild_adam()
 
@@ -201,9 +245,14 @@ class FusedEngine(EngineBase):
         # CTM contextual path on the fused kernels: CombinedTM (ctx_fwd / ctx_bwd) and
         # ZeroShotTM (dense input layer in enc_in / win_update); _plan_ctx may fall back
         self.ctx_fused = tm.kind == "ctm"
-        self.update_mode = UPDATE_FUSED if (tm.kind != "ctm" or self.ctx_fused) else UPDATE_GRAD
-        self.lr, self.beta1, self.beta2 = float(tm.lr), float(tm.momentum), 0.99
-        self.eps, self.weight_decay = 1e-8, 0.0
+        # Adam runs in the kernels' epilogues; the other solvers in gradient mode
+        # (kernels write gradients, the generic optimizer kernel applies the rule)
+        self.solver = tm.solver
+        self.update_mode = (UPDATE_FUSED if (tm.kind != "ctm" or self.ctx_fused)
+                            and self.solver == "adam" else UPDATE_GRAD)
+        hp = solver_hparams(self.solver, float(tm.momentum))
+        self.lr, self.beta1, self.beta2 = float(tm.lr), hp["beta1"], hp["beta2"]
+        self.eps, self.weight_decay = hp["eps"], 0.0
         self.fedavg_scale: Optional[float] = None
         self.bmax = next(b for b in BMAX_CHOICES if b >= tm.batch_size)
         self.param_order: List[Tuple[str, torch.nn.Parameter]] = list(self.model.named_parameters())
@@ -243,6 +292,8 @@ class FusedEngine(EngineBase):
         gradients and the generic Adam kernel follows."""
         if mode == UPDATE_FUSED and self.kind == "ctm" and not self.ctx_fused:
             raise ValueError("the fused update mode needs the fused contextual path")
+        if mode == UPDATE_FUSED and self.solver != "adam":
+            raise ValueError(f"the fused update mode is Adam only (solver {self.solver})")
         self.update_mode = mode
         self._m.update_mode = mode
         self._rebuild_adam()
@@ -483,6 +534,7 @@ class FusedEngine(EngineBase):
         a.m, a.v = self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr()
         a.lr, a.beta1, a.beta2 = self.lr, self.beta1, self.beta2
         a.eps, a.weight_decay = self.eps, self.weight_decay
+        a.solver = abi.SOLVER_CODES[self.solver]
         a.scale = 1.0 if self.fedavg_scale is None else float(self.fedavg_scale)
         a.t = self.adam_t.data_ptr()
         a.coef = self.adam_coef.data_ptr()

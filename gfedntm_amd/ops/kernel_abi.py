@@ -116,10 +116,14 @@ class GfkUpdate(C.Structure):
                 ("v", GfkVJob * MAX_VJOBS)]
 
 
+# update rules of the generic optimizer kernel (csrc/gfk_common.h GFK_SOLVER_*)
+SOLVER_CODES = {"adam": 0, "sgd": 1, "adagrad": 2, "adadelta": 3, "rmsprop": 4}
+
+
 class GfkAdam(C.Structure):
     _fields_ = [
         ("p", P), ("g", P), ("m", P), ("v", P),
-        ("n_seg", C.c_int32), ("pad", C.c_int32),
+        ("n_seg", C.c_int32), ("solver", C.c_int32),
         ("seg_start", C.c_int64 * MAX_SEGS), ("seg_end", C.c_int64 * MAX_SEGS),
         ("seg_flags", C.c_int32 * MAX_SEGS),
         ("lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float),
