@@ -68,6 +68,9 @@ def parse():
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--no-npmi", action="store_true")
+    p.add_argument("--solver", default="adam",
+                   choices=["adam", "sgd", "adagrad", "adadelta", "rmsprop"],
+                   help="optimizer (reference default adam; the others run in gradient mode)")
     return p.parse_args()
 
 
@@ -109,7 +112,8 @@ def main():
     torch.manual_seed(args.seed)
     kw = dict(input_size=len(terms), n_components=args.topics, model_type=args.model,
               hidden_sizes=hidden, batch_size=args.batch, verbose=False, backend=args.backend,
-              device=device, shared_keys=DEFAULT_GRADS_TO_SHARE, seed=args.seed)
+              device=device, shared_keys=DEFAULT_GRADS_TO_SHARE, seed=args.seed,
+              solver=args.solver)
     ctx = None
     if args.family in ("ctm", "zeroshot"):
         # SBERT is not available offline: per-document embeddings are synthetic
@@ -236,6 +240,7 @@ def main():
                        "per_client_batch": args.batch, "clients": n_clients,
                        "parallelism": f"fedavg-dp{n_clients}",
                        "backend": args.backend + ("" if args.no_graph else "+hipgraph"),
+                       "solver": args.solver,
                        "aggregation": "per-minibatch sample-weighted FedAvg of 20 shared tensors"
                                       + (f" ({comm} all-reduce)" if world > 1 else "")},
             "npmi": None if npmi is None else round(npmi, 4),

@@ -11,6 +11,9 @@
 
 #define GFK_MAX_LAYERS 8
 #define GFK_MAX_SEGS 48
+// float4 per workgroup of the generic optimizer kernel (one per thread of a 256-thread
+// workgroup: ~450 workgroups for the K=50 model, every CU busy)
+#define GFK_ADAM_CHUNK 256
 #define GFK_WAVE 64
 
 // ---------------------------------------------------------------------------
@@ -180,7 +183,7 @@ typedef struct GfkAdam {
   float lr, beta1, beta2, eps, weight_decay, scale;
   const int32_t *t;                  // device Adam step count (already incremented)
   const float *coef;                 // [2] step size, 1/sqrt(bias correction 2) (see GfkModel)
-  int32_t seg_first_block[GFK_MAX_SEGS];   // first workgroup of each segment (1024 float4 per block)
+  int32_t seg_first_block[GFK_MAX_SEGS];   // first workgroup of each segment (GFK_ADAM_CHUNK float4 each)
   uint64_t* dbg;                     // diagnostic stamps (GFK_STAMPS builds)
 } GfkAdam;
 
@@ -529,7 +532,7 @@ __device__ __forceinline__ void prepare_next_batch(const GfkModel& m) {
 
 
 // One workgroup's share of the multi-segment Adam: workgroups are dealt to
-// segments in proportion to their size (1024 float4 per workgroup, segment s
+// segments in proportion to their size (GFK_ADAM_CHUNK float4 per workgroup, segment s
 // starts at workgroup seg_first_block[s]).  A ballot over the segment table
 // finds the segment in one round trip.  Used by the generic Adam kernel and by
 // the extra workgroups of win_update (small tensors in fused mode).
@@ -548,7 +551,8 @@ __device__ __forceinline__ void adam_block(const GfkAdam& a, int blk, int tid, i
   const int64_t s0 = a.seg_start[s], n4 = (a.seg_end[s] - s0) >> 2;
   const int flags = a.seg_flags[s];
   const bool do_adam = flags & 1, do_scale = flags & 2;
-  const int64_t lo = (int64_t)(blk - first) * 1024, hi = lo + 1024 < n4 ? lo + 1024 : n4;
+  const int64_t lo = (int64_t)(blk - first) * GFK_ADAM_CHUNK,
+                hi = lo + GFK_ADAM_CHUNK < n4 ? lo + GFK_ADAM_CHUNK : n4;
   for (int64_t i = lo + tid; i < hi; i += nthreads) {
     const int64_t o = s0 + 4 * i;
     float4 p = *reinterpret_cast<float4*>(a.p + o);

@@ -529,7 +529,7 @@ class FusedEngine(EngineBase):
         """Segment table of a GfkAdam: [start, end) float ranges of parameters (all,
         or the slots of ``keys``) with ADAM, plus SCALE on the shared prefix.
         Batch-norm running statistics are scaled by the kernels that update them.
-        Returns the number of workgroups (1024 float4 each)."""
+        Returns the number of workgroups (abi.ADAM_CHUNK float4 each)."""
         a.p, a.g = self.flat.buffer.data_ptr(), self.grad.data_ptr()
         a.m, a.v = self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr()
         a.lr, a.beta1, a.beta2 = self.lr, self.beta1, self.beta2
@@ -563,7 +563,7 @@ class FusedEngine(EngineBase):
         for i, (s0, s1, fl) in enumerate(segs):
             a.seg_start[i], a.seg_end[i], a.seg_flags[i] = s0, s1, fl
             a.seg_first_block[i] = nblk
-            nblk += -(-((s1 - s0) // 4) // 1024)
+            nblk += -(-((s1 - s0) // 4) // abi.ADAM_CHUNK)
         return nblk
 
     def _rebuild_adam(self):

@@ -117,6 +117,7 @@ class GfkUpdate(C.Structure):
 
 
 # update rules of the generic optimizer kernel (csrc/gfk_common.h GFK_SOLVER_*)
+ADAM_CHUNK = 256      # float4 per workgroup of the generic optimizer kernel (GFK_ADAM_CHUNK)
 SOLVER_CODES = {"adam": 0, "sgd": 1, "adagrad": 2, "adadelta": 3, "rmsprop": 4}
 
 
