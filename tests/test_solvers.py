@@ -29,10 +29,10 @@ def test_wire_codec_accepts_every_solver_state(solver):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("model_type", ["prodLDA", "LDA"])
+@pytest.mark.parametrize("model_type", ["prodLDA", "LDA", "combined", "zeroshot"])
 @pytest.mark.parametrize("solver", SOLVERS)
 def test_fused_solver_matches_torch_optimizer(solver, model_type):
-    from gfedntm_amd.models import AVITM
+    from gfedntm_amd.models import AVITM, CombinedTM, ZeroShotTM
     from gfedntm_amd.ops import kernel_abi as abi
     from gfedntm_amd.ops.engine import UPDATE_FUSED, UPDATE_GRAD
     from tests.helpers import random_csr
@@ -42,8 +42,16 @@ def test_fused_solver_matches_torch_optimizer(solver, model_type):
     kw = dict(input_size=700, n_components=20, model_type=model_type, hidden_sizes=(32, 24),
               batch_size=64, solver=solver, lr=2e-3, momentum=0.99, verbose=False,
               device="cuda", reduce_on_plateau=True)
-    fused = AVITM(backend="fused", **kw)
-    ref = AVITM(backend="torch", **kw)
+    ctx = None
+    if model_type in ("combined", "zeroshot"):
+        cls = CombinedTM if model_type == "combined" else ZeroShotTM
+        kw.update(model_type="prodLDA", contextual_size=96)
+        ctx = np.random.default_rng(4).standard_normal((200, 96)).astype(np.float32)
+    else:
+        cls = AVITM
+    fused = cls(backend="fused", **kw)
+    assert fused.backend == "fused"
+    ref = cls(backend="torch", **kw)
     ref.model.load_state_dict(fused.model.state_dict())
     e = fused.engine
     assert type(e).__name__ == "FusedEngine"
@@ -54,7 +62,7 @@ def test_fused_solver_matches_torch_optimizer(solver, model_type):
             e.set_update_mode(UPDATE_FUSED)
     e.set_update_mode(UPDATE_GRAD)
     X = random_csr(200, 700, 40, seed=1)
-    data = DeviceCSR(X, "cuda")
+    data = DeviceCSR(X, "cuda", contextual=ctx)
     e.bind_data(data, BatchPlan.build(data.n_docs, 64, 3, seed=0))
     phases = e.phases()
     assert phases[-1] == abi.PH_ADAM
