@@ -28,6 +28,24 @@ def test_wire_codec_accepts_every_solver_state(solver):
     assert len(msg.adamUpdate.state.contentState) == (1 if solver == "adam" else 0)
 
 
+@pytest.mark.parametrize("solver", SOLVERS)
+def test_fused_param_group_matches_torch(solver):
+    """The fused engine's optimizer param group has the installed torch optimizer's keys
+    and the reference's hyperparameters (avitm.py:141-153)."""
+    from types import SimpleNamespace
+    from gfedntm_amd.ops.engine import FusedAdamState, solver_hparams
+
+    hp = solver_hparams(solver, 0.99)
+    e = SimpleNamespace(solver=solver, lr=2e-3, weight_decay=0.0, **hp)
+    pg = FusedAdamState(e).param_groups[0]
+    p = torch.nn.Parameter(torch.zeros(3))
+    tg = make_optimizer([p], solver, 2e-3, 0.99).param_groups[0]
+    assert set(pg) == set(tg) - {"params"}
+    for k, v in tg.items():
+        if k != "params":
+            assert pg[k] == pytest.approx(v) if isinstance(v, float) else pg[k] == v, k
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("model_type", ["prodLDA", "LDA", "combined", "zeroshot"])
 @pytest.mark.parametrize("solver", SOLVERS)
