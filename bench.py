@@ -11,20 +11,34 @@ One *step* = one federation round exactly as the reference defines it
 (federated_avitm.py:51-147 + server.py:436-521): every client does one local
 minibatch step (forward, backward, Adam) and the sample-weighted average of
 all shared tensors (the 20 AVITM state_dict tensors of grads_to_share) replaces
-every client's copy.  On MI355X: fused HIP step (hipGraph replay) + one RCCL
-all-reduce of the pre-scaled flat state over xGMI.
+every client's copy.  On MI355X: fused HIP step + the FedAvg all-reduce over
+xGMI captured in the same hipGraph (one replay per round).
+
+``--path runner`` (default) times the PRODUCTION round loop,
+:func:`gfedntm_amd.federation.runner.run_distributed` -- what ``main.py
+--backend rccl`` users get, with its per-round client bookkeeping -- and reports
+the engine-only replay loop of the same engine next to it
+(``engine_only_ms_per_step``).  ``--path engine`` times the bare replay loop.
 
 Weak scaling: per-GPU work (one client, batch 64) is fixed as N grows.
-``value`` = N * 64 / round_time (all clients' training documents per second).
-Vocabulary consensus, init broadcast and the NPMI evaluation run outside the
-timed region.
+``value`` = total training documents of all clients / round time.  Vocabulary
+consensus, init broadcast and the NPMI evaluation run outside the timed region;
+the NPMI comes from a SEPARATE untimed federation of ``--npmi-steps`` rounds
+(default 2000), so it does not depend on ``--steps``.
 
-Launch: ``python bench.py`` (1 GPU) or
-``python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N``.
+``--sim-clients M`` (one GPU): M simulated clients in one process
+(:class:`LocalFederation`: all clients' steps + the in-process FedAvg kernel in
+one hipGraph per round) -- a side measurement with its own metric label.
+
+Launch: ``python bench.py`` (1 GPU); ``python bench.py --gpus N`` spawns N ranks
+itself (one per GPU) unless it was started by ``torch.distributed.run``
+(RANK / WORLD_SIZE in the environment).  ``GFEDNTM_REHEARSE_1GPU=1`` puts every
+rank on cuda:0 over gloo (protocol rehearsal on a one-GPU box; timings meaningless).
 """
 import argparse
 import json
 import os
+import socket
 import sys
 import time
 
@@ -35,25 +49,24 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from gfedntm_amd.data.bow import BatchPlan, DeviceCSR  # noqa: E402
-from gfedntm_amd.data.synthetic import (generate_synthetic, node_vocabulary_terms,  # noqa: E402
-                                        remap_to_vocabulary)
-from gfedntm_amd.data.vocab import union_vocabulary, vocabulary_dict  # noqa: E402
-from gfedntm_amd.models import AVITM, CombinedTM, ZeroShotTM  # noqa: E402
-from gfedntm_amd.parallel.aggregator import CollectiveAggregator  # noqa: E402
-from gfedntm_amd.utils.config import DEFAULT_GRADS_TO_SHARE  # noqa: E402
-
 # Reference numbers (BASELINE.md part B, measured on the unmodified reference):
 # 8-client loopback gRPC federation with the built-in sleeps removed.
 BASELINE_FED_DOCS_PER_S = 111.0
 BASELINE_CPU_CENTRALIZED_DOCS_PER_S = 17300.0
+METRIC = "docs/sec (whole node) + NPMI, ProdLDA K=50 8-client fed on synthetic BoW"
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=2000)
     p.add_argument("--warmup", type=int, default=200)
+    p.add_argument("--path", default="runner", choices=["runner", "engine"])
+    p.add_argument("--sim-clients", type=int, default=0,
+                   help="M > 0: M simulated clients on one GPU (LocalFederation round graph)")
+    p.add_argument("--serial-clients", action="store_true",
+                   help="--sim-clients: capture the clients' steps one after the other "
+                        "(default: each client on its own graph branch)")
     p.add_argument("--model", default="prodLDA", choices=["prodLDA", "LDA"])
     p.add_argument("--family", default="avitm", choices=["avitm", "ctm", "zeroshot"],
                    help="ctm = CombinedTM, zeroshot = ZeroShotTM, with --contextual-size "
@@ -64,196 +77,318 @@ def parse():
     p.add_argument("--hidden", default="50,50")
     p.add_argument("--batch", type=int, default=64)
     p.add_argument("--docs", type=int, default=1000)
+    p.add_argument("--nwords", default="150,250", help="document length range [lo, hi)")
     p.add_argument("--backend", default="fused", choices=["fused", "torch"])
+    p.add_argument("--allreduce", default=None, choices=[None, "auto", "xgmi", "rccl"],
+                   help="FedAvg collective (default: auto = validated xGMI kernel, else RCCL)")
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--npmi-steps", type=int, default=2000,
+                   help="rounds of the separate untimed federation the NPMI is computed on "
+                        "(0 = skip)")
     p.add_argument("--no-npmi", action="store_true")
     p.add_argument("--solver", default="adam",
                    choices=["adam", "sgd", "adagrad", "adadelta", "rmsprop"],
                    help="optimizer (reference default adam; the others run in gradient mode)")
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
-def main():
-    args = parse()
+# ---------------------------------------------------------------------------
+# process setup
+# ---------------------------------------------------------------------------
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawned(local_rank: int, world: int, port: int, argv):
+    os.environ.update(RANK=str(local_rank), LOCAL_RANK=str(local_rank), WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    run(parse(argv))
+
+
+def _init(args):
+    """(rank, world, device, rehearse); initialises the process group (also for one rank,
+    so the production runner sees the same control plane at every N)."""
+    rehearse = os.environ.get("GFEDNTM_REHEARSE_1GPU") == "1"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    # GFEDNTM_REHEARSE_1GPU=1: rehearse the multi-rank path on a one-GPU box -- every
-    # rank on cuda:0, gloo process group (timings are meaningless, the code path and
-    # the xGMI all-reduce protocol are the real ones)
-    rehearse = os.environ.get("GFEDNTM_REHEARSE_1GPU") == "1"
+    local_rank = 0 if rehearse else int(os.environ.get("LOCAL_RANK", "0"))
+    if "MASTER_PORT" not in os.environ:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
+                          RANK="0", WORLD_SIZE="1")
+    torch.cuda.set_device(local_rank)
     if rehearse:
-        local_rank = 0
-    if world > 1:
-        torch.cuda.set_device(local_rank)
-        if rehearse:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    device = torch.device("cuda", local_rank)
-    n_clients = world
-
-    # ---- data: reference synthetic generator, one node per client ----
-    corpus = generate_synthetic(vocab_size=args.vocab, n_topics=args.topics, n_docs=args.docs,
-                                n_nodes=max(n_clients, 1), frozen_topics=5, seed=args.seed)
-    # ---- stage 1: vocabulary consensus (sorted union of local vocabularies) ----
-    local_terms = node_vocabulary_terms(corpus, rank)
-    if world > 1:
-        gathered = [None] * world
-        dist.all_gather_object(gathered, local_terms)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     else:
-        gathered = [local_terms]
-    terms = union_vocabulary(gathered)
-    vocab = vocabulary_dict(terms)
-    X = remap_to_vocabulary(corpus, rank, vocab)
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local_rank))
+    return rank, world, torch.device("cuda", local_rank), rehearse
 
-    hidden = tuple(int(h) for h in args.hidden.split(","))
-    torch.manual_seed(args.seed)
-    kw = dict(input_size=len(terms), n_components=args.topics, model_type=args.model,
-              hidden_sizes=hidden, batch_size=args.batch, verbose=False, backend=args.backend,
-              device=device, shared_keys=DEFAULT_GRADS_TO_SHARE, seed=args.seed,
-              solver=args.solver)
-    ctx = None
+
+# ---------------------------------------------------------------------------
+# data / params
+# ---------------------------------------------------------------------------
+def _corpus(args, n_nodes: int):
+    from gfedntm_amd.data.synthetic import generate_synthetic
+    lo, hi = (int(x) for x in args.nwords.split(","))
+    return generate_synthetic(vocab_size=args.vocab, n_topics=args.topics, n_docs=args.docs,
+                              n_nodes=max(n_nodes, 1), frozen_topics=5, nwords=(lo, hi),
+                              seed=args.seed)
+
+
+def _client_corpus(args, sc, node: int):
+    from gfedntm_amd.federation.data import ClientCorpus
+    emb = None
     if args.family in ("ctm", "zeroshot"):
         # SBERT is not available offline: per-document embeddings are synthetic
         # (a fixed random projection of the document's topic mixture plus noise)
-        rng = np.random.default_rng(args.seed + 17 * rank)
+        rng = np.random.default_rng(args.seed + 17 * node)
         proj = np.random.default_rng(args.seed).standard_normal(
             (args.topics, args.contextual_size)).astype(np.float32)
-        ctx = (np.asarray(corpus.doc_topics[rank], dtype=np.float32) @ proj
-               + 0.1 * rng.standard_normal((X.shape[0], args.contextual_size)).astype(np.float32))
-        cls = CombinedTM if args.family == "ctm" else ZeroShotTM
-        tm = cls(contextual_size=args.contextual_size, **kw)
-    else:
-        tm = AVITM(**kw)
-    eng = tm.engine
-    agg, comm = None, None
-    if world > 1:
-        dist.broadcast(tm.flat.buffer, src=0)        # identical W0 on every client
-        agg = CollectiveAggregator(method="rccl")
-        w = agg.weights(X.shape[0], device)
-        if args.backend == "fused":
-            eng.set_fedavg_scale(w[rank])
-            # the all-reduce becomes part of the step (custom xGMI kernel captured in the
-            # step graph, beta's share overlapped with the encoder backward) or follows
-            # it (RCCL) -- see FusedEngine.attach_fedavg
-            comm = eng.attach_fedavg()
-        else:
-            comm = agg.prepare(tm.flat.shared)
-    data = DeviceCSR(X, device, contextual=ctx)
-    n_steps = args.warmup + args.steps
-    plan = BatchPlan.build(data.n_docs, args.batch, n_steps, seed=args.seed + rank)
-    eng.bind_data(data, plan)
-    if args.backend == "fused" and not args.no_graph:
-        eng.enable_graph(True)
-        eng.warm_graph()
-    if world > 1:                 # ranks enter the first (collective) step together
-        torch.cuda.synchronize()
-        dist.barrier()
+        dt = np.asarray(sc.doc_topics[node], dtype=np.float32)
+        emb = dt @ proj + 0.1 * rng.standard_normal(
+            (dt.shape[0], args.contextual_size)).astype(np.float32)
+    return ClientCorpus(synthetic=sc, node=node, embeddings=emb)
 
-    shared = tm.flat.shared
 
-    def round_(s):
-        eng.step(s)
-        if agg is not None and args.backend != "fused":
-            shared.mul_(w[rank])
-            agg.allreduce_(shared)
+def _params(args):
+    from gfedntm_amd.utils.config import load_config
+    p = dict(load_config().training_params)
+    p.update(n_components=args.topics, model_type=args.model, batch_size=args.batch,
+             hidden_sizes=tuple(int(h) for h in args.hidden.split(",")), solver=args.solver,
+             contextual_size=args.contextual_size, num_epochs=10 ** 6)
+    return p
 
-    for s in range(args.warmup):
-        round_(s)
+
+def _model_type(args) -> str:
+    return {"avitm": "avitm", "ctm": "ctm", "zeroshot": "zeroshot"}[args.family]
+
+
+def _npmi(tm, sc, terms, n_nodes, device) -> float:
+    import scipy.sparse as sp
+    from gfedntm_amd.data.synthetic import remap_to_vocabulary
+    from gfedntm_amd.data.vocab import vocabulary_dict
+    from gfedntm_amd.eval.metrics import npmi_coherence
+    vocab = vocabulary_dict(terms)
+    ref = sp.vstack([remap_to_vocabulary(sc, i, vocab) for i in range(n_nodes)])
+    topics_idx = torch.topk(tm.model.beta.detach(), 10, dim=1).indices.cpu().numpy()
+    return float(npmi_coherence(topics_idx, ref, device=device))
+
+
+def _union_terms(sc, n_nodes):
+    from gfedntm_amd.data.synthetic import node_vocabulary_terms
+    from gfedntm_amd.data.vocab import union_vocabulary
+    return union_vocabulary([node_vocabulary_terms(sc, i) for i in range(n_nodes)])
+
+
+# ---------------------------------------------------------------------------
+# measurements
+# ---------------------------------------------------------------------------
+def _max_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64)
+    g = _ctrl_group()
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=g)
+    return float(t.item())
+
+
+_CTRL = None
+
+
+def _ctrl_group():
+    global _CTRL
+    if _CTRL is None:
+        _CTRL = dist.new_group(backend="gloo") if dist.get_backend() != "gloo" else dist.group.WORLD
+    return _CTRL
+
+
+def _engine_loop(eng, s0: int, s1: int, world: int) -> float:
+    """Bare replay loop over steps [s0, s1) of an already warmed engine: seconds (max over
+    ranks), barrier + device sync on both sides."""
     torch.cuda.synchronize()
     if world > 1:
-        dist.barrier()
+        dist.barrier(group=_ctrl_group())
     t0 = time.perf_counter()
-    for s in range(args.warmup, n_steps):
-        round_(s)
+    for s in range(s0, s1):
+        eng.step(s)
     torch.cuda.synchronize()
     if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    comm_error = eng.fedavg_error() if args.backend == "fused" else 0
-    if comm_error:                              # a timed-out wait invalidates the run
-        raise RuntimeError(f"xGMI all-reduce reported error {comm_error}")
-    ms = dt / args.steps * 1e3
-    docs_per_s = n_clients * args.batch * args.steps / dt
-    losses = eng.loss_hist.detach().cpu().numpy()
+        dist.barrier(group=_ctrl_group())
+    return _max_over_ranks(time.perf_counter() - t0, world)
 
+
+def run_federated(args):
+    from gfedntm_amd.federation.runner import run_distributed
+    rank, world, device, rehearse = _init(args)
+    _ctrl_group()
+    sc = _corpus(args, world)
+    corpus = _client_corpus(args, sc, rank)
+    params = _params(args)
+    n_rounds = args.warmup + args.steps
+    kw = dict(params=params, model_type=_model_type(args), backend=args.backend,
+              seed=args.seed, graph=not args.no_graph, allreduce=args.allreduce,
+              rehearse_1gpu=rehearse)
+    # ---- timed: the production round loop ----
+    out = run_distributed(corpus, max_iters=n_rounds, timing_warmup=args.warmup, **kw)
+    client = out["client"]
+    eng = client.tm.engine
+    wall = _max_over_ranks(out["wall_s"], world)
+    timed_rounds = out["timed_rounds"]
+    t = torch.tensor([float(out["docs"])], dtype=torch.float64)
+    dist.all_reduce(t, group=_ctrl_group())
+    docs = float(t.item())                       # all clients' training documents
+    ms_runner = wall / max(timed_rounds, 1) * 1e3
+    # ---- the same engine's bare replay loop (collective still attached) ----
+    engine_ms = None
+    compute_ms = None
+    if args.backend == "fused":
+        dt = _engine_loop(eng, args.warmup, n_rounds, world)
+        engine_ms = dt / args.steps * 1e3
+        err = eng.fedavg_error()
+        if world > 1:
+            # round split: the same steps again with the collective detached
+            saved = eng.detach_fedavg(close=False)
+            dt2 = _engine_loop(eng, args.warmup, n_rounds, world)
+            compute_ms = dt2 / args.steps * 1e3
+            eng.restore_fedavg(saved)
+        if err:
+            raise RuntimeError(f"xGMI all-reduce reported error {err}")
+    used = out["allreduce"]
+    final_loss = float(np.mean(eng.loss_hist[max(0, n_rounds - 20): n_rounds].cpu().numpy()))
+    if args.backend == "fused":
+        eng.detach_fedavg()
+    # ---- NPMI: a separate untimed federation of a fixed number of rounds ----
     npmi = None
-    if rank == 0 and not args.no_npmi:
-        from gfedntm_amd.eval.metrics import npmi_coherence
-        from gfedntm_amd.data.synthetic import remap_to_vocabulary as remap
-        import scipy.sparse as sp
-        ref_corpus = sp.vstack([remap(corpus, i, vocab) for i in range(max(n_clients, 1))])
-        topics_idx = torch.topk(tm.model.beta.detach(), 10, dim=1).indices.cpu().numpy()
-        npmi = float(npmi_coherence(topics_idx, ref_corpus, device=device))
-
-    # round latency split (BASELINE: compute / all-reduce / host): the same number of
-    # steps again with the collective detached, after the timed region
-    split = None
-    if world > 1 and args.backend == "fused" and eng._comm is not None:
-        saved_comm = eng._comm
-        eng._comm = None
-        eng._invalidate_graph()
-        k2 = max(1, min(args.steps, 500))
-        for s in range(n_steps, n_steps + min(args.warmup, 50)):
-            eng.step(s % n_steps)
-        torch.cuda.synchronize()
-        dist.barrier()
-        t1 = time.perf_counter()
-        for s in range(k2):
-            eng.step(s % n_steps)
-        torch.cuda.synchronize()
-        tc = torch.tensor([(time.perf_counter() - t1) / k2 * 1e3], dtype=torch.float64,
-                          device=device)
-        dist.all_reduce(tc, op=dist.ReduceOp.MAX)
-        eng._comm = saved_comm
-        split = {"compute_ms": round(float(tc.item()), 5)}
-    if split is not None:
-        split["allreduce_exposed_ms"] = round(max(ms - split["compute_ms"], 0.0), 5)
-
+    if not args.no_npmi and args.npmi_steps > 0:
+        out2 = run_distributed(corpus, max_iters=args.npmi_steps, **kw)
+        if rank == 0:
+            npmi = _npmi(out2["client"].tm, sc, _union_terms(sc, world), world, device)
+        if args.backend == "fused":
+            out2["client"].tm.engine.detach_fedavg()
     if rank == 0:
-        out = {
-            "metric": "docs/sec (whole node) + NPMI, ProdLDA K=50 8-client fed on synthetic BoW",
-            "value": round(docs_per_s, 1),
-            "unit": "docs/s",
-            "n_gpus": n_clients,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms, 5),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": round(docs_per_s / BASELINE_FED_DOCS_PER_S, 2),
-            "dtype": "fp32",
-            "data": "synthetic (reference LDA generator: V=5000, K=50, 1000 docs/client, "
-                    "150-250 tokens, 5 frozen topics), random init",
-            "config": {"model": ((f"CombinedTM-{args.model} C={args.contextual_size}"
-                                  if args.family == "ctm" else
-                                  f"ZeroShotTM-{args.model} C={args.contextual_size}")
-                                 if args.family in ("ctm", "zeroshot") else args.model)
-                                + f" K={args.topics} H={hidden} V={len(terms)}",
-                       "global_batch": args.batch * n_clients, "seq_len": None,
-                       "per_client_batch": args.batch, "clients": n_clients,
-                       "parallelism": f"fedavg-dp{n_clients}",
-                       "backend": args.backend + ("" if args.no_graph else "+hipgraph"),
-                       "solver": args.solver,
-                       "aggregation": "per-minibatch sample-weighted FedAvg of 20 shared tensors"
-                                      + (f" ({comm} all-reduce)" if world > 1 else "")},
-            "npmi": None if npmi is None else round(npmi, 4),
-            "round_split_ms": split if split is not None else {"compute_ms": round(ms, 5),
-                                                               "allreduce_exposed_ms": 0.0},
-            "final_loss": float(np.mean(losses[-20:])),
-            "baseline": {"fed_grpc_8clients_docs_per_s": BASELINE_FED_DOCS_PER_S,
-                         "cpu_centralized_docs_per_s": BASELINE_CPU_CENTRALIZED_DOCS_PER_S},
-        }
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+        value = docs / wall
+        terms_n = len(client.tm.train_data.idx2token) if hasattr(client.tm.train_data, "idx2token") \
+            else client.tm.input_size
+        record = _record(args, world, value, ms_runner, terms_n, npmi, final_loss)
+        record["path"] = args.path
+        record["engine_only_ms_per_step"] = None if engine_ms is None else round(engine_ms, 5)
+        record["runner_overhead_pct"] = (None if engine_ms is None else
+                                         round(100.0 * (ms_runner / engine_ms - 1.0), 2))
+        if args.path == "engine" and engine_ms is not None:
+            # headline from the bare replay loop instead
+            record["ms_per_step"] = round(engine_ms, 5)
+            record["value"] = round(world * args.batch / (engine_ms * 1e-3), 1)
+            record["vs_baseline"] = round(record["value"] / BASELINE_FED_DOCS_PER_S, 2)
+        record["config"]["aggregation"] += f" ({used or 'none: one client'} all-reduce)"
+        split = {"round_ms": round(record["ms_per_step"], 5)}
+        if compute_ms is not None:
+            split["compute_ms"] = round(compute_ms, 5)
+            split["allreduce_exposed_ms"] = round(max(engine_ms - compute_ms, 0.0), 5)
+        split["host_ms"] = round(max(ms_runner - (engine_ms or ms_runner), 0.0), 5)
+        record["round_split_ms"] = split
+        if rehearse:
+            record["note"] = "GFEDNTM_REHEARSE_1GPU: all ranks on one GPU -- timings meaningless"
+        print(json.dumps(record), flush=True)
+    dist.barrier(group=_ctrl_group())
+    dist.destroy_process_group()
+
+
+def run_simulated(args):
+    """M simulated clients on one GPU (LocalFederation round graph)."""
+    from gfedntm_amd.federation.runner import LocalFederation
+    device = torch.device("cuda", 0)
+    torch.cuda.set_device(device)
+    M = args.sim_clients
+    sc = _corpus(args, M)
+    corpora = [_client_corpus(args, sc, i) for i in range(M)]
+    n_rounds = args.warmup + args.steps
+    fed = LocalFederation(corpora, _params(args), _model_type(args), n_rounds, device=device,
+                          backend=args.backend, seed=args.seed, graph=not args.no_graph,
+                          round_streams=not args.serial_clients)
+    out = fed.run(timing_warmup=args.warmup)
+    ms = out["wall_s"] / max(out["timed_rounds"], 1) * 1e3
+    value = out["docs"] / out["wall_s"]
+    npmi = None
+    if not args.no_npmi and args.npmi_steps > 0:
+        fed2 = LocalFederation(corpora, _params(args), _model_type(args), args.npmi_steps,
+                               device=device, backend=args.backend, seed=args.seed,
+                               graph=not args.no_graph, round_streams=not args.serial_clients)
+        fed2.run()
+        npmi = _npmi(fed2.clients[0].tm, sc, fed.terms, M, device)
+    eng = fed.clients[0].tm.engine
+    final_loss = float(np.mean(eng.loss_hist[max(0, n_rounds - 20): n_rounds].cpu().numpy()))
+    rec = _record(args, 1, value, ms, len(fed.terms), npmi, final_loss, clients=M)
+    rec["metric"] = f"docs/sec, ProdLDA K={args.topics} {M} simulated clients on ONE GPU"
+    rec["vs_baseline"] = None
+    rec["config"]["parallelism"] = f"fedavg-sim{M} (1 GPU)"
+    rec["config"]["aggregation"] += (" (in-process FedAvg kernel in one round graph"
+                                     + (", client branches" if not args.serial_clients else "") + ")"
+                                     if fed.round_graph else " (eager)")
+    rec["path"] = "LocalFederation"
+    print(json.dumps(rec), flush=True)
+
+
+def _record(args, n_gpus, value, ms, V, npmi, final_loss, clients=None):
+    hidden = tuple(int(h) for h in args.hidden.split(","))
+    clients = n_gpus if clients is None else clients
+    fam = {"avitm": "", "ctm": "CombinedTM-", "zeroshot": "ZeroShotTM-"}[args.family]
+    ctx = f" C={args.contextual_size}" if args.family != "avitm" else ""
+    return {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "docs/s",
+        "n_gpus": n_gpus,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value / BASELINE_FED_DOCS_PER_S, 2),
+        "dtype": "fp32",
+        "data": (f"synthetic (reference LDA generator: V={args.vocab}, K={args.topics}, "
+                 f"{args.docs} docs/client, {args.nwords.replace(',', '-')} tokens, "
+                 "5 frozen topics), random init"),
+        "config": {"model": f"{fam}{args.model}{ctx} K={args.topics} H={hidden} V={V}",
+                   "global_batch": args.batch * clients, "seq_len": None,
+                   "per_client_batch": args.batch, "clients": clients,
+                   "parallelism": f"fedavg-dp{clients}",
+                   "backend": args.backend + ("" if args.no_graph else "+hipgraph"),
+                   "solver": args.solver,
+                   "aggregation": "per-minibatch sample-weighted FedAvg of the shared state"},
+        "clients_note": ("one client: FedAvg over one client is the identity; the 8-client "
+                         "figure is the --gpus 8 run" if clients == 1 else
+                         f"{clients} federated clients"),
+        "npmi": None if npmi is None else round(npmi, 4),
+        "npmi_rounds": None if npmi is None else args.npmi_steps,
+        "final_loss": final_loss,
+        "baseline": {"fed_grpc_8clients_docs_per_s": BASELINE_FED_DOCS_PER_S,
+                     "cpu_centralized_docs_per_s": BASELINE_CPU_CENTRALIZED_DOCS_PER_S},
+    }
+
+
+def run(args):
+    if args.sim_clients:
+        return run_simulated(args)
+    return run_federated(args)
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.sim_clients:
+        # self-launch: one rank per GPU, spawned before this process touches the GPU
+        import torch.multiprocessing as mp
+        port = _free_port()
+        mp.start_processes(_spawned, args=(args.gpus, port, argv), nprocs=args.gpus,
+                           start_method="spawn")
+        return
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws != args.gpus and not args.sim_clients:
+        print(f"bench.py: WORLD_SIZE={ws} overrides --gpus {args.gpus}", file=sys.stderr)
+    run(args)
 
 
 if __name__ == "__main__":

@@ -189,6 +189,51 @@ extern "C" __global__ void __launch_bounds__(CT) gfk_xgmi_allreduce(GfkComm c, f
 }
 
 // ---------------------------------------------------------------------------
+// In-process FedAvg of N simulated clients on one GPU (LocalFederation): every
+// client's pre-scaled shared state f_i becomes sum_i f_i, summed in client order
+// starting from f_0 (the same order as the xGMI kernel's phase 1, so one-GPU
+// simulations and the multi-GPU run agree bit for bit).  One launch replaces the
+// 2N + 1 eager kernels of a zero / add / copy sequence and is captured into the
+// federation's round graph.  The pointers are 16-byte aligned; a partial last float4 is summed
+// element-wise.
+// ---------------------------------------------------------------------------
+constexpr int LMAX = 16;
+
+struct GfkLocalAvg {
+  float* f[LMAX];
+  int32_t n_clients;
+  int32_t pad;
+  int64_t n;                     // floats
+};
+
+extern "C" __global__ void __launch_bounds__(256) gfk_local_fedavg(GfkLocalAvg a) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n4 = a.n >> 2;
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int64_t i = g; i < n4; i += stride) {
+    float4 acc = reinterpret_cast<const float4*>(a.f[0])[i];
+    for (int j = 1; j < a.n_clients; ++j) acc = add4(acc, reinterpret_cast<const float4*>(a.f[j])[i]);
+    for (int j = 0; j < a.n_clients; ++j) reinterpret_cast<float4*>(a.f[j])[i] = acc;
+  }
+  if (g < (a.n & 3)) {           // the partial float4 at the end: nothing past n is touched
+    const int64_t i = (n4 << 2) + g;
+    float acc = a.f[0][i];
+    for (int j = 1; j < a.n_clients; ++j) acc += a.f[j][i];
+    for (int j = 0; j < a.n_clients; ++j) a.f[j][i] = acc;
+  }
+}
+
+extern "C" size_t gfk_local_avg_struct_size() { return sizeof(GfkLocalAvg); }
+
+extern "C" int gfk_local_fedavg_launch(const GfkLocalAvg* a, int grid, hipStream_t s) {
+  if (a->n_clients < 1 || a->n_clients > LMAX || grid < 1) return -1;
+  for (int j = 0; j < a->n_clients; ++j)
+    if ((uintptr_t)a->f[j] & 15) return -1;
+  hipLaunchKernelGGL(gfk_local_fedavg, dim3(grid), dim3(256), 0, s, *a);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // host API (ctypes)
 // ---------------------------------------------------------------------------
 extern "C" size_t gfk_comm_struct_size() { return sizeof(GfkComm); }

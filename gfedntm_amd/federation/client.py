@@ -21,8 +21,10 @@ identical -- and the batch-norm running statistics are averaged separately
 
 Differences by design: the per-minibatch loss line needs the loss on the host,
 which would force a device sync every round, so it is logged every
-``log_every`` rounds (0 = never); the epoch summary reads the whole epoch's
-device-resident loss history with one sync.  The results are saved once when
+``log_every`` rounds (0 = never).  The epoch summary never stalls the device:
+at an epoch end the epoch's loss sum is reduced on device and copied into
+pinned host memory behind an event; the line is emitted (with the reference
+arithmetic) by :meth:`poll` once the event has completed, or by :meth:`flush`.  The results are saved once when
 ``num_epochs`` is reached (the reference re-runs inference and re-saves on every
 later round, B16) and, optionally, the client stops (``stop_at_num_epochs``).
 """
@@ -30,7 +32,7 @@ from __future__ import annotations
 
 import datetime
 import logging
-from typing import Optional
+from typing import List, Optional
 
 import numpy as np
 import torch
@@ -73,6 +75,19 @@ class FederatedClient:
         self.epoch_first_step = 0
         self.results_saved = False
         tm.best_components = tm.model.beta       # the reference keeps a live reference
+        # epoch summaries in flight: (epoch index, samples processed, pinned loss, event).
+        # The pinned ring, the events and the reduction kernel are set up here, not at
+        # the first epoch end, so no one-time cost lands inside the round loop.
+        self._pending: List[tuple] = []
+        self._pinned = None
+        self._events: List = []
+        self._slot = 0
+        hist = tm.engine.loss_hist
+        if hist.device.type == "cuda":
+            self._pinned = torch.zeros(64, dtype=torch.float32, pin_memory=True)
+            self._events = [torch.cuda.Event() for _ in range(self._pinned.numel())]
+            self._pinned[:1].copy_(hist[:1].sum().view(1), non_blocking=True)
+            torch.cuda.synchronize(hist.device)
 
     # ------------------------------------------------------------------ state
     @property
@@ -143,28 +158,94 @@ class FederatedClient:
                              loss, self.samples_processed)
         self.current_mb += 1
         if bool(self.plan.epoch_end[it]):
-            epoch_loss = float(self.tm.engine.loss_hist[self.epoch_first_step: it + 1].sum().item())
-            # reference arithmetic: train_loss accumulates and is divided by the running
-            # sample count at every epoch end (federated_avitm.py:107-119)
-            self.train_loss += epoch_loss
-            self.train_loss /= self.samples_processed
-            self.logger.info("Epoch: [%d/%d]\tSamples: [%d/%d]\tTrain Loss: %s\tTime: %s",
-                             self.current_epoch + 1, self.tm.num_epochs, self.samples_processed,
-                             self.n_docs * self.tm.num_epochs, self.train_loss,
-                             datetime.datetime.now())
-            if self.current_epoch == 0 or self.train_loss < self.tm.best_loss_train:
-                self.tm.best_loss_train = min(self.tm.best_loss_train, self.train_loss)
+            self._queue_epoch_summary(self.epoch_first_step, it)
             if self.epoch_snapshots and self.save_path:
+                self.flush()
                 self.save_results(self.save_path.replace(".npz", f"_epoch_{self.current_epoch}.npz"))
             self.current_epoch += 1
             self.current_mb = 0
             self.epoch_first_step = it + 1
         if self.current_epoch >= self.tm.num_epochs and not self.results_saved:
+            self.flush()
             self.logger.info("Epoch end reached")
             if self.save_path:
                 self.save_results(self.save_path)
             self.results_saved = True
+        self.poll()
         return self.results_saved
+
+    # ---- asynchronous epoch summaries
+    def _queue_epoch_summary(self, first: int, last: int):
+        hist = self.tm.engine.loss_hist
+        if hist.device.type != "cuda":
+            self._pending.append((self.current_epoch, self.samples_processed,
+                                  float(hist[first: last + 1].sum()), None))
+            self.poll()
+            return
+        # a ring of pinned slots: more epochs than slots can't be in flight at once
+        if len(self._pending) >= self._pinned.numel():
+            self.flush()
+        slot = self._slot
+        self._slot = (slot + 1) % self._pinned.numel()
+        dst = self._pinned[slot: slot + 1]
+        dst.copy_(hist[first: last + 1].sum().view(1), non_blocking=True)
+        ev = self._events[slot]
+        ev.record()
+        self._pending.append((self.current_epoch, self.samples_processed, dst, ev))
+
+    def _emit(self, epoch: int, samples: int, epoch_loss: float):
+        # reference arithmetic: train_loss accumulates and is divided by the running
+        # sample count at every epoch end (federated_avitm.py:107-119)
+        self.train_loss += epoch_loss
+        self.train_loss /= samples
+        self.logger.info("Epoch: [%d/%d]\tSamples: [%d/%d]\tTrain Loss: %s\tTime: %s",
+                         epoch + 1, self.tm.num_epochs, samples,
+                         self.n_docs * self.tm.num_epochs, self.train_loss,
+                         datetime.datetime.now())
+        if epoch == 0 or self.train_loss < self.tm.best_loss_train:
+            self.tm.best_loss_train = min(self.tm.best_loss_train, self.train_loss)
+
+    def poll(self, block: bool = False):
+        """Emit the epoch summaries whose device reduction has landed (in order)."""
+        while self._pending:
+            epoch, samples, val, ev = self._pending[0]
+            if ev is not None:
+                if not block and not ev.query():
+                    return
+                ev.synchronize()
+                val = float(val.item())
+            self._pending.pop(0)
+            self._emit(epoch, samples, float(val))
+
+    def flush(self):
+        """Emit every pending epoch summary (waits for the device)."""
+        self.poll(block=True)
+
+    def host_heavy_rounds(self) -> List[int]:
+        """Rounds after which this client does long host-side work (results / epoch
+        snapshot saves: full-shard inference + npz write).  A pure function of the
+        shard size, batch size and num_epochs, so every rank can agree on them up
+        front (the distributed runner aligns all ranks there)."""
+        if not self.save_path:
+            return []
+        ends = [int(i) for i in np.flatnonzero(self.plan.epoch_end)]
+        out = set(ends) if self.epoch_snapshots else set()
+        ne = int(self.tm.num_epochs)
+        if not self.results_saved:
+            if ne <= 0:
+                out.add(0)
+            elif len(ends) >= ne:
+                out.add(ends[ne - 1])
+        return sorted(out)
+
+    def done_round(self) -> Optional[int]:
+        """The round at whose end this client reaches ``num_epochs`` (None: never
+        within the plan)."""
+        ne = int(self.tm.num_epochs)
+        if ne <= 0:
+            return 0
+        ends = np.flatnonzero(self.plan.epoch_end)
+        return int(ends[ne - 1]) if len(ends) >= ne else None
 
     # ------------------------------------------------------------------ results
     def results(self):

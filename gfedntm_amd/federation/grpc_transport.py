@@ -161,7 +161,11 @@ class FederationServicer:
         nn_update = pb.NNUpdate(
             modelUpdate=wire.model_update_from_state(sd, -1),
             optUpdate=wire.adam_update_from_state_dict(self.global_tm.engine.optimizer_state_dict()))
-        fu = pb.FeatureUnion(initialNN=nn_update, model_params=wire.dictionary_from_params(self.params),
+        # the round count travels with the typed params, so every client sizes its batch
+        # plan (and loss history) for the rounds the server will actually drive
+        fu = pb.FeatureUnion(initialNN=nn_update,
+                             model_params=wire.dictionary_from_params(
+                                 {**self.params, "max_iters": int(self.max_iters)}),
                              model_type=self.model_type)
         fu.dic.append(wire.dictionary_from_vocab(vocab))
         self.shared_keys = [k for k in sd if k in set(self.grads_to_share)]
@@ -290,12 +294,18 @@ class ClientServicer:
 
     def getGradient(self, request, context):
         with self.lock:
-            return self._get_gradient(int(request.iter))
+            return self._get_gradient(int(request.iter), context)
 
-    def _get_gradient(self, it: int):
+    def _get_gradient(self, it: int, context=None):
         c = self.client
         if self._last is not None and self._last[0] == it:
             return self._last[1]
+        if not 0 <= it < c.max_iters:
+            msg = f"round {it} outside this client's plan of {c.max_iters} rounds"
+            if context is not None:
+                import grpc
+                context.abort(grpc.StatusCode.OUT_OF_RANGE, msg)
+            raise IndexError(msg)
         self.it = it
         c.local_step(self.it)
         hdr = pb.MessageHeader(id_request=f"ID{c.id}_{round(time.time())}",
@@ -359,6 +369,8 @@ def run_client(corpus, client_id: int, server_address: str, port: int, backend: 
         vocab = wire.vocab_from_dictionary(fu.dic[0])
         terms = [t for t, _ in sorted(vocab.items(), key=lambda kv: kv[1])]
         params = wire.params_from_dictionary(fu.model_params)
+        if "max_iters" in params:                 # the server's round count wins
+            max_iters = int(params.pop("max_iters"))
         ds = build_dataset(fu.model_type, corpus, vocab, terms)
         tm = make_topic_model(fu.model_type, params, len(terms), device, backend, grads_to_share,
                               seed=seed, logger=logger)
@@ -371,7 +383,8 @@ def run_client(corpus, client_id: int, server_address: str, port: int, backend: 
         path = client_model_path(save_client, client_id, stamp) if save_client else None
         client = FederatedClient(client_id, tm, ds, max_iters=max_iters,
                                  logger=logger, seed=seed + client_id, save_path=path,
-                                 log_every=log_every, epoch_snapshots=(fu.model_type == "ctm"))
+                                 log_every=log_every,
+                                 epoch_snapshots=(fu.model_type in ("ctm", "zeroshot")))
         client.enable_graph(graph)
         impl = ClientServicer(client, logger)
         server = grpc.server(cf.ThreadPoolExecutor(max_workers=2), options=list(server_options))

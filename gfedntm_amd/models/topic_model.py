@@ -157,7 +157,20 @@ class TopicModelBase:
     def _choose_backend(self, backend: str) -> str:
         if backend == "auto":
             from ..ops import engine as fused
-            return "fused" if fused.supports(self) else "torch"
+            from ..ops import native
+            if self.device.type != "cuda":
+                return "torch"
+            if not native.kernels_available():
+                # never a silent downgrade on a GPU: the kernel library is part of the build
+                raise RuntimeError(f"{native.KERNELS_SO} is missing on a GPU device: build it "
+                                   "(__graft_entry__.build()) or pass backend='torch'")
+            try:
+                fused.supports(self, explain=True)
+                return "fused"
+            except RuntimeError as e:
+                logging.getLogger("gfedntm_amd").warning(
+                    "%s; this configuration runs on the PyTorch engine", e)
+                return "torch"
         if backend == "fused":
             from ..ops import engine as fused
             if not fused.supports(self, explain=True):

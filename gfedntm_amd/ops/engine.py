@@ -676,6 +676,23 @@ class FusedEngine(EngineBase):
         self._invalidate_graph()
         return used
 
+    def detach_fedavg(self, close: bool = True):
+        """Remove the in-step all-reduce (returns it for :meth:`restore_fedavg` when
+        ``close`` is False; otherwise frees the xGMI buffers)."""
+        c, self._comm = self._comm, None
+        self._invalidate_graph()
+        if c is not None and close:
+            for k in ("rest", "beta"):
+                if k in c and c[k][0].xgmi is not None:
+                    c[k][0].xgmi.close()
+                    c[k][0].xgmi = None
+            return None
+        return c
+
+    def restore_fedavg(self, c):
+        self._comm = c
+        self._invalidate_graph()
+
     def fedavg_error(self) -> int:
         """Non-zero if an xGMI all-reduce wait timed out (synchronises)."""
         if self._comm is None:
@@ -868,13 +885,11 @@ class FusedEngine(EngineBase):
             self._ctx_bwd()
             torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph()
-        saved =(self.d_step.clone(), self.adam_t.clone(), self.adam_pow.clone(),
+        saved = (self.d_step.clone(), self.adam_t.clone(), self.adam_pow.clone(),
                  self.adam_coef.clone())
-        snap = self._snapshot()
         with torch.cuda.graph(g):
             self._launch(self.phases())
-        # capture does not execute; restore anything touched defensively
-        self._restore(snap)
+        # capture does not execute; restore the device counters defensively
         self.d_step.copy_(saved[0])
         self.adam_t.copy_(saved[1])
         self.adam_pow.copy_(saved[2])
@@ -887,11 +902,25 @@ class FusedEngine(EngineBase):
         if self.graph_enabled and self._graph is None:
             self._capture()
 
-    def _snapshot(self):
-        return None
+    # ---- external capture (LocalFederation's round graph: all clients' steps and
+    # the in-process FedAvg kernel in one hipGraph)
+    def prepare_external_capture(self):
+        """Run anything that must not happen for the first time inside a capture."""
+        if self._ctx is not None and not self.ctx_fused:
+            self._ctx_fwd()
+            self._ctx_bwd()
+            torch.cuda.synchronize(self.device)
 
-    def _restore(self, snap):
-        return None
+    def launch_step_phases(self):
+        """Enqueue one step's kernels on the current stream (no graph of its own;
+        the device step counter advances itself, the host tracks it with
+        :meth:`advance_host_step`)."""
+        if self._comm is not None:
+            raise RuntimeError("external capture is for in-process federations (no collective)")
+        self._launch(self.phases())
+
+    def advance_host_step(self, s: int):
+        self._host_step = s + 1
 
     def sync_step_counter(self, s: int):
         if s != self._host_step:

@@ -17,6 +17,8 @@ the caller can overlap host bookkeeping with the collective.
 """
 from __future__ import annotations
 
+import ctypes
+import time
 from typing import List, Optional, Sequence
 
 import torch
@@ -46,6 +48,7 @@ class CollectiveAggregator:
         self.method = (method or os.environ.get("GFEDNTM_ALLREDUCE", "auto")).lower()
         self.xgmi = None
         self.active = "rccl"
+        self.tuning = None
 
     def prepare(self, flat: torch.Tensor) -> str:
         """Choose the all-reduce for buffers shaped like ``flat`` (call once, on every
@@ -69,6 +72,20 @@ class CollectiveAggregator:
         flags: List = [None] * self.world
         dist.all_gather_object(flags, xg is not None, group=self.group)
         ok = ok and all(flags) and xg.validate()
+        if ok and self.method == "auto" and dist.get_backend(self.group) == "nccl":
+            # measured choice on this node: time both collectives on this size (the
+            # slowest rank's time decides, so every rank takes the same branch).  The
+            # xGMI kernel keeps a 10 % edge: it is captured in the step graph and
+            # overlapped with the backward, RCCL runs after the step.
+            tx = self._time(xg.allreduce_, flat)
+            tr = self._time(lambda b: dist.all_reduce(b, group=self.group), flat)
+            t = torch.tensor([tx, tr], dtype=torch.float64, device=flat.device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+            tx, tr = (float(v) for v in t.tolist())
+            self.tuning = {"xgmi_ms": round(tx, 4), "rccl_ms": round(tr, 4),
+                           "bytes": 4 * flat.numel()}
+            if tr < 0.9 * tx:
+                ok = False
         if ok:
             self.xgmi, self.active = xg, "xgmi"
         else:
@@ -78,6 +95,20 @@ class CollectiveAggregator:
                 raise RuntimeError("xGMI all-reduce requested but unavailable / failed validation")
             self.active = "rccl"
         return self.active
+
+    def _time(self, fn, like: torch.Tensor, iters: int = 10, warmup: int = 3) -> float:
+        """Mean ms of ``fn`` (an in-place all-reduce) on a scratch buffer shaped like
+        ``like``; every rank runs it the same number of times."""
+        buf = torch.zeros_like(like)
+        for _ in range(warmup):
+            fn(buf)
+        torch.cuda.synchronize(like.device)
+        dist.barrier(group=self.group)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn(buf)
+        torch.cuda.synchronize(like.device)
+        return (time.perf_counter() - t0) / iters * 1e3
 
     def weights(self, n_local: int, device) -> List[float]:
         t = torch.tensor([float(n_local)], dtype=torch.float64, device=device)
@@ -109,16 +140,66 @@ class CollectiveAggregator:
         self.allreduce_(flat)
 
 
+class _GfkLocalAvg(ctypes.Structure):
+    _fields_ = [("f", ctypes.c_void_p * 16), ("n_clients", ctypes.c_int32),
+                ("pad", ctypes.c_int32), ("n", ctypes.c_int64)]
+
+
 class LocalAggregator:
-    """In-process FedAvg over N client flat buffers (exact reference order of ops)."""
+    """In-process FedAvg over N client flat buffers (exact reference order of ops).
+
+    On a GPU, pre-scaled buffers of up to 16 clients are summed by one HIP kernel
+    (csrc/comm.hip ``gfk_local_fedavg``: client-order sum written back to every
+    client, capture-safe); the eager torch sequence is the CPU / oracle path."""
 
     def __init__(self, n_samples: Sequence[int]):
         self.n = [int(x) for x in n_samples]
         self.w = fedavg_weights(self.n)
+        self._desc = None
+
+    def _native(self, flats: Sequence[torch.Tensor]) -> bool:
+        if len(flats) > 16 or flats[0].device.type != "cuda":
+            return False
+        n = flats[0].numel()
+        return all(f.device == flats[0].device and f.dtype == torch.float32 and f.is_contiguous()
+                   and f.numel() == n and f.data_ptr() % 16 == 0 for f in flats)
+
+    def fused_sum_(self, flats: Sequence[torch.Tensor]):
+        """flats[i] <- sum_j flats[j] (client order) for all i, one kernel launch on the
+        current stream.  Returns False when the buffers don't qualify (caller falls back)."""
+        if len(flats) == 1:
+            return True
+        if not self._native(flats):
+            return False
+        C = ctypes
+        from ..ops import native
+        lib = native.kernels()
+        if not getattr(lib, "_gfk_local_avg_declared", False):
+            lib.gfk_local_avg_struct_size.restype = C.c_size_t
+            lib.gfk_local_fedavg_launch.argtypes = [C.POINTER(_GfkLocalAvg), C.c_int, C.c_void_p]
+            if lib.gfk_local_avg_struct_size() != C.sizeof(_GfkLocalAvg):
+                raise RuntimeError("GfkLocalAvg ABI mismatch between csrc/comm.hip and aggregator.py")
+            lib._gfk_local_avg_declared = True
+        d = _GfkLocalAvg()
+        for j, f in enumerate(flats):
+            d.f[j] = f.data_ptr()
+        d.n_clients, d.n = len(flats), flats[0].numel()
+        cu = torch.cuda.get_device_properties(flats[0].device).multi_processor_count
+        grid = int(max(1, min(-(-d.n // 1024), 4 * cu)))
+        stream = torch.cuda.current_stream(flats[0].device).cuda_stream
+        rc = lib.gfk_local_fedavg_launch(C.byref(d), grid, C.c_void_p(stream))
+        if rc:
+            raise RuntimeError(f"gfk_local_fedavg_launch failed ({rc})")
+        self._desc = d
+        return True
 
     def average_(self, flats: Sequence[torch.Tensor], prescaled: bool = False,
                  out: Optional[torch.Tensor] = None):
         """flats[i] <- sum_j w_j flats[j] for all i (in place)."""
+        if len(flats) == 1 and prescaled:
+            return flats[0]
+        if prescaled and out is None and self.fused_sum_(flats):
+            return flats[0]
         acc = torch.zeros_like(flats[0]) if out is None else out.zero_()
         for w, f in zip(self.w, flats):
             if prescaled:

@@ -12,7 +12,10 @@ main thread hangs while this rank waits for it in a collective); then the
 ``on_failure`` callback runs (default: log, then hard-exit the process, since
 the main thread is typically blocked inside a collective that will never
 complete; the last round checkpoint is the resume point).  A rank that finishes
-normally publishes ``done`` so its silence is not mistaken for a failure.
+normally publishes ``done`` so its silence is not mistaken for a failure.  A
+rank inside legitimate long host work (results / snapshot saves, checkpoint
+I/O) publishes ``busy`` (:meth:`Heartbeat.busy`): its peers keep requiring its
+beats but exempt it from the "behind and stuck" rule until it clears the flag.
 
 Store traffic, not collectives: a heartbeat collective would have to be matched
 by every rank the same number of times, which ranks that finish at different
@@ -48,10 +51,19 @@ class Heartbeat:
         self.failed: List[int] = []
         self._seen: Dict[int, tuple] = {}
         self.progress = 0
+        self._busy = 0
 
     def mark(self, rnd: int, phase: int = 0):
         """Training-loop progress: 2 * round + phase (0 = local step, 1 = all-reduce)."""
         self.progress = 2 * int(rnd) + int(phase)
+
+    def busy(self, on: bool = True):
+        """Long host-side work in progress (published with the next beat)."""
+        self._busy = int(bool(on))
+        try:
+            self.store.set(self._key("beat", self.rank), f"b:{self.progress}:{self._busy}")
+        except Exception:
+            pass
 
     def _key(self, kind: str, r: int) -> str:
         return f"{self.prefix}/{kind}/{r}"
@@ -84,7 +96,7 @@ class Heartbeat:
             n += 1
             try:
                 mine = self.progress
-                self.store.set(self._key("beat", self.rank), f"{n}:{mine}")
+                self.store.set(self._key("beat", self.rank), f"{n}:{mine}:{self._busy}")
                 now = time.monotonic()
                 dead = []
                 for r, (last, t, prog, tp) in list(self._seen.items()):
@@ -92,8 +104,10 @@ class Heartbeat:
                     if v == "done":
                         self._seen.pop(r)
                         continue
-                    p = int(v.split(":")[1]) if ":" in v else prog
-                    if p != prog:
+                    f = v.split(":")
+                    p = int(f[1]) if len(f) > 1 else prog
+                    peer_busy = len(f) > 2 and f[2] == "1"
+                    if p != prog or peer_busy:
                         prog, tp = p, now
                     if v != last:
                         last, t = v, now

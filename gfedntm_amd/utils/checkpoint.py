@@ -27,6 +27,8 @@ def checkpoint_path(ckpt_dir: str, client_id: int, round_: int) -> str:
 
 def save_client_checkpoint(ckpt_dir: str, client, round_: int) -> str:
     os.makedirs(ckpt_dir, exist_ok=True)
+    if hasattr(client, "flush"):      # pending epoch summaries update the bookkeeping
+        client.flush()
     tm = client.tm
     eng = tm.engine
     state = {

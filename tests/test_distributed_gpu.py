@@ -1,0 +1,123 @@
+"""The production one-process-per-client runner (``run_distributed``) with the fused
+engine and the in-step xGMI all-reduce, rehearsed on the one GPU of the test box
+(every rank on cuda:0 over gloo; the IPC peer-memory protocol is the one used
+across xGMI).
+
+Reference round: src/federation/server.py:436-521 + client.py:135-183.
+
+* unequal shards, so each client reaches ``num_epochs`` (and saves its results:
+  full-shard inference + npz write, host work while the peers could be spinning
+  in the next round's all-reduce) at a different round, plus one rank stalled on
+  the host for 1.5 s before a round: the final shared state must be bit-identical
+  to the in-process :class:`LocalFederation` golden (client-order sum), with the
+  all-reduce's error word 0;
+* a spin bound far below the injected stall: every rank must fail with
+  ``CommError`` instead of producing a model.
+"""
+import os
+import socket
+import time
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+SIZES = (100, 70, 45)           # docs per client: num_epochs=2 reached at rounds 7, 5, 3
+ROUNDS = 12
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _corpora():
+    from gfedntm_amd.data.synthetic import generate_synthetic
+    from gfedntm_amd.federation.data import ClientCorpus
+    sc = generate_synthetic(vocab_size=600, n_topics=10, n_docs=max(SIZES), n_nodes=len(SIZES),
+                            frozen_topics=2, nwords=(30, 60), seed=3)
+    return [ClientCorpus(texts=sc.texts(i)[:n]) for i, n in enumerate(SIZES)]
+
+
+def _params():
+    from gfedntm_amd.utils.config import load_config
+    p = dict(load_config().training_params)
+    p.update(num_epochs=2, batch_size=32, hidden_sizes=(32, 32), n_components=10)
+    return p
+
+
+def _worker(rank, world, port, tmp, stall, spin, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if spin is not None:
+        os.environ["GFEDNTM_XGMI_SPIN"] = str(spin)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    try:
+        from gfedntm_amd.federation.runner import CommError, run_distributed
+
+        def hook(it):
+            if rank == 1 and it == 5:
+                time.sleep(stall)
+
+        try:
+            out = run_distributed(_corpora()[rank], _params(), max_iters=ROUNDS, backend="fused",
+                                  seed=5, save_client=os.path.join(tmp, "client"),
+                                  stamp="20240101", rehearse_1gpu=True, round_hook=hook)
+        except CommError as e:
+            q.put((rank, "comm_error", str(e)))
+            return
+        c = out["client"]
+        q.put((rank, out["allreduce"], c.shared.detach().cpu().numpy().copy(),
+               c.tm.engine.fedavg_error(), c.results_saved, c.current_epoch))
+        c.tm.engine.detach_fedavg()
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, "exception", traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(tmp, stall, spin=None):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = len(SIZES)
+    ps = [ctx.Process(target=_worker, args=(r, world, port, str(tmp), stall, spin, q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda r: r[0])
+    for p in ps:
+        p.join(60)
+    return res
+
+
+def test_run_distributed_xgmi_matches_local_golden(tmp_path):
+    res = _run(tmp_path, stall=1.5)
+    for r in res:
+        assert r[1] not in ("exception", "comm_error"), r
+    # golden: the same federation in one process (client-order sum, fused engine)
+    from gfedntm_amd.federation.runner import LocalFederation
+    fed = LocalFederation(_corpora(), _params(), max_iters=ROUNDS, device="cuda",
+                          backend="fused", seed=5)
+    assert fed.round_graph
+    fed.run()
+    gold = fed.clients[0].shared.detach().cpu().numpy()
+    for rank, used, shared, err, saved, epoch in res:
+        assert used.startswith("xgmi"), used
+        assert err == 0
+        assert saved and epoch >= 2
+        np.testing.assert_array_equal(shared, gold)
+    for i in range(1, len(SIZES) + 1):
+        assert os.path.exists(tmp_path / f"client{i}" / f"model_{i}_20240101.npz")
+
+
+def test_run_distributed_fails_loudly_on_a_timed_out_wait(tmp_path):
+    res = _run(tmp_path, stall=2.0, spin=2000)
+    for r in res:
+        assert r[1] == "comm_error", r[:2]

@@ -3,7 +3,10 @@
   gfedntm_amd/_lib/libgfedntm_kernels.so  -- HIP kernels + C++ step launcher (hipcc)
   gfedntm_amd/_lib/libgfedntm_runtime.so  -- host C++ runtime (tokenizer, CSR builder)
 
-Incremental: an object is rebuilt only when its source or a header is newer.
+Incremental: an object is rebuilt when its source or a header is newer, or when
+the compiler, target arch or flags differ from the ones recorded for it (a
+``.cmd`` file next to every object), so changing ``PYTORCH_ROCM_ARCH`` or a flag
+never links stale objects.
 """
 import concurrent.futures as cf
 import glob
@@ -22,19 +25,49 @@ KERNEL_SRCS = ["ctx.hip", "encoder.hip", "posterior.hip", "prodlda.hip", "neural
 RUNTIME_SRCS = ["runtime.cpp"]
 
 
-def _newer(src, obj, deps):
+def _stale(src, obj, deps, cmd):
+    """Rebuild if the object is missing, older than its inputs, or was built with a
+    different command line (compiler / arch / flags)."""
     if not os.path.exists(obj):
+        return True
+    try:
+        with open(obj + ".cmd") as f:
+            if f.read() != " ".join(cmd):
+                return True
+    except OSError:
         return True
     t = os.path.getmtime(obj)
     return any(os.path.getmtime(p) > t for p in [src] + deps)
 
 
 def _compile(args):
-    cmd, src = args
+    cmd, src, obj = args
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"compile failed for {src}:\n{r.stderr[-4000:]}")
+    with open(obj + ".cmd", "w") as f:
+        f.write(" ".join(cmd))
     return src
+
+
+def _link_stale(so, objs, cmd):
+    if not os.path.exists(so) or any(os.path.getmtime(o) > os.path.getmtime(so) for o in objs):
+        return True
+    try:
+        with open(os.path.join(OBJ, os.path.basename(so) + ".cmd")) as f:
+            return f.read() != " ".join(cmd)
+    except OSError:
+        return True
+
+
+def _link(so, cmd, verbose):
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode:
+        raise RuntimeError(r.stderr[-4000:])
+    with open(os.path.join(OBJ, os.path.basename(so) + ".cmd"), "w") as f:
+        f.write(" ".join(cmd))
+    if verbose:
+        print(f"[build] linked {so}", flush=True)
 
 
 def build(verbose=True, jobs=8):
@@ -48,10 +81,10 @@ def build(verbose=True, jobs=8):
             continue
         obj = os.path.join(OBJ, s + ".o")
         kobjs.append(obj)
-        if _newer(src, obj, headers):
-            cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
-                   "-munsafe-fp-atomics", "-Wno-unused-result", "-c", src, "-o", obj]
-            jobs_list.append((cmd, s))
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
+               "-munsafe-fp-atomics", "-Wno-unused-result", "-c", src, "-o", obj]
+        if _stale(src, obj, headers, cmd):
+            jobs_list.append((cmd, s, obj))
     robjs = []
     for s in RUNTIME_SRCS:
         src = os.path.join(CSRC, s)
@@ -59,31 +92,21 @@ def build(verbose=True, jobs=8):
             continue
         obj = os.path.join(OBJ, s + ".host.o")
         robjs.append(obj)
-        if _newer(src, obj, headers):
-            jobs_list.append((["g++", "-O3", "-fPIC", "-std=c++17", "-pthread", "-Wall", "-c", src,
-                              "-o", obj], s))
+        cmd = ["g++", "-O3", "-fPIC", "-std=c++17", "-pthread", "-Wall", "-c", src, "-o", obj]
+        if _stale(src, obj, headers, cmd):
+            jobs_list.append((cmd, s, obj))
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         for s in ex.map(_compile, jobs_list):
             if verbose:
                 print(f"[build] compiled {s}", flush=True)
     kso = os.path.join(LIB, "libgfedntm_kernels.so")
-    if kobjs and (not os.path.exists(kso) or any(os.path.getmtime(o) > os.path.getmtime(kso)
-                                                 for o in kobjs)):
-        r = subprocess.run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", kso] + kobjs,
-                           capture_output=True, text=True)
-        if r.returncode:
-            raise RuntimeError(r.stderr[-4000:])
-        if verbose:
-            print(f"[build] linked {kso}", flush=True)
+    kcmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", kso] + kobjs
+    if kobjs and _link_stale(kso, kobjs, kcmd):
+        _link(kso, kcmd, verbose)
     rso = os.path.join(LIB, "libgfedntm_runtime.so")
-    if robjs and (not os.path.exists(rso) or any(os.path.getmtime(o) > os.path.getmtime(rso)
-                                                 for o in robjs)):
-        r = subprocess.run(["g++", "-shared", "-fPIC", "-pthread", "-o", rso] + robjs, capture_output=True,
-                           text=True)
-        if r.returncode:
-            raise RuntimeError(r.stderr[-4000:])
-        if verbose:
-            print(f"[build] linked {rso}", flush=True)
+    rcmd = ["g++", "-shared", "-fPIC", "-pthread", "-o", rso] + robjs
+    if robjs and _link_stale(rso, robjs, rcmd):
+        _link(rso, rcmd, verbose)
     return kso
 
 
