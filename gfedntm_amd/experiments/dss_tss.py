@@ -13,8 +13,19 @@ documents of each node and evaluated on the next ``n_docs_global_inf``:
                federation clients -- per-minibatch sample-weighted FedAvg,
                LocalFederation on one device
 
+  federated_matched  (new) the same federation run for as many rounds as the
+               centralized model takes optimizer steps (equal update budget)
+
 TSS = sum over true topics of the best Bhattacharyya coefficient with a learned
-topic (learned betas re-indexed onto the generator vocabulary); DSS = mean
+topic (learned betas re-indexed onto the generator vocabulary).  With
+``reference_tss`` (default on) the betas go through the reference simulator's
+softmax chain: ``get_topic_word_distribution()`` is already softmax(beta), the
+simulator applies ``softmax`` again (run_simulation.py:417, :469) and its
+``convert_topic_word_to_init_size`` a third time (run_simulation.py:257) before
+the re-indexing + L1 normalisation, and that re-indexing shifts every word by one
+column (:func:`_reference_reindex`) -- the resulting, nearly uniform and shifted,
+topics are what the published TSS numbers (8.679 centralized at eta=0.01)
+measure.  ``reference_tss=False`` scores softmax(beta) on the correct columns.  DSS = mean
 absolute difference of the documents' Bhattacharyya similarity matrices, true
 vs inferred.  ``experiment`` 0 sweeps ``frozen_topics_list``, 1 sweeps
 ``eta_list`` (the topic Dirichlet parameter beta).  Results: ``results.json`` and
@@ -28,6 +39,7 @@ import argparse
 import json
 import logging
 import os
+import time
 from typing import Dict, List
 
 import numpy as np
@@ -45,9 +57,10 @@ DEFAULTS = dict(n_nodes=5, vocab_size=5000, n_topics=50, beta=1e-2, alpha=0.1, n
                 # model (run_simulation.py:271-318)
                 hidden_sizes=[100, 100], num_epochs=100, batch_size=64, lr=2e-3,
                 # new
-                federated=True, device=None, backend="auto", seed=0, arms=None)
+                federated=True, device=None, backend="auto", seed=0, arms=None,
+                reference_tss=True)
 
-ARMS = ("centralized", "non_colab", "baseline", "federated")
+ARMS = ("centralized", "non_colab", "baseline", "federated", "federated_matched")
 
 
 def _vocab_of(counts: sp.csr_matrix):
@@ -95,16 +108,45 @@ def train_and_score(cfg, train_counts: sp.csr_matrix, inf_counts: sp.csr_matrix,
     return _score(tm, id2token, vocab, cfg, inf_counts, topic_vectors, inf_thetas)
 
 
+def _softmax_rows(x: np.ndarray) -> np.ndarray:
+    x = np.asarray(x, dtype=np.float64)
+    e = np.exp(x - x.max(axis=1, keepdims=True))
+    return e / e.sum(axis=1, keepdims=True)
+
+
+def _reference_reindex(wd: np.ndarray, id2token: Dict[int, str], vocab_size: int) -> np.ndarray:
+    """The reference simulator's re-indexing, defect included: its documents name
+    generator column j 'wd<j>' (run_simulation.py:174) but the lookup list is
+    ``all_words = ['wd1' .. 'wd<V>']`` (run_simulation.py:418-420), so token 'wd<j>'
+    lands in column j - 1 and 'wd0' is dropped -- every learned topic is compared
+    with the ground truth shifted by one word."""
+    out = np.zeros((wd.shape[0], vocab_size), dtype=np.float64)
+    src = [i for i in range(wd.shape[1]) if int(id2token[i][2:]) >= 1]
+    cols = np.array([int(id2token[i][2:]) - 1 for i in src], dtype=np.int64)
+    out[:, cols] = wd[:, src]
+    s = out.sum(axis=1, keepdims=True)
+    s[s == 0] = 1.0
+    return out / s
+
+
 def _score(tm, id2token, vocab, cfg, inf_counts, topic_vectors, inf_thetas):
-    betas = betas_to_ground_truth_vocab(tm.get_topic_word_distribution(), id2token,
-                                        cfg["vocab_size"])
+    wd = tm.get_topic_word_distribution()                  # softmax(beta)
+    # the TSS of the learned topic-word distribution on the right columns ...
+    true_tss = tss(betas_to_ground_truth_vocab(wd, id2token, cfg["vocab_size"]), topic_vectors)
+    if cfg.get("reference_tss", True):
+        # ... and the number the reference simulator would print for the same model
+        wd = _softmax_rows(_softmax_rows(wd))              # run_simulation.py:417 + :257
+        betas = _reference_reindex(wd, id2token, cfg["vocab_size"])
+    else:
+        betas = betas_to_ground_truth_vocab(wd, id2token, cfg["vocab_size"])
     thetas = np.asarray(tm.get_doc_topic_distribution(BOWDataset(_remap(inf_counts, vocab),
                                                                  id2token)))
-    return tss(betas, topic_vectors), dss(inf_thetas, thetas)
+    return tss(betas, topic_vectors), dss(inf_thetas, thetas), true_tss
 
 
 def run_iteration(cfg, frozen_topics: int, eta: float, device, seed: int) -> Dict[str, tuple]:
-    arms = cfg.get("arms") or [a for a in ARMS if a != "federated" or cfg["federated"]]
+    arms = cfg.get("arms") or [a for a in ARMS
+                               if not a.startswith("federated") or cfg["federated"]]
     n_nodes, K, V = cfg["n_nodes"], cfg["n_topics"], cfg["vocab_size"]
     n_tr, n_inf = cfg["n_docs"], cfg["n_docs_global_inf"]
     nw = cfg["nwords"]
@@ -116,25 +158,44 @@ def run_iteration(cfg, frozen_topics: int, eta: float, device, seed: int) -> Dic
     inf_counts = sp.vstack([c[n_tr:n_tr + n_inf] for c in sc.counts]).tocsr()
     inf_thetas = np.concatenate([t[n_tr:n_tr + n_inf] for t in sc.doc_topics])
     out: Dict[str, tuple] = {}
+    log = logging.getLogger("gfedntm_amd.dss_tss")
+    t0 = time.perf_counter()
+
+    def done(arm):
+        log.info("  %-18s TSS %.3f DSS %.1f (TSS of softmax(beta) on the right columns "
+                 "%.3f) (%.1f s)", arm, out[arm][0], out[arm][1], out[arm][2],
+                 time.perf_counter() - t0)
     if "baseline" in arms:
         rng = np.random.default_rng(seed + 7)
         rand_topics = rng.dirichlet(V * [eta], K)
         priors = node_priors(K, n_nodes, frozen_topics, cfg["alpha"])
         rand_thetas = np.concatenate([rng.dirichlet(p, n_inf) for p in priors])
-        out["baseline"] = (tss(rand_topics, sc.topic_vectors), dss(inf_thetas, rand_thetas))
+        t = tss(rand_topics, sc.topic_vectors)
+        out["baseline"] = (t, dss(inf_thetas, rand_thetas), t)
+        done("baseline")
     if "centralized" in arms:
         out["centralized"] = train_and_score(cfg, sp.vstack(train).tocsr(), inf_counts,
                                              sc.topic_vectors, inf_thetas, device, seed)
+        done("centralized")
     if "non_colab" in arms:
         s = [train_and_score(cfg, c, inf_counts, sc.topic_vectors, inf_thetas, device, seed + i)
              for i, c in enumerate(train)]
-        out["non_colab"] = (float(np.mean([a for a, _ in s])), float(np.mean([b for _, b in s])))
+        out["non_colab"] = tuple(float(np.mean([r[j] for r in s])) for j in range(3))
+        done("non_colab")
     if "federated" in arms:
         out["federated"] = _federated(cfg, sc, train, inf_counts, inf_thetas, device, seed)
+        done("federated")
+    if "federated_matched" in arms:
+        # as many rounds as the centralized fit's optimizer steps (75 % train split)
+        n_central = int(0.75 * sum(c.shape[0] for c in train))
+        rounds = cfg["num_epochs"] * -(-n_central // cfg["batch_size"])
+        out["federated_matched"] = _federated(cfg, sc, train, inf_counts, inf_thetas, device,
+                                              seed, rounds=rounds)
+        done("federated_matched")
     return out
 
 
-def _federated(cfg, sc, train, inf_counts, inf_thetas, device, seed):
+def _federated(cfg, sc, train, inf_counts, inf_thetas, device, seed, rounds=None):
     from ..federation.data import ClientCorpus
     from ..federation.runner import LocalFederation
     sub = SyntheticCorpus(sc.topic_vectors, [t[: c.shape[0]] for t, c in zip(sc.doc_topics, train)],
@@ -144,8 +205,11 @@ def _federated(cfg, sc, train, inf_counts, inf_thetas, device, seed):
     params = {k: v for k, v in _model_kw(cfg, 0, device).items()
               if k not in ("input_size", "verbose", "backend", "device")}
     steps_per_epoch = -(-max(c.shape[0] for c in train) // cfg["batch_size"])
-    fed = LocalFederation(corpora, params, max_iters=cfg["num_epochs"] * steps_per_epoch,
-                          device=device, backend=cfg["backend"], seed=seed)
+    if rounds is None:
+        rounds = cfg["num_epochs"] * steps_per_epoch
+    params["num_epochs"] = -(-rounds // steps_per_epoch)
+    fed = LocalFederation(corpora, params, max_iters=rounds, device=device,
+                          backend=cfg["backend"], seed=seed)
     fed.run()
     tm = fed.clients[0].tm                     # every client holds the averaged state
     id2token = dict(enumerate(fed.terms))
@@ -179,7 +243,8 @@ def run(cfg: Dict, out_dir: str, logger=None) -> Dict:
         for k, vals in acc.items():
             a = np.asarray(vals, dtype=np.float64)
             row.update({f"{k}_betas_mean": a[:, 0].mean(), f"{k}_betas_std": a[:, 0].std(),
-                        f"{k}_thetas_mean": a[:, 1].mean(), f"{k}_thetas_std": a[:, 1].std()})
+                        f"{k}_thetas_mean": a[:, 1].mean(), f"{k}_thetas_std": a[:, 1].std(),
+                        f"{k}_tss_true_mean": a[:, 2].mean(), f"{k}_tss_true_std": a[:, 2].std()})
         rows.append(row)
     os.makedirs(out_dir, exist_ok=True)
     with open(os.path.join(out_dir, "results.json"), "w") as f:
@@ -193,10 +258,13 @@ def main(argv=None):
     p = argparse.ArgumentParser(description="DSS / TSS simulation")
     p.add_argument("--config", required=True, help="config.json (reference schema + extras)")
     p.add_argument("--out", required=True, help="results folder")
+    p.add_argument("--iters", type=int, default=None, help="override the config's iters")
     a = p.parse_args(argv)
     logging.basicConfig(level="INFO")
     with open(a.config, encoding="utf8") as f:
         cfg = json.load(f)
+    if a.iters is not None:
+        cfg["iters"] = a.iters
     return run(cfg, a.out)
 
 

@@ -44,6 +44,12 @@ def save_client_checkpoint(ckpt_dir: str, client, round_: int) -> str:
         "rng_cuda": (torch.cuda.get_rng_state(eng.device) if eng.device.type == "cuda"
                      else torch.zeros(0, dtype=torch.uint8)),
     }
+    if hasattr(eng, "adam_pow"):
+        # the fused kernels advance beta^t on device by repeated fp64 products;
+        # recomputing beta ** t on resume could differ in the last bit, so the device
+        # values travel verbatim (bitwise-exact resume)
+        state["adam_pow"] = eng.adam_pow.detach().cpu()
+        state["adam_coef"] = eng.adam_coef.detach().cpu()
     path = checkpoint_path(ckpt_dir, client.id, round_)
     tmp = path + ".tmp"
     torch.save(state, tmp)
@@ -78,6 +84,9 @@ def load_client_checkpoint(ckpt_dir: str, client, round_: Optional[int] = None) 
     torch.set_rng_state(st["rng_cpu"])
     if eng.device.type == "cuda" and st["rng_cuda"].numel():
         torch.cuda.set_rng_state(st["rng_cuda"], eng.device)
+    if hasattr(eng, "adam_pow") and "adam_pow" in st:
+        eng.adam_pow.copy_(st["adam_pow"].to(eng.adam_pow.device))
+        eng.adam_coef.copy_(st["adam_coef"].to(eng.adam_coef.device))
     if hasattr(eng, "seed") and hasattr(eng, "_m"):
         eng.seed = st["seed"]
         eng._m.seed = st["seed"]

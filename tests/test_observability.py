@@ -48,6 +48,29 @@ def test_heartbeat_detects_a_dead_peer_and_ignores_a_finished_one():
     c.stop()
 
 
+def test_heartbeat_exempts_a_busy_peer_from_the_behind_rule():
+    """A peer inside long host work (results save) publishes busy: it stays alive as
+    long as it beats, even while behind this rank's progress."""
+    store = _store()
+    seen = []
+    a = Heartbeat(0, 2, store=store, interval=0.05, timeout=0.4, on_failure=seen.append,
+                  prefix="t3").start()
+    b = Heartbeat(1, 2, store=store, interval=0.05, timeout=0.4, on_failure=lambda d: None,
+                  prefix="t3").start()
+    a.mark(10, 1)                         # rank 0 is ahead
+    b.mark(5, 1)
+    b.busy(True)                          # rank 1 saves its results for a while
+    time.sleep(1.2)
+    assert not seen
+    b.busy(False)                         # done, but now stuck behind: detected
+    t0 = time.time()
+    while not seen and time.time() - t0 < 5:
+        time.sleep(0.05)
+    assert seen == [[1]]
+    a._stop.set()
+    b._stop.set()
+
+
 def test_trace_ranges_are_safe_without_a_profiler():
     with trace.trace_range("unit-test"):
         trace.mark("inside")

@@ -108,10 +108,52 @@ def test_dss_tss_simulation_tiny(tmp_path):
     res = dss_tss.run(cfg, str(tmp_path))
     assert [r["frozen_topics"] for r in res["rows"]] == [1, 3]
     for r in res["rows"]:
-        for arm in ("centralized", "non_colab", "baseline", "federated"):
+        for arm in ("centralized", "non_colab", "baseline", "federated", "federated_matched"):
             assert np.isfinite(r[f"{arm}_betas_mean"]) and np.isfinite(r[f"{arm}_thetas_mean"])
             assert 0 < r[f"{arm}_betas_mean"] <= cfg["n_topics"] + 1e-6
     assert os.path.exists(tmp_path / "results.csv")
+
+
+def test_reference_tss_softmax_chain():
+    """reference_tss: softmax(beta) (get_topic_word_distribution) -> softmax
+    (run_simulation.py:417) -> softmax (run_simulation.py:257) -> the reference's
+    one-off re-index onto 'wd1'..'wd<V>' + L1 normalisation, as a literal
+    re-statement of the reference loop."""
+    from scipy.special import softmax
+    from gfedntm_amd.experiments import dss_tss
+    from gfedntm_amd.eval.metrics import tss
+
+    rng = np.random.default_rng(0)
+    K, Vl, Vg = 4, 30, 50
+    beta = rng.standard_normal((K, Vl)) * 3
+    id2token = {i: f"wd{j}" for i, j in enumerate(sorted(rng.choice(Vg, Vl, replace=False)))}
+    topic_vectors = rng.dirichlet([0.05] * Vg, K)
+
+    class TM:
+        def get_topic_word_distribution(self):
+            return softmax(beta, axis=1)
+
+        def get_doc_topic_distribution(self, ds):
+            return np.full((2, K), 1.0 / K)
+
+    betas = softmax(TM().get_topic_word_distribution(), axis=1)
+    wd = softmax(betas, axis=1)
+    all_words = ["wd" + str(w) for w in np.arange(Vg + 1) if w > 0]     # run_simulation.py:418
+    ref = np.zeros((K, Vg))
+    for i in range(K):
+        for idx, word in id2token.items():
+            for j in range(len(all_words)):
+                if all_words[j] == word:
+                    ref[i, j] = wd[i][idx]
+                    break
+    ref = ref / ref.sum(1, keepdims=True)
+    cfg = dict(vocab_size=Vg, reference_tss=True)
+    import scipy.sparse as sp
+    inf = sp.csr_matrix(np.ones((2, Vl), dtype=np.float32))
+    vocab = {t: i for i, t in id2token.items()}
+    got_tss, _, _ = dss_tss._score(TM(), id2token, vocab, cfg, inf, topic_vectors,
+                                np.full((2, K), 1.0 / K))
+    assert abs(got_tss - tss(ref, topic_vectors)) < 1e-9
 
 
 def test_collab_and_wmd(tmp_path):

@@ -27,6 +27,9 @@ def _worker(rank, world, port, n, q):
         from gfedntm_amd.parallel.aggregator import CollectiveAggregator
         from gfedntm_amd.parallel.xgmi import XgmiAllReduce
         xg = XgmiAllReduce(n, "cuda:0")
+        cu = torch.cuda.get_device_properties(0).multi_processor_count
+        chunk = (-(-n // world) + 3) // 4 * 4          # floats per rank, multiple of 4
+        assert xg.nblk == max(1, min(cu // world, chunk // 1024)), xg.nblk
         ok = xg.validate(rounds=3)
         # graph capture: the captured kernel advances its epoch on every replay
         t = torch.zeros(n, device="cuda")
@@ -57,7 +60,9 @@ def _worker(rank, world, port, n, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n", [(2, 1_000_003), (3, 446_650), (2, 10)])
+# 20_000_003 floats = the 80 MB beta share of ProdLDA K=200, V=100K: the size-aware
+# grid (one workgroup per >= 4 KB slice, CUs split among the ranks sharing the GPU)
+@pytest.mark.parametrize("world,n", [(2, 1_000_003), (3, 446_650), (2, 10), (2, 20_000_003)])
 def test_xgmi_allreduce_exact(world, n):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
