@@ -315,8 +315,9 @@ __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkModel m) {
       for (int w = 0; w < ENC_WAVES; ++w) z += red[w * H0 + tid];
     }
     if (input != GFK_IN_BOW && !m.ctx_fused) z += m.ws_hctx[(size_t)b * H0 + tid];
-    float a = act_f(act, z);
-    m.ws_z[0][(size_t)b * H0 + tid] = z;
+    float zs;
+    float a = act_train(act, z, m.seed, (uint32_t)step, 0, (uint32_t)(b * H0 + tid), &zs);
+    m.ws_z[0][(size_t)b * H0 + tid] = zs;
     m.ws_a[0][(size_t)b * H0 + tid] = a;
     if (nh == 1) {
       a *= maskh[tid];
@@ -343,8 +344,9 @@ __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkModel m) {
     float* hdo = m.ws_hd + (size_t)b * Ho;
     rowvec_gemv(W, ain, Ho, Hi, tid, [&](int j, float acc) {
       const float z = acc + Bv[j];
-      float a = act_f(act, z);
-      zo[j] = z;
+      float zs;
+      float a = act_train(act, z, m.seed, (uint32_t)step, l + 1, (uint32_t)(b * Ho + j), &zs);
+      zo[j] = zs;
       ao[j] = a;
       if (last) {
         a *= maskh[j];

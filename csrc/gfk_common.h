@@ -21,9 +21,9 @@
 // ---------------------------------------------------------------------------
 extern "C" {
 
-// Activation codes (reference inference_network.py:45-60; rrelu is not fused).
+// Activation codes (reference inference_network.py:45-60).
 enum GfkAct { GFK_SOFTPLUS = 0, GFK_RELU = 1, GFK_SIGMOID = 2, GFK_TANH = 3,
-              GFK_LEAKYRELU = 4, GFK_ELU = 5, GFK_SELU = 6 };
+              GFK_LEAKYRELU = 4, GFK_ELU = 5, GFK_SELU = 6, GFK_RRELU = 7 };
 
 enum GfkModelKind { GFK_PRODLDA = 0, GFK_LDA = 1 };
 
@@ -224,7 +224,8 @@ __device__ __forceinline__ uint4 philox(uint32_t k0, uint32_t k1, uint4 c) {
 }
 
 // Stream tags keep the draws of different random tensors independent.
-enum : uint32_t { RNG_EPS = 1, RNG_DROP_ENC = 2, RNG_DROP_THETA = 3, RNG_INFER = 4 };
+enum : uint32_t { RNG_EPS = 1, RNG_DROP_ENC = 2, RNG_DROP_THETA = 3, RNG_INFER = 4,
+                  RNG_RRELU = 5 };   // RNG_RRELU | (layer << 8): one stream per hidden layer
 
 __device__ __forceinline__ uint4 rng4(uint64_t seed, uint32_t step, uint32_t tag, uint32_t idx) {
   return philox((uint32_t)seed, (uint32_t)(seed >> 32), make_uint4(idx, step, tag, 0x5eedu));
@@ -249,8 +250,14 @@ __device__ __forceinline__ float drop_scale(uint64_t seed, uint32_t step, uint32
   return u01(rng4(seed, step, tag, idx).x) >= p ? 1.f / (1.f - p) : 0.f;
 }
 
+// torch.nn.RReLU defaults (lower 1/8, upper 1/3): training draws the negative-side
+// slope per element from U(lower, upper); eval uses their mean.
+constexpr float RRELU_LO = 1.f / 8.f, RRELU_HI = 1.f / 3.f;
+
+// Activation in eval mode (inference) -- and every activation but RReLU in training.
 __device__ __forceinline__ float act_f(int a, float z) {
   switch (a) {
+    case GFK_RRELU: return z >= 0.f ? z : z * (0.5f * (RRELU_LO + RRELU_HI));
     case GFK_SOFTPLUS: return z > 20.f ? z : log1pf(expf(z));
     case GFK_RELU: return z > 0.f ? z : 0.f;
     case GFK_SIGMOID: return 1.f / (1.f + expf(-z));
@@ -264,9 +271,27 @@ __device__ __forceinline__ float act_f(int a, float z) {
   }
 }
 
-// d act / d z evaluated at the pre-activation z.
+// Training-mode activation of element idx of hidden layer `layer` (stored as the
+// pre-activation z in ws_z for act_d) -- except RReLU, whose slope is a Philox draw:
+// its ws_z entry holds d act / d z (1, or the drawn slope) instead, so the backward
+// needs neither the step nor the draw (*zs receives what is stored).
+__device__ __forceinline__ float act_train(int a, float z, uint64_t seed, uint32_t step, int layer,
+                                           uint32_t idx, float* zs) {
+  if (a != GFK_RRELU) {
+    *zs = z;
+    return act_f(a, z);
+  }
+  const float r = RRELU_LO + (RRELU_HI - RRELU_LO) *
+                  u01(rng4(seed, step, RNG_RRELU | ((uint32_t)layer << 8), idx).x);
+  *zs = z > 0.f ? 1.f : r;          // torch: the drawn slope applies to z <= 0
+  return z > 0.f ? z : z * r;
+}
+
+// d act / d z from the ws_z entry written by act_train (the pre-activation z; RReLU:
+// the derivative itself).
 __device__ __forceinline__ float act_d(int a, float z) {
   switch (a) {
+    case GFK_RRELU: return z;
     case GFK_SOFTPLUS: return z > 20.f ? 1.f : 1.f / (1.f + expf(-z));
     case GFK_RELU: return z > 0.f ? 1.f : 0.f;
     case GFK_SIGMOID: { const float s = 1.f / (1.f + expf(-z)); return s * (1.f - s); }

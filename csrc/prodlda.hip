@@ -59,29 +59,6 @@ constexpr float RL_EPS = 1e-10f;
 
 __host__ __device__ __forceinline__ int round_up(int x, int m) { return (x + m - 1) / m * m; }
 
-// beta[0:KP, c0:c0+VB] -> bt[KP x ld] (zero for k >= K or column >= V); one
-// round of independent loads per 16 elements per thread.
-__device__ __forceinline__ void stage_beta_tile(float* bt, int ld, const float* __restrict__ beta,
-                                                int K, int KP, int V, int c0, int tid) {
-  constexpr int U = 16;
-  const int n = KP * VB;
-  for (int base = tid; base < n; base += U * DEC_THREADS) {
-    float v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i = min(base + u * DEC_THREADS, n - 1);
-      const int k = min(i / VB, K - 1), c = min(c0 + i % VB, V - 1);
-      v[u] = beta[(size_t)k * V + c];
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i = base + u * DEC_THREADS;
-      const int k = i / VB, c = i % VB;
-      if (i < n) bt[k * ld + c] = (k < K && c0 + c < V) ? v[u] : 0.f;
-    }
-  }
-}
-
 // sum over the 4 lane groups (lanes l, l^16, l^32, l^48): a column reduction
 __device__ __forceinline__ float sum_groups(float v) {
   v += __shfl_xor(v, 16, 64);
@@ -96,11 +73,15 @@ __device__ __forceinline__ float sum_groups(float v) {
 // (max, sum-exp) partials are merged across the workgroup's tiles in registers
 // (ws_row_part holds dec_grid * 4 partials per row).  Wave w owns column strip
 // cs = w & 3 (16 columns) and row tiles rt = (w >> 2) + 4 i.
+// Several tiles per workgroup (large V): the next tile's beta block and running
+// statistics are loaded into registers right after this tile's staging barrier, so
+// they land while this tile's MFMAs / batch-norm / stores run.
 // dynamic LDS: th[BM*kt] + bt[KP*LDB_F] + colp[4][64] + colq[4][64] + stat[2][64]
 template <int BM>
 __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int K = m.K, V = m.V, KT = m.kt, tid = threadIdx.x;
+  const int K = m.K, V = m.V, KT = m.kt;
+  int tid = threadIdx.x;                      // re-made opaque per tile (no hoisted addresses)
   const int lane = tid & 63, wave = uniform(tid >> 6);
   const int KP = round_up(K, 4);
   float* th = smem;
@@ -109,6 +90,7 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
   float* colq = colp + 4 * VB;
   constexpr int RT = BM / 16;                 // row tiles
   constexpr int NRT = (RT + 3) / 4;           // row tiles per wave
+  constexpr int BU = 16;                      // beta tile elements per thread (K <= 256)
   const int cs = wave & 3, rt0 = wave >> 2;
   const int col = 16 * cs + (lane & 15);      // this lane's column within a tile
   float rm_[NRT][4], rs_[NRT][4];             // running (max, sum-exp) of this lane's rows
@@ -121,32 +103,69 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
   glds_copy(th, m.ws_thetad, BM * KT, tid, DEC_THREADS);
   const int nb = *m.ws_nb;
   if (blockIdx.x == 0 && tid == 0) *m.nbt_beta += 1;
+  // a tile's beta block [0, KP) x [c0, c0 + VB) and running statistics, into registers
+  float br[BU], rmr = 0.f, rvr = 0.f;
+  const int nbeta = KP * VB;
+  auto issue_tile = [&](int tile) {
+    const int c0 = tile * VB;
+#pragma unroll
+    for (int u = 0; u < BU; ++u) {
+      const int i = min(tid + u * DEC_THREADS, nbeta - 1);
+      // 32-bit element offsets (K V < 2^31): one VGPR per address, not a pair
+      br[u] = m.beta[min(i / VB, K - 1) * V + min(c0 + i % VB, V - 1)];
+    }
+    const int v = min(c0 + col, V - 1);
+    rmr = m.beta_rm[v];
+    rvr = m.beta_rv[v];
+  };
+  if ((int)blockIdx.x < m.n_tiles) issue_tile(blockIdx.x);
 #pragma unroll 1
   for (int tile = blockIdx.x; tile < m.n_tiles; tile += gridDim.x) {
   const int c0 = tile * VB;
-  // ---- one staging round: beta tile, running stats (theta_d: first iteration) ----
   const int v = c0 + col;
   const bool valid = v < V;
-  const float rm0 = m.beta_rm[min(v, V - 1)], rv0 = m.beta_rv[min(v, V - 1)];
-  if (tile != (int)blockIdx.x) __syncthreads();     // previous tile's bt / colp reads done
-  stage_beta_tile(bt, LDB_F, m.beta, K, KP, V, c0, tid);
-  __syncthreads();
-  GFK_STAMP(m, 17);
-  // ---- logits for this wave's row tiles x 16 columns ----
-  f32x4 acc[NRT];
+  // ---- staging: the registers of this tile -> LDS ----
+  if (tile != (int)blockIdx.x) lds_barrier();      // previous tile's bt / colp reads done
 #pragma unroll
-  for (int i = 0; i < NRT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int u = 0; u < BU; ++u) {
+    const int i = tid + u * DEC_THREADS;
+    const int k = i / VB, c = i % VB;
+    if (i < nbeta) bt[k * LDB_F + c] = (k < K && c0 + c < V) ? br[u] : 0.f;
+  }
+  const float rm0 = rmr, rv0 = rvr;
+  if (tile == (int)blockIdx.x) vm_barrier();       // + theta_d (LDS-DMA)
+  else lds_barrier();
+  GFK_STAMP(m, 17);
+  asm volatile("" : "+v"(tid));
+  if (tile + (int)gridDim.x < m.n_tiles) issue_tile(tile + gridDim.x);
+  // ---- logits for this wave's row tiles x 16 columns (two independent MFMA chains) ----
+  f32x4 acc[NRT];
   {
+    f32x4 acc2[NRT];
+#pragma unroll
+    for (int i = 0; i < NRT; ++i) acc[i] = acc2[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     const float* bp = bt + (lane >> 4) * LDB_F + col;
     const float* ap = th + (rt0 * 16 + (lane & 15)) * KT + (lane >> 4);
     if (rt0 < RT) {
-      for (int k0 = 0; k0 < KP; k0 += 4) {
-        const float b = bp[k0 * LDB_F];
+      int k0 = 0;
+      for (; k0 + 4 < KP; k0 += 8) {
+        const float b0 = bp[k0 * LDB_F], b1 = bp[(k0 + 4) * LDB_F];
 #pragma unroll
         for (int i = 0; i < NRT; ++i)
-          if (rt0 + 4 * i < RT) acc[i] = mfma16x16x4(ap[i * 64 * KT + k0], b, acc[i]);
+          if (rt0 + 4 * i < RT) {
+            acc[i] = mfma16x16x4(ap[i * 64 * KT + k0], b0, acc[i]);
+            acc2[i] = mfma16x16x4(ap[i * 64 * KT + k0 + 4], b1, acc2[i]);
+          }
+      }
+      if (k0 < KP) {
+        const float b0 = bp[k0 * LDB_F];
+#pragma unroll
+        for (int i = 0; i < NRT; ++i)
+          if (rt0 + 4 * i < RT) acc[i] = mfma16x16x4(ap[i * 64 * KT + k0], b0, acc[i]);
       }
     }
+#pragma unroll
+    for (int i = 0; i < NRT; ++i) acc[i] += acc2[i];
   }
   GFK_STAMP(m, 18);
 
@@ -162,7 +181,7 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
     }
   s = sum_groups(s);
   if (lane < 16) colp[rt0 * VB + col] = s;
-  __syncthreads();
+  lds_barrier();
   const float mean = (colp[col] + colp[VB + col] + colp[2 * VB + col] + colp[3 * VB + col]) * inv_nb;
   float q = 0.f;
 #pragma unroll
@@ -175,7 +194,7 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
     }
   q = sum_groups(q);
   if (lane < 16) colq[rt0 * VB + col] = q;
-  __syncthreads();
+  lds_barrier();
   const float var = (colq[col] + colq[VB + col] + colq[2 * VB + col] + colq[3 * VB + col]) * inv_nb;
   const float rstd = rsqrtf(var + m.bn_eps);
   if (rt0 == 0 && lane < 16 && valid) {
@@ -301,338 +320,221 @@ extern "C" __global__ void __launch_bounds__(64) gfk_prodlda_row_loss(GfkModel m
   }
 }
 
-// Backward.  grid: n_tiles workgroups of 16 waves.
-// dynamic LDS: th[BM*kt] + bt[KP16*LDB_B] + zt[BM*VB] + dt[BM*LDD] + lse[BM] + S[BM] + rstd[VB]
-// MAXU: dbeta 16x16 output tiles per wave = ceil(K / 64) (Adam state prefetched for
-// each; a compile-time count keeps the prefetch in registers)
-template <int BM, int MAXU>
-__global__ void __launch_bounds__(DEC_THREADS) prodlda_bwd_kernel(GfkModel m) {
+// Backward.  Two launch shapes of one kernel:
+//  * KQ = 1 (every vocab tile has its own workgroup of 16 waves -- the K=50 headline --
+//    or K <= 48): workgroup g owns tiles g, g + grid, ...;
+//  * KQ = 4 (large vocabularies: more tiles than resident workgroups): the topics are
+//    split in 4 ranges of 16-row k tiles; workgroup g handles range q = g % 4 of tiles
+//    g / 4, g / 4 + grid / 4, ...  A quarter of theta_d / beta / the Adam state per
+//    workgroup (8 waves, ~71 KB of LDS at K = 200, B = 64) lets TWO workgroups share a
+//    CU, so one computes while the other's staging round is in flight (a software
+//    pipeline inside one workgroup was measured first: the prefetch registers of the
+//    next tile are loop-carried, and the compiler's in-order vmcnt waits then serialise
+//    them with the current tile's Adam state anyway).  The logit-gradient tile (sparse
+//    + dense passes, cheap VALU work) is recomputed by the 4 range workgroups of a tile.
+// Every global read of a tile is issued in ONE staging round (theta_d's k range, lse
+// and S once per workgroup).  The d theta_d partial of the k range is accumulated in
+// registers over the workgroup's tiles (each element owned by one lane, fixed order:
+// deterministic) and stored once into slab g / KQ, so row_bwd reduces n_dpart = grid /
+// KQ partials.  p comes from the staged beta tile (LDS); the Adam results go to fresh
+// registers and are stored after every update, so no store waits on a load.
+// Per tile:
+//   sparse  dt[b, c] = -x p / (p + 1e-10) at the tile's non-zeros
+//   dense   dt = rstd * (d - mean_b d - z mean_b(d z)),  d = p S + dt  (column BN bwd)
+//   dbeta   g[k, c] = sum_b th[b, k] dt[b, c] -> Adam (+ FedAvg pre-scale) or gradient
+//   dtheta  acc[b, k] += sum_c dt[b, c] beta[k, c]          (MFMA, registers)
+// dynamic LDS: th[BM*KTQ] + bt[KPQ*LDB_B] + zt[BM*VB] + dt[BM*LDD] + lse[BM] + S[BM] + rstd[VB]
+//   (KPQ: rows of the k range, 16 * ceil(ceil(K/16) / KQ); KTQ = kt (KQ = 1) or
+//   kt_stride(KPQ))
+// MAXU = ceil(K / 64) bounds the k tiles (compile time, so the Adam state and the
+// accumulators stay in registers).
+__host__ __device__ __forceinline__ int kt_stride(int w) { return w % 32 == 16 ? w : w + 16; }
+__host__ __device__ __forceinline__ int bwd_kpq(int K, int kq) { return 16 * ((round_up(K, 16) / 16 + kq - 1) / kq); }
+
+template <int BM, int MAXU, int KQ>
+__global__ void __launch_bounds__(KQ == 1 ? DEC_THREADS : 512, KQ == 1 ? 1 : 2)
+prodlda_bwd_kernel(GfkModel m) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int K = m.K, V = m.V, KT = m.kt, tid = threadIdx.x;
-  const int lane = tid & 63, wave = uniform(tid >> 6);
-  const int KP16 = round_up(K, 16);
-  const int tile = blockIdx.x, c0 = tile * VB;
+  constexpr int NTH = KQ == 1 ? DEC_THREADS : 512;
+  // KQ = 1 with more than 3 k tiles only ever runs with one tile per workgroup (the
+  // persistent shape of such K is KQ = 4): no tile loop, no loop-carried registers
+  constexpr bool SINGLE = KQ == 1 && MAXU >= 2;
+  constexpr int NW = NTH / 64;                                  // waves
+  constexpr int NKS = (4 * MAXU + KQ - 1) / KQ;                 // max k tiles per range
+  constexpr int TPR = NTH / BM < 16 ? NTH / BM : 16;            // threads per row (sparse x)
+  constexpr int ZU = (BM * VB / 4 + NTH - 1) / NTH;             // float4 of the logit tile per thread
+  constexpr int BU = (NKS * 16 * VB + NTH - 1) / NTH;           // beta floats per thread
+  constexpr int MU = (NKS * 4 + NW - 1) / NW;                   // dbeta subtiles per wave
+  constexpr int NDT = ((BM / 16) * NKS + NW - 1) / NW;          // d theta_d subtiles per wave
+  const int K = m.K, V = m.V;
+  // the thread index is re-made opaque at every tile (below), so the compiler rebuilds
+  // the lane-dependent addresses inside the tile loop instead of hoisting them all out
+  // of it (which would cost tens of VGPRs and spill)
+  int tid = threadIdx.x;
+  int lane = tid & 63, wave = uniform(tid >> 6);
+  const int ksub = round_up(K, 16) / 16;
+  const int q = (int)blockIdx.x % KQ, slab = (int)blockIdx.x / KQ, nslab = (int)gridDim.x / KQ;
+  const int ks0 = q * ksub / KQ, nks = (q + 1) * ksub / KQ - ks0;   // this workgroup's k tiles
+  const int kb = 16 * ks0;                                      // first topic of the range
+  const int KPQ = bwd_kpq(K, KQ), KTQ = KQ == 1 ? m.kt : kt_stride(KPQ);
   float* th = smem;
-  float* bt = th + BM * KT;
-  float* zt = bt + KP16 * LDB_B;
+  float* bt = th + BM * KTQ;
+  float* zt = bt + KPQ * LDB_B;
   float* dt = zt + BM * VB;
   float* lse = dt + BM * LDD;
   float* Sb = lse + BM;
   float* rs = Sb + BM;
-  constexpr int TPR = DEC_THREADS / BM < 16 ? DEC_THREADS / BM : 16;   // threads per row (sparse x)
+  const int NB_T = nks * 4;                    // dbeta subtiles (k tile, column strip)
+  const int NDT_T = (BM / 16) * nks;           // d theta_d subtiles (row tile, k tile)
+  const bool fused = m.update_mode == 1;
+  const int nb = *m.ws_nb;
+  const AdamCoef ac = adam_coef(m);
+  const bool beta_shared = is_shared(m, m.beta);
 
   GFK_STAMP(m, 24);
-  // ---- one staging round ----
-  glds_copy(th, m.ws_thetad, BM * KT, tid, DEC_THREADS);
-  glds_copy(zt, m.ws_zn + (size_t)tile * BM * VB, BM * VB, tid, DEC_THREADS);
-  glds_copy(lse, m.ws_lse, BM, tid, DEC_THREADS);
-  glds_copy(Sb, m.ws_s, BM, tid, DEC_THREADS);
-  glds_copy(rs, m.ws_col_rstd + c0, VB, tid, DEC_THREADS);
-  const int nb = *m.ws_nb;
-  // sparse x of this tile: TPR threads per row, the first non-zero prefetched
-  const int xrow = tid / TPR, xsub = tid % TPR;
-  int xe0 = 0, xe1 = 0;
-  if (xrow < BM) {
-    const int32_t* ts = m.ws_tstart + (size_t)xrow * (m.n_tiles + 1) + tile;
-    xe0 = ts[0];
-    xe1 = ts[1];
+  // ---- once per workgroup: theta_d columns [kb, kb + 16 nks), lse, S ----
+  if (KQ == 1) {
+    glds_copy(th, m.ws_thetad, BM * m.kt, tid, NTH);           // KTQ == kt for one range
+  } else {
+    for (int i = tid; i < BM * 16 * NKS; i += NTH) {
+      const int b = i / (16 * NKS), c = i % (16 * NKS);
+      if (c < 16 * nks) th[b * KTQ + c] = m.ws_thetad[(size_t)b * m.kt + kb + c];
+    }
   }
-  const int xe = min(xe0 + xsub, max(xe1 - 1, 0));
-  const int xc0 = m.indices[xe];
-  const float xv0 = m.values[xe];
-  // optimizer state of this lane's dbeta outputs (fused mode): wave -> (k tile, column strip)
-  const int ksub = KP16 / 16;
-  const int NB_T = ksub * 4;
-  const bool fused = m.update_mode == 1;
-  float bp_[MAXU][4], bm_[MAXU][4], bv_[MAXU][4];
+  glds_copy(lse, m.ws_lse, BM, tid, NTH);
+  glds_copy(Sb, m.ws_s, BM, tid, NTH);
+
+  // ---- a tile's loads, into registers ----
+  float4 zr[ZU];
+  float br[BU];
+  float rsr = 0.f;
+  int xe0 = 0, xe1 = 0, xc0 = 0;
+  float xv0 = 0.f;
+  int xrow = tid / TPR, xsub = tid % TPR;
+  auto issue_tile = [&](int tile) {
+    const int c0 = tile * VB;
+    const float4* zsrc = reinterpret_cast<const float4*>(m.ws_zn + (size_t)tile * BM * VB);
 #pragma unroll
-  for (int u = 0; u < MAXU; ++u) {
-    const int t = wave + 16 * u;
-    const int ks = t >> 2, cst = t & 3;
-    const int c = min(c0 + cst * 16 + (lane & 15), V - 1);
+    for (int u = 0; u < ZU; ++u) zr[u] = zsrc[min(tid + u * NTH, BM * VB / 4 - 1)];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int k = min(ks * 16 + (lane >> 4) * 4 + r, K - 1);
-      bp_[u][r] = bm_[u][r] = bv_[u][r] = 0.f;
-      if (fused && t < NB_T) {
+    for (int u = 0; u < BU; ++u) {
+      const int i = tid + u * NTH;
+      const int k = min(kb + i / VB, K - 1), c = min(c0 + i % VB, V - 1);
+      br[u] = m.beta[k * V + c];                 // 32-bit offsets (K V < 2^31)
+    }
+    rsr = m.ws_col_rstd[c0 + (tid & (VB - 1))];
+    const int32_t* ts = m.ws_tstart + (size_t)min(xrow, BM - 1) * (m.n_tiles + 1) + tile;
+    xe0 = ts[0];                         // rows >= BM (BM < NTH / 16) are never used
+    xe1 = ts[1];
+  };
+  auto issue_first_nz = [&]() {          // depends on the tile-start loads
+    const int xe = min(xe0 + xsub, max(xe1 - 1, 0));
+    xc0 = m.indices[xe];
+    xv0 = m.values[xe];
+  };
+  // Adam state of this lane's dbeta outputs: subtile t -> (k tile kb/16 + t/4, strip t%4)
+  float bm_[MU][4], bv_[MU][4];
+  auto issue_state = [&](int tile) {
+    const int c0 = tile * VB;
+#pragma unroll
+    for (int u = 0; u < MU; ++u) {
+      const int t = wave + NW * u;
+      const int ks = t >> 2, cst = t & 3;
+      const int c = min(c0 + cst * 16 + (lane & 15), V - 1);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {   // unpredicated, clamped (no select on a pending load)
+        const int k = min(kb + ks * 16 + (lane >> 4) * 4 + r, K - 1);
         const float* p = m.beta + (size_t)k * V + c;
-        bp_[u][r] = *p;
         bm_[u][r] = p[m.off_m];
         bv_[u][r] = p[m.off_v];
       }
     }
-  }
-  stage_beta_tile(bt, LDB_B, m.beta, K, KP16, V, c0, tid);
-  // zero the dlogit tile (dense-pass layout: column tid>>4, rows (tid&15) + 16 i)
-  const int dcol = tid >> 4, dg = tid & 15;
-  for (int row = dg; row < BM; row += 16) dt[row * LDD + dcol] = 0.f;
-  __syncthreads();
-  GFK_STAMP(m, 25);
+  };
+  // this workgroup's d theta_d partial, per lane (summed over its tiles in order)
+  f32x4 dacc[NDT];
+#pragma unroll
+  for (int j = 0; j < NDT; ++j) dacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // ---- sparse term: dt[b, c] = -x p / (p + 1e-10) at this tile's non-zeros ----
-  if (xrow < nb && xrow < BM) {
-    const float l = lse[xrow];
-    for (int i = 0, e = xe0 + xsub; e < xe1; ++i, e += TPR) {
-      const int c = (i == 0 ? xc0 : m.indices[e]) - c0;
-      const float x = i == 0 ? xv0 : m.values[e];
-      const float p = __expf(zt[xrow * VB + (c ^ zswz(xrow))] - l);
-      dt[xrow * LDD + c] = -x * p / (p + RL_EPS);
-    }
-  }
-  __syncthreads();
-  GFK_STAMP(m, 26);
-
-  // ---- dense term p*S and the column BN backward: 16 lanes per column ----
-  {
-    const bool valid = c0 + dcol < V;
-    constexpr int NR = BM / 16;
-    float d[NR], z[NR];
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      const int row = dg + 16 * i;
-      z[i] = zt[row * VB + (dcol ^ zswz(row))];
-      const float p = __expf(z[i] - lse[row]);
-      d[i] = (row < nb && valid) ? p * Sb[row] + dt[row * LDD + dcol] : 0.f;
-      s1 += d[i];
-      s2 += d[i] * z[i];
-    }
-    s1 = row16_sum(s1) / (float)nb;
-    s2 = row16_sum(s2) / (float)nb;
-    const float r = valid ? rs[dcol] : 0.f;
-#pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      const int row = dg + 16 * i;
-      dt[row * LDD + dcol] = row < nb ? r * (d[i] - s1 - z[i] * s2) : 0.f;
-    }
-  }
-  __syncthreads();
-  GFK_STAMP(m, 27);
-
-  // ---- dbeta[k, c] = sum_b th[b, k] dlogit[b, c]  -> update (fused) or gradient ----
-  {
-    const AdamCoef ac = adam_coef(m);
-    const bool sh = is_shared(m, m.beta);
-#pragma unroll
-    for (int u = 0; u < MAXU; ++u) {
-      const int t = wave + 16 * u;
-      if (t >= NB_T) break;
-      const int ks = t >> 2, cst = t & 3;
-      const float* ap = th + (lane >> 4) * KT + ks * 16 + (lane & 15);
-      const float* bp = dt + (lane >> 4) * LDD + cst * 16 + (lane & 15);
-      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int b0 = 0; b0 < BM; b0 += 8) {
-        a0 = mfma16x16x4(ap[b0 * KT], bp[b0 * LDD], a0);
-        a1 = mfma16x16x4(ap[(b0 + 4) * KT], bp[(b0 + 4) * LDD], a1);
-      }
-      const int c = c0 + cst * 16 + (lane & 15);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int k = ks * 16 + (lane >> 4) * 4 + e;
-        if (k >= K || c >= V) continue;
-        float* p = m.beta + (size_t)k * V + c;
-        const float g = a0[e] + a1[e];
-        if (!fused) {
-          p[m.off_g] = g;
-        } else {
-          float mo = bm_[u][e], vo = bv_[u][e];
-          float np = adam_update(bp_[u][e], g, mo, vo, ac);
-          if (sh && m.fed_scale_on) np *= m.fed_scale;
-          p[m.off_m] = mo;
-          p[m.off_v] = vo;
-          *p = np;
-        }
-      }
-    }
-  }
-  // ---- this tile's partial dtheta_d[b, k] = sum_c dlogit[b, c] beta[k, c] (plain stores;
-  //      dtheta_reduce sums the n_tiles partials in a fixed order) ----
-  {
-    float* dpart = m.ws_dthetad + (size_t)tile * m.bmax * K;
-    for (int t = wave; t < (BM / 16) * ksub; t += 16) {
-      const int rt = t / ksub, ks = t % ksub;
-      const float* ap = dt + (rt * 16 + (lane & 15)) * LDD + (lane >> 4);
-      const float* bp = bt + (ks * 16 + (lane & 15)) * LDB_B + (lane >> 4);
-      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int c = 0; c < VB; c += 8) {
-        a0 = mfma16x16x4(ap[c], bp[c], a0);
-        a1 = mfma16x16x4(ap[c + 4], bp[c + 4], a1);
-      }
-      const int k = ks * 16 + (lane & 15);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = rt * 16 + (lane >> 4) * 4 + e;
-        if (row < nb && k < K) dpart[(size_t)row * K + k] = a0[e] + a1[e];
-      }
-    }
-  }
-  GFK_STAMP(m, 28);
-}
-
-// Backward, persistent variant for large vocabularies (n_tiles > dec_grid): the same
-// per-tile work; theta_d, lse and S staged once per workgroup, and the workgroup's
-// dtheta_d partial sums its tiles (first tile stores, later tiles add to the same slab,
-// each element owned by one lane -- deterministic), so row_bwd reduces dec_grid
-// partials instead of n_tiles.
-// dynamic LDS: th[BM*kt] + bt[KP16*LDB_B] + zt[BM*VB] + dt[BM*LDD] + lse[BM] + S[BM] + rstd[VB]
-// MAXU: dbeta 16x16 output tiles per wave = ceil(K / 64) (Adam state prefetched for
-// each; a compile-time count keeps the prefetch in registers)
-template <int BM, int MAXU>
-__global__ void __launch_bounds__(DEC_THREADS) prodlda_bwd_persist_kernel(GfkModel m) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int K = m.K, V = m.V, KT = m.kt, tid0 = threadIdx.x;
-  const int KP16 = round_up(K, 16);
-  float* th = smem;
-  float* bt = th + BM * KT;
-  float* zt = bt + KP16 * LDB_B;
-  float* dt = zt + BM * VB;
-  float* lse = dt + BM * LDD;
-  float* Sb = lse + BM;
-  float* rs = Sb + BM;
-  constexpr int TPR = DEC_THREADS / BM < 16 ? DEC_THREADS / BM : 16;   // threads per row (sparse x)
-
-  glds_copy(th, m.ws_thetad, BM * KT, tid0, DEC_THREADS);
-  glds_copy(lse, m.ws_lse, BM, tid0, DEC_THREADS);
-  glds_copy(Sb, m.ws_s, BM, tid0, DEC_THREADS);
+  int tile = slab;
+  const int dg = threadIdx.x & 15;             // dense-pass layout: row group (16 lanes per column)
 #pragma unroll 1
-  for (int tile = blockIdx.x; tile < m.n_tiles; tile += gridDim.x) {
-  // the thread index is made opaque per iteration so the compiler rebuilds the
-  // lane-dependent LDS / global addresses inside the loop instead of hoisting them
-  // all out of it (which costs ~60 VGPRs and spills)
-  int tid = tid0;
-  asm volatile("" : "+v"(tid));
-  const int lane = tid & 63, wave = uniform(tid >> 6);
-  const int c0 = tile * VB;
-  if (tile != (int)blockIdx.x) vm_barrier();   // previous tile: LDS reads and slab stores done
-  glds_copy(zt, m.ws_zn + (size_t)tile * BM * VB, BM * VB, tid, DEC_THREADS);
-  glds_copy(rs, m.ws_col_rstd + c0, VB, tid, DEC_THREADS);
-  const int nb = *m.ws_nb;
-  // sparse x of this tile: TPR threads per row, the first non-zero prefetched
-  const int xrow = tid / TPR, xsub = tid % TPR;
-  int xe0 = 0, xe1 = 0;
-  if (xrow < BM) {
-    const int32_t* ts = m.ws_tstart + (size_t)xrow * (m.n_tiles + 1) + tile;
-    xe0 = ts[0];
-    xe1 = ts[1];
-  }
-  const int xe = min(xe0 + xsub, max(xe1 - 1, 0));
-  const int xc0 = m.indices[xe];
-  const float xv0 = m.values[xe];
-  // optimizer state of this lane's dbeta outputs (fused mode): wave -> (k tile, column strip)
-  const int ksub = KP16 / 16;
-  const int NB_T = ksub * 4;
-  const bool fused = m.update_mode == 1;
-  float bp_[MAXU][4], bm_[MAXU][4], bv_[MAXU][4];
+  for (; tile < m.n_tiles; tile += nslab) {
+    const int c0 = tile * VB;
+    asm volatile("" : "+v"(tid));
+    lane = tid & 63;
+    wave = uniform(tid >> 6);
+    xrow = tid / TPR;
+    xsub = tid % TPR;
+    // one staging round per tile: every global read is issued before the barrier
+    issue_tile(tile);
+    issue_first_nz();
+    issue_state(tile);
+    if (tile != slab) lds_barrier();           // the previous tile's LDS reads are done
+    // ---- (1) this tile's registers -> LDS; zero the logit-gradient tile ----
 #pragma unroll
-  for (int u = 0; u < MAXU; ++u) {
-    const int t = wave + 16 * u;
-    const int ks = t >> 2, cst = t & 3;
-    const int c = min(c0 + cst * 16 + (lane & 15), V - 1);
+    for (int u = 0; u < ZU; ++u)
+      if (tid + u * NTH < BM * VB / 4) reinterpret_cast<float4*>(zt)[tid + u * NTH] = zr[u];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int k = min(ks * 16 + (lane >> 4) * 4 + r, K - 1);
-      bp_[u][r] = bm_[u][r] = bv_[u][r] = 0.f;
-      if (fused && t < NB_T) {
-        const float* p = m.beta + (size_t)k * V + c;
-        bp_[u][r] = *p;
-        bm_[u][r] = p[m.off_m];
-        bv_[u][r] = p[m.off_v];
+    for (int u = 0; u < BU; ++u) {
+      const int i = tid + u * NTH;
+      const int k = i / VB, c = i % VB;
+      if (k < 16 * nks) bt[k * LDB_B + c] = (kb + k < K && c0 + c < V) ? br[u] : 0.f;
+    }
+    if (tid < VB) rs[tid] = rsr;
+    for (int dcol = tid >> 4; dcol < VB; dcol += NTH / 16)
+      for (int row = dg; row < BM; row += 16) dt[row * LDD + dcol] = 0.f;
+    const int ye0 = xe0, ye1 = xe1, yc0 = xc0;
+    const float yv0 = xv0;
+    vm_barrier();                              // (+ theta_d / lse / S on the first tile)
+    GFK_STAMP(m, 25);
+
+    // ---- (3) sparse term: dt[b, c] = -x p / (p + 1e-10) at this tile's non-zeros ----
+    if (xrow < nb && xrow < BM) {
+      const float l = lse[xrow];
+      for (int i = 0, e = ye0 + xsub; e < ye1; ++i, e += TPR) {
+        const int c = (i == 0 ? yc0 : m.indices[e]) - c0;
+        const float x = i == 0 ? yv0 : m.values[e];
+        const float p = __expf(zt[xrow * VB + (c ^ zswz(xrow))] - l);
+        dt[xrow * LDD + c] = -x * p / (p + RL_EPS);
       }
     }
-  }
-  stage_beta_tile(bt, LDB_B, m.beta, K, KP16, V, c0, tid);
-  // zero the dlogit tile (dense-pass layout: column tid>>4, rows (tid&15) + 16 i)
-  const int dcol = tid >> 4, dg = tid & 15;
-  for (int row = dg; row < BM; row += 16) dt[row * LDD + dcol] = 0.f;
-  __syncthreads();
-  GFK_STAMP(m, 25);
+    lds_barrier();
+    GFK_STAMP(m, 26);
 
-  // ---- sparse term: dt[b, c] = -x p / (p + 1e-10) at this tile's non-zeros ----
-  if (xrow < nb && xrow < BM) {
-    const float l = lse[xrow];
-    for (int i = 0, e = xe0 + xsub; e < xe1; ++i, e += TPR) {
-      const int c = (i == 0 ? xc0 : m.indices[e]) - c0;
-      const float x = i == 0 ? xv0 : m.values[e];
-      const float p = __expf(zt[xrow * VB + (c ^ zswz(xrow))] - l);
-      dt[xrow * LDD + c] = -x * p / (p + RL_EPS);
-    }
-  }
-  __syncthreads();
-  GFK_STAMP(m, 26);
-
-  // ---- dense term p*S and the column BN backward: 16 lanes per column ----
-  {
-    const bool valid = c0 + dcol < V;
-    constexpr int NR = BM / 16;
-    float d[NR], z[NR];
-    float s1 = 0.f, s2 = 0.f;
+    // ---- (4) dense term p*S and the column BN backward: 16 lanes per column ----
+    for (int dcol = tid >> 4; dcol < VB; dcol += NTH / 16) {
+      const bool valid = c0 + dcol < V;
+      constexpr int NR = BM / 16;
+      float d[NR], z[NR];
+      float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      const int row = dg + 16 * i;
-      z[i] = zt[row * VB + (dcol ^ zswz(row))];
-      const float p = __expf(z[i] - lse[row]);
-      d[i] = (row < nb && valid) ? p * Sb[row] + dt[row * LDD + dcol] : 0.f;
-      s1 += d[i];
-      s2 += d[i] * z[i];
-    }
-    s1 = row16_sum(s1) / (float)nb;
-    s2 = row16_sum(s2) / (float)nb;
-    const float r = valid ? rs[dcol] : 0.f;
-#pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      const int row = dg + 16 * i;
-      dt[row * LDD + dcol] = row < nb ? r * (d[i] - s1 - z[i] * s2) : 0.f;
-    }
-  }
-  __syncthreads();
-  GFK_STAMP(m, 27);
-
-  // ---- dbeta[k, c] = sum_b th[b, k] dlogit[b, c]  -> update (fused) or gradient ----
-  {
-    const AdamCoef ac = adam_coef(m);
-    const bool sh = is_shared(m, m.beta);
-#pragma unroll
-    for (int u = 0; u < MAXU; ++u) {
-      const int t = wave + 16 * u;
-      if (t >= NB_T) break;
-      const int ks = t >> 2, cst = t & 3;
-      const float* ap = th + (lane >> 4) * KT + ks * 16 + (lane & 15);
-      const float* bp = dt + (lane >> 4) * LDD + cst * 16 + (lane & 15);
-      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int b0 = 0; b0 < BM; b0 += 8) {
-        a0 = mfma16x16x4(ap[b0 * KT], bp[b0 * LDD], a0);
-        a1 = mfma16x16x4(ap[(b0 + 4) * KT], bp[(b0 + 4) * LDD], a1);
+      for (int i = 0; i < NR; ++i) {
+        const int row = dg + 16 * i;
+        z[i] = zt[row * VB + (dcol ^ zswz(row))];
+        const float p = __expf(z[i] - lse[row]);
+        d[i] = (row < nb && valid) ? p * Sb[row] + dt[row * LDD + dcol] : 0.f;
+        s1 += d[i];
+        s2 += d[i] * z[i];
       }
-      const int c = c0 + cst * 16 + (lane & 15);
+      s1 = row16_sum(s1) / (float)nb;
+      s2 = row16_sum(s2) / (float)nb;
+      const float r = valid ? rs[dcol] : 0.f;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int k = ks * 16 + (lane >> 4) * 4 + e;
-        if (k >= K || c >= V) continue;
-        float* p = m.beta + (size_t)k * V + c;
-        const float g = a0[e] + a1[e];
-        if (!fused) {
-          p[m.off_g] = g;
-        } else {
-          float mo = bm_[u][e], vo = bv_[u][e];
-          float np = adam_update(bp_[u][e], g, mo, vo, ac);
-          if (sh && m.fed_scale_on) np *= m.fed_scale;
-          p[m.off_m] = mo;
-          p[m.off_v] = vo;
-          *p = np;
-        }
+      for (int i = 0; i < NR; ++i) {
+        const int row = dg + 16 * i;
+        dt[row * LDD + dcol] = row < nb ? r * (d[i] - s1 - z[i] * s2) : 0.f;
       }
     }
-  }
-  // ---- this tile's partial dtheta_d[b, k] = sum_c dlogit[b, c] beta[k, c] (plain stores;
-  //      dtheta_reduce sums the n_tiles partials in a fixed order) ----
-  {
-    const bool first = tile == (int)blockIdx.x;
-    float* dpart = m.ws_dthetad + (size_t)blockIdx.x * m.bmax * K;
-    for (int t = wave; t < (BM / 16) * ksub; t += 16) {
-      const int rt = t / ksub, ks = t % ksub;
+    lds_barrier();
+    GFK_STAMP(m, 27);
+
+    // ---- (5) d theta_d[b, k] += sum_c dlogit[b, c] beta[k, c] over the k range ----
+    auto dtheta_tile = [&]() {
+#pragma unroll
+    for (int j = 0; j < NDT; ++j) {
+      const int t = wave + NW * j;
+      if (t >= NDT_T) break;
+      const int rt = t / nks, ks = t % nks;
       const float* ap = dt + (rt * 16 + (lane & 15)) * LDD + (lane >> 4);
       const float* bp = bt + (ks * 16 + (lane & 15)) * LDB_B + (lane >> 4);
       f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
@@ -641,17 +543,83 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_bwd_persist_kernel(GfkMod
         a0 = mfma16x16x4(ap[c], bp[c], a0);
         a1 = mfma16x16x4(ap[c + 4], bp[c + 4], a1);
       }
-      const int k = ks * 16 + (lane & 15);
+      dacc[j] += a0 + a1;
+    }
+    };
+    // ---- (6) dbeta[k, c] = sum_b th[b, k] dlogit[b, c] -> update (fused) or gradient ----
+    auto dbeta_tile = [&]() {
+      // results in fresh registers: the stores below never wait on a load (the loaded
+      // m, v are consumed only by the fused-mode update)
+      float np_[MU][4], mo_[MU][4], vo_[MU][4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = rt * 16 + (lane >> 4) * 4 + e;
-        if (row < nb && k < K) {
-          float* q = dpart + (size_t)row * K + k;
-          *q = first ? a0[e] + a1[e] : *q + (a0[e] + a1[e]);
+      for (int u = 0; u < MU; ++u) {
+        const int t = wave + NW * u;
+        if (t >= NB_T) break;
+        const int ks = t >> 2, cst = t & 3;
+        const float* ap = th + (lane >> 4) * KTQ + ks * 16 + (lane & 15);
+        const float* bp = dt + (lane >> 4) * LDD + cst * 16 + (lane & 15);
+        f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int b0 = 0; b0 < BM; b0 += 8) {
+          a0 = mfma16x16x4(ap[b0 * KTQ], bp[b0 * LDD], a0);
+          a1 = mfma16x16x4(ap[(b0 + 4) * KTQ], bp[(b0 + 4) * LDD], a1);
+        }
+        const int cl = cst * 16 + (lane & 15);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float g = a0[e] + a1[e];
+          np_[u][e] = mo_[u][e] = vo_[u][e] = g;
+          if (fused) {
+            const int kl = ks * 16 + (lane >> 4) * 4 + e;
+            float mo = bm_[u][e], vo = bv_[u][e];
+            float np = adam_update(bt[kl * LDB_B + cl], g, mo, vo, ac);
+            np_[u][e] = beta_shared && m.fed_scale_on ? np * m.fed_scale : np;
+            mo_[u][e] = mo;
+            vo_[u][e] = vo;
+          }
         }
       }
-    }
+      // every store after every update: no load is pending between them
+#pragma unroll
+      for (int u = 0; u < MU; ++u) {
+        const int t = wave + NW * u;
+        if (t >= NB_T) break;
+        const int ks = t >> 2, cst = t & 3;
+        const int c = c0 + cst * 16 + (lane & 15);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int k = kb + ks * 16 + (lane >> 4) * 4 + e;
+          if (k >= K || c >= V) continue;
+          float* p = m.beta + (size_t)k * V + c;
+          if (!fused) {
+            p[m.off_g] = np_[u][e];
+          } else {
+            p[m.off_m] = mo_[u][e];
+            p[m.off_v] = vo_[u][e];
+            *p = np_[u][e];
+          }
+        }
+      }
+    };
+    // (6) first: the Adam state's registers are free before the accumulators are touched
+    dbeta_tile();
+    dtheta_tile();
+    GFK_STAMP(m, 28);
+    if (SINGLE) break;
   }
+  // ---- this workgroup's d theta_d partial (plain stores; row_bwd sums the slabs in order) ----
+  float* dpart = m.ws_dthetad + (size_t)slab * m.bmax * K;
+#pragma unroll
+  for (int j = 0; j < NDT; ++j) {
+    const int t = wave + NW * j;
+    if (t >= NDT_T) break;
+    const int rt = t / nks, ks = t % nks;
+    const int k = kb + ks * 16 + (lane & 15);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = rt * 16 + (lane >> 4) * 4 + e;
+      if (row < nb && k < K) dpart[(size_t)row * K + k] = dacc[j][e];
+    }
   }
 }
 
@@ -660,10 +628,20 @@ extern "C" size_t gfk_prodlda_fwd_smem(const GfkModel* m) {
   return sizeof(float) * ((size_t)m->bmax * m->kt + KP * LDB_F + 8 * VB);
 }
 
-extern "C" size_t gfk_prodlda_bwd_smem(const GfkModel* m) {
-  const size_t KP16 = round_up(m->K, 16), B = m->bmax;
-  return sizeof(float) * (B * m->kt + KP16 * LDB_B + B * VB + B * LDD + 2 * B + VB);
+// k ranges of the backward: 4 when the tiles outnumber the workgroups (n_dpart < n_tiles)
+// and K has at least 4 k tiles, else 1
+__host__ __device__ inline int bwd_kq(const GfkModel& m) {
+  return (m.n_dpart < m.n_tiles && round_up(m.K, 16) / 16 >= 4) ? 4 : 1;
 }
+
+static size_t bwd_smem(const GfkModel* m, int kq) {
+  const size_t KPQ = bwd_kpq(m->K, kq), B = m->bmax;
+  const size_t KTQ = kq == 1 ? (size_t)m->kt : (size_t)kt_stride((int)KPQ);
+  return sizeof(float) * (B * KTQ + KPQ * LDB_B + B * VB + B * LDD + 2 * B + VB);
+}
+
+// the LDS of the launch shape this model uses (the k-range split when it applies)
+extern "C" size_t gfk_prodlda_bwd_smem(const GfkModel* m) { return bwd_smem(m, bwd_kq(*m)); }
 
 extern "C" int gfk_launch_prodlda_fwd(const GfkModel* m, hipStream_t s) {
   const size_t sm = gfk_prodlda_fwd_smem(m);
@@ -678,35 +656,33 @@ extern "C" int gfk_launch_prodlda_fwd(const GfkModel* m, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-template <int MAXU>
-static void launch_bwd(const GfkModel* m, dim3 g, dim3 blk, size_t sm, hipStream_t s) {
-  if (m->n_dpart < m->n_tiles) {         // persistent: dec_grid workgroups, dec_grid partials
-    g = dim3(m->n_dpart);
-    switch (m->bmax) {
-      case 16: hipLaunchKernelGGL((prodlda_bwd_persist_kernel<16, MAXU>), g, blk, sm, s, *m); break;
-      case 32: hipLaunchKernelGGL((prodlda_bwd_persist_kernel<32, MAXU>), g, blk, sm, s, *m); break;
-      case 64: hipLaunchKernelGGL((prodlda_bwd_persist_kernel<64, MAXU>), g, blk, sm, s, *m); break;
-      default: hipLaunchKernelGGL((prodlda_bwd_persist_kernel<128, MAXU>), g, blk, sm, s, *m); break;
-    }
-    return;
-  }
+template <int MAXU, int KQ>
+static void launch_bwd_t(const GfkModel* m, dim3 g, size_t sm, hipStream_t s) {
+  const dim3 blk(KQ == 1 ? DEC_THREADS : 512);
   switch (m->bmax) {
-    case 16: hipLaunchKernelGGL((prodlda_bwd_kernel<16, MAXU>), g, blk, sm, s, *m); break;
-    case 32: hipLaunchKernelGGL((prodlda_bwd_kernel<32, MAXU>), g, blk, sm, s, *m); break;
-    case 64: hipLaunchKernelGGL((prodlda_bwd_kernel<64, MAXU>), g, blk, sm, s, *m); break;
-    default: hipLaunchKernelGGL((prodlda_bwd_kernel<128, MAXU>), g, blk, sm, s, *m); break;
+    case 16: hipLaunchKernelGGL((prodlda_bwd_kernel<16, MAXU, KQ>), g, blk, sm, s, *m); break;
+    case 32: hipLaunchKernelGGL((prodlda_bwd_kernel<32, MAXU, KQ>), g, blk, sm, s, *m); break;
+    case 64: hipLaunchKernelGGL((prodlda_bwd_kernel<64, MAXU, KQ>), g, blk, sm, s, *m); break;
+    default: hipLaunchKernelGGL((prodlda_bwd_kernel<128, MAXU, KQ>), g, blk, sm, s, *m); break;
   }
 }
 
+template <int MAXU>
+static void launch_bwd(const GfkModel* m, hipStream_t s) {
+  const int kq = bwd_kq(*m);
+  const int slabs = m->n_dpart < m->n_tiles ? m->n_dpart : m->n_tiles;
+  const size_t sm = bwd_smem(m, kq);
+  if (kq == 4) launch_bwd_t<MAXU, 4>(m, dim3(4 * slabs), sm, s);
+  else launch_bwd_t<MAXU, 1>(m, dim3(slabs), sm, s);
+}
+
 extern "C" int gfk_launch_prodlda_bwd(const GfkModel* m, hipStream_t s) {
-  const size_t sm = gfk_prodlda_bwd_smem(m);
-  dim3 g(m->n_tiles), blk(DEC_THREADS);          // one vocab tile per workgroup
   if (m->bmax != 16 && m->bmax != 32 && m->bmax != 64 && m->bmax != 128) return -1;
   switch ((m->K + 63) / 64) {
-    case 1: launch_bwd<1>(m, g, blk, sm, s); break;
-    case 2: launch_bwd<2>(m, g, blk, sm, s); break;
-    case 3: launch_bwd<3>(m, g, blk, sm, s); break;
-    default: launch_bwd<4>(m, g, blk, sm, s); break;
+    case 1: launch_bwd<1>(m, s); break;
+    case 2: launch_bwd<2>(m, s); break;
+    case 3: launch_bwd<3>(m, s); break;
+    default: launch_bwd<4>(m, s); break;
   }
   return (int)hipGetLastError();
 }
@@ -724,12 +700,12 @@ extern "C" int gfk_prodlda_set_smem(size_t bytes) {
   cur = bytes;
   const void* ks[] = {(const void*)prodlda_fwd_kernel<16>, (const void*)prodlda_fwd_kernel<32>,
                       (const void*)prodlda_fwd_kernel<64>, (const void*)prodlda_fwd_kernel<128>,
-#define GFK_BWD_PTRS(U) (const void*)prodlda_bwd_kernel<16, U>, (const void*)prodlda_bwd_kernel<32, U>, \
-    (const void*)prodlda_bwd_kernel<64, U>, (const void*)prodlda_bwd_kernel<128, U>, \
-    (const void*)prodlda_bwd_persist_kernel<16, U>, (const void*)prodlda_bwd_persist_kernel<32, U>, \
-    (const void*)prodlda_bwd_persist_kernel<64, U>, (const void*)prodlda_bwd_persist_kernel<128, U>
+#define GFK_BWD_PTRS1(U, T) (const void*)prodlda_bwd_kernel<16, U, T>, (const void*)prodlda_bwd_kernel<32, U, T>, \
+    (const void*)prodlda_bwd_kernel<64, U, T>, (const void*)prodlda_bwd_kernel<128, U, T>
+#define GFK_BWD_PTRS(U) GFK_BWD_PTRS1(U, 1), GFK_BWD_PTRS1(U, 4)
                       GFK_BWD_PTRS(1), GFK_BWD_PTRS(2), GFK_BWD_PTRS(3), GFK_BWD_PTRS(4)};
 #undef GFK_BWD_PTRS
+#undef GFK_BWD_PTRS1
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return (int)e;

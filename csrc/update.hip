@@ -27,8 +27,11 @@
 using namespace gfk;
 
 namespace {
-constexpr int UT = 1024;
-constexpr int UW = UT / 64;
+// Workgroup size UT: 16 waves when the grid fits the CUs (one round of workgroups: the
+// most waves per tile, the shortest critical path -- the K=50 headline); 8 waves for
+// large vocabularies, where the W_in tiles ([64, H0] blocks, 16 MFMA subtiles at H0 <= 64)
+// outnumber the CUs several times: four workgroups share a CU and one's staging round
+// overlaps another's MFMAs and stores.
 __host__ __device__ inline int rup(int x, int m) { return (x + m - 1) / m * m; }
 // LDS strides for ds_read_b32 MFMA operands (bank = dword % 32 per half-wave):
 // A-role reads (lane & 15 -> row, lane >> 4 -> k) want stride = 2 x odd, so 16 rows x
@@ -51,23 +54,29 @@ extern "C" size_t gfk_win_update_smem(const GfkModel* m) {
 }
 
 // Small weight tile job (see GfkWJob).  LDS: dz[B][LDJ] + a[B][LDJ]
+template <int UT>
 __device__ __forceinline__ void weight_job(const GfkModel& m, const GfkWJob& J, float* smem) {
+  constexpr int UW = UT / 64;
   constexpr int LDJ = 80;            // B-role stride (16 mod 32): conflict-free operand reads
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int B = m.bmax, nb = *m.ws_nb;
   float* dzs = smem;
   float* as = smem + B * LDJ;
   const bool fused = m.update_mode == 1;
-  // prefetch: the lane's 4 outputs of subtile (jt, it) = (wave >> 2, wave & 3)
-  const int jt = wave >> 2, it = wave & 3;
-  const int i = J.i0 + it * 16 + (lane & 15);
-  float pp[4], pm[4], pv[4];
+  // prefetch: the lane's 4 outputs of subtiles (jt, it) = (t >> 2, t & 3), t = wave + UW u
+  constexpr int WU = 16 / UW;
+  float pp[WU][4], pm[WU][4], pv[WU][4];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int j = J.j0 + jt * 16 + (lane >> 4) * 4 + r;
-    const float* p = J.param + (size_t)min(j, J.rows - 1) * J.cols + min(i, J.cols - 1);
-    pp[r] = pm[r] = pv[r] = 0.f;
-    if (fused) { pp[r] = *p; pm[r] = p[m.off_m]; pv[r] = p[m.off_v]; }
+  for (int u = 0; u < WU; ++u) {
+    const int t = wave + UW * u, jt = t >> 2, it = t & 3;
+    const int i = J.i0 + it * 16 + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = J.j0 + jt * 16 + (lane >> 4) * 4 + r;
+      const float* p = J.param + (size_t)min(j, J.rows - 1) * J.cols + min(i, J.cols - 1);
+      pp[u][r] = pm[u][r] = pv[u][r] = 0.f;
+      if (fused) { pp[u][r] = *p; pm[u][r] = p[m.off_m]; pv[u][r] = p[m.off_v]; }
+    }
   }
   // stage the two [B x 64] column slices (rows >= nb zero)
   for (int e0 = 0; e0 < B * 64; e0 += 4 * UT) {
@@ -88,35 +97,41 @@ __device__ __forceinline__ void weight_job(const GfkModel& m, const GfkWJob& J, 
     }
   }
   lds_barrier();
-  const float* ap = dzs + (lane >> 4) * LDJ + jt * 16 + (lane & 15);
-  const float* bp = as + (lane >> 4) * LDJ + it * 16 + (lane & 15);
-  f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
-  for (int k = 0; k < B; k += 8) {
-    c0 = mfma16x16x4(ap[k * LDJ], bp[k * LDJ], c0);
-    c1 = mfma16x16x4(ap[(k + 4) * LDJ], bp[(k + 4) * LDJ], c1);
-  }
-  const f32x4 g = c0 + c1;
   const AdamCoef ac = adam_coef(m);
   const bool sh = is_shared(m, J.param);
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int j = J.j0 + jt * 16 + (lane >> 4) * 4 + r;
-    if (j >= J.rows || i >= J.cols) continue;
-    float* p = J.param + (size_t)j * J.cols + i;
-    if (!fused) {
-      p[m.off_g] = g[r];
-    } else {
-      float mo = pm[r], vo = pv[r];
-      float np = adam_update(pp[r], g[r], mo, vo, ac);
-      if (sh && m.fed_scale_on) np *= m.fed_scale;
-      p[m.off_m] = mo;
-      p[m.off_v] = vo;
-      *p = np;
+  for (int u = 0; u < WU; ++u) {
+    const int t = wave + UW * u, jt = t >> 2, it = t & 3;
+    const int i = J.i0 + it * 16 + (lane & 15);
+    const float* ap = dzs + (lane >> 4) * LDJ + jt * 16 + (lane & 15);
+    const float* bp = as + (lane >> 4) * LDJ + it * 16 + (lane & 15);
+    f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < B; k += 8) {
+      c0 = mfma16x16x4(ap[k * LDJ], bp[k * LDJ], c0);
+      c1 = mfma16x16x4(ap[(k + 4) * LDJ], bp[(k + 4) * LDJ], c1);
+    }
+    const f32x4 g = c0 + c1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = J.j0 + jt * 16 + (lane >> 4) * 4 + r;
+      if (j >= J.rows || i >= J.cols) continue;
+      float* p = J.param + (size_t)j * J.cols + i;
+      if (!fused) {
+        p[m.off_g] = g[r];
+      } else {
+        float mo = pm[u][r], vo = pv[u][r];
+        float np = adam_update(pp[u][r], g[r], mo, vo, ac);
+        if (sh && m.fed_scale_on) np *= m.fed_scale;
+        p[m.off_m] = mo;
+        p[m.off_v] = vo;
+        *p = np;
+      }
     }
   }
 }
 
 // Vector job (see GfkVJob): 16 lanes per element split the batch rows.
+template <int UT>
 __device__ __forceinline__ void vector_job(const GfkModel& m, const GfkVJob& J) {
   const int tid = threadIdx.x, s = tid & 15;
   const int B = m.bmax, nb = *m.ws_nb;
@@ -158,12 +173,14 @@ __device__ __forceinline__ void vector_job(const GfkModel& m, const GfkVJob& J) 
 // rows A^T (ctx_fwd's output) in place of x^T, or ZeroShotTM's whole [C, H0] layer with
 // the batch's contextual rows x_ctx^T -- the same tile GEMM + Adam epilogue.
 // dynamic LDS: max(W_in tile: xt[64][stride_a(B)] + dz[B][stride_b(H0P)], weight job: 2 B 80)
-extern "C" __global__ void __launch_bounds__(UT) gfk_win_update(GfkModel m, GfkUpdate U) {
+template <int UT>
+__global__ void __launch_bounds__(UT) gfk_win_update_k(GfkModel m, GfkUpdate U) {
+  constexpr int UW = UT / 64;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   {
     const int r = (int)blockIdx.x - m.n_tiles;
-    if (r >= 0 && r < U.n_w) { weight_job(m, U.w[r], smem); return; }
-    if (r >= U.n_w && r < U.n_w + U.n_v) { vector_job(m, U.v[r - U.n_w]); return; }
+    if (r >= 0 && r < U.n_w) { weight_job<UT>(m, U.w[r], smem); return; }
+    if (r >= U.n_w && r < U.n_w + U.n_v) { vector_job<UT>(m, U.v[r - U.n_w]); return; }
     if (r == U.n_w + U.n_v) { prepare_next_batch(m); return; }
   }
   const bool zs = m.ctx_fused == 2;            // ZeroShotTM: W_in is the dense [C, H0] layer
@@ -204,26 +221,30 @@ extern "C" __global__ void __launch_bounds__(UT) gfk_win_update(GfkModel m, GfkU
   } else {
     for (int i = tid; i < 64 * XS; i += UT) xt[i] = 0.f;
   }
-  // 16 threads per row: the row's non-zeros inside this tile (rows tid/16 and, at
-  // bmax = 128, tid/16 + 64)
-  const int row = tid >> 4, sub = tid & 15, row2 = row + UT / 16;
-  int e0 = 0, e1 = 0, f0 = 0, f1 = 0;
-  if (!ctxt && row < nb && row < B) {
-    const int32_t* ts = tstart + (size_t)row * (n_tiles + 1) + tile;
-    e0 = ts[0];
-    e1 = ts[1];
+  // 16 threads per row: the row's non-zeros inside this tile (rows tid/16 + 32 i,
+  // i < B / 32 -- the tile-start loads of every row are issued in the staging round)
+  constexpr int XR = 128 / (UT / 16);          // row slots per thread (bmax <= 128)
+  const int row = tid >> 4, sub = tid & 15;
+  int xe0[XR], xe1[XR];
+#pragma unroll
+  for (int i = 0; i < XR; ++i) {
+    const int r = row + i * (UT / 16);
+    xe0[i] = xe1[i] = 0;
+    if (!ctxt && r < nb && r < B) {
+      const int32_t* ts = tstart + (size_t)r * (n_tiles + 1) + tile;
+      xe0[i] = ts[0];
+      xe1[i] = ts[1];
+    }
   }
-  if (!ctxt && row2 < nb && row2 < B) {
-    const int32_t* ts = tstart + (size_t)row2 * (n_tiles + 1) + tile;
-    f0 = ts[0];
-    f1 = ts[1];
-  }
-  // prefetch the optimizer state of this lane's 4 outputs (16x16 tile per wave)
+  // prefetch the optimizer state of this lane's outputs: subtiles t = wave + UW u
+  // (16x16 each; H0 <= 64 -> at most 16 subtiles, one pass; wider layers take passes
+  // of UW * PU subtiles below, the later ones prefetched after the scatter)
   const int MT = 4, NT = H0P / 16;
-  float pp[4][4], pm[4][4], pv[4][4];
+  constexpr int PU = 16 / UW;
+  float pp[PU][4], pm[PU][4], pv[PU][4];
   const bool fused = m.update_mode == 1;
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
+  for (int u = 0; u < PU; ++u) {
     const int t = wave + UW * u;
     const int i0 = (t / NT) * 16, j0 = (t % NT) * 16;
     const int j = min(j0 + (lane & 15), H0 - 1);
@@ -240,17 +261,40 @@ extern "C" __global__ void __launch_bounds__(UT) gfk_win_update(GfkModel m, GfkU
     }
   }
   __syncthreads();
-  for (int e = e0 + sub; e < e1; e += 16) xt[(indices[e] - c0) * XS + row] = values[e];
-  for (int e = f0 + sub; e < f1; e += 16) xt[(indices[e] - c0) * XS + row2] = values[e];
+#pragma unroll
+  for (int i = 0; i < XR; ++i) {
+    const int r = row + i * (UT / 16);
+    for (int e = xe0[i] + sub; e < xe1[i]; e += 16) xt[(indices[e] - c0) * XS + r] = values[e];
+  }
   __syncthreads();
 
   GFK_STAMP(m, 41);
   // ---- G[v, j] = sum_b xt[v, b] dz[b, j] and the update ----
   const AdamCoef ac = adam_coef(m);
   const bool sh = is_shared(m, w_in);
+  for (int pass = 0; pass * UW * PU < MT * NT; ++pass) {
+  if (pass > 0) {             // wide input layers (H0 > 64): the next subtiles' state
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int t = wave + UW * u;
+    for (int u = 0; u < PU; ++u) {
+      const int t = pass * UW * PU + wave + UW * u;
+      const int i0 = (t / NT) * 16, j0 = (t % NT) * 16;
+      const int j = min(j0 + (lane & 15), H0 - 1);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int v = min(c0 + i0 + (lane >> 4) * 4 + r, V - 1);
+        float* p = w_in + (size_t)v * H0 + j;
+        pp[u][r] = pm[u][r] = pv[u][r] = 0.f;
+        if (t < MT * NT && fused) {
+          pp[u][r] = *p;
+          pm[u][r] = p[m.off_m];
+          pv[u][r] = p[m.off_v];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < PU; ++u) {
+    const int t = pass * UW * PU + wave + UW * u;
     if (t >= MT * NT) break;
     const int i0 = (t / NT) * 16, j0 = (t % NT) * 16;
     const float* ap = xt + (i0 + (lane & 15)) * XS + (lane >> 4);
@@ -279,13 +323,18 @@ extern "C" __global__ void __launch_bounds__(UT) gfk_win_update(GfkModel m, GfkU
       }
     }
   }
+  }
   GFK_STAMP(m, 42);
 }
 
 extern "C" int gfk_launch_win_update(const GfkModel* m, const GfkUpdate* u, hipStream_t s) {
   const int extra = m->ctx_fused == 1 ? m->n_tiles : (m->ctx_fused == 2 ? (m->C + 63) / 64 : 0);
-  hipLaunchKernelGGL(gfk_win_update, dim3(m->n_tiles + u->n_w + u->n_v + 1 + extra), dim3(UT),
-                     gfk_win_update_smem(m), s, *m, *u);
+  const dim3 g(m->n_tiles + u->n_w + u->n_v + 1 + extra);
+  // more W_in tiles than two rounds of 16-wave workgroups (dec_grid = the CUs' slots)
+  if (m->n_tiles > 2 * m->dec_grid && m->n_tiles > 512)
+    hipLaunchKernelGGL(gfk_win_update_k<512>, g, dim3(512), gfk_win_update_smem(m), s, *m, *u);
+  else
+    hipLaunchKernelGGL(gfk_win_update_k<1024>, g, dim3(1024), gfk_win_update_smem(m), s, *m, *u);
   return (int)hipGetLastError();
 }
 
@@ -295,6 +344,9 @@ extern "C" int gfk_win_update_set_smem(size_t bytes) {
   static size_t cur = 0;
   if (bytes <= cur) return 0;
   cur = bytes;
-  return (int)hipFuncSetAttribute((const void*)gfk_win_update,
+  hipError_t e = hipFuncSetAttribute((const void*)gfk_win_update_k<512>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (e != hipSuccess) return (int)e;
+  return (int)hipFuncSetAttribute((const void*)gfk_win_update_k<1024>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }

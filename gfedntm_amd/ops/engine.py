@@ -47,8 +47,10 @@ LDS_LIMIT = 160 * 1024
 VB = 64
 # stage_flags plans, fastest first: bit 0 = MLP weights staged in LDS (enc_in,
 # post_bwd); bit 1 = the posterior kernels read the [B, K] batch matrices from L2
-# instead of staging them (large K)
-STAGE_PLANS = (1, 0, 2)
+# instead of staging them (large K).  Plan 3 (weights staged, batch matrices from L2)
+# is the large-K plan: the head weights [K, H] feed post_bwd's GEMVs from LDS instead
+# of one dependent L2 round trip per pass
+STAGE_PLANS = (1, 0, 3, 2)
 
 
 def _explain(ok: bool, why: str, explain: bool) -> bool:
@@ -120,7 +122,7 @@ def lds_required(tm, bmax: int) -> int:
     lib = native.kernels()
     which = (0, 1) if m.kind == abi.KIND_PRODLDA else (2, 3)
     need = 0
-    for flags in STAGE_PLANS[1:]:        # weights unstaged; batch matrices in LDS, then in L2
+    for flags in (0, 2):                 # weights unstaged; batch matrices in LDS, then in L2
         m.stage_flags = flags
         need = int(max(lib.gfk_smem_required(C.byref(m), w) for w in which + (4, 5, 7)))
         if need <= LDS_LIMIT:
@@ -400,10 +402,19 @@ class FusedEngine(EngineBase):
             cu = props.multi_processor_count
             sm = self.lib.gfk_smem_required(C.byref(m), 0)
             m.dec_grid = int(min(m.n_tiles, (2 if 2 * sm <= LDS_LIMIT else 1) * cu))
-            # backward: one workgroup per tile while the tiles fit the resident slots,
-            # else persistent (n_dpart workgroups, n_dpart dtheta partials)
-            sb = self.lib.gfk_smem_required(C.byref(m), 1)
-            m.n_dpart = int(min(m.n_tiles, (2 if 2 * sb <= LDS_LIMIT else 1) * cu))
+            # backward: one workgroup per tile while the tiles fit the resident slots;
+            # else persistent, n_dpart d theta_d slabs: with >= 4 k tiles the topics
+            # are split over 4 workgroups per slab (csrc/prodlda.hip, 8 waves each, two
+            # per CU when their LDS allows), otherwise one 16-wave workgroup per CU
+            sb = self.lib.gfk_smem_required(C.byref(m), 1)      # one tile per workgroup
+            if m.n_tiles <= (2 if 2 * sb <= LDS_LIMIT else 1) * cu:
+                m.n_dpart = m.n_tiles
+            elif -(-m.K // 16) >= 4:
+                m.n_dpart = cu // 2
+                if 2 * self.lib.gfk_smem_required(C.byref(m), 1) > LDS_LIMIT:
+                    m.n_dpart = cu // 4
+            else:
+                m.n_dpart = cu
         self._alloc_workspace()
         rc = self.lib.gfk_setup(C.byref(m))
         if rc:

@@ -13,7 +13,7 @@ P = C.c_void_p
 
 # activation / model / input codes
 ACT_CODES = {"softplus": 0, "relu": 1, "sigmoid": 2, "tanh": 3, "leakyrelu": 4, "elu": 5,
-             "selu": 6}
+             "selu": 6, "rrelu": 7}
 KIND_PRODLDA, KIND_LDA = 0, 1
 IN_BOW, IN_COMBINED, IN_CONTEXTUAL = 0, 1, 2
 

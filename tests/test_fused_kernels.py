@@ -71,7 +71,9 @@ def _grads_of(tm_fused):
                                             (64, 120, 25, (30, 20), 700),        # odd K, odd strides
                                             (64, 80, 50, (50, 50), 30000),       # many V tiles
                                             (64, 80, 50, (50, 50), 40000),       # persistent decoder
-                                            (64, 80, 200, (50, 50), 40000)])     # persistent, 3 tiles/WG
+                                            (64, 80, 200, (50, 50), 40000),      # persistent, 4 k ranges
+                                            (64, 80, 20, (32, 24), 40000),       # persistent, one k range
+                                            (128, 200, 100, (50, 50), 70000)])   # k ranges of 2 tiles, B=128
 def test_step_matches_oracle(model_type, B, n_docs, K, H, V):
     _oracle_step(model_type, B, n_docs, K, H, V)
 
@@ -128,7 +130,22 @@ def _oracle_step(model_type, B, n_docs, K, H, V, nnz=40):
     assert float(e.grad.abs().max().item()) == 0.0   # consumed and cleared
 
 
-@pytest.mark.parametrize("activation", ["relu", "tanh", "elu", "selu", "sigmoid", "leakyrelu"])
+class _SlopeAct(torch.nn.Module):
+    """RReLU with given per-element slopes (one tensor per call, in call order: the
+    input layer's activation, then each hidden layer's) -- the kernels' Philox draws."""
+
+    def __init__(self, slopes):
+        super().__init__()
+        self.slopes, self.i = slopes, 0
+
+    def forward(self, z):
+        r = self.slopes[self.i]
+        self.i += 1
+        return torch.where(z > 0, z, z * r)
+
+
+@pytest.mark.parametrize("activation", ["relu", "tanh", "elu", "selu", "sigmoid", "leakyrelu",
+                                        "rrelu"])
 def test_activations(activation):
     fused, ref = _pair("prodLDA", V=300, K=10, H=(16, 16, 8), B=32, activation=activation)
     X = random_csr(40, 300, 20, seed=3)
@@ -137,6 +154,16 @@ def test_activations(activation):
     e.run_phases(e.phases()[:-1])
     torch.cuda.synchronize()
     nb = int(plan.size[0])
+    if activation == "rrelu":
+        # ws_z holds d act / d z for RReLU: 1, or the element's drawn slope in [1/8, 1/3]
+        slopes = [e.ws[f"z{l}"][:nb].clone() for l in range(3)]
+        neg = torch.cat([s[s != 1.0] for s in slopes])
+        assert neg.numel() > 0 and float(neg.min()) >= 0.125 and float(neg.max()) <= 1 / 3 + 1e-6
+        act = _SlopeAct(slopes)
+        net = ref.model.inf_net
+        net.activation = act
+        for blk in net.hiddens:
+            blk[1] = act
     ids = torch.from_numpy(plan.batch(0).astype(np.int64)).cuda()
     x = data.dense_rows(ids)
     loss, _, _ = avitm_loss_explicit(ref.model, x, e.ws["eps"][:nb], e.ws["mask_h"][:nb],

@@ -58,10 +58,12 @@ def infer_normals(seed: int, n_docs: int, K: int, S: int) -> np.ndarray:
     return out
 
 
-def _trained(K=20, H=(32, 24), V=700, n_docs=300, steps=5, seed=0, model_type="prodLDA"):
+def _trained(K=20, H=(32, 24), V=700, n_docs=300, steps=5, seed=0, model_type="prodLDA",
+             activation="softplus"):
     torch.manual_seed(seed)
     tm = AVITM(input_size=V, n_components=K, model_type=model_type, hidden_sizes=H,
-               batch_size=64, verbose=False, device="cuda", backend="fused")
+               batch_size=64, verbose=False, device="cuda", backend="fused",
+               activation=activation)
     X = random_csr(n_docs, V, 40, seed=1)
     data = DeviceCSR(X, "cuda")
     tm.engine.bind_data(data, BatchPlan.build(n_docs, 64, steps, seed=seed))
@@ -76,6 +78,18 @@ def _trained(K=20, H=(32, 24), V=700, n_docs=300, steps=5, seed=0, model_type="p
                                  (50, (100, 100, 80)), (30, (200, 64))])
 def test_moments_match_eval_encoder(model_type, K, H):
     tm, X, data = _trained(K=K, H=H, model_type=model_type)
+    mom = tm.engine.theta_infer(data, moments=True)
+    tm.model.eval()
+    with torch.no_grad():
+        mu, ls = tm.model.inf_net(torch.from_numpy(X.toarray()).cuda())
+    torch.testing.assert_close(mom[:, 0], mu, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(mom[:, 1], ls, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("activation", ["rrelu", "selu"])
+def test_moments_eval_activation(activation):
+    """Eval-mode activations in the inference kernel (RReLU: the mean slope)."""
+    tm, X, data = _trained(K=20, H=(32, 24), activation=activation)
     mom = tm.engine.theta_infer(data, moments=True)
     tm.model.eval()
     with torch.no_grad():

@@ -22,8 +22,9 @@ dirs=""
 for pmc in "$SQ" "FETCH_SIZE" "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i + 1))
   echo "=== pmc pass $i: $pmc"
+  # counter passes serialise every dispatch: a short run (the later flags win)
   timeout -s KILL 180 rocprofv3 --pmc $pmc --output-format csv -d "$out/pmc$i" -o run \
-      -- python bench.py "$@" --no-npmi > "$out/pmc$i.log" 2>&1 || exit $?
+      -- python bench.py "$@" --no-npmi --steps 40 --warmup 10 > "$out/pmc$i.log" 2>&1 || exit $?
   f=$(find "$out/pmc$i" -name "*counter_collection.csv" | head -n 1)
   dirs="$dirs $(dirname "$f")"
 done
