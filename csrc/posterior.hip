@@ -69,15 +69,79 @@ __host__ __device__ inline bool batch_in_lds(const GfkModel& m) { return !(m.sta
 
 extern "C" size_t gfk_post_fwd_smem(const GfkModel* m) {
   const size_t mats = batch_in_lds(*m) ? 2 * (size_t)m->bmax * m->K : 0;
-  return sizeof(float) * (mats + 4 * (size_t)pad4(m->K));
+  return sizeof(float) * (mats + 4 * (size_t)pad4(m->K) + 2 * FT);
 }
 
-// Column statistics of the raw heads (16 lanes -- one DPP row -- per column, RPT =
-// rows per lane held in registers across the mean and variance passes, 64 columns
-// per pass); workgroup 0 also advances the running statistics (prefetched rmp /
-// rvp, one per pass).
-template <int RPT>
+// Column reductions over the batch of [B][K] matrices, lane-per-column: thread t owns
+// column c2 = t % 512 of the 2K (mu | log sigma^2) columns and the rows b = t / 512 + 2 i
+// (two row groups), so a wave's loads are 64 consecutive floats of a row (coalesced
+// from L2, bank-conflict free from LDS) -- the 16-lanes-per-column layout this replaced
+// touched 64 cache lines per load instruction.  RPG = rows per group (bmax / 2); the
+// two groups' partials meet in `red` [2][512] (LDS).
+constexpr int CG = 512;                 // columns per workgroup pass (2K <= 512)
+constexpr int NGR = FT / CG;            // row groups
+
+// Column statistics of the raw heads (mean, biased variance -> rstd); workgroup 0
+// also advances the running statistics (rm0 / rv0: this thread's column, prefetched).
+template <int RPG>
 __device__ __forceinline__ void post_colstats(const GfkModel& m, const float* mr, const float* lr,
+                                              float* cmean, float* crstd, float* red, float rm0,
+                                              float rv0, int nb, float inv_nb, int row, int tid) {
+  constexpr int RB = 16;                  // rows per load batch (registers)
+  const int K = m.K, c2 = tid % CG, grp = tid / CG;
+  const int cc = min(c2, 2 * K - 1);
+  const float* x = cc < K ? mr + cc : lr + (cc - K);
+  float s = 0.f;
+#pragma unroll 1
+  for (int i0 = 0; i0 < RPG; i0 += RB) {
+    float xv[RB];
+#pragma unroll
+    for (int i = 0; i < RB; ++i) xv[i] = x[min(grp + NGR * (i0 + i), nb - 1) * K];
+#pragma unroll
+    for (int i = 0; i < RB; ++i) s += grp + NGR * (i0 + i) < nb ? xv[i] : 0.f;
+  }
+  red[tid] = s;
+  lds_barrier();
+  const float mean = (red[c2] + red[CG + c2]) * inv_nb;
+  float q = 0.f;                          // two-pass variance (re-read, as torch's BN)
+#pragma unroll 1
+  for (int i0 = 0; i0 < RPG; i0 += RB) {
+    float xv[RB];
+#pragma unroll
+    for (int i = 0; i < RB; ++i) xv[i] = x[min(grp + NGR * (i0 + i), nb - 1) * K];
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      const float d = grp + NGR * (i0 + i) < nb ? xv[i] - mean : 0.f;
+      q += d * d;
+    }
+  }
+  red[FT + tid] = q;
+  lds_barrier();
+  if (grp == 0 && c2 < 2 * K) {
+    const float var = (red[FT + c2] + red[FT + CG + c2]) * inv_nb;
+    const float rstd = rsqrtf(var + m.bn_eps);
+    cmean[c2] = mean;
+    crstd[c2] = rstd;
+    if (row == 0) {
+      const int k = c2 < K ? c2 : c2 - K;
+      float* rm = c2 < K ? m.mu_rm + k : m.s_rm + k;
+      float* rv = c2 < K ? m.mu_rv + k : m.s_rv + k;
+      const float mom = m.bn_momentum;
+      const float unb = nb > 1 ? var * (float)nb / (float)(nb - 1) : var;
+      float nm = (1.f - mom) * rm0 + mom * mean, nv = (1.f - mom) * rv0 + mom * unb;
+      if (m.fed_scale_on && is_shared(m, rm)) { nm *= m.fed_scale; nv *= m.fed_scale; }
+      *rm = nm;
+      *rv = nv;
+      m.ws_bn_rstd[c2] = rstd;
+    }
+  }
+}
+
+// LDS-resident batch matrices (K small enough): 16 lanes -- one DPP row -- per column,
+// RPT rows per lane, 64 columns per pass (rmp / rvp: the running statistics of the
+// pass's column, prefetched).
+template <int RPT>
+__device__ __forceinline__ void post_colstats_dpp(const GfkModel& m, const float* mr, const float* lr,
                                               float* cmean, float* crstd, const float (&rmp)[8],
                                               const float (&rvp)[8], int nb, float inv_nb, int row,
                                               int tid) {
@@ -146,6 +210,7 @@ __global__ void __launch_bounds__(FT) gfk_post_fwd_k(GfkModel m) {
   const float* lr = in_lds ? smem + B * K : ls_raw;
   float* cmean = smem + (in_lds ? 2 * B * K : 0);
   float* crstd = cmean + 2 * pad4(K);
+  float* red = crstd + 2 * pad4(K);        // [2][FT] column-reduction scratch
   GFK_STAMP(m, 0);
 
   // ---- one round: the raw heads of every row (LDS-DMA) + the own row + stats ----
@@ -176,18 +241,25 @@ __global__ void __launch_bounds__(FT) gfk_post_fwd_k(GfkModel m) {
     nbt1 = *m.nbt_s;
     at0 = *m.adam_t;
   }
-  // running stats of the columns this thread updates (workgroup 0), one per column
-  // pass, prefetched with the staging round (K <= 256: at most 8 passes)
+  // running stats of the columns this thread updates (workgroup 0), prefetched: one
+  // per 64-column pass (LDS layout) or its one column (lane-per-column layout)
   constexpr int CP = 8;
   float rmp[CP], rvp[CP];
+  float rm0 = 0.f, rv0 = 0.f;
+  if constexpr (InLds) {
 #pragma unroll
-  for (int q = 0; q < CP; ++q) {
-    rmp[q] = rvp[q] = 0.f;
-    if (row == 0 && q * (FT / 16) < 2 * K) {
-      const int c2 = min(q * (FT / 16) + (tid >> 4), 2 * K - 1);
-      rmp[q] = c2 < K ? m.mu_rm[c2] : m.s_rm[c2 - K];
-      rvp[q] = c2 < K ? m.mu_rv[c2] : m.s_rv[c2 - K];
+    for (int q = 0; q < CP; ++q) {
+      rmp[q] = rvp[q] = 0.f;
+      if (row == 0 && q * (FT / 16) < 2 * K) {
+        const int c2 = min(q * (FT / 16) + (tid >> 4), 2 * K - 1);
+        rmp[q] = c2 < K ? m.mu_rm[c2] : m.s_rm[c2 - K];
+        rvp[q] = c2 < K ? m.mu_rv[c2] : m.s_rv[c2 - K];
+      }
     }
+  } else if (row == 0 && tid < CG) {
+    const int c2 = min(tid, 2 * K - 1);
+    rm0 = c2 < K ? m.mu_rm[c2] : m.s_rm[c2 - K];
+    rv0 = c2 < K ? m.mu_rv[c2] : m.s_rv[c2 - K];
   }
   // NeuralLDA: per-topic log-sum-exp over V from lda_beta_fwd's tile partials
   // (topics dealt to the workgroups' last wave)
@@ -212,8 +284,13 @@ __global__ void __launch_bounds__(FT) gfk_post_fwd_k(GfkModel m) {
   // ---- column statistics over the batch: 4 threads per column, the column's
   // values held in registers across the mean and variance passes ----
   const float inv_nb = 1.f / (float)nb;
-  if (B <= 64) post_colstats<4>(m, mr, lr, cmean, crstd, rmp, rvp, nb, inv_nb, row, tid);
-  else post_colstats<8>(m, mr, lr, cmean, crstd, rmp, rvp, nb, inv_nb, row, tid);
+  if constexpr (InLds) {
+    if (B <= 64) post_colstats_dpp<4>(m, mr, lr, cmean, crstd, rmp, rvp, nb, inv_nb, row, tid);
+    else post_colstats_dpp<8>(m, mr, lr, cmean, crstd, rmp, rvp, nb, inv_nb, row, tid);
+  } else {
+    if (B <= 64) post_colstats<32>(m, mr, lr, cmean, crstd, red, rm0, rv0, nb, inv_nb, row, tid);
+    else post_colstats<64>(m, mr, lr, cmean, crstd, red, rm0, rv0, nb, inv_nb, row, tid);
+  }
   if (row == 0 && tid == 0) {
     *m.nbt_mu = nbt0 + 1;
     *m.nbt_s = nbt1 + 1;
@@ -367,7 +444,7 @@ __global__ void __launch_bounds__(PT) gfk_row_bwd_k(GfkModel m) {
 // LDS plan (floats): dmu, dls, mu, ls [B][K] + s1..s4 [2K] + own-row vectors
 // (dmr|dlr [2K], dz ping-pong [2][hmax], z rows, mask) + staged weights.
 struct PostLds {
-  int dmu, dls, mu, ls, sums, pm, dr, v0, v1, zrow, mask, red, w, total;
+  int dmu, dls, mu, ls, sums, pm, dr, v0, v1, zrow, mask, red, red2, w, total;
 };
 
 __host__ __device__ inline PostLds post_lds(const GfkModel& m) {
@@ -390,6 +467,7 @@ __host__ __device__ inline PostLds post_lds(const GfkModel& m) {
     if (l < m.n_hidden) o += pad4(m.H[l]);
   L.mask = o; o += pad4(m.H[m.n_hidden - 1]);
   L.red = o; o += FT / 64;                // block_sum_wave0 scratch, one float per wave
+  L.red2 = o; o += 2 * FT;                // column-reduction scratch [2][FT]
   L.w = o;
   if (m.stage_flags & 1) o += post_weight_floats(m);
   L.total = o;
@@ -434,6 +512,79 @@ template <class Epi>
 __device__ __forceinline__ void colvec_gemv(const float* W, int ldw, const float* x, int n_out, int n_in,
                                             int tid, Epi epi) {
   gemv_cols(n_out, n_in, tid, [&](int k, int j) { return x[k] * W[k * ldw + j]; }, epi);
+}
+
+// Column sums over the batch for the BN backward of the heads: s1[c2] = sum_b dy,
+// s2[c2] = sum_b dy * xhat over the 2K columns (mu | log sigma^2), lane-per-column
+// (see CG / NGR above).  red: [2][FT] LDS scratch.
+template <int RPG>
+__device__ __forceinline__ void post_bn_sums(int K, int nb, const float* dmu, const float* dls,
+                                             const float* mu, const float* ls, float* s1o,
+                                             float* s2o, float* red, int tid) {
+  constexpr int RB = 16;                  // rows per load batch (registers)
+  const int c2 = tid % CG, grp = tid / CG;
+  const int cc = min(c2, 2 * K - 1), k = cc < K ? cc : cc - K;
+  const float* dy = cc < K ? dmu : dls;
+  const float* xh = cc < K ? mu : ls;
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int i0 = 0; i0 < RPG; i0 += RB) {
+    float dv[RB], xv[RB];
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      const int r = min(grp + NGR * (i0 + i), nb - 1);
+      dv[i] = dy[r * K + k];
+      xv[i] = xh[r * K + k];
+    }
+#pragma unroll
+    for (int i = 0; i < RB; ++i)
+      if (grp + NGR * (i0 + i) < nb) {
+        s1 += dv[i];
+        s2 += dv[i] * xv[i];
+      }
+  }
+  red[tid] = s1;
+  red[FT + tid] = s2;
+  lds_barrier();
+  if (grp == 0 && c2 < 2 * K) {
+    s1o[c2] = red[c2] + red[CG + c2];
+    s2o[c2] = red[FT + c2] + red[FT + CG + c2];
+  }
+}
+
+// The extra workgroup's sums for the prior gradients: s3[c2] = sum_b mu (c2 < K) |
+// sum_b exp(ls) (c2 >= K), s4[k] = sum_b (prior_mean - mu)^2 -- same layout.
+template <int RPG>
+__device__ __forceinline__ void post_prior_sums(int K, int nb, const float* mu, const float* ls,
+                                                const float* pmean, float* s3o, float* s4o,
+                                                float* red, int tid) {
+  constexpr int RB = 16;
+  const int c2 = tid % CG, grp = tid / CG;
+  const int cc = min(c2, 2 * K - 1), k = cc < K ? cc : cc - K;
+  const float* xh = cc < K ? mu : ls;
+  const float pm = pmean[k];
+  float s3 = 0.f, s4 = 0.f;
+#pragma unroll
+  for (int i0 = 0; i0 < RPG; i0 += RB) {
+    float xv[RB];
+#pragma unroll
+    for (int i = 0; i < RB; ++i) xv[i] = xh[min(grp + NGR * (i0 + i), nb - 1) * K + k];
+#pragma unroll
+    for (int i = 0; i < RB; ++i)
+      if (grp + NGR * (i0 + i) < nb) {
+        const float x = xv[i];
+        s3 += cc < K ? x : expf(x);
+        const float dm = pm - x;
+        s4 += cc < K ? dm * dm : 0.f;
+      }
+  }
+  red[tid] = s3;
+  red[FT + tid] = s4;
+  lds_barrier();
+  if (grp == 0 && c2 < 2 * K) {
+    s3o[c2] = red[c2] + red[CG + c2];
+    s4o[c2] = red[FT + c2] + red[FT + CG + c2];
+  }
 }
 
 // grid: bmax + 1 workgroups: row = blockIdx.x < bmax, plus one extra workgroup
@@ -502,7 +653,7 @@ __global__ void __launch_bounds__(FT) gfk_post_bwd_k(GfkModel m) {
   vm_barrier();
   GFK_STAMP(m, 11);
 
-  // ---- column sums over the batch: 4 threads per column ----
+  // ---- column sums over the batch (DPP rows in LDS, lane-per-column from L2) ----
   const float* dmu = in_lds ? smem + L.dmu : dmu_g;
   const float* dls = in_lds ? smem + L.dls : dls_g;
   const float* mu = in_lds ? smem + L.mu : mu_g;
@@ -513,27 +664,32 @@ __global__ void __launch_bounds__(FT) gfk_post_bwd_k(GfkModel m) {
   if (extra) {
     // ---- extra workgroup: prior gradients (-> grad slots), loss, step ----
     const float* pmean = smem + L.pm;   // prior mean, staged
-    for (int cb = 0; cb < 2 * K; cb += FT / 16) {
-      const int c2 = cb + (tid >> 4), g = tid & 15;
-      const bool valid = c2 < 2 * K;
-      const int k = c2 < K ? c2 : c2 - K;
-      const float* xh = c2 < K ? mu : ls;
-      const float pm = pmean[k];
-      float s3 = 0.f, s4 = 0.f;         // sum mu | sum exp(ls), sum (pm - mu)^2
-      if (valid)
+    if constexpr (in_lds) {             // LDS: 16 lanes per column, DPP reductions
+      for (int cb = 0; cb < 2 * K; cb += FT / 16) {
+        const int c2 = cb + (tid >> 4), g = tid & 15;
+        const bool valid = c2 < 2 * K;
+        const int k = c2 < K ? c2 : c2 - K;
+        const float* xh = c2 < K ? mu : ls;
+        const float pm = pmean[k];
+        float s3 = 0.f, s4 = 0.f;         // sum mu | sum exp(ls), sum (pm - mu)^2
+        if (valid)
 #pragma unroll 4
-        for (int r = g; r < nb; r += 16) {
-          const float x = xh[r * K + k];
-          s3 += c2 < K ? x : expf(x);
-          const float dm = pm - x;
-          s4 += c2 < K ? dm * dm : 0.f;
+          for (int r = g; r < nb; r += 16) {
+            const float x = xh[r * K + k];
+            s3 += c2 < K ? x : expf(x);
+            const float dm = pm - x;
+            s4 += c2 < K ? dm * dm : 0.f;
+          }
+        s3 = row16_sum(s3);
+        s4 = row16_sum(s4);
+        if (valid && g == 0) {
+          S[2 * P2 + c2] = s3;
+          S[3 * P2 + c2] = s4;
         }
-      s3 = row16_sum(s3);
-      s4 = row16_sum(s4);
-      if (valid && g == 0) {
-        S[2 * P2 + c2] = s3;
-        S[3 * P2 + c2] = s4;
       }
+    } else {                            // L2: lane-per-column (coalesced)
+      if (B <= 64) post_prior_sums<32>(K, nb, mu, ls, pmean, S + 2 * P2, S + 3 * P2, smem + L.red2, tid);
+      else post_prior_sums<64>(K, nb, mu, ls, pmean, S + 2 * P2, S + 3 * P2, smem + L.red2, tid);
     }
     lds_barrier();
     const float wk = m.kl_weight;
@@ -551,26 +707,31 @@ __global__ void __launch_bounds__(FT) gfk_post_bwd_k(GfkModel m) {
     }
     return;
   }
-  for (int cb = 0; cb < 2 * K; cb += FT / 16) {
-    const int c2 = cb + (tid >> 4), g = tid & 15;
-    const bool valid = c2 < 2 * K;
-    const int k = c2 < K ? c2 : c2 - K;
-    const float* dy = c2 < K ? dmu : dls;
-    const float* xh = c2 < K ? mu : ls;
-    float s1 = 0.f, s2 = 0.f;
-    if (valid)
+  if constexpr (in_lds) {               // LDS: 16 lanes per column, DPP reductions
+    for (int cb = 0; cb < 2 * K; cb += FT / 16) {
+      const int c2 = cb + (tid >> 4), g = tid & 15;
+      const bool valid = c2 < 2 * K;
+      const int k = c2 < K ? c2 : c2 - K;
+      const float* dy = c2 < K ? dmu : dls;
+      const float* xh = c2 < K ? mu : ls;
+      float s1 = 0.f, s2 = 0.f;
+      if (valid)
 #pragma unroll 4
-      for (int r = g; r < nb; r += 16) {
-        const float d = dy[r * K + k], x = xh[r * K + k];
-        s1 += d;
-        s2 += d * x;
+        for (int r = g; r < nb; r += 16) {
+          const float d = dy[r * K + k], x = xh[r * K + k];
+          s1 += d;
+          s2 += d * x;
+        }
+      s1 = row16_sum(s1);
+      s2 = row16_sum(s2);
+      if (valid && g == 0) {
+        S[c2] = s1;
+        S[P2 + c2] = s2;
       }
-    s1 = row16_sum(s1);
-    s2 = row16_sum(s2);
-    if (valid && g == 0) {
-      S[c2] = s1;
-      S[P2 + c2] = s2;
     }
+  } else {                              // L2: lane-per-column (coalesced)
+    if (B <= 64) post_bn_sums<32>(K, nb, dmu, dls, mu, ls, S, S + P2, smem + L.red2, tid);
+    else post_bn_sums<64>(K, nb, dmu, dls, mu, ls, S, S + P2, smem + L.red2, tid);
   }
   lds_barrier();
   GFK_STAMP(m, 12);

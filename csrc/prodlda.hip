@@ -124,6 +124,7 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
   const int c0 = tile * VB;
   const int v = c0 + col;
   const bool valid = v < V;
+  GFK_STAMP(m, 21);
   // ---- staging: the registers of this tile -> LDS ----
   if (tile != (int)blockIdx.x) lds_barrier();      // previous tile's bt / colp reads done
 #pragma unroll
@@ -465,6 +466,7 @@ prodlda_bwd_kernel(GfkModel m) {
     wave = uniform(tid >> 6);
     xrow = tid / TPR;
     xsub = tid % TPR;
+    GFK_STAMP(m, 23);
     // one staging round per tile: every global read is issued before the barrier
     issue_tile(tile);
     issue_first_nz();

@@ -1,52 +1,90 @@
 """Diagnostic: per-phase cycle counts inside the fused-step kernels (s_memtime stamps).
 
 Builds a -DGFK_STAMPS copy of the kernel library into build/stamps/, runs a few
-eager steps and prints the s_memtime deltas between phase stamps (lane 0 of
-workgroup 0).  Read the SHARES, not the absolute length (the stamps add fences).
+eager steps of a ProdLDA model of the given shape on random BoW rows and prints the
+s_memtime deltas between phase stamps (lane 0 of workgroup 0; in the vocab-tile loops
+of the decoder kernels: the workgroup's last tile).  Read the SHARES, not the
+absolute length (the stamps add fences).
+
+usage: python tools/stamps.py [--topics K] [--vocab V] [--hidden 50,50] [--batch B]
+                              [--nnz N] [--docs D] [--steps S]
 """
-import os, subprocess, sys, ctypes
+import argparse
+import os
+import subprocess
+import sys
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-out = os.path.join(ROOT, "build", "stamps")
-os.makedirs(out, exist_ok=True)
-from tools.build_native import KERNEL_SRCS
-srcs = [x for x in KERNEL_SRCS if os.path.exists(os.path.join(ROOT, "csrc", x))]
-objs = []
-for s in srcs:
-    o = os.path.join(out, s + ".o")
-    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17",
-                    "-munsafe-fp-atomics", "-DGFK_STAMPS", "-c", os.path.join(ROOT, "csrc", s), "-o", o],
+
+
+def build():
+    from tools.build_native import KERNEL_SRCS
+    out = os.path.join(ROOT, "build", "stamps")
+    os.makedirs(out, exist_ok=True)
+    objs = []
+    for s in KERNEL_SRCS:
+        src = os.path.join(ROOT, "csrc", s)
+        if not os.path.exists(src):
+            continue
+        o = os.path.join(out, s + ".o")
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17",
+                        "-munsafe-fp-atomics", "-DGFK_STAMPS", "-c", src, "-o", o], check=True)
+        objs.append(o)
+    so = os.path.join(out, "libgfedntm_kernels.so")
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-o", so] + objs,
                    check=True)
-    objs.append(o)
-so = os.path.join(out, "libgfedntm_kernels.so")
-subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-o", so] + objs, check=True)
-from gfedntm_amd.ops import native
-native.KERNELS_SO = so
-import torch
-from gfedntm_amd.models import AVITM
-from gfedntm_amd.data.bow import DeviceCSR, BatchPlan
-from tests.helpers import random_csr
-tm = AVITM(input_size=4466, n_components=50, hidden_sizes=(50, 50), verbose=False, backend="fused",
-           device="cuda")
-X = random_csr(1000, 4466, 170, seed=0)
-data = DeviceCSR(X, "cuda")
-tm.engine.bind_data(data, BatchPlan.build(1000, 64, 50))
-dbg = torch.zeros(64, dtype=torch.int64, device="cuda")
-tm.engine._m.dbg = dbg.data_ptr()
-tm.engine._a.dbg = dbg.data_ptr()
-for s in range(20):
-    tm.engine.step(s)
-torch.cuda.synchronize()
-d = dbg.cpu().numpy()
-nf = ["stage", "mfma", "bn", "store+rowlse"]
-print("prodlda_fwd cycles:", {nf[i]: int(d[17 + i] - d[16 + i]) for i in range(4)})
-nbw = ["stage", "sparse", "dense+bn_bwd", "mfma+update"]
-print("prodlda_bwd cycles:", {nbw[i]: int(d[25 + i] - d[24 + i]) for i in range(4)})
-print("post_fwd cycles: stage", int(d[1] - d[0]), "| colstats", int(d[2] - d[1]), "| row", int(d[3] - d[2]))
-print("row_bwd cycles:", int(d[9] - d[8]))
-print("post_bwd cycles: stage", int(d[11] - d[10]), "| colsums", int(d[12] - d[11]), "| rest", int(d[13] - d[12]))
-print("post_bwd rest: wg0 extras", int(d[14] - d[12]), "| bn_bwd", int(d[15] - d[14]),
-      "| heads", int(d[29] - d[15]), "| hidden", int(d[13] - d[29]))
-print("enc_in cycles: row+weights issue", int(d[5] - d[4]), "| gather+draws", int(d[6] - d[5]),
-      "| input+hidden", int(d[7] - d[6]))
-print("win_update (W_in tile 0) cycles: staging", int(d[41] - d[40]), "| mfma+update", int(d[42] - d[41]))
+    return so
+
+
+def main(argv=None):
+    p = argparse.ArgumentParser()
+    p.add_argument("--topics", type=int, default=50)
+    p.add_argument("--vocab", type=int, default=4466)
+    p.add_argument("--hidden", default="50,50")
+    p.add_argument("--batch", type=int, default=64)
+    p.add_argument("--nnz", type=int, default=170)
+    p.add_argument("--docs", type=int, default=1000)
+    p.add_argument("--steps", type=int, default=20)
+    a = p.parse_args(argv)
+    so = build()
+    from gfedntm_amd.ops import native
+    native.KERNELS_SO = so
+    import torch
+    from gfedntm_amd.data.bow import BatchPlan, DeviceCSR
+    from gfedntm_amd.models import AVITM
+    from tests.helpers import random_csr
+    tm = AVITM(input_size=a.vocab, n_components=a.topics,
+               hidden_sizes=tuple(int(h) for h in a.hidden.split(",")), batch_size=a.batch,
+               verbose=False, backend="fused", device="cuda")
+    X = random_csr(a.docs, a.vocab, a.nnz, seed=0)
+    data = DeviceCSR(X, "cuda")
+    tm.engine.bind_data(data, BatchPlan.build(a.docs, a.batch, a.steps))
+    dbg = torch.zeros(64, dtype=torch.int64, device="cuda")
+    tm.engine._m.dbg = dbg.data_ptr()
+    tm.engine._a.dbg = dbg.data_ptr()
+    for s in range(a.steps):
+        tm.engine.step(s)
+    torch.cuda.synchronize()
+    d = dbg.cpu().numpy()
+    m = tm.engine._m
+    print(f"K={a.topics} V={a.vocab} tiles={m.n_tiles} dec_grid={m.dec_grid} n_dpart={m.n_dpart} "
+          f"stage_flags={m.stage_flags}")
+    nf = ["stage", "mfma", "bn", "store+rowlse"]
+    print("prodlda_fwd (last tile of wg 0) cycles:", {"tile_start->stage": int(d[17] - d[21]),
+          **{nf[i]: int(d[17 + i] - d[16 + i]) for i in range(1, 4)}})
+    nbw = ["stage", "sparse", "dense+bn_bwd", "mfma+update"]
+    print("prodlda_bwd (last tile of wg 0) cycles:", {"stage": int(d[25] - d[23]),
+          **{nbw[i]: int(d[25 + i] - d[24 + i]) for i in range(1, 4)}})
+    print("post_fwd cycles: stage", int(d[1] - d[0]), "| colstats", int(d[2] - d[1]), "| row", int(d[3] - d[2]))
+    print("row_bwd cycles:", int(d[9] - d[8]))
+    print("post_bwd cycles: stage", int(d[11] - d[10]), "| colsums", int(d[12] - d[11]), "| rest", int(d[13] - d[12]))
+    print("post_bwd rest: wg0 extras", int(d[14] - d[12]), "| bn_bwd", int(d[15] - d[14]),
+          "| heads", int(d[29] - d[15]), "| hidden", int(d[13] - d[29]))
+    print("enc_in cycles: row+weights issue", int(d[5] - d[4]), "| gather+draws", int(d[6] - d[5]),
+          "| input+hidden", int(d[7] - d[6]))
+    print("win_update (W_in tile 0) cycles: staging", int(d[41] - d[40]), "| mfma+update", int(d[42] - d[41]))
+
+
+if __name__ == "__main__":
+    main()
