@@ -87,6 +87,10 @@ def parse(argv=None):
                    help="rounds of the separate untimed federation the NPMI is computed on "
                         "(0 = skip)")
     p.add_argument("--no-npmi", action="store_true")
+    p.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
+                   help="decoder GEMM operands (bf16: BASELINE config 'ProdLDA K=50 centralized "
+                        "bf16' -- bf16 MFMA operands, fp32 accumulation, fp32 master weights and "
+                        "Adam; the headline is fp32, the reference's precision)")
     p.add_argument("--solver", default="adam",
                    choices=["adam", "sgd", "adagrad", "adadelta", "rmsprop"],
                    help="optimizer (reference default adam; the others run in gradient mode)")
@@ -159,6 +163,8 @@ def _params(args):
     p.update(n_components=args.topics, model_type=args.model, batch_size=args.batch,
              hidden_sizes=tuple(int(h) for h in args.hidden.split(",")), solver=args.solver,
              contextual_size=args.contextual_size, num_epochs=10 ** 6)
+    if args.dtype != "fp32":
+        p["matmul_dtype"] = args.dtype
     return p
 
 
@@ -347,7 +353,7 @@ def _record(args, n_gpus, value, ms, V, npmi, final_loss, clients=None):
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": round(value / BASELINE_FED_DOCS_PER_S, 2),
-        "dtype": "fp32",
+        "dtype": args.dtype,
         "data": (f"synthetic (reference LDA generator: V={args.vocab}, K={args.topics}, "
                  f"{args.docs} docs/client, {args.nwords.replace(',', '-')} tokens, "
                  "5 frozen topics), random init"),
@@ -361,6 +367,9 @@ def _record(args, n_gpus, value, ms, V, npmi, final_loss, clients=None):
         "clients_note": ("one client: FedAvg over one client is the identity; the 8-client "
                          "figure is the --gpus 8 run" if clients == 1 else
                          f"{clients} federated clients"),
+        **({"precision": "bf16 operands of the ProdLDA decoder GEMMs (theta.beta, theta^T.dlogit, "
+                         "dlogit.beta^T) on v_mfma_f32_16x16x16_bf16, fp32 accumulation; fp32 "
+                         "parameters, Adam state and every other op"} if args.dtype == "bf16" else {}),
         "npmi": None if npmi is None else round(npmi, 4),
         "npmi_rounds": None if npmi is None else args.npmi_steps,
         "final_loss": final_loss,

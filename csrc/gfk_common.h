@@ -54,7 +54,8 @@ typedef struct GfkModel {
   float drop_enc, drop_theta;
   float bn_momentum, bn_eps;
   float kl_weight;       // CTM loss_weights["beta"], 1 for AVITM
-  float pad1;
+  int32_t beta_split;    // 1: prodlda_bwd writes beta's gradient (fused mode otherwise) and
+                         //    the generic optimizer kernel updates beta in one float4 pass
   uint64_t seed;
 
   // ---- parameters (views into the flat fp32 buffer) and their gradients ----
@@ -133,6 +134,12 @@ typedef struct GfkModel {
   // first); valid entries j < e1 - e0 of the row
   int32_t* ws_sidx;
   float* ws_sval;
+  // ---- precision of the decoder GEMMs (theta.beta, theta^T.dlogit, dlogit.beta^T):
+  // 0 = fp32 matrix cores (v_mfma_f32_16x16x4_f32, the reference's precision), 1 = bf16
+  // operands, fp32 accumulation (v_mfma_f32_16x16x16_bf16); parameters, Adam state and
+  // every other op stay fp32
+  int32_t mm_bf16;
+  int32_t pad2;
 } GfkModel;
 
 // Gradient + update jobs of the small tensors, run by the update kernel next to
@@ -179,7 +186,8 @@ typedef struct GfkAdam {
   int32_t solver;                    // GFK_SOLVER_*: update rule of the optimizer segments
   int64_t seg_start[GFK_MAX_SEGS];   // in floats, multiples of 4
   int64_t seg_end[GFK_MAX_SEGS];
-  int32_t seg_flags[GFK_MAX_SEGS];   // bit0: Adam update, bit1: FedAvg pre-scale
+  int32_t seg_flags[GFK_MAX_SEGS];   // bit0: Adam update, bit1: FedAvg pre-scale,
+                                     // bit2: keep the gradient (it is rewritten whole every step)
   float lr, beta1, beta2, eps, weight_decay, scale;
   const int32_t *t;                  // device Adam step count (already incremented)
   const float *coef;                 // [2] step size, 1/sqrt(bias correction 2) (see GfkModel)
@@ -466,6 +474,19 @@ __device__ __forceinline__ f32x4 mfma16x16x4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// 16x16x16 bf16 MFMA, fp32 accumulation: lane l supplies A[l&15][4(l>>4) + j] and
+// B[4(l>>4) + j][l&15] (j < 4) as fp32, rounded to bf16 here (v_cvt_pk_bf16_f32, RNE);
+// the result layout is the one of mfma16x16x4.
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 mfma16x16x16bf(const float (&a)[4], const float (&b)[4], f32x4 c) {
+  bf16x4 ab, bb;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { ab[j] = (__bf16)a[j]; bb[j] = (__bf16)b[j]; }
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4, ab),
+                                                   __builtin_bit_cast(s16x4, bb), c, 0, 0, 0);
+}
+
 // A strided, bounds-checked matrix view (LDS or global).  Out-of-range elements
 // read as 0 through a clamped address + select, so no load is predicated.
 struct MatView {
@@ -630,7 +651,7 @@ __device__ __forceinline__ void adam_block(const GfkAdam& a, int blk, int tid, i
       }
       *reinterpret_cast<float4*>(a.m + o) = m;
       *reinterpret_cast<float4*>(a.v + o) = v;
-      *reinterpret_cast<float4*>(a.g + o) = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (!(flags & 4)) *reinterpret_cast<float4*>(a.g + o) = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     if (do_scale) { p.x *= a.scale; p.y *= a.scale; p.z *= a.scale; p.w *= a.scale; }
     if (do_adam || do_scale) *reinterpret_cast<float4*>(a.p + o) = p;

@@ -77,13 +77,14 @@ __device__ __forceinline__ float sum_groups(float v) {
 // statistics are loaded into registers right after this tile's staging barrier, so
 // they land while this tile's MFMAs / batch-norm / stores run.
 // dynamic LDS: th[BM*kt] + bt[KP*LDB_F] + colp[4][64] + colq[4][64] + stat[2][64]
-template <int BM>
+// BF: bf16 MFMA operands (16x16x16, K padded to 16), fp32 accumulation.
+template <int BM, bool BF>
 __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int K = m.K, V = m.V, KT = m.kt;
   int tid = threadIdx.x;                      // re-made opaque per tile (no hoisted addresses)
   const int lane = tid & 63, wave = uniform(tid >> 6);
-  const int KP = round_up(K, 4);
+  const int KP = round_up(K, BF ? 16 : 4);
   float* th = smem;
   float* bt = th + BM * KT;
   float* colp = bt + KP * LDB_F;
@@ -141,7 +142,28 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
   if (tile + (int)gridDim.x < m.n_tiles) issue_tile(tile + gridDim.x);
   // ---- logits for this wave's row tiles x 16 columns (two independent MFMA chains) ----
   f32x4 acc[NRT];
-  {
+  if constexpr (BF) {
+#pragma unroll
+    for (int i = 0; i < NRT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int kq = 4 * (lane >> 4);
+    const float* bp = bt + kq * LDB_F + col;
+    const float* ap = th + (rt0 * 16 + (lane & 15)) * KT + kq;
+    if (rt0 < RT) {
+      for (int k0 = 0; k0 < KP; k0 += 16) {
+        float b[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = bp[(k0 + j) * LDB_F];
+#pragma unroll
+        for (int i = 0; i < NRT; ++i)
+          if (rt0 + 4 * i < RT) {
+            float a[4];     // theta_d rows hold kt >= K columns: mask the K..16-padding
+#pragma unroll
+            for (int j = 0; j < 4; ++j) a[j] = k0 + kq + j < K ? ap[i * 64 * KT + k0 + j] : 0.f;
+            acc[i] = mfma16x16x16bf(a, b, acc[i]);
+          }
+      }
+    }
+  } else {
     f32x4 acc2[NRT];
 #pragma unroll
     for (int i = 0; i < NRT; ++i) acc[i] = acc2[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -352,7 +374,8 @@ extern "C" __global__ void __launch_bounds__(64) gfk_prodlda_row_loss(GfkModel m
 __host__ __device__ __forceinline__ int kt_stride(int w) { return w % 32 == 16 ? w : w + 16; }
 __host__ __device__ __forceinline__ int bwd_kpq(int K, int kq) { return 16 * ((round_up(K, 16) / 16 + kq - 1) / kq); }
 
-template <int BM, int MAXU, int KQ>
+// BF: bf16 MFMA operands (16x16x16), fp32 accumulation, for both GEMMs.
+template <int BM, int MAXU, int KQ, bool BF>
 __global__ void __launch_bounds__(KQ == 1 ? DEC_THREADS : 512, KQ == 1 ? 1 : 2)
 prodlda_bwd_kernel(GfkModel m) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -387,7 +410,7 @@ prodlda_bwd_kernel(GfkModel m) {
   float* rs = Sb + BM;
   const int NB_T = nks * 4;                    // dbeta subtiles (k tile, column strip)
   const int NDT_T = (BM / 16) * nks;           // d theta_d subtiles (row tile, k tile)
-  const bool fused = m.update_mode == 1;
+  const bool fused = m.update_mode == 1 && !m.beta_split;
   const int nb = *m.ws_nb;
   const AdamCoef ac = adam_coef(m);
   const bool beta_shared = is_shared(m, m.beta);
@@ -470,7 +493,7 @@ prodlda_bwd_kernel(GfkModel m) {
     // one staging round per tile: every global read is issued before the barrier
     issue_tile(tile);
     issue_first_nz();
-    issue_state(tile);
+    if (fused) issue_state(tile);              // (beta_split: no Adam state here)
     if (tile != slab) lds_barrier();           // the previous tile's LDS reads are done
     // ---- (1) this tile's registers -> LDS; zero the logit-gradient tile ----
 #pragma unroll
@@ -537,15 +560,29 @@ prodlda_bwd_kernel(GfkModel m) {
       const int t = wave + NW * j;
       if (t >= NDT_T) break;
       const int rt = t / nks, ks = t % nks;
-      const float* ap = dt + (rt * 16 + (lane & 15)) * LDD + (lane >> 4);
-      const float* bp = bt + (ks * 16 + (lane & 15)) * LDB_B + (lane >> 4);
-      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (BF) {         // A[b][c] = dt row, B[c][k] = beta row: 4 consecutive c each
+        const float* ap = dt + (rt * 16 + (lane & 15)) * LDD + 4 * (lane >> 4);
+        const float* bp = bt + (ks * 16 + (lane & 15)) * LDB_B + 4 * (lane >> 4);
+        f32x4 a0 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int c = 0; c < VB; c += 8) {
-        a0 = mfma16x16x4(ap[c], bp[c], a0);
-        a1 = mfma16x16x4(ap[c + 4], bp[c + 4], a1);
+        for (int c = 0; c < VB; c += 16) {
+          float a[4], b[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) { a[q] = ap[c + q]; b[q] = bp[c + q]; }
+          a0 = mfma16x16x16bf(a, b, a0);
+        }
+        dacc[j] += a0;
+      } else {
+        const float* ap = dt + (rt * 16 + (lane & 15)) * LDD + (lane >> 4);
+        const float* bp = bt + (ks * 16 + (lane & 15)) * LDB_B + (lane >> 4);
+        f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < VB; c += 8) {
+          a0 = mfma16x16x4(ap[c], bp[c], a0);
+          a1 = mfma16x16x4(ap[c + 4], bp[c + 4], a1);
+        }
+        dacc[j] += a0 + a1;
       }
-      dacc[j] += a0 + a1;
     }
     };
     // ---- (6) dbeta[k, c] = sum_b th[b, k] dlogit[b, c] -> update (fused) or gradient ----
@@ -558,13 +595,25 @@ prodlda_bwd_kernel(GfkModel m) {
         const int t = wave + NW * u;
         if (t >= NB_T) break;
         const int ks = t >> 2, cst = t & 3;
-        const float* ap = th + (lane >> 4) * KTQ + ks * 16 + (lane & 15);
-        const float* bp = dt + (lane >> 4) * LDD + cst * 16 + (lane & 15);
         f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (BF) {       // A[k][b] = theta_d column, B[b][c] = dt column: 4 rows b each
+          const float* ap = th + 4 * (lane >> 4) * KTQ + ks * 16 + (lane & 15);
+          const float* bp = dt + 4 * (lane >> 4) * LDD + cst * 16 + (lane & 15);
 #pragma unroll
-        for (int b0 = 0; b0 < BM; b0 += 8) {
-          a0 = mfma16x16x4(ap[b0 * KTQ], bp[b0 * LDD], a0);
-          a1 = mfma16x16x4(ap[(b0 + 4) * KTQ], bp[(b0 + 4) * LDD], a1);
+          for (int b0 = 0; b0 < BM; b0 += 16) {
+            float a[4], b[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { a[q] = ap[(b0 + q) * KTQ]; b[q] = bp[(b0 + q) * LDD]; }
+            a0 = mfma16x16x16bf(a, b, a0);
+          }
+        } else {
+          const float* ap = th + (lane >> 4) * KTQ + ks * 16 + (lane & 15);
+          const float* bp = dt + (lane >> 4) * LDD + cst * 16 + (lane & 15);
+#pragma unroll
+          for (int b0 = 0; b0 < BM; b0 += 8) {
+            a0 = mfma16x16x4(ap[b0 * KTQ], bp[b0 * LDD], a0);
+            a1 = mfma16x16x4(ap[(b0 + 4) * KTQ], bp[(b0 + 4) * LDD], a1);
+          }
         }
         const int cl = cst * 16 + (lane & 15);
 #pragma unroll
@@ -626,7 +675,7 @@ prodlda_bwd_kernel(GfkModel m) {
 }
 
 extern "C" size_t gfk_prodlda_fwd_smem(const GfkModel* m) {
-  const size_t KP = round_up(m->K, 4);
+  const size_t KP = round_up(m->K, m->mm_bf16 ? 16 : 4);
   return sizeof(float) * ((size_t)m->bmax * m->kt + KP * LDB_F + 8 * VB);
 }
 
@@ -648,25 +697,35 @@ extern "C" size_t gfk_prodlda_bwd_smem(const GfkModel* m) { return bwd_smem(m, b
 extern "C" int gfk_launch_prodlda_fwd(const GfkModel* m, hipStream_t s) {
   const size_t sm = gfk_prodlda_fwd_smem(m);
   dim3 g(m->dec_grid), blk(DEC_THREADS);
+#define GFK_FWD(BM)                                                                  \
+  if (m->mm_bf16) hipLaunchKernelGGL((prodlda_fwd_kernel<BM, true>), g, blk, sm, s, *m);   \
+  else hipLaunchKernelGGL((prodlda_fwd_kernel<BM, false>), g, blk, sm, s, *m)
   switch (m->bmax) {
-    case 16: hipLaunchKernelGGL(prodlda_fwd_kernel<16>, g, blk, sm, s, *m); break;
-    case 32: hipLaunchKernelGGL(prodlda_fwd_kernel<32>, g, blk, sm, s, *m); break;
-    case 64: hipLaunchKernelGGL(prodlda_fwd_kernel<64>, g, blk, sm, s, *m); break;
-    case 128: hipLaunchKernelGGL(prodlda_fwd_kernel<128>, g, blk, sm, s, *m); break;
+    case 16: GFK_FWD(16); break;
+    case 32: GFK_FWD(32); break;
+    case 64: GFK_FWD(64); break;
+    case 128: GFK_FWD(128); break;
     default: return -1;
   }
+#undef GFK_FWD
   return (int)hipGetLastError();
+}
+
+template <int MAXU, int KQ, bool BF>
+static void launch_bwd_b(const GfkModel* m, dim3 g, size_t sm, hipStream_t s) {
+  const dim3 blk(KQ == 1 ? DEC_THREADS : 512);
+  switch (m->bmax) {
+    case 16: hipLaunchKernelGGL((prodlda_bwd_kernel<16, MAXU, KQ, BF>), g, blk, sm, s, *m); break;
+    case 32: hipLaunchKernelGGL((prodlda_bwd_kernel<32, MAXU, KQ, BF>), g, blk, sm, s, *m); break;
+    case 64: hipLaunchKernelGGL((prodlda_bwd_kernel<64, MAXU, KQ, BF>), g, blk, sm, s, *m); break;
+    default: hipLaunchKernelGGL((prodlda_bwd_kernel<128, MAXU, KQ, BF>), g, blk, sm, s, *m); break;
+  }
 }
 
 template <int MAXU, int KQ>
 static void launch_bwd_t(const GfkModel* m, dim3 g, size_t sm, hipStream_t s) {
-  const dim3 blk(KQ == 1 ? DEC_THREADS : 512);
-  switch (m->bmax) {
-    case 16: hipLaunchKernelGGL((prodlda_bwd_kernel<16, MAXU, KQ>), g, blk, sm, s, *m); break;
-    case 32: hipLaunchKernelGGL((prodlda_bwd_kernel<32, MAXU, KQ>), g, blk, sm, s, *m); break;
-    case 64: hipLaunchKernelGGL((prodlda_bwd_kernel<64, MAXU, KQ>), g, blk, sm, s, *m); break;
-    default: hipLaunchKernelGGL((prodlda_bwd_kernel<128, MAXU, KQ>), g, blk, sm, s, *m); break;
-  }
+  if (m->mm_bf16) launch_bwd_b<MAXU, KQ, true>(m, g, sm, s);
+  else launch_bwd_b<MAXU, KQ, false>(m, g, sm, s);
 }
 
 template <int MAXU>
@@ -700,14 +759,19 @@ extern "C" int gfk_prodlda_set_smem(size_t bytes) {
   static size_t cur = 0;
   if (bytes <= cur) return 0;
   cur = bytes;
-  const void* ks[] = {(const void*)prodlda_fwd_kernel<16>, (const void*)prodlda_fwd_kernel<32>,
-                      (const void*)prodlda_fwd_kernel<64>, (const void*)prodlda_fwd_kernel<128>,
-#define GFK_BWD_PTRS1(U, T) (const void*)prodlda_bwd_kernel<16, U, T>, (const void*)prodlda_bwd_kernel<32, U, T>, \
-    (const void*)prodlda_bwd_kernel<64, U, T>, (const void*)prodlda_bwd_kernel<128, U, T>
+  const void* ks[] = {(const void*)prodlda_fwd_kernel<16, false>, (const void*)prodlda_fwd_kernel<32, false>,
+                      (const void*)prodlda_fwd_kernel<64, false>, (const void*)prodlda_fwd_kernel<128, false>,
+                      (const void*)prodlda_fwd_kernel<16, true>, (const void*)prodlda_fwd_kernel<32, true>,
+                      (const void*)prodlda_fwd_kernel<64, true>, (const void*)prodlda_fwd_kernel<128, true>,
+#define GFK_BWD_PTRS2(U, T, F) (const void*)prodlda_bwd_kernel<16, U, T, F>, \
+    (const void*)prodlda_bwd_kernel<32, U, T, F>, (const void*)prodlda_bwd_kernel<64, U, T, F>, \
+    (const void*)prodlda_bwd_kernel<128, U, T, F>
+#define GFK_BWD_PTRS1(U, T) GFK_BWD_PTRS2(U, T, false), GFK_BWD_PTRS2(U, T, true)
 #define GFK_BWD_PTRS(U) GFK_BWD_PTRS1(U, 1), GFK_BWD_PTRS1(U, 4)
                       GFK_BWD_PTRS(1), GFK_BWD_PTRS(2), GFK_BWD_PTRS(3), GFK_BWD_PTRS(4)};
 #undef GFK_BWD_PTRS
 #undef GFK_BWD_PTRS1
+#undef GFK_BWD_PTRS2
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return (int)e;

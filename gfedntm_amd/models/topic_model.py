@@ -98,7 +98,7 @@ class TopicModelBase:
                  num_data_loader_workers: int = 0, verbose: bool = True,
                  backend: str = "auto", device=None, shared_keys=None, seed: Optional[int] = None,
                  loss_weights: Optional[Dict[str, float]] = None, compat_double_softmax=True,
-                 **extra):
+                 matmul_dtype: str = "fp32", **extra):
         if not (isinstance(input_size, (int, np.integer)) and input_size > 0):
             raise ValueError("input_size must be int > 0")
         if not (isinstance(n_components, (int, np.integer)) and n_components > 0):
@@ -130,6 +130,11 @@ class TopicModelBase:
         self.topic_prior_mean, self.topic_prior_variance = topic_prior_mean, topic_prior_variance
         self.num_samples, self.num_data_loader_workers = num_samples, num_data_loader_workers
         self.verbose = verbose
+        if matmul_dtype not in ("fp32", "bf16"):
+            raise ValueError("matmul_dtype must be 'fp32' or 'bf16'")
+        # "bf16": the ProdLDA decoder GEMMs take bf16 operands on the matrix cores (fp32
+        # accumulation, fp32 parameters / Adam state / everything else) -- fused engine only
+        self.matmul_dtype = matmul_dtype
         self.weights = loss_weights or {"beta": 1}
         self.compat_double_softmax = compat_double_softmax
         self.best_loss_train = float("inf")
@@ -144,6 +149,8 @@ class TopicModelBase:
             torch.manual_seed(seed)
         self.model = self._build_network(**extra).to(self.device)
         self.backend = self._choose_backend(backend)
+        if self.matmul_dtype == "bf16" and self.backend != "fused":
+            raise ValueError("matmul_dtype='bf16' runs on the fused HIP engine only")
         self.shared_keys = list(shared_keys) if shared_keys is not None else \
             list(self.model.state_dict().keys())
         self._build_engine()
@@ -375,7 +382,8 @@ class TopicModelBase:
         keys = ["input_size", "n_components", "model_type", "hidden_sizes", "activation",
                 "dropout", "learn_priors", "batch_size", "lr", "momentum", "solver",
                 "num_epochs", "reduce_on_plateau", "topic_prior_mean", "topic_prior_variance",
-                "num_samples", "nn_epoch", "best_loss_train"]
+                "num_samples", "nn_epoch", "best_loss_train",
+                "matmul_dtype"]
         return {k: getattr(self, k) for k in keys}
 
     def save(self, models_dir=None):

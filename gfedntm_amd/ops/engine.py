@@ -31,6 +31,7 @@ collective is one contiguous all-reduce of ``flat.shared``.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Dict, List, Optional, Tuple
 
 import numpy as np
@@ -72,6 +73,8 @@ def supports(tm, explain: bool = False) -> bool:
         (max(tm.hidden_sizes) <= 512 and len(tm.hidden_sizes) <= abi.MAX_LAYERS,
          "hidden layers too wide / too many"),
         (getattr(tm, "label_size", 0) == 0, "CTM labels not fused"),
+        (getattr(tm, "matmul_dtype", "fp32") == "fp32" or tm.model_type.lower() == "prodlda",
+         "bf16 decoder GEMMs are ProdLDA only"),
     ]
     # reduce_on_plateau needs nothing here: the reference builds ReduceLROnPlateau
     # (avitm.py:156-157) but never calls scheduler.step(), so the lr never changes
@@ -101,6 +104,7 @@ def _shape_model(tm, bmax: int) -> "abi.GfkModel":
     for i, h in enumerate(hs):
         m.H[i] = h
     m.kind = abi.KIND_PRODLDA if tm.model_type.lower() == "prodlda" else abi.KIND_LDA
+    m.mm_bf16 = int(getattr(tm, "matmul_dtype", "fp32") == "bf16")
     m.kt = theta_stride(m.K)
     m.vb, m.n_tiles = VB, -(-m.V // VB)
     m.n_dpart = m.n_tiles if m.kind == abi.KIND_PRODLDA else 1
@@ -116,6 +120,7 @@ def lds_required(tm, bmax: int) -> int:
     for i, h in enumerate(hs):
         m.H[i] = h
     m.kind = abi.KIND_PRODLDA if tm.model_type.lower() == "prodlda" else abi.KIND_LDA
+    m.mm_bf16 = int(getattr(tm, "matmul_dtype", "fp32") == "bf16")
     m.kt = theta_stride(m.K)
     m.vb, m.n_tiles = VB, -(-m.V // VB)
     m.n_dpart = m.n_tiles if m.kind == abi.KIND_PRODLDA else 1
@@ -322,6 +327,7 @@ class FusedEngine(EngineBase):
         for i, h in enumerate(hs):
             m.H[i] = h
         m.act = abi.ACT_CODES[tm.activation]
+        m.mm_bf16 = int(getattr(tm, "matmul_dtype", "fp32") == "bf16")
         m.kind = abi.KIND_PRODLDA if model.is_prodlda else abi.KIND_LDA
         if self.kind == "ctm":
             m.input = abi.IN_COMBINED if tm.inference_type == "combined" else abi.IN_CONTEXTUAL
@@ -415,6 +421,14 @@ class FusedEngine(EngineBase):
                     m.n_dpart = cu // 4
             else:
                 m.n_dpart = cu
+            # GFEDNTM_BETA_SPLIT=1: beta's Adam as one streaming float4 pass after
+            # prodlda_bwd (which then only writes the gradient) instead of the epilogue.
+            # The pass alone runs at 5.7-6.7 TB/s vs 4.2 for the epilogue's layout
+            # (profiles/r2/adam_rmw_bandwidth.jsonl), but the round is slower (K=200,
+            # V=112k: 0.446 vs 0.406 ms): prodlda_bwd's own staging / MFMA time does not
+            # shrink without the Adam work, so the extra pass is added, not overlapped
+            m.beta_split = int(os.environ.get("GFEDNTM_BETA_SPLIT", "0") == "1"
+                               and self.update_mode == UPDATE_FUSED)
         self._alloc_workspace()
         rc = self.lib.gfk_setup(C.byref(m))
         if rc:
@@ -536,7 +550,7 @@ class FusedEngine(EngineBase):
         m.fed_scale_on = int(self.fedavg_scale is not None)
         m.fed_scale = 1.0 if self.fedavg_scale is None else float(self.fedavg_scale)
 
-    def _fill_adam(self, a, keys=None):
+    def _fill_adam(self, a, keys=None, keep_grad: bool = False):
         """Segment table of a GfkAdam: [start, end) float ranges of parameters (all,
         or the slots of ``keys``) with ADAM, plus SCALE on the shared prefix.
         Batch-norm running statistics are scaled by the kernels that update them.
@@ -562,7 +576,8 @@ class FusedEngine(EngineBase):
         for x0, x1 in zip(cuts[:-1], cuts[1:]):
             if x1 <= x0 or not any(s0 <= x0 and x1 <= s1 for s0, s1 in pr):
                 continue
-            flags = abi.SEG_ADAM | (abi.SEG_SCALE if x1 <= shared_end else 0)
+            flags = abi.SEG_ADAM | (abi.SEG_SCALE if x1 <= shared_end else 0) | \
+                (abi.SEG_KEEP_GRAD if keep_grad else 0)
             if segs and segs[-1][1] == x0 and segs[-1][2] == flags:
                 segs[-1][1] = x1
             else:
@@ -580,7 +595,21 @@ class FusedEngine(EngineBase):
     def _rebuild_adam(self):
         self._sync_opt_fields()
         self.adam_grid = int(max(1, self._fill_adam(self._a)))
+        self._a_beta = abi.GfkAdam()
+        self.beta_adam_grid = int(max(1, self._fill_adam(self._a_beta, keys=["beta"],
+                                                         keep_grad=True)))
         self._invalidate_graph()
+
+    @property
+    def beta_split(self) -> bool:
+        """Beta's update runs as a separate streaming optimizer pass (large V)."""
+        return bool(self._m.beta_split) and self.update_mode == UPDATE_FUSED
+
+    def _beta_adam(self):
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        rc = self.lib.gfk_launch_adam(C.byref(self._a_beta), self.beta_adam_grid, stream)
+        if rc:
+            raise RuntimeError(f"gfk_launch_adam failed ({rc})")
 
     def set_fedavg_scale(self, w: Optional[float]):
         """Pre-scale the shared state by w after the update (None disables)."""
@@ -633,6 +662,8 @@ class FusedEngine(EngineBase):
                 ([abi.PH_ADAM] if self.update_mode == UPDATE_GRAD else [])
         else:
             ph = abi.PRODLDA_STEP + ([abi.PH_ADAM] if self.update_mode == UPDATE_GRAD else [])
+            if self.beta_split:
+                ph.insert(ph.index(abi.PH_PRODLDA_BWD) + 1, abi.PH_BETA_ADAM)
         if self.ctx_fused:
             if self._m.ctx_fused == 1:
                 ph.insert(ph.index(abi.PH_ENC_FWD), abi.PH_CTXF_FWD)
@@ -643,6 +674,8 @@ class FusedEngine(EngineBase):
         if self._comm is not None and self._comm["mode"] == "graph":
             if "beta" in self._comm:
                 last = abi.PH_PRODLDA_BWD if abi.PH_PRODLDA_BWD in ph else abi.PH_LDA_BETA_BWD
+                if abi.PH_BETA_ADAM in ph:
+                    last = abi.PH_BETA_ADAM
                 ph.insert(ph.index(last) + 1, abi.PH_FEDAVG_BETA)
             ph.append(abi.PH_FEDAVG_END)
         return ph
@@ -858,6 +891,8 @@ class FusedEngine(EngineBase):
                         self._ctx_fwd()
                     elif p == abi.PH_CTX_BWD:
                         self._ctx_bwd()
+                    elif p == abi.PH_BETA_ADAM:
+                        self._beta_adam()
                     elif p == abi.PH_FEDAVG_BETA:
                         self._fedavg_beta()
                     elif p == abi.PH_FEDAVG_END:

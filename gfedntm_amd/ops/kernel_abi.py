@@ -47,14 +47,17 @@ PH_CTX_BWD = 101
 # overlapping the encoder backward) and of the rest of the shared state
 PH_FEDAVG_BETA = 102
 PH_FEDAVG_END = 103
-HOST_PHASES = (PH_CTX_FWD, PH_CTX_BWD, PH_FEDAVG_BETA, PH_FEDAVG_END)
+# large-vocabulary ProdLDA (beta_split): prodlda_bwd leaves beta's gradient in the grad
+# slot and the generic float4 optimizer kernel updates beta (one streaming pass)
+PH_BETA_ADAM = 104
+HOST_PHASES = (PH_CTX_FWD, PH_CTX_BWD, PH_FEDAVG_BETA, PH_FEDAVG_END, PH_BETA_ADAM)
 
 PRODLDA_STEP = [PH_ENC_FWD, PH_POST_FWD, PH_PRODLDA_FWD, PH_PRODLDA_LOSS, PH_PRODLDA_BWD,
                 PH_POST_BWD, PH_ENC_BWD]
 LDA_STEP = [PH_LDA_BETA_FWD, PH_ENC_FWD, PH_POST_FWD, PH_LDA_ROW, PH_POST_BWD, PH_LDA_BETA_BWD,
             PH_ENC_BWD, PH_ADAM]
 
-SEG_ADAM, SEG_SCALE = 1, 2
+SEG_ADAM, SEG_SCALE, SEG_KEEP_GRAD = 1, 2, 4
 
 
 class GfkModel(C.Structure):
@@ -66,7 +69,7 @@ class GfkModel(C.Structure):
         ("learn_priors", C.c_int32), ("stage_flags", C.c_int32), ("kt", C.c_int32),
         ("scatter_chunks", C.c_int32), ("n_dpart", C.c_int32), ("n_steps", C.c_int32),
         ("drop_enc", C.c_float), ("drop_theta", C.c_float), ("bn_momentum", C.c_float),
-        ("bn_eps", C.c_float), ("kl_weight", C.c_float), ("pad1", C.c_float),
+        ("bn_eps", C.c_float), ("kl_weight", C.c_float), ("beta_split", C.c_int32),
         ("seed", C.c_uint64),
         ("prior_mean", P), ("prior_var", P), ("beta", P), ("w_in", P), ("b_in", P),
         ("w_h", P * MAX_LAYERS), ("b_h", P * MAX_LAYERS),
@@ -96,6 +99,7 @@ class GfkModel(C.Structure):
         ("w_a", P), ("b_a", P), ("ws_actx", P), ("ws_hpart", P),
         ("ctx_fused", C.c_int32), ("ctx_kb", C.c_int32), ("ctx_ckb", C.c_int32),
         ("slot_cap", C.c_int32), ("ws_sidx", P), ("ws_sval", P),
+        ("mm_bf16", C.c_int32), ("pad2", C.c_int32),
     ]
 
 
@@ -171,6 +175,8 @@ def declare(lib: C.CDLL) -> None:
     lib.gfk_smem_required.restype = C.c_size_t
     lib.gfk_scale.argtypes = [C.c_void_p, C.c_int64, C.c_float, C.c_void_p]
     lib.gfk_scale.restype = C.c_int
+    lib.gfk_launch_adam.argtypes = [C.POINTER(GfkAdam), C.c_int, C.c_void_p]
+    lib.gfk_launch_adam.restype = C.c_int
     lib.gfk_infer_struct_size.restype = C.c_size_t
     if lib.gfk_infer_struct_size() != C.sizeof(GfkInfer):
         raise RuntimeError("GfkInfer ABI mismatch")

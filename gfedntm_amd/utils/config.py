@@ -204,5 +204,5 @@ def model_kwargs_from_params(params: Dict[str, Any]) -> Dict[str, Any]:
     keys = ["n_components", "model_type", "hidden_sizes", "activation", "dropout",
             "learn_priors", "batch_size", "lr", "momentum", "solver", "num_epochs",
             "reduce_on_plateau", "topic_prior_mean", "topic_prior_variance",
-            "num_samples", "num_data_loader_workers", "verbose"]
+            "num_samples", "num_data_loader_workers", "verbose", "matmul_dtype"]
     return {k: params[k] for k in keys if k in params}

@@ -21,11 +21,12 @@ from tests.helpers import random_csr
 pytestmark = pytest.mark.gpu
 
 
-def _pair(model_type="prodLDA", V=700, K=20, H=(32, 24), B=64, activation="softplus", seed=0):
+def _pair(model_type="prodLDA", V=700, K=20, H=(32, 24), B=64, activation="softplus", seed=0,
+          **fused_kw):
     torch.manual_seed(seed)
     kw = dict(input_size=V, n_components=K, model_type=model_type, hidden_sizes=H,
               batch_size=B, activation=activation, verbose=False, device="cuda")
-    fused = AVITM(backend="fused", **kw)
+    fused = AVITM(backend="fused", **kw, **fused_kw)
     fused.engine.set_update_mode(UPDATE_GRAD)       # gradients materialised for the oracle
     ref = AVITM(backend="torch", **kw)
     ref.model.load_state_dict(fused.model.state_dict())
@@ -194,6 +195,47 @@ def test_graph_replay_matches_eager():
     torch.cuda.synchronize()
     torch.testing.assert_close(a.engine.loss_hist, b.engine.loss_hist, rtol=1e-5, atol=1e-4)
     torch.testing.assert_close(a.flat.buffer, b.flat.buffer, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("V,K", [(900, 50), (40000, 200), (40000, 20)])
+def test_beta_split_update_matches_fused(V, K, monkeypatch):
+    """Large-vocabulary beta update (prodlda_bwd writes the gradient, one streaming
+    optimizer pass applies it, GFEDNTM_BETA_SPLIT) vs Adam fused into prodlda_bwd: same
+    parameters, moments and losses, with the FedAvg pre-scale, over graph replays."""
+    tms = []
+    for split in ("0", "1"):
+        monkeypatch.setenv("GFEDNTM_BETA_SPLIT", split)
+        torch.manual_seed(0)
+        tms.append(AVITM(input_size=V, n_components=K, hidden_sizes=(50, 50), batch_size=64,
+                         verbose=False, device="cuda", backend="fused"))
+    a, b = tms
+    b.model.load_state_dict(a.model.state_dict())
+    b.engine.seed = b.engine._m.seed = a.engine.seed
+    assert not a.engine.beta_split and b.engine.beta_split
+    assert abi.PH_BETA_ADAM in b.engine.phases()
+    X = random_csr(200, V, 60, seed=2)
+    for tm in (a, b):
+        tm.engine.set_fedavg_scale(0.75)
+        _bind(tm, X, n_steps=6)
+        tm.engine.enable_graph(True)
+        for s in range(6):
+            tm.engine.step(s)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(a.engine.loss_hist, b.engine.loss_hist, rtol=1e-5, atol=1e-2)
+    # the same Adam arithmetic inlined into two kernels may differ by an ulp (FP
+    # contraction); tensors whose true gradient is 0 (rounding noise, _NOISE_KEYS) then
+    # drift by up to lr per step after Adam's normalisation
+    sa, sb = a.model.state_dict(), b.model.state_dict()
+    lr_steps = 2 * a.engine.lr * 6
+    for k in sb:
+        if not sb[k].is_floating_point():
+            assert torch.equal(sa[k], sb[k]), k
+            continue
+        noisy = k in _NOISE_KEYS or "batchnorm.running_mean" in k
+        torch.testing.assert_close(sa[k], sb[k], rtol=1e-4, atol=lr_steps if noisy else 1e-5,
+                                   msg=lambda m: f"{k}: {m}")
+    fa, fb = a.engine.view_like(a.engine.exp_avg, "beta"), b.engine.view_like(b.engine.exp_avg, "beta")
+    torch.testing.assert_close(fa, fb, rtol=1e-4, atol=1e-5)
 
 
 @pytest.mark.parametrize("model_type", ["prodLDA", "LDA"])
@@ -421,3 +463,73 @@ def test_fedavg_prescale_covers_every_shared_tensor(model_type, mode):
         if k in sb and sb[k].is_floating_point():
             torch.testing.assert_close(sa[k], 0.25 * sb[k], rtol=1e-5, atol=1e-7,
                                        msg=lambda m: f"{k}: {m}")
+
+
+def _bf(x):
+    return x.to(torch.bfloat16).float()
+
+
+@pytest.mark.parametrize("K,V", [(50, 2000), (200, 40000)])
+def test_bf16_decoder_matches_emulated_oracle(K, V):
+    """matmul_dtype='bf16': theta_d.beta, theta_d^T.dlogit and dlogit.beta^T take bf16
+    operands on the matrix cores with fp32 accumulation.  Oracle: the fp32 PyTorch step
+    with theta_d and beta rounded to bf16 before the logits GEMM (the backward GEMMs'
+    extra rounding of dlogit is inside the gradient tolerance)."""
+    from gfedntm_amd.models.functional import encoder_forward
+    from gfedntm_amd.models.networks import kl_terms, reconstruction_terms
+    import torch.nn.functional as F
+    fused, ref = _pair("prodLDA", V=V, K=K, H=(50, 50), B=64, matmul_dtype="bf16")
+    assert fused.engine._m.mm_bf16 == 1
+    X = random_csr(150, V, 60, seed=1)
+    data, plan = _bind(fused, X, B=64)
+    e = fused.engine
+    e.run_phases(e.phases()[:-1])
+    torch.cuda.synchronize()
+    nb = int(plan.size[0])
+    ids = torch.from_numpy(plan.batch(0).astype(np.int64)).cuda()
+    x = data.dense_rows(ids)
+    model = ref.model
+    model.train()
+    model.zero_grad()
+    mu, ls = encoder_forward(model.inf_net, x, e.ws["mask_h"][:nb])
+    theta = F.softmax(mu + e.ws["eps"][:nb] * torch.exp(0.5 * ls), dim=1)
+    thetad = theta * e.ws["mask_t"][:nb]
+    bf_round = lambda t: t + (_bf(t) - t).detach()      # noqa: E731  rounded forward, identity grad
+    bb = model.beta_batchnorm
+    logits = F.batch_norm(bf_round(thetad) @ bf_round(model.beta), bb.running_mean,
+                          bb.running_var, training=True, momentum=bb.momentum, eps=bb.eps)
+    wd = F.softmax(logits, dim=1)
+    kl = kl_terms(model.prior_mean, model.prior_variance, mu, torch.exp(ls), ls, K)
+    rl = reconstruction_terms(x, wd)
+    loss = (kl + rl).sum()
+    loss.backward()
+    torch.testing.assert_close(e.ws["rl"][:nb], rl.detach(), rtol=2e-4, atol=5e-2)
+    torch.testing.assert_close(e.loss_hist[0], loss.detach(), rtol=2e-4, atol=5e-2)
+    g = _grads_of(fused)
+    for k, p in model.named_parameters():
+        if k in _NOISE_KEYS:
+            continue
+        scale = p.grad.abs().max().item() + 1e-6
+        torch.testing.assert_close(g[k], p.grad, rtol=3e-2, atol=2e-2 * scale,
+                                   msg=lambda m: f"{k}: {m}")
+
+
+def test_bf16_training_tracks_fp32():
+    """300 graph-replayed steps: the bf16-GEMM decoder's loss curve stays within 1 % of
+    the fp32 one (same init, same data, same noise)."""
+    curves = []
+    X = random_csr(1000, 3000, 80, seed=4)
+    for dt in ("fp32", "bf16"):
+        torch.manual_seed(0)
+        tm = AVITM(input_size=3000, n_components=50, hidden_sizes=(50, 50), batch_size=64,
+                   verbose=False, device="cuda", backend="fused", matmul_dtype=dt)
+        tm.engine.seed = tm.engine._m.seed = 1234
+        _bind(tm, X, n_steps=300)
+        tm.engine.enable_graph(True)
+        for s in range(300):
+            tm.engine.step(s)
+        torch.cuda.synchronize()
+        curves.append(tm.engine.loss_hist[:300].cpu().numpy())
+    a, b = (c[-50:].mean() for c in curves)
+    assert np.isfinite(curves[1]).all()
+    assert abs(a - b) / a < 0.01, (a, b)
