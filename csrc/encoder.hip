@@ -123,9 +123,10 @@ __host__ __device__ inline int enc_hmax(const GfkModel& m) {
   return h;
 }
 
-// dynamic LDS: red[16][H0] + act[2][hmax] + mask[Hl] (+ staged weights)
+// dynamic LDS: red[16][H0] + act[2][hmax] + mask[Hl] + labels[L] (+ staged weights)
 extern "C" size_t gfk_enc_in_smem(const GfkModel* m) {
-  size_t n = (size_t)ENC_WAVES * m->H[0] + 2 * (size_t)pad4(enc_hmax(*m)) + pad4(m->H[m->n_hidden - 1]);
+  size_t n = (size_t)ENC_WAVES * m->H[0] + 2 * (size_t)pad4(enc_hmax(*m)) + pad4(m->H[m->n_hidden - 1]) +
+             (m->lab_on ? pad4(m->L) : 0);
   if (m->stage_flags & 1) n += enc_weight_floats(*m);
   return sizeof(float) * n;
 }
@@ -172,7 +173,8 @@ __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkModel m) {
   float* act0 = red + ENC_WAVES * H0;
   float* act1 = act0 + pad4(hm);
   float* maskh = act1 + pad4(hm);
-  float* wst = maskh + pad4(Hl);
+  float* labs = maskh + pad4(Hl);         // the row's labels (label head)
+  float* wst = labs + (m.lab_on ? pad4(m.L) : 0);
   constexpr bool staged = Staged;
 
   GFK_STAMP(m, 4);
@@ -206,10 +208,16 @@ __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkModel m) {
   const int gv = sidx[gj];
   const float gx = sval[gj];
   const int tv = sidx[tj], tvp = sidx[max(tj - 1, 0)];
+  const int L = m.L;
+  const float labv = m.lab_on ? m.labels[(size_t)doc * L + min(tid, L - 1)] : 0.f;
   __shared__ int last_tile;
   if (b >= nb) {            // drain the LDS-DMA before the workgroup retires
     vm_barrier();
     return;
+  }
+  if (m.lab_on && tid < L) {                 // the batch's label rows (classifier, W_in grads)
+    labs[tid] = labv;
+    m.ws_lab[(size_t)b * L + tid] = labv;
   }
   if (tid == 0) {           // publish the batch for the rest of the step
     m.ws_doc[b] = doc;
@@ -315,6 +323,10 @@ __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkModel m) {
       for (int w = 0; w < ENC_WAVES; ++w) z += red[w * H0 + tid];
     }
     if (input != GFK_IN_BOW && !m.ctx_fused) z += m.ws_hctx[(size_t)b * H0 + tid];
+    if (m.lab_on && m.lab_in_enc) {          // the label block of the input layer
+      const float* wl = w_in + (size_t)m.lab_off * H0 + tid;
+      for (int l = 0; l < L; ++l) z += labs[l] * wl[(size_t)l * H0];
+    }
     float zs;
     float a = act_train(act, z, m.seed, (uint32_t)step, 0, (uint32_t)(b * H0 + tid), &zs);
     m.ws_z[0][(size_t)b * H0 + tid] = zs;

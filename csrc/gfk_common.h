@@ -140,6 +140,21 @@ typedef struct GfkModel {
   // every other op stay fp32
   int32_t mm_bf16;
   int32_t pad2;
+
+  // ---- CTM label head (reference ctm decoding_network.py:84-85,156-159, ctm.py:292-296,
+  // inference_network.py:64,162): the labels widen the encoder input (rows lab_off ..
+  // lab_off + L of the transposed input layer) and feed a Linear(K -> L) classifier on
+  // theta_d whose mean cross-entropy against argmax(labels) joins the loss ----
+  int32_t lab_on;                // label head active (L > 0)
+  int32_t lab_off;               // first input-layer row of the label block
+  const float* labels;           // [D, L] the bound dataset's labels
+  float *w_cls, *b_cls;          // label_classification weight [L, K], bias [L]
+  float *ws_lab;                 // [bmax, L] the batch's label rows (enc_in)
+  float *ws_dlab;                // [bmax, L] d CE / d logits, mean over the batch (post_fwd)
+  float *ws_ce;                  // [bmax] the rows' CE terms / nb (post_fwd)
+  float *ws_thd;                 // [bmax, K] compact theta_d (the classifier's weight-gradient input)
+  int32_t lab_in_enc;            // enc_in adds the label rows (0: the host hctx carries them)
+  int32_t pad3;
 } GfkModel;
 
 // Gradient + update jobs of the small tensors, run by the update kernel next to
@@ -160,7 +175,7 @@ typedef struct GfkVJob {
   int32_t n, pad;
 } GfkVJob;
 
-#define GFK_MAX_WJOBS 24
+#define GFK_MAX_WJOBS 40
 #define GFK_MAX_VJOBS 16
 typedef struct GfkUpdate {
   int32_t n_w, n_v;

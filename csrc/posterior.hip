@@ -192,6 +192,76 @@ __device__ __forceinline__ void post_colstats_dpp(const GfkModel& m, const float
   }
 }
 
+// CTM label head of the own row (reference ctm decoding_network.py:156-159, ctm.py:292-296):
+// est = W_cls theta_d + b_cls, CE(est, argmax(labels)) averaged over the batch.  Writes
+// the row's CE / nb (joins the loss in post_bwd), d CE / d est (the classifier's
+// weight-gradient jobs in win_update) and d CE / d theta_d = W_cls^T d est as one more
+// d theta_d slab (index n_dpart), which row_bwd sums with the decoder's.
+// buf: LDS, theta_d of the row in [0, K) (written by wave 0 before the call).
+__device__ __forceinline__ void post_label_head(const GfkModel& m, float* buf, int row, int nb,
+                                                int tid) {
+  const int K = m.K, L = m.L, lane = tid & 63, wave = tid >> 6;
+  float* est = buf + 256;
+  float* dl = buf + 512;
+  lds_barrier();
+  // est[l] = b_cls[l] + sum_k theta_d[k] W_cls[l][k]: 16 lanes per output
+  for (int l0 = 0; l0 < L; l0 += FT / 16) {
+    const int l = l0 + (tid >> 4), s = tid & 15;
+    float acc = 0.f;
+    if (l < L) {
+      const float* w = m.w_cls + (size_t)l * K;
+      for (int k = s; k < K; k += 16) acc += buf[k] * w[k];
+    }
+    acc = row16_sum(acc);
+    if (s == 0 && l < L) est[l] = acc + m.b_cls[l];
+  }
+  lds_barrier();
+  if (wave == 0) {
+    constexpr int LQ = 4;                    // L <= 256
+    const float* lab = m.ws_lab + (size_t)row * L;
+    float e[LQ], mx = -INFINITY, best = -INFINITY;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int q = 0; q < LQ; ++q) {
+      const int l = lane + 64 * q;
+      e[q] = l < L ? est[l] : -INFINITY;
+      mx = fmaxf(mx, e[q]);
+      const float lv = l < L ? lab[l] : -INFINITY;
+      if (lv > best) { best = lv; bi = l; }   // first maximum, like torch.argmax
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float b2 = __shfl_xor(best, o, 64);
+      const int i2 = __shfl_xor(bi, o, 64);
+      if (b2 > best || (b2 == best && i2 < bi)) { best = b2; bi = i2; }
+    }
+    mx = wave_max(mx);
+    float se = 0.f;
+#pragma unroll
+    for (int q = 0; q < LQ; ++q) se += lane + 64 * q < L ? __expf(e[q] - mx) : 0.f;
+    const float lse = mx + logf(wave_sum(se));
+    const float inv_nb = 1.f / (float)nb;
+#pragma unroll
+    for (int q = 0; q < LQ; ++q) {
+      const int l = lane + 64 * q;
+      if (l < L) {
+        const float d = (expf(e[q] - lse) - (l == bi ? 1.f : 0.f)) * inv_nb;
+        dl[l] = d;
+        m.ws_dlab[(size_t)row * L + l] = d;
+      }
+    }
+    if (lane == 0) m.ws_ce[row] = (lse - est[bi]) * inv_nb;
+  }
+  lds_barrier();
+  // d theta_d[k] = sum_l dl[l] W_cls[l][k] -> slab n_dpart
+  float* slab = m.ws_dthetad + ((size_t)m.n_dpart * m.bmax + row) * K;
+  for (int k = tid; k < K; k += FT) {
+    float acc = 0.f;
+    for (int l = 0; l < L; ++l) acc += dl[l] * m.w_cls[(size_t)l * K + k];
+    slab[k] = acc;
+  }
+}
+
 // grid: bmax workgroups (row = blockIdx.x).  dynamic LDS: mr[B*K] + lr[B*K] (unless
 // read from L2) + mean[2K] + rstd[2K]
 // InLds: the batch matrices are staged in LDS (compile-time, so every access is a
@@ -348,10 +418,15 @@ __global__ void __launch_bounds__(FT) gfk_post_fwd_k(GfkModel m) {
         m.ws_ls[ix] = lsq[q];
         m.ws_theta[ix] = th;
         m.ws_thetad[row * m.kt + k] = th * mt[q];
+        if (m.lab_on) {
+          red[k] = th * mt[q];
+          m.ws_thd[ix] = th * mt[q];
+        }
       }
     }
     if (lane == 0) m.ws_kl[row] = 0.5f * (kl - (float)K + logpv);
   }
+  if (m.lab_on) post_label_head(m, red, row, nb, tid);
   GFK_STAMP(m, 3);
 }
 
@@ -368,7 +443,7 @@ extern "C" size_t gfk_row_bwd_smem(const GfkModel* m) { return sizeof(float) * 4
 template <int KQ>
 __global__ void __launch_bounds__(PT) gfk_row_bwd_k(GfkModel m) {
   extern __shared__ __attribute__((aligned(16))) float part[];
-  int K = m.K, B = m.bmax, np = m.n_dpart;
+  int K = m.K, B = m.bmax, np = m.n_dpart + (m.lab_on ? 1 : 0);   // + the label head's slab
   const float* dpart = m.ws_dthetad;
   const int32_t* nbp = m.ws_nb;
   keep(K, B, np, dpart, nbp);
@@ -642,7 +717,7 @@ __global__ void __launch_bounds__(FT) gfk_post_bwd_k(GfkModel m) {
   float lterm = 0.f, pmk = 0.f, pvk = 1.f;
   int step0 = 0;
   if (extra) {
-    if (tid < nb) lterm = m.kl_weight * m.ws_kl[tid] + m.ws_rl[tid];
+    if (tid < nb) lterm = m.kl_weight * m.ws_kl[tid] + m.ws_rl[tid] + (m.lab_on ? m.ws_ce[tid] : 0.f);
     if (tid < K) { pmk = m.prior_mean[tid]; pvk = m.prior_var[tid]; }
     if (tid == 0) step0 = *m.step;
   }

@@ -72,7 +72,7 @@ def supports(tm, explain: bool = False) -> bool:
         (tm.n_components <= 256, "n_components > 256"),
         (max(tm.hidden_sizes) <= 512 and len(tm.hidden_sizes) <= abi.MAX_LAYERS,
          "hidden layers too wide / too many"),
-        (getattr(tm, "label_size", 0) == 0, "CTM labels not fused"),
+        (getattr(tm, "label_size", 0) <= 256, "label_size > 256"),
         (getattr(tm, "matmul_dtype", "fp32") == "fp32" or tm.model_type.lower() == "prodlda",
          "bf16 decoder GEMMs are ProdLDA only"),
     ]
@@ -334,6 +334,12 @@ class FusedEngine(EngineBase):
             m.C = tm.contextual_size
         else:
             m.input = abi.IN_BOW
+        # CTM label head: the labels are the last L inputs of input_layer (CombinedTM
+        # [BoW | adapted | labels], ZeroShotTM [contextual | labels])
+        m.L = int(getattr(tm, "label_size", 0) or 0)
+        m.lab_on = int(m.L > 0)
+        if m.lab_on:
+            m.lab_off = 2 * tm.input_size if m.input == abi.IN_COMBINED else m.C
         props = torch.cuda.get_device_properties(self.device)
         if self.ctx_fused:
             self._plan_ctx(props.multi_processor_count)
@@ -349,6 +355,11 @@ class FusedEngine(EngineBase):
         m.bn_eps = float(model.beta_batchnorm.eps)
         m.kl_weight = float(self.beta_weight)
         m.seed = self.seed
+        if m.lab_on:
+            P0 = self.flat.buffer
+            m.w_cls = self._ptr(P0, "label_classification.weight")
+            m.b_cls = self._ptr(P0, "label_classification.bias")
+            m.lab_in_enc = int(bool(self.ctx_fused))   # else the host hctx carries the labels
         P, G = self.flat.buffer, self.grad
         if tm.learn_priors:
             m.prior_mean, m.prior_var = self._ptr(P, "prior_mean"), self._ptr(P, "prior_variance")
@@ -480,7 +491,7 @@ class FusedEngine(EngineBase):
             "zn": f(m.n_tiles * B * VB if m.kind == abi.KIND_PRODLDA else V * K),
             "col_rstd": f(m.n_tiles * VB),
             "row_part": f(max(m.n_tiles * 4 * B, m.dec_grid * K) * 2),
-            "dthetad": f(m.n_dpart * B * K),
+            "dthetad": f((m.n_dpart + m.lab_on) * B * K),     # + the label head's slab
             "dmr": f(B, K), "dlr": f(B, K), "dmu": f(B, K), "dls": f(B, K),
             "dbsm": f(1), "ck": f(K),        # LDA: per-non-zero coefficients, sized in bind_data
             "hctx": f(B, hs[0]),
@@ -492,6 +503,8 @@ class FusedEngine(EngineBase):
             "actx": f(m.n_tiles * B * 64 if m.ctx_fused == 1 else 1),
             "hpart": f(m.n_tiles * B * hs[0] if m.ctx_fused == 1 else 1),
         }
+        Lb = max(int(m.L), 1)
+        ws.update(lab=f(B, Lb), dlab=f(B, Lb), ce=f(B), thd=f(B, K))   # label head
         for i, h in enumerate(hs):
             ws[f"z{i}"] = f(B, h)
             ws[f"a{i}"] = f(B, h)
@@ -521,6 +534,13 @@ class FusedEngine(EngineBase):
             wj.append((f"inf_net.hiddens.l_{l}.0.weight", ws[f"dz{l + 1}"], ws[f"a{l}"], hs[l + 1], hs[l]))
         wj.append(("inf_net.f_mu.weight", ws["dmr"], ws["hd"], K, hs[-1]))
         wj.append(("inf_net.f_sigma.weight", ws["dlr"], ws["hd"], K, hs[-1]))
+        L = int(self._m.L)
+        if L:
+            # label head: the classifier [L, K] (d est x theta_d) and the input layer's
+            # label block [L, H0] of the transposed weight (labels x d z0)
+            wj.append(("label_classification.weight", ws["dlab"], ws["thd"], L, K))
+            lab_block = self._ptr(P, "inf_net.input_layer.weight") + 4 * int(self._m.lab_off) * hs[0]
+            wj.append((lab_block, ws["lab"], ws["dz0"], L, hs[0]))
         n = 0
         for key, dz, a, rows, cols in wj:
             for j0 in range(0, rows, 64):
@@ -528,7 +548,8 @@ class FusedEngine(EngineBase):
                     if n >= abi.MAX_WJOBS:
                         raise RuntimeError("too many weight tiles for the fused update")
                     J = u.w[n]
-                    J.param, J.dz, J.a = self._ptr(P, key), dz.data_ptr(), a.data_ptr()
+                    J.param = key if isinstance(key, int) else self._ptr(P, key)
+                    J.dz, J.a = dz.data_ptr(), a.data_ptr()
                     J.rows, J.cols, J.j0, J.i0 = rows, cols, j0, i0
                     n += 1
         u.n_w = n
@@ -538,6 +559,8 @@ class FusedEngine(EngineBase):
         vj += [("inf_net.f_mu.bias", ws["dmr"], K), ("inf_net.f_sigma.bias", ws["dlr"], K)]
         if self.tm.learn_priors:
             vj += [("prior_mean", None, K), ("prior_variance", None, K)]
+        if L:
+            vj.append(("label_classification.bias", ws["dlab"], L))
         for i, (key, src, nn_) in enumerate(vj):
             V = u.v[i]
             V.param, V.src, V.n = self._ptr(P, key), (src.data_ptr() if src is not None else None), nn_
@@ -639,6 +662,11 @@ class FusedEngine(EngineBase):
                 self.ws["dbsm"] = torch.zeros(nnz + 16, dtype=torch.float32, device=dev)
             m.ws_dbsm = self.ws["dbsm"].data_ptr()
         m.ctx = data.contextual.data_ptr() if data.contextual is not None else None
+        if m.lab_on:
+            if data.labels is None or data.labels.shape[1] != m.L:
+                raise ValueError(f"the model has a label head of size {m.L}: bind data with "
+                                 f"labels [n_docs, {m.L}]")
+            m.labels = data.labels.data_ptr()
         # the next batch's rows in fixed slots (prepare_next_batch -> enc_in / row_loss)
         cap = max(16, -(-int(data.row_len_max) // 16) * 16)
         if self.ws.get("sidx") is None or self.ws["sidx"].numel() < self.bmax * cap:
@@ -795,7 +823,10 @@ class FusedEngine(EngineBase):
                      gba=self.view_like(self.grad, "inf_net.adapt_bert.bias"),
                      Wc=w_in[V:2 * V], gWc=g_in[V:2 * V])
         else:
-            c.update(W=w_in, gW=g_in)                                           # [C, H0]
+            c.update(W=w_in[:C], gW=g_in[:C])                                   # [C, H0]
+        if m.lab_on:                 # the label block [L, H0] (its gradient: a win_update job)
+            c.update(Wl=w_in[int(m.lab_off): int(m.lab_off) + int(m.L)],
+                     lb=z(B, int(m.L)))
         self._ctx = c
 
     def raw_like(self, buf: torch.Tensor, key: str) -> torch.Tensor:
@@ -814,6 +845,9 @@ class FusedEngine(EngineBase):
             torch.mm(c["a"], c["Wc"], out=ws["hctx"])
         else:
             torch.mm(c["xc"], c["W"], out=ws["hctx"])
+        if "Wl" in c:                # labels' contribution (enc_in adds hctx)
+            torch.index_select(self.data.labels, 0, c["docs"], out=c["lb"])
+            ws["hctx"].addmm_(c["lb"], c["Wl"])
 
     def _ctx_bwd(self):
         c, ws = self._ctx, self.ws
@@ -834,9 +868,12 @@ class FusedEngine(EngineBase):
         input layer (ZeroShotTM) -- library GEMMs, as in the step's CTX_FWD."""
         c = self._ctx
         x = data.contextual[d0:d1]
-        if "Wa" in c:
-            return torch.addmm(c["ba"], x, c["Wa"].t()) @ c["Wc"]
-        return x @ c["W"]
+        h = torch.addmm(c["ba"], x, c["Wa"].t()) @ c["Wc"] if "Wa" in c else x @ c["W"]
+        if "Wl" in c:                # CTM label head: the labels are encoder inputs too
+            if data.labels is None:
+                raise ValueError("this model encodes labels: inference data needs them")
+            h = h + data.labels[d0:d1] @ c["Wl"]
+        return h
 
     @torch.no_grad()
     def theta_infer(self, data: DeviceCSR, n_samples: int = 20, seed: int = 0,

@@ -100,6 +100,9 @@ class GfkModel(C.Structure):
         ("ctx_fused", C.c_int32), ("ctx_kb", C.c_int32), ("ctx_ckb", C.c_int32),
         ("slot_cap", C.c_int32), ("ws_sidx", P), ("ws_sval", P),
         ("mm_bf16", C.c_int32), ("pad2", C.c_int32),
+        ("lab_on", C.c_int32), ("lab_off", C.c_int32), ("labels", P), ("w_cls", P), ("b_cls", P),
+        ("ws_lab", P), ("ws_dlab", P), ("ws_ce", P), ("ws_thd", P),
+        ("lab_in_enc", C.c_int32), ("pad3", C.c_int32),
     ]
 
 
@@ -112,7 +115,7 @@ class GfkVJob(C.Structure):
     _fields_ = [("param", P), ("src", P), ("n", C.c_int32), ("pad", C.c_int32)]
 
 
-MAX_WJOBS, MAX_VJOBS = 24, 16
+MAX_WJOBS, MAX_VJOBS = 40, 16
 
 
 class GfkUpdate(C.Structure):
