@@ -58,6 +58,8 @@ def build_parser() -> argparse.ArgumentParser:
                    help="comma list: client i trains on category i (local / rccl / gloo)")
     p.add_argument("--log_every", type=int, default=0, help="minibatch loss line every N rounds")
     p.add_argument("--no_graph", action="store_true", help="disable hipGraph replay")
+    p.add_argument("--matmul_dtype", type=str, default=None, choices=["fp32", "bf16"],
+                   help="ProdLDA decoder GEMM operands (default: [amd] matmul_dtype of the config)")
     p.add_argument("--agg", type=str, default="params", choices=["params", "grads"],
                    help="params: FedAvg of the shared state after every local step (reference); "
                         "grads: all-reduce of the sample-weighted gradients before one optimizer "
@@ -217,6 +219,11 @@ def main(argv: Optional[List[str]] = None):
         parser.error("start_server runs with --id 0")
     from .utils.config import load_config
     cfg = load_config(args.config)
+    if args.matmul_dtype is not None:
+        if args.matmul_dtype == "fp32":
+            cfg.training_params.pop("matmul_dtype", None)
+        else:
+            cfg.training_params["matmul_dtype"] = args.matmul_dtype
     if args.backend == "local":
         return run_local(args, cfg)
     if args.backend in ("rccl", "gloo"):

@@ -15,6 +15,9 @@ documents of each node and evaluated on the next ``n_docs_global_inf``:
 
   federated_matched  (new) the same federation run for as many rounds as the
                centralized model takes optimizer steps (equal update budget)
+  federated_grads    (new) the nodes as clients of classic synchronous data
+               parallelism (``agg="grads"``: the sample-weighted gradient average, one
+               optimizer step per round on every replica) -- not the reference protocol
 
 TSS = sum over true topics of the best Bhattacharyya coefficient with a learned
 topic (learned betas re-indexed onto the generator vocabulary).  With
@@ -60,7 +63,8 @@ DEFAULTS = dict(n_nodes=5, vocab_size=5000, n_topics=50, beta=1e-2, alpha=0.1, n
                 federated=True, device=None, backend="auto", seed=0, arms=None,
                 reference_tss=True)
 
-ARMS = ("centralized", "non_colab", "baseline", "federated", "federated_matched")
+ARMS = ("centralized", "non_colab", "baseline", "federated", "federated_matched",
+        "federated_grads")
 
 
 def _vocab_of(counts: sp.csr_matrix):
@@ -192,10 +196,15 @@ def run_iteration(cfg, frozen_topics: int, eta: float, device, seed: int) -> Dic
         out["federated_matched"] = _federated(cfg, sc, train, inf_counts, inf_thetas, device,
                                               seed, rounds=rounds)
         done("federated_matched")
+    if "federated_grads" in arms:
+        out["federated_grads"] = _federated(cfg, sc, train, inf_counts, inf_thetas, device, seed,
+                                            agg="grads")
+        done("federated_grads")
     return out
 
 
-def _federated(cfg, sc, train, inf_counts, inf_thetas, device, seed, rounds=None):
+def _federated(cfg, sc, train, inf_counts, inf_thetas, device, seed, rounds=None,
+               agg: str = "params"):
     from ..federation.data import ClientCorpus
     from ..federation.runner import LocalFederation
     sub = SyntheticCorpus(sc.topic_vectors, [t[: c.shape[0]] for t, c in zip(sc.doc_topics, train)],
@@ -209,7 +218,7 @@ def _federated(cfg, sc, train, inf_counts, inf_thetas, device, seed, rounds=None
         rounds = cfg["num_epochs"] * steps_per_epoch
     params["num_epochs"] = -(-rounds // steps_per_epoch)
     fed = LocalFederation(corpora, params, max_iters=rounds, device=device,
-                          backend=cfg["backend"], seed=seed)
+                          backend=cfg["backend"], seed=seed, agg=agg)
     fed.run()
     tm = fed.clients[0].tm                     # every client holds the averaged state
     id2token = dict(enumerate(fed.terms))

@@ -196,6 +196,9 @@ def load_config(file_path: Optional[str] = None) -> FedConfig:
     cfg.aggregate = get("amd", "aggregate", cfg.aggregate)
     cfg.checkpoint_every = get("amd", "checkpoint_every", cfg.checkpoint_every, int)
     cfg.stop_at_num_epochs = get("amd", "stop_at_num_epochs", cfg.stop_at_num_epochs, bool)
+    mm = get("amd", "matmul_dtype", "fp32")
+    if mm != "fp32":
+        cfg.training_params["matmul_dtype"] = mm
     return cfg
 
 

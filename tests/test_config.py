@@ -1,4 +1,5 @@
 """INI config parity with the reference typing rules (auxiliary_functions.py:387-438)."""
+import os
 import textwrap
 
 from gfedntm_amd.utils.config import (DEFAULT_GRADS_TO_SHARE, load_config,
@@ -62,3 +63,15 @@ def test_cli_accepts_reference_readme_syntax():
     assert build_parser().parse_args(["--id", "0"]).command is None
     with pytest.raises(SystemExit):
         main(["start_client", "--id", "0"])
+
+
+def test_matmul_dtype_knob(tmp_path):
+    """[amd] matmul_dtype reaches the model kwargs; fp32 (the reference's precision) is the
+    default and adds nothing."""
+    from gfedntm_amd.utils.config import load_config, model_kwargs_from_params
+    assert "matmul_dtype" not in load_config().training_params
+    src = open(os.path.join(os.path.dirname(__file__), "..", "config", "dft_params.cf")).read()
+    p = tmp_path / "bf16.cf"
+    p.write_text(src.replace("matmul_dtype = fp32", "matmul_dtype = bf16"))
+    cfg = load_config(str(p))
+    assert model_kwargs_from_params(cfg.training_params)["matmul_dtype"] == "bf16"

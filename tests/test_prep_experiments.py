@@ -108,7 +108,8 @@ def test_dss_tss_simulation_tiny(tmp_path):
     res = dss_tss.run(cfg, str(tmp_path))
     assert [r["frozen_topics"] for r in res["rows"]] == [1, 3]
     for r in res["rows"]:
-        for arm in ("centralized", "non_colab", "baseline", "federated", "federated_matched"):
+        for arm in ("centralized", "non_colab", "baseline", "federated", "federated_matched",
+                    "federated_grads"):
             assert np.isfinite(r[f"{arm}_betas_mean"]) and np.isfinite(r[f"{arm}_thetas_mean"])
             assert 0 < r[f"{arm}_betas_mean"] <= cfg["n_topics"] + 1e-6
     assert os.path.exists(tmp_path / "results.csv")
