@@ -246,11 +246,10 @@ class FusedEngine(EngineBase):
         self.adam_t = torch.zeros(1, dtype=torch.int32, device=dev)
         self.adam_pow = torch.ones(2, dtype=torch.float64, device=dev)     # beta1^t, beta2^t
         self.adam_coef = torch.zeros(2, dtype=torch.float32, device=dev)   # see csrc/gfk_common.h
-        # fused epilogue updates: AVITM and CombinedTM (contextual path on ctx_fwd /
-        # ctx_bwd); ZeroShotTM, whose dense input layer comes from host-issued GEMMs,
-        # runs the generic Adam
         # CTM contextual path on the fused kernels: CombinedTM (ctx_fwd / ctx_bwd) and
-        # ZeroShotTM (dense input layer in enc_in / win_update); _plan_ctx may fall back
+        # ZeroShotTM (dense input layer in enc_in / win_update).  _plan_ctx may fall back
+        # to host-issued GEMMs for shapes outside the kernels' plan; that path runs in
+        # gradient mode with the generic optimizer kernel
         self.ctx_fused = tm.kind == "ctm"
         # Adam runs in the kernels' epilogues; the other solvers in gradient mode
         # (kernels write gradients, the generic optimizer kernel applies the rule)
