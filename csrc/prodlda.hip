@@ -681,7 +681,10 @@ extern "C" size_t gfk_prodlda_fwd_smem(const GfkModel* m) {
 }
 
 // k ranges of the backward: 4 when the tiles outnumber the workgroups (n_dpart < n_tiles)
-// and K has at least 4 k tiles, else 1
+// and K has at least 4 k tiles, else 1.  (Also splitting the one-tile-per-workgroup
+// headline case, 70 tiles at K=50, was measured: the prologue copy of theta_d's k range
+// and the 8-wave dense pass cost more than the quartered MFMA work saved, 0.0652 vs 0.0615
+// ms per round.)
 __host__ __device__ inline int bwd_kq(const GfkModel& m) {
   return (m.n_dpart < m.n_tiles && round_up(m.K, 16) / 16 >= 4) ? 4 : 1;
 }
