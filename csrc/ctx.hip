@@ -120,6 +120,7 @@ __global__ void __launch_bounds__(FT) gfk_ctx_fwd_k(GfkModel m) {
   constexpr int RB = BM / 16, SU = 5;
   const int x = blockIdx.x, jx = x >> 3, rb = jx % RB, tile = (jx / RB) * 8 + (x & 7);
   if (tile >= m.n_tiles) return;
+  GFK_STAMP(m, 30);
   const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
   const int vt = wave & 3, kh = wave >> 2, r = lane & 15, g = lane >> 4;
   const int V = m.V, C = m.C, H0 = m.H[0];
@@ -181,6 +182,7 @@ __global__ void __launch_bounds__(FT) gfk_ctx_fwd_k(GfkModel m) {
   st(ra);
   if (NC > 2) ld(2, ra);
   __syncthreads();
+  GFK_STAMP(m, 31);
   for (int c = 0; c < NC; c += 2) {
     mma();
     if (c + 1 >= NC) break;
@@ -198,6 +200,7 @@ __global__ void __launch_bounds__(FT) gfk_ctx_fwd_k(GfkModel m) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) red[(kh * 16 + g * 4 + i) * 68 + vt * 16 + r] = acc[i];
   __syncthreads();
+  GFK_STAMP(m, 32);
 
   // ---- A = sum of the halves + bias: two elements per thread (16 x 64 = 2 FT) ----
 #pragma unroll
@@ -224,6 +227,7 @@ __global__ void __launch_bounds__(FT) gfk_ctx_fwd_k(GfkModel m) {
       for (int i = 0; i < 4; ++i) hg[(g * 4 + i) * H0 + j] = p[i];
     }
   }
+  GFK_STAMP(m, 33);
 }
 
 // grid: n_tiles * ctx_kb workgroups of 16 waves (one per CU).
@@ -231,6 +235,7 @@ template <int BM>
 __global__ void __launch_bounds__(CT) gfk_ctx_bwd_k(GfkModel m) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ int docs_s[BM];
+  GFK_STAMP(m, 34);
   const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
   const int n_tiles = m.n_tiles, tile = blockIdx.x % n_tiles, kc = blockIdx.x / n_tiles;
   const int V = m.V, C = m.C, H0 = m.H[0], ckb = m.ctx_ckb;
@@ -300,6 +305,7 @@ __global__ void __launch_bounds__(CT) gfk_ctx_bwd_k(GfkModel m) {
     if (b < BM) *reinterpret_cast<f32x4*>(xcs + b * L.ldxb + 4 * q) = rxc[u];
   }
   __syncthreads();
+  GFK_STAMP(m, 35);
 
   // ---- dA [BM, 64] = dz0 Wc_tile^T ----
   constexpr int RT = BM / 16;
@@ -313,6 +319,7 @@ __global__ void __launch_bounds__(CT) gfk_ctx_bwd_k(GfkModel m) {
     for (int r = 0; r < 4; ++r) das[(rt * 16 + (lane >> 4) * 4 + r) * 80 + vt * 16 + (lane & 15)] = acc[r];
   }
   lds_barrier();
+  GFK_STAMP(m, 36);
 
   const AdamCoef ac = adam_coef(m);
   // ---- g_ba = column sums of dA (chunk 0): 16 lanes per column ----
@@ -347,6 +354,7 @@ __global__ void __launch_bounds__(CT) gfk_ctx_bwd_k(GfkModel m) {
       gs[(vt * 16 + (lane >> 4) * 4 + r) * L.gs + ct * 16 + (lane & 15)] = gacc[u][r];
   }
   __syncthreads();
+  GFK_STAMP(m, 37);
 
   // ---- the update on coalesced float4 rows ----
   const bool sh = is_shared(m, m.w_a);
@@ -373,6 +381,7 @@ __global__ void __launch_bounds__(CT) gfk_ctx_bwd_k(GfkModel m) {
       p[0] = np;
     }
   }
+  GFK_STAMP(m, 38);
 }
 
 extern "C" size_t gfk_ctx_smem(const GfkModel* m) {

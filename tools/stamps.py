@@ -46,19 +46,24 @@ def main(argv=None):
     p.add_argument("--nnz", type=int, default=170)
     p.add_argument("--docs", type=int, default=1000)
     p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--ctx", type=int, default=0, help="contextual size: CombinedTM when > 0")
     a = p.parse_args(argv)
     so = build()
     from gfedntm_amd.ops import native
     native.KERNELS_SO = so
     import torch
     from gfedntm_amd.data.bow import BatchPlan, DeviceCSR
-    from gfedntm_amd.models import AVITM
+    import numpy as np
+    from gfedntm_amd.models import AVITM, CombinedTM
     from tests.helpers import random_csr
-    tm = AVITM(input_size=a.vocab, n_components=a.topics,
-               hidden_sizes=tuple(int(h) for h in a.hidden.split(",")), batch_size=a.batch,
-               verbose=False, backend="fused", device="cuda")
+    kw = dict(input_size=a.vocab, n_components=a.topics,
+              hidden_sizes=tuple(int(h) for h in a.hidden.split(",")), batch_size=a.batch,
+              verbose=False, backend="fused", device="cuda")
+    tm = CombinedTM(contextual_size=a.ctx, **kw) if a.ctx else AVITM(**kw)
     X = random_csr(a.docs, a.vocab, a.nnz, seed=0)
-    data = DeviceCSR(X, "cuda")
+    ctx = (np.random.default_rng(1).standard_normal((a.docs, a.ctx)).astype(np.float32)
+           if a.ctx else None)
+    data = DeviceCSR(X, "cuda", contextual=ctx)
     tm.engine.bind_data(data, BatchPlan.build(a.docs, a.batch, a.steps))
     dbg = torch.zeros(64, dtype=torch.int64, device="cuda")
     tm.engine._m.dbg = dbg.data_ptr()
@@ -83,6 +88,11 @@ def main(argv=None):
           "| heads", int(d[29] - d[15]), "| hidden", int(d[13] - d[29]))
     print("enc_in cycles: row+weights issue", int(d[5] - d[4]), "| gather+draws", int(d[6] - d[5]),
           "| input+hidden", int(d[7] - d[6]))
+    if a.ctx:
+        print("ctx_fwd (wg 0) cycles: prologue", int(d[31] - d[30]), "| C loop", int(d[32] - d[31]),
+              "| A + P", int(d[33] - d[32]))
+        print("ctx_bwd (wg 0) cycles: staging", int(d[35] - d[34]), "| dA", int(d[36] - d[35]),
+              "| g_ba + g_Wa", int(d[37] - d[36]), "| update", int(d[38] - d[37]))
     print("win_update (W_in tile 0) cycles: staging", int(d[41] - d[40]), "| mfma+update", int(d[42] - d[41]))
 
 
