@@ -387,10 +387,15 @@ prodlda_bwd_kernel(GfkModel m) {
   constexpr int NW = NTH / 64;                                  // waves
   constexpr int NKS = (4 * MAXU + KQ - 1) / KQ;                 // max k tiles per range
   constexpr int TPR = NTH / BM < 16 ? NTH / BM : 16;            // threads per row (sparse x)
-  constexpr int ZU = (BM * VB / 4 + NTH - 1) / NTH;             // float4 of the logit tile per thread
   constexpr int BU = (NKS * 16 * VB + NTH - 1) / NTH;           // beta floats per thread
   constexpr int MU = (NKS * 4 + NW - 1) / NW;                   // dbeta subtiles per wave
   constexpr int NDT = ((BM / 16) * NKS + NW - 1) / NW;          // d theta_d subtiles per wave
+  // RW: the dbeta tile goes through LDS (the logit tile's buffer, free after the dense
+  // pass) so the optimizer epilogue reads and writes m / v / beta along rows: every
+  // load / store instruction covers 256 contiguous bytes of one row, instead of the MFMA
+  // output layout's 4 rows x 64 B (adam_rmw_bandwidth.jsonl: 5.7 vs 4.2 TB/s)
+  constexpr bool RW = 16 * NKS <= BM;
+  constexpr int RU = RW ? (16 * NKS * VB + NTH - 1) / NTH : 1;  // row-wise elements per thread
   const int K = m.K, V = m.V;
   // the thread index is re-made opaque at every tile (below), so the compiler rebuilds
   // the lane-dependent addresses inside the tile loop instead of hoisting them all out
@@ -430,7 +435,6 @@ prodlda_bwd_kernel(GfkModel m) {
   glds_copy(Sb, m.ws_s, BM, tid, NTH);
 
   // ---- a tile's loads, into registers ----
-  float4 zr[ZU];
   float br[BU];
   float rsr = 0.f;
   int xe0 = 0, xe1 = 0, xc0 = 0;
@@ -438,9 +442,11 @@ prodlda_bwd_kernel(GfkModel m) {
   int xrow = tid / TPR, xsub = tid % TPR;
   auto issue_tile = [&](int tile) {
     const int c0 = tile * VB;
-    const float4* zsrc = reinterpret_cast<const float4*>(m.ws_zn + (size_t)tile * BM * VB);
-#pragma unroll
-    for (int u = 0; u < ZU; ++u) zr[u] = zsrc[min(tid + u * NTH, BM * VB / 4 - 1)];
+    // the tile-start loads first: the dependent first-non-zero load waits for them
+    // alone (vmcnt counts in order), not for the beta block behind them
+    const int32_t* ts = m.ws_tstart + (size_t)min(xrow, BM - 1) * (m.n_tiles + 1) + tile;
+    xe0 = ts[0];                         // rows >= BM (BM < NTH / 16) are never used
+    xe1 = ts[1];
 #pragma unroll
     for (int u = 0; u < BU; ++u) {
       const int i = tid + u * NTH;
@@ -448,9 +454,6 @@ prodlda_bwd_kernel(GfkModel m) {
       br[u] = m.beta[k * V + c];                 // 32-bit offsets (K V < 2^31)
     }
     rsr = m.ws_col_rstd[c0 + (tid & (VB - 1))];
-    const int32_t* ts = m.ws_tstart + (size_t)min(xrow, BM - 1) * (m.n_tiles + 1) + tile;
-    xe0 = ts[0];                         // rows >= BM (BM < NTH / 16) are never used
-    xe1 = ts[1];
   };
   auto issue_first_nz = [&]() {          // depends on the tile-start loads
     const int xe = min(xe0 + xsub, max(xe1 - 1, 0));
@@ -475,6 +478,18 @@ prodlda_bwd_kernel(GfkModel m) {
       }
     }
   };
+  float rm_[RU], rv_[RU];                       // (RW) row-wise Adam state of this thread
+  auto issue_state_rw = [&](int tile) {
+    const int c0 = tile * VB;
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int f = tid + NTH * u;
+      const int k = min(kb + f / VB, K - 1), c = min(c0 + f % VB, V - 1);
+      const float* p = m.beta + (size_t)k * V + c;
+      rm_[u] = p[m.off_m];
+      rv_[u] = p[m.off_v];
+    }
+  };
   // this workgroup's d theta_d partial, per lane (summed over its tiles in order)
   f32x4 dacc[NDT];
 #pragma unroll
@@ -494,12 +509,14 @@ prodlda_bwd_kernel(GfkModel m) {
     // one staging round per tile: every global read is issued before the barrier
     issue_tile(tile);
     issue_first_nz();
-    if (fused) issue_state(tile);              // (beta_split: no Adam state here)
+    if (fused) {                               // (beta_split: no Adam state here)
+      if constexpr (RW) issue_state_rw(tile);
+      else issue_state(tile);
+    }
     if (tile != slab) lds_barrier();           // the previous tile's LDS reads are done
-    // ---- (1) this tile's registers -> LDS; zero the logit-gradient tile ----
-#pragma unroll
-    for (int u = 0; u < ZU; ++u)
-      if (tid + u * NTH < BM * VB / 4) reinterpret_cast<float4*>(zt)[tid + u * NTH] = zr[u];
+    // ---- (1) the BN'ed logit tile by LDS-DMA (contiguous in ws_zn), this tile's
+    //      registers -> LDS; zero the logit-gradient tile ----
+    glds_copy(zt, m.ws_zn + (size_t)tile * BM * VB, BM * VB, tid, NTH);
 #pragma unroll
     for (int u = 0; u < BU; ++u) {
       const int i = tid + u * NTH;
@@ -512,6 +529,10 @@ prodlda_bwd_kernel(GfkModel m) {
     const int ye0 = xe0, ye1 = xe1, yc0 = xc0;
     const float yv0 = xv0;
     vm_barrier();                              // (+ theta_d / lse / S on the first tile)
+    // the same wait, visible to the compiler's waitcnt pass (it cannot see inside the
+    // asm): every load of the staging round is now known complete, so no later use of
+    // the Adam state waits on the epilogue's own stores (vmcnt counts stores too)
+    __builtin_amdgcn_s_waitcnt(0x0F70);        // vmcnt(0) expcnt(7) lgkmcnt(15)
     GFK_STAMP(m, 25);
 
     // ---- (3) sparse term: dt[b, c] = -x p / (p + 1e-10) at this tile's non-zeros ----
@@ -617,6 +638,14 @@ prodlda_bwd_kernel(GfkModel m) {
           }
         }
         const int cl = cst * 16 + (lane & 15);
+        if constexpr (RW) {       // into the G tile: row kl at columns XOR 16 (kl & 4), so a
+#pragma unroll                    // half-wave's 2 rows x 16 columns hit 32 distinct banks
+          for (int e = 0; e < 4; ++e) {
+            const int kl = ks * 16 + (lane >> 4) * 4 + e;
+            zt[kl * VB + (cl ^ ((kl & 4) << 2))] = a0[e] + a1[e];
+          }
+          continue;
+        }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float g = a0[e] + a1[e];
@@ -631,6 +660,7 @@ prodlda_bwd_kernel(GfkModel m) {
           }
         }
       }
+      if constexpr (RW) return;
       // every store after every update: no load is pending between them
 #pragma unroll
       for (int u = 0; u < MU; ++u) {
@@ -656,6 +686,27 @@ prodlda_bwd_kernel(GfkModel m) {
     // (6) first: the Adam state's registers are free before the accumulators are touched
     dbeta_tile();
     dtheta_tile();
+    if constexpr (RW) {       // the G tile, row-wise: update (fused) or gradient
+      lds_barrier();
+#pragma unroll
+      for (int u = 0; u < RU; ++u) {
+        const int f = tid + NTH * u, kl = f / VB, cl = f % VB;
+        const int k = kb + kl, c = c0 + cl;
+        if (kl >= 16 * nks || k >= K || c >= V) continue;
+        const float g = zt[kl * VB + (cl ^ ((kl & 4) << 2))];
+        float* p = m.beta + (size_t)k * V + c;
+        if (!fused) {
+          p[m.off_g] = g;
+        } else {
+          float mo = rm_[u], vo = rv_[u];
+          float np = adam_update(bt[kl * LDB_B + cl], g, mo, vo, ac);
+          if (beta_shared && m.fed_scale_on) np *= m.fed_scale;
+          p[m.off_m] = mo;
+          p[m.off_v] = vo;
+          *p = np;
+        }
+      }
+    }
     GFK_STAMP(m, 28);
     if (SINGLE) break;
   }
