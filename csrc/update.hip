@@ -49,7 +49,9 @@ __host__ __device__ inline int stride_b(int w) {   // w: multiple of 16
 
 extern "C" size_t gfk_win_update_smem(const GfkModel* m) {
   const int B = m->bmax, H0P = rup(m->H[0], 16);
-  const size_t a = (size_t)64 * stride_a(B) + (size_t)B * stride_b(H0P), b = 2 * (size_t)B * 80;
+  size_t a = (size_t)64 * stride_a(B) + (size_t)B * stride_b(H0P);
+  const size_t b = 2 * (size_t)B * 80;
+  if (a < 64 * 64) a = 64 * 64;      // the flat epilogue's gradient tile [64, H0 <= 64]
   return sizeof(float) * (a > b ? a : b);
 }
 
@@ -243,8 +245,40 @@ __global__ void __launch_bounds__(UT) gfk_win_update_k(GfkModel m, GfkUpdate U) 
   constexpr int PU = 16 / UW;
   float pp[PU][4], pm[PU][4], pv[PU][4];
   const bool fused = m.update_mode == 1;
+  // FLAT (H0 <= 64, one pass): a tile's W_in block [64, H0] is contiguous, so the
+  // epilogue moves p / m / v as flat quads (float4 when 16-B aligned): every load /
+  // store instruction covers whole cache lines, instead of the MFMA output layout's
+  // 4 rows x 64 B.  The gradient tile goes through LDS (the x^T buffer, free after the
+  // MFMAs).  Quad q of the block is thread (q % UT)'s slot q / UT.
+  // (the 8-wave large-vocabulary shape only: with one round of 16-wave workgroups the
+  // extra LDS pass and barriers measured slower than the bytes they save)
+  const bool flat = UT == 512 && NT <= 4;
+  const int nel = (min(V, c0 + 64) - c0) * H0;          // the block's elements
+  float* wblk = w_in + (size_t)c0 * H0;
+  const bool al4 = ((uintptr_t)wblk % 16 == 0) && m.off_m % 4 == 0 && m.off_v % 4 == 0 &&
+                   m.off_g % 4 == 0;
+  auto ld4 = [&](const float* q, int e) {      // elements e..e+3 of the block (bounded)
+    if (al4 && e + 3 < nel) return *reinterpret_cast<const f32x4*>(q + e);
+    f32x4 r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = e + i < nel ? q[e + i] : 0.f;
+    return r;
+  };
+  constexpr int FQ = 64 * 64 / 4 / UT;         // quads per thread (H0 <= 64)
+  static_assert(FQ <= PU, "flat epilogue reuses the prefetch registers");
+  if (flat) {
+#pragma unroll
+    for (int u = 0; u < FQ; ++u) {
+      const int e = 4 * (tid + UT * u);
+      f32x4 a = {0.f, 0.f, 0.f, 0.f}, b = a, c = a;
+      if (fused && e < nel) { a = ld4(wblk, e); b = ld4(wblk + m.off_m, e); c = ld4(wblk + m.off_v, e); }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { pp[u][i] = a[i]; pm[u][i] = b[i]; pv[u][i] = c[i]; }
+    }
+  }
 #pragma unroll
   for (int u = 0; u < PU; ++u) {
+    if (flat) break;
     const int t = wave + UW * u;
     const int i0 = (t / NT) * 16, j0 = (t % NT) * 16;
     const int j = min(j0 + (lane & 15), H0 - 1);
@@ -272,6 +306,7 @@ __global__ void __launch_bounds__(UT) gfk_win_update_k(GfkModel m, GfkUpdate U) 
   // ---- G[v, j] = sum_b xt[v, b] dz[b, j] and the update ----
   const AdamCoef ac = adam_coef(m);
   const bool sh = is_shared(m, w_in);
+  f32x4 gk[PU];
   for (int pass = 0; pass * UW * PU < MT * NT; ++pass) {
   if (pass > 0) {             // wide input layers (H0 > 64): the next subtiles' state
 #pragma unroll
@@ -306,6 +341,10 @@ __global__ void __launch_bounds__(UT) gfk_win_update_k(GfkModel m, GfkUpdate U) 
     }
     const f32x4 g = c0v + c1v;
     const int j = j0 + (lane & 15);
+    if (flat) {               // park the gradient in registers until every wave is done
+      gk[u] = g;
+      continue;
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int v = c0 + i0 + (lane >> 4) * 4 + r;
@@ -323,6 +362,47 @@ __global__ void __launch_bounds__(UT) gfk_win_update_k(GfkModel m, GfkUpdate U) 
       }
     }
   }
+  }
+  if (flat) {
+    // the gradient tile [64, H0] into x^T's buffer in the block's own (flat) order
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < PU; ++u) {
+      const int t = wave + UW * u;
+      if (t >= MT * NT) break;
+      const int i0 = (t / NT) * 16, j0 = (t % NT) * 16, j = j0 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (j < H0) xt[(i0 + (lane >> 4) * 4 + r) * H0 + j] = gk[u][r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < FQ; ++u) {
+      const int e = 4 * (tid + UT * u);
+      if (e >= nel) break;
+      const f32x4 g = *reinterpret_cast<const f32x4*>(xt + e);
+      f32x4 np, mo, vo;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float a = pm[u][i], b = pv[u][i];
+        float x = fused ? adam_update(pp[u][i], g[i], a, b, ac) : g[i];
+        np[i] = sh && m.fed_scale_on && fused ? x * m.fed_scale : x;
+        mo[i] = a;
+        vo[i] = b;
+      }
+      auto st4 = [&](float* q, const f32x4& x) {
+        if (al4 && e + 3 < nel) { *reinterpret_cast<f32x4*>(q + e) = x; return; }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) if (e + i < nel) q[e + i] = x[i];
+      };
+      if (!fused) {
+        st4(wblk + m.off_g, np);
+      } else {
+        st4(wblk + m.off_m, mo);
+        st4(wblk + m.off_v, vo);
+        st4(wblk, np);
+      }
+    }
   }
   GFK_STAMP(m, 42);
 }
