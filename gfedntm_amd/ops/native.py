@@ -19,7 +19,9 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_DIR = os.path.join(ROOT, "_lib")
-KERNELS_SO = os.path.join(LIB_DIR, "libgfedntm_kernels.so")
+# GFEDNTM_KERNELS_SO: another build of the kernel library (A/B timing of kernel variants,
+# tools/ab_libs.py); the in-tree library otherwise
+KERNELS_SO = os.environ.get("GFEDNTM_KERNELS_SO") or os.path.join(LIB_DIR, "libgfedntm_kernels.so")
 RUNTIME_SO = os.path.join(LIB_DIR, "libgfedntm_runtime.so")
 
 _kernels: Optional[ctypes.CDLL] = None
