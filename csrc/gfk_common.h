@@ -396,11 +396,15 @@ __device__ __forceinline__ AdamCoef adam_coef(const GfkModel& m) {
   return c;
 }
 
+// The square root and the division use the hardware's v_sqrt_f32 / v_rcp_f32 (1 ulp)
+// instead of the correctly rounded library sequences (~16 and ~10 VALU instructions
+// with their denormal scaling): the optimizer epilogues of the large-vocabulary
+// kernels are VALU-heavy, and the step's relative error stays ~1e-7 of an lr-sized term.
 __device__ __forceinline__ float adam_update(float p, float g, float& mo, float& vo, const AdamCoef& c) {
   if (c.wd != 0.f) g += c.wd * p;
   mo += (1.f - c.b1) * (g - mo);
   vo = c.b2 * vo + (1.f - c.b2) * g * g;
-  return p - c.step * mo / (sqrtf(vo) * c.ibc2 + c.eps);
+  return p - c.step * mo * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vo) * c.ibc2 + c.eps);
 }
 
 // Final value of a parameter element: fused mode applies Adam (and the FedAvg
