@@ -16,7 +16,7 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-from tools.build_native import ARCH, HIPCC, KERNEL_SRCS  # noqa: E402
+from tools.build_native import ARCH, HIPCC, KERNEL_SRCS, KFLAGS  # noqa: E402
 
 
 def main(argv):
@@ -44,8 +44,9 @@ def main(argv):
                 continue
             obj = os.path.join(tmp, s + ".o")
             objs.append(obj)
-            jobs.append([HIPCC, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17",
-                         "-munsafe-fp-atomics", "-Wno-unused-result", "-c", src, "-o", obj])
+            flags = KFLAGS if os.environ.get("AB_FLAGS", "new") == "new" else \
+                ["-O3", "-fPIC", "-std=c++17", "-munsafe-fp-atomics", "-Wno-unused-result"]
+            jobs.append([HIPCC, f"--offload-arch={ARCH}"] + flags + ["-c", src, "-o", obj])
         with cf.ThreadPoolExecutor(8) as ex:
             for r in ex.map(lambda c: subprocess.run(c, capture_output=True, text=True), jobs):
                 if r.returncode:

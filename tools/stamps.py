@@ -19,7 +19,7 @@ sys.path.insert(0, ROOT)
 
 
 def build():
-    from tools.build_native import KERNEL_SRCS
+    from tools.build_native import KERNEL_SRCS, KFLAGS
     out = os.path.join(ROOT, "build", "stamps")
     os.makedirs(out, exist_ok=True)
     objs = []
@@ -28,8 +28,8 @@ def build():
         if not os.path.exists(src):
             continue
         o = os.path.join(out, s + ".o")
-        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17",
-                        "-munsafe-fp-atomics", "-DGFK_STAMPS", "-c", src, "-o", o], check=True)
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950"] + KFLAGS +
+                       ["-DGFK_STAMPS", "-c", src, "-o", o], check=True)
         objs.append(o)
     so = os.path.join(out, "libgfedntm_kernels.so")
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-o", so] + objs,
