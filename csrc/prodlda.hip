@@ -139,6 +139,8 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
   else lds_barrier();
   GFK_STAMP(m, 17);
   asm volatile("" : "+v"(tid));
+  __builtin_assume(tid >= 0 && tid < DEC_THREADS);   // (unsigned index math: shifts, not
+                                                      // signed-division sequences)
   if (tile + (int)gridDim.x < m.n_tiles) issue_tile(tile + gridDim.x);
   // ---- logits for this wave's row tiles x 16 columns (two independent MFMA chains) ----
   f32x4 acc[NRT];
@@ -395,6 +397,8 @@ prodlda_bwd_kernel(GfkModel m) {
   // load / store instruction covers 256 contiguous bytes of one row, instead of the MFMA
   // output layout's 4 rows x 64 B (adam_rmw_bandwidth.jsonl: 5.7 vs 4.2 TB/s)
   constexpr bool RW = 16 * NKS <= BM;
+  constexpr int RPU = NTH / VB;                                 // block rows per thread slot
+  static_assert(NTH % VB == 0 && RPU % 8 == 0, "row-slot layout");
   constexpr int RU = RW ? (16 * NKS * VB + NTH - 1) / NTH : 1;  // row-wise elements per thread
   const int K = m.K, V = m.V;
   // the thread index is re-made opaque at every tile (below), so the compiler rebuilds
@@ -447,10 +451,11 @@ prodlda_bwd_kernel(GfkModel m) {
     const int32_t* ts = m.ws_tstart + (size_t)min(xrow, BM - 1) * (m.n_tiles + 1) + tile;
     xe0 = ts[0];                         // rows >= BM (BM < NTH / 16) are never used
     xe1 = ts[1];
+    // element tid + NTH u of the block is (row tid / VB + RPU u, column tid % VB)
+    const int c = min(c0 + (tid & (VB - 1)), V - 1);
 #pragma unroll
     for (int u = 0; u < BU; ++u) {
-      const int i = tid + u * NTH;
-      const int k = min(kb + i / VB, K - 1), c = min(c0 + i % VB, V - 1);
+      const int k = min(kb + tid / VB + RPU * u, K - 1);
       br[u] = m.beta[k * V + c];                 // 32-bit offsets (K V < 2^31)
     }
     rsr = m.ws_col_rstd[c0 + (tid & (VB - 1))];
@@ -480,11 +485,10 @@ prodlda_bwd_kernel(GfkModel m) {
   };
   float rm_[RU], rv_[RU];                       // (RW) row-wise Adam state of this thread
   auto issue_state_rw = [&](int tile) {
-    const int c0 = tile * VB;
+    const int c = min(tile * VB + (tid & (VB - 1)), V - 1);
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
-      const int f = tid + NTH * u;
-      const int k = min(kb + f / VB, K - 1), c = min(c0 + f % VB, V - 1);
+      const int k = min(kb + tid / VB + RPU * u, K - 1);
       const float* p = m.beta + (size_t)k * V + c;
       rm_[u] = p[m.off_m];
       rv_[u] = p[m.off_v];
@@ -501,6 +505,7 @@ prodlda_bwd_kernel(GfkModel m) {
   for (; tile < m.n_tiles; tile += nslab) {
     const int c0 = tile * VB;
     asm volatile("" : "+v"(tid));
+    __builtin_assume(tid >= 0 && tid < NTH);   // (unsigned index math after the opaque asm)
     lane = tid & 63;
     wave = uniform(tid >> 6);
     xrow = tid / TPR;
@@ -517,11 +522,13 @@ prodlda_bwd_kernel(GfkModel m) {
     // ---- (1) the BN'ed logit tile by LDS-DMA (contiguous in ws_zn), this tile's
     //      registers -> LDS; zero the logit-gradient tile ----
     glds_copy(zt, m.ws_zn + (size_t)tile * BM * VB, BM * VB, tid, NTH);
+    {
+      const int c = tid & (VB - 1), cok = c0 + c < V;
 #pragma unroll
-    for (int u = 0; u < BU; ++u) {
-      const int i = tid + u * NTH;
-      const int k = i / VB, c = i % VB;
-      if (k < 16 * nks) bt[k * LDB_B + c] = (kb + k < K && c0 + c < V) ? br[u] : 0.f;
+      for (int u = 0; u < BU; ++u) {
+        const int k = tid / VB + RPU * u;
+        if (k < 16 * nks) bt[k * LDB_B + c] = (kb + k < K && cok) ? br[u] : 0.f;
+      }
     }
     if (tid < VB) rs[tid] = rsr;
     for (int dcol = tid >> 4; dcol < VB; dcol += NTH / 16)
@@ -688,13 +695,17 @@ prodlda_bwd_kernel(GfkModel m) {
     dtheta_tile();
     if constexpr (RW) {       // the G tile, row-wise: update (fused) or gradient
       lds_barrier();
+      // per thread: one column, rows kl0 + RPU u (RPU a multiple of 8, so the row's
+      // XOR swizzle is the same for all u); the row pointer advances by RPU rows
+      const int cl = tid & (VB - 1), kl0 = tid / VB, c = c0 + cl;
+      const int cs = cl ^ ((kl0 & 4) << 2);
+      float* p0 = m.beta + (size_t)(kb + kl0) * V + c;
 #pragma unroll
       for (int u = 0; u < RU; ++u) {
-        const int f = tid + NTH * u, kl = f / VB, cl = f % VB;
-        const int k = kb + kl, c = c0 + cl;
+        const int kl = kl0 + RPU * u, k = kb + kl;
         if (kl >= 16 * nks || k >= K || c >= V) continue;
-        const float g = zt[kl * VB + (cl ^ ((kl & 4) << 2))];
-        float* p = m.beta + (size_t)k * V + c;
+        const float g = zt[kl * VB + cs];
+        float* p = p0 + (size_t)(RPU * u) * V;
         if (!fused) {
           p[m.off_g] = g;
         } else {
