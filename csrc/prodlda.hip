@@ -106,14 +106,14 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
   if (blockIdx.x == 0 && tid == 0) *m.nbt_beta += 1;
   // a tile's beta block [0, KP) x [c0, c0 + VB) and running statistics, into registers
   float br[BU], rmr = 0.f, rvr = 0.f;
-  const int nbeta = KP * VB;
+  // element tid + DEC_THREADS u of a beta block is (row tid / VB + 16 u, column tid % VB)
+  static_assert(DEC_THREADS == 16 * VB, "beta block row slots");
   auto issue_tile = [&](int tile) {
-    const int c0 = tile * VB;
+    const int c0 = tile * VB, c = min(c0 + (tid & (VB - 1)), V - 1);
 #pragma unroll
     for (int u = 0; u < BU; ++u) {
-      const int i = min(tid + u * DEC_THREADS, nbeta - 1);
       // 32-bit element offsets (K V < 2^31): one VGPR per address, not a pair
-      br[u] = m.beta[min(i / VB, K - 1) * V + min(c0 + i % VB, V - 1)];
+      br[u] = m.beta[min(tid / VB + 16 * u, K - 1) * V + c];
     }
     const int v = min(c0 + col, V - 1);
     rmr = m.beta_rm[v];
@@ -128,11 +128,13 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
   GFK_STAMP(m, 21);
   // ---- staging: the registers of this tile -> LDS ----
   if (tile != (int)blockIdx.x) lds_barrier();      // previous tile's bt / colp reads done
+  {
+    const int c = tid & (VB - 1), cok = c0 + c < V;
 #pragma unroll
-  for (int u = 0; u < BU; ++u) {
-    const int i = tid + u * DEC_THREADS;
-    const int k = i / VB, c = i % VB;
-    if (i < nbeta) bt[k * LDB_F + c] = (k < K && c0 + c < V) ? br[u] : 0.f;
+    for (int u = 0; u < BU; ++u) {
+      const int k = tid / VB + 16 * u;
+      if (k < KP) bt[k * LDB_F + c] = (k < K && cok) ? br[u] : 0.f;
+    }
   }
   const float rm0 = rmr, rv0 = rvr;
   if (tile == (int)blockIdx.x) vm_barrier();       // + theta_d (LDS-DMA)

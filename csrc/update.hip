@@ -205,9 +205,16 @@ __global__ void __launch_bounds__(UT) gfk_win_update_k(GfkModel m, GfkUpdate U) 
   GFK_STAMP(m, 40);
   // ---- staging: dz0 rows (zero padding), zero x^T tile, the tile's CSR extents ----
   const int nb = *nbp;
-  for (int i = tid; i < B * H0P; i += UT) {
-    const int r = i / H0P, c = i % H0P;
-    dz[r * ZS + c] = (c < H0 && r < nb) ? dz0[r * H0 + c] : 0.f;
+  if (H0P <= 64) {            // column tid % 64, rows tid / 64 + UT / 64 j: no runtime division
+    const int c = tid & 63;
+    if (c < H0P)
+      for (int r = tid >> 6; r < B; r += UT / 64)
+        dz[r * ZS + c] = (c < H0 && r < nb) ? dz0[r * H0 + c] : 0.f;
+  } else {
+    for (int i = tid; i < B * H0P; i += UT) {
+      const int r = i / H0P, c = i % H0P;
+      dz[r * ZS + c] = (c < H0 && r < nb) ? dz0[r * H0 + c] : 0.f;
+    }
   }
   if (zs) {                   // x_ctx^T tile: the batch rows' contextual features
     for (int i = tid; i < B * 64; i += UT) {
