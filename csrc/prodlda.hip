@@ -6,7 +6,7 @@
 // Tiling (MI355X-first): one workgroup (4 waves) owns one vocabulary tile of
 // VB=64 columns x ALL batch rows (B <= 128), so the per-column batch-norm
 // statistics (a reduction over B) never leave the workgroup, and the softmax
-// over V is an online (max, sum-exp) per row whose partials are merged by
+// over V is a per-row sum of exp (no max shift: BN bounds |z|) whose partials are merged by
 // row_loss.  The three GEMM-shaped products run on the fp32 matrix cores
 // (v_mfma_f32_16x16x4_f32, exact fp32 -- the reference is fp32):
 //     logits[B, VB]  = theta_d[B, K] @ beta[K, VB]           (forward)
@@ -19,7 +19,7 @@
 //    (global_load_lds_dwordx4), the beta tile through registers;
 //  * forward: wave w owns columns [16w, 16w+16) for all rows, so the column
 //    batch-norm statistics, the normalisation, the running-stat update and the
-//    per-row (max, sum-exp) partials are computed straight from the MFMA
+//    per-row sum-exp partials are computed straight from the MFMA
 //    accumulators (cross-lane shuffles, no LDS pass, no second barrier);
 //  * backward: the x tile is never materialised -- the sparse -x p/(p+1e-10)
 //    terms are written into a pre-zeroed dlogit tile, then one register pass
@@ -70,7 +70,7 @@ __device__ __forceinline__ float sum_groups(float v) {
 // grid: dec_grid workgroups of 16 waves (persistent: workgroup g owns vocab tiles
 // g, g + dec_grid, ...; the usual case is one tile each).  theta_d is staged once per
 // workgroup, so large vocabularies do not re-read it per tile, and the per-row
-// (max, sum-exp) partials are merged across the workgroup's tiles in registers
+// sum-exp partials are accumulated across the workgroup's tiles in registers
 // (ws_row_part holds dec_grid * 4 partials per row).  Wave w owns column strip
 // cs = w & 3 (16 columns) and row tiles rt = (w >> 2) + 4 i.
 // Several tiles per workgroup (large V): the next tile's beta block and running
@@ -94,11 +94,16 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
   constexpr int BU = 16;                      // beta tile elements per thread (K <= 256)
   const int cs = wave & 3, rt0 = wave >> 2;
   const int col = 16 * cs + (lane & 15);      // this lane's column within a tile
-  float rm_[NRT][4], rs_[NRT][4];             // running (max, sum-exp) of this lane's rows
+  // this lane's running sum of exp(z) over its columns of every tile, per row.  No max
+  // shift is needed: z is batch-normalised with the batch's own statistics, so
+  // |z| <= sqrt(nb - 1) <= sqrt(127) (Samuelson) and exp(z) <= 8e4 -- the sum over any
+  // vocabulary stays far inside fp32.  The 16 column lanes of a row are reduced once,
+  // after the last tile, not per tile.
+  float rs_[NRT][4];
 #pragma unroll
   for (int i = 0; i < NRT; ++i)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) { rm_[i][e] = -INFINITY; rs_[i][e] = 0.f; }
+    for (int e = 0; e < 4; ++e) rs_[i][e] = 0.f;
 
   GFK_STAMP(m, 16);
   glds_copy(th, m.ws_thetad, BM * KT, tid, DEC_THREADS);
@@ -235,7 +240,7 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
   }
   GFK_STAMP(m, 19);
 
-  // ---- normalise, store the BN'ed tile, merge the per-row (max, sum-exp) ----
+  // ---- normalise, store the BN'ed tile, accumulate the per-row sum of exp ----
   float* zt = m.ws_zn + (size_t)tile * BM * VB;
 #pragma unroll
   for (int i = 0; i < NRT; ++i) {
@@ -245,10 +250,7 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
       const int row = (rt0 + 4 * i) * 16 + (lane >> 4) * 4 + e;
       const float z = (acc[i][e] - mean) * rstd;
       if (row < nb) zt[row * VB + (col ^ zswz(row))] = z;
-      const float zv = valid ? z : -INFINITY;
-      const float mx = row16_max(zv);
-      const float se = row16_sum(valid ? __expf(zv - mx) : 0.f);
-      lse_merge(rm_[i][e], rs_[i][e], mx, se);
+      rs_[i][e] += valid ? __expf(z) : 0.f;
     }
   }
   GFK_STAMP(m, 20);
@@ -261,9 +263,10 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int row = (rt0 + 4 * i) * 16 + (lane >> 4) * 4 + e;
+      const float se = row16_sum(rs_[i][e]);
       if ((lane & 15) == 0 && row < nb) {
-        part[2 * row] = rm_[i][e];
-        part[2 * row + 1] = rs_[i][e];
+        part[2 * row] = 0.f;                   // (max, sum-exp) partial with max 0
+        part[2 * row + 1] = se;
       }
     }
   }
