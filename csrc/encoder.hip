@@ -142,7 +142,18 @@ __device__ __forceinline__ void rowvec_gemv(const float* W, const float* x, int 
     float acc = 0.f;
     if (j < n_out) {
       const float* wr = W + (size_t)j * n_in;
-      for (int i = s; i < n_in; i += 16) acc += wr[i] * x[i];
+      // 4 products per lane per round, their 8 LDS reads issued together (clamped
+      // addresses, masked values): one LDS round trip per 64 inputs, not per 16
+      for (int i0 = 0; i0 < n_in; i0 += 64) {
+        float p[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int i = i0 + s + 16 * q, ic = min(i, n_in - 1);
+          const float v = wr[ic] * x[ic];
+          p[q] = i < n_in ? v : 0.f;
+        }
+        acc += (p[0] + p[1]) + (p[2] + p[3]);
+      }
     }
     acc = row16_sum(acc);
     if (s == 0 && j < n_out) epi(j, acc);
@@ -313,6 +324,7 @@ __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkModel m) {
     int32_t* ts = m.ws_tstart + (size_t)b * (m.n_tiles + 1);
     for (int u = last_tile + 1 + tid; u <= m.n_tiles; u += ENC_THREADS) ts[u] = e1;
   }
+  GFK_STAMP(m, 44);
 
   // ---- input layer: z0 = sum of the wave partials + bias (+ dense contextual part) ----
   const int act = m.act;
@@ -338,6 +350,7 @@ __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkModel m) {
     act0[tid] = a;
   }
   lds_barrier();
+  GFK_STAMP(m, 43);
 
   // ---- hidden layers ----
   float* ain = act0;
@@ -366,6 +379,7 @@ __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkModel m) {
       }
       aout[j] = a;
     });
+    GFK_STAMP(m, 45);
     lds_barrier();
     float* t = ain; ain = aout; aout = t;
   }
@@ -380,6 +394,7 @@ __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkModel m) {
   float* lr = m.ws_ls_raw + (size_t)b * K;
   rowvec_gemv(Wmu, ain, K, Hl, tid, [&](int k, float acc) { mr[k] = acc + Bmu[k]; });
   rowvec_gemv(Ws, ain, K, Hl, tid, [&](int k, float acc) { lr[k] = acc + Bs[k]; });
+  GFK_STAMP(m, 39);
 }
 
 extern "C" int gfk_launch_enc_in(const GfkModel* m, hipStream_t s) {

@@ -87,7 +87,9 @@ def main(argv=None):
     print("post_bwd rest: wg0 extras", int(d[14] - d[12]), "| bn_bwd", int(d[15] - d[14]),
           "| heads", int(d[29] - d[15]), "| hidden", int(d[13] - d[29]))
     print("enc_in cycles: row+weights issue", int(d[5] - d[4]), "| gather+draws", int(d[6] - d[5]),
-          "| input+hidden", int(d[7] - d[6]))
+          "| input+hidden", int(d[7] - d[6]), "| heads", int(d[39] - d[7]))
+    print("enc_in input+hidden: tile-start tail", int(d[44] - d[6]), "| input layer", int(d[43] - d[44]),
+          "| hidden layers", int(d[7] - d[43]), "(last layer's gemv+epilogue ends at", int(d[45] - d[43]), ")")
     if a.ctx:
         print("ctx_fwd (wg 0) cycles: prologue", int(d[31] - d[30]), "| C loop", int(d[32] - d[31]),
               "| A + P", int(d[33] - d[32]))
