@@ -251,11 +251,35 @@ __global__ void __launch_bounds__(CT) gfk_ctx_bwd_k(GfkModel m) {
   const float* wcg = m.w_in + (size_t)V * H0;
   const int nb = *m.ws_nb;
   const bool fused = m.update_mode == 1;
+  const AdamCoef ac = adam_coef(m);     // (device loads: issued with the first round)
 
-  // ---- prefetch p / m / v of the Wa block [64, chunk] as coalesced float4 rows:
-  //      element u of a thread is (row, q) = (e / NQ, e % NQ), e = tid + 1024 u ----
-  constexpr int MAXQ = 4;               // 64 x 256 / 4 / 1024
+  // ---- one staging round, every load unconditional (clamped addresses; the masks are
+  //      applied when the values reach LDS), so the compiler can count them: dz0 and the
+  //      Wc tile, then the x_ctx chunk, then the Adam state p / m / v of the Wa block.
+  //      Only the first three are waited for before the products; the 192 KB of Adam
+  //      state is still arriving while dA and g_Wa run on the matrix cores. ----
+  const float* dz0 = m.ws_dz[0];
+  const int nbc = max(nb, 1);
+  constexpr int SR = 4;                 // dz0 / Wc elements per thread (H0 <= 64: all of them)
+  float rdz[SR], rwc[SR];
+#pragma unroll
+  for (int u = 0; u < SR; ++u) {
+    const int i = tid + CT * u, r = i / H0Q, j = min(i - r * H0Q, H0 - 1);
+    rdz[u] = dz0[min(r, nbc - 1) * H0 + j];
+    rwc[u] = wcg[(size_t)(c0 + min(r, nvv - 1)) * H0 + j];
+  }
+  __syncthreads();          // docs_s
+  constexpr int XU = (BM * 64 + CT - 1) / CT;   // float4 of the x_ctx chunk per thread
   const int NQ = ckb / 4;
+  f32x4 rxc[XU];
+#pragma unroll
+  for (int u = 0; u < XU; ++u) {
+    const int e = tid + CT * u, b = e / NQ, q = e - b * NQ;
+    const int bc = min(b, min(nbc, BM) - 1), qc = min(4 * q, kn - 4);
+    rxc[u] = *reinterpret_cast<const f32x4*>(m.ctx + (size_t)docs_s[bc] * C + k0 + qc);
+  }
+  // p / m / v: element u of a thread is (row, q) = (e / NQ, e % NQ), e = tid + 1024 u
+  constexpr int MAXQ = 4;               // 64 x 256 / 4 / 1024
   f32x4 pp[MAXQ], pm[MAXQ], pv[MAXQ];
   int prow[MAXQ], pq[MAXQ];
 #pragma unroll
@@ -263,46 +287,29 @@ __global__ void __launch_bounds__(CT) gfk_ctx_bwd_k(GfkModel m) {
     const int e = tid + CT * u;
     prow[u] = e / NQ;
     pq[u] = e - prow[u] * NQ;
-    pp[u] = pm[u] = pv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (fused && prow[u] < nvv && 4 * pq[u] < kn) {
-      const f32x4* p = reinterpret_cast<const f32x4*>(m.w_a + (size_t)(c0 + prow[u]) * C + k0 + 4 * pq[u]);
-      pp[u] = p[0];
-      pm[u] = p[m.off_m / 4];
-      pv[u] = p[m.off_v / 4];
-    }
+    const f32x4* p = reinterpret_cast<const f32x4*>(
+        m.w_a + (size_t)(c0 + min(prow[u], nvv - 1)) * C + k0 + min(4 * pq[u], kn - 4));
+    pp[u] = p[0];
+    pm[u] = p[m.off_m / 4];
+    pv[u] = p[m.off_v / 4];
   }
-  // ---- one staging round: dz0 (rows >= nb zero), Wc tile, x_ctx chunk; the
-  //      dz0 / Wc loads are in flight while the doc ids reach LDS ----
-  const float* dz0 = m.ws_dz[0];
-  auto ld_dz = [&](int i) {
-    const int b = i / H0Q, j = i - b * H0Q;
-    return (b < nb && j < H0) ? dz0[b * H0 + j] : 0.f;
-  };
-  auto st_dz = [&](int i, float x) { const int b = i / H0Q; dzs[b * L.ldz + i - b * H0Q] = x; };
-  auto ld_wc = [&](int i) {
-    const int v = i / H0Q, j = i - v * H0Q;
-    return (v < nvv && j < H0) ? wcg[(size_t)(c0 + v) * H0 + j] : 0.f;
-  };
-  auto st_wc = [&](int i, float x) { const int v = i / H0Q; wcs[v * L.ldz + i - v * H0Q] = x; };
-  float rdz[4], rwc[4];
-  reg_load<4>(rdz, BM * H0Q, ld_dz);
-  reg_load<4>(rwc, 64 * H0Q, ld_wc);
-  __syncthreads();          // docs_s
-  constexpr int XU = (BM * 64 + CT - 1) / CT;   // float4 of the x_ctx chunk per thread
-  f32x4 rxc[XU];
+#pragma unroll
+  for (int u = 0; u < SR; ++u) {
+    const int i = tid + CT * u, r = i / H0Q, j = i - r * H0Q;
+    if (r < BM) dzs[r * L.ldz + j] = (r < nb && j < H0) ? rdz[u] : 0.f;
+    if (r < 64) wcs[r * L.ldz + j] = (r < nvv && j < H0) ? rwc[u] : 0.f;
+  }
+  for (int i = tid + CT * SR; i < max(BM, 64) * H0Q; i += CT) {   // wide input layers
+    const int r = i / H0Q, j = i - r * H0Q;
+    if (r < BM) dzs[r * L.ldz + j] = (r < nb && j < H0) ? dz0[r * H0 + j] : 0.f;
+    if (r < 64) wcs[r * L.ldz + j] = (r < nvv && j < H0) ? wcg[(size_t)(c0 + r) * H0 + j] : 0.f;
+  }
 #pragma unroll
   for (int u = 0; u < XU; ++u) {
     const int e = tid + CT * u, b = e / NQ, q = e - b * NQ;
-    rxc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (b < nb && b < BM && 4 * q < kn)
-      rxc[u] = *reinterpret_cast<const f32x4*>(m.ctx + (size_t)docs_s[b] * C + k0 + 4 * q);
-  }
-  reg_store<4>(rdz, BM * H0Q, ld_dz, st_dz);
-  reg_store<4>(rwc, 64 * H0Q, ld_wc, st_wc);
-#pragma unroll
-  for (int u = 0; u < XU; ++u) {
-    const int e = tid + CT * u, b = e / NQ, q = e - b * NQ;
-    if (b < BM) *reinterpret_cast<f32x4*>(xcs + b * L.ldxb + 4 * q) = rxc[u];
+    if (b < BM)
+      *reinterpret_cast<f32x4*>(xcs + b * L.ldxb + 4 * q) =
+          (b < nb && 4 * q < kn) ? rxc[u] : f32x4{0.f, 0.f, 0.f, 0.f};
   }
   __syncthreads();
   GFK_STAMP(m, 35);
@@ -321,14 +328,13 @@ __global__ void __launch_bounds__(CT) gfk_ctx_bwd_k(GfkModel m) {
   lds_barrier();
   GFK_STAMP(m, 36);
 
-  const AdamCoef ac = adam_coef(m);
-  // ---- g_ba = column sums of dA (chunk 0): 16 lanes per column ----
+  // ---- g_ba = column sums of dA (chunk 0): 16 lanes per column; its update (a global
+  //      read-modify-write) waits until the end, so nothing here waits on the Wa state ----
+  float gba = 0.f;
   if (kc == 0) {
     const int v = tid >> 4, sub = tid & 15;
-    float s = 0.f;
-    for (int b = sub; b < BM; b += 16) s += das[b * 80 + v];
-    s = row16_sum(s);
-    if (sub == 0 && v < nvv) param_update(m, m.b_a + c0 + v, s, ac, is_shared(m, m.b_a));
+    for (int b = sub; b < BM; b += 16) gba += das[b * 80 + v];
+    gba = row16_sum(gba);
   }
   // ---- g_Wa [64, chunk] = dA^T x_ctx: wave tiles (vt, ct) = (t & 3, t >> 2),
   //      t = wave + 16 u, parked in registers until every wave has read dA / x_ctx ----
@@ -380,6 +386,10 @@ __global__ void __launch_bounds__(CT) gfk_ctx_bwd_k(GfkModel m) {
       p[m.off_v / 4] = vo;
       p[0] = np;
     }
+  }
+  if (kc == 0) {
+    const int v = tid >> 4;
+    if ((tid & 15) == 0 && v < nvv) param_update(m, m.b_a + c0 + v, gba, ac, is_shared(m, m.b_a));
   }
   GFK_STAMP(m, 38);
 }
