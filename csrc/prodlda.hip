@@ -272,6 +272,219 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
   }
 }
 
+// Strip forward for large K x large V (fp32, B <= 64; stage_flags bit 2, chosen by the
+// engine when the tile kernel's th + beta tile (118 KB at K = 200) admits only one
+// workgroup per CU and the vocabulary spans several rounds of them).  The tile kernel
+// runs its phases serially per tile -- staging, MFMA, two batch-norm barriers, stores.
+// Here each WAVE owns a 16-column strip of a vocab tile for ALL batch rows and works
+// through its strips independently:
+//  * the MFMA B operand (beta, the strip's 16 columns x K) comes straight from global
+//    memory into registers by buffer loads (one per-lane offset, rows past K read as 0),
+//    so the LDS holds theta_d alone and no beta tile;
+//  * the column batch-norm statistics are a reduction over the wave's own rows: register
+//    sums + two lane-group shuffles, no LDS, no barrier;
+//  * after theta_d is staged there is no barrier between the waves;
+//  * PF (stage_flags bit 3, the default): 8 waves of ~190 VGPRs (2 per SIMD), the next
+//    strip's beta block in flight while this one runs its MFMAs / batch norm / stores;
+//    PF = false: 16 waves of <= 128 VGPRs overlapping each other's loads instead.
+// k pairing: MFMA steps 2t and 2t + 1 take k = 8t + 2g and 8t + 2g + 1 for lane group
+// g = lane >> 4 (any bijection of k works if A and B agree), so a lane's two A operands
+// are one ds_read_b64, read one pair ahead of the MFMAs.  Strips s = tile * 4 + cs are
+// dealt to waves round-robin (the strips of a tile to neighbouring waves: their beta rows
+// share cache lines).  The per-row sum-exp partials of the waves are summed through LDS
+// once at the end and stored as the workgroup's 4 partial slots (slot 0 holds the sum,
+// 1..3 zero), so row_loss reads the same dec_grid * 4 partials as with the tile kernel.
+// Measured at K = 200 (profiles/r2/large_vocab.md): the forward 52 -> ~45 us at V = 112k,
+// rounds 0.346 -> 0.341 ms (V = 112k) and 0.255 -> 0.251 ms (V = 74k).
+// NP: k pairs held in registers (compile-time, the launcher's smallest instance >= K / 8).
+template <int BM, int NP, bool PF>
+__global__ void __launch_bounds__(PF ? 512 : 1024) prodlda_fwd_strip_kernel(GfkModel m) {
+  constexpr int STRIP_THREADS = PF ? 512 : 1024;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int K = m.K, V = m.V, KT = m.kt;
+  int tid = threadIdx.x;
+  const int lane = tid & 63, wave = uniform(tid >> 6);
+  constexpr int RT = BM / 16;
+  constexpr int NW = STRIP_THREADS / 64;
+  // theta_d re-staged with its own row stride KS = 8 NP + 2 (2 x odd: the 16 rows x 2
+  // floats of a half-wave's ds_read_b64 hit 32 distinct banks) and ZERO beyond K and in
+  // rows >= nb: the MFMA loop then needs no k masks (pairs past K multiply zero A and
+  // zero B) and the rows >= nb contribute exact zeros to the logits
+  constexpr int KS = 8 * NP + 2;
+  float* th = smem;                            // [BM][KS]
+  float* red = th + BM * KS;                   // [NW][BM] per-wave row partials
+  float rs_[RT][4];
+#pragma unroll
+  for (int i = 0; i < RT; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) rs_[i][e] = 0.f;
+
+  const int nb = *m.ws_nb;
+  if (blockIdx.x == 0 && tid == 0) *m.nbt_beta += 1;
+  {
+    constexpr int SU = (BM * KS + STRIP_THREADS - 1) / STRIP_THREADS;
+    float tv[SU];
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      // (clamped, unconditional loads: a guarded load compiles to a branch + vmcnt(0))
+      const int idx = tid + u * STRIP_THREADS, row = idx / KS, k = idx % KS;
+      tv[u] = m.ws_thetad[min(row, BM - 1) * KT + min(k, K - 1)];
+    }
+#pragma unroll
+    for (int u = 0; u < SU; ++u) asm volatile("" : "+v"(tv[u]));   // (not sunk into branches)
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      const int idx = tid + u * STRIP_THREADS, row = idx / KS, k = idx % KS;
+      tv[u] = (row < nb && k < K) ? tv[u] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < SU; ++u)
+      if (tid + u * STRIP_THREADS < BM * KS) th[tid + u * STRIP_THREADS] = tv[u];
+  }
+  const int g2 = 2 * (lane >> 4);
+  const float inv_nb = 1.f / (float)nb;
+  const int nstrips = m.n_tiles * 4;
+  const int stride = gridDim.x * NW;
+  lds_barrier();
+  asm volatile("" : "+v"(tid));
+  __builtin_assume(tid >= 0 && tid < STRIP_THREADS);
+  const int arow = (lane & 15) * KS + g2;
+  // beta [K, V] as a buffer resource of K V floats (K V < 2^29 checked by the launcher)
+  const __amdgpu_buffer_rsrc_t bres =
+      __builtin_amdgcn_make_buffer_rsrc((void*)m.beta, 0, K * V * 4, 0x00020000);
+  // A strip's beta block into registers: buffer loads with ONE per-lane offset (row g2,
+  // column) stepped by 8 rows per pair; rows k >= K lie past the resource's extent and
+  // read as 0 (no clamps, no per-load address VGPRs).  Unconditional: a guarded load
+  // becomes a branch + vmcnt(0) per pair in the ISA.  The row step is made opaque per
+  // call so the offsets are recomputed here, not hoisted out of the loop and spilled.
+  auto issue = [&](int st, float (&bb)[2 * NP], float& rm, float& rv) {
+    const int vc = min((st >> 2) * VB + 16 * (st & 3) + (lane & 15), V - 1);
+    int v4 = V * 4;
+    asm volatile("" : "+s"(v4));
+    int voff = g2 * v4 + vc * 4;
+    const int v32 = 8 * v4;
+#pragma unroll
+    for (int t = 0; t < NP; ++t) {
+      bb[2 * t] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bres, voff, 0, 0));
+      bb[2 * t + 1] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bres, voff, v4, 0));
+      voff += v32;
+    }
+    rm = m.beta_rm[vc];
+    rv = m.beta_rv[vc];
+  };
+  // software pipeline over the wave's strips: the NEXT strip's beta block is in flight
+  // while this one runs its MFMAs / batch norm / stores (2 waves per SIMD, ~160 VGPRs)
+  // PF = false: no prefetch, 16 waves per CU at <= 128 VGPRs (the waves overlap each
+  // other's loads instead)
+  float b[2 * NP], bn[2 * NP], rm0 = 0.f, rv0 = 0.f, rmn = 0.f, rvn = 0.f;
+  int s = blockIdx.x * NW + wave;
+  if (PF && s < nstrips) issue(s, b, rm0, rv0);
+#pragma unroll 1
+  for (; s < nstrips; s += stride) {
+    if (PF) issue(min(s + stride, nstrips - 1), bn, rmn, rvn);   // (the last one re-reads a strip)
+    else issue(s, b, rm0, rv0);
+    const int tile = s >> 2, cs = s & 3;
+    const int col = 16 * cs + (lane & 15);
+    const int v = tile * VB + col;
+    const bool valid = v < V;
+    int aoff = arow;                  // (an integer: an opaque pointer would turn the
+    asm volatile("" : "+v"(aoff));    //  LDS reads into FLAT loads)
+    const float* ap = th + aoff;
+    // ---- logits [BM, 16] on the matrix cores: RT independent accumulation chains ----
+    f32x4 acc[RT];
+#pragma unroll
+    for (int i = 0; i < RT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // (NP is the launcher's smallest instance >= the pairs of K; the pairs past K are
+    // zero in both operands)
+    // A reads one pair ahead of the MFMAs (double-buffered registers); the fences keep
+    // the scheduler from hoisting every pair's reads above the first MFMA (spills)
+    float2 a[2][RT];
+#pragma unroll
+    for (int i = 0; i < RT; ++i) a[0][i] = *reinterpret_cast<const float2*>(ap + i * 16 * KS);
+#pragma unroll
+    for (int t = 0; t < NP; ++t) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (t + 1 < NP) {
+#pragma unroll
+        for (int i = 0; i < RT; ++i)
+          a[(t + 1) & 1][i] = *reinterpret_cast<const float2*>(ap + i * 16 * KS + 8 * (t + 1));
+      }
+#pragma unroll
+      for (int i = 0; i < RT; ++i) acc[i] = mfma16x16x4(a[t & 1][i].x, b[2 * t], acc[i]);
+#pragma unroll
+      for (int i = 0; i < RT; ++i) acc[i] = mfma16x16x4(a[t & 1][i].y, b[2 * t + 1], acc[i]);
+    }
+    // ---- column batch-norm over the wave's own rows (rows >= nb excluded) ----
+    // (rows >= nb are exact zeros, so the sum needs no mask; lim is made opaque per strip
+    // so the 4 RT row compares are not hoisted out of the loop as live SGPR masks)
+    float sm = 0.f;
+#pragma unroll
+    for (int i = 0; i < RT; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sm += acc[i][e];
+    const float mean = sum_groups(sm) * inv_nb;
+    int lim = nb - (lane >> 4) * 4;
+    asm volatile("" : "+v"(lim));
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < RT; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float d = acc[i][e] - mean;
+        q += i * 16 + e < lim ? d * d : 0.f;
+      }
+    const float var = sum_groups(q) * inv_nb;
+    const float rstd = rsqrtf(var + m.bn_eps);
+    if (lane < 16 && valid) {
+      const float mom = m.bn_momentum;
+      const float unb = nb > 1 ? var * (float)nb / (float)(nb - 1) : var;
+      float nm = (1.f - mom) * rm0 + mom * mean, nv = (1.f - mom) * rv0 + mom * unb;
+      if (m.fed_scale_on && is_shared(m, m.beta_rm)) { nm *= m.fed_scale; nv *= m.fed_scale; }
+      m.beta_rm[v] = nm;
+      m.beta_rv[v] = nv;
+      m.ws_col_rstd[v] = rstd;
+    }
+    // ---- normalise, store the BN'ed strip, accumulate the per-row sum of exp ----
+    float* zt = m.ws_zn + (size_t)tile * BM * VB;
+#pragma unroll
+    for (int i = 0; i < RT; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = i * 16 + (lane >> 4) * 4 + e;
+        const float z = (acc[i][e] - mean) * rstd;
+        if (i * 16 + e < lim) zt[row * VB + (col ^ zswz(row))] = z;
+        rs_[i][e] += valid ? __expf(z) : 0.f;
+      }
+    if (PF) {
+#pragma unroll
+      for (int j = 0; j < 2 * NP; ++j) b[j] = bn[j];
+      rm0 = rmn;
+      rv0 = rvn;
+    }
+  }
+  // ---- the 16 waves' per-row partials -> the workgroup's partial slots ----
+#pragma unroll
+  for (int i = 0; i < RT; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float se = row16_sum(rs_[i][e]);
+      if ((lane & 15) == 0) red[wave * BM + i * 16 + (lane >> 4) * 4 + e] = se;
+    }
+  lds_barrier();
+  if (tid < 4 * BM) {
+    const int slot = tid / BM, row = tid % BM;
+    float se = 0.f;
+    if (slot == 0)
+#pragma unroll
+      for (int w = 0; w < NW; ++w) se += red[w * BM + row];
+    if (row < nb) {
+      float* part = m.ws_row_part + ((size_t)(blockIdx.x * 4 + slot) * m.bmax + row) * 2;
+      part[0] = 0.f;
+      part[1] = se;
+    }
+  }
+}
+
 // One wave per batch row: log-sum-exp from the per-wave partials, the sparse
 // reconstruction loss and S_b over the row's non-zeros (read from the row slots
 // prepared with the batch, so the logit gathers are the second round trip).
@@ -742,7 +955,20 @@ prodlda_bwd_kernel(GfkModel m) {
   }
 }
 
+// stage_flags bit 2: the strip forward (prodlda_fwd_strip_kernel) -- theta_d + the
+// per-wave row partials only
+constexpr int FWD_STRIP = 4;
+constexpr int FWD_STRIP_PF = 8;   // bit 3: its prefetching 8-wave variant
+__host__ __device__ inline int strip_pairs(int K) { return (K + 7) / 8; }
+// the kernel instance (k pairs in registers) for K
+__host__ __device__ inline int strip_np(int K) {
+  const int np = strip_pairs(K);
+  return np <= 8 ? 8 : np <= 13 ? 13 : np <= 16 ? 16 : np <= 25 ? 25 : 32;
+}
+
 extern "C" size_t gfk_prodlda_fwd_smem(const GfkModel* m) {
+  if (m->stage_flags & FWD_STRIP)
+    return sizeof(float) * ((size_t)m->bmax * (8 * strip_np(m->K) + 2) + (size_t)(1024 / 64) * m->bmax);
   const size_t KP = round_up(m->K, m->mm_bf16 ? 16 : 4);
   return sizeof(float) * ((size_t)m->bmax * m->kt + KP * LDB_F + 8 * VB);
 }
@@ -768,6 +994,33 @@ extern "C" size_t gfk_prodlda_bwd_smem(const GfkModel* m) { return bwd_smem(m, b
 extern "C" int gfk_launch_prodlda_fwd(const GfkModel* m, hipStream_t s) {
   const size_t sm = gfk_prodlda_fwd_smem(m);
   dim3 g(m->dec_grid), blk(DEC_THREADS);
+  if (m->stage_flags & FWD_STRIP) {
+    // fp32, B <= 64, K <= 256; the partial slots need 4 * grid <= 4 * n_tiles
+    const int np = strip_np(m->K);
+    if (m->mm_bf16 || m->bmax > 64 || m->K > 256 || m->dec_grid > m->n_tiles ||
+        (int64_t)m->K * m->V >= (1LL << 29)) return -1;
+#define GFK_FWS(BM, NP)                                                                        \
+    do {                                                                                       \
+      if (m->stage_flags & FWD_STRIP_PF)                                                       \
+        hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, true>), g, dim3(512), sm, s, *m); \
+      else                                                                                     \
+        hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, false>), g, dim3(1024), sm, s, *m); \
+    } while (0)
+#define GFK_FWS_B(BM)                                                      \
+    if (np == 8) GFK_FWS(BM, 8);                                           \
+    else if (np == 13) GFK_FWS(BM, 13);                                    \
+    else if (np == 16) GFK_FWS(BM, 16);                                    \
+    else if (np == 25) GFK_FWS(BM, 25);                                    \
+    else GFK_FWS(BM, 32)
+    switch (m->bmax) {
+      case 16: GFK_FWS_B(16); break;
+      case 32: GFK_FWS_B(32); break;
+      default: GFK_FWS_B(64); break;
+    }
+#undef GFK_FWS_B
+#undef GFK_FWS
+    return (int)hipGetLastError();
+  }
 #define GFK_FWD(BM)                                                                  \
   if (m->mm_bf16) hipLaunchKernelGGL((prodlda_fwd_kernel<BM, true>), g, blk, sm, s, *m);   \
   else hipLaunchKernelGGL((prodlda_fwd_kernel<BM, false>), g, blk, sm, s, *m)
@@ -834,6 +1087,13 @@ extern "C" int gfk_prodlda_set_smem(size_t bytes) {
                       (const void*)prodlda_fwd_kernel<64, false>, (const void*)prodlda_fwd_kernel<128, false>,
                       (const void*)prodlda_fwd_kernel<16, true>, (const void*)prodlda_fwd_kernel<32, true>,
                       (const void*)prodlda_fwd_kernel<64, true>, (const void*)prodlda_fwd_kernel<128, true>,
+#define GFK_FWS_PTRS1(BM, F) (const void*)prodlda_fwd_strip_kernel<BM, 8, F>, \
+    (const void*)prodlda_fwd_strip_kernel<BM, 13, F>, (const void*)prodlda_fwd_strip_kernel<BM, 16, F>, \
+    (const void*)prodlda_fwd_strip_kernel<BM, 25, F>, (const void*)prodlda_fwd_strip_kernel<BM, 32, F>
+#define GFK_FWS_PTRS(BM) GFK_FWS_PTRS1(BM, false), GFK_FWS_PTRS1(BM, true)
+                      GFK_FWS_PTRS(16), GFK_FWS_PTRS(32), GFK_FWS_PTRS(64),
+#undef GFK_FWS_PTRS
+#undef GFK_FWS_PTRS1
 #define GFK_BWD_PTRS2(U, T, F) (const void*)prodlda_bwd_kernel<16, U, T, F>, \
     (const void*)prodlda_bwd_kernel<32, U, T, F>, (const void*)prodlda_bwd_kernel<64, U, T, F>, \
     (const void*)prodlda_bwd_kernel<128, U, T, F>

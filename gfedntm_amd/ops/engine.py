@@ -52,6 +52,8 @@ VB = 64
 # is the large-K plan: the head weights [K, H] feed post_bwd's GEMVs from LDS instead
 # of one dependent L2 round trip per pass
 STAGE_PLANS = (1, 0, 3, 2)
+STAGE_FWD_STRIP = 4               # bit 2: ProdLDA strip forward (csrc/prodlda.hip)
+STAGE_FWD_STRIP_PF = 8            # bit 3: its prefetching 8-wave variant
 
 
 def _explain(ok: bool, why: str, explain: bool) -> bool:
@@ -418,6 +420,23 @@ class FusedEngine(EngineBase):
             cu = props.multi_processor_count
             sm = self.lib.gfk_smem_required(C.byref(m), 0)
             m.dec_grid = int(min(m.n_tiles, (2 if 2 * sm <= LDS_LIMIT else 1) * cu))
+            # strip forward (prodlda_fwd_strip_kernel, stage_flags bit 2): each wave owns
+            # 16 columns x all rows, beta straight into registers, batch norm without
+            # barriers.  Chosen when the tile kernel fits only one workgroup per CU and
+            # the vocabulary spans several rounds of them (K = 200, V >= 74k);
+            # GFEDNTM_FWD_STRIP=1 forces it wherever the kernel applies, 0 disables it
+            strip = os.environ.get("GFEDNTM_FWD_STRIP", "auto")
+            fits = (not m.mm_bf16 and m.bmax <= 64 and m.K <= 256 and m.K * m.V < (1 << 29))
+            if fits and (strip == "1" or (strip == "auto" and 2 * sm > LDS_LIMIT
+                                          and m.n_tiles > 2 * cu)):
+                m.stage_flags |= STAGE_FWD_STRIP
+                # the 8-wave variant that prefetches the next strip's beta block (2 waves
+                # per SIMD, ~190 VGPRs) measured ahead of 16 non-prefetching waves per CU
+                # (K=200: V=112k 0.341 vs 0.346 ms, V=74k 0.251 vs 0.260 ms; the tile
+                # kernel 0.346 / 0.255); GFEDNTM_FWD_STRIP_PF=0 selects the 16-wave one
+                if os.environ.get("GFEDNTM_FWD_STRIP_PF", "1") == "1":
+                    m.stage_flags |= STAGE_FWD_STRIP_PF
+                m.dec_grid = int(min(m.n_tiles, cu))
             # backward: one workgroup per tile while the tiles fit the resident slots;
             # else persistent, n_dpart d theta_d slabs: with >= 4 k tiles the topics
             # are split over 4 workgroups per slab (csrc/prodlda.hip, 8 waves each, two

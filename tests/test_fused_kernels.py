@@ -79,6 +79,21 @@ def test_step_matches_oracle(model_type, B, n_docs, K, H, V):
     _oracle_step(model_type, B, n_docs, K, H, V)
 
 
+@pytest.mark.parametrize("B,n_docs,K,H,V", [(64, 80, 200, (50, 50), 40000),   # the auto choice
+                                            (64, 80, 50, (50, 50), 30001),    # K % 8 = 2, V % 64 != 0
+                                            (32, 45, 25, (30, 20), 7000),     # odd K, B = 32
+                                            (16, 30, 20, (32, 24), 700),      # B = 16, K % 8 = 4
+                                            (32, 60, 250, (50,), 5000)])      # K = 250 (NP = 32)
+def test_strip_forward_matches_oracle(monkeypatch, B, n_docs, K, H, V):
+    """prodlda_fwd_strip_kernel (GFEDNTM_FWD_STRIP=1 forces it): per-wave column strips,
+    beta by buffer loads straight into the MFMA B registers, k paired for ds_read_b64."""
+    monkeypatch.setenv("GFEDNTM_FWD_STRIP", "1")
+    from gfedntm_amd.ops.engine import STAGE_FWD_STRIP
+    fused, _ = _pair("prodLDA", V=V, K=K, H=H, B=B)
+    assert fused.engine._m.stage_flags & STAGE_FWD_STRIP
+    _oracle_step("prodLDA", B, n_docs, K, H, V)
+
+
 @pytest.mark.parametrize("model_type", ["prodLDA", "LDA"])
 @pytest.mark.parametrize("B,K", [(64, 50), (128, 50)])
 def test_long_rows_match_oracle(model_type, B, K):
