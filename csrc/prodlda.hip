@@ -306,11 +306,13 @@ __global__ void __launch_bounds__(PF ? 512 : 1024) prodlda_fwd_strip_kernel(GfkM
   const int lane = tid & 63, wave = uniform(tid >> 6);
   constexpr int RT = BM / 16;
   constexpr int NW = STRIP_THREADS / 64;
-  // theta_d re-staged with its own row stride KS = 8 NP + 2 (2 x odd: the 16 rows x 2
-  // floats of a half-wave's ds_read_b64 hit 32 distinct banks) and ZERO beyond K and in
+  // theta_d re-staged with its own row stride KS = 8 NP + 4 (4 x odd: ds_read_b64 banks
+  // lanes {0-31} / {32-63} over 64 banks, and rows r * KS of 16 lanes + the two lane
+  // groups' k offsets 2g then cover all 64 -- measured 45 % conflicted cycles with the
+  // 2 x odd stride a 32-bank layout would want) and ZERO beyond K and in
   // rows >= nb: the MFMA loop then needs no k masks (pairs past K multiply zero A and
   // zero B) and the rows >= nb contribute exact zeros to the logits
-  constexpr int KS = 8 * NP + 2;
+  constexpr int KS = 8 * NP + 4;
   float* th = smem;                            // [BM][KS]
   float* red = th + BM * KS;                   // [NW][BM] per-wave row partials
   float rs_[RT][4];
@@ -968,7 +970,7 @@ __host__ __device__ inline int strip_np(int K) {
 
 extern "C" size_t gfk_prodlda_fwd_smem(const GfkModel* m) {
   if (m->stage_flags & FWD_STRIP)
-    return sizeof(float) * ((size_t)m->bmax * (8 * strip_np(m->K) + 2) + (size_t)(1024 / 64) * m->bmax);
+    return sizeof(float) * ((size_t)m->bmax * (8 * strip_np(m->K) + 4) + (size_t)(1024 / 64) * m->bmax);
   const size_t KP = round_up(m->K, m->mm_bf16 ? 16 : 4);
   return sizeof(float) * ((size_t)m->bmax * m->kt + KP * LDB_F + 8 * VB);
 }
