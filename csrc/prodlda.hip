@@ -290,8 +290,8 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
 // k pairing: MFMA steps 2t and 2t + 1 take k = 8t + 2g and 8t + 2g + 1 for lane group
 // g = lane >> 4 (any bijection of k works if A and B agree), so a lane's two A operands
 // are one ds_read_b64, read one pair ahead of the MFMAs.  Strips s = tile * 4 + cs are
-// dealt to waves round-robin (the strips of a tile to neighbouring waves: their beta rows
-// share cache lines).  The per-row sum-exp partials of the waves are summed through LDS
+// dealt to waves in whole tiles (the 4 strips of a tile to the 4 waves of a wave group:
+// their beta rows share cache lines).  The per-row sum-exp partials of the waves are summed through LDS
 // once at the end and stored as the workgroup's 4 partial slots (slot 0 holds the sum,
 // 1..3 zero), so row_loss reads the same dec_grid * 4 partials as with the tile kernel.
 // Measured at K = 200 (profiles/r2/large_vocab.md): the forward 52 -> ~45 us at V = 112k,
@@ -379,7 +379,11 @@ __global__ void __launch_bounds__(PF ? 512 : 1024) prodlda_fwd_strip_kernel(GfkM
   // PF = false: no prefetch, 16 waves per CU at <= 128 VGPRs (the waves overlap each
   // other's loads instead)
   float b[2 * NP], bn[2 * NP], rm0 = 0.f, rv0 = 0.f, rmn = 0.f, rvn = 0.f;
-  int s = blockIdx.x * NW + wave;
+  // wave group gq = wave >> 2 takes whole tiles gq * grid + g, + NW / 4 * grid, ...: the
+  // 4 strips of a tile stay on one CU (their beta rows share cache lines), and the
+  // tiles of the last, partial round are spread over every CU's wave group 0 instead
+  // of all 8 waves of the first CUs, so no SIMD gets more than ceil(strips / SIMDs) + 1
+  int s = 4 * ((wave >> 2) * (int)gridDim.x + (int)blockIdx.x) + (wave & 3);
   if (PF && s < nstrips) issue(s, b, rm0, rv0);
 #pragma unroll 1
   for (; s < nstrips; s += stride) {
