@@ -113,6 +113,20 @@ def _shape_model(tm, bmax: int) -> "abi.GfkModel":
     return m
 
 
+def _force_k_split(lib, m) -> bool:
+    """ProdLDA backward at large K with few vocab tiles: the one-range shape (a workgroup
+    per tile, all K topics of theta_d and the beta tile in LDS) exceeds the LDS at
+    K = 256, B >= 64.  Then use the 4-k-range shape anyway (persistent, n_dpart < n_tiles
+    slabs; ~71 KB at K = 256).  Returns True when it set n_dpart so."""
+    if m.kind != abi.KIND_PRODLDA or m.n_tiles < 2 or -(-m.K // 16) < 4:
+        return False
+    m.n_dpart = m.n_tiles
+    if lib.gfk_smem_required(C.byref(m), 1) <= LDS_LIMIT:
+        return False
+    m.n_dpart = m.n_tiles - 1
+    return True
+
+
 def lds_required(tm, bmax: int) -> int:
     """Largest dynamic LDS any fused kernel needs for this model (weights unstaged),
     as computed by the kernel library itself."""
@@ -127,6 +141,7 @@ def lds_required(tm, bmax: int) -> int:
     m.vb, m.n_tiles = VB, -(-m.V // VB)
     m.n_dpart = m.n_tiles if m.kind == abi.KIND_PRODLDA else 1
     lib = native.kernels()
+    _force_k_split(lib, m)
     which = (0, 1) if m.kind == abi.KIND_PRODLDA else (2, 3)
     need = 0
     for flags in (0, 2):                 # weights unstaged; batch matrices in LDS, then in L2
@@ -405,6 +420,7 @@ class FusedEngine(EngineBase):
         m.adam_pow, m.adam_coef = self.adam_pow.data_ptr(), self.adam_coef.data_ptr()
         self._sync_opt_fields()
         which = (0, 1) if m.kind == abi.KIND_PRODLDA else (2, 3)
+        k_split = _force_k_split(self.lib, m)
         need = lambda: max(self.lib.gfk_smem_required(C.byref(m), w)  # noqa: E731
                            for w in which + (4, 5, 7, 8))
         for flags in STAGE_PLANS:         # first plan that fits the 160 KiB of LDS
@@ -441,13 +457,14 @@ class FusedEngine(EngineBase):
             # else persistent, n_dpart d theta_d slabs: with >= 4 k tiles the topics
             # are split over 4 workgroups per slab (csrc/prodlda.hip, 8 waves each, two
             # per CU when their LDS allows), otherwise one 16-wave workgroup per CU
+            m.n_dpart = m.n_tiles
             sb = self.lib.gfk_smem_required(C.byref(m), 1)      # one tile per workgroup
-            if m.n_tiles <= (2 if 2 * sb <= LDS_LIMIT else 1) * cu:
+            if m.n_tiles <= (2 if 2 * sb <= LDS_LIMIT else 1) * cu and not k_split:
                 m.n_dpart = m.n_tiles
             elif -(-m.K // 16) >= 4:
-                m.n_dpart = cu // 2
+                m.n_dpart = min(cu // 2, m.n_tiles - 1)
                 if 2 * self.lib.gfk_smem_required(C.byref(m), 1) > LDS_LIMIT:
-                    m.n_dpart = cu // 4
+                    m.n_dpart = min(cu // 4, m.n_tiles - 1)
             else:
                 m.n_dpart = cu
             # GFEDNTM_BETA_SPLIT=1: beta's Adam as one streaming float4 pass after

@@ -83,7 +83,8 @@ def test_step_matches_oracle(model_type, B, n_docs, K, H, V):
                                             (64, 80, 50, (50, 50), 30001),    # K % 8 = 2, V % 64 != 0
                                             (32, 45, 25, (30, 20), 7000),     # odd K, B = 32
                                             (16, 30, 20, (32, 24), 700),      # B = 16, K % 8 = 4
-                                            (32, 60, 250, (50,), 5000)])      # K = 250 (NP = 32)
+                                            (32, 60, 250, (50,), 5000),       # K = 250 (NP = 32)
+                                            (64, 150, 256, (50,), 5000)])     # K = 256, B = 64: forced k split
 def test_strip_forward_matches_oracle(monkeypatch, B, n_docs, K, H, V):
     """prodlda_fwd_strip_kernel (GFEDNTM_FWD_STRIP=1 forces it): per-wave column strips,
     beta by buffer loads straight into the MFMA B registers, k paired for ds_read_b64."""
@@ -92,6 +93,16 @@ def test_strip_forward_matches_oracle(monkeypatch, B, n_docs, K, H, V):
     fused, _ = _pair("prodLDA", V=V, K=K, H=H, B=B)
     assert fused.engine._m.stage_flags & STAGE_FWD_STRIP
     _oracle_step("prodLDA", B, n_docs, K, H, V)
+
+
+def test_large_k_few_tiles_forces_k_split(monkeypatch):
+    """K = 256, B = 64, 79 vocab tiles: the one-range backward (a workgroup per tile) needs
+    more than 160 KiB of LDS, so the engine uses the 4-k-range shape (n_dpart < n_tiles)."""
+    monkeypatch.setenv("GFEDNTM_FWD_STRIP", "0")
+    fused, _ = _pair("prodLDA", V=5000, K=256, H=(50,), B=64)
+    m = fused.engine._m
+    assert m.n_dpart < m.n_tiles
+    _oracle_step("prodLDA", 64, 150, 256, (50,), 5000)
 
 
 @pytest.mark.parametrize("model_type", ["prodLDA", "LDA"])
