@@ -272,12 +272,10 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
   }
 }
 
-// Strip forward for large K x large V (fp32, B <= 64; stage_flags bit 2, chosen by the
-// engine when the tile kernel's th + beta tile (118 KB at K = 200) admits only one
-// workgroup per CU and the vocabulary spans several rounds of them).  The tile kernel
-// runs its phases serially per tile -- staging, MFMA, two batch-norm barriers, stores.
-// Here each WAVE owns a 16-column strip of a vocab tile for ALL batch rows and works
-// through its strips independently:
+// Strip forward (fp32, B <= 64; stage_flags bit 2, the engine's default where it
+// applies).  The tile kernel above runs its phases serially per tile -- staging, MFMA,
+// two batch-norm barriers, stores.  Here each WAVE owns a 16-column strip of a vocab
+// tile for ALL batch rows and works through its strips independently:
 //  * the MFMA B operand (beta, the strip's 16 columns x K) comes straight from global
 //    memory into registers by buffer loads (one per-lane offset, rows past K read as 0),
 //    so the LDS holds theta_d alone and no beta tile;
@@ -294,8 +292,9 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
 // their beta rows share cache lines).  The per-row sum-exp partials of the waves are summed through LDS
 // once at the end and stored as the workgroup's 4 partial slots (slot 0 holds the sum,
 // 1..3 zero), so row_loss reads the same dec_grid * 4 partials as with the tile kernel.
-// Measured at K = 200 (profiles/r2/large_vocab.md): the forward 52 -> ~45 us at V = 112k,
-// rounds 0.346 -> 0.341 ms (V = 112k) and 0.255 -> 0.251 ms (V = 74k).
+// The first strip's beta block is issued behind theta_d's staging loads, so the two
+// global rounds overlap.  Measured (profiles/r2/ab_strip_forward.txt): K=50 headline
+// round 0.0589 -> 0.0583 ms, K=50 V=28k 0.101 -> 0.092, K=200 V=112k 0.349 -> 0.342.
 // NP: k pairs held in registers (compile-time, the launcher's smallest instance >= K / 8).
 template <int BM, int NP, bool PF>
 __global__ void __launch_bounds__(PF ? 512 : 1024) prodlda_fwd_strip_kernel(GfkModel m) {
@@ -323,33 +322,10 @@ __global__ void __launch_bounds__(PF ? 512 : 1024) prodlda_fwd_strip_kernel(GfkM
 
   const int nb = *m.ws_nb;
   if (blockIdx.x == 0 && tid == 0) *m.nbt_beta += 1;
-  {
-    constexpr int SU = (BM * KS + STRIP_THREADS - 1) / STRIP_THREADS;
-    float tv[SU];
-#pragma unroll
-    for (int u = 0; u < SU; ++u) {
-      // (clamped, unconditional loads: a guarded load compiles to a branch + vmcnt(0))
-      const int idx = tid + u * STRIP_THREADS, row = idx / KS, k = idx % KS;
-      tv[u] = m.ws_thetad[min(row, BM - 1) * KT + min(k, K - 1)];
-    }
-#pragma unroll
-    for (int u = 0; u < SU; ++u) asm volatile("" : "+v"(tv[u]));   // (not sunk into branches)
-#pragma unroll
-    for (int u = 0; u < SU; ++u) {
-      const int idx = tid + u * STRIP_THREADS, row = idx / KS, k = idx % KS;
-      tv[u] = (row < nb && k < K) ? tv[u] : 0.f;
-    }
-#pragma unroll
-    for (int u = 0; u < SU; ++u)
-      if (tid + u * STRIP_THREADS < BM * KS) th[tid + u * STRIP_THREADS] = tv[u];
-  }
   const int g2 = 2 * (lane >> 4);
   const float inv_nb = 1.f / (float)nb;
   const int nstrips = m.n_tiles * 4;
   const int stride = gridDim.x * NW;
-  lds_barrier();
-  asm volatile("" : "+v"(tid));
-  __builtin_assume(tid >= 0 && tid < STRIP_THREADS);
   const int arow = (lane & 15) * KS + g2;
   // beta [K, V] as a buffer resource of K V floats (K V < 2^29 checked by the launcher)
   const __amdgpu_buffer_rsrc_t bres =
@@ -375,7 +351,7 @@ __global__ void __launch_bounds__(PF ? 512 : 1024) prodlda_fwd_strip_kernel(GfkM
     rv = m.beta_rv[vc];
   };
   // software pipeline over the wave's strips: the NEXT strip's beta block is in flight
-  // while this one runs its MFMAs / batch norm / stores (2 waves per SIMD, ~160 VGPRs)
+  // while this one runs its MFMAs / batch norm / stores (2 waves per SIMD, ~190 VGPRs)
   // PF = false: no prefetch, 16 waves per CU at <= 128 VGPRs (the waves overlap each
   // other's loads instead)
   float b[2 * NP], bn[2 * NP], rm0 = 0.f, rv0 = 0.f, rmn = 0.f, rvn = 0.f;
@@ -384,7 +360,37 @@ __global__ void __launch_bounds__(PF ? 512 : 1024) prodlda_fwd_strip_kernel(GfkM
   // tiles of the last, partial round are spread over every CU's wave group 0 instead
   // of all 8 waves of the first CUs, so no SIMD gets more than ceil(strips / SIMDs) + 1
   int s = 4 * ((wave >> 2) * (int)gridDim.x + (int)blockIdx.x) + (wave & 3);
-  if (PF && s < nstrips) issue(s, b, rm0, rv0);
+  {
+    constexpr int SU = (BM * KS + STRIP_THREADS - 1) / STRIP_THREADS;
+    float tv[SU];
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      // (clamped, unconditional loads: a guarded load compiles to a branch + vmcnt(0))
+      const int idx = tid + u * STRIP_THREADS, row = idx / KS, k = idx % KS;
+      tv[u] = m.ws_thetad[min(row, BM - 1) * KT + min(k, K - 1)];
+    }
+    // the first strip's beta block is issued BEHIND theta_d's loads: waiting for those
+    // (vmcnt counts in order) leaves it in flight across the staging barrier, so the
+    // two global rounds overlap instead of following each other
+    // (unconditional, clamped: behind a branch the waitcnt pass would assume the loads
+    // absent at the join and wait for everything)
+    if (PF) issue(min(s, nstrips - 1), b, rm0, rv0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      // an integer mask, not a select: a select lets the compiler sink the load into a
+      // branch (+ vmcnt(0) each), and 0 * x would keep a NaN of the unused rows
+      const int idx = tid + u * STRIP_THREADS, row = idx / KS, k = idx % KS;
+      const unsigned keepm = (row < nb && k < K) ? ~0u : 0u;
+      tv[u] = __uint_as_float(__float_as_uint(tv[u]) & keepm);
+    }
+#pragma unroll
+    for (int u = 0; u < SU; ++u)
+      if (tid + u * STRIP_THREADS < BM * KS) th[tid + u * STRIP_THREADS] = tv[u];
+  }
+  lds_barrier();
+  asm volatile("" : "+v"(tid));
+  __builtin_assume(tid >= 0 && tid < STRIP_THREADS);
 #pragma unroll 1
   for (; s < nstrips; s += stride) {
     if (PF) issue(min(s + stride, nstrips - 1), bn, rmn, rvn);   // (the last one re-reads a strip)

@@ -438,13 +438,13 @@ class FusedEngine(EngineBase):
             m.dec_grid = int(min(m.n_tiles, (2 if 2 * sm <= LDS_LIMIT else 1) * cu))
             # strip forward (prodlda_fwd_strip_kernel, stage_flags bit 2): each wave owns
             # 16 columns x all rows, beta straight into registers, batch norm without
-            # barriers.  Chosen when the tile kernel fits only one workgroup per CU and
-            # the vocabulary spans several rounds of them (K = 200, V >= 74k);
-            # GFEDNTM_FWD_STRIP=1 forces it wherever the kernel applies, 0 disables it
+            # barriers.  The default wherever it applies (fp32, B <= 64): interleaved A/B
+            # vs the tile kernel (profiles/r2/ab_strip_forward.txt) K=50 headline 0.0583
+            # vs 0.0589 ms, K=50 V=28k 0.092 vs 0.101, K=200 V=112k 0.342 vs 0.349, CTM /
+            # ZeroShotTM K=100 neutral.  GFEDNTM_FWD_STRIP=0 selects the tile kernel
             strip = os.environ.get("GFEDNTM_FWD_STRIP", "auto")
             fits = (not m.mm_bf16 and m.bmax <= 64 and m.K <= 256 and m.K * m.V < (1 << 29))
-            if fits and (strip == "1" or (strip == "auto" and 2 * sm > LDS_LIMIT
-                                          and m.n_tiles > 2 * cu)):
+            if fits and strip in ("1", "auto"):
                 m.stage_flags |= STAGE_FWD_STRIP
                 # the 8-wave variant that prefetches the next strip's beta block (2 waves
                 # per SIMD, ~190 VGPRs) measured ahead of 16 non-prefetching waves per CU
