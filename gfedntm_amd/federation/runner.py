@@ -44,6 +44,7 @@ from ..parallel.aggregator import CollectiveAggregator, LocalAggregator, fedavg_
 from ..utils import checkpoint as ckpt
 from ..utils.config import DEFAULT_GRADS_TO_SHARE, model_kwargs_from_params
 from ..utils.logging import MetricsWriter
+from ..utils.misc import graph_capture
 from ..utils.trace import RoundWindow, trace_range
 from .client import FederatedClient
 from .data import ClientCorpus
@@ -181,7 +182,7 @@ class LocalFederation:
         if self.round_streams:
             streams = [torch.cuda.Stream(self.device) for _ in engines]
             joins = [torch.cuda.Event() for _ in engines]
-        with torch.cuda.graph(g):
+        with graph_capture(g):
             if self.round_streams:
                 main = torch.cuda.current_stream(self.device)
                 fork = torch.cuda.Event()

@@ -40,6 +40,7 @@ import torch
 from ..data.bow import BatchPlan, DeviceCSR
 from ..models.engine import EngineBase
 from ..utils.flat import ALIGN
+from ..utils.misc import graph_capture
 from . import kernel_abi as abi
 from . import native
 
@@ -1005,7 +1006,7 @@ class FusedEngine(EngineBase):
         g = torch.cuda.CUDAGraph()
         saved = (self.d_step.clone(), self.adam_t.clone(), self.adam_pow.clone(),
                  self.adam_coef.clone())
-        with torch.cuda.graph(g):
+        with graph_capture(g):
             self._launch(self.phases())
         # capture does not execute; restore the device counters defensively
         self.d_step.copy_(saved[0])

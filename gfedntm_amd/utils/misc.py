@@ -6,6 +6,8 @@ document per line, ``<id> 0 <text>``.
 from __future__ import annotations
 
 import configparser
+import contextlib
+import gc
 from typing import Any, Dict
 
 _INT_KEYS = {"ntopics", "num_iterations", "batch_size", "num_threads", "optimize_interval",
@@ -58,3 +60,24 @@ def read_config_experiments(file_path: str) -> Dict[str, Any]:
             else:
                 out[opt] = v
     return out
+
+
+@contextlib.contextmanager
+def graph_capture(g, **kw):
+    """``torch.cuda.graph(g)`` with Python's cyclic GC held off for the capture.
+
+    torch 2.10 no longer collects at capture start, so a GC pass triggered by an
+    allocation inside the capture can finalize an unreachable CUDAGraph of an earlier
+    engine; destroying its executable graph while a stream captures is illegal and
+    aborts the process.  Collect first, then disable the collector until the capture
+    ends (the garbage is freed by the next pass)."""
+    import torch
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        with torch.cuda.graph(g, **kw):
+            yield
+    finally:
+        if was:
+            gc.enable()

@@ -10,6 +10,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from gfedntm_amd.utils.misc import graph_capture
+
 pytestmark = pytest.mark.gpu
 
 
@@ -34,7 +36,7 @@ def _worker(rank, world, port, n, q):
         # graph capture: the captured kernel advances its epoch on every replay
         t = torch.zeros(n, device="cuda")
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with graph_capture(g):
             xg.allreduce_(t)
         ar = torch.arange(n, device="cuda", dtype=torch.float32)
         good = []
