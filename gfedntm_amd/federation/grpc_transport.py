@@ -131,6 +131,7 @@ class FederationServicer:
         self.aggregated = None
         self.training: Optional[threading.Thread] = None
         self.done = threading.Event()
+        self.round_ends: List[float] = []      # perf_counter() at the end of every round
         self.error: Optional[BaseException] = None
         self.rounds = 0
 
@@ -237,6 +238,7 @@ class FederationServicer:
                 msg.nndata.modelUpdate.CopyFrom(wire.model_update_from_state(self.aggregated, it))
                 list(pool.map(lambda c: call(push[c], msg), cids))
                 self.rounds = it + 1
+                self.round_ends.append(time.perf_counter())
                 if self.stop_at_num_epochs and all(
                         r.metadata.current_epoch >= r.metadata.num_max_epochs for r in replies):
                     self.logger.info("-- -- All clients reached num_epochs; stopping at round %d",
