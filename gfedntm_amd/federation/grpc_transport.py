@@ -43,6 +43,7 @@ import torch
 from ..data.vocab import union_vocabulary, vocabulary_dict
 from ..eval.export import client_model_path, save_model_as_npz, server_model_path
 from ..utils.config import DEFAULT_GRADS_TO_SHARE
+from ..utils.misc import DEVICE_LOCK
 from . import wire
 from .client import FederatedClient
 from .runner import build_dataset, make_topic_model
@@ -292,7 +293,10 @@ class ClientServicer:
         self.it = -1
         self.applied = -1
         self._last = None          # (iter, response): a retried request gets it again
-        self.lock = threading.Lock()
+        # GPU clients share the process-wide device lock: several clients served from one
+        # process must not capture / synchronise concurrently (utils.misc.graph_capture)
+        on_gpu = getattr(getattr(client.tm, "device", None), "type", "cpu") == "cuda"
+        self.lock = DEVICE_LOCK if on_gpu else threading.Lock()
 
     def getGradient(self, request, context):
         with self.lock:

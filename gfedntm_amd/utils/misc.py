@@ -8,6 +8,7 @@ from __future__ import annotations
 import configparser
 import contextlib
 import gc
+import threading
 from typing import Any, Dict
 
 _INT_KEYS = {"ntopics", "num_iterations", "batch_size", "num_threads", "optimize_interval",
@@ -62,6 +63,12 @@ def read_config_experiments(file_path: str) -> Dict[str, Any]:
     return out
 
 
+# One lock per process around graph captures and the device work of request handlers
+# that may run on several threads (gRPC clients served from one process): a capture must
+# not overlap another thread's device-wide synchronisation.
+DEVICE_LOCK = threading.RLock()
+
+
 @contextlib.contextmanager
 def graph_capture(g, **kw):
     """``torch.cuda.graph(g)`` with Python's cyclic GC held off for the capture.
@@ -70,14 +77,21 @@ def graph_capture(g, **kw):
     allocation inside the capture can finalize an unreachable CUDAGraph of an earlier
     engine; destroying its executable graph while a stream captures is illegal and
     aborts the process.  Collect first, then disable the collector until the capture
-    ends (the garbage is freed by the next pass)."""
+    ends (the garbage is freed by the next pass).
+
+    The capture mode defaults to ``thread_local``: several engines may live in one
+    process on different threads (e.g. gRPC clients served from one process), and in
+    the ``global`` mode another thread's ordinary HIP call during this thread's capture
+    fails with hipErrorIllegalState."""
     import torch
-    gc.collect()
-    was = gc.isenabled()
-    gc.disable()
-    try:
-        with torch.cuda.graph(g, **kw):
-            yield
-    finally:
-        if was:
-            gc.enable()
+    kw.setdefault("capture_error_mode", "thread_local")
+    with DEVICE_LOCK:
+        gc.collect()
+        was = gc.isenabled()
+        gc.disable()
+        try:
+            with torch.cuda.graph(g, **kw):
+                yield
+        finally:
+            if was:
+                gc.enable()

@@ -83,3 +83,55 @@ def test_fused_checkpoint_resume_is_bitwise(tmp_path, model_type):
         assert torch.equal(eb.loss_hist[:15], ef.loss_hist[:15])
         assert cb.current_epoch == cf.current_epoch and cb.samples_processed == cf.samples_processed
         assert int(eb.adam_t.item()) == int(ef.adam_t.item()) == 15
+
+
+def test_grpc_two_fused_gpu_clients_in_one_process(tmp_path):
+    """Two fused-engine clients served from ONE process over the reference gRPC protocol:
+    their graph captures and device synchronisations must not overlap (the process-wide
+    device lock and thread-local capture mode in utils.misc.graph_capture); each client
+    ends holding the server's aggregate of the last round."""
+    import socket
+    import threading
+    from gfedntm_amd.federation.grpc_transport import FederationServicer, run_client, serve
+    params = _params(num_epochs=100, batch_size=32, hidden_sizes=(32, 32), n_components=10)
+    sc = generate_synthetic(vocab_size=400, n_topics=10, n_docs=120, n_nodes=2, frozen_topics=3,
+                            nwords=(30, 60), seed=4)
+    corpora = [ClientCorpus(synthetic=sc, node=i) for i in range(2)]
+    base = None
+    for b in range(47000, 60000, 41):
+        try:
+            for p in range(b, b + 3):
+                with socket.socket() as s:
+                    s.bind(("127.0.0.1", p))
+            base = b
+            break
+        except OSError:
+            continue
+    iters = 6
+    svc = FederationServicer(params, "avitm", 2, iters, client_host="127.0.0.1", base_port=base,
+                             save_server=str(tmp_path / "server" / ""), wait_timeout=60)
+    server = serve(svc, base)
+    clients, errors = {}, []
+
+    def run(i):
+        try:
+            clients[i] = run_client(corpora[i - 1], i, f"127.0.0.1:{base}", base + i,
+                                    backend="fused", device="cuda", seed=0,
+                                    save_client=str(tmp_path / "client"), timeout=60,
+                                    max_iters=iters)
+        except BaseException as e:  # pragma: no cover - surfaced below
+            errors.append(e)
+
+    ts = [threading.Thread(target=run, args=(i,)) for i in (1, 2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(100)
+    assert svc.done.wait(10)
+    server.stop(0)
+    assert not errors, errors
+    assert svc.error is None and svc.rounds == iters
+    for c in clients.values():
+        sd = c.tm.model.state_dict()
+        for k, v in svc.aggregated.items():
+            np.testing.assert_allclose(sd[k].cpu().numpy(), v, rtol=0, atol=1e-6, err_msg=k)

@@ -67,7 +67,7 @@ def main():
     tmp = tempfile.mkdtemp(prefix="bench_grpc_")
     svc = FederationServicer(params, "avitm", args.clients, args.iters, client_host="127.0.0.1",
                              base_port=base, save_server=os.path.join(tmp, "server", ""),
-                             wait_timeout=600)
+                             wait_timeout=120)
     server = serve(svc, base)
     errors = []
 
@@ -75,7 +75,7 @@ def main():
         try:
             run_client(corpora[i - 1], i, f"127.0.0.1:{base}", base + i, backend=args.backend,
                        device=args.device, seed=0, save_client=os.path.join(tmp, "client"),
-                       timeout=600, max_iters=args.iters)
+                       timeout=120, max_iters=args.iters)
         except BaseException as e:  # pragma: no cover - reported below
             errors.append(e)
 
@@ -84,7 +84,7 @@ def main():
     for t in ts:
         t.start()
     for t in ts:
-        t.join()
+        t.join(300)
     svc.done.wait(60)
     server.stop(0)
     if errors or svc.error is not None:
