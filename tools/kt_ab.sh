@@ -9,7 +9,6 @@ for val in "$a" "$b"; do
   out="gpurun_out/kt_${var}_${val}"
   mkdir -p "$out"
   echo "=== $var=$val"
-  env "$var=$val" true
   export "$var=$val"
   timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$out/kt" -o run \
       -- python bench.py "$@" --no-npmi > "$out/kt.log" 2>&1 || exit $?
