@@ -54,6 +54,11 @@ sys.path.insert(0, ROOT)
 BASELINE_FED_DOCS_PER_S = 111.0
 BASELINE_CPU_CENTRALIZED_DOCS_PER_S = 17300.0
 METRIC = "docs/sec (whole node) + NPMI, ProdLDA K=50 8-client fed on synthetic BoW"
+# the configuration BASELINE.json's metric is quoted on (reference dft_params.cf defaults +
+# the reference generator); only a line of exactly this config carries METRIC / vs_baseline
+HEADLINE = {"family": "avitm", "model": "prodLDA", "vocab": 5000, "topics": 50, "hidden": "50,50",
+            "batch": 64, "docs": 1000, "nwords": "150,250", "dtype": "fp32", "solver": "adam",
+            "backend": "fused", "contextual_size": 768}
 
 
 def parse(argv=None):
@@ -211,25 +216,42 @@ def _ctrl_group():
     return _CTRL
 
 
-def _engine_loop(eng, s0: int, s1: int, world: int) -> float:
-    """Bare replay loop over steps [s0, s1) of an already warmed engine: seconds (max over
-    ranks), barrier + device sync on both sides."""
+def _engine_loop(eng, s0: int, s1: int, world: int):
+    """Bare replay loop over steps [s0, s1) of an already warmed engine, barrier + device
+    sync on both sides: (host wall seconds, device seconds between two events recorded
+    around the replays), each the max over ranks."""
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier(group=_ctrl_group())
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record()
     for s in range(s0, s1):
         eng.step(s)
+    ev1.record()
     torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
     if world > 1:
         dist.barrier(group=_ctrl_group())
-    return _max_over_ranks(time.perf_counter() - t0, world)
+    return _max_over_ranks(wall, world), _max_over_ranks(ev0.elapsed_time(ev1) * 1e-3, world)
+
+
+def _physical_gpus(device, world: int) -> int:
+    """Distinct GPUs under the ranks (a one-GPU rehearsal of N ranks is 1)."""
+    props = torch.cuda.get_device_properties(device)
+    key = (socket.gethostname(), props.pci_domain_id, props.pci_bus_id, props.pci_device_id)
+    if world == 1:
+        return 1
+    keys = [None] * world
+    dist.all_gather_object(keys, key, group=_ctrl_group())
+    return len(set(keys))
 
 
 def run_federated(args):
     from gfedntm_amd.federation.runner import run_distributed
     rank, world, device, rehearse = _init(args)
     _ctrl_group()
+    physical = _physical_gpus(device, world)
     sc = _corpus(args, world)
     corpus = _client_corpus(args, sc, rank)
     params = _params(args)
@@ -242,23 +264,24 @@ def run_federated(args):
     client = out["client"]
     eng = client.tm.engine
     wall = _max_over_ranks(out["wall_s"], world)
+    dev_s = out.get("device_s")
+    dev_s = None if dev_s is None else _max_over_ranks(dev_s, world)
     timed_rounds = out["timed_rounds"]
     t = torch.tensor([float(out["docs"])], dtype=torch.float64)
     dist.all_reduce(t, group=_ctrl_group())
     docs = float(t.item())                       # all clients' training documents
     ms_runner = wall / max(timed_rounds, 1) * 1e3
     # ---- the same engine's bare replay loop (collective still attached) ----
-    engine_ms = None
-    compute_ms = None
+    engine_ms = engine_dev_ms = compute_ms = None
     if args.backend == "fused":
-        dt = _engine_loop(eng, args.warmup, n_rounds, world)
-        engine_ms = dt / args.steps * 1e3
+        dt, ddev = _engine_loop(eng, args.warmup, n_rounds, world)
+        engine_ms, engine_dev_ms = dt / args.steps * 1e3, ddev / args.steps * 1e3
         err = eng.fedavg_error()
         if world > 1:
             # round split: the same steps again with the collective detached
             saved = eng.detach_fedavg(close=False)
-            dt2 = _engine_loop(eng, args.warmup, n_rounds, world)
-            compute_ms = dt2 / args.steps * 1e3
+            _, ddev2 = _engine_loop(eng, args.warmup, n_rounds, world)
+            compute_ms = ddev2 / args.steps * 1e3
             eng.restore_fedavg(saved)
         if err:
             raise RuntimeError(f"xGMI all-reduce reported error {err}")
@@ -278,25 +301,36 @@ def run_federated(args):
         value = docs / wall
         terms_n = len(client.tm.train_data.idx2token) if hasattr(client.tm.train_data, "idx2token") \
             else client.tm.input_size
-        record = _record(args, world, value, ms_runner, terms_n, npmi, final_loss)
+        record = _record(args, value, ms_runner, terms_n, npmi, final_loss, clients=world,
+                         ranks=world, physical=physical)
         record["path"] = args.path
+        record["device_ms_per_step"] = None if dev_s is None else round(dev_s / max(timed_rounds, 1) * 1e3, 5)
         record["engine_only_ms_per_step"] = None if engine_ms is None else round(engine_ms, 5)
-        record["runner_overhead_pct"] = (None if engine_ms is None else
-                                         round(100.0 * (ms_runner / engine_ms - 1.0), 2))
+        record["engine_only_device_ms_per_step"] = (None if engine_dev_ms is None
+                                                    else round(engine_dev_ms, 5))
+        record["runner_overhead_pct"] = (None if engine_dev_ms is None or dev_s is None else
+                                         round(100.0 * (dev_s / max(timed_rounds, 1) * 1e3
+                                                        / engine_dev_ms - 1.0), 2))
         if args.path == "engine" and engine_ms is not None:
             # headline from the bare replay loop instead
             record["ms_per_step"] = round(engine_ms, 5)
             record["value"] = round(world * args.batch / (engine_ms * 1e-3), 1)
-            record["vs_baseline"] = round(record["value"] / BASELINE_FED_DOCS_PER_S, 2)
+            if record["vs_baseline"] is not None:
+                record["vs_baseline"] = round(record["value"] / BASELINE_FED_DOCS_PER_S, 2)
         record["config"]["aggregation"] += f" ({used or 'none: one client'} all-reduce)"
+        if out.get("attach"):
+            record["fedavg_attach"] = out["attach"]
+        _ctx_note(record, args, eng)
         split = {"round_ms": round(record["ms_per_step"], 5)}
         if compute_ms is not None:
-            split["compute_ms"] = round(compute_ms, 5)
-            split["allreduce_exposed_ms"] = round(max(engine_ms - compute_ms, 0.0), 5)
-        split["host_ms"] = round(max(ms_runner - (engine_ms or ms_runner), 0.0), 5)
+            split["compute_device_ms"] = round(compute_ms, 5)
+            split["allreduce_exposed_device_ms"] = round(max(engine_dev_ms - compute_ms, 0.0), 5)
+        if record["device_ms_per_step"] is not None:
+            split["host_ms"] = round(max(ms_runner - record["device_ms_per_step"], 0.0), 5)
         record["round_split_ms"] = split
         if rehearse:
-            record["note"] = "GFEDNTM_REHEARSE_1GPU: all ranks on one GPU -- timings meaningless"
+            record["note"] = (f"GFEDNTM_REHEARSE_1GPU: {world} ranks share {physical} GPU -- "
+                              "protocol rehearsal, timings meaningless")
         print(json.dumps(record), flush=True)
     dist.barrier(group=_ctrl_group())
     dist.destroy_process_group()
@@ -326,33 +360,65 @@ def run_simulated(args):
         npmi = _npmi(fed2.clients[0].tm, sc, fed.terms, M, device)
     eng = fed.clients[0].tm.engine
     final_loss = float(np.mean(eng.loss_hist[max(0, n_rounds - 20): n_rounds].cpu().numpy()))
-    rec = _record(args, 1, value, ms, len(fed.terms), npmi, final_loss, clients=M)
-    rec["metric"] = f"docs/sec, ProdLDA K={args.topics} {M} simulated clients on ONE GPU"
-    rec["vs_baseline"] = None
-    rec["config"]["parallelism"] = f"fedavg-sim{M} (1 GPU)"
+    rec = _record(args, value, ms, len(fed.terms), npmi, final_loss, clients=M, ranks=1,
+                  physical=1)
+    if out.get("device_s") is not None:
+        rec["device_ms_per_step"] = round(out["device_s"] / max(out["timed_rounds"], 1) * 1e3, 5)
     rec["config"]["aggregation"] += (" (in-process FedAvg kernel in one round graph"
                                      + (", client branches" if not args.serial_clients else "") + ")"
                                      if fed.round_graph else " (eager)")
     rec["path"] = "LocalFederation"
+    _ctx_note(rec, args, eng)
     print(json.dumps(rec), flush=True)
 
 
-def _record(args, n_gpus, value, ms, V, npmi, final_loss, clients=None):
+def _ctx_note(rec, args, eng):
+    """CTM lines say whether the contextual path ran on the fused kernels or on the
+    host-GEMM fallback (and why)."""
+    if args.family == "avitm" or args.backend != "fused":
+        return
+    why = getattr(eng, "ctx_fallback_reason", None)
+    rec["ctx_path"] = "fused kernels" if why is None else f"host-GEMM fallback: {why}"
+
+
+def _is_headline(args) -> bool:
+    return all(getattr(args, k) == v for k, v in HEADLINE.items())
+
+
+def _metric(args, V, clients: int, ranks: int, physical: int) -> str:
+    """BASELINE.json's metric string for the headline config (one client per GPU);
+    otherwise a label derived from what actually ran."""
+    if _is_headline(args) and clients == ranks and physical == ranks:
+        return METRIC
+    fam = {"avitm": "ProdLDA" if args.model == "prodLDA" else "NeuralLDA",
+           "ctm": "CombinedTM", "zeroshot": "ZeroShotTM"}[args.family]
+    ctx = f" C={args.contextual_size}" if args.family != "avitm" else ""
+    where = (f"{clients} clients" + (f" on {ranks} ranks" if ranks != clients else "")
+             + f" on {physical} GPU" + ("s" if physical != 1 else ""))
+    return (f"docs/sec (whole node), {fam} K={args.topics} V={V} H=({args.hidden}){ctx} "
+            f"{args.dtype}, {where}, synthetic BoW")
+
+
+def _record(args, value, ms, V, npmi, final_loss, clients: int, ranks: int, physical: int):
     hidden = tuple(int(h) for h in args.hidden.split(","))
-    clients = n_gpus if clients is None else clients
     fam = {"avitm": "", "ctm": "CombinedTM-", "zeroshot": "ZeroShotTM-"}[args.family]
     ctx = f" C={args.contextual_size}" if args.family != "avitm" else ""
+    metric = _metric(args, V, clients, ranks, physical)
+    headline = metric == METRIC
     return {
-        "metric": METRIC,
+        "metric": metric,
         "value": round(value, 1),
         "unit": "docs/s",
-        "n_gpus": n_gpus,
+        "n_gpus": physical,
+        "ranks": ranks,
+        "physical_gpus": physical,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms, 5),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": round(value / BASELINE_FED_DOCS_PER_S, 2),
+        # only the headline config is comparable with the reference's 8-client number
+        "vs_baseline": round(value / BASELINE_FED_DOCS_PER_S, 2) if headline else None,
         "dtype": args.dtype,
         "data": (f"synthetic (reference LDA generator: V={args.vocab}, K={args.topics}, "
                  f"{args.docs} docs/client, {args.nwords.replace(',', '-')} tokens, "
@@ -360,13 +426,14 @@ def _record(args, n_gpus, value, ms, V, npmi, final_loss, clients=None):
         "config": {"model": f"{fam}{args.model}{ctx} K={args.topics} H={hidden} V={V}",
                    "global_batch": args.batch * clients, "seq_len": None,
                    "per_client_batch": args.batch, "clients": clients,
-                   "parallelism": f"fedavg-dp{clients}",
+                   "parallelism": (f"fedavg-dp{clients}" if clients == ranks else
+                                   f"fedavg {clients} clients / {ranks} ranks"),
                    "backend": args.backend + ("" if args.no_graph else "+hipgraph"),
                    "solver": args.solver,
                    "aggregation": "per-minibatch sample-weighted FedAvg of the shared state"},
         "clients_note": ("one client: FedAvg over one client is the identity; the 8-client "
                          "figure is the --gpus 8 run" if clients == 1 else
-                         f"{clients} federated clients"),
+                         f"{clients} federated clients on {physical} physical GPU(s)"),
         **({"precision": "bf16 operands of the ProdLDA decoder GEMMs (theta.beta, theta^T.dlogit, "
                          "dlogit.beta^T) on v_mfma_f32_16x16x16_bf16, fp32 accumulation; fp32 "
                          "parameters, Adam state and every other op"} if args.dtype == "bf16" else {}),
@@ -376,7 +443,6 @@ def _record(args, n_gpus, value, ms, V, npmi, final_loss, clients=None):
         "baseline": {"fed_grpc_8clients_docs_per_s": BASELINE_FED_DOCS_PER_S,
                      "cpu_centralized_docs_per_s": BASELINE_CPU_CENTRALIZED_DOCS_PER_S},
     }
-
 
 def run(args):
     if args.sim_clients:

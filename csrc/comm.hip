@@ -282,6 +282,12 @@ extern "C" int gfk_comm_error(const GfkComm* c) {
   return v;
 }
 
+// The error word copied to (pinned) host memory behind the stream's work: the runner polls
+// it between rounds without synchronising the device.
+extern "C" int gfk_comm_error_async(const GfkComm* c, int32_t* host, hipStream_t s) {
+  return (int)hipMemcpyAsync(host, c->err, sizeof(int32_t), hipMemcpyDeviceToHost, s);
+}
+
 extern "C" int gfk_comm_launch(const GfkComm* c, float* data, hipStream_t s) {
   if (c->world < 1 || c->world > CMAX || c->nblk < 1 || (c->chunk & 3) || (c->slice & 3) ||
       (int64_t)c->slice * c->nblk < c->chunk || (int64_t)c->chunk * c->world < c->n ||

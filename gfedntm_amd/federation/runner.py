@@ -150,8 +150,11 @@ class LocalFederation:
         # plus the eager aggregation), each client on its own stream: parallel graph
         # branches joined before the FedAvg kernel (8 clients: 0.35 ms / round
         # with branches vs 0.49 ms serialised, profiles/sim_clients.md)
+        # (engines on the CTM host-GEMM fallback stay out of it: their hipBLASLt GEMMs
+        # would run for the first time on the capture's per-client branch streams)
         can = (agg == "params" and graph and self.device.type == "cuda"
-               and all(c.fused for c in self.clients) and len(self.clients) > 1
+               and all(c.fused and not c.tm.engine.host_gemm_fallback for c in self.clients)
+               and len(self.clients) > 1
                and self.agg._native([c.shared for c in self.clients]))
         self.round_graph = can if round_graph is None else (bool(round_graph) and can)
         self.round_streams = bool(round_streams)
@@ -200,10 +203,16 @@ class LocalFederation:
             if not self.agg.fused_sum_(shared):
                 raise RuntimeError("round graph needs the native FedAvg kernel")
         self._rg = g
+        self._rg_gens = self._engine_gens()
+
+    def _engine_gens(self):
+        return tuple(c.tm.engine.graph_gen for c in self.clients)
 
     def _round_graph_step(self, it: int):
         for c in self.clients:
             c.tm.engine.sync_step_counter(it)     # no-op unless resuming / out of sequence
+        if self._rg is not None and self._rg_gens != self._engine_gens():
+            self._rg = None           # an engine was rebound / reconfigured since the capture
         if self._rg is None:
             self._capture_round()
         self._rg.replay()
@@ -237,6 +246,8 @@ class LocalFederation:
         last = start - 1
         self._stop = False
         win = RoundWindow(self._sync)
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) \
+            if (self.device.type == "cuda" and timing_warmup) else None
         with trace_range("rounds"):
             for it in range(self.round, self.max_iters):
                 self._round(it)
@@ -246,12 +257,17 @@ class LocalFederation:
                 if timing_warmup and it == start + timing_warmup - 1:
                     self._sync()
                     t0 = time.perf_counter()
+                    if ev is not None:
+                        ev[0].record()
                     timed_from = it + 1
                     win.reset()
                 if self._stop:
                     break
+        if ev is not None:
+            ev[1].record()
         self._sync()
         wall = time.perf_counter() - t0
+        device_s = ev[0].elapsed_time(ev[1]) * 1e-3 if ev is not None and timed_from > start else None
         n_rounds = last + 1 - timed_from
         docs = sum(int(c.plan.size[timed_from:last + 1].sum()) for c in self.clients) \
             if n_rounds > 0 else 0
@@ -262,7 +278,8 @@ class LocalFederation:
                            ms_per_round=1e3 * wall / max(n_rounds, 1))
         with trace_range("finish"):
             self.finish()
-        return {"rounds": self.round, "timed_rounds": n_rounds, "wall_s": wall, "docs": docs}
+        return {"rounds": self.round, "timed_rounds": n_rounds, "wall_s": wall, "docs": docs,
+                "device_s": device_s}
 
     def _after_round(self, it: int, win: RoundWindow, done: List[bool]):
         self.round = it + 1
@@ -439,6 +456,23 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
                             f"(error {int(flag.item())}); the shared state is invalid -- "
                             "resume from the last round checkpoint")
 
+    # a timed-out xGMI wait is also caught between the aligned rounds: every poll_every
+    # rounds each rank reads the error word copied behind its enqueued rounds (no device
+    # sync) and the ranks agree on it over the control plane, so a run fails within about
+    # two poll intervals of the timeout instead of training on for the whole run
+    poll_every = int(os.environ.get("GFEDNTM_COMM_POLL", "512")) \
+        if in_step is not None and in_step.startswith("xgmi") else 0
+
+    def poll_comm(it: int):
+        err = tm.engine.fedavg_error_poll()
+        flag = torch.tensor([int(err)], dtype=torch.int64)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=ctrl)
+        if int(flag.item()):
+            raise CommError(f"rank {rank}: an xGMI all-reduce wait timed out before round "
+                            f"{it + 1} (error {int(flag.item())}); the shared state is invalid "
+                            "-- resume from the last round checkpoint")
+        tm.engine.fedavg_error_async()
+
     def meet(where: str):
         sync()
         check_comm(where)
@@ -446,6 +480,10 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
 
     dist.barrier(group=ctrl)
     win = RoundWindow(sync)
+    # device time of the timed rounds: events on the round stream around them (the host
+    # wall clock below brackets the same rounds with a sync + barrier)
+    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) \
+        if (device.type == "cuda" and timing_warmup) else None
     t0 = time.perf_counter()
     timed_from = start
     last = start - 1
@@ -477,12 +515,16 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
                 if hb is not None:
                     hb.busy(False)
                 dist.barrier(group=ctrl)
+            if poll_every and (it + 1) % poll_every == 0 and it != stop_after:
+                poll_comm(it)
             if round_hook is not None:
                 round_hook(it)
             win.add(int(client.plan.size[it]))
             if timing_warmup and it == start + timing_warmup - 1:
                 meet("the timed region")
                 t0 = time.perf_counter()
+                if ev is not None:
+                    ev[0].record()
                 timed_from = it + 1
                 win.reset()
             if metrics_every and (it + 1) % metrics_every == 0:
@@ -498,8 +540,11 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
                     if hb is not None:
                         hb.busy(False)
                     dist.barrier(group=ctrl)
+    if ev is not None:
+        ev[1].record()
     sync()
     wall = time.perf_counter() - t0
+    device_s = ev[0].elapsed_time(ev[1]) * 1e-3 if ev is not None and timed_from > start else None
     check_comm("the end of training")
     client.flush()
     n_rounds = last + 1 - timed_from
@@ -517,4 +562,5 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
     if hb is not None:
         hb.stop()
     return {"rounds": last + 1, "timed_rounds": n_rounds, "wall_s": wall, "docs": docs,
-            "client": client, "allreduce": in_step}
+            "device_s": device_s, "client": client, "allreduce": in_step,
+            "attach": getattr(tm.engine, "fedavg_attach", None) if in_step else None}

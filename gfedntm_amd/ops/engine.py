@@ -269,6 +269,7 @@ class FusedEngine(EngineBase):
         # to host-issued GEMMs for shapes outside the kernels' plan; that path runs in
         # gradient mode with the generic optimizer kernel
         self.ctx_fused = tm.kind == "ctm"
+        self.ctx_fallback_reason: Optional[str] = None
         # Adam runs in the kernels' epilogues; the other solvers in gradient mode
         # (kernels write gradients, the generic optimizer kernel applies the rule)
         self.solver = tm.solver
@@ -285,6 +286,7 @@ class FusedEngine(EngineBase):
         self._host_step = 0
         self.graph_enabled = False
         self._graph = None
+        self.graph_gen = 0
         self._graph_key = None
         self._comm = None
         self._m = abi.GfkModel()
@@ -493,8 +495,7 @@ class FusedEngine(EngineBase):
             # gradient + Adam are ceil(C / 64) extra win_update tiles
             m.ctx_fused = 2 if int(m.H[0]) <= 512 else 0
             if not m.ctx_fused:
-                self.ctx_fused = False
-                self.update_mode = UPDATE_GRAD
+                self._ctx_fallback(f"H0 = {int(m.H[0])} > 512")
             return
         n_tiles, Cs = -(-int(m.V) // VB), int(m.C)
         k = max(1, min(cu // n_tiles, -(-Cs // 16)))      # one round, one workgroup per CU
@@ -502,11 +503,27 @@ class FusedEngine(EngineBase):
         m.ctx_kb = -(-Cs // m.ctx_ckb)
         m.ctx_fused = 1
         aligned = self.flat.slots["inf_net.adapt_bert.weight"].offset % 4 == 0
-        if (self.lib.gfk_smem_required(C.byref(m), 8) > LDS_LIMIT or int(m.H[0]) > 512
-                or Cs % 4 or not aligned):
+        why = [w for ok, w in (
+            (self.lib.gfk_smem_required(C.byref(m), 8) <= LDS_LIMIT, "LDS plan exceeds 160 KiB"),
+            (int(m.H[0]) <= 512, f"H0 = {int(m.H[0])} > 512"),
+            (Cs % 4 == 0, f"contextual_size = {Cs} is not a multiple of 4"),
+            (aligned, "adapt_bert is not 16-byte aligned in the flat buffer")) if not ok]
+        if why:
             m.ctx_fused, m.ctx_kb = 0, 0
-            self.ctx_fused = False
-            self.update_mode = UPDATE_GRAD
+            self._ctx_fallback("; ".join(why))
+
+    def _ctx_fallback(self, why: str):
+        """Leave the fused contextual kernels for host-issued hipBLASLt GEMMs (gradient
+        mode + the generic optimizer kernel).  Logged, and visible as
+        ``ctx_fallback_reason`` (the bench records it): the GEMMs are launched between
+        the fused kernels on the step's stream, and cost several extra dispatches and the
+        [B, V] adapted matrix's round trip through HBM per step."""
+        import logging
+        self.ctx_fused = False
+        self.update_mode = UPDATE_GRAD
+        self.ctx_fallback_reason = why
+        logging.getLogger("gfedntm_amd.engine").warning(
+            "CTM contextual path on host GEMMs (fused ctx kernels unavailable: %s)", why)
 
     def _alloc_workspace(self):
         m, dev = self._m, self.device
@@ -765,6 +782,10 @@ class FusedEngine(EngineBase):
             parts = {"rest": shared[:b0], "beta": shared[b0:]}
         aggs = {k: CollectiveAggregator(group, method=method) for k in parts}
         methods = {k: aggs[k].prepare(v) for k, v in parts.items()}
+        # setup cost of the data plane (IPC mapping, validation, RCCL-vs-xGMI timing)
+        self.fedavg_attach = {"s": round(sum(a.setup_s for a in aggs.values()), 4),
+                              "bytes": {k: 4 * v.numel() for k, v in parts.items()},
+                              "tuning": {k: a.tuning for k, a in aggs.items() if a.tuning}}
         if all(m == "xgmi" for m in methods.values()):
             c = {"mode": "graph", "rest": (aggs["rest"], parts["rest"])}
             if "beta" in parts:
@@ -811,6 +832,30 @@ class FusedEngine(EngineBase):
                 err = err or self._comm[k][0].xgmi.error()
         return err
 
+    def fedavg_error_async(self):
+        """Start a non-blocking read of the xGMI error words (behind the enqueued rounds);
+        :meth:`fedavg_error_poll` returns it once the copies have landed."""
+        if self._comm is None or self._comm["mode"] != "graph":
+            return
+        c = self._comm
+        if "err_host" not in c:
+            c["err_host"] = torch.zeros(2, dtype=torch.int32, pin_memory=True)
+            c["err_ev"] = torch.cuda.Event()
+        for i, k in enumerate(("rest", "beta")):
+            if k in c and c[k][0].xgmi is not None:
+                c[k][0].xgmi.error_async(c["err_host"][i:i + 1])
+        c["err_ev"].record()
+        c["err_pending"] = True
+
+    def fedavg_error_poll(self) -> int:
+        """The error word of the last :meth:`fedavg_error_async` if it has landed, else 0
+        (not known yet); never synchronises."""
+        c = self._comm
+        if not c or not c.get("err_pending") or not c["err_ev"].query():
+            return 0
+        c["err_pending"] = False
+        return int(c["err_host"].max().item())
+
     def _fedavg_beta(self):
         c = self._comm
         cur = torch.cuda.current_stream(self.device)
@@ -831,14 +876,16 @@ class FusedEngine(EngineBase):
 
     # ------------------------------------------------------------------ CTM
     def _alloc_ctx(self):
-        """CTM contextual path (reference ctm inference_network.py:97-193).  The
-        dense GEMMs -- adapt_bert [B,C]x[C,V], the contextual half of input_layer
-        [B,V]x[V,H0] and their weight gradients -- are plain library GEMMs
-        (hipBLASLt through torch, fp32), issued on the step's stream between the
-        fused kernels: CTX_FWD fills ws_hctx (added to the input layer's
-        pre-activation by enc_in), CTX_BWD turns enc's d z0 into the gradients of
-        the contextual tensors (generic Adam follows).  The BoW half of input_layer
-        stays on the sparse enc_in / win_update path."""
+        """Buffers of the CTM contextual path (reference ctm inference_network.py:97-193)
+        when it runs on host-issued GEMMs.  The default path is the fused kernels
+        (_plan_ctx: CombinedTM's ctx_fwd / ctx_bwd in csrc/ctx.hip, ZeroShotTM's dense
+        input layer in enc_in / win_update); these buffers serve (a) the fallback for
+        shapes outside the kernels' plan (C % 4, H0 > 512, LDS, alignment -- logged by
+        _ctx_fallback), where adapt_bert [B,C]x[C,V], the contextual half of
+        input_layer [B,V]x[V,H0] and their weight gradients are hipBLASLt GEMMs on the
+        step's stream between the fused kernels (CTX_FWD fills ws_hctx, CTX_BWD turns
+        d z0 into the contextual gradients, the generic optimizer kernel follows), and
+        (b) the dense contextual term of theta inference (_ctx_dense)."""
         self._ctx = None
         if self.kind != "ctm":
             return
@@ -988,7 +1035,16 @@ class FusedEngine(EngineBase):
         self._launch(phases)
 
     def _invalidate_graph(self):
+        # the generation lets external captures (LocalFederation's round graph) see that
+        # the kernel arguments / buffers they baked in are stale
         self._graph = None
+        self.graph_gen += 1
+
+    @property
+    def host_gemm_fallback(self) -> bool:
+        """True when the CTM contextual path runs as host-issued library GEMMs (shapes
+        outside the fused ctx kernels' plan, see _plan_ctx)."""
+        return self.kind == "ctm" and not self.ctx_fused
 
     def enable_graph(self, on: bool = True):
         self.graph_enabled = on

@@ -49,10 +49,18 @@ class CollectiveAggregator:
         self.xgmi = None
         self.active = "rccl"
         self.tuning = None
+        self.setup_s = 0.0
 
     def prepare(self, flat: torch.Tensor) -> str:
         """Choose the all-reduce for buffers shaped like ``flat`` (call once, on every
         rank, before the timed / captured region).  Returns the method in use."""
+        t_setup = time.perf_counter()
+        try:
+            return self._prepare(flat)
+        finally:
+            self.setup_s = time.perf_counter() - t_setup
+
+    def _prepare(self, flat: torch.Tensor) -> str:
         if self.world == 1 or self.method == "rccl" or flat.device.type != "cuda":
             self.active = "rccl"
             return self.active
@@ -77,14 +85,24 @@ class CollectiveAggregator:
             # slowest rank's time decides, so every rank takes the same branch).  The
             # xGMI kernel keeps a 10 % edge: it is captured in the step graph and
             # overlapped with the backward, RCCL runs after the step.
-            tx = self._time(xg.allreduce_, flat)
+            # the warm-up launches run before the timing barrier, with the ranks only
+            # loosely aligned: the generous validation spin bound, and a timed-out wait
+            # (sticky error word) counts as a failed validation instead of surfacing as a
+            # CommError after training
+            spin = xg.c.spin_limit
+            xg.c.spin_limit = max(spin, 1 << 26)
+            try:
+                tx = self._time(xg.allreduce_, flat)
+            finally:
+                xg.c.spin_limit = spin
+            err = xg.error()
             tr = self._time(lambda b: dist.all_reduce(b, group=self.group), flat)
-            t = torch.tensor([tx, tr], dtype=torch.float64, device=flat.device)
+            t = torch.tensor([tx, tr, float(err != 0)], dtype=torch.float64, device=flat.device)
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
-            tx, tr = (float(v) for v in t.tolist())
+            tx, tr, bad = (float(v) for v in t.tolist())
             self.tuning = {"xgmi_ms": round(tx, 4), "rccl_ms": round(tr, 4),
                            "bytes": 4 * flat.numel()}
-            if tr < 0.9 * tx:
+            if tr < 0.9 * tx or bad:
                 ok = False
         if ok:
             self.xgmi, self.active = xg, "xgmi"

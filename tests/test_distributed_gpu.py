@@ -51,10 +51,12 @@ def _params():
     return p
 
 
-def _worker(rank, world, port, tmp, stall, spin, q):
+def _worker(rank, world, port, tmp, stall, spin, q, poll=None, rounds=ROUNDS, epochs=2):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     if spin is not None:
         os.environ["GFEDNTM_XGMI_SPIN"] = str(spin)
+    if poll is not None:
+        os.environ["GFEDNTM_COMM_POLL"] = str(poll)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
     try:
@@ -65,7 +67,8 @@ def _worker(rank, world, port, tmp, stall, spin, q):
                 time.sleep(stall)
 
         try:
-            out = run_distributed(_corpora()[rank], _params(), max_iters=ROUNDS, backend="fused",
+            params = dict(_params(), num_epochs=epochs)
+            out = run_distributed(_corpora()[rank], params, max_iters=rounds, backend="fused",
                                   seed=5, save_client=os.path.join(tmp, "client"),
                                   stamp="20240101", rehearse_1gpu=True, round_hook=hook)
         except CommError as e:
@@ -82,12 +85,12 @@ def _worker(rank, world, port, tmp, stall, spin, q):
         dist.destroy_process_group()
 
 
-def _run(tmp, stall, spin=None):
+def _run(tmp, stall, spin=None, **kw):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     world = len(SIZES)
-    ps = [ctx.Process(target=_worker, args=(r, world, port, str(tmp), stall, spin, q))
+    ps = [ctx.Process(target=_worker, args=(r, world, port, str(tmp), stall, spin, q), kwargs=kw)
           for r in range(world)]
     for p in ps:
         p.start()
@@ -121,3 +124,15 @@ def test_run_distributed_fails_loudly_on_a_timed_out_wait(tmp_path):
     res = _run(tmp_path, stall=2.0, spin=2000)
     for r in res:
         assert r[1] == "comm_error", r[:2]
+
+
+def test_timed_out_wait_is_caught_between_aligned_rounds(tmp_path):
+    """No host-heavy round before the end (num_epochs never reached, no checkpoints, no
+    metrics): the periodic error-word poll still stops every rank within a few rounds of
+    the timeout (the host may run ahead of the device by the enqueued rounds) instead of
+    training on to max_iters on invalid shared state."""
+    res = _run(tmp_path, stall=2.0, spin=2000, poll=4, rounds=400, epochs=10 ** 6)
+    for r in res:
+        assert r[1] == "comm_error", r[:2]
+        before = int(r[2].split("before round ")[1].split()[0])
+        assert before < 400, r[2]         # stopped before max_iters

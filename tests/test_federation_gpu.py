@@ -135,3 +135,56 @@ def test_grpc_two_fused_gpu_clients_in_one_process(tmp_path):
         sd = c.tm.model.state_dict()
         for k, v in svc.aggregated.items():
             np.testing.assert_allclose(sd[k].cpu().numpy(), v, rtol=0, atol=1e-6, err_msg=k)
+
+
+def _ctx_corpora(n_nodes, C, seed=7, labels=0):
+    sc = generate_synthetic(vocab_size=400, n_topics=10, n_docs=80, n_nodes=n_nodes,
+                            frozen_topics=2, nwords=(30, 60), seed=seed)
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n_nodes):
+        emb = rng.standard_normal((sc.counts[i].shape[0], C)).astype(np.float32)
+        out.append(ClientCorpus(synthetic=sc, node=i, embeddings=emb))
+    return out
+
+
+@pytest.mark.parametrize("model_type,C", [("ctm", 64), ("zeroshot", 64), ("ctm", 30)])
+def test_round_graph_matches_per_client_graphs(model_type, C):
+    """CombinedTM / ZeroShotTM federations: the one-graph-per-round path equals the
+    per-client step graphs + eager FedAvg kernel bit for bit.  C = 30 (C % 4 != 0) puts
+    CombinedTM on the host-GEMM fallback, which must stay out of the round graph."""
+    corpora = _ctx_corpora(3, C)
+    p = _params(contextual_size=C)
+    kw = dict(model_type=model_type, max_iters=6, device="cuda", backend="fused", seed=5)
+    rg = LocalFederation(corpora, p, round_graph=True, **kw)
+    ref = LocalFederation(corpora, p, round_graph=False, **kw)
+    fallback = any(c.tm.engine.host_gemm_fallback for c in rg.clients)
+    assert fallback == (C % 4 != 0)
+    assert rg.round_graph == (not fallback) and not ref.round_graph
+    rg.run()
+    ref.run()
+    for a, b in zip(rg.clients, ref.clients):
+        assert torch.equal(a.tm.flat.buffer, b.tm.flat.buffer)
+        assert torch.equal(a.tm.engine.loss_hist[:6], b.tm.engine.loss_hist[:6])
+
+
+def test_round_graph_recaptures_after_engine_change():
+    """An engine reconfigured between run() calls (here: a new learning rate, which
+    rebuilds the optimizer tables and invalidates the engine's graph) must not be
+    replayed through a stale round graph."""
+    sc = generate_synthetic(vocab_size=400, n_topics=10, n_docs=90, n_nodes=2, frozen_topics=2,
+                            nwords=(30, 60), seed=8)
+    corpora = [ClientCorpus(synthetic=sc, node=i) for i in range(2)]
+    kw = dict(device="cuda", backend="fused", seed=9)
+    a = LocalFederation(corpora, _params(), max_iters=9, round_graph=True, **kw)
+    b = LocalFederation(corpora, _params(), max_iters=9, round_graph=False, **kw)
+    for fed in (a, b):
+        fed.max_iters = 4           # (the clients' batch plans cover 9 rounds)
+        fed.run()
+        for c in fed.clients:
+            c.tm.engine.set_lr(5e-3)
+        fed.max_iters = 9
+        fed.run()
+    assert a.round == b.round == 9
+    for x, y in zip(a.clients, b.clients):
+        assert torch.equal(x.tm.flat.buffer, y.tm.flat.buffer)

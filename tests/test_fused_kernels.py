@@ -647,3 +647,44 @@ def test_ctm_label_head_fused_update_trains():
             torch.cuda.synchronize()
             ce.append(float(tm.engine.ws["ce"][:64].sum()))
     assert np.isfinite(ce).all() and ce[1] < 0.85 * ce[0], ce
+
+
+@pytest.mark.parametrize("model_type", ["prodLDA", "LDA"])
+def test_ctm_host_gemm_fallback_matches_oracle(model_type):
+    """C % 4 != 0 is outside the fused contextual kernels' plan: the engine says why, runs
+    adapt_bert / the contextual input half as host GEMMs between its kernels (gradient
+    mode + generic optimizer), and the step still matches the fp32 oracle."""
+    from gfedntm_amd.models import CombinedTM
+    V, K, H, B, n_docs, Cdim = 500, 20, (32, 24), 64, 150, 30
+    torch.manual_seed(0)
+    kw = dict(input_size=V, contextual_size=Cdim, n_components=K, model_type=model_type,
+              hidden_sizes=H, batch_size=B, verbose=False, device="cuda")
+    fused = CombinedTM(backend="fused", **kw)
+    ref = CombinedTM(backend="torch", **kw)
+    ref.model.load_state_dict(fused.model.state_dict())
+    e = fused.engine
+    assert not e.ctx_fused and e.host_gemm_fallback and e.update_mode == UPDATE_GRAD
+    assert "multiple of 4" in e.ctx_fallback_reason
+    X = random_csr(n_docs, V, 40, seed=1)
+    ctx = np.random.default_rng(2).standard_normal((n_docs, Cdim)).astype(np.float32)
+    data = DeviceCSR(X, "cuda", contextual=ctx)
+    plan = BatchPlan.build(data.n_docs, B, 3, seed=0)
+    e.bind_data(data, plan)
+    phases = e.phases()
+    assert abi.PH_CTX_FWD in phases and abi.PH_CTX_BWD in phases and phases[-1] == abi.PH_ADAM
+    e.run_phases(phases[:-1])
+    torch.cuda.synchronize()
+    nb = int(plan.size[0])
+    ids = torch.from_numpy(plan.batch(0).astype(np.int64)).cuda()
+    x, xc = data.dense_rows(ids), data.contextual[ids]
+    eps, mask_h, mask_t = (e.ws[k][:nb].clone() for k in ("eps", "mask_h", "mask_t"))
+    ref.model.train()
+    ref.model.zero_grad()
+    net = ref.model.inf_net
+    x_enc = torch.cat([x, net.adapt_bert(xc)], 1)
+    loss, kl, rl = avitm_loss_explicit(ref.model, x, eps, mask_h, mask_t,
+                                       kl_weight=float(ref.weights.get("beta", 1.0)), x_enc=x_enc)
+    loss.backward()
+    torch.testing.assert_close(e.ws["kl"][:nb], kl.detach(), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(e.ws["rl"][:nb], rl.detach(), rtol=1e-4, atol=1e-2)
+    _check_grads(_grads_of(fused), ref)
