@@ -69,6 +69,9 @@ def parse(argv=None):
     p.add_argument("--path", default="runner", choices=["runner", "engine"])
     p.add_argument("--sim-clients", type=int, default=0,
                    help="M > 0: M simulated clients on one GPU (LocalFederation round graph)")
+    p.add_argument("--unbatched", action="store_true",
+                   help="--sim-clients: one graph branch per client instead of one batched "
+                        "launch per phase for all clients (grid z = client)")
     p.add_argument("--serial-clients", action="store_true",
                    help="--sim-clients: capture the clients' steps one after the other "
                         "(default: each client on its own graph branch)")
@@ -347,7 +350,8 @@ def run_simulated(args):
     n_rounds = args.warmup + args.steps
     fed = LocalFederation(corpora, _params(args), _model_type(args), n_rounds, device=device,
                           backend=args.backend, seed=args.seed, graph=not args.no_graph,
-                          round_streams=not args.serial_clients)
+                          round_streams=not args.serial_clients,
+                          round_batched=not args.unbatched)
     out = fed.run(timing_warmup=args.warmup)
     ms = out["wall_s"] / max(out["timed_rounds"], 1) * 1e3
     value = out["docs"] / out["wall_s"]
@@ -364,8 +368,9 @@ def run_simulated(args):
                   physical=1)
     if out.get("device_s") is not None:
         rec["device_ms_per_step"] = round(out["device_s"] / max(out["timed_rounds"], 1) * 1e3, 5)
-    rec["config"]["aggregation"] += (" (in-process FedAvg kernel in one round graph"
-                                     + (", client branches" if not args.serial_clients else "") + ")"
+    mode = ("batched kernels (grid z = client)" if fed._batched is not None else
+            "client branches" if not args.serial_clients else "serial clients")
+    rec["config"]["aggregation"] += (f" (in-process FedAvg kernel in one round graph, {mode})"
                                      if fed.round_graph else " (eager)")
     rec["path"] = "LocalFederation"
     _ctx_note(rec, args, eng)

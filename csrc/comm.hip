@@ -21,6 +21,14 @@
 // it); every wait is bounded: on timeout the workgroup records an error word and
 // finishes (the host checks it), it never hangs the device.
 //
+// In-place mode (large shared states, e.g. beta at V ~ 100k: 90 MB): the data buffer
+// itself is IPC-mapped into every peer, so phase 0 is only the publish (no copy of the
+// whole state into the stage: 2 S of local HBM traffic saved); phase 1 writes the reduced
+// chunk back into the data with system-scope stores; and a phase 3 publish / await keeps
+// every rank from returning -- and its next step from overwriting its data -- before all
+// peers have read their chunks from it.  The system release in the phase-0 publish writes
+// the step kernels' dirty L2 lines back, so the peers' system-scope loads see them.
+//
 // Visibility across devices (MI355X_MICROARCH.md inter-workgroup rules, lifted
 // to system scope): payload stores sc0 sc1 (write-through) -> s_waitcnt
 // vmcnt(0) -> barrier -> system release -> one lane per rank stores the flag at
@@ -38,12 +46,14 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 }  // namespace
 
 struct GfkComm {
-  float* stage[2][CMAX];         // every rank's stage buffers (own one included)
-  uint32_t* flags[CMAX];         // every rank's flag array [2][nblk][CMAX]
+  float* stage[2][CMAX];         // every rank's stage buffers (own one included); in-place:
+                                 // every rank's DATA buffer (both entries)
+  uint32_t* flags[CMAX];         // every rank's flag array [2 (3 in-place)][nblk][CMAX]
   uint32_t* epoch;               // own per-workgroup round counter [nblk]
   int32_t* err;                  // own error word (timeouts)
   int32_t rank, world, nblk, spin_limit;
   int64_t n, chunk, slice;       // floats; chunk, slice multiples of 4
+  int32_t inplace, pad;          // 1: the data buffers themselves are IPC-mapped (no stage)
 };
 
 namespace {
@@ -133,14 +143,16 @@ extern "C" __global__ void __launch_bounds__(CT) gfk_xgmi_allreduce(GfkComm c, f
 
   // (slices are float4-aligned; only the last one of the last chunk can end in a
   // partial float4, handled element-wise: nothing past n is ever touched)
-  // ---- phase 0: publish slice b of every chunk ----
-  for (int ch = 0; ch < W; ++ch) {
-    int64_t s0, s1;
-    slice_range(c, ch, b, s0, s1);
-    const int64_t s4 = s0 + ((s1 - s0) & ~(int64_t)3);
-    for (int64_t i = s0 + 4 * t; i < s4; i += 4 * CT)
-      st_sys(mine, i, *reinterpret_cast<const float4*>(data + i));
-    if (s4 + t < s1) st_sys1(mine, s4 + t, data[s4 + t]);
+  // ---- phase 0: publish slice b of every chunk (in-place: the data is the stage) ----
+  if (!c.inplace) {
+    for (int ch = 0; ch < W; ++ch) {
+      int64_t s0, s1;
+      slice_range(c, ch, b, s0, s1);
+      const int64_t s4 = s0 + ((s1 - s0) & ~(int64_t)3);
+      for (int64_t i = s0 + 4 * t; i < s4; i += 4 * CT)
+        st_sys(mine, i, *reinterpret_cast<const float4*>(data + i));
+      if (s4 + t < s1) st_sys1(mine, s4 + t, data[s4 + t]);
+    }
   }
   publish(c, 0, b, e);
   await_all(c, 0, b, e);
@@ -153,11 +165,12 @@ extern "C" __global__ void __launch_bounds__(CT) gfk_xgmi_allreduce(GfkComm c, f
 #pragma unroll
     for (int j = 0; j < CMAX; ++j) src[j] = rsrc(c.stage[buf][j < W ? j : 0], sbytes);
     const int64_t s4 = s0 + ((s1 - s0) & ~(int64_t)3);
+    // (in-place: mine IS the data, so the system-scope store is the data update)
     if (s4 + t < s1) {
       float acc = ld_sys1(src[0], s4 + t);
       for (int j = 1; j < W; ++j) acc += ld_sys1(src[j], s4 + t);
       st_sys1(mine, s4 + t, acc);
-      data[s4 + t] = acc;
+      if (!c.inplace) data[s4 + t] = acc;
     }
     for (int64_t i = s0 + 4 * t; i < s4; i += 4 * CT) {
       float4 v[CMAX];
@@ -169,7 +182,7 @@ extern "C" __global__ void __launch_bounds__(CT) gfk_xgmi_allreduce(GfkComm c, f
       for (int j = 1; j < CMAX; ++j)
         if (j < W) acc = add4(acc, v[j]);
       st_sys(mine, i, acc);
-      *reinterpret_cast<float4*>(data + i) = acc;
+      if (!c.inplace) *reinterpret_cast<float4*>(data + i) = acc;
     }
   }
   publish(c, 1, b, e);
@@ -186,47 +199,84 @@ extern "C" __global__ void __launch_bounds__(CT) gfk_xgmi_allreduce(GfkComm c, f
       *reinterpret_cast<float4*>(data + i) = ld_sys(src, i);
     if (s4 + t < s1) data[s4 + t] = ld_sys1(src, s4 + t);
   }
+  // ---- phase 3 (in-place): nobody leaves while a peer may still read its data ----
+  if (c.inplace) {
+    publish(c, 2, b, e);
+    await_all(c, 2, b, e);
+  }
 }
 
 // ---------------------------------------------------------------------------
-// In-process FedAvg of N simulated clients on one GPU (LocalFederation): every
-// client's pre-scaled shared state f_i becomes sum_i f_i, summed in client order
-// starting from f_0 (the same order as the xGMI kernel's phase 1, so one-GPU
-// simulations and the multi-GPU run agree bit for bit).  One launch replaces the
-// 2N + 1 eager kernels of a zero / add / copy sequence and is captured into the
-// federation's round graph.  The pointers are 16-byte aligned; a partial last float4 is summed
-// element-wise.
+// In-process FedAvg of N simulated clients on one GPU (LocalFederation), and the
+// in-rank half of the hierarchical FedAvg of a rank that hosts several clients
+// (run_distributed with more clients than ranks).  Every client's pre-scaled shared
+// state f_i is summed as a left fold per GROUP of consecutive clients, and the group
+// sums as a left fold in group order:  sum = (f_0 + .. + f_{e0-1}) + (f_{e0} + ..) + ..
+// With one group this is the plain client-order sum; with one group per rank it is
+// exactly the order of "each rank folds its own clients, then the xGMI kernel folds
+// the ranks' partial sums in rank order" -- so a one-GPU simulation and the multi-rank
+// run agree bit for bit.  Modes:
+//   0  the sum is written back to every client's buffer (LocalFederation round);
+//   1  the sum is written to f_0 only (a rank's local partial, before the collective);
+//   2  broadcast: f_0 is copied into f_1 .. f_{n-1} (after the collective).
+// One launch replaces the 2N + 1 eager kernels of a zero / add / copy sequence and is
+// captured into the round graphs.  The pointers are 16-byte aligned; a partial last
+// float4 is handled element-wise.
 // ---------------------------------------------------------------------------
 constexpr int LMAX = 16;
 
 struct GfkLocalAvg {
   float* f[LMAX];
   int32_t n_clients;
-  int32_t pad;
+  int32_t mode;
   int64_t n;                     // floats
+  int32_t n_groups;
+  int32_t gend[LMAX];            // exclusive end of each group (gend[n_groups - 1] = n_clients)
+  int32_t pad;
 };
+
+namespace {
+template <class T>
+__device__ __forceinline__ T fold(const GfkLocalAvg& a, int64_t i) {
+  const T* const* f = reinterpret_cast<const T* const*>(a.f);
+  T tot{};
+  int j = 0;
+  for (int g = 0; g < a.n_groups; ++g) {
+    T s = f[j][i];
+    for (++j; j < a.gend[g]; ++j) s = s + f[j][i];
+    tot = g == 0 ? s : tot + s;
+  }
+  return tot;
+}
+}  // namespace
 
 extern "C" __global__ void __launch_bounds__(256) gfk_local_fedavg(GfkLocalAvg a) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t n4 = a.n >> 2;
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int w1 = a.mode == 1 ? 1 : a.n_clients;     // buffers written
+  const int w0 = a.mode == 2 ? 1 : 0;
   for (int64_t i = g; i < n4; i += stride) {
-    float4 acc = reinterpret_cast<const float4*>(a.f[0])[i];
-    for (int j = 1; j < a.n_clients; ++j) acc = add4(acc, reinterpret_cast<const float4*>(a.f[j])[i]);
-    for (int j = 0; j < a.n_clients; ++j) reinterpret_cast<float4*>(a.f[j])[i] = acc;
+    const float4 acc = a.mode == 2 ? reinterpret_cast<const float4*>(a.f[0])[i] : fold<float4>(a, i);
+    for (int j = w0; j < w1; ++j) reinterpret_cast<float4*>(a.f[j])[i] = acc;
   }
   if (g < (a.n & 3)) {           // the partial float4 at the end: nothing past n is touched
     const int64_t i = (n4 << 2) + g;
-    float acc = a.f[0][i];
-    for (int j = 1; j < a.n_clients; ++j) acc += a.f[j][i];
-    for (int j = 0; j < a.n_clients; ++j) a.f[j][i] = acc;
+    const float acc = a.mode == 2 ? a.f[0][i] : fold<float>(a, i);
+    for (int j = w0; j < w1; ++j) a.f[j][i] = acc;
   }
 }
 
 extern "C" size_t gfk_local_avg_struct_size() { return sizeof(GfkLocalAvg); }
 
 extern "C" int gfk_local_fedavg_launch(const GfkLocalAvg* a, int grid, hipStream_t s) {
-  if (a->n_clients < 1 || a->n_clients > LMAX || grid < 1) return -1;
+  if (a->n_clients < 1 || a->n_clients > LMAX || grid < 1 || a->mode < 0 || a->mode > 2 ||
+      a->n_groups < 1 || a->n_groups > a->n_clients || a->gend[a->n_groups - 1] != a->n_clients)
+    return -1;
+  for (int g = 0, e = 0; g < a->n_groups; ++g) {
+    if (a->gend[g] <= e) return -1;
+    e = a->gend[g];
+  }
   for (int j = 0; j < a->n_clients; ++j)
     if ((uintptr_t)a->f[j] & 15) return -1;
   hipLaunchKernelGGL(gfk_local_fedavg, dim3(grid), dim3(256), 0, s, *a);
@@ -274,6 +324,17 @@ extern "C" int gfk_ipc_open(const void* handle, void** ptr) {
 }
 
 extern "C" int gfk_ipc_close(void* ptr) { return (int)hipIpcCloseMemHandle(ptr); }
+
+// The IPC handle of the allocation holding ptr (a caching-allocator sub-block) and
+// ptr's byte offset into it: peers open the handle and add the offset.
+extern "C" int gfk_ipc_get_range(void* ptr, void* handle, int64_t* offset) {
+  void* base = nullptr;
+  size_t size = 0;
+  hipError_t e = hipMemGetAddressRange(&base, &size, ptr);
+  if (e != hipSuccess) return (int)e;
+  *offset = (int64_t)((char*)ptr - (char*)base);
+  return (int)hipIpcGetMemHandle(reinterpret_cast<hipIpcMemHandle_t*>(handle), base);
+}
 
 // The error word (0 = fine, 1 / 2 = a phase-0 / phase-1 wait timed out); synchronous.
 extern "C" int gfk_comm_error(const GfkComm* c) {

@@ -115,7 +115,8 @@ __device__ __forceinline__ void st_f4_as_f2(float* p, const f32x4& x) {   // 8-b
 // ((tid + 512 u) / 32, (tid + 512 u) % 32): u = 0 covers the 16 x_ctx rows, u >= 1
 // the 64 Wa rows, 32 consecutive lanes per 512-byte row segment.
 template <int BM>
-__global__ void __launch_bounds__(FT) gfk_ctx_fwd_k(GfkModel m) {
+__global__ void __launch_bounds__(FT) gfk_ctx_fwd_k(const GfkModel* __restrict__ gm_) {
+  const GfkModel& m = gm_[blockIdx.z];
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int RB = BM / 16, SU = 5;
   const int x = blockIdx.x, jx = x >> 3, rb = jx % RB, tile = (jx / RB) * 8 + (x & 7);
@@ -232,7 +233,8 @@ __global__ void __launch_bounds__(FT) gfk_ctx_fwd_k(GfkModel m) {
 
 // grid: n_tiles * ctx_kb workgroups of 16 waves (one per CU).
 template <int BM>
-__global__ void __launch_bounds__(CT) gfk_ctx_bwd_k(GfkModel m) {
+__global__ void __launch_bounds__(CT) gfk_ctx_bwd_k(const GfkModel* __restrict__ gm_) {
+  const GfkModel& m = gm_[blockIdx.z];
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ int docs_s[BM];
   GFK_STAMP(m, 34);
@@ -431,10 +433,10 @@ extern "C" int gfk_launch_ctx_fwd(const GfkModel* m, hipStream_t s) {
   const dim3 g(8 * ((m->n_tiles + 7) / 8) * (m->bmax / 16)), t(FT);
   const size_t sm = sizeof(float) * fwd_lds_floats(*m);
   switch (m->bmax) {
-    case 16: hipLaunchKernelGGL(gfk_ctx_fwd_k<16>, g, t, sm, s, *m); break;
-    case 32: hipLaunchKernelGGL(gfk_ctx_fwd_k<32>, g, t, sm, s, *m); break;
-    case 64: hipLaunchKernelGGL(gfk_ctx_fwd_k<64>, g, t, sm, s, *m); break;
-    case 128: hipLaunchKernelGGL(gfk_ctx_fwd_k<128>, g, t, sm, s, *m); break;
+    case 16: hipLaunchKernelGGL(gfk_ctx_fwd_k<16>, gfk_grid(g, m), t, sm, s, gfk_dev(m)); break;
+    case 32: hipLaunchKernelGGL(gfk_ctx_fwd_k<32>, gfk_grid(g, m), t, sm, s, gfk_dev(m)); break;
+    case 64: hipLaunchKernelGGL(gfk_ctx_fwd_k<64>, gfk_grid(g, m), t, sm, s, gfk_dev(m)); break;
+    case 128: hipLaunchKernelGGL(gfk_ctx_fwd_k<128>, gfk_grid(g, m), t, sm, s, gfk_dev(m)); break;
     default: return -1;
   }
   return (int)hipGetLastError();
@@ -445,10 +447,10 @@ extern "C" int gfk_launch_ctx_bwd(const GfkModel* m, hipStream_t s) {
   const dim3 g(m->n_tiles * m->ctx_kb), t(CT);
   const size_t sm = sizeof(float) * bwd_lds(*m).total;
   switch (m->bmax) {
-    case 16: hipLaunchKernelGGL(gfk_ctx_bwd_k<16>, g, t, sm, s, *m); break;
-    case 32: hipLaunchKernelGGL(gfk_ctx_bwd_k<32>, g, t, sm, s, *m); break;
-    case 64: hipLaunchKernelGGL(gfk_ctx_bwd_k<64>, g, t, sm, s, *m); break;
-    case 128: hipLaunchKernelGGL(gfk_ctx_bwd_k<128>, g, t, sm, s, *m); break;
+    case 16: hipLaunchKernelGGL(gfk_ctx_bwd_k<16>, gfk_grid(g, m), t, sm, s, gfk_dev(m)); break;
+    case 32: hipLaunchKernelGGL(gfk_ctx_bwd_k<32>, gfk_grid(g, m), t, sm, s, gfk_dev(m)); break;
+    case 64: hipLaunchKernelGGL(gfk_ctx_bwd_k<64>, gfk_grid(g, m), t, sm, s, gfk_dev(m)); break;
+    case 128: hipLaunchKernelGGL(gfk_ctx_bwd_k<128>, gfk_grid(g, m), t, sm, s, gfk_dev(m)); break;
     default: return -1;
   }
   return (int)hipGetLastError();

@@ -170,7 +170,8 @@ __device__ __forceinline__ void rowvec_gemv(const float* W, const float* x, int 
 // Staged (compile-time): the MLP weights are read from LDS (ds_read); a runtime
 // select between the LDS copy and global memory would make every read a flat load.
 template <bool Staged>
-__global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkModel m) {
+__global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(const GfkModel* __restrict__ gm_) {
+  const GfkModel& m = gm_[blockIdx.z];
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int b = blockIdx.x, tid = threadIdx.x;
   const int lane = tid & 63, wave = uniform(tid >> 6);
@@ -399,9 +400,9 @@ __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkModel m) {
 
 extern "C" int gfk_launch_enc_in(const GfkModel* m, hipStream_t s) {
   if (m->stage_flags & 1)
-    hipLaunchKernelGGL(gfk_enc_in_k<true>, dim3(m->bmax), dim3(ENC_THREADS), gfk_enc_in_smem(m), s, *m);
+    hipLaunchKernelGGL(gfk_enc_in_k<true>, gfk_grid(dim3(m->bmax), m), dim3(ENC_THREADS), gfk_enc_in_smem(m), s, gfk_dev(m));
   else
-    hipLaunchKernelGGL(gfk_enc_in_k<false>, dim3(m->bmax), dim3(ENC_THREADS), gfk_enc_in_smem(m), s, *m);
+    hipLaunchKernelGGL(gfk_enc_in_k<false>, gfk_grid(dim3(m->bmax), m), dim3(ENC_THREADS), gfk_enc_in_smem(m), s, gfk_dev(m));
   return (int)hipGetLastError();
 }
 

@@ -154,8 +154,30 @@ typedef struct GfkModel {
   float *ws_ce;                  // [bmax] the rows' CE terms / nb (post_fwd)
   float *ws_thd;                 // [bmax, K] compact theta_d (the classifier's weight-gradient input)
   int32_t lab_in_enc;            // enc_in adds the label rows (0: the host hctx carries them)
-  int32_t pad3;
+  // ---- ProdLDA backward, persistent k-range shape (large vocabularies): the logit
+  // gradient dlogit = BN_bwd(p S - x p / (p + 1e-10)) is computed ONCE per vocab tile by
+  // prodlda_dlogit into ws_dt ([n_tiles][bmax][66], the bwd's LDS tile layout, copied
+  // verbatim by LDS-DMA) instead of by each of the tile's 4 k-range workgroups ----
+  int32_t bwd_pre;
+  float* ws_dt;
+  // ---- batched launches: every kernel reads its model from a DEVICE array of n_batch
+  // GfkModels (grid z = the model index), so one launch per phase can run the local
+  // steps of several federated clients at once (dev: that array, for a single client a
+  // device copy of this struct; dev_upd: the matching GfkUpdate array) ----
+  const void* dev;
+  const void* dev_upd;
+  int32_t n_batch;
+  int32_t pad4;
 } GfkModel;
+
+// launch helpers: grid z = the batched models, the kernel argument = the device array
+__host__ inline dim3 gfk_grid(dim3 g, const GfkModel* m) {
+  g.z = m->n_batch > 1 ? (unsigned)m->n_batch : 1u;
+  return g;
+}
+__host__ inline const GfkModel* gfk_dev(const GfkModel* m) {
+  return reinterpret_cast<const GfkModel*>(m->dev);
+}
 
 // Gradient + update jobs of the small tensors, run by the update kernel next to
 // the W_in tiles (csrc/update.hip).  Weight job: G[j][i] = sum_{b < nb} dz[b][j]

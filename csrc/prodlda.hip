@@ -79,7 +79,8 @@ __device__ __forceinline__ float sum_groups(float v) {
 // dynamic LDS: th[BM*kt] + bt[KP*LDB_F] + colp[4][64] + colq[4][64] + stat[2][64]
 // BF: bf16 MFMA operands (16x16x16, K padded to 16), fp32 accumulation.
 template <int BM, bool BF>
-__global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
+__global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(const GfkModel* __restrict__ gm_) {
+  const GfkModel& m = gm_[blockIdx.z];
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int K = m.K, V = m.V, KT = m.kt;
   int tid = threadIdx.x;                      // re-made opaque per tile (no hoisted addresses)
@@ -297,7 +298,8 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkModel m) {
 // round 0.0589 -> 0.0583 ms, K=50 V=28k 0.101 -> 0.092, K=200 V=112k 0.349 -> 0.342.
 // NP: k pairs held in registers (compile-time, the launcher's smallest instance >= K / 8).
 template <int BM, int NP, bool PF>
-__global__ void __launch_bounds__(PF ? 512 : 1024) prodlda_fwd_strip_kernel(GfkModel m) {
+__global__ void __launch_bounds__(PF ? 512 : 1024) prodlda_fwd_strip_kernel(const GfkModel* __restrict__ gm_) {
+  const GfkModel& m = gm_[blockIdx.z];
   constexpr int STRIP_THREADS = PF ? 512 : 1024;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int K = m.K, V = m.V, KT = m.kt;
@@ -500,7 +502,8 @@ __global__ void __launch_bounds__(PF ? 512 : 1024) prodlda_fwd_strip_kernel(GfkM
 // One wave per batch row: log-sum-exp from the per-wave partials, the sparse
 // reconstruction loss and S_b over the row's non-zeros (read from the row slots
 // prepared with the batch, so the logit gathers are the second round trip).
-extern "C" __global__ void __launch_bounds__(64) gfk_prodlda_row_loss(GfkModel m) {
+extern "C" __global__ void __launch_bounds__(64) gfk_prodlda_row_loss(const GfkModel* __restrict__ gm_) {
+  const GfkModel& m = gm_[blockIdx.z];
   int n_tiles = m.n_tiles, bmax = m.bmax;
   const int32_t *nbp = m.ws_nb, *erange = m.ws_erange;
   const float *row_part = m.ws_row_part, *zn = m.ws_zn;
@@ -607,10 +610,91 @@ extern "C" __global__ void __launch_bounds__(64) gfk_prodlda_row_loss(GfkModel m
 __host__ __device__ __forceinline__ int kt_stride(int w) { return w % 32 == 16 ? w : w + 16; }
 __host__ __device__ __forceinline__ int bwd_kpq(int K, int kq) { return 16 * ((round_up(K, 16) / 16 + kq - 1) / kq); }
 
+// Logit gradient of one vocabulary tile, computed ONCE (bwd_pre: the persistent k-range
+// backward at large V, whose 4 range workgroups per tile each recomputed it, each behind
+// a dependent tile-start -> first-non-zero load chain):
+//   sparse  dt[b, c] = -x p / (p + 1e-10) at the tile's non-zeros  (p = exp(z - lse_b))
+//   dense   dt = rstd * (d - mean_b d - z mean_b(d z)),  d = p S_b + dt  (column BN bwd)
+// written to ws_dt[tile] in the backward's LDS tile layout ([BM][LDD], rows >= nb and the
+// padding columns zero), so prodlda_bwd stages it with one contiguous LDS-DMA copy.
+// grid: n_tiles workgroups of 256 threads.  Static LDS: z tile + dt tile + lse / S / rstd.
+template <int BM>
+__global__ void __launch_bounds__(256) prodlda_dlogit_kernel(const GfkModel* __restrict__ gm_) {
+  const GfkModel& m = gm_[blockIdx.z];
+  constexpr int NT = 256;
+  constexpr int TPR = NT / BM;                 // threads per row (sparse term)
+  __shared__ __attribute__((aligned(16))) float zt[BM * VB];
+  __shared__ __attribute__((aligned(16))) float dt[BM * LDD];
+  __shared__ __attribute__((aligned(16))) float ls[BM], Sb[BM], rs[VB];
+  const int tid = threadIdx.x, tile = blockIdx.x, c0 = tile * VB;
+  const int V = m.V, nb = *m.ws_nb;
+  // ---- one staging round: z tile, lse, S (LDS-DMA), rstd, the rows' tile extents ----
+  glds_copy(zt, m.ws_zn + (size_t)tile * BM * VB, BM * VB, tid, NT);
+  glds_copy(ls, m.ws_lse, BM, tid, NT);
+  glds_copy(Sb, m.ws_s, BM, tid, NT);
+  const int xrow = tid / TPR, xsub = tid % TPR;
+  const int32_t* ts = m.ws_tstart + (size_t)xrow * (m.n_tiles + 1) + tile;
+  const int xe0 = ts[0], xe1 = ts[1];
+  const float rsr = m.ws_col_rstd[min(c0 + (tid & (VB - 1)), m.n_tiles * VB - 1)];
+  {
+    f32x4* d4 = reinterpret_cast<f32x4*>(dt);
+    for (int i = tid; i < BM * LDD / 4; i += NT) d4[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  if (tid < VB) rs[tid] = c0 + tid < V ? rsr : 0.f;
+  vm_barrier();
+  // ---- sparse term at this tile's non-zeros ----
+  if (xrow < nb) {
+    const float l = ls[xrow];
+    for (int e = xe0 + xsub; e < xe1; e += TPR) {
+      const int c = m.indices[e] - c0;
+      const float x = m.values[e];
+      const float p = __expf(zt[xrow * VB + (c ^ zswz(xrow))] - l);
+      dt[xrow * LDD + c] = -x * p / (p + RL_EPS);
+    }
+  }
+  lds_barrier();
+  // ---- dense term p S and the column BN backward: 16 lanes per column ----
+  const int dg = tid & 15;
+  const float inv_nb = 1.f / (float)nb;
+  for (int dcol = tid >> 4; dcol < VB; dcol += NT / 16) {
+    constexpr int NR = BM / 16;
+    float d[NR], z[NR];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int row = dg + 16 * i;
+      z[i] = zt[row * VB + (dcol ^ zswz(row))];
+      const float p = __expf(z[i] - ls[row]);
+      d[i] = row < nb ? p * Sb[row] + dt[row * LDD + dcol] : 0.f;
+      s1 += d[i];
+      s2 += d[i] * z[i];
+    }
+    s1 = row16_sum(s1) * inv_nb;
+    s2 = row16_sum(s2) * inv_nb;
+    const float r = rs[dcol];
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int row = dg + 16 * i;
+      dt[row * LDD + dcol] = row < nb ? r * (d[i] - s1 - z[i] * s2) : 0.f;
+    }
+  }
+  lds_barrier();
+  // ---- the tile, verbatim (float4 over the flat [BM][LDD] block) ----
+  f32x4* out = reinterpret_cast<f32x4*>(m.ws_dt + (size_t)tile * BM * LDD);
+  const f32x4* d4 = reinterpret_cast<const f32x4*>(dt);
+  for (int i = tid; i < BM * LDD / 4; i += NT) out[i] = d4[i];
+}
+
 // BF: bf16 MFMA operands (16x16x16), fp32 accumulation, for both GEMMs.
-template <int BM, int MAXU, int KQ, bool BF>
-__global__ void __launch_bounds__(KQ == 1 ? DEC_THREADS : 512, KQ == 1 ? 1 : 2)
-prodlda_bwd_kernel(GfkModel m) {
+// PRE (bwd_pre, KQ = 4 only): the logit-gradient tile comes precomputed from ws_dt
+// (prodlda_dlogit): no sparse / dense passes, no dependent loads in the staging round.
+// Its LDS is th [BM][64] (theta_d's k range, row r's columns XOR 16 (r & 1): the dbeta
+// A-role reads, 2 rows x 16 columns per half-wave, hit 32 distinct banks with the
+// swizzle a per-lane constant) + bt + dt, and the dbeta tile G reuses dt's space (one
+// extra barrier): ~50 KB at B = 64, K = 200, so THREE workgroups share a CU (24 waves)
+// instead of two.
+template <int BM, int MAXU, int KQ, bool BF, bool PRE>
+__device__ __forceinline__ void prodlda_bwd_body(const GfkModel& m) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int NTH = KQ == 1 ? DEC_THREADS : 512;
   // KQ = 1 with more than 3 k tiles only ever runs with one tile per workgroup (the
@@ -640,11 +724,11 @@ prodlda_bwd_kernel(GfkModel m) {
   const int q = (int)blockIdx.x % KQ, slab = (int)blockIdx.x / KQ, nslab = (int)gridDim.x / KQ;
   const int ks0 = q * ksub / KQ, nks = (q + 1) * ksub / KQ - ks0;   // this workgroup's k tiles
   const int kb = 16 * ks0;                                      // first topic of the range
-  const int KPQ = bwd_kpq(K, KQ), KTQ = KQ == 1 ? m.kt : kt_stride(KPQ);
+  const int KPQ = bwd_kpq(K, KQ), KTQ = PRE ? 64 : KQ == 1 ? m.kt : kt_stride(KPQ);
   float* th = smem;
   float* bt = th + BM * KTQ;
-  float* zt = bt + KPQ * LDB_B;
-  float* dt = zt + BM * VB;
+  float* zt = bt + KPQ * LDB_B;                 // PRE: no logit tile; the G tile aliases dt
+  float* dt = PRE ? zt : zt + BM * VB;
   float* lse = dt + BM * LDD;
   float* Sb = lse + BM;
   float* rs = Sb + BM;
@@ -662,11 +746,14 @@ prodlda_bwd_kernel(GfkModel m) {
   } else {
     for (int i = tid; i < BM * 16 * NKS; i += NTH) {
       const int b = i / (16 * NKS), c = i % (16 * NKS);
-      if (c < 16 * nks) th[b * KTQ + c] = m.ws_thetad[(size_t)b * m.kt + kb + c];
+      if (PRE) th[b * 64 + (c ^ (((b >> 3) & 1) << 4))] = c < 16 * nks ? m.ws_thetad[(size_t)b * m.kt + kb + c] : 0.f;
+      else if (c < 16 * nks) th[b * KTQ + c] = m.ws_thetad[(size_t)b * m.kt + kb + c];
     }
   }
-  glds_copy(lse, m.ws_lse, BM, tid, NTH);
-  glds_copy(Sb, m.ws_s, BM, tid, NTH);
+  if (!PRE) {
+    glds_copy(lse, m.ws_lse, BM, tid, NTH);
+    glds_copy(Sb, m.ws_s, BM, tid, NTH);
+  }
 
   // ---- a tile's loads, into registers ----
   float br[BU];
@@ -678,9 +765,11 @@ prodlda_bwd_kernel(GfkModel m) {
     const int c0 = tile * VB;
     // the tile-start loads first: the dependent first-non-zero load waits for them
     // alone (vmcnt counts in order), not for the beta block behind them
-    const int32_t* ts = m.ws_tstart + (size_t)min(xrow, BM - 1) * (m.n_tiles + 1) + tile;
-    xe0 = ts[0];                         // rows >= BM (BM < NTH / 16) are never used
-    xe1 = ts[1];
+    if (!PRE) {
+      const int32_t* ts = m.ws_tstart + (size_t)min(xrow, BM - 1) * (m.n_tiles + 1) + tile;
+      xe0 = ts[0];                       // rows >= BM (BM < NTH / 16) are never used
+      xe1 = ts[1];
+    }
     // element tid + NTH u of the block is (row tid / VB + RPU u, column tid % VB)
     const int c = min(c0 + (tid & (VB - 1)), V - 1);
 #pragma unroll
@@ -688,7 +777,7 @@ prodlda_bwd_kernel(GfkModel m) {
       const int k = min(kb + tid / VB + RPU * u, K - 1);
       br[u] = m.beta[k * V + c];                 // 32-bit offsets (K V < 2^31)
     }
-    rsr = m.ws_col_rstd[c0 + (tid & (VB - 1))];
+    if (!PRE) rsr = m.ws_col_rstd[c0 + (tid & (VB - 1))];
   };
   auto issue_first_nz = [&]() {          // depends on the tile-start loads
     const int xe = min(xe0 + xsub, max(xe1 - 1, 0));
@@ -743,7 +832,7 @@ prodlda_bwd_kernel(GfkModel m) {
     GFK_STAMP(m, 23);
     // one staging round per tile: every global read is issued before the barrier
     issue_tile(tile);
-    issue_first_nz();
+    if (!PRE) issue_first_nz();
     if (fused) {                               // (beta_split: no Adam state here)
       if constexpr (RW) issue_state_rw(tile);
       else issue_state(tile);
@@ -751,7 +840,8 @@ prodlda_bwd_kernel(GfkModel m) {
     if (tile != slab) lds_barrier();           // the previous tile's LDS reads are done
     // ---- (1) the BN'ed logit tile by LDS-DMA (contiguous in ws_zn), this tile's
     //      registers -> LDS; zero the logit-gradient tile ----
-    glds_copy(zt, m.ws_zn + (size_t)tile * BM * VB, BM * VB, tid, NTH);
+    if (PRE) glds_copy(dt, m.ws_dt + (size_t)tile * BM * LDD, BM * LDD, tid, NTH);
+    else glds_copy(zt, m.ws_zn + (size_t)tile * BM * VB, BM * VB, tid, NTH);
     {
       const int c = tid & (VB - 1), cok = c0 + c < V;
 #pragma unroll
@@ -760,9 +850,11 @@ prodlda_bwd_kernel(GfkModel m) {
         if (k < 16 * nks) bt[k * LDB_B + c] = (kb + k < K && cok) ? br[u] : 0.f;
       }
     }
-    if (tid < VB) rs[tid] = rsr;
-    for (int dcol = tid >> 4; dcol < VB; dcol += NTH / 16)
-      for (int row = dg; row < BM; row += 16) dt[row * LDD + dcol] = 0.f;
+    if (!PRE) {
+      if (tid < VB) rs[tid] = rsr;
+      for (int dcol = tid >> 4; dcol < VB; dcol += NTH / 16)
+        for (int row = dg; row < BM; row += 16) dt[row * LDD + dcol] = 0.f;
+    }
     const int ye0 = xe0, ye1 = xe1, yc0 = xc0;
     const float yv0 = xv0;
     vm_barrier();                              // (+ theta_d / lse / S on the first tile)
@@ -773,6 +865,7 @@ prodlda_bwd_kernel(GfkModel m) {
     GFK_STAMP(m, 25);
 
     // ---- (3) sparse term: dt[b, c] = -x p / (p + 1e-10) at this tile's non-zeros ----
+    if (!PRE) {
     if (xrow < nb && xrow < BM) {
       const float l = lse[xrow];
       for (int i = 0, e = ye0 + xsub; e < ye1; ++i, e += TPR) {
@@ -810,6 +903,7 @@ prodlda_bwd_kernel(GfkModel m) {
       }
     }
     lds_barrier();
+    }  // !PRE
     GFK_STAMP(m, 27);
 
     // ---- (5) d theta_d[b, k] += sum_c dlogit[b, c] beta[k, c] over the k range ----
@@ -845,6 +939,7 @@ prodlda_bwd_kernel(GfkModel m) {
     }
     };
     // ---- (6) dbeta[k, c] = sum_b th[b, k] dlogit[b, c] -> update (fused) or gradient ----
+    float gr[MU][4];                           // (PRE: the dbeta subtiles, until G is free)
     auto dbeta_tile = [&]() {
       // results in fresh registers: the stores below never wait on a load (the loaded
       // m, v are consumed only by the fused-mode update)
@@ -856,22 +951,46 @@ prodlda_bwd_kernel(GfkModel m) {
         const int ks = t >> 2, cst = t & 3;
         f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
         if constexpr (BF) {       // A[k][b] = theta_d column, B[b][c] = dt column: 4 rows b each
-          const float* ap = th + 4 * (lane >> 4) * KTQ + ks * 16 + (lane & 15);
+          // (PRE: theta_d rows 4 g + b0 + q, b0 a multiple of 16: swizzle 16 ((g >> 1) & 1))
+          const float* ap = th + 4 * (lane >> 4) * KTQ +
+                            (PRE ? (ks * 16 + (lane & 15)) ^ ((((lane >> 4) >> 1) & 1) << 4)
+                                 : ks * 16 + (lane & 15));
           const float* bp = dt + 4 * (lane >> 4) * LDD + cst * 16 + (lane & 15);
 #pragma unroll
           for (int b0 = 0; b0 < BM; b0 += 16) {
             float a[4], b[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) { a[q] = ap[(b0 + q) * KTQ]; b[q] = bp[(b0 + q) * LDD]; }
+            for (int q = 0; q < 4; ++q) {
+              a[q] = ap[(b0 + q) * KTQ];
+              b[q] = bp[(b0 + q) * LDD];
+            }
             a0 = mfma16x16x16bf(a, b, a0);
           }
         } else {
-          const float* ap = th + (lane >> 4) * KTQ + ks * 16 + (lane & 15);
-          const float* bp = dt + (lane >> 4) * LDD + cst * 16 + (lane & 15);
+          // The batch index b is the MFMA's reduction axis, so any bijection of b over
+          // the (step, lane group) pairs works if A and B agree.  Step j, lane group g takes
+          // b = 8 g + (j & 7) + 32 (j >> 3) (B >= 32): a half-wave reads rows r and r + 8,
+          // whose 16-column runs sit 8 LDD = 528 = 16 (mod 32) banks apart in dt (and
+          // 8 KTQ apart in theta_d: 16 mod 32 for the K = 50 stride 50) -- the consecutive
+          // rows of the plain mapping (offset LDD = 2 mod 32) overlapped on 14 banks.
+          // (PRE: theta_d rows XOR 16 ((b >> 3) & 1) = 16 (g & 1): fixed per lane.)
+          constexpr bool R8 = BM >= 32;
+          const int g = lane >> 4;
+          const int gr = R8 ? 8 * g : g;
+          const int kc = ks * 16 + (lane & 15);
+          const float* ap = th + gr * KTQ + (PRE && R8 ? kc ^ ((g & 1) << 4) : kc);
+          const float* bp = dt + gr * LDD + cst * 16 + (lane & 15);
+          // theta_d operand of row r (relative to gr); B = 16 with PRE: per-row swizzle
+          auto tha = [&](int r) {
+            if (PRE && !R8) return th[(gr + r) * KTQ + (kc ^ ((((gr + r) >> 3) & 1) << 4))];
+            return ap[r * KTQ];
+          };
 #pragma unroll
-          for (int b0 = 0; b0 < BM; b0 += 8) {
-            a0 = mfma16x16x4(ap[b0 * KTQ], bp[b0 * LDD], a0);
-            a1 = mfma16x16x4(ap[(b0 + 4) * KTQ], bp[(b0 + 4) * LDD], a1);
+          for (int j = 0; j < BM / 4; j += 2) {
+            const int r0 = R8 ? (j & 7) + 32 * (j >> 3) : 4 * j;
+            const int r1 = R8 ? ((j + 1) & 7) + 32 * ((j + 1) >> 3) : 4 * j + 4;
+            a0 = mfma16x16x4(tha(r0), bp[r0 * LDD], a0);
+            a1 = mfma16x16x4(tha(r1), bp[r1 * LDD], a1);
           }
         }
         const int cl = cst * 16 + (lane & 15);
@@ -879,7 +998,8 @@ prodlda_bwd_kernel(GfkModel m) {
 #pragma unroll                    // half-wave's 2 rows x 16 columns hit 32 distinct banks
           for (int e = 0; e < 4; ++e) {
             const int kl = ks * 16 + (lane >> 4) * 4 + e;
-            zt[kl * VB + (cl ^ ((kl & 4) << 2))] = a0[e] + a1[e];
+            if (PRE) gr[u][e] = a0[e] + a1[e];    // (G aliases dt: stored after a barrier)
+            else zt[kl * VB + (cl ^ ((kl & 4) << 2))] = a0[e] + a1[e];
           }
           continue;
         }
@@ -920,9 +1040,28 @@ prodlda_bwd_kernel(GfkModel m) {
         }
       }
     };
-    // (6) first: the Adam state's registers are free before the accumulators are touched
-    dbeta_tile();
-    dtheta_tile();
+    if (PRE && RW) {
+      // d theta_d first, then dbeta into registers; every wave is done reading dt before
+      // the G tile overwrites it
+      dtheta_tile();
+      dbeta_tile();
+      lds_barrier();
+#pragma unroll
+      for (int u = 0; u < MU; ++u) {
+        const int t = wave + NW * u;
+        if (t >= NB_T) break;
+        const int ks = t >> 2, cl = (t & 3) * 16 + (lane & 15);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int kl = ks * 16 + (lane >> 4) * 4 + e;
+          zt[kl * VB + (cl ^ ((kl & 4) << 2))] = gr[u][e];
+        }
+      }
+    } else {
+      // (6) first: the Adam state's registers are free before the accumulators are touched
+      dbeta_tile();
+      dtheta_tile();
+    }
     if constexpr (RW) {       // the G tile, row-wise: update (fused) or gradient
       lds_barrier();
       // per thread: one column, rows kl0 + RPU u (RPU a multiple of 8, so the row's
@@ -967,6 +1106,28 @@ prodlda_bwd_kernel(GfkModel m) {
   }
 }
 
+template <int BM, int MAXU, int KQ, bool BF>
+__global__ void __launch_bounds__(KQ == 1 ? DEC_THREADS : 512, KQ == 1 ? 1 : 2)
+prodlda_bwd_kernel(const GfkModel* __restrict__ gm_) {
+  const GfkModel& m = gm_[blockIdx.z];
+  prodlda_bwd_body<BM, MAXU, KQ, BF, false>(m);
+}
+
+// the precomputed-dlogit shape: bwd_pre = 1: <= 80 VGPRs (6 waves per SIMD), so three
+// 8-wave workgroups share a CU; bwd_pre = 2: the compiler's register budget (two per CU)
+template <int BM, int MAXU, bool BF>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6)))
+prodlda_bwd_pre_kernel(const GfkModel* __restrict__ gm_) {
+  const GfkModel& m = gm_[blockIdx.z];
+  prodlda_bwd_body<BM, MAXU, 4, BF, true>(m);
+}
+
+template <int BM, int MAXU, bool BF>
+__global__ void __launch_bounds__(512, 2) prodlda_bwd_pre2_kernel(const GfkModel* __restrict__ gm_) {
+  const GfkModel& m = gm_[blockIdx.z];
+  prodlda_bwd_body<BM, MAXU, 4, BF, true>(m);
+}
+
 // stage_flags bit 2: the strip forward (prodlda_fwd_strip_kernel) -- theta_d + the
 // per-wave row partials only
 constexpr int FWD_STRIP = 4;
@@ -996,6 +1157,8 @@ __host__ __device__ inline int bwd_kq(const GfkModel& m) {
 
 static size_t bwd_smem(const GfkModel* m, int kq) {
   const size_t KPQ = bwd_kpq(m->K, kq), B = m->bmax;
+  if (kq == 4 && m->bwd_pre && B <= 64)       // th [B][64] + bt + dt (G aliases dt)
+    return sizeof(float) * (B * 64 + KPQ * LDB_B + B * LDD);
   const size_t KTQ = kq == 1 ? (size_t)m->kt : (size_t)kt_stride((int)KPQ);
   return sizeof(float) * (B * KTQ + KPQ * LDB_B + B * VB + B * LDD + 2 * B + VB);
 }
@@ -1014,9 +1177,9 @@ extern "C" int gfk_launch_prodlda_fwd(const GfkModel* m, hipStream_t s) {
 #define GFK_FWS(BM, NP)                                                                        \
     do {                                                                                       \
       if (m->stage_flags & FWD_STRIP_PF)                                                       \
-        hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, true>), g, dim3(512), sm, s, *m); \
+        hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, true>), gfk_grid(g, m), dim3(512), sm, s, gfk_dev(m)); \
       else                                                                                     \
-        hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, false>), g, dim3(1024), sm, s, *m); \
+        hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, false>), gfk_grid(g, m), dim3(1024), sm, s, gfk_dev(m)); \
     } while (0)
 #define GFK_FWS_B(BM)                                                      \
     if (np == 8) GFK_FWS(BM, 8);                                           \
@@ -1034,8 +1197,8 @@ extern "C" int gfk_launch_prodlda_fwd(const GfkModel* m, hipStream_t s) {
     return (int)hipGetLastError();
   }
 #define GFK_FWD(BM)                                                                  \
-  if (m->mm_bf16) hipLaunchKernelGGL((prodlda_fwd_kernel<BM, true>), g, blk, sm, s, *m);   \
-  else hipLaunchKernelGGL((prodlda_fwd_kernel<BM, false>), g, blk, sm, s, *m)
+  if (m->mm_bf16) hipLaunchKernelGGL((prodlda_fwd_kernel<BM, true>), gfk_grid(g, m), blk, sm, s, gfk_dev(m));   \
+  else hipLaunchKernelGGL((prodlda_fwd_kernel<BM, false>), gfk_grid(g, m), blk, sm, s, gfk_dev(m))
   switch (m->bmax) {
     case 16: GFK_FWD(16); break;
     case 32: GFK_FWD(32); break;
@@ -1047,14 +1210,45 @@ extern "C" int gfk_launch_prodlda_fwd(const GfkModel* m, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+template <int MAXU, int KQ, bool BF, bool PRE>
+static void launch_bwd_p(const GfkModel* m, dim3 g, size_t sm, hipStream_t s) {
+  const dim3 blk(KQ == 1 ? DEC_THREADS : 512);
+  if (PRE && m->bwd_pre == 2) {
+    switch (m->bmax) {
+      case 16: hipLaunchKernelGGL((prodlda_bwd_pre2_kernel<16, MAXU, BF>), gfk_grid(g, m), blk, sm, s, gfk_dev(m)); break;
+      case 32: hipLaunchKernelGGL((prodlda_bwd_pre2_kernel<32, MAXU, BF>), gfk_grid(g, m), blk, sm, s, gfk_dev(m)); break;
+      default: hipLaunchKernelGGL((prodlda_bwd_pre2_kernel<64, MAXU, BF>), gfk_grid(g, m), blk, sm, s, gfk_dev(m)); break;
+    }
+    return;
+  }
+  if (PRE) {
+    switch (m->bmax) {
+      case 16: hipLaunchKernelGGL((prodlda_bwd_pre_kernel<16, MAXU, BF>), gfk_grid(g, m), blk, sm, s, gfk_dev(m)); break;
+      case 32: hipLaunchKernelGGL((prodlda_bwd_pre_kernel<32, MAXU, BF>), gfk_grid(g, m), blk, sm, s, gfk_dev(m)); break;
+      default: hipLaunchKernelGGL((prodlda_bwd_pre_kernel<64, MAXU, BF>), gfk_grid(g, m), blk, sm, s, gfk_dev(m)); break;
+    }
+    return;
+  }
+  switch (m->bmax) {
+    case 16: hipLaunchKernelGGL((prodlda_bwd_kernel<16, MAXU, KQ, BF>), gfk_grid(g, m), blk, sm, s, gfk_dev(m)); break;
+    case 32: hipLaunchKernelGGL((prodlda_bwd_kernel<32, MAXU, KQ, BF>), gfk_grid(g, m), blk, sm, s, gfk_dev(m)); break;
+    case 64: hipLaunchKernelGGL((prodlda_bwd_kernel<64, MAXU, KQ, BF>), gfk_grid(g, m), blk, sm, s, gfk_dev(m)); break;
+    default: hipLaunchKernelGGL((prodlda_bwd_kernel<128, MAXU, KQ, BF>), gfk_grid(g, m), blk, sm, s, gfk_dev(m)); break;
+  }
+}
+
 template <int MAXU, int KQ, bool BF>
 static void launch_bwd_b(const GfkModel* m, dim3 g, size_t sm, hipStream_t s) {
-  const dim3 blk(KQ == 1 ? DEC_THREADS : 512);
-  switch (m->bmax) {
-    case 16: hipLaunchKernelGGL((prodlda_bwd_kernel<16, MAXU, KQ, BF>), g, blk, sm, s, *m); break;
-    case 32: hipLaunchKernelGGL((prodlda_bwd_kernel<32, MAXU, KQ, BF>), g, blk, sm, s, *m); break;
-    case 64: hipLaunchKernelGGL((prodlda_bwd_kernel<64, MAXU, KQ, BF>), g, blk, sm, s, *m); break;
-    default: hipLaunchKernelGGL((prodlda_bwd_kernel<128, MAXU, KQ, BF>), g, blk, sm, s, *m); break;
+  if (KQ == 4 && m->bwd_pre && m->bmax <= 64) {      // (static LDS: B <= 64)
+    const dim3 gd(m->n_tiles), bd(256);
+    switch (m->bmax) {
+      case 16: hipLaunchKernelGGL(prodlda_dlogit_kernel<16>, gfk_grid(gd, m), bd, 0, s, gfk_dev(m)); break;
+      case 32: hipLaunchKernelGGL(prodlda_dlogit_kernel<32>, gfk_grid(gd, m), bd, 0, s, gfk_dev(m)); break;
+      default: hipLaunchKernelGGL(prodlda_dlogit_kernel<64>, gfk_grid(gd, m), bd, 0, s, gfk_dev(m)); break;
+    }
+    launch_bwd_p<MAXU, KQ, BF, KQ == 4>(m, g, sm, s);
+  } else {
+    launch_bwd_p<MAXU, KQ, BF, false>(m, g, sm, s);
   }
 }
 
@@ -1085,7 +1279,7 @@ extern "C" int gfk_launch_prodlda_bwd(const GfkModel* m, hipStream_t s) {
 }
 
 extern "C" int gfk_launch_prodlda_row_loss(const GfkModel* m, hipStream_t s) {
-  hipLaunchKernelGGL(gfk_prodlda_row_loss, dim3(m->bmax), dim3(64), 0, s, *m);
+  hipLaunchKernelGGL(gfk_prodlda_row_loss, gfk_grid(dim3(m->bmax), m), dim3(64), 0, s, gfk_dev(m));
   return (int)hipGetLastError();
 }
 
@@ -1110,9 +1304,15 @@ extern "C" int gfk_prodlda_set_smem(size_t bytes) {
     (const void*)prodlda_bwd_kernel<32, U, T, F>, (const void*)prodlda_bwd_kernel<64, U, T, F>, \
     (const void*)prodlda_bwd_kernel<128, U, T, F>
 #define GFK_BWD_PTRS1(U, T) GFK_BWD_PTRS2(U, T, false), GFK_BWD_PTRS2(U, T, true)
-#define GFK_BWD_PTRS(U) GFK_BWD_PTRS1(U, 1), GFK_BWD_PTRS1(U, 4)
+#define GFK_BWD_PTRS3(U, F) (const void*)prodlda_bwd_pre_kernel<16, U, F>, \
+    (const void*)prodlda_bwd_pre_kernel<32, U, F>, (const void*)prodlda_bwd_pre_kernel<64, U, F>, \
+    (const void*)prodlda_bwd_pre2_kernel<16, U, F>, (const void*)prodlda_bwd_pre2_kernel<32, U, F>, \
+    (const void*)prodlda_bwd_pre2_kernel<64, U, F>
+#define GFK_BWD_PTRS(U) GFK_BWD_PTRS1(U, 1), GFK_BWD_PTRS1(U, 4), GFK_BWD_PTRS3(U, false), \
+    GFK_BWD_PTRS3(U, true)
                       GFK_BWD_PTRS(1), GFK_BWD_PTRS(2), GFK_BWD_PTRS(3), GFK_BWD_PTRS(4)};
 #undef GFK_BWD_PTRS
+#undef GFK_BWD_PTRS3
 #undef GFK_BWD_PTRS1
 #undef GFK_BWD_PTRS2
   for (const void* k : ks) {

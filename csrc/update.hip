@@ -52,6 +52,8 @@ extern "C" size_t gfk_win_update_smem(const GfkModel* m) {
   size_t a = (size_t)64 * stride_a(B) + (size_t)B * stride_b(H0P);
   const size_t b = 2 * (size_t)B * 80;
   if (a < 64 * 64) a = 64 * 64;      // the flat epilogue's gradient tile [64, H0 <= 64]
+  const size_t c = (size_t)B * m->H[0] + 2 * 512 + 129;   // the sparse tile (bit 4)
+  if (a < c) a = c;
   return sizeof(float) * (a > b ? a : b);
 }
 
@@ -169,6 +171,182 @@ __device__ __forceinline__ void vector_job(const GfkModel& m, const GfkVJob& J) 
   }
 }
 
+// Sparse W_in tile (stage_flags bit 4, large vocabularies: a 64-word tile holds only a
+// few of the batch's non-zeros, ~7 at V = 112k).  The dense x^T tile + MFMA GEMM of the
+// default path spends its staging on zero-filling and scattering a mostly empty [64, B]
+// tile; here the tile's non-zeros become an entry list (rows in order, CSR order within a
+// row: a scan of the rows' counts gives every row its slot range) and every thread
+// accumulates its own elements of the flat [64, H0] block over the list,
+//   G[v, h] = sum_{entries (b, v, x), b ascending} x dz0[b, h],
+// a fixed order (deterministic, no atomics).  The W_in / m / v block moves as flat quads
+// (one round, issued first); Adam (+ FedAvg pre-scale) or the gradient store follows.
+// More entries than CAP are taken in passes of CAP (each thread's sums stay in registers).
+constexpr int WIN_SPARSE = 16;
+template <int UT>
+__device__ __forceinline__ void win_tile_sparse(const GfkModel& m, float* smem, int tile) {
+  constexpr int CAP = 512;
+  constexpr int TPR = UT / 64;                 // threads per row, 64 rows per pass
+  constexpr int FQ = 64 * 64 / 4 / UT;         // quads per thread (H0 <= 64)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int B = m.bmax, H0 = m.H[0], V = m.V, c0 = tile * 64;
+  const int nb = *m.ws_nb;
+  float* dz = smem;                            // [B][H0]
+  int* ecol = reinterpret_cast<int*>(dz + B * H0);   // [CAP] (row << 8) | local column
+  float* ex = reinterpret_cast<float*>(ecol + CAP);  // [CAP]
+  int* offs = reinterpret_cast<int*>(ex + CAP);      // [129] rows' first slots, total
+  float* wblk = m.w_in + (size_t)c0 * H0;
+  const int nel = (min(V, c0 + 64) - c0) * H0;
+  const bool fused = m.update_mode == 1;
+  const bool al4 = ((uintptr_t)wblk % 16 == 0) && m.off_m % 4 == 0 && m.off_v % 4 == 0 &&
+                   m.off_g % 4 == 0;
+  auto ld4 = [&](const float* q, int e) {
+    if (al4 && e + 3 < nel) return *reinterpret_cast<const f32x4*>(q + e);
+    f32x4 r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = e + i < nel ? q[e + i] : 0.f;
+    return r;
+  };
+  // ---- one staging round.  Issue order matters (vmcnt counts in order): the rows' tile
+  // extents first, so the dependent first-entry loads wait for them alone while the
+  // block's p / m / v quads and dz0 stay in flight ----
+  const int32_t* tst = m.ws_tstart;
+  const int ntp = m.n_tiles + 1;
+  const int sub = tid % TPR;
+  int xe0[2], xe1[2], cnt[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {              // rows tid / TPR (+ 64): the entry loads
+    const int r = min(tid / TPR + 64 * i, B - 1);
+    xe0[i] = tst[(size_t)r * ntp + tile];
+    xe1[i] = tst[(size_t)r * ntp + tile + 1];
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {              // wave 0: rows lane (+ 64): the slot scan
+    const int r = min(lane + 64 * i, B - 1);
+    cnt[i] = wave == 0 ? tst[(size_t)r * ntp + tile + 1] - tst[(size_t)r * ntp + tile] : 0;
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  f32x4 pp[FQ], pm[FQ], pv[FQ];
+#pragma unroll
+  for (int u = 0; u < FQ; ++u) {
+    const int e = 4 * (tid + UT * u);
+    pp[u] = pm[u] = pv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (fused && e < nel) { pp[u] = ld4(wblk, e); pm[u] = ld4(wblk + m.off_m, e); pv[u] = ld4(wblk + m.off_v, e); }
+  }
+  glds_copy(dz, m.ws_dz[0], B * H0, tid, UT);
+  __builtin_amdgcn_sched_barrier(0);
+  // each thread's first entry of each of its rows (clamped, unconditional)
+  int fi[2];
+  float fv[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int e = min(xe0[i] + sub, max(xe1[i] - 1, 0));
+    fi[i] = m.indices[e];
+    fv[i] = m.values[e];
+  }
+  if (wave == 0) {             // row counts -> slots, rows in order
+    int base = 0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = lane + 64 * i < nb ? cnt[i] : 0;
+      int x = c;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+      }
+      offs[lane + 64 * i] = base + x - c;
+      base += __shfl(x, 63, 64);
+    }
+    if (lane == 0) offs[128] = base;
+  }
+  vm_barrier();
+  const int total = offs[128];
+  // this thread's quads: word (row) v0 and column h0 of the first element; a quad spans at
+  // most two words (H0 >= 4): elements with h0 + i >= H0 belong to word v0 + 1
+  int qv[FQ], qh[FQ];
+#pragma unroll
+  for (int u = 0; u < FQ; ++u) {
+    const int el = 4 * (tid + UT * u);
+    qv[u] = el < nel ? el / H0 : -2;
+    qh[u] = el % H0;
+  }
+  f32x4 g[FQ];
+#pragma unroll
+  for (int u = 0; u < FQ; ++u) g[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int p0 = 0; p0 < total; p0 += CAP) {
+    if (p0) __syncthreads();                   // the previous pass's list reads are done
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = tid / TPR + 64 * i;
+      if (r >= nb) continue;
+      const int o = offs[r] - xe0[i];
+      int e = xe0[i] + sub;
+      if (e < xe1[i]) {                        // the first entry: already in registers
+        const int s = o + e - p0;
+        if (s >= 0 && s < CAP) {
+          ecol[s] = (r << 8) | (fi[i] - c0);
+          ex[s] = fv[i];
+        }
+      }
+      for (e += TPR; e < xe1[i]; e += TPR) {   // (rows with more than TPR entries here)
+        const int s = o + e - p0;
+        if (s >= 0 && s < CAP) {
+          ecol[s] = (r << 8) | (m.indices[e] - c0);
+          ex[s] = m.values[e];
+        }
+      }
+    }
+    __syncthreads();
+    const int n = min(CAP, total - p0);
+    for (int j = 0; j < n; ++j) {
+      const int cb = ecol[j];
+      const float x = ex[j];
+      const int col = cb & 255;
+      const float* dr = dz + (cb >> 8) * H0;
+#pragma unroll
+      for (int u = 0; u < FQ; ++u) {
+        const int d = col - qv[u];             // 0: this word, 1: the next one
+        if (d == 0 || d == 1) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int h = qh[u] + i - d * H0;  // the element's column in word col
+            if (h >= 0 && h < H0 && 4 * (tid + UT * u) + i < nel) g[u][i] += x * dr[h];
+          }
+        }
+      }
+    }
+  }
+  // ---- update (fused: Adam + FedAvg pre-scale) or the gradient ----
+  const AdamCoef ac = adam_coef(m);
+  const bool sh = is_shared(m, m.w_in);
+#pragma unroll
+  for (int u = 0; u < FQ; ++u) {
+    const int e = 4 * (tid + UT * u);
+    if (e >= nel) break;
+    f32x4 np, mo, vo;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float a = pm[u][i], b = pv[u][i];
+      const float x = fused ? adam_update(pp[u][i], g[u][i], a, b, ac) : g[u][i];
+      np[i] = sh && m.fed_scale_on && fused ? x * m.fed_scale : x;
+      mo[i] = a;
+      vo[i] = b;
+    }
+    auto st4 = [&](float* q, const f32x4& x) {
+      if (al4 && e + 3 < nel) { *reinterpret_cast<f32x4*>(q + e) = x; return; }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) if (e + i < nel) q[e + i] = x[i];
+    };
+    if (!fused) {
+      st4(wblk + m.off_g, np);
+    } else {
+      st4(wblk + m.off_m, mo);
+      st4(wblk + m.off_v, vo);
+      st4(wblk, np);
+    }
+  }
+}
+
 // grid: n_tiles + n_w + n_v + 1 (+ n_tiles for fused CombinedTM, + ceil(C / 64) for fused
 // ZeroShotTM) workgroups of 1024 threads.  The trailing tiles are the contextual input
 // layer: CombinedTM's Wc = rows V..2V-1 of the transposed W_in with the dense adapted
@@ -176,18 +354,21 @@ __device__ __forceinline__ void vector_job(const GfkModel& m, const GfkVJob& J) 
 // the batch's contextual rows x_ctx^T -- the same tile GEMM + Adam epilogue.
 // dynamic LDS: max(W_in tile: xt[64][stride_a(B)] + dz[B][stride_b(H0P)], weight job: 2 B 80)
 template <int UT>
-__global__ void __launch_bounds__(UT) gfk_win_update_k(GfkModel m, GfkUpdate U) {
+__global__ void __launch_bounds__(UT) gfk_win_update_k(const GfkModel* __restrict__ gm_, const GfkUpdate* __restrict__ gu_) {
+  const GfkModel& m = gm_[blockIdx.z];
+  const GfkUpdate& U = gu_[blockIdx.z];
   constexpr int UW = UT / 64;
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int nt_here = m.n_tiles;
   {
-    const int r = (int)blockIdx.x - m.n_tiles;
+    const int r = (int)blockIdx.x - nt_here;
     if (r >= 0 && r < U.n_w) { weight_job<UT>(m, U.w[r], smem); return; }
     if (r >= U.n_w && r < U.n_w + U.n_v) { vector_job<UT>(m, U.v[r - U.n_w]); return; }
     if (r == U.n_w + U.n_v) { prepare_next_batch(m); return; }
   }
   const bool zs = m.ctx_fused == 2;            // ZeroShotTM: W_in is the dense [C, H0] layer
   if (m.input == GFK_IN_CONTEXTUAL && !zs) return;   // (host GEMMs when not fused)
-  const int rr = (int)blockIdx.x - (m.n_tiles + U.n_w + U.n_v + 1);
+  const int rr = (int)blockIdx.x - (nt_here + U.n_w + U.n_v + 1);
   const bool ctxt = rr >= 0;                   // a Wc tile (CombinedTM) / W tile (ZeroShotTM)
   if (zs && !ctxt) return;                     // ZeroShotTM has no bag-of-words half
   const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
@@ -414,14 +595,36 @@ __global__ void __launch_bounds__(UT) gfk_win_update_k(GfkModel m, GfkUpdate U) 
   GFK_STAMP(m, 42);
 }
 
+// the sparse W_in tiles (stage_flags bit 4) as their own kernel: its register budget is
+// its own (the job paths of gfk_win_update_k need ~86 VGPRs)
+// grid: n_w + n_v + 1 job workgroups FIRST (they start with the tiles, not after them),
+// then the n_tiles sparse W_in tiles
+template <int UT>
+__global__ void __launch_bounds__(UT) gfk_win_sparse_k(const GfkModel* __restrict__ gm_, const GfkUpdate* __restrict__ gu_) {
+  const GfkModel& m = gm_[blockIdx.z];
+  const GfkUpdate& U = gu_[blockIdx.z];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int r = (int)blockIdx.x;
+  if (r < U.n_w) { weight_job<UT>(m, U.w[r], smem); return; }
+  if (r < U.n_w + U.n_v) { vector_job<UT>(m, U.v[r - U.n_w]); return; }
+  if (r == U.n_w + U.n_v) { prepare_next_batch(m); return; }
+  win_tile_sparse<UT>(m, smem, r - (U.n_w + U.n_v + 1));
+}
+
 extern "C" int gfk_launch_win_update(const GfkModel* m, const GfkUpdate* u, hipStream_t s) {
   const int extra = m->ctx_fused == 1 ? m->n_tiles : (m->ctx_fused == 2 ? (m->C + 63) / 64 : 0);
+  if (m->stage_flags & WIN_SPARSE) {
+    if (m->H[0] > 64 || m->input != GFK_IN_BOW || m->bmax > 128) return -1;
+    hipLaunchKernelGGL(gfk_win_sparse_k<512>, gfk_grid(dim3(u->n_w + u->n_v + 1 + m->n_tiles), m), dim3(512),
+                       gfk_win_update_smem(m), s, gfk_dev(m), reinterpret_cast<const GfkUpdate*>(m->dev_upd));
+    return (int)hipGetLastError();
+  }
   const dim3 g(m->n_tiles + u->n_w + u->n_v + 1 + extra);
   // more W_in tiles than two rounds of 16-wave workgroups (dec_grid = the CUs' slots)
   if (m->n_tiles > 2 * m->dec_grid && m->n_tiles > 512)
-    hipLaunchKernelGGL(gfk_win_update_k<512>, g, dim3(512), gfk_win_update_smem(m), s, *m, *u);
+    hipLaunchKernelGGL(gfk_win_update_k<512>, gfk_grid(g, m), dim3(512), gfk_win_update_smem(m), s, gfk_dev(m), reinterpret_cast<const GfkUpdate*>(m->dev_upd));
   else
-    hipLaunchKernelGGL(gfk_win_update_k<1024>, g, dim3(1024), gfk_win_update_smem(m), s, *m, *u);
+    hipLaunchKernelGGL(gfk_win_update_k<1024>, gfk_grid(g, m), dim3(1024), gfk_win_update_smem(m), s, gfk_dev(m), reinterpret_cast<const GfkUpdate*>(m->dev_upd));
   return (int)hipGetLastError();
 }
 
@@ -433,6 +636,9 @@ extern "C" int gfk_win_update_set_smem(size_t bytes) {
   cur = bytes;
   hipError_t e = hipFuncSetAttribute((const void*)gfk_win_update_k<512>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (e != hipSuccess) return (int)e;
+  e = hipFuncSetAttribute((const void*)gfk_win_sparse_k<512>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
   if (e != hipSuccess) return (int)e;
   return (int)hipFuncSetAttribute((const void*)gfk_win_update_k<1024>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);

@@ -65,6 +65,8 @@ class FederatedClient:
             from ..ops.engine import UPDATE_GRAD
             tm.engine.set_update_mode(UPDATE_GRAD)
         tm.engine.bind_data(self.data, self.plan)
+        if hasattr(tm.engine, "own_rng"):     # PyTorch engine: a per-client noise stream
+            tm.engine.own_rng(seed)
         tm.model.train()
         self.weight: Optional[float] = None
         # reference bookkeeping

@@ -106,7 +106,8 @@ class LocalFederation:
                  stop_at_num_epochs: bool = False, checkpoint_dir: Optional[str] = None,
                  checkpoint_every: int = 0, stamp: Optional[str] = None,
                  metrics_path: Optional[str] = None, metrics_every: int = 0, agg: str = "params",
-                 round_graph: Optional[bool] = None, round_streams: bool = True):
+                 round_graph: Optional[bool] = None, round_streams: bool = True,
+                 groups: Optional[Sequence[int]] = None, round_batched: Optional[bool] = None):
         self.logger = logger or logging.getLogger("gfedntm_amd.federation")
         self.agg_mode = agg
         self.metrics = MetricsWriter(metrics_path)
@@ -144,7 +145,9 @@ class LocalFederation:
             c.set_fedavg_weight(self.weights[i])
             c.enable_graph(graph and agg == "params")
             self.clients.append(c)
-        self.agg = LocalAggregator(n)
+        # groups: client-block sizes of a multi-rank layout (hierarchical/run_distributed_multi)
+        # -- the FedAvg sums each block first, then the block sums, in that run's order
+        self.agg = LocalAggregator(n, groups)
         # fused clients on one GPU: every client's step and the FedAvg kernel are
         # captured into ONE hipGraph per round (one replay instead of N step graphs
         # plus the eager aggregation), each client on its own stream: parallel graph
@@ -158,6 +161,11 @@ class LocalFederation:
                and self.agg._native([c.shared for c in self.clients]))
         self.round_graph = can if round_graph is None else (bool(round_graph) and can)
         self.round_streams = bool(round_streams)
+        # batched kernels (one launch per phase for every client, csrc grid z = client);
+        # GFEDNTM_ROUND_BATCHED=0 keeps one graph branch per client
+        self.round_batched = (round_batched if round_batched is not None else
+                              os.environ.get("GFEDNTM_ROUND_BATCHED", "1") == "1")
+        self._batched = None
         self._rg = None
         self._stop = False
         if self.round_graph:
@@ -182,6 +190,20 @@ class LocalFederation:
             e.prepare_external_capture()
         g = torch.cuda.CUDAGraph()
         shared = [c.shared for c in self.clients]
+        self._batched = None
+        if self.round_batched:
+            from ..ops.engine import BatchedSteps
+            if BatchedSteps.possible(engines):
+                # one launch per phase for all clients (grid z = client), then the FedAvg kernel
+                self._batched = BatchedSteps(engines)
+                self._batched.prepare()
+                with graph_capture(g):
+                    self._batched.launch()
+                    if not self.agg.fused_sum_(shared):
+                        raise RuntimeError("round graph needs the native FedAvg kernel")
+                self._rg = g
+                self._rg_gens = self._engine_gens()
+                return
         if self.round_streams:
             streams = [torch.cuda.Stream(self.device) for _ in engines]
             joins = [torch.cuda.Event() for _ in engines]

@@ -101,6 +101,39 @@ class TorchEngine(EngineBase):
         self.scheduler = (optim.lr_scheduler.ReduceLROnPlateau(self.optimizer, patience=10)
                           if reduce_on_plateau else None)
 
+    # ---- per-client random streams: dropout / reparameterisation noise drawn from the
+    # engine's own generator state instead of the process-global one, so a client's
+    # noise does not depend on how many other clients share its process (LocalFederation
+    # vs one or several clients per rank)
+    _rng_cpu = None
+    _rng_dev = None
+
+    def own_rng(self, seed: int):
+        self._rng_cpu = torch.Generator().manual_seed(int(seed)).get_state()
+        if self.device.type == "cuda":
+            self._rng_dev = torch.Generator(device=self.device).manual_seed(int(seed)).get_state()
+
+    def rng_state(self):
+        return None if self._rng_cpu is None else (self._rng_cpu, self._rng_dev)
+
+    def set_rng_state(self, st):
+        if st is not None:
+            self._rng_cpu, self._rng_dev = st
+
+    def _run_with_rng(self, fn):
+        if self._rng_cpu is None:
+            return fn()
+        cuda = self.device.type == "cuda"
+        with torch.random.fork_rng(devices=[self.device] if cuda else []):
+            torch.set_rng_state(self._rng_cpu)
+            if cuda:
+                torch.cuda.set_rng_state(self._rng_dev, self.device)
+            out = fn()
+            self._rng_cpu = torch.get_rng_state()
+            if cuda:
+                self._rng_dev = torch.cuda.get_rng_state(self.device)
+        return out
+
     def _batch(self, s: int):
         ids = torch.from_numpy(self.plan.batch(s).astype(np.int64)).to(self.device)
         x = self.data.dense_rows(ids)
@@ -124,6 +157,9 @@ class TorchEngine(EngineBase):
         return loss
 
     def step(self, s: int) -> torch.Tensor:
+        return self._run_with_rng(lambda: self._step(s))
+
+    def _step(self, s: int) -> torch.Tensor:
         self.model.train()
         x, ctx, lab = self._batch(s)
         self.model.zero_grad()
@@ -140,6 +176,9 @@ class TorchEngine(EngineBase):
         return self._grad_buf
 
     def compute_grads(self, s: int) -> torch.Tensor:
+        return self._run_with_rng(lambda: self._compute_grads(s))
+
+    def _compute_grads(self, s: int) -> torch.Tensor:
         self.model.train()
         x, ctx, lab = self._batch(s)
         self.model.zero_grad()

@@ -55,6 +55,7 @@ VB = 64
 STAGE_PLANS = (1, 0, 3, 2)
 STAGE_FWD_STRIP = 4               # bit 2: ProdLDA strip forward (csrc/prodlda.hip)
 STAGE_FWD_STRIP_PF = 8            # bit 3: its prefetching 8-wave variant
+STAGE_WIN_SPARSE = 16             # bit 4: sparse W_in tiles (csrc/update.hip win_tile_sparse)
 
 
 def _explain(ok: bool, why: str, explain: bool) -> bool:
@@ -292,6 +293,14 @@ class FusedEngine(EngineBase):
         self._m = abi.GfkModel()
         self._a = abi.GfkAdam()
         self._u = abi.GfkUpdate()
+        # the kernels read the model / update descriptors from device memory (one entry per
+        # client of a batched launch: csrc gfk_dev / gfk_grid); this engine's own copies,
+        # uploaded whenever the host structs change (_sync_dev)
+        self._dev_m = torch.zeros(C.sizeof(abi.GfkModel), dtype=torch.uint8, device=self.device)
+        self._dev_u = torch.zeros(C.sizeof(abi.GfkUpdate), dtype=torch.uint8, device=self.device)
+        self._dev_bytes = (None, None)
+        self._m.dev, self._m.dev_upd, self._m.n_batch = (self._dev_m.data_ptr(),
+                                                         self._dev_u.data_ptr(), 1)
         self._phases = None
         self._nb_int = {}
         self._fill_static()
@@ -470,6 +479,19 @@ class FusedEngine(EngineBase):
                     m.n_dpart = min(cu // 4, m.n_tiles - 1)
             else:
                 m.n_dpart = cu
+            # the persistent k-range backward (4 workgroups per vocab tile) takes its
+            # logit-gradient tiles precomputed once per tile by prodlda_dlogit instead of
+            # recomputing them in each range workgroup; GFEDNTM_BWD_PRE=0 selects the
+            # recomputing variant
+            kq4 = m.n_dpart < m.n_tiles and -(-m.K // 16) >= 4
+            pre = os.environ.get("GFEDNTM_BWD_PRE", "2")
+            m.bwd_pre = int(pre) if kq4 and m.bmax <= 64 and pre in ("1", "2") else 0
+            if m.bwd_pre == 1 and 3 * self.lib.gfk_smem_required(C.byref(m), 1) <= LDS_LIMIT:
+                # its smaller LDS plan (no logit tile, G aliases dt) and <= 80 VGPRs fit
+                # THREE range workgroups per CU: 3/4 of a CU's slots per slab of 4
+                m.n_dpart = min(3 * cu // 4, m.n_tiles - 1)
+            elif m.bwd_pre:
+                m.bwd_pre = 2            # two per CU, no register cap
             # GFEDNTM_BETA_SPLIT=1: beta's Adam as one streaming float4 pass after
             # prodlda_bwd (which then only writes the gradient) instead of the epilogue.
             # The pass alone runs at 5.7-6.7 TB/s vs 4.2 for the epilogue's layout
@@ -478,6 +500,14 @@ class FusedEngine(EngineBase):
             # shrink without the Adam work, so the extra pass is added, not overlapped
             m.beta_split = int(os.environ.get("GFEDNTM_BETA_SPLIT", "0") == "1"
                                and self.update_mode == UPDATE_FUSED)
+        # W_in tiles as entry lists instead of dense x^T MFMA tiles where a 64-word tile
+        # holds few non-zeros (large vocabularies, the 8-wave update shape: more tiles than
+        # two rounds of workgroups); GFEDNTM_WIN_SPARSE=0 keeps the dense tiles
+        cu_n = props.multi_processor_count
+        ws_env = os.environ.get("GFEDNTM_WIN_SPARSE", "auto")
+        if m.input == abi.IN_BOW and int(m.H[0]) <= 64 and m.bmax <= 128 and (
+                ws_env == "1" or (ws_env == "auto" and m.n_tiles > 4 * cu_n)):
+            m.stage_flags |= STAGE_WIN_SPARSE
         self._alloc_workspace()
         rc = self.lib.gfk_setup(C.byref(m))
         if rc:
@@ -555,6 +585,8 @@ class FusedEngine(EngineBase):
             # pre-activation partials (csrc/ctx.hip)
             "actx": f(m.n_tiles * B * 64 if m.ctx_fused == 1 else 1),
             "hpart": f(m.n_tiles * B * hs[0] if m.ctx_fused == 1 else 1),
+            # precomputed logit-gradient tiles [n_tiles][B][66] (bwd_pre)
+            "dt": f(m.n_tiles * B * 66 if m.bwd_pre else 1),
         }
         Lb = max(int(m.L), 1)
         ws.update(lab=f(B, Lb), dlab=f(B, Lb), ce=f(B), thd=f(B, K))   # label head
@@ -781,7 +813,11 @@ class FusedEngine(EngineBase):
             b0 = flat.slots["beta"].offset
             parts = {"rest": shared[:b0], "beta": shared[b0:]}
         aggs = {k: CollectiveAggregator(group, method=method) for k in parts}
-        methods = {k: aggs[k].prepare(v) for k, v in parts.items()}
+        # large parts (beta at V ~ 100k: 90 MB) are all-reduced in place: the xGMI kernel
+        # maps the state itself into the peers instead of copying it into a stage first
+        # (2 S of local HBM traffic per round saved, one extra hand-off)
+        big = int(float(os.environ.get("GFEDNTM_XGMI_INPLACE_MB", "8")) * (1 << 20))
+        methods = {k: aggs[k].prepare(v, inplace=4 * v.numel() >= big) for k, v in parts.items()}
         # setup cost of the data plane (IPC mapping, validation, RCCL-vs-xGMI timing)
         self.fedavg_attach = {"s": round(sum(a.setup_s for a in aggs.values()), 4),
                               "bytes": {k: 4 * v.numel() for k, v in parts.items()},
@@ -993,6 +1029,7 @@ class FusedEngine(EngineBase):
                     (abi.INFER_MOMENTS if moments else 0)
                 p.thr, p.seed, p.doc0 = float(threshold), int(seed) % (1 << 64), d0
                 p.grid = int(max(1, min(-(-(d1 - d0) // 8), 4 * cu)))   # 8 waves (docs) per WG
+                self._sync_dev()
                 rc = self.lib.gfk_theta_infer(C.byref(m), C.byref(p), stream)
                 if rc:
                     raise RuntimeError(f"gfk_theta_infer failed ({rc})")
@@ -1022,7 +1059,20 @@ class FusedEngine(EngineBase):
             return
         self._launch_native(phases)
 
+    def _sync_dev(self):
+        """Upload the model / update descriptors if the host structs changed (a stream-
+        ordered copy; never inside a graph capture: captures sync first)."""
+        bm, bu = bytes(self._m), bytes(self._u)
+        if (bm, bu) == self._dev_bytes:
+            return
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("fused engine descriptors changed inside a graph capture")
+        self._dev_m.copy_(torch.frombuffer(bytearray(bm), dtype=torch.uint8))
+        self._dev_u.copy_(torch.frombuffer(bytearray(bu), dtype=torch.uint8))
+        self._dev_bytes = (bm, bu)
+
     def _launch_native(self, phases):
+        self._sync_dev()
         arr, n = abi.phase_array(phases)
         stream = torch.cuda.current_stream(self.device).cuda_stream
         rc = self.lib.gfk_run(C.byref(self._m), C.byref(self._a), self.adam_grid,
@@ -1059,6 +1109,7 @@ class FusedEngine(EngineBase):
             self._ctx_fwd()
             self._ctx_bwd()
             torch.cuda.synchronize(self.device)
+        self._sync_dev()
         g = torch.cuda.CUDAGraph()
         saved = (self.d_step.clone(), self.adam_t.clone(), self.adam_pow.clone(),
                  self.adam_coef.clone())
@@ -1081,6 +1132,7 @@ class FusedEngine(EngineBase):
     # the in-process FedAvg kernel in one hipGraph)
     def prepare_external_capture(self):
         """Run anything that must not happen for the first time inside a capture."""
+        self._sync_dev()
         if self._ctx is not None and not self.ctx_fused:
             self._ctx_fwd()
             self._ctx_bwd()
@@ -1145,3 +1197,96 @@ class FusedEngine(EngineBase):
 
     def load_optimizer_state_dict(self, sd):
         self.optimizer.load_state_dict(sd)
+
+
+# the GfkModel fields that fix a launch's grid, block and LDS: engines batched into one
+# launch per phase must agree on all of them (their pointers and per-client values differ)
+_BATCH_SHAPE_FIELDS = ("bmax", "V", "K", "n_hidden", "act", "kind", "input", "C", "L", "vb",
+                       "n_tiles", "dec_grid", "learn_priors", "stage_flags", "kt", "n_dpart",
+                       "beta_split", "update_mode", "ctx_fused", "ctx_kb", "ctx_ckb", "mm_bf16",
+                       "lab_on", "lab_off", "lab_in_enc", "bwd_pre")
+
+
+class BatchedSteps:
+    """One launch per phase for the local steps of several fused engines (clients).
+
+    Every kernel reads its GfkModel / GfkUpdate from a device array indexed by blockIdx.z
+    (csrc gfk_dev / gfk_grid), so M clients' step = the kernels of ONE client with
+    gridDim.z = M: a K = 50 client fills ~70 of the 256 CUs per kernel, M of them fill the
+    GPU in the same few microseconds, instead of M graph branches of small kernels
+    competing for hardware queues.  Requirements: the same shapes (_BATCH_SHAPE_FIELDS),
+    the same phase list, every phase native (no host GEMMs / host collectives)."""
+
+    def __init__(self, engines: List["FusedEngine"]):
+        self.validate(engines)
+        self.engines = list(engines)
+        e0 = engines[0]
+        self.device = e0.device
+        M = len(engines)
+        self._arr_m = torch.zeros(M * C.sizeof(abi.GfkModel), dtype=torch.uint8, device=self.device)
+        self._arr_u = torch.zeros(M * C.sizeof(abi.GfkUpdate), dtype=torch.uint8, device=self.device)
+        self._blob = None
+        self._host = None
+        self._phases = e0.phases()
+
+    @staticmethod
+    def possible(engines) -> bool:
+        try:
+            BatchedSteps.validate(engines)
+            return True
+        except (ValueError, AttributeError):
+            return False
+
+    @staticmethod
+    def validate(engines):
+        if len(engines) < 1:
+            raise ValueError("no engines")
+        e0 = engines[0]
+        ph = e0.phases()
+        if abi.PH_ADAM in ph:
+            raise ValueError("batched launches run the fused update mode (no generic optimizer)")
+        for e in engines:
+            if e.device != e0.device:
+                raise ValueError("batched engines must share a device")
+            if e.phases() != ph:
+                raise ValueError("batched engines must run the same phases")
+            if any(p in abi.HOST_PHASES for p in ph) or e._comm is not None:
+                raise ValueError("batched launches need native phases only")
+            for f in _BATCH_SHAPE_FIELDS:
+                a, b = getattr(e._m, f), getattr(e0._m, f)
+                if (list(a) if hasattr(a, "__len__") else a) != (list(b) if hasattr(b, "__len__") else b):
+                    raise ValueError(f"batched engines differ in {f}")
+            if list(e._m.H) != list(e0._m.H) or e._u.n_w != e0._u.n_w or e._u.n_v != e0._u.n_v:
+                raise ValueError("batched engines differ in their layer / job tables")
+
+    def _refresh(self):
+        M = len(self.engines)
+        ms, us = [], []
+        for e in self.engines:
+            mm = abi.GfkModel.from_buffer_copy(bytes(e._m))
+            mm.dev, mm.dev_upd, mm.n_batch = self._arr_m.data_ptr(), self._arr_u.data_ptr(), M
+            ms.append(bytes(mm))
+            us.append(bytes(e._u))
+        blob = b"".join(ms) + b"".join(us)
+        if blob != self._blob:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("batched engine descriptors changed inside a graph capture")
+            self._arr_m.copy_(torch.frombuffer(bytearray(b"".join(ms)), dtype=torch.uint8))
+            self._arr_u.copy_(torch.frombuffer(bytearray(b"".join(us)), dtype=torch.uint8))
+            self._blob = blob
+        self._host = abi.GfkModel.from_buffer_copy(ms[0])
+
+    def prepare(self):
+        """Upload the descriptors now (before a capture)."""
+        self._refresh()
+
+    def launch(self):
+        """Enqueue one local step of every engine on the current stream."""
+        self._refresh()
+        e0 = self.engines[0]
+        arr, n = abi.phase_array(self._phases)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        rc = e0.lib.gfk_run(C.byref(self._host), C.byref(e0._a), e0.adam_grid,
+                            C.byref(e0._u), stream, arr, n)
+        if rc:
+            raise RuntimeError(f"gfk_run (batched) failed: code {rc}")

@@ -51,16 +51,18 @@ class CollectiveAggregator:
         self.tuning = None
         self.setup_s = 0.0
 
-    def prepare(self, flat: torch.Tensor) -> str:
+    def prepare(self, flat: torch.Tensor, inplace: bool = False) -> str:
         """Choose the all-reduce for buffers shaped like ``flat`` (call once, on every
-        rank, before the timed / captured region).  Returns the method in use."""
+        rank, before the timed / captured region).  ``inplace``: the xGMI kernel maps
+        ``flat`` itself into the peers (no stage copy; every later call must pass this
+        very buffer).  Returns the method in use."""
         t_setup = time.perf_counter()
         try:
-            return self._prepare(flat)
+            return self._prepare(flat, inplace)
         finally:
             self.setup_s = time.perf_counter() - t_setup
 
-    def _prepare(self, flat: torch.Tensor) -> str:
+    def _prepare(self, flat: torch.Tensor, inplace: bool = False) -> str:
         if self.world == 1 or self.method == "rccl" or flat.device.type != "cuda":
             self.active = "rccl"
             return self.active
@@ -72,7 +74,8 @@ class CollectiveAggregator:
         if ok:
             from .xgmi import XgmiAllReduce
             try:
-                xg = XgmiAllReduce(flat.numel(), flat.device, group=self.group)
+                xg = XgmiAllReduce(flat.numel(), flat.device, group=self.group,
+                                   data=flat if inplace else None)
             except Exception as e:   # every rank must reach the agreement below
                 import logging
                 logging.getLogger("gfedntm_amd.xgmi").warning("xGMI all-reduce setup failed: %s", e)
@@ -91,10 +94,15 @@ class CollectiveAggregator:
             # CommError after training
             spin = xg.c.spin_limit
             xg.c.spin_limit = max(spin, 1 << 26)
+            saved = flat.clone() if inplace else None
             try:
-                tx = self._time(xg.allreduce_, flat)
+                # (in-place: timed on the registered buffer itself, restored after)
+                tx = self._time(xg.allreduce_, flat, on=flat if inplace else None)
             finally:
                 xg.c.spin_limit = spin
+                if saved is not None:
+                    flat.copy_(saved)
+                    del saved
             err = xg.error()
             tr = self._time(lambda b: dist.all_reduce(b, group=self.group), flat)
             t = torch.tensor([tx, tr, float(err != 0)], dtype=torch.float64, device=flat.device)
@@ -114,10 +122,11 @@ class CollectiveAggregator:
             self.active = "rccl"
         return self.active
 
-    def _time(self, fn, like: torch.Tensor, iters: int = 10, warmup: int = 3) -> float:
+    def _time(self, fn, like: torch.Tensor, iters: int = 10, warmup: int = 3,
+              on: Optional[torch.Tensor] = None) -> float:
         """Mean ms of ``fn`` (an in-place all-reduce) on a scratch buffer shaped like
-        ``like``; every rank runs it the same number of times."""
-        buf = torch.zeros_like(like)
+        ``like`` (or on ``on``); every rank runs it the same number of times."""
+        buf = torch.zeros_like(like) if on is None else on
         for _ in range(warmup):
             fn(buf)
         torch.cuda.synchronize(like.device)
@@ -160,7 +169,46 @@ class CollectiveAggregator:
 
 class _GfkLocalAvg(ctypes.Structure):
     _fields_ = [("f", ctypes.c_void_p * 16), ("n_clients", ctypes.c_int32),
-                ("pad", ctypes.c_int32), ("n", ctypes.c_int64)]
+                ("mode", ctypes.c_int32), ("n", ctypes.c_int64), ("n_groups", ctypes.c_int32),
+                ("gend", ctypes.c_int32 * 16), ("pad", ctypes.c_int32)]
+
+
+LOCAL_ALL, LOCAL_FIRST, LOCAL_BCAST = 0, 1, 2     # gfk_local_fedavg modes (csrc/comm.hip)
+
+
+def local_fedavg(flats: Sequence[torch.Tensor], mode: int = LOCAL_ALL,
+                 groups: Optional[Sequence[int]] = None):
+    """One launch of csrc/comm.hip ``gfk_local_fedavg`` on the current stream (capture
+    safe): the group-wise left-fold sum of ``flats`` (``groups``: sizes of consecutive
+    client groups, default one group) written to every buffer (LOCAL_ALL) or to
+    flats[0] only (LOCAL_FIRST), or flats[0] copied to the others (LOCAL_BCAST)."""
+    C = ctypes
+    from ..ops import native
+    lib = native.kernels()
+    if not getattr(lib, "_gfk_local_avg_declared", False):
+        lib.gfk_local_avg_struct_size.restype = C.c_size_t
+        lib.gfk_local_fedavg_launch.argtypes = [C.POINTER(_GfkLocalAvg), C.c_int, C.c_void_p]
+        if lib.gfk_local_avg_struct_size() != C.sizeof(_GfkLocalAvg):
+            raise RuntimeError("GfkLocalAvg ABI mismatch between csrc/comm.hip and aggregator.py")
+        lib._gfk_local_avg_declared = True
+    groups = [len(flats)] if groups is None else [int(g) for g in groups]
+    if sum(groups) != len(flats) or min(groups) < 1:
+        raise ValueError(f"groups {groups} do not partition {len(flats)} clients")
+    d = _GfkLocalAvg()
+    for j, f in enumerate(flats):
+        d.f[j] = f.data_ptr()
+    d.n_clients, d.n, d.mode, d.n_groups = len(flats), flats[0].numel(), int(mode), len(groups)
+    e = 0
+    for i, g in enumerate(groups):
+        e += g
+        d.gend[i] = e
+    cu = torch.cuda.get_device_properties(flats[0].device).multi_processor_count
+    grid = int(max(1, min(-(-d.n // 1024), 4 * cu)))
+    stream = torch.cuda.current_stream(flats[0].device).cuda_stream
+    rc = lib.gfk_local_fedavg_launch(C.byref(d), grid, C.c_void_p(stream))
+    if rc:
+        raise RuntimeError(f"gfk_local_fedavg_launch failed ({rc})")
+    return d
 
 
 class LocalAggregator:
@@ -168,11 +216,18 @@ class LocalAggregator:
 
     On a GPU, pre-scaled buffers of up to 16 clients are summed by one HIP kernel
     (csrc/comm.hip ``gfk_local_fedavg``: client-order sum written back to every
-    client, capture-safe); the eager torch sequence is the CPU / oracle path."""
+    client, capture-safe); the eager torch sequence is the CPU / oracle path.
+    ``groups`` (sizes of consecutive client groups) sums group-wise first, then the
+    group sums in order: the summation tree of the same clients spread over ranks
+    (each rank folds its clients, the collective folds the ranks), so the in-process
+    golden and the distributed run agree bit for bit."""
 
-    def __init__(self, n_samples: Sequence[int]):
+    def __init__(self, n_samples: Sequence[int], groups: Optional[Sequence[int]] = None):
         self.n = [int(x) for x in n_samples]
         self.w = fedavg_weights(self.n)
+        self.groups = None if groups is None else [int(g) for g in groups]
+        if self.groups is not None and sum(self.groups) != len(self.n):
+            raise ValueError(f"groups {self.groups} do not partition {len(self.n)} clients")
         self._desc = None
 
     def _native(self, flats: Sequence[torch.Tensor]) -> bool:
@@ -183,32 +238,14 @@ class LocalAggregator:
                    and f.numel() == n and f.data_ptr() % 16 == 0 for f in flats)
 
     def fused_sum_(self, flats: Sequence[torch.Tensor]):
-        """flats[i] <- sum_j flats[j] (client order) for all i, one kernel launch on the
-        current stream.  Returns False when the buffers don't qualify (caller falls back)."""
+        """flats[i] <- sum_j flats[j] (client order, group-wise) for all i, one kernel
+        launch on the current stream.  Returns False when the buffers don't qualify
+        (caller falls back)."""
         if len(flats) == 1:
             return True
         if not self._native(flats):
             return False
-        C = ctypes
-        from ..ops import native
-        lib = native.kernels()
-        if not getattr(lib, "_gfk_local_avg_declared", False):
-            lib.gfk_local_avg_struct_size.restype = C.c_size_t
-            lib.gfk_local_fedavg_launch.argtypes = [C.POINTER(_GfkLocalAvg), C.c_int, C.c_void_p]
-            if lib.gfk_local_avg_struct_size() != C.sizeof(_GfkLocalAvg):
-                raise RuntimeError("GfkLocalAvg ABI mismatch between csrc/comm.hip and aggregator.py")
-            lib._gfk_local_avg_declared = True
-        d = _GfkLocalAvg()
-        for j, f in enumerate(flats):
-            d.f[j] = f.data_ptr()
-        d.n_clients, d.n = len(flats), flats[0].numel()
-        cu = torch.cuda.get_device_properties(flats[0].device).multi_processor_count
-        grid = int(max(1, min(-(-d.n // 1024), 4 * cu)))
-        stream = torch.cuda.current_stream(flats[0].device).cuda_stream
-        rc = lib.gfk_local_fedavg_launch(C.byref(d), grid, C.c_void_p(stream))
-        if rc:
-            raise RuntimeError(f"gfk_local_fedavg_launch failed ({rc})")
-        self._desc = d
+        self._desc = local_fedavg(flats, LOCAL_ALL, self.groups)
         return True
 
     def average_(self, flats: Sequence[torch.Tensor], prescaled: bool = False,
@@ -219,11 +256,27 @@ class LocalAggregator:
         if prescaled and out is None and self.fused_sum_(flats):
             return flats[0]
         acc = torch.zeros_like(flats[0]) if out is None else out.zero_()
-        for w, f in zip(self.w, flats):
-            if prescaled:
-                acc.add_(f)
+        if self.groups is None:
+            for w, f in zip(self.w, flats):
+                if prescaled:
+                    acc.add_(f)
+                else:
+                    acc.add_(f, alpha=w)
+            for f in flats:
+                f.copy_(acc)
+            return acc
+        groups = self.groups
+        j = 0
+        for gi, g in enumerate(groups):
+            part = None
+            for _ in range(g):
+                f = flats[j] if prescaled else flats[j] * self.w[j]
+                part = f.clone() if part is None else part.add_(f)
+                j += 1
+            if gi == 0:
+                acc.copy_(part)
             else:
-                acc.add_(f, alpha=w)
+                acc.add_(part)
         for f in flats:
             f.copy_(acc)
         return acc

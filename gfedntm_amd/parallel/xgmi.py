@@ -38,7 +38,7 @@ class GfkComm(C.Structure):
     _fields_ = [("stage", (P * CMAX) * 2), ("flags", P * CMAX), ("epoch", P), ("err", P),
                 ("rank", C.c_int32), ("world", C.c_int32), ("nblk", C.c_int32),
                 ("spin_limit", C.c_int32), ("n", C.c_int64), ("chunk", C.c_int64),
-                ("slice", C.c_int64)]
+                ("slice", C.c_int64), ("inplace", C.c_int32), ("pad", C.c_int32)]
 
 
 def _declare(lib):
@@ -51,6 +51,7 @@ def _declare(lib):
     lib.gfk_ipc_get.argtypes = [P, P]
     lib.gfk_ipc_open.argtypes = [P, C.POINTER(P)]
     lib.gfk_ipc_close.argtypes = [P]
+    lib.gfk_ipc_get_range.argtypes = [P, P, C.POINTER(C.c_int64)]
     lib.gfk_comm_launch.argtypes = [C.POINTER(GfkComm), P, P]
     lib.gfk_comm_error.argtypes = [C.POINTER(GfkComm)]
     lib.gfk_comm_error_async.argtypes = [C.POINTER(GfkComm), P, P]
@@ -68,7 +69,9 @@ class XgmiAllReduce:
     single-node process group (≤ 8 ranks; several ranks may share one GPU)."""
 
     def __init__(self, n: int, device, group=None, nblk: Optional[int] = None,
-                 spin_limit: Optional[int] = None):
+                 spin_limit: Optional[int] = None, data: Optional[torch.Tensor] = None):
+        """``data``: in-place mode -- this fixed buffer (every call must pass it) is itself
+        IPC-mapped into the peers, so no stage copy of the state is made (large states)."""
         self.lib = native.kernels()
         _declare(self.lib)
         self.group = group
@@ -88,10 +91,15 @@ class XgmiAllReduce:
         self.nblk = nblk
         slice_ = _up4(-(-chunk // nblk))
         self._handles: List[int] = []
+        self.data = data
+        inplace = data is not None
+        if inplace and (data.dtype != torch.float32 or not data.is_contiguous()
+                        or data.numel() != self.n or data.data_ptr() % 16):
+            raise ValueError("xGMI in-place buffer: fp32, contiguous, 16-B aligned, n floats")
         with torch.cuda.device(self.device):
             stage, flags, state = P(), P(), P()
-            stage_bytes = self.world * chunk * 4
-            flag_bytes = 2 * nblk * CMAX * 4
+            stage_bytes = 16 if inplace else self.world * chunk * 4
+            flag_bytes = (3 if inplace else 2) * nblk * CMAX * 4
             rc = self.lib.gfk_comm_alloc(stage_bytes, flag_bytes, nblk * 4 + 16,
                                          C.byref(stage), C.byref(flags), C.byref(state))
             if rc:
@@ -99,23 +107,32 @@ class XgmiAllReduce:
             self._own = (stage.value, flags.value, state.value)
             hs = self.lib.gfk_ipc_handle_size()
             mine = []
-            for ptr in (stage.value, flags.value):
+            offset = 0
+            for ptr in ((data.data_ptr() if inplace else stage.value), flags.value):
                 h = C.create_string_buffer(hs)
-                rc = self.lib.gfk_ipc_get(P(ptr), h)
+                if inplace and not mine:
+                    off = C.c_int64(0)
+                    rc = self.lib.gfk_ipc_get_range(P(ptr), h, C.byref(off))
+                    offset = int(off.value)
+                else:
+                    rc = self.lib.gfk_ipc_get(P(ptr), h)
                 if rc:
                     raise RuntimeError(f"hipIpcGetMemHandle failed ({rc})")
                 mine.append(h.raw)
+            mine.append(offset)
             allh: List = [None] * self.world
             dist.all_gather_object(allh, mine, group=group)
             c = GfkComm()
             for j in range(self.world):
                 if j == self.rank:
-                    sp, fp = stage.value, flags.value
+                    sp = data.data_ptr() if inplace else stage.value
+                    fp = flags.value
                 else:
-                    sp, fp = self._open(allh[j][0]), self._open(allh[j][1])
+                    sp, fp = self._open(allh[j][0]) + allh[j][2], self._open(allh[j][1])
                 c.stage[0][j] = sp
-                c.stage[1][j] = sp + stage_bytes
+                c.stage[1][j] = sp if inplace else sp + stage_bytes
                 c.flags[j] = fp
+            c.inplace = int(inplace)
             c.epoch = state.value
             c.err = state.value + nblk * 4
             c.rank, c.world, c.nblk, c.spin_limit = self.rank, self.world, nblk, int(spin_limit)
@@ -150,6 +167,8 @@ class XgmiAllReduce:
         if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != self.n \
                 or t.device != self.device or t.data_ptr() % 16:
             raise ValueError("xGMI all-reduce: fp32, contiguous, 16-B aligned, fixed size")
+        if self.data is not None and t.data_ptr() != self.data.data_ptr():
+            raise ValueError("xGMI in-place all-reduce: only on the registered buffer")
         stream = torch.cuda.current_stream(self.device).cuda_stream
         rc = self.lib.gfk_comm_launch(C.byref(self.c), P(t.data_ptr()), P(stream))
         if rc:
@@ -186,10 +205,14 @@ class XgmiAllReduce:
         ok = True
         spin = self.c.spin_limit
         self.c.spin_limit = max(spin, 1 << 26)
+        saved = self.data.clone() if self.data is not None else None
         try:
             with torch.cuda.device(self.device):
                 for r in range(rounds):
                     t = self._probe(self.rank, r)
+                    if self.data is not None:     # in-place: the probe goes through the buffer
+                        self.data.copy_(t)
+                        t = self.data
                     self.allreduce_(t)
                     exp = self._probe(0, r)
                     for j in range(1, self.world):      # the kernel's order: rank 0, 1, ...
@@ -202,6 +225,9 @@ class XgmiAllReduce:
             ok = False
         finally:
             self.c.spin_limit = spin
+            if saved is not None:
+                self.data.copy_(saved)
+                torch.cuda.synchronize(self.device)
         flags: List = [None] * self.world
         dist.all_gather_object(flags, ok, group=self.group)
         return all(flags)

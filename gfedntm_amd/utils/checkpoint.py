@@ -39,11 +39,16 @@ def save_client_checkpoint(ckpt_dir: str, client, round_: int) -> str:
         "book": {k: getattr(client, k) for k in _BOOK},
         "best_loss_train": float(tm.best_loss_train),
         "seed": int(getattr(eng, "seed", 0)),
-        # the torch engine draws dropout / reparameterisation noise from the global RNG
+        # the global RNG (anything not on an engine-owned stream)
         "rng_cpu": torch.get_rng_state(),
         "rng_cuda": (torch.cuda.get_rng_state(eng.device) if eng.device.type == "cuda"
                      else torch.zeros(0, dtype=torch.uint8)),
     }
+    if getattr(eng, "rng_state", None) is not None and eng.rng_state() is not None:
+        # the PyTorch engine's own per-client noise stream (cpu, device)
+        cpu_st, dev_st = eng.rng_state()
+        state["rng_engine_cpu"] = cpu_st
+        state["rng_engine_dev"] = dev_st if dev_st is not None else torch.zeros(0, dtype=torch.uint8)
     if hasattr(eng, "adam_pow"):
         # the fused kernels advance beta^t on device by repeated fp64 products;
         # recomputing beta ** t on resume could differ in the last bit, so the device
@@ -84,6 +89,9 @@ def load_client_checkpoint(ckpt_dir: str, client, round_: Optional[int] = None) 
     torch.set_rng_state(st["rng_cpu"])
     if eng.device.type == "cuda" and st["rng_cuda"].numel():
         torch.cuda.set_rng_state(st["rng_cuda"], eng.device)
+    if "rng_engine_cpu" in st and hasattr(eng, "set_rng_state"):
+        dev_st = st["rng_engine_dev"]
+        eng.set_rng_state((st["rng_engine_cpu"], dev_st if dev_st.numel() else None))
     if hasattr(eng, "adam_pow") and "adam_pow" in st:
         eng.adam_pow.copy_(st["adam_pow"].to(eng.adam_pow.device))
         eng.adam_coef.copy_(st["adam_coef"].to(eng.adam_coef.device))

@@ -136,3 +136,65 @@ def test_timed_out_wait_is_caught_between_aligned_rounds(tmp_path):
         assert r[1] == "comm_error", r[:2]
         before = int(r[2].split("before round ")[1].split()[0])
         assert before < 400, r[2]         # stopped before max_iters
+
+
+N_MULTI = 8                      # clients, over 2 ranks: 4 per rank
+
+
+def _multi_corpora():
+    from gfedntm_amd.data.synthetic import generate_synthetic
+    from gfedntm_amd.federation.data import ClientCorpus
+    sc = generate_synthetic(vocab_size=500, n_topics=10, n_docs=60, n_nodes=N_MULTI,
+                            frozen_topics=2, nwords=(30, 60), seed=9)
+    return [ClientCorpus(synthetic=sc, node=i) for i in range(N_MULTI)]
+
+
+def _multi_worker(rank, world, port, tmp, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    try:
+        from gfedntm_amd.federation.hierarchical import assign_clients, run_distributed_multi
+        ids = assign_clients(N_MULTI, world)[rank]
+        corpora = _multi_corpora()
+        out = run_distributed_multi([corpora[i - 1] for i in ids], ids, _params(), max_iters=ROUNDS,
+                                    backend="fused", seed=5, rehearse_1gpu=True,
+                                    save_client=os.path.join(tmp, "client"), stamp="20240101")
+        q.put((rank, out["allreduce"], [c.shared.detach().cpu().numpy().copy() for c in out["clients"]],
+               [c.id for c in out["clients"]]))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, "exception", traceback.format_exc(), None))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_more_clients_than_ranks_xgmi_matches_grouped_golden(tmp_path):
+    """8 clients on 2 ranks (4 per rank, one GPU): every rank's round graph holds its 4
+    clients' steps, the in-rank fold, the xGMI all-reduce of the partial sums and the
+    broadcast; the final state of all 8 clients equals the in-process federation with
+    the same grouping bit for bit, and every client saves its results."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_multi_worker, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(2)], key=lambda r: r[0])
+    for p in ps:
+        p.join(60)
+    for r in res:
+        assert r[1] != "exception", r[2]
+        assert r[1].startswith("xgmi"), r[1]
+    assert [i for r in res for i in r[3]] == list(range(1, N_MULTI + 1))
+    from gfedntm_amd.federation.runner import LocalFederation
+    fed = LocalFederation(_multi_corpora(), _params(), max_iters=ROUNDS, device="cuda",
+                          backend="fused", seed=5, groups=[4, 4])
+    assert fed.round_graph
+    fed.run()
+    gold = fed.clients[0].shared.detach().cpu().numpy()
+    for r in res:
+        for sh in r[2]:
+            np.testing.assert_array_equal(sh, gold)
+    for i in range(1, N_MULTI + 1):
+        assert os.path.exists(tmp_path / f"client{i}" / f"model_{i}_20240101.npz")

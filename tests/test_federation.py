@@ -43,16 +43,20 @@ def test_rounds_match_reference_semantics():
         models.append((m, make_optimizer(m.parameters(), "adam", 2e-3, 0.99)))
     n = np.array([c.n_docs for c in fed.clients], dtype=np.float64)
     w = n / n.sum()
-    torch.manual_seed(7)
     fed.run()
-    torch.manual_seed(7)
+    # each client draws its noise from its own stream seeded with its client seed (as
+    # the reference's clients, one process each, do)
+    states = [torch.Generator().manual_seed(2 + c.id).get_state() for c in fed.clients]
     for it in range(6):
-        for (m, opt), c in zip(models, fed.clients):
+        for i, ((m, opt), c) in enumerate(zip(models, fed.clients)):
             ids = torch.from_numpy(c.plan.batch(it).astype(np.int64))
             x = c.data.dense_rows(ids)
             m.train()
             opt.zero_grad()
-            pm, pv, mu, var, lv, wd = m(x)
+            with torch.random.fork_rng(devices=[]):
+                torch.set_rng_state(states[i])
+                pm, pv, mu, var, lv, wd = m(x)
+                states[i] = torch.get_rng_state()
             loss = (kl_terms(pm, pv, mu, var, lv, 5) + reconstruction_terms(x, wd)).sum()
             loss.backward()
             opt.step()
@@ -175,3 +179,72 @@ def test_load_client_corpus(tmp_path):
     df.to_parquet(pq)
     r = load_client_corpus("real", pq, 1, fos="cs")
     assert r.n_docs == 2 and r.embeddings.shape == (2, 2) and "gamma" in r.local_terms()
+
+
+def test_assign_clients_partitions():
+    from gfedntm_amd.federation.hierarchical import assign_clients
+    assert assign_clients(16, 2) == [list(range(1, 9)), list(range(9, 17))]
+    assert assign_clients(5, 2) == [[1, 2, 3], [4, 5]]
+    assert assign_clients(8, 8) == [[i] for i in range(1, 9)]
+    with pytest.raises(ValueError):
+        assign_clients(2, 3)
+
+
+def _multi_worker(rank, world, port, tmp, n_clients, q):
+    import torch.distributed as dist
+    from gfedntm_amd.federation.hierarchical import assign_clients, run_distributed_multi
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ids = assign_clients(n_clients, world)[rank]
+        corpora = _corpora(n_clients)
+        torch.manual_seed(11)
+        out = run_distributed_multi([corpora[i - 1] for i in ids], ids, _params(), max_iters=5,
+                                    backend="torch", seed=0,
+                                    save_client=os.path.join(tmp, "client"),
+                                    save_server=os.path.join(tmp, "server"), stamp="20240101")
+        q.put((rank, [c.shared.numpy().copy() for c in out["clients"]], out["rounds"],
+               [c.id for c in out["clients"]]))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, traceback.format_exc(), None, None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_clients,world", [(4, 2), (5, 2)])
+def test_more_clients_than_ranks_matches_grouped_golden(tmp_path, n_clients, world):
+    """N clients on R < N gloo ranks (contiguous blocks per rank, hierarchical FedAvg)
+    equal the in-process federation with the same grouping; every client of every rank
+    ends holding the same state, and every client's results are written."""
+    import socket
+    import torch.multiprocessing as mp
+    from gfedntm_amd.federation.hierarchical import assign_clients
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_multi_worker, args=(r, world, port, str(tmp_path), n_clients, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=240) for _ in procs), key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert r[2] == 5, r[1]
+    ids = [i for r in res for i in r[3]]
+    assert ids == list(range(1, n_clients + 1))
+    torch.manual_seed(11)
+    groups = [len(b) for b in assign_clients(n_clients, world)]
+    gold = LocalFederation(_corpora(n_clients), _params(), max_iters=5, device="cpu",
+                           backend="torch", seed=0, groups=groups)
+    gold.run()
+    g = gold.clients[0].shared.numpy()
+    for r in res:
+        for sh in r[1]:
+            np.testing.assert_array_equal(sh, g)
+    for i in range(1, n_clients + 1):
+        assert os.path.exists(tmp_path / f"client{i}" / f"model_{i}_20240101.npz")
+    assert os.path.exists(tmp_path / "server" / "global_model_20240101.npz")

@@ -188,3 +188,21 @@ def test_round_graph_recaptures_after_engine_change():
     assert a.round == b.round == 9
     for x, y in zip(a.clients, b.clients):
         assert torch.equal(x.tm.flat.buffer, y.tm.flat.buffer)
+
+
+@pytest.mark.parametrize("model_type", ["prodLDA", "LDA"])
+def test_batched_round_matches_branch_round(model_type):
+    """One launch per phase for all clients (grid z = client) == one graph branch per
+    client, bit for bit (same kernels, per-client descriptors read from device memory)."""
+    sc = generate_synthetic(vocab_size=500, n_topics=10, n_docs=70, n_nodes=4, frozen_topics=2,
+                            nwords=(30, 60), seed=12)
+    corpora = [ClientCorpus(synthetic=sc, node=i) for i in range(4)]
+    kw = dict(max_iters=12, device="cuda", backend="fused", seed=4)
+    a = LocalFederation(corpora, _params(model_type=model_type), round_batched=True, **kw)
+    b = LocalFederation(corpora, _params(model_type=model_type), round_batched=False, **kw)
+    a.run()
+    b.run()
+    assert a._batched is not None and b._batched is None
+    for x, y in zip(a.clients, b.clients):
+        assert torch.equal(x.tm.flat.buffer, y.tm.flat.buffer)
+        assert torch.equal(x.tm.engine.loss_hist[:12], y.tm.engine.loss_hist[:12])

@@ -95,6 +95,19 @@ def test_strip_forward_matches_oracle(monkeypatch, B, n_docs, K, H, V):
     _oracle_step("prodLDA", B, n_docs, K, H, V)
 
 
+@pytest.mark.parametrize("pre", ["1", "2", "0"])
+@pytest.mark.parametrize("B,n_docs,K,V", [(64, 80, 200, 40000), (32, 60, 64, 40000)])
+def test_bwd_precomputed_dlogit_matches_oracle(monkeypatch, pre, B, n_docs, K, V):
+    """Persistent 4-k-range backward: the logit-gradient tiles precomputed once per tile
+    by prodlda_dlogit (GFEDNTM_BWD_PRE=1, the default) or recomputed by every range
+    workgroup (=0) both match the oracle."""
+    monkeypatch.setenv("GFEDNTM_BWD_PRE", pre)
+    fused, _ = _pair("prodLDA", V=V, K=K, H=(50, 50), B=B)
+    m = fused.engine._m
+    assert m.n_dpart < m.n_tiles and m.bwd_pre == {"1": 1, "2": 2, "0": 0}[pre]
+    _oracle_step("prodLDA", B, n_docs, K, (50, 50), V)
+
+
 def test_large_k_few_tiles_forces_k_split(monkeypatch):
     """K = 256, B = 64, 79 vocab tiles: the one-range backward (a workgroup per tile) needs
     more than 160 KiB of LDS, so the engine uses the 4-k-range shape (n_dpart < n_tiles)."""
@@ -688,3 +701,16 @@ def test_ctm_host_gemm_fallback_matches_oracle(model_type):
     torch.testing.assert_close(e.ws["kl"][:nb], kl.detach(), rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(e.ws["rl"][:nb], rl.detach(), rtol=1e-4, atol=1e-2)
     _check_grads(_grads_of(fused), ref)
+
+
+@pytest.mark.parametrize("model_type", ["prodLDA", "LDA"])
+@pytest.mark.parametrize("B,n_docs,K,H,V", [(64, 80, 50, (50, 50), 3000), (128, 200, 20, (64,), 9000),
+                                            (32, 45, 20, (30, 20), 20000)])
+def test_sparse_win_tiles_match_oracle(monkeypatch, model_type, B, n_docs, K, H, V):
+    """W_in tiles as entry lists (GFEDNTM_WIN_SPARSE=1 forces the large-vocabulary path,
+    csrc/update.hip win_tile_sparse) give the oracle's input-layer gradient."""
+    monkeypatch.setenv("GFEDNTM_WIN_SPARSE", "1")
+    from gfedntm_amd.ops.engine import STAGE_WIN_SPARSE
+    fused, _ = _pair(model_type, V=V, K=K, H=H, B=B)
+    assert fused.engine._m.stage_flags & STAGE_WIN_SPARSE
+    _oracle_step(model_type, B, n_docs, K, H, V)

@@ -27,17 +27,20 @@ def test_grads_mode_matches_synchronous_data_parallel():
         models.append((m, make_optimizer(m.parameters(), "adam", 2e-3, 0.99)))
     n = np.array([c.n_docs for c in fed.clients], dtype=np.float64)
     w = n / n.sum()
-    torch.manual_seed(5)
     fed.run()
-    torch.manual_seed(5)
+    # every client's noise comes from its own stream (seeded with its client seed)
+    states = [torch.Generator().manual_seed(2 + c.id).get_state() for c in fed.clients]
     for it in range(5):
         grads = []
-        for (m, opt), c in zip(models, fed.clients):
+        for i, ((m, opt), c) in enumerate(zip(models, fed.clients)):
             ids = torch.from_numpy(c.plan.batch(it).astype(np.int64))
             x = c.data.dense_rows(ids)
             m.train()
             opt.zero_grad()
-            pm, pv, mu, var, lv, wd = m(x)
+            with torch.random.fork_rng(devices=[]):
+                torch.set_rng_state(states[i])
+                pm, pv, mu, var, lv, wd = m(x)
+                states[i] = torch.get_rng_state()
             loss = (kl_terms(pm, pv, mu, var, lv, 5) + reconstruction_terms(x, wd)).sum()
             loss.backward()
             grads.append({k: p.grad.clone() for k, p in m.named_parameters()})

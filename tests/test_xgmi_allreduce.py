@@ -132,3 +132,63 @@ def test_fused_fedavg_overlap_matches_eager():
         assert used_auto == "xgmi+overlap" and used_rccl == "rccl", r[:5]
         assert same and err == 0, r[:5]
     assert res[0][5] == res[1][5]                    # ranks hold the same averaged state
+
+
+def _inplace_worker(rank, world, port, n, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    try:
+        from gfedntm_amd.parallel.xgmi import XgmiAllReduce
+        # a sub-block of a larger allocation, as the shared state is a slice of the flat buffer
+        big = torch.zeros(n + 4096, device="cuda")
+        buf = big[1024: 1024 + n]
+        state = torch.remainder(torch.arange(n, device="cuda", dtype=torch.float32) * (rank + 3), 7.0)
+        buf.copy_(state)
+        xg = XgmiAllReduce(n, "cuda:0", data=buf)
+        ok = xg.validate(rounds=2)
+        restored = bool(torch.equal(buf, state))            # validation left the state alone
+        g = torch.cuda.CUDAGraph()
+        with graph_capture(g):
+            xg.allreduce_(buf)
+        ar = torch.arange(n, device="cuda", dtype=torch.float32)
+        good = []
+        for r in range(4):
+            buf.copy_(torch.remainder(ar * (rank + 1 + r), 13.0))
+            g.replay()
+            torch.cuda.synchronize()
+            exp = sum(torch.remainder(ar * (j + 1 + r), 13.0) for j in range(world))
+            good.append(bool(torch.equal(buf, exp)))
+        err = xg.error()
+        try:
+            xg.allreduce_(torch.zeros(n, device="cuda"))
+            wrong_buf_refused = False
+        except ValueError:
+            wrong_buf_refused = True
+        xg.close()
+        q.put((rank, ok, restored, all(good), err, wrong_buf_refused))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 1_000_003), (3, 2_500_001)])
+def test_xgmi_allreduce_inplace_exact(world, n):
+    """In-place mode (large states): the data buffer itself is IPC-mapped (sub-block of a
+    caching-allocator block: handle of the base + offset), no stage copy, a phase-3
+    hand-off before returning; exact rank-ordered sums, graph replays, the validation
+    restores the state, other buffers are refused."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_inplace_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in ps:
+        p.join(60)
+    for r in res:
+        assert len(r) == 6, r
+        _, ok, restored, graph_ok, err, refused = r
+        assert ok and restored and graph_ok and err == 0 and refused, r
