@@ -69,6 +69,9 @@ def parse(argv=None):
     p.add_argument("--path", default="runner", choices=["runner", "engine"])
     p.add_argument("--sim-clients", type=int, default=0,
                    help="M > 0: M simulated clients on one GPU (LocalFederation round graph)")
+    p.add_argument("--clients-per-gpu", type=int, default=1,
+                   help="M > 1: every rank hosts M federated clients (hierarchical FedAvg: "
+                        "batched client steps, in-rank fold, cross-rank all-reduce)")
     p.add_argument("--unbatched", action="store_true",
                    help="--sim-clients: one graph branch per client instead of one batched "
                         "launch per phase for all clients (grid z = client)")
@@ -250,8 +253,50 @@ def _physical_gpus(device, world: int) -> int:
     return len(set(keys))
 
 
+def run_multi(args):
+    """M clients per rank (federation/hierarchical.py): the production runner for more
+    clients than GPUs."""
+    from gfedntm_amd.federation.hierarchical import assign_clients, run_distributed_multi
+    rank, world, device, rehearse = _init(args)
+    _ctrl_group()
+    physical = _physical_gpus(device, world)
+    M = args.clients_per_gpu
+    sc = _corpus(args, world * M)
+    ids = assign_clients(world * M, world)[rank]
+    corpora = [_client_corpus(args, sc, i - 1) for i in ids]
+    out = run_distributed_multi(corpora, ids, _params(args), _model_type(args),
+                                max_iters=args.warmup + args.steps, backend=args.backend,
+                                seed=args.seed, graph=not args.no_graph, allreduce=args.allreduce,
+                                rehearse_1gpu=rehearse, timing_warmup=args.warmup)
+    wall = _max_over_ranks(out["wall_s"], world)
+    dev_s = None if out.get("device_s") is None else _max_over_ranks(out["device_s"], world)
+    t = torch.tensor([float(out["docs"])], dtype=torch.float64)
+    dist.all_reduce(t, group=_ctrl_group())
+    docs = float(t.item())
+    eng = out["clients"][0].tm.engine
+    n_rounds = args.warmup + args.steps
+    final_loss = float(np.mean(eng.loss_hist[max(0, n_rounds - 20): n_rounds].cpu().numpy()))
+    if rank == 0:
+        ms = wall / max(out["timed_rounds"], 1) * 1e3
+        rec = _record(args, docs / wall, ms, len(out["clients"][0].tm.train_data.idx2token), None,
+                      final_loss, clients=world * M, ranks=world, physical=physical)
+        rec["device_ms_per_step"] = (None if dev_s is None else
+                                     round(dev_s / max(out["timed_rounds"], 1) * 1e3, 5))
+        rec["config"]["aggregation"] += (f" (hierarchical: {M} clients per rank folded in-rank, "
+                                         f"{out['allreduce'] or 'no'} all-reduce across ranks)")
+        rec["path"] = "run_distributed_multi"
+        if rehearse:
+            rec["note"] = (f"GFEDNTM_REHEARSE_1GPU: {world} ranks share {physical} GPU -- "
+                           "protocol rehearsal, timings meaningless")
+        print(json.dumps(rec), flush=True)
+    dist.barrier(group=_ctrl_group())
+    dist.destroy_process_group()
+
+
 def run_federated(args):
     from gfedntm_amd.federation.runner import run_distributed
+    if args.clients_per_gpu > 1:
+        return run_multi(args)
     rank, world, device, rehearse = _init(args)
     _ctrl_group()
     physical = _physical_gpus(device, world)

@@ -114,9 +114,9 @@ __device__ __forceinline__ void st_f4_as_f2(float* p, const f32x4& x) {   // 8-b
 // chunk.  Staging: thread element u (< 5) of a chunk is float4 (row, q) =
 // ((tid + 512 u) / 32, (tid + 512 u) % 32): u = 0 covers the 16 x_ctx rows, u >= 1
 // the 64 Wa rows, 32 consecutive lanes per 512-byte row segment.
-template <int BM>
-__global__ void __launch_bounds__(FT) gfk_ctx_fwd_k(const GfkModel* __restrict__ gm_) {
-  const GfkModel& m = gm_[blockIdx.z];
+template <int BM, bool GB = false>
+__global__ void __launch_bounds__(FT) gfk_ctx_fwd_k(GfkArgT<GB> ga) {
+  const GfkModel& m = gfk_model(ga);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int RB = BM / 16, SU = 5;
   const int x = blockIdx.x, jx = x >> 3, rb = jx % RB, tile = (jx / RB) * 8 + (x & 7);
@@ -232,9 +232,9 @@ __global__ void __launch_bounds__(FT) gfk_ctx_fwd_k(const GfkModel* __restrict__
 }
 
 // grid: n_tiles * ctx_kb workgroups of 16 waves (one per CU).
-template <int BM>
-__global__ void __launch_bounds__(CT) gfk_ctx_bwd_k(const GfkModel* __restrict__ gm_) {
-  const GfkModel& m = gm_[blockIdx.z];
+template <int BM, bool GB = false>
+__global__ void __launch_bounds__(CT) gfk_ctx_bwd_k(GfkArgT<GB> ga) {
+  const GfkModel& m = gfk_model(ga);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ int docs_s[BM];
   GFK_STAMP(m, 34);
@@ -407,10 +407,10 @@ extern "C" int gfk_ctx_set_smem(size_t bytes) {
   static size_t cur = 0;
   if (bytes <= cur) return 0;
   cur = bytes;
-  const void* ks[] = {(const void*)gfk_ctx_fwd_k<16>, (const void*)gfk_ctx_fwd_k<32>,
-                      (const void*)gfk_ctx_fwd_k<64>, (const void*)gfk_ctx_fwd_k<128>,
-                      (const void*)gfk_ctx_bwd_k<16>, (const void*)gfk_ctx_bwd_k<32>,
-                      (const void*)gfk_ctx_bwd_k<64>, (const void*)gfk_ctx_bwd_k<128>};
+  const void* ks[] = {(const void*)gfk_ctx_fwd_k<16>, (const void*)gfk_ctx_fwd_k<16, true>, (const void*)gfk_ctx_fwd_k<32>, (const void*)gfk_ctx_fwd_k<32, true>,
+                      (const void*)gfk_ctx_fwd_k<64>, (const void*)gfk_ctx_fwd_k<64, true>, (const void*)gfk_ctx_fwd_k<128>, (const void*)gfk_ctx_fwd_k<128, true>,
+                      (const void*)gfk_ctx_bwd_k<16>, (const void*)gfk_ctx_bwd_k<16, true>, (const void*)gfk_ctx_bwd_k<32>, (const void*)gfk_ctx_bwd_k<32, true>,
+                      (const void*)gfk_ctx_bwd_k<64>, (const void*)gfk_ctx_bwd_k<64, true>, (const void*)gfk_ctx_bwd_k<128>, (const void*)gfk_ctx_bwd_k<128, true>};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return (int)e;
@@ -433,10 +433,10 @@ extern "C" int gfk_launch_ctx_fwd(const GfkModel* m, hipStream_t s) {
   const dim3 g(8 * ((m->n_tiles + 7) / 8) * (m->bmax / 16)), t(FT);
   const size_t sm = sizeof(float) * fwd_lds_floats(*m);
   switch (m->bmax) {
-    case 16: hipLaunchKernelGGL(gfk_ctx_fwd_k<16>, gfk_grid(g, m), t, sm, s, gfk_dev(m)); break;
-    case 32: hipLaunchKernelGGL(gfk_ctx_fwd_k<32>, gfk_grid(g, m), t, sm, s, gfk_dev(m)); break;
-    case 64: hipLaunchKernelGGL(gfk_ctx_fwd_k<64>, gfk_grid(g, m), t, sm, s, gfk_dev(m)); break;
-    case 128: hipLaunchKernelGGL(gfk_ctx_fwd_k<128>, gfk_grid(g, m), t, sm, s, gfk_dev(m)); break;
+    case 16: do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_ctx_fwd_k<16, true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_ctx_fwd_k<16, false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0); break;
+    case 32: do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_ctx_fwd_k<32, true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_ctx_fwd_k<32, false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0); break;
+    case 64: do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_ctx_fwd_k<64, true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_ctx_fwd_k<64, false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0); break;
+    case 128: do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_ctx_fwd_k<128, true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_ctx_fwd_k<128, false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0); break;
     default: return -1;
   }
   return (int)hipGetLastError();
@@ -447,10 +447,10 @@ extern "C" int gfk_launch_ctx_bwd(const GfkModel* m, hipStream_t s) {
   const dim3 g(m->n_tiles * m->ctx_kb), t(CT);
   const size_t sm = sizeof(float) * bwd_lds(*m).total;
   switch (m->bmax) {
-    case 16: hipLaunchKernelGGL(gfk_ctx_bwd_k<16>, gfk_grid(g, m), t, sm, s, gfk_dev(m)); break;
-    case 32: hipLaunchKernelGGL(gfk_ctx_bwd_k<32>, gfk_grid(g, m), t, sm, s, gfk_dev(m)); break;
-    case 64: hipLaunchKernelGGL(gfk_ctx_bwd_k<64>, gfk_grid(g, m), t, sm, s, gfk_dev(m)); break;
-    case 128: hipLaunchKernelGGL(gfk_ctx_bwd_k<128>, gfk_grid(g, m), t, sm, s, gfk_dev(m)); break;
+    case 16: do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_ctx_bwd_k<16, true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_ctx_bwd_k<16, false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0); break;
+    case 32: do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_ctx_bwd_k<32, true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_ctx_bwd_k<32, false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0); break;
+    case 64: do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_ctx_bwd_k<64, true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_ctx_bwd_k<64, false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0); break;
+    case 128: do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_ctx_bwd_k<128, true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_ctx_bwd_k<128, false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0); break;
     default: return -1;
   }
   return (int)hipGetLastError();

@@ -169,9 +169,9 @@ __device__ __forceinline__ void rowvec_gemv(const float* W, const float* x, int 
 // LDS with LDS-only barriers: its global stores are never waited on.
 // Staged (compile-time): the MLP weights are read from LDS (ds_read); a runtime
 // select between the LDS copy and global memory would make every read a flat load.
-template <bool Staged>
-__global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(const GfkModel* __restrict__ gm_) {
-  const GfkModel& m = gm_[blockIdx.z];
+template <bool Staged, bool GB = false>
+__global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkArgT<GB> ga) {
+  const GfkModel& m = gfk_model(ga);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int b = blockIdx.x, tid = threadIdx.x;
   const int lane = tid & 63, wave = uniform(tid >> 6);
@@ -400,9 +400,9 @@ __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(const GfkModel* __re
 
 extern "C" int gfk_launch_enc_in(const GfkModel* m, hipStream_t s) {
   if (m->stage_flags & 1)
-    hipLaunchKernelGGL(gfk_enc_in_k<true>, gfk_grid(dim3(m->bmax), m), dim3(ENC_THREADS), gfk_enc_in_smem(m), s, gfk_dev(m));
+    do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_enc_in_k<true, true>), gfk_grid(dim3(m->bmax), m), dim3(ENC_THREADS), gfk_enc_in_smem(m), s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_enc_in_k<true, false>), dim3(m->bmax), dim3(ENC_THREADS), gfk_enc_in_smem(m), s, GfkArgT<false>{*m}); } while (0);
   else
-    hipLaunchKernelGGL(gfk_enc_in_k<false>, gfk_grid(dim3(m->bmax), m), dim3(ENC_THREADS), gfk_enc_in_smem(m), s, gfk_dev(m));
+    do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_enc_in_k<false, true>), gfk_grid(dim3(m->bmax), m), dim3(ENC_THREADS), gfk_enc_in_smem(m), s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_enc_in_k<false, false>), dim3(m->bmax), dim3(ENC_THREADS), gfk_enc_in_smem(m), s, GfkArgT<false>{*m}); } while (0);
   return (int)hipGetLastError();
 }
 
@@ -412,7 +412,7 @@ extern "C" int gfk_enc_in_set_smem(size_t bytes) {
   static size_t cur = 0;
   if (bytes <= cur) return 0;
   cur = bytes;
-  const void* ks[] = {(const void*)gfk_enc_in_k<true>, (const void*)gfk_enc_in_k<false>};
+  const void* ks[] = {(const void*)gfk_enc_in_k<true>, (const void*)gfk_enc_in_k<true, true>, (const void*)gfk_enc_in_k<false>, (const void*)gfk_enc_in_k<false, true>};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return (int)e;

@@ -234,6 +234,22 @@ typedef struct GfkAdam {
 
 }  // extern "C"
 
+// Kernel argument of every model kernel, in two instantiations: <false> the descriptor BY
+// VALUE (one client: kernarg memory, so the pointers in it are known global and the
+// kernels keep global_load / global_store), <true> a pointer to the device array of
+// gridDim.z descriptors (batched clients: model blockIdx.z; accesses through its pointers
+// become FLAT instructions, the price of one launch for many clients).
+template <bool B> struct GfkArgT;
+template <> struct GfkArgT<false> { GfkModel m; };
+template <> struct GfkArgT<true> { const GfkModel* p; };
+__device__ __forceinline__ const GfkModel& gfk_model(const GfkArgT<false>& a) { return a.m; }
+__device__ __forceinline__ const GfkModel& gfk_model(const GfkArgT<true>& a) { return a.p[blockIdx.z]; }
+template <bool B> struct GfkUArgT;
+template <> struct GfkUArgT<false> { GfkUpdate u; };
+template <> struct GfkUArgT<true> { const GfkUpdate* p; };
+__device__ __forceinline__ const GfkUpdate& gfk_upd(const GfkUArgT<false>& a) { return a.u; }
+__device__ __forceinline__ const GfkUpdate& gfk_upd(const GfkUArgT<true>& a) { return a.p[blockIdx.z]; }
+
 // ---------------------------------------------------------------------------
 // Device helpers
 // ---------------------------------------------------------------------------

@@ -125,9 +125,9 @@ __device__ __forceinline__ void randn4(uint64_t seed, uint32_t ctr, uint32_t idx
 }
 
 // NQ: input-layer outputs per lane (H0 <= 64 NQ); KQ: topics per lane (K <= 64 KQ).
-template <bool Staged, int NQ, int KQ>
-__global__ void __launch_bounds__(INF_THREADS) gfk_theta_infer_k(const GfkModel* __restrict__ gm_, GfkInfer p) {
-  const GfkModel& m = gm_[blockIdx.z];
+template <bool Staged, int NQ, int KQ, bool GB = false>
+__global__ void __launch_bounds__(INF_THREADS) gfk_theta_infer_k(GfkArgT<GB> ga, GfkInfer p) {
+  const GfkModel& m = gfk_model(ga);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
   const int H0 = m.H[0], K = m.K, nh = m.n_hidden, act = m.act, input = m.input;
@@ -322,7 +322,7 @@ __global__ void __launch_bounds__(INF_THREADS) gfk_theta_infer_k(const GfkModel*
 template <bool Staged, int NQ>
 int launch_kq(const GfkModel* m, const GfkInfer* p, size_t smem, hipStream_t s) {
   const int KQ = (m->K + 63) / 64;
-  void (*k)(const GfkModel* __restrict__, GfkInfer) = nullptr;
+  void (*k)(GfkArgT<false>, GfkInfer) = nullptr;
   switch (KQ) {
     case 1: k = gfk_theta_infer_k<Staged, NQ, 1>; break;
     case 2: k = gfk_theta_infer_k<Staged, NQ, 2>; break;
@@ -332,7 +332,7 @@ int launch_kq(const GfkModel* m, const GfkInfer* p, size_t smem, hipStream_t s) 
   }
   hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(k, gfk_grid(dim3(p->grid), m), dim3(INF_THREADS), smem, s, gfk_dev(m), *p);
+  hipLaunchKernelGGL(k, dim3(p->grid), dim3(INF_THREADS), smem, s, GfkArgT<false>{*m}, *p);
   return (int)hipGetLastError();
 }
 

@@ -30,8 +30,9 @@ constexpr float RL_EPS = 1e-10f;
 constexpr int LBT = 1024;
 constexpr int LBW = LBT / 64;
 
-extern "C" __global__ void __launch_bounds__(LBT) gfk_lda_beta_fwd(const GfkModel* __restrict__ gm_) {
-  const GfkModel& m = gm_[blockIdx.z];
+template <bool GB = false>
+__global__ void __launch_bounds__(LBT) gfk_lda_beta_fwd(GfkArgT<GB> ga) {
+  const GfkModel& m = gfk_model(ga);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int K = m.K, V = m.V, tid = threadIdx.x;
   float* bn = smem;
@@ -122,9 +123,9 @@ extern "C" __global__ void __launch_bounds__(LBT) gfk_lda_beta_fwd(const GfkMode
 constexpr int LDA_ROW_THREADS = 1024;
 constexpr int LDA_ROW_WAVES = LDA_ROW_THREADS / 64;
 
-template <int KQ>
-__global__ void __launch_bounds__(LDA_ROW_THREADS) gfk_lda_row_k(const GfkModel* __restrict__ gm_) {
-  const GfkModel& m = gm_[blockIdx.z];
+template <int KQ, bool GB = false>
+__global__ void __launch_bounds__(LDA_ROW_THREADS) gfk_lda_row_k(GfkArgT<GB> ga) {
+  const GfkModel& m = gfk_model(ga);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int b = blockIdx.x, nb = *m.ws_nb;
   if (b >= nb) return;
@@ -219,9 +220,9 @@ __host__ __device__ inline int lda_xs(int B) {
 // outputs this thread updates (fused mode).  Second round: the tile's per-non-zero
 // coefficients (ws_dbsm).  Then c_k, the x^T theta_d MFMA, the BN backward over the
 // topics and the update, all out of LDS.
-template <bool ThLds>
-__global__ void __launch_bounds__(LBT) gfk_lda_beta_bwd_k(const GfkModel* __restrict__ gm_) {
-  const GfkModel& m = gm_[blockIdx.z];
+template <bool ThLds, bool GB = false>
+__global__ void __launch_bounds__(LBT) gfk_lda_beta_bwd_k(GfkArgT<GB> ga) {
+  const GfkModel& m = gfk_model(ga);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int K = m.K, V = m.V, tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
   const int B = m.bmax, kt = m.kt, XS = lda_xs(B), nb = *m.ws_nb;
@@ -390,8 +391,7 @@ extern "C" size_t gfk_lda_bwd_smem(const GfkModel* m) {
 }
 
 extern "C" int gfk_launch_lda_beta_fwd(const GfkModel* m, hipStream_t s) {
-  hipLaunchKernelGGL(gfk_lda_beta_fwd, gfk_grid(dim3(m->dec_grid), m), dim3(LBT), gfk_lda_fwd_smem(m->K),
-                     s, gfk_dev(m));
+  do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_lda_beta_fwd<true>), gfk_grid(dim3(m->dec_grid), m), dim3(LBT), gfk_lda_fwd_smem(m->K), s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_lda_beta_fwd<false>), dim3(m->dec_grid), dim3(LBT), gfk_lda_fwd_smem(m->K), s, GfkArgT<false>{*m}); } while (0);
   return (int)hipGetLastError();
 }
 
@@ -399,19 +399,19 @@ extern "C" int gfk_launch_lda_row(const GfkModel* m, hipStream_t s) {
   const dim3 g(m->bmax), t(LDA_ROW_THREADS);
   const size_t sm = gfk_lda_row_smem(m->K);
   const int kq = (m->K + 63) / 64;
-  if (kq <= 1) hipLaunchKernelGGL(gfk_lda_row_k<1>, gfk_grid(g, m), t, sm, s, gfk_dev(m));
-  else if (kq == 2) hipLaunchKernelGGL(gfk_lda_row_k<2>, gfk_grid(g, m), t, sm, s, gfk_dev(m));
-  else if (kq == 3) hipLaunchKernelGGL(gfk_lda_row_k<3>, gfk_grid(g, m), t, sm, s, gfk_dev(m));
-  else hipLaunchKernelGGL(gfk_lda_row_k<4>, gfk_grid(g, m), t, sm, s, gfk_dev(m));
+  if (kq <= 1) do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_lda_row_k<1, true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_lda_row_k<1, false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0);
+  else if (kq == 2) do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_lda_row_k<2, true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_lda_row_k<2, false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0);
+  else if (kq == 3) do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_lda_row_k<3, true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_lda_row_k<3, false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0);
+  else do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_lda_row_k<4, true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_lda_row_k<4, false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0);
   return (int)hipGetLastError();
 }
 
 extern "C" int gfk_launch_lda_beta_bwd(const GfkModel* m, hipStream_t s) {
   const dim3 g(m->dec_grid), t(LBT);
   if (lda_bwd_th_lds(m))
-    hipLaunchKernelGGL(gfk_lda_beta_bwd_k<true>, gfk_grid(g, m), t, gfk_lda_bwd_smem(m), s, gfk_dev(m));
+    do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_lda_beta_bwd_k<true, true>), gfk_grid(g, m), t, gfk_lda_bwd_smem(m), s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_lda_beta_bwd_k<true, false>), g, t, gfk_lda_bwd_smem(m), s, GfkArgT<false>{*m}); } while (0);
   else
-    hipLaunchKernelGGL(gfk_lda_beta_bwd_k<false>, gfk_grid(g, m), t, gfk_lda_bwd_smem(m), s, gfk_dev(m));
+    do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_lda_beta_bwd_k<false, true>), gfk_grid(g, m), t, gfk_lda_bwd_smem(m), s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_lda_beta_bwd_k<false, false>), g, t, gfk_lda_bwd_smem(m), s, GfkArgT<false>{*m}); } while (0);
   return (int)hipGetLastError();
 }
 
@@ -421,8 +421,8 @@ extern "C" int gfk_lda_set_smem(size_t bytes) {
   static size_t cur = 0;
   if (bytes <= cur) return 0;
   cur = bytes;
-  const void* ks[] = {(const void*)gfk_lda_beta_fwd, (const void*)gfk_lda_beta_bwd_k<true>,
-                      (const void*)gfk_lda_beta_bwd_k<false>};
+  const void* ks[] = {(const void*)gfk_lda_beta_fwd<false>, (const void*)gfk_lda_beta_fwd<true>, (const void*)gfk_lda_beta_bwd_k<true>, (const void*)gfk_lda_beta_bwd_k<true, true>,
+                      (const void*)gfk_lda_beta_bwd_k<false>, (const void*)gfk_lda_beta_bwd_k<false, true>};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return (int)e;

@@ -266,9 +266,9 @@ __device__ __forceinline__ void post_label_head(const GfkModel& m, float* buf, i
 // read from L2) + mean[2K] + rstd[2K]
 // InLds: the batch matrices are staged in LDS (compile-time, so every access is a
 // ds_read; a runtime select of the pointer would turn them into flat loads).
-template <bool InLds>
-__global__ void __launch_bounds__(FT) gfk_post_fwd_k(const GfkModel* __restrict__ gm_) {
-  const GfkModel& m = gm_[blockIdx.z];
+template <bool InLds, bool GB = false>
+__global__ void __launch_bounds__(FT) gfk_post_fwd_k(GfkArgT<GB> ga) {
+  const GfkModel& m = gfk_model(ga);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   int K = m.K, B = m.bmax;
   const float *mu_raw = m.ws_mu_raw, *ls_raw = m.ws_ls_raw;
@@ -441,9 +441,9 @@ extern "C" size_t gfk_row_bwd_smem(const GfkModel* m) { return sizeof(float) * 4
 // KQ = ceil(K / 64) topics per lane: only live topics are loaded (K <= 64 -> one
 // load per partial), U partials per wave per round so a row's partials are in
 // flight at once.
-template <int KQ>
-__global__ void __launch_bounds__(PT) gfk_row_bwd_k(const GfkModel* __restrict__ gm_) {
-  const GfkModel& m = gm_[blockIdx.z];
+template <int KQ, bool GB = false>
+__global__ void __launch_bounds__(PT) gfk_row_bwd_k(GfkArgT<GB> ga) {
+  const GfkModel& m = gfk_model(ga);
   extern __shared__ __attribute__((aligned(16))) float part[];
   int K = m.K, B = m.bmax, np = m.n_dpart + (m.lab_on ? 1 : 0);   // + the label head's slab
   const float* dpart = m.ws_dthetad;
@@ -667,9 +667,9 @@ __device__ __forceinline__ void post_prior_sums(int K, int nb, const float* mu, 
 // grid: bmax + 1 workgroups: row = blockIdx.x < bmax, plus one extra workgroup
 // (the last) for the batch-level work -- prior gradients, the loss, the step
 // counter -- so no row workgroup carries it on the critical path.
-template <bool InLds, bool Staged>
-__global__ void __launch_bounds__(FT) gfk_post_bwd_k(const GfkModel* __restrict__ gm_) {
-  const GfkModel& m = gm_[blockIdx.z];
+template <bool InLds, bool Staged, bool GB = false>
+__global__ void __launch_bounds__(FT) gfk_post_bwd_k(GfkArgT<GB> ga) {
+  const GfkModel& m = gfk_model(ga);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   int K = m.K, B = m.bmax, nh = m.n_hidden, sflags = m.stage_flags;
   const float *dmu_g = m.ws_dmu, *dls_g = m.ws_dls, *mu_g = m.ws_mu, *ls_g = m.ws_ls;
@@ -888,12 +888,14 @@ __global__ void __launch_bounds__(FT) gfk_post_bwd_k(const GfkModel* __restrict_
 // ---------------------------------------------------------------------------
 // next batch
 // ---------------------------------------------------------------------------
-extern "C" __global__ void gfk_batch_prep(const GfkModel* __restrict__ gm_) { prepare_next_batch(gm_[blockIdx.z]); }
+template <bool GB>
+__global__ void gfk_batch_prep(GfkArgT<GB> ga) { prepare_next_batch(gfk_model(ga)); }
 
 // Publishes the prepared batch (doc ids of every row < bmax, nb) before the dense
 // contextual GEMMs of the CTM encoders, which run on all bmax rows.
-extern "C" __global__ void gfk_batch_docs(const GfkModel* __restrict__ gm_) {
-  const GfkModel& m = gm_[blockIdx.z];
+template <bool GB = false>
+__global__ void gfk_batch_docs(GfkArgT<GB> ga) {
+  const GfkModel& m = gfk_model(ga);
   const int32_t* nxt = m.ws_next;
   for (int b = threadIdx.x; b < m.bmax; b += blockDim.x) m.ws_doc[b] = nxt[1 + b];
   if (threadIdx.x == 0) *m.ws_nb = nxt[0];
@@ -904,9 +906,9 @@ extern "C" __global__ void gfk_batch_docs(const GfkModel* __restrict__ gm_) {
 // ---------------------------------------------------------------------------
 extern "C" int gfk_launch_post_fwd(const GfkModel* m, hipStream_t s) {
   if (batch_in_lds(*m))
-    hipLaunchKernelGGL(gfk_post_fwd_k<true>, gfk_grid(dim3(m->bmax), m), dim3(FT), gfk_post_fwd_smem(m), s, gfk_dev(m));
+    do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_post_fwd_k<true, true>), gfk_grid(dim3(m->bmax), m), dim3(FT), gfk_post_fwd_smem(m), s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_post_fwd_k<true, false>), dim3(m->bmax), dim3(FT), gfk_post_fwd_smem(m), s, GfkArgT<false>{*m}); } while (0);
   else
-    hipLaunchKernelGGL(gfk_post_fwd_k<false>, gfk_grid(dim3(m->bmax), m), dim3(FT), gfk_post_fwd_smem(m), s, gfk_dev(m));
+    do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_post_fwd_k<false, true>), gfk_grid(dim3(m->bmax), m), dim3(FT), gfk_post_fwd_smem(m), s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_post_fwd_k<false, false>), dim3(m->bmax), dim3(FT), gfk_post_fwd_smem(m), s, GfkArgT<false>{*m}); } while (0);
   return (int)hipGetLastError();
 }
 
@@ -914,32 +916,32 @@ extern "C" int gfk_launch_post_bwd(const GfkModel* m, hipStream_t s) {
   const int kq = (m->K + 63) / 64;
   const dim3 g(m->bmax), t(PT);
   const size_t sm = gfk_row_bwd_smem(m);
-  if (kq <= 1) hipLaunchKernelGGL(gfk_row_bwd_k<1>, gfk_grid(g, m), t, sm, s, gfk_dev(m));
-  else if (kq == 2) hipLaunchKernelGGL(gfk_row_bwd_k<2>, gfk_grid(g, m), t, sm, s, gfk_dev(m));
-  else if (kq == 3) hipLaunchKernelGGL(gfk_row_bwd_k<3>, gfk_grid(g, m), t, sm, s, gfk_dev(m));
-  else hipLaunchKernelGGL(gfk_row_bwd_k<4>, gfk_grid(g, m), t, sm, s, gfk_dev(m));
+  if (kq <= 1) do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_row_bwd_k<1, true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_row_bwd_k<1, false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0);
+  else if (kq == 2) do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_row_bwd_k<2, true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_row_bwd_k<2, false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0);
+  else if (kq == 3) do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_row_bwd_k<3, true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_row_bwd_k<3, false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0);
+  else do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_row_bwd_k<4, true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_row_bwd_k<4, false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   const dim3 gb(m->bmax + 1), tb(FT);     // + the prior / loss / step workgroup
   const size_t sb = gfk_post_bwd_smem(m);
   const bool st = m->stage_flags & 1;
   if (batch_in_lds(*m)) {
-    if (st) hipLaunchKernelGGL((gfk_post_bwd_k<true, true>), gfk_grid(gb, m), tb, sb, s, gfk_dev(m));
-    else hipLaunchKernelGGL((gfk_post_bwd_k<true, false>), gfk_grid(gb, m), tb, sb, s, gfk_dev(m));
+    if (st) do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_post_bwd_k<true, true, true>), gfk_grid(gb, m), tb, sb, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_post_bwd_k<true, true, false>), gb, tb, sb, s, GfkArgT<false>{*m}); } while (0);
+    else do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_post_bwd_k<true, false, true>), gfk_grid(gb, m), tb, sb, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_post_bwd_k<true, false, false>), gb, tb, sb, s, GfkArgT<false>{*m}); } while (0);
   } else {
-    if (st) hipLaunchKernelGGL((gfk_post_bwd_k<false, true>), gfk_grid(gb, m), tb, sb, s, gfk_dev(m));
-    else hipLaunchKernelGGL((gfk_post_bwd_k<false, false>), gfk_grid(gb, m), tb, sb, s, gfk_dev(m));
+    if (st) do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_post_bwd_k<false, true, true>), gfk_grid(gb, m), tb, sb, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_post_bwd_k<false, true, false>), gb, tb, sb, s, GfkArgT<false>{*m}); } while (0);
+    else do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_post_bwd_k<false, false, true>), gfk_grid(gb, m), tb, sb, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_post_bwd_k<false, false, false>), gb, tb, sb, s, GfkArgT<false>{*m}); } while (0);
   }
   return (int)hipGetLastError();
 }
 
 extern "C" int gfk_launch_batch_prep(const GfkModel* m, hipStream_t s) {
-  hipLaunchKernelGGL(gfk_batch_prep, gfk_grid(dim3(1), m), dim3(256), 0, s, gfk_dev(m));
+  do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_batch_prep<true>), gfk_grid(dim3(1), m), dim3(256), 0, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_batch_prep<false>), dim3(1), dim3(256), 0, s, GfkArgT<false>{*m}); } while (0);
   return (int)hipGetLastError();
 }
 
 extern "C" int gfk_launch_batch_docs(const GfkModel* m, hipStream_t s) {
-  hipLaunchKernelGGL(gfk_batch_docs, gfk_grid(dim3(1), m), dim3(256), 0, s, gfk_dev(m));
+  do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_batch_docs<true>), gfk_grid(dim3(1), m), dim3(256), 0, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_batch_docs<false>), dim3(1), dim3(256), 0, s, GfkArgT<false>{*m}); } while (0);
   return (int)hipGetLastError();
 }
 
@@ -949,11 +951,11 @@ extern "C" int gfk_post_set_smem(size_t bytes) {
   static size_t cur = 0;
   if (bytes <= cur) return 0;
   cur = bytes;
-  const void* ks[] = {(const void*)gfk_post_fwd_k<true>, (const void*)gfk_post_fwd_k<false>,
-                      (const void*)gfk_row_bwd_k<1>, (const void*)gfk_row_bwd_k<2>,
-                      (const void*)gfk_row_bwd_k<3>, (const void*)gfk_row_bwd_k<4>,
-                      (const void*)gfk_post_bwd_k<true, true>, (const void*)gfk_post_bwd_k<true, false>,
-                      (const void*)gfk_post_bwd_k<false, true>, (const void*)gfk_post_bwd_k<false, false>};
+  const void* ks[] = {(const void*)gfk_post_fwd_k<true>, (const void*)gfk_post_fwd_k<true, true>, (const void*)gfk_post_fwd_k<false>, (const void*)gfk_post_fwd_k<false, true>,
+                      (const void*)gfk_row_bwd_k<1>, (const void*)gfk_row_bwd_k<1, true>, (const void*)gfk_row_bwd_k<2>, (const void*)gfk_row_bwd_k<2, true>,
+                      (const void*)gfk_row_bwd_k<3>, (const void*)gfk_row_bwd_k<3, true>, (const void*)gfk_row_bwd_k<4>, (const void*)gfk_row_bwd_k<4, true>,
+                      (const void*)gfk_post_bwd_k<true, true>, (const void*)gfk_post_bwd_k<true, true, true>, (const void*)gfk_post_bwd_k<true, false>, (const void*)gfk_post_bwd_k<true, false, true>,
+                      (const void*)gfk_post_bwd_k<false, true>, (const void*)gfk_post_bwd_k<false, true, true>, (const void*)gfk_post_bwd_k<false, false>, (const void*)gfk_post_bwd_k<false, false, true>};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return (int)e;

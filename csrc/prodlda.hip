@@ -78,9 +78,9 @@ __device__ __forceinline__ float sum_groups(float v) {
 // they land while this tile's MFMAs / batch-norm / stores run.
 // dynamic LDS: th[BM*kt] + bt[KP*LDB_F] + colp[4][64] + colq[4][64] + stat[2][64]
 // BF: bf16 MFMA operands (16x16x16, K padded to 16), fp32 accumulation.
-template <int BM, bool BF>
-__global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(const GfkModel* __restrict__ gm_) {
-  const GfkModel& m = gm_[blockIdx.z];
+template <int BM, bool BF, bool GB = false>
+__global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkArgT<GB> ga) {
+  const GfkModel& m = gfk_model(ga);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int K = m.K, V = m.V, KT = m.kt;
   int tid = threadIdx.x;                      // re-made opaque per tile (no hoisted addresses)
@@ -297,9 +297,9 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(const GfkModel
 // global rounds overlap.  Measured (profiles/r2/ab_strip_forward.txt): K=50 headline
 // round 0.0589 -> 0.0583 ms, K=50 V=28k 0.101 -> 0.092, K=200 V=112k 0.349 -> 0.342.
 // NP: k pairs held in registers (compile-time, the launcher's smallest instance >= K / 8).
-template <int BM, int NP, bool PF>
-__global__ void __launch_bounds__(PF ? 512 : 1024) prodlda_fwd_strip_kernel(const GfkModel* __restrict__ gm_) {
-  const GfkModel& m = gm_[blockIdx.z];
+template <int BM, int NP, bool PF, bool GB = false>
+__global__ void __launch_bounds__(PF ? 512 : 1024) prodlda_fwd_strip_kernel(GfkArgT<GB> ga) {
+  const GfkModel& m = gfk_model(ga);
   constexpr int STRIP_THREADS = PF ? 512 : 1024;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int K = m.K, V = m.V, KT = m.kt;
@@ -502,8 +502,9 @@ __global__ void __launch_bounds__(PF ? 512 : 1024) prodlda_fwd_strip_kernel(cons
 // One wave per batch row: log-sum-exp from the per-wave partials, the sparse
 // reconstruction loss and S_b over the row's non-zeros (read from the row slots
 // prepared with the batch, so the logit gathers are the second round trip).
-extern "C" __global__ void __launch_bounds__(64) gfk_prodlda_row_loss(const GfkModel* __restrict__ gm_) {
-  const GfkModel& m = gm_[blockIdx.z];
+template <bool GB = false>
+__global__ void __launch_bounds__(64) gfk_prodlda_row_loss(GfkArgT<GB> ga) {
+  const GfkModel& m = gfk_model(ga);
   int n_tiles = m.n_tiles, bmax = m.bmax;
   const int32_t *nbp = m.ws_nb, *erange = m.ws_erange;
   const float *row_part = m.ws_row_part, *zn = m.ws_zn;
@@ -618,9 +619,9 @@ __host__ __device__ __forceinline__ int bwd_kpq(int K, int kq) { return 16 * ((r
 // written to ws_dt[tile] in the backward's LDS tile layout ([BM][LDD], rows >= nb and the
 // padding columns zero), so prodlda_bwd stages it with one contiguous LDS-DMA copy.
 // grid: n_tiles workgroups of 256 threads.  Static LDS: z tile + dt tile + lse / S / rstd.
-template <int BM>
-__global__ void __launch_bounds__(256) prodlda_dlogit_kernel(const GfkModel* __restrict__ gm_) {
-  const GfkModel& m = gm_[blockIdx.z];
+template <int BM, bool GB = false>
+__global__ void __launch_bounds__(256) prodlda_dlogit_kernel(GfkArgT<GB> ga) {
+  const GfkModel& m = gfk_model(ga);
   constexpr int NT = 256;
   constexpr int TPR = NT / BM;                 // threads per row (sparse term)
   __shared__ __attribute__((aligned(16))) float zt[BM * VB];
@@ -1106,25 +1107,25 @@ __device__ __forceinline__ void prodlda_bwd_body(const GfkModel& m) {
   }
 }
 
-template <int BM, int MAXU, int KQ, bool BF>
+template <int BM, int MAXU, int KQ, bool BF, bool GB = false>
 __global__ void __launch_bounds__(KQ == 1 ? DEC_THREADS : 512, KQ == 1 ? 1 : 2)
-prodlda_bwd_kernel(const GfkModel* __restrict__ gm_) {
-  const GfkModel& m = gm_[blockIdx.z];
+prodlda_bwd_kernel(GfkArgT<GB> ga) {
+  const GfkModel& m = gfk_model(ga);
   prodlda_bwd_body<BM, MAXU, KQ, BF, false>(m);
 }
 
 // the precomputed-dlogit shape: bwd_pre = 1: <= 80 VGPRs (6 waves per SIMD), so three
 // 8-wave workgroups share a CU; bwd_pre = 2: the compiler's register budget (two per CU)
-template <int BM, int MAXU, bool BF>
+template <int BM, int MAXU, bool BF, bool GB = false>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6)))
-prodlda_bwd_pre_kernel(const GfkModel* __restrict__ gm_) {
-  const GfkModel& m = gm_[blockIdx.z];
+prodlda_bwd_pre_kernel(GfkArgT<GB> ga) {
+  const GfkModel& m = gfk_model(ga);
   prodlda_bwd_body<BM, MAXU, 4, BF, true>(m);
 }
 
-template <int BM, int MAXU, bool BF>
-__global__ void __launch_bounds__(512, 2) prodlda_bwd_pre2_kernel(const GfkModel* __restrict__ gm_) {
-  const GfkModel& m = gm_[blockIdx.z];
+template <int BM, int MAXU, bool BF, bool GB = false>
+__global__ void __launch_bounds__(512, 2) prodlda_bwd_pre2_kernel(GfkArgT<GB> ga) {
+  const GfkModel& m = gfk_model(ga);
   prodlda_bwd_body<BM, MAXU, 4, BF, true>(m);
 }
 
@@ -1177,9 +1178,9 @@ extern "C" int gfk_launch_prodlda_fwd(const GfkModel* m, hipStream_t s) {
 #define GFK_FWS(BM, NP)                                                                        \
     do {                                                                                       \
       if (m->stage_flags & FWD_STRIP_PF)                                                       \
-        hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, true>), gfk_grid(g, m), dim3(512), sm, s, gfk_dev(m)); \
+        do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, true, true>), gfk_grid(g, m), dim3(512), sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, true, false>), g, dim3(512), sm, s, GfkArgT<false>{*m}); } while (0); \
       else                                                                                     \
-        hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, false>), gfk_grid(g, m), dim3(1024), sm, s, gfk_dev(m)); \
+        do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, false, true>), gfk_grid(g, m), dim3(1024), sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, false, false>), g, dim3(1024), sm, s, GfkArgT<false>{*m}); } while (0); \
     } while (0)
 #define GFK_FWS_B(BM)                                                      \
     if (np == 8) GFK_FWS(BM, 8);                                           \
@@ -1197,8 +1198,8 @@ extern "C" int gfk_launch_prodlda_fwd(const GfkModel* m, hipStream_t s) {
     return (int)hipGetLastError();
   }
 #define GFK_FWD(BM)                                                                  \
-  if (m->mm_bf16) hipLaunchKernelGGL((prodlda_fwd_kernel<BM, true>), gfk_grid(g, m), blk, sm, s, gfk_dev(m));   \
-  else hipLaunchKernelGGL((prodlda_fwd_kernel<BM, false>), gfk_grid(g, m), blk, sm, s, gfk_dev(m))
+  if (m->mm_bf16) do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_fwd_kernel<BM, true, true>), gfk_grid(g, m), blk, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_fwd_kernel<BM, true, false>), g, blk, sm, s, GfkArgT<false>{*m}); } while (0);   \
+  else do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_fwd_kernel<BM, false, true>), gfk_grid(g, m), blk, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_fwd_kernel<BM, false, false>), g, blk, sm, s, GfkArgT<false>{*m}); } while (0)
   switch (m->bmax) {
     case 16: GFK_FWD(16); break;
     case 32: GFK_FWD(32); break;
@@ -1215,25 +1216,25 @@ static void launch_bwd_p(const GfkModel* m, dim3 g, size_t sm, hipStream_t s) {
   const dim3 blk(KQ == 1 ? DEC_THREADS : 512);
   if (PRE && m->bwd_pre == 2) {
     switch (m->bmax) {
-      case 16: hipLaunchKernelGGL((prodlda_bwd_pre2_kernel<16, MAXU, BF>), gfk_grid(g, m), blk, sm, s, gfk_dev(m)); break;
-      case 32: hipLaunchKernelGGL((prodlda_bwd_pre2_kernel<32, MAXU, BF>), gfk_grid(g, m), blk, sm, s, gfk_dev(m)); break;
-      default: hipLaunchKernelGGL((prodlda_bwd_pre2_kernel<64, MAXU, BF>), gfk_grid(g, m), blk, sm, s, gfk_dev(m)); break;
+      case 16: do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_bwd_pre2_kernel<16, MAXU, BF, true>), gfk_grid(g, m), blk, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_bwd_pre2_kernel<16, MAXU, BF, false>), g, blk, sm, s, GfkArgT<false>{*m}); } while (0); break;
+      case 32: do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_bwd_pre2_kernel<32, MAXU, BF, true>), gfk_grid(g, m), blk, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_bwd_pre2_kernel<32, MAXU, BF, false>), g, blk, sm, s, GfkArgT<false>{*m}); } while (0); break;
+      default: do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_bwd_pre2_kernel<64, MAXU, BF, true>), gfk_grid(g, m), blk, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_bwd_pre2_kernel<64, MAXU, BF, false>), g, blk, sm, s, GfkArgT<false>{*m}); } while (0); break;
     }
     return;
   }
   if (PRE) {
     switch (m->bmax) {
-      case 16: hipLaunchKernelGGL((prodlda_bwd_pre_kernel<16, MAXU, BF>), gfk_grid(g, m), blk, sm, s, gfk_dev(m)); break;
-      case 32: hipLaunchKernelGGL((prodlda_bwd_pre_kernel<32, MAXU, BF>), gfk_grid(g, m), blk, sm, s, gfk_dev(m)); break;
-      default: hipLaunchKernelGGL((prodlda_bwd_pre_kernel<64, MAXU, BF>), gfk_grid(g, m), blk, sm, s, gfk_dev(m)); break;
+      case 16: do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_bwd_pre_kernel<16, MAXU, BF, true>), gfk_grid(g, m), blk, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_bwd_pre_kernel<16, MAXU, BF, false>), g, blk, sm, s, GfkArgT<false>{*m}); } while (0); break;
+      case 32: do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_bwd_pre_kernel<32, MAXU, BF, true>), gfk_grid(g, m), blk, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_bwd_pre_kernel<32, MAXU, BF, false>), g, blk, sm, s, GfkArgT<false>{*m}); } while (0); break;
+      default: do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_bwd_pre_kernel<64, MAXU, BF, true>), gfk_grid(g, m), blk, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_bwd_pre_kernel<64, MAXU, BF, false>), g, blk, sm, s, GfkArgT<false>{*m}); } while (0); break;
     }
     return;
   }
   switch (m->bmax) {
-    case 16: hipLaunchKernelGGL((prodlda_bwd_kernel<16, MAXU, KQ, BF>), gfk_grid(g, m), blk, sm, s, gfk_dev(m)); break;
-    case 32: hipLaunchKernelGGL((prodlda_bwd_kernel<32, MAXU, KQ, BF>), gfk_grid(g, m), blk, sm, s, gfk_dev(m)); break;
-    case 64: hipLaunchKernelGGL((prodlda_bwd_kernel<64, MAXU, KQ, BF>), gfk_grid(g, m), blk, sm, s, gfk_dev(m)); break;
-    default: hipLaunchKernelGGL((prodlda_bwd_kernel<128, MAXU, KQ, BF>), gfk_grid(g, m), blk, sm, s, gfk_dev(m)); break;
+    case 16: do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_bwd_kernel<16, MAXU, KQ, BF, true>), gfk_grid(g, m), blk, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_bwd_kernel<16, MAXU, KQ, BF, false>), g, blk, sm, s, GfkArgT<false>{*m}); } while (0); break;
+    case 32: do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_bwd_kernel<32, MAXU, KQ, BF, true>), gfk_grid(g, m), blk, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_bwd_kernel<32, MAXU, KQ, BF, false>), g, blk, sm, s, GfkArgT<false>{*m}); } while (0); break;
+    case 64: do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_bwd_kernel<64, MAXU, KQ, BF, true>), gfk_grid(g, m), blk, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_bwd_kernel<64, MAXU, KQ, BF, false>), g, blk, sm, s, GfkArgT<false>{*m}); } while (0); break;
+    default: do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_bwd_kernel<128, MAXU, KQ, BF, true>), gfk_grid(g, m), blk, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_bwd_kernel<128, MAXU, KQ, BF, false>), g, blk, sm, s, GfkArgT<false>{*m}); } while (0); break;
   }
 }
 
@@ -1242,9 +1243,9 @@ static void launch_bwd_b(const GfkModel* m, dim3 g, size_t sm, hipStream_t s) {
   if (KQ == 4 && m->bwd_pre && m->bmax <= 64) {      // (static LDS: B <= 64)
     const dim3 gd(m->n_tiles), bd(256);
     switch (m->bmax) {
-      case 16: hipLaunchKernelGGL(prodlda_dlogit_kernel<16>, gfk_grid(gd, m), bd, 0, s, gfk_dev(m)); break;
-      case 32: hipLaunchKernelGGL(prodlda_dlogit_kernel<32>, gfk_grid(gd, m), bd, 0, s, gfk_dev(m)); break;
-      default: hipLaunchKernelGGL(prodlda_dlogit_kernel<64>, gfk_grid(gd, m), bd, 0, s, gfk_dev(m)); break;
+      case 16: do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_dlogit_kernel<16, true>), gfk_grid(gd, m), bd, 0, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_dlogit_kernel<16, false>), gd, bd, 0, s, GfkArgT<false>{*m}); } while (0); break;
+      case 32: do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_dlogit_kernel<32, true>), gfk_grid(gd, m), bd, 0, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_dlogit_kernel<32, false>), gd, bd, 0, s, GfkArgT<false>{*m}); } while (0); break;
+      default: do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_dlogit_kernel<64, true>), gfk_grid(gd, m), bd, 0, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_dlogit_kernel<64, false>), gd, bd, 0, s, GfkArgT<false>{*m}); } while (0); break;
     }
     launch_bwd_p<MAXU, KQ, BF, KQ == 4>(m, g, sm, s);
   } else {
@@ -1279,7 +1280,7 @@ extern "C" int gfk_launch_prodlda_bwd(const GfkModel* m, hipStream_t s) {
 }
 
 extern "C" int gfk_launch_prodlda_row_loss(const GfkModel* m, hipStream_t s) {
-  hipLaunchKernelGGL(gfk_prodlda_row_loss, gfk_grid(dim3(m->bmax), m), dim3(64), 0, s, gfk_dev(m));
+  do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_prodlda_row_loss<true>), gfk_grid(dim3(m->bmax), m), dim3(64), 0, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_prodlda_row_loss<false>), dim3(m->bmax), dim3(64), 0, s, GfkArgT<false>{*m}); } while (0);
   return (int)hipGetLastError();
 }
 
@@ -1289,25 +1290,25 @@ extern "C" int gfk_prodlda_set_smem(size_t bytes) {
   static size_t cur = 0;
   if (bytes <= cur) return 0;
   cur = bytes;
-  const void* ks[] = {(const void*)prodlda_fwd_kernel<16, false>, (const void*)prodlda_fwd_kernel<32, false>,
-                      (const void*)prodlda_fwd_kernel<64, false>, (const void*)prodlda_fwd_kernel<128, false>,
-                      (const void*)prodlda_fwd_kernel<16, true>, (const void*)prodlda_fwd_kernel<32, true>,
-                      (const void*)prodlda_fwd_kernel<64, true>, (const void*)prodlda_fwd_kernel<128, true>,
-#define GFK_FWS_PTRS1(BM, F) (const void*)prodlda_fwd_strip_kernel<BM, 8, F>, \
-    (const void*)prodlda_fwd_strip_kernel<BM, 13, F>, (const void*)prodlda_fwd_strip_kernel<BM, 16, F>, \
-    (const void*)prodlda_fwd_strip_kernel<BM, 25, F>, (const void*)prodlda_fwd_strip_kernel<BM, 32, F>
+  const void* ks[] = {(const void*)prodlda_fwd_kernel<16, false>, (const void*)prodlda_fwd_kernel<16, false, true>, (const void*)prodlda_fwd_kernel<32, false>, (const void*)prodlda_fwd_kernel<32, false, true>,
+                      (const void*)prodlda_fwd_kernel<64, false>, (const void*)prodlda_fwd_kernel<64, false, true>, (const void*)prodlda_fwd_kernel<128, false>, (const void*)prodlda_fwd_kernel<128, false, true>,
+                      (const void*)prodlda_fwd_kernel<16, true>, (const void*)prodlda_fwd_kernel<16, true, true>, (const void*)prodlda_fwd_kernel<32, true>, (const void*)prodlda_fwd_kernel<32, true, true>,
+                      (const void*)prodlda_fwd_kernel<64, true>, (const void*)prodlda_fwd_kernel<64, true, true>, (const void*)prodlda_fwd_kernel<128, true>, (const void*)prodlda_fwd_kernel<128, true, true>,
+#define GFK_FWS_PTRS1(BM, F) (const void*)prodlda_fwd_strip_kernel<BM, 8, F>, (const void*)prodlda_fwd_strip_kernel<BM, 8, F, true>, \
+    (const void*)prodlda_fwd_strip_kernel<BM, 13, F>, (const void*)prodlda_fwd_strip_kernel<BM, 13, F, true>, (const void*)prodlda_fwd_strip_kernel<BM, 16, F>, (const void*)prodlda_fwd_strip_kernel<BM, 16, F, true>, \
+    (const void*)prodlda_fwd_strip_kernel<BM, 25, F>, (const void*)prodlda_fwd_strip_kernel<BM, 25, F, true>, (const void*)prodlda_fwd_strip_kernel<BM, 32, F>, (const void*)prodlda_fwd_strip_kernel<BM, 32, F, true>
 #define GFK_FWS_PTRS(BM) GFK_FWS_PTRS1(BM, false), GFK_FWS_PTRS1(BM, true)
                       GFK_FWS_PTRS(16), GFK_FWS_PTRS(32), GFK_FWS_PTRS(64),
 #undef GFK_FWS_PTRS
 #undef GFK_FWS_PTRS1
-#define GFK_BWD_PTRS2(U, T, F) (const void*)prodlda_bwd_kernel<16, U, T, F>, \
-    (const void*)prodlda_bwd_kernel<32, U, T, F>, (const void*)prodlda_bwd_kernel<64, U, T, F>, \
-    (const void*)prodlda_bwd_kernel<128, U, T, F>
+#define GFK_BWD_PTRS2(U, T, F) (const void*)prodlda_bwd_kernel<16, U, T, F>, (const void*)prodlda_bwd_kernel<16, U, T, F, true>, \
+    (const void*)prodlda_bwd_kernel<32, U, T, F>, (const void*)prodlda_bwd_kernel<32, U, T, F, true>, (const void*)prodlda_bwd_kernel<64, U, T, F>, (const void*)prodlda_bwd_kernel<64, U, T, F, true>, \
+    (const void*)prodlda_bwd_kernel<128, U, T, F>, (const void*)prodlda_bwd_kernel<128, U, T, F, true>
 #define GFK_BWD_PTRS1(U, T) GFK_BWD_PTRS2(U, T, false), GFK_BWD_PTRS2(U, T, true)
-#define GFK_BWD_PTRS3(U, F) (const void*)prodlda_bwd_pre_kernel<16, U, F>, \
-    (const void*)prodlda_bwd_pre_kernel<32, U, F>, (const void*)prodlda_bwd_pre_kernel<64, U, F>, \
-    (const void*)prodlda_bwd_pre2_kernel<16, U, F>, (const void*)prodlda_bwd_pre2_kernel<32, U, F>, \
-    (const void*)prodlda_bwd_pre2_kernel<64, U, F>
+#define GFK_BWD_PTRS3(U, F) (const void*)prodlda_bwd_pre_kernel<16, U, F>, (const void*)prodlda_bwd_pre_kernel<16, U, F, true>, \
+    (const void*)prodlda_bwd_pre_kernel<32, U, F>, (const void*)prodlda_bwd_pre_kernel<32, U, F, true>, (const void*)prodlda_bwd_pre_kernel<64, U, F>, (const void*)prodlda_bwd_pre_kernel<64, U, F, true>, \
+    (const void*)prodlda_bwd_pre2_kernel<16, U, F>, (const void*)prodlda_bwd_pre2_kernel<16, U, F, true>, (const void*)prodlda_bwd_pre2_kernel<32, U, F>, (const void*)prodlda_bwd_pre2_kernel<32, U, F, true>, \
+    (const void*)prodlda_bwd_pre2_kernel<64, U, F>, (const void*)prodlda_bwd_pre2_kernel<64, U, F, true>
 #define GFK_BWD_PTRS(U) GFK_BWD_PTRS1(U, 1), GFK_BWD_PTRS1(U, 4), GFK_BWD_PTRS3(U, false), \
     GFK_BWD_PTRS3(U, true)
                       GFK_BWD_PTRS(1), GFK_BWD_PTRS(2), GFK_BWD_PTRS(3), GFK_BWD_PTRS(4)};

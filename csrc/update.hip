@@ -353,10 +353,10 @@ __device__ __forceinline__ void win_tile_sparse(const GfkModel& m, float* smem, 
 // rows A^T (ctx_fwd's output) in place of x^T, or ZeroShotTM's whole [C, H0] layer with
 // the batch's contextual rows x_ctx^T -- the same tile GEMM + Adam epilogue.
 // dynamic LDS: max(W_in tile: xt[64][stride_a(B)] + dz[B][stride_b(H0P)], weight job: 2 B 80)
-template <int UT>
-__global__ void __launch_bounds__(UT) gfk_win_update_k(const GfkModel* __restrict__ gm_, const GfkUpdate* __restrict__ gu_) {
-  const GfkModel& m = gm_[blockIdx.z];
-  const GfkUpdate& U = gu_[blockIdx.z];
+template <int UT, bool GB = false>
+__global__ void __launch_bounds__(UT) gfk_win_update_k(GfkArgT<GB> ga, GfkUArgT<GB> gua) {
+  const GfkModel& m = gfk_model(ga);
+  const GfkUpdate& U = gfk_upd(gua);
   constexpr int UW = UT / 64;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int nt_here = m.n_tiles;
@@ -599,10 +599,10 @@ __global__ void __launch_bounds__(UT) gfk_win_update_k(const GfkModel* __restric
 // its own (the job paths of gfk_win_update_k need ~86 VGPRs)
 // grid: n_w + n_v + 1 job workgroups FIRST (they start with the tiles, not after them),
 // then the n_tiles sparse W_in tiles
-template <int UT>
-__global__ void __launch_bounds__(UT) gfk_win_sparse_k(const GfkModel* __restrict__ gm_, const GfkUpdate* __restrict__ gu_) {
-  const GfkModel& m = gm_[blockIdx.z];
-  const GfkUpdate& U = gu_[blockIdx.z];
+template <int UT, bool GB = false>
+__global__ void __launch_bounds__(UT) gfk_win_sparse_k(GfkArgT<GB> ga, GfkUArgT<GB> gua) {
+  const GfkModel& m = gfk_model(ga);
+  const GfkUpdate& U = gfk_upd(gua);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int r = (int)blockIdx.x;
   if (r < U.n_w) { weight_job<UT>(m, U.w[r], smem); return; }
@@ -615,16 +615,15 @@ extern "C" int gfk_launch_win_update(const GfkModel* m, const GfkUpdate* u, hipS
   const int extra = m->ctx_fused == 1 ? m->n_tiles : (m->ctx_fused == 2 ? (m->C + 63) / 64 : 0);
   if (m->stage_flags & WIN_SPARSE) {
     if (m->H[0] > 64 || m->input != GFK_IN_BOW || m->bmax > 128) return -1;
-    hipLaunchKernelGGL(gfk_win_sparse_k<512>, gfk_grid(dim3(u->n_w + u->n_v + 1 + m->n_tiles), m), dim3(512),
-                       gfk_win_update_smem(m), s, gfk_dev(m), reinterpret_cast<const GfkUpdate*>(m->dev_upd));
+    do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_win_sparse_k<512, true>), gfk_grid(dim3(u->n_w + u->n_v + 1 + m->n_tiles), m), dim3(512), gfk_win_update_smem(m), s, GfkArgT<true>{gfk_dev(m)}, GfkUArgT<true>{reinterpret_cast<const GfkUpdate*>(m->dev_upd)}); else hipLaunchKernelGGL((gfk_win_sparse_k<512, false>), dim3(u->n_w + u->n_v + 1 + m->n_tiles), dim3(512), gfk_win_update_smem(m), s, GfkArgT<false>{*m}, GfkUArgT<false>{*u}); } while (0);
     return (int)hipGetLastError();
   }
   const dim3 g(m->n_tiles + u->n_w + u->n_v + 1 + extra);
   // more W_in tiles than two rounds of 16-wave workgroups (dec_grid = the CUs' slots)
   if (m->n_tiles > 2 * m->dec_grid && m->n_tiles > 512)
-    hipLaunchKernelGGL(gfk_win_update_k<512>, gfk_grid(g, m), dim3(512), gfk_win_update_smem(m), s, gfk_dev(m), reinterpret_cast<const GfkUpdate*>(m->dev_upd));
+    do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_win_update_k<512, true>), gfk_grid(g, m), dim3(512), gfk_win_update_smem(m), s, GfkArgT<true>{gfk_dev(m)}, GfkUArgT<true>{reinterpret_cast<const GfkUpdate*>(m->dev_upd)}); else hipLaunchKernelGGL((gfk_win_update_k<512, false>), g, dim3(512), gfk_win_update_smem(m), s, GfkArgT<false>{*m}, GfkUArgT<false>{*u}); } while (0);
   else
-    hipLaunchKernelGGL(gfk_win_update_k<1024>, gfk_grid(g, m), dim3(1024), gfk_win_update_smem(m), s, gfk_dev(m), reinterpret_cast<const GfkUpdate*>(m->dev_upd));
+    do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_win_update_k<1024, true>), gfk_grid(g, m), dim3(1024), gfk_win_update_smem(m), s, GfkArgT<true>{gfk_dev(m)}, GfkUArgT<true>{reinterpret_cast<const GfkUpdate*>(m->dev_upd)}); else hipLaunchKernelGGL((gfk_win_update_k<1024, false>), g, dim3(1024), gfk_win_update_smem(m), s, GfkArgT<false>{*m}, GfkUArgT<false>{*u}); } while (0);
   return (int)hipGetLastError();
 }
 
@@ -634,12 +633,12 @@ extern "C" int gfk_win_update_set_smem(size_t bytes) {
   static size_t cur = 0;
   if (bytes <= cur) return 0;
   cur = bytes;
-  hipError_t e = hipFuncSetAttribute((const void*)gfk_win_update_k<512>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-  if (e != hipSuccess) return (int)e;
-  e = hipFuncSetAttribute((const void*)gfk_win_sparse_k<512>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-  if (e != hipSuccess) return (int)e;
-  return (int)hipFuncSetAttribute((const void*)gfk_win_update_k<1024>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  const void* ks[] = {(const void*)gfk_win_update_k<512, false>, (const void*)gfk_win_update_k<512, true>,
+                      (const void*)gfk_win_update_k<1024, false>, (const void*)gfk_win_update_k<1024, true>,
+                      (const void*)gfk_win_sparse_k<512, false>, (const void*)gfk_win_sparse_k<512, true>};
+  for (const void* k : ks) {
+    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e != hipSuccess) return (int)e;
+  }
+  return 0;
 }

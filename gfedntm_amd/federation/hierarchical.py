@@ -6,8 +6,10 @@ src/federation/server.py:442-484,500).  On one node the natural unit is one rank
 GPU, so with N clients on R < N ranks each rank hosts a contiguous block of clients:
 
   round r, rank q (clients i in block q):
-    1. every local client does its local step (fused engine: one hipGraph branch per
-       client), its shared state pre-scaled by its GLOBAL weight w_i = n_i / sum_all n;
+    1. every local client does its local step -- fused engine: one launch per kernel
+       phase for all local clients (ops/engine.py BatchedSteps, grid z = client), or one
+       graph branch per client where the clients cannot be batched -- its shared state
+       pre-scaled by its GLOBAL weight w_i = n_i / sum_all n;
     2. the rank folds its clients' states in client order into the first client's
        buffer (csrc/comm.hip gfk_local_fedavg, mode "first");
     3. the ranks all-reduce that partial sum (the xGMI two-shot kernel: rank-order
@@ -16,7 +18,8 @@ GPU, so with N clients on R < N ranks each rank hosts a contiguous block of clie
 
 Steps 1-4 are one hipGraph per round when the collective is the xGMI kernel.  The sum
 is fold_ranks(fold_clients_of_rank(w_i W_i)): the in-process golden with the same
-grouping (``LocalFederation(..., groups=sizes)``) produces it bit for bit.
+grouping (``LocalFederation(..., groups=sizes)``, batched the same way) produces it bit
+for bit.
 
 Control plane (gloo): the ranks agree on the client-to-rank map (every rank announces
 its client ids; they must partition 1..N in rank order), the vocabulary (union of every

@@ -106,8 +106,10 @@ def test_run_distributed_xgmi_matches_local_golden(tmp_path):
         assert r[1] not in ("exception", "comm_error"), r
     # golden: the same federation in one process (client-order sum, fused engine)
     from gfedntm_amd.federation.runner import LocalFederation
+    # (per-client kernels, as the one-client ranks run: the batched instances of the
+    # kernels are compiled separately and need not round identically)
     fed = LocalFederation(_corpora(), _params(), max_iters=ROUNDS, device="cuda",
-                          backend="fused", seed=5)
+                          backend="fused", seed=5, round_batched=False)
     assert fed.round_graph
     fed.run()
     gold = fed.clients[0].shared.detach().cpu().numpy()

@@ -248,3 +248,17 @@ def test_more_clients_than_ranks_matches_grouped_golden(tmp_path, n_clients, wor
     for i in range(1, n_clients + 1):
         assert os.path.exists(tmp_path / f"client{i}" / f"model_{i}_20240101.npz")
     assert os.path.exists(tmp_path / "server" / "global_model_20240101.npz")
+
+
+def test_cli_more_clients_than_ranks(tmp_path):
+    """main.py --backend gloo --min_clients_federation 4 --nproc 2: two ranks host two
+    clients each (hierarchical FedAvg); every client saves its results, rank 0 the
+    global model."""
+    from gfedntm_amd.cli import main
+    main(["--backend", "gloo", "--workdir", str(tmp_path), "--min_clients_federation", "4",
+          "--nproc", "2", "--max_iters", "4", "--engine", "torch", "--device", "cpu",
+          "--generate_synthetic", str(tmp_path / "syn.npz")])
+    found = [f for _, _, fs in os.walk(tmp_path) for f in fs]
+    assert any(f.startswith("global_model_") for f in found)
+    for i in range(1, 5):
+        assert any(f.startswith(f"model_{i}_") for f in found), (i, found)
