@@ -231,6 +231,137 @@ __global__ void __launch_bounds__(FT) gfk_ctx_fwd_k(GfkArgT<GB> ga) {
   GFK_STAMP(m, 33);
 }
 
+// Large vocabularies (stage_flags bit 5): ONE workgroup per vocab tile for ALL batch rows
+// (B <= 64).  The row-block split above re-stages the tile's whole Wa block [64, C] for
+// each 16-row block (4 x at B = 64: 1.7 GB of L2 -> LDS traffic at V = 112k for an
+// 11 GFLOP product); here every Wa element is staged once and feeds 4x the MFMA work.
+// Wave w owns output subtiles (row tile w >> 1, column strips 2 (w & 1), +1) of the
+// [64, 64] tile over the full chunk; chunk c + 1 is in flight in registers while c is
+// multiplied.  The Wc tile stays in registers through the C loop and is stored into
+// the freed chunk buffers afterwards, so the LDS holds one chunk pair (67 KB: two
+// workgroups per CU).
+constexpr int CTX_FULL = 32;
+template <bool GB = false>
+__global__ void __launch_bounds__(FT) gfk_ctx_fwd_full_k(GfkArgT<GB> ga) {
+  const GfkModel& m = gfk_model(ga);
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int BMF = 64, SU = (BMF + 64) * FK / 4 / FT;     // float4 per thread per chunk: 8
+  const int tile = blockIdx.x;
+  if (tile >= m.n_tiles) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
+  const int r = lane & 15, g = lane >> 4;
+  const int V = m.V, C = m.C, H0 = m.H[0], nb = *m.ws_nb;
+  const int c0 = tile * 64, nvv = min(64, V - c0), H0P = rup(H0, 16), LDC = fwd_ldc(m);
+  float* xs = smem;                      // [64 x_ctx rows + 64 Wa rows][LDK]
+  float* as = smem;                      // after the loop: A [64][66]
+  float* wc = smem + 64 * 66;            //                 Wc tile [64][LDC]
+  const float* wcg = m.w_in + (size_t)V * H0;
+  auto ld_wc = [&](int i) {
+    const int vv = i / H0P, j = i - vv * H0P;
+    return (vv < nvv && j < H0) ? wcg[(size_t)(c0 + vv) * H0 + j] : 0.f;
+  };
+  auto st_wc = [&](int i, float xv) { const int vv = i / H0P; wc[vv * LDC + i - vv * H0P] = xv; };
+  float wcr[8];
+  reg_load<8, FT>(wcr, 64 * H0P, ld_wc);
+  const int bv = tid & 63;
+  const float bias = bv < nvv ? m.b_a[c0 + bv] : 0.f;
+  // staging element u of a chunk: float4 (row, q) = ((tid + FT u) / 32, (tid + FT u) % 32);
+  // rows 0..63 the batch's x_ctx rows (rows >= nb read row 0: finite, never stored),
+  // rows 64..127 the tile's Wa rows
+  const int q4 = (tid & 31) * 4;
+  const float* rowp[SU];
+  bool rok[SU];
+#pragma unroll
+  for (int u = 0; u < SU; ++u) {
+    const int row = (tid + FT * u) >> 5;
+    if (row < BMF) {
+      const int doc = m.ws_next[1 + min(row, m.bmax - 1)];
+      rowp[u] = m.ctx + (size_t)doc * C + q4;
+      rok[u] = true;
+    } else {
+      const int vv = row - BMF;
+      rowp[u] = m.w_a + (size_t)(c0 + min(vv, nvv - 1)) * C + q4;
+      rok[u] = vv < nvv;
+    }
+  }
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  auto ld = [&](int c, f32x4 (&rg)[SU]) {
+    const int k = c * FK;
+    const bool kin = k + q4 < C;
+#pragma unroll
+    for (int u = 0; u < SU; ++u)
+      rg[u] = (kin && rok[u]) ? *reinterpret_cast<const f32x4*>(rowp[u] + k) : z4;
+  };
+  auto st = [&](const f32x4 (&rg)[SU]) {
+#pragma unroll
+    for (int u = 0; u < SU; ++u) st_f4_as_f2(xs + ((tid + FT * u) >> 5) * LDK + q4, rg[u]);
+  };
+  const int rt = wave >> 1, cs0 = 2 * (wave & 1);
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+  const float* ap = xs + (rt * 16 + r) * LDK + g;
+  const float* bp0 = xs + (BMF + cs0 * 16 + r) * LDK + g;
+  const float* bp1 = bp0 + 16 * LDK;
+  auto mma = [&]() {
+#pragma unroll
+    for (int k = 0; k < FK; k += 4) {
+      const float a = ap[k];
+      acc0 = mfma16x16x4(a, bp0[k], acc0);
+      acc1 = mfma16x16x4(a, bp1[k], acc1);
+    }
+  };
+  const int NC = (C + FK - 1) / FK;
+  f32x4 ra[SU];
+  ld(0, ra);
+  st(ra);
+  if (NC > 1) ld(1, ra);
+  __syncthreads();
+  for (int c = 0; c < NC; ++c) {
+    mma();
+    if (c + 1 >= NC) break;
+    __syncthreads();
+    st(ra);
+    if (c + 2 < NC) ld(c + 2, ra);
+    __syncthreads();
+  }
+  __syncthreads();                       // every wave done with the chunk buffers
+  // ---- A = acc + bias -> LDS (for P) and ws_actx (for ctx_bwd / win_update) ----
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const f32x4& a4 = h ? acc1 : acc0;
+    const int col = (cs0 + h) * 16 + r;
+    const float bb = __shfl(bias, col, 64);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = rt * 16 + g * 4 + i;
+      const float a = col < nvv ? a4[i] + bb : 0.f;
+      as[row * 66 + col] = a;
+      if (row < m.bmax) m.ws_actx[((size_t)tile * m.bmax + row) * 64 + col] = a;
+    }
+  }
+  reg_store<8, FT>(wcr, 64 * H0P, ld_wc, st_wc);
+  __syncthreads();
+  // ---- P [64, H0] = A Wc_tile: subtiles (row tile, column tile) dealt to the waves ----
+  float* hg = m.ws_hpart + (size_t)tile * m.bmax * H0;
+  const int NJT = H0P / 16;
+  for (int t = wave; t < 4 * NJT; t += FT / 64) {
+    const int prt = t / NJT, jt = t % NJT;
+    f32x4 p = {0.f, 0.f, 0.f, 0.f};
+    const float* pa = as + (prt * 16 + r) * 66 + g;
+    const float* pb = wc + g * LDC + jt * 16 + r;
+#pragma unroll 4
+    for (int k = 0; k < 64; k += 4) p = mfma16x16x4(pa[k], pb[k * LDC], p);
+    const int j = jt * 16 + r;
+    if (j < H0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = prt * 16 + g * 4 + i;
+        if (row < m.bmax) hg[(size_t)row * H0 + j] = p[i];
+      }
+    }
+  }
+  (void)nb;
+}
+
 // grid: n_tiles * ctx_kb workgroups of 16 waves (one per CU).
 template <int BM, bool GB = false>
 __global__ void __launch_bounds__(CT) gfk_ctx_bwd_k(GfkArgT<GB> ga) {
@@ -396,8 +527,14 @@ __global__ void __launch_bounds__(CT) gfk_ctx_bwd_k(GfkArgT<GB> ga) {
   GFK_STAMP(m, 38);
 }
 
+__host__ __device__ inline int fwd_full_lds_floats(const GfkModel& m) {
+  const int a = 128 * LDK, b = 64 * 66 + 64 * fwd_ldc(m);
+  return a > b ? a : b;
+}
+
 extern "C" size_t gfk_ctx_smem(const GfkModel* m) {
-  const size_t a = fwd_lds_floats(*m), b = bwd_lds(*m).total;
+  size_t a = fwd_lds_floats(*m), b = bwd_lds(*m).total;
+  if ((m->stage_flags & CTX_FULL) && (size_t)fwd_full_lds_floats(*m) > a) a = fwd_full_lds_floats(*m);
   return sizeof(float) * (a > b ? a : b);
 }
 
@@ -410,7 +547,8 @@ extern "C" int gfk_ctx_set_smem(size_t bytes) {
   const void* ks[] = {(const void*)gfk_ctx_fwd_k<16>, (const void*)gfk_ctx_fwd_k<16, true>, (const void*)gfk_ctx_fwd_k<32>, (const void*)gfk_ctx_fwd_k<32, true>,
                       (const void*)gfk_ctx_fwd_k<64>, (const void*)gfk_ctx_fwd_k<64, true>, (const void*)gfk_ctx_fwd_k<128>, (const void*)gfk_ctx_fwd_k<128, true>,
                       (const void*)gfk_ctx_bwd_k<16>, (const void*)gfk_ctx_bwd_k<16, true>, (const void*)gfk_ctx_bwd_k<32>, (const void*)gfk_ctx_bwd_k<32, true>,
-                      (const void*)gfk_ctx_bwd_k<64>, (const void*)gfk_ctx_bwd_k<64, true>, (const void*)gfk_ctx_bwd_k<128>, (const void*)gfk_ctx_bwd_k<128, true>};
+                      (const void*)gfk_ctx_bwd_k<64>, (const void*)gfk_ctx_bwd_k<64, true>, (const void*)gfk_ctx_bwd_k<128>, (const void*)gfk_ctx_bwd_k<128, true>,
+                      (const void*)gfk_ctx_fwd_full_k<false>, (const void*)gfk_ctx_fwd_full_k<true>};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return (int)e;
@@ -430,6 +568,12 @@ static bool ctx_ok(const GfkModel* m) {
 
 extern "C" int gfk_launch_ctx_fwd(const GfkModel* m, hipStream_t s) {
   if (!ctx_ok(m)) return -9;
+  if ((m->stage_flags & CTX_FULL) && m->bmax <= 64) {
+    const dim3 g(m->n_tiles), t(FT);
+    const size_t sm = sizeof(float) * fwd_full_lds_floats(*m);
+    do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_ctx_fwd_full_k<true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_ctx_fwd_full_k<false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0);
+    return (int)hipGetLastError();
+  }
   const dim3 g(8 * ((m->n_tiles + 7) / 8) * (m->bmax / 16)), t(FT);
   const size_t sm = sizeof(float) * fwd_lds_floats(*m);
   switch (m->bmax) {

@@ -523,6 +523,25 @@ __device__ __forceinline__ void glds_copy(float* dst, const float* src, int n, i
                                        (lds_void_ptr)(dst + 4 * c0), 16, 0, 0);
 }
 
+// glds_copy of a COMPILE-TIME size: straight-line instructions (no loop), so the
+// compiler's vmcnt bookkeeping stays exact across it (after a copy loop of unknown trip
+// count it can only wait for vmcnt(0)).  N floats, a multiple of 4; NT threads.
+template <int N, int NT>
+__device__ __forceinline__ void glds_copy_n(float* dst, const float* src, int tid) {
+  static_assert(N % 4 == 0 && NT % 64 == 0, "whole chunks, whole waves");
+  constexpr int NCH = N / 4, PASS = NT, FULL = NCH / PASS, REM = NCH % PASS;
+  const int lane = tid & 63, w = tid >> 6;
+#pragma unroll
+  for (int p = 0; p < FULL; ++p)
+    __builtin_amdgcn_global_load_lds((gbl_void_ptr)(src + 4 * (p * PASS + w * 64 + lane)),
+                                     (lds_void_ptr)(dst + 4 * (p * PASS + w * 64)), 16, 0, 0);
+  if constexpr (REM > 0) {
+    if (w * 64 + lane < REM)
+      __builtin_amdgcn_global_load_lds((gbl_void_ptr)(src + 4 * (FULL * PASS + w * 64 + lane)),
+                                       (lds_void_ptr)(dst + 4 * (FULL * PASS + w * 64)), 16, 0, 0);
+  }
+}
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // 16x16x4 fp32 MFMA: lane l supplies A[l&15][l>>4] and B[l>>4][l&15];

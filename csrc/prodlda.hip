@@ -297,10 +297,18 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkArgT<GB> ga
 // global rounds overlap.  Measured (profiles/r2/ab_strip_forward.txt): K=50 headline
 // round 0.0589 -> 0.0583 ms, K=50 V=28k 0.101 -> 0.092, K=200 V=112k 0.349 -> 0.342.
 // NP: k pairs held in registers (compile-time, the launcher's smallest instance >= K / 8).
-template <int BM, int NP, bool PF, bool GB = false>
-__global__ void __launch_bounds__(PF ? 512 : 1024) prodlda_fwd_strip_kernel(GfkArgT<GB> ga) {
+// PF = 2 (stage_flags bit 6, the default): ROLLING prefetch at 16 waves of <= 128 VGPRs:
+// right after the MFMAs that consume a k pair of this strip's beta block, the same pair of
+// the wave's NEXT strip is loaded into those registers, so each pair has a whole strip of
+// compute to arrive, with no second register block (PF = 1 holds two: 190 VGPRs, 2 waves
+// per SIMD, the MFMA pipe ~40 % busy at K = 200).
+// (PF = 2 with more than 13 k pairs: 12 waves of <= 168 VGPRs, 3 per SIMD -- the 50-register
+// beta block + accumulators + A operands spill at 128)
+__host__ __device__ constexpr int strip_threads(int pf, int np) { return pf == 1 ? 512 : pf == 2 && np > 13 ? 768 : 1024; }
+template <int BM, int NP, int PF, bool GB = false>
+__global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kernel(GfkArgT<GB> ga) {
   const GfkModel& m = gfk_model(ga);
-  constexpr int STRIP_THREADS = PF ? 512 : 1024;
+  constexpr int STRIP_THREADS = strip_threads(PF, NP);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int K = m.K, V = m.V, KT = m.kt;
   int tid = threadIdx.x;
@@ -376,7 +384,7 @@ __global__ void __launch_bounds__(PF ? 512 : 1024) prodlda_fwd_strip_kernel(GfkA
     // two global rounds overlap instead of following each other
     // (unconditional, clamped: behind a branch the waitcnt pass would assume the loads
     // absent at the join and wait for everything)
-    if (PF) issue(min(s, nstrips - 1), b, rm0, rv0);
+    if (PF != 0) issue(min(s, nstrips - 1), b, rm0, rv0);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < SU; ++u) {
@@ -395,8 +403,20 @@ __global__ void __launch_bounds__(PF ? 512 : 1024) prodlda_fwd_strip_kernel(GfkA
   __builtin_assume(tid >= 0 && tid < STRIP_THREADS);
 #pragma unroll 1
   for (; s < nstrips; s += stride) {
-    if (PF) issue(min(s + stride, nstrips - 1), bn, rmn, rvn);   // (the last one re-reads a strip)
-    else issue(s, b, rm0, rv0);
+    // PF = 2: the next strip's per-lane buffer offset (its pairs are loaded in the MFMA loop)
+    int voffn = 0, v4n = V * 4;
+    if (PF == 1) {
+      issue(min(s + stride, nstrips - 1), bn, rmn, rvn);   // (the last one re-reads a strip)
+    } else if (PF == 2) {
+      const int sn = min(s + stride, nstrips - 1);
+      const int vcn = min((sn >> 2) * VB + 16 * (sn & 3) + (lane & 15), V - 1);
+      asm volatile("" : "+s"(v4n));
+      voffn = g2 * v4n + vcn * 4;
+      rmn = m.beta_rm[vcn];
+      rvn = m.beta_rv[vcn];
+    } else {
+      issue(s, b, rm0, rv0);
+    }
     const int tile = s >> 2, cs = s & 3;
     const int col = 16 * cs + (lane & 15);
     const int v = tile * VB + col;
@@ -427,6 +447,11 @@ __global__ void __launch_bounds__(PF ? 512 : 1024) prodlda_fwd_strip_kernel(GfkA
       for (int i = 0; i < RT; ++i) acc[i] = mfma16x16x4(a[t & 1][i].x, b[2 * t], acc[i]);
 #pragma unroll
       for (int i = 0; i < RT; ++i) acc[i] = mfma16x16x4(a[t & 1][i].y, b[2 * t + 1], acc[i]);
+      if (PF == 2) {                  // the next strip's pair t into the registers just read
+        b[2 * t] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bres, voffn, 0, 0));
+        b[2 * t + 1] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bres, voffn, v4n, 0));
+        voffn += 8 * v4n;
+      }
     }
     // ---- column batch-norm over the wave's own rows (rows >= nb excluded) ----
     // (rows >= nb are exact zeros, so the sum needs no mask; lim is made opaque per strip
@@ -469,9 +494,11 @@ __global__ void __launch_bounds__(PF ? 512 : 1024) prodlda_fwd_strip_kernel(GfkA
         if (i * 16 + e < lim) zt[row * VB + (col ^ zswz(row))] = z;
         rs_[i][e] += valid ? __expf(z) : 0.f;
       }
-    if (PF) {
+    if (PF == 1) {
 #pragma unroll
       for (int j = 0; j < 2 * NP; ++j) b[j] = bn[j];
+    }
+    if (PF != 0) {
       rm0 = rmn;
       rv0 = rvn;
     }
@@ -610,6 +637,11 @@ __global__ void __launch_bounds__(64) gfk_prodlda_row_loss(GfkArgT<GB> ga) {
 // accumulators stay in registers).
 __host__ __device__ __forceinline__ int kt_stride(int w) { return w % 32 == 16 ? w : w + 16; }
 __host__ __device__ __forceinline__ int bwd_kpq(int K, int kq) { return 16 * ((round_up(K, 16) / 16 + kq - 1) / kq); }
+// bwd_pre = 3 runs the software-pipelined backward (fp32, B = 64; else the bwd_pre = 2 one),
+// whose dlogit tiles are dense [B][64]
+__host__ __device__ __forceinline__ bool bwd_pipe(const GfkModel& m) {
+  return m.bwd_pre == 3 && m.bmax == 64 && !m.mm_bf16;
+}
 
 // Logit gradient of one vocabulary tile, computed ONCE (bwd_pre: the persistent k-range
 // backward at large V, whose 4 range workgroups per tile each recomputed it, each behind
@@ -680,6 +712,16 @@ __global__ void __launch_bounds__(256) prodlda_dlogit_kernel(GfkArgT<GB> ga) {
     }
   }
   lds_barrier();
+  if (bwd_pipe(m)) {
+    // ---- dense [BM][64] (the pipelined backward reads it into registers) ----
+    f32x4* out = reinterpret_cast<f32x4*>(m.ws_dt + (size_t)tile * BM * VB);
+    for (int i = tid; i < BM * VB / 4; i += NT) {
+      const float2* s2 = reinterpret_cast<const float2*>(dt + (i >> 4) * LDD + (i & 15) * 4);
+      const float2 a = s2[0], b = s2[1];
+      out[i] = f32x4{a.x, a.y, b.x, b.y};
+    }
+    return;
+  }
   // ---- the tile, verbatim (float4 over the flat [BM][LDD] block) ----
   f32x4* out = reinterpret_cast<f32x4*>(m.ws_dt + (size_t)tile * BM * LDD);
   const f32x4* d4 = reinterpret_cast<const f32x4*>(dt);
@@ -1129,10 +1171,227 @@ __global__ void __launch_bounds__(512, 2) prodlda_bwd_pre2_kernel(GfkArgT<GB> ga
   prodlda_bwd_body<BM, MAXU, 4, BF, true>(m);
 }
 
+// bwd_pre = 3: the precomputed-dlogit k-range backward, SOFTWARE-PIPELINED (fp32, B = 64).
+// The bwd_pre = 2 kernel waits for a tile's loads, computes, stores, and only then issues
+// the next tile's loads: each workgroup's memory traffic stops during its compute, and with
+// two workgroups per CU the chip moved ~3.8 TB/s (k200v112k_pre2_sparsewin_counters.md:
+// 41 % of wave cycles waiting on memory).  Here, per tile t:
+//   top      stage t's beta slice and dlogit tile (registers, loaded during tile t - 1) to LDS
+//            issue t's Adam m / v (consumed only by the epilogue, after the MFMAs), then
+//            tile t + nslab's beta slice and dlogit tile into the staging registers
+//   compute  d theta_d / dbeta MFMAs, the G tile, the Adam epilogue and stores
+// so every load is in flight during a compute phase, with 16 extra VGPRs (K = 200) and no
+// LDS-DMA (whose pending copies make the compiler's vmcnt bookkeeping fall back to
+// vmcnt(0)): every wait is the compiler's own.  The dlogit tiles come dense ([B][64],
+// written so by prodlda_dlogit).  The 4 range workgroups of a slab sit on ONE XCD
+// (blockIdx -> XCD round-robin), so a tile's dlogit block is fetched from HBM once and
+// served to the other three from that XCD's L2.
+// LDS: th [64][64] (PRE swizzle) + bt [KPQ][LDB_B] + dt [64][LDD] (the G tile aliases dt).
+template <int BM, int MAXU, bool GB = false>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
+prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
+  static_assert(BM == 64, "pipelined backward: B = 64");
+  const GfkModel& m = gfk_model(ga);
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int NTH = 512, NW = NTH / 64, KQ = 4;
+  constexpr int NKS = MAXU;                                    // max k tiles per range
+  constexpr int RPU = NTH / VB;                                // 8 block rows per slot
+  constexpr int RU = 16 * NKS * VB / NTH;                      // block elements per thread
+  constexpr int MU = (NKS * 4 + NW - 1) / NW;                  // dbeta subtiles per wave
+  constexpr int NDT = ((BM / 16) * NKS + NW - 1) / NW;         // d theta_d subtiles per wave
+  constexpr int DU = BM * VB / 4 / NTH;                        // dlogit float4 per thread
+  const int K = m.K, V = m.V;
+  int tid = threadIdx.x;
+  int lane = tid & 63, wave = uniform(tid >> 6);
+  const int ksub = round_up(K, 16) / 16;
+  const int G = (int)gridDim.x, nslab = G / KQ;
+  int q, slab;
+  if ((G & 31) == 0) {             // XCD-aware: blockIdx b runs on XCD b % 8
+    const int b = (int)blockIdx.x, j = b >> 3;
+    q = j & 3;
+    slab = ((j >> 2) << 3) | (b & 7);
+  } else {
+    q = (int)blockIdx.x % KQ;
+    slab = (int)blockIdx.x / KQ;
+  }
+  const int ks0 = q * ksub / KQ, nks = (q + 1) * ksub / KQ - ks0;
+  const int kb = 16 * ks0;
+  const int KPQ = bwd_kpq(K, KQ);
+  float* th = smem;
+  float* bt = th + BM * 64;
+  float* dt = bt + KPQ * LDB_B;                 // (the G tile aliases it)
+  const int NB_T = nks * 4, NDT_T = (BM / 16) * nks;
+  const bool fused = m.update_mode == 1 && !m.beta_split;
+  const int nb = *m.ws_nb;
+  const AdamCoef ac = adam_coef(m);
+  const bool beta_shared = is_shared(m, m.beta);
+  const int n_tiles = m.n_tiles;
+
+  for (int i = tid; i < BM * 16 * NKS; i += NTH) {
+    const int b = i / (16 * NKS), c = i % (16 * NKS);
+    th[b * 64 + (c ^ (((b >> 3) & 1) << 4))] = c < 16 * nks ? m.ws_thetad[(size_t)b * m.kt + kb + c] : 0.f;
+  }
+
+  float br[RU], rm[RU], rv[RU];
+  f32x4 dr[DU];
+  // element tid + NTH u of the block is (row tid / VB + RPU u, column tid % VB)
+  auto issue_bd = [&](int tile) {             // beta slice + dlogit tile
+    const int c = min(tile * VB + (tid & (VB - 1)), V - 1);
+    const f32x4* d4 = reinterpret_cast<const f32x4*>(m.ws_dt + (size_t)tile * BM * VB);
+#pragma unroll
+    for (int j = 0; j < DU; ++j) dr[j] = d4[tid + NTH * j];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) br[u] = m.beta[(size_t)min(kb + tid / VB + RPU * u, K - 1) * V + c];
+  };
+  // Adam state (gradient mode: beta itself, unused -- unconditional, like every load and
+  // store of the tile loop, so the compiler's vmcnt bookkeeping stays exact across it)
+  const int64_t om = fused ? m.off_m : 0, ov = fused ? m.off_v : 0;
+  auto issue_mv = [&](int tile) {
+    const int c = min(tile * VB + (tid & (VB - 1)), V - 1);
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const float* p = m.beta + (size_t)min(kb + tid / VB + RPU * u, K - 1) * V + c;
+      rm[u] = p[om];
+      rv[u] = p[ov];
+    }
+  };
+  // out-of-range elements store into the slack behind the dense dlogit tiles (ws_dt holds
+  // [n_tiles][B][66] + 2048 floats; the dense layout uses [n_tiles][B][64]), which nothing
+  // reads
+  float* const sink = m.ws_dt + (size_t)n_tiles * BM * VB + (tid & 63);
+
+  f32x4 dacc[NDT];
+#pragma unroll
+  for (int j = 0; j < NDT; ++j) dacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue_bd(slab);
+  // the loop's epilogue issues 3 RU stores after the next tile's loads; the same number of
+  // sink stores here gives the loop entry that shape too, so the compiler's wait for the
+  // staged registers is vmcnt(3 RU + ...) on both edges (else vmcnt(0) at every tile:
+  // the previous tile's stores drained before staging)
+  // (distinct addresses, so the compiler cannot merge them; ws_dt has 2048 floats of slack)
+#pragma unroll
+  for (int u = 0; u < 3 * RU; ++u) sink[64 * (u + 1)] = 0.f;
+#pragma unroll 1
+  for (int tile = slab; tile < n_tiles; tile += nslab) {
+    const int c0 = tile * VB;
+    asm volatile("" : "+v"(tid));
+    __builtin_assume(tid >= 0 && tid < NTH);
+    lane = tid & 63;
+    wave = uniform(tid >> 6);
+    lds_barrier();                             // the previous tile's LDS reads are done
+    {
+      const int c = tid & (VB - 1), cok = c0 + c < V;
+#pragma unroll
+      for (int u = 0; u < RU; ++u) {
+        const int k = tid / VB + RPU * u;
+        if (k < 16 * nks) bt[k * LDB_B + c] = (kb + k < K && cok) ? br[u] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < DU; ++j) {           // dense [BM][64] -> [BM][LDD] (8-byte aligned)
+        const int i = tid + NTH * j, r = i >> 4, c4 = (i & 15) * 4;
+        float2* d2 = reinterpret_cast<float2*>(dt + r * LDD + c4);
+        d2[0] = make_float2(dr[j][0], dr[j][1]);
+        d2[1] = make_float2(dr[j][2], dr[j][3]);
+      }
+    }
+    // (the staging above consumed the registers; this tile's m / v first, then the next
+    // tile's beta / dlogit: the epilogue's wait for m / v leaves the latter in flight)
+    issue_mv(tile);
+    issue_bd(min(tile + nslab, n_tiles - 1));  // (last tile: a harmless reload)
+    lds_barrier();
+
+    // d theta_d[b, k] += sum_c dlogit[b, c] beta[k, c]
+#pragma unroll
+    for (int j = 0; j < NDT; ++j) {
+      const int t = wave + NW * j;
+      if (t >= NDT_T) break;
+      const int rt = t / nks, ks = t % nks;
+      const float* ap = dt + (rt * 16 + (lane & 15)) * LDD + (lane >> 4);
+      const float* bp = bt + (ks * 16 + (lane & 15)) * LDB_B + (lane >> 4);
+      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < VB; c += 8) {
+        a0 = mfma16x16x4(ap[c], bp[c], a0);
+        a1 = mfma16x16x4(ap[c + 4], bp[c + 4], a1);
+      }
+      dacc[j] += a0 + a1;
+    }
+    // dbeta[k, c] = sum_b th[b, k] dlogit[b, c]; batch mapping b = 8 g + (j & 7) + 32 (j >> 3)
+    // (see prodlda_bwd_body), theta_d's columns XOR 16 (g & 1)
+    float gr[MU][4];
+#pragma unroll
+    for (int u = 0; u < MU; ++u) {
+      const int t = wave + NW * u;
+      if (t >= NB_T) break;
+      const int ks = t >> 2, cst = t & 3;
+      const int g = lane >> 4;
+      const int kc = ks * 16 + (lane & 15);
+      const float* ap = th + 8 * g * 64 + (kc ^ ((g & 1) << 4));
+      const float* bp = dt + 8 * g * LDD + cst * 16 + (lane & 15);
+      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < BM / 4; j += 2) {
+        const int r0 = (j & 7) + 32 * (j >> 3), r1 = ((j + 1) & 7) + 32 * ((j + 1) >> 3);
+        a0 = mfma16x16x4(ap[r0 * 64], bp[r0 * LDD], a0);
+        a1 = mfma16x16x4(ap[r1 * 64], bp[r1 * LDD], a1);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gr[u][e] = a0[e] + a1[e];
+    }
+    lds_barrier();                             // every wave is done reading dt
+#pragma unroll
+    for (int u = 0; u < MU; ++u) {
+      const int t = wave + NW * u;
+      if (t >= NB_T) break;
+      const int ks = t >> 2, cl = (t & 3) * 16 + (lane & 15);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int kl = ks * 16 + (lane >> 4) * 4 + e;
+        dt[kl * VB + (cl ^ ((kl & 4) << 2))] = gr[u][e];
+      }
+    }
+    lds_barrier();
+    // the G tile, row-wise: update (fused) or gradient
+    const int cl = tid & (VB - 1), kl0 = tid / VB, c = c0 + cl;
+    const int cs = cl ^ ((kl0 & 4) << 2);
+    float* p0 = m.beta + (size_t)(kb + kl0) * V + c;
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int kl = kl0 + RPU * u, k = kb + kl;
+      const bool ok = kl < 16 * nks && k < K && c < V;
+      const float gv = dt[kl * VB + cs];
+      float* p = p0 + (size_t)(RPU * u) * V;
+      float mo = rm[u], vo = rv[u];
+      float np = adam_update(bt[kl * LDB_B + cl], gv, mo, vo, ac);
+      if (beta_shared && m.fed_scale_on) np *= m.fed_scale;
+      // fused: m, v, beta; gradient mode: the gradient (+ two sink stores)
+      *(ok ? p + (fused ? m.off_m : m.off_g) : sink) = fused ? mo : gv;
+      *(ok && fused ? p + m.off_v : sink) = vo;
+      *(ok && fused ? p : sink) = np;
+    }
+  }
+  // this workgroup's d theta_d partial (plain stores; row_bwd sums the slabs in order)
+  float* dpart = m.ws_dthetad + (size_t)slab * m.bmax * K;
+#pragma unroll
+  for (int j = 0; j < NDT; ++j) {
+    const int t = wave + NW * j;
+    if (t >= NDT_T) break;
+    const int rt = t / nks, ks = t % nks;
+    const int k = kb + ks * 16 + (lane & 15);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = rt * 16 + (lane >> 4) * 4 + e;
+      if (row < nb && k < K) dpart[(size_t)row * K + k] = dacc[j][e];
+    }
+  }
+}
+
 // stage_flags bit 2: the strip forward (prodlda_fwd_strip_kernel) -- theta_d + the
 // per-wave row partials only
 constexpr int FWD_STRIP = 4;
 constexpr int FWD_STRIP_PF = 8;   // bit 3: its prefetching 8-wave variant
+constexpr int FWD_STRIP_ROLL = 64;  // bit 6: its rolling-prefetch 16-wave variant (PF = 2)
 __host__ __device__ inline int strip_pairs(int K) { return (K + 7) / 8; }
 // the kernel instance (k pairs in registers) for K
 __host__ __device__ inline int strip_np(int K) {
@@ -1177,10 +1436,12 @@ extern "C" int gfk_launch_prodlda_fwd(const GfkModel* m, hipStream_t s) {
         (int64_t)m->K * m->V >= (1LL << 29)) return -1;
 #define GFK_FWS(BM, NP)                                                                        \
     do {                                                                                       \
-      if (m->stage_flags & FWD_STRIP_PF)                                                       \
-        do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, true, true>), gfk_grid(g, m), dim3(512), sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, true, false>), g, dim3(512), sm, s, GfkArgT<false>{*m}); } while (0); \
+      if (m->stage_flags & FWD_STRIP_ROLL)                                                     \
+        do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 2, true>), gfk_grid(g, m), dim3(strip_threads(2, NP)), sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 2, false>), g, dim3(strip_threads(2, NP)), sm, s, GfkArgT<false>{*m}); } while (0); \
+      else if (m->stage_flags & FWD_STRIP_PF)                                                  \
+        do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 1, true>), gfk_grid(g, m), dim3(512), sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 1, false>), g, dim3(512), sm, s, GfkArgT<false>{*m}); } while (0); \
       else                                                                                     \
-        do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, false, true>), gfk_grid(g, m), dim3(1024), sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, false, false>), g, dim3(1024), sm, s, GfkArgT<false>{*m}); } while (0); \
+        do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 0, true>), gfk_grid(g, m), dim3(1024), sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 0, false>), g, dim3(1024), sm, s, GfkArgT<false>{*m}); } while (0); \
     } while (0)
 #define GFK_FWS_B(BM)                                                      \
     if (np == 8) GFK_FWS(BM, 8);                                           \
@@ -1214,7 +1475,14 @@ extern "C" int gfk_launch_prodlda_fwd(const GfkModel* m, hipStream_t s) {
 template <int MAXU, int KQ, bool BF, bool PRE>
 static void launch_bwd_p(const GfkModel* m, dim3 g, size_t sm, hipStream_t s) {
   const dim3 blk(KQ == 1 ? DEC_THREADS : 512);
-  if (PRE && m->bwd_pre == 2) {
+  if constexpr (PRE && !BF) {
+    if (bwd_pipe(*m)) {
+      if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_bwd_pipe_kernel<64, MAXU, true>), gfk_grid(g, m), blk, sm, s, GfkArgT<true>{gfk_dev(m)});
+      else hipLaunchKernelGGL((prodlda_bwd_pipe_kernel<64, MAXU, false>), g, blk, sm, s, GfkArgT<false>{*m});
+      return;
+    }
+  }
+  if (PRE && m->bwd_pre >= 2) {
     switch (m->bmax) {
       case 16: do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_bwd_pre2_kernel<16, MAXU, BF, true>), gfk_grid(g, m), blk, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_bwd_pre2_kernel<16, MAXU, BF, false>), g, blk, sm, s, GfkArgT<false>{*m}); } while (0); break;
       case 32: do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_bwd_pre2_kernel<32, MAXU, BF, true>), gfk_grid(g, m), blk, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_bwd_pre2_kernel<32, MAXU, BF, false>), g, blk, sm, s, GfkArgT<false>{*m}); } while (0); break;
@@ -1297,7 +1565,7 @@ extern "C" int gfk_prodlda_set_smem(size_t bytes) {
 #define GFK_FWS_PTRS1(BM, F) (const void*)prodlda_fwd_strip_kernel<BM, 8, F>, (const void*)prodlda_fwd_strip_kernel<BM, 8, F, true>, \
     (const void*)prodlda_fwd_strip_kernel<BM, 13, F>, (const void*)prodlda_fwd_strip_kernel<BM, 13, F, true>, (const void*)prodlda_fwd_strip_kernel<BM, 16, F>, (const void*)prodlda_fwd_strip_kernel<BM, 16, F, true>, \
     (const void*)prodlda_fwd_strip_kernel<BM, 25, F>, (const void*)prodlda_fwd_strip_kernel<BM, 25, F, true>, (const void*)prodlda_fwd_strip_kernel<BM, 32, F>, (const void*)prodlda_fwd_strip_kernel<BM, 32, F, true>
-#define GFK_FWS_PTRS(BM) GFK_FWS_PTRS1(BM, false), GFK_FWS_PTRS1(BM, true)
+#define GFK_FWS_PTRS(BM) GFK_FWS_PTRS1(BM, 0), GFK_FWS_PTRS1(BM, 1), GFK_FWS_PTRS1(BM, 2)
                       GFK_FWS_PTRS(16), GFK_FWS_PTRS(32), GFK_FWS_PTRS(64),
 #undef GFK_FWS_PTRS
 #undef GFK_FWS_PTRS1
@@ -1310,7 +1578,7 @@ extern "C" int gfk_prodlda_set_smem(size_t bytes) {
     (const void*)prodlda_bwd_pre2_kernel<16, U, F>, (const void*)prodlda_bwd_pre2_kernel<16, U, F, true>, (const void*)prodlda_bwd_pre2_kernel<32, U, F>, (const void*)prodlda_bwd_pre2_kernel<32, U, F, true>, \
     (const void*)prodlda_bwd_pre2_kernel<64, U, F>, (const void*)prodlda_bwd_pre2_kernel<64, U, F, true>
 #define GFK_BWD_PTRS(U) GFK_BWD_PTRS1(U, 1), GFK_BWD_PTRS1(U, 4), GFK_BWD_PTRS3(U, false), \
-    GFK_BWD_PTRS3(U, true)
+    GFK_BWD_PTRS3(U, true), (const void*)prodlda_bwd_pipe_kernel<64, U>, (const void*)prodlda_bwd_pipe_kernel<64, U, true>
                       GFK_BWD_PTRS(1), GFK_BWD_PTRS(2), GFK_BWD_PTRS(3), GFK_BWD_PTRS(4)};
 #undef GFK_BWD_PTRS
 #undef GFK_BWD_PTRS3

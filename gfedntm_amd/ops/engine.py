@@ -56,6 +56,8 @@ STAGE_PLANS = (1, 0, 3, 2)
 STAGE_FWD_STRIP = 4               # bit 2: ProdLDA strip forward (csrc/prodlda.hip)
 STAGE_FWD_STRIP_PF = 8            # bit 3: its prefetching 8-wave variant
 STAGE_WIN_SPARSE = 16             # bit 4: sparse W_in tiles (csrc/update.hip win_tile_sparse)
+STAGE_CTX_FULL = 32               # bit 5: CombinedTM forward, one workgroup per tile (csrc/ctx.hip)
+STAGE_FWD_STRIP_ROLL = 64         # bit 6: the strip forward's rolling-prefetch variant
 
 
 def _explain(ok: bool, why: str, explain: bool) -> bool:
@@ -462,8 +464,14 @@ class FusedEngine(EngineBase):
                 # per SIMD, ~190 VGPRs) measured ahead of 16 non-prefetching waves per CU
                 # (K=200: V=112k 0.341 vs 0.346 ms, V=74k 0.251 vs 0.260 ms; the tile
                 # kernel 0.346 / 0.255); GFEDNTM_FWD_STRIP_PF=0 selects the 16-wave one
-                if os.environ.get("GFEDNTM_FWD_STRIP_PF", "1") == "1":
+                # 2, the default: the rolling prefetch (the next strip's k pair loaded into
+                # the registers its MFMAs just consumed; 12-16 waves per CU, no second
+                # register block)
+                pf = os.environ.get("GFEDNTM_FWD_STRIP_PF", "2")
+                if pf == "1":
                     m.stage_flags |= STAGE_FWD_STRIP_PF
+                elif pf == "2":
+                    m.stage_flags |= STAGE_FWD_STRIP_ROLL
                 m.dec_grid = int(min(m.n_tiles, cu))
             # backward: one workgroup per tile while the tiles fit the resident slots;
             # else persistent, n_dpart d theta_d slabs: with >= 4 k tiles the topics
@@ -484,12 +492,17 @@ class FusedEngine(EngineBase):
             # recomputing them in each range workgroup; GFEDNTM_BWD_PRE=0 selects the
             # recomputing variant
             kq4 = m.n_dpart < m.n_tiles and -(-m.K // 16) >= 4
-            pre = os.environ.get("GFEDNTM_BWD_PRE", "2")
-            m.bwd_pre = int(pre) if kq4 and m.bmax <= 64 and pre in ("1", "2") else 0
+            # (1: <= 80 VGPRs, three per CU; 2: two per CU; 3, the default: two per CU,
+            # software-pipelined -- the next tile's loads in flight during this tile's
+            # compute and stores -- where it applies: fp32, B = 64)
+            pre = os.environ.get("GFEDNTM_BWD_PRE", "3")
+            m.bwd_pre = int(pre) if kq4 and m.bmax <= 64 and pre in ("1", "2", "3") else 0
             if m.bwd_pre == 1 and 3 * self.lib.gfk_smem_required(C.byref(m), 1) <= LDS_LIMIT:
                 # its smaller LDS plan (no logit tile, G aliases dt) and <= 80 VGPRs fit
                 # THREE range workgroups per CU: 3/4 of a CU's slots per slab of 4
                 m.n_dpart = min(3 * cu // 4, m.n_tiles - 1)
+            elif m.bwd_pre == 3 and m.bmax == 64 and not m.mm_bf16:
+                pass
             elif m.bwd_pre:
                 m.bwd_pre = 2            # two per CU, no register cap
             # GFEDNTM_BETA_SPLIT=1: beta's Adam as one streaming float4 pass after
@@ -504,6 +517,12 @@ class FusedEngine(EngineBase):
         # holds few non-zeros (large vocabularies, the 8-wave update shape: more tiles than
         # two rounds of workgroups); GFEDNTM_WIN_SPARSE=0 keeps the dense tiles
         cu_n = props.multi_processor_count
+        # CombinedTM at large V: ctx_fwd with all batch rows per vocab tile (each Wa block
+        # staged once instead of once per 16-row block); GFEDNTM_CTX_FULL=0 / 1 overrides
+        cf_env = os.environ.get("GFEDNTM_CTX_FULL", "auto")
+        if m.ctx_fused == 1 and m.bmax <= 64 and (
+                cf_env == "1" or (cf_env == "auto" and m.n_tiles > 2 * cu_n)):
+            m.stage_flags |= STAGE_CTX_FULL
         ws_env = os.environ.get("GFEDNTM_WIN_SPARSE", "auto")
         if m.input == abi.IN_BOW and int(m.H[0]) <= 64 and m.bmax <= 128 and (
                 ws_env == "1" or (ws_env == "auto" and m.n_tiles > 4 * cu_n)):
@@ -585,8 +604,9 @@ class FusedEngine(EngineBase):
             # pre-activation partials (csrc/ctx.hip)
             "actx": f(m.n_tiles * B * 64 if m.ctx_fused == 1 else 1),
             "hpart": f(m.n_tiles * B * hs[0] if m.ctx_fused == 1 else 1),
-            # precomputed logit-gradient tiles [n_tiles][B][66] (bwd_pre)
-            "dt": f(m.n_tiles * B * 66 if m.bwd_pre else 1),
+            # precomputed logit-gradient tiles [n_tiles][B][66] (bwd_pre; + the pipelined
+            # backward's store sink)
+            "dt": f(m.n_tiles * B * 66 + 2048 if m.bwd_pre else 1),
         }
         Lb = max(int(m.L), 1)
         ws.update(lab=f(B, Lb), dlab=f(B, Lb), ce=f(B), thd=f(B, K))   # label head

@@ -95,16 +95,20 @@ def test_strip_forward_matches_oracle(monkeypatch, B, n_docs, K, H, V):
     _oracle_step("prodLDA", B, n_docs, K, H, V)
 
 
-@pytest.mark.parametrize("pre", ["1", "2", "0"])
-@pytest.mark.parametrize("B,n_docs,K,V", [(64, 80, 200, 40000), (32, 60, 64, 40000)])
+@pytest.mark.parametrize("pre", ["3", "1", "2", "0"])
+@pytest.mark.parametrize("B,n_docs,K,V", [(64, 80, 200, 40000), (32, 60, 64, 40000),
+                                          (64, 100, 64, 40000), (64, 70, 100, 30011)])
 def test_bwd_precomputed_dlogit_matches_oracle(monkeypatch, pre, B, n_docs, K, V):
     """Persistent 4-k-range backward: the logit-gradient tiles precomputed once per tile
-    by prodlda_dlogit (GFEDNTM_BWD_PRE=1, the default) or recomputed by every range
-    workgroup (=0) both match the oracle."""
+    by prodlda_dlogit -- software-pipelined (GFEDNTM_BWD_PRE=3, the default at B = 64;
+    B = 32 runs the =2 kernel), two or three workgroups per CU (=2 / =1) -- or recomputed
+    by every range workgroup (=0): all match the oracle (K = 100: a partial last k tile;
+    V = 30011: a partial last vocabulary tile)."""
     monkeypatch.setenv("GFEDNTM_BWD_PRE", pre)
     fused, _ = _pair("prodLDA", V=V, K=K, H=(50, 50), B=B)
     m = fused.engine._m
-    assert m.n_dpart < m.n_tiles and m.bwd_pre == {"1": 1, "2": 2, "0": 0}[pre]
+    want = 2 if (pre == "3" and B != 64) else int(pre)
+    assert m.n_dpart < m.n_tiles and m.bwd_pre == want
     _oracle_step("prodLDA", B, n_docs, K, (50, 50), V)
 
 
@@ -336,16 +340,21 @@ def test_training_decreases_loss():
     assert h[-10:].mean() < 0.9 * h[:10].mean()
 
 
-@pytest.mark.parametrize("inference_type,Cdim", [("combined", 96), ("combined", 100),
-                                                 ("combined", 16), ("zeroshot", 96)])
+@pytest.mark.parametrize("inference_type,Cdim,V,K", [("combined", 96, 600, 20), ("combined", 100, 600, 20),
+                                                     ("combined", 16, 600, 20), ("zeroshot", 96, 600, 20),
+                                                     # the BASELINE CTM class at large V
+                                                     ("combined", 768, 74000, 100)])
 @pytest.mark.parametrize("model_type", ["prodLDA", "LDA"])
-def test_ctm_step_matches_oracle(inference_type, Cdim, model_type):
+def test_ctm_step_matches_oracle(inference_type, Cdim, V, K, model_type):
     """CTM on the fused engine: CombinedTM's contextual path on ctx_fwd / ctx_bwd
-    (csrc/ctx.hip, C split into chunks), ZeroShotTM's dense input layer on host GEMMs;
-    compared with the explicit-noise oracle through the CTM encoder (gradient mode)."""
+    (csrc/ctx.hip, C split into chunks), ZeroShotTM's dense input layer in enc_in /
+    win_update; compared with the explicit-noise oracle through the CTM encoder
+    (gradient mode), up to CombinedTM K = 100, C = 768, V = 74k."""
     from gfedntm_amd.models import CombinedTM, ZeroShotTM
+    if V > 10000 and model_type == "LDA":
+        pytest.skip("large-V point: ProdLDA (the BASELINE CTM configuration)")
     cls = CombinedTM if inference_type == "combined" else ZeroShotTM
-    V, K, H, B, n_docs = 600, 20, (32, 24), 64, 150
+    H, B, n_docs = (32, 24), 64, 150
     torch.manual_seed(0)
     kw = dict(input_size=V, contextual_size=Cdim, n_components=K, model_type=model_type,
               hidden_sizes=H, batch_size=B, verbose=False, device="cuda")
@@ -714,3 +723,11 @@ def test_sparse_win_tiles_match_oracle(monkeypatch, model_type, B, n_docs, K, H,
     fused, _ = _pair(model_type, V=V, K=K, H=H, B=B)
     assert fused.engine._m.stage_flags & STAGE_WIN_SPARSE
     _oracle_step(model_type, B, n_docs, K, H, V)
+
+
+@pytest.mark.parametrize("Cdim,V", [(96, 600), (768, 9000)])
+def test_ctm_full_tile_forward_matches_oracle(monkeypatch, Cdim, V):
+    """ctx_fwd with all batch rows per vocab tile (stage_flags bit 5, the large-V shape;
+    GFEDNTM_CTX_FULL=1 forces it at small V)."""
+    monkeypatch.setenv("GFEDNTM_CTX_FULL", "1")
+    test_ctm_step_matches_oracle("combined", Cdim, V, 20, "prodLDA")
