@@ -1186,7 +1186,17 @@ __global__ void __launch_bounds__(512, 2) prodlda_bwd_pre2_kernel(GfkArgT<GB> ga
 // written so by prodlda_dlogit).  The 4 range workgroups of a slab sit on ONE XCD
 // (blockIdx -> XCD round-robin), so a tile's dlogit block is fetched from HBM once and
 // served to the other three from that XCD's L2.
-// LDS: th [64][64] (PRE swizzle) + bt [KPQ][LDB_B] + dt [64][LDD] (the G tile aliases dt).
+// MFMA operands: both products reduce over a 64-long axis, and the reduction index of MFMA
+// step 4 q + j for lane group g is 16 q + 4 g + j (a bijection, the same for A and B), so a
+// lane's operands for 4 steps are ONE ds_read_b128 along a row.  Each operand therefore
+// lives in LDS with the reduction axis contiguous (row stride 68: 16-byte aligned, and
+// the 8 lanes of a b128 read phase hit distinct banks):
+//   d theta_d[b, k] = sum_c dt[b][c] bt[k][c]       (dt: [b][c], bt: [k][c])
+//   dbeta[k, c]    = sum_b thT[k][b] dtT[c][b]      (theta_d and dlogit staged transposed)
+// -- 8 b128 reads per 16 MFMAs, all issued ahead of them, instead of 16 ds_read2_b32 one
+// step ahead (whose LDS latency stalled every MFMA pair: s_waitcnt lgkmcnt(0) each).
+// LDS: thT, bt, dt, dtT: 4 x [64][68] floats (70 KB; the G tile aliases dtT).
+constexpr int LDP = 68;
 template <int BM, int MAXU, bool GB = false>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
 prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
@@ -1216,10 +1226,10 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
   }
   const int ks0 = q * ksub / KQ, nks = (q + 1) * ksub / KQ - ks0;
   const int kb = 16 * ks0;
-  const int KPQ = bwd_kpq(K, KQ);
-  float* th = smem;
-  float* bt = th + BM * 64;
-  float* dt = bt + KPQ * LDB_B;                 // (the G tile aliases it)
+  float* thT = smem;                            // [64 k][LDP]   theta_d^T of the k range
+  float* bt = thT + 64 * LDP;                   // [64 k][LDP]   beta slice
+  float* dt = bt + 64 * LDP;                    // [64 b][LDP]   dlogit
+  float* dtT = dt + 64 * LDP;                   // [64 c][LDP]   dlogit^T (then the G tile)
   const int NB_T = nks * 4, NDT_T = (BM / 16) * nks;
   const bool fused = m.update_mode == 1 && !m.beta_split;
   const int nb = *m.ws_nb;
@@ -1227,9 +1237,9 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
   const bool beta_shared = is_shared(m, m.beta);
   const int n_tiles = m.n_tiles;
 
-  for (int i = tid; i < BM * 16 * NKS; i += NTH) {
-    const int b = i / (16 * NKS), c = i % (16 * NKS);
-    th[b * 64 + (c ^ (((b >> 3) & 1) << 4))] = c < 16 * nks ? m.ws_thetad[(size_t)b * m.kt + kb + c] : 0.f;
+  for (int i = tid; i < BM * 64; i += NTH) {   // (k >= the range: zero)
+    const int b = i >> 6, c = i & 63;
+    thT[c * LDP + b] = c < 16 * nks ? m.ws_thetad[(size_t)b * m.kt + kb + c] : 0.f;
   }
 
   float br[RU], rm[RU], rv[RU];
@@ -1259,6 +1269,25 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
   // [n_tiles][B][66] + 2048 floats; the dense layout uses [n_tiles][B][64]), which nothing
   // reads
   float* const sink = m.ws_dt + (size_t)n_tiles * BM * VB + (tid & 63);
+  // one 16 x 16 output subtile over the 64-long reduction: ar / br_ point at this lane's
+  // row (lane & 15) + 4 (lane >> 4); step 4 q + j takes reduction index 16 q + 4 g + j
+  auto mm64 = [&](const float* ar, const float* bq) {
+    f32x4 a[4], b[4];
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      a[qq] = *reinterpret_cast<const f32x4*>(ar + 16 * qq);
+      b[qq] = *reinterpret_cast<const f32x4*>(bq + 16 * qq);
+    }
+    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      a0 = mfma16x16x4(a[qq][0], b[qq][0], a0);
+      a1 = mfma16x16x4(a[qq][1], b[qq][1], a1);
+      a0 = mfma16x16x4(a[qq][2], b[qq][2], a0);
+      a1 = mfma16x16x4(a[qq][3], b[qq][3], a1);
+    }
+    return a0 + a1;
+  };
 
   f32x4 dacc[NDT];
 #pragma unroll
@@ -1285,14 +1314,14 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
 #pragma unroll
       for (int u = 0; u < RU; ++u) {
         const int k = tid / VB + RPU * u;
-        if (k < 16 * nks) bt[k * LDB_B + c] = (kb + k < K && cok) ? br[u] : 0.f;
+        if (k < 16 * nks) bt[k * LDP + c] = (kb + k < K && cok) ? br[u] : 0.f;
       }
 #pragma unroll
-      for (int j = 0; j < DU; ++j) {           // dense [BM][64] -> [BM][LDD] (8-byte aligned)
+      for (int j = 0; j < DU; ++j) {           // dense [BM][64] -> dt [b][c] and dtT [c][b]
         const int i = tid + NTH * j, r = i >> 4, c4 = (i & 15) * 4;
-        float2* d2 = reinterpret_cast<float2*>(dt + r * LDD + c4);
-        d2[0] = make_float2(dr[j][0], dr[j][1]);
-        d2[1] = make_float2(dr[j][2], dr[j][3]);
+        *reinterpret_cast<f32x4*>(dt + r * LDP + c4) = dr[j];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dtT[(c4 + e) * LDP + r] = dr[j][e];
       }
     }
     // (the staging above consumed the registers; this tile's m / v first, then the next
@@ -1301,45 +1330,28 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
     issue_bd(min(tile + nslab, n_tiles - 1));  // (last tile: a harmless reload)
     lds_barrier();
 
-    // d theta_d[b, k] += sum_c dlogit[b, c] beta[k, c]
+    const int r = lane & 15, g4 = 4 * (lane >> 4);
+    // d theta_d[b, k] += sum_c dt[b][c] bt[k][c]
 #pragma unroll
     for (int j = 0; j < NDT; ++j) {
       const int t = wave + NW * j;
       if (t >= NDT_T) break;
       const int rt = t / nks, ks = t % nks;
-      const float* ap = dt + (rt * 16 + (lane & 15)) * LDD + (lane >> 4);
-      const float* bp = bt + (ks * 16 + (lane & 15)) * LDB_B + (lane >> 4);
-      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int c = 0; c < VB; c += 8) {
-        a0 = mfma16x16x4(ap[c], bp[c], a0);
-        a1 = mfma16x16x4(ap[c + 4], bp[c + 4], a1);
-      }
-      dacc[j] += a0 + a1;
+      dacc[j] += mm64(dt + (rt * 16 + r) * LDP + g4, bt + (ks * 16 + r) * LDP + g4);
     }
-    // dbeta[k, c] = sum_b th[b, k] dlogit[b, c]; batch mapping b = 8 g + (j & 7) + 32 (j >> 3)
-    // (see prodlda_bwd_body), theta_d's columns XOR 16 (g & 1)
+    // dbeta[k, c] = sum_b thT[k][b] dtT[c][b]
     float gr[MU][4];
 #pragma unroll
     for (int u = 0; u < MU; ++u) {
       const int t = wave + NW * u;
       if (t >= NB_T) break;
       const int ks = t >> 2, cst = t & 3;
-      const int g = lane >> 4;
-      const int kc = ks * 16 + (lane & 15);
-      const float* ap = th + 8 * g * 64 + (kc ^ ((g & 1) << 4));
-      const float* bp = dt + 8 * g * LDD + cst * 16 + (lane & 15);
-      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+      const f32x4 a = mm64(thT + (ks * 16 + r) * LDP + g4, dtT + (cst * 16 + r) * LDP + g4);
 #pragma unroll
-      for (int j = 0; j < BM / 4; j += 2) {
-        const int r0 = (j & 7) + 32 * (j >> 3), r1 = ((j + 1) & 7) + 32 * ((j + 1) >> 3);
-        a0 = mfma16x16x4(ap[r0 * 64], bp[r0 * LDD], a0);
-        a1 = mfma16x16x4(ap[r1 * 64], bp[r1 * LDD], a1);
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) gr[u][e] = a0[e] + a1[e];
+      for (int e = 0; e < 4; ++e) gr[u][e] = a[e];
     }
-    lds_barrier();                             // every wave is done reading dt
+    lds_barrier();                             // every wave is done reading dt / dtT
+    float* gt = dtT;                           // the G tile [64 k][64 c], columns XOR 16 (k & 4)
 #pragma unroll
     for (int u = 0; u < MU; ++u) {
       const int t = wave + NW * u;
@@ -1348,7 +1360,7 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int kl = ks * 16 + (lane >> 4) * 4 + e;
-        dt[kl * VB + (cl ^ ((kl & 4) << 2))] = gr[u][e];
+        gt[kl * VB + (cl ^ ((kl & 4) << 2))] = gr[u][e];
       }
     }
     lds_barrier();
@@ -1360,10 +1372,10 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
     for (int u = 0; u < RU; ++u) {
       const int kl = kl0 + RPU * u, k = kb + kl;
       const bool ok = kl < 16 * nks && k < K && c < V;
-      const float gv = dt[kl * VB + cs];
+      const float gv = gt[kl * VB + cs];
       float* p = p0 + (size_t)(RPU * u) * V;
       float mo = rm[u], vo = rv[u];
-      float np = adam_update(bt[kl * LDB_B + cl], gv, mo, vo, ac);
+      float np = adam_update(bt[kl * LDP + cl], gv, mo, vo, ac);
       if (beta_shared && m.fed_scale_on) np *= m.fed_scale;
       // fused: m, v, beta; gradient mode: the gradient (+ two sink stores)
       *(ok ? p + (fused ? m.off_m : m.off_g) : sink) = fused ? mo : gv;
@@ -1417,6 +1429,7 @@ __host__ __device__ inline int bwd_kq(const GfkModel& m) {
 
 static size_t bwd_smem(const GfkModel* m, int kq) {
   const size_t KPQ = bwd_kpq(m->K, kq), B = m->bmax;
+  if (kq == 4 && bwd_pipe(*m)) return sizeof(float) * 4 * 64 * 68;   // thT, bt, dt, dtT
   if (kq == 4 && m->bwd_pre && B <= 64)       // th [B][64] + bt + dt (G aliases dt)
     return sizeof(float) * (B * 64 + KPQ * LDB_B + B * LDD);
   const size_t KTQ = kq == 1 ? (size_t)m->kt : (size_t)kt_stride((int)KPQ);
