@@ -233,8 +233,8 @@ __global__ void __launch_bounds__(FT) gfk_ctx_fwd_k(GfkArgT<GB> ga) {
 
 // Large vocabularies (stage_flags bit 5): ONE workgroup per vocab tile for ALL batch rows
 // (B <= 64).  The row-block split above re-stages the tile's whole Wa block [64, C] for
-// each 16-row block (4 x at B = 64: 1.7 GB of L2 -> LDS traffic at V = 112k for an
-// 11 GFLOP product); here every Wa element is staged once and feeds 4x the MFMA work.
+// each 16-row block (4 x at B = 64: 1.2 GB of L2 -> LDS traffic at V = 99k for a
+// 9.8 GFLOP product); here every Wa element is staged once and feeds 4x the MFMA work.
 // Wave w owns output subtiles (row tile w >> 1, column strips 2 (w & 1), +1) of the
 // [64, 64] tile over the full chunk; chunk c + 1 is in flight in registers while c is
 // multiplied.  The Wc tile stays in registers through the C loop and is stored into

@@ -167,7 +167,9 @@ typedef struct GfkModel {
   const void* dev;
   const void* dev_upd;
   int32_t n_batch;
-  int32_t pad4;
+  // beta's row stride in floats (>= V: the flat layout pads beta's rows to 128-B lines at
+  // large V, utils/flat.py); m / v / the gradient share it
+  int32_t ldb;
 } GfkModel;
 
 // launch helpers: grid z = the batched models, the kernel argument = the device array
@@ -257,6 +259,9 @@ namespace gfk {
 
 // In-kernel phase timestamps for diagnostic builds (-DGFK_STAMPS): lane 0 of
 // workgroup 0 writes s_memtime into dbg[slot].  Compiled out otherwise.
+#ifndef GFK_DIAG_BWD
+#define GFK_DIAG_BWD 0      // diagnostic variants of prodlda_bwd_pipe_kernel (tools/ab_libs.py AB_DEFS)
+#endif
 #ifdef GFK_STAMPS
 #define GFK_STAMP(m, slot)                                                        \
   do {                                                                            \

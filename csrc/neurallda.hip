@@ -50,7 +50,7 @@ __global__ void __launch_bounds__(LBT) gfk_lda_beta_fwd(GfkArgT<GB> ga) {
 #pragma unroll
     for (int u = 0; u < BU; ++u) {
       const int i = tid + LBT * u, k = i / VB, cc = i % VB;
-      bv[u] = (i < K * VB && cc < nv) ? m.beta[(size_t)k * V + c0 + cc] : 0.f;
+      bv[u] = (i < K * VB && cc < nv) ? m.beta[(size_t)k * m.ldb + c0 + cc] : 0.f;
     }
     float rm0 = 0.f, rv0 = 0.f;
     if (sub == 0 && valid) { rm0 = m.beta_rm[c0 + c]; rv0 = m.beta_rv[c0 + c]; }
@@ -269,7 +269,7 @@ __global__ void __launch_bounds__(LBT) gfk_lda_beta_bwd_k(GfkArgT<GB> ga) {
       pp[u] = pm[u] = pv[u] = 0.f;
       const int i = tid + LBT * u, k = i / VB, c = i % VB;
       if (fused && u < n_upd && k < K && c < nv) {
-        const float* p = m.beta + (size_t)k * V + c0 + c;
+        const float* p = m.beta + (size_t)k * m.ldb + c0 + c;
         pp[u] = *p;
         pm[u] = p[m.off_m];
         pv[u] = p[m.off_v];
@@ -356,7 +356,7 @@ __global__ void __launch_bounds__(LBT) gfk_lda_beta_bwd_k(GfkArgT<GB> ga) {
       for (int i = tid; i < K * VB; i += LBT, ++u) {
         const int k = i / VB, c = i % VB;
         if (c >= nv) continue;
-        float* p = m.beta + (size_t)k * V + c0 + c;
+        float* p = m.beta + (size_t)k * m.ldb + c0 + c;
         const float g = d[k * LD + c];
         if (!fused) {
           p[m.off_g] = g;

@@ -119,7 +119,7 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkArgT<GB> ga
 #pragma unroll
     for (int u = 0; u < BU; ++u) {
       // 32-bit element offsets (K V < 2^31): one VGPR per address, not a pair
-      br[u] = m.beta[min(tid / VB + 16 * u, K - 1) * V + c];
+      br[u] = m.beta[min(tid / VB + 16 * u, K - 1) * m.ldb + c];
     }
     const int v = min(c0 + col, V - 1);
     rmr = m.beta_rm[v];
@@ -311,6 +311,7 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
   constexpr int STRIP_THREADS = strip_threads(PF, NP);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int K = m.K, V = m.V, KT = m.kt;
+  const int LDB = uniform(m.ldb);              // beta's row stride (>= V)
   int tid = threadIdx.x;
   const int lane = tid & 63, wave = uniform(tid >> 6);
   constexpr int RT = BM / 16;
@@ -339,7 +340,7 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
   const int arow = (lane & 15) * KS + g2;
   // beta [K, V] as a buffer resource of K V floats (K V < 2^29 checked by the launcher)
   const __amdgpu_buffer_rsrc_t bres =
-      __builtin_amdgcn_make_buffer_rsrc((void*)m.beta, 0, K * V * 4, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)m.beta, 0, K * LDB * 4, 0x00020000);
   // A strip's beta block into registers: buffer loads with ONE per-lane offset (row g2,
   // column) stepped by 8 rows per pair; rows k >= K lie past the resource's extent and
   // read as 0 (no clamps, no per-load address VGPRs).  Unconditional: a guarded load
@@ -347,7 +348,7 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
   // call so the offsets are recomputed here, not hoisted out of the loop and spilled.
   auto issue = [&](int st, float (&bb)[2 * NP], float& rm, float& rv) {
     const int vc = min((st >> 2) * VB + 16 * (st & 3) + (lane & 15), V - 1);
-    int v4 = V * 4;
+    int v4 = LDB * 4;
     asm volatile("" : "+s"(v4));
     int voff = g2 * v4 + vc * 4;
     const int v32 = 8 * v4;
@@ -404,7 +405,7 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
 #pragma unroll 1
   for (; s < nstrips; s += stride) {
     // PF = 2: the next strip's per-lane buffer offset (its pairs are loaded in the MFMA loop)
-    int voffn = 0, v4n = V * 4;
+    int voffn = 0, v4n = LDB * 4;
     if (PF == 1) {
       issue(min(s + stride, nstrips - 1), bn, rmn, rvn);   // (the last one re-reads a strip)
     } else if (PF == 2) {
@@ -818,7 +819,7 @@ __device__ __forceinline__ void prodlda_bwd_body(const GfkModel& m) {
 #pragma unroll
     for (int u = 0; u < BU; ++u) {
       const int k = min(kb + tid / VB + RPU * u, K - 1);
-      br[u] = m.beta[k * V + c];                 // 32-bit offsets (K V < 2^31)
+      br[u] = m.beta[k * m.ldb + c];             // 32-bit offsets (K ldb < 2^31)
     }
     if (!PRE) rsr = m.ws_col_rstd[c0 + (tid & (VB - 1))];
   };
@@ -839,7 +840,7 @@ __device__ __forceinline__ void prodlda_bwd_body(const GfkModel& m) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {   // unpredicated, clamped (no select on a pending load)
         const int k = min(kb + ks * 16 + (lane >> 4) * 4 + r, K - 1);
-        const float* p = m.beta + (size_t)k * V + c;
+        const float* p = m.beta + (size_t)k * m.ldb + c;
         bm_[u][r] = p[m.off_m];
         bv_[u][r] = p[m.off_v];
       }
@@ -851,7 +852,7 @@ __device__ __forceinline__ void prodlda_bwd_body(const GfkModel& m) {
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
       const int k = min(kb + tid / VB + RPU * u, K - 1);
-      const float* p = m.beta + (size_t)k * V + c;
+      const float* p = m.beta + (size_t)k * m.ldb + c;
       rm_[u] = p[m.off_m];
       rv_[u] = p[m.off_v];
     }
@@ -1072,7 +1073,7 @@ __device__ __forceinline__ void prodlda_bwd_body(const GfkModel& m) {
         for (int e = 0; e < 4; ++e) {
           const int k = kb + ks * 16 + (lane >> 4) * 4 + e;
           if (k >= K || c >= V) continue;
-          float* p = m.beta + (size_t)k * V + c;
+          float* p = m.beta + (size_t)k * m.ldb + c;
           if (!fused) {
             p[m.off_g] = np_[u][e];
           } else {
@@ -1111,13 +1112,13 @@ __device__ __forceinline__ void prodlda_bwd_body(const GfkModel& m) {
       // XOR swizzle is the same for all u); the row pointer advances by RPU rows
       const int cl = tid & (VB - 1), kl0 = tid / VB, c = c0 + cl;
       const int cs = cl ^ ((kl0 & 4) << 2);
-      float* p0 = m.beta + (size_t)(kb + kl0) * V + c;
+      float* p0 = m.beta + (size_t)(kb + kl0) * m.ldb + c;
 #pragma unroll
       for (int u = 0; u < RU; ++u) {
         const int kl = kl0 + RPU * u, k = kb + kl;
         if (kl >= 16 * nks || k >= K || c >= V) continue;
         const float g = zt[kl * VB + cs];
-        float* p = p0 + (size_t)(RPU * u) * V;
+        float* p = p0 + (size_t)(RPU * u) * m.ldb;
         if (!fused) {
           p[m.off_g] = g;
         } else {
@@ -1177,10 +1178,12 @@ __global__ void __launch_bounds__(512, 2) prodlda_bwd_pre2_kernel(GfkArgT<GB> ga
 // two workgroups per CU the chip moved ~3.8 TB/s (k200v112k_pre2_sparsewin_counters.md:
 // 41 % of wave cycles waiting on memory).  Here, per tile t:
 //   top      stage t's beta slice and dlogit tile (registers, loaded during tile t - 1) to LDS
-//            issue t's Adam m / v (consumed only by the epilogue, after the MFMAs), then
-//            tile t + nslab's beta slice and dlogit tile into the staging registers
+//            issue tile t + nslab's beta slice, dlogit tile and Adam m / v (the latter into
+//            the second of two m / v register sets: t's were loaded during tile t - 1)
 //   compute  d theta_d / dbeta MFMAs, the G tile, the Adam epilogue and stores
-// so every load is in flight during a compute phase, with 16 extra VGPRs (K = 200) and no
+// so every load has a whole tile of compute to arrive (g13 diagnostics: with t's m / v
+// issued at the top of tile t, their latency alone held the loop at 117 us without any
+// stores), with 32 extra VGPRs (K = 200) and no
 // LDS-DMA (whose pending copies make the compiler's vmcnt bookkeeping fall back to
 // vmcnt(0)): every wait is the compiler's own.  The dlogit tiles come dense ([B][64],
 // written so by prodlda_dlogit).  The 4 range workgroups of a slab sit on ONE XCD
@@ -1189,14 +1192,18 @@ __global__ void __launch_bounds__(512, 2) prodlda_bwd_pre2_kernel(GfkArgT<GB> ga
 // MFMA operands: both products reduce over a 64-long axis, and the reduction index of MFMA
 // step 4 q + j for lane group g is 16 q + 4 g + j (a bijection, the same for A and B), so a
 // lane's operands for 4 steps are ONE ds_read_b128 along a row.  Each operand therefore
-// lives in LDS with the reduction axis contiguous (row stride 68: 16-byte aligned, and
-// the 8 lanes of a b128 read phase hit distinct banks):
+// lives in LDS with the reduction axis contiguous (row stride 72 floats: 16-byte aligned,
+// and every 16-lane ds_read_b128 group of these reads hits distinct banks):
 //   d theta_d[b, k] = sum_c dt[b][c] bt[k][c]       (dt: [b][c], bt: [k][c])
 //   dbeta[k, c]    = sum_b thT[k][b] dtT[c][b]      (theta_d and dlogit staged transposed)
 // -- 8 b128 reads per 16 MFMAs, all issued ahead of them, instead of 16 ds_read2_b32 one
 // step ahead (whose LDS latency stalled every MFMA pair: s_waitcnt lgkmcnt(0) each).
-// LDS: thT, bt, dt, dtT: 4 x [64][68] floats (70 KB; the G tile aliases dtT).
-constexpr int LDP = 68;
+// dtT is written transposed from the row-major registers (16 lanes: one b, 16 c rows):
+// its columns are XORed with 4 ((c >> 2) & 7), which cuts those ds_write_b32 from 8-way to
+// 2-way bank conflicts and keeps the b128 reads conflict-free.
+// LDS: thT, bt, dt, dtT: 4 x [64][72] floats (74 KB; the G tile aliases dtT).
+constexpr int LDP = 72;
+__device__ __forceinline__ int dtt_swz(int c) { return ((c >> 2) & 7) << 2; }
 template <int BM, int MAXU, bool GB = false>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
 prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
@@ -1229,7 +1236,7 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
   float* thT = smem;                            // [64 k][LDP]   theta_d^T of the k range
   float* bt = thT + 64 * LDP;                   // [64 k][LDP]   beta slice
   float* dt = bt + 64 * LDP;                    // [64 b][LDP]   dlogit
-  float* dtT = dt + 64 * LDP;                   // [64 c][LDP]   dlogit^T (then the G tile)
+  float* dtT = dt + 64 * LDP;                   // [64 c][LDP ^ swz] dlogit^T (then the G tile)
   const int NB_T = nks * 4, NDT_T = (BM / 16) * nks;
   const bool fused = m.update_mode == 1 && !m.beta_split;
   const int nb = *m.ws_nb;
@@ -1242,7 +1249,7 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
     thT[c * LDP + b] = c < 16 * nks ? m.ws_thetad[(size_t)b * m.kt + kb + c] : 0.f;
   }
 
-  float br[RU], rm[RU], rv[RU];
+  float br[RU];
   f32x4 dr[DU];
   // element tid + NTH u of the block is (row tid / VB + RPU u, column tid % VB)
   auto issue_bd = [&](int tile) {             // beta slice + dlogit tile
@@ -1251,32 +1258,34 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
 #pragma unroll
     for (int j = 0; j < DU; ++j) dr[j] = d4[tid + NTH * j];
 #pragma unroll
-    for (int u = 0; u < RU; ++u) br[u] = m.beta[(size_t)min(kb + tid / VB + RPU * u, K - 1) * V + c];
+    for (int u = 0; u < RU; ++u) br[u] = m.beta[(size_t)min(kb + tid / VB + RPU * u, K - 1) * m.ldb + c];
   };
   // Adam state (gradient mode: beta itself, unused -- unconditional, like every load and
   // store of the tile loop, so the compiler's vmcnt bookkeeping stays exact across it)
   const int64_t om = fused ? m.off_m : 0, ov = fused ? m.off_v : 0;
-  auto issue_mv = [&](int tile) {
+  auto issue_mv = [&](int tile, float (&rm)[RU], float (&rv)[RU]) __attribute__((always_inline)) {
     const int c = min(tile * VB + (tid & (VB - 1)), V - 1);
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
-      const float* p = m.beta + (size_t)min(kb + tid / VB + RPU * u, K - 1) * V + c;
+      const float* p = m.beta + (size_t)min(kb + tid / VB + RPU * u, K - 1) * m.ldb + c;
       rm[u] = p[om];
       rv[u] = p[ov];
     }
   };
-  // out-of-range elements store into the slack behind the dense dlogit tiles (ws_dt holds
-  // [n_tiles][B][66] + 2048 floats; the dense layout uses [n_tiles][B][64]), which nothing
-  // reads
-  float* const sink = m.ws_dt + (size_t)n_tiles * BM * VB + (tid & 63);
-  // one 16 x 16 output subtile over the 64-long reduction: ar / br_ point at this lane's
-  // row (lane & 15) + 4 (lane >> 4); step 4 q + j takes reduction index 16 q + 4 g + j
-  auto mm64 = [&](const float* ar, const float* bq) {
+  // out-of-range elements store into this workgroup's 64-float slot behind the dense dlogit
+  // tiles (ws_dt holds [n_tiles][B][66] + 64 (grid + 32) floats; the dense layout uses
+  // [n_tiles][B][64]), which nothing reads.  One slot per workgroup: a sink shared by all
+  // of them would put every workgroup's stores on the same cache lines
+  float* const sink = m.ws_dt + (size_t)n_tiles * BM * VB + 64 * (size_t)blockIdx.x + (tid & 63);
+  // one 16 x 16 output subtile over the 64-long reduction: ar / bq point at this lane's
+  // operand rows, g4 = 4 (lane >> 4); step 4 q + j takes reduction index 16 q + 4 g + j
+  // (stored at column (16 q + g4) ^ bx in bq's row: the dtT swizzle)
+  auto mm64 = [&](const float* ar, const float* bq, int g4, int bx) {
     f32x4 a[4], b[4];
 #pragma unroll
     for (int qq = 0; qq < 4; ++qq) {
-      a[qq] = *reinterpret_cast<const f32x4*>(ar + 16 * qq);
-      b[qq] = *reinterpret_cast<const f32x4*>(bq + 16 * qq);
+      a[qq] = *reinterpret_cast<const f32x4*>(ar + 16 * qq + g4);
+      b[qq] = *reinterpret_cast<const f32x4*>(bq + ((16 * qq + g4) ^ bx));
     }
     f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -1293,16 +1302,19 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
 #pragma unroll
   for (int j = 0; j < NDT; ++j) dacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  float rm0[RU], rv0[RU], rm1[RU], rv1[RU];
   issue_bd(slab);
+  issue_mv(slab, rm0, rv0);
   // the loop's epilogue issues 3 RU stores after the next tile's loads; the same number of
   // sink stores here gives the loop entry that shape too, so the compiler's wait for the
   // staged registers is vmcnt(3 RU + ...) on both edges (else vmcnt(0) at every tile:
   // the previous tile's stores drained before staging)
-  // (distinct addresses, so the compiler cannot merge them; ws_dt has 2048 floats of slack)
+  // (addresses the compiler cannot prove equal, so it cannot merge them)
+  float* const wsink = sink - (tid & 63);
 #pragma unroll
-  for (int u = 0; u < 3 * RU; ++u) sink[64 * (u + 1)] = 0.f;
-#pragma unroll 1
-  for (int tile = slab; tile < n_tiles; tile += nslab) {
+  for (int u = 0; u < 3 * RU; ++u) wsink[(tid + 5 * u) & 63] = 0.f;
+  auto body = [&](int tile, float (&rm)[RU], float (&rv)[RU], float (&nm)[RU], float (&nv)[RU])
+      __attribute__((always_inline)) {
     const int c0 = tile * VB;
     asm volatile("" : "+v"(tid));
     __builtin_assume(tid >= 0 && tid < NTH);
@@ -1314,30 +1326,35 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
 #pragma unroll
       for (int u = 0; u < RU; ++u) {
         const int k = tid / VB + RPU * u;
-        if (k < 16 * nks) bt[k * LDP + c] = (kb + k < K && cok) ? br[u] : 0.f;
+        if (k < 16 * nks) bt[__mul24(k, LDP) + c] = (kb + k < K && cok) ? br[u] : 0.f;
       }
 #pragma unroll
       for (int j = 0; j < DU; ++j) {           // dense [BM][64] -> dt [b][c] and dtT [c][b]
         const int i = tid + NTH * j, r = i >> 4, c4 = (i & 15) * 4;
-        *reinterpret_cast<f32x4*>(dt + r * LDP + c4) = dr[j];
+        *reinterpret_cast<f32x4*>(dt + __mul24(r, LDP) + c4) = dr[j];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) dtT[(c4 + e) * LDP + r] = dr[j][e];
+        for (int e = 0; e < 4; ++e) dtT[__mul24(c4 + e, LDP) + (r ^ dtt_swz(c4 + e))] = dr[j][e];
       }
     }
-    // (the staging above consumed the registers; this tile's m / v first, then the next
-    // tile's beta / dlogit: the epilogue's wait for m / v leaves the latter in flight)
-    issue_mv(tile);
-    issue_bd(min(tile + nslab, n_tiles - 1));  // (last tile: a harmless reload)
+    // (the staging above consumed the registers) the next tile's beta / dlogit / m / v
+    {
+      const int tn = min(tile + nslab, n_tiles - 1);    // (last tile: a harmless reload)
+      issue_bd(tn);
+      issue_mv(tn, nm, nv);
+    }
     lds_barrier();
 
     const int r = lane & 15, g4 = 4 * (lane >> 4);
     // d theta_d[b, k] += sum_c dt[b][c] bt[k][c]
+#if GFK_DIAG_BWD == 1                          // (diagnostic builds: no MFMA phase)
+    if (nb < 0)
+#endif
 #pragma unroll
     for (int j = 0; j < NDT; ++j) {
       const int t = wave + NW * j;
       if (t >= NDT_T) break;
       const int rt = t / nks, ks = t % nks;
-      dacc[j] += mm64(dt + (rt * 16 + r) * LDP + g4, bt + (ks * 16 + r) * LDP + g4);
+      dacc[j] += mm64(dt + __mul24(rt * 16 + r, LDP), bt + __mul24(ks * 16 + r, LDP), g4, 0);
     }
     // dbeta[k, c] = sum_b thT[k][b] dtT[c][b]
     float gr[MU][4];
@@ -1345,8 +1362,13 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
     for (int u = 0; u < MU; ++u) {
       const int t = wave + NW * u;
       if (t >= NB_T) break;
+#if GFK_DIAG_BWD == 1
+      for (int e = 0; e < 4; ++e) gr[u][e] = 0.f;
+      continue;
+#endif
       const int ks = t >> 2, cst = t & 3;
-      const f32x4 a = mm64(thT + (ks * 16 + r) * LDP + g4, dtT + (cst * 16 + r) * LDP + g4);
+      const int cr = cst * 16 + r;
+      const f32x4 a = mm64(thT + __mul24(ks * 16 + r, LDP), dtT + __mul24(cr, LDP), g4, dtt_swz(cr));
 #pragma unroll
       for (int e = 0; e < 4; ++e) gr[u][e] = a[e];
     }
@@ -1360,28 +1382,51 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int kl = ks * 16 + (lane >> 4) * 4 + e;
-        gt[kl * VB + (cl ^ ((kl & 4) << 2))] = gr[u][e];
+        gt[__mul24(kl, VB) + (cl ^ ((kl & 4) << 2))] = gr[u][e];
       }
     }
     lds_barrier();
     // the G tile, row-wise: update (fused) or gradient
     const int cl = tid & (VB - 1), kl0 = tid / VB, c = c0 + cl;
     const int cs = cl ^ ((kl0 & 4) << 2);
-    float* p0 = m.beta + (size_t)(kb + kl0) * V + c;
+    float* p0 = m.beta + (size_t)(kb + kl0) * m.ldb + c;
+    // row pointers stepped by constants (folded into the ds_read offsets).  LDS index
+    // products are __mul24 throughout: a plain 32-bit multiply-add became v_mad_u64_u32,
+    // whose unused high addend half was a register with a load in flight, and the waitcnt
+    // pass then waited vmcnt(0) -- the previous tile's stores drained -- at every tile
+    const float* gtp = gt + __mul24(kl0, VB) + cs;
+    const float* btp = bt + __mul24(kl0, LDP) + cl;
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
       const int kl = kl0 + RPU * u, k = kb + kl;
       const bool ok = kl < 16 * nks && k < K && c < V;
-      const float gv = gt[kl * VB + cs];
-      float* p = p0 + (size_t)(RPU * u) * V;
+      const float gv = gtp[RPU * u * VB];
+      float* p = p0 + (size_t)(RPU * u) * m.ldb;
       float mo = rm[u], vo = rv[u];
-      float np = adam_update(bt[kl * LDP + cl], gv, mo, vo, ac);
+      float np = adam_update(btp[RPU * u * LDP], gv, mo, vo, ac);
       if (beta_shared && m.fed_scale_on) np *= m.fed_scale;
       // fused: m, v, beta; gradient mode: the gradient (+ two sink stores)
+#if GFK_DIAG_BWD == 2                          // (diagnostic builds: no stores)
+      if (np == 1234.5f)
+#endif
       *(ok ? p + (fused ? m.off_m : m.off_g) : sink) = fused ? mo : gv;
+#if GFK_DIAG_BWD == 2
+      if (np == 1234.5f)
+#endif
       *(ok && fused ? p + m.off_v : sink) = vo;
+#if GFK_DIAG_BWD == 2
+      if (np == 1234.5f)
+#endif
       *(ok && fused ? p : sink) = np;
     }
+  };
+#pragma unroll 1
+  for (int tile = slab; tile < n_tiles;) {
+    body(tile, rm0, rv0, rm1, rv1);
+    tile += nslab;
+    if (tile >= n_tiles) break;
+    body(tile, rm1, rv1, rm0, rv0);
+    tile += nslab;
   }
   // this workgroup's d theta_d partial (plain stores; row_bwd sums the slabs in order)
   float* dpart = m.ws_dthetad + (size_t)slab * m.bmax * K;
@@ -1429,7 +1474,7 @@ __host__ __device__ inline int bwd_kq(const GfkModel& m) {
 
 static size_t bwd_smem(const GfkModel* m, int kq) {
   const size_t KPQ = bwd_kpq(m->K, kq), B = m->bmax;
-  if (kq == 4 && bwd_pipe(*m)) return sizeof(float) * 4 * 64 * 68;   // thT, bt, dt, dtT
+  if (kq == 4 && bwd_pipe(*m)) return sizeof(float) * 4 * 64 * 72;   // thT, bt, dt, dtT
   if (kq == 4 && m->bwd_pre && B <= 64)       // th [B][64] + bt + dt (G aliases dt)
     return sizeof(float) * (B * 64 + KPQ * LDB_B + B * LDD);
   const size_t KTQ = kq == 1 ? (size_t)m->kt : (size_t)kt_stride((int)KPQ);
@@ -1446,7 +1491,7 @@ extern "C" int gfk_launch_prodlda_fwd(const GfkModel* m, hipStream_t s) {
     // fp32, B <= 64, K <= 256; the partial slots need 4 * grid <= 4 * n_tiles
     const int np = strip_np(m->K);
     if (m->mm_bf16 || m->bmax > 64 || m->K > 256 || m->dec_grid > m->n_tiles ||
-        (int64_t)m->K * m->V >= (1LL << 29)) return -1;
+        (int64_t)m->K * m->ldb >= (1LL << 29)) return -1;
 #define GFK_FWS(BM, NP)                                                                        \
     do {                                                                                       \
       if (m->stage_flags & FWD_STRIP_ROLL)                                                     \

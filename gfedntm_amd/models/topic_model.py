@@ -186,9 +186,15 @@ class TopicModelBase:
 
     def _build_engine(self):
         transposed = TRANSPOSED_KEYS if self.backend == "fused" else ()
+        padded = {}
+        if self.backend == "fused":
+            from ..ops.engine import BETA_PAD, BETA_PAD_MIN_V
+            if self.input_size >= BETA_PAD_MIN_V:
+                padded = {"beta": BETA_PAD}        # beta rows on 128-B lines (utils/flat.py)
         self.flat = FlatState(self.model, self.shared_keys, transposed=transposed,
                               device=self.device,
-                              shared_last=("beta",) if self.backend == "fused" else ())
+                              shared_last=("beta",) if self.backend == "fused" else (),
+                              padded=padded)
         if self.backend == "fused":
             from ..ops.engine import FusedEngine
             self.engine = FusedEngine(self)

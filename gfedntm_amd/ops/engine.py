@@ -39,7 +39,7 @@ import torch
 
 from ..data.bow import BatchPlan, DeviceCSR
 from ..models.engine import EngineBase
-from ..utils.flat import ALIGN
+from ..utils.flat import ALIGN, slot_view
 from ..utils.misc import graph_capture
 from . import kernel_abi as abi
 from . import native
@@ -103,10 +103,22 @@ def theta_stride(K: int) -> int:
     return kt + 2 if (kt // 2) % 2 == 0 else kt
 
 
+# beta rows padded to 128-B lines from this vocabulary size on (utils/flat.py): the large-V
+# kernels' 64-column RMW tiles then never split a cache line with another tile
+BETA_PAD_MIN_V = 8192
+BETA_PAD = 32
+
+
+def beta_ld(V: int) -> int:
+    """beta's row stride in the fused engine's flat layout."""
+    return -(-V // BETA_PAD) * BETA_PAD if V >= BETA_PAD_MIN_V else V
+
+
 def _shape_model(tm, bmax: int) -> "abi.GfkModel":
     m = abi.GfkModel()
     hs = list(tm.hidden_sizes)
     m.bmax, m.V, m.K, m.n_hidden = bmax, tm.input_size, tm.n_components, len(hs)
+    m.ldb = beta_ld(m.V)
     for i, h in enumerate(hs):
         m.H[i] = h
     m.kind = abi.KIND_PRODLDA if tm.model_type.lower() == "prodlda" else abi.KIND_LDA
@@ -137,6 +149,7 @@ def lds_required(tm, bmax: int) -> int:
     m = abi.GfkModel()
     hs = list(tm.hidden_sizes)
     m.bmax, m.V, m.K, m.n_hidden = bmax, tm.input_size, tm.n_components, len(hs)
+    m.ldb = beta_ld(m.V)
     for i, h in enumerate(hs):
         m.H[i] = h
     m.kind = abi.KIND_PRODLDA if tm.model_type.lower() == "prodlda" else abi.KIND_LDA
@@ -311,11 +324,7 @@ class FusedEngine(EngineBase):
     # ------------------------------------------------------------------ layout
     def view_like(self, buf: torch.Tensor, key: str) -> torch.Tensor:
         """The slot of ``key`` inside another flat-layout buffer (grad, m, v)."""
-        s = self.flat.slots[key]
-        flat = buf[s.offset: s.offset + s.numel]
-        if s.transposed:
-            return flat.view(s.shape[1], s.shape[0]).t()
-        return flat.view(s.shape)
+        return slot_view(buf, self.flat.slots[key])
 
     def gradient(self, key: str) -> torch.Tensor:
         """The pending gradient of parameter ``key`` (gradient mode, before Adam
@@ -354,6 +363,9 @@ class FusedEngine(EngineBase):
         net = model.inf_net
         hs = list(tm.hidden_sizes)
         m.bmax, m.V, m.K, m.n_hidden = self.bmax, tm.input_size, tm.n_components, len(hs)
+        # beta's row stride (a padded slot: rows start on 128-B lines, utils/flat.py)
+        bs = self.flat.slots.get("beta")
+        m.ldb = int(bs.ld or bs.shape[1]) if bs is not None else int(m.V)
         for i, h in enumerate(hs):
             m.H[i] = h
         m.act = abi.ACT_CODES[tm.activation]
@@ -457,7 +469,7 @@ class FusedEngine(EngineBase):
             # vs 0.0589 ms, K=50 V=28k 0.092 vs 0.101, K=200 V=112k 0.342 vs 0.349, CTM /
             # ZeroShotTM K=100 neutral.  GFEDNTM_FWD_STRIP=0 selects the tile kernel
             strip = os.environ.get("GFEDNTM_FWD_STRIP", "auto")
-            fits = (not m.mm_bf16 and m.bmax <= 64 and m.K <= 256 and m.K * m.V < (1 << 29))
+            fits = (not m.mm_bf16 and m.bmax <= 64 and m.K <= 256 and m.K * m.ldb < (1 << 29))
             if fits and strip in ("1", "auto"):
                 m.stage_flags |= STAGE_FWD_STRIP
                 # the 8-wave variant that prefetches the next strip's beta block (2 waves
@@ -605,8 +617,8 @@ class FusedEngine(EngineBase):
             "actx": f(m.n_tiles * B * 64 if m.ctx_fused == 1 else 1),
             "hpart": f(m.n_tiles * B * hs[0] if m.ctx_fused == 1 else 1),
             # precomputed logit-gradient tiles [n_tiles][B][66] (bwd_pre; + the pipelined
-            # backward's store sink)
-            "dt": f(m.n_tiles * B * 66 + 2048 if m.bwd_pre else 1),
+            # backward's store sinks, 64 floats per workgroup)
+            "dt": f(m.n_tiles * B * 66 + 64 * (4 * m.n_dpart + 32) if m.bwd_pre else 1),
         }
         Lb = max(int(m.L), 1)
         ws.update(lab=f(B, Lb), dlab=f(B, Lb), ce=f(B), thd=f(B, K))   # label head
@@ -969,9 +981,7 @@ class FusedEngine(EngineBase):
         self._ctx = c
 
     def raw_like(self, buf: torch.Tensor, key: str) -> torch.Tensor:
-        s = self.flat.slots[key]
-        flat = buf[s.offset: s.offset + s.numel]
-        return flat.view(s.shape[1], s.shape[0]) if s.transposed else flat.view(s.shape)
+        return slot_view(buf, self.flat.slots[key], storage=True)
 
     def _ctx_fwd(self):
         c, ws = self._ctx, self.ws
@@ -1221,7 +1231,7 @@ class FusedEngine(EngineBase):
 
 # the GfkModel fields that fix a launch's grid, block and LDS: engines batched into one
 # launch per phase must agree on all of them (their pointers and per-client values differ)
-_BATCH_SHAPE_FIELDS = ("bmax", "V", "K", "n_hidden", "act", "kind", "input", "C", "L", "vb",
+_BATCH_SHAPE_FIELDS = ("bmax", "V", "ldb", "K", "n_hidden", "act", "kind", "input", "C", "L", "vb",
                        "n_tiles", "dec_grid", "learn_priors", "stage_flags", "kt", "n_dpart",
                        "beta_split", "update_mode", "ctx_fused", "ctx_kb", "ctx_ckb", "mm_bf16",
                        "lab_on", "lab_off", "lab_in_enc", "bwd_pre")

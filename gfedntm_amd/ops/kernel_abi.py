@@ -103,7 +103,7 @@ class GfkModel(C.Structure):
         ("lab_on", C.c_int32), ("lab_off", C.c_int32), ("labels", P), ("w_cls", P), ("b_cls", P),
         ("ws_lab", P), ("ws_dlab", P), ("ws_ce", P), ("ws_thd", P),
         ("lab_in_enc", C.c_int32), ("bwd_pre", C.c_int32), ("ws_dt", P),
-        ("dev", P), ("dev_upd", P), ("n_batch", C.c_int32), ("pad4", C.c_int32),
+        ("dev", P), ("dev_upd", P), ("n_batch", C.c_int32), ("ldb", C.c_int32),
     ]
 
 

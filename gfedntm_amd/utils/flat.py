@@ -18,6 +18,15 @@ starts at a multiple of 16 floats (64 B) so kernels can use 16-B vector loads.
 ``inf_net.input_layer.weight`` is [H0, V] in PyTorch but the sparse encoder
 gathers one *column* per non-zero token, so it is stored as [V, H0] and the
 module sees the ``.t()`` view.
+
+``padded`` maps 2-D weights to a row-stride multiple: ``{"beta": 32}`` stores the
+[K, V] topic-word matrix with rows of ``round_up(V, 32)`` floats (128 B), so every row
+starts on a cache line.  The fused large-vocabulary kernels read-modify-write beta, Adam
+m and v in 64-column tiles; with rows of V = 112 027 floats each tile row straddles
+three cache lines and the same RMW stream ran at 3.4 instead of 5.0 TB/s
+(``profiles/r3/adam_rmw_alignment.jsonl``).  The module sees the [K, V] slice of the
+padded [K, ld] storage (a strided view); the pad columns are zero and stay zero (zero
+gradients, Adam steps of zero, FedAvg of zeros).
 """
 from __future__ import annotations
 
@@ -35,9 +44,24 @@ class Slot:
     key: str
     offset: int
     shape: Tuple[int, ...]
-    numel: int
+    numel: int                  # storage floats (rows x ld for a padded slot)
     transposed: bool
     is_param: bool
+    ld: int = 0                 # storage row stride of a padded 2-D slot (0: unpadded)
+
+
+def slot_view(buf: torch.Tensor, s: Slot, storage: bool = False) -> torch.Tensor:
+    """The tensor of slot ``s`` inside a flat-layout buffer: the module-shaped view, or
+    with ``storage`` the contiguous storage-order one ([in, out] for a transposed weight,
+    [rows, ld] for a padded one)."""
+    flat = buf[s.offset: s.offset + s.numel]
+    if s.transposed:
+        t = flat.view(s.shape[1], s.shape[0])
+        return t if storage else t.t()
+    if s.ld:
+        t = flat.view(s.shape[0], s.ld)
+        return t if storage else t[:, : s.shape[1]]
+    return flat.view(s.shape)
 
 
 def _resolve(module: nn.Module, key: str):
@@ -50,7 +74,8 @@ def _resolve(module: nn.Module, key: str):
 
 class FlatState:
     def __init__(self, model: nn.Module, shared_keys: Sequence[str] = (),
-                 transposed: Iterable[str] = (), device=None, shared_last: Sequence[str] = ()):
+                 transposed: Iterable[str] = (), device=None, shared_last: Sequence[str] = (),
+                 padded: Optional[Dict[str, int]] = None):
         self.model = model
         sd = model.state_dict(keep_vars=True)
         params = dict(model.named_parameters())
@@ -63,12 +88,18 @@ class FlatState:
         self.transposed = set(transposed)
         self.slots: Dict[str, Slot] = {}
         off = 0
+        padded = padded or {}
         for k in shared + rest:
             t = sd[k]
             off = -(-off // ALIGN) * ALIGN
-            self.slots[k] = Slot(k, off, tuple(t.shape), t.numel(), k in self.transposed,
-                                 k in params)
-            off += t.numel()
+            ld, numel = 0, t.numel()
+            if k in padded and t.dim() == 2 and k not in self.transposed:
+                ld = -(-t.shape[1] // padded[k]) * padded[k]
+                off = -(-off // padded[k]) * padded[k]      # rows aligned as well
+                numel = t.shape[0] * ld
+            self.slots[k] = Slot(k, off, tuple(t.shape), numel, k in self.transposed,
+                                 k in params, ld)
+            off += numel
         last_shared = self.slots[shared[-1]] if shared else None
         self.n_shared = 0 if last_shared is None else last_shared.offset + last_shared.numel
         self.n_total = -(-off // ALIGN) * ALIGN
@@ -88,29 +119,20 @@ class FlatState:
                 owner._buffers[leaf] = view
 
     def view(self, key: str) -> torch.Tensor:
-        s = self.slots[key]
-        flat = self.buffer[s.offset: s.offset + s.numel]
-        if s.transposed:
-            return flat.view(s.shape[1], s.shape[0]).t()
-        return flat.view(s.shape)
+        return slot_view(self.buffer, self.slots[key])
 
     def view_like(self, buf: torch.Tensor, key: str) -> torch.Tensor:
         """The slot of ``key`` inside another buffer with this layout (gradients)."""
-        s = self.slots[key]
-        flat = buf[s.offset: s.offset + s.numel]
-        if s.transposed:
-            return flat.view(s.shape[1], s.shape[0]).t()
-        return flat.view(s.shape)
+        return slot_view(buf, self.slots[key])
 
     def shared_buffer_slots(self) -> List[Slot]:
         """Shared float tensors that are not parameters (batch-norm running stats)."""
         return [self.slots[k] for k in self.shared_keys if not self.slots[k].is_param]
 
     def raw(self, key: str) -> torch.Tensor:
-        """Storage-order (contiguous) view: [in, out] for transposed weights."""
-        s = self.slots[key]
-        flat = self.buffer[s.offset: s.offset + s.numel]
-        return flat.view(s.shape[1], s.shape[0]) if s.transposed else flat.view(s.shape)
+        """Storage-order (contiguous) view: [in, out] for transposed weights, [rows, ld]
+        for padded ones."""
+        return slot_view(self.buffer, self.slots[key], storage=True)
 
     @property
     def shared(self) -> torch.Tensor:

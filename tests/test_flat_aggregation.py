@@ -36,6 +36,34 @@ def test_flat_views_and_shared_prefix():
     assert torch.equal(m.beta, 2 * before["beta"])
 
 
+def test_padded_beta_rows():
+    """beta stored with 128-B rows ({"beta": 32}): the module sees the [K, V] slice, the
+    state_dict / load_state_dict round trip is exact, the pad columns are zero and in the
+    slot's storage (param ranges, FedAvg prefix), and rows start on 32-float boundaries."""
+    m = _net()                                   # beta [5, 60] -> rows of 64 floats
+    before = {k: v.clone() for k, v in m.state_dict().items()}
+    fs = FlatState(m, ["beta", "prior_mean"], padded={"beta": 32}, shared_last=("beta",))
+    s = fs.slots["beta"]
+    assert s.ld == 64 and s.numel == 5 * 64 and s.offset % 32 == 0
+    assert m.beta.shape == (5, 60) and m.beta.stride() == (64, 1)
+    assert m.beta.data_ptr() == fs.buffer[s.offset:].data_ptr()
+    for k, v in m.state_dict().items():
+        assert torch.equal(v, before[k]), k
+    raw = fs.raw("beta")
+    assert raw.shape == (5, 64) and torch.count_nonzero(raw[:, 60:]) == 0
+    # FedAvg prefix ends with beta's padded storage
+    assert fs.n_shared == s.offset + s.numel
+    assert any(a <= s.offset and s.offset + s.numel <= b for a, b in fs.param_ranges())
+    # a write through the module lands in the strided slot; load_state_dict round trip
+    with torch.no_grad():
+        m.beta.add_(1.0)
+    assert torch.equal(raw[:, :60], before["beta"] + 1) and torch.count_nonzero(raw[:, 60:]) == 0
+    m.load_state_dict(before)
+    assert torch.equal(m.beta, before["beta"])
+    g = torch.zeros_like(fs.buffer)
+    assert fs.view_like(g, "beta").shape == (5, 60)
+
+
 def test_fedavg_golden():
     rng = np.random.default_rng(0)
     n = [120, 80, 200]

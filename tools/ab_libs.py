@@ -46,7 +46,9 @@ def main(argv):
             objs.append(obj)
             flags = KFLAGS if os.environ.get("AB_FLAGS", "new") == "new" else \
                 ["-O3", "-fPIC", "-std=c++17", "-munsafe-fp-atomics", "-Wno-unused-result"]
-            jobs.append([HIPCC, f"--offload-arch={ARCH}"] + flags + ["-c", src, "-o", obj])
+            # AB_DEFS: extra -D definitions (diagnostic variants, e.g. "GFK_DIAG_BWD=1")
+            defs = ["-D" + d for d in os.environ.get("AB_DEFS", "").split()]
+            jobs.append([HIPCC, f"--offload-arch={ARCH}"] + flags + defs + ["-c", src, "-o", obj])
         with cf.ThreadPoolExecutor(8) as ex:
             for r in ex.map(lambda c: subprocess.run(c, capture_output=True, text=True), jobs):
                 if r.returncode:

@@ -10,8 +10,8 @@ r inplace112 --gpus 2 --topics 200 --vocab 150000 --docs 1500 --steps 100 --warm
 GFEDNTM_XGMI_INPLACE_MB=100000 r staged112b --gpus 2 --topics 200 --vocab 150000 --docs 1500 --steps 100 --warmup 10 || exit $?
 r inplace112b --gpus 2 --topics 200 --vocab 150000 --docs 1500 --steps 100 --warmup 10 || exit $?
 r multi2x4 --gpus 2 --clients-per-gpu 4 --steps 200 --warmup 20 || exit $?
-# CombinedTM K=100 V=112k over 2 ranks: the ~450 MB shared state's attach (in place)
-r ctm112x2 --gpus 2 --family ctm --topics 100 --vocab 150000 --docs 1500 --steps 40 --warmup 5 || exit $?
+# CombinedTM K=100 V=99k over 2 ranks: the ~400 MB shared state's attach (in place)
+r ctm99x2 --gpus 2 --family ctm --topics 100 --vocab 150000 --docs 1500 --steps 40 --warmup 5 || exit $?
 # per-rank kernel traces (each rank its own rocprofv3 process; no launcher re-exec):
 # staged vs in-place xGMI all-reduce kernels at K=200 / V=112k
 export TMPDIR=/tmp

@@ -83,6 +83,33 @@ __global__ void __launch_bounds__(512) rmw_rows4(float* p, float* m, float* v, i
   }
 }
 
+// rows1: the pipelined prodlda backward's pattern -- one dword per lane along a row (a wave
+// instruction: one row x 256 B), 8 rows per thread, quarter-K ranges, 512 threads
+__global__ void __launch_bounds__(512) rmw_rows1(float* p, float* m, float* v, int K, int V,
+                                                 int n_tiles) {
+  const int tid = threadIdx.x;
+  const int q = blockIdx.x % 4, slab = blockIdx.x / 4, nslab = gridDim.x / 4;
+  const int ksub = (K + 15) / 16, ks0 = q * ksub / 4, nks = (q + 1) * ksub / 4 - ks0;
+  const int k0 = 16 * ks0, nk = min(16 * nks, K - k0);
+  for (int tile = slab; tile < n_tiles; tile += nslab) {
+    const int c = min(tile * 64 + (tid & 63), V - 1);
+    float pp[8], mm[8], vv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const size_t o = (size_t)(k0 + min(tid / 64 + 8 * u, nk - 1)) * V + c;
+      pp[u] = p[o]; mm[u] = m[o]; vv[u] = v[o];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int kr = tid / 64 + 8 * u;
+      if (kr >= nk || tile * 64 + (tid & 63) >= V) continue;
+      const size_t o = (size_t)(k0 + kr) * V + c;
+      const float np = upd(pp[u], mm[u], vv[u]);
+      p[o] = np; m[o] = mm[u]; v[o] = vv[u];
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256) rmw_flat4(float4* p, float4* m, float4* v, long n4) {
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
     float4 a = p[i], b = m[i], d = v[i];
@@ -98,6 +125,7 @@ extern "C" int launch(int which, float* p, float* m, float* v, int K, int V, int
   const int n_tiles = (V + 63) / 64;
   if (which == 0) hipLaunchKernelGGL(rmw_mfma, dim3(grid), dim3(512), 0, s, p, m, v, K, V, n_tiles);
   else if (which == 1) hipLaunchKernelGGL(rmw_rows4, dim3(grid), dim3(512), 0, s, p, m, v, K, V, n_tiles);
+  else if (which == 3) hipLaunchKernelGGL(rmw_rows1, dim3(grid), dim3(512), 0, s, p, m, v, K, V, n_tiles);
   else hipLaunchKernelGGL(rmw_flat4, dim3(grid), dim3(256), 0, s, (float4*)p, (float4*)m, (float4*)v,
                           (long)K * V / 4);
   return (int)hipGetLastError();
