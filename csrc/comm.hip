@@ -87,6 +87,13 @@ __device__ __forceinline__ float4 add4(float4 a, float4 b) {
 }
 
 // All storing waves drained, then one lane per destination rank raises the flag.
+// The flag goes through this rank's IPC mapping of the peer's flag array, which may be
+// cached in this XCD's L2 (same-device mappings of coarse-grained memory are; a peer GPU's
+// lines may be too): the store is followed by an L2 write-back, so the flag reaches
+// memory now and not at the next write-back of this L2.  Without it a 2-rank rehearsal
+// on one GPU intermittently left a rank spinning to the wait bound (g9 / g16 / g17: error
+// 2 on one rank, every epoch and flag correct once the other kernel's end-of-kernel
+// release had written its L2 back).
 __device__ __forceinline__ void publish(const GfkComm& c, int phase, int b, uint32_t e) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -96,6 +103,8 @@ __device__ __forceinline__ void publish(const GfkComm& c, int phase, int b, uint
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_store(c.flags[t] + ((size_t)phase * c.nblk + b) * CMAX + c.rank, e,
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   }
 }
 
@@ -341,6 +350,16 @@ extern "C" int gfk_comm_error(const GfkComm* c) {
   int32_t v = 0;
   if (hipMemcpy(&v, c->err, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) return -1;
   return v;
+}
+
+// Diagnostics: this rank's per-workgroup epochs [nblk] and its own flag array
+// [phases][nblk][CMAX] (what the peers published to it), copied to host; synchronous.
+extern "C" int gfk_comm_dump(const GfkComm* c, uint32_t* epoch, uint32_t* flags, int phases) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpy(epoch, c->epoch, sizeof(uint32_t) * c->nblk, hipMemcpyDeviceToHost) != hipSuccess) return -2;
+  const size_t fb = sizeof(uint32_t) * (size_t)phases * c->nblk * CMAX;
+  if (hipMemcpy(flags, c->flags[c->rank], fb, hipMemcpyDeviceToHost) != hipSuccess) return -3;
+  return 0;
 }
 
 // The error word copied to (pinned) host memory behind the stream's work: the runner polls

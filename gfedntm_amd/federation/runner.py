@@ -474,6 +474,8 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
         flag = torch.tensor([int(err)], dtype=torch.int64)
         dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=ctrl)
         if int(flag.item()):
+            if os.environ.get("GFEDNTM_COMM_DEBUG") == "1" and in_step is not None:
+                logger.warning("rank %d xGMI state: %s", rank, tm.engine.fedavg_debug())
             raise CommError(f"rank {rank}: an xGMI all-reduce wait timed out before {where} "
                             f"(error {int(flag.item())}); the shared state is invalid -- "
                             "resume from the last round checkpoint")
@@ -501,6 +503,10 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
         dist.barrier(group=ctrl)
 
     dist.barrier(group=ctrl)
+    # GFEDNTM_COMM_DEBUG=1: the first rounds synchronised one by one, with their times and
+    # the xGMI error word (which round a timed-out wait happened in, and the ranks' skew)
+    debug_comm = os.environ.get("GFEDNTM_COMM_DEBUG") == "1" and in_step is not None
+    t_dbg0 = time.perf_counter()
     win = RoundWindow(sync)
     # device time of the timed rounds: events on the round stream around them (the host
     # wall clock below brackets the same rounds with a sync + barrier)
@@ -514,6 +520,12 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
             if hb is not None:
                 hb.mark(it, 0)
             client.local_step(it)
+            if debug_comm and it < start + 16:
+                t_dbg = time.perf_counter()
+                sync()
+                logger.warning("rank %d round %d: enqueued at %.3f s, done at %.3f s, xGMI "
+                               "error %d", rank, it, t_dbg - t_dbg0, time.perf_counter() - t_dbg0,
+                               tm.engine.fedavg_error() if in_step is not None else 0)
             if hb is not None:
                 hb.mark(it, 1)
             if agg_mode == "grads":

@@ -900,6 +900,14 @@ class FusedEngine(EngineBase):
                 err = err or self._comm[k][0].xgmi.error()
         return err
 
+    def fedavg_debug(self) -> dict:
+        """Per-part diagnostics of the xGMI all-reduces (epochs, lagging flags)."""
+        out = {}
+        for k in ("rest", "beta"):
+            if self._comm is not None and k in self._comm and self._comm[k][0].xgmi is not None:
+                out[k] = self._comm[k][0].xgmi.debug_state()
+        return out
+
     def fedavg_error_async(self):
         """Start a non-blocking read of the xGMI error words (behind the enqueued rounds);
         :meth:`fedavg_error_poll` returns it once the copies have landed."""

@@ -55,6 +55,7 @@ def _declare(lib):
     lib.gfk_comm_launch.argtypes = [C.POINTER(GfkComm), P, P]
     lib.gfk_comm_error.argtypes = [C.POINTER(GfkComm)]
     lib.gfk_comm_error_async.argtypes = [C.POINTER(GfkComm), P, P]
+    lib.gfk_comm_dump.argtypes = [C.POINTER(GfkComm), P, P, C.c_int]
     if lib.gfk_comm_struct_size() != C.sizeof(GfkComm):
         raise RuntimeError("GfkComm ABI mismatch between csrc/comm.hip and xgmi.py")
     lib._gfk_comm_declared = True
@@ -179,6 +180,24 @@ class XgmiAllReduce:
         """Non-zero once a bounded wait timed out (results since are invalid)."""
         torch.cuda.synchronize(self.device)
         return int(self.lib.gfk_comm_error(C.byref(self.c)))
+
+    def debug_state(self) -> dict:
+        """Diagnostics after a timed-out wait: this rank's per-workgroup epochs and the
+        epochs its peers published into its flag rows, per phase (synchronises)."""
+        import numpy as np
+        phases = 3 if self.c.inplace else 2
+        ep = np.zeros(self.nblk, np.uint32)
+        fl = np.zeros((phases, self.nblk, CMAX), np.uint32)
+        rc = self.lib.gfk_comm_dump(C.byref(self.c), P(ep.ctypes.data), P(fl.ctypes.data), phases)
+        if rc:
+            return {"error": rc}
+        fl = fl[:, :, : self.world]
+        lag = {ph: sorted({(int(b), int(r), int(fl[ph, b, r])) for b in range(self.nblk)
+                           for r in range(self.world) if fl[ph, b, r] != ep[b]})[:8]
+               for ph in range(phases)}
+        return {"rank": self.rank, "nblk": self.nblk, "epoch_min": int(ep.min()),
+                "epoch_max": int(ep.max()), "err": self.lib.gfk_comm_error(C.byref(self.c)),
+                "flags_not_at_epoch(b, rank, flag)": lag}
 
     def _probe(self, rank: int, r: int) -> torch.Tensor:
         """Rank ``rank``'s validation input of round ``r``: a seeded device draw, so every

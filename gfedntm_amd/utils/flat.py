@@ -12,7 +12,9 @@ are untouched.
 Layout: tensors listed in ``shared`` (the ``grads_to_share`` keys present in
 the model) come first, in state_dict order, so the collective covers one
 prefix ``flat[:n_shared]``; the remaining float tensors follow.  Every tensor
-starts at a multiple of 16 floats (64 B) so kernels can use 16-B vector loads.
+starts at a multiple of 32 floats (128 B, a cache line): kernels use 16-B vector loads,
+and the large-vocabulary update kernels' tile blocks (64 words of W_in, rows of
+adapt_bert) then start on a line.
 
 ``transposed`` names 2-D weights stored column-major ([in, out] row-major):
 ``inf_net.input_layer.weight`` is [H0, V] in PyTorch but the sparse encoder
@@ -36,7 +38,7 @@ from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 import torch
 from torch import nn
 
-ALIGN = 16
+ALIGN = 32
 
 
 @dataclasses.dataclass
