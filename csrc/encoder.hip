@@ -132,13 +132,24 @@ extern "C" size_t gfk_enc_in_smem(const GfkModel* m) {
 }
 
 // out[j] = sum_i W[j][i] x[i] (+ bias) for j < n_out: 16 lanes (one DPP row) per
-// output split the inputs, 64 outputs per pass of the workgroup.
+// output split the inputs, 64 outputs per pass of the workgroup.  A ds_read_b32 is
+// banked per 32-lane half-wave, whose two 16-lane rows read 16 consecutive words of two
+// weight rows: rows j and j + 1 (n_in = 50 words apart) shared banks (11 % LDS conflict
+// cycles, k50_counters.md).  The half-wave's second row is j + d instead, with
+// d n_in = 16 (mod 32) -- d = 16 / (the largest power of two dividing n_in, <= 16) --
+// so the two rows cover all 32 banks once; (P, g) -> (P / d) 2d + P % d + g d maps the
+// 32 half-waves x 2 rows onto the pass's 64 outputs one to one.  Each output's sum is
+// the same sequence of operations as before (only which lanes compute it changed).
 template <class Epi>
 __device__ __forceinline__ void rowvec_gemv(const float* W, const float* x, int n_out, int n_in, int tid,
                                             Epi epi) {
   const int s = tid & 15;
+  const int tz = n_in & -n_in;                          // lowest set bit of n_in
+  const int ld = tz >= 16 ? 0 : 4 - __builtin_ctz(tz);  // log2 d
+  const int P = tid >> 5, g = (tid >> 4) & 1;
+  const int jo = ((P >> ld) << (ld + 1)) + (P & ((1 << ld) - 1)) + (g << ld);
   for (int j0 = 0; j0 < n_out; j0 += ENC_THREADS / 16) {
-    const int j = j0 + (tid >> 4);
+    const int j = j0 + jo;
     float acc = 0.f;
     if (j < n_out) {
       const float* wr = W + (size_t)j * n_in;

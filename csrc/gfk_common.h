@@ -170,7 +170,16 @@ typedef struct GfkModel {
   // beta's row stride in floats (>= V: the flat layout pads beta's rows to 128-B lines at
   // large V, utils/flat.py); m / v / the gradient share it
   int32_t ldb;
+  int32_t pad3;
+  // ---- split W_in update (stage_flags bit 7, GFK_WIN_SPLIT): prepare_next_batch stamps
+  // every word of the next batch with a fresh generation (ws_wstamp[V], ws_wgen[1]); the
+  // words NOT in the batch get their zero-gradient Adam step from gfk_win_dense_k on a side
+  // stream while the decoder runs, and the sparse W_in tiles update only the batch's words
+  int32_t* ws_wstamp;
+  int32_t* ws_wgen;
 } GfkModel;
+
+constexpr int GFK_WIN_SPLIT = 128;
 
 // launch helpers: grid z = the batched models, the kernel argument = the device array
 __host__ inline dim3 gfk_grid(dim3 g, const GfkModel* m) {
@@ -439,15 +448,33 @@ __device__ __forceinline__ AdamCoef adam_coef(const GfkModel& m) {
   return c;
 }
 
+// One optimizer step's advance of the running powers and the bias-correction coefficients
+// (post_fwd; and gfk_win_dense_k from prepare_next_batch's snapshot of the powers, which
+// must produce the same bits: contraction off, every operation explicit).
+__device__ __forceinline__ void adam_advance(const GfkModel& m, double pw0, double pw1, double& p1,
+                                             double& p2, float& c0, float& c1) {
+#pragma clang fp contract(off)
+  p1 = pw0 * (double)m.beta1;
+  p2 = pw1 * (double)m.beta2;
+  c0 = (float)((double)m.lr / (1.0 - p1));
+  c1 = (float)(1.0 / sqrt(1.0 - p2));
+}
+
 // The square root and the division use the hardware's v_sqrt_f32 / v_rcp_f32 (1 ulp)
 // instead of the correctly rounded library sequences (~16 and ~10 VALU instructions
 // with their denormal scaling): the optimizer epilogues of the large-vocabulary
 // kernels are VALU-heavy, and the step's relative error stays ~1e-7 of an lr-sized term.
+// Every fused multiply-add is explicit and contraction is off, so the update rounds the
+// same way in every kernel it is inlined into (the split W_in update's two halves must
+// agree bit for bit with the one-kernel update; the compiler's own contraction choices
+// differ between kernels).
 __device__ __forceinline__ float adam_update(float p, float g, float& mo, float& vo, const AdamCoef& c) {
-  if (c.wd != 0.f) g += c.wd * p;
-  mo += (1.f - c.b1) * (g - mo);
-  vo = c.b2 * vo + (1.f - c.b2) * g * g;
-  return p - c.step * mo * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vo) * c.ibc2 + c.eps);
+#pragma clang fp contract(off)
+  if (c.wd != 0.f) g = __builtin_fmaf(c.wd, p, g);
+  mo = __builtin_fmaf(1.f - c.b1, g - mo, mo);
+  vo = __builtin_fmaf(c.b2, vo, (1.f - c.b2) * g * g);
+  const float den = __builtin_fmaf(__builtin_amdgcn_sqrtf(vo), c.ibc2, c.eps);
+  return __builtin_fmaf(-(c.step * mo), __builtin_amdgcn_rcpf(den), p);
 }
 
 // Final value of a parameter element: fused mode applies Adam (and the FedAvg
@@ -628,7 +655,20 @@ __device__ __forceinline__ void prepare_next_batch(const GfkModel& m) {
   if (threadIdx.x == 0) nxt[0] = nb;
   const int cap = m.slot_cap;
   if (cap <= 0) return;
+  // split W_in update: the next batch's words get generation gen (read by every thread
+  // before thread 0 publishes it after the barrier; a generation, not the step index, so
+  // a stamp left from an earlier epoch never matches)
+  const bool split = m.stage_flags & GFK_WIN_SPLIT;
+  const int gen = split ? *m.ws_wgen + 1 : 0;
   __syncthreads();
+  if (split && threadIdx.x == 0) {
+    *m.ws_wgen = gen;
+    // the running powers the next step's post_fwd advances: gfk_win_dense_k, forked at the
+    // start of that step, derives the step's Adam coefficients from them (adam_advance)
+    double* snap = reinterpret_cast<double*>(m.ws_wgen + 2);
+    snap[0] = m.adam_pow[0];
+    snap[1] = m.adam_pow[1];
+  }
   // the rows' non-zeros into their slots: G threads per row, U loads in flight each
   constexpr int U = 8;
   const int G = max(1, (int)blockDim.x / bmax);
@@ -651,6 +691,7 @@ __device__ __forceinline__ void prepare_next_batch(const GfkModel& m) {
         if (j < n) {
           si[j] = ci[u];
           sv[j] = xv[u];
+          if (split) m.ws_wstamp[ci[u]] = gen;
         }
       }
     }

@@ -367,11 +367,13 @@ __global__ void __launch_bounds__(FT) gfk_post_fwd_k(GfkArgT<GB> ga) {
     *m.nbt_s = nbt1 + 1;
     // the optimizer step of this minibatch: t and the bias corrections
     *m.adam_t = at0 + 1;
-    const double p1 = pw0 * (double)m.beta1, p2 = pw1 * (double)m.beta2;
+    double p1, p2;
+    float c0, c1;
+    adam_advance(m, pw0, pw1, p1, p2, c0, c1);
     m.adam_pow[0] = p1;
     m.adam_pow[1] = p2;
-    m.adam_coef[0] = (float)((double)m.lr / (1.0 - p1));
-    m.adam_coef[1] = (float)(1.0 / sqrt(1.0 - p2));
+    m.adam_coef[0] = c0;
+    m.adam_coef[1] = c1;
   }
   lds_barrier();
   GFK_STAMP(m, 2);

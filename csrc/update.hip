@@ -52,7 +52,8 @@ extern "C" size_t gfk_win_update_smem(const GfkModel* m) {
   size_t a = (size_t)64 * stride_a(B) + (size_t)B * stride_b(H0P);
   const size_t b = 2 * (size_t)B * 80;
   if (a < 64 * 64) a = 64 * 64;      // the flat epilogue's gradient tile [64, H0 <= 64]
-  const size_t c = (size_t)B * m->H[0] + 2 * 512 + 129;   // the sparse tile (bit 4)
+  // the sparse tile (bit 4): dz0, the entry list, the row slots (+ the word mask and list)
+  const size_t c = (size_t)B * m->H[0] + 2 * 512 + 129 + 128;
   if (a < c) a = c;
   return sizeof(float) * (a > b ? a : b);
 }
@@ -310,7 +311,7 @@ __device__ __forceinline__ void win_tile_sparse(const GfkModel& m, float* smem, 
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int h = qh[u] + i - d * H0;  // the element's column in word col
-            if (h >= 0 && h < H0 && 4 * (tid + UT * u) + i < nel) g[u][i] += x * dr[h];
+            if (h >= 0 && h < H0 && 4 * (tid + UT * u) + i < nel) g[u][i] = __builtin_fmaf(x, dr[h], g[u][i]);
           }
         }
       }
@@ -343,6 +344,258 @@ __device__ __forceinline__ void win_tile_sparse(const GfkModel& m, float* smem, 
       st4(wblk + m.off_m, mo);
       st4(wblk + m.off_v, vo);
       st4(wblk, np);
+    }
+  }
+}
+
+// Split W_in update (stage_flags GFK_WIN_SPLIT, fused mode): the sparse tile updates only
+// the words of the batch -- the words stamped with this batch's generation by
+// prepare_next_batch, which are exactly the words with entries in the tiles' lists --
+// and gfk_win_dense_k gives every other word its zero-gradient Adam step, earlier in the
+// step on a side stream.  The tile's words come from its entry list (a word mask in LDS,
+// compacted by one ballot); thread t owns elements t, t + UT, .. of the [n_words, H0]
+// block, loads its p / m / v rows (contiguous 4 H0-byte runs), and sums its gradient
+// over the list in the same order as win_tile_sparse: the update is bit-identical to the
+// unsplit kernel's, at ~1/9 of its bytes at V = 112k (~7 words per 64-word tile).
+template <int UT>
+__device__ __forceinline__ void win_tile_sparse_rows(const GfkModel& m, float* smem, int tile) {
+  constexpr int CAP = 512;
+  constexpr int TPR = UT / 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int B = m.bmax, H0 = m.H[0], c0 = tile * 64;
+  const int nb = *m.ws_nb;
+  float* dz = smem;                            // [B][H0]
+  int* ecol = reinterpret_cast<int*>(dz + B * H0);   // [CAP] (row << 8) | local column
+  float* ex = reinterpret_cast<float*>(ecol + CAP);  // [CAP]
+  int* offs = reinterpret_cast<int*>(ex + CAP);      // [129] rows' first slots, total
+  int* wmark = offs + 129;                           // [64] word present / word list
+  __shared__ int s_nw;
+  const int32_t* tst = m.ws_tstart;
+  const int ntp = m.n_tiles + 1;
+  const int sub = tid % TPR;
+  int xe0[2], xe1[2], cnt[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = min(tid / TPR + 64 * i, B - 1);
+    xe0[i] = tst[(size_t)r * ntp + tile];
+    xe1[i] = tst[(size_t)r * ntp + tile + 1];
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = min(lane + 64 * i, B - 1);
+    cnt[i] = wave == 0 ? tst[(size_t)r * ntp + tile + 1] - tst[(size_t)r * ntp + tile] : 0;
+  }
+  glds_copy(dz, m.ws_dz[0], B * H0, tid, UT);
+  if (tid < 64) wmark[tid] = 0;
+  int fi[2];
+  float fv[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int e = min(xe0[i] + sub, max(xe1[i] - 1, 0));
+    fi[i] = m.indices[e];
+    fv[i] = m.values[e];
+  }
+  if (wave == 0) {             // row counts -> slots, rows in order
+    int base = 0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = lane + 64 * i < nb ? cnt[i] : 0;
+      int x = c;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+      }
+      offs[lane + 64 * i] = base + x - c;
+      base += __shfl(x, 63, 64);
+    }
+    if (lane == 0) offs[128] = base;
+  }
+  vm_barrier();
+  // the words with entries (every entry of the thread's rows, not only this pass's)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = tid / TPR + 64 * i;
+    if (r >= nb) continue;
+    int e = xe0[i] + sub;
+    if (e < xe1[i]) wmark[fi[i] - c0] = 1;
+    for (e += TPR; e < xe1[i]; e += TPR) wmark[m.indices[e] - c0] = 1;
+  }
+  __syncthreads();
+  if (wave == 0) {             // compact: wmark[0 .. nw) = the tile's words, ascending
+    const uint64_t mask = __ballot(wmark[lane] != 0);
+    const int pos = __popcll(mask & ((1ull << lane) - 1));
+    if ((mask >> lane) & 1) offs[129 + 64 + pos] = lane;   // (the word list after wmark)
+    if (lane == 0) s_nw = __popcll(mask);
+  }
+  __syncthreads();
+  const int nw = s_nw, nel = nw * H0;
+  const int* wl = offs + 129 + 64;
+  const int total = offs[128];
+  const AdamCoef ac = adam_coef(m);
+  const bool sh = is_shared(m, m.w_in);
+  // element groups of EG per thread (one group for a typical tile: ~7 words x H0 <= 512);
+  // the entry list is built once when it fits CAP, else once per pass of each group
+  constexpr int EG = 2;
+  for (int base = 0; base < nel; base += EG * UT) {
+    int ew[EG], eh[EG];
+    float pp[EG], pm[EG], pv[EG], g[EG];
+#pragma unroll
+    for (int u = 0; u < EG; ++u) {
+      const int el = min(base + tid + UT * u, nel - 1);
+      const int wi = el / H0;
+      eh[u] = el - wi * H0;
+      ew[u] = wl[wi];
+      const float* p = m.w_in + (size_t)(c0 + ew[u]) * H0 + eh[u];
+      pp[u] = *p;
+      pm[u] = p[m.off_m];
+      pv[u] = p[m.off_v];
+      g[u] = 0.f;
+    }
+    for (int p0 = 0; p0 < total; p0 += CAP) {
+      if (!(total <= CAP && base > 0)) {         // (uniform) build this pass's list
+        if (p0 || base) __syncthreads();         // the previous list's reads are done
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int r = tid / TPR + 64 * i;
+          if (r >= nb) continue;
+          const int o = offs[r] - xe0[i];
+          int e = xe0[i] + sub;
+          if (e < xe1[i]) {
+            const int s = o + e - p0;
+            if (s >= 0 && s < CAP) {
+              ecol[s] = (r << 8) | (fi[i] - c0);
+              ex[s] = fv[i];
+            }
+          }
+          for (e += TPR; e < xe1[i]; e += TPR) {
+            const int s = o + e - p0;
+            if (s >= 0 && s < CAP) {
+              ecol[s] = (r << 8) | (m.indices[e] - c0);
+              ex[s] = m.values[e];
+            }
+          }
+        }
+        __syncthreads();
+      }
+      const int n = min(CAP, total - p0);
+      for (int j = 0; j < n; ++j) {
+        const int cb = ecol[j];
+        const float x = ex[j];
+        const int col = cb & 255;
+        const float* dr = dz + (cb >> 8) * H0;
+#pragma unroll
+        for (int u = 0; u < EG; ++u)
+          if (col == ew[u]) g[u] = __builtin_fmaf(x, dr[eh[u]], g[u]);   // (as win_tile_sparse)
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < EG; ++u) {
+      if (base + tid + UT * u >= nel) break;
+      float* p = m.w_in + (size_t)(c0 + ew[u]) * H0 + eh[u];
+      float a = pm[u], b = pv[u];
+      float x = adam_update(pp[u], g[u], a, b, ac);
+      if (sh && m.fed_scale_on) x *= m.fed_scale;
+      p[m.off_m] = a;
+      p[m.off_v] = b;
+      *p = x;
+    }
+  }
+}
+
+// The zero-gradient Adam step of every input-layer word NOT in the batch (split W_in
+// update): flat float4 quads of the [V, H0] block, QU per thread in one round (the
+// stamps of the quads' words first, then p / m / v unconditionally -- the batch's words
+// are only read here; their writer, the sparse tile, runs after this kernel); an element
+// is stored iff its word's stamp differs from the batch's generation.  adam_update with
+// g = 0 is exactly what the unsplit tile computes for a word without entries.
+// It runs at the START of the step, on a side stream next to enc_in / post_fwd (latency-
+// bound, ~64 CUs busy), so its coefficients cannot come from adam_coef (post_fwd writes
+// them): they are derived from the powers snapshotted by prepare_next_batch.
+// grid: ceil(V H0 / 4 / (256 QU)) workgroups of 256 threads (short-lived, so the kernels
+// this overlaps keep getting CUs).
+constexpr int WD_QU = 4;
+template <bool GB = false>
+__global__ void __launch_bounds__(256) gfk_win_dense_k(GfkArgT<GB> ga) {
+  const GfkModel& m = gfk_model(ga);
+  const int H0 = m.H[0];
+  const int64_t n = (int64_t)m.V * H0;
+  const int64_t q0 = ((int64_t)blockIdx.x * 256 * WD_QU) + threadIdx.x;
+  const int32_t* st = m.ws_wstamp;
+  const int tag = *m.ws_wgen;
+  int sa[WD_QU], sb[WD_QU];
+#pragma unroll
+  for (int u = 0; u < WD_QU; ++u) {
+    const int64_t e = min(4 * (q0 + 256 * u), n - 1);
+    sa[u] = st[e / H0];
+    sb[u] = st[min(e + 3, n - 1) / H0];
+  }
+  f32x4 pp[WD_QU], pm[WD_QU], pv[WD_QU];
+#pragma unroll
+  for (int u = 0; u < WD_QU; ++u) {
+    const int64_t e = 4 * (q0 + 256 * u);
+    if (e + 3 < n) {
+      pp[u] = *reinterpret_cast<const f32x4*>(m.w_in + e);
+      pm[u] = *reinterpret_cast<const f32x4*>(m.w_in + m.off_m + e);
+      pv[u] = *reinterpret_cast<const f32x4*>(m.w_in + m.off_v + e);
+    } else {                                   // the partial last quad / past the end
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool in = e + i < n;
+        pp[u][i] = in ? m.w_in[e + i] : 0.f;
+        pm[u][i] = in ? m.w_in[m.off_m + e + i] : 0.f;
+        pv[u][i] = in ? m.w_in[m.off_v + e + i] : 0.f;
+      }
+    }
+  }
+  // this step's coefficients, from the powers prepare_next_batch saw (post_fwd advances the
+  // same powers concurrently: adam_advance reproduces its bits)
+  AdamCoef ac = adam_coef(m);
+  {
+    const double* snap = reinterpret_cast<const double*>(m.ws_wgen + 2);
+    double p1, p2;
+    adam_advance(m, snap[0], snap[1], p1, p2, ac.step, ac.ibc2);
+  }
+  const bool sh = is_shared(m, m.w_in);
+  // a zero the compiler cannot fold: the same Adam instruction sequence as the sparse
+  // tile's (whose g is a runtime sum), so both halves round identically
+  float gz = 0.f;
+  asm volatile("" : "+v"(gz));
+#pragma unroll
+  for (int u = 0; u < WD_QU; ++u) {
+    const int64_t e = 4 * (q0 + 256 * u);
+    if (e >= n) break;
+    const int64_t wa = e / H0;
+    bool ok[4];
+    bool all = e + 3 < n;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t w = (e + i) / H0;
+      ok[i] = e + i < n && (w == wa ? sa[u] : sb[u]) != tag;
+      all = all && ok[i];
+    }
+    f32x4 np, mo, vo;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float a = pm[u][i], b = pv[u][i];
+      float x = adam_update(pp[u][i], gz, a, b, ac);
+      np[i] = sh && m.fed_scale_on ? x * m.fed_scale : x;
+      mo[i] = a;
+      vo[i] = b;
+    }
+    float* p = m.w_in + e;
+    if (all) {
+      *reinterpret_cast<f32x4*>(p + m.off_m) = mo;
+      *reinterpret_cast<f32x4*>(p + m.off_v) = vo;
+      *reinterpret_cast<f32x4*>(p) = np;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (!ok[i]) continue;
+        p[m.off_m + i] = mo[i];
+        p[m.off_v + i] = vo[i];
+        p[i] = np[i];
+      }
     }
   }
 }
@@ -611,11 +864,41 @@ __global__ void __launch_bounds__(UT) gfk_win_sparse_k(GfkArgT<GB> ga, GfkUArgT<
   win_tile_sparse<UT>(m, smem, r - (U.n_w + U.n_v + 1));
 }
 
+// the split update's sparse half: the same job workgroups, then the batch words' tiles (its
+// own kernel, so neither tile body inflates the other's register budget)
+template <int UT, bool GB = false>
+__global__ void __launch_bounds__(UT) gfk_win_rows_k(GfkArgT<GB> ga, GfkUArgT<GB> gua) {
+  const GfkModel& m = gfk_model(ga);
+  const GfkUpdate& U = gfk_upd(gua);
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int r = (int)blockIdx.x;
+  if (r < U.n_w) { weight_job<UT>(m, U.w[r], smem); return; }
+  if (r < U.n_w + U.n_v) { vector_job<UT>(m, U.v[r - U.n_w]); return; }
+  if (r == U.n_w + U.n_v) { prepare_next_batch(m); return; }
+  win_tile_sparse_rows<UT>(m, smem, r - (U.n_w + U.n_v + 1));
+}
+
+// the zero-gradient half of the split W_in update (fused mode, sparse tiles, float4-aligned
+// W_in / m / v: checked by the engine before it sets GFK_WIN_SPLIT)
+extern "C" int gfk_launch_win_dense(const GfkModel* m, hipStream_t s) {
+  if (!(m->stage_flags & GFK_WIN_SPLIT) || !(m->stage_flags & WIN_SPARSE) || m->update_mode != 1 ||
+      m->H[0] < 4 || ((uintptr_t)m->w_in & 15) || (m->off_m & 3) || (m->off_v & 3))
+    return -1;
+  const int64_t quads = ((int64_t)m->V * m->H[0] + 3) / 4;
+  const dim3 g((unsigned)((quads + 256 * WD_QU - 1) / (256 * WD_QU)));
+  do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_win_dense_k<true>), gfk_grid(g, m), dim3(256), 0, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_win_dense_k<false>), g, dim3(256), 0, s, GfkArgT<false>{*m}); } while (0);
+  return (int)hipGetLastError();
+}
+
 extern "C" int gfk_launch_win_update(const GfkModel* m, const GfkUpdate* u, hipStream_t s) {
   const int extra = m->ctx_fused == 1 ? m->n_tiles : (m->ctx_fused == 2 ? (m->C + 63) / 64 : 0);
   if (m->stage_flags & WIN_SPARSE) {
     if (m->H[0] > 64 || m->input != GFK_IN_BOW || m->bmax > 128) return -1;
-    do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_win_sparse_k<512, true>), gfk_grid(dim3(u->n_w + u->n_v + 1 + m->n_tiles), m), dim3(512), gfk_win_update_smem(m), s, GfkArgT<true>{gfk_dev(m)}, GfkUArgT<true>{reinterpret_cast<const GfkUpdate*>(m->dev_upd)}); else hipLaunchKernelGGL((gfk_win_sparse_k<512, false>), dim3(u->n_w + u->n_v + 1 + m->n_tiles), dim3(512), gfk_win_update_smem(m), s, GfkArgT<false>{*m}, GfkUArgT<false>{*u}); } while (0);
+    const dim3 gs(u->n_w + u->n_v + 1 + m->n_tiles);
+    if (m->stage_flags & GFK_WIN_SPLIT)
+      do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_win_rows_k<512, true>), gfk_grid(gs, m), dim3(512), gfk_win_update_smem(m), s, GfkArgT<true>{gfk_dev(m)}, GfkUArgT<true>{reinterpret_cast<const GfkUpdate*>(m->dev_upd)}); else hipLaunchKernelGGL((gfk_win_rows_k<512, false>), gs, dim3(512), gfk_win_update_smem(m), s, GfkArgT<false>{*m}, GfkUArgT<false>{*u}); } while (0);
+    else
+      do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_win_sparse_k<512, true>), gfk_grid(gs, m), dim3(512), gfk_win_update_smem(m), s, GfkArgT<true>{gfk_dev(m)}, GfkUArgT<true>{reinterpret_cast<const GfkUpdate*>(m->dev_upd)}); else hipLaunchKernelGGL((gfk_win_sparse_k<512, false>), gs, dim3(512), gfk_win_update_smem(m), s, GfkArgT<false>{*m}, GfkUArgT<false>{*u}); } while (0);
     return (int)hipGetLastError();
   }
   const dim3 g(m->n_tiles + u->n_w + u->n_v + 1 + extra);
@@ -635,7 +918,8 @@ extern "C" int gfk_win_update_set_smem(size_t bytes) {
   cur = bytes;
   const void* ks[] = {(const void*)gfk_win_update_k<512, false>, (const void*)gfk_win_update_k<512, true>,
                       (const void*)gfk_win_update_k<1024, false>, (const void*)gfk_win_update_k<1024, true>,
-                      (const void*)gfk_win_sparse_k<512, false>, (const void*)gfk_win_sparse_k<512, true>};
+                      (const void*)gfk_win_sparse_k<512, false>, (const void*)gfk_win_sparse_k<512, true>,
+                      (const void*)gfk_win_rows_k<512, false>, (const void*)gfk_win_rows_k<512, true>};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return (int)e;

@@ -58,6 +58,7 @@ STAGE_FWD_STRIP_PF = 8            # bit 3: its prefetching 8-wave variant
 STAGE_WIN_SPARSE = 16             # bit 4: sparse W_in tiles (csrc/update.hip win_tile_sparse)
 STAGE_CTX_FULL = 32               # bit 5: CombinedTM forward, one workgroup per tile (csrc/ctx.hip)
 STAGE_FWD_STRIP_ROLL = 64         # bit 6: the strip forward's rolling-prefetch variant
+STAGE_WIN_SPLIT = 128             # bit 7: split W_in update (csrc/update.hip gfk_win_dense_k)
 
 
 def _explain(ok: bool, why: str, explain: bool) -> bool:
@@ -342,7 +343,16 @@ class FusedEngine(EngineBase):
             raise ValueError(f"the fused update mode is Adam only (solver {self.solver})")
         self.update_mode = mode
         self._m.update_mode = mode
+        was = self.win_split
+        if getattr(self, "_win_split_ok", False):     # the split W_in update is fused-mode only
+            if mode == UPDATE_FUSED:
+                self._m.stage_flags |= STAGE_WIN_SPLIT
+            else:
+                self._m.stage_flags &= ~STAGE_WIN_SPLIT
         self._rebuild_adam()
+        if self.win_split and not was and self.plan is not None:
+            # the bound batch was prepared without word stamps: prepare it again
+            self._launch([abi.PH_BATCH_PREP])
 
     def set_adam_t(self, t: int):
         """Set the optimizer step count and the device bias-correction state."""
@@ -352,6 +362,9 @@ class FusedEngine(EngineBase):
         if t > 0:
             self.adam_coef.copy_(torch.tensor([self.lr / (1.0 - p1), 1.0 / np.sqrt(1.0 - p2)],
                                               dtype=torch.float32))
+        if self.win_split and getattr(self, "plan", None) is not None:
+            # the split W_in update snapshots the powers when it prepares a batch
+            self._launch([abi.PH_BATCH_PREP])
 
     def _ptr(self, buf, key):
         if key not in self.flat.slots:
@@ -539,6 +552,19 @@ class FusedEngine(EngineBase):
         if m.input == abi.IN_BOW and int(m.H[0]) <= 64 and m.bmax <= 128 and (
                 ws_env == "1" or (ws_env == "auto" and m.n_tiles > 4 * cu_n)):
             m.stage_flags |= STAGE_WIN_SPARSE
+            # split W_in update (GFEDNTM_WIN_SPLIT=1, fused mode): the words not in the batch
+            # (~89 % at V = 112k) get their zero-gradient Adam step from gfk_win_dense_k on a
+            # side stream from the start of the step; the sparse tiles then move only the
+            # batch's words.  Bit-identical to the one-kernel update (tests/test_win_split.py)
+            # but slower, so not the default: K=200 V=112k 0.320 vs 0.294 ms per round
+            # (profiles/r3/win_split.md) -- the 134 MB streaming kernel does not hide
+            # behind enc_in / post_fwd (enc_in 14 -> 29 us) and its sparse half still pays
+            # three dependent rounds per tile (28 us)
+            win_al = (int(m.w_in or 0) % 16 == 0
+                      and m.off_m % 4 == 0 and m.off_v % 4 == 0)
+            self._win_split_ok = os.environ.get("GFEDNTM_WIN_SPLIT", "0") == "1" and win_al
+            if self._win_split_ok and self.update_mode == UPDATE_FUSED:
+                m.stage_flags |= STAGE_WIN_SPLIT
         self._alloc_workspace()
         rc = self.lib.gfk_setup(C.byref(m))
         if rc:
@@ -619,6 +645,11 @@ class FusedEngine(EngineBase):
             # precomputed logit-gradient tiles [n_tiles][B][66] (bwd_pre; + the pipelined
             # backward's store sinks, 64 floats per workgroup)
             "dt": f(m.n_tiles * B * 66 + 64 * (4 * m.n_dpart + 32) if m.bwd_pre else 1),
+            # split W_in update: per-word generation stamps of the batch's words + the
+            # current generation (prepare_next_batch -> gfk_win_dense_k)
+            "wstamp": torch.zeros((V if getattr(self, "_win_split_ok", False) else 1) + 16,
+                                  dtype=torch.int32, device=dev),
+            "wgen": torch.zeros(16, dtype=torch.int32, device=dev),
         }
         Lb = max(int(m.L), 1)
         ws.update(lab=f(B, Lb), dlab=f(B, Lb), ce=f(B), thd=f(B, K))   # label head
@@ -629,6 +660,10 @@ class FusedEngine(EngineBase):
         for i, h in enumerate(hs):
             ws[f"dz{i}"] = f(B, h)
         self.ws = ws
+        # the split W_in update's side stream and fork / join events (created here, never
+        # inside a graph capture)
+        self._win_side = ((torch.cuda.Stream(dev), torch.cuda.Event(), torch.cuda.Event())
+                          if getattr(self, "_win_split_ok", False) else None)
         self._alloc_ctx()
         for k, t in ws.items():
             if k[0] in "za" and k[1:].isdigit():
@@ -745,6 +780,22 @@ class FusedEngine(EngineBase):
         """Beta's update runs as a separate streaming optimizer pass (large V)."""
         return bool(self._m.beta_split) and self.update_mode == UPDATE_FUSED
 
+    @property
+    def win_split(self) -> bool:
+        """W_in's update is split: the words not in the batch on a side stream."""
+        return bool(self._m.stage_flags & STAGE_WIN_SPLIT)
+
+    def _win_fork(self):
+        side, ev_fork, ev_join = self._win_side
+        ev_fork.record(torch.cuda.current_stream(self.device))
+        side.wait_event(ev_fork)
+        with torch.cuda.stream(side):
+            self._launch_native([abi.PH_WIN_DENSE])
+        ev_join.record(side)
+
+    def _win_join(self):
+        torch.cuda.current_stream(self.device).wait_event(self._win_side[2])
+
     def _beta_adam(self):
         stream = torch.cuda.current_stream(self.device).cuda_stream
         rc = self.lib.gfk_launch_adam(C.byref(self._a_beta), self.beta_adam_grid, stream)
@@ -809,6 +860,9 @@ class FusedEngine(EngineBase):
             ph = abi.PRODLDA_STEP + ([abi.PH_ADAM] if self.update_mode == UPDATE_GRAD else [])
             if self.beta_split:
                 ph.insert(ph.index(abi.PH_PRODLDA_BWD) + 1, abi.PH_BETA_ADAM)
+        if self.win_split:
+            ph.insert(0, abi.PH_WIN_FORK)
+            ph.insert(ph.index(abi.PH_ENC_BWD), abi.PH_WIN_JOIN)
         if self.ctx_fused:
             if self._m.ctx_fused == 1:
                 ph.insert(ph.index(abi.PH_ENC_FWD), abi.PH_CTXF_FWD)
@@ -1092,6 +1146,10 @@ class FusedEngine(EngineBase):
                         self._fedavg_beta()
                     elif p == abi.PH_FEDAVG_END:
                         self._fedavg_end()
+                    elif p == abi.PH_WIN_FORK:
+                        self._win_fork()
+                    elif p == abi.PH_WIN_JOIN:
+                        self._win_join()
                 else:
                     run.append(p)
             return
@@ -1245,6 +1303,9 @@ _BATCH_SHAPE_FIELDS = ("bmax", "V", "ldb", "K", "n_hidden", "act", "kind", "inpu
                        "lab_on", "lab_off", "lab_in_enc", "bwd_pre")
 
 
+_BATCH_FORK_PHASES = (abi.PH_WIN_FORK, abi.PH_WIN_JOIN)
+
+
 class BatchedSteps:
     """One launch per phase for the local steps of several fused engines (clients).
 
@@ -1266,6 +1327,7 @@ class BatchedSteps:
         self._blob = None
         self._host = None
         self._phases = e0.phases()
+        self._side = (torch.cuda.Stream(self.device), torch.cuda.Event(), torch.cuda.Event())
 
     @staticmethod
     def possible(engines) -> bool:
@@ -1288,7 +1350,8 @@ class BatchedSteps:
                 raise ValueError("batched engines must share a device")
             if e.phases() != ph:
                 raise ValueError("batched engines must run the same phases")
-            if any(p in abi.HOST_PHASES for p in ph) or e._comm is not None:
+            if any(p in abi.HOST_PHASES and p not in _BATCH_FORK_PHASES for p in ph) \
+                    or e._comm is not None:
                 raise ValueError("batched launches need native phases only")
             for f in _BATCH_SHAPE_FIELDS:
                 a, b = getattr(e._m, f), getattr(e0._m, f)
@@ -1318,13 +1381,33 @@ class BatchedSteps:
         """Upload the descriptors now (before a capture)."""
         self._refresh()
 
-    def launch(self):
-        """Enqueue one local step of every engine on the current stream."""
-        self._refresh()
+    def _run(self, phases):
         e0 = self.engines[0]
-        arr, n = abi.phase_array(self._phases)
+        arr, n = abi.phase_array(phases)
         stream = torch.cuda.current_stream(self.device).cuda_stream
         rc = e0.lib.gfk_run(C.byref(self._host), C.byref(e0._a), e0.adam_grid,
                             C.byref(e0._u), stream, arr, n)
         if rc:
             raise RuntimeError(f"gfk_run (batched) failed: code {rc}")
+
+    def launch(self):
+        """Enqueue one local step of every engine on the current stream (the split W_in
+        update's dense half forked onto a side stream, as in a single engine's step)."""
+        self._refresh()
+        run: List[int] = []
+        for p in list(self._phases) + [None]:
+            if p is not None and p not in _BATCH_FORK_PHASES:
+                run.append(p)
+                continue
+            if run:
+                self._run(run)
+                run = []
+            if p == abi.PH_WIN_FORK:
+                side, ev_fork, ev_join = self._side
+                ev_fork.record(torch.cuda.current_stream(self.device))
+                side.wait_event(ev_fork)
+                with torch.cuda.stream(side):
+                    self._run([abi.PH_WIN_DENSE])
+                ev_join.record(side)
+            elif p == abi.PH_WIN_JOIN:
+                torch.cuda.current_stream(self.device).wait_event(self._side[2])

@@ -33,6 +33,7 @@ PH_ADAM = 11
 PH_BATCH_PREP = 12
 PH_CTXF_FWD = 13      # CombinedTM contextual forward on the fused kernels (ctx_fwd)
 PH_CTXF_BWD = 14      # ... and its backward + adapt_bert updates (ctx_bwd)
+PH_WIN_DENSE = 15     # split W_in update: the zero-gradient Adam of the words not in the batch
 
 # PH_ENC_FWD = enc_in (sparse gather, MLP, heads, random draws), PH_POST_FWD =
 # post_fwd (batch-norm, reparameterisation, softmax, KL), PH_POST_BWD = row_bwd +
@@ -50,7 +51,12 @@ PH_FEDAVG_END = 103
 # large-vocabulary ProdLDA (beta_split): prodlda_bwd leaves beta's gradient in the grad
 # slot and the generic float4 optimizer kernel updates beta (one streaming pass)
 PH_BETA_ADAM = 104
-HOST_PHASES = (PH_CTX_FWD, PH_CTX_BWD, PH_FEDAVG_BETA, PH_FEDAVG_END, PH_BETA_ADAM)
+# split W_in update (large vocabularies): PH_WIN_DENSE forked onto a side stream at the
+# start of the step, joined before win_update
+PH_WIN_FORK = 105
+PH_WIN_JOIN = 106
+HOST_PHASES = (PH_CTX_FWD, PH_CTX_BWD, PH_FEDAVG_BETA, PH_FEDAVG_END, PH_BETA_ADAM, PH_WIN_FORK,
+               PH_WIN_JOIN)
 
 PRODLDA_STEP = [PH_ENC_FWD, PH_POST_FWD, PH_PRODLDA_FWD, PH_PRODLDA_LOSS, PH_PRODLDA_BWD,
                 PH_POST_BWD, PH_ENC_BWD]
@@ -104,6 +110,7 @@ class GfkModel(C.Structure):
         ("ws_lab", P), ("ws_dlab", P), ("ws_ce", P), ("ws_thd", P),
         ("lab_in_enc", C.c_int32), ("bwd_pre", C.c_int32), ("ws_dt", P),
         ("dev", P), ("dev_upd", P), ("n_batch", C.c_int32), ("ldb", C.c_int32),
+        ("pad3", C.c_int32), ("ws_wstamp", P), ("ws_wgen", P),
     ]
 
 
