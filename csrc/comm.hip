@@ -136,16 +136,15 @@ __device__ __forceinline__ void slice_range(const GfkComm& c, int ch, int b, int
 }
 }  // namespace
 
+// No LDS at all (the epoch is read by every thread before thread 0 advances it): a kernel
+// that waits on peers must not hold LDS a co-running kernel needs -- CombinedTM's ctx_bwd
+// takes a whole CU's LDS, and a spinning all-reduce workgroup with even 4 bytes of it on
+// every CU kept ctx_bwd from launching (a 2-rank one-GPU rehearsal waited out its bound).
 extern "C" __global__ void __launch_bounds__(CT) gfk_xgmi_allreduce(GfkComm c, float* data) {
-  __shared__ uint32_t s_epoch;
   const int b = blockIdx.x, t = threadIdx.x;
-  if (t == 0) {
-    const uint32_t e = c.epoch[b] + 1;
-    c.epoch[b] = e;
-    s_epoch = e;
-  }
+  const uint32_t e = c.epoch[b] + 1;
   __syncthreads();
-  const uint32_t e = s_epoch;
+  if (t == 0) c.epoch[b] = e;
   const int buf = e & 1, R = c.rank, W = c.world;
   const int64_t sbytes = (int64_t)W * c.chunk * 4;
   const __amdgpu_buffer_rsrc_t mine = rsrc(c.stage[buf][R], sbytes);

@@ -640,8 +640,11 @@ __host__ __device__ __forceinline__ int kt_stride(int w) { return w % 32 == 16 ?
 __host__ __device__ __forceinline__ int bwd_kpq(int K, int kq) { return 16 * ((round_up(K, 16) / 16 + kq - 1) / kq); }
 // bwd_pre = 3 runs the software-pipelined backward (fp32, B = 64; else the bwd_pre = 2 one),
 // whose dlogit tiles are dense [B][64]
+// (its buffer-descriptor stores need beta's rows padded to whole 64-column tiles and the
+// slot under 2 GB)
 __host__ __device__ __forceinline__ bool bwd_pipe(const GfkModel& m) {
-  return m.bwd_pre == 3 && m.bmax == 64 && !m.mm_bf16;
+  return m.bwd_pre == 3 && m.bmax == 64 && !m.mm_bf16 && (m.ldb & 63) == 0 &&
+         (int64_t)m.K * m.ldb * 4 < 0x7FFF0000LL;
 }
 
 // Logit gradient of one vocabulary tile, computed ONCE (bwd_pre: the persistent k-range
@@ -1203,8 +1206,17 @@ __global__ void __launch_bounds__(512, 2) prodlda_bwd_pre2_kernel(GfkArgT<GB> ga
 // 2-way bank conflicts and keeps the b128 reads conflict-free.
 // LDS: thT, bt, dt, dtT: 4 x [64][72] floats (74 KB; the G tile aliases dtT).
 constexpr int LDP = 72;
+typedef unsigned int gfk_u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ int dtt_swz(int c) { return ((c >> 2) & 7) << 2; }
-template <int BM, int MAXU, bool GB = false>
+// Memory operations (r3): beta / m / v / the gradient through buffer descriptors with one
+// VGPR column offset per tile and per-row SGPR offsets (row k of a range is wave-uniform:
+// k = kb + wave + 8 u), instead of a 64-bit address per element and a select between the
+// element and a sink: rows past K (the last k range's padding) get an out-of-range voffset
+// (the descriptor's range check: loads return 0, stores are dropped); columns past V
+// fall into beta's row padding (ldb is a multiple of 64 on this path; padding columns have
+// a zero gradient and stay zero).  FUSED (Adam + pre-scale, else the gradient) is a
+// template parameter: no per-element mode selects.
+template <int BM, int MAXU, bool FUSED, bool GB = false>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
 prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
   static_assert(BM == 64, "pipelined backward: B = 64");
@@ -1238,7 +1250,6 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
   float* dt = bt + 64 * LDP;                    // [64 b][LDP]   dlogit
   float* dtT = dt + 64 * LDP;                   // [64 c][LDP ^ swz] dlogit^T (then the G tile)
   const int NB_T = nks * 4, NDT_T = (BM / 16) * nks;
-  const bool fused = m.update_mode == 1 && !m.beta_split;
   const int nb = *m.ws_nb;
   const AdamCoef ac = adam_coef(m);
   const bool beta_shared = is_shared(m, m.beta);
@@ -1251,25 +1262,40 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
 
   float br[RU];
   f32x4 dr[DU];
+  // buffer descriptors over beta's slot and its m / v / gradient twins (host-checked:
+  // K ldb 4 < 2^31), the dlogit tiles, and the per-row offsets of this wave's elements
+  const int nrec = K * m.ldb * 4;
+  const __amdgpu_buffer_rsrc_t rs_b = __builtin_amdgcn_make_buffer_rsrc((void*)m.beta, 0, nrec, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_m = __builtin_amdgcn_make_buffer_rsrc((void*)(m.beta + (FUSED ? m.off_m : m.off_g)), 0, nrec, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_v = __builtin_amdgcn_make_buffer_rsrc((void*)(m.beta + m.off_v), 0, nrec, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_d = __builtin_amdgcn_make_buffer_rsrc((void*)m.ws_dt, 0, n_tiles * BM * VB * 4, 0x00020000);
+  int rowoff[RU];                              // bytes; rows outside the range / K: out of range
+#pragma unroll
+  for (int u = 0; u < RU; ++u) {
+    const int kl = wave + RPU * u, k = kb + kl;
+    rowoff[u] = uniform(kl < 16 * nks && k < K ? k * m.ldb * 4 : 0x7FFF0000);
+  }
+  const int lane4 = 4 * (tid & (VB - 1));
   // element tid + NTH u of the block is (row tid / VB + RPU u, column tid % VB)
   auto issue_bd = [&](int tile) {             // beta slice + dlogit tile
-    const int c = min(tile * VB + (tid & (VB - 1)), V - 1);
-    const f32x4* d4 = reinterpret_cast<const f32x4*>(m.ws_dt + (size_t)tile * BM * VB);
+    const int vc = tile * VB * 4 + lane4;
 #pragma unroll
-    for (int j = 0; j < DU; ++j) dr[j] = d4[tid + NTH * j];
+    for (int j = 0; j < DU; ++j) {
+      const gfk_u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs_d, (tid + NTH * j) * 16, uniform(tile * BM * VB * 4), 0);
+      dr[j] = f32x4{__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), __uint_as_float(x.w)};
+    }
 #pragma unroll
-    for (int u = 0; u < RU; ++u) br[u] = m.beta[(size_t)min(kb + tid / VB + RPU * u, K - 1) * m.ldb + c];
+    for (int u = 0; u < RU; ++u) br[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_b, vc + rowoff[u], 0, 0));
   };
-  // Adam state (gradient mode: beta itself, unused -- unconditional, like every load and
-  // store of the tile loop, so the compiler's vmcnt bookkeeping stays exact across it)
-  const int64_t om = fused ? m.off_m : 0, ov = fused ? m.off_v : 0;
+  // Adam state (fused mode only)
   auto issue_mv = [&](int tile, float (&rm)[RU], float (&rv)[RU]) __attribute__((always_inline)) {
-    const int c = min(tile * VB + (tid & (VB - 1)), V - 1);
+    if constexpr (FUSED) {
+      const int vc = tile * VB * 4 + lane4;
 #pragma unroll
-    for (int u = 0; u < RU; ++u) {
-      const float* p = m.beta + (size_t)min(kb + tid / VB + RPU * u, K - 1) * m.ldb + c;
-      rm[u] = p[om];
-      rv[u] = p[ov];
+      for (int u = 0; u < RU; ++u) {
+        rm[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_m, vc + rowoff[u], 0, 0));
+        rv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_v, vc + rowoff[u], 0, 0));
+      }
     }
   };
   // out-of-range elements store into this workgroup's 64-float slot behind the dense dlogit
@@ -1311,8 +1337,9 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
   // the previous tile's stores drained before staging)
   // (addresses the compiler cannot prove equal, so it cannot merge them)
   float* const wsink = sink - (tid & 63);
+  constexpr int NST = FUSED ? 3 : 1;           // stores per element in the loop's epilogue
 #pragma unroll
-  for (int u = 0; u < 3 * RU; ++u) wsink[(tid + 5 * u) & 63] = 0.f;
+  for (int u = 0; u < NST * RU; ++u) wsink[(tid + 5 * u) & 63] = 0.f;
   auto body = [&](int tile, float (&rm)[RU], float (&rv)[RU], float (&nm)[RU], float (&nv)[RU])
       __attribute__((always_inline)) {
     const int c0 = tile * VB;
@@ -1322,12 +1349,10 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
     wave = uniform(tid >> 6);
     lds_barrier();                             // the previous tile's LDS reads are done
     {
-      const int c = tid & (VB - 1), cok = c0 + c < V;
+      // (rows past the range / K and columns past V were loaded as 0)
+      const int c = tid & (VB - 1);
 #pragma unroll
-      for (int u = 0; u < RU; ++u) {
-        const int k = tid / VB + RPU * u;
-        if (k < 16 * nks) bt[__mul24(k, LDP) + c] = (kb + k < K && cok) ? br[u] : 0.f;
-      }
+      for (int u = 0; u < RU; ++u) bt[__mul24(tid / VB + RPU * u, LDP) + c] = br[u];
 #pragma unroll
       for (int j = 0; j < DU; ++j) {           // dense [BM][64] -> dt [b][c] and dtT [c][b]
         const int i = tid + NTH * j, r = i >> 4, c4 = (i & 15) * 4;
@@ -1387,9 +1412,9 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
     }
     lds_barrier();
     // the G tile, row-wise: update (fused) or gradient
-    const int cl = tid & (VB - 1), kl0 = tid / VB, c = c0 + cl;
+    const int cl = tid & (VB - 1), kl0 = tid / VB;
     const int cs = cl ^ ((kl0 & 4) << 2);
-    float* p0 = m.beta + (size_t)(kb + kl0) * m.ldb + c;
+    const int vc = c0 * 4 + lane4;
     // row pointers stepped by constants (folded into the ds_read offsets).  LDS index
     // products are __mul24 throughout: a plain 32-bit multiply-add became v_mad_u64_u32,
     // whose unused high addend half was a register with a load in flight, and the waitcnt
@@ -1398,26 +1423,18 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
     const float* btp = bt + __mul24(kl0, LDP) + cl;
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
-      const int kl = kl0 + RPU * u, k = kb + kl;
-      const bool ok = kl < 16 * nks && k < K && c < V;
       const float gv = gtp[RPU * u * VB];
-      float* p = p0 + (size_t)(RPU * u) * m.ldb;
-      float mo = rm[u], vo = rv[u];
-      float np = adam_update(btp[RPU * u * LDP], gv, mo, vo, ac);
-      if (beta_shared && m.fed_scale_on) np *= m.fed_scale;
-      // fused: m, v, beta; gradient mode: the gradient (+ two sink stores)
-#if GFK_DIAG_BWD == 2                          // (diagnostic builds: no stores)
-      if (np == 1234.5f)
-#endif
-      *(ok ? p + (fused ? m.off_m : m.off_g) : sink) = fused ? mo : gv;
-#if GFK_DIAG_BWD == 2
-      if (np == 1234.5f)
-#endif
-      *(ok && fused ? p + m.off_v : sink) = vo;
-#if GFK_DIAG_BWD == 2
-      if (np == 1234.5f)
-#endif
-      *(ok && fused ? p : sink) = np;
+      if constexpr (FUSED) {
+        float mo = rm[u], vo = rv[u];
+        float np = adam_update(btp[RPU * u * LDP], gv, mo, vo, ac);
+        if (beta_shared && m.fed_scale_on) np *= m.fed_scale;
+        const int vo4 = vc + rowoff[u];
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mo), rs_m, vo4, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vo), rs_v, vo4, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(np), rs_b, vo4, 0, 0);
+      } else {                                 // the gradient (rs_m is the gradient slot)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gv), rs_m, vc + rowoff[u], 0, 0);
+      }
     }
   };
 #pragma unroll 1
@@ -1535,8 +1552,13 @@ static void launch_bwd_p(const GfkModel* m, dim3 g, size_t sm, hipStream_t s) {
   const dim3 blk(KQ == 1 ? DEC_THREADS : 512);
   if constexpr (PRE && !BF) {
     if (bwd_pipe(*m)) {
-      if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_bwd_pipe_kernel<64, MAXU, true>), gfk_grid(g, m), blk, sm, s, GfkArgT<true>{gfk_dev(m)});
-      else hipLaunchKernelGGL((prodlda_bwd_pipe_kernel<64, MAXU, false>), g, blk, sm, s, GfkArgT<false>{*m});
+      if (m->update_mode == 1 && !m->beta_split) {
+        if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_bwd_pipe_kernel<64, MAXU, true, true>), gfk_grid(g, m), blk, sm, s, GfkArgT<true>{gfk_dev(m)});
+        else hipLaunchKernelGGL((prodlda_bwd_pipe_kernel<64, MAXU, true, false>), g, blk, sm, s, GfkArgT<false>{*m});
+      } else {
+        if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_bwd_pipe_kernel<64, MAXU, false, true>), gfk_grid(g, m), blk, sm, s, GfkArgT<true>{gfk_dev(m)});
+        else hipLaunchKernelGGL((prodlda_bwd_pipe_kernel<64, MAXU, false, false>), g, blk, sm, s, GfkArgT<false>{*m});
+      }
       return;
     }
   }
@@ -1636,7 +1658,8 @@ extern "C" int gfk_prodlda_set_smem(size_t bytes) {
     (const void*)prodlda_bwd_pre2_kernel<16, U, F>, (const void*)prodlda_bwd_pre2_kernel<16, U, F, true>, (const void*)prodlda_bwd_pre2_kernel<32, U, F>, (const void*)prodlda_bwd_pre2_kernel<32, U, F, true>, \
     (const void*)prodlda_bwd_pre2_kernel<64, U, F>, (const void*)prodlda_bwd_pre2_kernel<64, U, F, true>
 #define GFK_BWD_PTRS(U) GFK_BWD_PTRS1(U, 1), GFK_BWD_PTRS1(U, 4), GFK_BWD_PTRS3(U, false), \
-    GFK_BWD_PTRS3(U, true), (const void*)prodlda_bwd_pipe_kernel<64, U>, (const void*)prodlda_bwd_pipe_kernel<64, U, true>
+    GFK_BWD_PTRS3(U, true), (const void*)prodlda_bwd_pipe_kernel<64, U, false>, (const void*)prodlda_bwd_pipe_kernel<64, U, false, true>, \
+    (const void*)prodlda_bwd_pipe_kernel<64, U, true>, (const void*)prodlda_bwd_pipe_kernel<64, U, true, true>
                       GFK_BWD_PTRS(1), GFK_BWD_PTRS(2), GFK_BWD_PTRS(3), GFK_BWD_PTRS(4)};
 #undef GFK_BWD_PTRS
 #undef GFK_BWD_PTRS3

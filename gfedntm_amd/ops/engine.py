@@ -104,10 +104,11 @@ def theta_stride(K: int) -> int:
     return kt + 2 if (kt // 2) % 2 == 0 else kt
 
 
-# beta rows padded to 128-B lines from this vocabulary size on (utils/flat.py): the large-V
-# kernels' 64-column RMW tiles then never split a cache line with another tile
+# beta rows padded to whole 64-column tiles (256 B) from this vocabulary size on
+# (utils/flat.py): the large-V kernels' RMW tiles never split a cache line with another
+# tile, and a tile's columns past V are row padding (prodlda_bwd_pipe_kernel stores there)
 BETA_PAD_MIN_V = 8192
-BETA_PAD = 32
+BETA_PAD = 64                     # whole 64-column tiles (the pipelined backward's stores rely on it)
 
 
 def beta_ld(V: int) -> int:
@@ -526,7 +527,8 @@ class FusedEngine(EngineBase):
                 # its smaller LDS plan (no logit tile, G aliases dt) and <= 80 VGPRs fit
                 # THREE range workgroups per CU: 3/4 of a CU's slots per slab of 4
                 m.n_dpart = min(3 * cu // 4, m.n_tiles - 1)
-            elif m.bwd_pre == 3 and m.bmax == 64 and not m.mm_bf16:
+            elif (m.bwd_pre == 3 and m.bmax == 64 and not m.mm_bf16 and m.ldb % 64 == 0
+                  and m.K * m.ldb * 4 < 0x7FFF0000):
                 pass
             elif m.bwd_pre:
                 m.bwd_pre = 2            # two per CU, no register cap
