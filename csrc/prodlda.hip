@@ -304,7 +304,14 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkArgT<GB> ga
 // per SIMD, the MFMA pipe ~40 % busy at K = 200).
 // (PF = 2 with more than 13 k pairs: 12 waves of <= 168 VGPRs, 3 per SIMD -- the 50-register
 // beta block + accumulators + A operands spill at 128)
+// PF = 3 (stage_flags bit 8): the rolling prefetch through a RING of strip_ring(NP) <= 13
+// pairs instead of the whole strip's NP: pair t's registers receive pair t + R -- of this
+// strip while t + R < NP, else of the next one -- so a load still has R pairs of MFMAs
+// (x 4 waves per SIMD) to arrive, and K = 200 (25 pairs) fits 128 VGPRs: 16 waves per CU
+// instead of 12, and 7004 strips over 4096 waves (at most 2 each; 76 -> 85 % of the last
+// round's slots busy) instead of 3072 (at most 3).
 __host__ __device__ constexpr int strip_threads(int pf, int np) { return pf == 1 ? 512 : pf == 2 && np > 13 ? 768 : 1024; }
+__host__ __device__ constexpr int strip_ring(int pf, int np) { return pf == 3 && np > 13 ? 13 : np; }
 template <int BM, int NP, int PF, bool GB = false>
 __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kernel(GfkArgT<GB> ga) {
   const GfkModel& m = gfk_model(ga);
@@ -346,14 +353,15 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
   // read as 0 (no clamps, no per-load address VGPRs).  Unconditional: a guarded load
   // becomes a branch + vmcnt(0) per pair in the ISA.  The row step is made opaque per
   // call so the offsets are recomputed here, not hoisted out of the loop and spilled.
-  auto issue = [&](int st, float (&bb)[2 * NP], float& rm, float& rv) {
+  auto issue = [&](int st, auto& bb, float& rm, float& rv) {
+    constexpr int NL = sizeof(bb) / sizeof(float) / 2;    // pairs: NR (the ring) or NP
     const int vc = min((st >> 2) * VB + 16 * (st & 3) + (lane & 15), V - 1);
     int v4 = LDB * 4;
     asm volatile("" : "+s"(v4));
     int voff = g2 * v4 + vc * 4;
     const int v32 = 8 * v4;
 #pragma unroll
-    for (int t = 0; t < NP; ++t) {
+    for (int t = 0; t < NL; ++t) {
       bb[2 * t] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bres, voff, 0, 0));
       bb[2 * t + 1] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bres, voff, v4, 0));
       voff += v32;
@@ -365,7 +373,8 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
   // while this one runs its MFMAs / batch norm / stores (2 waves per SIMD, ~190 VGPRs)
   // PF = false: no prefetch, 16 waves per CU at <= 128 VGPRs (the waves overlap each
   // other's loads instead)
-  float b[2 * NP], bn[2 * NP], rm0 = 0.f, rv0 = 0.f, rmn = 0.f, rvn = 0.f;
+  constexpr int NR = strip_ring(PF, NP);       // pairs held in registers
+  float b[2 * NR], bn[2 * (PF == 1 ? NP : 1)], rm0 = 0.f, rv0 = 0.f, rmn = 0.f, rvn = 0.f;
   // wave group gq = wave >> 2 takes whole tiles gq * grid + g, + NW / 4 * grid, ...: the
   // 4 strips of a tile stay on one CU (their beta rows share cache lines), and the
   // tiles of the last, partial round are spread over every CU's wave group 0 instead
@@ -402,13 +411,20 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
   lds_barrier();
   asm volatile("" : "+v"(tid));
   __builtin_assume(tid >= 0 && tid < STRIP_THREADS);
+  // PF = 3: this strip's per-lane offset of pair 0 (its pairs R.. are loaded in the loop)
+  int voffc = 0;
+  if (PF == 3) {
+    const int s0 = min(s, nstrips - 1);
+    const int vc0 = min((s0 >> 2) * VB + 16 * (s0 & 3) + (lane & 15), V - 1);
+    voffc = g2 * (LDB * 4) + vc0 * 4;
+  }
 #pragma unroll 1
   for (; s < nstrips; s += stride) {
     // PF = 2: the next strip's per-lane buffer offset (its pairs are loaded in the MFMA loop)
     int voffn = 0, v4n = LDB * 4;
     if (PF == 1) {
       issue(min(s + stride, nstrips - 1), bn, rmn, rvn);   // (the last one re-reads a strip)
-    } else if (PF == 2) {
+    } else if (PF == 2 || PF == 3) {
       const int sn = min(s + stride, nstrips - 1);
       const int vcn = min((sn >> 2) * VB + 16 * (sn & 3) + (lane & 15), V - 1);
       asm volatile("" : "+s"(v4n));
@@ -445,15 +461,21 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
           a[(t + 1) & 1][i] = *reinterpret_cast<const float2*>(ap + i * 16 * KS + 8 * (t + 1));
       }
 #pragma unroll
-      for (int i = 0; i < RT; ++i) acc[i] = mfma16x16x4(a[t & 1][i].x, b[2 * t], acc[i]);
+      for (int i = 0; i < RT; ++i) acc[i] = mfma16x16x4(a[t & 1][i].x, b[2 * (t % NR)], acc[i]);
 #pragma unroll
-      for (int i = 0; i < RT; ++i) acc[i] = mfma16x16x4(a[t & 1][i].y, b[2 * t + 1], acc[i]);
+      for (int i = 0; i < RT; ++i) acc[i] = mfma16x16x4(a[t & 1][i].y, b[2 * (t % NR) + 1], acc[i]);
       if (PF == 2) {                  // the next strip's pair t into the registers just read
         b[2 * t] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bres, voffn, 0, 0));
         b[2 * t + 1] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bres, voffn, v4n, 0));
         voffn += 8 * v4n;
+      } else if (PF == 3) {           // pair t + NR (this strip's, else the next one's)
+        const int pn = t + NR;
+        const int vo = pn < NP ? voffc + pn * 8 * v4n : voffn + (pn - NP) * 8 * v4n;
+        b[2 * (t % NR)] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bres, vo, 0, 0));
+        b[2 * (t % NR) + 1] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bres, vo, v4n, 0));
       }
     }
+    if (PF == 3) voffc = voffn;
     // ---- column batch-norm over the wave's own rows (rows >= nb excluded) ----
     // (rows >= nb are exact zeros, so the sum needs no mask; lim is made opaque per strip
     // so the 4 RT row compares are not hoisted out of the loop as live SGPR masks)
@@ -1466,6 +1488,7 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
 constexpr int FWD_STRIP = 4;
 constexpr int FWD_STRIP_PF = 8;   // bit 3: its prefetching 8-wave variant
 constexpr int FWD_STRIP_ROLL = 64;  // bit 6: its rolling-prefetch 16-wave variant (PF = 2)
+constexpr int FWD_STRIP_RING = 256; // bit 8: the rolling prefetch through a 13-pair ring (PF = 3)
 __host__ __device__ inline int strip_pairs(int K) { return (K + 7) / 8; }
 // the kernel instance (k pairs in registers) for K
 __host__ __device__ inline int strip_np(int K) {
@@ -1511,7 +1534,9 @@ extern "C" int gfk_launch_prodlda_fwd(const GfkModel* m, hipStream_t s) {
         (int64_t)m->K * m->ldb >= (1LL << 29)) return -1;
 #define GFK_FWS(BM, NP)                                                                        \
     do {                                                                                       \
-      if (m->stage_flags & FWD_STRIP_ROLL)                                                     \
+      if (m->stage_flags & FWD_STRIP_RING)                                                     \
+        do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 3, true>), gfk_grid(g, m), dim3(strip_threads(3, NP)), sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 3, false>), g, dim3(strip_threads(3, NP)), sm, s, GfkArgT<false>{*m}); } while (0); \
+      else if (m->stage_flags & FWD_STRIP_ROLL)                                                \
         do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 2, true>), gfk_grid(g, m), dim3(strip_threads(2, NP)), sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 2, false>), g, dim3(strip_threads(2, NP)), sm, s, GfkArgT<false>{*m}); } while (0); \
       else if (m->stage_flags & FWD_STRIP_PF)                                                  \
         do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 1, true>), gfk_grid(g, m), dim3(512), sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 1, false>), g, dim3(512), sm, s, GfkArgT<false>{*m}); } while (0); \
@@ -1645,7 +1670,7 @@ extern "C" int gfk_prodlda_set_smem(size_t bytes) {
 #define GFK_FWS_PTRS1(BM, F) (const void*)prodlda_fwd_strip_kernel<BM, 8, F>, (const void*)prodlda_fwd_strip_kernel<BM, 8, F, true>, \
     (const void*)prodlda_fwd_strip_kernel<BM, 13, F>, (const void*)prodlda_fwd_strip_kernel<BM, 13, F, true>, (const void*)prodlda_fwd_strip_kernel<BM, 16, F>, (const void*)prodlda_fwd_strip_kernel<BM, 16, F, true>, \
     (const void*)prodlda_fwd_strip_kernel<BM, 25, F>, (const void*)prodlda_fwd_strip_kernel<BM, 25, F, true>, (const void*)prodlda_fwd_strip_kernel<BM, 32, F>, (const void*)prodlda_fwd_strip_kernel<BM, 32, F, true>
-#define GFK_FWS_PTRS(BM) GFK_FWS_PTRS1(BM, 0), GFK_FWS_PTRS1(BM, 1), GFK_FWS_PTRS1(BM, 2)
+#define GFK_FWS_PTRS(BM) GFK_FWS_PTRS1(BM, 0), GFK_FWS_PTRS1(BM, 1), GFK_FWS_PTRS1(BM, 2), GFK_FWS_PTRS1(BM, 3)
                       GFK_FWS_PTRS(16), GFK_FWS_PTRS(32), GFK_FWS_PTRS(64),
 #undef GFK_FWS_PTRS
 #undef GFK_FWS_PTRS1

@@ -59,6 +59,7 @@ STAGE_WIN_SPARSE = 16             # bit 4: sparse W_in tiles (csrc/update.hip wi
 STAGE_CTX_FULL = 32               # bit 5: CombinedTM forward, one workgroup per tile (csrc/ctx.hip)
 STAGE_FWD_STRIP_ROLL = 64         # bit 6: the strip forward's rolling-prefetch variant
 STAGE_WIN_SPLIT = 128             # bit 7: split W_in update (csrc/update.hip gfk_win_dense_k)
+STAGE_FWD_STRIP_RING = 256        # bit 8: the strip forward's ring-prefetch variant (PF = 3)
 
 
 def _explain(ok: bool, why: str, explain: bool) -> bool:
@@ -493,11 +494,16 @@ class FusedEngine(EngineBase):
                 # 2, the default: the rolling prefetch (the next strip's k pair loaded into
                 # the registers its MFMAs just consumed; 12-16 waves per CU, no second
                 # register block)
-                pf = os.environ.get("GFEDNTM_FWD_STRIP_PF", "2")
+                # 3, the default since g26: the same rolling prefetch through a 13-pair ring
+                # (K > 104: 128 VGPRs, 16 waves per CU instead of 12; K = 200 V = 112k forward
+                # 39.7 -> 36.5 us, round 0.2794 -> 0.2751 ms; identical code for K <= 104)
+                pf = os.environ.get("GFEDNTM_FWD_STRIP_PF", "3")
                 if pf == "1":
                     m.stage_flags |= STAGE_FWD_STRIP_PF
                 elif pf == "2":
                     m.stage_flags |= STAGE_FWD_STRIP_ROLL
+                elif pf == "3":
+                    m.stage_flags |= STAGE_FWD_STRIP_RING
                 m.dec_grid = int(min(m.n_tiles, cu))
             # backward: one workgroup per tile while the tiles fit the resident slots;
             # else persistent, n_dpart d theta_d slabs: with >= 4 k tiles the topics

@@ -85,10 +85,14 @@ def test_step_matches_oracle(model_type, B, n_docs, K, H, V):
                                             (16, 30, 20, (32, 24), 700),      # B = 16, K % 8 = 4
                                             (32, 60, 250, (50,), 5000),       # K = 250 (NP = 32)
                                             (64, 150, 256, (50,), 5000)])     # K = 256, B = 64: forced k split
-def test_strip_forward_matches_oracle(monkeypatch, B, n_docs, K, H, V):
+@pytest.mark.parametrize("pf", ["2", "3"])
+def test_strip_forward_matches_oracle(monkeypatch, pf, B, n_docs, K, H, V):
     """prodlda_fwd_strip_kernel (GFEDNTM_FWD_STRIP=1 forces it): per-wave column strips,
-    beta by buffer loads straight into the MFMA B registers, k paired for ds_read_b64."""
+    beta by buffer loads straight into the MFMA B registers, k paired for ds_read_b64;
+    pf = 2 rolls the next strip's whole beta block through the registers, pf = 3 a
+    13-pair ring (more than 13 pairs: the current strip's later pairs, then the next's)."""
     monkeypatch.setenv("GFEDNTM_FWD_STRIP", "1")
+    monkeypatch.setenv("GFEDNTM_FWD_STRIP_PF", pf)
     from gfedntm_amd.ops.engine import STAGE_FWD_STRIP
     fused, _ = _pair("prodLDA", V=V, K=K, H=H, B=B)
     assert fused.engine._m.stage_flags & STAGE_FWD_STRIP
