@@ -294,7 +294,7 @@ def run_multi(args):
 
 
 def run_federated(args):
-    from gfedntm_amd.federation.runner import run_distributed
+    from gfedntm_amd.federation.runner import CommError, run_distributed
     if args.clients_per_gpu > 1:
         return run_multi(args)
     rank, world, device, rehearse = _init(args)
@@ -308,7 +308,20 @@ def run_federated(args):
               seed=args.seed, graph=not args.no_graph, allreduce=args.allreduce,
               rehearse_1gpu=rehearse)
     # ---- timed: the production round loop ----
-    out = run_distributed(corpus, max_iters=n_rounds, timing_warmup=args.warmup, **kw)
+    fallback = None
+    try:
+        out = run_distributed(corpus, max_iters=n_rounds, timing_warmup=args.warmup, **kw)
+    except CommError as e:
+        # every rank raised the same agreed error: an xGMI wait timed out.  With the data
+        # plane left to auto-selection, measure the same federation over RCCL instead (and
+        # say so in the record) rather than reporting nothing
+        if args.allreduce not in (None, "auto"):
+            raise
+        fallback = f"xGMI all-reduce failed ({e}); re-run over RCCL"
+        if rank == 0:
+            print(f"[bench] {fallback}", file=sys.stderr, flush=True)
+        kw["allreduce"] = "rccl"
+        out = run_distributed(corpus, max_iters=n_rounds, timing_warmup=args.warmup, **kw)
     client = out["client"]
     eng = client.tm.engine
     wall = _max_over_ranks(out["wall_s"], world)
@@ -352,6 +365,8 @@ def run_federated(args):
         record = _record(args, value, ms_runner, terms_n, npmi, final_loss, clients=world,
                          ranks=world, physical=physical)
         record["path"] = args.path
+        if fallback:
+            record["allreduce_fallback"] = fallback
         record["device_ms_per_step"] = None if dev_s is None else round(dev_s / max(timed_rounds, 1) * 1e3, 5)
         record["engine_only_ms_per_step"] = None if engine_ms is None else round(engine_ms, 5)
         record["engine_only_device_ms_per_step"] = (None if engine_dev_ms is None

@@ -388,10 +388,19 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
 
     ``timing_warmup``: the first rounds (after ``start``) are excluded from the
     reported wall time (bench).  ``round_hook(it)`` is called after every round
-    (tests inject host stalls with it)."""
+    (tests inject host stalls with it).  ``GFEDNTM_INJECT_STALL=rank:round:seconds``
+    injects one such stall from the environment (failure-injection tests of processes
+    this code does not start itself, e.g. bench.py's ranks)."""
     import torch.distributed as dist
     logger = logger or logging.getLogger("gfedntm_amd.federation")
     rank, world = dist.get_rank(), dist.get_world_size()
+    inj = os.environ.get("GFEDNTM_INJECT_STALL")
+    if inj and round_hook is None:
+        r_s, it_s, sec_s = inj.split(":")
+        if int(r_s) == rank:
+            def round_hook(it, _at=int(it_s), _sec=float(sec_s)):
+                if it == _at:
+                    time.sleep(_sec)
     data_backend = data_backend or dist.get_backend()
     rehearse = rehearsal_enabled() if rehearse_1gpu is None else bool(rehearse_1gpu)
     ctrl = dist.new_group(backend="gloo") if data_backend != "gloo" else None

@@ -200,3 +200,23 @@ def test_more_clients_than_ranks_xgmi_matches_grouped_golden(tmp_path):
             np.testing.assert_array_equal(sh, gold)
     for i in range(1, N_MULTI + 1):
         assert os.path.exists(tmp_path / f"client{i}" / f"model_{i}_20240101.npz")
+
+
+def test_bench_falls_back_to_rccl_when_xgmi_times_out(tmp_path):
+    """bench.py (2 ranks on the one GPU): an injected host stall longer than the xGMI spin
+    bound makes every rank raise CommError in the timed region; with the data plane on
+    auto-selection the bench re-measures the same federation over RCCL and records why,
+    instead of printing no number."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, GFEDNTM_REHEARSE_1GPU="1", GFEDNTM_XGMI_SPIN="2000",
+               GFEDNTM_INJECT_STALL="1:8:2.0")
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "20",
+                        "--warmup", "5", "--no-npmi"], cwd=root, env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    rec = json.loads(p.stdout.strip().splitlines()[-1])
+    assert "xGMI all-reduce failed" in rec["allreduce_fallback"]
+    assert rec["value"] > 0 and rec["ranks"] == 2
