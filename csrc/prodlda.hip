@@ -872,14 +872,28 @@ __device__ __forceinline__ void prodlda_bwd_body(const GfkModel& m) {
     }
   };
   float rm_[RU], rv_[RU];                       // (RW) row-wise Adam state of this thread
+  // (RW) the row-wise epilogue's beta / m / v / gradient traffic through buffer descriptors:
+  // one column offset per tile (columns past V: an offset outside the descriptor, so loads
+  // return 0 and stores are dropped -- beta's rows need no padding here) and a row offset
+  // per element; element rows are wave-uniform (row = kb + wave + RPU u), checked by a
+  // scalar branch.  Replaces a 64-bit address + bounds branch per element.
+  const int nrec = K * m.ldb * 4;               // (K ldb 4 < 0x7FFF0000: the launcher)
+  const __amdgpu_buffer_rsrc_t rs_b = __builtin_amdgcn_make_buffer_rsrc((void*)m.beta, 0, nrec, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_m = __builtin_amdgcn_make_buffer_rsrc((void*)(m.beta + m.off_m), 0, nrec, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_v = __builtin_amdgcn_make_buffer_rsrc((void*)(m.beta + m.off_v), 0, nrec, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_g = __builtin_amdgcn_make_buffer_rsrc((void*)(m.beta + m.off_g), 0, nrec, 0x00020000);
+  auto rw_col = [&](int tile) {                 // byte offset of this thread's column
+    const int c = tile * VB + (tid & (VB - 1));
+    return c < V ? c * 4 : 0x7FFF0000;
+  };
   auto issue_state_rw = [&](int tile) {
-    const int c = min(tile * VB + (tid & (VB - 1)), V - 1);
+    const int vcol = rw_col(tile);
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
       const int k = min(kb + tid / VB + RPU * u, K - 1);
-      const float* p = m.beta + (size_t)k * m.ldb + c;
-      rm_[u] = p[m.off_m];
-      rv_[u] = p[m.off_v];
+      const int vo = vcol + k * m.ldb * 4;
+      rm_[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_m, vo, 0, 0));
+      rv_[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_v, vo, 0, 0));
     }
   };
   // this workgroup's d theta_d partial, per lane (summed over its tiles in order)
@@ -1135,24 +1149,24 @@ __device__ __forceinline__ void prodlda_bwd_body(const GfkModel& m) {
       lds_barrier();
       // per thread: one column, rows kl0 + RPU u (RPU a multiple of 8, so the row's
       // XOR swizzle is the same for all u); the row pointer advances by RPU rows
-      const int cl = tid & (VB - 1), kl0 = tid / VB, c = c0 + cl;
+      const int cl = tid & (VB - 1), kl0 = tid / VB;
       const int cs = cl ^ ((kl0 & 4) << 2);
-      float* p0 = m.beta + (size_t)(kb + kl0) * m.ldb + c;
+      const int vcol = rw_col(tile);
 #pragma unroll
       for (int u = 0; u < RU; ++u) {
         const int kl = kl0 + RPU * u, k = kb + kl;
-        if (kl >= 16 * nks || k >= K || c >= V) continue;
+        if (kl >= 16 * nks || k >= K) continue;   // (wave-uniform)
         const float g = zt[kl * VB + cs];
-        float* p = p0 + (size_t)(RPU * u) * m.ldb;
+        const int off = vcol + k * m.ldb * 4;
         if (!fused) {
-          p[m.off_g] = g;
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(g), rs_g, off, 0, 0);
         } else {
           float mo = rm_[u], vo = rv_[u];
           float np = adam_update(bt[kl * LDB_B + cl], g, mo, vo, ac);
           if (beta_shared && m.fed_scale_on) np *= m.fed_scale;
-          p[m.off_m] = mo;
-          p[m.off_v] = vo;
-          *p = np;
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mo), rs_m, off, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vo), rs_v, off, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(np), rs_b, off, 0, 0);
         }
       }
     }
@@ -1643,6 +1657,7 @@ static void launch_bwd(const GfkModel* m, hipStream_t s) {
 
 extern "C" int gfk_launch_prodlda_bwd(const GfkModel* m, hipStream_t s) {
   if (m->bmax != 16 && m->bmax != 32 && m->bmax != 64 && m->bmax != 128) return -1;
+  if ((int64_t)m->K * m->ldb * 4 >= 0x7FFF0000LL) return -1;   // 32-bit buffer offsets
   switch ((m->K + 63) / 64) {
     case 1: launch_bwd<1>(m, s); break;
     case 2: launch_bwd<2>(m, s); break;
