@@ -183,6 +183,7 @@ __device__ __forceinline__ void vector_job(const GfkModel& m, const GfkVJob& J) 
 // (one round, issued first); Adam (+ FedAvg pre-scale) or the gradient store follows.
 // More entries than CAP are taken in passes of CAP (each thread's sums stay in registers).
 constexpr int WIN_SPARSE = 16;
+constexpr int WIN_BATCH8 = 512;
 template <int UT>
 __device__ __forceinline__ void win_tile_sparse(const GfkModel& m, float* smem, int tile) {
   constexpr int CAP = 512;
@@ -902,8 +903,10 @@ extern "C" int gfk_launch_win_update(const GfkModel* m, const GfkUpdate* u, hipS
     return (int)hipGetLastError();
   }
   const dim3 g(m->n_tiles + u->n_w + u->n_v + 1 + extra);
-  // more W_in tiles than two rounds of 16-wave workgroups (dec_grid = the CUs' slots)
-  if (m->n_tiles > 2 * m->dec_grid && m->n_tiles > 512)
+  // more W_in tiles than two rounds of 16-wave workgroups (dec_grid = the CUs' slots), or the
+  // batched launch of several clients' tiles asks for the 8-wave shape (stage_flags bit 9,
+  // set by BatchedSteps when all clients' tiles together exceed two rounds)
+  if ((m->n_tiles > 2 * m->dec_grid && m->n_tiles > 512) || (m->stage_flags & WIN_BATCH8))
     do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_win_update_k<512, true>), gfk_grid(g, m), dim3(512), gfk_win_update_smem(m), s, GfkArgT<true>{gfk_dev(m)}, GfkUArgT<true>{reinterpret_cast<const GfkUpdate*>(m->dev_upd)}); else hipLaunchKernelGGL((gfk_win_update_k<512, false>), g, dim3(512), gfk_win_update_smem(m), s, GfkArgT<false>{*m}, GfkUArgT<false>{*u}); } while (0);
   else
     do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_win_update_k<1024, true>), gfk_grid(g, m), dim3(1024), gfk_win_update_smem(m), s, GfkArgT<true>{gfk_dev(m)}, GfkUArgT<true>{reinterpret_cast<const GfkUpdate*>(m->dev_upd)}); else hipLaunchKernelGGL((gfk_win_update_k<1024, false>), g, dim3(1024), gfk_win_update_smem(m), s, GfkArgT<false>{*m}, GfkUArgT<false>{*u}); } while (0);

@@ -60,6 +60,7 @@ STAGE_CTX_FULL = 32               # bit 5: CombinedTM forward, one workgroup per
 STAGE_FWD_STRIP_ROLL = 64         # bit 6: the strip forward's rolling-prefetch variant
 STAGE_WIN_SPLIT = 128             # bit 7: split W_in update (csrc/update.hip gfk_win_dense_k)
 STAGE_FWD_STRIP_RING = 256        # bit 8: the strip forward's ring-prefetch variant (PF = 3)
+STAGE_WIN_BATCH8 = 512            # bit 9: batched launches: win_update's 8-wave tile shape
 
 
 def _explain(ok: bool, why: str, explain: bool) -> bool:
@@ -1336,6 +1337,7 @@ class BatchedSteps:
         self._host = None
         self._phases = e0.phases()
         self._side = (torch.cuda.Stream(self.device), torch.cuda.Event(), torch.cuda.Event())
+        self._cu = torch.cuda.get_device_properties(self.device).multi_processor_count
 
     @staticmethod
     def possible(engines) -> bool:
@@ -1374,6 +1376,18 @@ class BatchedSteps:
         for e in self.engines:
             mm = abi.GfkModel.from_buffer_copy(bytes(e._m))
             mm.dev, mm.dev_upd, mm.n_batch = self._arr_m.data_ptr(), self._arr_u.data_ptr(), M
+            # the strip forward: with M clients' tiles in one launch the 16-wave variant (one
+            # workgroup per CU) runs M dec_grid workgroups in rounds; the 8-wave prefetching
+            # variant fits two per CU (GFEDNTM_BATCH_STRIP_PF=0 keeps the engines' choice)
+            if (mm.stage_flags & STAGE_FWD_STRIP and M * mm.dec_grid > self._cu
+                    and os.environ.get("GFEDNTM_BATCH_STRIP_PF", "1") != "0"):
+                mm.stage_flags = (mm.stage_flags & ~(STAGE_FWD_STRIP_ROLL | STAGE_FWD_STRIP_RING)) \
+                    | STAGE_FWD_STRIP_PF
+            # win_update: all clients' W_in tiles in one launch -> the 8-wave tile shape once
+            # they exceed two rounds of 16-wave workgroups (GFEDNTM_BATCH_WIN8=0: off)
+            if (M * (mm.n_tiles + 8) > 2 * self._cu
+                    and os.environ.get("GFEDNTM_BATCH_WIN8", "1") != "0"):
+                mm.stage_flags |= STAGE_WIN_BATCH8
             ms.append(bytes(mm))
             us.append(bytes(e._u))
         blob = b"".join(ms) + b"".join(us)

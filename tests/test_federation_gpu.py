@@ -221,3 +221,32 @@ def test_batched_round_matches_branch_round(model_type):
     d.run()
     for x, y in zip(c.clients, d.clients):
         assert torch.equal(x.tm.flat.buffer, y.tm.flat.buffer)
+
+
+def test_batched_large_round_variants_match_branch_round():
+    """8 clients at the headline's vocabulary (70 tiles each): the batched launch switches
+    the strip forward to its 8-wave variant and win_update to its 8-wave tile shape (all
+    clients' tiles exceed two rounds of 16-wave workgroups).  The round must still agree
+    with the per-client branch round within fp32 rounding."""
+    from gfedntm_amd.ops.engine import STAGE_FWD_STRIP_PF, STAGE_WIN_BATCH8
+    sc = generate_synthetic(vocab_size=5000, n_topics=50, n_docs=1000, n_nodes=8, frozen_topics=5,
+                            nwords=(150, 250), seed=13)
+    corpora = [ClientCorpus(synthetic=sc, node=i) for i in range(8)]
+    kw = dict(device="cuda", backend="fused", seed=4)
+    p = _params(batch_size=64, n_components=50)
+    a = LocalFederation(corpora, p, max_iters=1, round_batched=True, **kw)
+    b = LocalFederation(corpora, p, max_iters=1, round_batched=False, **kw)
+    a.run()
+    b.run()
+    assert a._batched is not None
+    host = a._batched._host
+    cu = torch.cuda.get_device_properties(0).multi_processor_count
+    assert 8 * host.dec_grid > cu and 8 * (host.n_tiles + 8) > 2 * cu, (host.n_tiles, host.dec_grid)
+    assert host.stage_flags & STAGE_FWD_STRIP_PF and host.stage_flags & STAGE_WIN_BATCH8
+    lr = a.clients[0].tm.engine.lr
+    for x, y in zip(a.clients, b.clients):
+        diff = (x.tm.flat.buffer - y.tm.flat.buffer).abs()
+        assert float(diff.max()) <= 2.5 * lr
+        assert int((diff > 1e-5).sum()) <= 0.01 * diff.numel()
+        torch.testing.assert_close(x.tm.engine.loss_hist[:1], y.tm.engine.loss_hist[:1],
+                                   rtol=1e-6, atol=1e-3)
