@@ -58,6 +58,9 @@ __host__ __device__ __forceinline__ int zswz(int row) { return (row & 15) << 1; 
 constexpr float RL_EPS = 1e-10f;
 
 __host__ __device__ __forceinline__ int round_up(int x, int m) { return (x + m - 1) / m * m; }
+// byte offset sum for buffer voffsets: unsigned (wrapping) arithmetic, since an out-of-range
+// marker (0x7FFF0000) plus a row / column offset exceeds INT_MAX
+__device__ __forceinline__ int boff(int a, int b) { return (int)((unsigned)a + (unsigned)b); }
 
 // sum over the 4 lane groups (lanes l, l^16, l^32, l^48): a column reduction
 __device__ __forceinline__ float sum_groups(float v) {
@@ -891,7 +894,7 @@ __device__ __forceinline__ void prodlda_bwd_body(const GfkModel& m) {
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
       const int k = min(kb + tid / VB + RPU * u, K - 1);
-      const int vo = vcol + k * m.ldb * 4;
+      const int vo = boff(vcol, k * m.ldb * 4);
       rm_[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_m, vo, 0, 0));
       rv_[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_v, vo, 0, 0));
     }
@@ -1157,7 +1160,7 @@ __device__ __forceinline__ void prodlda_bwd_body(const GfkModel& m) {
         const int kl = kl0 + RPU * u, k = kb + kl;
         if (kl >= 16 * nks || k >= K) continue;   // (wave-uniform)
         const float g = zt[kl * VB + cs];
-        const int off = vcol + k * m.ldb * 4;
+        const int off = boff(vcol, k * m.ldb * 4);
         if (!fused) {
           __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(g), rs_g, off, 0, 0);
         } else {
@@ -1321,7 +1324,7 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
       dr[j] = f32x4{__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), __uint_as_float(x.w)};
     }
 #pragma unroll
-    for (int u = 0; u < RU; ++u) br[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_b, vc + rowoff[u], 0, 0));
+    for (int u = 0; u < RU; ++u) br[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_b, boff(vc, rowoff[u]), 0, 0));
   };
   // Adam state (fused mode only)
   auto issue_mv = [&](int tile, float (&rm)[RU], float (&rv)[RU]) __attribute__((always_inline)) {
@@ -1329,8 +1332,8 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
       const int vc = tile * VB * 4 + lane4;
 #pragma unroll
       for (int u = 0; u < RU; ++u) {
-        rm[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_m, vc + rowoff[u], 0, 0));
-        rv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_v, vc + rowoff[u], 0, 0));
+        rm[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_m, boff(vc, rowoff[u]), 0, 0));
+        rv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_v, boff(vc, rowoff[u]), 0, 0));
       }
     }
   };
@@ -1464,12 +1467,12 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
         float mo = rm[u], vo = rv[u];
         float np = adam_update(btp[RPU * u * LDP], gv, mo, vo, ac);
         if (beta_shared && m.fed_scale_on) np *= m.fed_scale;
-        const int vo4 = vc + rowoff[u];
+        const int vo4 = boff(vc, rowoff[u]);
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mo), rs_m, vo4, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vo), rs_v, vo4, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(np), rs_b, vo4, 0, 0);
       } else {                                 // the gradient (rs_m is the gradient slot)
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gv), rs_m, vc + rowoff[u], 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gv), rs_m, boff(vc, rowoff[u]), 0, 0);
       }
     }
   };

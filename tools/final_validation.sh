@@ -11,7 +11,7 @@ run() {  # name limit args...
   grep '^{' "$o/$n.log" > "$o/bench_$n.jsonl"
   python -c "import json,sys; r=json.loads(open('$o/bench_$n.jsonl').read().splitlines()[-1]); print('$n', r['config']['model'], r['dtype'], r['ms_per_step'], r['value'])"
 }
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 280 --timeout-method thread \
     -p no:cacheprovider > "$o/gpu_tests.log" 2>&1 || { tail -30 "$o/gpu_tests.log"; exit 1; }
 tail -n 1 "$o/gpu_tests.log" | tee "$o/gpu_tests.txt"
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" 2>&1 | tail -n 1 || exit 1
