@@ -1,6 +1,6 @@
 # round-3 sweep on the final kernels: every README configuration, one bench.py line each
 set -o pipefail
-o=gpurun_out/g27; mkdir -p $o; export TMPDIR=/tmp
+o=gpurun_out/sweep; mkdir -p $o; export TMPDIR=/tmp
 r() { local n="$1"; shift; timeout -k 10 240 python bench.py "$@" > $o/$n.log 2>&1 || return $?; python -c "import json;r=json.loads(open('$o/$n.log').read().strip().splitlines()[-1]);print('$n', r['ms_per_step'], r.get('device_ms_per_step'), r['value'], r.get('npmi'))"; }
 r k50 --steps 2000 --warmup 200 || exit $?
 r lda --model LDA --steps 2000 --warmup 200 --no-npmi || exit $?
