@@ -632,8 +632,11 @@ __device__ __forceinline__ void mfma_gemm(int M, int N, int R, const MatView& A,
 // dependent reads (step -> plan -> doc -> indptr) that runs in an extra
 // workgroup of win_update, off the critical path, so the next enc_in starts one
 // round trip from its data.  Rows past the batch repeat its first doc.
-__device__ __forceinline__ void prepare_next_batch(const GfkModel& m) {
-  __shared__ int pnb_e[2 * 128];       // (e0, e1) of the next batch's rows (bmax <= 128)
+// pnb_e: 2 * 128 ints of LDS, the (e0, e1) of the next batch's rows (bmax <= 128) -- the
+// caller's dynamic LDS where it has some, so the win_update kernels carry no static LDS on
+// top of their dynamic budget (40 KB + 1 KB would cost the sparse tile its 4th workgroup
+// per CU)
+__device__ __forceinline__ void prepare_next_batch(const GfkModel& m, int* pnb_e) {
   const int step = *m.step;
   int32_t* nxt = m.ws_next;
   if (step >= m.n_steps) {
@@ -696,6 +699,11 @@ __device__ __forceinline__ void prepare_next_batch(const GfkModel& m) {
       }
     }
   }
+}
+
+__device__ __forceinline__ void prepare_next_batch(const GfkModel& m) {
+  __shared__ int pnb_e[2 * 128];
+  prepare_next_batch(m, pnb_e);
 }
 
 

@@ -184,7 +184,11 @@ __device__ __forceinline__ void vector_job(const GfkModel& m, const GfkVJob& J) 
 // More entries than CAP are taken in passes of CAP (each thread's sums stay in registers).
 constexpr int WIN_SPARSE = 16;
 constexpr int WIN_BATCH8 = 512;
-template <int UT>
+// VL: the second moment goes through LDS (one LDS-DMA copy of the block, issued with the
+// other staging loads) instead of 2 quads of registers per thread, so the tile fits 64
+// VGPRs and 4 workgroups per CU (fused mode; the launcher picks it when the block fits the
+// kernel's existing LDS budget)
+template <int UT, bool VL = false>
 __device__ __forceinline__ void win_tile_sparse(const GfkModel& m, float* smem, int tile) {
   constexpr int CAP = 512;
   constexpr int TPR = UT / 64;                 // threads per row, 64 rows per pass
@@ -196,6 +200,7 @@ __device__ __forceinline__ void win_tile_sparse(const GfkModel& m, float* smem, 
   int* ecol = reinterpret_cast<int*>(dz + B * H0);   // [CAP] (row << 8) | local column
   float* ex = reinterpret_cast<float*>(ecol + CAP);  // [CAP]
   int* offs = reinterpret_cast<int*>(ex + CAP);      // [129] rows' first slots, total
+  float* vb = smem + ((B * H0 + 2 * CAP + 129 + 3) & ~3);  // VL: [64 * H0] second moment
   float* wblk = m.w_in + (size_t)c0 * H0;
   const int nel = (min(V, c0 + 64) - c0) * H0;
   const bool fused = m.update_mode == 1;
@@ -227,12 +232,27 @@ __device__ __forceinline__ void win_tile_sparse(const GfkModel& m, float* smem, 
     cnt[i] = wave == 0 ? tst[(size_t)r * ntp + tile + 1] - tst[(size_t)r * ntp + tile] : 0;
   }
   __builtin_amdgcn_sched_barrier(0);
-  f32x4 pp[FQ], pm[FQ], pv[FQ];
+  f32x4 pp[FQ], pm[FQ], pv[VL ? 1 : FQ];
 #pragma unroll
   for (int u = 0; u < FQ; ++u) {
     const int e = 4 * (tid + UT * u);
-    pp[u] = pm[u] = pv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (fused && e < nel) { pp[u] = ld4(wblk, e); pm[u] = ld4(wblk + m.off_m, e); pv[u] = ld4(wblk + m.off_v, e); }
+    pp[u] = pm[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (!VL) pv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (fused && e < nel) {
+      pp[u] = ld4(wblk, e);
+      pm[u] = ld4(wblk + m.off_m, e);
+      if constexpr (!VL) pv[u] = ld4(wblk + m.off_v, e);
+    }
+  }
+  if constexpr (VL) {
+    if (!fused) {
+    } else if (al4) {
+      const int n4 = nel & ~3;
+      glds_copy(vb, wblk + m.off_v, n4, tid, UT);
+      if (tid < nel - n4) vb[n4 + tid] = wblk[m.off_v + n4 + tid];
+    } else {
+      for (int e = tid; e < nel; e += UT) vb[e] = wblk[m.off_v + e];
+    }
   }
   glds_copy(dz, m.ws_dz[0], B * H0, tid, UT);
   __builtin_amdgcn_sched_barrier(0);
@@ -275,31 +295,8 @@ __device__ __forceinline__ void win_tile_sparse(const GfkModel& m, float* smem, 
   f32x4 g[FQ];
 #pragma unroll
   for (int u = 0; u < FQ; ++u) g[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int p0 = 0; p0 < total; p0 += CAP) {
-    if (p0) __syncthreads();                   // the previous pass's list reads are done
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int r = tid / TPR + 64 * i;
-      if (r >= nb) continue;
-      const int o = offs[r] - xe0[i];
-      int e = xe0[i] + sub;
-      if (e < xe1[i]) {                        // the first entry: already in registers
-        const int s = o + e - p0;
-        if (s >= 0 && s < CAP) {
-          ecol[s] = (r << 8) | (fi[i] - c0);
-          ex[s] = fv[i];
-        }
-      }
-      for (e += TPR; e < xe1[i]; e += TPR) {   // (rows with more than TPR entries here)
-        const int s = o + e - p0;
-        if (s >= 0 && s < CAP) {
-          ecol[s] = (r << 8) | (m.indices[e] - c0);
-          ex[s] = m.values[e];
-        }
-      }
-    }
-    __syncthreads();
-    const int n = min(CAP, total - p0);
+  // the list sums of one pass (fixed order: slots ascending)
+  auto sums = [&](int n) {
     for (int j = 0; j < n; ++j) {
       const int cb = ecol[j];
       const float x = ex[j];
@@ -317,6 +314,45 @@ __device__ __forceinline__ void win_tile_sparse(const GfkModel& m, float* smem, 
         }
       }
     }
+  };
+  // pass 0 from the staged registers (the first entries are already loaded); later passes
+  // (more than CAP entries in the tile) re-read the rows' extents, so neither the extents
+  // nor the first entries stay live across the sums
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = tid / TPR + 64 * i;
+    if (r >= nb) continue;
+    const int o = offs[r] - xe0[i];
+    int e = xe0[i] + sub;
+    if (e < xe1[i] && o + e < CAP) {
+      ecol[o + e] = (r << 8) | (fi[i] - c0);
+      ex[o + e] = fv[i];
+    }
+    for (e += TPR; e < xe1[i] && o + e < CAP; e += TPR) {   // (rows with more than TPR entries)
+      ecol[o + e] = (r << 8) | (m.indices[e] - c0);
+      ex[o + e] = m.values[e];
+    }
+  }
+  __syncthreads();
+  sums(min(CAP, total));
+  for (int p0 = CAP; p0 < total; p0 += CAP) {
+    __syncthreads();                           // the previous pass's list reads are done
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = tid / TPR + 64 * i;
+      if (r >= nb) continue;
+      const int a0 = tst[(size_t)r * ntp + tile], a1 = tst[(size_t)r * ntp + tile + 1];
+      const int o = offs[r] - a0;
+      for (int e = a0 + sub; e < a1; e += TPR) {
+        const int s = o + e - p0;
+        if (s >= 0 && s < CAP) {
+          ecol[s] = (r << 8) | (m.indices[e] - c0);
+          ex[s] = m.values[e];
+        }
+      }
+    }
+    __syncthreads();
+    sums(min(CAP, total - p0));
   }
   // ---- update (fused: Adam + FedAvg pre-scale) or the gradient ----
   const AdamCoef ac = adam_coef(m);
@@ -328,7 +364,9 @@ __device__ __forceinline__ void win_tile_sparse(const GfkModel& m, float* smem, 
     f32x4 np, mo, vo;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      float a = pm[u][i], b = pv[u][i];
+      float a = pm[u][i], b;
+      if constexpr (VL) b = e + i < nel ? vb[e + i] : 0.f;
+      else b = pv[u][i];
       const float x = fused ? adam_update(pp[u][i], g[u][i], a, b, ac) : g[u][i];
       np[i] = sh && m.fed_scale_on && fused ? x * m.fed_scale : x;
       mo[i] = a;
@@ -618,7 +656,7 @@ __global__ void __launch_bounds__(UT) gfk_win_update_k(GfkArgT<GB> ga, GfkUArgT<
     const int r = (int)blockIdx.x - nt_here;
     if (r >= 0 && r < U.n_w) { weight_job<UT>(m, U.w[r], smem); return; }
     if (r >= U.n_w && r < U.n_w + U.n_v) { vector_job<UT>(m, U.v[r - U.n_w]); return; }
-    if (r == U.n_w + U.n_v) { prepare_next_batch(m); return; }
+    if (r == U.n_w + U.n_v) { prepare_next_batch(m, reinterpret_cast<int*>(smem)); return; }
   }
   const bool zs = m.ctx_fused == 2;            // ZeroShotTM: W_in is the dense [C, H0] layer
   if (m.input == GFK_IN_CONTEXTUAL && !zs) return;   // (host GEMMs when not fused)
@@ -853,16 +891,16 @@ __global__ void __launch_bounds__(UT) gfk_win_update_k(GfkArgT<GB> ga, GfkUArgT<
 // its own (the job paths of gfk_win_update_k need ~86 VGPRs)
 // grid: n_w + n_v + 1 job workgroups FIRST (they start with the tiles, not after them),
 // then the n_tiles sparse W_in tiles
-template <int UT, bool GB = false>
-__global__ void __launch_bounds__(UT) gfk_win_sparse_k(GfkArgT<GB> ga, GfkUArgT<GB> gua) {
+template <int UT, bool GB = false, bool VL = false>
+__global__ void __launch_bounds__(UT, VL ? 4096 / UT : 1) gfk_win_sparse_k(GfkArgT<GB> ga, GfkUArgT<GB> gua) {
   const GfkModel& m = gfk_model(ga);
   const GfkUpdate& U = gfk_upd(gua);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int r = (int)blockIdx.x;
   if (r < U.n_w) { weight_job<UT>(m, U.w[r], smem); return; }
   if (r < U.n_w + U.n_v) { vector_job<UT>(m, U.v[r - U.n_w]); return; }
-  if (r == U.n_w + U.n_v) { prepare_next_batch(m); return; }
-  win_tile_sparse<UT>(m, smem, r - (U.n_w + U.n_v + 1));
+  if (r == U.n_w + U.n_v) { prepare_next_batch(m, reinterpret_cast<int*>(smem)); return; }
+  win_tile_sparse<UT, VL>(m, smem, r - (U.n_w + U.n_v + 1));
 }
 
 // the split update's sparse half: the same job workgroups, then the batch words' tiles (its
@@ -875,7 +913,7 @@ __global__ void __launch_bounds__(UT) gfk_win_rows_k(GfkArgT<GB> ga, GfkUArgT<GB
   const int r = (int)blockIdx.x;
   if (r < U.n_w) { weight_job<UT>(m, U.w[r], smem); return; }
   if (r < U.n_w + U.n_v) { vector_job<UT>(m, U.v[r - U.n_w]); return; }
-  if (r == U.n_w + U.n_v) { prepare_next_batch(m); return; }
+  if (r == U.n_w + U.n_v) { prepare_next_batch(m, reinterpret_cast<int*>(smem)); return; }
   win_tile_sparse_rows<UT>(m, smem, r - (U.n_w + U.n_v + 1));
 }
 
@@ -891,6 +929,17 @@ extern "C" int gfk_launch_win_dense(const GfkModel* m, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// the sparse tile's LDS second-moment variant: fused mode, and the block fits the LDS the
+// kernel is given anyway (gfk_win_update_smem: no occupancy lost to LDS).  stage_flags
+// bit 10 (GFEDNTM_WIN_VL=0) keeps the register variant.
+constexpr int WIN_VREG = 1024;
+static bool win_sparse_vl(const GfkModel* m) {
+  if ((m->stage_flags & WIN_VREG) || m->update_mode != 1) return false;
+  const size_t need = sizeof(float) * ((((size_t)m->bmax * m->H[0] + 2 * 512 + 129 + 3) & ~(size_t)3) +
+                                       (size_t)64 * m->H[0]);
+  return need <= gfk_win_update_smem(m);
+}
+
 extern "C" int gfk_launch_win_update(const GfkModel* m, const GfkUpdate* u, hipStream_t s) {
   const int extra = m->ctx_fused == 1 ? m->n_tiles : (m->ctx_fused == 2 ? (m->C + 63) / 64 : 0);
   if (m->stage_flags & WIN_SPARSE) {
@@ -898,6 +947,8 @@ extern "C" int gfk_launch_win_update(const GfkModel* m, const GfkUpdate* u, hipS
     const dim3 gs(u->n_w + u->n_v + 1 + m->n_tiles);
     if (m->stage_flags & GFK_WIN_SPLIT)
       do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_win_rows_k<512, true>), gfk_grid(gs, m), dim3(512), gfk_win_update_smem(m), s, GfkArgT<true>{gfk_dev(m)}, GfkUArgT<true>{reinterpret_cast<const GfkUpdate*>(m->dev_upd)}); else hipLaunchKernelGGL((gfk_win_rows_k<512, false>), gs, dim3(512), gfk_win_update_smem(m), s, GfkArgT<false>{*m}, GfkUArgT<false>{*u}); } while (0);
+    else if (win_sparse_vl(m))
+      do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_win_sparse_k<512, true, true>), gfk_grid(gs, m), dim3(512), gfk_win_update_smem(m), s, GfkArgT<true>{gfk_dev(m)}, GfkUArgT<true>{reinterpret_cast<const GfkUpdate*>(m->dev_upd)}); else hipLaunchKernelGGL((gfk_win_sparse_k<512, false, true>), gs, dim3(512), gfk_win_update_smem(m), s, GfkArgT<false>{*m}, GfkUArgT<false>{*u}); } while (0);
     else
       do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_win_sparse_k<512, true>), gfk_grid(gs, m), dim3(512), gfk_win_update_smem(m), s, GfkArgT<true>{gfk_dev(m)}, GfkUArgT<true>{reinterpret_cast<const GfkUpdate*>(m->dev_upd)}); else hipLaunchKernelGGL((gfk_win_sparse_k<512, false>), gs, dim3(512), gfk_win_update_smem(m), s, GfkArgT<false>{*m}, GfkUArgT<false>{*u}); } while (0);
     return (int)hipGetLastError();
@@ -922,6 +973,7 @@ extern "C" int gfk_win_update_set_smem(size_t bytes) {
   const void* ks[] = {(const void*)gfk_win_update_k<512, false>, (const void*)gfk_win_update_k<512, true>,
                       (const void*)gfk_win_update_k<1024, false>, (const void*)gfk_win_update_k<1024, true>,
                       (const void*)gfk_win_sparse_k<512, false>, (const void*)gfk_win_sparse_k<512, true>,
+                      (const void*)gfk_win_sparse_k<512, false, true>, (const void*)gfk_win_sparse_k<512, true, true>,
                       (const void*)gfk_win_rows_k<512, false>, (const void*)gfk_win_rows_k<512, true>};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);

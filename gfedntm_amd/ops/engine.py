@@ -61,6 +61,7 @@ STAGE_FWD_STRIP_ROLL = 64         # bit 6: the strip forward's rolling-prefetch 
 STAGE_WIN_SPLIT = 128             # bit 7: split W_in update (csrc/update.hip gfk_win_dense_k)
 STAGE_FWD_STRIP_RING = 256        # bit 8: the strip forward's ring-prefetch variant (PF = 3)
 STAGE_WIN_BATCH8 = 512            # bit 9: batched launches: win_update's 8-wave tile shape
+STAGE_WIN_VREG = 1024             # bit 10: sparse W_in tiles keep the second moment in registers
 
 
 def _explain(ok: bool, why: str, explain: bool) -> bool:
@@ -561,6 +562,10 @@ class FusedEngine(EngineBase):
         if m.input == abi.IN_BOW and int(m.H[0]) <= 64 and m.bmax <= 128 and (
                 ws_env == "1" or (ws_env == "auto" and m.n_tiles > 4 * cu_n)):
             m.stage_flags |= STAGE_WIN_SPARSE
+            # fused mode: the tile's second moment goes through LDS (64 VGPRs, 4 workgroups
+            # per CU; profiles/r3/win_vl/); GFEDNTM_WIN_VL=0 keeps it in registers
+            if os.environ.get("GFEDNTM_WIN_VL", "1") == "0":
+                m.stage_flags |= STAGE_WIN_VREG
             # split W_in update (GFEDNTM_WIN_SPLIT=1, fused mode): the words not in the batch
             # (~89 % at V = 112k) get their zero-gradient Adam step from gfk_win_dense_k on a
             # side stream from the start of the step; the sparse tiles then move only the

@@ -718,7 +718,8 @@ def test_ctm_host_gemm_fallback_matches_oracle(model_type):
 
 @pytest.mark.parametrize("model_type", ["prodLDA", "LDA"])
 @pytest.mark.parametrize("B,n_docs,K,H,V", [(64, 80, 50, (50, 50), 3000), (128, 200, 20, (64,), 9000),
-                                            (32, 45, 20, (30, 20), 20000)])
+                                            (32, 45, 20, (30, 20), 20000),
+                                            (128, 160, 20, (32,), 300)])   # > 512 entries per tile: list passes
 def test_sparse_win_tiles_match_oracle(monkeypatch, model_type, B, n_docs, K, H, V):
     """W_in tiles as entry lists (GFEDNTM_WIN_SPARSE=1 forces the large-vocabulary path,
     csrc/update.hip win_tile_sparse) give the oracle's input-layer gradient."""

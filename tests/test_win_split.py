@@ -13,7 +13,8 @@ import torch
 from gfedntm_amd.data.bow import BatchPlan, DeviceCSR
 from gfedntm_amd.models import AVITM
 from gfedntm_amd.ops import kernel_abi as abi
-from gfedntm_amd.ops.engine import STAGE_WIN_SPARSE, STAGE_WIN_SPLIT, UPDATE_FUSED, UPDATE_GRAD
+from gfedntm_amd.ops.engine import (STAGE_WIN_SPARSE, STAGE_WIN_SPLIT, STAGE_WIN_VREG, UPDATE_FUSED,
+                                     UPDATE_GRAD)
 from tests.helpers import random_csr
 
 pytestmark = pytest.mark.gpu
@@ -116,3 +117,27 @@ def test_split_batched_clients_match_unsplit(monkeypatch):
         outs.append([c.tm.flat.buffer.clone() for c in fed.clients])
     for x, y in zip(*outs):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("V,K,H,B,n_docs,graph", [
+    (20000, 20, (50, 50), 64, 150, True),
+    (9000, 30, (30, 20), 128, 300, False),     # quads spanning two words
+    (300, 20, (32,), 128, 300, True),          # > 512 entries per tile: several list passes
+])
+def test_lds_second_moment_is_bit_identical(monkeypatch, V, K, H, B, n_docs, graph):
+    """The sparse tile's LDS second-moment variant (the fused-mode default: 64 VGPRs, 4
+    workgroups per CU) against the register variant (GFEDNTM_WIN_VL=0): the same state bit
+    for bit, the FedAvg pre-scale included."""
+    monkeypatch.setenv("GFEDNTM_WIN_VL", "0")
+    a = _make(monkeypatch, "0", "prodLDA", V, K, H, B)
+    monkeypatch.setenv("GFEDNTM_WIN_VL", "1")
+    b = _make(monkeypatch, "0", "prodLDA", V, K, H, B)
+    assert a.engine._m.stage_flags & STAGE_WIN_VREG
+    assert b.engine._m.stage_flags & STAGE_WIN_SPARSE and not b.engine._m.stage_flags & STAGE_WIN_VREG
+    b.model.load_state_dict(a.model.state_dict())
+    b.engine.seed = b.engine._m.seed = a.engine.seed
+    X = random_csr(n_docs, V, 60, seed=5)
+    n_steps = 2 * -(-n_docs // B)
+    for tm in (a, b):
+        _run(tm, X, n_steps, B, graph)
+    _assert_same_state(a, b)
