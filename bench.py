@@ -254,8 +254,8 @@ def _physical_gpus(device, world: int) -> int:
 
 
 def run_multi(args):
-    """M clients per rank (federation/hierarchical.py): the production runner for more
-    clients than GPUs."""
+    """M clients per rank: the production runner (federation/runner.py run_distributed)
+    with a block of clients per rank (federation/rank_round.py MultiClientRound)."""
     from gfedntm_amd.federation.hierarchical import assign_clients, run_distributed_multi
     rank, world, device, rehearse = _init(args)
     _ctrl_group()
@@ -274,6 +274,7 @@ def run_multi(args):
     dist.all_reduce(t, group=_ctrl_group())
     docs = float(t.item())
     eng = out["clients"][0].tm.engine
+    out["round"].close()
     n_rounds = args.warmup + args.steps
     final_loss = float(np.mean(eng.loss_hist[max(0, n_rounds - 20): n_rounds].cpu().numpy()))
     if rank == 0:
@@ -284,7 +285,9 @@ def run_multi(args):
                                      round(dev_s / max(out["timed_rounds"], 1) * 1e3, 5))
         rec["config"]["aggregation"] += (f" (hierarchical: {M} clients per rank folded in-rank, "
                                          f"{out['allreduce'] or 'no'} all-reduce across ranks)")
-        rec["path"] = "run_distributed_multi"
+        rec["path"] = "run_distributed (multi-client ranks)"
+        if out.get("attach"):
+            rec["fedavg_attach"] = out["attach"]
         if rehearse:
             rec["note"] = (f"GFEDNTM_REHEARSE_1GPU: {world} ranks share {physical} GPU -- "
                            "protocol rehearsal, timings meaningless")
@@ -321,6 +324,8 @@ def run_federated(args):
         if rank == 0:
             print(f"[bench] {fallback}", file=sys.stderr, flush=True)
         kw["allreduce"] = "rccl"
+        # a failure injection (tests) belongs to the failed attempt, not the re-measure
+        os.environ.pop("GFEDNTM_INJECT_STALL", None)
         out = run_distributed(corpus, max_iters=n_rounds, timing_warmup=args.warmup, **kw)
     client = out["client"]
     eng = client.tm.engine
@@ -464,6 +469,13 @@ def _metric(args, V, clients: int, ranks: int, physical: int) -> str:
             f"{args.dtype}, {where}, synthetic BoW")
 
 
+def _kernels_hash(args):
+    if args.backend != "fused":
+        return None
+    from gfedntm_amd.ops import native
+    return native.kernels_hash()
+
+
 def _record(args, value, ms, V, npmi, final_loss, clients: int, ranks: int, physical: int):
     hidden = tuple(int(h) for h in args.hidden.split(","))
     fam = {"avitm": "", "ctm": "CombinedTM-", "zeroshot": "ZeroShotTM-"}[args.family]
@@ -502,6 +514,8 @@ def _record(args, value, ms, V, npmi, final_loss, clients: int, ranks: int, phys
         **({"precision": "bf16 operands of the ProdLDA decoder GEMMs (theta.beta, theta^T.dlogit, "
                          "dlogit.beta^T) on v_mfma_f32_16x16x16_bf16, fp32 accumulation; fp32 "
                          "parameters, Adam state and every other op"} if args.dtype == "bf16" else {}),
+        # the source hash embedded in the kernel library that ran (gfedntm_amd/ops/srchash.py)
+        "kernels_src_hash": _kernels_hash(args),
         "npmi": None if npmi is None else round(npmi, 4),
         "npmi_rounds": None if npmi is None else args.npmi_steps,
         "final_loss": final_loss,

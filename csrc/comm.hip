@@ -228,30 +228,38 @@ extern "C" __global__ void __launch_bounds__(CT) gfk_xgmi_allreduce(GfkComm c, f
 //   1  the sum is written to f_0 only (a rank's local partial, before the collective);
 //   2  broadcast: f_0 is copied into f_1 .. f_{n-1} (after the collective).
 // One launch replaces the 2N + 1 eager kernels of a zero / add / copy sequence and is
-// captured into the round graphs.  The pointers are 16-byte aligned; a partial last
-// float4 is handled element-wise.
+// captured into the round graphs.  The client buffers and the group ends come from small
+// DEVICE tables (uploaded once per client set, before any capture), so the number of
+// clients a rank folds is not bounded by the kernel's argument block.  [off, off + n) is
+// the float range folded in every buffer (the whole shared state, or only beta's part
+// when it is reduced ahead of the rest); off is a multiple of 4, the pointers 16-byte
+// aligned, and a partial last float4 is handled element-wise.
 // ---------------------------------------------------------------------------
-constexpr int LMAX = 16;
-
 struct GfkLocalAvg {
-  float* f[LMAX];
+  const uint64_t* f;             // device table [n_clients]: float* of every client's buffer
+  const int32_t* gend;           // device table [n_groups]: exclusive end of each group
+  int64_t off;                   // first float of the folded range
+  int64_t n;                     // floats in the range
   int32_t n_clients;
   int32_t mode;
-  int64_t n;                     // floats
   int32_t n_groups;
-  int32_t gend[LMAX];            // exclusive end of each group (gend[n_groups - 1] = n_clients)
   int32_t pad;
 };
 
 namespace {
 template <class T>
+__device__ __forceinline__ T* lptr(const GfkLocalAvg& a, int j) {
+  return reinterpret_cast<T*>(reinterpret_cast<float*>(a.f[j]) + a.off);
+}
+
+template <class T>
 __device__ __forceinline__ T fold(const GfkLocalAvg& a, int64_t i) {
-  const T* const* f = reinterpret_cast<const T* const*>(a.f);
   T tot{};
   int j = 0;
   for (int g = 0; g < a.n_groups; ++g) {
-    T s = f[j][i];
-    for (++j; j < a.gend[g]; ++j) s = s + f[j][i];
+    const int e = a.gend[g];
+    T s = lptr<const T>(a, j)[i];
+    for (++j; j < e; ++j) s = s + lptr<const T>(a, j)[i];
     tot = g == 0 ? s : tot + s;
   }
   return tot;
@@ -265,28 +273,24 @@ extern "C" __global__ void __launch_bounds__(256) gfk_local_fedavg(GfkLocalAvg a
   const int w1 = a.mode == 1 ? 1 : a.n_clients;     // buffers written
   const int w0 = a.mode == 2 ? 1 : 0;
   for (int64_t i = g; i < n4; i += stride) {
-    const float4 acc = a.mode == 2 ? reinterpret_cast<const float4*>(a.f[0])[i] : fold<float4>(a, i);
-    for (int j = w0; j < w1; ++j) reinterpret_cast<float4*>(a.f[j])[i] = acc;
+    const float4 acc = a.mode == 2 ? lptr<const float4>(a, 0)[i] : fold<float4>(a, i);
+    for (int j = w0; j < w1; ++j) lptr<float4>(a, j)[i] = acc;
   }
   if (g < (a.n & 3)) {           // the partial float4 at the end: nothing past n is touched
     const int64_t i = (n4 << 2) + g;
-    const float acc = a.mode == 2 ? a.f[0][i] : fold<float>(a, i);
-    for (int j = w0; j < w1; ++j) a.f[j][i] = acc;
+    const float acc = a.mode == 2 ? lptr<const float>(a, 0)[i] : fold<float>(a, i);
+    for (int j = w0; j < w1; ++j) lptr<float>(a, j)[i] = acc;
   }
 }
 
 extern "C" size_t gfk_local_avg_struct_size() { return sizeof(GfkLocalAvg); }
 
+// the tables' contents (client count, group ends, pointer alignment) are checked by the
+// caller when it builds them (parallel/aggregator.py _LocalTable)
 extern "C" int gfk_local_fedavg_launch(const GfkLocalAvg* a, int grid, hipStream_t s) {
-  if (a->n_clients < 1 || a->n_clients > LMAX || grid < 1 || a->mode < 0 || a->mode > 2 ||
-      a->n_groups < 1 || a->n_groups > a->n_clients || a->gend[a->n_groups - 1] != a->n_clients)
+  if (a->n_clients < 1 || grid < 1 || a->mode < 0 || a->mode > 2 || a->n_groups < 1 ||
+      a->n_groups > a->n_clients || !a->f || !a->gend || (a->off & 3) || a->off < 0 || a->n < 0)
     return -1;
-  for (int g = 0, e = 0; g < a->n_groups; ++g) {
-    if (a->gend[g] <= e) return -1;
-    e = a->gend[g];
-  }
-  for (int j = 0; j < a->n_clients; ++j)
-    if ((uintptr_t)a->f[j] & 15) return -1;
   hipLaunchKernelGGL(gfk_local_fedavg, dim3(grid), dim3(256), 0, s, *a);
   return (int)hipGetLastError();
 }

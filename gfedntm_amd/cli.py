@@ -161,43 +161,28 @@ def _rank_main(args, cfg) -> dict:
     dist.broadcast_object_list(obj, src=0)
     source = obj[0]
     stamp, save_client, save_server, logs_client, _ = _paths(args, cfg)
-    if n_clients > world:
-        # more clients than ranks: each rank hosts a contiguous block (hierarchical FedAvg)
-        from .federation.hierarchical import assign_clients, run_distributed_multi
-        ids = assign_clients(n_clients, world)[rank]
-        logger = setup_logger(f"gfedntm_amd.rank{rank}", f"{logs_client}{ids[0]}", stamp,
-                              stdout=(rank == 0))
-        corpora = [load_client_corpus(args.data_type, source, i, _client_fos(args, i),
-                                      args.allow_pickle) for i in ids]
-        if args.agg != "params":
-            raise SystemExit("--agg grads with more clients than ranks is not supported")
-        return run_distributed_multi(
-            corpora, ids, cfg.training_params, args.model_type, args.max_iters,
-            backend=args.engine or cfg.backend, grads_to_share=cfg.grads_to_share, seed=args.seed,
-            save_client=save_client, save_server=save_server, logger=logger,
-            graph=cfg.graph and not args.no_graph, log_every=args.log_every,
-            stop_at_num_epochs=args.stop_at_num_epochs or cfg.stop_at_num_epochs,
-            checkpoint_dir=args.checkpoint_dir,
-            checkpoint_every=args.checkpoint_every if args.checkpoint_every is not None
-            else cfg.checkpoint_every, stamp=stamp,
-            metrics_path=os.path.join(f"{logs_client}{ids[0]}", f"metrics_{stamp}.jsonl"),
-            metrics_every=args.metrics_every)
-    cid = rank + 1
-    logger = setup_logger(f"gfedntm_amd.client{cid}", f"{logs_client}{cid}", stamp,
-                          stdout=(rank == 0))
-    corpus = load_client_corpus(args.data_type, source, cid, _client_fos(args, cid), args.allow_pickle)
+    # each rank hosts a contiguous block of clients (one each when N = R; more clients
+    # than ranks: hierarchical FedAvg) -- the same runner either way
+    from .federation.hierarchical import assign_clients
+    ids = assign_clients(n_clients, world)[rank]
+    if len(ids) > 1 and args.agg != "params":
+        raise SystemExit("--agg grads with more clients than ranks is not supported")
+    logger = setup_logger(f"gfedntm_amd.client{ids[0]}" if len(ids) == 1 else f"gfedntm_amd.rank{rank}",
+                          f"{logs_client}{ids[0]}", stamp, stdout=(rank == 0))
+    corpora = [load_client_corpus(args.data_type, source, i, _client_fos(args, i), args.allow_pickle)
+               for i in ids]
     return run_distributed(
-        corpus, cfg.training_params, args.model_type, args.max_iters,
-        backend=args.engine or cfg.backend, grads_to_share=cfg.grads_to_share, seed=args.seed,
-        save_client=save_client, save_server=save_server, logger=logger,
+        corpora[0] if len(ids) == 1 else corpora, cfg.training_params, args.model_type,
+        args.max_iters, backend=args.engine or cfg.backend, grads_to_share=cfg.grads_to_share,
+        seed=args.seed, save_client=save_client, save_server=save_server, logger=logger,
         graph=cfg.graph and not args.no_graph, log_every=args.log_every,
         stop_at_num_epochs=args.stop_at_num_epochs or cfg.stop_at_num_epochs,
         checkpoint_dir=args.checkpoint_dir,
         checkpoint_every=args.checkpoint_every if args.checkpoint_every is not None
         else cfg.checkpoint_every, stamp=stamp,
-        metrics_path=os.path.join(f"{logs_client}{cid}", f"metrics_{stamp}.jsonl"),
+        metrics_path=os.path.join(f"{logs_client}{ids[0]}", f"metrics_{stamp}.jsonl"),
         metrics_every=args.metrics_every, heartbeat_timeout=args.heartbeat_timeout,
-        agg_mode=args.agg)
+        agg_mode=args.agg, client_ids=ids)
 
 
 def _spawned(local_rank: int, world: int, port: int, argv: List[str]):

@@ -1,0 +1,324 @@
+"""One rank's round: its clients' local steps and the round's FedAvg.
+
+The reference federates any number of clients (``--min_clients_federation``,
+/root/reference/main.py:200,259); every round loops over all of them
+(src/federation/server.py:442-484: pull every client's post-step state, :477-487:
+the n_i-weighted average, :500-521: push it back).  On one node a rank drives one GPU,
+so a rank hosts one client (N = R) or a contiguous block of them (N > R).  Both layouts
+go through the same round loop (:func:`~gfedntm_amd.federation.runner.run_distributed`)
+and one of the two classes below:
+
+* :class:`SingleClientRound` -- the fused engine's own step with the FedAvg all-reduce
+  inside it (graph-captured xGMI kernel, beta overlapped with the encoder backward) or
+  right after it (RCCL / gloo), or classic gradient all-reduce (``agg_mode="grads"``);
+* :class:`MultiClientRound` -- M clients' steps in ONE launch per kernel phase
+  (ops/engine.py BatchedSteps, grid z = client), the in-rank fold of their pre-scaled
+  states into the first client's buffer (csrc/comm.hip gfk_local_fedavg, any number of
+  clients), the collective over the ranks' partial sums, the broadcast back -- one
+  hipGraph per round with the xGMI kernel.  Beta's share is folded, all-reduced (in
+  place for large states) and broadcast on a side stream as soon as the backward has
+  finished it, overlapping the encoder backward and W_in update of all M clients, like
+  the single-client step does.
+
+The sum is fold_ranks(fold_clients_of_rank(w_i W_i)); ``LocalFederation(..., groups=
+sizes)`` reproduces it bit for bit in one process.
+
+Both expose the same failure-detection surface as the engine (error word of the xGMI
+waits: synchronous, or copied asynchronously behind the enqueued rounds and polled), so
+the runner's heartbeat, periodic polls and aligned checks work for either layout.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, List, Optional
+
+import torch
+
+from ..parallel.aggregator import (LOCAL_ALL, LOCAL_BCAST, LOCAL_FIRST, CollectiveAggregator,
+                                   local_fedavg, prepare_local_fedavg)
+from ..utils.misc import graph_capture
+from .client import FederatedClient
+
+
+def inplace_threshold_bytes() -> int:
+    """Parts of at least this many bytes are all-reduced in place (xGMI maps the state
+    itself into the peers instead of copying it into a stage first)."""
+    return int(float(os.environ.get("GFEDNTM_XGMI_INPLACE_MB", "8")) * (1 << 20))
+
+
+class SingleClientRound:
+    """The rank's one client (N = R)."""
+
+    def __init__(self, client: FederatedClient, world: int, device, on_gpu_plane: bool,
+                 allreduce: Optional[str], agg_mode: str, bucket_bytes: int, logger):
+        self.clients = [client]
+        self.client = client
+        self.agg_mode = agg_mode
+        self.agg = CollectiveAggregator(bucket_bytes=bucket_bytes, method="rccl")
+        self.in_step = None
+        if on_gpu_plane and client.fused and agg_mode == "params" and world > 1:
+            self.in_step = client.tm.engine.attach_fedavg(method=allreduce)
+            logger.info("-- -- FedAvg all-reduce: %s", self.in_step)
+        self.method = self.in_step if self.in_step else (None if world == 1 else "rccl")
+        self.attach = getattr(client.tm.engine, "fedavg_attach", None) if self.in_step else None
+
+    @property
+    def xgmi(self) -> bool:
+        return bool(self.in_step) and self.in_step.startswith("xgmi")
+
+    def step(self, it: int, hb=None):
+        """Enqueue round ``it``; ``hb`` (parallel/heartbeat.py) is marked in the
+        all-reduce phase once the local step is enqueued (a peer stuck before its step
+        is then behind this rank)."""
+        c = self.client
+        c.local_step(it)
+        if hb is not None:
+            hb.mark(it, 1)
+        if self.agg_mode == "grads":
+            self.agg.allreduce_(c.shared_grads)
+            c.apply_step(it)
+            packed = c.pack_buffers()
+            self.agg.allreduce_(packed)
+            c.unpack_buffers(packed)
+        elif self.in_step is None:
+            self.agg.allreduce_(c.shared)
+
+    def error(self) -> int:
+        e = self.client.tm.engine
+        return e.fedavg_error() if self.in_step is not None and self.client.fused else 0
+
+    def error_async(self):
+        self.client.tm.engine.fedavg_error_async()
+
+    def error_poll(self) -> int:
+        return self.client.tm.engine.fedavg_error_poll()
+
+    def debug(self) -> dict:
+        return self.client.tm.engine.fedavg_debug() if self.in_step is not None else {}
+
+    def close(self):
+        if self.in_step is not None and self.client.fused:
+            self.client.tm.engine.detach_fedavg()
+            self.in_step = None
+
+
+class MultiClientRound:
+    """The rank's block of M > 1 clients (N > R)."""
+
+    def __init__(self, clients: List[FederatedClient], world: int, device, on_gpu_plane: bool,
+                 allreduce: Optional[str], graph: bool, logger):
+        self.clients = clients
+        self.device = device
+        self.world = world
+        self.shared = [c.shared for c in clients]
+        engines = [c.tm.engine for c in clients]
+        self.fused = all(c.fused for c in clients) and device.type == "cuda"
+        n = self.shared[0].numel()
+        # the shared state's parts: beta (final after the decoder backward in the fused
+        # update mode) and the rest, each with its own collective
+        self.parts: Dict[str, tuple] = {"rest": (0, n)}
+        from ..ops.engine import UPDATE_FUSED
+        flat = clients[0].tm.flat
+        if (self.fused and world > 1 and on_gpu_plane
+                and all(e.update_mode == UPDATE_FUSED for e in engines)
+                and flat.shared_keys and flat.shared_keys[-1] == "beta" and len(flat.shared_keys) > 1):
+            b0 = flat.slots["beta"].offset
+            self.parts = {"rest": (0, b0), "beta": (b0, n)}
+        self.colls: Dict[str, CollectiveAggregator] = {}
+        self.attach = None
+        if world > 1:
+            method = allreduce if on_gpu_plane else "rccl"
+            big = inplace_threshold_bytes()
+            for k, (a, b) in self.parts.items():
+                coll = CollectiveAggregator(method=method)
+                coll.prepare(self.shared[0][a:b], inplace=self.fused and 4 * (b - a) >= big)
+                self.colls[k] = coll
+            self.attach = {"s": round(sum(c.setup_s for c in self.colls.values()), 4),
+                           "bytes": {k: 4 * (b - a) for k, (a, b) in self.parts.items()},
+                           "inplace": {k: c.xgmi is not None and c.xgmi.data is not None
+                                       for k, c in self.colls.items()},
+                           "tuning": {k: c.tuning for k, c in self.colls.items() if c.tuning}}
+        self.coll_in_graph = bool(self.colls) and all(c.xgmi is not None for c in self.colls.values())
+        if not self.coll_in_graph and "beta" in self.parts:
+            # one RCCL all-reduce of the whole state after the round graph
+            for c in self.colls.values():
+                if c.xgmi is not None:
+                    c.xgmi.close()
+                    c.xgmi = None
+            self.parts = {"rest": (0, n)}
+            coll = CollectiveAggregator(method="rccl")
+            coll.prepare(self.shared[0])
+            self.colls = {"rest": coll}
+        self.method = (None if world == 1 else
+                       "xgmi" + ("+overlap" if "beta" in self.parts else "")
+                       if self.coll_in_graph else self.colls["rest"].active)
+        self.graph = (graph and self.fused and not any(e.host_gemm_fallback for e in engines))
+        if self.graph:
+            for c in clients:
+                c.enable_graph(False)     # the round graph carries every client's step
+        if self.fused:
+            prepare_local_fedavg(self.shared)
+        self._g = None
+        self._gens = None
+        self._streams = None
+        self._side = None
+        self._err = None
+        if logger is not None:
+            logger.info("-- -- FedAvg: %d local clients folded in-rank, %s across %d ranks",
+                        len(clients), self.method or "no collective", world)
+
+    # ---- pieces of the round (enqueued on the current stream) ----
+    def _fold(self, part: str, mode: int):
+        a, b = self.parts[part]
+        if len(self.shared) > 1 and b > a:
+            local_fedavg(self.shared, mode, off=a, n=b - a)
+
+    def _reduce_part(self, part: str):
+        """Fold the rank's clients, sum over the ranks, broadcast back (one part)."""
+        if not self.colls:
+            self._fold(part, LOCAL_ALL)
+            return
+        self._fold(part, LOCAL_FIRST)
+        a, b = self.parts[part]
+        self.colls[part].allreduce_(self.shared[0][a:b])
+        self._fold(part, LOCAL_BCAST)
+
+    def _fork_beta(self):
+        main = torch.cuda.current_stream(self.device)
+        side, ev_fork, ev_join = self._side
+        ev_fork.record(main)
+        side.wait_event(ev_fork)
+        with torch.cuda.stream(side):
+            self._reduce_part("beta")
+        ev_join.record(side)
+
+    def _capture(self):
+        engines = [c.tm.engine for c in self.clients]
+        for e in engines:
+            e.prepare_external_capture()
+        g = torch.cuda.CUDAGraph()
+        from ..ops.engine import BatchedSteps
+        batched = (os.environ.get("GFEDNTM_ROUND_BATCHED", "1") == "1"
+                   and BatchedSteps.possible(engines))
+        if self._side is None:
+            self._side = (torch.cuda.Stream(self.device), torch.cuda.Event(), torch.cuda.Event())
+        if batched:
+            bs = BatchedSteps(engines)
+            bs.prepare()
+            # beta's share on the side stream once the backward has finished it (else it
+            # is reduced with the rest at the end of the round: the same arithmetic)
+            beta_at = bs.beta_final_phase() if (self.coll_in_graph and "beta" in self.parts) else None
+            overlap = beta_at is not None
+            hooks = {beta_at: self._fork_beta} if overlap else None
+            with graph_capture(g):
+                bs.launch(after=hooks)
+                if self.coll_in_graph or not self.colls:
+                    for part in self.parts:
+                        if part != "beta" or not overlap:
+                            self._reduce_part(part)
+                    if overlap:
+                        torch.cuda.current_stream(self.device).wait_event(self._side[2])
+                else:
+                    self._fold("rest", LOCAL_FIRST)
+            self._g, self._batched = g, bs
+        else:
+            if self._streams is None:
+                self._streams = [torch.cuda.Stream(self.device) for _ in engines]
+            joins = [torch.cuda.Event() for _ in engines]
+            with graph_capture(g):
+                main = torch.cuda.current_stream(self.device)
+                fork = torch.cuda.Event()
+                fork.record(main)
+                for e, st, ev in zip(engines, self._streams, joins):
+                    st.wait_event(fork)
+                    with torch.cuda.stream(st):
+                        e.launch_step_phases()
+                    ev.record(st)
+                for ev in joins:
+                    main.wait_event(ev)
+                if self.coll_in_graph or not self.colls:
+                    for part in self.parts:
+                        self._reduce_part(part)
+                else:
+                    self._fold("rest", LOCAL_FIRST)
+            self._g = g
+        self._gens = tuple(e.graph_gen for e in engines)
+
+    def step(self, it: int, hb=None):
+        if self.graph:
+            engines = [c.tm.engine for c in self.clients]
+            for e in engines:
+                e.sync_step_counter(it)
+            if self._g is not None and self._gens != tuple(e.graph_gen for e in engines):
+                self._g = None
+            if self._g is None:
+                self._capture()
+            self._g.replay()
+            for e in engines:
+                e.advance_host_step(it)
+            if hb is not None:
+                hb.mark(it, 1)
+            if self.colls and not self.coll_in_graph:
+                # RCCL after the replay (the graph left the rank's partial sum in client 1)
+                self.colls["rest"].allreduce_(self.shared[0])
+                self._fold("rest", LOCAL_BCAST)
+            return
+        for c in self.clients:
+            c.local_step(it)
+        if hb is not None:
+            hb.mark(it, 1)
+        if self.fused:
+            for part in self.parts:
+                self._reduce_part(part)
+            return
+        # CPU / torch engines: client-order fold, then the ranks' sum, then broadcast
+        acc = self.shared[0]
+        for f in self.shared[1:]:
+            acc.add_(f)
+        if self.colls:
+            self.colls["rest"].allreduce_(acc)
+        for f in self.shared[1:]:
+            f.copy_(acc)
+
+    # ---- failure detection (the engine's surface, over this rank's collectives) ----
+    def _xgmis(self):
+        return [c.xgmi for c in self.colls.values() if c.xgmi is not None]
+
+    @property
+    def xgmi(self) -> bool:
+        return bool(self._xgmis())
+
+    def error(self) -> int:
+        err = 0
+        for x in self._xgmis():
+            err = err or x.error()
+        return err
+
+    def error_async(self):
+        xs = self._xgmis()
+        if not xs:
+            return
+        if self._err is None:
+            self._err = {"host": torch.zeros(len(xs), dtype=torch.int32, pin_memory=True),
+                         "ev": torch.cuda.Event(), "pending": False}
+        for i, x in enumerate(xs):
+            x.error_async(self._err["host"][i:i + 1])
+        self._err["ev"].record()
+        self._err["pending"] = True
+
+    def error_poll(self) -> int:
+        e = self._err
+        if not e or not e["pending"] or not e["ev"].query():
+            return 0
+        e["pending"] = False
+        return int(e["host"].max().item())
+
+    def debug(self) -> dict:
+        return {k: c.xgmi.debug_state() for k, c in self.colls.items() if c.xgmi is not None}
+
+    def close(self):
+        self._g = None
+        for c in self.colls.values():
+            if c.xgmi is not None:
+                c.xgmi.close()
+                c.xgmi = None

@@ -190,6 +190,7 @@ class LocalFederation:
             e.prepare_external_capture()
         g = torch.cuda.CUDAGraph()
         shared = [c.shared for c in self.clients]
+        self.agg.prepare(shared)          # the FedAvg kernel's device table, before capturing
         self._batched = None
         if self.round_batched:
             from ..ops.engine import BatchedSteps
@@ -355,7 +356,7 @@ class CommError(RuntimeError):
     """A bounded xGMI all-reduce wait timed out: the shared state since is invalid."""
 
 
-def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm",
+def run_distributed(corpus, params: Dict, model_type: str = "avitm",
                     max_iters: int = 100, backend: str = "auto", data_backend: Optional[str] = None,
                     grads_to_share: Sequence[str] = DEFAULT_GRADS_TO_SHARE, seed: int = 0,
                     save_client: Optional[str] = None, save_server: Optional[str] = None,
@@ -366,25 +367,30 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
                     metrics_every: int = 0, heartbeat_timeout: float = 0.0,
                     agg_mode: str = "params", timing_warmup: int = 0,
                     rehearse_1gpu: Optional[bool] = None, allreduce: Optional[str] = None,
-                    round_hook=None) -> Dict:
-    """Runs this process's client; torch.distributed must be initialised (RANK /
-    WORLD_SIZE).  Rank r is client r+1; rank 0 also plays the coordinator (global
-    save).  ``data_backend`` is the process group's backend ('nccl' = RCCL or
-    'gloo'); a separate gloo group carries the control plane.  ``agg_mode``
-    "params" is the reference FedAvg of the shared state after every local step;
-    "grads" all-reduces the pre-scaled gradients before one optimizer step on
-    every rank (classic synchronous data parallelism; BN statistics averaged).
+                    round_hook=None, client_ids: Optional[Sequence[int]] = None) -> Dict:
+    """Runs this process's client(s); torch.distributed must be initialised (RANK /
+    WORLD_SIZE).  ``corpus`` is this rank's one client (id rank + 1), or a list of client
+    corpora with their ids ``client_ids`` -- a contiguous block of a federation of more
+    clients than ranks (federation/hierarchical.py assign_clients; the ranks' blocks
+    must partition 1..N in rank order).  Rank 0 also plays the coordinator (global
+    save).  ``data_backend`` is the process group's backend ('nccl' = RCCL or 'gloo'); a
+    separate gloo group carries the control plane.  ``agg_mode`` "params" is the
+    reference FedAvg of the shared state after every local step; "grads" all-reduces the
+    pre-scaled gradients before one optimizer step on every rank (classic synchronous data
+    parallelism; BN statistics averaged; one client per rank).
 
     Round loop (reference server.py:436-521 + client.py:135-183): the host only
     enqueues work -- one hipGraph replay per round with the FedAvg all-reduce
-    captured inside it (fused engine) -- and never waits for the device, except at
-    the rounds where some rank does long host work (results / snapshot saves,
-    checkpoints, metrics windows).  Those rounds are known to every rank up front
-    (:meth:`FederatedClient.host_heavy_rounds`), so all ranks meet there on the
-    control plane: no rank's device is left spinning in the in-step xGMI
-    all-reduce while a peer's host is busy.  At each such point, and at the end,
-    the ranks agree on the all-reduce's error word; a timed-out wait aborts every
-    rank with :class:`CommError` before anything is saved.
+    captured inside it (fused engine; federation/rank_round.py) -- and never waits for the
+    device, except at the rounds where some client does long host work (results /
+    snapshot saves, checkpoints, metrics windows).  Those rounds are known to every rank
+    up front (:meth:`FederatedClient.host_heavy_rounds`), so all ranks meet there on the
+    control plane: no rank's device is left spinning in the in-step xGMI all-reduce while
+    a peer's host is busy.  At each such point, every ``GFEDNTM_COMM_POLL`` rounds in
+    between (an error word copied behind the enqueued rounds, no sync) and at the end,
+    the ranks agree on the all-reduce's error word; a timed-out wait aborts every rank
+    with :class:`CommError` (its xGMI resources released) before anything is saved.
+    ``heartbeat_timeout`` > 0 adds the control-plane watchdog (parallel/heartbeat.py).
 
     ``timing_warmup``: the first rounds (after ``start``) are excluded from the
     reported wall time (bench).  ``round_hook(it)`` is called after every round
@@ -392,8 +398,20 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
     injects one such stall from the environment (failure-injection tests of processes
     this code does not start itself, e.g. bench.py's ranks)."""
     import torch.distributed as dist
+    from .hierarchical import agree_client_map
+    from .rank_round import MultiClientRound, SingleClientRound
     logger = logger or logging.getLogger("gfedntm_amd.federation")
     rank, world = dist.get_rank(), dist.get_world_size()
+    corpora = [corpus] if isinstance(corpus, ClientCorpus) else list(corpus)
+    if client_ids is None:
+        if len(corpora) != 1:
+            raise ValueError("several client corpora need their client_ids")
+        client_ids = [rank + 1]
+    client_ids = [int(i) for i in client_ids]
+    if len(corpora) != len(client_ids) or not corpora:
+        raise ValueError("one corpus per local client id")
+    if len(corpora) > 1 and agg_mode != "params":
+        raise ValueError("agg_mode 'grads' runs one client per rank")
     inj = os.environ.get("GFEDNTM_INJECT_STALL")
     if inj and round_hook is None:
         r_s, it_s, sec_s = inj.split(":")
@@ -404,107 +422,116 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
     data_backend = data_backend or dist.get_backend()
     rehearse = rehearsal_enabled() if rehearse_1gpu is None else bool(rehearse_1gpu)
     ctrl = dist.new_group(backend="gloo") if data_backend != "gloo" else None
-    if data_backend == "nccl":
-        device = torch.device("cuda", torch.cuda.current_device())
-    elif rehearse:
+    on_gpu_plane = data_backend == "nccl" or rehearse
+    if on_gpu_plane:
         device = torch.device("cuda", torch.cuda.current_device())
     else:
         device = torch.device("cpu")
     stamp = stamp or datetime.datetime.now().strftime("%Y%m%d")
-    # ---- stage 1: vocabulary consensus + counts over the control plane ----
     metrics = MetricsWriter(metrics_path)
     hb = None
     if heartbeat_timeout and world > 1:
         from ..parallel.heartbeat import Heartbeat
         hb = Heartbeat(rank, world, timeout=heartbeat_timeout,
                        interval=max(0.5, min(5.0, heartbeat_timeout / 10))).start()
-    local = corpus.local_terms()
-    gathered = [None] * world
+    # ---- stage 1: client map, vocabulary union, weights (control plane) ----
     with trace_range("consensus"):
-        dist.all_gather_object(gathered, (local, corpus.n_docs), group=ctrl)
-    terms = union_vocabulary([g[0] for g in gathered])
+        cmap = agree_client_map(client_ids, world, group=ctrl)
+        gathered: List = [None] * world
+        dist.all_gather_object(gathered, [(c.local_terms(), c.n_docs) for c in corpora],
+                               group=ctrl)
+    every = [x for g in gathered for x in g]              # client-id order
+    terms = union_vocabulary([t for t, _ in every])
     vocab = vocabulary_dict(terms)
-    n = [g[1] for g in gathered]
-    weights = fedavg_weights(n)
+    weights = fedavg_weights([nd for _, nd in every])
     if rank == 0:
-        logger.info("-- -- Global vocabulary agreed: %d terms from %d clients", len(terms), world)
-    ds = build_dataset(model_type, corpus, vocab, terms)
-    tm = make_topic_model(model_type, params, len(terms), device, backend, grads_to_share,
-                          seed=seed, logger=logger)
-    # identical W0 on every client: the flat buffer holds every float parameter and buffer
-    with trace_range("w0_broadcast"):
-        if data_backend == "gloo" and device.type == "cuda":
-            host = tm.flat.buffer.cpu()
-            dist.broadcast(host, src=0)
-            tm.flat.buffer.copy_(host)
+        logger.info("-- -- Global vocabulary agreed: %d terms from %d clients%s", len(terms),
+                    len(every), f" on {world} ranks" if len(every) != world else "")
+    clients: List[FederatedClient] = []
+    for k, (cid, corp) in enumerate(zip(client_ids, corpora)):
+        ds = build_dataset(model_type, corp, vocab, terms)
+        tm = make_topic_model(model_type, params, len(terms), device, backend, grads_to_share,
+                              seed=seed, logger=logger)
+        if k == 0:
+            # identical W0 on every client: the flat buffer holds every float parameter and buffer
+            with trace_range("w0_broadcast"):
+                if data_backend == "gloo" and device.type == "cuda":
+                    host = tm.flat.buffer.cpu()
+                    dist.broadcast(host, src=0)
+                    tm.flat.buffer.copy_(host)
+                else:
+                    dist.broadcast(tm.flat.buffer, src=0)
         else:
-            dist.broadcast(tm.flat.buffer, src=0)
-    cid = rank + 1
-    path = None
-    if save_client is not None:
-        from ..eval.export import client_model_path
-        path = client_model_path(save_client, cid, stamp)
-    client = FederatedClient(cid, tm, ds, max_iters, logger=logger, seed=seed + cid,
-                             save_path=path, log_every=log_every,
-                             epoch_snapshots=(model_type in CTM_TYPES), agg=agg_mode)
-    client.set_fedavg_weight(weights[rank])
-    client.enable_graph(graph and agg_mode == "params")
-    agg = CollectiveAggregator(bucket_bytes=bucket_bytes, method="rccl")
-    in_step = None
-    if (data_backend == "nccl" or rehearse) and client.fused and agg_mode == "params" and world > 1:
-        # the FedAvg all-reduce runs inside the step (graph-captured xGMI kernel, beta
-        # overlapped with the encoder backward) or right after it (RCCL)
-        in_step = tm.engine.attach_fedavg(method=allreduce)
-        logger.info("-- -- FedAvg all-reduce: %s", in_step)
+            tm.flat.buffer.copy_(clients[0].tm.flat.buffer)
+        path = None
+        if save_client is not None:
+            from ..eval.export import client_model_path
+            path = client_model_path(save_client, cid, stamp)
+        c = FederatedClient(cid, tm, ds, max_iters, logger=logger, seed=seed + cid,
+                            save_path=path, log_every=log_every,
+                            epoch_snapshots=(model_type in CTM_TYPES), agg=agg_mode)
+        c.set_fedavg_weight(weights[cid - 1])
+        c.enable_graph(graph and agg_mode == "params")
+        clients.append(c)
+    # ---- data plane: this rank's round (its clients' steps + the FedAvg) ----
+    if len(clients) == 1:
+        rr = SingleClientRound(clients[0], world, device, on_gpu_plane, allreduce, agg_mode,
+                               bucket_bytes, logger)
+    else:
+        rr = MultiClientRound(clients, world, device, on_gpu_plane, allreduce, graph, logger)
     start = 0
     if checkpoint_dir:
-        start = ckpt.load_client_checkpoint(checkpoint_dir, client)
+        starts = {ckpt.load_client_checkpoint(checkpoint_dir, c) for c in clients}
+        if len(starts) != 1:
+            raise RuntimeError(f"inconsistent client checkpoints on rank {rank}: {sorted(starts)}")
+        start = starts.pop()
         rounds = [None] * world
         dist.all_gather_object(rounds, start, group=ctrl)
         if len(set(rounds)) != 1:
             raise RuntimeError(f"inconsistent client checkpoints: rounds {rounds}")
-    # ---- rounds where every rank meets (some rank does long host work after them)
-    plan_info = [None] * world
-    dist.all_gather_object(plan_info, (client.host_heavy_rounds(), client.done_round()),
+    # ---- rounds where every rank meets (some client does long host work after them)
+    plan_info: List = [None] * world
+    dist.all_gather_object(plan_info, [(c.host_heavy_rounds(), c.done_round()) for c in clients],
                            group=ctrl)
-    align = set()
-    for heavy, _ in plan_info:
-        align.update(heavy)
+    align, dones = set(), []
+    for per_rank in plan_info:
+        for heavy, d in per_rank:
+            align.update(heavy)
+            dones.append(d)
     stop_after = max_iters - 1
-    if stop_at_num_epochs:
-        dones = [d for _, d in plan_info]
-        if all(d is not None for d in dones):
-            stop_after = min(stop_after, max(dones))
+    if stop_at_num_epochs and all(d is not None for d in dones):
+        stop_after = min(stop_after, max(dones))
     sync = (lambda: torch.cuda.synchronize(device)) if device.type == "cuda" else (lambda: None)
+
+    def fail(err: int, where: str):
+        if os.environ.get("GFEDNTM_COMM_DEBUG") == "1":
+            logger.warning("rank %d xGMI state: %s", rank, rr.debug())
+        rr.close()                 # release the IPC mappings / step graph before raising
+        if hb is not None:
+            hb.stop()
+        raise CommError(f"rank {rank}: an xGMI all-reduce wait timed out before {where} "
+                        f"(error {err}); the shared state is invalid -- resume from the last "
+                        "round checkpoint")
 
     def check_comm(where: str):
         """Agree on the xGMI error word across ranks (synchronises the device)."""
-        err = tm.engine.fedavg_error() if in_step is not None and client.fused else 0
-        flag = torch.tensor([int(err)], dtype=torch.int64)
+        flag = torch.tensor([int(rr.error())], dtype=torch.int64)
         dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=ctrl)
         if int(flag.item()):
-            if os.environ.get("GFEDNTM_COMM_DEBUG") == "1" and in_step is not None:
-                logger.warning("rank %d xGMI state: %s", rank, tm.engine.fedavg_debug())
-            raise CommError(f"rank {rank}: an xGMI all-reduce wait timed out before {where} "
-                            f"(error {int(flag.item())}); the shared state is invalid -- "
-                            "resume from the last round checkpoint")
+            fail(int(flag.item()), where)
 
     # a timed-out xGMI wait is also caught between the aligned rounds: every poll_every
     # rounds each rank reads the error word copied behind its enqueued rounds (no device
     # sync) and the ranks agree on it over the control plane, so a run fails within about
     # two poll intervals of the timeout instead of training on for the whole run
-    poll_every = int(os.environ.get("GFEDNTM_COMM_POLL", "512")) \
-        if in_step is not None and in_step.startswith("xgmi") else 0
+    poll_every = int(os.environ.get("GFEDNTM_COMM_POLL", "512")) if rr.xgmi else 0
 
     def poll_comm(it: int):
-        err = tm.engine.fedavg_error_poll()
-        flag = torch.tensor([int(err)], dtype=torch.int64)
+        flag = torch.tensor([int(rr.error_poll())], dtype=torch.int64)
         dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=ctrl)
         if int(flag.item()):
-            raise CommError(f"rank {rank}: an xGMI all-reduce wait timed out before round "
-                            f"{it + 1} (error {int(flag.item())}); the shared state is invalid "
-                            "-- resume from the last round checkpoint")
-        tm.engine.fedavg_error_async()
+            fail(int(flag.item()), f"round {it + 1}")
+        rr.error_async()
 
     def meet(where: str):
         sync()
@@ -514,7 +541,7 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
     dist.barrier(group=ctrl)
     # GFEDNTM_COMM_DEBUG=1: the first rounds synchronised one by one, with their times and
     # the xGMI error word (which round a timed-out wait happened in, and the ranks' skew)
-    debug_comm = os.environ.get("GFEDNTM_COMM_DEBUG") == "1" and in_step is not None
+    debug_comm = os.environ.get("GFEDNTM_COMM_DEBUG") == "1" and rr.xgmi
     t_dbg0 = time.perf_counter()
     win = RoundWindow(sync)
     # device time of the timed rounds: events on the round stream around them (the host
@@ -528,23 +555,13 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
         for it in range(start, stop_after + 1):
             if hb is not None:
                 hb.mark(it, 0)
-            client.local_step(it)
+            rr.step(it, hb)
             if debug_comm and it < start + 16:
                 t_dbg = time.perf_counter()
                 sync()
                 logger.warning("rank %d round %d: enqueued at %.3f s, done at %.3f s, xGMI "
                                "error %d", rank, it, t_dbg - t_dbg0, time.perf_counter() - t_dbg0,
-                               tm.engine.fedavg_error() if in_step is not None else 0)
-            if hb is not None:
-                hb.mark(it, 1)
-            if agg_mode == "grads":
-                agg.allreduce_(client.shared_grads)
-                client.apply_step(it)
-                packed = client.pack_buffers()
-                agg.allreduce_(packed)
-                client.unpack_buffers(packed)
-            elif in_step is None:
-                agg.allreduce_(client.shared)
+                               rr.error())
             heavy = it in align
             if heavy:
                 # validate the state before anything is exported
@@ -552,7 +569,8 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
                 check_comm(f"the host work of round {it}")
                 if hb is not None:
                     hb.busy(True)
-            client.end_round(it)
+            for c in clients:
+                c.end_round(it)
             last = it
             if heavy:
                 if hb is not None:
@@ -562,7 +580,7 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
                 poll_comm(it)
             if round_hook is not None:
                 round_hook(it)
-            win.add(int(client.plan.size[it]))
+            win.add(sum(int(c.plan.size[it]) for c in clients))
             if timing_warmup and it == start + timing_warmup - 1:
                 meet("the timed region")
                 t0 = time.perf_counter()
@@ -579,7 +597,8 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
                     meet(f"checkpoint {it + 1}")
                     if hb is not None:
                         hb.busy(True)
-                    ckpt.save_client_checkpoint(checkpoint_dir, client, it + 1)
+                    for c in clients:
+                        ckpt.save_client_checkpoint(checkpoint_dir, c, it + 1)
                     if hb is not None:
                         hb.busy(False)
                     dist.barrier(group=ctrl)
@@ -589,21 +608,24 @@ def run_distributed(corpus: ClientCorpus, params: Dict, model_type: str = "avitm
     wall = time.perf_counter() - t0
     device_s = ev[0].elapsed_time(ev[1]) * 1e-3 if ev is not None and timed_from > start else None
     check_comm("the end of training")
-    client.flush()
+    for c in clients:
+        c.flush()
     n_rounds = last + 1 - timed_from
-    docs = int(client.plan.size[timed_from: last + 1].sum()) if n_rounds > 0 else 0
-    metrics.write(event="train_end", rank=rank, rounds=n_rounds, wall_s=wall, docs=docs,
-                  docs_per_s=docs / wall if wall and docs else None,
+    docs = sum(int(c.plan.size[timed_from: last + 1].sum()) for c in clients) if n_rounds > 0 else 0
+    metrics.write(event="train_end", rank=rank, clients=list(client_ids), rounds=n_rounds,
+                  wall_s=wall, docs=docs, docs_per_s=docs / wall if wall and docs else None,
                   ms_per_round=1e3 * wall / max(n_rounds, 1))
-    if client.save_path and not client.results_saved:
-        client.save_results(client.save_path)
+    for c in clients:
+        if c.save_path and not c.results_saved:
+            c.save_results(c.save_path)
     if rank == 0 and save_server:
         logger.info("-- -- Saving global model...")
-        save_model_as_npz(server_model_path(save_server, stamp), tm.get_topic_word_distribution(),
-                          None, tm.n_components, None)
+        tm0 = clients[0].tm
+        save_model_as_npz(server_model_path(save_server, stamp), tm0.get_topic_word_distribution(),
+                          None, tm0.n_components, None)
     dist.barrier(group=ctrl)
     if hb is not None:
         hb.stop()
     return {"rounds": last + 1, "timed_rounds": n_rounds, "wall_s": wall, "docs": docs,
-            "device_s": device_s, "client": client, "allreduce": in_step,
-            "attach": getattr(tm.engine, "fedavg_attach", None) if in_step else None}
+            "device_s": device_s, "client": clients[0], "clients": clients, "client_map": cmap,
+            "allreduce": rr.method, "attach": rr.attach, "round": rr}

@@ -190,7 +190,7 @@ class TopicModelBase:
         if self.backend == "fused":
             from ..ops.engine import BETA_PAD, BETA_PAD_MIN_V
             if self.input_size >= BETA_PAD_MIN_V:
-                padded = {"beta": BETA_PAD}        # beta rows on 128-B lines (utils/flat.py)
+                padded = {"beta": BETA_PAD}        # beta rows of whole 64-column tiles (utils/flat.py)
         self.flat = FlatState(self.model, self.shared_keys, transposed=transposed,
                               device=self.device,
                               shared_last=("beta",) if self.backend == "fused" else (),

@@ -1417,19 +1417,25 @@ class BatchedSteps:
         if rc:
             raise RuntimeError(f"gfk_run (batched) failed: code {rc}")
 
-    def launch(self):
+    def launch(self, after=None):
         """Enqueue one local step of every engine on the current stream (the split W_in
-        update's dense half forked onto a side stream, as in a single engine's step)."""
+        update's dense half forked onto a side stream, as in a single engine's step).
+        ``after``: {phase: callable} called (on the host, while enqueuing) right after
+        that phase's launch -- the multi-client rank round forks beta's FedAvg there."""
         self._refresh()
+        after = after or {}
         run: List[int] = []
         for p in list(self._phases) + [None]:
             if p is not None and p not in _BATCH_FORK_PHASES:
                 run.append(p)
-                continue
+                if p not in after:
+                    continue
             if run:
                 self._run(run)
                 run = []
-            if p == abi.PH_WIN_FORK:
+            if p in after:
+                after[p]()
+            elif p == abi.PH_WIN_FORK:
                 side, ev_fork, ev_join = self._side
                 ev_fork.record(torch.cuda.current_stream(self.device))
                 side.wait_event(ev_fork)
@@ -1438,3 +1444,14 @@ class BatchedSteps:
                 ev_join.record(side)
             elif p == abi.PH_WIN_JOIN:
                 torch.cuda.current_stream(self.device).wait_event(self._side[2])
+
+    def beta_final_phase(self) -> Optional[int]:
+        """The phase after which every client's beta is final in the fused update mode
+        (Adam + the FedAvg pre-scale in its epilogue), or None."""
+        e0 = self.engines[0]
+        if e0.update_mode != UPDATE_FUSED:
+            return None
+        for p in (abi.PH_PRODLDA_BWD, abi.PH_LDA_BETA_BWD):
+            if p in self._phases:
+                return p
+        return None

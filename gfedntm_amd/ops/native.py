@@ -7,7 +7,9 @@
   compatible tokenizer / CSR builder, batch-plan builder.
 
 On a GPU box the kernels library is REQUIRED: :func:`kernels` raises if it is
-missing instead of silently falling back to PyTorch.
+missing instead of silently falling back to PyTorch, and if it was built from other
+sources than the ``csrc/`` of this tree (the source hash embedded by the build,
+``ops/srchash.py``) -- unless ``GFEDNTM_KERNELS_SO`` names another build on purpose.
 """
 from __future__ import annotations
 
@@ -21,7 +23,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_DIR = os.path.join(ROOT, "_lib")
 # GFEDNTM_KERNELS_SO: another build of the kernel library (A/B timing of kernel variants,
 # tools/ab_libs.py); the in-tree library otherwise
-KERNELS_SO = os.environ.get("GFEDNTM_KERNELS_SO") or os.path.join(LIB_DIR, "libgfedntm_kernels.so")
+KERNELS_SO_OVERRIDE = os.environ.get("GFEDNTM_KERNELS_SO") or None
+KERNELS_SO = KERNELS_SO_OVERRIDE or os.path.join(LIB_DIR, "libgfedntm_kernels.so")
 RUNTIME_SO = os.path.join(LIB_DIR, "libgfedntm_runtime.so")
 
 _kernels: Optional[ctypes.CDLL] = None
@@ -39,10 +42,47 @@ def kernels() -> ctypes.CDLL:
         if not kernels_available():
             raise RuntimeError(
                 f"{KERNELS_SO} is missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
-        _kernels = ctypes.CDLL(KERNELS_SO, mode=ctypes.RTLD_GLOBAL)
+        lib = ctypes.CDLL(KERNELS_SO, mode=ctypes.RTLD_GLOBAL)
+        _check_source(lib)
         from . import kernel_abi
-        kernel_abi.declare(_kernels)
+        kernel_abi.declare(lib)
+        _kernels = lib
     return _kernels
+
+
+def _embedded_hash(lib) -> Optional[str]:
+    try:
+        f = lib.gfk_source_hash
+    except AttributeError:
+        return None
+    f.restype = ctypes.c_char_p
+    f.argtypes = []
+    return f().decode()
+
+
+def _check_source(lib) -> None:
+    """Refuse a kernel library whose embedded source hash is not this tree's."""
+    from . import srchash
+    if not os.path.isdir(srchash.CSRC):
+        return                       # no sources next to the package: nothing to compare
+    got = _embedded_hash(lib)
+    want = srchash.source_hash(os.environ.get("PYTORCH_ROCM_ARCH", "gfx950"))
+    if got == want:
+        return
+    if KERNELS_SO_OVERRIDE:
+        import logging
+        logging.getLogger("gfedntm_amd.native").warning(
+            "GFEDNTM_KERNELS_SO=%s: source hash %s, tree %s (A/B build, not checked)",
+            KERNELS_SO, got, want)
+        return
+    raise RuntimeError(
+        f"{KERNELS_SO} was built from other sources (embedded hash {got}, csrc/ hashes to "
+        f"{want}): rebuild with `python -c 'import __graft_entry__ as g; g.build()'`")
+
+
+def kernels_hash() -> Optional[str]:
+    """The source hash embedded in the loaded kernel library (None if not loaded)."""
+    return _embedded_hash(kernels()) if kernels_available() else None
 
 
 def runtime() -> Optional[ctypes.CDLL]:

@@ -18,6 +18,7 @@ the caller can overlap host bookkeeping with the collective.
 from __future__ import annotations
 
 import ctypes
+import itertools
 import time
 from typing import List, Optional, Sequence
 
@@ -168,20 +169,53 @@ class CollectiveAggregator:
 
 
 class _GfkLocalAvg(ctypes.Structure):
-    _fields_ = [("f", ctypes.c_void_p * 16), ("n_clients", ctypes.c_int32),
-                ("mode", ctypes.c_int32), ("n", ctypes.c_int64), ("n_groups", ctypes.c_int32),
-                ("gend", ctypes.c_int32 * 16), ("pad", ctypes.c_int32)]
+    _fields_ = [("f", ctypes.c_void_p), ("gend", ctypes.c_void_p), ("off", ctypes.c_int64),
+                ("n", ctypes.c_int64), ("n_clients", ctypes.c_int32), ("mode", ctypes.c_int32),
+                ("n_groups", ctypes.c_int32), ("pad", ctypes.c_int32)]
 
 
 LOCAL_ALL, LOCAL_FIRST, LOCAL_BCAST = 0, 1, 2     # gfk_local_fedavg modes (csrc/comm.hip)
 
+# device tables of the in-process fold (client buffer pointers + group ends), one per
+# (device, pointers, groups): built outside graph captures, kept alive for the graphs
+# that baked their addresses in
+_TABLES = {}
+
+
+def _local_table(flats: Sequence[torch.Tensor], groups: Sequence[int]) -> torch.Tensor:
+    dev = flats[0].device
+    ptrs = tuple(int(f.data_ptr()) for f in flats)
+    key = (str(dev), ptrs, tuple(groups))
+    t = _TABLES.get(key)
+    if t is None:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("local_fedavg: call prepare_local_fedavg() on these buffers "
+                               "before the graph capture (its device table is uploaded once)")
+        if any(p % 16 for p in ptrs):
+            raise ValueError("local_fedavg buffers must be 16-byte aligned")
+        ends = list(itertools.accumulate(int(g) for g in groups))
+        # one int64 tensor: the pointers, then the group ends as int32 pairs
+        host = torch.tensor([int(p) for p in ptrs], dtype=torch.int64)
+        gend = torch.tensor(ends + [0] * (len(ends) & 1), dtype=torch.int32).view(torch.int64)
+        t = torch.cat([host, gend]).to(dev)
+        _TABLES[key] = t
+    return t
+
+
+def prepare_local_fedavg(flats: Sequence[torch.Tensor], groups: Optional[Sequence[int]] = None):
+    """Upload the device table of ``flats`` (call before capturing local_fedavg)."""
+    groups = [len(flats)] if groups is None else [int(g) for g in groups]
+    return _local_table(flats, groups)
+
 
 def local_fedavg(flats: Sequence[torch.Tensor], mode: int = LOCAL_ALL,
-                 groups: Optional[Sequence[int]] = None):
+                 groups: Optional[Sequence[int]] = None, off: int = 0, n: Optional[int] = None):
     """One launch of csrc/comm.hip ``gfk_local_fedavg`` on the current stream (capture
-    safe): the group-wise left-fold sum of ``flats`` (``groups``: sizes of consecutive
-    client groups, default one group) written to every buffer (LOCAL_ALL) or to
-    flats[0] only (LOCAL_FIRST), or flats[0] copied to the others (LOCAL_BCAST)."""
+    safe once :func:`prepare_local_fedavg` ran on the same buffers): the group-wise left-
+    fold sum of ``flats`` (``groups``: sizes of consecutive client groups, default one
+    group) written to every buffer (LOCAL_ALL) or to flats[0] only (LOCAL_FIRST), or
+    flats[0] copied to the others (LOCAL_BCAST).  ``off`` / ``n``: the float range folded
+    (default the whole buffers).  Any number of clients."""
     C = ctypes
     from ..ops import native
     lib = native.kernels()
@@ -194,27 +228,30 @@ def local_fedavg(flats: Sequence[torch.Tensor], mode: int = LOCAL_ALL,
     groups = [len(flats)] if groups is None else [int(g) for g in groups]
     if sum(groups) != len(flats) or min(groups) < 1:
         raise ValueError(f"groups {groups} do not partition {len(flats)} clients")
+    total = flats[0].numel()
+    n = total - off if n is None else int(n)
+    if off % 4 or off < 0 or off + n > total or any(f.numel() != total for f in flats):
+        raise ValueError(f"bad local_fedavg range [{off}, {off + n}) of {total}")
+    table = _local_table(flats, groups)
     d = _GfkLocalAvg()
-    for j, f in enumerate(flats):
-        d.f[j] = f.data_ptr()
-    d.n_clients, d.n, d.mode, d.n_groups = len(flats), flats[0].numel(), int(mode), len(groups)
-    e = 0
-    for i, g in enumerate(groups):
-        e += g
-        d.gend[i] = e
+    d.f = table.data_ptr()
+    d.gend = table.data_ptr() + 8 * len(flats)
+    d.off, d.n = int(off), n
+    d.n_clients, d.mode, d.n_groups = len(flats), int(mode), len(groups)
     cu = torch.cuda.get_device_properties(flats[0].device).multi_processor_count
-    grid = int(max(1, min(-(-d.n // 1024), 4 * cu)))
+    grid = int(max(1, min(-(-n // 1024), 4 * cu)))
     stream = torch.cuda.current_stream(flats[0].device).cuda_stream
     rc = lib.gfk_local_fedavg_launch(C.byref(d), grid, C.c_void_p(stream))
     if rc:
         raise RuntimeError(f"gfk_local_fedavg_launch failed ({rc})")
+    d._table = table
     return d
 
 
 class LocalAggregator:
     """In-process FedAvg over N client flat buffers (exact reference order of ops).
 
-    On a GPU, pre-scaled buffers of up to 16 clients are summed by one HIP kernel
+    On a GPU, pre-scaled buffers of any number of clients are summed by one HIP kernel
     (csrc/comm.hip ``gfk_local_fedavg``: client-order sum written back to every
     client, capture-safe); the eager torch sequence is the CPU / oracle path.
     ``groups`` (sizes of consecutive client groups) sums group-wise first, then the
@@ -231,11 +268,18 @@ class LocalAggregator:
         self._desc = None
 
     def _native(self, flats: Sequence[torch.Tensor]) -> bool:
-        if len(flats) > 16 or flats[0].device.type != "cuda":
+        if flats[0].device.type != "cuda":
             return False
         n = flats[0].numel()
         return all(f.device == flats[0].device and f.dtype == torch.float32 and f.is_contiguous()
                    and f.numel() == n and f.data_ptr() % 16 == 0 for f in flats)
+
+    def prepare(self, flats: Sequence[torch.Tensor]) -> bool:
+        """Upload the fold's device table (before capturing :meth:`fused_sum_`)."""
+        if len(flats) > 1 and self._native(flats):
+            prepare_local_fedavg(flats, self.groups)
+            return True
+        return False
 
     def fused_sum_(self, flats: Sequence[torch.Tensor]):
         """flats[i] <- sum_j flats[j] (client order, group-wise) for all i, one kernel

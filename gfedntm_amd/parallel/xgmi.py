@@ -61,6 +61,36 @@ def _declare(lib):
     lib._gfk_comm_declared = True
 
 
+# peer allocations mapped into this process, keyed by (exporter pid, exporter base address):
+# two all-reduces whose in-place parts are slices of ONE caching-allocator block (the
+# 'rest' and 'beta' parts of a flat state) share one mapping, refcounted, instead of
+# opening the same memory twice and unmapping it under the other on close()
+_IPC_OPEN = {}
+
+
+def _ipc_open(lib, handle: bytes, key) -> int:
+    ent = _IPC_OPEN.get(key)
+    if ent is not None:
+        ent[1] += 1
+        return ent[0]
+    p = P()
+    rc = lib.gfk_ipc_open(C.create_string_buffer(handle, len(handle)), C.byref(p))
+    if rc:
+        raise RuntimeError(f"hipIpcOpenMemHandle failed ({rc})")
+    _IPC_OPEN[key] = [p.value, 1]
+    return p.value
+
+
+def _ipc_close(lib, key):
+    ent = _IPC_OPEN.get(key)
+    if ent is None:
+        return
+    ent[1] -= 1
+    if ent[1] == 0:
+        lib.gfk_ipc_close(P(ent[0]))
+        del _IPC_OPEN[key]
+
+
 def _up4(x: int) -> int:
     return -(-x // 4) * 4
 
@@ -91,7 +121,7 @@ class XgmiAllReduce:
             nblk = self.grid_for(chunk, self.device, group)
         self.nblk = nblk
         slice_ = _up4(-(-chunk // nblk))
-        self._handles: List[int] = []
+        self._handles: List = []
         self.data = data
         inplace = data is not None
         if inplace and (data.dtype != torch.float32 or not data.is_contiguous()
@@ -109,6 +139,7 @@ class XgmiAllReduce:
             hs = self.lib.gfk_ipc_handle_size()
             mine = []
             offset = 0
+            pid = os.getpid()
             for ptr in ((data.data_ptr() if inplace else stage.value), flags.value):
                 h = C.create_string_buffer(hs)
                 if inplace and not mine:
@@ -119,7 +150,8 @@ class XgmiAllReduce:
                     rc = self.lib.gfk_ipc_get(P(ptr), h)
                 if rc:
                     raise RuntimeError(f"hipIpcGetMemHandle failed ({rc})")
-                mine.append(h.raw)
+                # (handle, identity of the exported allocation: pid + its base address)
+                mine.append((h.raw, (pid, ptr - (offset if not mine else 0))))
             mine.append(offset)
             allh: List = [None] * self.world
             dist.all_gather_object(allh, mine, group=group)
@@ -129,7 +161,7 @@ class XgmiAllReduce:
                     sp = data.data_ptr() if inplace else stage.value
                     fp = flags.value
                 else:
-                    sp, fp = self._open(allh[j][0]) + allh[j][2], self._open(allh[j][1])
+                    sp, fp = self._open(*allh[j][0]) + allh[j][2], self._open(*allh[j][1])
                 c.stage[0][j] = sp
                 c.stage[1][j] = sp if inplace else sp + stage_bytes
                 c.flags[j] = fp
@@ -156,13 +188,10 @@ class XgmiAllReduce:
         cap = max(1, props.multi_processor_count // sharing)
         return int(max(1, min(cap, chunk // 1024)))
 
-    def _open(self, handle: bytes) -> int:
-        p = P()
-        rc = self.lib.gfk_ipc_open(C.create_string_buffer(handle, len(handle)), C.byref(p))
-        if rc:
-            raise RuntimeError(f"hipIpcOpenMemHandle failed ({rc})")
-        self._handles.append(p.value)
-        return p.value
+    def _open(self, handle: bytes, key) -> int:
+        p = _ipc_open(self.lib, handle, key)
+        self._handles.append(key)
+        return p
 
     def allreduce_(self, t: torch.Tensor) -> torch.Tensor:
         if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != self.n \
@@ -252,8 +281,8 @@ class XgmiAllReduce:
         return all(flags)
 
     def close(self):
-        for p in self._handles:
-            self.lib.gfk_ipc_close(P(p))
+        for key in self._handles:
+            _ipc_close(self.lib, key)
         self._handles = []
         if getattr(self, "_own", None):
             self.lib.gfk_comm_free(*[P(x) for x in self._own])

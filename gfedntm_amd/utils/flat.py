@@ -21,9 +21,11 @@ adapt_bert) then start on a line.
 gathers one *column* per non-zero token, so it is stored as [V, H0] and the
 module sees the ``.t()`` view.
 
-``padded`` maps 2-D weights to a row-stride multiple: ``{"beta": 32}`` stores the
-[K, V] topic-word matrix with rows of ``round_up(V, 32)`` floats (128 B), so every row
-starts on a cache line.  The fused large-vocabulary kernels read-modify-write beta, Adam
+``padded`` maps 2-D weights to a row-stride multiple: the fused engine's
+``{"beta": BETA_PAD}`` (64, ops/engine.py) stores the [K, V] topic-word matrix with rows of
+``round_up(V, 64)`` floats (256 B), so every row starts on a cache line and a row is whole
+64-column tiles -- the pipelined large-V backward (bwd_pre = 3) requires ``ld % 64 == 0``
+and stores a partial last tile's columns into the padding.  The fused large-vocabulary kernels read-modify-write beta, Adam
 m and v in 64-column tiles; with rows of V = 112 027 floats each tile row straddles
 three cache lines and the same RMW stream ran at 3.4 instead of 5.0 TB/s
 (``profiles/r3/adam_rmw_alignment.jsonl``).  The module sees the [K, V] slice of the

@@ -143,63 +143,105 @@ def test_timed_out_wait_is_caught_between_aligned_rounds(tmp_path):
 N_MULTI = 8                      # clients, over 2 ranks: 4 per rank
 
 
-def _multi_corpora():
+def _multi_corpora(n=N_MULTI):
     from gfedntm_amd.data.synthetic import generate_synthetic
     from gfedntm_amd.federation.data import ClientCorpus
-    sc = generate_synthetic(vocab_size=500, n_topics=10, n_docs=60, n_nodes=N_MULTI,
+    sc = generate_synthetic(vocab_size=500, n_topics=10, n_docs=60, n_nodes=n,
                             frozen_topics=2, nwords=(30, 60), seed=9)
-    return [ClientCorpus(synthetic=sc, node=i) for i in range(N_MULTI)]
+    return [ClientCorpus(synthetic=sc, node=i) for i in range(n)]
 
 
-def _multi_worker(rank, world, port, tmp, q):
+def _multi_worker(rank, world, port, tmp, q, n_clients=N_MULTI, env=None, stall=None,
+                  rounds=ROUNDS, epochs=2):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(env or {})
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
     try:
         from gfedntm_amd.federation.hierarchical import assign_clients, run_distributed_multi
-        ids = assign_clients(N_MULTI, world)[rank]
-        corpora = _multi_corpora()
-        out = run_distributed_multi([corpora[i - 1] for i in ids], ids, _params(), max_iters=ROUNDS,
-                                    backend="fused", seed=5, rehearse_1gpu=True,
-                                    save_client=os.path.join(tmp, "client"), stamp="20240101")
+        from gfedntm_amd.federation.runner import CommError
+        ids = assign_clients(n_clients, world)[rank]
+        corpora = _multi_corpora(n_clients)
+
+        def hook(it):
+            if stall and rank == 1 and it == 5:
+                time.sleep(stall)
+
+        try:
+            out = run_distributed_multi([corpora[i - 1] for i in ids], ids,
+                                        dict(_params(), num_epochs=epochs), max_iters=rounds,
+                                        backend="fused", seed=5, rehearse_1gpu=True,
+                                        save_client=os.path.join(tmp, "client"), stamp="20240101",
+                                        round_hook=hook)
+        except CommError as e:
+            q.put((rank, "comm_error", str(e), None, None))
+            return
+        rr = out["round"]
         q.put((rank, out["allreduce"], [c.shared.detach().cpu().numpy().copy() for c in out["clients"]],
-               [c.id for c in out["clients"]]))
+               [c.id for c in out["clients"]], (out["attach"] or {}).get("inplace")))
+        rr.close()
     except Exception:  # pragma: no cover - reported to the parent
         import traceback
-        q.put((rank, "exception", traceback.format_exc(), None))
+        q.put((rank, "exception", traceback.format_exc(), None, None))
     finally:
         dist.destroy_process_group()
 
 
-def test_more_clients_than_ranks_xgmi_matches_grouped_golden(tmp_path):
-    """8 clients on 2 ranks (4 per rank, one GPU): every rank's round graph holds its 4
-    clients' steps, the in-rank fold, the xGMI all-reduce of the partial sums and the
-    broadcast; the final state of all 8 clients equals the in-process federation with
-    the same grouping bit for bit, and every client saves its results."""
+def _run_multi(tmp, **kw):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_multi_worker, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    ps = [ctx.Process(target=_multi_worker, args=(r, 2, port, str(tmp), q), kwargs=kw)
+          for r in range(2)]
     for p in ps:
         p.start()
     res = sorted([q.get(timeout=300) for _ in range(2)], key=lambda r: r[0])
     for p in ps:
         p.join(60)
+    return res
+
+
+@pytest.mark.parametrize("n_clients,inplace_mb", [(N_MULTI, None), (40, "0")])
+def test_more_clients_than_ranks_xgmi_matches_grouped_golden(tmp_path, n_clients, inplace_mb):
+    """8 clients on 2 ranks (4 per rank, one GPU): every rank's round graph holds its 4
+    clients' steps (one launch per phase), the in-rank fold, the xGMI all-reduce of the
+    partial sums and the broadcast -- beta's share forked onto a side stream after the
+    decoder backward; the final state of all clients equals the in-process federation
+    with the same grouping bit for bit, and every client saves its results.  40 clients
+    (20 per rank, past the old 16-buffer fold) with both parts all-reduced in place
+    (GFEDNTM_XGMI_INPLACE_MB=0: two in-place parts of one allocation, one shared mapping)."""
+    env = {} if inplace_mb is None else {"GFEDNTM_XGMI_INPLACE_MB": inplace_mb}
+    res = _run_multi(tmp_path, n_clients=n_clients, env=env)
     for r in res:
-        assert r[1] != "exception", r[2]
-        assert r[1].startswith("xgmi"), r[1]
-    assert [i for r in res for i in r[3]] == list(range(1, N_MULTI + 1))
+        assert r[1] not in ("exception", "comm_error"), r[2]
+        assert r[1] == "xgmi+overlap", r[1]
+        if inplace_mb == "0":
+            assert r[4] == {"rest": True, "beta": True}, r[4]
+    assert [i for r in res for i in r[3]] == list(range(1, n_clients + 1))
     from gfedntm_amd.federation.runner import LocalFederation
-    fed = LocalFederation(_multi_corpora(), _params(), max_iters=ROUNDS, device="cuda",
-                          backend="fused", seed=5, groups=[4, 4])
+    half = n_clients // 2
+    fed = LocalFederation(_multi_corpora(n_clients), _params(), max_iters=ROUNDS, device="cuda",
+                          backend="fused", seed=5, groups=[half, half])
     assert fed.round_graph
     fed.run()
     gold = fed.clients[0].shared.detach().cpu().numpy()
     for r in res:
         for sh in r[2]:
             np.testing.assert_array_equal(sh, gold)
-    for i in range(1, N_MULTI + 1):
+    for i in range(1, n_clients + 1):
         assert os.path.exists(tmp_path / f"client{i}" / f"model_{i}_20240101.npz")
+
+
+def test_more_clients_than_ranks_timed_out_wait_is_polled(tmp_path):
+    """The multi-client runner inherits the periodic error-word poll: a host stall longer
+    than the xGMI spin bound, with no host-heavy round before the end, stops every rank
+    with CommError within a few rounds instead of training on to max_iters."""
+    res = _run_multi(tmp_path, env={"GFEDNTM_XGMI_SPIN": "2000", "GFEDNTM_COMM_POLL": "4"},
+                     stall=2.0, rounds=400, epochs=10 ** 6)
+    for r in res:
+        assert r[1] == "comm_error", r[:3]
+        before = int(r[2].split("before round ")[1].split()[0])
+        assert before < 400, r[2]
 
 
 def test_bench_falls_back_to_rccl_when_xgmi_times_out(tmp_path):
@@ -220,3 +262,6 @@ def test_bench_falls_back_to_rccl_when_xgmi_times_out(tmp_path):
     rec = json.loads(p.stdout.strip().splitlines()[-1])
     assert "xGMI all-reduce failed" in rec["allreduce_fallback"]
     assert rec["value"] > 0 and rec["ranks"] == 2
+    # the injected stall belongs to the failed attempt only: the RCCL re-measure's rounds
+    # are plain (a 2 s stall over 20 rounds would be >= 100 ms per round)
+    assert rec["ms_per_step"] < 50, rec["ms_per_step"]

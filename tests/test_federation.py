@@ -212,11 +212,12 @@ def _multi_worker(rank, world, port, tmp, n_clients, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n_clients,world", [(4, 2), (5, 2)])
+@pytest.mark.parametrize("n_clients,world", [(4, 2), (5, 2), (40, 2)])
 def test_more_clients_than_ranks_matches_grouped_golden(tmp_path, n_clients, world):
     """N clients on R < N gloo ranks (contiguous blocks per rank, hierarchical FedAvg)
     equal the in-process federation with the same grouping; every client of every rank
-    ends holding the same state, and every client's results are written."""
+    ends holding the same state, and every client's results are written.  40 clients on
+    2 ranks: 20 per rank, beyond the old 16-buffer limit of the in-rank fold."""
     import socket
     import torch.multiprocessing as mp
     from gfedntm_amd.federation.hierarchical import assign_clients
@@ -262,3 +263,51 @@ def test_cli_more_clients_than_ranks(tmp_path):
     assert any(f.startswith("global_model_") for f in found)
     for i in range(1, 5):
         assert any(f.startswith(f"model_{i}_") for f in found), (i, found)
+
+
+def _multi_hang_worker(rank, world, port):
+    import datetime
+    import time as _time
+    import torch.distributed as dist
+    from gfedntm_amd.federation import client as client_mod
+    from gfedntm_amd.federation.hierarchical import assign_clients
+    from gfedntm_amd.federation.runner import run_distributed
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=600))
+    orig = client_mod.FederatedClient.local_step
+
+    def local_step(self, it):
+        if rank == 1 and it == 3 and self.id == 3:
+            _time.sleep(600)                  # the main thread hangs; its heartbeat lives on
+        return orig(self, it)
+
+    client_mod.FederatedClient.local_step = local_step
+    ids = assign_clients(4, world)[rank]
+    corpora = _corpora(4)
+    run_distributed([corpora[i - 1] for i in ids], _params(), max_iters=50, backend="torch",
+                    heartbeat_timeout=10.0, client_ids=ids)
+
+
+def test_heartbeat_with_more_clients_than_ranks():
+    """--heartbeat_timeout with N > R (2 clients per rank): a rank whose loop hangs in one
+    of its clients' steps is detected by its peer, which aborts (exit code 3) instead of
+    blocking in the collective -- the same watchdog as one client per rank."""
+    import socket
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ps = [ctx.Process(target=_multi_hang_worker, args=(r, 2, port)) for r in range(2)]
+    for p in ps:
+        p.start()
+    ps[0].join(120)
+    try:
+        assert ps[0].exitcode == 3, ps[0].exitcode
+    finally:
+        for p in ps:
+            if p.is_alive():
+                p.kill()
+            p.join(10)

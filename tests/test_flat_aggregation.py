@@ -4,6 +4,7 @@ import numpy as np
 import torch
 
 from gfedntm_amd.models.networks import DecoderNetwork
+from gfedntm_amd.ops.engine import BETA_PAD
 from gfedntm_amd.parallel.aggregator import LocalAggregator, fedavg_weights
 from gfedntm_amd.utils.config import DEFAULT_GRADS_TO_SHARE
 from gfedntm_amd.utils.flat import ALIGN, FlatState
@@ -37,12 +38,12 @@ def test_flat_views_and_shared_prefix():
 
 
 def test_padded_beta_rows():
-    """beta stored with 128-B rows ({"beta": 32}): the module sees the [K, V] slice, the
+    """beta stored with 256-B rows ({"beta": BETA_PAD}, the fused engine's layout): the module sees the [K, V] slice, the
     state_dict / load_state_dict round trip is exact, the pad columns are zero and in the
     slot's storage (param ranges, FedAvg prefix), and rows start on 32-float boundaries."""
     m = _net()                                   # beta [5, 60] -> rows of 64 floats
     before = {k: v.clone() for k, v in m.state_dict().items()}
-    fs = FlatState(m, ["beta", "prior_mean"], padded={"beta": 32}, shared_last=("beta",))
+    fs = FlatState(m, ["beta", "prior_mean"], padded={"beta": BETA_PAD}, shared_last=("beta",))
     s = fs.slots["beta"]
     assert s.ld == 64 and s.numel == 5 * 64 and s.offset % 32 == 0
     assert m.beta.shape == (5, 60) and m.beta.stride() == (64, 1)

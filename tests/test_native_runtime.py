@@ -60,3 +60,32 @@ def test_runtime_under_asan_ubsan(tmp_path):
                UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
     run = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=300)
     assert run.returncode == 0 and "runtime sanitize ok" in run.stdout, run.stderr[-2000:]
+
+
+def test_kernel_library_is_tied_to_the_sources(monkeypatch):
+    """The kernel library embeds the hash of the csrc/ it was built from; the loader
+    accepts exactly the tree's hash and refuses any other build unless
+    GFEDNTM_KERNELS_SO names it on purpose (A/B timing)."""
+    from gfedntm_amd.ops import srchash
+    if not native.kernels_available():
+        pytest.skip("kernel library not built")
+    assert native.kernels_hash() == srchash.source_hash()
+
+    class _Fn:
+        def __init__(self, v):
+            self.v = v
+            self.restype = self.argtypes = None
+
+        def __call__(self):
+            return self.v
+
+    class _Lib:
+        def __init__(self, v):
+            self.gfk_source_hash = _Fn(v)
+
+    native._check_source(_Lib(srchash.source_hash().encode()))
+    monkeypatch.setattr(native, "KERNELS_SO_OVERRIDE", None)
+    with pytest.raises(RuntimeError, match="other sources"):
+        native._check_source(_Lib(b"0000000000000000"))
+    monkeypatch.setattr(native, "KERNELS_SO_OVERRIDE", "/tmp/ab/libgfedntm_kernels.so")
+    native._check_source(_Lib(b"0000000000000000"))      # explicit A/B build: warn only

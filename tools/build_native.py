@@ -10,6 +10,7 @@ never links stale objects.
 """
 import concurrent.futures as cf
 import glob
+import importlib.util
 import os
 import subprocess
 import sys
@@ -20,15 +21,14 @@ LIB = os.path.join(ROOT, "gfedntm_amd", "_lib")
 OBJ = os.path.join(ROOT, "build", "obj")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-KERNEL_SRCS = ["ctx.hip", "encoder.hip", "posterior.hip", "prodlda.hip", "neurallda.hip", "update.hip",
-               "adam.hip", "comm.hip", "infer.hip", "step.cpp"]
+# the kernel sources and flags live next to the hash that identifies them
+# (gfedntm_amd/ops/srchash.py, loaded standalone: no torch import at build time)
+_spec = importlib.util.spec_from_file_location(
+    "_gfk_srchash", os.path.join(ROOT, "gfedntm_amd", "ops", "srchash.py"))
+srchash = importlib.util.module_from_spec(_spec)
+_spec.loader.exec_module(srchash)
+KERNEL_SRCS, KFLAGS = srchash.KERNEL_SRCS, srchash.KFLAGS
 RUNTIME_SRCS = ["runtime.cpp"]
-# kernel flags.  fp32 division / sqrt and expf / logf use the hardware instructions
-# (v_rcp / v_sqrt / v_exp / v_log, ~1 ulp) instead of the correctly rounded library
-# sequences: the fused kernels' epilogues are VALU-bound, and every numerics test
-# compares with a PyTorch fp32 oracle under tolerances, never bitwise.
-KFLAGS = ["-O3", "-fPIC", "-std=c++17", "-munsafe-fp-atomics", "-Wno-unused-result",
-          "-fno-hip-fp32-correctly-rounded-divide-sqrt", "-fgpu-approx-transcendentals"]
 
 
 def _stale(src, obj, deps, cmd):
@@ -90,6 +90,18 @@ def build(verbose=True, jobs=8):
         cmd = [HIPCC, f"--offload-arch={ARCH}"] + KFLAGS + ["-c", src, "-o", obj]
         if _stale(src, obj, headers, cmd):
             jobs_list.append((cmd, s, obj))
+    # the source identity (gfk_source_hash), checked by gfedntm_amd/ops/native.py at load
+    digest = srchash.source_hash(ARCH)
+    hsrc = os.path.join(OBJ, "srchash.cpp")
+    text = ('extern "C" const char* gfk_source_hash() { return "%s"; }\n' % digest)
+    if not os.path.exists(hsrc) or open(hsrc).read() != text:
+        with open(hsrc, "w") as f:
+            f.write(text)
+    hobj = os.path.join(OBJ, "srchash.cpp.o")
+    kobjs.append(hobj)
+    hcmd = ["g++", "-O2", "-fPIC", "-c", hsrc, "-o", hobj]
+    if _stale(hsrc, hobj, [], hcmd):
+        jobs_list.append((hcmd, "srchash.cpp", hobj))
     robjs = []
     for s in RUNTIME_SRCS:
         src = os.path.join(CSRC, s)
