@@ -512,7 +512,7 @@ def _record(args, value, ms, V, npmi, final_loss, clients: int, ranks: int, phys
                          "figure is the --gpus 8 run" if clients == 1 else
                          f"{clients} federated clients on {physical} physical GPU(s)"),
         **({"precision": "bf16 operands of the ProdLDA decoder GEMMs (theta.beta, theta^T.dlogit, "
-                         "dlogit.beta^T) on v_mfma_f32_16x16x16_bf16, fp32 accumulation; fp32 "
+                         "dlogit.beta^T) on v_mfma_f32_16x16x32_bf16, fp32 accumulation; fp32 "
                          "parameters, Adam state and every other op"} if args.dtype == "bf16" else {}),
         # the source hash embedded in the kernel library that ran (gfedntm_amd/ops/srchash.py)
         "kernels_src_hash": _kernels_hash(args),

@@ -136,7 +136,7 @@ typedef struct GfkModel {
   float* ws_sval;
   // ---- precision of the decoder GEMMs (theta.beta, theta^T.dlogit, dlogit.beta^T):
   // 0 = fp32 matrix cores (v_mfma_f32_16x16x4_f32, the reference's precision), 1 = bf16
-  // operands, fp32 accumulation (v_mfma_f32_16x16x16_bf16); parameters, Adam state and
+  // operands, fp32 accumulation (v_mfma_f32_16x16x32_bf16); parameters, Adam state and
   // every other op stay fp32
   int32_t mm_bf16;
   int32_t pad2;
@@ -582,9 +582,18 @@ __device__ __forceinline__ f32x4 mfma16x16x4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// 16x16x16 bf16 MFMA, fp32 accumulation: lane l supplies A[l&15][4(l>>4) + j] and
-// B[4(l>>4) + j][l&15] (j < 4) as fp32, rounded to bf16 here (v_cvt_pk_bf16_f32, RNE);
-// the result layout is the one of mfma16x16x4.
+// bf16 MFMA, fp32 accumulation.  gfx950's 16x16x32 (v_mfma_f32_16x16x32_bf16, twice the
+// K of the CDNA3-era 16x16x16 per instruction): lane l supplies A[l&15][8(l>>4) + j] and
+// B[8(l>>4) + j][l&15] (j < 8) as fp32, rounded to bf16 here (v_cvt_pk_bf16_f32, RNE);
+// the 16x16x16 form (j < 4, 4(l>>4) + j) serves a K tail of 16.  The result layout is
+// the one of mfma16x16x4.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f32x4 mfma16x16x32bf(const float (&a)[8], const float (&b)[8], f32x4 c) {
+  bf16x8 ab, bb;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { ab[j] = (__bf16)a[j]; bb[j] = (__bf16)b[j]; }
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ab, bb, c, 0, 0, 0);
+}
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f32x4 mfma16x16x16bf(const float (&a)[4], const float (&b)[4], f32x4 c) {

@@ -80,7 +80,7 @@ __device__ __forceinline__ float sum_groups(float v) {
 // statistics are loaded into registers right after this tile's staging barrier, so
 // they land while this tile's MFMAs / batch-norm / stores run.
 // dynamic LDS: th[BM*kt] + bt[KP*LDB_F] + colp[4][64] + colq[4][64] + stat[2][64]
-// BF: bf16 MFMA operands (16x16x16, K padded to 16), fp32 accumulation.
+// BF: bf16 MFMA operands (16x16x32, a 16x16x16 tail; K padded to 16), fp32 accumulation.
 template <int BM, bool BF, bool GB = false>
 __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkArgT<GB> ga) {
   const GfkModel& m = gfk_model(ga);
@@ -158,18 +158,39 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkArgT<GB> ga
   if constexpr (BF) {
 #pragma unroll
     for (int i = 0; i < NRT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int kq = 4 * (lane >> 4);
-    const float* bp = bt + kq * LDB_F + col;
-    const float* ap = th + (rt0 * 16 + (lane & 15)) * KT + kq;
+    const float* ap0 = th + (rt0 * 16 + (lane & 15)) * KT;
     if (rt0 < RT) {
-      for (int k0 = 0; k0 < KP; k0 += 16) {
+      // K in steps of 32 (16x16x32), a tail of 16 when KP % 32 == 16 (16x16x16)
+      int k0 = 0;
+      {
+        const int kq = 8 * (lane >> 4);
+        const float* bp = bt + kq * LDB_F + col;
+        const float* ap = ap0 + kq;
+        for (; k0 + 32 <= KP; k0 += 32) {
+          float b[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) b[j] = bp[(k0 + j) * LDB_F];
+#pragma unroll
+          for (int i = 0; i < NRT; ++i)
+            if (rt0 + 4 * i < RT) {
+              float a[8];     // theta_d rows hold kt >= K columns: mask the K..16-padding
+#pragma unroll
+              for (int j = 0; j < 8; ++j) a[j] = k0 + kq + j < K ? ap[i * 64 * KT + k0 + j] : 0.f;
+              acc[i] = mfma16x16x32bf(a, b, acc[i]);
+            }
+        }
+      }
+      if (k0 < KP) {
+        const int kq = 4 * (lane >> 4);
+        const float* bp = bt + kq * LDB_F + col;
+        const float* ap = ap0 + kq;
         float b[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) b[j] = bp[(k0 + j) * LDB_F];
 #pragma unroll
         for (int i = 0; i < NRT; ++i)
           if (rt0 + 4 * i < RT) {
-            float a[4];     // theta_d rows hold kt >= K columns: mask the K..16-padding
+            float a[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) a[j] = k0 + kq + j < K ? ap[i * 64 * KT + k0 + j] : 0.f;
             acc[i] = mfma16x16x16bf(a, b, acc[i]);
@@ -757,7 +778,7 @@ __global__ void __launch_bounds__(256) prodlda_dlogit_kernel(GfkArgT<GB> ga) {
   for (int i = tid; i < BM * LDD / 4; i += NT) out[i] = d4[i];
 }
 
-// BF: bf16 MFMA operands (16x16x16), fp32 accumulation, for both GEMMs.
+// BF: bf16 MFMA operands (16x16x32 / 16x16x16), fp32 accumulation, for both GEMMs.
 // PRE (bwd_pre, KQ = 4 only): the logit-gradient tile comes precomputed from ws_dt
 // (prodlda_dlogit): no sparse / dense passes, no dependent loads in the staging round.
 // Its LDS is th [BM][64] (theta_d's k range, row r's columns XOR 16 (r & 1): the dbeta
@@ -999,16 +1020,16 @@ __device__ __forceinline__ void prodlda_bwd_body(const GfkModel& m) {
       const int t = wave + NW * j;
       if (t >= NDT_T) break;
       const int rt = t / nks, ks = t % nks;
-      if constexpr (BF) {         // A[b][c] = dt row, B[c][k] = beta row: 4 consecutive c each
-        const float* ap = dt + (rt * 16 + (lane & 15)) * LDD + 4 * (lane >> 4);
-        const float* bp = bt + (ks * 16 + (lane & 15)) * LDB_B + 4 * (lane >> 4);
+      if constexpr (BF) {         // A[b][c] = dt row, B[c][k] = beta row: 8 consecutive c each
+        const float* ap = dt + (rt * 16 + (lane & 15)) * LDD + 8 * (lane >> 4);
+        const float* bp = bt + (ks * 16 + (lane & 15)) * LDB_B + 8 * (lane >> 4);
         f32x4 a0 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int c = 0; c < VB; c += 16) {
-          float a[4], b[4];
+        for (int c = 0; c < VB; c += 32) {
+          float a[8], b[8];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) { a[q] = ap[c + q]; b[q] = bp[c + q]; }
-          a0 = mfma16x16x16bf(a, b, a0);
+          for (int q = 0; q < 8; ++q) { a[q] = ap[c + q]; b[q] = bp[c + q]; }
+          a0 = mfma16x16x32bf(a, b, a0);
         }
         dacc[j] += a0;
       } else {
@@ -1036,21 +1057,39 @@ __device__ __forceinline__ void prodlda_bwd_body(const GfkModel& m) {
         if (t >= NB_T) break;
         const int ks = t >> 2, cst = t & 3;
         f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
-        if constexpr (BF) {       // A[k][b] = theta_d column, B[b][c] = dt column: 4 rows b each
-          // (PRE: theta_d rows 4 g + b0 + q, b0 a multiple of 16: swizzle 16 ((g >> 1) & 1))
-          const float* ap = th + 4 * (lane >> 4) * KTQ +
-                            (PRE ? (ks * 16 + (lane & 15)) ^ ((((lane >> 4) >> 1) & 1) << 4)
-                                 : ks * 16 + (lane & 15));
-          const float* bp = dt + 4 * (lane >> 4) * LDD + cst * 16 + (lane & 15);
+        if constexpr (BF) {       // A[k][b] = theta_d column, B[b][c] = dt column
+          if constexpr (BM % 32 == 0) {
+            // 8 rows b each: rows 8 g + b0 + q, b0 a multiple of 32 (PRE: swizzle 16 (g & 1))
+            const float* ap = th + 8 * (lane >> 4) * KTQ +
+                              (PRE ? (ks * 16 + (lane & 15)) ^ (((lane >> 4) & 1) << 4)
+                                   : ks * 16 + (lane & 15));
+            const float* bp = dt + 8 * (lane >> 4) * LDD + cst * 16 + (lane & 15);
 #pragma unroll
-          for (int b0 = 0; b0 < BM; b0 += 16) {
-            float a[4], b[4];
+            for (int b0 = 0; b0 < BM; b0 += 32) {
+              float a[8], b[8];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              a[q] = ap[(b0 + q) * KTQ];
-              b[q] = bp[(b0 + q) * LDD];
+              for (int q = 0; q < 8; ++q) {
+                a[q] = ap[(b0 + q) * KTQ];
+                b[q] = bp[(b0 + q) * LDD];
+              }
+              a0 = mfma16x16x32bf(a, b, a0);
             }
-            a0 = mfma16x16x16bf(a, b, a0);
+          } else {
+            // 4 rows b each: rows 4 g + b0 + q, b0 a multiple of 16 (PRE: 16 ((g >> 1) & 1))
+            const float* ap = th + 4 * (lane >> 4) * KTQ +
+                              (PRE ? (ks * 16 + (lane & 15)) ^ ((((lane >> 4) >> 1) & 1) << 4)
+                                   : ks * 16 + (lane & 15));
+            const float* bp = dt + 4 * (lane >> 4) * LDD + cst * 16 + (lane & 15);
+#pragma unroll
+            for (int b0 = 0; b0 < BM; b0 += 16) {
+              float a[4], b[4];
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                a[q] = ap[(b0 + q) * KTQ];
+                b[q] = bp[(b0 + q) * LDD];
+              }
+              a0 = mfma16x16x16bf(a, b, a0);
+            }
           }
         } else {
           // The batch index b is the MFMA's reduction axis, so any bijection of b over

@@ -55,6 +55,10 @@ extern "C" size_t gfk_win_update_smem(const GfkModel* m) {
   // the sparse tile (bit 4): dz0, the entry list, the row slots (+ the word mask and list)
   const size_t c = (size_t)B * m->H[0] + 2 * 512 + 129 + 128;
   if (a < c) a = c;
+  // the dense contextual tile next to them (fused CombinedTM): dz0 + the A block / G tile
+  const size_t d = (((size_t)B * m->H[0] + 3) & ~(size_t)3) +
+                   ((size_t)B * 64 > (size_t)64 * m->H[0] ? (size_t)B * 64 : (size_t)64 * m->H[0]);
+  if (m->input == GFK_IN_COMBINED && a < d) a = d;
   return sizeof(float) * (a > b ? a : b);
 }
 
@@ -368,6 +372,114 @@ __device__ __forceinline__ void win_tile_sparse(const GfkModel& m, float* smem, 
       if constexpr (VL) b = e + i < nel ? vb[e + i] : 0.f;
       else b = pv[u][i];
       const float x = fused ? adam_update(pp[u][i], g[u][i], a, b, ac) : g[u][i];
+      np[i] = sh && m.fed_scale_on && fused ? x * m.fed_scale : x;
+      mo[i] = a;
+      vo[i] = b;
+    }
+    auto st4 = [&](float* q, const f32x4& x) {
+      if (al4 && e + 3 < nel) { *reinterpret_cast<f32x4*>(q + e) = x; return; }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) if (e + i < nel) q[e + i] = x[i];
+    };
+    if (!fused) {
+      st4(wblk + m.off_g, np);
+    } else {
+      st4(wblk + m.off_m, mo);
+      st4(wblk + m.off_v, vo);
+      st4(wblk, np);
+    }
+  }
+}
+
+// CombinedTM's contextual input-layer tile next to the sparse bag-of-words tiles (one
+// launch, stage_flags bit 4 with ctx_fused == 1): Wc = rows V..2V-1 of the transposed
+// input layer, G[v, h] = sum_{b < nb} A[b, v] dz0[b, h] with A the tile's adapted rows
+// (ctx_fwd's ws_actx slab, [B][64]).  Both operand blocks arrive by LDS-DMA in their
+// global layout ([B][64] and [B][H0], contiguous) -- no transposing scatter: the MFMA's
+// reduction axis is b, and both roles read 16 consecutive columns of 4 rows per wave.
+// The gradient tile is parked in the A block's LDS (free after the products) in the
+// W block's flat order, and the epilogue moves p / m / v as flat quads prefetched before
+// the products, like the sparse tile's.  B <= 64, H0 <= 64.
+template <int UT>
+__device__ __forceinline__ void win_tile_ctx(const GfkModel& m, float* smem, int tile) {
+  constexpr int UW = UT / 64;
+  constexpr int FQ = 64 * 64 / 4 / UT;         // quads per thread (H0 <= 64)
+  const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
+  const int B = m.bmax, H0 = m.H[0], V = m.V, c0 = tile * 64;
+  const int nb = *m.ws_nb;
+  float* dz = smem;                                       // [B][H0]
+  float* at = smem + ((B * H0 + 3) & ~3);                 // [B][64], then G [64][H0]
+  float* wblk = m.w_in + (size_t)(V + c0) * H0;
+  const int nel = (min(V, c0 + 64) - c0) * H0;
+  const bool fused = m.update_mode == 1;
+  const bool al4 = ((uintptr_t)wblk % 16 == 0) && m.off_m % 4 == 0 && m.off_v % 4 == 0 &&
+                   m.off_g % 4 == 0;
+  auto ld4 = [&](const float* q, int e) {
+    if (al4 && e + 3 < nel) return *reinterpret_cast<const f32x4*>(q + e);
+    f32x4 r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = e + i < nel ? q[e + i] : 0.f;
+    return r;
+  };
+  // ---- one staging round: the operand blocks (LDS-DMA), then the W block's p / m / v ----
+  glds_copy(dz, m.ws_dz[0], B * H0, tid, UT);
+  glds_copy(at, m.ws_actx + (size_t)tile * B * 64, B * 64, tid, UT);
+  f32x4 pp[FQ], pm[FQ], pv[FQ];
+#pragma unroll
+  for (int u = 0; u < FQ; ++u) {
+    const int e = 4 * (tid + UT * u);
+    pp[u] = pm[u] = pv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (fused && e < nel) {
+      pp[u] = ld4(wblk, e);
+      pm[u] = ld4(wblk + m.off_m, e);
+      pv[u] = ld4(wblk + m.off_v, e);
+    }
+  }
+  vm_barrier();
+  // ---- G subtiles (v tile, h tile) = t = wave + UW u: rows b >= nb masked in the A role;
+  //      columns h >= H0 read the next row's dz (discarded outputs) ----
+  const int NT = (H0 + 15) / 16, NST = 4 * NT;
+  constexpr int SU = 16 / UW;                   // subtiles per wave (H0 <= 64: <= 16 in all)
+  f32x4 acc[SU];
+#pragma unroll
+  for (int u = 0; u < SU; ++u) {
+    const int t = wave + UW * u;
+    acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (t >= NST) continue;
+    const int i0 = (t / NT) * 16, j0 = (t % NT) * 16;
+    const float* ap = at + (lane >> 4) * 64 + i0 + (lane & 15);
+    const float* bp = dz + (lane >> 4) * H0 + j0 + (lane & 15);
+    for (int k = 0; k < B; k += 4) {
+      const float a = k + (lane >> 4) < nb ? ap[k * 64] : 0.f;
+      acc[u] = mfma16x16x4(a, bp[k * H0], acc[u]);
+    }
+  }
+  lds_barrier();                                // every wave is done reading the A block
+#pragma unroll
+  for (int u = 0; u < SU; ++u) {
+    const int t = wave + UW * u;
+    if (t >= NST) continue;
+    const int i0 = (t / NT) * 16, j = (t % NT) * 16 + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (j < H0) at[(i0 + (lane >> 4) * 4 + r) * H0 + j] = acc[u][r];
+  }
+  lds_barrier();
+  // ---- update (fused: Adam + FedAvg pre-scale) or the gradient, flat quads ----
+  const AdamCoef ac = adam_coef(m);
+  const bool sh = is_shared(m, m.w_in);
+#pragma unroll
+  for (int u = 0; u < FQ; ++u) {
+    const int e = 4 * (tid + UT * u);
+    if (e >= nel) break;
+    f32x4 g;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) g[i] = e + i < nel ? at[e + i] : 0.f;
+    f32x4 np, mo, vo;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float a = pm[u][i], b = pv[u][i];
+      const float x = fused ? adam_update(pp[u][i], g[i], a, b, ac) : g[i];
       np[i] = sh && m.fed_scale_on && fused ? x * m.fed_scale : x;
       mo[i] = a;
       vo[i] = b;
@@ -890,8 +1002,8 @@ __global__ void __launch_bounds__(UT) gfk_win_update_k(GfkArgT<GB> ga, GfkUArgT<
 // the sparse W_in tiles (stage_flags bit 4) as their own kernel: its register budget is
 // its own (the job paths of gfk_win_update_k need ~86 VGPRs)
 // grid: n_w + n_v + 1 job workgroups FIRST (they start with the tiles, not after them),
-// then the n_tiles sparse W_in tiles
-template <int UT, bool GB = false, bool VL = false>
+// then the n_tiles sparse W_in tiles (+ n_tiles dense contextual tiles: fused CombinedTM)
+template <int UT, bool GB = false, bool VL = false, bool CTX = false>
 __global__ void __launch_bounds__(UT, VL ? 4096 / UT : 1) gfk_win_sparse_k(GfkArgT<GB> ga, GfkUArgT<GB> gua) {
   const GfkModel& m = gfk_model(ga);
   const GfkUpdate& U = gfk_upd(gua);
@@ -900,7 +1012,11 @@ __global__ void __launch_bounds__(UT, VL ? 4096 / UT : 1) gfk_win_sparse_k(GfkAr
   if (r < U.n_w) { weight_job<UT>(m, U.w[r], smem); return; }
   if (r < U.n_w + U.n_v) { vector_job<UT>(m, U.v[r - U.n_w]); return; }
   if (r == U.n_w + U.n_v) { prepare_next_batch(m, reinterpret_cast<int*>(smem)); return; }
-  win_tile_sparse<UT, VL>(m, smem, r - (U.n_w + U.n_v + 1));
+  const int t = r - (U.n_w + U.n_v + 1);
+  if constexpr (CTX) {
+    if (t >= m.n_tiles) { win_tile_ctx<UT>(m, smem, t - m.n_tiles); return; }
+  }
+  win_tile_sparse<UT, VL>(m, smem, t);
 }
 
 // the split update's sparse half: the same job workgroups, then the batch words' tiles (its
@@ -940,17 +1056,37 @@ static bool win_sparse_vl(const GfkModel* m) {
   return need <= gfk_win_update_smem(m);
 }
 
+#define GFK_WIN_SPARSE_LAUNCH(VL, CTX)                                                               \
+  do {                                                                                           \
+    if (m->n_batch > 1)                                                                          \
+      hipLaunchKernelGGL((gfk_win_sparse_k<512, true, VL, CTX>), gfk_grid(gs, m), dim3(512),     \
+                         gfk_win_update_smem(m), s, GfkArgT<true>{gfk_dev(m)},                   \
+                         GfkUArgT<true>{reinterpret_cast<const GfkUpdate*>(m->dev_upd)});        \
+    else                                                                                         \
+      hipLaunchKernelGGL((gfk_win_sparse_k<512, false, VL, CTX>), gs, dim3(512),                 \
+                         gfk_win_update_smem(m), s, GfkArgT<false>{*m}, GfkUArgT<false>{*u});    \
+  } while (0)
+
 extern "C" int gfk_launch_win_update(const GfkModel* m, const GfkUpdate* u, hipStream_t s) {
   const int extra = m->ctx_fused == 1 ? m->n_tiles : (m->ctx_fused == 2 ? (m->C + 63) / 64 : 0);
   if (m->stage_flags & WIN_SPARSE) {
-    if (m->H[0] > 64 || m->input != GFK_IN_BOW || m->bmax > 128) return -1;
-    const dim3 gs(u->n_w + u->n_v + 1 + m->n_tiles);
+    // bag-of-words inputs, or fused CombinedTM (its contextual half as dense tiles after
+    // the sparse ones: B <= 64 so the operand blocks fit the kernel's LDS)
+    const bool comb = m->input == GFK_IN_COMBINED && m->ctx_fused == 1;
+    if (m->H[0] > 64 || m->bmax > (comb ? 64 : 128) || !(m->input == GFK_IN_BOW || comb) ||
+        (comb && (m->stage_flags & GFK_WIN_SPLIT)))
+      return -1;
+    const dim3 gs(u->n_w + u->n_v + 1 + m->n_tiles * (comb ? 2 : 1));
     if (m->stage_flags & GFK_WIN_SPLIT)
       do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_win_rows_k<512, true>), gfk_grid(gs, m), dim3(512), gfk_win_update_smem(m), s, GfkArgT<true>{gfk_dev(m)}, GfkUArgT<true>{reinterpret_cast<const GfkUpdate*>(m->dev_upd)}); else hipLaunchKernelGGL((gfk_win_rows_k<512, false>), gs, dim3(512), gfk_win_update_smem(m), s, GfkArgT<false>{*m}, GfkUArgT<false>{*u}); } while (0);
+    else if (comb && win_sparse_vl(m))
+      GFK_WIN_SPARSE_LAUNCH(true, true);
+    else if (comb)
+      GFK_WIN_SPARSE_LAUNCH(false, true);
     else if (win_sparse_vl(m))
-      do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_win_sparse_k<512, true, true>), gfk_grid(gs, m), dim3(512), gfk_win_update_smem(m), s, GfkArgT<true>{gfk_dev(m)}, GfkUArgT<true>{reinterpret_cast<const GfkUpdate*>(m->dev_upd)}); else hipLaunchKernelGGL((gfk_win_sparse_k<512, false, true>), gs, dim3(512), gfk_win_update_smem(m), s, GfkArgT<false>{*m}, GfkUArgT<false>{*u}); } while (0);
+      GFK_WIN_SPARSE_LAUNCH(true, false);
     else
-      do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_win_sparse_k<512, true>), gfk_grid(gs, m), dim3(512), gfk_win_update_smem(m), s, GfkArgT<true>{gfk_dev(m)}, GfkUArgT<true>{reinterpret_cast<const GfkUpdate*>(m->dev_upd)}); else hipLaunchKernelGGL((gfk_win_sparse_k<512, false>), gs, dim3(512), gfk_win_update_smem(m), s, GfkArgT<false>{*m}, GfkUArgT<false>{*u}); } while (0);
+      GFK_WIN_SPARSE_LAUNCH(false, false);
     return (int)hipGetLastError();
   }
   const dim3 g(m->n_tiles + u->n_w + u->n_v + 1 + extra);
@@ -974,6 +1110,8 @@ extern "C" int gfk_win_update_set_smem(size_t bytes) {
                       (const void*)gfk_win_update_k<1024, false>, (const void*)gfk_win_update_k<1024, true>,
                       (const void*)gfk_win_sparse_k<512, false>, (const void*)gfk_win_sparse_k<512, true>,
                       (const void*)gfk_win_sparse_k<512, false, true>, (const void*)gfk_win_sparse_k<512, true, true>,
+                      (const void*)gfk_win_sparse_k<512, false, false, true>, (const void*)gfk_win_sparse_k<512, true, false, true>,
+                      (const void*)gfk_win_sparse_k<512, false, true, true>, (const void*)gfk_win_sparse_k<512, true, true, true>,
                       (const void*)gfk_win_rows_k<512, false>, (const void*)gfk_win_rows_k<512, true>};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);

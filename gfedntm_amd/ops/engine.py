@@ -559,7 +559,10 @@ class FusedEngine(EngineBase):
                 cf_env == "1" or (cf_env == "auto" and m.n_tiles > 2 * cu_n)):
             m.stage_flags |= STAGE_CTX_FULL
         ws_env = os.environ.get("GFEDNTM_WIN_SPARSE", "auto")
-        if m.input == abi.IN_BOW and int(m.H[0]) <= 64 and m.bmax <= 128 and (
+        # (fused CombinedTM too: its bag-of-words half as sparse tiles, the contextual half
+        # as dense tiles of the same launch -- csrc/update.hip win_tile_ctx; B <= 64)
+        comb = m.input == abi.IN_COMBINED and m.ctx_fused == 1 and m.bmax <= 64
+        if (m.input == abi.IN_BOW or comb) and int(m.H[0]) <= 64 and m.bmax <= 128 and (
                 ws_env == "1" or (ws_env == "auto" and m.n_tiles > 4 * cu_n)):
             m.stage_flags |= STAGE_WIN_SPARSE
             # fused mode: the tile's second moment goes through LDS (64 VGPRs, 4 workgroups
@@ -576,7 +579,8 @@ class FusedEngine(EngineBase):
             # three dependent rounds per tile (28 us)
             win_al = (int(m.w_in or 0) % 16 == 0
                       and m.off_m % 4 == 0 and m.off_v % 4 == 0)
-            self._win_split_ok = os.environ.get("GFEDNTM_WIN_SPLIT", "0") == "1" and win_al
+            self._win_split_ok = (os.environ.get("GFEDNTM_WIN_SPLIT", "0") == "1" and win_al
+                                  and m.input == abi.IN_BOW)
             if self._win_split_ok and self.update_mode == UPDATE_FUSED:
                 m.stage_flags |= STAGE_WIN_SPLIT
         self._alloc_workspace()

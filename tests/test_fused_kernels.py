@@ -736,3 +736,49 @@ def test_ctm_full_tile_forward_matches_oracle(monkeypatch, Cdim, V):
     GFEDNTM_CTX_FULL=1 forces it at small V)."""
     monkeypatch.setenv("GFEDNTM_CTX_FULL", "1")
     test_ctm_step_matches_oracle("combined", Cdim, V, 20, "prodLDA")
+
+
+@pytest.mark.parametrize("Cdim,V", [(96, 600), (768, 9000)])
+def test_ctm_sparse_win_tiles_match_oracle(monkeypatch, Cdim, V):
+    """CombinedTM with the sparse W_in tiles (GFEDNTM_WIN_SPARSE=1 forces the large-V
+    path): the bag-of-words half as entry-list tiles and the contextual half as dense
+    A^T dz0 tiles of the same launch (csrc/update.hip win_tile_ctx) give the oracle's
+    input-layer gradient (both halves)."""
+    monkeypatch.setenv("GFEDNTM_WIN_SPARSE", "1")
+    test_ctm_step_matches_oracle("combined", Cdim, V, 20, "prodLDA")
+
+
+def test_ctm_sparse_win_tiles_fused_update(monkeypatch):
+    """The same tiles in the fused update mode (Adam + FedAvg pre-scale in win_tile_ctx's
+    epilogue) == gradient mode + the generic Adam."""
+    monkeypatch.setenv("GFEDNTM_WIN_SPARSE", "1")
+    from gfedntm_amd.ops.engine import STAGE_WIN_SPARSE
+    from gfedntm_amd.models import CombinedTM
+    torch.manual_seed(0)
+    kw = dict(input_size=900, contextual_size=64, n_components=30, hidden_sizes=(48, 40),
+              batch_size=64, verbose=False, device="cuda", backend="fused")
+    a, b = CombinedTM(**kw), CombinedTM(**kw)
+    assert a.engine._m.stage_flags & STAGE_WIN_SPARSE
+    b.model.load_state_dict(a.model.state_dict())
+    b.engine.seed = b.engine._m.seed = a.engine.seed
+    b.engine.set_update_mode(UPDATE_GRAD)
+    X = random_csr(200, 900, 40, seed=3)
+    ctx = np.random.default_rng(4).standard_normal((200, 64)).astype(np.float32)
+    for t in (a, b):
+        t.engine.set_fedavg_scale(0.75)
+        t.engine.bind_data(DeviceCSR(X, "cuda", contextual=ctx), BatchPlan.build(200, 64, 5, seed=0))
+    for s in range(5):
+        a.engine.step(s)
+        b.engine.step(s)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(a.engine.loss_hist, b.engine.loss_hist, rtol=1e-4, atol=1e-2)
+    sa, sb = a.model.state_dict(), b.model.state_dict()
+    lr_steps = 2 * a.engine.lr * 5
+    for k in sb:
+        if not sb[k].is_floating_point():
+            assert torch.equal(sa[k], sb[k]), k
+            continue
+        noisy = k in _NOISE_KEYS or k.startswith(("inf_net.f_mu_batchnorm.running_mean",
+                                                   "inf_net.f_sigma_batchnorm.running_mean"))
+        torch.testing.assert_close(sa[k], sb[k], rtol=1e-3, atol=lr_steps if noisy else 5e-5,
+                                   msg=lambda m: f"{k}: {m}")

@@ -1,9 +1,9 @@
 """Diagnostic: build the kernel library of a git revision (or of the working tree) into
-ab/<name>/libgfedntm_kernels.so, for A/B timing of kernel variants in ONE GPU call:
+abtmp/<name>/libgfedntm_kernels.so, for A/B timing of kernel variants in ONE GPU call:
 
     python tools/ab_libs.py A HEAD        # the committed sources
     python tools/ab_libs.py B             # the working tree
-    GFEDNTM_KERNELS_SO=ab/A/libgfedntm_kernels.so python bench.py ...
+    GFEDNTM_KERNELS_SO=abtmp/A/libgfedntm_kernels.so python bench.py ...
 
 (the Python package and the runtime library stay the working tree's: only variants
 with the same kernel ABI can be compared this way).
@@ -22,7 +22,7 @@ from tools.build_native import ARCH, HIPCC, KERNEL_SRCS, KFLAGS  # noqa: E402
 def main(argv):
     name = argv[0]
     rev = argv[1] if len(argv) > 1 else None
-    out = os.path.join(ROOT, "ab", name)
+    out = os.path.join(ROOT, "abtmp", name)   # (delete after the A/B call: not product)
     os.makedirs(out, exist_ok=True)
     with tempfile.TemporaryDirectory() as tmp:
         src_dir = os.path.join(ROOT, "csrc")
