@@ -276,9 +276,23 @@ __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkArgT<GB> ga) {
     else if (H0 <= 256) gather_slots<4>(sidx, sval, n, gv, gx, wave, w_in, H0, lane, acc);
     else gather_slots<8>(sidx, sval, n, gv, gx, wave, w_in, H0, lane, acc);
     if (m.ctx_fused) {      // CombinedTM: the row's contextual partials from ctx_fwd (fixed order)
-      const int P = m.n_tiles;
+      const int P = m.ctx_parts > 0 ? m.ctx_parts : m.n_tiles;
       const size_t ps = (size_t)bmax * H0;
       const float* hp = m.ws_hpart + (size_t)b * H0;
+      if (H0 <= 64) {
+        // one column per lane: 16 partials in flight per wave (the per-tile partials of a
+        // large vocabulary are ~100 per wave: a round trip per 4 of them was most of the
+        // kernel), summed in the same order as below
+        constexpr int PU = 16;
+        const int jl = min(lane, H0 - 1);
+        for (int p0 = wave; p0 < P; p0 += PU * ENC_WAVES) {
+          float hv[PU];
+#pragma unroll
+          for (int u = 0; u < PU; ++u) hv[u] = hp[(size_t)min(p0 + u * ENC_WAVES, P - 1) * ps + jl];
+#pragma unroll
+          for (int u = 0; u < PU; ++u) acc[0] += p0 + u * ENC_WAVES < P ? hv[u] : 0.f;
+        }
+      } else
       for (int p0 = wave; p0 < P; p0 += 4 * ENC_WAVES) {
         float hv[4][8];
 #pragma unroll

@@ -123,7 +123,8 @@ typedef struct GfkModel {
   // ---- CombinedTM contextual path on the fused kernels (csrc/ctx.hip) ----
   float *w_a, *b_a;              // adapt_bert.weight [V, C], adapt_bert.bias [V]
   float *ws_actx;                // [n_tiles][bmax][64] adapted rows A (ctx_fwd)
-  float *ws_hpart;               // [n_tiles][bmax][H0] per-tile contextual z0 terms
+  float *ws_hpart;               // [n_parts][bmax][H0] contextual z0 partials (per tile, or per
+                                 // workgroup of the balanced forward: ctx_parts)
   int32_t ctx_fused;             // 1 (CombinedTM): adapt_bert + contextual input layer in
                                  //    ctx_fwd / ctx_bwd / win_update; 2 (ZeroShotTM): the dense
                                  //    [C, H0] input layer in enc_in / win_update (no host GEMMs)
@@ -139,7 +140,10 @@ typedef struct GfkModel {
   // operands, fp32 accumulation (v_mfma_f32_16x16x32_bf16); parameters, Adam state and
   // every other op stay fp32
   int32_t mm_bf16;
-  int32_t pad2;
+  // CombinedTM forward, balanced persistent shape (stage_flags bit 11): ctx_parts
+  // workgroups each own a contiguous range of 16-column units and leave ONE partial of the
+  // contextual z0 terms in ws_hpart (0: one partial per vocab tile)
+  int32_t ctx_parts;
 
   // ---- CTM label head (reference ctm decoding_network.py:84-85,156-159, ctm.py:292-296,
   // inference_network.py:64,162): the labels widen the encoder input (rows lab_off ..

@@ -757,8 +757,10 @@ __global__ void __launch_bounds__(256) gfk_win_dense_k(GfkArgT<GB> ga) {
 // rows A^T (ctx_fwd's output) in place of x^T, or ZeroShotTM's whole [C, H0] layer with
 // the batch's contextual rows x_ctx^T -- the same tile GEMM + Adam epilogue.
 // dynamic LDS: max(W_in tile: xt[64][stride_a(B)] + dz[B][stride_b(H0P)], weight job: 2 B 80)
+// (8-wave shape: at most 64 VGPRs, so the 4 workgroups its 37 KB of LDS allows per CU also
+// fit the register file -- the batched instance compiled to 68 VGPRs, 7 waves per SIMD)
 template <int UT, bool GB = false>
-__global__ void __launch_bounds__(UT) gfk_win_update_k(GfkArgT<GB> ga, GfkUArgT<GB> gua) {
+__global__ void __launch_bounds__(UT, UT == 512 ? 8 : 1) gfk_win_update_k(GfkArgT<GB> ga, GfkUArgT<GB> gua) {
   const GfkModel& m = gfk_model(ga);
   const GfkUpdate& U = gfk_upd(gua);
   constexpr int UW = UT / 64;

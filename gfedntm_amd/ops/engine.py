@@ -62,6 +62,7 @@ STAGE_WIN_SPLIT = 128             # bit 7: split W_in update (csrc/update.hip gf
 STAGE_FWD_STRIP_RING = 256        # bit 8: the strip forward's ring-prefetch variant (PF = 3)
 STAGE_WIN_BATCH8 = 512            # bit 9: batched launches: win_update's 8-wave tile shape
 STAGE_WIN_VREG = 1024             # bit 10: sparse W_in tiles keep the second moment in registers
+STAGE_CTX_BAL = 2048              # bit 11: CombinedTM forward, balanced persistent shape (csrc/ctx.hip)
 
 
 def _explain(ok: bool, why: str, explain: bool) -> bool:
@@ -558,6 +559,14 @@ class FusedEngine(EngineBase):
         if m.ctx_fused == 1 and m.bmax <= 64 and (
                 cf_env == "1" or (cf_env == "auto" and m.n_tiles > 2 * cu_n)):
             m.stage_flags |= STAGE_CTX_FULL
+            # ... as the balanced persistent kernel: ctx_parts workgroups (two per CU) own
+            # equal column ranges instead of one workgroup per tile (whose last round runs
+            # mostly empty) and leave one contextual z0 partial each; slices staged by DMA.
+            # GFEDNTM_CTX_BAL=0 keeps the one-workgroup-per-tile kernel
+            if (os.environ.get("GFEDNTM_CTX_BAL", "1") != "0" and int(m.H[0]) <= 64
+                    and m.V * m.C * 4 < (1 << 31)):
+                m.stage_flags |= STAGE_CTX_BAL
+                m.ctx_parts = int(min(m.n_tiles, 2 * cu_n))
         ws_env = os.environ.get("GFEDNTM_WIN_SPARSE", "auto")
         # (fused CombinedTM too: its bag-of-words half as sparse tiles, the contextual half
         # as dense tiles of the same launch -- csrc/update.hip win_tile_ctx; B <= 64)
@@ -848,6 +857,11 @@ class FusedEngine(EngineBase):
                 self.ws["dbsm"] = torch.zeros(nnz + 16, dtype=torch.float32, device=dev)
             m.ws_dbsm = self.ws["dbsm"].data_ptr()
         m.ctx = data.contextual.data_ptr() if data.contextual is not None else None
+        if m.stage_flags & STAGE_CTX_BAL and data.contextual is not None \
+                and 4 * data.contextual.numel() >= (1 << 31):
+            # the balanced forward addresses x_ctx with 32-bit buffer offsets
+            m.stage_flags &= ~STAGE_CTX_BAL
+            m.ctx_parts = 0
         if m.lab_on:
             if data.labels is None or data.labels.shape[1] != m.L:
                 raise ValueError(f"the model has a label head of size {m.L}: bind data with "
@@ -1315,7 +1329,7 @@ class FusedEngine(EngineBase):
 
 # the GfkModel fields that fix a launch's grid, block and LDS: engines batched into one
 # launch per phase must agree on all of them (their pointers and per-client values differ)
-_BATCH_SHAPE_FIELDS = ("bmax", "V", "ldb", "K", "n_hidden", "act", "kind", "input", "C", "L", "vb",
+_BATCH_SHAPE_FIELDS = ("bmax", "V", "ldb", "K", "n_hidden", "act", "kind", "input", "C", "L", "vb", "ctx_parts",
                        "n_tiles", "dec_grid", "learn_priors", "stage_flags", "kt", "n_dpart",
                        "beta_split", "update_mode", "ctx_fused", "ctx_kb", "ctx_ckb", "mm_bf16",
                        "lab_on", "lab_off", "lab_in_enc", "bwd_pre")

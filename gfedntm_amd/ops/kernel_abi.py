@@ -105,7 +105,7 @@ class GfkModel(C.Structure):
         ("w_a", P), ("b_a", P), ("ws_actx", P), ("ws_hpart", P),
         ("ctx_fused", C.c_int32), ("ctx_kb", C.c_int32), ("ctx_ckb", C.c_int32),
         ("slot_cap", C.c_int32), ("ws_sidx", P), ("ws_sval", P),
-        ("mm_bf16", C.c_int32), ("pad2", C.c_int32),
+        ("mm_bf16", C.c_int32), ("ctx_parts", C.c_int32),
         ("lab_on", C.c_int32), ("lab_off", C.c_int32), ("labels", P), ("w_cls", P), ("b_cls", P),
         ("ws_lab", P), ("ws_dlab", P), ("ws_ce", P), ("ws_thd", P),
         ("lab_in_enc", C.c_int32), ("bwd_pre", C.c_int32), ("ws_dt", P),

@@ -730,11 +730,15 @@ def test_sparse_win_tiles_match_oracle(monkeypatch, model_type, B, n_docs, K, H,
     _oracle_step(model_type, B, n_docs, K, H, V)
 
 
-@pytest.mark.parametrize("Cdim,V", [(96, 600), (768, 9000)])
-def test_ctm_full_tile_forward_matches_oracle(monkeypatch, Cdim, V):
+@pytest.mark.parametrize("bal", ["1", "0"])
+@pytest.mark.parametrize("Cdim,V", [(96, 600), (768, 9000), (100, 5000)])
+def test_ctm_full_tile_forward_matches_oracle(monkeypatch, Cdim, V, bal):
     """ctx_fwd with all batch rows per vocab tile (stage_flags bit 5, the large-V shape;
-    GFEDNTM_CTX_FULL=1 forces it at small V)."""
+    GFEDNTM_CTX_FULL=1 forces it at small V): the balanced persistent kernel (bit 11,
+    DMA-staged slices, column ranges of 16-column units not aligned to the 64-column
+    tiles, a partial last C slice at C = 96 / 100) or one workgroup per tile (bal = 0)."""
     monkeypatch.setenv("GFEDNTM_CTX_FULL", "1")
+    monkeypatch.setenv("GFEDNTM_CTX_BAL", bal)
     test_ctm_step_matches_oracle("combined", Cdim, V, 20, "prodLDA")
 
 

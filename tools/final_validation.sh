@@ -24,3 +24,8 @@ run zs 200 --family zeroshot --topics 100 --steps 1000 --warmup 100 --no-npmi
 run b74 200 --topics 200 --vocab 100000 --docs 1000 --steps 300 --warmup 30 --no-npmi
 run b112 200 --topics 200 --vocab 150000 --docs 1500 --steps 300 --warmup 30 --no-npmi
 run sim8 240 --sim-clients 8 --steps 500 --warmup 50 --no-npmi
+run sim8lda 240 --sim-clients 8 --model LDA --steps 500 --warmup 50 --no-npmi
+run b112bf 200 --topics 200 --vocab 150000 --docs 1500 --steps 300 --warmup 30 --no-npmi --dtype bf16
+run ctm99 240 --family ctm --topics 100 --vocab 150000 --docs 1500 --steps 200 --warmup 20 --no-npmi
+run zs99 240 --family zeroshot --topics 100 --vocab 150000 --docs 1500 --steps 200 --warmup 20 --no-npmi
+run multi17 240 --clients-per-gpu 17 --steps 300 --warmup 30 --no-npmi
