@@ -705,6 +705,195 @@ __global__ void __launch_bounds__(CT) gfk_ctx_bwd_k(GfkArgT<GB> ga) {
   GFK_STAMP(m, 38);
 }
 
+// Persistent pipelined backward (stage_flags bit 12, B <= 64, H0 <= 64): ctx_bgrid
+// workgroups of 16 waves (one per CU) walk contiguous ranges of the (tile, chunk) items
+// (tile-major, chunks of PK = 128 floats of C), so every CU does the same Wa update
+// traffic to within one item and never idles between workgroups: while item i's products
+// and Adam epilogue run, item i + 1's Wa p / m / v quads and x_ctx slice are already in
+// flight in a second register set (the (tile, chunk) grid started each workgroup's loads
+// only after the previous workgroup on its CU had finished its stores, with its 115 KB of
+// LDS leaving room for one).  dz0 is staged once per workgroup; dA = dz0 Wc_tile^T (and
+// g_ba, on the tile's chunk-0 item) is recomputed only when the tile changes.
+constexpr int CTX_BWDPP = 4096;
+constexpr int PK = 128;                 // chunk of C per item
+struct PPLds {
+  int ldz, dz, wc, da, xc, gs, total;
+};
+__host__ __device__ inline PPLds pp_lds(const GfkModel& m) {
+  PPLds L;
+  L.ldz = stride_a(rup(m.H[0], 4));
+  int o = 0;
+  L.dz = o; o += 64 * L.ldz;
+  L.wc = o; o += 64 * L.ldz;
+  L.da = o; o += 64 * 80;
+  L.xc = o; o += 64 * (PK + 16);        // B-role rows: stride 144 = 16 mod 32
+  L.gs = o; o += 64 * (PK + 4);         // g_Wa tile rows: 4 x stride = 16 mod 32
+  L.total = o;
+  return L;
+}
+template <bool GB = false>
+__global__ void __launch_bounds__(CT) gfk_ctx_bwd_pp_k(GfkArgT<GB> ga) {
+  const GfkModel& m = gfk_model(ga);
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ int docs_s[64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
+  const int V = m.V, C = m.C, H0 = m.H[0], n_tiles = m.n_tiles;
+  const int NCK = (C + PK - 1) / PK;
+  const int64_t N = (int64_t)n_tiles * NCK;
+  const int G = (int)gridDim.x, w = (int)blockIdx.x;
+  const int i0 = (int)(N * w / G), i1 = (int)(N * (w + 1) / G);
+  const int H0Q = rup(H0, 4);
+  const PPLds L = pp_lds(m);
+  float* dzs = smem + L.dz;
+  float* wcs = smem + L.wc;
+  float* das = smem + L.da;
+  float* xcs = smem + L.xc;
+  float* gs = smem + L.gs;
+  const float* wcg = m.w_in + (size_t)V * H0;
+  const int nb = *m.ws_nb;
+  const bool fused = m.update_mode == 1;
+  const AdamCoef ac = adam_coef(m);
+  const bool sh = is_shared(m, m.w_a);
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  if (tid < 64) docs_s[tid] = m.ws_doc[min(tid, m.bmax - 1)];
+  // ---- dz0 once (rows >= nb zero) ----
+  for (int i = tid; i < 64 * H0Q; i += CT) {
+    const int r = i / H0Q, j = i - r * H0Q;
+    dzs[r * L.ldz + j] = (r < nb && j < H0) ? m.ws_dz[0][r * H0 + j] : 0.f;
+  }
+  __syncthreads();
+  // ---- per-thread element maps: quad u (< 2) of the [64, PK] block = (row, q) ----
+  int er[2], eq[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int e = tid + CT * u;
+    er[u] = e >> 5;                      // PK / 4 = 32 quads per row
+    eq[u] = e & 31;
+  }
+  // item loads: Wa p / m / v quads, the x_ctx slice and the tile's Wc rows (for dA when
+  // the tile changes; L2 hits) -- clamped addresses, always issued
+  auto ld_item = [&](int it, f32x4 (&P)[6], f32x4 (&X)[2], float (&W)[4]) {
+    const int t = it / NCK, k0 = (it - t * NCK) * PK;
+    const int c0 = t * 64, nvv = min(64, V - c0), kn = min(PK, C - k0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = tid + CT * u, r = i / H0Q, j = i - r * H0Q;
+      W[u] = wcg[(size_t)(c0 + min(r, nvv - 1)) * H0 + min(j, H0 - 1)];
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const f32x4* p = reinterpret_cast<const f32x4*>(
+          m.w_a + (size_t)(c0 + min(er[u], nvv - 1)) * C + k0 + min(4 * eq[u], kn - 4));
+      P[3 * u] = p[0];
+      P[3 * u + 1] = fused ? p[m.off_m / 4] : z4;
+      P[3 * u + 2] = fused ? p[m.off_v / 4] : z4;
+      X[u] = *reinterpret_cast<const f32x4*>(m.ctx + (size_t)docs_s[min(er[u], max(nb, 1) - 1)] * C + k0 +
+                                             min(4 * eq[u], kn - 4));
+    }
+  };
+  int cur_tile = -1;
+  // one item: products + update, with the next item's loads already in flight
+  // item part 1: its x_ctx slice into LDS and, for a new tile, dA (the Wc registers are
+  // free afterwards: the next item's loads reuse them)
+  auto stage = [&](int it, const f32x4 (&X)[2], const float (&W)[4]) {
+    const int t = it / NCK, kc = it - t * NCK, k0 = kc * PK;
+    const int c0 = t * 64, nvv = min(64, V - c0), kn = min(PK, C - k0);
+    // the x_ctx slice -> LDS (rows >= nb, columns >= kn zero)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      *reinterpret_cast<f32x4*>(xcs + er[u] * (PK + 16) + 4 * eq[u]) =
+          (er[u] < nb && 4 * eq[u] < kn) ? X[u] : z4;
+    if (t != cur_tile) {                 // (uniform) dA for the new tile
+      cur_tile = t;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {      // 64 x H0Q <= 4096 = 4 CT
+        const int i = tid + CT * u, r = i / H0Q, j = i - r * H0Q;
+        if (r < 64) wcs[r * L.ldz + j] = (r < nvv && j < H0) ? W[u] : 0.f;
+      }
+      lds_barrier();
+      {
+        const int rt = wave >> 2, vt = wave & 3;      // 16 subtiles, one per wave
+        f32x4 acc = z4;
+        const float* ap = dzs + (rt * 16 + (lane & 15)) * L.ldz + (lane >> 4);
+        const float* bp = wcs + (vt * 16 + (lane & 15)) * L.ldz + (lane >> 4);
+        for (int k = 0; k < H0Q; k += 4) acc = mfma16x16x4(ap[k], bp[k], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) das[(rt * 16 + (lane >> 4) * 4 + r) * 80 + vt * 16 + (lane & 15)] = acc[r];
+      }
+    }
+  };
+  // item part 2: g_ba, g_Wa and the update
+  auto compute = [&](int it, const f32x4 (&P)[6]) {
+    const int t = it / NCK, kc = it - t * NCK, k0 = kc * PK;
+    const int c0 = t * 64, nvv = min(64, V - c0), kn = min(PK, C - k0);
+    lds_barrier();                       // x_ctx slice and dA visible
+    // ---- g_ba (the tile's chunk-0 item): column sums of dA, 16 lanes per column ----
+    if (kc == 0) {
+      const int v = tid >> 4, sub = tid & 15;
+      float gba = 0.f;
+      for (int b = sub; b < 64; b += 16) gba += das[b * 80 + v];
+      gba = row16_sum(gba);
+      if (sub == 0 && v < nvv) param_update(m, m.b_a + c0 + v, gba, ac, is_shared(m, m.b_a));
+    }
+    // ---- g_Wa [64, PK] = dA^T x_ctx: subtiles t2 = wave, wave + 16 (vt, ct) = (t2 & 3, t2 >> 2) ----
+    f32x4 gacc[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int t2 = wave + 16 * u, vt = t2 & 3, ct = t2 >> 2;
+      gacc[u] = z4;
+      const float* ap = das + (lane >> 4) * 80 + vt * 16 + (lane & 15);
+      const float* bp = xcs + (lane >> 4) * (PK + 16) + ct * 16 + (lane & 15);
+#pragma unroll 4
+      for (int b = 0; b < 64; b += 4) gacc[u] = mfma16x16x4(ap[b * 80], bp[b * (PK + 16)], gacc[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int t2 = wave + 16 * u, vt = t2 & 3, ct = t2 >> 2;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        gs[(vt * 16 + (lane >> 4) * 4 + r) * (PK + 4) + ct * 16 + (lane & 15)] = gacc[u][r];
+    }
+    lds_barrier();
+    // ---- the update on coalesced float4 rows ----
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (er[u] >= nvv || 4 * eq[u] >= kn) continue;
+      const f32x4 gr = *reinterpret_cast<const f32x4*>(gs + er[u] * (PK + 4) + 4 * eq[u]);
+      f32x4* p = reinterpret_cast<f32x4*>(m.w_a + (size_t)(c0 + er[u]) * C + k0 + 4 * eq[u]);
+      if (!fused) {
+        p[m.off_g / 4] = gr;
+      } else {
+        f32x4 np, mo = P[3 * u + 1], vo = P[3 * u + 2];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float a = mo[r], b2 = vo[r];
+          float xv = adam_update(P[3 * u][r], gr[r], a, b2, ac);
+          if (sh && m.fed_scale_on) xv *= m.fed_scale;
+          mo[r] = a;
+          vo[r] = b2;
+          np[r] = xv;
+        }
+        p[m.off_m / 4] = mo;
+        p[m.off_v / 4] = vo;
+        p[0] = np;
+      }
+    }
+    lds_barrier();                       // before the next item rewrites the slice / dA / g tile
+  };
+  f32x4 PA[6], XA[2], PB[6], XB[2];
+  float W[4];
+  if (i0 < i1) ld_item(i0, PA, XA, W);
+  for (int it = i0; it < i1; it += 2) {
+    stage(it, XA, W);
+    if (it + 1 < i1) ld_item(it + 1, PB, XB, W);
+    compute(it, PA);
+    if (it + 1 >= i1) break;
+    stage(it + 1, XB, W);
+    if (it + 2 < i1) ld_item(it + 2, PA, XA, W);
+    compute(it + 1, PB);
+  }
+}
+
 __host__ __device__ inline int fwd_full_lds_floats(const GfkModel& m) {
   const int a = 128 * LDK, b = 64 * 66 + 64 * fwd_ldc(m);
   return a > b ? a : b;
@@ -714,6 +903,7 @@ extern "C" size_t gfk_ctx_smem(const GfkModel* m) {
   size_t a = fwd_lds_floats(*m), b = bwd_lds(*m).total;
   if ((m->stage_flags & CTX_FULL) && (size_t)fwd_full_lds_floats(*m) > a) a = fwd_full_lds_floats(*m);
   if ((m->stage_flags & CTX_BAL) && (size_t)fwd_bal_lds_floats() > a) a = fwd_bal_lds_floats();
+  if ((m->stage_flags & CTX_BWDPP) && (size_t)pp_lds(*m).total > b) b = pp_lds(*m).total;
   return sizeof(float) * (a > b ? a : b);
 }
 
@@ -728,7 +918,8 @@ extern "C" int gfk_ctx_set_smem(size_t bytes) {
                       (const void*)gfk_ctx_bwd_k<16>, (const void*)gfk_ctx_bwd_k<16, true>, (const void*)gfk_ctx_bwd_k<32>, (const void*)gfk_ctx_bwd_k<32, true>,
                       (const void*)gfk_ctx_bwd_k<64>, (const void*)gfk_ctx_bwd_k<64, true>, (const void*)gfk_ctx_bwd_k<128>, (const void*)gfk_ctx_bwd_k<128, true>,
                       (const void*)gfk_ctx_fwd_full_k<false>, (const void*)gfk_ctx_fwd_full_k<true>,
-                      (const void*)gfk_ctx_fwd_bal_k<false>, (const void*)gfk_ctx_fwd_bal_k<true>};
+                      (const void*)gfk_ctx_fwd_bal_k<false>, (const void*)gfk_ctx_fwd_bal_k<true>,
+                      (const void*)gfk_ctx_bwd_pp_k<false>, (const void*)gfk_ctx_bwd_pp_k<true>};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return (int)e;
@@ -775,6 +966,12 @@ extern "C" int gfk_launch_ctx_fwd(const GfkModel* m, hipStream_t s) {
 
 extern "C" int gfk_launch_ctx_bwd(const GfkModel* m, hipStream_t s) {
   if (!ctx_ok(m)) return -9;
+  if ((m->stage_flags & CTX_BWDPP) && m->bmax <= 64 && m->H[0] <= 64 && m->ctx_bgrid > 0) {
+    const dim3 g(m->ctx_bgrid), t(CT);
+    const size_t sm = sizeof(float) * pp_lds(*m).total;
+    do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_ctx_bwd_pp_k<true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_ctx_bwd_pp_k<false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0);
+    return (int)hipGetLastError();
+  }
   const dim3 g(m->n_tiles * m->ctx_kb), t(CT);
   const size_t sm = sizeof(float) * bwd_lds(*m).total;
   switch (m->bmax) {

@@ -174,7 +174,9 @@ typedef struct GfkModel {
   // beta's row stride in floats (>= V: the flat layout pads beta's rows to 128-B lines at
   // large V, utils/flat.py); m / v / the gradient share it
   int32_t ldb;
-  int32_t pad3;
+  // CombinedTM backward, persistent pipelined shape (stage_flags bit 12): workgroups
+  // (one per CU) of csrc/ctx.hip gfk_ctx_bwd_pp_k (0: the (tile, chunk) grid)
+  int32_t ctx_bgrid;
   // ---- split W_in update (stage_flags bit 7, GFK_WIN_SPLIT): prepare_next_batch stamps
   // every word of the next batch with a fresh generation (ws_wstamp[V], ws_wgen[1]); the
   // words NOT in the batch get their zero-gradient Adam step from gfk_win_dense_k on a side

@@ -63,6 +63,7 @@ STAGE_FWD_STRIP_RING = 256        # bit 8: the strip forward's ring-prefetch var
 STAGE_WIN_BATCH8 = 512            # bit 9: batched launches: win_update's 8-wave tile shape
 STAGE_WIN_VREG = 1024             # bit 10: sparse W_in tiles keep the second moment in registers
 STAGE_CTX_BAL = 2048              # bit 11: CombinedTM forward, balanced persistent shape (csrc/ctx.hip)
+STAGE_CTX_BWDPP = 4096            # bit 12: CombinedTM backward, persistent pipelined shape (csrc/ctx.hip)
 
 
 def _explain(ok: bool, why: str, explain: bool) -> bool:
@@ -567,6 +568,14 @@ class FusedEngine(EngineBase):
                     and m.V * m.C * 4 < (1 << 31)):
                 m.stage_flags |= STAGE_CTX_BAL
                 m.ctx_parts = int(min(m.n_tiles, 2 * cu_n))
+        # CombinedTM backward as one persistent workgroup per CU walking equal ranges of the
+        # (tile, C chunk) items with the next item's Wa state in flight (csrc/ctx.hip
+        # gfk_ctx_bwd_pp_k); GFEDNTM_CTX_BWDPP=0 keeps the (tile, chunk) grid
+        if (m.ctx_fused == 1 and m.bmax <= 64 and int(m.H[0]) <= 64
+                and os.environ.get("GFEDNTM_CTX_BWDPP", "auto") in ("1", "auto")
+                and (os.environ.get("GFEDNTM_CTX_BWDPP", "auto") == "1" or m.n_tiles > 2 * cu_n)):
+            m.stage_flags |= STAGE_CTX_BWDPP
+            m.ctx_bgrid = int(cu_n)
         ws_env = os.environ.get("GFEDNTM_WIN_SPARSE", "auto")
         # (fused CombinedTM too: its bag-of-words half as sparse tiles, the contextual half
         # as dense tiles of the same launch -- csrc/update.hip win_tile_ctx; B <= 64)

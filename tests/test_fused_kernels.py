@@ -786,3 +786,51 @@ def test_ctm_sparse_win_tiles_fused_update(monkeypatch):
                                                    "inf_net.f_sigma_batchnorm.running_mean"))
         torch.testing.assert_close(sa[k], sb[k], rtol=1e-3, atol=lr_steps if noisy else 5e-5,
                                    msg=lambda m: f"{k}: {m}")
+
+
+@pytest.mark.parametrize("bwdpp", ["1", "0"])
+@pytest.mark.parametrize("Cdim,V", [(96, 600), (768, 9000), (100, 5000)])
+def test_ctm_persistent_backward_matches_oracle(monkeypatch, Cdim, V, bwdpp):
+    """ctx_bwd as one persistent workgroup per CU over equal ranges of (tile, 128-float C
+    chunk) items, the next item's Wa state in flight (stage_flags bit 12, forced at small
+    V), vs the (tile, chunk) grid (bwdpp = 0): the oracle's adapt_bert / input-layer
+    gradients (C = 96 / 100: a partial last chunk; V = 5000: a partial last tile)."""
+    monkeypatch.setenv("GFEDNTM_CTX_BWDPP", bwdpp)
+    test_ctm_step_matches_oracle("combined", Cdim, V, 20, "prodLDA")
+
+
+def test_ctm_persistent_backward_fused_update(monkeypatch):
+    """The persistent backward's Adam epilogue (adapt_bert weight and bias, FedAvg
+    pre-scale) == gradient mode + the generic Adam, over several steps."""
+    monkeypatch.setenv("GFEDNTM_CTX_BWDPP", "1")
+    from gfedntm_amd.ops.engine import STAGE_CTX_BWDPP
+    from gfedntm_amd.models import CombinedTM
+    torch.manual_seed(0)
+    kw = dict(input_size=1900, contextual_size=136, n_components=30, hidden_sizes=(48, 40),
+              batch_size=64, verbose=False, device="cuda", backend="fused")
+    a, b = CombinedTM(**kw), CombinedTM(**kw)
+    assert a.engine._m.stage_flags & STAGE_CTX_BWDPP
+    b.model.load_state_dict(a.model.state_dict())
+    b.engine.seed = b.engine._m.seed = a.engine.seed
+    b.engine.set_update_mode(UPDATE_GRAD)
+    X = random_csr(200, 1900, 40, seed=3)
+    ctx = np.random.default_rng(4).standard_normal((200, 136)).astype(np.float32)
+    for t in (a, b):
+        t.engine.set_fedavg_scale(0.75)
+        t.engine.bind_data(DeviceCSR(X, "cuda", contextual=ctx), BatchPlan.build(200, 64, 5, seed=0))
+        t.engine.enable_graph(True)
+    for s in range(5):
+        a.engine.step(s)
+        b.engine.step(s)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(a.engine.loss_hist, b.engine.loss_hist, rtol=1e-4, atol=1e-2)
+    sa, sb = a.model.state_dict(), b.model.state_dict()
+    lr_steps = 2 * a.engine.lr * 5
+    for k in sb:
+        if not sb[k].is_floating_point():
+            assert torch.equal(sa[k], sb[k]), k
+            continue
+        noisy = k in _NOISE_KEYS or k.startswith(("inf_net.f_mu_batchnorm.running_mean",
+                                                   "inf_net.f_sigma_batchnorm.running_mean"))
+        torch.testing.assert_close(sa[k], sb[k], rtol=1e-3, atol=lr_steps if noisy else 5e-5,
+                                   msg=lambda m: f"{k}: {m}")
