@@ -384,6 +384,7 @@ __global__ void __launch_bounds__(FT) gfk_ctx_fwd_full_k(GfkArgT<GB> ga) {
 // Wc^T of the chunk, P [64, H0] += A Wc accumulates in registers, and A goes to ws_actx;
 // the workgroup leaves ONE partial of the contextual z0 terms (ctx_parts for enc_in).
 constexpr int CTX_BAL = 2048;
+constexpr int CTX_BAL3 = 8192;          // stage_flags bit 13: the 16-wave 3-deep variant
 constexpr int FD = 64;                  // slice width (floats); one slice buffer: 128 rows x 64
 template <bool GB = false>
 __global__ void __launch_bounds__(FT, 4) gfk_ctx_fwd_bal_k(GfkArgT<GB> ga) {
@@ -539,6 +540,190 @@ __global__ void __launch_bounds__(FT, 4) gfk_ctx_fwd_bal_k(GfkArgT<GB> ga) {
 }
 
 __host__ __device__ inline int fwd_bal_lds_floats() { return 2 * 128 * FD; }
+
+// The 16-wave, 3-deep variant (ctx_parts = one workgroup per CU, H0 <= 63): slice s + 2 is in
+// flight while slice s is multiplied (a 3-buffer ring, 96 KB), the waits counted per slice
+// (s_waitcnt vmcnt(2) / (3): only the newer slice's 2 DMA instructions -- and the next
+// chunk's Wc block -- may still be outstanding; a full drain once per chunk, after the
+// epilogue's stores).  The 16 waves split each slice's 4 16-float blocks in two halves
+// (kh = wave >> 3) over the same 8 (row tile, column pair) subtiles; the halves are summed
+// through LDS in the epilogue.  The chunk's Wc rows and bias come by DMA as well (double-
+// buffered), so the epilogue never waits on a global load issued before the slices'.
+constexpr int FT3 = 1024;
+__host__ __device__ inline int bal3_wcb_floats() { return 4096 + 64; }
+__host__ __device__ inline int fwd_bal3_lds_floats() { return 3 * 128 * FD + 2 * bal3_wcb_floats() + 64 * FD; }
+template <bool GB = false>
+__global__ void __launch_bounds__(FT3) gfk_ctx_fwd_bal3_k(GfkArgT<GB> ga) {
+  const GfkModel& m = gfk_model(ga);
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
+  const int r = lane & 15, g = lane >> 4;
+  const int V = m.V, C = m.C, H0 = m.H[0];
+  const int G = (int)gridDim.x, w = (int)blockIdx.x;
+  const int U = (V + 15) / 16;
+  const int cs = (int)((int64_t)w * U / G) * 16;
+  const int ce = min(V, (int)((int64_t)(w + 1) * U / G) * 16);
+  const int NSL = (C + FD - 1) / FD;
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  const __amdgpu_buffer_rsrc_t rs_x = __builtin_amdgcn_make_buffer_rsrc((void*)m.ctx, 0, 0x7FFFFFFF, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_w =
+      __builtin_amdgcn_make_buffer_rsrc((void*)m.w_a, 0, (int)((uint32_t)V * (uint32_t)C * 4u), 0x00020000);
+  // Wc and ba through one resource on the flat parameter buffer (offsets < 2 GB: host check)
+  const __amdgpu_buffer_rsrc_t rs_f = __builtin_amdgcn_make_buffer_rsrc((void*)m.flat_base, 0, 0x7FFFFFFF, 0x00020000);
+  const uint32_t wc_off = (uint32_t)((m.w_in + (size_t)V * H0) - m.flat_base) * 4u;
+  const uint32_t ba_off = (uint32_t)(m.b_a - m.flat_base) * 4u;
+  constexpr uint32_t OOB = 0x80000000u;
+  float* ring = smem;                               // [3][128][64]
+  float* wcb0 = smem + 3 * 128 * FD;                // [2][Wc block (64 H0, at most 4032) | bias (64 at 4032)]
+  float* ar = wcb0 + 2 * bal3_wcb_floats();         // [64][64] A (swizzled rows) / kh partials
+  // ---- slice DMA: instruction j (0: x_ctx, 1: Wa) of wave w moves quads 1024 j + 64 w + lane,
+  //      LDS row R = 64 j + 4 w + lane >> 4, LDS quad p = lane & 15, global quad p ^ (R & 15) ----
+  const int R0 = 4 * wave + (lane >> 4);
+  const int q = (lane & 15) ^ (R0 & 15);
+  const uint32_t xoff = ((uint32_t)m.ws_next[1 + min(R0, m.bmax - 1)] * (uint32_t)C + 4u * q) * 4u;
+  auto dma = [&](int sl, int c0c, int nvvc, float* buf) {
+    const int k0 = sl * FD;
+    const int so = uniform(k0 * 4);
+    const bool kin = k0 + 4 * q < C;
+    const uint32_t vw = (kin && R0 < nvvc) ? ((uint32_t)(c0c + R0) * (uint32_t)C + 4u * q) * 4u : OOB;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_x, (lds_void_ptr)(buf + 64 * wave * 4), 16, kin ? xoff : OOB, so, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_w, (lds_void_ptr)(buf + (1024 + 64 * wave) * 4), 16, vw, so, 0, 0);
+  };
+  // ---- the chunk's Wc rows (quads 64 w + lane < 16 H0) and bias (quads 1008..1023): one
+  //      instruction per wave, one (flat) resource ----
+  auto aux = [&](int c0c, int nvvc, float* wb) {
+    const int Q = 64 * wave + lane;
+    uint32_t vo;
+    if (Q >= 1008) {
+      const int cb = c0c + 4 * (Q - 1008);
+      vo = cb < V ? ba_off + (uint32_t)cb * 4u : OOB;
+    } else {
+      const int e = 4 * Q;
+      vo = e < nvvc * H0 ? wc_off + ((uint32_t)c0c * (uint32_t)H0 + (uint32_t)e) * 4u : OOB;
+    }
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_f, (lds_void_ptr)(wb + 64 * wave * 4), 16, vo, 0, 0, 0);
+  };
+  const int kh = wave >> 3, w8 = wave & 7;
+  const int rt = w8 >> 1, cs0 = 2 * (w8 & 1);
+  const int ra_row = rt * 16 + r, rb0 = 64 + cs0 * 16 + r, rb1 = rb0 + 16;
+  auto qaddr = [&](int row, int quad) { return row * FD + 4 * (quad ^ (row & 15)); };
+  const int NJT = (H0 + 15) / 16;
+  f32x4 pacc = z4;
+  // the slice wait: everything a wave issued after slice s's DMA is what it issued at the top
+  // of slice s - 1 (`newer`: 0, 2 or 3 instructions) -- except at a chunk's first slice, after
+  // the epilogue's stores: drain
+  int newer = 0;
+  auto wait_slice = [&](int sl) {
+    if (sl == 0) { vm_barrier(); return; }
+    if (sl == 1) { lds_barrier(); return; }               // drained at sl == 0
+    if (newer == 3) asm volatile("s_waitcnt vmcnt(3)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else if (newer == 2) asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else vm_barrier();
+  };
+  int s = 0, j = 0;
+  if (cs < ce) {
+    const int nvv0 = min(64, ce - cs);
+    dma(0, cs, nvv0, ring);
+    aux(cs, nvv0, wcb0);
+    if (NSL > 1) dma(1, cs, nvv0, ring + 128 * FD);
+    else if (cs + 64 < ce) dma(0, cs + 64, min(64, ce - cs - 64), ring + 128 * FD);
+  }
+  for (int c0 = cs; c0 < ce; c0 += 64, ++j) {
+    const int nvv = min(64, ce - c0);
+    f32x4 acc0 = z4, acc1 = z4;
+    for (int sl = 0; sl < NSL; ++sl, ++s) {
+      wait_slice(sl);
+      __builtin_amdgcn_sched_barrier(0);
+      float* cur = ring + (s % 3) * 128 * FD;
+      float* nx2 = ring + ((s + 2) % 3) * 128 * FD;
+      // slice s + 2: this chunk's, or the next chunk's first (with its Wc block / bias: NSL >= 4)
+      newer = 0;
+      {
+        const int sl2 = sl + 2 < NSL ? sl + 2 : sl + 2 - NSL;
+        const int c2 = sl + 2 < NSL ? c0 : c0 + 64;
+        if (c2 < ce) {
+          const int nv2 = min(64, ce - c2);
+          dma(sl2, c2, nv2, nx2);
+          newer = 2;
+          if (sl2 == 0) {
+            aux(c2, nv2, wcb0 + ((j + 1) & 1) * bal3_wcb_floats());
+            newer = 3;
+          }
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // this wave's two 16-float blocks (2 kh, 2 kh + 1): all 6 operand reads, then 16 MFMAs
+      f32x4 a4[2], b4[2], c4[2];
+#pragma unroll
+      for (int bb = 0; bb < 2; ++bb) {
+        const int b = 2 * kh + bb;
+        a4[bb] = *reinterpret_cast<const f32x4*>(cur + qaddr(ra_row, 4 * b + g));
+        b4[bb] = *reinterpret_cast<const f32x4*>(cur + qaddr(rb0, 4 * b + g));
+        c4[bb] = *reinterpret_cast<const f32x4*>(cur + qaddr(rb1, 4 * b + g));
+      }
+#pragma unroll
+      for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          acc0 = mfma16x16x4(a4[bb][jj], b4[bb][jj], acc0);
+          acc1 = mfma16x16x4(a4[bb][jj], c4[bb][jj], acc1);
+        }
+    }
+    // ---- epilogue: the k-halves summed in ar, + bias, -> ar (swizzled) and ws_actx; P += A Wc ----
+    const float* wb = wcb0 + (j & 1) * bal3_wcb_floats();
+    if (kh == 1) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4& a4v = h ? acc1 : acc0;
+        const int col = (cs0 + h) * 16 + r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ar[qaddr(rt * 16 + g * 4 + i, col >> 2) + (col & 3)] = a4v[i];
+      }
+    }
+    lds_barrier();
+    if (kh == 0) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4& a4v = h ? acc1 : acc0;
+        const int col = (cs0 + h) * 16 + r;
+        const float bb = wb[4032 + col];
+        const int gc = c0 + col;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = rt * 16 + g * 4 + i;
+          const int ad = qaddr(row, col >> 2) + (col & 3);
+          const float a = col < nvv ? a4v[i] + ar[ad] + bb : 0.f;
+          ar[ad] = a;
+          if (row < m.bmax && col < nvv)
+            m.ws_actx[((size_t)(gc >> 6) * m.bmax + row) * 64 + (gc & 63)] = a;
+        }
+      }
+    }
+    lds_barrier();
+    if (wave < 4 * NJT) {                 // P subtile (row tile, h tile) = (wave / NJT, wave % NJT)
+      const int prt = wave / NJT, jt = wave % NJT;
+      const int hh = min(jt * 16 + r, H0 - 1);
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const f32x4 av = *reinterpret_cast<const f32x4*>(ar + qaddr(prt * 16 + r, 4 * b + g));
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) pacc = mfma16x16x4(av[jj], wb[(16 * b + 4 * g + jj) * H0 + hh], pacc);
+      }
+    }
+  }
+  vm_barrier();                         // nothing in flight when the workgroup retires
+  float* hg = m.ws_hpart + (size_t)w * m.bmax * H0;
+  if (wave < 4 * NJT) {
+    const int prt = wave / NJT, jt = wave % NJT, jh = jt * 16 + r;
+    if (jh < H0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = prt * 16 + g * 4 + i;
+        if (row < m.bmax) hg[(size_t)row * H0 + jh] = pacc[i];
+      }
+    }
+  }
+}
 
 // grid: n_tiles * ctx_kb workgroups of 16 waves (one per CU).
 template <int BM, bool GB = false>
@@ -903,6 +1088,7 @@ extern "C" size_t gfk_ctx_smem(const GfkModel* m) {
   size_t a = fwd_lds_floats(*m), b = bwd_lds(*m).total;
   if ((m->stage_flags & CTX_FULL) && (size_t)fwd_full_lds_floats(*m) > a) a = fwd_full_lds_floats(*m);
   if ((m->stage_flags & CTX_BAL) && (size_t)fwd_bal_lds_floats() > a) a = fwd_bal_lds_floats();
+  if ((m->stage_flags & CTX_BAL3) && (size_t)fwd_bal3_lds_floats() > a) a = fwd_bal3_lds_floats();
   if ((m->stage_flags & CTX_BWDPP) && (size_t)pp_lds(*m).total > b) b = pp_lds(*m).total;
   return sizeof(float) * (a > b ? a : b);
 }
@@ -919,7 +1105,8 @@ extern "C" int gfk_ctx_set_smem(size_t bytes) {
                       (const void*)gfk_ctx_bwd_k<64>, (const void*)gfk_ctx_bwd_k<64, true>, (const void*)gfk_ctx_bwd_k<128>, (const void*)gfk_ctx_bwd_k<128, true>,
                       (const void*)gfk_ctx_fwd_full_k<false>, (const void*)gfk_ctx_fwd_full_k<true>,
                       (const void*)gfk_ctx_fwd_bal_k<false>, (const void*)gfk_ctx_fwd_bal_k<true>,
-                      (const void*)gfk_ctx_bwd_pp_k<false>, (const void*)gfk_ctx_bwd_pp_k<true>};
+                      (const void*)gfk_ctx_bwd_pp_k<false>, (const void*)gfk_ctx_bwd_pp_k<true>,
+                      (const void*)gfk_ctx_fwd_bal3_k<false>, (const void*)gfk_ctx_fwd_bal3_k<true>};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return (int)e;
@@ -939,6 +1126,13 @@ static bool ctx_ok(const GfkModel* m) {
 
 extern "C" int gfk_launch_ctx_fwd(const GfkModel* m, hipStream_t s) {
   if (!ctx_ok(m)) return -9;
+  if ((m->stage_flags & CTX_FULL) && (m->stage_flags & CTX_BAL3) && m->bmax <= 64 && m->H[0] <= 63 && m->C > 3 * FD &&
+      m->ctx_parts > 0 && m->ctx_parts <= m->n_tiles) {
+    const dim3 g(m->ctx_parts), t(FT3);
+    const size_t sm = sizeof(float) * fwd_bal3_lds_floats();
+    do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_ctx_fwd_bal3_k<true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_ctx_fwd_bal3_k<false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0);
+    return (int)hipGetLastError();
+  }
   if ((m->stage_flags & CTX_FULL) && (m->stage_flags & CTX_BAL) && m->bmax <= 64 && m->H[0] <= 64 &&
       m->ctx_parts > 0 && m->ctx_parts <= m->n_tiles) {
     const dim3 g(m->ctx_parts), t(FT);

@@ -499,6 +499,138 @@ __device__ __forceinline__ void win_tile_ctx(const GfkModel& m, float* smem, int
   }
 }
 
+// CombinedTM's contextual input-layer half as a persistent kernel (stage_flags bit 14,
+// launched after the sparse bag-of-words tiles): ctx_bgrid x 2 workgroups own contiguous
+// ranges of 16-word units of Wc (rows V..2V-1 of the transposed input layer), walked in
+// blocks of up to 64 words, so every slot moves the same p / m / v bytes to within a unit
+// (one short-lived workgroup per 64-word tile spent most of its time starting up and
+// waiting), with block i + 1's adapted columns and Adam state in flight in a second
+// register set while block i's gradient G[v, h] = sum_{b < nb} A[b, v] dz0[b, h] runs on the
+// matrix cores and its update is stored.  p / m / v go through buffer loads / stores at
+// 4-byte granularity (a block's [words, H0] run need not be 16-byte aligned).
+constexpr int WIN_CTXPP = 16384;
+constexpr int WCT = 512;
+__host__ __device__ inline int win_ctxpp_lds_floats(const GfkModel& m) {
+  return ((m.bmax * m.H[0] + 3) & ~3) + 64 * 80 + 64 * 64;
+}
+template <bool GB = false>
+__global__ void __launch_bounds__(WCT, 4) gfk_win_ctx_pp_k(GfkArgT<GB> ga) {
+  const GfkModel& m = gfk_model(ga);
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
+  const int V = m.V, H0 = m.H[0], B = m.bmax, nb = *m.ws_nb;
+  const int G = (int)gridDim.x, w = (int)blockIdx.x;
+  const int U = (V + 15) / 16;
+  const int cs = (int)((int64_t)w * U / G) * 16;
+  const int ce = min(V, (int)((int64_t)(w + 1) * U / G) * 16);
+  float* dz = smem;                                   // [B][H0]
+  float* at = smem + ((B * H0 + 3) & ~3);             // [64 b][80] the block's adapted columns
+  float* gt = at + 64 * 80;                           // [64 words][H0] gradient, flat
+  const bool fused = m.update_mode == 1;
+  const AdamCoef ac = adam_coef(m);
+  const bool sh = is_shared(m, m.w_in);
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  const __amdgpu_buffer_rsrc_t rs_p = __builtin_amdgcn_make_buffer_rsrc((void*)m.flat_base, 0, 0x7FFFFFFF, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_m =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(m.flat_base + (fused ? m.off_m : m.off_g)), 0, 0x7FFFFFFF, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_v = __builtin_amdgcn_make_buffer_rsrc((void*)(m.flat_base + m.off_v), 0, 0x7FFFFFFF, 0x00020000);
+  const uint32_t wc0 = (uint32_t)((m.w_in + (size_t)V * H0) - m.flat_base) * 4u;   // Wc's first byte
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  glds_copy(dz, m.ws_dz[0], B * H0, tid, WCT);
+  // per-thread quads of a block's flat [words, H0] run: e = 4 (tid + WCT u), u < 2
+  // A columns: (b, q) = ((tid + WCT u) >> 4, (tid + WCT u) & 15): 4 consecutive words of row b
+  auto ld_blk = [&](int v0, int nw, f32x4 (&P)[6], f32x4 (&A)[2]) {
+    const int nel = nw * H0;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = 4 * (tid + WCT * u);
+      const uint32_t off = wc0 + ((uint32_t)v0 * (uint32_t)H0 + (uint32_t)min(e, max(nel - 4, 0))) * 4u;
+      P[3 * u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_p, off, 0, 0));
+      P[3 * u + 1] = fused ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_m, off, 0, 0)) : z4;
+      P[3 * u + 2] = fused ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_v, off, 0, 0)) : z4;
+      const int i = tid + WCT * u, b = i >> 4, q = i & 15, v = v0 + 4 * q;
+      A[u] = (b < B && 4 * q < nw)
+                 ? *reinterpret_cast<const f32x4*>(m.ws_actx + ((size_t)(v >> 6) * B + b) * 64 + (v & 63))
+                 : z4;
+    }
+  };
+  const int NT = (H0 + 15) / 16;
+  auto do_blk = [&](int v0, int nw, const f32x4 (&P)[6], const f32x4 (&A)[2]) {
+    const int nel = nw * H0;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = tid + WCT * u, b = i >> 4, q = i & 15;
+      *reinterpret_cast<f32x4*>(at + b * 80 + 4 * q) = b < nb ? A[u] : z4;
+    }
+    vm_barrier();                                     // (first block: dz0's LDS-DMA too)
+    // G subtiles (word tile, h tile) = t = wave + 8 u: A-role at[b][v] (b = k + lane >> 4),
+    // B-role dz[b][h] (columns >= H0 read the next row: discarded)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int t = wave + (WCT / 64) * u;
+      if (t >= 4 * NT) break;
+      const int i0 = (t / NT) * 16, j0 = (t % NT) * 16;
+      f32x4 acc = z4;
+      const float* ap = at + (lane >> 4) * 80 + i0 + (lane & 15);
+      const float* bp = dz + (lane >> 4) * H0 + j0 + (lane & 15);
+      for (int k = 0; k < B; k += 4) acc = mfma16x16x4(ap[k * 80], bp[k * H0], acc);
+      const int j = j0 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (j < H0) gt[(i0 + (lane >> 4) * 4 + r) * H0 + j] = acc[r];
+    }
+    lds_barrier();
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = 4 * (tid + WCT * u);
+      if (e >= nel) break;
+      const uint32_t off = wc0 + ((uint32_t)v0 * (uint32_t)H0 + (uint32_t)e) * 4u;
+      f32x4 g4 = *reinterpret_cast<const f32x4*>(gt + e);
+      f32x4 np, mo, vo;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float a = P[3 * u + 1][i], b2 = P[3 * u + 2][i];
+        const float x = fused ? adam_update(P[3 * u][i], g4[i], a, b2, ac) : g4[i];
+        np[i] = sh && m.fed_scale_on && fused ? x * m.fed_scale : x;
+        mo[i] = a;
+        vo[i] = b2;
+      }
+      if (e + 3 < nel) {
+        if (fused) {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, mo), rs_m, off, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, vo), rs_v, off, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, np), rs_p, off, 0, 0);
+        } else {
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, np), rs_m, off, 0, 0);   // (rs_m = grad)
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (e + i >= nel) break;
+          if (fused) {
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mo[i]), rs_m, off + 4 * i, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vo[i]), rs_v, off + 4 * i, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(np[i]), rs_p, off + 4 * i, 0, 0);
+          } else {
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(np[i]), rs_m, off + 4 * i, 0, 0);
+          }
+        }
+      }
+    }
+    lds_barrier();                                    // before the next block's A columns / G
+  };
+  f32x4 PA[6], AA[2], PB[6], AB[2];
+  if (cs < ce) ld_blk(cs, min(64, ce - cs), PA, AA);
+  for (int v0 = cs; v0 < ce; v0 += 128) {
+    const int n0 = min(64, ce - v0);
+    if (v0 + 64 < ce) ld_blk(v0 + 64, min(64, ce - v0 - 64), PB, AB);
+    do_blk(v0, n0, PA, AA);
+    if (v0 + 64 >= ce) break;
+    if (v0 + 128 < ce) ld_blk(v0 + 128, min(64, ce - v0 - 128), PA, AA);
+    do_blk(v0 + 64, min(64, ce - v0 - 64), PB, AB);
+  }
+}
+
 // Split W_in update (stage_flags GFK_WIN_SPLIT, fused mode): the sparse tile updates only
 // the words of the batch -- the words stamped with this batch's generation by
 // prepare_next_batch, which are exactly the words with entries in the tiles' lists --
@@ -1069,6 +1201,15 @@ static bool win_sparse_vl(const GfkModel* m) {
                          gfk_win_update_smem(m), s, GfkArgT<false>{*m}, GfkUArgT<false>{*u});    \
   } while (0)
 
+static int launch_win_sparse_bow(const GfkModel* m, const GfkUpdate* u, hipStream_t s) {
+  const dim3 gs(u->n_w + u->n_v + 1 + m->n_tiles);
+  if (win_sparse_vl(m))
+    GFK_WIN_SPARSE_LAUNCH(true, false);
+  else
+    GFK_WIN_SPARSE_LAUNCH(false, false);
+  return (int)hipGetLastError();
+}
+
 extern "C" int gfk_launch_win_update(const GfkModel* m, const GfkUpdate* u, hipStream_t s) {
   const int extra = m->ctx_fused == 1 ? m->n_tiles : (m->ctx_fused == 2 ? (m->C + 63) / 64 : 0);
   if (m->stage_flags & WIN_SPARSE) {
@@ -1078,6 +1219,16 @@ extern "C" int gfk_launch_win_update(const GfkModel* m, const GfkUpdate* u, hipS
     if (m->H[0] > 64 || m->bmax > (comb ? 64 : 128) || !(m->input == GFK_IN_BOW || comb) ||
         (comb && (m->stage_flags & GFK_WIN_SPLIT)))
       return -1;
+    // the contextual half: dense tiles of this launch, or the persistent kernel after it
+    const bool ctxpp = comb && (m->stage_flags & WIN_CTXPP) && m->ctx_bgrid > 0;
+    if (ctxpp) {
+      const int e = launch_win_sparse_bow(m, u, s);
+      if (e) return e;
+      const dim3 gp(2 * m->ctx_bgrid);
+      const size_t sp = sizeof(float) * win_ctxpp_lds_floats(*m);
+      do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_win_ctx_pp_k<true>), gfk_grid(gp, m), dim3(WCT), sp, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_win_ctx_pp_k<false>), gp, dim3(WCT), sp, s, GfkArgT<false>{*m}); } while (0);
+      return (int)hipGetLastError();
+    }
     const dim3 gs(u->n_w + u->n_v + 1 + m->n_tiles * (comb ? 2 : 1));
     if (m->stage_flags & GFK_WIN_SPLIT)
       do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_win_rows_k<512, true>), gfk_grid(gs, m), dim3(512), gfk_win_update_smem(m), s, GfkArgT<true>{gfk_dev(m)}, GfkUArgT<true>{reinterpret_cast<const GfkUpdate*>(m->dev_upd)}); else hipLaunchKernelGGL((gfk_win_rows_k<512, false>), gs, dim3(512), gfk_win_update_smem(m), s, GfkArgT<false>{*m}, GfkUArgT<false>{*u}); } while (0);

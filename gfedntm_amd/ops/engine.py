@@ -64,6 +64,8 @@ STAGE_WIN_BATCH8 = 512            # bit 9: batched launches: win_update's 8-wave
 STAGE_WIN_VREG = 1024             # bit 10: sparse W_in tiles keep the second moment in registers
 STAGE_CTX_BAL = 2048              # bit 11: CombinedTM forward, balanced persistent shape (csrc/ctx.hip)
 STAGE_CTX_BWDPP = 4096            # bit 12: CombinedTM backward, persistent pipelined shape (csrc/ctx.hip)
+STAGE_CTX_BAL3 = 8192             # bit 13: the balanced forward's 16-wave 3-deep variant (csrc/ctx.hip)
+STAGE_WIN_CTXPP = 16384           # bit 14: CombinedTM's contextual W_in half as a persistent kernel
 
 
 def _explain(ok: bool, why: str, explain: bool) -> bool:
@@ -564,10 +566,17 @@ class FusedEngine(EngineBase):
             # equal column ranges instead of one workgroup per tile (whose last round runs
             # mostly empty) and leave one contextual z0 partial each; slices staged by DMA.
             # GFEDNTM_CTX_BAL=0 keeps the one-workgroup-per-tile kernel
-            if (os.environ.get("GFEDNTM_CTX_BAL", "1") != "0" and int(m.H[0]) <= 64
-                    and m.V * m.C * 4 < (1 << 31)):
+            bal = os.environ.get("GFEDNTM_CTX_BAL", "3")
+            if bal != "0" and int(m.H[0]) <= 64 and m.V * m.C * 4 < (1 << 31):
                 m.stage_flags |= STAGE_CTX_BAL
                 m.ctx_parts = int(min(m.n_tiles, 2 * cu_n))
+                # "3": one 16-wave workgroup per CU, slices three deep (counted waits), the
+                # Wc rows / bias by DMA too; needs C > 192, H0 <= 63 and the flat buffer
+                # under 2 GB (32-bit buffer offsets)
+                if (bal == "3" and int(m.H[0]) <= 63 and m.C > 192
+                        and 4 * self.flat.n_total < (1 << 31)):
+                    m.stage_flags |= STAGE_CTX_BAL3
+                    m.ctx_parts = int(min(m.n_tiles, cu_n))
         # CombinedTM backward as one persistent workgroup per CU walking equal ranges of the
         # (tile, C chunk) items with the next item's Wa state in flight (csrc/ctx.hip
         # gfk_ctx_bwd_pp_k); GFEDNTM_CTX_BWDPP=0 keeps the (tile, chunk) grid
@@ -583,6 +592,16 @@ class FusedEngine(EngineBase):
         if (m.input == abi.IN_BOW or comb) and int(m.H[0]) <= 64 and m.bmax <= 128 and (
                 ws_env == "1" or (ws_env == "auto" and m.n_tiles > 4 * cu_n)):
             m.stage_flags |= STAGE_WIN_SPARSE
+            # fused CombinedTM: the contextual half (Wc) as dense tiles of the same launch, or
+            # (GFEDNTM_WIN_CTXPP=1) as a persistent kernel after the sparse tiles (csrc/
+            # update.hip gfk_win_ctx_pp_k: equal word ranges per slot, the next block's state
+            # in flight).  Not the default: V = 99k, interleaved on one box, round 0.7309 /
+            # 0.7415 ms with the tiles vs 0.7389 / 0.7389 (the kernel moves Wc's 120 MB at
+            # 2.4 TB/s: Wc's rows start V H0 floats into W_in, not 16-byte aligned at odd V)
+            if (comb and os.environ.get("GFEDNTM_WIN_CTXPP", "0") == "1"
+                    and 4 * self.flat.n_total < (1 << 31)):
+                m.stage_flags |= STAGE_WIN_CTXPP
+                m.ctx_bgrid = int(cu_n)
             # fused mode: the tile's second moment goes through LDS (64 VGPRs, 4 workgroups
             # per CU; profiles/r3/win_vl/); GFEDNTM_WIN_VL=0 keeps it in registers
             if os.environ.get("GFEDNTM_WIN_VL", "1") == "0":
@@ -869,7 +888,7 @@ class FusedEngine(EngineBase):
         if m.stage_flags & STAGE_CTX_BAL and data.contextual is not None \
                 and 4 * data.contextual.numel() >= (1 << 31):
             # the balanced forward addresses x_ctx with 32-bit buffer offsets
-            m.stage_flags &= ~STAGE_CTX_BAL
+            m.stage_flags &= ~(STAGE_CTX_BAL | STAGE_CTX_BAL3)
             m.ctx_parts = 0
         if m.lab_on:
             if data.labels is None or data.labels.shape[1] != m.L:

@@ -730,25 +730,30 @@ def test_sparse_win_tiles_match_oracle(monkeypatch, model_type, B, n_docs, K, H,
     _oracle_step(model_type, B, n_docs, K, H, V)
 
 
-@pytest.mark.parametrize("bal", ["1", "0"])
-@pytest.mark.parametrize("Cdim,V", [(96, 600), (768, 9000), (100, 5000)])
+@pytest.mark.parametrize("bal", ["3", "1", "0"])
+@pytest.mark.parametrize("Cdim,V", [(96, 600), (768, 9000), (100, 5000), (260, 3000), (768, 40000)])
 def test_ctm_full_tile_forward_matches_oracle(monkeypatch, Cdim, V, bal):
     """ctx_fwd with all batch rows per vocab tile (stage_flags bit 5, the large-V shape;
     GFEDNTM_CTX_FULL=1 forces it at small V): the balanced persistent kernel (bit 11,
     DMA-staged slices, column ranges of 16-column units not aligned to the 64-column
-    tiles, a partial last C slice at C = 96 / 100) or one workgroup per tile (bal = 0)."""
+    tiles, a partial last C slice at C = 96 / 100 / 260), its 16-wave 3-deep variant (bal = 3,
+    C > 192: the counted slice waits across chunk boundaries) or one workgroup per tile
+    (bal = 0)."""
     monkeypatch.setenv("GFEDNTM_CTX_FULL", "1")
     monkeypatch.setenv("GFEDNTM_CTX_BAL", bal)
     test_ctm_step_matches_oracle("combined", Cdim, V, 20, "prodLDA")
 
 
+@pytest.mark.parametrize("ctxpp", ["1", "0"])
 @pytest.mark.parametrize("Cdim,V", [(96, 600), (768, 9000)])
-def test_ctm_sparse_win_tiles_match_oracle(monkeypatch, Cdim, V):
+def test_ctm_sparse_win_tiles_match_oracle(monkeypatch, Cdim, V, ctxpp):
     """CombinedTM with the sparse W_in tiles (GFEDNTM_WIN_SPARSE=1 forces the large-V
     path): the bag-of-words half as entry-list tiles and the contextual half as dense
     A^T dz0 tiles of the same launch (csrc/update.hip win_tile_ctx) give the oracle's
-    input-layer gradient (both halves)."""
+    input-layer gradient (both halves); ctxpp = 1: the contextual half by the persistent
+    kernel after the sparse launch (csrc/update.hip gfk_win_ctx_pp_k)."""
     monkeypatch.setenv("GFEDNTM_WIN_SPARSE", "1")
+    monkeypatch.setenv("GFEDNTM_WIN_CTXPP", ctxpp)
     test_ctm_step_matches_oracle("combined", Cdim, V, 20, "prodLDA")
 
 
