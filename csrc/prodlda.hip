@@ -1286,10 +1286,11 @@ __global__ void __launch_bounds__(512, 2) prodlda_bwd_pre2_kernel(GfkArgT<GB> ga
 constexpr int LDP = 72;
 typedef unsigned int gfk_u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ int dtt_swz(int c) { return ((c >> 2) & 7) << 2; }
-// Memory operations (r3): beta / m / v / the gradient through buffer descriptors with one
-// VGPR column offset per tile and per-row SGPR offsets (row k of a range is wave-uniform:
-// k = kb + wave + 8 u), instead of a 64-bit address per element and a select between the
-// element and a sink: rows past K (the last k range's padding) get an out-of-range voffset
+// Memory operations: beta / m / v / the gradient through buffer descriptors, one 16-byte
+// quad per instruction (r4; r3 moved one float per lane: 4x the memory instructions), a
+// column offset per tile and per-quad row offsets, instead of a 64-bit address per element
+// and a select between the element and a sink: rows past K (the last k range's padding) get
+// an out-of-range voffset
 // (the descriptor's range check: loads return 0, stores are dropped); columns past V
 // fall into beta's row padding (ldb is a multiple of 64 on this path; padding columns have
 // a zero gradient and stay zero).  FUSED (Adam + pre-scale, else the gradient) is a
@@ -1304,6 +1305,9 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
   constexpr int NKS = MAXU;                                    // max k tiles per range
   constexpr int RPU = NTH / VB;                                // 8 block rows per slot
   constexpr int RU = 16 * NKS * VB / NTH;                      // block elements per thread
+  constexpr int RQ = (NKS + 1) / 2;                            // ... as quads (4 columns; rows
+                                                               //  past 16 NKS: out of range)
+  constexpr int RPQ = NTH / (VB / 4);                          // 32 block rows per quad slot
   constexpr int MU = (NKS * 4 + NW - 1) / NW;                  // dbeta subtiles per wave
   constexpr int NDT = ((BM / 16) * NKS + NW - 1) / NW;         // d theta_d subtiles per wave
   constexpr int DU = BM * VB / 4 / NTH;                        // dlogit float4 per thread
@@ -1338,41 +1342,44 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
     thT[c * LDP + b] = c < 16 * nks ? m.ws_thetad[(size_t)b * m.kt + kb + c] : 0.f;
   }
 
-  float br[RU];
+  f32x4 br[RQ];
   f32x4 dr[DU];
   // buffer descriptors over beta's slot and its m / v / gradient twins (host-checked:
-  // K ldb 4 < 2^31), the dlogit tiles, and the per-row offsets of this wave's elements
+  // K ldb 4 < 2^31), the dlogit tiles, and the row offsets of this thread's quads
   const int nrec = K * m.ldb * 4;
   const __amdgpu_buffer_rsrc_t rs_b = __builtin_amdgcn_make_buffer_rsrc((void*)m.beta, 0, nrec, 0x00020000);
   const __amdgpu_buffer_rsrc_t rs_m = __builtin_amdgcn_make_buffer_rsrc((void*)(m.beta + (FUSED ? m.off_m : m.off_g)), 0, nrec, 0x00020000);
   const __amdgpu_buffer_rsrc_t rs_v = __builtin_amdgcn_make_buffer_rsrc((void*)(m.beta + m.off_v), 0, nrec, 0x00020000);
   const __amdgpu_buffer_rsrc_t rs_d = __builtin_amdgcn_make_buffer_rsrc((void*)m.ws_dt, 0, n_tiles * BM * VB * 4, 0x00020000);
-  int rowoff[RU];                              // bytes; rows outside the range / K: out of range
+  // quad u of a thread: block row tid / 16 + 32 u, columns 4 (tid % 16) .. + 3 -- every
+  // beta / m / v load and store moves 16 bytes (a wave covers 4 rows x 256 B) instead of 4
+  // (one row x 256 B per instruction: 4x the memory instructions for the same bytes)
+  int rowoff[RQ];                              // bytes; rows outside the range / K: out of range
 #pragma unroll
-  for (int u = 0; u < RU; ++u) {
-    const int kl = wave + RPU * u, k = kb + kl;
-    rowoff[u] = uniform(kl < 16 * nks && k < K ? k * m.ldb * 4 : 0x7FFF0000);
+  for (int u = 0; u < RQ; ++u) {
+    const int kl = (tid >> 4) + RPQ * u, k = kb + kl;
+    rowoff[u] = kl < 16 * nks && k < K ? k * m.ldb * 4 : 0x7FFF0000;
   }
-  const int lane4 = 4 * (tid & (VB - 1));
-  // element tid + NTH u of the block is (row tid / VB + RPU u, column tid % VB)
+  const int lane16 = 16 * (tid & 15);
   auto issue_bd = [&](int tile) {             // beta slice + dlogit tile
-    const int vc = tile * VB * 4 + lane4;
+    const int vc = tile * VB * 4 + lane16;
 #pragma unroll
     for (int j = 0; j < DU; ++j) {
       const gfk_u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs_d, (tid + NTH * j) * 16, uniform(tile * BM * VB * 4), 0);
       dr[j] = f32x4{__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z), __uint_as_float(x.w)};
     }
 #pragma unroll
-    for (int u = 0; u < RU; ++u) br[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_b, boff(vc, rowoff[u]), 0, 0));
+    for (int u = 0; u < RQ; ++u)
+      br[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_b, boff(vc, rowoff[u]), 0, 0));
   };
   // Adam state (fused mode only)
-  auto issue_mv = [&](int tile, float (&rm)[RU], float (&rv)[RU]) __attribute__((always_inline)) {
+  auto issue_mv = [&](int tile, f32x4 (&rm)[RQ], f32x4 (&rv)[RQ]) __attribute__((always_inline)) {
     if constexpr (FUSED) {
-      const int vc = tile * VB * 4 + lane4;
+      const int vc = tile * VB * 4 + lane16;
 #pragma unroll
-      for (int u = 0; u < RU; ++u) {
-        rm[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_m, boff(vc, rowoff[u]), 0, 0));
-        rv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_v, boff(vc, rowoff[u]), 0, 0));
+      for (int u = 0; u < RQ; ++u) {
+        rm[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_m, boff(vc, rowoff[u]), 0, 0));
+        rv[u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_v, boff(vc, rowoff[u]), 0, 0));
       }
     }
   };
@@ -1406,7 +1413,7 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
 #pragma unroll
   for (int j = 0; j < NDT; ++j) dacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  float rm0[RU], rv0[RU], rm1[RU], rv1[RU];
+  f32x4 rm0[RQ], rv0[RQ], rm1[RQ], rv1[RQ];
   issue_bd(slab);
   issue_mv(slab, rm0, rv0);
   // the loop's epilogue issues 3 RU stores after the next tile's loads; the same number of
@@ -1417,8 +1424,8 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
   float* const wsink = sink - (tid & 63);
   constexpr int NST = FUSED ? 3 : 1;           // stores per element in the loop's epilogue
 #pragma unroll
-  for (int u = 0; u < NST * RU; ++u) wsink[(tid + 5 * u) & 63] = 0.f;
-  auto body = [&](int tile, float (&rm)[RU], float (&rv)[RU], float (&nm)[RU], float (&nv)[RU])
+  for (int u = 0; u < NST * RQ; ++u) wsink[(tid + 5 * u) & 63] = 0.f;
+  auto body = [&](int tile, f32x4 (&rm)[RQ], f32x4 (&rv)[RQ], f32x4 (&nm)[RQ], f32x4 (&nv)[RQ])
       __attribute__((always_inline)) {
     const int c0 = tile * VB;
     asm volatile("" : "+v"(tid));
@@ -1428,9 +1435,9 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
     lds_barrier();                             // the previous tile's LDS reads are done
     {
       // (rows past the range / K and columns past V were loaded as 0)
-      const int c = tid & (VB - 1);
 #pragma unroll
-      for (int u = 0; u < RU; ++u) bt[__mul24(tid / VB + RPU * u, LDP) + c] = br[u];
+      for (int u = 0; u < RQ; ++u)
+        *reinterpret_cast<f32x4*>(bt + __mul24((tid >> 4) + RPQ * u, LDP) + 4 * (tid & 15)) = br[u];
 #pragma unroll
       for (int j = 0; j < DU; ++j) {           // dense [BM][64] -> dt [b][c] and dtT [c][b]
         const int i = tid + NTH * j, r = i >> 4, c4 = (i & 15) * 4;
@@ -1489,29 +1496,32 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
       }
     }
     lds_barrier();
-    // the G tile, row-wise: update (fused) or gradient
-    const int cl = tid & (VB - 1), kl0 = tid / VB;
-    const int cs = cl ^ ((kl0 & 4) << 2);
-    const int vc = c0 * 4 + lane4;
-    // row pointers stepped by constants (folded into the ds_read offsets).  LDS index
-    // products are __mul24 throughout: a plain 32-bit multiply-add became v_mad_u64_u32,
-    // whose unused high addend half was a register with a load in flight, and the waitcnt
-    // pass then waited vmcnt(0) -- the previous tile's stores drained -- at every tile
-    const float* gtp = gt + __mul24(kl0, VB) + cs;
-    const float* btp = bt + __mul24(kl0, LDP) + cl;
+    // the G tile, row-wise quads: update (fused) or gradient (the XOR 16 (k & 4) column
+    // swizzle keeps a quad's 4 columns together)
+    const int kl0 = tid >> 4, c4 = 4 * (tid & 15);
+    const int vc = c0 * 4 + lane16;
 #pragma unroll
-    for (int u = 0; u < RU; ++u) {
-      const float gv = gtp[RPU * u * VB];
+    for (int u = 0; u < RQ; ++u) {
+      const int kl = kl0 + RPQ * u;
+      const f32x4 gv = *reinterpret_cast<const f32x4*>(gt + __mul24(kl, VB) + (c4 ^ ((kl & 4) << 2)));
+      const int vo4 = boff(vc, rowoff[u]);
       if constexpr (FUSED) {
-        float mo = rm[u], vo = rv[u];
-        float np = adam_update(btp[RPU * u * LDP], gv, mo, vo, ac);
-        if (beta_shared && m.fed_scale_on) np *= m.fed_scale;
-        const int vo4 = boff(vc, rowoff[u]);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mo), rs_m, vo4, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vo), rs_v, vo4, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(np), rs_b, vo4, 0, 0);
+        const f32x4 pv = *reinterpret_cast<const f32x4*>(bt + __mul24(kl, LDP) + c4);
+        f32x4 mo = rm[u], vo = rv[u], np;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float a = mo[e], b2 = vo[e];
+          float x = adam_update(pv[e], gv[e], a, b2, ac);
+          if (beta_shared && m.fed_scale_on) x *= m.fed_scale;
+          mo[e] = a;
+          vo[e] = b2;
+          np[e] = x;
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(gfk_u32x4, mo), rs_m, vo4, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(gfk_u32x4, vo), rs_v, vo4, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(gfk_u32x4, np), rs_b, vo4, 0, 0);
       } else {                                 // the gradient (rs_m is the gradient slot)
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(gv), rs_m, boff(vc, rowoff[u]), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(gfk_u32x4, gv), rs_m, vo4, 0, 0);
       }
     }
   };
