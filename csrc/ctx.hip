@@ -725,6 +725,255 @@ __global__ void __launch_bounds__(FT3) gfk_ctx_fwd_bal3_k(GfkArgT<GB> ga) {
   }
 }
 
+// Register-streamed forward (stage_flags bit 15, GFEDNTM_CTX_BAL=4; B <= 64, H0 <= 64, at
+// most 32 16-column units per workgroup).  The DMA-staged variants above move every Wa slice
+// AND the matching x_ctx slice through LDS once per 64-column chunk (x_ctx re-staged per
+// chunk, a barrier per slice, and at most two slices = 1.7 us of Wa in flight per CU).  Here
+// one 16-wave workgroup per CU owns a contiguous range of nu 16-column units; wave w owns
+// units w and w + 16 of it, and computes A^T[v, b] = sum_k Wa[v, k] x[b, k] with Wa as the
+// MFMA A operand straight from global memory into registers:
+//  * lane (r, g) loads Wa[v = 16 unit + r][16 j + 4 g .. + 3] as ONE 128-bit buffer load per
+//    16-float block j, consumed by 4 k steps x 4 batch-row tiles (16 MFMAs);
+//  * a ring of RS_R = 8 blocks per wave (32 VGPRs) is refilled right after each block is
+//    read, with the next block of this unit or the first ones of the wave's next (phase,
+//    unit) segment: 8 blocks x 4 waves per SIMD of MFMA work to arrive (~7 us), 256 KB per CU;
+//  * x_ctx, the batch's 64 rows, is the B operand from LDS in phases of 256 k (64 KB, two
+//    buffers: phase p + 1 arrives by LDS-DMA while phase p is multiplied; quads XOR-swizzled
+//    by (row & 15), so a ds_read_b128 of 16 rows x 4 quads hits every bank once); each phase
+//    is staged ONCE per workgroup (one barrier per phase, 3 at C = 768) instead of per chunk;
+//  * the accumulators of both units (32 VGPRs) live across the phases;
+//  * balance: the unit is the grain, so a 25-unit workgroup (V = 99k) would give one SIMD
+//    7 units and the others 6.  With nu = 16 + 4 q + 1 (17, 21, 25, 29) the last unit is
+//    split by phase instead: phase p of it goes to helper wave 4 q + 1 + p % 3 (SIMDs 1..3,
+//    waves with one full unit: their second accumulator), so the SIMDs carry 6, 6 1/3,
+//    6 1/3, 6 1/3; the partials meet in LDS in the epilogue (fixed order: deterministic).
+// Epilogue: A + bias -> ws_actx and, in [b][v] layout, into the freed LDS; then P^T[h, b] +=
+// Wc^T A^T over the workgroup's words on the matrix cores (wave -> subtile (b tile, h tile),
+// Wc from global in chunks of 8 k steps, the next chunk in flight): ONE z0 partial per
+// workgroup in ws_hpart (ctx_parts = the grid), as the balanced kernels leave it.
+constexpr int CTX_RS = 32768;
+constexpr int RS_T = 1024, RS_KP = 256, RS_R = 8, RS_AL = 512;
+// x phases / A [64][RS_AL] (the same 128 KB), + 3 split-unit partials [64][16]
+__host__ __device__ inline int fwd_rs_lds_floats() { return 2 * 64 * RS_KP + 3 * 64 * 16; }
+template <bool GB = false>
+__global__ void __launch_bounds__(RS_T) gfk_ctx_fwd_rs_k(GfkArgT<GB> ga) {
+  const GfkModel& m = gfk_model(ga);
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
+  const int r = lane & 15, g = lane >> 4;
+  const int V = m.V, C = m.C, H0 = m.H[0], bmax = m.bmax;
+  const int G = (int)gridDim.x, w = (int)blockIdx.x;
+  const int U = (V + 15) / 16;
+  const int u0 = (int)((int64_t)w * U / G), nu = (int)((int64_t)(w + 1) * U / G) - u0;
+  const int NPH = (C + RS_KP - 1) / RS_KP;
+  const bool split = nu > 16 && (nu & 3) == 1;
+  const int nuf = split ? nu - 1 : nu;              // full units
+  const int hw0 = nuf - 15;                         // split: helpers hw0 .. hw0 + 2
+  const bool full1 = wave + 16 < nuf;               // a second full unit
+  const bool helper = split && wave >= hw0 && wave < hw0 + min(NPH, 3);
+  const bool has0 = wave < nuf;
+  // (phase, slot) segments of this wave; slot 1 = the second full unit, or a helper's
+  // phases p of the split unit (p % 3 == wave - hw0)
+  auto has = [&](int p, int t) { return t == 0 ? has0 : (full1 || (helper && p % 3 == wave - hw0)); };
+  auto unit_of = [&](int t) { return t == 0 ? u0 + wave : (full1 ? u0 + wave + 16 : u0 + nuf); };
+  constexpr uint32_t OOB = 0x80000000u;
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  const __amdgpu_buffer_rsrc_t rs_x = __builtin_amdgcn_make_buffer_rsrc((void*)m.ctx, 0, 0x7FFFFFFF, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_w =
+      __builtin_amdgcn_make_buffer_rsrc((void*)m.w_a, 0, (int)((uint32_t)V * (uint32_t)C * 4u), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_f = __builtin_amdgcn_make_buffer_rsrc((void*)m.flat_base, 0, 0x7FFFFFFF, 0x00020000);
+  const uint32_t wc_off = (uint32_t)((m.w_in + (size_t)V * H0) - m.flat_base) * 4u;
+  const uint32_t ba_off = (uint32_t)(m.b_a - m.flat_base) * 4u;
+  // ---- x_ctx phase DMA: wave w moves rows 4 w .. 4 w + 3, one 1 KB row per instruction:
+  //      LDS quad `lane` of row b <- global quad lane ^ (b & 15) of the phase ----
+  uint32_t xrow[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int b = 4 * wave + i;
+    xrow[i] = b < bmax ? (uint32_t)m.ws_next[1 + b] * (uint32_t)C * 4u : OOB;
+  }
+  auto dma_x = [&](int p, float* buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int b = 4 * wave + i;
+      const int k = p * RS_KP + 4 * (lane ^ (b & 15));
+      const uint32_t off = (xrow[i] != OOB && k < C) ? xrow[i] + (uint32_t)k * 4u : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_x, (lds_void_ptr)(buf + b * RS_KP), 16, off, 0, 0, 0);
+    }
+  };
+  // per-lane Wa offset of segment (p, t); past the last segment (p = NPH) and for words >= V
+  // out of range: the loads return zeros
+  auto seg_off = [&](int p, int t) -> uint32_t {
+    if (p >= NPH) return OOB;
+    const int v = unit_of(t) * 16 + r;
+    return v < V ? ((uint32_t)v * (uint32_t)C + (uint32_t)(p * RS_KP + 4 * g)) * 4u : OOB;
+  };
+  // the segment after (p, t) in (phase, slot) order (p = NPH: none)
+  auto succ = [&](int& p, int& t) {
+    do {
+      if (++t > 1) { t = 0; ++p; }
+    } while (p < NPH && !has(p, t));
+  };
+  auto ldw = [&](uint32_t off, int j) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_w, off + 64u * j, 0, 0));
+  };
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int bt = 0; bt < 4; ++bt) acc[t][bt] = z4;
+  dma_x(0, smem);
+  int pc = 0, tc = 0;                   // the first segment, then the one after it
+  if (!has(0, 0)) succ(pc, tc);
+  int pn = pc, tn = tc;
+  succ(pn, tn);
+  uint32_t offc = seg_off(pc, tc), offn = seg_off(pn, tn);
+  f32x4 ring[RS_R];
+  // (sched_barrier fences keep the loads in ring order and where they are written: the
+  // scheduler otherwise sinks each refill to its use, 8 blocks later, under register
+  // pressure -- and vmcnt counts in issue order)
+#pragma unroll
+  for (int q = 0; q < RS_R; ++q) {
+    ring[q] = ldw(offc, q);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  for (int p = 0; p < NPH; ++p) {
+    // phase p's x: issued before every ring load still in flight (RS_R of them, issued
+    // after it by any wave with a segment since; a wave without one may have issued none)
+    if (has0 || helper) asm volatile("s_waitcnt vmcnt(8)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else vm_barrier();
+    // (4 j + g) ^ r = 16 (j >> 2) + 4 ((j & 3) ^ (r >> 2)) + (g ^ (r & 3)): four lane
+    // offsets, the rest immediates
+    const float* xc = smem + (p & 1) * 64 * RS_KP + r * RS_KP + (g ^ (r & 3)) * 4;
+    if (p + 1 < NPH) dma_x(p + 1, smem + ((p + 1) & 1) * 64 * RS_KP);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      if (has(p, t)) {
+#pragma unroll
+        for (int j = 0; j < RS_KP / 16; ++j) {
+          f32x4 xv[4];
+#pragma unroll
+          for (int bt = 0; bt < 4; ++bt)
+            xv[bt] = *reinterpret_cast<const f32x4*>(xc + bt * 16 * RS_KP + 64 * (j >> 2) + 16 * ((j & 3) ^ (r >> 2)));
+          const f32x4 wv = ring[j % RS_R];
+          __builtin_amdgcn_sched_barrier(0);
+          ring[j % RS_R] = j + RS_R < RS_KP / 16 ? ldw(offc, j + RS_R) : ldw(offn, j + RS_R - RS_KP / 16);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int bt = 0; bt < 4; ++bt) acc[t][bt] = mfma16x16x4(wv[i], xv[bt][i], acc[t][bt]);
+        }
+        offc = offn;
+        succ(pn, tn);
+        offn = seg_off(pn, tn);
+      }
+    }
+  }
+  // ---- epilogue: the first Wc chunk in flight while A (+ bias) goes to ws_actx and LDS ----
+  const int NJT = (H0 + 15) / 16;
+  const int bt = wave & 3, ht = wave >> 2, hh = ht * 16 + r;
+  auto ldwc = [&](f32x4 (&wc)[8], int c) {
+#pragma unroll
+    for (int sx = 0; sx < 8; ++sx)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int vl = 16 * (8 * c + sx) + 4 * g + i, v = u0 * 16 + vl;
+        const uint32_t o = (vl < 16 * nu && v < V && hh < H0) ? wc_off + ((uint32_t)v * (uint32_t)H0 + (uint32_t)hh) * 4u : OOB;
+        wc[sx][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_f, o, 0, 0));
+      }
+  };
+  f32x4 wA[8], wB[8];
+  if (ht < NJT) ldwc(wA, 0);
+  // bias of the wave's full units; the split unit's (its summing wave: hw0)
+  const bool summer = split && wave == hw0;
+  f32x4 bias[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int v = (t == 0 ? u0 + wave : (full1 ? u0 + wave + 16 : u0 + nuf)) * 16 + 4 * g + i;
+      const bool on = t == 0 ? has0 : (full1 || summer);
+      bias[t][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_f, on && v < V ? ba_off + (uint32_t)v * 4u : OOB, 0, 0));
+    }
+  lds_barrier();                        // every wave done with the last phase's x
+  float* al = smem;                     // [64 b][RS_AL v], quads XOR (b & 15)
+  float* sp = smem + 2 * 64 * RS_KP;    // [3][64 b][16 v] split-unit partials
+  // A of unit ul (+ bias) into LDS and ws_actx
+  auto put_a = [&](int ul, const f32x4 (&a4)[4], const f32x4& bs) {
+    const int v0 = (u0 + ul) * 16 + 4 * g;
+#pragma unroll
+    for (int b4 = 0; b4 < 4; ++b4) {
+      const int b = b4 * 16 + r;
+      f32x4 a;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = v0 + i < V ? a4[b4][i] + bs[i] : 0.f;
+      *reinterpret_cast<f32x4*>(al + b * RS_AL + 4 * ((4 * ul + g) ^ r)) = a;
+      if (b < bmax) {
+        float* dst = m.ws_actx + ((size_t)(v0 >> 6) * bmax + b) * 64 + (v0 & 63);
+        if (v0 + 3 < V) *reinterpret_cast<f32x4*>(dst) = a;
+        else
+#pragma unroll
+          for (int i = 0; i < 4; ++i) if (v0 + i < V) dst[i] = a[i];
+      }
+    }
+  };
+  if (has0) put_a(wave, acc[0], bias[0]);
+  if (full1) put_a(wave + 16, acc[1], bias[1]);
+  if (helper) {                         // this helper's phases of the split unit
+#pragma unroll
+    for (int b4 = 0; b4 < 4; ++b4)
+      *reinterpret_cast<f32x4*>(sp + ((wave - hw0) * 64 + b4 * 16 + r) * 16 + 4 * g) = acc[1][b4];
+  }
+  lds_barrier();
+  if (summer) {                         // partials summed in helper order (fixed), + bias
+    f32x4 a4[4];
+#pragma unroll
+    for (int b4 = 0; b4 < 4; ++b4) {
+      a4[b4] = *reinterpret_cast<const f32x4*>(sp + (b4 * 16 + r) * 16 + 4 * g);
+      for (int h = 1; h < min(NPH, 3); ++h) {
+        const f32x4 q = *reinterpret_cast<const f32x4*>(sp + (h * 64 + b4 * 16 + r) * 16 + 4 * g);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a4[b4][i] += q[i];
+      }
+    }
+    put_a(nuf, a4, bias[1]);
+  }
+  if (split) lds_barrier();
+  // ---- P^T[h, b] over the workgroup's 16 nu words: k steps v = 16 s + 4 g + i ----
+  f32x4 pacc = z4;
+  if (ht < NJT) {
+    auto part = [&](const f32x4 (&wc)[8], int c) {
+#pragma unroll
+      for (int sx = 0; sx < 8; ++sx) {
+        const int sq = 8 * c + sx;
+        if (sq < nu) {
+          const f32x4 av = *reinterpret_cast<const f32x4*>(al + (bt * 16 + r) * RS_AL + 4 * ((4 * sq + g) ^ r));
+#pragma unroll
+          for (int i = 0; i < 4; ++i) pacc = mfma16x16x4(wc[sx][i], av[i], pacc);
+        }
+      }
+    };
+    for (int c = 0; c < 4; c += 2) {
+      if (8 * c >= nu) break;
+      if (8 * (c + 1) < nu) ldwc(wB, c + 1);
+      part(wA, c);
+      if (8 * (c + 1) >= nu) break;
+      if (8 * (c + 2) < nu) ldwc(wA, c + 2);
+      part(wB, c + 1);
+    }
+    float* hg = m.ws_hpart + (size_t)w * bmax * H0;
+    const int b = bt * 16 + r;
+    if (b < bmax) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int h = ht * 16 + g * 4 + e;
+        if (h < H0) hg[(size_t)b * H0 + h] = pacc[e];
+      }
+    }
+  }
+}
+
 // grid: n_tiles * ctx_kb workgroups of 16 waves (one per CU).
 template <int BM, bool GB = false>
 __global__ void __launch_bounds__(CT) gfk_ctx_bwd_k(GfkArgT<GB> ga) {
@@ -1089,6 +1338,7 @@ extern "C" size_t gfk_ctx_smem(const GfkModel* m) {
   if ((m->stage_flags & CTX_FULL) && (size_t)fwd_full_lds_floats(*m) > a) a = fwd_full_lds_floats(*m);
   if ((m->stage_flags & CTX_BAL) && (size_t)fwd_bal_lds_floats() > a) a = fwd_bal_lds_floats();
   if ((m->stage_flags & CTX_BAL3) && (size_t)fwd_bal3_lds_floats() > a) a = fwd_bal3_lds_floats();
+  if ((m->stage_flags & CTX_RS) && (size_t)fwd_rs_lds_floats() > a) a = fwd_rs_lds_floats();
   if ((m->stage_flags & CTX_BWDPP) && (size_t)pp_lds(*m).total > b) b = pp_lds(*m).total;
   return sizeof(float) * (a > b ? a : b);
 }
@@ -1106,7 +1356,8 @@ extern "C" int gfk_ctx_set_smem(size_t bytes) {
                       (const void*)gfk_ctx_fwd_full_k<false>, (const void*)gfk_ctx_fwd_full_k<true>,
                       (const void*)gfk_ctx_fwd_bal_k<false>, (const void*)gfk_ctx_fwd_bal_k<true>,
                       (const void*)gfk_ctx_bwd_pp_k<false>, (const void*)gfk_ctx_bwd_pp_k<true>,
-                      (const void*)gfk_ctx_fwd_bal3_k<false>, (const void*)gfk_ctx_fwd_bal3_k<true>};
+                      (const void*)gfk_ctx_fwd_bal3_k<false>, (const void*)gfk_ctx_fwd_bal3_k<true>,
+                      (const void*)gfk_ctx_fwd_rs_k<false>, (const void*)gfk_ctx_fwd_rs_k<true>};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return (int)e;
@@ -1126,6 +1377,16 @@ static bool ctx_ok(const GfkModel* m) {
 
 extern "C" int gfk_launch_ctx_fwd(const GfkModel* m, hipStream_t s) {
   if (!ctx_ok(m)) return -9;
+  // register-streamed forward: at most 2 units per wave (32 per workgroup), 32-bit buffer
+  // offsets into Wa and the flat buffer (engine checks), Wa rows 16-byte aligned
+  if ((m->stage_flags & CTX_FULL) && (m->stage_flags & CTX_RS) && m->bmax <= 64 && m->H[0] <= 64 &&
+      m->ctx_parts > 0 && ((m->V + 15) / 16 + m->ctx_parts - 1) / m->ctx_parts <= 32 &&
+      (int64_t)m->V * m->C * 4 < 0x7FFFFFFFLL) {
+    const dim3 g(m->ctx_parts), t(RS_T);
+    const size_t sm = sizeof(float) * fwd_rs_lds_floats();
+    do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_ctx_fwd_rs_k<true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_ctx_fwd_rs_k<false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0);
+    return (int)hipGetLastError();
+  }
   if ((m->stage_flags & CTX_FULL) && (m->stage_flags & CTX_BAL3) && m->bmax <= 64 && m->H[0] <= 63 && m->C > 3 * FD &&
       m->ctx_parts > 0 && m->ctx_parts <= m->n_tiles) {
     const dim3 g(m->ctx_parts), t(FT3);

@@ -66,6 +66,7 @@ STAGE_CTX_BAL = 2048              # bit 11: CombinedTM forward, balanced persist
 STAGE_CTX_BWDPP = 4096            # bit 12: CombinedTM backward, persistent pipelined shape (csrc/ctx.hip)
 STAGE_CTX_BAL3 = 8192             # bit 13: the balanced forward's 16-wave 3-deep variant (csrc/ctx.hip)
 STAGE_WIN_CTXPP = 16384           # bit 14: CombinedTM's contextual W_in half as a persistent kernel
+STAGE_CTX_RS = 32768              # bit 15: CombinedTM forward, Wa register-streamed (csrc/ctx.hip)
 
 
 def _explain(ok: bool, why: str, explain: bool) -> bool:
@@ -566,16 +567,26 @@ class FusedEngine(EngineBase):
             # equal column ranges instead of one workgroup per tile (whose last round runs
             # mostly empty) and leave one contextual z0 partial each; slices staged by DMA.
             # GFEDNTM_CTX_BAL=0 keeps the one-workgroup-per-tile kernel
-            bal = os.environ.get("GFEDNTM_CTX_BAL", "3")
+            bal = os.environ.get("GFEDNTM_CTX_BAL", "4")
             if bal != "0" and int(m.H[0]) <= 64 and m.V * m.C * 4 < (1 << 31):
                 m.stage_flags |= STAGE_CTX_BAL
                 m.ctx_parts = int(min(m.n_tiles, 2 * cu_n))
                 # "3": one 16-wave workgroup per CU, slices three deep (counted waits), the
                 # Wc rows / bias by DMA too; needs C > 192, H0 <= 63 and the flat buffer
                 # under 2 GB (32-bit buffer offsets)
-                if (bal == "3" and int(m.H[0]) <= 63 and m.C > 192
+                if (bal in ("3", "4") and int(m.H[0]) <= 63 and m.C > 192
                         and 4 * self.flat.n_total < (1 << 31)):
                     m.stage_flags |= STAGE_CTX_BAL3
+                    m.ctx_parts = int(min(m.n_tiles, cu_n))
+                # "4" (the default; "3" where it does not apply): Wa streamed from global
+                # memory into registers as the MFMA A operand, x_ctx staged once per
+                # workgroup in 256-float phases (at most 32 16-column units per CU: V <= 131k
+                # on 256 CUs).  V = 99k, interleaved: ctx_fwd 134 -> 122 us, round 0.7386 /
+                # 0.7396 -> 0.7287 / 0.7304 ms (profiles/r4/ab_s8)
+                n_units = -(-int(m.V) // 16)
+                if (bal == "4" and -(-n_units // min(m.n_tiles, cu_n)) <= 32
+                        and 4 * self.flat.n_total < (1 << 31)):
+                    m.stage_flags |= STAGE_CTX_RS
                     m.ctx_parts = int(min(m.n_tiles, cu_n))
         # CombinedTM backward as one persistent workgroup per CU walking equal ranges of the
         # (tile, C chunk) items with the next item's Wa state in flight (csrc/ctx.hip
@@ -888,7 +899,7 @@ class FusedEngine(EngineBase):
         if m.stage_flags & STAGE_CTX_BAL and data.contextual is not None \
                 and 4 * data.contextual.numel() >= (1 << 31):
             # the balanced forward addresses x_ctx with 32-bit buffer offsets
-            m.stage_flags &= ~(STAGE_CTX_BAL | STAGE_CTX_BAL3)
+            m.stage_flags &= ~(STAGE_CTX_BAL | STAGE_CTX_BAL3 | STAGE_CTX_RS)
             m.ctx_parts = 0
         if m.lab_on:
             if data.labels is None or data.labels.shape[1] != m.L:

@@ -373,7 +373,9 @@ def test_ctm_step_matches_oracle(inference_type, Cdim, V, K, model_type):
     e = fused.engine
     assert e.update_mode == UPDATE_FUSED
     if inference_type == "combined":
-        assert e._m.ctx_fused == 1 and (e._m.ctx_kb > 1) == (Cdim > 16)
+        # (C split over the CUs' slots: one chunk of <= 256 at large V, more at small V)
+        assert e._m.ctx_fused == 1 and e._m.ctx_kb * e._m.ctx_ckb >= Cdim
+        assert (e._m.ctx_kb > 1) == (Cdim > 16) or V > 50000
     else:
         assert e._m.ctx_fused == 2           # dense input layer in enc_in / win_update
     e.set_update_mode(UPDATE_GRAD)
@@ -730,15 +732,18 @@ def test_sparse_win_tiles_match_oracle(monkeypatch, model_type, B, n_docs, K, H,
     _oracle_step(model_type, B, n_docs, K, H, V)
 
 
-@pytest.mark.parametrize("bal", ["3", "1", "0"])
-@pytest.mark.parametrize("Cdim,V", [(96, 600), (768, 9000), (100, 5000), (260, 3000), (768, 40000)])
+@pytest.mark.parametrize("bal", ["4", "3", "1", "0"])
+@pytest.mark.parametrize("Cdim,V", [(96, 600), (768, 9000), (100, 5000), (260, 3000), (768, 40000),
+                                    (96, 69600), (260, 69600)])
 def test_ctm_full_tile_forward_matches_oracle(monkeypatch, Cdim, V, bal):
     """ctx_fwd with all batch rows per vocab tile (stage_flags bit 5, the large-V shape;
     GFEDNTM_CTX_FULL=1 forces it at small V): the balanced persistent kernel (bit 11,
     DMA-staged slices, column ranges of 16-column units not aligned to the 64-column
     tiles, a partial last C slice at C = 96 / 100 / 260), its 16-wave 3-deep variant (bal = 3,
-    C > 192: the counted slice waits across chunk boundaries) or one workgroup per tile
-    (bal = 0)."""
+    C > 192: the counted slice waits across chunk boundaries), the register-streamed
+    kernel (bal = 4: a partial last 256-float phase at C = 96 / 100 / 260; V = 69.6k: 17
+    units in some workgroups, the last split over the helper waves' phases, one or two
+    phases) or one workgroup per tile (bal = 0)."""
     monkeypatch.setenv("GFEDNTM_CTX_FULL", "1")
     monkeypatch.setenv("GFEDNTM_CTX_BAL", bal)
     test_ctm_step_matches_oracle("combined", Cdim, V, 20, "prodLDA")

@@ -128,16 +128,21 @@ def test_large_v_fused_matches_gradient_mode(monkeypatch, B, K, V, win):
     _assert_beta_padding_zero(b)
 
 
-def test_ctm_large_v_fused_matches_gradient_mode():
+@pytest.mark.parametrize("bal,V", [("3", 74000), ("4", 74000), ("4", 69600)])
+def test_ctm_large_v_fused_matches_gradient_mode(monkeypatch, bal, V):
     """CombinedTM K = 100, C = 768, V = 74k (the BASELINE CTM class): ctx_fwd full tiles,
-    Adam in ctx_bwd (adapt_bert) and win_update (both input-layer halves) vs gradient mode."""
+    Adam in ctx_bwd (adapt_bert) and win_update (both input-layer halves) vs gradient mode;
+    bal = 4: the register-streamed forward (18-19 units per workgroup on 256 CUs: waves with
+    two; V = 69.6k: 16-17, the 17th unit split by phase over three helper waves)."""
     from gfedntm_amd.models import CombinedTM
-    from gfedntm_amd.ops.engine import STAGE_CTX_FULL
-    V, K, Cdim, B = 74000, 100, 768, 64
+    from gfedntm_amd.ops.engine import STAGE_CTX_FULL, STAGE_CTX_RS
+    monkeypatch.setenv("GFEDNTM_CTX_BAL", bal)
+    K, Cdim, B = 100, 768, 64
     kw = dict(input_size=V, contextual_size=Cdim, n_components=K, hidden_sizes=(50, 50),
               batch_size=B, verbose=False, device="cuda")
     a, b = _twins(CombinedTM, kw)
     assert a.engine._m.ctx_fused == 1 and a.engine._m.stage_flags & STAGE_CTX_FULL
+    assert bool(a.engine._m.stage_flags & STAGE_CTX_RS) == (bal == "4")
     n_docs = 2 * B + 5
     X = random_csr(n_docs, V, 60, seed=3)
     ctx = np.random.default_rng(4).standard_normal((n_docs, Cdim)).astype(np.float32)
