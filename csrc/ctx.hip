@@ -734,9 +734,9 @@ __global__ void __launch_bounds__(FT3) gfk_ctx_fwd_bal3_k(GfkArgT<GB> ga) {
 // MFMA A operand straight from global memory into registers:
 //  * lane (r, g) loads Wa[v = 16 unit + r][16 j + 4 g .. + 3] as ONE 128-bit buffer load per
 //    16-float block j, consumed by 4 k steps x 4 batch-row tiles (16 MFMAs);
-//  * a ring of RS_R = 8 blocks per wave (32 VGPRs) is refilled right after each block is
+//  * a ring of RS_R = 4 blocks per wave (16 VGPRs) is refilled right after each block is
 //    read, with the next block of this unit or the first ones of the wave's next (phase,
-//    unit) segment: 8 blocks x 4 waves per SIMD of MFMA work to arrive (~7 us), 256 KB per CU;
+//    unit) segment: 4 blocks x 4 waves per SIMD of MFMA work to arrive (~4 us), 64 KB per CU;
 //  * x_ctx, the batch's 64 rows, is the B operand from LDS in phases of 256 k (64 KB, two
 //    buffers: phase p + 1 arrives by LDS-DMA while phase p is multiplied; quads XOR-swizzled
 //    by (row & 15), so a ds_read_b128 of 16 rows x 4 quads hits every bank once); each phase
@@ -752,7 +752,17 @@ __global__ void __launch_bounds__(FT3) gfk_ctx_fwd_bal3_k(GfkArgT<GB> ga) {
 // Wc from global in chunks of 8 k steps, the next chunk in flight): ONE z0 partial per
 // workgroup in ws_hpart (ctx_parts = the grid), as the balanced kernels leave it.
 constexpr int CTX_RS = 32768;
-constexpr int RS_T = 1024, RS_KP = 256, RS_R = 8, RS_AL = 512;
+// GFK_RS_RING: ring blocks per wave.  Interleaved at V = 99k (profiles/r4/ab_s9): 4 blocks
+// 121.4 us, 8 blocks 124.9 us; 4 + the next block's x operands read before this block's
+// MFMAs 121.1 us (not kept) -- the ring's depth and the LDS reads are not the limit: the
+// busiest SIMD's MFMAs (main + P) are ~75 % of the kernel's cycles
+#ifndef GFK_RS_RING
+#define GFK_RS_RING 4
+#endif
+#define GFK_STR2(x) #x
+#define GFK_STR(x) GFK_STR2(x)
+constexpr int RS_T = 1024, RS_KP = 256, RS_R = GFK_RS_RING, RS_AL = 512;
+static_assert((RS_KP / 16) % RS_R == 0, "a segment's blocks cycle the ring whole");
 // x phases / A [64][RS_AL] (the same 128 KB), + 3 split-unit partials [64][16]
 __host__ __device__ inline int fwd_rs_lds_floats() { return 2 * 64 * RS_KP + 3 * 64 * 16; }
 template <bool GB = false>
@@ -840,7 +850,7 @@ __global__ void __launch_bounds__(RS_T) gfk_ctx_fwd_rs_k(GfkArgT<GB> ga) {
   for (int p = 0; p < NPH; ++p) {
     // phase p's x: issued before every ring load still in flight (RS_R of them, issued
     // after it by any wave with a segment since; a wave without one may have issued none)
-    if (has0 || helper) asm volatile("s_waitcnt vmcnt(8)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (has0 || helper) asm volatile("s_waitcnt vmcnt(" GFK_STR(GFK_RS_RING) ")\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     else vm_barrier();
     // (4 j + g) ^ r = 16 (j >> 2) + 4 ((j & 3) ^ (r >> 2)) + (g ^ (r & 3)): four lane
     // offsets, the rest immediates
