@@ -335,9 +335,24 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkArgT<GB> ga
 // instead of 12, and 7004 strips over 4096 waves (at most 2 each; 76 -> 85 % of the last
 // round's slots busy) instead of 3072 (at most 3).
 __host__ __device__ constexpr int strip_threads(int pf, int np) { return pf == 1 ? 512 : pf == 2 && np > 13 ? 768 : 1024; }
-__host__ __device__ constexpr int strip_ring(int pf, int np) { return pf == 3 && np > 13 ? 13 : np; }
-template <int BM, int NP, int PF, bool GB = false>
+// The ring must divide NP: the next strip's pair p is written into the slot of pair
+// p + NP - R of this one, and read back from slot p % R.  (A 13-pair ring with NP = 25
+// -- K = 200 until round 4 -- shifted every later strip's beta pairs by one slot: wrong
+// logits wherever a wave had a second strip, i.e. more than 4096 strips, V > 65k.)
+__host__ __device__ constexpr int strip_ring(int pf, int np) {
+  if (pf != 3 || np <= 13) return np;
+  int d = 13;
+  while (np % d) --d;
+  return d;
+}
+// BF (mm_bf16, PF = 3 only): the logits on v_mfma_f32_16x16x32_bf16 -- pairs t = 4 s + u hold
+// k = 32 s + 8 g + 2 u (+ 1) for lane group g, so the 4 pairs of step s are the 8 consecutive
+// k of the lane's B operand (B[8 g + j][col]); A = 8 consecutive k of theta_d's row from LDS
+// (two ds_read_b128); both rounded to bf16 in registers, fp32 accumulation.  16x fewer MFMA
+// cycles than the fp32 path, which is what bounds it at K = 200 (not the beta stream).
+template <int BM, int NP, int PF, bool GB = false, bool BF = false>
 __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kernel(GfkArgT<GB> ga) {
+  static_assert(!BF || (PF == 3 && NP % 4 == 0), "bf16 strips: ring variant, whole 32-k steps");
   const GfkModel& m = gfk_model(ga);
   constexpr int STRIP_THREADS = strip_threads(PF, NP);
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -365,10 +380,13 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
   const int nb = *m.ws_nb;
   if (blockIdx.x == 0 && tid == 0) *m.nbt_beta += 1;
   const int g2 = 2 * (lane >> 4);
+  const int gb = BF ? 8 * (lane >> 4) : g2;    // the lane group's first beta row
+  // first beta row of pair t (relative to gb)
+  auto prow = [](int t) constexpr { return BF ? 32 * (t >> 2) + 2 * (t & 3) : 8 * t; };
   const float inv_nb = 1.f / (float)nb;
   const int nstrips = m.n_tiles * 4;
   const int stride = gridDim.x * NW;
-  const int arow = (lane & 15) * KS + g2;
+  const int arow = (lane & 15) * KS + (BF ? gb : g2);
   // beta [K, V] as a buffer resource of K V floats (K V < 2^29 checked by the launcher)
   const __amdgpu_buffer_rsrc_t bres =
       __builtin_amdgcn_make_buffer_rsrc((void*)m.beta, 0, K * LDB * 4, 0x00020000);
@@ -382,13 +400,12 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
     const int vc = min((st >> 2) * VB + 16 * (st & 3) + (lane & 15), V - 1);
     int v4 = LDB * 4;
     asm volatile("" : "+s"(v4));
-    int voff = g2 * v4 + vc * 4;
-    const int v32 = 8 * v4;
+    int voff = gb * v4 + vc * 4;
 #pragma unroll
     for (int t = 0; t < NL; ++t) {
       bb[2 * t] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bres, voff, 0, 0));
       bb[2 * t + 1] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bres, voff, v4, 0));
-      voff += v32;
+      if (t + 1 < NL) voff += (prow(t + 1) - prow(t)) * v4;
     }
     rm = m.beta_rm[vc];
     rv = m.beta_rv[vc];
@@ -398,6 +415,7 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
   // PF = false: no prefetch, 16 waves per CU at <= 128 VGPRs (the waves overlap each
   // other's loads instead)
   constexpr int NR = strip_ring(PF, NP);       // pairs held in registers
+  static_assert(NP % NR == 0, "the ring's slots must repeat whole strips");
   float b[2 * NR], bn[2 * (PF == 1 ? NP : 1)], rm0 = 0.f, rv0 = 0.f, rmn = 0.f, rvn = 0.f;
   // wave group gq = wave >> 2 takes whole tiles gq * grid + g, + NW / 4 * grid, ...: the
   // 4 strips of a tile stay on one CU (their beta rows share cache lines), and the
@@ -440,7 +458,7 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
   if (PF == 3) {
     const int s0 = min(s, nstrips - 1);
     const int vc0 = min((s0 >> 2) * VB + 16 * (s0 & 3) + (lane & 15), V - 1);
-    voffc = g2 * (LDB * 4) + vc0 * 4;
+    voffc = gb * (LDB * 4) + vc0 * 4;
   }
 #pragma unroll 1
   for (; s < nstrips; s += stride) {
@@ -452,7 +470,7 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
       const int sn = min(s + stride, nstrips - 1);
       const int vcn = min((sn >> 2) * VB + 16 * (sn & 3) + (lane & 15), V - 1);
       asm volatile("" : "+s"(v4n));
-      voffn = g2 * v4n + vcn * 4;
+      voffn = gb * v4n + vcn * 4;
       rmn = m.beta_rm[vcn];
       rvn = m.beta_rv[vcn];
     } else {
@@ -473,6 +491,32 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
     // zero in both operands)
     // A reads one pair ahead of the MFMAs (double-buffered registers); the fences keep
     // the scheduler from hoisting every pair's reads above the first MFMA (spills)
+    if constexpr (BF) {
+#pragma unroll
+      for (int st = 0; st < NP / 4; ++st) {
+        __builtin_amdgcn_sched_barrier(0);
+        float b8[8];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          b8[2 * u] = b[2 * ((4 * st + u) % NR)];
+          b8[2 * u + 1] = b[2 * ((4 * st + u) % NR) + 1];
+        }
+#pragma unroll
+        for (int i = 0; i < RT; ++i) {
+          const f32x4 lo = *reinterpret_cast<const f32x4*>(ap + i * 16 * KS + 32 * st);
+          const f32x4 hi = *reinterpret_cast<const f32x4*>(ap + i * 16 * KS + 32 * st + 4);
+          const float a8[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          acc[i] = mfma16x16x32bf(a8, b8, acc[i]);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {       // pair t + NR (this strip's, else the next one's)
+          const int t = 4 * st + u, pn = t + NR;
+          const int vo = pn < NP ? voffc + prow(pn) * v4n : voffn + prow(pn - NP) * v4n;
+          b[2 * (t % NR)] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bres, vo, 0, 0));
+          b[2 * (t % NR) + 1] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bres, vo, v4n, 0));
+        }
+      }
+    } else {
     float2 a[2][RT];
 #pragma unroll
     for (int i = 0; i < RT; ++i) a[0][i] = *reinterpret_cast<const float2*>(ap + i * 16 * KS);
@@ -498,6 +542,7 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
         b[2 * (t % NR)] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bres, vo, 0, 0));
         b[2 * (t % NR) + 1] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bres, vo, v4n, 0));
       }
+    }
     }
     if (PF == 3) voffc = voffn;
     // ---- column batch-norm over the wave's own rows (rows >= nb excluded) ----
@@ -1559,12 +1604,18 @@ __host__ __device__ inline int strip_pairs(int K) { return (K + 7) / 8; }
 // the kernel instance (k pairs in registers) for K
 __host__ __device__ inline int strip_np(int K) {
   const int np = strip_pairs(K);
-  return np <= 8 ? 8 : np <= 13 ? 13 : np <= 16 ? 16 : np <= 25 ? 25 : 32;
+  // (26 = 2 x 13: the ring of 13 pairs divides it; K <= 208)
+  return np <= 8 ? 8 : np <= 13 ? 13 : np <= 16 ? 16 : np <= 26 ? 26 : 32;
 }
 
+// the bf16 strip instance: whole 32-k steps (NP a multiple of 4, ring of 8 pairs)
+__host__ __device__ inline int strip_np_bf(int K) { return K <= 64 ? 8 : K <= 128 ? 16 : 32; }
+
 extern "C" size_t gfk_prodlda_fwd_smem(const GfkModel* m) {
-  if (m->stage_flags & FWD_STRIP)
-    return sizeof(float) * ((size_t)m->bmax * (8 * strip_np(m->K) + 4) + (size_t)(1024 / 64) * m->bmax);
+  if (m->stage_flags & FWD_STRIP) {
+    const int np = m->mm_bf16 ? strip_np_bf(m->K) : strip_np(m->K);
+    return sizeof(float) * ((size_t)m->bmax * (8 * np + 4) + (size_t)(1024 / 64) * m->bmax);
+  }
   const size_t KP = round_up(m->K, m->mm_bf16 ? 16 : 4);
   return sizeof(float) * ((size_t)m->bmax * m->kt + KP * LDB_F + 8 * VB);
 }
@@ -1596,8 +1647,23 @@ extern "C" int gfk_launch_prodlda_fwd(const GfkModel* m, hipStream_t s) {
   if (m->stage_flags & FWD_STRIP) {
     // fp32, B <= 64, K <= 256; the partial slots need 4 * grid <= 4 * n_tiles
     const int np = strip_np(m->K);
-    if (m->mm_bf16 || m->bmax > 64 || m->K > 256 || m->dec_grid > m->n_tiles ||
+    if (m->bmax > 64 || m->K > 256 || m->dec_grid > m->n_tiles ||
         (int64_t)m->K * m->ldb >= (1LL << 29)) return -1;
+    if (m->mm_bf16) {                   // bf16: the ring variant only
+      if (!(m->stage_flags & FWD_STRIP_RING)) return -1;
+      const int nb = strip_np_bf(m->K);
+#define GFK_FWSB(BM, NP)                                                                       \
+      do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 3, true, true>), gfk_grid(g, m), dim3(strip_threads(3, NP)), sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 3, false, true>), g, dim3(strip_threads(3, NP)), sm, s, GfkArgT<false>{*m}); } while (0)
+#define GFK_FWSB_B(BM) if (nb == 8) GFK_FWSB(BM, 8); else if (nb == 16) GFK_FWSB(BM, 16); else GFK_FWSB(BM, 32)
+      switch (m->bmax) {
+        case 16: GFK_FWSB_B(16); break;
+        case 32: GFK_FWSB_B(32); break;
+        default: GFK_FWSB_B(64); break;
+      }
+#undef GFK_FWSB_B
+#undef GFK_FWSB
+      return (int)hipGetLastError();
+    }
 #define GFK_FWS(BM, NP)                                                                        \
     do {                                                                                       \
       if (m->stage_flags & FWD_STRIP_RING)                                                     \
@@ -1613,7 +1679,7 @@ extern "C" int gfk_launch_prodlda_fwd(const GfkModel* m, hipStream_t s) {
     if (np == 8) GFK_FWS(BM, 8);                                           \
     else if (np == 13) GFK_FWS(BM, 13);                                    \
     else if (np == 16) GFK_FWS(BM, 16);                                    \
-    else if (np == 25) GFK_FWS(BM, 25);                                    \
+    else if (np == 26) GFK_FWS(BM, 26);                                    \
     else GFK_FWS(BM, 32)
     switch (m->bmax) {
       case 16: GFK_FWS_B(16); break;
@@ -1736,10 +1802,14 @@ extern "C" int gfk_prodlda_set_smem(size_t bytes) {
                       (const void*)prodlda_fwd_kernel<64, true>, (const void*)prodlda_fwd_kernel<64, true, true>, (const void*)prodlda_fwd_kernel<128, true>, (const void*)prodlda_fwd_kernel<128, true, true>,
 #define GFK_FWS_PTRS1(BM, F) (const void*)prodlda_fwd_strip_kernel<BM, 8, F>, (const void*)prodlda_fwd_strip_kernel<BM, 8, F, true>, \
     (const void*)prodlda_fwd_strip_kernel<BM, 13, F>, (const void*)prodlda_fwd_strip_kernel<BM, 13, F, true>, (const void*)prodlda_fwd_strip_kernel<BM, 16, F>, (const void*)prodlda_fwd_strip_kernel<BM, 16, F, true>, \
-    (const void*)prodlda_fwd_strip_kernel<BM, 25, F>, (const void*)prodlda_fwd_strip_kernel<BM, 25, F, true>, (const void*)prodlda_fwd_strip_kernel<BM, 32, F>, (const void*)prodlda_fwd_strip_kernel<BM, 32, F, true>
-#define GFK_FWS_PTRS(BM) GFK_FWS_PTRS1(BM, 0), GFK_FWS_PTRS1(BM, 1), GFK_FWS_PTRS1(BM, 2), GFK_FWS_PTRS1(BM, 3)
+    (const void*)prodlda_fwd_strip_kernel<BM, 26, F>, (const void*)prodlda_fwd_strip_kernel<BM, 26, F, true>, (const void*)prodlda_fwd_strip_kernel<BM, 32, F>, (const void*)prodlda_fwd_strip_kernel<BM, 32, F, true>
+#define GFK_FWS_PTRSB(BM) (const void*)prodlda_fwd_strip_kernel<BM, 8, 3, false, true>, (const void*)prodlda_fwd_strip_kernel<BM, 8, 3, true, true>, \
+    (const void*)prodlda_fwd_strip_kernel<BM, 16, 3, false, true>, (const void*)prodlda_fwd_strip_kernel<BM, 16, 3, true, true>, \
+    (const void*)prodlda_fwd_strip_kernel<BM, 32, 3, false, true>, (const void*)prodlda_fwd_strip_kernel<BM, 32, 3, true, true>
+#define GFK_FWS_PTRS(BM) GFK_FWS_PTRS1(BM, 0), GFK_FWS_PTRS1(BM, 1), GFK_FWS_PTRS1(BM, 2), GFK_FWS_PTRS1(BM, 3), GFK_FWS_PTRSB(BM)
                       GFK_FWS_PTRS(16), GFK_FWS_PTRS(32), GFK_FWS_PTRS(64),
 #undef GFK_FWS_PTRS
+#undef GFK_FWS_PTRSB
 #undef GFK_FWS_PTRS1
 #define GFK_BWD_PTRS2(U, T, F) (const void*)prodlda_bwd_kernel<16, U, T, F>, (const void*)prodlda_bwd_kernel<16, U, T, F, true>, \
     (const void*)prodlda_bwd_kernel<32, U, T, F>, (const void*)prodlda_bwd_kernel<32, U, T, F, true>, (const void*)prodlda_bwd_kernel<64, U, T, F>, (const void*)prodlda_bwd_kernel<64, U, T, F, true>, \

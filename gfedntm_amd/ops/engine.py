@@ -491,7 +491,8 @@ class FusedEngine(EngineBase):
             # vs 0.0589 ms, K=50 V=28k 0.092 vs 0.101, K=200 V=112k 0.342 vs 0.349, CTM /
             # ZeroShotTM K=100 neutral.  GFEDNTM_FWD_STRIP=0 selects the tile kernel
             strip = os.environ.get("GFEDNTM_FWD_STRIP", "auto")
-            fits = (not m.mm_bf16 and m.bmax <= 64 and m.K <= 256 and m.K * m.ldb < (1 << 29))
+            # (bf16 GEMMs: the ring variant with v_mfma_f32_16x16x32_bf16, 32-k steps)
+            fits = (m.bmax <= 64 and m.K <= 256 and m.K * m.ldb < (1 << 29))
             if fits and strip in ("1", "auto"):
                 m.stage_flags |= STAGE_FWD_STRIP
                 # the 8-wave variant that prefetches the next strip's beta block (2 waves
@@ -504,7 +505,7 @@ class FusedEngine(EngineBase):
                 # 3, the default since g26: the same rolling prefetch through a 13-pair ring
                 # (K > 104: 128 VGPRs, 16 waves per CU instead of 12; K = 200 V = 112k forward
                 # 39.7 -> 36.5 us, round 0.2794 -> 0.2751 ms; identical code for K <= 104)
-                pf = os.environ.get("GFEDNTM_FWD_STRIP_PF", "3")
+                pf = "3" if m.mm_bf16 else os.environ.get("GFEDNTM_FWD_STRIP_PF", "3")
                 if pf == "1":
                     m.stage_flags |= STAGE_FWD_STRIP_PF
                 elif pf == "2":

@@ -84,7 +84,13 @@ def test_step_matches_oracle(model_type, B, n_docs, K, H, V):
                                             (32, 45, 25, (30, 20), 7000),     # odd K, B = 32
                                             (16, 30, 20, (32, 24), 700),      # B = 16, K % 8 = 4
                                             (32, 60, 250, (50,), 5000),       # K = 250 (NP = 32)
-                                            (64, 150, 256, (50,), 5000)])     # K = 256, B = 64: forced k split
+                                            (64, 150, 256, (50,), 5000),      # K = 256, B = 64: forced k split
+                                            # more strips than waves (V > 65k on 256 CUs): a
+                                            # wave's second strip reads its first pairs from
+                                            # the ring slots the previous strip refilled
+                                            (64, 80, 200, (50, 50), 80000),   # NP = 26, ring 13
+                                            (64, 80, 120, (50,), 80000),      # NP = 16, ring 8
+                                            (64, 80, 250, (50,), 80000)])     # NP = 32, ring 8
 @pytest.mark.parametrize("pf", ["2", "3"])
 def test_strip_forward_matches_oracle(monkeypatch, pf, B, n_docs, K, H, V):
     """prodlda_fwd_strip_kernel (GFEDNTM_FWD_STRIP=1 forces it): per-wave column strips,
@@ -523,17 +529,20 @@ def _bf(x):
     return x.to(torch.bfloat16).float()
 
 
-@pytest.mark.parametrize("K,V", [(50, 2000), (200, 40000)])
+@pytest.mark.parametrize("K,V", [(50, 2000), (200, 40000), (120, 9000), (200, 80000)])
 def test_bf16_decoder_matches_emulated_oracle(K, V):
     """matmul_dtype='bf16': theta_d.beta, theta_d^T.dlogit and dlogit.beta^T take bf16
     operands on the matrix cores with fp32 accumulation.  Oracle: the fp32 PyTorch step
     with theta_d and beta rounded to bf16 before the logits GEMM (the backward GEMMs'
-    extra rounding of dlogit is inside the gradient tolerance)."""
+    extra rounding of dlogit is inside the gradient tolerance).  The forward is the bf16
+    strip kernel (32-k steps: 8, 16 or 32 pairs, a ring of 8); V = 80k: waves with a
+    second strip (the ring's cross-strip slots)."""
     from gfedntm_amd.models.functional import encoder_forward
     from gfedntm_amd.models.networks import kl_terms, reconstruction_terms
     import torch.nn.functional as F
+    from gfedntm_amd.ops.engine import STAGE_FWD_STRIP
     fused, ref = _pair("prodLDA", V=V, K=K, H=(50, 50), B=64, matmul_dtype="bf16")
-    assert fused.engine._m.mm_bf16 == 1
+    assert fused.engine._m.mm_bf16 == 1 and fused.engine._m.stage_flags & STAGE_FWD_STRIP
     X = random_csr(150, V, 60, seed=1)
     data, plan = _bind(fused, X, B=64)
     e = fused.engine
