@@ -74,7 +74,8 @@ def _grads_of(tm_fused):
                                             (64, 80, 50, (50, 50), 40000),       # persistent decoder
                                             (64, 80, 200, (50, 50), 40000),      # persistent, 4 k ranges
                                             (64, 80, 20, (32, 24), 40000),       # persistent, one k range
-                                            (128, 200, 100, (50, 50), 70000)])   # k ranges of 2 tiles, B=128
+                                            (128, 200, 100, (50, 50), 70000),    # k ranges of 2 tiles, B=128
+                                            (64, 80, 200, (50, 50), 112000)])    # the BASELINE K=200 class
 def test_step_matches_oracle(model_type, B, n_docs, K, H, V):
     _oracle_step(model_type, B, n_docs, K, H, V)
 
@@ -756,6 +757,12 @@ def test_ctm_full_tile_forward_matches_oracle(monkeypatch, Cdim, V, bal):
     monkeypatch.setenv("GFEDNTM_CTX_FULL", "1")
     monkeypatch.setenv("GFEDNTM_CTX_BAL", bal)
     test_ctm_step_matches_oracle("combined", Cdim, V, 20, "prodLDA")
+
+
+def test_ctm_v99k_step_matches_oracle():
+    """The BASELINE CombinedTM class on its default kernels (C = 768: three 256-float x
+    phases; V = 99k: 24-25 units per workgroup, the 25th split by phase) vs the oracle."""
+    test_ctm_step_matches_oracle("combined", 768, 99000, 100, "prodLDA")
 
 
 @pytest.mark.parametrize("ctxpp", ["1", "0"])
