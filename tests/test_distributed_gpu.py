@@ -51,7 +51,27 @@ def _params():
     return p
 
 
-def _worker(rank, world, port, tmp, stall, spin, q, poll=None, rounds=ROUNDS, epochs=2):
+LARGE_SIZES = (260, 220, 180)
+
+
+def _corpora_large():
+    """K = 200 class at large V: a 150k-word generator vocabulary, ~70k words in the union
+    (more strips than waves, the persistent pipelined backward, in-place xGMI parts)."""
+    from gfedntm_amd.data.synthetic import generate_synthetic
+    from gfedntm_amd.federation.data import ClientCorpus
+    sc = generate_synthetic(vocab_size=150000, n_topics=200, n_docs=max(LARGE_SIZES),
+                            n_nodes=len(LARGE_SIZES), frozen_topics=5, nwords=(150, 250), seed=7)
+    return [ClientCorpus(texts=sc.texts(i)[:n]) for i, n in enumerate(LARGE_SIZES)]
+
+
+def _params_large():
+    from gfedntm_amd.utils.config import load_config
+    p = dict(load_config().training_params)
+    p.update(num_epochs=1, batch_size=64, hidden_sizes=(50, 50), n_components=200)
+    return p
+
+
+def _worker(rank, world, port, tmp, stall, spin, q, poll=None, rounds=ROUNDS, epochs=2, large=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     if spin is not None:
         os.environ["GFEDNTM_XGMI_SPIN"] = str(spin)
@@ -67,8 +87,9 @@ def _worker(rank, world, port, tmp, stall, spin, q, poll=None, rounds=ROUNDS, ep
                 time.sleep(stall)
 
         try:
-            params = dict(_params(), num_epochs=epochs)
-            out = run_distributed(_corpora()[rank], params, max_iters=rounds, backend="fused",
+            params = dict(_params_large() if large else _params(), num_epochs=epochs)
+            corpus = (_corpora_large() if large else _corpora())[rank]
+            out = run_distributed(corpus, params, max_iters=rounds, backend="fused",
                                   seed=5, save_client=os.path.join(tmp, "client"),
                                   stamp="20240101", rehearse_1gpu=True, round_hook=hook)
         except CommError as e:
@@ -120,6 +141,28 @@ def test_run_distributed_xgmi_matches_local_golden(tmp_path):
         np.testing.assert_array_equal(shared, gold)
     for i in range(1, len(SIZES) + 1):
         assert os.path.exists(tmp_path / f"client{i}" / f"model_{i}_20240101.npz")
+
+
+def test_run_distributed_large_v_matches_local_golden(tmp_path):
+    """K = 200 at V ~ 70k over 3 ranks: the production large-state path (in-place xGMI
+    parts, beta's share overlapped with the encoder backward, the pipelined backward,
+    multi-strip forward) leaves the shared state bit-identical to LocalFederation."""
+    rounds = 6
+    res = _run(tmp_path, stall=0.0, rounds=rounds, epochs=1, large=True)
+    for r in res:
+        assert r[1] not in ("exception", "comm_error"), r
+    from gfedntm_amd.federation.runner import LocalFederation
+    fed = LocalFederation(_corpora_large(), _params_large(), max_iters=rounds, device="cuda",
+                          backend="fused", seed=5, round_batched=False)
+    fed.run()
+    gold = fed.clients[0].shared.detach().cpu().numpy()
+    e = fed.clients[0].tm.engine
+    assert e._m.bwd_pre == 3 and e._m.n_tiles * 4 > 4096
+    assert 4 * gold.size > (8 << 20)              # above the in-place threshold
+    for rank, used, shared, err, saved, epoch in res:
+        assert used.startswith("xgmi"), used
+        assert err == 0
+        np.testing.assert_array_equal(shared, gold)
 
 
 def test_run_distributed_fails_loudly_on_a_timed_out_wait(tmp_path):
