@@ -1604,8 +1604,10 @@ __host__ __device__ inline int strip_pairs(int K) { return (K + 7) / 8; }
 // the kernel instance (k pairs in registers) for K
 __host__ __device__ inline int strip_np(int K) {
   const int np = strip_pairs(K);
-  // (26 = 2 x 13: the ring of 13 pairs divides it; K <= 208)
-  return np <= 8 ? 8 : np <= 13 ? 13 : np <= 16 ? 16 : np <= 26 ? 26 : 32;
+  // (the ring divides NP: 25 pairs (K <= 200) with a ring of 5, 26 = 2 x 13 with 13.
+  // K = 200, V = 112k interleaved (profiles/r4/ab_s15): 25 / ring 5 forward 34.9 us, round
+  // 0.2625 / 0.2625 ms; 26 / ring 13 (one zero pair) 37.2 us, 0.2647 / 0.2635 ms)
+  return np <= 8 ? 8 : np <= 13 ? 13 : np <= 16 ? 16 : np <= 25 ? 25 : np <= 26 ? 26 : 32;
 }
 
 // the bf16 strip instance: whole 32-k steps (NP a multiple of 4, ring of 8 pairs)
@@ -1679,6 +1681,7 @@ extern "C" int gfk_launch_prodlda_fwd(const GfkModel* m, hipStream_t s) {
     if (np == 8) GFK_FWS(BM, 8);                                           \
     else if (np == 13) GFK_FWS(BM, 13);                                    \
     else if (np == 16) GFK_FWS(BM, 16);                                    \
+    else if (np == 25) GFK_FWS(BM, 25);                                    \
     else if (np == 26) GFK_FWS(BM, 26);                                    \
     else GFK_FWS(BM, 32)
     switch (m->bmax) {
@@ -1802,6 +1805,7 @@ extern "C" int gfk_prodlda_set_smem(size_t bytes) {
                       (const void*)prodlda_fwd_kernel<64, true>, (const void*)prodlda_fwd_kernel<64, true, true>, (const void*)prodlda_fwd_kernel<128, true>, (const void*)prodlda_fwd_kernel<128, true, true>,
 #define GFK_FWS_PTRS1(BM, F) (const void*)prodlda_fwd_strip_kernel<BM, 8, F>, (const void*)prodlda_fwd_strip_kernel<BM, 8, F, true>, \
     (const void*)prodlda_fwd_strip_kernel<BM, 13, F>, (const void*)prodlda_fwd_strip_kernel<BM, 13, F, true>, (const void*)prodlda_fwd_strip_kernel<BM, 16, F>, (const void*)prodlda_fwd_strip_kernel<BM, 16, F, true>, \
+    (const void*)prodlda_fwd_strip_kernel<BM, 25, F>, (const void*)prodlda_fwd_strip_kernel<BM, 25, F, true>, \
     (const void*)prodlda_fwd_strip_kernel<BM, 26, F>, (const void*)prodlda_fwd_strip_kernel<BM, 26, F, true>, (const void*)prodlda_fwd_strip_kernel<BM, 32, F>, (const void*)prodlda_fwd_strip_kernel<BM, 32, F, true>
 #define GFK_FWS_PTRSB(BM) (const void*)prodlda_fwd_strip_kernel<BM, 8, 3, false, true>, (const void*)prodlda_fwd_strip_kernel<BM, 8, 3, true, true>, \
     (const void*)prodlda_fwd_strip_kernel<BM, 16, 3, false, true>, (const void*)prodlda_fwd_strip_kernel<BM, 16, 3, true, true>, \

@@ -115,15 +115,13 @@ class MultiClientRound:
         self.fused = all(c.fused for c in clients) and device.type == "cuda"
         n = self.shared[0].numel()
         # the shared state's parts: beta (final after the decoder backward in the fused
-        # update mode) and the rest, each with its own collective
+        # update mode), CombinedTM's adapt_bert (after ctx_bwd) and the rest, each with its
+        # own collective (FusedEngine.fedavg_parts)
         self.parts: Dict[str, tuple] = {"rest": (0, n)}
         from ..ops.engine import UPDATE_FUSED
-        flat = clients[0].tm.flat
         if (self.fused and world > 1 and on_gpu_plane
-                and all(e.update_mode == UPDATE_FUSED for e in engines)
-                and flat.shared_keys and flat.shared_keys[-1] == "beta" and len(flat.shared_keys) > 1):
-            b0 = flat.slots["beta"].offset
-            self.parts = {"rest": (0, b0), "beta": (b0, n)}
+                and all(e.update_mode == UPDATE_FUSED for e in engines)):
+            self.parts = dict(engines[0].fedavg_parts())
         self.colls: Dict[str, CollectiveAggregator] = {}
         self.attach = None
         if world > 1:
@@ -139,7 +137,7 @@ class MultiClientRound:
                                        for k, c in self.colls.items()},
                            "tuning": {k: c.tuning for k, c in self.colls.items() if c.tuning}}
         self.coll_in_graph = bool(self.colls) and all(c.xgmi is not None for c in self.colls.values())
-        if not self.coll_in_graph and "beta" in self.parts:
+        if not self.coll_in_graph and len(self.parts) > 1:
             # one RCCL all-reduce of the whole state after the round graph
             for c in self.colls.values():
                 if c.xgmi is not None:
@@ -150,7 +148,7 @@ class MultiClientRound:
             coll.prepare(self.shared[0])
             self.colls = {"rest": coll}
         self.method = (None if world == 1 else
-                       "xgmi" + ("+overlap" if "beta" in self.parts else "")
+                       "xgmi" + ("+overlap" if len(self.parts) > 1 else "")
                        if self.coll_in_graph else self.colls["rest"].active)
         self.graph = (graph and self.fused and not any(e.host_gemm_fallback for e in engines))
         if self.graph:
@@ -183,13 +181,16 @@ class MultiClientRound:
         self.colls[part].allreduce_(self.shared[0][a:b])
         self._fold(part, LOCAL_BCAST)
 
-    def _fork_beta(self):
+    def _fork(self, part: str):
+        """``part``'s fold + all-reduce + broadcast on the side stream, from this point of
+        the main stream (the side stream runs the forked parts in order)."""
         main = torch.cuda.current_stream(self.device)
-        side, ev_fork, ev_join = self._side
-        ev_fork.record(main)
-        side.wait_event(ev_fork)
+        side, ev_join, forks = self._side
+        ev = forks[part]
+        ev.record(main)
+        side.wait_event(ev)
         with torch.cuda.stream(side):
-            self._reduce_part("beta")
+            self._reduce_part(part)
         ev_join.record(side)
 
     def _capture(self):
@@ -201,23 +202,28 @@ class MultiClientRound:
         batched = (os.environ.get("GFEDNTM_ROUND_BATCHED", "1") == "1"
                    and BatchedSteps.possible(engines))
         if self._side is None:
-            self._side = (torch.cuda.Stream(self.device), torch.cuda.Event(), torch.cuda.Event())
+            self._side = (torch.cuda.Stream(self.device), torch.cuda.Event(),
+                          {k: torch.cuda.Event() for k in ("beta", "wa")})
         if batched:
             bs = BatchedSteps(engines)
             bs.prepare()
-            # beta's share on the side stream once the backward has finished it (else it
-            # is reduced with the rest at the end of the round: the same arithmetic)
-            beta_at = bs.beta_final_phase() if (self.coll_in_graph and "beta" in self.parts) else None
-            overlap = beta_at is not None
-            hooks = {beta_at: self._fork_beta} if overlap else None
+            # beta's / adapt_bert's shares on the side stream once the backward has
+            # finished them (else reduced with the rest at the end of the round: the same
+            # arithmetic)
+            hooks, forked = {}, set()
+            if self.coll_in_graph:
+                for part, at in (("beta", bs.beta_final_phase()), ("wa", bs.wa_final_phase())):
+                    if part in self.parts and at is not None:
+                        hooks[at] = (lambda p=part: self._fork(p))
+                        forked.add(part)
             with graph_capture(g):
-                bs.launch(after=hooks)
+                bs.launch(after=hooks or None)
                 if self.coll_in_graph or not self.colls:
                     for part in self.parts:
-                        if part != "beta" or not overlap:
+                        if part not in forked:
                             self._reduce_part(part)
-                    if overlap:
-                        torch.cuda.current_stream(self.device).wait_event(self._side[2])
+                    if forked:
+                        torch.cuda.current_stream(self.device).wait_event(self._side[1])
                 else:
                     self._fold("rest", LOCAL_FIRST)
             self._g, self._batched = g, bs

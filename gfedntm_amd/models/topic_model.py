@@ -184,6 +184,8 @@ class TopicModelBase:
                 raise RuntimeError("fused backend does not support this configuration")
         return backend
 
+    FUSED_SHARED_LAST = ("inf_net.adapt_bert.weight", "inf_net.adapt_bert.bias", "beta")
+
     def _build_engine(self):
         transposed = TRANSPOSED_KEYS if self.backend == "fused" else ()
         padded = {}
@@ -193,7 +195,10 @@ class TopicModelBase:
                 padded = {"beta": BETA_PAD}        # beta rows of whole 64-column tiles (utils/flat.py)
         self.flat = FlatState(self.model, self.shared_keys, transposed=transposed,
                               device=self.device,
-                              shared_last=("beta",) if self.backend == "fused" else (),
+                              # (the shared tail in the order its parts become final in
+                              # a fused step: CombinedTM's adapt_bert after ctx_bwd, beta
+                              # after the decoder backward -- ops/engine.py attach_fedavg)
+                              shared_last=self.FUSED_SHARED_LAST if self.backend == "fused" else (),
                               padded=padded)
         if self.backend == "fused":
             from ..ops.engine import FusedEngine

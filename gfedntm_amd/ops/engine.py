@@ -948,6 +948,8 @@ class FusedEngine(EngineBase):
                 if abi.PH_BETA_ADAM in ph:
                     last = abi.PH_BETA_ADAM
                 ph.insert(ph.index(last) + 1, abi.PH_FEDAVG_BETA)
+            if "wa" in self._comm:
+                ph.insert(ph.index(abi.PH_CTXF_BWD) + 1, abi.PH_FEDAVG_WA)
             ph.append(abi.PH_FEDAVG_END)
         return ph
 
@@ -964,12 +966,8 @@ class FusedEngine(EngineBase):
         follows the step eagerly.  Returns the method in use."""
         from ..parallel.aggregator import CollectiveAggregator
         self._comm = None
-        shared, flat = self.flat.shared, self.flat
-        parts = {"rest": shared}
-        if (self.update_mode == UPDATE_FUSED and flat.shared_keys
-                and flat.shared_keys[-1] == "beta" and len(flat.shared_keys) > 1):
-            b0 = flat.slots["beta"].offset
-            parts = {"rest": shared[:b0], "beta": shared[b0:]}
+        shared = self.flat.shared
+        parts = {k: shared[a:b] for k, (a, b) in self.fedavg_parts().items()}
         aggs = {k: CollectiveAggregator(group, method=method) for k in parts}
         # large parts (beta at V ~ 100k: 90 MB) are all-reduced in place: the xGMI kernel
         # maps the state itself into the peers instead of copying it into a stage first
@@ -981,14 +979,14 @@ class FusedEngine(EngineBase):
                               "bytes": {k: 4 * v.numel() for k, v in parts.items()},
                               "tuning": {k: a.tuning for k, a in aggs.items() if a.tuning}}
         if all(m == "xgmi" for m in methods.values()):
-            c = {"mode": "graph", "rest": (aggs["rest"], parts["rest"])}
-            if "beta" in parts:
-                c["beta"] = (aggs["beta"], parts["beta"])
+            c = {"mode": "graph", **{k: (aggs[k], parts[k]) for k in parts}}
+            if len(parts) > 1:
                 c["stream"] = torch.cuda.Stream(self.device)
                 c["ev_fork"] = torch.cuda.Event()
+                c["ev_fork_wa"] = torch.cuda.Event()
                 c["ev_join"] = torch.cuda.Event()
             self._comm = c
-            used = "xgmi" + ("+overlap" if "beta" in parts else "")
+            used = "xgmi" + ("+overlap" if len(parts) > 1 else "")
         else:
             for a in aggs.values():
                 if a.xgmi is not None:
@@ -999,13 +997,32 @@ class FusedEngine(EngineBase):
         self._invalidate_graph()
         return used
 
+    def fedavg_parts(self) -> Dict[str, Tuple[int, int]]:
+        """The shared state's FedAvg parts as (start, end) offsets, each with its own
+        collective: in the fused update mode beta is final after the decoder backward
+        and CombinedTM's adapt_bert after ctx_bwd (their Adam + pre-scale epilogues), so
+        those all-reduces run on a side stream while the rest of the step proceeds; the
+        rest of the state follows win_update.  (The layout puts them last: topic_model
+        FUSED_SHARED_LAST.)"""
+        flat = self.flat
+        keys = flat.shared_keys
+        n = flat.n_shared
+        if not (self.update_mode == UPDATE_FUSED and keys and keys[-1] == "beta" and len(keys) > 1):
+            return {"rest": (0, n)}
+        b0 = flat.slots["beta"].offset
+        wa = ["inf_net.adapt_bert.weight", "inf_net.adapt_bert.bias"]
+        if self._m.ctx_fused == 1 and len(keys) > 3 and keys[-3:-1] == wa:
+            w0 = flat.slots[wa[0]].offset
+            return {"rest": (0, w0), "wa": (w0, b0), "beta": (b0, n)}
+        return {"rest": (0, b0), "beta": (b0, n)}
+
     def detach_fedavg(self, close: bool = True):
         """Remove the in-step all-reduce (returns it for :meth:`restore_fedavg` when
         ``close`` is False; otherwise frees the xGMI buffers)."""
         c, self._comm = self._comm, None
         self._invalidate_graph()
         if c is not None and close:
-            for k in ("rest", "beta"):
+            for k in ("rest", "beta", "wa"):
                 if k in c and c[k][0].xgmi is not None:
                     c[k][0].xgmi.close()
                     c[k][0].xgmi = None
@@ -1021,7 +1038,7 @@ class FusedEngine(EngineBase):
         if self._comm is None:
             return 0
         err = 0
-        for k in ("rest", "beta"):
+        for k in ("rest", "beta", "wa"):
             if k in self._comm and self._comm[k][0].xgmi is not None:
                 err = err or self._comm[k][0].xgmi.error()
         return err
@@ -1029,7 +1046,7 @@ class FusedEngine(EngineBase):
     def fedavg_debug(self) -> dict:
         """Per-part diagnostics of the xGMI all-reduces (epochs, lagging flags)."""
         out = {}
-        for k in ("rest", "beta"):
+        for k in ("rest", "beta", "wa"):
             if self._comm is not None and k in self._comm and self._comm[k][0].xgmi is not None:
                 out[k] = self._comm[k][0].xgmi.debug_state()
         return out
@@ -1041,9 +1058,9 @@ class FusedEngine(EngineBase):
             return
         c = self._comm
         if "err_host" not in c:
-            c["err_host"] = torch.zeros(2, dtype=torch.int32, pin_memory=True)
+            c["err_host"] = torch.zeros(3, dtype=torch.int32, pin_memory=True)
             c["err_ev"] = torch.cuda.Event()
-        for i, k in enumerate(("rest", "beta")):
+        for i, k in enumerate(("rest", "beta", "wa")):
             if k in c and c[k][0].xgmi is not None:
                 c[k][0].xgmi.error_async(c["err_host"][i:i + 1])
         c["err_ev"].record()
@@ -1069,11 +1086,22 @@ class FusedEngine(EngineBase):
             agg.allreduce_(buf)
         c["ev_join"].record(side)
 
+    def _fedavg_wa(self):
+        c = self._comm
+        cur = torch.cuda.current_stream(self.device)
+        c["ev_fork_wa"].record(cur)
+        side = c["stream"]
+        side.wait_event(c["ev_fork_wa"])          # (behind beta's on the same side stream)
+        with torch.cuda.stream(side):
+            agg, buf = c["wa"]
+            agg.allreduce_(buf)
+        c["ev_join"].record(side)
+
     def _fedavg_end(self):
         c = self._comm
         agg, buf = c["rest"]
         agg.allreduce_(buf)
-        if "beta" in c:
+        if "beta" in c or "wa" in c:
             torch.cuda.current_stream(self.device).wait_event(c["ev_join"])
 
     # ------------------------------------------------------------------ CTM
@@ -1216,6 +1244,8 @@ class FusedEngine(EngineBase):
                         self._beta_adam()
                     elif p == abi.PH_FEDAVG_BETA:
                         self._fedavg_beta()
+                    elif p == abi.PH_FEDAVG_WA:
+                        self._fedavg_wa()
                     elif p == abi.PH_FEDAVG_END:
                         self._fedavg_end()
                     elif p == abi.PH_WIN_FORK:
@@ -1336,7 +1366,7 @@ class FusedEngine(EngineBase):
             raise RuntimeError("bind_data() first")
         self.sync_step_counter(s)
         self._launch([p for p in self.phases() if p not in (abi.PH_ADAM, abi.PH_FEDAVG_BETA,
-                                                           abi.PH_FEDAVG_END)])
+                                                           abi.PH_FEDAVG_WA, abi.PH_FEDAVG_END)])
         self._host_step = s + 1
         return self.loss_hist[s]
 
@@ -1502,6 +1532,14 @@ class BatchedSteps:
                 ev_join.record(side)
             elif p == abi.PH_WIN_JOIN:
                 torch.cuda.current_stream(self.device).wait_event(self._side[2])
+
+    def wa_final_phase(self) -> Optional[int]:
+        """The phase after which every client's adapt_bert (CombinedTM) is final in the
+        fused update mode, or None."""
+        e0 = self.engines[0]
+        if e0.update_mode != UPDATE_FUSED or abi.PH_CTXF_BWD not in self._phases:
+            return None
+        return abi.PH_CTXF_BWD
 
     def beta_final_phase(self) -> Optional[int]:
         """The phase after which every client's beta is final in the fused update mode

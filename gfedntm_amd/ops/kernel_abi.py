@@ -55,8 +55,11 @@ PH_BETA_ADAM = 104
 # start of the step, joined before win_update
 PH_WIN_FORK = 105
 PH_WIN_JOIN = 106
+# CombinedTM (fused): adapt_bert's share of the FedAvg forked onto the side stream once
+# ctx_bwd has finished it (overlapping win_update), behind beta's
+PH_FEDAVG_WA = 107
 HOST_PHASES = (PH_CTX_FWD, PH_CTX_BWD, PH_FEDAVG_BETA, PH_FEDAVG_END, PH_BETA_ADAM, PH_WIN_FORK,
-               PH_WIN_JOIN)
+               PH_WIN_JOIN, PH_FEDAVG_WA)
 
 PRODLDA_STEP = [PH_ENC_FWD, PH_POST_FWD, PH_PRODLDA_FWD, PH_PRODLDA_LOSS, PH_PRODLDA_BWD,
                 PH_POST_BWD, PH_ENC_BWD]

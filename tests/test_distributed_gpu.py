@@ -186,16 +186,32 @@ def test_timed_out_wait_is_caught_between_aligned_rounds(tmp_path):
 N_MULTI = 8                      # clients, over 2 ranks: 4 per rank
 
 
-def _multi_corpora(n=N_MULTI):
+CTM_C = 48                       # contextual size of the CombinedTM rehearsals
+
+
+def _multi_corpora(n=N_MULTI, ctm=False):
     from gfedntm_amd.data.synthetic import generate_synthetic
     from gfedntm_amd.federation.data import ClientCorpus
     sc = generate_synthetic(vocab_size=500, n_topics=10, n_docs=60, n_nodes=n,
                             frozen_topics=2, nwords=(30, 60), seed=9)
-    return [ClientCorpus(synthetic=sc, node=i) for i in range(n)]
+    if not ctm:
+        return [ClientCorpus(synthetic=sc, node=i) for i in range(n)]
+    proj = np.random.default_rng(3).standard_normal((10, CTM_C)).astype(np.float32)
+    out = []
+    for i in range(n):      # synthetic embeddings: a projection of the topic mixture + noise
+        dt = np.asarray(sc.doc_topics[i], dtype=np.float32)
+        emb = dt @ proj + 0.1 * np.random.default_rng(11 + i).standard_normal(
+            (dt.shape[0], CTM_C)).astype(np.float32)
+        out.append(ClientCorpus(synthetic=sc, node=i, embeddings=emb))
+    return out
+
+
+def _ctm_params():
+    return dict(_params(), contextual_size=CTM_C)
 
 
 def _multi_worker(rank, world, port, tmp, q, n_clients=N_MULTI, env=None, stall=None,
-                  rounds=ROUNDS, epochs=2):
+                  rounds=ROUNDS, epochs=2, ctm=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     os.environ.update(env or {})
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -204,7 +220,7 @@ def _multi_worker(rank, world, port, tmp, q, n_clients=N_MULTI, env=None, stall=
         from gfedntm_amd.federation.hierarchical import assign_clients, run_distributed_multi
         from gfedntm_amd.federation.runner import CommError
         ids = assign_clients(n_clients, world)[rank]
-        corpora = _multi_corpora(n_clients)
+        corpora = _multi_corpora(n_clients, ctm=ctm)
 
         def hook(it):
             if stall and rank == 1 and it == 5:
@@ -212,7 +228,8 @@ def _multi_worker(rank, world, port, tmp, q, n_clients=N_MULTI, env=None, stall=
 
         try:
             out = run_distributed_multi([corpora[i - 1] for i in ids], ids,
-                                        dict(_params(), num_epochs=epochs), max_iters=rounds,
+                                        dict(_ctm_params() if ctm else _params(), num_epochs=epochs),
+                                        model_type="ctm" if ctm else "avitm", max_iters=rounds,
                                         backend="fused", seed=5, rehearse_1gpu=True,
                                         save_client=os.path.join(tmp, "client"), stamp="20240101",
                                         round_hook=hook)
@@ -273,6 +290,30 @@ def test_more_clients_than_ranks_xgmi_matches_grouped_golden(tmp_path, n_clients
             np.testing.assert_array_equal(sh, gold)
     for i in range(1, n_clients + 1):
         assert os.path.exists(tmp_path / f"client{i}" / f"model_{i}_20240101.npz")
+
+
+@pytest.mark.parametrize("n_clients", [2, 6])
+def test_combined_tm_adapt_bert_overlap_matches_golden(tmp_path, n_clients):
+    """CombinedTM over 2 ranks (one client each, or 3 per rank): the shared state's three
+    parts -- beta forked after the decoder backward, adapt_bert after ctx_bwd (both on the
+    side stream, overlapping the encoder backward / win_update), the rest after the step --
+    leave every client's state bit-identical to the in-process federation."""
+    res = _run_multi(tmp_path, n_clients=n_clients, ctm=True)
+    for r in res:
+        assert r[1] not in ("exception", "comm_error"), r[2]
+        assert r[1] == "xgmi+overlap", r[1]
+    from gfedntm_amd.federation.runner import LocalFederation
+    half = n_clients // 2
+    fed = LocalFederation(_multi_corpora(n_clients, ctm=True), _ctm_params(), model_type="ctm",
+                          max_iters=ROUNDS, device="cuda", backend="fused", seed=5,
+                          **({"groups": [half, half]} if half > 1 else {"round_batched": False}))
+    fed.run()
+    e = fed.clients[0].tm.engine
+    assert set(e.fedavg_parts()) == {"rest", "wa", "beta"}
+    gold = fed.clients[0].shared.detach().cpu().numpy()
+    for r in res:
+        for sh in r[2]:
+            np.testing.assert_array_equal(sh, gold)
 
 
 def test_more_clients_than_ranks_timed_out_wait_is_polled(tmp_path):

@@ -89,7 +89,8 @@ def test_step_matches_oracle(model_type, B, n_docs, K, H, V):
                                             # more strips than waves (V > 65k on 256 CUs): a
                                             # wave's second strip reads its first pairs from
                                             # the ring slots the previous strip refilled
-                                            (64, 80, 200, (50, 50), 80000),   # NP = 26, ring 13
+                                            (64, 80, 200, (50, 50), 80000),   # NP = 25, ring 5
+                                            (64, 80, 204, (50,), 80000),      # NP = 26, ring 13
                                             (64, 80, 120, (50,), 80000),      # NP = 16, ring 8
                                             (64, 80, 250, (50,), 80000)])     # NP = 32, ring 8
 @pytest.mark.parametrize("pf", ["2", "3"])
