@@ -138,7 +138,8 @@ typedef struct GfkModel {
   // ---- precision of the decoder GEMMs (theta.beta, theta^T.dlogit, dlogit.beta^T):
   // 0 = fp32 matrix cores (v_mfma_f32_16x16x4_f32, the reference's precision), 1 = bf16
   // operands, fp32 accumulation (v_mfma_f32_16x16x32_bf16); parameters, Adam state and
-  // every other op stay fp32
+  // every other op stay fp32.  The large-V pipelined backward (bwd_pre = 3) keeps fp32
+  // operands in both modes: it is bound by beta / Adam-state HBM traffic
   int32_t mm_bf16;
   // CombinedTM forward, balanced persistent shape (stage_flags bit 11): ctx_parts
   // workgroups each own a contiguous range of 16-column units and leave ONE partial of the

@@ -734,7 +734,7 @@ __host__ __device__ __forceinline__ int bwd_kpq(int K, int kq) { return 16 * ((r
 // (its buffer-descriptor stores need beta's rows padded to whole 64-column tiles and the
 // slot under 2 GB)
 __host__ __device__ __forceinline__ bool bwd_pipe(const GfkModel& m) {
-  return m.bwd_pre == 3 && m.bmax == 64 && !m.mm_bf16 && (m.ldb & 63) == 0 &&
+  return m.bwd_pre == 3 && m.bmax == 64 && (m.ldb & 63) == 0 &&
          (int64_t)m.K * m.ldb * 4 < 0x7FFF0000LL;
 }
 
@@ -1710,7 +1710,9 @@ extern "C" int gfk_launch_prodlda_fwd(const GfkModel* m, hipStream_t s) {
 template <int MAXU, int KQ, bool BF, bool PRE>
 static void launch_bwd_p(const GfkModel* m, dim3 g, size_t sm, hipStream_t s) {
   const dim3 blk(KQ == 1 ? DEC_THREADS : 512);
-  if constexpr (PRE && !BF) {
+  // (the pipelined backward also serves mm_bf16: its GEMMs keep fp32 operands -- the
+  // kernel is bound by its beta / Adam-state HBM traffic, not by the matrix cores)
+  if constexpr (PRE) {
     if (bwd_pipe(*m)) {
       if (m->update_mode == 1 && !m->beta_split) {
         if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_bwd_pipe_kernel<64, MAXU, true, true>), gfk_grid(g, m), blk, sm, s, GfkArgT<true>{gfk_dev(m)});

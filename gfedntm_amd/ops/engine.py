@@ -541,7 +541,7 @@ class FusedEngine(EngineBase):
                 # its smaller LDS plan (no logit tile, G aliases dt) and <= 80 VGPRs fit
                 # THREE range workgroups per CU: 3/4 of a CU's slots per slab of 4
                 m.n_dpart = min(3 * cu // 4, m.n_tiles - 1)
-            elif (m.bwd_pre == 3 and m.bmax == 64 and not m.mm_bf16 and m.ldb % 64 == 0
+            elif (m.bwd_pre == 3 and m.bmax == 64 and m.ldb % 64 == 0
                   and m.K * m.ldb * 4 < 0x7FFF0000):
                 pass
             elif m.bwd_pre:

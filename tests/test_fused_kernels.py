@@ -538,7 +538,8 @@ def test_bf16_decoder_matches_emulated_oracle(K, V):
     with theta_d and beta rounded to bf16 before the logits GEMM (the backward GEMMs'
     extra rounding of dlogit is inside the gradient tolerance).  The forward is the bf16
     strip kernel (32-k steps: 8, 16 or 32 pairs, a ring of 8); V = 80k: waves with a
-    second strip (the ring's cross-strip slots)."""
+    second strip (the ring's cross-strip slots).  At V = 40k / 80k the backward is the
+    pipelined kernel, whose GEMMs keep fp32 operands in bf16 mode (HBM-bound)."""
     from gfedntm_amd.models.functional import encoder_forward
     from gfedntm_amd.models.networks import kl_terms, reconstruction_terms
     import torch.nn.functional as F
