@@ -50,7 +50,7 @@ def main(argv=None):
     a = p.parse_args(argv)
     so = build()
     from gfedntm_amd.ops import native
-    native.KERNELS_SO = so
+    native.KERNELS_SO = native.KERNELS_SO_OVERRIDE = so    # (a diagnostic build: not hash-checked)
     import torch
     from gfedntm_amd.data.bow import BatchPlan, DeviceCSR
     import numpy as np
