@@ -769,6 +769,7 @@ template <bool GB = false>
 __global__ void __launch_bounds__(RS_T) gfk_ctx_fwd_rs_k(GfkArgT<GB> ga) {
   const GfkModel& m = gfk_model(ga);
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  GFK_STAMP(m, 30);
   const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
   const int r = lane & 15, g = lane >> 4;
   const int V = m.V, C = m.C, H0 = m.H[0], bmax = m.bmax;
@@ -854,6 +855,7 @@ __global__ void __launch_bounds__(RS_T) gfk_ctx_fwd_rs_k(GfkArgT<GB> ga) {
     else vm_barrier();
     // (4 j + g) ^ r = 16 (j >> 2) + 4 ((j & 3) ^ (r >> 2)) + (g ^ (r & 3)): four lane
     // offsets, the rest immediates
+    if (p == 0) GFK_STAMP(m, 31);
     const float* xc = smem + (p & 1) * 64 * RS_KP + r * RS_KP + (g ^ (r & 3)) * 4;
     if (p + 1 < NPH) dma_x(p + 1, smem + ((p + 1) & 1) * 64 * RS_KP);
 #pragma unroll
@@ -880,6 +882,7 @@ __global__ void __launch_bounds__(RS_T) gfk_ctx_fwd_rs_k(GfkArgT<GB> ga) {
       }
     }
   }
+  GFK_STAMP(m, 32);
   // ---- epilogue: the first Wc chunk in flight while A (+ bias) goes to ws_actx and LDS ----
   const int NJT = (H0 + 15) / 16;
   const int bt = wave & 3, ht = wave >> 2, hh = ht * 16 + r;
@@ -982,6 +985,7 @@ __global__ void __launch_bounds__(RS_T) gfk_ctx_fwd_rs_k(GfkArgT<GB> ga) {
       }
     }
   }
+  GFK_STAMP(m, 33);
 }
 
 // grid: n_tiles * ctx_kb workgroups of 16 waves (one per CU).

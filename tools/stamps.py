@@ -91,6 +91,8 @@ def main(argv=None):
     print("enc_in input+hidden: tile-start tail", int(d[44] - d[6]), "| input layer", int(d[43] - d[44]),
           "| hidden layers", int(d[7] - d[43]), "(last layer's gemv+epilogue ends at", int(d[45] - d[43]), ")")
     if a.ctx:
+        # (register-streamed forward, the default at large V: prologue = first x phase +
+        # ring fill, C loop = the phases' MFMAs, A + P = the epilogue, of wave 0 of wg 0)
         print("ctx_fwd (wg 0) cycles: prologue", int(d[31] - d[30]), "| C loop", int(d[32] - d[31]),
               "| A + P", int(d[33] - d[32]))
         print("ctx_bwd (wg 0) cycles: staging", int(d[35] - d[34]), "| dA", int(d[36] - d[35]),
