@@ -88,3 +88,26 @@ def test_default_shared_keys_on_avitm():
     # every float tensor of the AVITM state is shared (adapt_bert keys are absent: B2)
     float_keys = [k for k, v in m.state_dict().items() if v.is_floating_point()]
     assert fs.n_shared >= sum(fs.slots[k].numel for k in float_keys)
+
+
+def test_fused_shared_tail_orders_the_fedavg_parts():
+    """The fused engine's FedAvg parts are contiguous ranges at the end of the shared
+    prefix (ops/engine.py fedavg_parts): with topic_model.FUSED_SHARED_LAST a CombinedTM's
+    shared state ends [... | adapt_bert.weight, adapt_bert.bias | beta], in the order the
+    step finishes them (ctx_bwd before the decoder's beta is reduced... both after the rest's
+    producers); a ProdLDA's ends with beta alone (the adapt_bert keys are absent)."""
+    from gfedntm_amd.models.networks import CTMDecoderNetwork
+    from gfedntm_amd.models.topic_model import TopicModelBase
+    tail = TopicModelBase.FUSED_SHARED_LAST
+    torch.manual_seed(0)
+    ctm = CTMDecoderNetwork(60, 12, "combined", 5, "prodLDA", (8, 6))
+    keys = list(ctm.state_dict().keys())
+    fs = FlatState(ctm, keys, transposed=("inf_net.input_layer.weight",), shared_last=tail)
+    assert fs.shared_keys[-3:] == list(tail)
+    w0 = fs.slots[tail[0]].offset
+    b0 = fs.slots["beta"].offset
+    rest = [k for k in fs.shared_keys if k not in tail]
+    assert max(fs.slots[k].offset + fs.slots[k].numel for k in rest) <= w0 < b0
+    assert fs.slots["beta"].offset + fs.slots["beta"].numel == fs.n_shared
+    pl = FlatState(_net(), list(_net().state_dict().keys()), shared_last=tail)
+    assert pl.shared_keys[-1] == "beta" and tail[0] not in pl.slots
