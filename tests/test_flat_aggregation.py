@@ -93,9 +93,8 @@ def test_default_shared_keys_on_avitm():
 def test_fused_shared_tail_orders_the_fedavg_parts():
     """The fused engine's FedAvg parts are contiguous ranges at the end of the shared
     prefix (ops/engine.py fedavg_parts): with topic_model.FUSED_SHARED_LAST a CombinedTM's
-    shared state ends [... | adapt_bert.weight, adapt_bert.bias | beta], in the order the
-    step finishes them (ctx_bwd before the decoder's beta is reduced... both after the rest's
-    producers); a ProdLDA's ends with beta alone (the adapt_bert keys are absent)."""
+    shared state ends [... | adapt_bert.weight, adapt_bert.bias | beta], each part one
+    contiguous range; a ProdLDA's ends with beta alone (the adapt_bert keys are absent)."""
     from gfedntm_amd.models.networks import CTMDecoderNetwork
     from gfedntm_amd.models.topic_model import TopicModelBase
     tail = TopicModelBase.FUSED_SHARED_LAST
