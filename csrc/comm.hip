@@ -317,10 +317,8 @@ extern "C" int gfk_comm_alloc(int64_t stage_bytes, int64_t flag_bytes, int64_t s
 }
 
 extern "C" int gfk_comm_free(void* stage, void* flags, void* state) {
-  hipFree(stage);
-  hipFree(flags);
-  hipFree(state);
-  return 0;
+  const hipError_t e0 = hipFree(stage), e1 = hipFree(flags), e2 = hipFree(state);
+  return (int)(e0 ? e0 : e1 ? e1 : e2);
 }
 
 extern "C" int gfk_ipc_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }

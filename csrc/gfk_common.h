@@ -188,15 +188,6 @@ typedef struct GfkModel {
 
 constexpr int GFK_WIN_SPLIT = 128;
 
-// launch helpers: grid z = the batched models, the kernel argument = the device array
-__host__ inline dim3 gfk_grid(dim3 g, const GfkModel* m) {
-  g.z = m->n_batch > 1 ? (unsigned)m->n_batch : 1u;
-  return g;
-}
-__host__ inline const GfkModel* gfk_dev(const GfkModel* m) {
-  return reinterpret_cast<const GfkModel*>(m->dev);
-}
-
 // Gradient + update jobs of the small tensors, run by the update kernel next to
 // the W_in tiles (csrc/update.hip).  Weight job: G[j][i] = sum_{b < nb} dz[b][j]
 // a[b][i] for the 64 x 64 output tile at (j0, i0) of param [rows][cols].  Vector
@@ -251,6 +242,15 @@ typedef struct GfkAdam {
 } GfkAdam;
 
 }  // extern "C"
+
+// launch helpers: grid z = the batched models, the kernel argument = the device array
+__host__ inline dim3 gfk_grid(dim3 g, const GfkModel* m) {
+  g.z = m->n_batch > 1 ? (unsigned)m->n_batch : 1u;
+  return g;
+}
+__host__ inline const GfkModel* gfk_dev(const GfkModel* m) {
+  return reinterpret_cast<const GfkModel*>(m->dev);
+}
 
 // Kernel argument of every model kernel, in two instantiations: <false> the descriptor BY
 // VALUE (one client: kernarg memory, so the pointers in it are known global and the

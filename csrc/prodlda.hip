@@ -345,6 +345,19 @@ __host__ __device__ constexpr int strip_ring(int pf, int np) {
   while (np % d) --d;
   return d;
 }
+// (GFK_STAMPS builds: per-wave timeline of workgroups 0 and grid-1, tools/stamps.py)
+#ifdef GFK_STAMPS
+#define STRIP_STAMP(j, rt)                                                                \
+  do {                                                                                    \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    if ((blockIdx.x == 0 || blockIdx.x == gridDim.x - 1) && lane == 0 && m.dbg)           \
+      m.dbg[64 + (blockIdx.x ? 16 * 10 : 0) + wave * 10 + (j)] =                          \
+          (rt) ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime();         \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+  } while (0)
+#else
+#define STRIP_STAMP(j, rt) do { } while (0)
+#endif
 // BF (mm_bf16, PF = 3 only): the logits on v_mfma_f32_16x16x32_bf16 -- pairs t = 4 s + u hold
 // k = 32 s + 8 g + 2 u (+ 1) for lane group g, so the 4 pairs of step s are the 8 consecutive
 // k of the lane's B operand (B[8 g + j][col]); A = 8 consecutive k of theta_d's row from LDS
@@ -362,6 +375,8 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
   const int lane = tid & 63, wave = uniform(tid >> 6);
   constexpr int RT = BM / 16;
   constexpr int NW = STRIP_THREADS / 64;
+  STRIP_STAMP(0, false);
+  STRIP_STAMP(1, true);
   // theta_d re-staged with its own row stride KS = 8 NP + 4 (4 x odd: ds_read_b64 banks
   // lanes {0-31} / {32-63} over 64 banks, and rows r * KS of 16 lanes + the two lane
   // groups' k offsets 2g then cover all 64 -- measured 45 % conflicted cycles with the
@@ -451,8 +466,12 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
       if (tid + u * STRIP_THREADS < BM * KS) th[tid + u * STRIP_THREADS] = tv[u];
   }
   lds_barrier();
+  STRIP_STAMP(2, false);
   asm volatile("" : "+v"(tid));
   __builtin_assume(tid >= 0 && tid < STRIP_THREADS);
+#ifdef GFK_STAMPS
+  int it_ = 0;
+#endif
   // PF = 3: this strip's per-lane offset of pair 0 (its pairs R.. are loaded in the loop)
   int voffc = 0;
   if (PF == 3) {
@@ -545,6 +564,9 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
     }
     }
     if (PF == 3) voffc = voffn;
+#ifdef GFK_STAMPS
+    if (it_ < 2) STRIP_STAMP(3 + 2 * it_, false);
+#endif
     // ---- column batch-norm over the wave's own rows (rows >= nb excluded) ----
     // (rows >= nb are exact zeros, so the sum needs no mask; lim is made opaque per strip
     // so the 4 RT row compares are not hoisted out of the loop as live SGPR masks)
@@ -594,7 +616,13 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
       rm0 = rmn;
       rv0 = rvn;
     }
+#ifdef GFK_STAMPS
+    if (it_ < 2) STRIP_STAMP(4 + 2 * it_, false);
+    ++it_;
+#endif
   }
+  STRIP_STAMP(7, false);
+  STRIP_STAMP(8, true);
   // ---- the 16 waves' per-row partials -> the workgroup's partial slots ----
 #pragma unroll
   for (int i = 0; i < RT; ++i)

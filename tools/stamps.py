@@ -6,6 +6,9 @@ s_memtime deltas between phase stamps (lane 0 of workgroup 0; in the vocab-tile 
 of the decoder kernels: the workgroup's last tile).  Read the SHARES, not the
 absolute length (the stamps add fences).
 
+(python tools/stamps.py --build-only on the CPU host, then --so build/stamps/... copied
+to a travelling path on the GPU box, so the box does not compile)
+
 usage: python tools/stamps.py [--topics K] [--vocab V] [--hidden 50,50] [--batch B]
                               [--nnz N] [--docs D] [--steps S]
 """
@@ -47,8 +50,13 @@ def main(argv=None):
     p.add_argument("--docs", type=int, default=1000)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--ctx", type=int, default=0, help="contextual size: CombinedTM when > 0")
+    p.add_argument("--so", default=None, help="a prebuilt -DGFK_STAMPS library (--build-only)")
+    p.add_argument("--build-only", action="store_true", help="build it on the host and stop")
     a = p.parse_args(argv)
-    so = build()
+    if a.build_only:
+        print(build())
+        return
+    so = a.so or build()
     from gfedntm_amd.ops import native
     native.KERNELS_SO = native.KERNELS_SO_OVERRIDE = so    # (a diagnostic build: not hash-checked)
     import torch
@@ -65,7 +73,7 @@ def main(argv=None):
            if a.ctx else None)
     data = DeviceCSR(X, "cuda", contextual=ctx)
     tm.engine.bind_data(data, BatchPlan.build(a.docs, a.batch, a.steps))
-    dbg = torch.zeros(64, dtype=torch.int64, device="cuda")
+    dbg = torch.zeros(512, dtype=torch.int64, device="cuda")
     tm.engine._m.dbg = dbg.data_ptr()
     tm.engine._a.dbg = dbg.data_ptr()
     for s in range(a.steps):
@@ -98,6 +106,21 @@ def main(argv=None):
         print("ctx_bwd (wg 0) cycles: staging", int(d[35] - d[34]), "| dA", int(d[36] - d[35]),
               "| g_ba + g_Wa", int(d[37] - d[36]), "| update", int(d[38] - d[37]))
     print("win_update (W_in tile 0) cycles: staging", int(d[41] - d[40]), "| mfma+update", int(d[42] - d[41]))
+    # strip forward (stage_flags bit 2): per-wave timelines of workgroups 0 and grid - 1,
+    # memtime cycles from the earliest wave's entry; clock = memtime / memrealtime (100 MHz)
+    for wg, base in (("0", 64), ("last", 224)):
+        w = d[base:base + 160].reshape(16, 10)
+        if not w[:, 0].any():
+            continue
+        t0 = w[:, 0].min()
+        rt = (w[:, 8] - w[:, 1]).max()
+        ghz = (w[:, 7] - w[:, 0]).max() / rt / 10.0 if rt else 0.0
+        print(f"strip_fwd wg {wg}: clock {ghz:.2f} GHz (memtime/realtime)")
+        for i in range(16):
+            r = w[i]
+            ev = [("entry", r[0]), ("staged", r[2]), ("mfma0", r[3]), ("epi0", r[4]),
+                  ("mfma1", r[5]), ("epi1", r[6]), ("end", r[7])]
+            print(f"  wave {i:2d}: " + " ".join(f"{n} {int(v - t0)}" for n, v in ev if v))
 
 
 if __name__ == "__main__":
