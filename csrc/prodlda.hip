@@ -351,7 +351,7 @@ __host__ __device__ constexpr int strip_ring(int pf, int np) {
   do {                                                                                    \
     __builtin_amdgcn_sched_barrier(0);                                                    \
     if ((blockIdx.x == 0 || blockIdx.x == gridDim.x - 1) && lane == 0 && m.dbg)           \
-      m.dbg[64 + (blockIdx.x ? 16 * 10 : 0) + wave * 10 + (j)] =                          \
+      m.dbg[64 + (blockIdx.x ? 16 * 16 : 0) + wave * 16 + (j)] =                          \
           (rt) ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime();         \
     __builtin_amdgcn_sched_barrier(0);                                                    \
   } while (0)
@@ -576,6 +576,9 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
 #pragma unroll
       for (int e = 0; e < 4; ++e) sm += acc[i][e];
     const float mean = sum_groups(sm) * inv_nb;
+#ifdef GFK_STAMPS
+    if (it_ == 0) STRIP_STAMP(9, false);
+#endif
     int lim = nb - (lane >> 4) * 4;
     asm volatile("" : "+v"(lim));
     float q = 0.f;
@@ -588,6 +591,9 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
       }
     const float var = sum_groups(q) * inv_nb;
     const float rstd = rsqrtf(var + m.bn_eps);
+#ifdef GFK_STAMPS
+    if (it_ == 0) STRIP_STAMP(10, false);
+#endif
     if (lane < 16 && valid) {
       const float mom = m.bn_momentum;
       const float unb = nb > 1 ? var * (float)nb / (float)(nb - 1) : var;
@@ -597,6 +603,9 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
       m.beta_rv[v] = nv;
       m.ws_col_rstd[v] = rstd;
     }
+#ifdef GFK_STAMPS
+    if (it_ == 0) STRIP_STAMP(11, false);
+#endif
     // ---- normalise, store the BN'ed strip, accumulate the per-row sum of exp ----
     float* zt = m.ws_zn + (size_t)tile * BM * VB;
 #pragma unroll

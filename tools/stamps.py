@@ -73,7 +73,7 @@ def main(argv=None):
            if a.ctx else None)
     data = DeviceCSR(X, "cuda", contextual=ctx)
     tm.engine.bind_data(data, BatchPlan.build(a.docs, a.batch, a.steps))
-    dbg = torch.zeros(512, dtype=torch.int64, device="cuda")
+    dbg = torch.zeros(1024, dtype=torch.int64, device="cuda")
     tm.engine._m.dbg = dbg.data_ptr()
     tm.engine._a.dbg = dbg.data_ptr()
     for s in range(a.steps):
@@ -108,8 +108,8 @@ def main(argv=None):
     print("win_update (W_in tile 0) cycles: staging", int(d[41] - d[40]), "| mfma+update", int(d[42] - d[41]))
     # strip forward (stage_flags bit 2): per-wave timelines of workgroups 0 and grid - 1,
     # memtime cycles from the earliest wave's entry; clock = memtime / memrealtime (100 MHz)
-    for wg, base in (("0", 64), ("last", 224)):
-        w = d[base:base + 160].reshape(16, 10)
+    for wg, base in (("0", 64), ("last", 320)):
+        w = d[base:base + 256].reshape(16, 16)
         if not w[:, 0].any():
             continue
         t0 = w[:, 0].min()
@@ -118,8 +118,9 @@ def main(argv=None):
         print(f"strip_fwd wg {wg}: clock {ghz:.2f} GHz (memtime/realtime)")
         for i in range(16):
             r = w[i]
-            ev = [("entry", r[0]), ("staged", r[2]), ("mfma0", r[3]), ("epi0", r[4]),
-                  ("mfma1", r[5]), ("epi1", r[6]), ("end", r[7])]
+            ev = [("entry", r[0]), ("staged", r[2]), ("mfma0", r[3]), ("mean0", r[9]),
+                  ("rstd0", r[10]), ("bnst0", r[11]), ("epi0", r[4]), ("mfma1", r[5]),
+                  ("epi1", r[6]), ("end", r[7])]
             print(f"  wave {i:2d}: " + " ".join(f"{n} {int(v - t0)}" for n, v in ev if v))
 
 
