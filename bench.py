@@ -1,5 +1,5 @@
 #!/usr/bin/env python
-"""Headline benchmark: whole-node docs/s of federated ProdLDA K=50, one client per GPU.
+"""Headline benchmark: whole-node docs/s of the 8-client federated ProdLDA K=50.
 
 BASELINE.json metric: "docs/sec (whole node) + NPMI, ProdLDA K=50 8-client fed on
 synthetic BoW".  Config (reference config/dft_params.cf defaults + the reference
@@ -14,13 +14,18 @@ all shared tensors (the 20 AVITM state_dict tensors of grads_to_share) replaces
 every client's copy.  On MI355X: fused HIP step + the FedAvg all-reduce over
 xGMI captured in the same hipGraph (one replay per round).
 
+Default: the 8-client federation of BASELINE.json (``--clients 8``) spread over the N
+ranks in contiguous blocks -- all eight clients on one GPU at N = 1 (their steps batched
+into one launch per kernel phase, the FedAvg an in-rank fold), four per GPU at N = 2, one
+per GPU at N = 8 (the in-step xGMI all-reduce).  The total work per round is fixed
+(``scaling: strong``); ``--clients-per-gpu M`` instead fixes M clients per GPU (weak).
+
 ``--path runner`` (default) times the PRODUCTION round loop,
 :func:`gfedntm_amd.federation.runner.run_distributed` -- what ``main.py
 --backend rccl`` users get, with its per-round client bookkeeping -- and reports
 the engine-only replay loop of the same engine next to it
 (``engine_only_ms_per_step``).  ``--path engine`` times the bare replay loop.
 
-Weak scaling: per-GPU work (one client, batch 64) is fixed as N grows.
 ``value`` = total training documents of all clients / round time.  Vocabulary
 consensus, init broadcast and the NPMI evaluation run outside the timed region;
 the NPMI comes from a SEPARATE untimed federation of ``--npmi-steps`` rounds
@@ -69,9 +74,13 @@ def parse(argv=None):
     p.add_argument("--path", default="runner", choices=["runner", "engine"])
     p.add_argument("--sim-clients", type=int, default=0,
                    help="M > 0: M simulated clients on one GPU (LocalFederation round graph)")
-    p.add_argument("--clients-per-gpu", type=int, default=1,
-                   help="M > 1: every rank hosts M federated clients (hierarchical FedAvg: "
-                        "batched client steps, in-rank fold, cross-rank all-reduce)")
+    p.add_argument("--clients", type=int, default=8,
+                   help="federated clients in total (BASELINE: 8), spread over the ranks in "
+                        "contiguous blocks -- one per GPU at --gpus 8, all eight on one GPU at "
+                        "--gpus 1 (total work fixed: strong scaling)")
+    p.add_argument("--clients-per-gpu", type=int, default=None,
+                   help="instead of --clients: every rank hosts M clients, M x N in total "
+                        "(per-GPU work fixed: weak scaling)")
     p.add_argument("--unbatched", action="store_true",
                    help="--sim-clients: one graph branch per client instead of one batched "
                         "launch per phase for all clients (grid z = client)")
@@ -253,21 +262,42 @@ def _physical_gpus(device, world: int) -> int:
     return len(set(keys))
 
 
-def run_multi(args):
-    """M clients per rank: the production runner (federation/runner.py run_distributed)
-    with a block of clients per rank (federation/rank_round.py MultiClientRound)."""
+def total_clients(args, world: int) -> int:
+    return args.clients_per_gpu * world if args.clients_per_gpu else args.clients
+
+
+def run_multi(args, rank, world, device, rehearse):
+    """A block of clients per rank: the production runner (federation/runner.py
+    run_distributed) with federation/rank_round.py MultiClientRound (or the one-client
+    round on ranks that host one)."""
     from gfedntm_amd.federation.hierarchical import assign_clients, run_distributed_multi
-    rank, world, device, rehearse = _init(args)
-    _ctrl_group()
     physical = _physical_gpus(device, world)
-    M = args.clients_per_gpu
-    sc = _corpus(args, world * M)
-    ids = assign_clients(world * M, world)[rank]
+    n_clients = total_clients(args, world)
+    sc = _corpus(args, n_clients)
+    ids = assign_clients(n_clients, world)[rank]
     corpora = [_client_corpus(args, sc, i - 1) for i in ids]
-    out = run_distributed_multi(corpora, ids, _params(args), _model_type(args),
-                                max_iters=args.warmup + args.steps, backend=args.backend,
-                                seed=args.seed, graph=not args.no_graph, allreduce=args.allreduce,
-                                rehearse_1gpu=rehearse, timing_warmup=args.warmup)
+    kw = dict(backend=args.backend, seed=args.seed, graph=not args.no_graph,
+              allreduce=args.allreduce, rehearse_1gpu=rehearse)
+    from gfedntm_amd.federation.runner import CommError
+    fallback = None
+    try:
+        out = run_distributed_multi(corpora, ids, _params(args), _model_type(args),
+                                    max_iters=args.warmup + args.steps,
+                                    timing_warmup=args.warmup, keep_round=True, **kw)
+    except CommError as e:
+        # the ranks agreed on a data-plane failure (a timed-out xGMI wait or diverged
+        # replicas): with auto-selection, measure the same federation over RCCL instead
+        if args.allreduce not in (None, "auto"):
+            raise
+        fallback = f"xGMI all-reduce failed ({e}); re-run over RCCL"
+        if rank == 0:
+            print(f"[bench] {fallback}", file=sys.stderr, flush=True)
+        kw["allreduce"] = "rccl"
+        for k in ("GFEDNTM_INJECT_STALL", "GFEDNTM_INJECT_CORRUPT"):
+            os.environ.pop(k, None)
+        out = run_distributed_multi(corpora, ids, _params(args), _model_type(args),
+                                    max_iters=args.warmup + args.steps,
+                                    timing_warmup=args.warmup, keep_round=True, **kw)
     wall = _max_over_ranks(out["wall_s"], world)
     dev_s = None if out.get("device_s") is None else _max_over_ranks(out["device_s"], world)
     t = torch.tensor([float(out["docs"])], dtype=torch.float64)
@@ -277,15 +307,25 @@ def run_multi(args):
     out["round"].close()
     n_rounds = args.warmup + args.steps
     final_loss = float(np.mean(eng.loss_hist[max(0, n_rounds - 20): n_rounds].cpu().numpy()))
+    # ---- quality: a separate untimed federation of --npmi-steps rounds (all clients) ----
+    quality = _quality(args, corpora, ids, sc, n_clients, rank, device, kw)
     if rank == 0:
         ms = wall / max(out["timed_rounds"], 1) * 1e3
-        rec = _record(args, docs / wall, ms, len(out["clients"][0].tm.train_data.idx2token), None,
-                      final_loss, clients=world * M, ranks=world, physical=physical)
+        rec = _record(args, docs / wall, ms, len(out["clients"][0].tm.train_data.idx2token),
+                      quality.get("npmi"), final_loss, clients=n_clients, ranks=world,
+                      physical=physical)
+        rec.update({k: v for k, v in quality.items() if k != "npmi"})
         rec["device_ms_per_step"] = (None if dev_s is None else
                                      round(dev_s / max(out["timed_rounds"], 1) * 1e3, 5))
-        rec["config"]["aggregation"] += (f" (hierarchical: {M} clients per rank folded in-rank, "
-                                         f"{out['allreduce'] or 'no'} all-reduce across ranks)")
-        rec["path"] = "run_distributed (multi-client ranks)"
+        per_rank = sorted({len(b) for b in assign_clients(n_clients, world)})
+        rec["config"]["aggregation"] += (
+            f" ({'/'.join(map(str, per_rank))} client(s) per rank"
+            + (", batched steps + in-rank fold" if per_rank[-1] > 1 else "")
+            + f", {out['allreduce'] or 'no'} all-reduce across ranks)")
+        rec["path"] = "run_distributed"
+        rec["digests"] = out.get("digests")
+        if fallback:
+            rec["allreduce_fallback"] = fallback
         if out.get("attach"):
             rec["fedavg_attach"] = out["attach"]
         if rehearse:
@@ -296,12 +336,34 @@ def run_multi(args):
     dist.destroy_process_group()
 
 
+def _quality(args, corpora, ids, sc, n_clients, rank, device, kw) -> dict:
+    """NPMI (top-10 words of client 1's topics over every client's documents) and client
+    1's TSS / DSS against the generator's ground truth, from a separate untimed federation
+    of --npmi-steps rounds, so the numbers do not depend on --steps."""
+    if args.no_npmi or args.npmi_steps <= 0:
+        return {}
+    from gfedntm_amd.federation.hierarchical import run_distributed_multi
+    out = run_distributed_multi(corpora, ids, _params(args), _model_type(args),
+                                max_iters=args.npmi_steps, **kw)
+    q = {}
+    if rank == 0:
+        c = out["clients"][0]
+        q["npmi"] = _npmi(c.tm, sc, _union_terms(sc, n_clients), n_clients, device)
+        if args.family == "avitm":
+            c.ground_truth = (np.asarray(sc.doc_topics[c.id - 1]), np.asarray(sc.topic_vectors))
+            betas, thetas, _ = c.results()
+            ev = c.evaluate_synthetic(betas, thetas)
+            q["tss_client1"] = round(ev["tss"], 4)
+            q["dss_client1"] = round(ev["dss"], 4)
+    return q
+
+
 def run_federated(args):
     from gfedntm_amd.federation.runner import CommError, run_distributed
-    if args.clients_per_gpu > 1:
-        return run_multi(args)
     rank, world, device, rehearse = _init(args)
     _ctrl_group()
+    if total_clients(args, world) != world:
+        return run_multi(args, rank, world, device, rehearse)
     physical = _physical_gpus(device, world)
     sc = _corpus(args, world)
     corpus = _client_corpus(args, sc, rank)
@@ -313,7 +375,8 @@ def run_federated(args):
     # ---- timed: the production round loop ----
     fallback = None
     try:
-        out = run_distributed(corpus, max_iters=n_rounds, timing_warmup=args.warmup, **kw)
+        out = run_distributed(corpus, max_iters=n_rounds, timing_warmup=args.warmup,
+                              keep_round=True, **kw)
     except CommError as e:
         # every rank raised the same agreed error: an xGMI wait timed out.  With the data
         # plane left to auto-selection, measure the same federation over RCCL instead (and
@@ -326,7 +389,9 @@ def run_federated(args):
         kw["allreduce"] = "rccl"
         # a failure injection (tests) belongs to the failed attempt, not the re-measure
         os.environ.pop("GFEDNTM_INJECT_STALL", None)
-        out = run_distributed(corpus, max_iters=n_rounds, timing_warmup=args.warmup, **kw)
+        os.environ.pop("GFEDNTM_INJECT_CORRUPT", None)
+        out = run_distributed(corpus, max_iters=n_rounds, timing_warmup=args.warmup,
+                              keep_round=True, **kw)
     client = out["client"]
     eng = client.tm.engine
     wall = _max_over_ranks(out["wall_s"], world)
@@ -355,21 +420,20 @@ def run_federated(args):
     final_loss = float(np.mean(eng.loss_hist[max(0, n_rounds - 20): n_rounds].cpu().numpy()))
     if args.backend == "fused":
         eng.detach_fedavg()
-    # ---- NPMI: a separate untimed federation of a fixed number of rounds ----
-    npmi = None
-    if not args.no_npmi and args.npmi_steps > 0:
-        out2 = run_distributed(corpus, max_iters=args.npmi_steps, **kw)
-        if rank == 0:
-            npmi = _npmi(out2["client"].tm, sc, _union_terms(sc, world), world, device)
-        if args.backend == "fused":
-            out2["client"].tm.engine.detach_fedavg()
+    # ---- quality: a separate untimed federation of a fixed number of rounds ----
+    quality = _quality(args, [corpus], [rank + 1], sc, world, rank, device,
+                       {k: v for k, v in kw.items() if k not in ("params", "model_type")})
+    npmi = quality.get("npmi")
     if rank == 0:
         value = docs / wall
         terms_n = len(client.tm.train_data.idx2token) if hasattr(client.tm.train_data, "idx2token") \
             else client.tm.input_size
+        out_digests = out.get("digests")
         record = _record(args, value, ms_runner, terms_n, npmi, final_loss, clients=world,
                          ranks=world, physical=physical)
+        record.update({k: v for k, v in quality.items() if k != "npmi"})
         record["path"] = args.path
+        record["digests"] = out_digests
         if fallback:
             record["allreduce_fallback"] = fallback
         record["device_ms_per_step"] = None if dev_s is None else round(dev_s / max(timed_rounds, 1) * 1e3, 5)
@@ -456,9 +520,9 @@ def _is_headline(args) -> bool:
 
 
 def _metric(args, V, clients: int, ranks: int, physical: int) -> str:
-    """BASELINE.json's metric string for the headline config (one client per GPU);
-    otherwise a label derived from what actually ran."""
-    if _is_headline(args) and clients == ranks and physical == ranks:
+    """BASELINE.json's metric string for the headline config -- exactly 8 federated clients,
+    each rank on its own GPU; otherwise a label derived from what actually ran."""
+    if _is_headline(args) and clients == 8 and physical == ranks:
         return METRIC
     fam = {"avitm": "ProdLDA" if args.model == "prodLDA" else "NeuralLDA",
            "ctm": "CombinedTM", "zeroshot": "ZeroShotTM"}[args.family]
@@ -493,7 +557,9 @@ def _record(args, value, ms, V, npmi, final_loss, clients: int, ranks: int, phys
         "warmup": args.warmup,
         "ms_per_step": round(ms, 5),
         "higher_is_better": True,
-        "scaling": "weak",
+        # --clients (default): the 8-client federation whatever N -- total work fixed;
+        # --clients-per-gpu: M clients on every GPU -- per-GPU work fixed
+        "scaling": "weak" if args.clients_per_gpu else "strong",
         # only the headline config is comparable with the reference's 8-client number
         "vs_baseline": round(value / BASELINE_FED_DOCS_PER_S, 2) if headline else None,
         "dtype": args.dtype,
@@ -508,9 +574,10 @@ def _record(args, value, ms, V, npmi, final_loss, clients: int, ranks: int, phys
                    "backend": args.backend + ("" if args.no_graph else "+hipgraph"),
                    "solver": args.solver,
                    "aggregation": "per-minibatch sample-weighted FedAvg of the shared state"},
-        "clients_note": ("one client: FedAvg over one client is the identity; the 8-client "
-                         "figure is the --gpus 8 run" if clients == 1 else
-                         f"{clients} federated clients on {physical} physical GPU(s)"),
+        "clients_note": (f"{clients} federated client(s) on {ranks} rank(s) / {physical} "
+                         f"physical GPU(s): every round all {clients} clients do one local "
+                         "minibatch step and the sample-weighted FedAvg of their shared state "
+                         "replaces every client's copy"),
         **({"precision": "bf16 operands of the ProdLDA decoder GEMMs (theta.beta, theta^T.dlogit, "
                          "dlogit.beta^T) on v_mfma_f32_16x16x32_bf16, fp32 accumulation; fp32 "
                          "parameters, Adam state and every other op"} if args.dtype == "bf16" else {}),
@@ -532,6 +599,8 @@ def run(args):
 def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
     args = parse(argv)
+    if args.clients_per_gpu is None and args.clients < 1:
+        raise SystemExit("--clients must be >= 1")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.sim_clients:
         # self-launch: one rank per GPU, spawned before this process touches the GPU
         import torch.multiprocessing as mp

@@ -296,18 +296,109 @@ extern "C" int gfk_local_fedavg_launch(const GfkLocalAvg* a, int grid, hipStream
 }
 
 // ---------------------------------------------------------------------------
+// Cross-rank state digest (failure detection of the data plane, federation/runner.py).
+// After a round's FedAvg every rank must hold the SAME shared state bit for bit (each
+// chunk is summed by exactly one rank).  A stale peer line, a lost write-back or a
+// broken IPC mapping would instead leave the replicas silently diverged; the ranks
+// therefore compare a digest of their shared prefix every few hundred rounds and at
+// every aligned round:
+//     D = sum over i of mix(i << 32 | bits(x_i))   (mod 2^64, mix = splitmix64's finaliser)
+// Position-sensitive, and a sum mod 2^64 is order-independent, so the per-workgroup
+// partials and their fold give the same value however the grid is cut -- the numpy
+// re-statement in parallel/digest.py computes it bit for bit (CPU ranks, tests).
+// Two launches on the stream behind the round (partials, then a one-workgroup fold),
+// no atomics; the 8-byte result is copied to pinned host memory asynchronously.
+// ---------------------------------------------------------------------------
+namespace {
+__device__ __forceinline__ uint64_t dg_mix(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ uint64_t dg_word(int64_t i, uint32_t w) {
+  return dg_mix(((uint64_t)i << 32) | w);
+}
+
+// block-wide sum of one uint64 per thread (256 threads), result in thread 0
+__device__ __forceinline__ uint64_t dg_block_sum(uint64_t v, uint64_t* red) {
+  const int t = threadIdx.x;
+  red[t] = v;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (t < s) red[t] += red[t + s];
+    __syncthreads();
+  }
+  return red[0];
+}
+}  // namespace
+
+extern "C" __global__ void __launch_bounds__(256)
+gfk_digest_part(const uint32_t* __restrict__ w, int64_t n, uint64_t* __restrict__ part) {
+  __shared__ uint64_t red[256];
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  const int64_t n4 = n >> 2;
+  uint64_t acc = 0;
+  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < n4; q += stride) {
+    const uint4 v = reinterpret_cast<const uint4*>(w)[q];
+    const int64_t i = q << 2;
+    acc += dg_word(i, v.x) + dg_word(i + 1, v.y) + dg_word(i + 2, v.z) + dg_word(i + 3, v.w);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+    const int64_t i = (n4 << 2) + threadIdx.x;
+    acc += dg_word(i, w[i]);
+  }
+  const uint64_t s = dg_block_sum(acc, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+extern "C" __global__ void __launch_bounds__(256)
+gfk_digest_fold(const uint64_t* __restrict__ part, int nblk, uint64_t* __restrict__ out) {
+  __shared__ uint64_t red[256];
+  uint64_t acc = 0;
+  for (int b = threadIdx.x; b < nblk; b += 256) acc += part[b];
+  const uint64_t s = dg_block_sum(acc, red);
+  if (threadIdx.x == 0) out[0] = s;
+}
+
+// digest of n words at w (16-byte aligned) into out[0]; part: nblk uint64 of scratch;
+// host (pinned, optional): the result copied there behind the two kernels
+extern "C" int gfk_digest_launch(const void* w, int64_t n, void* part, int nblk, void* out,
+                                 void* host, hipStream_t s) {
+  if (!w || !part || !out || n < 0 || nblk < 1 || ((uintptr_t)w & 15)) return -1;
+  hipLaunchKernelGGL(gfk_digest_part, dim3(nblk), dim3(256), 0, s,
+                     static_cast<const uint32_t*>(w), n, static_cast<uint64_t*>(part));
+  hipLaunchKernelGGL(gfk_digest_fold, dim3(1), dim3(256), 0, s,
+                     static_cast<const uint64_t*>(part), nblk, static_cast<uint64_t*>(out));
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess && host)
+    e = hipMemcpyAsync(host, out, sizeof(uint64_t), hipMemcpyDeviceToHost, s);
+  return (int)e;
+}
+
+// ---------------------------------------------------------------------------
 // host API (ctypes)
 // ---------------------------------------------------------------------------
 extern "C" size_t gfk_comm_struct_size() { return sizeof(GfkComm); }
 
+// The kernel addresses the stage (or, in place, the data) through buffer descriptors with
+// 32-bit byte offsets: a state must stay below this many bytes (XgmiAllReduce refuses
+// larger ones, and the caller keeps RCCL for them).
+extern "C" int64_t gfk_comm_max_bytes() { return ((int64_t)1 << 31) - 64; }
+
 // stage: 2 * stage_bytes (regular); flags: uncached, zeroed; state: epoch[nblk] + err, zeroed.
+// *uncached = 1 if the flag array got uncached memory, 0 if it fell back to hipMalloc (the
+// flags' L2 write-backs in publish() then carry the protocol alone; recorded by the caller).
 extern "C" int gfk_comm_alloc(int64_t stage_bytes, int64_t flag_bytes, int64_t state_bytes,
-                              void** stage, void** flags, void** state) {
+                              void** stage, void** flags, void** state, int* uncached) {
   hipError_t e;
   if ((e = hipMalloc(stage, 2 * stage_bytes))) return (int)e;
   if ((e = hipMemset(*stage, 0, 2 * stage_bytes))) return (int)e;
+  *uncached = 1;
   if (hipExtMallocWithFlags(flags, flag_bytes, hipDeviceMallocUncached) != hipSuccess) {
     (void)hipGetLastError();
+    *uncached = 0;
     if ((e = hipMalloc(flags, flag_bytes))) return (int)e;
   }
   if ((e = hipMemset(*flags, 0, flag_bytes))) return (int)e;
@@ -346,7 +437,8 @@ extern "C" int gfk_ipc_get_range(void* ptr, void* handle, int64_t* offset) {
   return (int)hipIpcGetMemHandle(reinterpret_cast<hipIpcMemHandle_t*>(handle), base);
 }
 
-// The error word (0 = fine, 1 / 2 = a phase-0 / phase-1 wait timed out); synchronous.
+// The error word (0 = fine; 1 / 2 / 3 = a phase-0 / phase-1 / in-place phase-3 wait timed
+// out: 1 + the phase's flag row); synchronous.
 extern "C" int gfk_comm_error(const GfkComm* c) {
   int32_t v = 0;
   if (hipMemcpy(&v, c->err, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) return -1;
@@ -372,7 +464,7 @@ extern "C" int gfk_comm_error_async(const GfkComm* c, int32_t* host, hipStream_t
 extern "C" int gfk_comm_launch(const GfkComm* c, float* data, hipStream_t s) {
   if (c->world < 1 || c->world > CMAX || c->nblk < 1 || (c->chunk & 3) || (c->slice & 3) ||
       (int64_t)c->slice * c->nblk < c->chunk || (int64_t)c->chunk * c->world < c->n ||
-      ((uintptr_t)data & 15))
+      ((uintptr_t)data & 15) || (int64_t)c->world * c->chunk * 4 > gfk_comm_max_bytes())
     return -1;
   hipLaunchKernelGGL(gfk_xgmi_allreduce, dim3(c->nblk), dim3(CT), 0, s, *c, data);
   return (int)hipGetLastError();

@@ -544,10 +544,27 @@ __global__ void __launch_bounds__(WCT, 4) gfk_win_ctx_pp_k(GfkArgT<GB> ga) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int e = 4 * (tid + WCT * u);
-      const uint32_t off = wc0 + ((uint32_t)v0 * (uint32_t)H0 + (uint32_t)min(e, max(nel - 4, 0))) * 4u;
-      P[3 * u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_p, off, 0, 0));
-      P[3 * u + 1] = fused ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_m, off, 0, 0)) : z4;
-      P[3 * u + 2] = fused ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_v, off, 0, 0)) : z4;
+      // the thread's own quad, at the offset do_blk stores it to: whole quads as 128-bit
+      // loads, the block's partial last quad (nel % 4 != 0: odd word counts at H0 = 50)
+      // element by element, nothing past the block's run
+      const uint32_t off = wc0 + ((uint32_t)v0 * (uint32_t)H0 + (uint32_t)e) * 4u;
+      if (e + 3 < nel) {
+        P[3 * u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_p, off, 0, 0));
+        P[3 * u + 1] = fused ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_m, off, 0, 0)) : z4;
+        P[3 * u + 2] = fused ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_v, off, 0, 0)) : z4;
+      } else {
+        P[3 * u] = P[3 * u + 1] = P[3 * u + 2] = z4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (e + i < nel) {
+            P[3 * u][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_p, off + 4 * i, 0, 0));
+            if (fused) {
+              P[3 * u + 1][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_m, off + 4 * i, 0, 0));
+              P[3 * u + 2][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_v, off + 4 * i, 0, 0));
+            }
+          }
+        }
+      }
       const int i = tid + WCT * u, b = i >> 4, q = i & 15, v = v0 + 4 * q;
       A[u] = (b < B && 4 * q < nw)
                  ? *reinterpret_cast<const f32x4*>(m.ws_actx + ((size_t)(v >> 6) * B + b) * 64 + (v & 63))

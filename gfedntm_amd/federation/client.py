@@ -69,6 +69,10 @@ class FederatedClient:
             tm.engine.own_rng(seed)
         tm.model.train()
         self.weight: Optional[float] = None
+        # synthetic ground truth (doc-topic, topic-word over the generator vocabulary):
+        # scored at every results save, like the reference's evaluate_synthetic_model
+        self.ground_truth = None
+        self.synthetic_eval: Optional[dict] = None
         # reference bookkeeping
         self.current_mb = 0
         self.current_epoch = 0
@@ -264,7 +268,29 @@ class FederatedClient:
         was_training = self.tm.model.training
         save_model_as_npz(path, betas, thetas, self.tm.n_components, topics)
         self.tm.model.train(was_training)
+        if self.ground_truth is not None:
+            self.evaluate_synthetic(betas, thetas)
         return path
+
+    def evaluate_synthetic(self, betas: np.ndarray, thetas: np.ndarray) -> dict:
+        """TSS / DSS of this client's model against the generator's ground truth, logged
+        with the reference's lines (federated_avitm.py:152-193 evaluate_synthetic_model):
+        the learned topic-word matrix re-indexed onto the generator vocabulary ('wd<j>' ->
+        column j, auxiliary_functions.py:441-483), TSS = sum over ground-truth topics of
+        the best Bhattacharyya coefficient, DSS = mean |sqrt(theta) sqrt(theta)^T
+        difference| over this client's documents."""
+        from ..eval.metrics import betas_to_ground_truth_vocab, dss, tss
+        gt_thetas, gt_betas = self.ground_truth
+        id2token = getattr(self.dataset, "idx2token", None) or \
+            {i: t for i, t in enumerate(getattr(self.tm, "id2token", {}) or {})}
+        b = betas_to_ground_truth_vocab(np.asarray(betas), id2token, gt_betas.shape[1])
+        th = thetas.toarray() if hasattr(thetas, "toarray") else np.asarray(thetas)
+        t_score = tss(b, gt_betas)
+        d_score = dss(gt_thetas[: th.shape[0]], th)
+        self.logger.info("-- -- Tópicos (equivalentes) evaluados correctamente: %s", t_score)
+        self.logger.info("-- -- Difference in evaluation of doc similarity: %s", d_score)
+        self.synthetic_eval = {"tss": float(t_score), "dss": float(d_score)}
+        return self.synthetic_eval
 
     def loss_history(self) -> np.ndarray:
         return self.tm.engine.loss_hist.detach().cpu().numpy()

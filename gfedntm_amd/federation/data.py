@@ -39,6 +39,16 @@ class ClientCorpus:
             return self.synthetic.counts[self.node].shape[0]
         return len(self.texts)
 
+    def ground_truth(self):
+        """(doc-topic [D, K], topic-word [K, V_gen]) of the generator, or None: explicit
+        fields (loaded files) or the node of an in-memory synthetic corpus."""
+        if self.ground_truth_thetas is not None and self.ground_truth_betas is not None:
+            return np.asarray(self.ground_truth_thetas), np.asarray(self.ground_truth_betas)
+        if self.synthetic is not None and getattr(self.synthetic, "topic_vectors", None) is not None:
+            return (np.asarray(self.synthetic.doc_topics[self.node]),
+                    np.asarray(self.synthetic.topic_vectors))
+        return None
+
     def local_terms(self) -> List[str]:
         if self.synthetic is not None:
             return sorted(node_vocabulary_terms(self.synthetic, self.node))

@@ -391,6 +391,7 @@ def run_client(corpus, client_id: int, server_address: str, port: int, backend: 
                                  logger=logger, seed=seed + client_id, save_path=path,
                                  log_every=log_every,
                                  epoch_snapshots=(fu.model_type in ("ctm", "zeroshot")))
+        client.ground_truth = corpus.ground_truth()
         client.enable_graph(graph)
         impl = ClientServicer(client, logger)
         server = grpc.server(cf.ThreadPoolExecutor(max_workers=2), options=list(server_options))

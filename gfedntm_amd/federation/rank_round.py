@@ -135,7 +135,8 @@ class MultiClientRound:
                            "bytes": {k: 4 * (b - a) for k, (a, b) in self.parts.items()},
                            "inplace": {k: c.xgmi is not None and c.xgmi.data is not None
                                        for k, c in self.colls.items()},
-                           "tuning": {k: c.tuning for k, c in self.colls.items() if c.tuning}}
+                           "tuning": {k: c.tuning for k, c in self.colls.items() if c.tuning},
+                           "plane": {k: c.describe() for k, c in self.colls.items()}}
         self.coll_in_graph = bool(self.colls) and all(c.xgmi is not None for c in self.colls.values())
         if not self.coll_in_graph and len(self.parts) > 1:
             # one RCCL all-reduce of the whole state after the round graph

@@ -143,6 +143,7 @@ class LocalFederation:
                                 save_path=path, log_every=log_every,
                                 epoch_snapshots=(model_type in CTM_TYPES), agg=agg)
             c.set_fedavg_weight(self.weights[i])
+            c.ground_truth = corpora[i].ground_truth()
             c.enable_graph(graph and agg == "params")
             self.clients.append(c)
         # groups: client-block sizes of a multi-rank layout (hierarchical/run_distributed_multi)
@@ -367,7 +368,8 @@ def run_distributed(corpus, params: Dict, model_type: str = "avitm",
                     metrics_every: int = 0, heartbeat_timeout: float = 0.0,
                     agg_mode: str = "params", timing_warmup: int = 0,
                     rehearse_1gpu: Optional[bool] = None, allreduce: Optional[str] = None,
-                    round_hook=None, client_ids: Optional[Sequence[int]] = None) -> Dict:
+                    round_hook=None, client_ids: Optional[Sequence[int]] = None,
+                    keep_round: bool = False) -> Dict:
     """Runs this process's client(s); torch.distributed must be initialised (RANK /
     WORLD_SIZE).  ``corpus`` is this rank's one client (id rank + 1), or a list of client
     corpora with their ids ``client_ids`` -- a contiguous block of a federation of more
@@ -396,7 +398,21 @@ def run_distributed(corpus, params: Dict, model_type: str = "avitm",
     reported wall time (bench).  ``round_hook(it)`` is called after every round
     (tests inject host stalls with it).  ``GFEDNTM_INJECT_STALL=rank:round:seconds``
     injects one such stall from the environment (failure-injection tests of processes
-    this code does not start itself, e.g. bench.py's ranks)."""
+    this code does not start itself, e.g. bench.py's ranks).
+
+    Cross-rank state check (parallel/digest.py): every ``GFEDNTM_DIGEST_EVERY`` rounds
+    (default: the poll interval) each rank digests its clients' shared state behind the
+    round (two small kernels + an 8-byte copy, no sync) and the ranks compare the digests
+    at the next interval; at the start (W0), at every aligned round and at the end they
+    compare synchronously.  A mismatch -- replicas that silently diverged although every
+    wait returned -- stops every rank with :class:`CommError`.
+    ``GFEDNTM_INJECT_CORRUPT=rank:round`` flips one word of that rank's shared state after
+    every round from ``round`` on (a persistent data-plane fault; a one-off divergence is
+    re-averaged by the next all-reduce and leaves the replicas equal again).
+
+    ``keep_round``: leave the rank's data plane attached after the run (the caller closes
+    ``out["round"]``; bench.py times the bare engine loop on it); by default it is
+    released before returning, on success or error."""
     import torch.distributed as dist
     from .hierarchical import agree_client_map
     from .rank_round import MultiClientRound, SingleClientRound
@@ -471,6 +487,7 @@ def run_distributed(corpus, params: Dict, model_type: str = "avitm",
                             save_path=path, log_every=log_every,
                             epoch_snapshots=(model_type in CTM_TYPES), agg=agg_mode)
         c.set_fedavg_weight(weights[cid - 1])
+        c.ground_truth = corp.ground_truth()
         c.enable_graph(graph and agg_mode == "params")
         clients.append(c)
     # ---- data plane: this rank's round (its clients' steps + the FedAvg) ----
@@ -479,6 +496,41 @@ def run_distributed(corpus, params: Dict, model_type: str = "avitm",
                                bucket_bytes, logger)
     else:
         rr = MultiClientRound(clients, world, device, on_gpu_plane, allreduce, graph, logger)
+    ok = False
+    try:
+        out = _round_loop(rr, clients, client_ids, cmap, world, rank, device, ctrl, hb, logger,
+                          max_iters, stop_at_num_epochs, checkpoint_dir, checkpoint_every,
+                          metrics, metrics_every, timing_warmup, round_hook, agg_mode,
+                          save_server, stamp)
+        ok = True
+        return out
+    finally:
+        if hb is not None:
+            hb.stop()
+        if not (ok and keep_round):
+            rr.close()
+
+
+def _inject_corrupt(rank: int):
+    """GFEDNTM_INJECT_CORRUPT=rank:round -> the first round it applies on this rank."""
+    inj = os.environ.get("GFEDNTM_INJECT_CORRUPT")
+    if not inj:
+        return None
+    r_s, it_s = inj.split(":")[:2]
+    return int(it_s) if int(r_s) == rank else None
+
+
+def _flip_word(t: torch.Tensor):
+    """Flip the low bit of the middle word of a shared state (enqueued on the stream)."""
+    j = t.numel() // 2
+    t.view(torch.int32)[j:j + 1].bitwise_xor_(1)
+
+
+def _round_loop(rr, clients, client_ids, cmap, world, rank, device, ctrl, hb, logger, max_iters,
+                stop_at_num_epochs, checkpoint_dir, checkpoint_every, metrics, metrics_every,
+                timing_warmup, round_hook, agg_mode, save_server, stamp) -> Dict:
+    import torch.distributed as dist
+    from ..parallel.digest import DigestProbe, compare
     start = 0
     if checkpoint_dir:
         starts = {ckpt.load_client_checkpoint(checkpoint_dir, c) for c in clients}
@@ -506,12 +558,40 @@ def run_distributed(corpus, params: Dict, model_type: str = "avitm",
     def fail(err: int, where: str):
         if os.environ.get("GFEDNTM_COMM_DEBUG") == "1":
             logger.warning("rank %d xGMI state: %s", rank, rr.debug())
-        rr.close()                 # release the IPC mappings / step graph before raising
-        if hb is not None:
-            hb.stop()
+        # (the IPC mappings / step graph are released by run_distributed's finally)
         raise CommError(f"rank {rank}: an xGMI all-reduce wait timed out before {where} "
                         f"(error {err}); the shared state is invalid -- resume from the last "
                         "round checkpoint")
+
+    # ---- cross-rank digests of the shared state (parallel/digest.py) ----
+    poll_default = os.environ.get("GFEDNTM_COMM_POLL", "512")
+    digest_every = (int(os.environ.get("GFEDNTM_DIGEST_EVERY", poll_default))
+                    if world > 1 and agg_mode == "params" else 0)
+    probe = DigestProbe([c.shared for c in clients]) if digest_every else None
+    corrupt_from = _inject_corrupt(rank)
+    dstats = {"checked": 0, "last": None}
+
+    def digest_check(res):
+        """All-gather every rank's (round, digests) and agree: raise on a divergence."""
+        if res is None:
+            return
+        per_rank: List = [None] * world
+        dist.all_gather_object(per_rank, res, group=ctrl)
+        why = compare(per_rank, rank)
+        if why is not None:
+            logger.error("rank %d: %s", rank, why)
+            raise CommError(f"rank {rank}: {why}; the shared state is invalid -- resume from "
+                            "the last round checkpoint")
+        dstats["checked"] += 1
+        dstats["last"] = (per_rank[0][0], f"{per_rank[0][1][0]:016x}")
+
+    def digest_now(it: int):
+        """Synchronous digest of round ``it`` (the device must be synchronised)."""
+        if probe is None:
+            return
+        digest_check(probe.result())      # a pending asynchronous one first
+        probe.take(it)
+        digest_check(probe.result())
 
     def check_comm(where: str):
         """Agree on the xGMI error word across ranks (synchronises the device)."""
@@ -539,6 +619,9 @@ def run_distributed(corpus, params: Dict, model_type: str = "avitm",
         dist.barrier(group=ctrl)
 
     dist.barrier(group=ctrl)
+    if probe is not None:
+        sync()
+        digest_now(start - 1)            # identical W0 (or resumed state) on every rank
     # GFEDNTM_COMM_DEBUG=1: the first rounds synchronised one by one, with their times and
     # the xGMI error word (which round a timed-out wait happened in, and the ranks' skew)
     debug_comm = os.environ.get("GFEDNTM_COMM_DEBUG") == "1" and rr.xgmi
@@ -556,6 +639,8 @@ def run_distributed(corpus, params: Dict, model_type: str = "avitm",
             if hb is not None:
                 hb.mark(it, 0)
             rr.step(it, hb)
+            if corrupt_from is not None and it >= corrupt_from:
+                _flip_word(clients[0].shared)
             if debug_comm and it < start + 16:
                 t_dbg = time.perf_counter()
                 sync()
@@ -567,6 +652,7 @@ def run_distributed(corpus, params: Dict, model_type: str = "avitm",
                 # validate the state before anything is exported
                 sync()
                 check_comm(f"the host work of round {it}")
+                digest_now(it)
                 if hb is not None:
                     hb.busy(True)
             for c in clients:
@@ -578,6 +664,10 @@ def run_distributed(corpus, params: Dict, model_type: str = "avitm",
                 dist.barrier(group=ctrl)
             if poll_every and (it + 1) % poll_every == 0 and it != stop_after:
                 poll_comm(it)
+            if digest_every and (it + 1) % digest_every == 0 and it != stop_after and not heavy:
+                # the previous interval's digest (landed long ago), then this round's
+                digest_check(probe.result())
+                probe.take(it)
             if round_hook is not None:
                 round_hook(it)
             win.add(sum(int(c.plan.size[it]) for c in clients))
@@ -608,6 +698,7 @@ def run_distributed(corpus, params: Dict, model_type: str = "avitm",
     wall = time.perf_counter() - t0
     device_s = ev[0].elapsed_time(ev[1]) * 1e-3 if ev is not None and timed_from > start else None
     check_comm("the end of training")
+    digest_now(last)
     for c in clients:
         c.flush()
     n_rounds = last + 1 - timed_from
@@ -624,8 +715,7 @@ def run_distributed(corpus, params: Dict, model_type: str = "avitm",
         save_model_as_npz(server_model_path(save_server, stamp), tm0.get_topic_word_distribution(),
                           None, tm0.n_components, None)
     dist.barrier(group=ctrl)
-    if hb is not None:
-        hb.stop()
     return {"rounds": last + 1, "timed_rounds": n_rounds, "wall_s": wall, "docs": docs,
             "device_s": device_s, "client": clients[0], "clients": clients, "client_map": cmap,
-            "allreduce": rr.method, "attach": rr.attach, "round": rr}
+            "allreduce": rr.method, "attach": rr.attach, "round": rr,
+            "digests": dict(dstats, every=digest_every)}

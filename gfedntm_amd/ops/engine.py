@@ -977,7 +977,10 @@ class FusedEngine(EngineBase):
         # setup cost of the data plane (IPC mapping, validation, RCCL-vs-xGMI timing)
         self.fedavg_attach = {"s": round(sum(a.setup_s for a in aggs.values()), 4),
                               "bytes": {k: 4 * v.numel() for k, v in parts.items()},
-                              "tuning": {k: a.tuning for k, a in aggs.items() if a.tuning}}
+                              "tuning": {k: a.tuning for k, a in aggs.items() if a.tuning},
+                              # per part: method, in-place, uncached flags (csrc/comm.hip
+                              # gfk_comm_alloc) or why it is not on the xGMI kernel
+                              "plane": {k: a.describe() for k, a in aggs.items()}}
         if all(m == "xgmi" for m in methods.values()):
             c = {"mode": "graph", **{k: (aggs[k], parts[k]) for k in parts}}
             if len(parts) > 1:

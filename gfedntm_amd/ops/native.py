@@ -50,14 +50,23 @@ def kernels() -> ctypes.CDLL:
     return _kernels
 
 
-def _embedded_hash(lib) -> Optional[str]:
+def _embedded_str(lib, name: str) -> Optional[str]:
     try:
-        f = lib.gfk_source_hash
+        f = getattr(lib, name)
     except AttributeError:
         return None
     f.restype = ctypes.c_char_p
     f.argtypes = []
     return f().decode()
+
+
+def _embedded_hash(lib) -> Optional[str]:
+    return _embedded_str(lib, "gfk_source_hash")
+
+
+def build_arch(lib=None) -> Optional[str]:
+    """The offload arch the kernel library was compiled for (embedded by the build)."""
+    return _embedded_str(lib if lib is not None else kernels(), "gfk_build_arch")
 
 
 def _check_source(lib) -> None:
@@ -66,7 +75,10 @@ def _check_source(lib) -> None:
     if not os.path.isdir(srchash.CSRC):
         return                       # no sources next to the package: nothing to compare
     got = _embedded_hash(lib)
-    want = srchash.source_hash(os.environ.get("PYTORCH_ROCM_ARCH", "gfx950"))
+    # the hash covers the arch the library was built for (embedded next to it), not the
+    # PYTORCH_ROCM_ARCH of the loading process
+    arch = _embedded_str(lib, "gfk_build_arch") or os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+    want = srchash.source_hash(arch)
     if got == want:
         return
     if KERNELS_SO_OVERRIDE:

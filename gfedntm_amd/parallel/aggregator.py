@@ -51,6 +51,7 @@ class CollectiveAggregator:
         self.active = "rccl"
         self.tuning = None
         self.setup_s = 0.0
+        self.fallback_reason = None      # why "auto" / "xgmi" did not get the xGMI kernel
 
     def prepare(self, flat: torch.Tensor, inplace: bool = False) -> str:
         """Choose the all-reduce for buffers shaped like ``flat`` (call once, on every
@@ -79,7 +80,9 @@ class CollectiveAggregator:
                                    data=flat if inplace else None)
             except Exception as e:   # every rank must reach the agreement below
                 import logging
-                logging.getLogger("gfedntm_amd.xgmi").warning("xGMI all-reduce setup failed: %s", e)
+                logging.getLogger("gfedntm_amd.xgmi").warning(
+                    "xGMI all-reduce setup failed (RCCL instead): %s", e)
+                self.fallback_reason = f"setup: {e}"
                 xg = None
         flags: List = [None] * self.world
         dist.all_gather_object(flags, xg is not None, group=self.group)
@@ -116,6 +119,9 @@ class CollectiveAggregator:
         if ok:
             self.xgmi, self.active = xg, "xgmi"
         else:
+            if self.fallback_reason is None:
+                self.fallback_reason = ("not one node of <= 8 ranks" if xg is None and self.world > 8
+                                        else "measured slower than RCCL or failed validation")
             if xg is not None:
                 xg.close()
             if self.method == "xgmi":
@@ -137,6 +143,17 @@ class CollectiveAggregator:
             fn(buf)
         torch.cuda.synchronize(like.device)
         return (time.perf_counter() - t0) / iters * 1e3
+
+    def describe(self) -> dict:
+        """What the data plane of this buffer is (for the fedavg_attach records)."""
+        d = {"method": self.active}
+        if self.xgmi is not None:
+            d["inplace"] = self.xgmi.data is not None
+            d["flags_uncached"] = self.xgmi.flags_uncached
+            d["nblk"] = self.xgmi.nblk
+        elif self.fallback_reason:
+            d["fallback"] = self.fallback_reason
+        return d
 
     def weights(self, n_local: int, device) -> List[float]:
         t = torch.tensor([float(n_local)], dtype=torch.float64, device=device)

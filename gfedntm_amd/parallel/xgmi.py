@@ -46,7 +46,8 @@ def _declare(lib):
         return
     lib.gfk_comm_struct_size.restype = C.c_size_t
     lib.gfk_comm_alloc.argtypes = [C.c_int64, C.c_int64, C.c_int64, C.POINTER(P), C.POINTER(P),
-                                   C.POINTER(P)]
+                                   C.POINTER(P), C.POINTER(C.c_int)]
+    lib.gfk_comm_max_bytes.restype = C.c_int64
     lib.gfk_comm_free.argtypes = [P, P, P]
     lib.gfk_ipc_get.argtypes = [P, P]
     lib.gfk_ipc_open.argtypes = [P, C.POINTER(P)]
@@ -61,10 +62,13 @@ def _declare(lib):
     lib._gfk_comm_declared = True
 
 
-# peer allocations mapped into this process, keyed by (exporter pid, exporter base address):
+# peer allocations mapped into this process, keyed by (exporter pid, IPC handle bytes):
 # two all-reduces whose in-place parts are slices of ONE caching-allocator block (the
-# 'rest' and 'beta' parts of a flat state) share one mapping, refcounted, instead of
-# opening the same memory twice and unmapping it under the other on close()
+# 'rest' and 'beta' parts of a flat state) export the same allocation and share one
+# mapping, refcounted, instead of opening the same memory twice and unmapping it under
+# the other on close().  The handle identifies the allocation, not its address: a block
+# the exporter freed and reallocated at the same address gets a new handle, so a later
+# all-reduce never reuses a stale mapping (tests/test_xgmi_allreduce.py pins both)
 _IPC_OPEN = {}
 
 
@@ -117,6 +121,12 @@ class XgmiAllReduce:
             # healthy skew; GFEDNTM_XGMI_SPIN lowers it (failure-injection tests)
             spin_limit = int(os.environ.get("GFEDNTM_XGMI_SPIN", str(1 << 28)))
         chunk = _up4(-(-self.n // self.world))
+        # 32-bit buffer offsets in the kernel (csrc/comm.hip rsrc / ld_sys / st_sys): a
+        # larger state is refused here and the caller keeps RCCL for it (logged there)
+        limit = int(self.lib.gfk_comm_max_bytes())
+        if 4 * self.world * chunk > limit:
+            raise ValueError(f"xGMI all-reduce: {4 * self.world * chunk} B of stage exceed the "
+                             f"kernel's 32-bit offset range ({limit} B)")
         if nblk is None:
             nblk = self.grid_for(chunk, self.device, group)
         self.nblk = nblk
@@ -128,13 +138,16 @@ class XgmiAllReduce:
                         or data.numel() != self.n or data.data_ptr() % 16):
             raise ValueError("xGMI in-place buffer: fp32, contiguous, 16-B aligned, n floats")
         with torch.cuda.device(self.device):
-            stage, flags, state = P(), P(), P()
+            stage, flags, state, unc = P(), P(), P(), C.c_int(0)
             stage_bytes = 16 if inplace else self.world * chunk * 4
             flag_bytes = (3 if inplace else 2) * nblk * CMAX * 4
             rc = self.lib.gfk_comm_alloc(stage_bytes, flag_bytes, nblk * 4 + 16,
-                                         C.byref(stage), C.byref(flags), C.byref(state))
+                                         C.byref(stage), C.byref(flags), C.byref(state),
+                                         C.byref(unc))
             if rc:
                 raise RuntimeError(f"gfk_comm_alloc failed ({rc})")
+            # uncached flag memory (hipDeviceMallocUncached) or the cached fallback
+            self.flags_uncached = bool(unc.value)
             self._own = (stage.value, flags.value, state.value)
             hs = self.lib.gfk_ipc_handle_size()
             mine = []
@@ -150,8 +163,8 @@ class XgmiAllReduce:
                     rc = self.lib.gfk_ipc_get(P(ptr), h)
                 if rc:
                     raise RuntimeError(f"hipIpcGetMemHandle failed ({rc})")
-                # (handle, identity of the exported allocation: pid + its base address)
-                mine.append((h.raw, (pid, ptr - (offset if not mine else 0))))
+                # (handle, identity of the exported allocation: pid + its handle)
+                mine.append((h.raw, (pid, h.raw)))
             mine.append(offset)
             allh: List = [None] * self.world
             dist.all_gather_object(allh, mine, group=group)

@@ -91,7 +91,8 @@ def _worker(rank, world, port, tmp, stall, spin, q, poll=None, rounds=ROUNDS, ep
             corpus = (_corpora_large() if large else _corpora())[rank]
             out = run_distributed(corpus, params, max_iters=rounds, backend="fused",
                                   seed=5, save_client=os.path.join(tmp, "client"),
-                                  stamp="20240101", rehearse_1gpu=True, round_hook=hook)
+                                  stamp="20240101", rehearse_1gpu=True, round_hook=hook,
+                                  keep_round=True)
         except CommError as e:
             q.put((rank, "comm_error", str(e)))
             return
@@ -328,20 +329,26 @@ def test_more_clients_than_ranks_timed_out_wait_is_polled(tmp_path):
         assert before < 400, r[2]
 
 
-def test_bench_falls_back_to_rccl_when_xgmi_times_out(tmp_path):
-    """bench.py (2 ranks on the one GPU): an injected host stall longer than the xGMI spin
-    bound makes every rank raise CommError in the timed region; with the data plane on
-    auto-selection the bench re-measures the same federation over RCCL and records why,
-    instead of printing no number."""
+@pytest.mark.parametrize("clients,inject", [("2", "GFEDNTM_INJECT_STALL=1:8:2.0"),
+                                             ("8", "GFEDNTM_INJECT_STALL=1:8:2.0"),
+                                             ("2", "GFEDNTM_INJECT_CORRUPT=1:3")])
+def test_bench_falls_back_to_rccl_when_xgmi_times_out(tmp_path, clients, inject):
+    """bench.py (2 ranks on the one GPU; one client per rank, or the default 8 clients as 4
+    per rank): an injected host stall longer than the xGMI spin bound -- or a replica that
+    diverges (GFEDNTM_INJECT_CORRUPT: the digest check) -- makes every rank raise
+    CommError in the timed region; with the data plane on auto-selection the bench
+    re-measures the same federation over RCCL and records why, instead of printing no
+    number."""
     import json
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    k, v = inject.split("=")
     env = dict(os.environ, GFEDNTM_REHEARSE_1GPU="1", GFEDNTM_XGMI_SPIN="2000",
-               GFEDNTM_INJECT_STALL="1:8:2.0")
+               GFEDNTM_DIGEST_EVERY="4", **{k: v})
     p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "20",
-                        "--warmup", "5", "--no-npmi"], cwd=root, env=env, capture_output=True,
-                       text=True, timeout=240)
+                        "--warmup", "5", "--no-npmi", "--clients", clients], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-3000:]
     rec = json.loads(p.stdout.strip().splitlines()[-1])
     assert "xGMI all-reduce failed" in rec["allreduce_fallback"]

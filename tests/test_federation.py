@@ -311,3 +311,29 @@ def test_heartbeat_with_more_clients_than_ranks():
             if p.is_alive():
                 p.kill()
             p.join(10)
+
+
+def test_federated_synthetic_evaluation_is_logged(tmp_path, caplog):
+    """On synthetic sources every client scores its saved model against the generator's
+    ground truth (reference federated_avitm.py:152-193): TSS over the generator vocabulary
+    and DSS over its own documents, logged with the reference's lines and recomputable
+    from the saved npz."""
+    import logging
+    from gfedntm_amd.eval.metrics import betas_to_ground_truth_vocab, dss, tss
+    corpora = _corpora(2)
+    log = logging.getLogger("tests.synthetic_eval")      # propagates to caplog
+    log.propagate = True
+    with caplog.at_level(logging.INFO):
+        fed = LocalFederation(corpora, _params(num_epochs=1), max_iters=5, device="cpu",
+                              backend="torch", save_client=str(tmp_path / "client"), seed=0,
+                              stamp="20240101", logger=log)
+        fed.run()
+    assert "evaluados correctamente" in caplog.text and "doc similarity" in caplog.text
+    for c, corp in zip(fed.clients, corpora):
+        ev = c.synthetic_eval
+        assert ev is not None and ev["tss"] > 0 and ev["dss"] >= 0
+        z = load_model_npz(str(tmp_path / f"client{c.id}" / f"model_{c.id}_20240101.npz"))
+        gt_th, gt_b = corp.ground_truth()
+        b = betas_to_ground_truth_vocab(z["betas"], c.dataset.idx2token, gt_b.shape[1])
+        assert abs(tss(b, gt_b) - ev["tss"]) < 1e-9
+        assert abs(dss(gt_th, z["thetas"]) - ev["dss"]) < 1e-9

@@ -154,3 +154,29 @@ def test_ctm_large_v_fused_matches_gradient_mode(monkeypatch, bal, V):
     fb = b.engine.view_like(b.engine.exp_avg, "inf_net.adapt_bert.weight")
     torch.testing.assert_close(fa, fb, rtol=1e-2, atol=1e-4 * (float(fb.abs().max()) + 1e-12))
     _assert_beta_padding_zero(a)
+
+
+@pytest.mark.parametrize("V", [9001, 12347])
+def test_ctm_win_ctxpp_fused_update_odd_vocab(monkeypatch, V):
+    """CombinedTM's contextual W_in half as the persistent kernel (GFEDNTM_WIN_CTXPP=1) in
+    the FUSED update mode at H0 = 50 and an odd vocabulary: a block's last quad of its
+    [words, H0] run is partial (odd word count x 50 floats), and its Adam update must use
+    the parameter / moments of the elements it stores (csrc/update.hip gfk_win_ctx_pp_k;
+    the clamped 128-bit load shifted them by 1-3 elements)."""
+    from gfedntm_amd.models import CombinedTM
+    from gfedntm_amd.ops.engine import STAGE_WIN_CTXPP
+    monkeypatch.setenv("GFEDNTM_WIN_SPARSE", "1")
+    monkeypatch.setenv("GFEDNTM_WIN_CTXPP", "1")
+    K, Cdim, B = 20, 64, 64
+    kw = dict(input_size=V, contextual_size=Cdim, n_components=K, hidden_sizes=(50, 50),
+              batch_size=B, verbose=False, device="cuda")
+    a, b = _twins(CombinedTM, kw)
+    for tm in (a, b):
+        assert tm.engine._m.stage_flags & STAGE_WIN_CTXPP, "expected the persistent Wc kernel"
+    n_docs = 2 * B + 5
+    X = random_csr(n_docs, V, 60, seed=5)
+    ctx = np.random.default_rng(6).standard_normal((n_docs, Cdim)).astype(np.float32)
+    data = DeviceCSR(X, "cuda", contextual=ctx)
+    plan = BatchPlan.build(n_docs, B, 4, seed=0)
+    _run((a, b), data, plan)
+    _compare(a, b, 4)

@@ -89,3 +89,22 @@ def test_kernel_library_is_tied_to_the_sources(monkeypatch):
         native._check_source(_Lib(b"0000000000000000"))
     monkeypatch.setattr(native, "KERNELS_SO_OVERRIDE", "/tmp/ab/libgfedntm_kernels.so")
     native._check_source(_Lib(b"0000000000000000"))      # explicit A/B build: warn only
+
+
+def test_source_check_uses_the_embedded_build_arch(monkeypatch):
+    """The hash is recomputed with the arch the library was built for (embedded next to
+    it), so a loader with another PYTORCH_ROCM_ARCH in its environment (or none) still
+    accepts the tree's own build."""
+    from gfedntm_amd.ops import srchash
+    if not native.kernels_available():
+        pytest.skip("kernel library not built")
+    lib = native.kernels()
+    assert native.build_arch(lib) == "gfx950"
+    monkeypatch.setattr(native, "KERNELS_SO_OVERRIDE", None)
+    for env in ("gfx942", None):
+        if env is None:
+            monkeypatch.delenv("PYTORCH_ROCM_ARCH", raising=False)
+        else:
+            monkeypatch.setenv("PYTORCH_ROCM_ARCH", env)
+        native._check_source(lib)
+    assert native.kernels_hash() == srchash.source_hash("gfx950")

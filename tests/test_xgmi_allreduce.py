@@ -192,3 +192,29 @@ def test_xgmi_allreduce_inplace_exact(world, n):
         assert len(r) == 6, r
         _, ok, restored, graph_ok, err, refused = r
         assert ok and restored and graph_ok and err == 0 and refused, r
+
+
+def test_ipc_handles_identify_the_allocation():
+    """The peer-mapping cache (parallel/xgmi.py _IPC_OPEN) is keyed by the exporter's pid
+    and IPC handle bytes: two slices of ONE allocation must export the same handle (one
+    shared mapping, refcounted), a different allocation a different one (never a stale
+    mapping of freed memory at a reused address)."""
+    import ctypes as C
+    from gfedntm_amd.ops import native
+    from gfedntm_amd.parallel.xgmi import _declare
+    lib = native.kernels()
+    _declare(lib)
+    hs = lib.gfk_ipc_handle_size()
+
+    def export(t):
+        h, off = C.create_string_buffer(hs), C.c_int64(0)
+        assert lib.gfk_ipc_get_range(C.c_void_p(t.data_ptr()), h, C.byref(off)) == 0
+        return h.raw, off.value
+
+    a = torch.zeros(1 << 22, device="cuda")
+    b = torch.zeros(1 << 22, device="cuda")
+    h0, o0 = export(a[:1024])
+    h1, o1 = export(a[1 << 20:])
+    assert h0 == h1 and o1 - o0 == 4 << 20
+    hb, _ = export(b)
+    assert hb != h0

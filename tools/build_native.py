@@ -93,7 +93,8 @@ def build(verbose=True, jobs=8):
     # the source identity (gfk_source_hash), checked by gfedntm_amd/ops/native.py at load
     digest = srchash.source_hash(ARCH)
     hsrc = os.path.join(OBJ, "srchash.cpp")
-    text = ('extern "C" const char* gfk_source_hash() { return "%s"; }\n' % digest)
+    text = ('extern "C" const char* gfk_source_hash() { return "%s"; }\n'
+            'extern "C" const char* gfk_build_arch() { return "%s"; }\n' % (digest, ARCH))
     if not os.path.exists(hsrc) or open(hsrc).read() != text:
         with open(hsrc, "w") as f:
             f.write(text)
