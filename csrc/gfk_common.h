@@ -188,6 +188,15 @@ typedef struct GfkModel {
 
 constexpr int GFK_WIN_SPLIT = 128;
 
+// stage_flags bit 16 (GFK_FWD_POSTFOLD): the ProdLDA strip forward's ring variant computes
+// the batch-coupled posterior itself (csrc/prodlda.hip, FP) and post_fwd is not launched --
+// where it applies: strip ring forward (bit 2 + bit 8), K <= 64, B <= 64, no label head
+constexpr int GFK_FWD_POSTFOLD = 65536;
+__host__ __device__ inline bool gfk_postfold(const GfkModel& m) {
+  return (m.stage_flags & GFK_FWD_POSTFOLD) && (m.stage_flags & 4) && (m.stage_flags & 256) &&
+         m.K <= 64 && m.bmax <= 64 && !m.lab_on && m.kind == GFK_PRODLDA;
+}
+
 // Gradient + update jobs of the small tensors, run by the update kernel next to
 // the W_in tiles (csrc/update.hip).  Weight job: G[j][i] = sum_{b < nb} dz[b][j]
 // a[b][i] for the 64 x 64 output tile at (j0, i0) of param [rows][cols].  Vector

@@ -363,9 +363,23 @@ __host__ __device__ constexpr int strip_ring(int pf, int np) {
 // k of the lane's B operand (B[8 g + j][col]); A = 8 consecutive k of theta_d's row from LDS
 // (two ds_read_b128); both rounded to bf16 in registers, fp32 accumulation.  16x fewer MFMA
 // cycles than the fp32 path, which is what bounds it at K = 200 (not the beta stream).
-template <int BM, int NP, int PF, bool GB = false, bool BF = false>
+//
+// FP (stage_flags GFK_FWD_POSTFOLD; ring variant, K <= 64, no label head): the batch-coupled
+// posterior of post_fwd runs here, in the theta_d staging phase, and post_fwd is not launched
+// (one kernel boundary and one dependent round trip less per step).  Every workgroup
+// loads the raw [B, 2K] heads (mu | log sigma^2, 2 B K floats from L2), its rows' noise and
+// dropout masks, computes the column batch-norm statistics, and for every row the
+// normalised heads, the reparameterised sample, softmax(theta) and theta_d = theta * mask
+// straight into its LDS theta_d block -- redundant across workgroups, but a few KB of
+// reads and ~2 B K exps instead of a launch.  Row r's outputs for the backward (mu, log
+// sigma^2, theta, theta_d, KL) are stored by workgroup r % grid only; workgroup 0 advances
+// the running statistics, the counters and the optimizer step, as post_fwd's row 0 did.
+// Same arithmetic as gfk_post_fwd_k (csrc/posterior.hip; reference inference_network.py:
+// 82-83 + decoder_network.py:102-118 + avitm.py:207-220).
+template <int BM, int NP, int PF, bool GB = false, bool BF = false, bool FP = false>
 __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kernel(GfkArgT<GB> ga) {
   static_assert(!BF || (PF == 3 && NP % 4 == 0), "bf16 strips: ring variant, whole 32-k steps");
+  static_assert(!FP || (PF == 3 && NP == 8), "fused posterior: ring variant, K <= 64");
   const GfkModel& m = gfk_model(ga);
   constexpr int STRIP_THREADS = strip_threads(PF, NP);
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -437,7 +451,144 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
   // tiles of the last, partial round are spread over every CU's wave group 0 instead
   // of all 8 waves of the first CUs, so no SIMD gets more than ceil(strips / SIMDs) + 1
   int s = 4 * ((wave >> 2) * (int)gridDim.x + (int)blockIdx.x) + (wave & 3);
-  {
+  if constexpr (FP) {
+    // ---- fused posterior: one round of loads (heads, the rows' noise / masks, priors,
+    // workgroup 0's running statistics and counters), the first beta block behind them ----
+    static_assert(BM % NW == 0, "whole rows per wave");
+    constexpr int RPW = BM / NW;                 // rows per wave
+    constexpr int HU = (2 * BM * 64 + STRIP_THREADS - 1) / STRIP_THREADS;
+    constexpr int CPASS = 2;                     // 2K <= 128 columns, 64 per pass
+    float* hm = red + NW * BM;                   // [2][BM][K]: mu_raw | ls_raw
+    float* cm = hm + 2 * BM * 64;                // [128] column means
+    float* cr = cm + 128;                        // [128] column rstd
+    const int BK = BM * K;
+    float hv[HU];
+#pragma unroll
+    for (int u = 0; u < HU; ++u) {
+      const int e = min(tid + u * STRIP_THREADS, 2 * BK - 1);
+      const float* src = e < BK ? m.ws_mu_raw + e : m.ws_ls_raw + (e - BK);
+      hv[u] = *src;
+    }
+    const int kc = min(lane, K - 1);
+    float ep[RPW], mk[RPW];
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      const int r = wave + NW * i;
+      ep[i] = m.ws_eps[r * K + kc];
+      mk[i] = m.ws_mask_t[r * K + kc];
+    }
+    const float pmk = m.prior_mean[kc], pvk = m.prior_var[kc];
+    // (unconditional: every workgroup loads them, workgroup 0 uses them -- a load behind a
+    // branch would make the waitcnt pass drain the beta block below at its first use)
+    float rmp[CPASS], rvp[CPASS];
+#pragma unroll
+    for (int p = 0; p < CPASS; ++p) {
+      const int c2 = min(p * 64 + (tid >> 4), 2 * K - 1);
+      rmp[p] = c2 < K ? m.mu_rm[c2] : m.s_rm[c2 - K];
+      rvp[p] = c2 < K ? m.mu_rv[c2] : m.s_rv[c2 - K];
+    }
+    const double pw0 = m.adam_pow[0], pw1 = m.adam_pow[1];
+    const int64_t nbt0 = *m.nbt_mu, nbt1 = *m.nbt_s;
+    const int32_t at0 = *m.adam_t;
+    if (PF != 0) issue(min(s, nstrips - 1), b, rm0, rv0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < HU; ++u)
+      if (tid + u * STRIP_THREADS < 2 * BK) hm[tid + u * STRIP_THREADS] = hv[u];
+    lds_barrier();
+    // ---- column batch-norm statistics of the 2K heads over the nb rows: 16 lanes per
+    // column (rows g, g + 16, ..), 64 columns per pass ----
+    const bool w0 = blockIdx.x == 0;
+#pragma unroll
+    for (int p = 0; p < CPASS; ++p) {
+      if (p * 64 >= 2 * K) break;
+      const int c2 = p * 64 + (tid >> 4), g = tid & 15;
+      const bool valid = c2 < 2 * K;
+      const int cc = min(c2, 2 * K - 1);
+      const float* x = hm + (cc < K ? cc : BK + (cc - K));
+      constexpr int RPT = BM / 16;
+      float xv[RPT], sm = 0.f;
+#pragma unroll
+      for (int i = 0; i < RPT; ++i) {
+        const int r = g + 16 * i;
+        xv[i] = r < nb ? x[r * K] : 0.f;
+        sm += xv[i];
+      }
+      const float mean = row16_sum(sm) * inv_nb;
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < RPT; ++i) {
+        const float d = g + 16 * i < nb ? xv[i] - mean : 0.f;
+        q += d * d;
+      }
+      const float var = row16_sum(q) * inv_nb;
+      const float rstd = rsqrtf(var + m.bn_eps);
+      if (valid && g == 0) {
+        cm[c2] = mean;
+        cr[c2] = rstd;
+        if (w0) {
+          const int k = c2 < K ? c2 : c2 - K;
+          float* rmq = c2 < K ? m.mu_rm + k : m.s_rm + k;
+          float* rvq = c2 < K ? m.mu_rv + k : m.s_rv + k;
+          const float mom = m.bn_momentum;
+          const float unb = nb > 1 ? var * (float)nb / (float)(nb - 1) : var;
+          float nm = (1.f - mom) * rmp[p] + mom * mean, nv = (1.f - mom) * rvp[p] + mom * unb;
+          if (m.fed_scale_on && is_shared(m, rmq)) { nm *= m.fed_scale; nv *= m.fed_scale; }
+          *rmq = nm;
+          *rvq = nv;
+          m.ws_bn_rstd[c2] = rstd;
+        }
+      }
+    }
+    if (w0 && tid == 0) {
+      *m.nbt_mu = nbt0 + 1;
+      *m.nbt_s = nbt1 + 1;
+      *m.adam_t = at0 + 1;                       // the optimizer step of this minibatch
+      double p1, p2;
+      float c0, c1;
+      adam_advance(m, pw0, pw1, p1, p2, c0, c1);
+      m.adam_pow[0] = p1;
+      m.adam_pow[1] = p2;
+      m.adam_coef[0] = c0;
+      m.adam_coef[1] = c1;
+    }
+    lds_barrier();
+    // ---- per row (wave w: rows w, w + NW, ..; lane = topic): normalise, reparameterise,
+    // softmax, dropout -> theta_d in LDS (zero past K and in rows >= nb); the row's
+    // writer workgroup stores what row_bwd / post_bwd / the backward read ----
+    const int KTs = KT;
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      const int r = wave + NW * i;
+      const bool live = r < nb;
+      float mu = 0.f, ls = 0.f, z = -INFINITY, klt = 0.f, lpv = 0.f;
+      if (lane < K) {
+        mu = (hm[r * K + lane] - cm[lane]) * cr[lane];
+        ls = (hm[BK + r * K + lane] - cm[K + lane]) * cr[K + lane];
+        const float sd = expf(0.5f * ls);
+        z = mu + ep[i] * sd;
+        const float dm = pmk - mu;
+        klt = sd * sd / pvk + dm * dm / pvk - ls;
+        lpv = logf(pvk);
+      }
+      const float zmax = wave_max(z);
+      const float ez = lane < K ? expf(z - zmax) : 0.f;
+      const float tht = ez * (1.f / wave_sum(ez));
+      const float thd = tht * mk[i];
+      th[r * KS + lane] = (live && lane < K) ? thd : 0.f;
+      if (lane < KS - 64) th[r * KS + 64 + lane] = 0.f;
+      if (live && r % (int)gridDim.x == (int)blockIdx.x) {
+        if (lane < K) {
+          m.ws_mu[r * K + lane] = mu;
+          m.ws_ls[r * K + lane] = ls;
+          m.ws_theta[r * K + lane] = tht;
+          m.ws_thetad[r * KTs + lane] = thd;
+        }
+        const float kl = wave_sum(klt), lp = wave_sum(lpv);
+        if (lane == 0) m.ws_kl[r] = 0.5f * (kl - (float)K + lp);
+      }
+    }
+  } else {
     constexpr int SU = (BM * KS + STRIP_THREADS - 1) / STRIP_THREADS;
     float tv[SU];
 #pragma unroll
@@ -1637,6 +1788,7 @@ constexpr int FWD_STRIP = 4;
 constexpr int FWD_STRIP_PF = 8;   // bit 3: its prefetching 8-wave variant
 constexpr int FWD_STRIP_ROLL = 64;  // bit 6: its rolling-prefetch 16-wave variant (PF = 2)
 constexpr int FWD_STRIP_RING = 256; // bit 8: the rolling prefetch through a 13-pair ring (PF = 3)
+__host__ __device__ inline bool strip_postfold(const GfkModel& m) { return gfk_postfold(m); }
 __host__ __device__ inline int strip_pairs(int K) { return (K + 7) / 8; }
 // the kernel instance (k pairs in registers) for K
 __host__ __device__ inline int strip_np(int K) {
@@ -1653,7 +1805,9 @@ __host__ __device__ inline int strip_np_bf(int K) { return K <= 64 ? 8 : K <= 12
 extern "C" size_t gfk_prodlda_fwd_smem(const GfkModel* m) {
   if (m->stage_flags & FWD_STRIP) {
     const int np = m->mm_bf16 ? strip_np_bf(m->K) : strip_np(m->K);
-    return sizeof(float) * ((size_t)m->bmax * (8 * np + 4) + (size_t)(1024 / 64) * m->bmax);
+    // (+ the fused posterior's raw heads [2][B][64] and column statistics [2][128])
+    const size_t fp = strip_postfold(*m) ? 2 * (size_t)m->bmax * 64 + 256 : 0;
+    return sizeof(float) * ((size_t)m->bmax * (8 * np + 4) + (size_t)(1024 / 64) * m->bmax + fp);
   }
   const size_t KP = round_up(m->K, m->mm_bf16 ? 16 : 4);
   return sizeof(float) * ((size_t)m->bmax * m->kt + KP * LDB_F + 8 * VB);
@@ -1688,24 +1842,30 @@ extern "C" int gfk_launch_prodlda_fwd(const GfkModel* m, hipStream_t s) {
     const int np = strip_np(m->K);
     if (m->bmax > 64 || m->K > 256 || m->dec_grid > m->n_tiles ||
         (int64_t)m->K * m->ldb >= (1LL << 29)) return -1;
+    const bool fp = strip_postfold(*m);
     if (m->mm_bf16) {                   // bf16: the ring variant only
       if (!(m->stage_flags & FWD_STRIP_RING)) return -1;
       const int nb = strip_np_bf(m->K);
 #define GFK_FWSB(BM, NP)                                                                       \
       do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 3, true, true>), gfk_grid(g, m), dim3(strip_threads(3, NP)), sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 3, false, true>), g, dim3(strip_threads(3, NP)), sm, s, GfkArgT<false>{*m}); } while (0)
-#define GFK_FWSB_B(BM) if (nb == 8) GFK_FWSB(BM, 8); else if (nb == 16) GFK_FWSB(BM, 16); else GFK_FWSB(BM, 32)
+#define GFK_FWSB_FP(BM)                                                                        \
+      do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, 8, 3, true, true, true>), gfk_grid(g, m), dim3(1024), sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, 8, 3, false, true, true>), g, dim3(1024), sm, s, GfkArgT<false>{*m}); } while (0)
+#define GFK_FWSB_B(BM) if (fp) GFK_FWSB_FP(BM); else if (nb == 8) GFK_FWSB(BM, 8); else if (nb == 16) GFK_FWSB(BM, 16); else GFK_FWSB(BM, 32)
       switch (m->bmax) {
         case 16: GFK_FWSB_B(16); break;
         case 32: GFK_FWSB_B(32); break;
         default: GFK_FWSB_B(64); break;
       }
 #undef GFK_FWSB_B
+#undef GFK_FWSB_FP
 #undef GFK_FWSB
       return (int)hipGetLastError();
     }
 #define GFK_FWS(BM, NP)                                                                        \
     do {                                                                                       \
-      if (m->stage_flags & FWD_STRIP_RING)                                                     \
+      if (NP == 8 && fp)                                                                       \
+        do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, 8, 3, true, false, true>), gfk_grid(g, m), dim3(1024), sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, 8, 3, false, false, true>), g, dim3(1024), sm, s, GfkArgT<false>{*m}); } while (0); \
+      else if (m->stage_flags & FWD_STRIP_RING)                                                \
         do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 3, true>), gfk_grid(g, m), dim3(strip_threads(3, NP)), sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 3, false>), g, dim3(strip_threads(3, NP)), sm, s, GfkArgT<false>{*m}); } while (0); \
       else if (m->stage_flags & FWD_STRIP_ROLL)                                                \
         do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 2, true>), gfk_grid(g, m), dim3(strip_threads(2, NP)), sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 2, false>), g, dim3(strip_threads(2, NP)), sm, s, GfkArgT<false>{*m}); } while (0); \
@@ -1849,9 +2009,12 @@ extern "C" int gfk_prodlda_set_smem(size_t bytes) {
 #define GFK_FWS_PTRSB(BM) (const void*)prodlda_fwd_strip_kernel<BM, 8, 3, false, true>, (const void*)prodlda_fwd_strip_kernel<BM, 8, 3, true, true>, \
     (const void*)prodlda_fwd_strip_kernel<BM, 16, 3, false, true>, (const void*)prodlda_fwd_strip_kernel<BM, 16, 3, true, true>, \
     (const void*)prodlda_fwd_strip_kernel<BM, 32, 3, false, true>, (const void*)prodlda_fwd_strip_kernel<BM, 32, 3, true, true>
-#define GFK_FWS_PTRS(BM) GFK_FWS_PTRS1(BM, 0), GFK_FWS_PTRS1(BM, 1), GFK_FWS_PTRS1(BM, 2), GFK_FWS_PTRS1(BM, 3), GFK_FWS_PTRSB(BM)
+#define GFK_FWS_PTRSF(BM) (const void*)prodlda_fwd_strip_kernel<BM, 8, 3, false, false, true>, (const void*)prodlda_fwd_strip_kernel<BM, 8, 3, true, false, true>, \
+    (const void*)prodlda_fwd_strip_kernel<BM, 8, 3, false, true, true>, (const void*)prodlda_fwd_strip_kernel<BM, 8, 3, true, true, true>
+#define GFK_FWS_PTRS(BM) GFK_FWS_PTRS1(BM, 0), GFK_FWS_PTRS1(BM, 1), GFK_FWS_PTRS1(BM, 2), GFK_FWS_PTRS1(BM, 3), GFK_FWS_PTRSB(BM), GFK_FWS_PTRSF(BM)
                       GFK_FWS_PTRS(16), GFK_FWS_PTRS(32), GFK_FWS_PTRS(64),
 #undef GFK_FWS_PTRS
+#undef GFK_FWS_PTRSF
 #undef GFK_FWS_PTRSB
 #undef GFK_FWS_PTRS1
 #define GFK_BWD_PTRS2(U, T, F) (const void*)prodlda_bwd_kernel<16, U, T, F>, (const void*)prodlda_bwd_kernel<16, U, T, F, true>, \

@@ -106,7 +106,8 @@ int gfk_run(const GfkModel* m, const GfkAdam* a, int adam_grid, const GfkUpdate*
     switch (phases[i]) {
       case GFK_PH_BATCH_DOCS: e = gfk_launch_batch_docs(m, s); break;
       case GFK_PH_ENC_FWD: e = gfk_launch_enc_in(m, s); break;
-      case GFK_PH_POST_FWD: e = gfk_launch_post_fwd(m, s); break;
+      // (folded into the strip forward: running it as well would advance the step twice)
+      case GFK_PH_POST_FWD: e = gfk_postfold(*m) ? 0 : gfk_launch_post_fwd(m, s); break;
       case GFK_PH_PRODLDA_FWD: e = gfk_launch_prodlda_fwd(m, s); break;
       case GFK_PH_PRODLDA_LOSS: e = gfk_launch_prodlda_row_loss(m, s); break;
       case GFK_PH_PRODLDA_BWD: e = gfk_launch_prodlda_bwd(m, s); break;

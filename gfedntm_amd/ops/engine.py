@@ -67,6 +67,7 @@ STAGE_CTX_BWDPP = 4096            # bit 12: CombinedTM backward, persistent pipe
 STAGE_CTX_BAL3 = 8192             # bit 13: the balanced forward's 16-wave 3-deep variant (csrc/ctx.hip)
 STAGE_WIN_CTXPP = 16384           # bit 14: CombinedTM's contextual W_in half as a persistent kernel
 STAGE_CTX_RS = 32768              # bit 15: CombinedTM forward, Wa register-streamed (csrc/ctx.hip)
+STAGE_FWD_POSTFOLD = 65536        # bit 16: the strip forward computes post_fwd (csrc/prodlda.hip FP)
 
 
 def _explain(ok: bool, why: str, explain: bool) -> bool:
@@ -513,6 +514,13 @@ class FusedEngine(EngineBase):
                 elif pf == "3":
                     m.stage_flags |= STAGE_FWD_STRIP_RING
                 m.dec_grid = int(min(m.n_tiles, cu))
+                # the batch-coupled posterior (BN of the heads, reparameterisation, softmax,
+                # dropout, KL) inside the ring forward's theta_d staging: post_fwd is not
+                # launched (K <= 64, no label head; csrc/gfk_common.h gfk_postfold).
+                # GFEDNTM_POSTFOLD=0 keeps the separate post_fwd kernel
+                if (m.stage_flags & STAGE_FWD_STRIP_RING and m.K <= 64 and not m.lab_on
+                        and os.environ.get("GFEDNTM_POSTFOLD", "1") != "0"):
+                    m.stage_flags |= STAGE_FWD_POSTFOLD
             # backward: one workgroup per tile while the tiles fit the resident slots;
             # else persistent, n_dpart d theta_d slabs: with >= 4 k tiles the topics
             # are split over 4 workgroups per slab (csrc/prodlda.hip, 8 waves each, two
@@ -930,6 +938,8 @@ class FusedEngine(EngineBase):
                 ([abi.PH_ADAM] if self.update_mode == UPDATE_GRAD else [])
         else:
             ph = abi.PRODLDA_STEP + ([abi.PH_ADAM] if self.update_mode == UPDATE_GRAD else [])
+            if self._m.stage_flags & STAGE_FWD_POSTFOLD:
+                ph.remove(abi.PH_POST_FWD)          # computed by the strip forward
             if self.beta_split:
                 ph.insert(ph.index(abi.PH_PRODLDA_BWD) + 1, abi.PH_BETA_ADAM)
         if self.win_split:
@@ -1475,8 +1485,20 @@ class BatchedSteps:
             # the strip forward: with M clients' tiles in one launch the 16-wave variant (one
             # workgroup per CU) runs M dec_grid workgroups in rounds; the 8-wave prefetching
             # variant fits two per CU (GFEDNTM_BATCH_STRIP_PF=0 keeps the engines' choice)
-            if (mm.stage_flags & STAGE_FWD_STRIP and M * mm.dec_grid > self._cu
-                    and os.environ.get("GFEDNTM_BATCH_STRIP_PF", "1") != "0"):
+            # GFEDNTM_BATCH_STRIP: "fill" -- every 16-wave workgroup of the ring variant takes
+            # 4 whole tiles (one strip per wave), so M clients' strips need M n_tiles / 4
+            # workgroups instead of M n_tiles with 12 of 16 waves idle (a single client's
+            # layout: one tile per CU, the fastest for ONE client); "pf" -- the 8-wave
+            # prefetching variant, two per CU (round 4); "keep" -- the engines' choice
+            # (fill only where it is one round: 16-wave ring workgroups are one per CU)
+            bstrip = os.environ.get("GFEDNTM_BATCH_STRIP", "fill")
+            fill = -(-mm.n_tiles // 4)
+            if (mm.stage_flags & STAGE_FWD_STRIP and M > 1 and bstrip == "fill"
+                    and mm.stage_flags & STAGE_FWD_STRIP_RING and mm.dec_grid == mm.n_tiles
+                    and M * fill <= self._cu):
+                mm.dec_grid = fill
+            elif (mm.stage_flags & STAGE_FWD_STRIP and M * mm.dec_grid > self._cu
+                    and bstrip != "keep"):
                 mm.stage_flags = (mm.stage_flags & ~(STAGE_FWD_STRIP_ROLL | STAGE_FWD_STRIP_RING)) \
                     | STAGE_FWD_STRIP_PF
             # win_update: all clients' W_in tiles in one launch -> the 8-wave tile shape once

@@ -862,3 +862,53 @@ def test_ctm_persistent_backward_fused_update(monkeypatch):
                                                    "inf_net.f_sigma_batchnorm.running_mean"))
         torch.testing.assert_close(sa[k], sb[k], rtol=1e-3, atol=lr_steps if noisy else 5e-5,
                                    msg=lambda m: f"{k}: {m}")
+
+
+@pytest.mark.parametrize("B,K,V", [(64, 50, 4500), (64, 64, 3000), (32, 25, 7001), (16, 10, 700),
+                                   (64, 50, 40000)])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_postfold_matches_separate_post_fwd(monkeypatch, B, K, V, dtype):
+    """The strip forward with the posterior folded in (stage_flags GFK_FWD_POSTFOLD: BN of the
+    heads, reparameterisation, softmax, dropout, KL, running statistics and the optimizer
+    step counters computed in its theta_d staging; post_fwd not launched) matches the
+    separate post_fwd kernel over several fused-update graph replays -- same workspace
+    outputs for the backward, same counters, same trained state."""
+    from gfedntm_amd.ops.engine import STAGE_FWD_POSTFOLD
+    kw = dict(input_size=V, n_components=K, hidden_sizes=(50, 50), batch_size=B,
+              verbose=False, device="cuda")
+    if dtype == "bf16":
+        kw["matmul_dtype"] = "bf16"
+    tms = []
+    for fold in ("1", "0"):
+        monkeypatch.setenv("GFEDNTM_POSTFOLD", fold)
+        torch.manual_seed(3)
+        tm = AVITM(backend="fused", **kw)
+        assert bool(tm.engine._m.stage_flags & STAGE_FWD_POSTFOLD) == (fold == "1")
+        assert (abi.PH_POST_FWD in tm.engine.phases()) == (fold == "0")
+        tms.append(tm)
+    a, b = tms
+    b.model.load_state_dict(a.model.state_dict())
+    b.engine.seed = b.engine._m.seed = a.engine.seed
+    X = random_csr(3 * B + 5, V, 40, seed=4)
+    data = DeviceCSR(X, "cuda")
+    plan = BatchPlan.build(data.n_docs, B, 5, seed=1)
+    for tm in (a, b):
+        tm.engine.set_fedavg_scale(0.5)
+        tm.engine.bind_data(data, plan)
+        tm.engine.enable_graph(True)
+        for s in range(5):
+            tm.engine.step(s)
+    torch.cuda.synchronize()
+    for key in ("mu", "ls", "theta", "thetad", "kl", "bn_rstd"):
+        torch.testing.assert_close(a.engine.ws[key], b.engine.ws[key], rtol=1e-5, atol=1e-6,
+                                   msg=lambda m: f"ws[{key}]: {m}")
+    assert int(a.engine.adam_t.item()) == int(b.engine.adam_t.item()) == 5
+    torch.testing.assert_close(a.engine.adam_coef, b.engine.adam_coef, rtol=0, atol=0)
+    torch.testing.assert_close(a.engine.loss_hist[:5], b.engine.loss_hist[:5], rtol=1e-5, atol=1e-3)
+    sa, sb = a.model.state_dict(), b.model.state_dict()
+    for k in sa:
+        if not sa[k].is_floating_point():
+            assert torch.equal(sa[k], sb[k]), k
+            continue
+        torch.testing.assert_close(sa[k], sb[k], rtol=1e-4, atol=5e-5 if "bias" not in k else 2e-3,
+                                   msg=lambda m: f"{k}: {m}")
