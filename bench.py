@@ -513,6 +513,8 @@ def _ctx_note(rec, args, eng):
         return
     why = getattr(eng, "ctx_fallback_reason", None)
     rec["ctx_path"] = "fused kernels" if why is None else f"host-GEMM fallback: {why}"
+    if getattr(eng, "ctx_gemm_dtype", None):
+        rec["ctx_gemm_dtype"] = eng.ctx_gemm_dtype
 
 
 def _is_headline(args) -> bool:
@@ -579,8 +581,10 @@ def _record(args, value, ms, V, npmi, final_loss, clients: int, ranks: int, phys
                          "minibatch step and the sample-weighted FedAvg of their shared state "
                          "replaces every client's copy"),
         **({"precision": "bf16 operands of the ProdLDA decoder GEMMs (theta.beta, theta^T.dlogit, "
-                         "dlogit.beta^T) on v_mfma_f32_16x16x32_bf16, fp32 accumulation; fp32 "
-                         "parameters, Adam state and every other op"} if args.dtype == "bf16" else {}),
+                         "dlogit.beta^T) and, for CombinedTM, of the contextual forward GEMMs "
+                         "(x_ctx.Wa^T, A.Wc^T; see ctx_gemm_dtype) on v_mfma_f32_16x16x32_bf16, "
+                         "fp32 accumulation; fp32 parameters, Adam state and every other op"}
+           if args.dtype == "bf16" else {}),
         # the source hash embedded in the kernel library that ran (gfedntm_amd/ops/srchash.py)
         "kernels_src_hash": _kernels_hash(args),
         "npmi": None if npmi is None else round(npmi, 4),

@@ -765,7 +765,13 @@ constexpr int RS_T = 1024, RS_KP = 256, RS_R = GFK_RS_RING, RS_AL = 512;
 static_assert((RS_KP / 16) % RS_R == 0, "a segment's blocks cycle the ring whole");
 // x phases / A [64][RS_AL] (the same 128 KB), + 3 split-unit partials [64][16]
 __host__ __device__ inline int fwd_rs_lds_floats() { return 2 * 64 * RS_KP + 3 * 64 * 16; }
-template <bool GB = false>
+// BF (matmul_dtype = "bf16"): both GEMMs on v_mfma_f32_16x16x32_bf16 with fp32
+// accumulation -- blocks j, j + 1 of a segment form one 32-k step (lane group g: the 8 k
+// 16 j + 4 g + i, 16 (j + 1) + 4 g + i of its Wa row AND of x's row, any pairing of k
+// works when A and B agree), Wa's pair converted once per step for the 4 row tiles; the
+// epilogue's P^T = Wc^T A^T pairs word groups sq, sq + 1 the same way.  8x fewer MFMA
+// instructions than the fp32 16x16x4 path, which bounds it (the Wa stream does not).
+template <bool GB = false, bool BF = false>
 __global__ void __launch_bounds__(RS_T) gfk_ctx_fwd_rs_k(GfkArgT<GB> ga) {
   const GfkModel& m = gfk_model(ga);
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -861,6 +867,26 @@ __global__ void __launch_bounds__(RS_T) gfk_ctx_fwd_rs_k(GfkArgT<GB> ga) {
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       if (has(p, t)) {
+        if constexpr (BF) {
+#pragma unroll
+          for (int j = 0; j < RS_KP / 16; j += 2) {
+            f32x4 xv[2][4];
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+              for (int bt = 0; bt < 4; ++bt)
+                xv[h][bt] = *reinterpret_cast<const f32x4*>(xc + bt * 16 * RS_KP + 64 * ((j + h) >> 2) + 16 * (((j + h) & 3) ^ (r >> 2)));
+            const f32x4 w0v = ring[j % RS_R], w1v = ring[(j + 1) % RS_R];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+              ring[(j + h) % RS_R] = j + h + RS_R < RS_KP / 16 ? ldw(offc, j + h + RS_R) : ldw(offn, j + h + RS_R - RS_KP / 16);
+            __builtin_amdgcn_sched_barrier(0);
+            const bf16x8 wa = to_bf16x8(w0v, w1v);
+#pragma unroll
+            for (int bt = 0; bt < 4; ++bt) acc[t][bt] = mfma_bf16x8(wa, to_bf16x8(xv[0][bt], xv[1][bt]), acc[t][bt]);
+          }
+        } else {
 #pragma unroll
         for (int j = 0; j < RS_KP / 16; ++j) {
           f32x4 xv[4];
@@ -875,6 +901,7 @@ __global__ void __launch_bounds__(RS_T) gfk_ctx_fwd_rs_k(GfkArgT<GB> ga) {
           for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int bt = 0; bt < 4; ++bt) acc[t][bt] = mfma16x16x4(wv[i], xv[bt][i], acc[t][bt]);
+        }
         }
         offc = offn;
         succ(pn, tn);
@@ -957,6 +984,22 @@ __global__ void __launch_bounds__(RS_T) gfk_ctx_fwd_rs_k(GfkArgT<GB> ga) {
   f32x4 pacc = z4;
   if (ht < NJT) {
     auto part = [&](const f32x4 (&wc)[8], int c) {
+      if constexpr (BF) {
+        // (word groups past nu: Wc reads 0 there, and A is masked to 0 too)
+#pragma unroll
+        for (int sx = 0; sx < 8; sx += 2) {
+          const int sq = 8 * c + sx;
+          if (sq < nu) {
+            f32x4 av[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              av[h] = *reinterpret_cast<const f32x4*>(al + (bt * 16 + r) * RS_AL + 4 * ((4 * (sq + h) + g) ^ r));
+              if (sq + h >= nu) av[h] = z4;
+            }
+            pacc = mfma_bf16x8(to_bf16x8(wc[sx], wc[sx + 1]), to_bf16x8(av[0], av[1]), pacc);
+          }
+        }
+      } else {
 #pragma unroll
       for (int sx = 0; sx < 8; ++sx) {
         const int sq = 8 * c + sx;
@@ -965,6 +1008,7 @@ __global__ void __launch_bounds__(RS_T) gfk_ctx_fwd_rs_k(GfkArgT<GB> ga) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) pacc = mfma16x16x4(wc[sx][i], av[i], pacc);
         }
+      }
       }
     };
     for (int c = 0; c < 4; c += 2) {
@@ -1371,7 +1415,8 @@ extern "C" int gfk_ctx_set_smem(size_t bytes) {
                       (const void*)gfk_ctx_fwd_bal_k<false>, (const void*)gfk_ctx_fwd_bal_k<true>,
                       (const void*)gfk_ctx_bwd_pp_k<false>, (const void*)gfk_ctx_bwd_pp_k<true>,
                       (const void*)gfk_ctx_fwd_bal3_k<false>, (const void*)gfk_ctx_fwd_bal3_k<true>,
-                      (const void*)gfk_ctx_fwd_rs_k<false>, (const void*)gfk_ctx_fwd_rs_k<true>};
+                      (const void*)gfk_ctx_fwd_rs_k<false>, (const void*)gfk_ctx_fwd_rs_k<true>,
+                      (const void*)gfk_ctx_fwd_rs_k<false, true>, (const void*)gfk_ctx_fwd_rs_k<true, true>};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return (int)e;
@@ -1398,7 +1443,10 @@ extern "C" int gfk_launch_ctx_fwd(const GfkModel* m, hipStream_t s) {
       (int64_t)m->V * m->C * 4 < 0x7FFFFFFFLL) {
     const dim3 g(m->ctx_parts), t(RS_T);
     const size_t sm = sizeof(float) * fwd_rs_lds_floats();
-    do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_ctx_fwd_rs_k<true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_ctx_fwd_rs_k<false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0);
+    if (m->mm_bf16)
+      do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_ctx_fwd_rs_k<true, true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_ctx_fwd_rs_k<false, true>), g, t, sm, s, GfkArgT<false>{*m}); } while (0);
+    else
+      do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_ctx_fwd_rs_k<true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_ctx_fwd_rs_k<false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0);
     return (int)hipGetLastError();
   }
   if ((m->stage_flags & CTX_FULL) && (m->stage_flags & CTX_BAL3) && m->bmax <= 64 && m->H[0] <= 63 && m->C > 3 * FD &&

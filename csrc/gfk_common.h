@@ -610,6 +610,16 @@ __device__ __forceinline__ f32x4 mfma16x16x32bf(const float (&a)[8], const float
   for (int j = 0; j < 8; ++j) { ab[j] = (__bf16)a[j]; bb[j] = (__bf16)b[j]; }
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ab, bb, c, 0, 0, 0);
 }
+// The same with operands converted once by the caller (an operand reused by several MFMAs).
+__device__ __forceinline__ bf16x8 to_bf16x8(const f32x4& lo, const f32x4& hi) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { r[j] = (__bf16)lo[j]; r[4 + j] = (__bf16)hi[j]; }
+  return r;
+}
+__device__ __forceinline__ f32x4 mfma_bf16x8(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f32x4 mfma16x16x16bf(const float (&a)[4], const float (&b)[4], f32x4 c) {

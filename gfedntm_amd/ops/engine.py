@@ -569,8 +569,10 @@ class FusedEngine(EngineBase):
         # CombinedTM at large V: ctx_fwd with all batch rows per vocab tile (each Wa block
         # staged once instead of once per 16-row block); GFEDNTM_CTX_FULL=0 / 1 overrides
         cf_env = os.environ.get("GFEDNTM_CTX_FULL", "auto")
+        # (matmul_dtype = "bf16": the register-streamed forward at any V -- the variant with
+        # bf16 operands on the matrix cores; the other shapes keep fp32 GEMMs)
         if m.ctx_fused == 1 and m.bmax <= 64 and (
-                cf_env == "1" or (cf_env == "auto" and m.n_tiles > 2 * cu_n)):
+                cf_env == "1" or (cf_env == "auto" and (m.n_tiles > 2 * cu_n or m.mm_bf16))):
             m.stage_flags |= STAGE_CTX_FULL
             # ... as the balanced persistent kernel: ctx_parts workgroups (two per CU) own
             # equal column ranges instead of one workgroup per tile (whose last round runs
@@ -849,6 +851,17 @@ class FusedEngine(EngineBase):
         self.beta_adam_grid = int(max(1, self._fill_adam(self._a_beta, keys=["beta"],
                                                          keep_grad=True)))
         self._invalidate_graph()
+
+    @property
+    def ctx_gemm_dtype(self) -> Optional[str]:
+        """Operand precision of CombinedTM's contextual GEMMs (adapt_bert and its input-layer
+        term) in the forward: "bf16" where matmul_dtype = "bf16" runs the register-streamed
+        kernel (csrc/ctx.hip gfk_ctx_fwd_rs_k<BF>), else "fp32"; None without them."""
+        m = self._m
+        if not self.ctx_fused or m.ctx_fused != 1:
+            return None
+        rs = STAGE_CTX_FULL | STAGE_CTX_RS
+        return "bf16" if m.mm_bf16 and (m.stage_flags & rs) == rs else "fp32"
 
     @property
     def beta_split(self) -> bool:

@@ -912,3 +912,75 @@ def test_postfold_matches_separate_post_fwd(monkeypatch, B, K, V, dtype):
             continue
         torch.testing.assert_close(sa[k], sb[k], rtol=1e-4, atol=5e-5 if "bias" not in k else 2e-3,
                                    msg=lambda m: f"{k}: {m}")
+
+
+@pytest.mark.parametrize("V", [6000, 40000, 99000])
+def test_ctm_bf16_contextual_matches_emulated_oracle(V):
+    """matmul_dtype='bf16' on CombinedTM: the contextual GEMMs of ctx_fwd (A = x_ctx Wa^T + b
+    and its input-layer term A Wc^T, register-streamed kernel, v_mfma_f32_16x16x32_bf16 with
+    fp32 accumulation) and the decoder's theta_d beta take bf16 operands; master weights,
+    Adam state and every other op stay fp32.  Oracle: the fp32 PyTorch step with exactly
+    those operands rounded to bf16 (C = 768, K = 100; V = 6k / 40k / 99k -- the BASELINE
+    CombinedTM class).  Reference: ctm inference_network.py:160-185."""
+    import torch.nn.functional as F
+    from gfedntm_amd.models import CombinedTM
+    from gfedntm_amd.models.networks import kl_terms, reconstruction_terms
+    from gfedntm_amd.ops.engine import STAGE_CTX_RS
+    K, Cdim, B, n_docs = 100, 768, 64, 150
+    torch.manual_seed(0)
+    kw = dict(input_size=V, contextual_size=Cdim, n_components=K, hidden_sizes=(50, 50),
+              batch_size=B, verbose=False, device="cuda")
+    fused = CombinedTM(backend="fused", matmul_dtype="bf16", **kw)
+    ref = CombinedTM(backend="torch", **kw)
+    ref.model.load_state_dict(fused.model.state_dict())
+    e = fused.engine
+    assert e._m.mm_bf16 == 1 and e._m.ctx_fused == 1 and e._m.stage_flags & STAGE_CTX_RS
+    assert e.ctx_gemm_dtype == "bf16"
+    X = random_csr(n_docs, V, 60, seed=1)
+    ctx = np.random.default_rng(2).standard_normal((n_docs, Cdim)).astype(np.float32)
+    data = DeviceCSR(X, "cuda", contextual=ctx)
+    plan = BatchPlan.build(data.n_docs, B, 3, seed=0)
+    e.set_update_mode(UPDATE_GRAD)
+    e.bind_data(data, plan)
+    e.run_phases(e.phases()[:-1])
+    torch.cuda.synchronize()
+    nb = int(plan.size[0])
+    ids = torch.from_numpy(plan.batch(0).astype(np.int64)).cuda()
+    x, xc = data.dense_rows(ids), data.contextual[ids]
+    model = ref.model
+    model.train()
+    model.zero_grad()
+    net = model.inf_net
+    bfr = lambda t: t + (_bf(t) - t).detach()      # noqa: E731  rounded forward, identity grad
+    W = net.input_layer.weight                        # [H0, 2V]: BoW half | contextual half
+    A = bfr(xc) @ bfr(net.adapt_bert.weight).t() + net.adapt_bert.bias
+    z0 = x @ W[:, :V].t() + bfr(A) @ bfr(W[:, V:2 * V]).t() + net.input_layer.bias
+    h = net.hiddens(net.activation(z0)) * e.ws["mask_h"][:nb]
+    bn, bs = net.f_mu_batchnorm, net.f_sigma_batchnorm
+    mu = F.batch_norm(net.f_mu(h), bn.running_mean, bn.running_var, training=True,
+                      momentum=bn.momentum, eps=bn.eps)
+    ls = F.batch_norm(net.f_sigma(h), bs.running_mean, bs.running_var, training=True,
+                      momentum=bs.momentum, eps=bs.eps)
+    theta = F.softmax(mu + e.ws["eps"][:nb] * torch.exp(0.5 * ls), dim=1)
+    thetad = theta * e.ws["mask_t"][:nb]
+    bb = model.beta_batchnorm
+    logits = F.batch_norm(bfr(thetad) @ bfr(model.beta), bb.running_mean, bb.running_var,
+                          training=True, momentum=bb.momentum, eps=bb.eps)
+    wd = F.softmax(logits, dim=1)
+    kl = kl_terms(model.prior_mean, model.prior_variance, mu, torch.exp(ls), ls, K)
+    rl = reconstruction_terms(x, wd)
+    w_kl = float(ref.weights.get("beta", 1.0))
+    loss = (w_kl * kl + rl).sum()
+    loss.backward()
+    torch.testing.assert_close(e.ws["kl"][:nb], kl.detach(), rtol=2e-3, atol=2e-2)
+    torch.testing.assert_close(e.ws["rl"][:nb], rl.detach(), rtol=2e-4, atol=5e-2)
+    # the adapted rows themselves: A (+ bias) per vocabulary tile in ws_actx [tile][b][64]
+    act = e.ws["actx"].view(-1, B, 64)[:, :nb].permute(1, 0, 2).reshape(nb, -1)[:, :V]
+    torch.testing.assert_close(act, A.detach(), rtol=1e-3, atol=1e-3)
+    g = _grads_of(fused)
+    for k, p in model.named_parameters():
+        if k in _NOISE_KEYS:
+            continue
+        scale = p.grad.abs().max().item() + 1e-6
+        torch.testing.assert_close(g[k], p.grad, rtol=3e-2, atol=2e-2 * scale,
+                                   msg=lambda m: f"{k}: {m}")
