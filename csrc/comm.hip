@@ -54,6 +54,11 @@ struct GfkComm {
   int32_t rank, world, nblk, spin_limit;
   int64_t n, chunk, slice;       // floats; chunk, slice multiples of 4
   int32_t inplace, pad;          // 1: the data buffers themselves are IPC-mapped (no stage)
+  // bf16-delta wire (gfk_xgmi_allreduce_bf16d): the stages hold bf16; ref = this rank's copy
+  // of the last averaged state (n floats), wgt = this rank's FedAvg weight sum
+  float* ref;
+  float wgt;
+  int32_t wire;                  // 0: fp32 sum (gfk_xgmi_allreduce), 1: bf16 deltas
 };
 
 namespace {
@@ -211,6 +216,131 @@ extern "C" __global__ void __launch_bounds__(CT) gfk_xgmi_allreduce(GfkComm c, f
   if (c.inplace) {
     publish(c, 2, b, e);
     await_all(c, 2, b, e);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// bf16-delta wire (opt-in, --fedavg_wire bf16delta): half the bytes of the fp32 sum.
+// Every rank holds ref = the last averaged state (identical on all ranks) and sends its
+// pre-scaled state's DEPARTURE from it, d_r = f_r - w_r ref (sum_r w_r = 1, so
+// sum_r d_r = W_new - ref), rounded to bf16 (RNE); the owner of a chunk sums the peers'
+// bf16 deltas in fp32 in rank order and publishes the sum rounded to bf16, S; every rank
+// (the owner too) sets W_new = ref + S and ref = W_new.  So the replicas stay bit-identical
+// and the rounding touches only the per-round change (~lr), never the weights themselves.
+// Same phases, flags, epochs and bounded waits as the fp32 kernel; always staged (the
+// peers read deltas, not the state).  Stage: [2][world * chunk] bf16.
+// ---------------------------------------------------------------------------
+namespace {
+__device__ __forceinline__ uint32_t bf16_bits(float f) {
+  const __bf16 h = (__bf16)f;                      // v_cvt_pk_bf16_f32: round to nearest even
+  return (uint32_t)__builtin_bit_cast(unsigned short, h);
+}
+__device__ __forceinline__ float bf16_val(uint32_t b) { return __uint_as_float(b << 16); }
+__device__ __forceinline__ uint2 pack4(float4 f) {
+  return make_uint2(bf16_bits(f.x) | (bf16_bits(f.y) << 16), bf16_bits(f.z) | (bf16_bits(f.w) << 16));
+}
+__device__ __forceinline__ float4 unpack4(uint2 u) {
+  return make_float4(bf16_val(u.x & 0xFFFFu), bf16_val(u.x >> 16), bf16_val(u.y & 0xFFFFu),
+                     bf16_val(u.y >> 16));
+}
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+// element i of a bf16 stage (byte offset 2 i)
+__device__ __forceinline__ uint2 ld4h(__amdgpu_buffer_rsrc_t r, int64_t i) {
+  const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(i * 2), 0, AUX_SYS);
+  return make_uint2(v.x, v.y);
+}
+__device__ __forceinline__ void st4h(__amdgpu_buffer_rsrc_t r, int64_t i, uint2 u) {
+  u32x2 v;
+  v.x = u.x; v.y = u.y;
+  __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)(i * 2), 0, AUX_SYS);
+}
+__device__ __forceinline__ uint32_t ld1h(__amdgpu_buffer_rsrc_t r, int64_t i) {
+  return (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, (int)(i * 2), 0, AUX_SYS);
+}
+__device__ __forceinline__ void st1h(__amdgpu_buffer_rsrc_t r, int64_t i, uint32_t b) {
+  __builtin_amdgcn_raw_buffer_store_b16((unsigned short)b, r, (int)(i * 2), 0, AUX_SYS);
+}
+__device__ __forceinline__ float4 ld4f(const float* p, int64_t i) { return *reinterpret_cast<const float4*>(p + i); }
+__device__ __forceinline__ void st4f(float* p, int64_t i, float4 v) { *reinterpret_cast<float4*>(p + i) = v; }
+}  // namespace
+
+extern "C" __global__ void __launch_bounds__(CT) gfk_xgmi_allreduce_bf16d(GfkComm c, float* data) {
+  // (every product and sum rounded on its own: XgmiAllReduce.expected_bf16delta restates it)
+#pragma clang fp contract(off)
+  const int b = blockIdx.x, t = threadIdx.x;
+  const uint32_t e = c.epoch[b] + 1;
+  __syncthreads();
+  if (t == 0) c.epoch[b] = e;
+  const int buf = e & 1, R = c.rank, W = c.world;
+  const int64_t sbytes = (int64_t)W * c.chunk * 2;
+  const __amdgpu_buffer_rsrc_t mine = rsrc(c.stage[buf][R], sbytes);
+  float* ref = c.ref;
+  const float w = c.wgt;
+  // ---- phase 0: my bf16 deltas of slice b of every chunk ----
+  for (int ch = 0; ch < W; ++ch) {
+    int64_t s0, s1;
+    slice_range(c, ch, b, s0, s1);
+    const int64_t s4 = s0 + ((s1 - s0) & ~(int64_t)3);
+    for (int64_t i = s0 + 4 * t; i < s4; i += 4 * CT) {
+      const float4 d = ld4f(data, i), r = ld4f(ref, i);
+      st4h(mine, i, pack4(make_float4(d.x - w * r.x, d.y - w * r.y, d.z - w * r.z, d.w - w * r.w)));
+    }
+    if (s4 + t < s1) st1h(mine, s4 + t, bf16_bits(data[s4 + t] - w * ref[s4 + t]));
+  }
+  publish(c, 0, b, e);
+  await_all(c, 0, b, e);
+  // ---- phase 1: my chunk, slice b: fp32 sum of the ranks' deltas in rank order ----
+  {
+    int64_t s0, s1;
+    slice_range(c, R, b, s0, s1);
+    __amdgpu_buffer_rsrc_t src[CMAX];
+#pragma unroll
+    for (int j = 0; j < CMAX; ++j) src[j] = rsrc(c.stage[buf][j < W ? j : 0], sbytes);
+    const int64_t s4 = s0 + ((s1 - s0) & ~(int64_t)3);
+    if (s4 + t < s1) {
+      float acc = bf16_val(ld1h(src[0], s4 + t));
+      for (int j = 1; j < W; ++j) acc += bf16_val(ld1h(src[j], s4 + t));
+      const uint32_t sb = bf16_bits(acc);
+      st1h(mine, s4 + t, sb);
+      const float wn = ref[s4 + t] + bf16_val(sb);
+      data[s4 + t] = wn;
+      ref[s4 + t] = wn;
+    }
+    for (int64_t i = s0 + 4 * t; i < s4; i += 4 * CT) {
+      uint2 v[CMAX];
+#pragma unroll
+      for (int j = 0; j < CMAX; ++j)
+        if (j < W) v[j] = ld4h(src[j], i);
+      float4 acc = unpack4(v[0]);
+#pragma unroll
+      for (int j = 1; j < CMAX; ++j)
+        if (j < W) acc = add4(acc, unpack4(v[j]));
+      const uint2 sb = pack4(acc);
+      st4h(mine, i, sb);
+      const float4 wn = add4(ld4f(ref, i), unpack4(sb));
+      st4f(data, i, wn);
+      st4f(ref, i, wn);
+    }
+  }
+  publish(c, 1, b, e);
+  await_all(c, 1, b, e);
+  // ---- phase 2: the other chunks' summed deltas from their owners ----
+  for (int ch = 0; ch < W; ++ch) {
+    if (ch == R) continue;
+    int64_t s0, s1;
+    slice_range(c, ch, b, s0, s1);
+    const __amdgpu_buffer_rsrc_t src = rsrc(c.stage[buf][ch], sbytes);
+    const int64_t s4 = s0 + ((s1 - s0) & ~(int64_t)3);
+    for (int64_t i = s0 + 4 * t; i < s4; i += 4 * CT) {
+      const float4 wn = add4(ld4f(ref, i), unpack4(ld4h(src, i)));
+      st4f(data, i, wn);
+      st4f(ref, i, wn);
+    }
+    if (s4 + t < s1) {
+      const float wn = ref[s4 + t] + bf16_val(ld1h(src, s4 + t));
+      data[s4 + t] = wn;
+      ref[s4 + t] = wn;
+    }
   }
 }
 
@@ -466,6 +596,11 @@ extern "C" int gfk_comm_launch(const GfkComm* c, float* data, hipStream_t s) {
       (int64_t)c->slice * c->nblk < c->chunk || (int64_t)c->chunk * c->world < c->n ||
       ((uintptr_t)data & 15) || (int64_t)c->world * c->chunk * 4 > gfk_comm_max_bytes())
     return -1;
-  hipLaunchKernelGGL(gfk_xgmi_allreduce, dim3(c->nblk), dim3(CT), 0, s, *c, data);
+  if (c->wire == 1) {
+    if (c->inplace || !c->ref || ((uintptr_t)c->ref & 15)) return -1;
+    hipLaunchKernelGGL(gfk_xgmi_allreduce_bf16d, dim3(c->nblk), dim3(CT), 0, s, *c, data);
+  } else {
+    hipLaunchKernelGGL(gfk_xgmi_allreduce, dim3(c->nblk), dim3(CT), 0, s, *c, data);
+  }
   return (int)hipGetLastError();
 }

@@ -64,6 +64,10 @@ def build_parser() -> argparse.ArgumentParser:
                    help="params: FedAvg of the shared state after every local step (reference); "
                         "grads: all-reduce of the sample-weighted gradients before one optimizer "
                         "step on every client (classic synchronous data parallelism)")
+    p.add_argument("--fedavg_wire", type=str, default=None, choices=["fp32", "bf16delta"],
+                   help="FedAvg transport: fp32 (reference averaging; default: [amd] fedavg_wire) "
+                        "or bf16delta (opt-in: each client sends its post-step departure from "
+                        "the last averaged state in bf16, summed in fp32 -- half the bytes)")
     p.add_argument("--checkpoint_dir", type=str, default=None)
     p.add_argument("--checkpoint_every", type=int, default=None)
     p.add_argument("--stop_at_num_epochs", action="store_true")
@@ -144,7 +148,8 @@ def run_local(args, cfg) -> dict:
         stop_at_num_epochs=args.stop_at_num_epochs or cfg.stop_at_num_epochs,
         checkpoint_dir=args.checkpoint_dir,
         checkpoint_every=args.checkpoint_every if args.checkpoint_every is not None
-        else cfg.checkpoint_every, stamp=stamp, agg=args.agg)
+        else cfg.checkpoint_every, stamp=stamp, agg=args.agg,
+        fedavg_wire=args.fedavg_wire or cfg.fedavg_wire)
     return fed.run()
 
 
@@ -182,7 +187,7 @@ def _rank_main(args, cfg) -> dict:
         else cfg.checkpoint_every, stamp=stamp,
         metrics_path=os.path.join(f"{logs_client}{ids[0]}", f"metrics_{stamp}.jsonl"),
         metrics_every=args.metrics_every, heartbeat_timeout=args.heartbeat_timeout,
-        agg_mode=args.agg, client_ids=ids)
+        agg_mode=args.agg, client_ids=ids, fedavg_wire=args.fedavg_wire or cfg.fedavg_wire)
 
 
 def _spawned(local_rank: int, world: int, port: int, argv: List[str]):
@@ -238,6 +243,9 @@ def main(argv: Optional[List[str]] = None):
     if args.agg != "params":
         raise SystemExit("--agg grads needs a collective backend (local / rccl / gloo): the "
                          "reference wire protocol carries parameters, not gradients")
+    if (args.fedavg_wire or cfg.fedavg_wire) != "fp32":
+        raise SystemExit("--fedavg_wire bf16delta needs a collective backend (local / rccl / "
+                         "gloo): the reference wire protocol carries fp32 tensors")
     from .federation import grpc_transport
     if args.id == 0:
         return grpc_transport.start_server(args, cfg)

@@ -50,14 +50,20 @@ class SingleClientRound:
     """The rank's one client (N = R)."""
 
     def __init__(self, client: FederatedClient, world: int, device, on_gpu_plane: bool,
-                 allreduce: Optional[str], agg_mode: str, bucket_bytes: int, logger):
+                 allreduce: Optional[str], agg_mode: str, bucket_bytes: int, logger,
+                 wire: str = "fp32"):
         self.clients = [client]
         self.client = client
         self.agg_mode = agg_mode
-        self.agg = CollectiveAggregator(bucket_bytes=bucket_bytes, method="rccl")
+        if wire != "fp32" and agg_mode != "params":
+            raise ValueError("fedavg_wire bf16delta averages parameters (agg_mode 'params')")
+        self.wire = wire
+        self.agg = CollectiveAggregator(bucket_bytes=bucket_bytes, method="rccl", wire=wire,
+                                        weight=client.weight if wire != "fp32" else None)
+        self.agg.set_reference(client.shared)
         self.in_step = None
         if on_gpu_plane and client.fused and agg_mode == "params" and world > 1:
-            self.in_step = client.tm.engine.attach_fedavg(method=allreduce)
+            self.in_step = client.tm.engine.attach_fedavg(method=allreduce, wire=wire)
             logger.info("-- -- FedAvg all-reduce: %s", self.in_step)
         self.method = self.in_step if self.in_step else (None if world == 1 else "rccl")
         self.attach = getattr(client.tm.engine, "fedavg_attach", None) if self.in_step else None
@@ -83,6 +89,14 @@ class SingleClientRound:
         elif self.in_step is None:
             self.agg.allreduce_(c.shared)
 
+    def resync_reference(self):
+        """bf16delta: the (loaded) shared state is the last averaged state."""
+        if self.wire == "fp32":
+            return
+        self.agg.set_reference(self.client.shared)
+        if self.in_step is not None:
+            self.client.tm.engine.fedavg_set_reference()
+
     def error(self) -> int:
         e = self.client.tm.engine
         return e.fedavg_error() if self.in_step is not None and self.client.fused else 0
@@ -106,8 +120,11 @@ class MultiClientRound:
     """The rank's block of M > 1 clients (N > R)."""
 
     def __init__(self, clients: List[FederatedClient], world: int, device, on_gpu_plane: bool,
-                 allreduce: Optional[str], graph: bool, logger):
+                 allreduce: Optional[str], graph: bool, logger, wire: str = "fp32"):
         self.clients = clients
+        self.wire = wire
+        # the rank's FedAvg weight: its clients' weights summed in client order (bf16delta)
+        self.weight = sum(c.weight for c in clients) if wire != "fp32" else None
         self.device = device
         self.world = world
         self.shared = [c.shared for c in clients]
@@ -128,7 +145,7 @@ class MultiClientRound:
             method = allreduce if on_gpu_plane else "rccl"
             big = inplace_threshold_bytes()
             for k, (a, b) in self.parts.items():
-                coll = CollectiveAggregator(method=method)
+                coll = CollectiveAggregator(method=method, wire=wire, weight=self.weight)
                 coll.prepare(self.shared[0][a:b], inplace=self.fused and 4 * (b - a) >= big)
                 self.colls[k] = coll
             self.attach = {"s": round(sum(c.setup_s for c in self.colls.values()), 4),
@@ -145,7 +162,7 @@ class MultiClientRound:
                     c.xgmi.close()
                     c.xgmi = None
             self.parts = {"rest": (0, n)}
-            coll = CollectiveAggregator(method="rccl")
+            coll = CollectiveAggregator(method="rccl", wire=wire, weight=self.weight)
             coll.prepare(self.shared[0])
             self.colls = {"rest": coll}
         self.method = (None if world == 1 else
@@ -286,6 +303,12 @@ class MultiClientRound:
             self.colls["rest"].allreduce_(acc)
         for f in self.shared[1:]:
             f.copy_(acc)
+
+    def resync_reference(self):
+        """bf16delta: the (loaded) shared state is the last averaged state."""
+        for k, coll in self.colls.items():
+            a, b = self.parts[k]
+            coll.set_reference(self.shared[0][a:b])
 
     # ---- failure detection (the engine's surface, over this rank's collectives) ----
     def _xgmis(self):

@@ -107,9 +107,12 @@ class LocalFederation:
                  checkpoint_every: int = 0, stamp: Optional[str] = None,
                  metrics_path: Optional[str] = None, metrics_every: int = 0, agg: str = "params",
                  round_graph: Optional[bool] = None, round_streams: bool = True,
-                 groups: Optional[Sequence[int]] = None, round_batched: Optional[bool] = None):
+                 groups: Optional[Sequence[int]] = None, round_batched: Optional[bool] = None,
+                 fedavg_wire: str = "fp32"):
         self.logger = logger or logging.getLogger("gfedntm_amd.federation")
         self.agg_mode = agg
+        if fedavg_wire != "fp32" and agg != "params":
+            raise ValueError("fedavg_wire bf16delta averages parameters (agg 'params')")
         self.metrics = MetricsWriter(metrics_path)
         self.metrics_every = int(metrics_every)
         self.device = torch.device(device) if device is not None else \
@@ -148,7 +151,10 @@ class LocalFederation:
             self.clients.append(c)
         # groups: client-block sizes of a multi-rank layout (hierarchical/run_distributed_multi)
         # -- the FedAvg sums each block first, then the block sums, in that run's order
-        self.agg = LocalAggregator(n, groups)
+        # fedavg_wire "bf16delta": the in-process golden of the reduced-byte FedAvg (every
+        # group -- by default every client -- one rank); eager rounds
+        self.agg = LocalAggregator(n, groups, wire=fedavg_wire)
+        self.agg.set_reference(self.clients[0].shared)
         # fused clients on one GPU: every client's step and the FedAvg kernel are
         # captured into ONE hipGraph per round (one replay instead of N step graphs
         # plus the eager aggregation), each client on its own stream: parallel graph
@@ -156,7 +162,7 @@ class LocalFederation:
         # with branches vs 0.49 ms serialised, profiles/sim_clients.md)
         # (engines on the CTM host-GEMM fallback stay out of it: their hipBLASLt GEMMs
         # would run for the first time on the capture's per-client branch streams)
-        can = (agg == "params" and graph and self.device.type == "cuda"
+        can = (agg == "params" and graph and self.device.type == "cuda" and fedavg_wire == "fp32"
                and all(c.fused and not c.tm.engine.host_gemm_fallback for c in self.clients)
                and len(self.clients) > 1
                and self.agg._native([c.shared for c in self.clients]))
@@ -180,6 +186,7 @@ class LocalFederation:
             self.round = starts.pop()
             if self.round:
                 self.logger.info("-- -- Resuming the federation at round %d", self.round)
+            self.agg.set_reference(self.clients[0].shared)
 
     def _sync(self):
         if self.device.type == "cuda":
@@ -369,7 +376,7 @@ def run_distributed(corpus, params: Dict, model_type: str = "avitm",
                     agg_mode: str = "params", timing_warmup: int = 0,
                     rehearse_1gpu: Optional[bool] = None, allreduce: Optional[str] = None,
                     round_hook=None, client_ids: Optional[Sequence[int]] = None,
-                    keep_round: bool = False) -> Dict:
+                    keep_round: bool = False, fedavg_wire: str = "fp32") -> Dict:
     """Runs this process's client(s); torch.distributed must be initialised (RANK /
     WORLD_SIZE).  ``corpus`` is this rank's one client (id rank + 1), or a list of client
     corpora with their ids ``client_ids`` -- a contiguous block of a federation of more
@@ -409,6 +416,11 @@ def run_distributed(corpus, params: Dict, model_type: str = "avitm",
     ``GFEDNTM_INJECT_CORRUPT=rank:round`` flips one word of that rank's shared state after
     every round from ``round`` on (a persistent data-plane fault; a one-off divergence is
     re-averaged by the next all-reduce and leaves the replicas equal again).
+
+    ``fedavg_wire``: "fp32" (default; the reference's averaging) or "bf16delta" -- the
+    opt-in reduced-byte FedAvg: each rank sends its pre-scaled state's departure from the
+    last averaged state in bf16 (half the bytes over xGMI), summed in fp32
+    (parallel/aggregator.py, csrc/comm.hip gfk_xgmi_allreduce_bf16d).
 
     ``keep_round``: leave the rank's data plane attached after the run (the caller closes
     ``out["round"]``; bench.py times the bare engine loop on it); by default it is
@@ -493,9 +505,10 @@ def run_distributed(corpus, params: Dict, model_type: str = "avitm",
     # ---- data plane: this rank's round (its clients' steps + the FedAvg) ----
     if len(clients) == 1:
         rr = SingleClientRound(clients[0], world, device, on_gpu_plane, allreduce, agg_mode,
-                               bucket_bytes, logger)
+                               bucket_bytes, logger, wire=fedavg_wire)
     else:
-        rr = MultiClientRound(clients, world, device, on_gpu_plane, allreduce, graph, logger)
+        rr = MultiClientRound(clients, world, device, on_gpu_plane, allreduce, graph, logger,
+                              wire=fedavg_wire)
     ok = False
     try:
         out = _round_loop(rr, clients, client_ids, cmap, world, rank, device, ctrl, hb, logger,
@@ -541,6 +554,7 @@ def _round_loop(rr, clients, client_ids, cmap, world, rank, device, ctrl, hb, lo
         dist.all_gather_object(rounds, start, group=ctrl)
         if len(set(rounds)) != 1:
             raise RuntimeError(f"inconsistent client checkpoints: rounds {rounds}")
+        rr.resync_reference()            # bf16delta: the loaded state is the last average
     # ---- rounds where every rank meets (some client does long host work after them)
     plan_info: List = [None] * world
     dist.all_gather_object(plan_info, [(c.host_heavy_rounds(), c.done_round()) for c in clients],

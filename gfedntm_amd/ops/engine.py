@@ -977,7 +977,7 @@ class FusedEngine(EngineBase):
         return ph
 
     # ------------------------------------------------------------------ FedAvg
-    def attach_fedavg(self, group=None, method: Optional[str] = None) -> str:
+    def attach_fedavg(self, group=None, method: Optional[str] = None, wire: str = "fp32") -> str:
         """Make the round's FedAvg all-reduce part of :meth:`step` (collective: call on
         every rank, after the shared state is pre-scaled).
 
@@ -986,12 +986,17 @@ class FusedEngine(EngineBase):
         final after prodlda_bwd (Adam + pre-scale in its epilogue), so its all-reduce
         runs on a side stream while row_bwd / post_bwd / win_update proceed, and only
         the encoder part stays on the critical path.  Otherwise (RCCL) the all-reduce
-        follows the step eagerly.  Returns the method in use."""
+        follows the step eagerly.  ``wire="bf16delta"``: the opt-in reduced-byte FedAvg
+        (parallel/aggregator.py; this engine's pre-scale is the rank's weight).  Returns the
+        method in use."""
         from ..parallel.aggregator import CollectiveAggregator
         self._comm = None
         shared = self.flat.shared
         parts = {k: shared[a:b] for k, (a, b) in self.fedavg_parts().items()}
-        aggs = {k: CollectiveAggregator(group, method=method) for k in parts}
+        if wire != "fp32" and self.fedavg_scale is None:
+            raise ValueError("bf16delta FedAvg needs the FedAvg pre-scale (set_fedavg_scale)")
+        aggs = {k: CollectiveAggregator(group, method=method, wire=wire, weight=self.fedavg_scale)
+                for k in parts}
         # large parts (beta at V ~ 100k: 90 MB) are all-reduced in place: the xGMI kernel
         # maps the state itself into the peers instead of copying it into a stage first
         # (2 S of local HBM traffic per round saved, one extra hand-off)
@@ -1017,7 +1022,8 @@ class FusedEngine(EngineBase):
             for a in aggs.values():
                 if a.xgmi is not None:
                     a.xgmi.close()
-            agg = CollectiveAggregator(group, method="rccl")
+            agg = CollectiveAggregator(group, method="rccl", wire=wire, weight=self.fedavg_scale)
+            agg.set_reference(shared)
             self._comm = {"mode": "eager", "rest": (agg, shared)}
             used = agg.active
         self._invalidate_graph()
@@ -1041,6 +1047,16 @@ class FusedEngine(EngineBase):
             w0 = flat.slots[wa[0]].offset
             return {"rest": (0, w0), "wa": (w0, b0), "beta": (b0, n)}
         return {"rest": (0, b0), "beta": (b0, n)}
+
+    def fedavg_set_reference(self):
+        """bf16delta: the current shared state becomes every part's last averaged state
+        (after a checkpoint was loaded into it)."""
+        if self._comm is None:
+            return
+        for k in ("rest", "beta", "wa"):
+            if k in self._comm:
+                agg, buf = self._comm[k]
+                agg.set_reference(buf)
 
     def detach_fedavg(self, close: bool = True):
         """Remove the in-step all-reduce (returns it for :meth:`restore_fedavg` when

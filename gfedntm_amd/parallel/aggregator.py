@@ -22,6 +22,7 @@ import itertools
 import time
 from typing import List, Optional, Sequence
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -40,8 +41,20 @@ class CollectiveAggregator:
     exactness check at :meth:`prepare`, RCCL otherwise.  The environment variable
     ``GFEDNTM_ALLREDUCE`` (rccl|xgmi|auto) overrides the default."""
 
-    def __init__(self, group=None, bucket_bytes: int = 64 << 20, method: Optional[str] = None):
+    def __init__(self, group=None, bucket_bytes: int = 64 << 20, method: Optional[str] = None,
+                 wire: str = "fp32", weight: Optional[float] = None):
+        """``wire``: "fp32" (the reference's averaging: the sum of the pre-scaled states) or
+        "bf16delta" (opt-in, half the bytes: bf16 departures of the rank's pre-scaled state
+        from the last averaged state, ``weight`` = the rank's FedAvg weight sum; see
+        csrc/comm.hip gfk_xgmi_allreduce_bf16d and :meth:`_delta_allreduce`)."""
         import os
+        if wire not in ("fp32", "bf16delta"):
+            raise ValueError("wire must be 'fp32' or 'bf16delta'")
+        if wire == "bf16delta" and weight is None:
+            raise ValueError("bf16delta needs this rank's FedAvg weight")
+        self.wire = wire
+        self.weight = None if weight is None else float(np.float32(weight))
+        self.ref: Optional[torch.Tensor] = None      # bf16delta over RCCL / gloo
         self.group = group
         self.bucket_elems = max(1, bucket_bytes // 4)
         self.world = dist.get_world_size(group)
@@ -59,10 +72,25 @@ class CollectiveAggregator:
         ``flat`` itself into the peers (no stage copy; every later call must pass this
         very buffer).  Returns the method in use."""
         t_setup = time.perf_counter()
+        if self.wire == "bf16delta":
+            inplace = False                  # the peers read deltas, not the state
+        initial = flat.detach().clone() if self.wire == "bf16delta" else None
         try:
             return self._prepare(flat, inplace)
         finally:
             self.setup_s = time.perf_counter() - t_setup
+            if initial is not None:          # the last averaged state so far: the state itself
+                self.set_reference(initial)
+
+    def set_reference(self, t: torch.Tensor):
+        """bf16delta: reset the last averaged state (W0 at setup; the loaded state after a
+        checkpoint resume).  Identical on every rank."""
+        if self.wire != "bf16delta":
+            return
+        if self.xgmi is not None:
+            self.xgmi.set_reference(t)
+        else:
+            self.ref = t.detach().reshape(-1).clone()
 
     def _prepare(self, flat: torch.Tensor, inplace: bool = False) -> str:
         if self.world == 1 or self.method == "rccl" or flat.device.type != "cuda":
@@ -77,7 +105,8 @@ class CollectiveAggregator:
             from .xgmi import XgmiAllReduce
             try:
                 xg = XgmiAllReduce(flat.numel(), flat.device, group=self.group,
-                                   data=flat if inplace else None)
+                                   data=flat if inplace else None, wire=self.wire,
+                                   weight=self.weight)
             except Exception as e:   # every rank must reach the agreement below
                 import logging
                 logging.getLogger("gfedntm_amd.xgmi").warning(
@@ -108,7 +137,9 @@ class CollectiveAggregator:
                     flat.copy_(saved)
                     del saved
             err = xg.error()
-            tr = self._time(lambda b: dist.all_reduce(b, group=self.group), flat)
+            tr = self._time((lambda b: dist.all_reduce(b, group=self.group)) if self.wire == "fp32"
+                            else (lambda b: dist.all_reduce(b.to(torch.bfloat16), group=self.group)),
+                            flat)
             t = torch.tensor([tx, tr, float(err != 0)], dtype=torch.float64, device=flat.device)
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
             tx, tr, bad = (float(v) for v in t.tolist())
@@ -146,7 +177,7 @@ class CollectiveAggregator:
 
     def describe(self) -> dict:
         """What the data plane of this buffer is (for the fedavg_attach records)."""
-        d = {"method": self.active}
+        d = {"method": self.active, "wire": self.wire}
         if self.xgmi is not None:
             d["inplace"] = self.xgmi.data is not None
             d["flags_uncached"] = self.xgmi.flags_uncached
@@ -169,6 +200,9 @@ class CollectiveAggregator:
         if self.xgmi is not None and n == self.xgmi.n and not async_op:
             self.xgmi.allreduce_(flat)
             return []
+        if self.wire == "bf16delta":
+            self._delta_allreduce(flat)
+            return []
         works = []
         for a in range(0, n, self.bucket_elems):
             w = dist.all_reduce(flat[a: a + self.bucket_elems], op=dist.ReduceOp.SUM,
@@ -176,6 +210,26 @@ class CollectiveAggregator:
             if async_op:
                 works.append(w)
         return works
+
+    def _delta_allreduce(self, flat: torch.Tensor):
+        """bf16delta over torch.distributed (RCCL / gloo): d = bf16(f - w ref) on the wire
+        (RCCL sums bf16), W = ref + sum, ref = W -- identical on every rank.  A backend
+        without bf16 reductions (gloo builds) sums the bf16-rounded values in fp32 and rounds
+        the sum to bf16 instead (the xGMI kernel's arithmetic)."""
+        if self.ref is None:
+            self.ref = flat.detach().reshape(-1).clone()
+        ref = self.ref
+        t = ref * torch.tensor(self.weight, dtype=torch.float32, device=ref.device)
+        d = (flat.reshape(-1) - t).to(torch.bfloat16)
+        try:
+            dist.all_reduce(d, op=dist.ReduceOp.SUM, group=self.group)
+            s = d.float()
+        except (RuntimeError, ValueError):
+            s = d.float()
+            dist.all_reduce(s, op=dist.ReduceOp.SUM, group=self.group)
+            s = s.to(torch.bfloat16).float()
+        flat.reshape(-1).copy_(ref + s)
+        ref.copy_(flat.reshape(-1))
 
     def average_(self, flat: torch.Tensor, weight: float):
         """Weighted average without a prior pre-scale (generic path)."""
@@ -276,13 +330,54 @@ class LocalAggregator:
     (each rank folds its clients, the collective folds the ranks), so the in-process
     golden and the distributed run agree bit for bit."""
 
-    def __init__(self, n_samples: Sequence[int], groups: Optional[Sequence[int]] = None):
+    def __init__(self, n_samples: Sequence[int], groups: Optional[Sequence[int]] = None,
+                 wire: str = "fp32"):
         self.n = [int(x) for x in n_samples]
         self.w = fedavg_weights(self.n)
         self.groups = None if groups is None else [int(g) for g in groups]
         if self.groups is not None and sum(self.groups) != len(self.n):
             raise ValueError(f"groups {self.groups} do not partition {len(self.n)} clients")
+        if wire not in ("fp32", "bf16delta"):
+            raise ValueError("wire must be 'fp32' or 'bf16delta'")
+        # bf16delta: the in-process golden of the distributed bf16-delta FedAvg -- every group
+        # (default: every client) is one rank of csrc/comm.hip gfk_xgmi_allreduce_bf16d
+        self.wire = wire
+        self.ref: Optional[torch.Tensor] = None
         self._desc = None
+
+    def set_reference(self, t: torch.Tensor):
+        """bf16delta: the last averaged state (W0 at the start, or a resumed state)."""
+        self.ref = t.detach().reshape(-1).clone()
+
+    def group_weights(self) -> List[float]:
+        """Every group's FedAvg weight sum as the float32 the ranks use."""
+        groups = self.groups or [1] * len(self.n)
+        out, j = [], 0
+        for g in groups:
+            out.append(float(np.float32(sum(self.w[j:j + g]))))
+            j += g
+        return out
+
+    def _delta_(self, flats: Sequence[torch.Tensor]):
+        """bf16delta round on pre-scaled client states: per group, d_g = bf16(fold_g - w_g ref);
+        S = bf16(fp32 sum of the d_g in group order); every client <- ref + S = ref."""
+        if self.ref is None:
+            raise RuntimeError("bf16delta: set_reference(W0) first")
+        ref = self.ref
+        groups = self.groups or [1] * len(flats)
+        s, j = None, 0
+        for g, wg in zip(groups, self.group_weights()):
+            part = flats[j].detach().reshape(-1).clone()
+            for f in flats[j + 1:j + g]:
+                part.add_(f.reshape(-1))
+            j += g
+            t = ref * torch.tensor(wg, dtype=torch.float32, device=ref.device)
+            d = (part - t).to(torch.bfloat16).float()
+            s = d if s is None else s + d
+        ref.copy_(ref + s.to(torch.bfloat16).float())
+        for f in flats:
+            f.reshape(-1).copy_(ref)
+        return flats[0]
 
     def _native(self, flats: Sequence[torch.Tensor]) -> bool:
         if flats[0].device.type != "cuda":
@@ -302,6 +397,8 @@ class LocalAggregator:
         """flats[i] <- sum_j flats[j] (client order, group-wise) for all i, one kernel
         launch on the current stream.  Returns False when the buffers don't qualify
         (caller falls back)."""
+        if self.wire != "fp32":
+            return False
         if len(flats) == 1:
             return True
         if not self._native(flats):
@@ -312,6 +409,11 @@ class LocalAggregator:
     def average_(self, flats: Sequence[torch.Tensor], prescaled: bool = False,
                  out: Optional[torch.Tensor] = None):
         """flats[i] <- sum_j w_j flats[j] for all i (in place)."""
+        if self.wire == "bf16delta":
+            if not prescaled:
+                for w, f in zip(self.w, flats):
+                    f.mul_(w)
+            return self._delta_(flats)
         if len(flats) == 1 and prescaled:
             return flats[0]
         if prescaled and out is None and self.fused_sum_(flats):

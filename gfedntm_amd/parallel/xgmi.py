@@ -38,7 +38,11 @@ class GfkComm(C.Structure):
     _fields_ = [("stage", (P * CMAX) * 2), ("flags", P * CMAX), ("epoch", P), ("err", P),
                 ("rank", C.c_int32), ("world", C.c_int32), ("nblk", C.c_int32),
                 ("spin_limit", C.c_int32), ("n", C.c_int64), ("chunk", C.c_int64),
-                ("slice", C.c_int64), ("inplace", C.c_int32), ("pad", C.c_int32)]
+                ("slice", C.c_int64), ("inplace", C.c_int32), ("pad", C.c_int32),
+                ("ref", P), ("wgt", C.c_float), ("wire", C.c_int32)]
+
+
+WIRES = ("fp32", "bf16delta")
 
 
 def _declare(lib):
@@ -104,9 +108,19 @@ class XgmiAllReduce:
     single-node process group (≤ 8 ranks; several ranks may share one GPU)."""
 
     def __init__(self, n: int, device, group=None, nblk: Optional[int] = None,
-                 spin_limit: Optional[int] = None, data: Optional[torch.Tensor] = None):
+                 spin_limit: Optional[int] = None, data: Optional[torch.Tensor] = None,
+                 wire: str = "fp32", weight: Optional[float] = None):
         """``data``: in-place mode -- this fixed buffer (every call must pass it) is itself
-        IPC-mapped into the peers, so no stage copy of the state is made (large states)."""
+        IPC-mapped into the peers, so no stage copy of the state is made (large states).
+        ``wire="bf16delta"``: the opt-in reduced-byte FedAvg (csrc/comm.hip
+        gfk_xgmi_allreduce_bf16d) -- bf16 departures from the last averaged state
+        (:attr:`ref`, set with :meth:`set_reference`), ``weight`` = this rank's FedAvg weight
+        sum; always staged."""
+        if wire not in WIRES:
+            raise ValueError(f"wire must be one of {WIRES}")
+        if wire == "bf16delta" and (data is not None or weight is None):
+            raise ValueError("bf16delta: staged only, and it needs the rank's FedAvg weight")
+        self.wire = wire
         self.lib = native.kernels()
         _declare(self.lib)
         self.group = group
@@ -124,6 +138,7 @@ class XgmiAllReduce:
         # 32-bit buffer offsets in the kernel (csrc/comm.hip rsrc / ld_sys / st_sys): a
         # larger state is refused here and the caller keeps RCCL for it (logged there)
         limit = int(self.lib.gfk_comm_max_bytes())
+        esz = 2 if wire == "bf16delta" else 4          # stage element bytes
         if 4 * self.world * chunk > limit:
             raise ValueError(f"xGMI all-reduce: {4 * self.world * chunk} B of stage exceed the "
                              f"kernel's 32-bit offset range ({limit} B)")
@@ -139,7 +154,7 @@ class XgmiAllReduce:
             raise ValueError("xGMI in-place buffer: fp32, contiguous, 16-B aligned, n floats")
         with torch.cuda.device(self.device):
             stage, flags, state, unc = P(), P(), P(), C.c_int(0)
-            stage_bytes = 16 if inplace else self.world * chunk * 4
+            stage_bytes = 16 if inplace else self.world * chunk * esz
             flag_bytes = (3 if inplace else 2) * nblk * CMAX * 4
             rc = self.lib.gfk_comm_alloc(stage_bytes, flag_bytes, nblk * 4 + 16,
                                          C.byref(stage), C.byref(flags), C.byref(state),
@@ -183,6 +198,16 @@ class XgmiAllReduce:
             c.err = state.value + nblk * 4
             c.rank, c.world, c.nblk, c.spin_limit = self.rank, self.world, nblk, int(spin_limit)
             c.n, c.chunk, c.slice = self.n, chunk, slice_
+            self.ref = None
+            self.weight = None
+            if wire == "bf16delta":
+                # every rank's weight (the validation regenerates each peer's delta)
+                self.weight = float(torch.tensor(float(weight), dtype=torch.float32).item())
+                ws: List = [None] * self.world
+                dist.all_gather_object(ws, self.weight, group=group)
+                self.weights = [float(x) for x in ws]
+                self.ref = torch.zeros(self.n + 16, dtype=torch.float32, device=self.device)[:self.n]
+                c.ref, c.wgt, c.wire = self.ref.data_ptr(), self.weight, 1
             self.c = c
             self._err_ptr = c.err
 
@@ -255,6 +280,23 @@ class XgmiAllReduce:
         if rc:
             raise RuntimeError(f"gfk_comm_error_async failed ({rc})")
 
+    def set_reference(self, t: torch.Tensor):
+        """bf16delta: the last averaged state (identical on every rank): W0 at attach, the
+        loaded state after a checkpoint resume."""
+        if self.ref is not None:
+            self.ref.copy_(t.reshape(-1))
+
+    def expected_bf16delta(self, datas, ref: torch.Tensor) -> torch.Tensor:
+        """The kernel's arithmetic on explicit inputs (every rank's data, the common ref), in
+        torch: d_r = bf16(f_r - w_r ref) (product rounded, then the difference), the fp32 sum
+        of the d_r in rank order rounded to bf16, ref + that."""
+        s = None
+        for j, f in enumerate(datas):
+            t = ref * torch.tensor(self.weights[j], dtype=torch.float32, device=ref.device)
+            d = (f - t).to(torch.bfloat16).float()
+            s = d if s is None else s + d
+        return ref + s.to(torch.bfloat16).float()
+
     def validate(self, rounds: int = 3) -> bool:
         """All-reduce rank-dependent data ``rounds`` times and compare with the exact
         rank-ordered fp32 sum; True only if every rank agrees.  The peers' inputs are
@@ -274,10 +316,18 @@ class XgmiAllReduce:
                     if self.data is not None:     # in-place: the probe goes through the buffer
                         self.data.copy_(t)
                         t = self.data
-                    self.allreduce_(t)
-                    exp = self._probe(0, r)
-                    for j in range(1, self.world):      # the kernel's order: rank 0, 1, ...
-                        exp.add_(self._probe(j, r))
+                    if self.wire == "bf16delta":
+                        ref = self._probe(self.world + 7, r)    # the same on every rank
+                        self.ref.copy_(ref)
+                        self.allreduce_(t)
+                        exp = self.expected_bf16delta([self._probe(j, r) for j in range(self.world)],
+                                                      ref)
+                        ok &= bool(torch.equal(self.ref, exp))
+                    else:
+                        self.allreduce_(t)
+                        exp = self._probe(0, r)
+                        for j in range(1, self.world):      # the kernel's order: rank 0, 1, ...
+                            exp.add_(self._probe(j, r))
                     ok &= bool(torch.equal(t, exp))
                     del t, exp
                 ok &= self.error() == 0

@@ -121,6 +121,8 @@ class FedConfig:
     aggregate: str = "params"
     checkpoint_every: int = 0
     stop_at_num_epochs: bool = False
+    # FedAvg wire: "fp32" (the reference's averaging) | "bf16delta" (opt-in, half the bytes)
+    fedavg_wire: str = "fp32"
 
     def grpc_client_options(self):
         """Channel options used by a process dialing out (reference main.py:219-231)."""
@@ -196,6 +198,9 @@ def load_config(file_path: Optional[str] = None) -> FedConfig:
     cfg.aggregate = get("amd", "aggregate", cfg.aggregate)
     cfg.checkpoint_every = get("amd", "checkpoint_every", cfg.checkpoint_every, int)
     cfg.stop_at_num_epochs = get("amd", "stop_at_num_epochs", cfg.stop_at_num_epochs, bool)
+    cfg.fedavg_wire = get("amd", "fedavg_wire", cfg.fedavg_wire)
+    if cfg.fedavg_wire not in ("fp32", "bf16delta"):
+        raise ValueError(f"[amd] fedavg_wire must be fp32 or bf16delta, got {cfg.fedavg_wire!r}")
     mm = get("amd", "matmul_dtype", "fp32")
     if mm != "fp32":
         cfg.training_params["matmul_dtype"] = mm
