@@ -323,6 +323,7 @@ def run_multi(args, rank, world, device, rehearse):
             + (", batched steps + in-rank fold" if per_rank[-1] > 1 else "")
             + f", {out['allreduce'] or 'no'} all-reduce across ranks)")
         rec["path"] = "run_distributed"
+        rec["engine_ran"] = out["clients"][0].tm.engine_info
         rec["digests"] = out.get("digests")
         if fallback:
             rec["allreduce_fallback"] = fallback
@@ -433,6 +434,7 @@ def run_federated(args):
                          ranks=world, physical=physical)
         record.update({k: v for k, v in quality.items() if k != "npmi"})
         record["path"] = args.path
+        record["engine_ran"] = client.tm.engine_info
         record["digests"] = out_digests
         if fallback:
             record["allreduce_fallback"] = fallback
@@ -502,6 +504,7 @@ def run_simulated(args):
     rec["config"]["aggregation"] += (f" (in-process FedAvg kernel in one round graph, {mode})"
                                      if fed.round_graph else " (eager)")
     rec["path"] = "LocalFederation"
+    rec["engine_ran"] = fed.clients[0].tm.engine_info
     _ctx_note(rec, args, eng)
     print(json.dumps(rec), flush=True)
 

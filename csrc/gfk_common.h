@@ -610,6 +610,11 @@ __device__ __forceinline__ f32x4 mfma16x16x32bf(const float (&a)[8], const float
   for (int j = 0; j < 8; ++j) { ab[j] = (__bf16)a[j]; bb[j] = (__bf16)b[j]; }
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ab, bb, c, 0, 0, 0);
 }
+// fp32 -> bf16 (round to nearest even) -> fp32: a bf16 operand of an fp32 product (the
+// products of bf16 values are exact in fp32, so a bf16 dot / GEMM with fp32 accumulation is
+// this rounding followed by fp32 multiply-adds)
+__device__ __forceinline__ float bf16_round(float x) { return (float)(__bf16)x; }
+
 // The same with operands converted once by the caller (an operand reused by several MFMAs).
 __device__ __forceinline__ bf16x8 to_bf16x8(const f32x4& lo, const f32x4& hi) {
   bf16x8 r;

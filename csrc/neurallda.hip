@@ -130,6 +130,9 @@ __global__ void __launch_bounds__(LDA_ROW_THREADS) gfk_lda_row_k(GfkArgT<GB> ga)
   const int b = blockIdx.x, nb = *m.ws_nb;
   if (b >= nb) return;
   const int K = m.K, tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
+  // matmul_dtype = "bf16": theta_d and beta_sm are bf16 operands of word_dist = theta_d
+  // beta_sm and of d theta_d = g beta_sm^T (fp32 accumulation)
+  const bool bfo = m.mm_bf16;
   float* dth = smem;
   float* rls = dth + LDA_ROW_WAVES * K;
   float th[KQ], ls[KQ];
@@ -137,6 +140,7 @@ __global__ void __launch_bounds__(LDA_ROW_THREADS) gfk_lda_row_k(GfkArgT<GB> ga)
   for (int q = 0; q < KQ; ++q) {
     const int k = lane + 64 * q;
     th[q] = k < K ? m.ws_thetad[(size_t)b * m.kt + k] : 0.f;
+    if (bfo) th[q] = bf16_round(th[q]);
     ls[q] = k < K ? m.ws_lse[k] : 0.f;
   }
   const int e0 = m.ws_erange[2 * b], e1 = m.ws_erange[2 * b + 1];
@@ -167,6 +171,7 @@ __global__ void __launch_bounds__(LDA_ROW_THREADS) gfk_lda_row_k(GfkArgT<GB> ga)
 #pragma unroll
       for (int q = 0; q < KQ; ++q) {
         bs[q] = lane + 64 * q < K ? __expf(z[u][q] - ls[q]) : 0.f;
+        if (bfo) bs[q] = bf16_round(bs[q]);
         wd += th[q] * bs[q];
       }
       wd = wave_sum(wd);
@@ -316,7 +321,10 @@ __global__ void __launch_bounds__(LBT) gfk_lda_beta_bwd_k(GfkArgT<GB> ga) {
       const float* ap = xt + (i0 + (lane & 15)) * XS + (lane >> 4);
       const float* bp = thv + (lane >> 4) * kt + j0 + (lane & 15);
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      for (int kb = 0; kb < B; kb += 4) acc = mfma16x16x4(ap[kb], bp[kb * kt], acc);
+      if (m.mm_bf16)        // bf16 operands (the coefficients and theta_d), fp32 accumulation
+        for (int kb = 0; kb < B; kb += 4) acc = mfma16x16x4(bf16_round(ap[kb]), bf16_round(bp[kb * kt]), acc);
+      else
+        for (int kb = 0; kb < B; kb += 4) acc = mfma16x16x4(ap[kb], bp[kb * kt], acc);
       const int k = j0 + (lane & 15);
       if (k < K) {
         const float ck = ckl[k];

@@ -18,6 +18,8 @@ documents of each node and evaluated on the next ``n_docs_global_inf``:
   federated_grads    (new) the nodes as clients of classic synchronous data
                parallelism (``agg="grads"``: the sample-weighted gradient average, one
                optimizer step per round on every replica) -- not the reference protocol
+  federated_bf16delta (new) the federated arm over the opt-in reduced-byte FedAvg wire
+               (``fedavg_wire="bf16delta"``: bf16 departures from the last average)
 
 TSS = sum over true topics of the best Bhattacharyya coefficient with a learned
 topic (learned betas re-indexed onto the generator vocabulary).  With
@@ -64,7 +66,7 @@ DEFAULTS = dict(n_nodes=5, vocab_size=5000, n_topics=50, beta=1e-2, alpha=0.1, n
                 reference_tss=True)
 
 ARMS = ("centralized", "non_colab", "baseline", "federated", "federated_matched",
-        "federated_grads")
+        "federated_grads", "federated_bf16delta")
 
 
 def _vocab_of(counts: sp.csr_matrix):
@@ -200,11 +202,15 @@ def run_iteration(cfg, frozen_topics: int, eta: float, device, seed: int) -> Dic
         out["federated_grads"] = _federated(cfg, sc, train, inf_counts, inf_thetas, device, seed,
                                             agg="grads")
         done("federated_grads")
+    if "federated_bf16delta" in arms:
+        out["federated_bf16delta"] = _federated(cfg, sc, train, inf_counts, inf_thetas, device,
+                                                seed, wire="bf16delta")
+        done("federated_bf16delta")
     return out
 
 
 def _federated(cfg, sc, train, inf_counts, inf_thetas, device, seed, rounds=None,
-               agg: str = "params"):
+               agg: str = "params", wire: str = "fp32"):
     from ..federation.data import ClientCorpus
     from ..federation.runner import LocalFederation
     sub = SyntheticCorpus(sc.topic_vectors, [t[: c.shape[0]] for t, c in zip(sc.doc_topics, train)],
@@ -218,7 +224,7 @@ def _federated(cfg, sc, train, inf_counts, inf_thetas, device, seed, rounds=None
         rounds = cfg["num_epochs"] * steps_per_epoch
     params["num_epochs"] = -(-rounds // steps_per_epoch)
     fed = LocalFederation(corpora, params, max_iters=rounds, device=device,
-                          backend=cfg["backend"], seed=seed, agg=agg)
+                          backend=cfg["backend"], seed=seed, agg=agg, fedavg_wire=wire)
     fed.run()
     tm = fed.clients[0].tm                     # every client holds the averaged state
     id2token = dict(enumerate(fed.terms))

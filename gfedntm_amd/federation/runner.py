@@ -305,6 +305,7 @@ class LocalFederation:
         for c in self.clients:
             c.flush()
         self.metrics.write(event="train_end", rounds=n_rounds, wall_s=wall,
+                           **self.clients[0].tm.engine_info,
                            docs=docs, docs_per_s=docs / wall if wall and docs else None,
                            ms_per_round=1e3 * wall / max(n_rounds, 1))
         with trace_range("finish"):
@@ -718,6 +719,7 @@ def _round_loop(rr, clients, client_ids, cmap, world, rank, device, ctrl, hb, lo
     n_rounds = last + 1 - timed_from
     docs = sum(int(c.plan.size[timed_from: last + 1].sum()) for c in clients) if n_rounds > 0 else 0
     metrics.write(event="train_end", rank=rank, clients=list(client_ids), rounds=n_rounds,
+                  **clients[0].tm.engine_info,
                   wall_s=wall, docs=docs, docs_per_s=docs / wall if wall and docs else None,
                   ms_per_round=1e3 * wall / max(n_rounds, 1))
     for c in clients:

@@ -161,6 +161,16 @@ class TopicModelBase:
     def _build_network(self, **extra):
         raise NotImplementedError
 
+    backend_fallback_reason = None
+
+    @property
+    def engine_info(self) -> dict:
+        """Which local-step engine runs this model, and why not the fused one if not."""
+        d = {"engine": self.backend}
+        if self.backend_fallback_reason:
+            d["fused_unavailable"] = self.backend_fallback_reason
+        return d
+
     def _choose_backend(self, backend: str) -> str:
         if backend == "auto":
             from ..ops import engine as fused
@@ -177,6 +187,8 @@ class TopicModelBase:
             except RuntimeError as e:
                 logging.getLogger("gfedntm_amd").warning(
                     "%s; this configuration runs on the PyTorch engine", e)
+                # recorded (engine_info: bench / metrics records say which engine ran)
+                self.backend_fallback_reason = str(e)
                 return "torch"
         if backend == "fused":
             from ..ops import engine as fused

@@ -89,8 +89,6 @@ def supports(tm, explain: bool = False) -> bool:
         (max(tm.hidden_sizes) <= 512 and len(tm.hidden_sizes) <= abi.MAX_LAYERS,
          "hidden layers too wide / too many"),
         (getattr(tm, "label_size", 0) <= 256, "label_size > 256"),
-        (getattr(tm, "matmul_dtype", "fp32") == "fp32" or tm.model_type.lower() == "prodlda",
-         "bf16 decoder GEMMs are ProdLDA only"),
     ]
     # reduce_on_plateau needs nothing here: the reference builds ReduceLROnPlateau
     # (avitm.py:156-157) but never calls scheduler.step(), so the lr never changes

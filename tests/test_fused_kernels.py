@@ -984,3 +984,48 @@ def test_ctm_bf16_contextual_matches_emulated_oracle(V):
         scale = p.grad.abs().max().item() + 1e-6
         torch.testing.assert_close(g[k], p.grad, rtol=3e-2, atol=2e-2 * scale,
                                    msg=lambda m: f"{k}: {m}")
+
+
+@pytest.mark.parametrize("K,V", [(50, 2000), (100, 30000)])
+def test_bf16_neurallda_matches_emulated_oracle(K, V):
+    """matmul_dtype='bf16' on NeuralLDA: word_dist = theta_d beta_sm with bf16 theta_d and
+    beta_sm (lda_row: per non-zero dot products, fp32 accumulation; the same bf16 beta_sm in
+    d theta_d) and the backward's coefficient x theta_d product (lda_beta_bwd) on bf16
+    operands.  Oracle: the fp32 step with theta_d and beta_sm rounded to bf16 before their
+    product (reference decoder_network.py:127-132)."""
+    import torch.nn.functional as F
+    from gfedntm_amd.models.functional import encoder_forward
+    from gfedntm_amd.models.networks import kl_terms, reconstruction_terms
+    fused, ref = _pair("LDA", V=V, K=K, H=(50, 50), B=64, matmul_dtype="bf16")
+    assert fused.engine._m.mm_bf16 == 1
+    X = random_csr(150, V, 60, seed=1)
+    data, plan = _bind(fused, X, B=64)
+    e = fused.engine
+    e.run_phases(e.phases()[:-1])
+    torch.cuda.synchronize()
+    nb = int(plan.size[0])
+    ids = torch.from_numpy(plan.batch(0).astype(np.int64)).cuda()
+    x = data.dense_rows(ids)
+    model = ref.model
+    model.train()
+    model.zero_grad()
+    mu, ls = encoder_forward(model.inf_net, x, e.ws["mask_h"][:nb])
+    theta = F.softmax(mu + e.ws["eps"][:nb] * torch.exp(0.5 * ls), dim=1)
+    thetad = theta * e.ws["mask_t"][:nb]
+    bfr = lambda t: t + (_bf(t) - t).detach()      # noqa: E731
+    bb = model.beta_batchnorm
+    bnb = F.batch_norm(model.beta, bb.running_mean, bb.running_var, training=True,
+                       momentum=bb.momentum, eps=bb.eps)
+    wd = bfr(thetad) @ bfr(F.softmax(bnb, dim=1))
+    kl = kl_terms(model.prior_mean, model.prior_variance, mu, torch.exp(ls), ls, K)
+    rl = reconstruction_terms(x, wd)
+    loss = (kl + rl).sum()
+    loss.backward()
+    torch.testing.assert_close(e.ws["rl"][:nb], rl.detach(), rtol=2e-4, atol=5e-2)
+    g = _grads_of(fused)
+    for k, p in model.named_parameters():
+        if k in _NOISE_KEYS:
+            continue
+        scale = p.grad.abs().max().item() + 1e-6
+        torch.testing.assert_close(g[k], p.grad, rtol=3e-2, atol=2e-2 * scale,
+                                   msg=lambda m: f"{k}: {m}")
