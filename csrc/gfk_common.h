@@ -192,6 +192,11 @@ constexpr int GFK_WIN_SPLIT = 128;
 // the batch-coupled posterior itself (csrc/prodlda.hip, FP) and post_fwd is not launched --
 // where it applies: strip ring forward (bit 2 + bit 8), K <= 64, B <= 64, no label head
 constexpr int GFK_FWD_POSTFOLD = 65536;
+// stage_flags bit 17 (GFK_POST_EXTRA_ROWBWD): post_bwd's batch-level workgroup (prior
+// gradients, the loss, the step counter) runs as an extra workgroup of row_bwd instead, so
+// post_bwd is exactly bmax workgroups (batched launches: M clients' post_bwd then fits one
+// round of the CUs' slots; its inputs -- mu, log sigma^2, KL, RL -- are final before row_bwd)
+constexpr int GFK_POST_EXTRA_ROWBWD = 131072;
 __host__ __device__ inline bool gfk_postfold(const GfkModel& m) {
   return (m.stage_flags & GFK_FWD_POSTFOLD) && (m.stage_flags & 4) && (m.stage_flags & 256) &&
          m.K <= 64 && m.bmax <= 64 && !m.lab_on && m.kind == GFK_PRODLDA;

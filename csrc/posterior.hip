@@ -437,8 +437,45 @@ __global__ void __launch_bounds__(FT) gfk_post_fwd_k(GfkArgT<GB> ga) {
 // backward, part 1 (own row): d theta_d from the decoder partials, softmax /
 // reparameterisation / KL backward
 // ---------------------------------------------------------------------------
-// grid: bmax workgroups.  dynamic LDS: part[4][K]
+// grid: bmax workgroups (+ the batch-level one, stage_flags GFK_POST_EXTRA_ROWBWD).
+// dynamic LDS: part[4][K]
 extern "C" size_t gfk_row_bwd_smem(const GfkModel* m) { return sizeof(float) * 4 * (size_t)pad4(m->K); }
+
+// The batch-level work of the step's backward (post_bwd's extra workgroup, here as row_bwd's
+// last workgroup of PT threads): the priors' gradients -> their grad slots,
+//   d prior_mean = w (nb pm - sum_b mu_b) / pv,
+//   d prior_var  = w / 2 (nb / pv - sum_b exp(ls_b) / pv^2 - sum_b (pm - mu_b)^2 / pv^2),
+// the loss sum_b (w KL_b + RL_b [+ CE_b]) -> loss_hist[step], and the step counter.  Thread k
+// sums topic k's column over the rows (coalesced across threads), in row order.
+__device__ __forceinline__ void post_batch_level(const GfkModel& m, int nb, float* scratch, int tid) {
+  const int K = m.K;
+  const float wk = m.kl_weight;
+  const int step0 = *m.step;
+  float lterm = 0.f;
+  for (int b = tid; b < nb; b += PT)
+    lterm += wk * m.ws_kl[b] + m.ws_rl[b] + (m.lab_on ? m.ws_ce[b] : 0.f);
+  if (m.learn_priors) {
+    for (int k = tid; k < K; k += PT) {
+      const float pm = m.prior_mean[k], pv = m.prior_var[k];
+      float smu = 0.f, svar = 0.f, sdm2 = 0.f;
+#pragma unroll 4
+      for (int b = 0; b < nb; ++b) {
+        const float mu = m.ws_mu[b * K + k], ls = m.ws_ls[b * K + k];
+        smu += mu;
+        svar += expf(ls);
+        const float dm = pm - mu;
+        sdm2 += dm * dm;
+      }
+      m.prior_mean[k + m.off_g] = wk * ((float)nb * pm - smu) / pv;
+      m.prior_var[k + m.off_g] = wk * 0.5f * ((float)nb / pv - svar / (pv * pv) - sdm2 / (pv * pv));
+    }
+  }
+  const float l = block_sum_wave0(lterm, scratch);
+  if (tid == 0) {
+    m.loss_hist[step0] = l;
+    *m.step = step0 + 1;
+  }
+}
 
 // KQ = ceil(K / 64) topics per lane: only live topics are loaded (K <= 64 -> one
 // load per partial), U partials per wave per round so a row's partials are in
@@ -454,6 +491,10 @@ __global__ void __launch_bounds__(PT) gfk_row_bwd_k(GfkArgT<GB> ga) {
   const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
   const int row = blockIdx.x;
   const int nb = *nbp;
+  if ((m.stage_flags & GFK_POST_EXTRA_ROWBWD) && row == B) {
+    post_batch_level(m, nb, part, tid);    // the batch-level workgroup (grid = bmax + 1)
+    return;
+  }
   if (row >= nb) return;
   GFK_STAMP(m, 8);
   // ---- wave w sums partials w, w + 4, ... of the row (lane = topic), all loads first ----
@@ -679,7 +720,7 @@ __global__ void __launch_bounds__(FT) gfk_post_bwd_k(GfkArgT<GB> ga) {
   keep(K, B, nh, sflags, dmu_g, dls_g, mu_g, ls_g, nbp);
   const int tid = threadIdx.x, lane = tid & 63;
   const int row = blockIdx.x;
-  const bool extra = row == (int)gridDim.x - 1;
+  const bool extra = !(sflags & GFK_POST_EXTRA_ROWBWD) && row == (int)gridDim.x - 1;
   const PostLds L = post_lds(m);
   const int Hl = m.H[nh - 1];
   constexpr bool staged = Staged;
@@ -916,7 +957,8 @@ extern "C" int gfk_launch_post_fwd(const GfkModel* m, hipStream_t s) {
 
 extern "C" int gfk_launch_post_bwd(const GfkModel* m, hipStream_t s) {
   const int kq = (m->K + 63) / 64;
-  const dim3 g(m->bmax), t(PT);
+  const bool moved = m->stage_flags & GFK_POST_EXTRA_ROWBWD;
+  const dim3 g(m->bmax + (moved ? 1 : 0)), t(PT);
   const size_t sm = gfk_row_bwd_smem(m);
   if (kq <= 1) do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_row_bwd_k<1, true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_row_bwd_k<1, false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0);
   else if (kq == 2) do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_row_bwd_k<2, true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_row_bwd_k<2, false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0);
@@ -924,7 +966,7 @@ extern "C" int gfk_launch_post_bwd(const GfkModel* m, hipStream_t s) {
   else do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_row_bwd_k<4, true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_row_bwd_k<4, false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  const dim3 gb(m->bmax + 1), tb(FT);     // + the prior / loss / step workgroup
+  const dim3 gb(m->bmax + (moved ? 0 : 1)), tb(FT);   // + the prior / loss / step workgroup
   const size_t sb = gfk_post_bwd_smem(m);
   const bool st = m->stage_flags & 1;
   if (batch_in_lds(*m)) {

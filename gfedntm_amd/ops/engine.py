@@ -68,6 +68,7 @@ STAGE_CTX_BAL3 = 8192             # bit 13: the balanced forward's 16-wave 3-dee
 STAGE_WIN_CTXPP = 16384           # bit 14: CombinedTM's contextual W_in half as a persistent kernel
 STAGE_CTX_RS = 32768              # bit 15: CombinedTM forward, Wa register-streamed (csrc/ctx.hip)
 STAGE_FWD_POSTFOLD = 65536        # bit 16: the strip forward computes post_fwd (csrc/prodlda.hip FP)
+STAGE_POST_EXTRA_ROWBWD = 131072  # bit 17: post_bwd's batch-level workgroup runs in row_bwd
 
 
 def _explain(ok: bool, why: str, explain: bool) -> bool:
@@ -1528,6 +1529,13 @@ class BatchedSteps:
                     and bstrip != "keep"):
                 mm.stage_flags = (mm.stage_flags & ~(STAGE_FWD_STRIP_ROLL | STAGE_FWD_STRIP_RING)) \
                     | STAGE_FWD_STRIP_PF
+            # post_bwd: M clients x (bmax + 1) workgroups of 16 waves with the batch matrices
+            # in LDS (~93 KB: one per CU) ran in three rounds at M = 8; with the matrices read
+            # from L2 (stage_flags bit 1, ~42 KB) and the batch-level workgroup moved into
+            # row_bwd, M bmax workgroups fit one round at two per CU (GFEDNTM_BATCH_POST=0: off)
+            if (M > 1 and M * (mm.bmax + 1) > self._cu
+                    and os.environ.get("GFEDNTM_BATCH_POST", "1") != "0"):
+                mm.stage_flags |= 2 | STAGE_POST_EXTRA_ROWBWD
             # win_update: all clients' W_in tiles in one launch -> the 8-wave tile shape once
             # they exceed two rounds of 16-wave workgroups (GFEDNTM_BATCH_WIN8=0: off)
             if (M * (mm.n_tiles + 8) > 2 * self._cu
