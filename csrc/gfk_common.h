@@ -197,6 +197,11 @@ constexpr int GFK_FWD_POSTFOLD = 65536;
 // post_bwd is exactly bmax workgroups (batched launches: M clients' post_bwd then fits one
 // round of the CUs' slots; its inputs -- mu, log sigma^2, KL, RL -- are final before row_bwd)
 constexpr int GFK_POST_EXTRA_ROWBWD = 131072;
+// stage_flags bit 18 (GFK_BWD_KQ1): the ProdLDA backward keeps the one-k-range shape with
+// fewer slabs than vocabulary tiles (n_dpart < n_tiles: each 16-wave workgroup walks
+// several tiles), K <= 64 -- batched launches, where M clients' one-workgroup-per-tile grid
+// would run in two rounds
+constexpr int GFK_BWD_KQ1 = 262144;
 __host__ __device__ inline bool gfk_postfold(const GfkModel& m) {
   return (m.stage_flags & GFK_FWD_POSTFOLD) && (m.stage_flags & 4) && (m.stage_flags & 256) &&
          m.K <= 64 && m.bmax <= 64 && !m.lab_on && m.kind == GFK_PRODLDA;

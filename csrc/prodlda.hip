@@ -1819,6 +1819,7 @@ extern "C" size_t gfk_prodlda_fwd_smem(const GfkModel* m) {
 // and the 8-wave dense pass cost more than the quartered MFMA work saved, 0.0652 vs 0.0615
 // ms per round.)
 __host__ __device__ inline int bwd_kq(const GfkModel& m) {
+  if ((m.stage_flags & GFK_BWD_KQ1) && m.K <= 64) return 1;      // persistent one-range tiles
   return (m.n_dpart < m.n_tiles && round_up(m.K, 16) / 16 >= 4) ? 4 : 1;
 }
 

@@ -69,6 +69,7 @@ STAGE_WIN_CTXPP = 16384           # bit 14: CombinedTM's contextual W_in half as
 STAGE_CTX_RS = 32768              # bit 15: CombinedTM forward, Wa register-streamed (csrc/ctx.hip)
 STAGE_FWD_POSTFOLD = 65536        # bit 16: the strip forward computes post_fwd (csrc/prodlda.hip FP)
 STAGE_POST_EXTRA_ROWBWD = 131072  # bit 17: post_bwd's batch-level workgroup runs in row_bwd
+STAGE_BWD_KQ1 = 262144            # bit 18: one-k-range backward walking several tiles (K <= 64)
 
 
 def _explain(ok: bool, why: str, explain: bool) -> bool:
@@ -1536,6 +1537,17 @@ class BatchedSteps:
             if (M > 1 and M * (mm.bmax + 1) > self._cu
                     and os.environ.get("GFEDNTM_BATCH_POST", "1") != "0"):
                 mm.stage_flags |= 2 | STAGE_POST_EXTRA_ROWBWD
+            # prodlda_bwd at K <= 64: one 16-wave workgroup per tile (~61 KB of LDS, two per
+            # CU) -- M clients' tiles beyond two per CU ran in a second round (592 on 512
+            # slots at M = 8, V = 4.7k); instead each workgroup walks t tiles (n_dpart =
+            # n_tiles / t slabs, the persistent one-range shape), t the smallest that fits
+            # one round (GFEDNTM_BATCH_BWD=0: off)
+            if (M > 1 and mm.kind == abi.KIND_PRODLDA and mm.K <= 64 and mm.n_dpart == mm.n_tiles
+                    and M * mm.n_tiles > 2 * self._cu
+                    and os.environ.get("GFEDNTM_BATCH_BWD", "1") != "0"):
+                t = -(-(M * mm.n_tiles) // (2 * self._cu))
+                mm.n_dpart = -(-mm.n_tiles // t)
+                mm.stage_flags |= STAGE_BWD_KQ1
             # win_update: all clients' W_in tiles in one launch -> the 8-wave tile shape once
             # they exceed two rounds of 16-wave workgroups (GFEDNTM_BATCH_WIN8=0: off)
             if (M * (mm.n_tiles + 8) > 2 * self._cu
