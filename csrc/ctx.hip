@@ -119,7 +119,7 @@ __global__ void __launch_bounds__(FT) gfk_ctx_fwd_k(GfkArgT<GB> ga) {
   const GfkModel& m = gfk_model(ga);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int RB = BM / 16, SU = 5;
-  const int x = blockIdx.x, jx = x >> 3, rb = jx % RB, tile = (jx / RB) * 8 + (x & 7);
+  const int x = gfk_bx(), jx = x >> 3, rb = jx % RB, tile = (jx / RB) * 8 + (x & 7);
   if (tile >= m.n_tiles) return;
   GFK_STAMP(m, 30);
   const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
@@ -246,7 +246,7 @@ __global__ void __launch_bounds__(FT) gfk_ctx_fwd_full_k(GfkArgT<GB> ga) {
   const GfkModel& m = gfk_model(ga);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int BMF = 64, SU = (BMF + 64) * FK / 4 / FT;     // float4 per thread per chunk: 8
-  const int tile = blockIdx.x;
+  const int tile = gfk_bx();
   if (tile >= m.n_tiles) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
   const int r = lane & 15, g = lane >> 4;
@@ -393,7 +393,7 @@ __global__ void __launch_bounds__(FT, 4) gfk_ctx_fwd_bal_k(GfkArgT<GB> ga) {
   const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
   const int r = lane & 15, g = lane >> 4;
   const int V = m.V, C = m.C, H0 = m.H[0];
-  const int G = (int)gridDim.x, w = (int)blockIdx.x;
+  const int G = (int)gridDim.x, w = (int)gfk_bx();
   const int U = (V + 15) / 16;
   const int cs = (int)((int64_t)w * U / G) * 16;
   const int ce = min(V, (int)((int64_t)(w + 1) * U / G) * 16);
@@ -559,7 +559,7 @@ __global__ void __launch_bounds__(FT3) gfk_ctx_fwd_bal3_k(GfkArgT<GB> ga) {
   const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
   const int r = lane & 15, g = lane >> 4;
   const int V = m.V, C = m.C, H0 = m.H[0];
-  const int G = (int)gridDim.x, w = (int)blockIdx.x;
+  const int G = (int)gridDim.x, w = (int)gfk_bx();
   const int U = (V + 15) / 16;
   const int cs = (int)((int64_t)w * U / G) * 16;
   const int ce = min(V, (int)((int64_t)(w + 1) * U / G) * 16);
@@ -779,7 +779,7 @@ __global__ void __launch_bounds__(RS_T) gfk_ctx_fwd_rs_k(GfkArgT<GB> ga) {
   const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
   const int r = lane & 15, g = lane >> 4;
   const int V = m.V, C = m.C, H0 = m.H[0], bmax = m.bmax;
-  const int G = (int)gridDim.x, w = (int)blockIdx.x;
+  const int G = (int)gridDim.x, w = (int)gfk_bx();
   const int U = (V + 15) / 16;
   const int u0 = (int)((int64_t)w * U / G), nu = (int)((int64_t)(w + 1) * U / G) - u0;
   const int NPH = (C + RS_KP - 1) / RS_KP;
@@ -1040,7 +1040,7 @@ __global__ void __launch_bounds__(CT) gfk_ctx_bwd_k(GfkArgT<GB> ga) {
   __shared__ int docs_s[BM];
   GFK_STAMP(m, 34);
   const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
-  const int n_tiles = m.n_tiles, tile = blockIdx.x % n_tiles, kc = blockIdx.x / n_tiles;
+  const int n_tiles = m.n_tiles, tile = gfk_bx() % n_tiles, kc = gfk_bx() / n_tiles;
   const int V = m.V, C = m.C, H0 = m.H[0], ckb = m.ctx_ckb;
   if (tid < BM) docs_s[tid] = m.ws_doc[tid];
   const int c0 = tile * 64, nvv = min(64, V - c0), k0 = kc * ckb, kn = min(ckb, C - k0);
@@ -1232,7 +1232,7 @@ __global__ void __launch_bounds__(CT) gfk_ctx_bwd_pp_k(GfkArgT<GB> ga) {
   const int V = m.V, C = m.C, H0 = m.H[0], n_tiles = m.n_tiles;
   const int NCK = (C + PK - 1) / PK;
   const int64_t N = (int64_t)n_tiles * NCK;
-  const int G = (int)gridDim.x, w = (int)blockIdx.x;
+  const int G = (int)gridDim.x, w = (int)gfk_bx();
   const int i0 = (int)(N * w / G), i1 = (int)(N * (w + 1) / G);
   const int H0Q = rup(H0, 4);
   const PPLds L = pp_lds(m);

@@ -184,7 +184,7 @@ template <bool Staged, bool GB = false>
 __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkArgT<GB> ga) {
   const GfkModel& m = gfk_model(ga);
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int b = blockIdx.x, tid = threadIdx.x;
+  const int b = gfk_bx(), tid = threadIdx.x;
   const int lane = tid & 63, wave = uniform(tid >> 6);
   int H0 = m.H[0], K = m.K, bmax = m.bmax, nh = m.n_hidden, input = m.input, sflags = m.stage_flags;
   const int32_t *nxt = m.ws_next, *indices = m.indices, *stepp = m.step;

@@ -202,6 +202,17 @@ constexpr int GFK_POST_EXTRA_ROWBWD = 131072;
 // several tiles), K <= 64 -- batched launches, where M clients' one-workgroup-per-tile grid
 // would run in two rounds
 constexpr int GFK_BWD_KQ1 = 262144;
+// stage_flags bit 19 (GFK_LB): the large-batch plan, 128 < bmax <= GFK_BMAX_LIMIT.  The
+// ProdLDA decoder's three products (logits = theta_d beta, dbeta = theta_d^T dlogit,
+// d theta_d = dlogit beta^T) are library GEMMs issued by the engine on the step's stream
+// between prodlda_lb_colbn (column batch-norm, BN'ed tiles, row sum-exp partials) and
+// prodlda_lb_dlogit (the logit gradient as a plain [bmax][ldb] matrix in ws_dt); the
+// row-parallel encoder / posterior kernels run as usual with their batch matrices read
+// from L2 (bit 1), the weight-gradient jobs stage the batch in row chunks, NeuralLDA's
+// beta backward builds its x^T tile per 128-row chunk; gradient mode + the generic
+// optimizer kernel
+constexpr int GFK_LB = 524288;
+constexpr int GFK_BMAX_LIMIT = 512;
 __host__ __device__ inline bool gfk_postfold(const GfkModel& m) {
   return (m.stage_flags & GFK_FWD_POSTFOLD) && (m.stage_flags & 4) && (m.stage_flags & 256) &&
          m.K <= 64 && m.bmax <= 64 && !m.lab_on && m.kind == GFK_PRODLDA;
@@ -279,13 +290,44 @@ __host__ inline const GfkModel* gfk_dev(const GfkModel* m) {
 template <bool B> struct GfkArgT;
 template <> struct GfkArgT<false> { GfkModel m; };
 template <> struct GfkArgT<true> { const GfkModel* p; };
+// Workgroup -> (client, index) of a launch.  One client (gridDim.z = 1): (0, blockIdx.x).
+// Batched (gridDim.z = M clients of gridDim.x workgroups each): the dispatcher deals
+// workgroups round-robin over the 8 XCDs in linear order L = x + gx z (observed placement,
+// MI355X_MICROARCH.md "Workgroup dispatch"; speed only, never correctness), so the
+// bijection L -> (client L % M, index L / M) puts ALL of a client's workgroups on the XCD(s)
+// L % 8 = client (mod 8) -- at M = 8 one client per XCD: each kernel of the round finds the
+// client's previous outputs (heads, theta_d, logit tiles, ...) and parameters in its own
+// XCD's L2 instead of another die's.  Indices b and b + 8 of a client still share an XCD
+// (their L differ by 8 M), which the pipelined backward's tile grouping relies on.
+// (-DGFK_NO_XCD_MAP: the plain (blockIdx.z, blockIdx.x), for A/B builds.)
+// (power-of-two client counts only -- shifts and masks on scalar registers; a division here
+// would run on the VALU and cost the 64-VGPR kernels spills -- other counts keep the plain
+// placement)
+__device__ __forceinline__ int gfk_bz() {
+#ifdef GFK_NO_XCD_MAP
+  return (int)blockIdx.z;
+#else
+  const unsigned M = gridDim.z;
+  if (M & (M - 1)) return (int)blockIdx.z;
+  return (int)((blockIdx.x + gridDim.x * blockIdx.z) & (M - 1));
+#endif
+}
+__device__ __forceinline__ int gfk_bx() {
+#ifdef GFK_NO_XCD_MAP
+  return (int)blockIdx.x;
+#else
+  const unsigned M = gridDim.z;
+  if (M & (M - 1)) return (int)blockIdx.x;
+  return (int)((blockIdx.x + gridDim.x * blockIdx.z) >> __builtin_ctz(M));
+#endif
+}
 __device__ __forceinline__ const GfkModel& gfk_model(const GfkArgT<false>& a) { return a.m; }
-__device__ __forceinline__ const GfkModel& gfk_model(const GfkArgT<true>& a) { return a.p[blockIdx.z]; }
+__device__ __forceinline__ const GfkModel& gfk_model(const GfkArgT<true>& a) { return a.p[gfk_bz()]; }
 template <bool B> struct GfkUArgT;
 template <> struct GfkUArgT<false> { GfkUpdate u; };
 template <> struct GfkUArgT<true> { const GfkUpdate* p; };
 __device__ __forceinline__ const GfkUpdate& gfk_upd(const GfkUArgT<false>& a) { return a.u; }
-__device__ __forceinline__ const GfkUpdate& gfk_upd(const GfkUArgT<true>& a) { return a.p[blockIdx.z]; }
+__device__ __forceinline__ const GfkUpdate& gfk_upd(const GfkUArgT<true>& a) { return a.p[gfk_bz()]; }
 
 // ---------------------------------------------------------------------------
 // Device helpers
@@ -301,7 +343,7 @@ namespace gfk {
 #define GFK_STAMP(m, slot)                                                        \
   do {                                                                            \
     __builtin_amdgcn_sched_barrier(0);                                            \
-    if (blockIdx.x == 0 && threadIdx.x == 0 && (m).dbg)                           \
+    if (gfk_bx() == 0 && threadIdx.x == 0 && (m).dbg)                           \
       (m).dbg[slot] = __builtin_amdgcn_s_memtime();                               \
     __builtin_amdgcn_sched_barrier(0);                                            \
   } while (0)
@@ -682,7 +724,7 @@ __device__ __forceinline__ void mfma_gemm(int M, int N, int R, const MatView& A,
 // dependent reads (step -> plan -> doc -> indptr) that runs in an extra
 // workgroup of win_update, off the critical path, so the next enc_in starts one
 // round trip from its data.  Rows past the batch repeat its first doc.
-// pnb_e: 2 * 128 ints of LDS, the (e0, e1) of the next batch's rows (bmax <= 128) -- the
+// pnb_e: 2 * bmax ints of LDS, the (e0, e1) of the next batch's rows -- the
 // caller's dynamic LDS where it has some, so the win_update kernels carry no static LDS on
 // top of their dynamic budget (40 KB + 1 KB would cost the sparse tile its 4th workgroup
 // per CU)
@@ -752,7 +794,7 @@ __device__ __forceinline__ void prepare_next_batch(const GfkModel& m, int* pnb_e
 }
 
 __device__ __forceinline__ void prepare_next_batch(const GfkModel& m) {
-  __shared__ int pnb_e[2 * 128];
+  __shared__ int pnb_e[2 * GFK_BMAX_LIMIT];
   prepare_next_batch(m, pnb_e);
 }
 

@@ -39,10 +39,10 @@ __global__ void __launch_bounds__(LBT) gfk_lda_beta_fwd(GfkArgT<GB> ga) {
   float* rowm = bn + K * LD;
   float* rows = rowm + K;
   for (int k = tid; k < K; k += LBT) { rowm[k] = -INFINITY; rows[k] = 0.f; }
-  if (blockIdx.x == 0 && tid == 0) *m.nbt_beta += 1;
+  if (gfk_bx() == 0 && tid == 0) *m.nbt_beta += 1;
   constexpr int BU = (256 * VB + LBT - 1) / LBT;      // K <= 256
   const int c = tid >> 4, sub = tid & 15;             // BN: 16 lanes per column
-  for (int tile = blockIdx.x; tile < m.n_tiles; tile += gridDim.x) {
+  for (int tile = gfk_bx(); tile < m.n_tiles; tile += gridDim.x) {
     const int c0 = tile * VB, nv = min(VB, V - c0);
     const bool valid = c < nv;
     __syncthreads();
@@ -108,7 +108,7 @@ __global__ void __launch_bounds__(LBT) gfk_lda_beta_fwd(GfkArgT<GB> ga) {
   }
   __syncthreads();
   for (int k = tid; k < K; k += LBT) {
-    float* p = m.ws_row_part + ((size_t)blockIdx.x * K + k) * 2;
+    float* p = m.ws_row_part + ((size_t)gfk_bx() * K + k) * 2;
     p[0] = rowm[k];
     p[1] = rows[k];
   }
@@ -127,7 +127,7 @@ template <int KQ, bool GB = false>
 __global__ void __launch_bounds__(LDA_ROW_THREADS) gfk_lda_row_k(GfkArgT<GB> ga) {
   const GfkModel& m = gfk_model(ga);
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int b = blockIdx.x, nb = *m.ws_nb;
+  const int b = gfk_bx(), nb = *m.ws_nb;
   if (b >= nb) return;
   const int K = m.K, tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
   // matmul_dtype = "bf16": theta_d and beta_sm are bf16 operands of word_dist = theta_d
@@ -212,6 +212,7 @@ __global__ void __launch_bounds__(LDA_ROW_THREADS) gfk_lda_row_k(GfkArgT<GB> ga)
 // dynamic LDS: bn[K*LD] + d[K*LD] + xt[64*XS] (+ thd[B*kt + 64]) + ck[pad4(K)] (+ dth[B*K])
 // x^T tile stride: 2 x odd, so the A-role MFMA reads (16 rows x 2 k per half-wave)
 // hit 32 distinct ds_read_b32 banks
+constexpr int LDA_XB = 128;            // rows of the x^T tile (larger batches: chunks)
 __host__ __device__ inline int lda_xs(int B) {
   int s = (B + 1) & ~1;
   if ((s / 2) % 2 == 0) s += 2;
@@ -225,12 +226,16 @@ __host__ __device__ inline int lda_xs(int B) {
 // outputs this thread updates (fused mode).  Second round: the tile's per-non-zero
 // coefficients (ws_dbsm).  Then c_k, the x^T theta_d MFMA, the BN backward over the
 // topics and the update, all out of LDS.
-template <bool ThLds, bool GB = false>
+// CH (the large-batch plan, bmax > 128): the x^T tile built and multiplied in row chunks
+template <bool ThLds, bool GB = false, bool CH = false>
 __global__ void __launch_bounds__(LBT) gfk_lda_beta_bwd_k(GfkArgT<GB> ga) {
   const GfkModel& m = gfk_model(ga);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int K = m.K, V = m.V, tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
-  const int B = m.bmax, kt = m.kt, XS = lda_xs(B), nb = *m.ws_nb;
+  // the x^T tile holds XB = min(bmax, 128) rows: larger batches take it in row chunks,
+  // the G accumulators carrying over (one chunk, and the same summation order, up to 128)
+  const int B = m.bmax, kt = m.kt, XB = B < LDA_XB ? B : LDA_XB, XS = lda_xs(XB), nb = *m.ws_nb;
+  const int nch = (B + XB - 1) / XB;
   float* bn = smem;
   float* d = bn + ((K * LD + 3) & ~3);
   float* xt = d + ((K * LD + 3) & ~3);      // 16-B aligned: thd / dtl are LDS-DMA destinations
@@ -250,20 +255,20 @@ __global__ void __launch_bounds__(LBT) gfk_lda_beta_bwd_k(GfkArgT<GB> ga) {
   const bool fused = m.update_mode == 1;
   constexpr int PU = 4;                               // prefetched updates per thread (K <= 64)
   const int n_upd = (K * VB + LBT - 1) / LBT;
-  for (int tile = blockIdx.x; tile < m.n_tiles; tile += gridDim.x) {
+  for (int tile = gfk_bx(); tile < m.n_tiles; tile += gridDim.x) {
     const int c0 = tile * VB, nv = min(VB, V - c0);
     __syncthreads();
     // ---- round 1 ----
     glds_copy(d, m.ws_zn + (size_t)c0 * K, nv * K, tid, LBT);
-    // 16 threads per batch row: rows tid/16 and, at bmax = 128, tid/16 + 64
+    // 16 threads per batch row: rows tid/16 and, at bmax >= 128, tid/16 + 64 (of the chunk)
     const int xrow = tid >> 4, xsub = tid & 15, xrow2 = xrow + LBT / 16;
     int es = 0, ee = 0, fs = 0, fe = 0;
-    if (xrow < nb && xrow < B) {
+    if (xrow < nb && xrow < XB) {
       const int32_t* ts = m.ws_tstart + (size_t)xrow * (m.n_tiles + 1) + tile;
       es = ts[0];
       ee = ts[1];
     }
-    if (xrow2 < nb && xrow2 < B) {
+    if (xrow2 < nb && xrow2 < XB) {
       const int32_t* ts = m.ws_tstart + (size_t)xrow2 * (m.n_tiles + 1) + tile;
       fs = ts[0];
       fe = ts[1];
@@ -286,7 +291,7 @@ __global__ void __launch_bounds__(LBT) gfk_lda_beta_bwd_k(GfkArgT<GB> ga) {
     for (int e = es + xsub; e < ee; e += 16) xt[(m.indices[e] - c0) * XS + xrow] = m.ws_dbsm[e];
     for (int e = fs + xsub; e < fe; e += 16) xt[(m.indices[e] - c0) * XS + xrow2] = m.ws_dbsm[e];
     // c_k = sum_b theta_d[b, k] d theta_d[b, k] (softmax-over-V backward), 16 lanes per topic
-    if (tile == (int)blockIdx.x) {
+    if (tile == (int)gfk_bx()) {
       for (int k0 = 0; k0 < K; k0 += LBT / 16) {
         const int k = k0 + (tid >> 4), sub = tid & 15;
         float s = 0.f;
@@ -315,6 +320,7 @@ __global__ void __launch_bounds__(LBT) gfk_lda_beta_bwd_k(GfkArgT<GB> ga) {
       }
     }
     lds_barrier();
+    if constexpr (!CH) {
     // G[c][k] = sum_b xt[c][b] theta_d[b][k]; then d <- beta_sm * (G - c_k)
     for (int t = wave; t < 4 * NT; t += LBW) {
       const int i0 = (t / NT) * 16, j0 = (t % NT) * 16;
@@ -334,6 +340,62 @@ __global__ void __launch_bounds__(LBT) gfk_lda_beta_bwd_k(GfkArgT<GB> ga) {
           d[k * LD + c] = d[k * LD + c] * (acc[r] - ck);
         }
       }
+    }
+    } else {
+    // G[c][k] = sum_b xt[c][b] theta_d[b][k] (x^T chunk by chunk); then d <- beta_sm (G - c_k)
+    constexpr int TW = (4 * 16 + LBW - 1) / LBW;       // subtiles per wave (K <= 256)
+    f32x4 acc[TW];
+#pragma unroll
+    for (int u = 0; u < TW; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int ch = 0; ch < nch; ++ch) {
+      const int b0 = ch * XB, cb = min(XB, B - b0);
+      if (ch > 0) {                     // the next chunk's coefficients into the x^T tile
+        lds_barrier();                  // (the previous chunk's MFMA reads are done)
+        for (int i = tid; i < VB * XS; i += LBT) xt[i] = 0.f;
+        int s0 = 0, s1 = 0, t0 = 0, t1 = 0;
+        if (b0 + xrow < nb && xrow < cb) {
+          const int32_t* ts = m.ws_tstart + (size_t)(b0 + xrow) * (m.n_tiles + 1) + tile;
+          s0 = ts[0];
+          s1 = ts[1];
+        }
+        if (b0 + xrow2 < nb && xrow2 < cb) {
+          const int32_t* ts = m.ws_tstart + (size_t)(b0 + xrow2) * (m.n_tiles + 1) + tile;
+          t0 = ts[0];
+          t1 = ts[1];
+        }
+        lds_barrier();
+        for (int e = s0 + xsub; e < s1; e += 16) xt[(m.indices[e] - c0) * XS + xrow] = m.ws_dbsm[e];
+        for (int e = t0 + xsub; e < t1; e += 16) xt[(m.indices[e] - c0) * XS + xrow2] = m.ws_dbsm[e];
+        lds_barrier();
+      }
+#pragma unroll
+      for (int u = 0; u < TW; ++u) {
+        const int t = wave + LBW * u;
+        if (t >= 4 * NT) break;
+        const int i0 = (t / NT) * 16, j0 = (t % NT) * 16;
+        const float* ap = xt + (i0 + (lane & 15)) * XS + (lane >> 4);
+        const float* bp = thv + (size_t)(b0 + (lane >> 4)) * kt + j0 + (lane & 15);
+        if (m.mm_bf16)      // bf16 operands (the coefficients and theta_d), fp32 accumulation
+          for (int kb = 0; kb < cb; kb += 4) acc[u] = mfma16x16x4(bf16_round(ap[kb]), bf16_round(bp[kb * kt]), acc[u]);
+        else
+          for (int kb = 0; kb < cb; kb += 4) acc[u] = mfma16x16x4(ap[kb], bp[kb * kt], acc[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < TW; ++u) {
+      const int t = wave + LBW * u;
+      if (t >= 4 * NT) break;
+      const int i0 = (t / NT) * 16, j0 = (t % NT) * 16;
+      const int k = j0 + (lane & 15);
+      if (k < K) {
+        const float ck = ckl[k];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = i0 + (lane >> 4) * 4 + r;
+          d[k * LD + c] = d[k * LD + c] * (acc[u][r] - ck);
+        }
+      }
+    }
     }
     lds_barrier();
     {  // BN backward over the K topics of each column: 16 lanes per column
@@ -388,12 +450,15 @@ extern "C" size_t gfk_lda_row_smem(int K) {
   return sizeof(float) * ((size_t)K * LDA_ROW_WAVES + LDA_ROW_WAVES);
 }
 static size_t lda_bwd_floats(const GfkModel* m, bool th_lds) {
-  size_t n = ((((size_t)m->K * LD) + 3) & ~(size_t)3) * 2 + (size_t)VB * lda_xs(m->bmax) +
+  const int xb = m->bmax < LDA_XB ? m->bmax : LDA_XB;
+  size_t n = ((((size_t)m->K * LD) + 3) & ~(size_t)3) * 2 + (size_t)VB * lda_xs(xb) +
              (((size_t)m->K + 3) & ~(size_t)3);
   if (th_lds) n += (size_t)m->bmax * m->kt + 64 + (((size_t)m->bmax * m->K + 3) & ~(size_t)3);
   return n + (((size_t)m->K + 3) & ~(size_t)3);     // per-topic log-sum-exp
 }
-static bool lda_bwd_th_lds(const GfkModel* m) { return sizeof(float) * lda_bwd_floats(m, true) <= 160 * 1024; }
+static bool lda_bwd_th_lds(const GfkModel* m) {
+  return m->bmax <= LDA_XB && sizeof(float) * lda_bwd_floats(m, true) <= 160 * 1024;
+}
 extern "C" size_t gfk_lda_bwd_smem(const GfkModel* m) {
   return sizeof(float) * lda_bwd_floats(m, lda_bwd_th_lds(m));
 }
@@ -416,7 +481,9 @@ extern "C" int gfk_launch_lda_row(const GfkModel* m, hipStream_t s) {
 
 extern "C" int gfk_launch_lda_beta_bwd(const GfkModel* m, hipStream_t s) {
   const dim3 g(m->dec_grid), t(LBT);
-  if (lda_bwd_th_lds(m))
+  if (m->bmax > LDA_XB)
+    do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_lda_beta_bwd_k<false, true, true>), gfk_grid(g, m), t, gfk_lda_bwd_smem(m), s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_lda_beta_bwd_k<false, false, true>), g, t, gfk_lda_bwd_smem(m), s, GfkArgT<false>{*m}); } while (0);
+  else if (lda_bwd_th_lds(m))
     do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_lda_beta_bwd_k<true, true>), gfk_grid(g, m), t, gfk_lda_bwd_smem(m), s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_lda_beta_bwd_k<true, false>), g, t, gfk_lda_bwd_smem(m), s, GfkArgT<false>{*m}); } while (0);
   else
     do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_lda_beta_bwd_k<false, true>), gfk_grid(g, m), t, gfk_lda_bwd_smem(m), s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_lda_beta_bwd_k<false, false>), g, t, gfk_lda_bwd_smem(m), s, GfkArgT<false>{*m}); } while (0);
@@ -430,7 +497,8 @@ extern "C" int gfk_lda_set_smem(size_t bytes) {
   if (bytes <= cur) return 0;
   cur = bytes;
   const void* ks[] = {(const void*)gfk_lda_beta_fwd<false>, (const void*)gfk_lda_beta_fwd<true>, (const void*)gfk_lda_beta_bwd_k<true>, (const void*)gfk_lda_beta_bwd_k<true, true>,
-                      (const void*)gfk_lda_beta_bwd_k<false>, (const void*)gfk_lda_beta_bwd_k<false, true>};
+                      (const void*)gfk_lda_beta_bwd_k<false>, (const void*)gfk_lda_beta_bwd_k<false, true>,
+                      (const void*)gfk_lda_beta_bwd_k<false, false, true>, (const void*)gfk_lda_beta_bwd_k<false, true, true>};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return (int)e;

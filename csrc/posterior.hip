@@ -262,7 +262,7 @@ __device__ __forceinline__ void post_label_head(const GfkModel& m, float* buf, i
   }
 }
 
-// grid: bmax workgroups (row = blockIdx.x).  dynamic LDS: mr[B*K] + lr[B*K] (unless
+// grid: bmax workgroups (row = gfk_bx()).  dynamic LDS: mr[B*K] + lr[B*K] (unless
 // read from L2) + mean[2K] + rstd[2K]
 // InLds: the batch matrices are staged in LDS (compile-time, so every access is a
 // ds_read; a runtime select of the pointer would turn them into flat loads).
@@ -275,7 +275,7 @@ __global__ void __launch_bounds__(FT) gfk_post_fwd_k(GfkArgT<GB> ga) {
   const int32_t* nbp = m.ws_nb;
   keep(K, B, mu_raw, ls_raw, nbp);
   const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
-  const int row = blockIdx.x;
+  const int row = gfk_bx();
   constexpr bool in_lds = InLds;
   const float* mr = in_lds ? smem : mu_raw;
   const float* lr = in_lds ? smem + B * K : ls_raw;
@@ -360,7 +360,8 @@ __global__ void __launch_bounds__(FT) gfk_post_fwd_k(GfkArgT<GB> ga) {
     else post_colstats_dpp<8>(m, mr, lr, cmean, crstd, rmp, rvp, nb, inv_nb, row, tid);
   } else {
     if (B <= 64) post_colstats<32>(m, mr, lr, cmean, crstd, red, rm0, rv0, nb, inv_nb, row, tid);
-    else post_colstats<64>(m, mr, lr, cmean, crstd, red, rm0, rv0, nb, inv_nb, row, tid);
+    else if (B <= 128) post_colstats<64>(m, mr, lr, cmean, crstd, red, rm0, rv0, nb, inv_nb, row, tid);
+    else post_colstats<GFK_BMAX_LIMIT / 2>(m, mr, lr, cmean, crstd, red, rm0, rv0, nb, inv_nb, row, tid);
   }
   if (row == 0 && tid == 0) {
     *m.nbt_mu = nbt0 + 1;
@@ -489,7 +490,7 @@ __global__ void __launch_bounds__(PT) gfk_row_bwd_k(GfkArgT<GB> ga) {
   const int32_t* nbp = m.ws_nb;
   keep(K, B, np, dpart, nbp);
   const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
-  const int row = blockIdx.x;
+  const int row = gfk_bx();
   const int nb = *nbp;
   if ((m.stage_flags & GFK_POST_EXTRA_ROWBWD) && row == B) {
     post_batch_level(m, nb, part, tid);    // the batch-level workgroup (grid = bmax + 1)
@@ -707,7 +708,7 @@ __device__ __forceinline__ void post_prior_sums(int K, int nb, const float* mu, 
   }
 }
 
-// grid: bmax + 1 workgroups: row = blockIdx.x < bmax, plus one extra workgroup
+// grid: bmax + 1 workgroups: row = gfk_bx() < bmax, plus one extra workgroup
 // (the last) for the batch-level work -- prior gradients, the loss, the step
 // counter -- so no row workgroup carries it on the critical path.
 template <bool InLds, bool Staged, bool GB = false>
@@ -719,7 +720,7 @@ __global__ void __launch_bounds__(FT) gfk_post_bwd_k(GfkArgT<GB> ga) {
   const int32_t* nbp = m.ws_nb;
   keep(K, B, nh, sflags, dmu_g, dls_g, mu_g, ls_g, nbp);
   const int tid = threadIdx.x, lane = tid & 63;
-  const int row = blockIdx.x;
+  const int row = gfk_bx();
   const bool extra = !(sflags & GFK_POST_EXTRA_ROWBWD) && row == (int)gridDim.x - 1;
   const PostLds L = post_lds(m);
   const int Hl = m.H[nh - 1];
@@ -810,7 +811,8 @@ __global__ void __launch_bounds__(FT) gfk_post_bwd_k(GfkArgT<GB> ga) {
       }
     } else {                            // L2: lane-per-column (coalesced)
       if (B <= 64) post_prior_sums<32>(K, nb, mu, ls, pmean, S + 2 * P2, S + 3 * P2, smem + L.red2, tid);
-      else post_prior_sums<64>(K, nb, mu, ls, pmean, S + 2 * P2, S + 3 * P2, smem + L.red2, tid);
+      else if (B <= 128) post_prior_sums<64>(K, nb, mu, ls, pmean, S + 2 * P2, S + 3 * P2, smem + L.red2, tid);
+      else post_prior_sums<GFK_BMAX_LIMIT / 2>(K, nb, mu, ls, pmean, S + 2 * P2, S + 3 * P2, smem + L.red2, tid);
     }
     lds_barrier();
     const float wk = m.kl_weight;
@@ -852,7 +854,8 @@ __global__ void __launch_bounds__(FT) gfk_post_bwd_k(GfkArgT<GB> ga) {
     }
   } else {                              // L2: lane-per-column (coalesced)
     if (B <= 64) post_bn_sums<32>(K, nb, dmu, dls, mu, ls, S, S + P2, smem + L.red2, tid);
-    else post_bn_sums<64>(K, nb, dmu, dls, mu, ls, S, S + P2, smem + L.red2, tid);
+    else if (B <= 128) post_bn_sums<64>(K, nb, dmu, dls, mu, ls, S, S + P2, smem + L.red2, tid);
+    else post_bn_sums<GFK_BMAX_LIMIT / 2>(K, nb, dmu, dls, mu, ls, S, S + P2, smem + L.red2, tid);
   }
   lds_barrier();
   GFK_STAMP(m, 12);

@@ -112,7 +112,7 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkArgT<GB> ga
   GFK_STAMP(m, 16);
   glds_copy(th, m.ws_thetad, BM * KT, tid, DEC_THREADS);
   const int nb = *m.ws_nb;
-  if (blockIdx.x == 0 && tid == 0) *m.nbt_beta += 1;
+  if (gfk_bx() == 0 && tid == 0) *m.nbt_beta += 1;
   // a tile's beta block [0, KP) x [c0, c0 + VB) and running statistics, into registers
   float br[BU], rmr = 0.f, rvr = 0.f;
   // element tid + DEC_THREADS u of a beta block is (row tid / VB + 16 u, column tid % VB)
@@ -128,15 +128,15 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkArgT<GB> ga
     rmr = m.beta_rm[v];
     rvr = m.beta_rv[v];
   };
-  if ((int)blockIdx.x < m.n_tiles) issue_tile(blockIdx.x);
+  if ((int)gfk_bx() < m.n_tiles) issue_tile(gfk_bx());
 #pragma unroll 1
-  for (int tile = blockIdx.x; tile < m.n_tiles; tile += gridDim.x) {
+  for (int tile = gfk_bx(); tile < m.n_tiles; tile += gridDim.x) {
   const int c0 = tile * VB;
   const int v = c0 + col;
   const bool valid = v < V;
   GFK_STAMP(m, 21);
   // ---- staging: the registers of this tile -> LDS ----
-  if (tile != (int)blockIdx.x) lds_barrier();      // previous tile's bt / colp reads done
+  if (tile != (int)gfk_bx()) lds_barrier();      // previous tile's bt / colp reads done
   {
     const int c = tid & (VB - 1), cok = c0 + c < V;
 #pragma unroll
@@ -146,7 +146,7 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkArgT<GB> ga
     }
   }
   const float rm0 = rmr, rv0 = rvr;
-  if (tile == (int)blockIdx.x) vm_barrier();       // + theta_d (LDS-DMA)
+  if (tile == (int)gfk_bx()) vm_barrier();       // + theta_d (LDS-DMA)
   else lds_barrier();
   GFK_STAMP(m, 17);
   asm volatile("" : "+v"(tid));
@@ -281,7 +281,7 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkArgT<GB> ga
   GFK_STAMP(m, 20);
   }
   // ---- this workgroup's per-row partials (one per wave column strip) ----
-  float* part = m.ws_row_part + (size_t)(blockIdx.x * 4 + cs) * m.bmax * 2;
+  float* part = m.ws_row_part + (size_t)(gfk_bx() * 4 + cs) * m.bmax * 2;
 #pragma unroll
   for (int i = 0; i < NRT; ++i) {
     if (rt0 + 4 * i >= RT) continue;
@@ -350,8 +350,8 @@ __host__ __device__ constexpr int strip_ring(int pf, int np) {
 #define STRIP_STAMP(j, rt)                                                                \
   do {                                                                                    \
     __builtin_amdgcn_sched_barrier(0);                                                    \
-    if ((blockIdx.x == 0 || blockIdx.x == gridDim.x - 1) && lane == 0 && m.dbg)           \
-      m.dbg[64 + (blockIdx.x ? 16 * 16 : 0) + wave * 16 + (j)] =                          \
+    if ((gfk_bx() == 0 || gfk_bx() == gridDim.x - 1) && lane == 0 && m.dbg)           \
+      m.dbg[64 + (gfk_bx() ? 16 * 16 : 0) + wave * 16 + (j)] =                          \
           (rt) ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime();         \
     __builtin_amdgcn_sched_barrier(0);                                                    \
   } while (0)
@@ -407,7 +407,7 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
     for (int e = 0; e < 4; ++e) rs_[i][e] = 0.f;
 
   const int nb = *m.ws_nb;
-  if (blockIdx.x == 0 && tid == 0) *m.nbt_beta += 1;
+  if (gfk_bx() == 0 && tid == 0) *m.nbt_beta += 1;
   const int g2 = 2 * (lane >> 4);
   const int gb = BF ? 8 * (lane >> 4) : g2;    // the lane group's first beta row
   // first beta row of pair t (relative to gb)
@@ -450,7 +450,7 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
   // 4 strips of a tile stay on one CU (their beta rows share cache lines), and the
   // tiles of the last, partial round are spread over every CU's wave group 0 instead
   // of all 8 waves of the first CUs, so no SIMD gets more than ceil(strips / SIMDs) + 1
-  int s = 4 * ((wave >> 2) * (int)gridDim.x + (int)blockIdx.x) + (wave & 3);
+  int s = 4 * ((wave >> 2) * (int)gridDim.x + (int)gfk_bx()) + (wave & 3);
   if constexpr (FP) {
     // ---- fused posterior: one round of loads (heads, the rows' noise / masks, priors,
     // workgroup 0's running statistics and counters), the first beta block behind them ----
@@ -498,7 +498,7 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
     lds_barrier();
     // ---- column batch-norm statistics of the 2K heads over the nb rows: 16 lanes per
     // column (rows g, g + 16, ..), 64 columns per pass ----
-    const bool w0 = blockIdx.x == 0;
+    const bool w0 = gfk_bx() == 0;
 #pragma unroll
     for (int p = 0; p < CPASS; ++p) {
       if (p * 64 >= 2 * K) break;
@@ -577,7 +577,7 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
       const float thd = tht * mk[i];
       th[r * KS + lane] = (live && lane < K) ? thd : 0.f;
       if (lane < KS - 64) th[r * KS + 64 + lane] = 0.f;
-      if (live && r % (int)gridDim.x == (int)blockIdx.x) {
+      if (live && r % (int)gridDim.x == (int)gfk_bx()) {
         if (lane < K) {
           m.ws_mu[r * K + lane] = mu;
           m.ws_ls[r * K + lane] = ls;
@@ -799,7 +799,7 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
 #pragma unroll
       for (int w = 0; w < NW; ++w) se += red[w * BM + row];
     if (row < nb) {
-      float* part = m.ws_row_part + ((size_t)(blockIdx.x * 4 + slot) * m.bmax + row) * 2;
+      float* part = m.ws_row_part + ((size_t)(gfk_bx() * 4 + slot) * m.bmax + row) * 2;
       part[0] = 0.f;
       part[1] = se;
     }
@@ -816,7 +816,7 @@ __global__ void __launch_bounds__(64) gfk_prodlda_row_loss(GfkArgT<GB> ga) {
   const int32_t *nbp = m.ws_nb, *erange = m.ws_erange;
   const float *row_part = m.ws_row_part, *zn = m.ws_zn;
   keep(n_tiles, bmax, nbp, erange, row_part, zn);
-  const int b = blockIdx.x, lane = threadIdx.x;
+  const int b = gfk_bx(), lane = threadIdx.x;
   // ---- round 1: batch size, the row's extent, LSE partials, its non-zeros (slots) ----
   const int nb = *nbp;
   const int np = m.dec_grid * 4;                 // per-workgroup partials of prodlda_fwd
@@ -886,6 +886,170 @@ __global__ void __launch_bounds__(64) gfk_prodlda_row_loss(GfkArgT<GB> ga) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Large batches (stage_flags GFK_LB, bmax 256 / 512; csrc/gfk_common.h).  The decoder's three
+// products are library GEMMs the engine issues on the step's stream (at B >= 256 they are
+// big enough for hipBLASLt to run them near the matrix cores' peak): logits = theta_d beta
+// into ws_dt as a plain [bmax][ldb] matrix, then dbeta = theta_d^T dlogit (beta's gradient
+// slot) and d theta_d = dlogit beta^T (slab 0) from the logit gradient these kernels leave
+// in ws_dt.  What is batch-coupled around them runs here:
+//   prodlda_lb_colbn  : column batch-norm of the logits over the batch (+ running statistics,
+//                       rstd), the BN'ed tile into ws_zn (row_loss's layout), per-row
+//                       sum-exp partials (the same ws_row_part layout as the forward kernels);
+//   prodlda_lb_dlogit : the logit gradient -- dense p S_b, the sparse -x p / (p + 1e-10) at
+//                       the row's non-zeros of the tile, the column BN backward -- over the
+//                       logits in ws_dt (rows >= nb and padding columns zero: the GEMMs read
+//                       the whole matrix).
+// Layout: thread (wave w, lane c) owns column c of a 64-column tile and rows w + 16 i, so
+// every global access of a wave is one 256-B row segment, a row's sparse entries are handled
+// by the one wave that owns the row (a wave-uniform loop: the owning lane adds the term --
+// no LDS tile, no barrier), and the column sums reduce over the 16 waves through LDS.
+// grid: dec_grid workgroups of 1024 threads, persistent over the tiles.
+// ---------------------------------------------------------------------------
+constexpr int LB_THREADS = 1024;
+
+template <int BM, bool GB = false>
+__global__ void __launch_bounds__(LB_THREADS) prodlda_lb_colbn_kernel(GfkArgT<GB> ga) {
+  const GfkModel& m = gfk_model(ga);
+  constexpr int NR = BM / 16;
+  __shared__ float red[2][16][VB];
+  const int tid = threadIdx.x, lane = tid & 63, w = uniform(tid >> 6);
+  const int V = m.V, ldb = m.ldb, nb = *m.ws_nb;
+  const float inv_nb = 1.f / (float)nb;
+  // the logits / zn through buffer descriptors: a row's offset is wave-uniform (the scalar
+  // offset), the column's the one vector offset -- no 64-bit address per row in registers
+  const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)m.ws_dt, 0, (int)((size_t)m.bmax * ldb * 4), 0x00020000);
+  if (gfk_bx() == 0 && tid == 0) *m.nbt_beta += 1;
+  float rs[NR];                       // this lane's sum of exp(z) per row over its tiles
+#pragma unroll
+  for (int i = 0; i < NR; ++i) rs[i] = 0.f;
+#pragma unroll 1
+  for (int tile = gfk_bx(); tile < m.n_tiles; tile += gridDim.x) {
+    const int v = tile * VB + lane, vc = min(v, V - 1);
+    const bool valid = v < V;
+    float rm0 = 0.f, rv0 = 0.f;
+    if (w == 0) { rm0 = m.beta_rm[vc]; rv0 = m.beta_rv[vc]; }
+    float x[NR], sm = 0.f;
+#pragma unroll
+    for (int i = 0; i < NR; ++i)
+      x[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rl, vc * 4, min(w + 16 * i, nb - 1) * ldb * 4, 0));
+#pragma unroll
+    for (int i = 0; i < NR; ++i) sm += w + 16 * i < nb ? x[i] : 0.f;
+    red[0][w][lane] = sm;
+    __syncthreads();
+    float mean = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) mean += red[0][j][lane];
+    mean *= inv_nb;
+    float q = 0.f;                    // two-pass variance, as torch's batch norm
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const float d = x[i] - mean;
+      q += w + 16 * i < nb ? d * d : 0.f;
+    }
+    red[1][w][lane] = q;
+    __syncthreads();
+    float var = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) var += red[1][j][lane];
+    var *= inv_nb;
+    const float rstd = rsqrtf(var + m.bn_eps);
+    if (w == 0 && valid) {
+      const float mom = m.bn_momentum;
+      const float unb = nb > 1 ? var * (float)nb / (float)(nb - 1) : var;
+      float nm = (1.f - mom) * rm0 + mom * mean, nv = (1.f - mom) * rv0 + mom * unb;
+      if (m.fed_scale_on && is_shared(m, m.beta_rm)) { nm *= m.fed_scale; nv *= m.fed_scale; }
+      m.beta_rm[v] = nm;
+      m.beta_rv[v] = nv;
+      m.ws_col_rstd[v] = rstd;
+    }
+    const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(m.ws_zn + (size_t)tile * BM * VB), 0, BM * VB * 4, 0x00020000);
+    const int zc = (lane ^ zswz(w)) * 4;     // (zswz(w + 16 i) == zswz(w))
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int r = w + 16 * i;
+      const float z = (x[i] - mean) * rstd;
+      if (r < nb) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(z), rz, zc, r * VB * 4, 0);
+      rs[i] += (valid && r < nb) ? __expf(z) : 0.f;
+    }
+    // (red[0] is rewritten next tile only after every wave passed the second barrier, which
+    // follows its reads; red[1]'s reads precede the next tile's first barrier)
+  }
+  float* part = m.ws_row_part + (size_t)gfk_bx() * 4 * m.bmax * 2;
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    const int r = w + 16 * i;
+    const float se = row16_sum(rs[i]);
+    if ((lane & 15) == 0 && r < nb) {
+      float* p = part + ((size_t)(lane >> 4) * m.bmax + r) * 2;
+      p[0] = 0.f;                     // (max, sum-exp) with max 0: |z| <= sqrt(nb - 1)
+      p[1] = se;
+    }
+  }
+}
+
+template <int BM, bool GB = false>
+__global__ void __launch_bounds__(LB_THREADS) prodlda_lb_dlogit_kernel(GfkArgT<GB> ga) {
+  const GfkModel& m = gfk_model(ga);
+  constexpr int NR = BM / 16;
+  __shared__ float red[2][16][VB];
+  const int tid = threadIdx.x, lane = tid & 63, w = uniform(tid >> 6);
+  const int V = m.V, ldb = m.ldb, nb = *m.ws_nb, ntp = m.n_tiles + 1;
+  const float inv_nb = 1.f / (float)nb;
+  const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)m.ws_dt, 0, (int)((size_t)m.bmax * ldb * 4), 0x00020000);
+  const int zc = (lane ^ zswz(w)) * 4;       // (zswz(w + 16 i) == zswz(w))
+#pragma unroll 1
+  for (int tile = gfk_bx(); tile < m.n_tiles; tile += gridDim.x) {
+    const int c0 = tile * VB, v = c0 + lane;
+    const bool valid = v < V;
+    const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(m.ws_zn + (size_t)tile * BM * VB), 0, BM * VB * 4, 0x00020000);
+    const float rsd = m.ws_col_rstd[min(v, V - 1)];
+    float z[NR], d[NR], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int r = w + 16 * i;
+      z[i] = d[i] = 0.f;
+      if (r < nb) {                   // (wave-uniform)
+        z[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rz, zc, r * VB * 4, 0));
+        const float p = __expf(z[i] - m.ws_lse[r]);
+        float dd = p * m.ws_s[r];
+        const int e0 = m.ws_tstart[(size_t)r * ntp + tile], e1 = m.ws_tstart[(size_t)r * ntp + tile + 1];
+        for (int e = e0; e < e1; ++e) {   // the row's non-zeros in this tile (few)
+          const float xv = m.values[e];
+          if (m.indices[e] - c0 == lane) dd += -xv * p / (p + RL_EPS);
+        }
+        d[i] = valid ? dd : 0.f;
+        s1 += d[i];
+        s2 += d[i] * z[i];
+      }
+    }
+    red[0][w][lane] = s1;
+    red[1][w][lane] = s2;
+    __syncthreads();
+    float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      a1 += red[0][j][lane];
+      a2 += red[1][j][lane];
+    }
+    a1 *= inv_nb;
+    a2 *= inv_nb;
+    const float rr = valid ? rsd : 0.f;
+    const int vo = v < ldb ? v * 4 : 0x7FFF0000;   // (columns past ldb: dropped stores)
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int r = w + 16 * i;
+      const float o = r < nb ? rr * (d[i] - a1 - z[i] * a2) : 0.f;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o), ro, vo, r * ldb * 4, 0);
+    }
+    __syncthreads();                  // every wave's red reads before the next tile's writes
+  }
+}
+
 // Backward.  Two launch shapes of one kernel:
 //  * KQ = 1 (every vocab tile has its own workgroup of 16 waves -- the K=50 headline --
 //    or K <= 48): workgroup g owns tiles g, g + grid, ...;
@@ -942,7 +1106,7 @@ __global__ void __launch_bounds__(256) prodlda_dlogit_kernel(GfkArgT<GB> ga) {
   __shared__ __attribute__((aligned(16))) float zt[BM * VB];
   __shared__ __attribute__((aligned(16))) float dt[BM * LDD];
   __shared__ __attribute__((aligned(16))) float ls[BM], Sb[BM], rs[VB];
-  const int tid = threadIdx.x, tile = blockIdx.x, c0 = tile * VB;
+  const int tid = threadIdx.x, tile = gfk_bx(), c0 = tile * VB;
   const int V = m.V, nb = *m.ws_nb;
   // ---- one staging round: z tile, lse, S (LDS-DMA), rstd, the rows' tile extents ----
   glds_copy(zt, m.ws_zn + (size_t)tile * BM * VB, BM * VB, tid, NT);
@@ -1047,7 +1211,7 @@ __device__ __forceinline__ void prodlda_bwd_body(const GfkModel& m) {
   int tid = threadIdx.x;
   int lane = tid & 63, wave = uniform(tid >> 6);
   const int ksub = round_up(K, 16) / 16;
-  const int q = (int)blockIdx.x % KQ, slab = (int)blockIdx.x / KQ, nslab = (int)gridDim.x / KQ;
+  const int q = (int)gfk_bx() % KQ, slab = (int)gfk_bx() / KQ, nslab = (int)gridDim.x / KQ;
   const int ks0 = q * ksub / KQ, nks = (q + 1) * ksub / KQ - ks0;   // this workgroup's k tiles
   const int kb = 16 * ks0;                                      // first topic of the range
   const int KPQ = bwd_kpq(K, KQ), KTQ = PRE ? 64 : KQ == 1 ? m.kt : kt_stride(KPQ);
@@ -1551,12 +1715,12 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
   const int G = (int)gridDim.x, nslab = G / KQ;
   int q, slab;
   if ((G & 31) == 0) {             // XCD-aware: blockIdx b runs on XCD b % 8
-    const int b = (int)blockIdx.x, j = b >> 3;
+    const int b = (int)gfk_bx(), j = b >> 3;
     q = j & 3;
     slab = ((j >> 2) << 3) | (b & 7);
   } else {
-    q = (int)blockIdx.x % KQ;
-    slab = (int)blockIdx.x / KQ;
+    q = (int)gfk_bx() % KQ;
+    slab = (int)gfk_bx() / KQ;
   }
   const int ks0 = q * ksub / KQ, nks = (q + 1) * ksub / KQ - ks0;
   const int kb = 16 * ks0;
@@ -1620,7 +1784,7 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
   // tiles (ws_dt holds [n_tiles][B][66] + 64 (grid + 32) floats; the dense layout uses
   // [n_tiles][B][64]), which nothing reads.  One slot per workgroup: a sink shared by all
   // of them would put every workgroup's stores on the same cache lines
-  float* const sink = m.ws_dt + (size_t)n_tiles * BM * VB + 64 * (size_t)blockIdx.x + (tid & 63);
+  float* const sink = m.ws_dt + (size_t)n_tiles * BM * VB + 64 * (size_t)gfk_bx() + (tid & 63);
   // one 16 x 16 output subtile over the 64-long reduction: ar / bq point at this lane's
   // operand rows, g4 = 4 (lane >> 4); step 4 q + j takes reduction index 16 q + 4 g + j
   // (stored at column (16 q + g4) ^ bx in bq's row: the dtT swizzle)
@@ -1803,6 +1967,7 @@ __host__ __device__ inline int strip_np(int K) {
 __host__ __device__ inline int strip_np_bf(int K) { return K <= 64 ? 8 : K <= 128 ? 16 : 32; }
 
 extern "C" size_t gfk_prodlda_fwd_smem(const GfkModel* m) {
+  if (m->stage_flags & GFK_LB) return 0;           // (static LDS only)
   if (m->stage_flags & FWD_STRIP) {
     const int np = m->mm_bf16 ? strip_np_bf(m->K) : strip_np(m->K);
     // (+ the fused posterior's raw heads [2][B][64] and column statistics [2][128])
@@ -1833,9 +1998,27 @@ static size_t bwd_smem(const GfkModel* m, int kq) {
 }
 
 // the LDS of the launch shape this model uses (the k-range split when it applies)
-extern "C" size_t gfk_prodlda_bwd_smem(const GfkModel* m) { return bwd_smem(m, bwd_kq(*m)); }
+extern "C" size_t gfk_prodlda_bwd_smem(const GfkModel* m) {
+  return (m->stage_flags & GFK_LB) ? 0 : bwd_smem(m, bwd_kq(*m));
+}
+
+// the large-batch kernels (stage_flags GFK_LB): bmax 256 or 512, ws_dt the [bmax][ldb] matrix
+#define GFK_LB_LAUNCH(KERN, BM)                                                                      do { if (m->n_batch > 1) hipLaunchKernelGGL((KERN<BM, true>), gfk_grid(dim3(m->dec_grid), m), dim3(LB_THREADS), 0, s, GfkArgT<true>{gfk_dev(m)});        else hipLaunchKernelGGL((KERN<BM, false>), dim3(m->dec_grid), dim3(LB_THREADS), 0, s, GfkArgT<false>{*m}); } while (0)
+static int launch_lb(const GfkModel* m, hipStream_t s, bool fwd) {
+  if ((m->bmax != 256 && m->bmax != 512) || m->dec_grid < 1 || !m->ws_dt || m->ldb < m->V) return -1;
+  if (fwd) {
+    if (m->bmax == 256) GFK_LB_LAUNCH(prodlda_lb_colbn_kernel, 256);
+    else GFK_LB_LAUNCH(prodlda_lb_colbn_kernel, 512);
+  } else {
+    if (m->bmax == 256) GFK_LB_LAUNCH(prodlda_lb_dlogit_kernel, 256);
+    else GFK_LB_LAUNCH(prodlda_lb_dlogit_kernel, 512);
+  }
+  return (int)hipGetLastError();
+}
+#undef GFK_LB_LAUNCH
 
 extern "C" int gfk_launch_prodlda_fwd(const GfkModel* m, hipStream_t s) {
+  if (m->stage_flags & GFK_LB) return launch_lb(m, s, true);
   const size_t sm = gfk_prodlda_fwd_smem(m);
   dim3 g(m->dec_grid), blk(DEC_THREADS);
   if (m->stage_flags & FWD_STRIP) {
@@ -1977,6 +2160,7 @@ static void launch_bwd(const GfkModel* m, hipStream_t s) {
 }
 
 extern "C" int gfk_launch_prodlda_bwd(const GfkModel* m, hipStream_t s) {
+  if (m->stage_flags & GFK_LB) return launch_lb(m, s, false);
   if (m->bmax != 16 && m->bmax != 32 && m->bmax != 64 && m->bmax != 128) return -1;
   if ((int64_t)m->K * m->ldb * 4 >= 0x7FFF0000LL) return -1;   // 32-bit buffer offsets
   switch ((m->K + 63) / 64) {

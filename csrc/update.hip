@@ -47,13 +47,18 @@ __host__ __device__ inline int stride_b(int w) {   // w: multiple of 16
 }
 }  // namespace
 
+// weight jobs stage the batch in chunks of at most WJ_ROWS rows (large batches: several)
+constexpr int WJ_ROWS = 128;
+
 extern "C" size_t gfk_win_update_smem(const GfkModel* m) {
   const int B = m->bmax, H0P = rup(m->H[0], 16);
-  size_t a = (size_t)64 * stride_a(B) + (size_t)B * stride_b(H0P);
-  const size_t b = 2 * (size_t)B * 80;
+  // (the dense x^T tile path does not run at bmax > 128: the large-batch plan always takes
+  // the sparse tiles)
+  size_t a = B > 128 ? 0 : (size_t)64 * stride_a(B) + (size_t)B * stride_b(H0P);
+  const size_t b = 2 * (size_t)(B < WJ_ROWS ? B : WJ_ROWS) * 80;
   if (a < 64 * 64) a = 64 * 64;      // the flat epilogue's gradient tile [64, H0 <= 64]
   // the sparse tile (bit 4): dz0, the entry list, the row slots (+ the word mask and list)
-  const size_t c = (size_t)B * m->H[0] + 2 * 512 + 129 + 128;
+  const size_t c = (size_t)B * m->H[0] + 2 * 512 + (B + 1 > 129 ? B + 1 : 129) + 128;
   if (a < c) a = c;
   // the dense contextual tile next to them (fused CombinedTM): dz0 + the A block / G tile
   const size_t d = (((size_t)B * m->H[0] + 3) & ~(size_t)3) +
@@ -139,8 +144,65 @@ __device__ __forceinline__ void weight_job(const GfkModel& m, const GfkWJob& J, 
   }
 }
 
-// Vector job (see GfkVJob): 16 lanes per element split the batch rows.
+// The large-batch plan's weight job (bmax > WJ_ROWS, gradient mode): the two [B x 64] column
+// slices staged WJ_ROWS rows at a time, the MFMA accumulators carried over the chunks, the
+// gradient stored.  LDS: dz[WJ_ROWS][LDJ] + a[WJ_ROWS][LDJ]
 template <int UT>
+__device__ __forceinline__ void weight_job_lb(const GfkModel& m, const GfkWJob& J, float* smem) {
+  constexpr int UW = UT / 64, WU = 16 / UW;
+  constexpr int LDJ = 80;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int B = m.bmax, nb = *m.ws_nb;
+  float* dzs = smem;
+  float* as = smem + WJ_ROWS * LDJ;
+  f32x4 c0[WU], c1[WU];
+#pragma unroll
+  for (int u = 0; u < WU; ++u) c0[u] = c1[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int b0 = 0; b0 < B; b0 += WJ_ROWS) {
+    if (b0) lds_barrier();             // the previous chunk's operand reads are done
+    for (int e0 = 0; e0 < WJ_ROWS * 64; e0 += 4 * UT) {
+      float vz[4], va[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = e0 + u * UT + tid, b = b0 + (e >> 6), c = e & 63;
+        vz[u] = J.dz[(size_t)b * J.rows + min(J.j0 + c, J.rows - 1)];
+        va[u] = J.a[(size_t)b * J.cols + min(J.i0 + c, J.cols - 1)];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = e0 + u * UT + tid, bl = e >> 6, b = b0 + bl, c = e & 63;
+        dzs[bl * LDJ + c] = (b < nb && J.j0 + c < J.rows) ? vz[u] : 0.f;
+        as[bl * LDJ + c] = (b < nb && J.i0 + c < J.cols) ? va[u] : 0.f;
+      }
+    }
+    lds_barrier();
+#pragma unroll
+    for (int u = 0; u < WU; ++u) {
+      const int t = wave + UW * u, jt = t >> 2, it = t & 3;
+      const float* ap = dzs + (lane >> 4) * LDJ + jt * 16 + (lane & 15);
+      const float* bp = as + (lane >> 4) * LDJ + it * 16 + (lane & 15);
+      for (int k = 0; k < WJ_ROWS; k += 8) {
+        c0[u] = mfma16x16x4(ap[k * LDJ], bp[k * LDJ], c0[u]);
+        c1[u] = mfma16x16x4(ap[(k + 4) * LDJ], bp[(k + 4) * LDJ], c1[u]);
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < WU; ++u) {
+    const int t = wave + UW * u, jt = t >> 2, it = t & 3;
+    const int i = J.i0 + it * 16 + (lane & 15);
+    const f32x4 g = c0[u] + c1[u];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = J.j0 + jt * 16 + (lane >> 4) * 4 + r;
+      if (j < J.rows && i < J.cols) J.param[(size_t)j * J.cols + i + m.off_g] = g[r];
+    }
+  }
+}
+
+// Vector job (see GfkVJob): 16 lanes per element split the batch rows.  LB: the large-batch
+// instance (rows in passes of 128)
+template <int UT, bool LB = false>
 __device__ __forceinline__ void vector_job(const GfkModel& m, const GfkVJob& J) {
   const int tid = threadIdx.x, s = tid & 15;
   const int B = m.bmax, nb = *m.ws_nb;
@@ -153,12 +215,20 @@ __device__ __forceinline__ void vector_job(const GfkModel& m, const GfkVJob& J) 
     float pp = 0.f, pm = 0.f, pv = 0.f, g = 0.f;
     if (fused) { pp = *p; pm = p[m.off_m]; pv = p[m.off_v]; }
     if (J.src) {
-      constexpr int RU = 8;                  // B <= 128: 8 rows per lane
+      constexpr int RU = 8;                  // 8 rows per lane per pass (LB: B / 128 passes)
       float v[RU];
 #pragma unroll
       for (int u = 0; u < RU; ++u) v[u] = J.src[(size_t)min(s + 16 * u, B - 1) * J.n + cc];
 #pragma unroll
       for (int u = 0; u < RU; ++u) g += s + 16 * u < nb ? v[u] : 0.f;
+      if constexpr (LB) {
+        for (int r0 = 16 * RU; r0 < B; r0 += 16 * RU) {
+#pragma unroll
+          for (int u = 0; u < RU; ++u) v[u] = J.src[(size_t)min(r0 + s + 16 * u, B - 1) * J.n + cc];
+#pragma unroll
+          for (int u = 0; u < RU; ++u) g += r0 + s + 16 * u < nb ? v[u] : 0.f;
+        }
+      }
       g = row16_sum(g);
     } else {
       g = p[m.off_g];
@@ -192,7 +262,9 @@ constexpr int WIN_BATCH8 = 512;
 // other staging loads) instead of 2 quads of registers per thread, so the tile fits 64
 // VGPRs and 4 workgroups per CU (fused mode; the launcher picks it when the block fits the
 // kernel's existing LDS budget)
-template <int UT, bool VL = false>
+// RS: row slots per thread (64 rows each): 2 up to bmax = 128, GFK_BMAX_LIMIT / 64 for the
+// large-batch plan
+template <int UT, bool VL = false, int RS = 2>
 __device__ __forceinline__ void win_tile_sparse(const GfkModel& m, float* smem, int tile) {
   constexpr int CAP = 512;
   constexpr int TPR = UT / 64;                 // threads per row, 64 rows per pass
@@ -203,8 +275,8 @@ __device__ __forceinline__ void win_tile_sparse(const GfkModel& m, float* smem, 
   float* dz = smem;                            // [B][H0]
   int* ecol = reinterpret_cast<int*>(dz + B * H0);   // [CAP] (row << 8) | local column
   float* ex = reinterpret_cast<float*>(ecol + CAP);  // [CAP]
-  int* offs = reinterpret_cast<int*>(ex + CAP);      // [129] rows' first slots, total
-  float* vb = smem + ((B * H0 + 2 * CAP + 129 + 3) & ~3);  // VL: [64 * H0] second moment
+  int* offs = reinterpret_cast<int*>(ex + CAP);      // [64 RS + 1] rows' first slots, total
+  float* vb = smem + ((B * H0 + 2 * CAP + 64 * RS + 1 + 3) & ~3);  // VL: [64 * H0] second moment
   float* wblk = m.w_in + (size_t)c0 * H0;
   const int nel = (min(V, c0 + 64) - c0) * H0;
   const bool fused = m.update_mode == 1;
@@ -223,15 +295,15 @@ __device__ __forceinline__ void win_tile_sparse(const GfkModel& m, float* smem, 
   const int32_t* tst = m.ws_tstart;
   const int ntp = m.n_tiles + 1;
   const int sub = tid % TPR;
-  int xe0[2], xe1[2], cnt[2];
+  int xe0[RS], xe1[RS], cnt[RS];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {              // rows tid / TPR (+ 64): the entry loads
+  for (int i = 0; i < RS; ++i) {             // rows tid / TPR (+ 64 i): the entry loads
     const int r = min(tid / TPR + 64 * i, B - 1);
     xe0[i] = tst[(size_t)r * ntp + tile];
     xe1[i] = tst[(size_t)r * ntp + tile + 1];
   }
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {              // wave 0: rows lane (+ 64): the slot scan
+  for (int i = 0; i < RS; ++i) {             // wave 0: rows lane (+ 64 i): the slot scan
     const int r = min(lane + 64 * i, B - 1);
     cnt[i] = wave == 0 ? tst[(size_t)r * ntp + tile + 1] - tst[(size_t)r * ntp + tile] : 0;
   }
@@ -261,10 +333,10 @@ __device__ __forceinline__ void win_tile_sparse(const GfkModel& m, float* smem, 
   glds_copy(dz, m.ws_dz[0], B * H0, tid, UT);
   __builtin_amdgcn_sched_barrier(0);
   // each thread's first entry of each of its rows (clamped, unconditional)
-  int fi[2];
-  float fv[2];
+  int fi[RS];
+  float fv[RS];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < RS; ++i) {
     const int e = min(xe0[i] + sub, max(xe1[i] - 1, 0));
     fi[i] = m.indices[e];
     fv[i] = m.values[e];
@@ -272,7 +344,7 @@ __device__ __forceinline__ void win_tile_sparse(const GfkModel& m, float* smem, 
   if (wave == 0) {             // row counts -> slots, rows in order
     int base = 0;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < RS; ++i) {
       const int c = lane + 64 * i < nb ? cnt[i] : 0;
       int x = c;
 #pragma unroll
@@ -283,10 +355,10 @@ __device__ __forceinline__ void win_tile_sparse(const GfkModel& m, float* smem, 
       offs[lane + 64 * i] = base + x - c;
       base += __shfl(x, 63, 64);
     }
-    if (lane == 0) offs[128] = base;
+    if (lane == 0) offs[64 * RS] = base;
   }
   vm_barrier();
-  const int total = offs[128];
+  const int total = offs[64 * RS];
   // this thread's quads: word (row) v0 and column h0 of the first element; a quad spans at
   // most two words (H0 >= 4): elements with h0 + i >= H0 belong to word v0 + 1
   int qv[FQ], qh[FQ];
@@ -323,7 +395,7 @@ __device__ __forceinline__ void win_tile_sparse(const GfkModel& m, float* smem, 
   // (more than CAP entries in the tile) re-read the rows' extents, so neither the extents
   // nor the first entries stay live across the sums
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < RS; ++i) {
     const int r = tid / TPR + 64 * i;
     if (r >= nb) continue;
     const int o = offs[r] - xe0[i];
@@ -342,7 +414,7 @@ __device__ __forceinline__ void win_tile_sparse(const GfkModel& m, float* smem, 
   for (int p0 = CAP; p0 < total; p0 += CAP) {
     __syncthreads();                           // the previous pass's list reads are done
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < RS; ++i) {
       const int r = tid / TPR + 64 * i;
       if (r >= nb) continue;
       const int a0 = tst[(size_t)r * ntp + tile], a1 = tst[(size_t)r * ntp + tile + 1];
@@ -519,7 +591,7 @@ __global__ void __launch_bounds__(WCT, 4) gfk_win_ctx_pp_k(GfkArgT<GB> ga) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
   const int V = m.V, H0 = m.H[0], B = m.bmax, nb = *m.ws_nb;
-  const int G = (int)gridDim.x, w = (int)blockIdx.x;
+  const int G = (int)gridDim.x, w = (int)gfk_bx();
   const int U = (V + 15) / 16;
   const int cs = (int)((int64_t)w * U / G) * 16;
   const int ce = min(V, (int)((int64_t)(w + 1) * U / G) * 16);
@@ -820,7 +892,7 @@ __global__ void __launch_bounds__(256) gfk_win_dense_k(GfkArgT<GB> ga) {
   const GfkModel& m = gfk_model(ga);
   const int H0 = m.H[0];
   const int64_t n = (int64_t)m.V * H0;
-  const int64_t q0 = ((int64_t)blockIdx.x * 256 * WD_QU) + threadIdx.x;
+  const int64_t q0 = ((int64_t)gfk_bx() * 256 * WD_QU) + threadIdx.x;
   const int32_t* st = m.ws_wstamp;
   const int tag = *m.ws_wgen;
   int sa[WD_QU], sb[WD_QU];
@@ -916,14 +988,14 @@ __global__ void __launch_bounds__(UT, UT == 512 ? 8 : 1) gfk_win_update_k(GfkArg
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int nt_here = m.n_tiles;
   {
-    const int r = (int)blockIdx.x - nt_here;
+    const int r = (int)gfk_bx() - nt_here;
     if (r >= 0 && r < U.n_w) { weight_job<UT>(m, U.w[r], smem); return; }
     if (r >= U.n_w && r < U.n_w + U.n_v) { vector_job<UT>(m, U.v[r - U.n_w]); return; }
     if (r == U.n_w + U.n_v) { prepare_next_batch(m, reinterpret_cast<int*>(smem)); return; }
   }
   const bool zs = m.ctx_fused == 2;            // ZeroShotTM: W_in is the dense [C, H0] layer
   if (m.input == GFK_IN_CONTEXTUAL && !zs) return;   // (host GEMMs when not fused)
-  const int rr = (int)blockIdx.x - (nt_here + U.n_w + U.n_v + 1);
+  const int rr = (int)gfk_bx() - (nt_here + U.n_w + U.n_v + 1);
   const bool ctxt = rr >= 0;                   // a Wc tile (CombinedTM) / W tile (ZeroShotTM)
   if (zs && !ctxt) return;                     // ZeroShotTM has no bag-of-words half
   const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
@@ -936,7 +1008,7 @@ __global__ void __launch_bounds__(UT, UT == 512 ? 8 : 1) gfk_win_update_k(GfkArg
   const int XS = stride_a(B), ZS = stride_b(H0P);
   float* xt = smem;
   float* dz = smem + 64 * XS;
-  const int tile = ctxt ? rr : (int)blockIdx.x, c0 = tile * 64;
+  const int tile = ctxt ? rr : (int)gfk_bx(), c0 = tile * 64;
 
   GFK_STAMP(m, 40);
   // ---- staging: dz0 rows (zero padding), zero x^T tile, the tile's CSR extents ----
@@ -1154,20 +1226,24 @@ __global__ void __launch_bounds__(UT, UT == 512 ? 8 : 1) gfk_win_update_k(GfkArg
 // its own (the job paths of gfk_win_update_k need ~86 VGPRs)
 // grid: n_w + n_v + 1 job workgroups FIRST (they start with the tiles, not after them),
 // then the n_tiles sparse W_in tiles (+ n_tiles dense contextual tiles: fused CombinedTM)
-template <int UT, bool GB = false, bool VL = false, bool CTX = false>
+template <int UT, bool GB = false, bool VL = false, bool CTX = false, int RS = 2>
 __global__ void __launch_bounds__(UT, VL ? 4096 / UT : 1) gfk_win_sparse_k(GfkArgT<GB> ga, GfkUArgT<GB> gua) {
   const GfkModel& m = gfk_model(ga);
   const GfkUpdate& U = gfk_upd(gua);
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int r = (int)blockIdx.x;
-  if (r < U.n_w) { weight_job<UT>(m, U.w[r], smem); return; }
-  if (r < U.n_w + U.n_v) { vector_job<UT>(m, U.v[r - U.n_w]); return; }
+  const int r = (int)gfk_bx();
+  if (r < U.n_w) {
+    if constexpr (RS > 2) weight_job_lb<UT>(m, U.w[r], smem);
+    else weight_job<UT>(m, U.w[r], smem);
+    return;
+  }
+  if (r < U.n_w + U.n_v) { vector_job<UT, (RS > 2)>(m, U.v[r - U.n_w]); return; }
   if (r == U.n_w + U.n_v) { prepare_next_batch(m, reinterpret_cast<int*>(smem)); return; }
   const int t = r - (U.n_w + U.n_v + 1);
   if constexpr (CTX) {
     if (t >= m.n_tiles) { win_tile_ctx<UT>(m, smem, t - m.n_tiles); return; }
   }
-  win_tile_sparse<UT, VL>(m, smem, t);
+  win_tile_sparse<UT, VL, RS>(m, smem, t);
 }
 
 // the split update's sparse half: the same job workgroups, then the batch words' tiles (its
@@ -1177,7 +1253,7 @@ __global__ void __launch_bounds__(UT) gfk_win_rows_k(GfkArgT<GB> ga, GfkUArgT<GB
   const GfkModel& m = gfk_model(ga);
   const GfkUpdate& U = gfk_upd(gua);
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int r = (int)blockIdx.x;
+  const int r = (int)gfk_bx();
   if (r < U.n_w) { weight_job<UT>(m, U.w[r], smem); return; }
   if (r < U.n_w + U.n_v) { vector_job<UT>(m, U.v[r - U.n_w]); return; }
   if (r == U.n_w + U.n_v) { prepare_next_batch(m, reinterpret_cast<int*>(smem)); return; }
@@ -1202,6 +1278,7 @@ extern "C" int gfk_launch_win_dense(const GfkModel* m, hipStream_t s) {
 constexpr int WIN_VREG = 1024;
 static bool win_sparse_vl(const GfkModel* m) {
   if ((m->stage_flags & WIN_VREG) || m->update_mode != 1) return false;
+  if (m->bmax > 128) return false;      // (the large-batch instance keeps it in registers)
   const size_t need = sizeof(float) * ((((size_t)m->bmax * m->H[0] + 2 * 512 + 129 + 3) & ~(size_t)3) +
                                        (size_t)64 * m->H[0]);
   return need <= gfk_win_update_smem(m);
@@ -1218,9 +1295,23 @@ static bool win_sparse_vl(const GfkModel* m) {
                          gfk_win_update_smem(m), s, GfkArgT<false>{*m}, GfkUArgT<false>{*u});    \
   } while (0)
 
+#define GFK_WIN_SPARSE_LB_LAUNCH()                                                                   \
+  do {                                                                                           \
+    constexpr int RSL = GFK_BMAX_LIMIT / 64;                                                     \
+    if (m->n_batch > 1)                                                                          \
+      hipLaunchKernelGGL((gfk_win_sparse_k<512, true, false, false, RSL>), gfk_grid(gs, m),     \
+                         dim3(512), gfk_win_update_smem(m), s, GfkArgT<true>{gfk_dev(m)},        \
+                         GfkUArgT<true>{reinterpret_cast<const GfkUpdate*>(m->dev_upd)});        \
+    else                                                                                         \
+      hipLaunchKernelGGL((gfk_win_sparse_k<512, false, false, false, RSL>), gs, dim3(512),       \
+                         gfk_win_update_smem(m), s, GfkArgT<false>{*m}, GfkUArgT<false>{*u});    \
+  } while (0)
+
 static int launch_win_sparse_bow(const GfkModel* m, const GfkUpdate* u, hipStream_t s) {
   const dim3 gs(u->n_w + u->n_v + 1 + m->n_tiles);
-  if (win_sparse_vl(m))
+  if (m->bmax > 128)
+    GFK_WIN_SPARSE_LB_LAUNCH();
+  else if (win_sparse_vl(m))
     GFK_WIN_SPARSE_LAUNCH(true, false);
   else
     GFK_WIN_SPARSE_LAUNCH(false, false);
@@ -1233,8 +1324,9 @@ extern "C" int gfk_launch_win_update(const GfkModel* m, const GfkUpdate* u, hipS
     // bag-of-words inputs, or fused CombinedTM (its contextual half as dense tiles after
     // the sparse ones: B <= 64 so the operand blocks fit the kernel's LDS)
     const bool comb = m->input == GFK_IN_COMBINED && m->ctx_fused == 1;
-    if (m->H[0] > 64 || m->bmax > (comb ? 64 : 128) || !(m->input == GFK_IN_BOW || comb) ||
-        (comb && (m->stage_flags & GFK_WIN_SPLIT)))
+    if (m->H[0] > 64 || m->bmax > (comb ? 64 : GFK_BMAX_LIMIT) || !(m->input == GFK_IN_BOW || comb) ||
+        (comb && (m->stage_flags & GFK_WIN_SPLIT)) ||
+        (m->bmax > 128 && (m->stage_flags & GFK_WIN_SPLIT)))
       return -1;
     // the contextual half: dense tiles of this launch, or the persistent kernel after it
     const bool ctxpp = comb && (m->stage_flags & WIN_CTXPP) && m->ctx_bgrid > 0;
@@ -1247,7 +1339,9 @@ extern "C" int gfk_launch_win_update(const GfkModel* m, const GfkUpdate* u, hipS
       return (int)hipGetLastError();
     }
     const dim3 gs(u->n_w + u->n_v + 1 + m->n_tiles * (comb ? 2 : 1));
-    if (m->stage_flags & GFK_WIN_SPLIT)
+    if (m->bmax > 128)
+      GFK_WIN_SPARSE_LB_LAUNCH();
+    else if (m->stage_flags & GFK_WIN_SPLIT)
       do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_win_rows_k<512, true>), gfk_grid(gs, m), dim3(512), gfk_win_update_smem(m), s, GfkArgT<true>{gfk_dev(m)}, GfkUArgT<true>{reinterpret_cast<const GfkUpdate*>(m->dev_upd)}); else hipLaunchKernelGGL((gfk_win_rows_k<512, false>), gs, dim3(512), gfk_win_update_smem(m), s, GfkArgT<false>{*m}, GfkUArgT<false>{*u}); } while (0);
     else if (comb && win_sparse_vl(m))
       GFK_WIN_SPARSE_LAUNCH(true, true);
@@ -1259,6 +1353,7 @@ extern "C" int gfk_launch_win_update(const GfkModel* m, const GfkUpdate* u, hipS
       GFK_WIN_SPARSE_LAUNCH(false, false);
     return (int)hipGetLastError();
   }
+  if (m->bmax > 128) return -1;      // (large batches: the sparse tiles only)
   const dim3 g(m->n_tiles + u->n_w + u->n_v + 1 + extra);
   // more W_in tiles than two rounds of 16-wave workgroups (dec_grid = the CUs' slots), or the
   // batched launch of several clients' tiles asks for the 8-wave shape (stage_flags bit 9,
@@ -1282,7 +1377,9 @@ extern "C" int gfk_win_update_set_smem(size_t bytes) {
                       (const void*)gfk_win_sparse_k<512, false, true>, (const void*)gfk_win_sparse_k<512, true, true>,
                       (const void*)gfk_win_sparse_k<512, false, false, true>, (const void*)gfk_win_sparse_k<512, true, false, true>,
                       (const void*)gfk_win_sparse_k<512, false, true, true>, (const void*)gfk_win_sparse_k<512, true, true, true>,
-                      (const void*)gfk_win_rows_k<512, false>, (const void*)gfk_win_rows_k<512, true>};
+                      (const void*)gfk_win_rows_k<512, false>, (const void*)gfk_win_rows_k<512, true>,
+                      (const void*)gfk_win_sparse_k<512, false, false, false, GFK_BMAX_LIMIT / 64>,
+                      (const void*)gfk_win_sparse_k<512, true, false, false, GFK_BMAX_LIMIT / 64>};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return (int)e;

@@ -202,12 +202,24 @@ class LocalFederation:
         self._batched = None
         if self.round_batched:
             from ..ops.engine import BatchedSteps
-            if BatchedSteps.possible(engines):
+            # groups (the golden of a multi-rank layout): one batched launch per group, as
+            # each rank batches its own clients -- the launch plan (grid fill, backward
+            # slabs) depends on the client count and fixes the summation order, so the
+            # golden mirrors it to stay bit-identical to the ranks
+            sizes = self.agg.groups or [len(engines)]
+            parts, o = [], 0
+            for s in sizes:
+                parts.append(engines[o:o + s])
+                o += s
+            if all(BatchedSteps.possible(p) for p in parts):
                 # one launch per phase for all clients (grid z = client), then the FedAvg kernel
-                self._batched = BatchedSteps(engines)
-                self._batched.prepare()
+                self._batched_parts = [BatchedSteps(p) for p in parts]
+                self._batched = self._batched_parts[0]
+                for b in self._batched_parts:
+                    b.prepare()
                 with graph_capture(g):
-                    self._batched.launch()
+                    for b in self._batched_parts:
+                        b.launch()
                     if not self.agg.fused_sum_(shared):
                         raise RuntimeError("round graph needs the native FedAvg kernel")
                 self._rg = g

@@ -44,7 +44,9 @@ from ..utils.misc import graph_capture
 from . import kernel_abi as abi
 from . import native
 
-BMAX_CHOICES = (16, 32, 64, 128)
+BMAX_CHOICES = (16, 32, 64, 128, 256, 512)
+# batch sizes above this run the large-batch plan (csrc/gfk_common.h GFK_LB)
+LB_MIN_BMAX = 256
 LDS_LIMIT = 160 * 1024
 VB = 64
 # stage_flags plans, fastest first: bit 0 = MLP weights staged in LDS (enc_in,
@@ -70,6 +72,7 @@ STAGE_CTX_RS = 32768              # bit 15: CombinedTM forward, Wa register-stre
 STAGE_FWD_POSTFOLD = 65536        # bit 16: the strip forward computes post_fwd (csrc/prodlda.hip FP)
 STAGE_POST_EXTRA_ROWBWD = 131072  # bit 17: post_bwd's batch-level workgroup runs in row_bwd
 STAGE_BWD_KQ1 = 262144            # bit 18: one-k-range backward walking several tiles (K <= 64)
+STAGE_LB = 524288                 # bit 19: the large-batch plan (bmax 256 / 512, csrc/gfk_common.h)
 
 
 def _explain(ok: bool, why: str, explain: bool) -> bool:
@@ -86,7 +89,7 @@ def supports(tm, explain: bool = False) -> bool:
         (native.kernels_available(), "kernel library not built"),
         (tm.solver in abi.SOLVER_CODES, f"solver {tm.solver} not fused"),
         (tm.activation in abi.ACT_CODES, f"activation {tm.activation} not fused"),
-        (tm.batch_size <= BMAX_CHOICES[-1], "batch_size > 128"),
+        (tm.batch_size <= BMAX_CHOICES[-1], f"batch_size > {BMAX_CHOICES[-1]}"),
         (tm.n_components <= 256, "n_components > 256"),
         (max(tm.hidden_sizes) <= 512 and len(tm.hidden_sizes) <= abi.MAX_LAYERS,
          "hidden layers too wide / too many"),
@@ -98,6 +101,15 @@ def supports(tm, explain: bool = False) -> bool:
         if not _explain(ok, why, explain):
             return False
     bmax = next(b for b in BMAX_CHOICES if b >= tm.batch_size)
+    if bmax >= LB_MIN_BMAX:
+        # the large-batch plan: bag-of-words AVITM, the sparse W_in tiles (H0 <= 64), the
+        # [bmax, ldb] logit matrix addressed with 32-bit buffer offsets
+        lb = [(tm.kind != "ctm", "batch_size > 128 needs a bag-of-words AVITM model"),
+              (tm.hidden_sizes[0] <= 64, "batch_size > 128 needs hidden_sizes[0] <= 64"),
+              (4 * bmax * beta_ld(tm.input_size) < (1 << 31), "batch_size x vocabulary too large")]
+        for ok, why in lb:
+            if not _explain(ok, why, explain):
+                return False
     need = lds_required(tm, bmax)
     return _explain(need <= LDS_LIMIT, f"LDS budget exceeded ({need} B)", explain)
 
@@ -169,8 +181,11 @@ def lds_required(tm, bmax: int) -> int:
     m.vb, m.n_tiles = VB, -(-m.V // VB)
     m.n_dpart = m.n_tiles if m.kind == abi.KIND_PRODLDA else 1
     lib = native.kernels()
-    _force_k_split(lib, m)
     which = (0, 1) if m.kind == abi.KIND_PRODLDA else (2, 3)
+    if bmax >= LB_MIN_BMAX:
+        m.stage_flags, m.n_dpart = 2 | STAGE_LB | STAGE_WIN_SPARSE, 1
+        return int(max(lib.gfk_smem_required(C.byref(m), w) for w in which + (4, 5, 7)))
+    _force_k_split(lib, m)
     need = 0
     for flags in (0, 2):                 # weights unstaged; batch matrices in LDS, then in L2
         m.stage_flags = flags
@@ -307,6 +322,11 @@ class FusedEngine(EngineBase):
         self.eps, self.weight_decay = hp["eps"], 0.0
         self.fedavg_scale: Optional[float] = None
         self.bmax = next(b for b in BMAX_CHOICES if b >= tm.batch_size)
+        # the large-batch plan (bmax 256 / 512): library GEMMs for the decoder products,
+        # gradient mode (the kernels write gradients; the generic optimizer kernel follows)
+        self.large_batch = self.bmax >= LB_MIN_BMAX
+        if self.large_batch:
+            self.update_mode = UPDATE_GRAD
         self.param_order: List[Tuple[str, torch.nn.Parameter]] = list(self.model.named_parameters())
         self.optimizer = FusedAdamState(self)
         self.seed = int(torch.randint(0, 2**62, (1,)).item())
@@ -349,6 +369,8 @@ class FusedEngine(EngineBase):
         gradients and the generic Adam kernel follows."""
         if mode == UPDATE_FUSED and self.kind == "ctm" and not self.ctx_fused:
             raise ValueError("the fused update mode needs the fused contextual path")
+        if mode == UPDATE_FUSED and self.large_batch:
+            raise ValueError("the large-batch plan runs in gradient mode")
         if mode == UPDATE_FUSED and self.solver != "adam":
             raise ValueError(f"the fused update mode is Adam only (solver {self.solver})")
         self.update_mode = mode
@@ -468,6 +490,13 @@ class FusedEngine(EngineBase):
         m.off_g = (self.grad.data_ptr() - P.data_ptr()) // 4
         m.adam_pow, m.adam_coef = self.adam_pow.data_ptr(), self.adam_coef.data_ptr()
         self._sync_opt_fields()
+        if self.large_batch:
+            self._plan_large_batch(props.multi_processor_count)
+            self._alloc_workspace()
+            rc = self.lib.gfk_setup(C.byref(m))
+            if rc:
+                raise RuntimeError(f"gfk_setup failed ({rc})")
+            return
         which = (0, 1) if m.kind == abi.KIND_PRODLDA else (2, 3)
         k_split = _force_k_split(self.lib, m)
         need = lambda: max(self.lib.gfk_smem_required(C.byref(m), w)  # noqa: E731
@@ -647,6 +676,49 @@ class FusedEngine(EngineBase):
         if rc:
             raise RuntimeError(f"gfk_setup failed ({rc})")
 
+    def _plan_large_batch(self, cu: int):
+        """The large-batch plan, 128 < batch_size <= 512 (csrc/gfk_common.h GFK_LB; reference
+        avitm.py:84-85 takes any batch_size).  The row-parallel kernels (enc_in, post_fwd,
+        row_loss, row_bwd, post_bwd) run as for small batches with the [B, K] batch matrices
+        read from L2 (bit 1), W_in's gradient on the sparse tiles (bit 4), the weight jobs and
+        NeuralLDA's beta backward in 128-row chunks.  ProdLDA's decoder: logits = theta_d beta,
+        dbeta = theta_d^T dlogit and d theta_d = dlogit beta^T are hipBLASLt GEMMs on the step's
+        stream (PH_LB_GEMM_FWD / _BWD: at B >= 256 they are large enough to run near the
+        matrix cores' fp32 peak) around prodlda_lb_colbn (column batch-norm, BN'ed tiles, row
+        sum-exp partials) and prodlda_lb_dlogit (the logit gradient) -- one slab of d theta_d,
+        the [B, ldb] logit / logit-gradient matrix in ws["dt"].  Gradient mode: the generic
+        optimizer kernel updates every tensor (as the CTM host-GEMM path)."""
+        m = self._m
+        m.stage_flags = 2 | STAGE_LB | STAGE_WIN_SPARSE
+        m.dec_grid = int(min(m.n_tiles, 2 * cu))
+        m.n_dpart = 1
+        m.bwd_pre = 0
+        m.beta_split = 0
+        self._win_split_ok = False
+        which = (0, 1) if m.kind == abi.KIND_PRODLDA else (2, 3)
+        need = max(self.lib.gfk_smem_required(C.byref(m), w) for w in which + (4, 5, 7))
+        if need > LDS_LIMIT:
+            raise RuntimeError(f"large-batch plan needs {need} B of LDS (> {LDS_LIMIT})")
+
+    def _lb_views(self):
+        """(theta_d [B, K], beta [K, ldb], beta's gradient [K, ldb], the logit matrix
+        [B, ldb], d theta_d slab 0 [B, K]) for the large-batch GEMMs."""
+        if getattr(self, "_lbv", None) is None:
+            B, K = self.bmax, int(self._m.K)
+            self._lbv = (self.ws["thetad"][:, :K], self.raw_like(self.flat.buffer, "beta"),
+                         self.raw_like(self.grad, "beta"), self.ws["dt"],
+                         self.ws["dthetad"][: B * K].view(B, K))
+        return self._lbv
+
+    def _lb_gemm_fwd(self):
+        th, beta, _, dt, _ = self._lb_views()
+        torch.mm(th, beta, out=dt)                       # logits [B, ldb]
+
+    def _lb_gemm_bwd(self):
+        th, beta, gbeta, dt, dth = self._lb_views()
+        torch.mm(th.t(), dt, out=gbeta)                  # dbeta = theta_d^T dlogit
+        torch.mm(dt, beta.t(), out=dth)                  # d theta_d = dlogit beta^T
+
     def _plan_ctx(self, cu: int):
         """Fused CombinedTM contextual kernels (csrc/ctx.hip).  The forward runs one
         workgroup per (vocab tile, 16-row block); the backward splits C into chunks
@@ -721,7 +793,9 @@ class FusedEngine(EngineBase):
             "hpart": f(m.n_tiles * B * hs[0] if m.ctx_fused == 1 else 1),
             # precomputed logit-gradient tiles [n_tiles][B][66] (bwd_pre; + the pipelined
             # backward's store sinks, 64 floats per workgroup)
-            "dt": f(m.n_tiles * B * 66 + 64 * (4 * m.n_dpart + 32) if m.bwd_pre else 1),
+            # (the large-batch plan: the [B, ldb] logit / logit-gradient matrix)
+            "dt": f(B * int(m.ldb) if m.stage_flags & STAGE_LB else
+                    m.n_tiles * B * 66 + 64 * (4 * m.n_dpart + 32) if m.bwd_pre else 1),
             # split W_in update: per-word generation stamps of the batch's words + the
             # current generation (prepare_next_batch -> gfk_win_dense_k)
             "wstamp": torch.zeros((V if getattr(self, "_win_split_ok", False) else 1) + 16,
@@ -864,6 +938,14 @@ class FusedEngine(EngineBase):
         return "bf16" if m.mm_bf16 and (m.stage_flags & rs) == rs else "fp32"
 
     @property
+    def plan(self) -> str:
+        """The launch plan in one phrase (recorded in bench / metrics records)."""
+        if self.large_batch:
+            return ("large-batch: hipBLASLt decoder GEMMs + HIP kernels, gradient mode"
+                    if self._m.kind == abi.KIND_PRODLDA else "large-batch: HIP kernels, gradient mode")
+        return "fused kernels" + (" (fused optimizer epilogues)" if self.update_mode == UPDATE_FUSED else "")
+
+    @property
     def beta_split(self) -> bool:
         """Beta's update runs as a separate streaming optimizer pass (large V)."""
         return bool(self._m.beta_split) and self.update_mode == UPDATE_FUSED
@@ -951,6 +1033,9 @@ class FusedEngine(EngineBase):
                 ([abi.PH_ADAM] if self.update_mode == UPDATE_GRAD else [])
         else:
             ph = abi.PRODLDA_STEP + ([abi.PH_ADAM] if self.update_mode == UPDATE_GRAD else [])
+            if self.large_batch:                    # the decoder's GEMMs around its kernels
+                ph.insert(ph.index(abi.PH_PRODLDA_FWD), abi.PH_LB_GEMM_FWD)
+                ph.insert(ph.index(abi.PH_PRODLDA_BWD) + 1, abi.PH_LB_GEMM_BWD)
             if self._m.stage_flags & STAGE_FWD_POSTFOLD:
                 ph.remove(abi.PH_POST_FWD)          # computed by the strip forward
             if self.beta_split:
@@ -1294,6 +1379,10 @@ class FusedEngine(EngineBase):
                         self._win_fork()
                     elif p == abi.PH_WIN_JOIN:
                         self._win_join()
+                    elif p == abi.PH_LB_GEMM_FWD:
+                        self._lb_gemm_fwd()
+                    elif p == abi.PH_LB_GEMM_BWD:
+                        self._lb_gemm_bwd()
                 else:
                     run.append(p)
             return
@@ -1332,9 +1421,22 @@ class FusedEngine(EngineBase):
 
     @property
     def host_gemm_fallback(self) -> bool:
-        """True when the CTM contextual path runs as host-issued library GEMMs (shapes
-        outside the fused ctx kernels' plan, see _plan_ctx)."""
-        return self.kind == "ctm" and not self.ctx_fused
+        """True when part of the step runs as host-issued library GEMMs: the CTM contextual
+        path outside the fused ctx kernels' plan (_plan_ctx), or the large-batch plan's
+        decoder (_plan_large_batch)."""
+        return (self.kind == "ctm" and not self.ctx_fused) or self.large_batch
+
+    def _warm_host_gemms(self):
+        """hipBLASLt picks algorithms / workspaces on a shape's first call, which is not
+        allowed while capturing: run the host GEMMs once eagerly (their outputs are fully
+        rewritten by the next step before anything reads them)."""
+        if self._ctx is not None and not self.ctx_fused:
+            self._ctx_fwd()
+            self._ctx_bwd()
+        if self.large_batch and self._m.kind == abi.KIND_PRODLDA:
+            self._lb_gemm_fwd()
+            self._lb_gemm_bwd()
+        torch.cuda.synchronize(self.device)
 
     def enable_graph(self, on: bool = True):
         self.graph_enabled = on
@@ -1342,13 +1444,8 @@ class FusedEngine(EngineBase):
 
     def _capture(self):
         # warm-up on a side stream is not needed: no lazy allocation in gfk_run
-        if self._ctx is not None and not self.ctx_fused:
-            # hipBLASLt picks algorithms / workspaces on a shape's first call, which is
-            # not allowed while capturing: run the host GEMMs once eagerly (their
-            # outputs are fully rewritten by the next step before anything reads them)
-            self._ctx_fwd()
-            self._ctx_bwd()
-            torch.cuda.synchronize(self.device)
+        if self.host_gemm_fallback:
+            self._warm_host_gemms()
         self._sync_dev()
         g = torch.cuda.CUDAGraph()
         saved = (self.d_step.clone(), self.adam_t.clone(), self.adam_pow.clone(),
@@ -1373,10 +1470,8 @@ class FusedEngine(EngineBase):
     def prepare_external_capture(self):
         """Run anything that must not happen for the first time inside a capture."""
         self._sync_dev()
-        if self._ctx is not None and not self.ctx_fused:
-            self._ctx_fwd()
-            self._ctx_bwd()
-            torch.cuda.synchronize(self.device)
+        if self.host_gemm_fallback:
+            self._warm_host_gemms()
 
     def launch_step_phases(self):
         """Enqueue one step's kernels on the current stream (no graph of its own;
@@ -1528,8 +1623,9 @@ class BatchedSteps:
                 mm.dec_grid = fill
             elif (mm.stage_flags & STAGE_FWD_STRIP and M * mm.dec_grid > self._cu
                     and bstrip != "keep"):
-                mm.stage_flags = (mm.stage_flags & ~(STAGE_FWD_STRIP_ROLL | STAGE_FWD_STRIP_RING)) \
-                    | STAGE_FWD_STRIP_PF
+                # (the prefetching variant has no folded posterior: post_fwd runs again)
+                mm.stage_flags = (mm.stage_flags & ~(STAGE_FWD_STRIP_ROLL | STAGE_FWD_STRIP_RING
+                                                     | STAGE_FWD_POSTFOLD)) | STAGE_FWD_STRIP_PF
             # post_bwd: M clients x (bmax + 1) workgroups of 16 waves with the batch matrices
             # in LDS (~93 KB: one per CU) ran in three rounds at M = 8; with the matrices read
             # from L2 (stage_flags bit 1, ~42 KB) and the batch-level workgroup moved into
@@ -1555,6 +1651,12 @@ class BatchedSteps:
                 mm.stage_flags |= STAGE_WIN_BATCH8
             ms.append(bytes(mm))
             us.append(bytes(e._u))
+        # the phases of the batched plan: post_fwd back in where the launch dropped the fold
+        ph = list(self.engines[0].phases())
+        if (abi.PH_PRODLDA_FWD in ph and abi.PH_POST_FWD not in ph
+                and not abi.GfkModel.from_buffer_copy(ms[0]).stage_flags & STAGE_FWD_POSTFOLD):
+            ph.insert(ph.index(abi.PH_PRODLDA_FWD), abi.PH_POST_FWD)
+        self._phases = ph
         blob = b"".join(ms) + b"".join(us)
         if blob != self._blob:
             if torch.cuda.is_current_stream_capturing():

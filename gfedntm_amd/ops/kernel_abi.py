@@ -58,8 +58,13 @@ PH_WIN_JOIN = 106
 # CombinedTM (fused): adapt_bert's share of the FedAvg forked onto the side stream once
 # ctx_bwd has finished it (overlapping win_update), behind beta's
 PH_FEDAVG_WA = 107
+# the large-batch plan (bmax 256 / 512): ProdLDA's decoder products as hipBLASLt GEMMs on the
+# step's stream -- logits = theta_d beta before prodlda_lb_colbn (PH_PRODLDA_FWD), dbeta and
+# d theta_d after prodlda_lb_dlogit (PH_PRODLDA_BWD)
+PH_LB_GEMM_FWD = 108
+PH_LB_GEMM_BWD = 109
 HOST_PHASES = (PH_CTX_FWD, PH_CTX_BWD, PH_FEDAVG_BETA, PH_FEDAVG_END, PH_BETA_ADAM, PH_WIN_FORK,
-               PH_WIN_JOIN, PH_FEDAVG_WA)
+               PH_WIN_JOIN, PH_FEDAVG_WA, PH_LB_GEMM_FWD, PH_LB_GEMM_BWD)
 
 PRODLDA_STEP = [PH_ENC_FWD, PH_POST_FWD, PH_PRODLDA_FWD, PH_PRODLDA_LOSS, PH_PRODLDA_BWD,
                 PH_POST_BWD, PH_ENC_BWD]

@@ -223,12 +223,17 @@ def test_batched_round_matches_branch_round(model_type):
         assert torch.equal(x.tm.flat.buffer, y.tm.flat.buffer)
 
 
-def test_batched_large_round_variants_match_branch_round():
-    """8 clients at the headline's vocabulary (70 tiles each): the batched launch switches
-    the strip forward to its 8-wave variant and win_update to its 8-wave tile shape (all
+@pytest.mark.parametrize("strip", ["fill", "pf"])
+def test_batched_large_round_variants_match_branch_round(monkeypatch, strip):
+    """8 clients at the headline's vocabulary (~74 tiles each): the batched launch switches
+    the strip forward to 4 tiles per 16-wave workgroup ("fill", the default; "pf": the
+    8-wave prefetching variant), prodlda_bwd to workgroups walking several tiles, post_bwd's
+    batch-level workgroup into row_bwd, and win_update to its 8-wave tile shape (all
     clients' tiles exceed two rounds of 16-wave workgroups).  The round must still agree
     with the per-client branch round within fp32 rounding."""
-    from gfedntm_amd.ops.engine import STAGE_FWD_STRIP_PF, STAGE_WIN_BATCH8
+    from gfedntm_amd.ops.engine import (STAGE_BWD_KQ1, STAGE_FWD_STRIP_PF, STAGE_FWD_STRIP_RING,
+                                        STAGE_POST_EXTRA_ROWBWD, STAGE_WIN_BATCH8)
+    monkeypatch.setenv("GFEDNTM_BATCH_STRIP", strip)
     sc = generate_synthetic(vocab_size=5000, n_topics=50, n_docs=1000, n_nodes=8, frozen_topics=5,
                             nwords=(150, 250), seed=13)
     corpora = [ClientCorpus(synthetic=sc, node=i) for i in range(8)]
@@ -241,8 +246,13 @@ def test_batched_large_round_variants_match_branch_round():
     assert a._batched is not None
     host = a._batched._host
     cu = torch.cuda.get_device_properties(0).multi_processor_count
-    assert 8 * host.dec_grid > cu and 8 * (host.n_tiles + 8) > 2 * cu, (host.n_tiles, host.dec_grid)
-    assert host.stage_flags & STAGE_FWD_STRIP_PF and host.stage_flags & STAGE_WIN_BATCH8
+    assert 8 * (host.n_tiles + 8) > 2 * cu and host.stage_flags & STAGE_WIN_BATCH8, host.n_tiles
+    if strip == "fill":
+        assert host.dec_grid == -(-host.n_tiles // 4) and host.stage_flags & STAGE_FWD_STRIP_RING
+    else:
+        assert 8 * host.dec_grid > cu and host.stage_flags & STAGE_FWD_STRIP_PF
+    assert host.stage_flags & STAGE_POST_EXTRA_ROWBWD and host.stage_flags & 2
+    assert host.stage_flags & STAGE_BWD_KQ1 and host.n_dpart < host.n_tiles, host.n_dpart
     lr = a.clients[0].tm.engine.lr
     for x, y in zip(a.clients, b.clients):
         diff = (x.tm.flat.buffer - y.tm.flat.buffer).abs()

@@ -1,0 +1,85 @@
+"""The fused engine's large-batch plan, 128 < batch_size <= 512 (csrc/gfk_common.h GFK_LB;
+ops/engine.py FusedEngine._plan_large_batch).  The reference takes any batch_size
+(avitm.py:84-85, SURVEY.md item 4 of round 4's verdict); up to 128 rows the fused kernels keep
+the batch in LDS, above it the row-parallel kernels read the batch matrices from L2, the weight
+jobs and NeuralLDA's beta backward stage 128-row chunks, and ProdLDA's decoder products are
+hipBLASLt GEMMs around two HIP kernels (column batch-norm / logit gradient).
+
+Oracle: the same PyTorch fp32 functional step as tests/test_fused_kernels.py (loss, KL, RL,
+every gradient, BN running statistics, the optimizer step) at B in {256, 512} x K in {50, 200}
+x V in {5k, 112k}, ProdLDA and NeuralLDA, plus a partial batch and a graph-replayed run.
+"""
+import numpy as np
+import pytest
+import torch
+
+from gfedntm_amd.data.bow import BatchPlan, DeviceCSR
+from gfedntm_amd.models import AVITM
+from gfedntm_amd.ops import kernel_abi as abi
+from gfedntm_amd.ops.engine import STAGE_LB, UPDATE_FUSED
+from tests.helpers import random_csr
+from tests.test_fused_kernels import _oracle_step
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("model_type", ["prodLDA", "LDA"])
+@pytest.mark.parametrize("B", [256, 512])
+@pytest.mark.parametrize("K", [50, 200])
+@pytest.mark.parametrize("V", [5000, 112000])
+def test_large_batch_step_matches_oracle(model_type, B, K, V):
+    _oracle_step(model_type, B, B + 37, K, (50, 50), V)
+
+
+@pytest.mark.parametrize("model_type", ["prodLDA", "LDA"])
+def test_large_batch_partial_batch_matches_oracle(model_type):
+    """Fewer documents than bmax: rows >= nb are masked out of every column statistic and
+    product (nb = 300 of bmax = 512)."""
+    _oracle_step(model_type, 512, 300, 50, (50, 50), 7000)
+
+
+def test_large_batch_plan_and_record():
+    torch.manual_seed(0)
+    tm = AVITM(backend="fused", input_size=5000, n_components=50, hidden_sizes=(50, 50),
+               batch_size=256, verbose=False, device="cuda")
+    e = tm.engine
+    assert e.large_batch and e.bmax == 256 and e._m.stage_flags & STAGE_LB
+    assert e.update_mode != UPDATE_FUSED and e.host_gemm_fallback
+    ph = e.phases()
+    assert ph.index(abi.PH_LB_GEMM_FWD) < ph.index(abi.PH_PRODLDA_FWD)
+    assert ph.index(abi.PH_PRODLDA_BWD) < ph.index(abi.PH_LB_GEMM_BWD) < ph.index(abi.PH_POST_BWD)
+    assert tm.engine_info["engine"] == "fused" and "large-batch" in tm.engine_info["plan"]
+    with pytest.raises(ValueError):
+        e.set_update_mode(UPDATE_FUSED)
+
+
+@pytest.mark.parametrize("model_type", ["prodLDA", "LDA"])
+def test_large_batch_graph_training_tracks_torch(model_type):
+    """30 graph-replayed steps (batch prep, the host GEMMs and the kernels in one hipGraph)
+    against the PyTorch engine from the same initial weights: the loss curves agree (the
+    dropout / reparameterisation draws differ, so per-step losses are compared as a trend)
+    and the trained state stays finite."""
+    kw = dict(input_size=3000, n_components=50, hidden_sizes=(50, 50), batch_size=256,
+              model_type=model_type, verbose=False, device="cuda")
+    torch.manual_seed(1)
+    fused = AVITM(backend="fused", **kw)
+    ref = AVITM(backend="torch", **kw)
+    ref.model.load_state_dict(fused.model.state_dict())
+    X = random_csr(256 * 4, 3000, 60, seed=3)
+    losses = []
+    for tm in (fused, ref):
+        data = DeviceCSR(X, "cuda")
+        plan = BatchPlan.build(data.n_docs, 256, 30, seed=0)
+        tm.engine.bind_data(data, plan)
+        if tm is fused:
+            tm.engine.enable_graph(True)
+        for s in range(30):
+            tm.engine.step(s)
+        torch.cuda.synchronize()
+        losses.append(tm.engine.loss_hist[:30].detach().cpu().numpy())
+    lf, lr_ = losses
+    assert np.isfinite(lf).all()
+    assert torch.isfinite(fused.flat.buffer).all()
+    # both decrease, to within a few percent of each other
+    assert lf[-5:].mean() < lf[:5].mean() and lr_[-5:].mean() < lr_[:5].mean()
+    np.testing.assert_allclose(lf[-5:].mean(), lr_[-5:].mean(), rtol=0.05)

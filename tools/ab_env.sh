@@ -12,7 +12,8 @@ mkdir -p "$out"
 for i in $(seq 1 "$reps"); do
   for spec in "$@"; do
     name="${spec%%=*}"; envs="${spec#*=}"
-    ( IFS=','; for kv in $envs; do [ -n "$kv" ] && export "$kv"; done
+    ( IFS=',' read -ra kvs <<< "$envs"
+      for kv in "${kvs[@]}"; do [ -n "$kv" ] && export "$kv"; done
       timeout -k 10 300 python bench.py $args > "$out/${name}_$i.json" 2> "$out/${name}_$i.err" ) || {
         echo "variant $name failed"; tail -5 "$out/${name}_$i.err"; exit 1; }
     python - "$out/${name}_$i.json" "$name" "$i" <<'EOF'
