@@ -67,8 +67,35 @@ __host__ __device__ inline int post_weight_floats(const GfkModel& m) {
 // four of them would not fit the 160 KiB.
 __host__ __device__ inline bool batch_in_lds(const GfkModel& m) { return !(m.stage_flags & 2); }
 
+// Row stride of the LDS-staged [B][K] batch matrices: K rounded up to 2 x odd.  The column
+// reductions read 16 rows x 2 columns per half-wave (ds_read_b32, bank = dword mod 32); a
+// stride of 2 x odd puts those 16 rows on 16 distinct even bank offsets (the two columns
+// fill the odd ones) -- at K = 100 (4 mod 32) rows r and r + 8 shared a bank, half of the
+// kernels' LDS cycles were conflicts (CombinedTM K = 100: 31 %, profiles/r4; the model:
+// tools/lds_bank_model.py).  K = 50 (the headline) is already 2 x odd: unchanged.
+__host__ __device__ inline int post_lds_ld(int K) {
+  const int k2 = (K + 1) / 2 * 2;
+  return (k2 / 2) % 2 ? k2 : k2 + 2;
+}
+
+// Rows of a row-major [rows][cols] global matrix into LDS rows of stride ld (LDS-DMA, one
+// dword per lane: 64 columns of a row per wave instruction; ld == cols: one contiguous copy)
+__device__ __forceinline__ void glds_rows(float* dst, const float* src, int rows, int cols, int ld,
+                                          int tid, int nt) {
+  if (ld == cols) {
+    glds_copy(dst, src, rows * cols, tid, nt);
+    return;
+  }
+  const int lane = tid & 63, w = tid >> 6, nw = nt >> 6;
+  for (int r = w; r < rows; r += nw)
+    for (int c0 = 0; c0 < cols; c0 += 64)
+      if (c0 + lane < cols)
+        __builtin_amdgcn_global_load_lds((gbl_void_ptr)(src + (size_t)r * cols + c0 + lane),
+                                         (lds_void_ptr)(dst + r * ld + c0), 4, 0, 0);
+}
+
 extern "C" size_t gfk_post_fwd_smem(const GfkModel* m) {
-  const size_t mats = batch_in_lds(*m) ? 2 * (size_t)m->bmax * m->K : 0;
+  const size_t mats = batch_in_lds(*m) ? 2 * (size_t)m->bmax * post_lds_ld(m->K) : 0;
   return sizeof(float) * (mats + 4 * (size_t)pad4(m->K) + 2 * FT);
 }
 
@@ -144,7 +171,7 @@ template <int RPT>
 __device__ __forceinline__ void post_colstats_dpp(const GfkModel& m, const float* mr, const float* lr,
                                               float* cmean, float* crstd, const float (&rmp)[8],
                                               const float (&rvp)[8], int nb, float inv_nb, int row,
-                                              int tid) {
+                                              int tid, int ld) {
   constexpr int CP = 8;
   const int K = m.K;
 #pragma unroll
@@ -158,7 +185,7 @@ __device__ __forceinline__ void post_colstats_dpp(const GfkModel& m, const float
 #pragma unroll
     for (int i = 0; i < RPT; ++i) {
       const int r = g + 16 * i;
-      xv[i] = (valid && r < nb) ? x[r * K] : 0.f;
+      xv[i] = (valid && r < nb) ? x[r * ld] : 0.f;
     }
     float s = 0.f;
 #pragma unroll
@@ -277,17 +304,18 @@ __global__ void __launch_bounds__(FT) gfk_post_fwd_k(GfkArgT<GB> ga) {
   const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
   const int row = gfk_bx();
   constexpr bool in_lds = InLds;
+  const int LD = in_lds ? post_lds_ld(K) : K;   // row stride of mr / lr
   const float* mr = in_lds ? smem : mu_raw;
-  const float* lr = in_lds ? smem + B * K : ls_raw;
-  float* cmean = smem + (in_lds ? 2 * B * K : 0);
+  const float* lr = in_lds ? smem + B * LD : ls_raw;
+  float* cmean = smem + (in_lds ? 2 * B * LD : 0);
   float* crstd = cmean + 2 * pad4(K);
   float* red = crstd + 2 * pad4(K);        // [2][FT] column-reduction scratch
   GFK_STAMP(m, 0);
 
   // ---- one round: the raw heads of every row (LDS-DMA) + the own row + stats ----
   if (in_lds) {
-    glds_copy(smem, mu_raw, B * K, tid, FT);
-    glds_copy(smem + B * K, ls_raw, B * K, tid, FT);
+    glds_rows(smem, mu_raw, B, K, LD, tid, FT);
+    glds_rows(smem + B * LD, ls_raw, B, K, LD, tid, FT);
   }
   const int nb = *nbp;
   constexpr int KQ = 4;                    // K <= 256
@@ -356,8 +384,8 @@ __global__ void __launch_bounds__(FT) gfk_post_fwd_k(GfkArgT<GB> ga) {
   // values held in registers across the mean and variance passes ----
   const float inv_nb = 1.f / (float)nb;
   if constexpr (InLds) {
-    if (B <= 64) post_colstats_dpp<4>(m, mr, lr, cmean, crstd, rmp, rvp, nb, inv_nb, row, tid);
-    else post_colstats_dpp<8>(m, mr, lr, cmean, crstd, rmp, rvp, nb, inv_nb, row, tid);
+    if (B <= 64) post_colstats_dpp<4>(m, mr, lr, cmean, crstd, rmp, rvp, nb, inv_nb, row, tid, LD);
+    else post_colstats_dpp<8>(m, mr, lr, cmean, crstd, rmp, rvp, nb, inv_nb, row, tid, LD);
   } else {
     if (B <= 64) post_colstats<32>(m, mr, lr, cmean, crstd, red, rm0, rv0, nb, inv_nb, row, tid);
     else if (B <= 128) post_colstats<64>(m, mr, lr, cmean, crstd, red, rm0, rv0, nb, inv_nb, row, tid);
@@ -389,8 +417,8 @@ __global__ void __launch_bounds__(FT) gfk_post_fwd_k(GfkArgT<GB> ga) {
       zq[q] = -INFINITY;
       muq[q] = lsq[q] = 0.f;
       if (k < K) {
-        const float mu = (mr[row * K + k] - cmean[k]) * crstd[k];
-        const float ls = (lr[row * K + k] - cmean[K + k]) * crstd[K + k];
+        const float mu = (mr[row * LD + k] - cmean[k]) * crstd[k];
+        const float ls = (lr[row * LD + k] - cmean[K + k]) * crstd[K + k];
         const float sd = expf(0.5f * ls);
         const float z = mu + ep[q] * sd;
         muq[q] = mu;
@@ -571,7 +599,7 @@ struct PostLds {
 __host__ __device__ inline PostLds post_lds(const GfkModel& m) {
   PostLds L;
   const int B = m.bmax, K = m.K, hm = pad4(post_hmax(m));
-  const int mat = batch_in_lds(m) ? B * K : 0;
+  const int mat = batch_in_lds(m) ? B * post_lds_ld(K) : 0;
   int o = 0;
   L.dmu = o; o += mat;
   L.dls = o; o += mat;
@@ -728,12 +756,13 @@ __global__ void __launch_bounds__(FT) gfk_post_bwd_k(GfkArgT<GB> ga) {
   GFK_STAMP(m, 10);
 
   constexpr bool in_lds = InLds;
+  const int LD = in_lds ? post_lds_ld(K) : K;   // row stride of the batch matrices
   // ---- one round: the four [B][K] matrices, the own row, the weights, stats ----
   if (in_lds) {
-    glds_copy(smem + L.dmu, dmu_g, B * K, tid, FT);
-    glds_copy(smem + L.dls, dls_g, B * K, tid, FT);
-    glds_copy(smem + L.mu, mu_g, B * K, tid, FT);
-    glds_copy(smem + L.ls, ls_g, B * K, tid, FT);
+    glds_rows(smem + L.dmu, dmu_g, B, K, LD, tid, FT);
+    glds_rows(smem + L.dls, dls_g, B, K, LD, tid, FT);
+    glds_rows(smem + L.mu, mu_g, B, K, LD, tid, FT);
+    glds_rows(smem + L.ls, ls_g, B, K, LD, tid, FT);
   }
   if (!extra) {                         // own row (the extra workgroup has none)
     int o = L.zrow;
@@ -797,7 +826,7 @@ __global__ void __launch_bounds__(FT) gfk_post_bwd_k(GfkArgT<GB> ga) {
         if (valid)
 #pragma unroll 4
           for (int r = g; r < nb; r += 16) {
-            const float x = xh[r * K + k];
+            const float x = xh[r * LD + k];
             s3 += c2 < K ? x : expf(x);
             const float dm = pm - x;
             s4 += c2 < K ? dm * dm : 0.f;
@@ -841,7 +870,7 @@ __global__ void __launch_bounds__(FT) gfk_post_bwd_k(GfkArgT<GB> ga) {
       if (valid)
 #pragma unroll 4
         for (int r = g; r < nb; r += 16) {
-          const float d = dy[r * K + k], x = xh[r * K + k];
+          const float d = dy[r * LD + k], x = xh[r * LD + k];
           s1 += d;
           s2 += d * x;
         }
@@ -871,7 +900,7 @@ __global__ void __launch_bounds__(FT) gfk_post_bwd_k(GfkArgT<GB> ga) {
       const float* dy = c2 < K ? dmu : dls;
       const float* xh = c2 < K ? mu : ls;
       const float v =
-          rs[q] * (dy[row * K + k] - S[c2] * inv_nb - xh[row * K + k] * S[P2 + c2] * inv_nb);
+          rs[q] * (dy[row * LD + k] - S[c2] * inv_nb - xh[row * LD + k] * S[P2 + c2] * inv_nb);
       dr[c2] = v;
       (c2 < K ? m.ws_dmr : m.ws_dlr)[row * K + k] = v;
     }

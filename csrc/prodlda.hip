@@ -1708,6 +1708,7 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
   constexpr int MU = (NKS * 4 + NW - 1) / NW;                  // dbeta subtiles per wave
   constexpr int NDT = ((BM / 16) * NKS + NW - 1) / NW;         // d theta_d subtiles per wave
   constexpr int DU = BM * VB / 4 / NTH;                        // dlogit float4 per thread
+  constexpr bool KEEP = FUSED && MAXU <= 2;                    // (register budget: K <= 128)
   const int K = m.K, V = m.V;
   int tid = threadIdx.x;
   int lane = tid & 63, wave = uniform(tid >> 6);
@@ -1839,9 +1840,18 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
       for (int j = 0; j < DU; ++j) {           // dense [BM][64] -> dt [b][c] and dtT [c][b]
         const int i = tid + NTH * j, r = i >> 4, c4 = (i & 15) * 4;
         *reinterpret_cast<f32x4*>(dt + __mul24(r, LDP) + c4) = dr[j];
+#if GFK_DIAG_BWD != 2                          // (diagnostic builds: no transposed stores)
 #pragma unroll
         for (int e = 0; e < 4; ++e) dtT[__mul24(c4 + e, LDP) + (r ^ dtt_swz(c4 + e))] = dr[j][e];
+#endif
       }
+    }
+    // (KEEP: the beta quads stay in registers for the Adam epilogue -- read back from bt
+    // they were the kernel's one conflicting LDS read, 2-way: tools/lds_bank_model.py)
+    f32x4 bkeep[KEEP ? RQ : 1];
+    if constexpr (KEEP) {
+#pragma unroll
+      for (int u = 0; u < RQ; ++u) bkeep[u] = br[u];
     }
     // (the staging above consumed the registers) the next tile's beta / dlogit / m / v
     {
@@ -1903,7 +1913,13 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
       const f32x4 gv = *reinterpret_cast<const f32x4*>(gt + __mul24(kl, VB) + (c4 ^ ((kl & 4) << 2)));
       const int vo4 = boff(vc, rowoff[u]);
       if constexpr (FUSED) {
-        const f32x4 pv = *reinterpret_cast<const f32x4*>(bt + __mul24(kl, LDP) + c4);
+        f32x4 pv;
+        if constexpr (KEEP) pv = bkeep[u];
+#if GFK_DIAG_BWD == 3                          // (diagnostic builds: no beta read-back)
+        else pv = f32x4{0.f, 0.f, 0.f, 0.f};
+#else
+        else pv = *reinterpret_cast<const f32x4*>(bt + __mul24(kl, LDP) + c4);
+#endif
         f32x4 mo = rm[u], vo = rv[u], np;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {

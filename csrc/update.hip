@@ -60,9 +60,10 @@ extern "C" size_t gfk_win_update_smem(const GfkModel* m) {
   // the sparse tile (bit 4): dz0, the entry list, the row slots (+ the word mask and list)
   const size_t c = (size_t)B * m->H[0] + 2 * 512 + (B + 1 > 129 ? B + 1 : 129) + 128;
   if (a < c) a = c;
-  // the dense contextual tile next to them (fused CombinedTM): dz0 + the A block / G tile
-  const size_t d = (((size_t)B * m->H[0] + 3) & ~(size_t)3) +
-                   ((size_t)B * 64 > (size_t)64 * m->H[0] ? (size_t)B * 64 : (size_t)64 * m->H[0]);
+  // the dense contextual tile next to them (fused CombinedTM): dz0 + the A block / G tile,
+  // rows at the padded stride (80 floats, win_tile_ctx)
+  const size_t d = (size_t)B * 80 +
+                   ((size_t)B * 80 > (size_t)64 * m->H[0] ? (size_t)B * 80 : (size_t)64 * m->H[0]);
   if (m->input == GFK_IN_COMBINED && a < d) a = d;
   return sizeof(float) * (a > b ? a : b);
 }
@@ -472,6 +473,7 @@ __device__ __forceinline__ void win_tile_sparse(const GfkModel& m, float* smem, 
 // The gradient tile is parked in the A block's LDS (free after the products) in the
 // W block's flat order, and the epilogue moves p / m / v as flat quads prefetched before
 // the products, like the sparse tile's.  B <= 64, H0 <= 64.
+constexpr int WCS = 80;
 template <int UT>
 __device__ __forceinline__ void win_tile_ctx(const GfkModel& m, float* smem, int tile) {
   constexpr int UW = UT / 64;
@@ -479,8 +481,12 @@ __device__ __forceinline__ void win_tile_ctx(const GfkModel& m, float* smem, int
   const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
   const int B = m.bmax, H0 = m.H[0], V = m.V, c0 = tile * 64;
   const int nb = *m.ws_nb;
-  float* dz = smem;                                       // [B][H0]
-  float* at = smem + ((B * H0 + 3) & ~3);                 // [B][64], then G [64][H0]
+  // operand rows at stride WCS = 80 floats (16 mod 32): a half-wave's two rows of 16 columns
+  // land on 32 distinct ds_read_b32 banks -- at the blocks' own strides (64, H0 = 50) the two
+  // rows shared banks, half of the LDS cycles of the MFMA loop were conflicts (CombinedTM
+  // K = 100: SQ_LDS_BANK_CONFLICT 49 % of SQ_LDS_IDX_ACTIVE, profiles/r4)
+  float* dz = smem;                                       // [B][WCS]
+  float* at = smem + B * WCS;                             // [B][WCS], then G [64][H0]
   float* wblk = m.w_in + (size_t)(V + c0) * H0;
   const int nel = (min(V, c0 + 64) - c0) * H0;
   const bool fused = m.update_mode == 1;
@@ -493,9 +499,18 @@ __device__ __forceinline__ void win_tile_ctx(const GfkModel& m, float* smem, int
     for (int i = 0; i < 4; ++i) r[i] = e + i < nel ? q[e + i] : 0.f;
     return r;
   };
-  // ---- one staging round: the operand blocks (LDS-DMA), then the W block's p / m / v ----
-  glds_copy(dz, m.ws_dz[0], B * H0, tid, UT);
-  glds_copy(at, m.ws_actx + (size_t)tile * B * 64, B * 64, tid, UT);
+  // ---- one staging round: the operand blocks (LDS-DMA, one dword per lane: a row per
+  //      wave instruction, at the padded stride), then the W block's p / m / v ----
+  {
+    const float* ag = m.ws_actx + (size_t)tile * B * 64;
+    for (int r = wave; r < B; r += UW) {
+      if (lane < H0)
+        __builtin_amdgcn_global_load_lds((gbl_void_ptr)(m.ws_dz[0] + r * H0 + lane),
+                                         (lds_void_ptr)(dz + r * WCS), 4, 0, 0);
+      __builtin_amdgcn_global_load_lds((gbl_void_ptr)(ag + r * 64 + lane),
+                                       (lds_void_ptr)(at + r * WCS), 4, 0, 0);
+    }
+  }
   f32x4 pp[FQ], pm[FQ], pv[FQ];
 #pragma unroll
   for (int u = 0; u < FQ; ++u) {
@@ -509,7 +524,7 @@ __device__ __forceinline__ void win_tile_ctx(const GfkModel& m, float* smem, int
   }
   vm_barrier();
   // ---- G subtiles (v tile, h tile) = t = wave + UW u: rows b >= nb masked in the A role;
-  //      columns h >= H0 read the next row's dz (discarded outputs) ----
+  //      columns h >= H0 read the row's padding (discarded outputs) ----
   const int NT = (H0 + 15) / 16, NST = 4 * NT;
   constexpr int SU = 16 / UW;                   // subtiles per wave (H0 <= 64: <= 16 in all)
   f32x4 acc[SU];
@@ -519,11 +534,11 @@ __device__ __forceinline__ void win_tile_ctx(const GfkModel& m, float* smem, int
     acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (t >= NST) continue;
     const int i0 = (t / NT) * 16, j0 = (t % NT) * 16;
-    const float* ap = at + (lane >> 4) * 64 + i0 + (lane & 15);
-    const float* bp = dz + (lane >> 4) * H0 + j0 + (lane & 15);
+    const float* ap = at + (lane >> 4) * WCS + i0 + (lane & 15);
+    const float* bp = dz + (lane >> 4) * WCS + j0 + (lane & 15);
     for (int k = 0; k < B; k += 4) {
-      const float a = k + (lane >> 4) < nb ? ap[k * 64] : 0.f;
-      acc[u] = mfma16x16x4(a, bp[k * H0], acc[u]);
+      const float a = k + (lane >> 4) < nb ? ap[k * WCS] : 0.f;
+      acc[u] = mfma16x16x4(a, bp[k * WCS], acc[u]);
     }
   }
   lds_barrier();                                // every wave is done reading the A block

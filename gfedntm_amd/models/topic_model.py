@@ -167,7 +167,7 @@ class TopicModelBase:
     def engine_info(self) -> dict:
         """Which local-step engine runs this model, and why not the fused one if not."""
         d = {"engine": self.backend}
-        plan = getattr(getattr(self, "engine", None), "plan", None)
+        plan = getattr(getattr(self, "engine", None), "launch_plan", None)
         if isinstance(plan, str):
             d["plan"] = plan
         if self.backend_fallback_reason:

@@ -938,7 +938,7 @@ class FusedEngine(EngineBase):
         return "bf16" if m.mm_bf16 and (m.stage_flags & rs) == rs else "fp32"
 
     @property
-    def plan(self) -> str:
+    def launch_plan(self) -> str:
         """The launch plan in one phrase (recorded in bench / metrics records)."""
         if self.large_batch:
             return ("large-batch: hipBLASLt decoder GEMMs + HIP kernels, gradient mode"
