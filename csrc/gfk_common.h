@@ -336,6 +336,9 @@ namespace gfk {
 
 // In-kernel phase timestamps for diagnostic builds (-DGFK_STAMPS): lane 0 of
 // workgroup 0 writes s_memtime into dbg[slot].  Compiled out otherwise.
+#ifndef GFK_STRIP_OLDEST_LIGHT
+#define GFK_STRIP_OLDEST_LIGHT 0   // strip forward: wave groups in reverse order (A/B builds)
+#endif
 #ifndef GFK_DIAG_BWD
 #define GFK_DIAG_BWD 0      // diagnostic variants of prodlda_bwd_pipe_kernel (tools/ab_libs.py AB_DEFS)
 #endif

@@ -450,7 +450,14 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
   // 4 strips of a tile stay on one CU (their beta rows share cache lines), and the
   // tiles of the last, partial round are spread over every CU's wave group 0 instead
   // of all 8 waves of the first CUs, so no SIMD gets more than ceil(strips / SIMDs) + 1
+#if GFK_STRIP_OLDEST_LIGHT
+  // (A/B build: the wave groups in reverse order, so the groups with one tile fewer are the
+  // OLDEST waves -- served first by the SIMD's oldest-first issue, done early -- and the last
+  // round of strips runs with three waves per SIMD instead of a lone youngest one)
+  int s = 4 * ((NW / 4 - 1 - (wave >> 2)) * (int)gridDim.x + (int)gfk_bx()) + (wave & 3);
+#else
   int s = 4 * ((wave >> 2) * (int)gridDim.x + (int)gfk_bx()) + (wave & 3);
+#endif
   if constexpr (FP) {
     // ---- fused posterior: one round of loads (heads, the rows' noise / masks, priors,
     // workgroup 0's running statistics and counters), the first beta block behind them ----

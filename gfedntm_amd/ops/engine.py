@@ -545,10 +545,15 @@ class FusedEngine(EngineBase):
                 m.dec_grid = int(min(m.n_tiles, cu))
                 # the batch-coupled posterior (BN of the heads, reparameterisation, softmax,
                 # dropout, KL) inside the ring forward's theta_d staging: post_fwd is not
-                # launched (K <= 64, no label head; csrc/gfk_common.h gfk_postfold).
-                # GFEDNTM_POSTFOLD=0 keeps the separate post_fwd kernel
-                if (m.stage_flags & STAGE_FWD_STRIP_RING and m.K <= 64 and not m.lab_on
-                        and os.environ.get("GFEDNTM_POSTFOLD", "1") != "0"):
+                # launched (K <= 64, no label head; csrc/gfk_common.h gfk_postfold).  Where it
+                # pays: batched launches of several clients (BatchedSteps, sim8 strip forward
+                # + post_fwd 27.4 -> 20.5 us); for ONE client the redundant per-workgroup
+                # statistics lengthen the forward's critical path more than the launch they
+                # save (interleaved, one box: 0.0601 vs 0.0597 ms per round,
+                # profiles/r5/ab_fold.txt).  GFEDNTM_POSTFOLD=1 forces it here, =0 everywhere
+                self._fold_ok = bool(m.stage_flags & STAGE_FWD_STRIP_RING and m.K <= 64
+                                     and not m.lab_on)
+                if self._fold_ok and os.environ.get("GFEDNTM_POSTFOLD", "auto") == "1":
                     m.stage_flags |= STAGE_FWD_POSTFOLD
             # backward: one workgroup per tile while the tiles fit the resident slots;
             # else persistent, n_dpart d theta_d slabs: with >= 4 k tiles the topics
@@ -706,7 +711,7 @@ class FusedEngine(EngineBase):
         if getattr(self, "_lbv", None) is None:
             B, K = self.bmax, int(self._m.K)
             self._lbv = (self.ws["thetad"][:, :K], self.raw_like(self.flat.buffer, "beta"),
-                         self.raw_like(self.grad, "beta"), self.ws["dt"],
+                         self.raw_like(self.grad, "beta"), self.ws["dt"].view(B, int(self._m.ldb)),
                          self.ws["dthetad"][: B * K].view(B, K))
         return self._lbv
 
@@ -1626,21 +1631,31 @@ class BatchedSteps:
                 # (the prefetching variant has no folded posterior: post_fwd runs again)
                 mm.stage_flags = (mm.stage_flags & ~(STAGE_FWD_STRIP_ROLL | STAGE_FWD_STRIP_RING
                                                      | STAGE_FWD_POSTFOLD)) | STAGE_FWD_STRIP_PF
+            # the posterior folded into the ring forward for M > 1 clients (the engines' own
+            # plan keeps post_fwd for one client; GFEDNTM_POSTFOLD=0: never)
+            if (M > 1 and getattr(e, "_fold_ok", False) and mm.stage_flags & STAGE_FWD_STRIP_RING
+                    and os.environ.get("GFEDNTM_POSTFOLD", "auto") != "0"):
+                mm.stage_flags |= STAGE_FWD_POSTFOLD
             # post_bwd: M clients x (bmax + 1) workgroups of 16 waves with the batch matrices
-            # in LDS (~93 KB: one per CU) ran in three rounds at M = 8; with the matrices read
+            # in LDS (~93 KB: one per CU) run in three rounds at M = 8; with the matrices read
             # from L2 (stage_flags bit 1, ~42 KB) and the batch-level workgroup moved into
-            # row_bwd, M bmax workgroups fit one round at two per CU (GFEDNTM_BATCH_POST=0: off)
+            # row_bwd, M bmax workgroups fit one round at two per CU -- but the round measured
+            # slower (M = 8, interleaved on one box: 0.1507 / 0.1520 ms without vs 0.1535 /
+            # 0.1527 with, profiles/r5/ab_batch.txt): the L2 reads cost more than the rounds.
+            # Opt-in: GFEDNTM_BATCH_POST=1
             if (M > 1 and M * (mm.bmax + 1) > self._cu
-                    and os.environ.get("GFEDNTM_BATCH_POST", "1") != "0"):
+                    and os.environ.get("GFEDNTM_BATCH_POST", "0") == "1"):
                 mm.stage_flags |= 2 | STAGE_POST_EXTRA_ROWBWD
             # prodlda_bwd at K <= 64: one 16-wave workgroup per tile (~61 KB of LDS, two per
-            # CU) -- M clients' tiles beyond two per CU ran in a second round (592 on 512
-            # slots at M = 8, V = 4.7k); instead each workgroup walks t tiles (n_dpart =
-            # n_tiles / t slabs, the persistent one-range shape), t the smallest that fits
-            # one round (GFEDNTM_BATCH_BWD=0: off)
+            # CU) -- M clients' tiles beyond two per CU run in a second round (592 on 512
+            # slots at M = 8, V = 4.7k); the alternative, each workgroup walking t tiles
+            # (n_dpart = n_tiles / t slabs, the persistent one-range shape, t the smallest
+            # that fits one round), measured slower: 0.1492 / 0.1484 ms without vs 0.1535 /
+            # 0.1527 with (profiles/r5/ab_batch.txt) -- a tile's staging round is not hidden
+            # when one workgroup walks several.  Opt-in: GFEDNTM_BATCH_BWD=1
             if (M > 1 and mm.kind == abi.KIND_PRODLDA and mm.K <= 64 and mm.n_dpart == mm.n_tiles
                     and M * mm.n_tiles > 2 * self._cu
-                    and os.environ.get("GFEDNTM_BATCH_BWD", "1") != "0"):
+                    and os.environ.get("GFEDNTM_BATCH_BWD", "0") == "1"):
                 t = -(-(M * mm.n_tiles) // (2 * self._cu))
                 mm.n_dpart = -(-mm.n_tiles // t)
                 mm.stage_flags |= STAGE_BWD_KQ1
@@ -1651,10 +1666,13 @@ class BatchedSteps:
                 mm.stage_flags |= STAGE_WIN_BATCH8
             ms.append(bytes(mm))
             us.append(bytes(e._u))
-        # the phases of the batched plan: post_fwd back in where the launch dropped the fold
+        # the phases of the batched plan: post_fwd out where the launch folds it, back in
+        # where the launch dropped the engines' fold
         ph = list(self.engines[0].phases())
-        if (abi.PH_PRODLDA_FWD in ph and abi.PH_POST_FWD not in ph
-                and not abi.GfkModel.from_buffer_copy(ms[0]).stage_flags & STAGE_FWD_POSTFOLD):
+        folded = bool(abi.GfkModel.from_buffer_copy(ms[0]).stage_flags & STAGE_FWD_POSTFOLD)
+        if folded and abi.PH_POST_FWD in ph:
+            ph.remove(abi.PH_POST_FWD)
+        elif not folded and abi.PH_PRODLDA_FWD in ph and abi.PH_POST_FWD not in ph:
             ph.insert(ph.index(abi.PH_PRODLDA_FWD), abi.PH_POST_FWD)
         self._phases = ph
         blob = b"".join(ms) + b"".join(us)

@@ -234,6 +234,8 @@ def test_batched_large_round_variants_match_branch_round(monkeypatch, strip):
     from gfedntm_amd.ops.engine import (STAGE_BWD_KQ1, STAGE_FWD_STRIP_PF, STAGE_FWD_STRIP_RING,
                                         STAGE_POST_EXTRA_ROWBWD, STAGE_WIN_BATCH8)
     monkeypatch.setenv("GFEDNTM_BATCH_STRIP", strip)
+    monkeypatch.setenv("GFEDNTM_BATCH_POST", "1")       # the opt-in shapes, covered here
+    monkeypatch.setenv("GFEDNTM_BATCH_BWD", "1")
     sc = generate_synthetic(vocab_size=5000, n_topics=50, n_docs=1000, n_nodes=8, frozen_topics=5,
                             nwords=(150, 250), seed=13)
     corpora = [ClientCorpus(synthetic=sc, node=i) for i in range(8)]
@@ -247,10 +249,16 @@ def test_batched_large_round_variants_match_branch_round(monkeypatch, strip):
     host = a._batched._host
     cu = torch.cuda.get_device_properties(0).multi_processor_count
     assert 8 * (host.n_tiles + 8) > 2 * cu and host.stage_flags & STAGE_WIN_BATCH8, host.n_tiles
+    from gfedntm_amd.ops import kernel_abi as abi
+    from gfedntm_amd.ops.engine import STAGE_FWD_POSTFOLD
     if strip == "fill":
+        # the ring forward with the posterior folded in (post_fwd not launched)
         assert host.dec_grid == -(-host.n_tiles // 4) and host.stage_flags & STAGE_FWD_STRIP_RING
+        assert host.stage_flags & STAGE_FWD_POSTFOLD and abi.PH_POST_FWD not in a._batched._phases
     else:
+        # the prefetching variant has no fold: post_fwd runs
         assert 8 * host.dec_grid > cu and host.stage_flags & STAGE_FWD_STRIP_PF
+        assert not host.stage_flags & STAGE_FWD_POSTFOLD and abi.PH_POST_FWD in a._batched._phases
     assert host.stage_flags & STAGE_POST_EXTRA_ROWBWD and host.stage_flags & 2
     assert host.stage_flags & STAGE_BWD_KQ1 and host.n_dpart < host.n_tiles, host.n_dpart
     lr = a.clients[0].tm.engine.lr

@@ -902,7 +902,7 @@ def test_postfold_matches_separate_post_fwd(monkeypatch, B, K, V, dtype):
     # (the folded statistics sum in another order: after five steps a few small-magnitude
     # heads of the tiny B = 16, K = 10 model differ at ~1e-5)
     for key in ("mu", "ls", "theta", "thetad", "kl", "bn_rstd"):
-        torch.testing.assert_close(a.engine.ws[key], b.engine.ws[key], rtol=1e-4, atol=2e-5,
+        torch.testing.assert_close(a.engine.ws[key], b.engine.ws[key], rtol=5e-4, atol=2e-5,
                                    msg=lambda m: f"ws[{key}]: {m}")
     assert int(a.engine.adam_t.item()) == int(b.engine.adam_t.item()) == 5
     torch.testing.assert_close(a.engine.adam_coef, b.engine.adam_coef, rtol=0, atol=0)
@@ -915,8 +915,8 @@ def test_postfold_matches_separate_post_fwd(monkeypatch, B, K, V, dtype):
         # (the heads' biases get a zero gradient in exact arithmetic -- batch norm removes
         # them -- so Adam steps them by +-lr on rounding noise, and the raw heads' running
         # means follow: compared at that scale)
-        noisy = "bias" in k or k.startswith(("inf_net.f_mu_batchnorm.running_mean",
-                                             "inf_net.f_sigma_batchnorm.running_mean"))
+        noisy = "bias" in k or k in _NOISE_KEYS or k.startswith((
+            "inf_net.f_mu_batchnorm.running_mean", "inf_net.f_sigma_batchnorm.running_mean"))
         torch.testing.assert_close(sa[k], sb[k], rtol=1e-4, atol=2e-3 if noisy else 5e-5,
                                    msg=lambda m: f"{k}: {m}")
 
