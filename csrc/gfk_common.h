@@ -184,6 +184,10 @@ typedef struct GfkModel {
   // stream while the decoder runs, and the sparse W_in tiles update only the batch's words
   int32_t* ws_wstamp;
   int32_t* ws_wgen;
+  // ---- the large-batch plan (stage_flags GFK_LB): the posterior's column statistics,
+  // computed once per step (csrc/posterior.hip gfk_post_colstats_lb_k): [mean | rstd] of the
+  // raw heads, [sum dy | sum dy xhat] of the backward, the priors' sums, 2K floats each ----
+  float* ws_colstat;
 } GfkModel;
 
 constexpr int GFK_WIN_SPLIT = 128;

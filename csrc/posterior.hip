@@ -293,7 +293,9 @@ __device__ __forceinline__ void post_label_head(const GfkModel& m, float* buf, i
 // read from L2) + mean[2K] + rstd[2K]
 // InLds: the batch matrices are staged in LDS (compile-time, so every access is a
 // ds_read; a runtime select of the pointer would turn them into flat loads).
-template <bool InLds, bool GB = false>
+// PS (the large-batch plan): the column statistics come precomputed from ws_colstat
+// (gfk_post_colstats_lb_k), which also did row 0's running-statistic / counter duties
+template <bool InLds, bool GB = false, bool PS = false>
 __global__ void __launch_bounds__(FT) gfk_post_fwd_k(GfkArgT<GB> ga) {
   const GfkModel& m = gfk_model(ga);
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -383,15 +385,19 @@ __global__ void __launch_bounds__(FT) gfk_post_fwd_k(GfkArgT<GB> ga) {
   // ---- column statistics over the batch: 4 threads per column, the column's
   // values held in registers across the mean and variance passes ----
   const float inv_nb = 1.f / (float)nb;
-  if constexpr (InLds) {
+  if constexpr (PS) {
+    for (int c = tid; c < 2 * K; c += FT) {
+      cmean[c] = m.ws_colstat[c];
+      crstd[c] = m.ws_colstat[2 * K + c];
+    }
+  } else if constexpr (InLds) {
     if (B <= 64) post_colstats_dpp<4>(m, mr, lr, cmean, crstd, rmp, rvp, nb, inv_nb, row, tid, LD);
     else post_colstats_dpp<8>(m, mr, lr, cmean, crstd, rmp, rvp, nb, inv_nb, row, tid, LD);
   } else {
     if (B <= 64) post_colstats<32>(m, mr, lr, cmean, crstd, red, rm0, rv0, nb, inv_nb, row, tid);
-    else if (B <= 128) post_colstats<64>(m, mr, lr, cmean, crstd, red, rm0, rv0, nb, inv_nb, row, tid);
-    else post_colstats<GFK_BMAX_LIMIT / 2>(m, mr, lr, cmean, crstd, red, rm0, rv0, nb, inv_nb, row, tid);
+    else post_colstats<64>(m, mr, lr, cmean, crstd, red, rm0, rv0, nb, inv_nb, row, tid);
   }
-  if (row == 0 && tid == 0) {
+  if (!PS && row == 0 && tid == 0) {
     *m.nbt_mu = nbt0 + 1;
     *m.nbt_s = nbt1 + 1;
     // the optimizer step of this minibatch: t and the bias corrections
@@ -739,7 +745,8 @@ __device__ __forceinline__ void post_prior_sums(int K, int nb, const float* mu, 
 // grid: bmax + 1 workgroups: row = gfk_bx() < bmax, plus one extra workgroup
 // (the last) for the batch-level work -- prior gradients, the loss, the step
 // counter -- so no row workgroup carries it on the critical path.
-template <bool InLds, bool Staged, bool GB = false>
+// PS (the large-batch plan): the column sums come precomputed from ws_colstat
+template <bool InLds, bool Staged, bool GB = false, bool PS = false>
 __global__ void __launch_bounds__(FT) gfk_post_bwd_k(GfkArgT<GB> ga) {
   const GfkModel& m = gfk_model(ga);
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -838,10 +845,14 @@ __global__ void __launch_bounds__(FT) gfk_post_bwd_k(GfkArgT<GB> ga) {
           S[3 * P2 + c2] = s4;
         }
       }
+    } else if constexpr (PS) {          // precomputed (gfk_post_colstats_lb_k)
+      for (int c = tid; c < 2 * K; c += FT) {
+        S[2 * P2 + c] = m.ws_colstat[8 * K + c];
+        S[3 * P2 + c] = m.ws_colstat[10 * K + c];
+      }
     } else {                            // L2: lane-per-column (coalesced)
       if (B <= 64) post_prior_sums<32>(K, nb, mu, ls, pmean, S + 2 * P2, S + 3 * P2, smem + L.red2, tid);
-      else if (B <= 128) post_prior_sums<64>(K, nb, mu, ls, pmean, S + 2 * P2, S + 3 * P2, smem + L.red2, tid);
-      else post_prior_sums<GFK_BMAX_LIMIT / 2>(K, nb, mu, ls, pmean, S + 2 * P2, S + 3 * P2, smem + L.red2, tid);
+      else post_prior_sums<64>(K, nb, mu, ls, pmean, S + 2 * P2, S + 3 * P2, smem + L.red2, tid);
     }
     lds_barrier();
     const float wk = m.kl_weight;
@@ -881,10 +892,14 @@ __global__ void __launch_bounds__(FT) gfk_post_bwd_k(GfkArgT<GB> ga) {
         S[P2 + c2] = s2;
       }
     }
+  } else if constexpr (PS) {            // precomputed (gfk_post_colstats_lb_k)
+    for (int c = tid; c < 2 * K; c += FT) {
+      S[c] = m.ws_colstat[4 * K + c];
+      S[P2 + c] = m.ws_colstat[6 * K + c];
+    }
   } else {                              // L2: lane-per-column (coalesced)
     if (B <= 64) post_bn_sums<32>(K, nb, dmu, dls, mu, ls, S, S + P2, smem + L.red2, tid);
-    else if (B <= 128) post_bn_sums<64>(K, nb, dmu, dls, mu, ls, S, S + P2, smem + L.red2, tid);
-    else post_bn_sums<GFK_BMAX_LIMIT / 2>(K, nb, dmu, dls, mu, ls, S, S + P2, smem + L.red2, tid);
+    else post_bn_sums<64>(K, nb, dmu, dls, mu, ls, S, S + P2, smem + L.red2, tid);
   }
   lds_barrier();
   GFK_STAMP(m, 12);
@@ -979,7 +994,139 @@ __global__ void gfk_batch_docs(GfkArgT<GB> ga) {
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
+// ---------------------------------------------------------------------------
+// Large batches (stage_flags GFK_LB): the column statistics of the [B][2K] batch matrices,
+// computed ONCE per step by ceil(2K / 64) workgroups -- the row workgroups' own recomputation
+// (one round trip, no grid sync: the right trade at B <= 128) reads the whole matrices per
+// row, B^2 K floats from L2 per kernel (post_fwd 36 us, post_bwd 62 us at B = 256, K = 50:
+// profiles/r5/lb256_k50_kernels.md).  Lane = column c2 = 64 blockIdx + lane of the 2K
+// (mu | log sigma^2) columns, wave w = rows w + 16 i (coalesced 256-B row segments), the 16
+// waves' partials met in LDS.  BWD = false: mean / rstd of the raw heads (two-pass variance,
+// as torch's batch norm) -> ws_colstat[0, 2K) / [2K, 4K) and ws_bn_rstd, the running
+// statistics, and (workgroup 0) the counters and the optimizer step -- post_fwd's row-0
+// duties.  BWD = true: S1 = sum_b dy, S2 = sum_b dy xhat -> ws_colstat[4K, 6K) / [6K, 8K), and
+// the prior gradients' sums -> [8K, 10K) / [10K, 12K) (post_bwd's batch-level workgroup:
+// alone over all rows it was the kernel's tail, 39 us at B = 256).
+template <bool BWD>
+__global__ void __launch_bounds__(FT) gfk_post_colstats_lb_k(GfkArgT<false> ga) {
+  const GfkModel& m = ga.m;
+  __shared__ float red[2][16][64];
+  const int K = m.K, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int c2 = 64 * (int)blockIdx.x + lane, cc = min(c2, 2 * K - 1);
+  const int k = cc < K ? cc : cc - K;
+  const int nb = *m.ws_nb;
+  const float inv_nb = 1.f / (float)nb;
+  float* cs = m.ws_colstat;
+  if constexpr (!BWD) {
+    const float* x = (cc < K ? m.ws_mu_raw : m.ws_ls_raw) + k;
+    float rm0 = 0.f, rv0 = 0.f;
+    if (w == 0) {
+      rm0 = cc < K ? m.mu_rm[k] : m.s_rm[k];
+      rv0 = cc < K ? m.mu_rv[k] : m.s_rv[k];
+    }
+    float sm = 0.f;
+#pragma unroll 4
+    for (int r = w; r < nb; r += 16) sm += x[r * K];
+    red[0][w][lane] = sm;
+    __syncthreads();
+    float mean = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) mean += red[0][j][lane];
+    mean *= inv_nb;
+    float q = 0.f;
+#pragma unroll 4
+    for (int r = w; r < nb; r += 16) {
+      const float d = x[r * K] - mean;
+      q += d * d;
+    }
+    red[1][w][lane] = q;
+    __syncthreads();
+    float var = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) var += red[1][j][lane];
+    var *= inv_nb;
+    const float rstd = rsqrtf(var + m.bn_eps);
+    if (w == 0 && c2 < 2 * K) {
+      cs[c2] = mean;
+      cs[2 * K + c2] = rstd;
+      m.ws_bn_rstd[c2] = rstd;
+      float* rm = c2 < K ? m.mu_rm + k : m.s_rm + k;
+      float* rv = c2 < K ? m.mu_rv + k : m.s_rv + k;
+      const float mom = m.bn_momentum;
+      const float unb = nb > 1 ? var * (float)nb / (float)(nb - 1) : var;
+      float nm = (1.f - mom) * rm0 + mom * mean, nv = (1.f - mom) * rv0 + mom * unb;
+      if (m.fed_scale_on && is_shared(m, rm)) { nm *= m.fed_scale; nv *= m.fed_scale; }
+      *rm = nm;
+      *rv = nv;
+    }
+    if (blockIdx.x == 0 && tid == 0) {
+      const double pw0 = m.adam_pow[0], pw1 = m.adam_pow[1];
+      *m.nbt_mu += 1;
+      *m.nbt_s += 1;
+      *m.adam_t += 1;
+      double p1, p2;
+      float c0, c1;
+      adam_advance(m, pw0, pw1, p1, p2, c0, c1);
+      m.adam_pow[0] = p1;
+      m.adam_pow[1] = p2;
+      m.adam_coef[0] = c0;
+      m.adam_coef[1] = c1;
+    }
+  } else {
+    // + the prior gradients' sums (post_bwd's batch-level workgroup): S3 = sum_b mu
+    // (c2 < K) | sum_b exp(ls) (c2 >= K), S4 = sum_b (prior_mean - mu)^2 (c2 < K)
+    const float* dy = (cc < K ? m.ws_dmu : m.ws_dls) + k;
+    const float* xh = (cc < K ? m.ws_mu : m.ws_ls) + k;
+    const float pm = m.prior_mean[k];
+    float s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f;
+#pragma unroll 4
+    for (int r = w; r < nb; r += 16) {
+      const float d = dy[r * K], x = xh[r * K];
+      s1 += d;
+      s2 += d * x;
+      s3 += cc < K ? x : expf(x);
+      const float dm = pm - x;
+      s4 += cc < K ? dm * dm : 0.f;
+    }
+    __shared__ float red2[2][16][64];
+    red[0][w][lane] = s1;
+    red[1][w][lane] = s2;
+    red2[0][w][lane] = s3;
+    red2[1][w][lane] = s4;
+    __syncthreads();
+    if (w == 0 && c2 < 2 * K) {
+      float a1 = 0.f, a2 = 0.f, a3 = 0.f, a4 = 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        a1 += red[0][j][lane];
+        a2 += red[1][j][lane];
+        a3 += red2[0][j][lane];
+        a4 += red2[1][j][lane];
+      }
+      cs[4 * K + c2] = a1;
+      cs[6 * K + c2] = a2;
+      cs[8 * K + c2] = a3;
+      cs[10 * K + c2] = a4;
+    }
+  }
+}
+
+static int launch_colstats_lb(const GfkModel* m, hipStream_t s, bool bwd) {
+  if (m->n_batch > 1 || !m->ws_colstat) return -1;
+  const dim3 g((2 * m->K + 63) / 64);
+  if (bwd) hipLaunchKernelGGL((gfk_post_colstats_lb_k<true>), g, dim3(FT), 0, s, GfkArgT<false>{*m});
+  else hipLaunchKernelGGL((gfk_post_colstats_lb_k<false>), g, dim3(FT), 0, s, GfkArgT<false>{*m});
+  return (int)hipGetLastError();
+}
+
 extern "C" int gfk_launch_post_fwd(const GfkModel* m, hipStream_t s) {
+  if (m->stage_flags & GFK_LB) {        // large batches: statistics once, then the rows
+    if (batch_in_lds(*m)) return -1;
+    const int e = launch_colstats_lb(m, s, false);
+    if (e) return e;
+    hipLaunchKernelGGL((gfk_post_fwd_k<false, false, true>), dim3(m->bmax), dim3(FT), gfk_post_fwd_smem(m), s, GfkArgT<false>{*m});
+    return (int)hipGetLastError();
+  }
   if (batch_in_lds(*m))
     do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_post_fwd_k<true, true>), gfk_grid(dim3(m->bmax), m), dim3(FT), gfk_post_fwd_smem(m), s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_post_fwd_k<true, false>), dim3(m->bmax), dim3(FT), gfk_post_fwd_smem(m), s, GfkArgT<false>{*m}); } while (0);
   else
@@ -1001,6 +1148,14 @@ extern "C" int gfk_launch_post_bwd(const GfkModel* m, hipStream_t s) {
   const dim3 gb(m->bmax + (moved ? 0 : 1)), tb(FT);   // + the prior / loss / step workgroup
   const size_t sb = gfk_post_bwd_smem(m);
   const bool st = m->stage_flags & 1;
+  if (m->stage_flags & GFK_LB) {        // large batches: the column sums once, then the rows
+    if (batch_in_lds(*m)) return -1;
+    const int e2 = launch_colstats_lb(m, s, true);
+    if (e2) return e2;
+    if (st) hipLaunchKernelGGL((gfk_post_bwd_k<false, true, false, true>), gb, tb, sb, s, GfkArgT<false>{*m});
+    else hipLaunchKernelGGL((gfk_post_bwd_k<false, false, false, true>), gb, tb, sb, s, GfkArgT<false>{*m});
+    return (int)hipGetLastError();
+  }
   if (batch_in_lds(*m)) {
     if (st) do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_post_bwd_k<true, true, true>), gfk_grid(gb, m), tb, sb, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_post_bwd_k<true, true, false>), gb, tb, sb, s, GfkArgT<false>{*m}); } while (0);
     else do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_post_bwd_k<true, false, true>), gfk_grid(gb, m), tb, sb, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_post_bwd_k<true, false, false>), gb, tb, sb, s, GfkArgT<false>{*m}); } while (0);
@@ -1031,7 +1186,9 @@ extern "C" int gfk_post_set_smem(size_t bytes) {
                       (const void*)gfk_row_bwd_k<1>, (const void*)gfk_row_bwd_k<1, true>, (const void*)gfk_row_bwd_k<2>, (const void*)gfk_row_bwd_k<2, true>,
                       (const void*)gfk_row_bwd_k<3>, (const void*)gfk_row_bwd_k<3, true>, (const void*)gfk_row_bwd_k<4>, (const void*)gfk_row_bwd_k<4, true>,
                       (const void*)gfk_post_bwd_k<true, true>, (const void*)gfk_post_bwd_k<true, true, true>, (const void*)gfk_post_bwd_k<true, false>, (const void*)gfk_post_bwd_k<true, false, true>,
-                      (const void*)gfk_post_bwd_k<false, true>, (const void*)gfk_post_bwd_k<false, true, true>, (const void*)gfk_post_bwd_k<false, false>, (const void*)gfk_post_bwd_k<false, false, true>};
+                      (const void*)gfk_post_bwd_k<false, true>, (const void*)gfk_post_bwd_k<false, true, true>, (const void*)gfk_post_bwd_k<false, false>, (const void*)gfk_post_bwd_k<false, false, true>,
+                      (const void*)gfk_post_fwd_k<false, false, true>, (const void*)gfk_post_bwd_k<false, true, false, true>,
+                      (const void*)gfk_post_bwd_k<false, false, false, true>};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return (int)e;

@@ -1000,14 +1000,16 @@ __global__ void __launch_bounds__(LB_THREADS) prodlda_lb_colbn_kernel(GfkArgT<GB
 template <int BM, bool GB = false>
 __global__ void __launch_bounds__(LB_THREADS) prodlda_lb_dlogit_kernel(GfkArgT<GB> ga) {
   const GfkModel& m = gfk_model(ga);
-  constexpr int NR = BM / 16;
+  constexpr int NR = BM / 16, RB = 8;        // rows per thread; rows per load block
   __shared__ float red[2][16][VB];
+  __shared__ float sx[16][VB];               // per wave: the current row's sparse x by column
   const int tid = threadIdx.x, lane = tid & 63, w = uniform(tid >> 6);
   const int V = m.V, ldb = m.ldb, nb = *m.ws_nb, ntp = m.n_tiles + 1;
   const float inv_nb = 1.f / (float)nb;
   const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
       (void*)m.ws_dt, 0, (int)((size_t)m.bmax * ldb * 4), 0x00020000);
   const int zc = (lane ^ zswz(w)) * 4;       // (zswz(w + 16 i) == zswz(w))
+  sx[w][lane] = 0.f;
 #pragma unroll 1
   for (int tile = gfk_bx(); tile < m.n_tiles; tile += gridDim.x) {
     const int c0 = tile * VB, v = c0 + lane;
@@ -1015,23 +1017,47 @@ __global__ void __launch_bounds__(LB_THREADS) prodlda_lb_dlogit_kernel(GfkArgT<G
     const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(m.ws_zn + (size_t)tile * BM * VB), 0, BM * VB * 4, 0x00020000);
     const float rsd = m.ws_col_rstd[min(v, V - 1)];
+    // the tile extents of this wave's rows in one round: lane i holds row w + 16 i's
+    int ex0 = 0, ex1 = 0;
+    if (lane < NR && w + 16 * lane < nb) {
+      const int32_t* ts = m.ws_tstart + (size_t)(w + 16 * lane) * ntp + tile;
+      ex0 = ts[0];
+      ex1 = ts[1];
+    }
     float z[NR], d[NR], s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      const int r = w + 16 * i;
-      z[i] = d[i] = 0.f;
-      if (r < nb) {                   // (wave-uniform)
-        z[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rz, zc, r * VB * 4, 0));
-        const float p = __expf(z[i] - m.ws_lse[r]);
-        float dd = p * m.ws_s[r];
-        const int e0 = m.ws_tstart[(size_t)r * ntp + tile], e1 = m.ws_tstart[(size_t)r * ntp + tile + 1];
-        for (int e = e0; e < e1; ++e) {   // the row's non-zeros in this tile (few)
-          const float xv = m.values[e];
-          if (m.indices[e] - c0 == lane) dd += -xv * p / (p + RL_EPS);
+    for (int i0 = 0; i0 < NR; i0 += RB) {
+      // the block's non-zeros (lane j: the row's j-th entry in this tile), z, lse, S: one round
+      int ci[RB];
+      float xi[RB];
+#pragma unroll
+      for (int i = 0; i < RB; ++i) {
+        const int e0 = __builtin_amdgcn_readlane(ex0, i0 + i), n = __builtin_amdgcn_readlane(ex1, i0 + i) - e0;
+        ci[i] = -1;
+        xi[i] = 0.f;
+        if (lane < n) {
+          ci[i] = m.indices[e0 + lane] - c0;
+          xi[i] = m.values[e0 + lane];
         }
-        d[i] = valid ? dd : 0.f;
-        s1 += d[i];
-        s2 += d[i] * z[i];
+        z[i0 + i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rz, zc, (w + 16 * (i0 + i)) * VB * 4, 0));
+      }
+#pragma unroll
+      for (int i = 0; i < RB; ++i) {
+        const int r = w + 16 * (i0 + i);
+        d[i0 + i] = 0.f;
+        if (r < nb) {                        // (wave-uniform)
+          const float p = __expf(z[i0 + i] - m.ws_lse[r]);
+          // the row's sparse x to the lanes that own their columns (LDS, in wave order)
+          if (ci[i] >= 0) sx[w][ci[i]] = xi[i];
+          const float xs = sx[w][lane];
+          sx[w][lane] = 0.f;
+          const float dd = p * m.ws_s[r] - xs * p / (p + RL_EPS);
+          d[i0 + i] = valid ? dd : 0.f;
+          s1 += d[i0 + i];
+          s2 += d[i0 + i] * z[i0 + i];
+        } else {
+          z[i0 + i] = 0.f;
+        }
       }
     }
     red[0][w][lane] = s1;

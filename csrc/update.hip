@@ -54,7 +54,9 @@ extern "C" size_t gfk_win_update_smem(const GfkModel* m) {
   const int B = m->bmax, H0P = rup(m->H[0], 16);
   // (the dense x^T tile path does not run at bmax > 128: the large-batch plan always takes
   // the sparse tiles)
-  size_t a = B > 128 ? 0 : (size_t)64 * stride_a(B) + (size_t)B * stride_b(H0P);
+  // (bmax > 128: the chunked dense tile, 128 rows at a time, win_tile_dense_ch)
+  const int BR = B > WJ_ROWS ? WJ_ROWS : B;
+  size_t a = (size_t)64 * stride_a(BR) + (size_t)BR * stride_b(H0P);
   const size_t b = 2 * (size_t)(B < WJ_ROWS ? B : WJ_ROWS) * 80;
   if (a < 64 * 64) a = 64 * 64;      // the flat epilogue's gradient tile [64, H0 <= 64]
   // the sparse tile (bit 4): dz0, the entry list, the row slots (+ the word mask and list)
@@ -1237,6 +1239,99 @@ __global__ void __launch_bounds__(UT, UT == 512 ? 8 : 1) gfk_win_update_k(GfkArg
   GFK_STAMP(m, 42);
 }
 
+// The large-batch plan's dense W_in tile (bmax > 128, gradient mode, H0 <= 64): the W_in
+// tile body above with the batch taken in chunks of 128 rows -- per chunk the x^T tile
+// [64][130] is rebuilt from the chunk rows' tile extents and dz0's chunk [128][ZS] staged,
+// the MFMA accumulators carrying over (the small vocabularies' dense tiles: at V = 4.5k
+// a 64-word tile holds ~700 of a 256-row batch's non-zeros, which the entry-list walk of the
+// sparse tile serialises).  LDS: 64 x 130 + 128 x stride_b(H0) floats.
+template <int UT>
+__device__ __forceinline__ void win_tile_dense_ch(const GfkModel& m, float* smem, int tile) {
+  constexpr int UW = UT / 64, RC = WJ_ROWS;
+  constexpr int PU = 16 / UW;                  // subtiles per wave (H0 <= 64: 16 in all)
+  constexpr int XR = RC / (UT / 16);           // row slots per thread per chunk
+  const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
+  const int B = m.bmax, H0 = m.H[0], V = m.V, n_tiles = m.n_tiles, c0 = tile * 64;
+  const int nb = *m.ws_nb;
+  const int H0P = rup(H0, 16), NT = H0P / 16, MT = 4;
+  const int XS = stride_a(RC), ZS = stride_b(H0P);
+  float* xt = smem;
+  float* dz = smem + 64 * XS;
+  const float* dz0 = m.ws_dz[0];
+  const int row = tid >> 4, sub = tid & 15;
+  f32x4 g[PU];
+#pragma unroll
+  for (int u = 0; u < PU; ++u) g[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int b0 = 0; b0 < B; b0 += RC) {
+    if (b0) __syncthreads();                   // the previous chunk's operand reads are done
+    {
+      const int c = tid & 63;
+      if (c < H0P)
+        for (int r = tid >> 6; r < RC; r += UT / 64)
+          dz[r * ZS + c] = (c < H0 && b0 + r < nb) ? dz0[(size_t)(b0 + r) * H0 + c] : 0.f;
+    }
+    for (int i = tid; i < 64 * XS; i += UT) xt[i] = 0.f;
+    int xe0[XR], xe1[XR];
+#pragma unroll
+    for (int i = 0; i < XR; ++i) {
+      const int r = b0 + row + i * (UT / 16);
+      xe0[i] = xe1[i] = 0;
+      if (r < nb) {
+        const int32_t* ts = m.ws_tstart + (size_t)r * (n_tiles + 1) + tile;
+        xe0[i] = ts[0];
+        xe1[i] = ts[1];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < XR; ++i) {
+      const int rl = row + i * (UT / 16);
+      for (int e = xe0[i] + sub; e < xe1[i]; e += 16) xt[(m.indices[e] - c0) * XS + rl] = m.values[e];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < PU; ++u) {
+      const int t = wave + UW * u;
+      if (t >= MT * NT) break;
+      const int i0 = (t / NT) * 16, j0 = (t % NT) * 16;
+      const float* ap = xt + (i0 + (lane & 15)) * XS + (lane >> 4);
+      const float* bp = dz + (lane >> 4) * ZS + j0 + (lane & 15);
+      f32x4 c0v = {0.f, 0.f, 0.f, 0.f}, c1v = {0.f, 0.f, 0.f, 0.f};
+      for (int k = 0; k < RC; k += 8) {
+        c0v = mfma16x16x4(ap[k], bp[k * ZS], c0v);
+        c1v = mfma16x16x4(ap[k + 4], bp[(k + 4) * ZS], c1v);
+      }
+      g[u] += c0v + c1v;
+    }
+  }
+  float* w_in = m.w_in;
+#pragma unroll
+  for (int u = 0; u < PU; ++u) {
+    const int t = wave + UW * u;
+    if (t >= MT * NT) break;
+    const int i0 = (t / NT) * 16, j = (t % NT) * 16 + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int v = c0 + i0 + (lane >> 4) * 4 + r;
+      if (v < V && j < H0) w_in[(size_t)v * H0 + j + m.off_g] = g[u][r];
+    }
+  }
+}
+
+// the large-batch plan's update kernel with dense W_in tiles: job workgroups first, then the
+// n_tiles chunked tiles
+template <int UT>
+__global__ void __launch_bounds__(UT) gfk_win_lb_k(GfkArgT<false> ga, GfkUArgT<false> gua) {
+  const GfkModel& m = ga.m;
+  const GfkUpdate& U = gua.u;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int r = (int)blockIdx.x;
+  if (r < U.n_w) { weight_job_lb<UT>(m, U.w[r], smem); return; }
+  if (r < U.n_w + U.n_v) { vector_job<UT, true>(m, U.v[r - U.n_w]); return; }
+  if (r == U.n_w + U.n_v) { prepare_next_batch(m, reinterpret_cast<int*>(smem)); return; }
+  win_tile_dense_ch<UT>(m, smem, r - (U.n_w + U.n_v + 1));
+}
+
 // the sparse W_in tiles (stage_flags bit 4) as their own kernel: its register budget is
 // its own (the job paths of gfk_win_update_k need ~86 VGPRs)
 // grid: n_w + n_v + 1 job workgroups FIRST (they start with the tiles, not after them),
@@ -1368,7 +1463,12 @@ extern "C" int gfk_launch_win_update(const GfkModel* m, const GfkUpdate* u, hipS
       GFK_WIN_SPARSE_LAUNCH(false, false);
     return (int)hipGetLastError();
   }
-  if (m->bmax > 128) return -1;      // (large batches: the sparse tiles only)
+  if (m->bmax > 128) {                 // large batches: the chunked dense tiles
+    if (m->H[0] > 64 || m->update_mode != 0 || m->input != GFK_IN_BOW || m->n_batch > 1) return -1;
+    const dim3 gl(u->n_w + u->n_v + 1 + m->n_tiles);
+    hipLaunchKernelGGL((gfk_win_lb_k<1024>), gl, dim3(1024), gfk_win_update_smem(m), s, GfkArgT<false>{*m}, GfkUArgT<false>{*u});
+    return (int)hipGetLastError();
+  }
   const dim3 g(m->n_tiles + u->n_w + u->n_v + 1 + extra);
   // more W_in tiles than two rounds of 16-wave workgroups (dec_grid = the CUs' slots), or the
   // batched launch of several clients' tiles asks for the 8-wave shape (stage_flags bit 9,
@@ -1394,7 +1494,8 @@ extern "C" int gfk_win_update_set_smem(size_t bytes) {
                       (const void*)gfk_win_sparse_k<512, false, true, true>, (const void*)gfk_win_sparse_k<512, true, true, true>,
                       (const void*)gfk_win_rows_k<512, false>, (const void*)gfk_win_rows_k<512, true>,
                       (const void*)gfk_win_sparse_k<512, false, false, false, GFK_BMAX_LIMIT / 64>,
-                      (const void*)gfk_win_sparse_k<512, true, false, false, GFK_BMAX_LIMIT / 64>};
+                      (const void*)gfk_win_sparse_k<512, true, false, false, GFK_BMAX_LIMIT / 64>,
+                      (const void*)gfk_win_lb_k<1024>};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return (int)e;

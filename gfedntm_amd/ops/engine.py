@@ -183,8 +183,11 @@ def lds_required(tm, bmax: int) -> int:
     lib = native.kernels()
     which = (0, 1) if m.kind == abi.KIND_PRODLDA else (2, 3)
     if bmax >= LB_MIN_BMAX:
-        m.stage_flags, m.n_dpart = 2 | STAGE_LB | STAGE_WIN_SPARSE, 1
-        return int(max(lib.gfk_smem_required(C.byref(m), w) for w in which + (4, 5, 7)))
+        need = 0
+        for win in (0, STAGE_WIN_SPARSE):        # (either W_in tile shape)
+            m.stage_flags, m.n_dpart = 2 | STAGE_LB | win, 1
+            need = max(need, int(max(lib.gfk_smem_required(C.byref(m), w) for w in which + (4, 5, 7))))
+        return need
     _force_k_split(lib, m)
     need = 0
     for flags in (0, 2):                 # weights unstaged; batch matrices in LDS, then in L2
@@ -694,7 +697,10 @@ class FusedEngine(EngineBase):
         the [B, ldb] logit / logit-gradient matrix in ws["dt"].  Gradient mode: the generic
         optimizer kernel updates every tensor (as the CTM host-GEMM path)."""
         m = self._m
-        m.stage_flags = 2 | STAGE_LB | STAGE_WIN_SPARSE
+        # W_in's gradient: the sparse entry-list tiles where a 64-word tile holds few of the
+        # batch's non-zeros (more tiles than 4 rounds of the CUs, as for small batches), else
+        # the dense tiles in 128-row chunks (csrc/update.hip win_tile_dense_ch)
+        m.stage_flags = 2 | STAGE_LB | (STAGE_WIN_SPARSE if m.n_tiles > 4 * cu else 0)
         m.dec_grid = int(min(m.n_tiles, 2 * cu))
         m.n_dpart = 1
         m.bwd_pre = 0
@@ -806,6 +812,8 @@ class FusedEngine(EngineBase):
             "wstamp": torch.zeros((V if getattr(self, "_win_split_ok", False) else 1) + 16,
                                   dtype=torch.int32, device=dev),
             "wgen": torch.zeros(16, dtype=torch.int32, device=dev),
+            # the large-batch plan's posterior column statistics (6 x 2K floats)
+            "colstat": f(12 * K if m.stage_flags & STAGE_LB else 1),
         }
         Lb = max(int(m.L), 1)
         ws.update(lab=f(B, Lb), dlab=f(B, Lb), ce=f(B), thd=f(B, K))   # label head

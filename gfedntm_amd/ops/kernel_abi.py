@@ -118,7 +118,7 @@ class GfkModel(C.Structure):
         ("ws_lab", P), ("ws_dlab", P), ("ws_ce", P), ("ws_thd", P),
         ("lab_in_enc", C.c_int32), ("bwd_pre", C.c_int32), ("ws_dt", P),
         ("dev", P), ("dev_upd", P), ("n_batch", C.c_int32), ("ldb", C.c_int32),
-        ("ctx_bgrid", C.c_int32), ("ws_wstamp", P), ("ws_wgen", P),
+        ("ctx_bgrid", C.c_int32), ("ws_wstamp", P), ("ws_wgen", P), ("ws_colstat", P),
     ]
 
 
