@@ -340,6 +340,9 @@ namespace gfk {
 
 // In-kernel phase timestamps for diagnostic builds (-DGFK_STAMPS): lane 0 of
 // workgroup 0 writes s_memtime into dbg[slot].  Compiled out otherwise.
+#ifndef GFK_POST_PLAIN_LDS
+#define GFK_POST_PLAIN_LDS 0       // posterior batch matrices staged contiguously (A/B builds)
+#endif
 #ifndef GFK_STRIP_OLDEST_LIGHT
 #define GFK_STRIP_OLDEST_LIGHT 0   // strip forward: wave groups in reverse order (A/B builds)
 #endif

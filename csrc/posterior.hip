@@ -74,8 +74,12 @@ __host__ __device__ inline bool batch_in_lds(const GfkModel& m) { return !(m.sta
 // kernels' LDS cycles were conflicts (CombinedTM K = 100: 31 %, profiles/r4; the model:
 // tools/lds_bank_model.py).  K = 50 (the headline) is already 2 x odd: unchanged.
 __host__ __device__ inline int post_lds_ld(int K) {
+#if GFK_POST_PLAIN_LDS                  // (A/B builds: the contiguous staging of round 4)
+  return K;
+#else
   const int k2 = (K + 1) / 2 * 2;
   return (k2 / 2) % 2 ? k2 : k2 + 2;
+#endif
 }
 
 // Rows of a row-major [rows][cols] global matrix into LDS rows of stride ld (LDS-DMA, one
