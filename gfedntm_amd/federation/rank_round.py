@@ -136,10 +136,7 @@ class MultiClientRound:
         # own collective (FusedEngine.fedavg_parts)
         self.parts: Dict[str, tuple] = {"rest": (0, n)}
         from ..ops.engine import UPDATE_FUSED
-        # (one rank: the in-rank fold of beta's share runs on the side stream from the
-        # batched decoder backward on, overlapping the encoder backward -- only the rest's
-        # fold is left after the round's last kernel)
-        if (self.fused and (world == 1 or on_gpu_plane)
+        if (self.fused and world > 1 and on_gpu_plane
                 and all(e.update_mode == UPDATE_FUSED for e in engines)):
             self.parts = dict(engines[0].fedavg_parts())
         self.colls: Dict[str, CollectiveAggregator] = {}
@@ -158,7 +155,7 @@ class MultiClientRound:
                            "tuning": {k: c.tuning for k, c in self.colls.items() if c.tuning},
                            "plane": {k: c.describe() for k, c in self.colls.items()}}
         self.coll_in_graph = bool(self.colls) and all(c.xgmi is not None for c in self.colls.values())
-        if world > 1 and not self.coll_in_graph and len(self.parts) > 1:
+        if not self.coll_in_graph and len(self.parts) > 1:
             # one RCCL all-reduce of the whole state after the round graph
             for c in self.colls.values():
                 if c.xgmi is not None:
@@ -232,7 +229,7 @@ class MultiClientRound:
             # finished them (else reduced with the rest at the end of the round: the same
             # arithmetic)
             hooks, forked = {}, set()
-            if self.coll_in_graph or not self.colls:
+            if self.coll_in_graph:
                 for part, at in (("beta", bs.beta_final_phase()), ("wa", bs.wa_final_phase())):
                     if part in self.parts and at is not None:
                         hooks[at] = (lambda p=part: self._fork(p))

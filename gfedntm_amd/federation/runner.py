@@ -217,34 +217,10 @@ class LocalFederation:
                 self._batched = self._batched_parts[0]
                 for b in self._batched_parts:
                     b.prepare()
-                # beta's share of the fold on a side stream from the (last group's) decoder
-                # backward on -- final there in the fused update mode -- overlapping the
-                # encoder backward; the rest folded after the round's last kernel (the same
-                # element-wise arithmetic as one fold of the whole state)
-                fp = engines[0].fedavg_parts()
-                hooks, split = {}, None
-                at = self._batched_parts[-1].beta_final_phase()
-                if "beta" in fp and "wa" not in fp and at is not None:
-                    from ..parallel.aggregator import LOCAL_ALL, local_fedavg
-                    (b0, b1), split = fp["beta"], fp["beta"][0]
-                    side, ev_fork, ev_join = (torch.cuda.Stream(self.device), torch.cuda.Event(),
-                                              torch.cuda.Event())
-                    self._fold_side = (side, ev_fork, ev_join)
-
-                    def fork():
-                        ev_fork.record(torch.cuda.current_stream(self.device))
-                        side.wait_event(ev_fork)
-                        with torch.cuda.stream(side):
-                            local_fedavg(shared, LOCAL_ALL, self.agg.groups, off=b0, n=b1 - b0)
-                        ev_join.record(side)
-                    hooks[at] = fork
                 with graph_capture(g):
-                    for i, b in enumerate(self._batched_parts):
-                        b.launch(after=hooks if i == len(self._batched_parts) - 1 else None)
-                    if split is not None:
-                        local_fedavg(shared, LOCAL_ALL, self.agg.groups, off=0, n=split)
-                        torch.cuda.current_stream(self.device).wait_event(self._fold_side[2])
-                    elif not self.agg.fused_sum_(shared):
+                    for b in self._batched_parts:
+                        b.launch()
+                    if not self.agg.fused_sum_(shared):
                         raise RuntimeError("round graph needs the native FedAvg kernel")
                 self._rg = g
                 self._rg_gens = self._engine_gens()
