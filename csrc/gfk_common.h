@@ -341,7 +341,12 @@ namespace gfk {
 // In-kernel phase timestamps for diagnostic builds (-DGFK_STAMPS): lane 0 of
 // workgroup 0 writes s_memtime into dbg[slot].  Compiled out otherwise.
 #ifndef GFK_POST_PLAIN_LDS
-#define GFK_POST_PLAIN_LDS 0       // posterior batch matrices staged contiguously (A/B builds)
+// posterior batch matrices staged contiguously (the default): the padded 2 x odd row stride
+// removes the K = 100 column reductions' bank conflicts (31 % -> 0 %) but its per-row dword
+// LDS-DMA costs more than they did -- CombinedTM K = 100 V = 99k, interleaved on one box:
+// 0.7296 / 0.7355 ms contiguous vs 0.7369 / 0.7432 padded (profiles/r5/ab_post_stride.txt).
+// -DGFK_POST_PLAIN_LDS=0 builds the padded layout
+#define GFK_POST_PLAIN_LDS 1
 #endif
 #ifndef GFK_STRIP_OLDEST_LIGHT
 #define GFK_STRIP_OLDEST_LIGHT 0   // strip forward: wave groups in reverse order (A/B builds)

@@ -328,6 +328,7 @@ int launch_kq(const GfkModel* m, const GfkInfer* p, size_t smem, hipStream_t s) 
     case 2: k = gfk_theta_infer_k<Staged, NQ, 2>; break;
     case 3: k = gfk_theta_infer_k<Staged, NQ, 3>; break;
     case 4: k = gfk_theta_infer_k<Staged, NQ, 4>; break;
+    case 5: case 6: case 7: case 8: k = gfk_theta_infer_k<Staged, NQ, 8>; break;   // (K <= 512)
     default: return -3;
   }
   hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
@@ -356,11 +357,11 @@ extern "C" size_t gfk_theta_infer_smem(const GfkModel* m) {
   return sizeof(float) * ((size_t)inf_weight_floats(*m) + inf_act_floats(*m));
 }
 
-// Host checks mirror the kernel's assumptions: K <= 256, H0 <= 512, a CSR with
+// Host checks mirror the kernel's assumptions: K <= 512, H0 <= 512, a CSR with
 // n_docs + 1 row pointers (or, for contextual-only input, hctx), grid >= 1.
 extern "C" int gfk_theta_infer(const GfkModel* m, const GfkInfer* p, hipStream_t s) {
   if (p->n_docs <= 0) return 0;
-  if (m->K <= 0 || m->K > 256 || m->H[0] <= 0 || m->H[0] > 512 || p->grid <= 0 || !p->out) return -5;
+  if (m->K <= 0 || m->K > 512 || m->H[0] <= 0 || m->H[0] > 512 || p->grid <= 0 || !p->out) return -5;
   if (!(p->flags & 2) && p->n_samples <= 0) return -6;
   if (m->input != GFK_IN_CONTEXTUAL && (!p->indptr || !p->indices || !p->values)) return -7;
   if (m->input != GFK_IN_BOW && !p->hctx) return -8;

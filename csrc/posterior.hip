@@ -67,12 +67,13 @@ __host__ __device__ inline int post_weight_floats(const GfkModel& m) {
 // four of them would not fit the 160 KiB.
 __host__ __device__ inline bool batch_in_lds(const GfkModel& m) { return !(m.stage_flags & 2); }
 
-// Row stride of the LDS-staged [B][K] batch matrices: K rounded up to 2 x odd.  The column
-// reductions read 16 rows x 2 columns per half-wave (ds_read_b32, bank = dword mod 32); a
-// stride of 2 x odd puts those 16 rows on 16 distinct even bank offsets (the two columns
-// fill the odd ones) -- at K = 100 (4 mod 32) rows r and r + 8 shared a bank, half of the
-// kernels' LDS cycles were conflicts (CombinedTM K = 100: 31 %, profiles/r4; the model:
-// tools/lds_bank_model.py).  K = 50 (the headline) is already 2 x odd: unchanged.
+// Row stride of the LDS-staged [B][K] batch matrices (GFK_POST_PLAIN_LDS=0 builds): K rounded
+// up to 2 x odd.  The column reductions read 16 rows x 2 columns per half-wave (ds_read_b32,
+// bank = dword mod 32); a stride of 2 x odd puts those 16 rows on 16 distinct even bank
+// offsets (the two columns fill the odd ones) -- at K = 100 (4 mod 32) rows r and r + 8
+// share a bank, half of the kernels' LDS cycles are conflicts (CombinedTM K = 100: 31 %,
+// profiles/r4; the model: tools/lds_bank_model.py).  Measured slower overall (the per-row
+// staging, gfk_common.h GFK_POST_PLAIN_LDS), so the default build keeps the contiguous rows.
 __host__ __device__ inline int post_lds_ld(int K) {
 #if GFK_POST_PLAIN_LDS                  // (A/B builds: the contiguous staging of round 4)
   return K;
@@ -298,8 +299,9 @@ __device__ __forceinline__ void post_label_head(const GfkModel& m, float* buf, i
 // InLds: the batch matrices are staged in LDS (compile-time, so every access is a
 // ds_read; a runtime select of the pointer would turn them into flat loads).
 // PS (the large-batch plan): the column statistics come precomputed from ws_colstat
-// (gfk_post_colstats_lb_k), which also did row 0's running-statistic / counter duties
-template <bool InLds, bool GB = false, bool PS = false>
+// (gfk_post_colstats_lb_k), which also did row 0's running-statistic / counter duties.
+// KQ: topics per lane of the own row (K <= 64 KQ: 4, or 8 for the plan's K <= 512)
+template <bool InLds, bool GB = false, bool PS = false, int KQ = 4>
 __global__ void __launch_bounds__(FT) gfk_post_fwd_k(GfkArgT<GB> ga) {
   const GfkModel& m = gfk_model(ga);
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -324,7 +326,6 @@ __global__ void __launch_bounds__(FT) gfk_post_fwd_k(GfkArgT<GB> ga) {
     glds_rows(smem + B * LD, ls_raw, B, K, LD, tid, FT);
   }
   const int nb = *nbp;
-  constexpr int KQ = 4;                    // K <= 256
   float ep[KQ], mt[KQ], pm[KQ], pv[KQ];
   const int rc = min(row, max(nb - 1, 0));
 #pragma unroll
@@ -1128,7 +1129,12 @@ extern "C" int gfk_launch_post_fwd(const GfkModel* m, hipStream_t s) {
     if (batch_in_lds(*m)) return -1;
     const int e = launch_colstats_lb(m, s, false);
     if (e) return e;
-    hipLaunchKernelGGL((gfk_post_fwd_k<false, false, true>), dim3(m->bmax), dim3(FT), gfk_post_fwd_smem(m), s, GfkArgT<false>{*m});
+    if (m->K <= 256)
+      hipLaunchKernelGGL((gfk_post_fwd_k<false, false, true>), dim3(m->bmax), dim3(FT), gfk_post_fwd_smem(m), s, GfkArgT<false>{*m});
+    else if (m->K <= 512)
+      hipLaunchKernelGGL((gfk_post_fwd_k<false, false, true, 8>), dim3(m->bmax), dim3(FT), gfk_post_fwd_smem(m), s, GfkArgT<false>{*m});
+    else
+      return -1;
     return (int)hipGetLastError();
   }
   if (batch_in_lds(*m))
@@ -1146,6 +1152,10 @@ extern "C" int gfk_launch_post_bwd(const GfkModel* m, hipStream_t s) {
   if (kq <= 1) do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_row_bwd_k<1, true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_row_bwd_k<1, false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0);
   else if (kq == 2) do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_row_bwd_k<2, true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_row_bwd_k<2, false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0);
   else if (kq == 3) do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_row_bwd_k<3, true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_row_bwd_k<3, false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0);
+  else if (kq > 4) {                   // K <= 512 (the large-batch plan; one client)
+    if (kq > 8 || m->n_batch > 1) return -1;
+    hipLaunchKernelGGL((gfk_row_bwd_k<8, false>), g, t, sm, s, GfkArgT<false>{*m});
+  }
   else do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_row_bwd_k<4, true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_row_bwd_k<4, false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
@@ -1191,7 +1201,8 @@ extern "C" int gfk_post_set_smem(size_t bytes) {
                       (const void*)gfk_row_bwd_k<3>, (const void*)gfk_row_bwd_k<3, true>, (const void*)gfk_row_bwd_k<4>, (const void*)gfk_row_bwd_k<4, true>,
                       (const void*)gfk_post_bwd_k<true, true>, (const void*)gfk_post_bwd_k<true, true, true>, (const void*)gfk_post_bwd_k<true, false>, (const void*)gfk_post_bwd_k<true, false, true>,
                       (const void*)gfk_post_bwd_k<false, true>, (const void*)gfk_post_bwd_k<false, true, true>, (const void*)gfk_post_bwd_k<false, false>, (const void*)gfk_post_bwd_k<false, false, true>,
-                      (const void*)gfk_post_fwd_k<false, false, true>, (const void*)gfk_post_bwd_k<false, true, false, true>,
+                      (const void*)gfk_post_fwd_k<false, false, true>, (const void*)gfk_post_fwd_k<false, false, true, 8>,
+                      (const void*)gfk_row_bwd_k<8>, (const void*)gfk_post_bwd_k<false, true, false, true>,
                       (const void*)gfk_post_bwd_k<false, false, false, true>};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);

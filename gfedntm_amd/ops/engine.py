@@ -75,6 +75,15 @@ STAGE_BWD_KQ1 = 262144            # bit 18: one-k-range backward walking several
 STAGE_LB = 524288                 # bit 19: the large-batch plan (bmax 256 / 512, csrc/gfk_common.h)
 
 
+def engine_bmax(tm) -> int:
+    """Rows the engine's workspaces are sized for: the batch size rounded up to a kernel
+    instance; K > 256 runs the large-batch plan (its posterior / decoder shapes take
+    K <= 512), so such a model's batch is padded to 256 rows (rows >= the batch are
+    masked everywhere, as a short last batch)."""
+    b = next(x for x in BMAX_CHOICES if x >= tm.batch_size)
+    return max(b, LB_MIN_BMAX) if tm.n_components > 256 else b
+
+
 def _explain(ok: bool, why: str, explain: bool) -> bool:
     if not ok and explain:
         raise RuntimeError(f"fused engine unsupported: {why}")
@@ -90,7 +99,7 @@ def supports(tm, explain: bool = False) -> bool:
         (tm.solver in abi.SOLVER_CODES, f"solver {tm.solver} not fused"),
         (tm.activation in abi.ACT_CODES, f"activation {tm.activation} not fused"),
         (tm.batch_size <= BMAX_CHOICES[-1], f"batch_size > {BMAX_CHOICES[-1]}"),
-        (tm.n_components <= 256, "n_components > 256"),
+        (tm.n_components <= 512, "n_components > 512"),
         (max(tm.hidden_sizes) <= 512 and len(tm.hidden_sizes) <= abi.MAX_LAYERS,
          "hidden layers too wide / too many"),
         (getattr(tm, "label_size", 0) <= 256, "label_size > 256"),
@@ -100,7 +109,10 @@ def supports(tm, explain: bool = False) -> bool:
     for ok, why in checks:
         if not _explain(ok, why, explain):
             return False
-    bmax = next(b for b in BMAX_CHOICES if b >= tm.batch_size)
+    bmax = engine_bmax(tm)
+    if tm.n_components > 256 and (tm.kind == "ctm" or tm.model_type.lower() != "prodlda"):
+        return _explain(False, "n_components > 256 needs the large-batch plan: ProdLDA, bag-of-words",
+                        explain)
     if bmax >= LB_MIN_BMAX:
         # the large-batch plan: bag-of-words AVITM, the sparse W_in tiles (H0 <= 64), the
         # [bmax, ldb] logit matrix addressed with 32-bit buffer offsets
@@ -324,7 +336,7 @@ class FusedEngine(EngineBase):
         self.lr, self.beta1, self.beta2 = float(tm.lr), hp["beta1"], hp["beta2"]
         self.eps, self.weight_decay = hp["eps"], 0.0
         self.fedavg_scale: Optional[float] = None
-        self.bmax = next(b for b in BMAX_CHOICES if b >= tm.batch_size)
+        self.bmax = engine_bmax(tm)
         # the large-batch plan (bmax 256 / 512): library GEMMs for the decoder products,
         # gradient mode (the kernels write gradients; the generic optimizer kernel follows)
         self.large_batch = self.bmax >= LB_MIN_BMAX

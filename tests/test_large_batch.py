@@ -7,7 +7,8 @@ hipBLASLt GEMMs around two HIP kernels (column batch-norm / logit gradient).
 
 Oracle: the same PyTorch fp32 functional step as tests/test_fused_kernels.py (loss, KL, RL,
 every gradient, BN running statistics, the optimizer step) at B in {256, 512} x K in {50, 200}
-x V in {5k, 112k}, ProdLDA and NeuralLDA, plus a partial batch and a graph-replayed run.
+x V in {5k, 112k}, ProdLDA and NeuralLDA, plus a partial batch, a graph-replayed run, and
+K in (256, 512] (ProdLDA: the same plan, the batch padded to 256 rows) with θ inference.
 """
 import numpy as np
 import pytest
@@ -83,3 +84,35 @@ def test_large_batch_graph_training_tracks_torch(model_type):
     # both decrease, to within a few percent of each other
     assert lf[-5:].mean() < lf[:5].mean() and lr_[-5:].mean() < lr_[:5].mean()
     np.testing.assert_allclose(lf[-5:].mean(), lr_[-5:].mean(), rtol=0.05)
+
+
+@pytest.mark.parametrize("B,K", [(64, 300), (256, 512), (100, 512)])
+def test_large_k_matches_oracle(B, K):
+    """K in (256, 512] (ProdLDA, bag of words) runs the large-batch plan, the batch padded to
+    256 rows when smaller (rows >= the batch masked everywhere): same oracle."""
+    from gfedntm_amd.ops.engine import engine_bmax
+    torch.manual_seed(0)
+    tm = AVITM(backend="fused", input_size=5000, n_components=K, hidden_sizes=(50, 50),
+               batch_size=B, verbose=False, device="cuda")
+    assert tm.engine.large_batch and tm.engine.bmax == engine_bmax(tm) >= 256
+    _oracle_step("prodLDA", B, B + 37, K, (50, 50), 5000)
+
+
+def test_large_k_theta_inference_matches_eval_encoder():
+    """θ inference at K = 512 (csrc/infer.hip's 8-topics-per-lane instance): the posterior
+    moments equal the eval-mode encoder's."""
+    torch.manual_seed(0)
+    tm = AVITM(backend="fused", input_size=3000, n_components=512, hidden_sizes=(50, 50),
+               batch_size=64, verbose=False, device="cuda")
+    X = random_csr(300, 3000, 40, seed=1)
+    data = DeviceCSR(X, "cuda")
+    tm.engine.bind_data(data, BatchPlan.build(300, 64, 5, seed=0))
+    for s in range(5):
+        tm.engine.step(s)
+    torch.cuda.synchronize()
+    mom = tm.engine.theta_infer(data, moments=True)
+    tm.model.eval()
+    with torch.no_grad():
+        mu, ls = tm.model.inf_net(torch.from_numpy(X.toarray()).cuda())
+    torch.testing.assert_close(mom[:, 0], mu, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(mom[:, 1], ls, rtol=1e-4, atol=1e-4)
