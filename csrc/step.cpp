@@ -86,11 +86,15 @@ size_t gfk_smem_required(const GfkModel* m, int which) {
 // more than the 64 KiB default (MI355X has 160 KiB per CU).
 int gfk_setup(const GfkModel* m) {
   int e = 0;
-  size_t p = gfk_prodlda_fwd_smem(m), q = gfk_prodlda_bwd_smem(m);
-  if ((e = gfk_prodlda_set_smem(p > q ? p : q))) return e;
-  p = gfk_lda_fwd_smem(m->K);
-  q = gfk_lda_bwd_smem(m);
-  if ((e = gfk_lda_set_smem(p > q ? p : q))) return e;
+  // (only the model's own decoder family: the other's plan for this shape may not even fit
+  // the LDS -- NeuralLDA's beta backward at K > 256)
+  if (m->kind == GFK_PRODLDA) {
+    const size_t p = gfk_prodlda_fwd_smem(m), q = gfk_prodlda_bwd_smem(m);
+    if ((e = gfk_prodlda_set_smem(p > q ? p : q))) return e;
+  } else {
+    const size_t p = gfk_lda_fwd_smem(m->K), q = gfk_lda_bwd_smem(m);
+    if ((e = gfk_lda_set_smem(p > q ? p : q))) return e;
+  }
   if ((e = gfk_enc_in_set_smem(gfk_enc_in_smem(m)))) return e;
   if ((e = gfk_post_set_smem(gfk_post_smem(m)))) return e;
   if (m->ctx_fused == 1 && (e = gfk_ctx_set_smem(gfk_ctx_smem(m)))) return e;
