@@ -216,6 +216,8 @@ constexpr int GFK_BWD_KQ1 = 262144;
 // beta backward builds its x^T tile per 128-row chunk; gradient mode + the generic
 // optimizer kernel
 constexpr int GFK_LB = 524288;
+// stage_flags bit 20 (GFK_POST_ROWS2): post_bwd takes two rows per workgroup (batched launches)
+constexpr int GFK_POST_ROWS2 = 1048576;
 constexpr int GFK_BMAX_LIMIT = 512;
 __host__ __device__ inline bool gfk_postfold(const GfkModel& m) {
   return (m.stage_flags & GFK_FWD_POSTFOLD) && (m.stage_flags & 4) && (m.stage_flags & 256) &&

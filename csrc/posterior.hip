@@ -750,8 +750,12 @@ __device__ __forceinline__ void post_prior_sums(int K, int nb, const float* mu, 
 // grid: bmax + 1 workgroups: row = gfk_bx() < bmax, plus one extra workgroup
 // (the last) for the batch-level work -- prior gradients, the loss, the step
 // counter -- so no row workgroup carries it on the critical path.
-// PS (the large-batch plan): the column sums come precomputed from ws_colstat
-template <bool InLds, bool Staged, bool GB = false, bool PS = false>
+// PS (the large-batch plan): the column sums come precomputed from ws_colstat.
+// R rows per workgroup (stage_flags GFK_POST_ROWS2, batched launches: R = 2): the batch
+// matrices, weights and column sums are staged / computed once for both rows, whose own-row
+// sections run one after the other -- M clients' bmax / 2 workgroups fill one round of the
+// CUs (one 16-wave workgroup per CU) where bmax + 1 ran in three
+template <bool InLds, bool Staged, bool GB = false, bool PS = false, int R = 1>
 __global__ void __launch_bounds__(FT) gfk_post_bwd_k(GfkArgT<GB> ga) {
   const GfkModel& m = gfk_model(ga);
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -760,8 +764,9 @@ __global__ void __launch_bounds__(FT) gfk_post_bwd_k(GfkArgT<GB> ga) {
   const int32_t* nbp = m.ws_nb;
   keep(K, B, nh, sflags, dmu_g, dls_g, mu_g, ls_g, nbp);
   const int tid = threadIdx.x, lane = tid & 63;
-  const int row = gfk_bx();
-  const bool extra = !(sflags & GFK_POST_EXTRA_ROWBWD) && row == (int)gridDim.x - 1;
+  const int r0 = gfk_bx() * R;          // this workgroup's first row
+  int row = r0;
+  const bool extra = !(sflags & GFK_POST_EXTRA_ROWBWD) && gfk_bx() == (int)gridDim.x - 1;
   const PostLds L = post_lds(m);
   const int Hl = m.H[nh - 1];
   constexpr bool staged = Staged;
@@ -910,6 +915,23 @@ __global__ void __launch_bounds__(FT) gfk_post_bwd_k(GfkArgT<GB> ga) {
   GFK_STAMP(m, 12);
   GFK_STAMP(m, 14);
 
+#pragma unroll 1
+  for (int rr = 0; rr < R; ++rr) {
+  row = r0 + rr;
+  if (row >= nb) break;                 // (uniform)
+  if (rr > 0) {                         // the next row's z / mask (the previous row's reads done)
+    lds_barrier();
+    int o = L.zrow;
+#pragma unroll
+    for (int l = 0; l < GFK_MAX_LAYERS; ++l) {
+      if (l < nh) {
+        glds_copy(smem + o, m.ws_z[l] + (size_t)row * m.H[l], m.H[l], tid, FT);
+        o += pad4(m.H[l]);
+      }
+    }
+    glds_copy(smem + L.mask, m.ws_mask_h + (size_t)row * Hl, Hl, tid, FT);
+    vm_barrier();
+  }
   // ---- own row: BN backward -> d mu_raw | d ls_raw ----
   float* dr = smem + L.dr;              // [2K]: dmr then dlr
 #pragma unroll
@@ -977,6 +999,7 @@ __global__ void __launch_bounds__(FT) gfk_post_bwd_k(GfkArgT<GB> ga) {
     lds_barrier();
     float* t = din; din = dout; dout = t;
   }
+  }                                     // (rows of the workgroup)
   GFK_STAMP(m, 13);
 }
 
@@ -1162,6 +1185,19 @@ extern "C" int gfk_launch_post_bwd(const GfkModel* m, hipStream_t s) {
   const dim3 gb(m->bmax + (moved ? 0 : 1)), tb(FT);   // + the prior / loss / step workgroup
   const size_t sb = gfk_post_bwd_smem(m);
   const bool st = m->stage_flags & 1;
+  if ((m->stage_flags & GFK_POST_ROWS2) && m->n_batch > 1 && !(m->stage_flags & GFK_LB)) {
+    // two rows per workgroup (batched launches)
+    const dim3 g2((m->bmax + 1) / 2 + (moved ? 0 : 1));
+    const GfkArgT<true> a{gfk_dev(m)};
+    if (batch_in_lds(*m)) {
+      if (st) hipLaunchKernelGGL((gfk_post_bwd_k<true, true, true, false, 2>), gfk_grid(g2, m), tb, sb, s, a);
+      else hipLaunchKernelGGL((gfk_post_bwd_k<true, false, true, false, 2>), gfk_grid(g2, m), tb, sb, s, a);
+    } else {
+      if (st) hipLaunchKernelGGL((gfk_post_bwd_k<false, true, true, false, 2>), gfk_grid(g2, m), tb, sb, s, a);
+      else hipLaunchKernelGGL((gfk_post_bwd_k<false, false, true, false, 2>), gfk_grid(g2, m), tb, sb, s, a);
+    }
+    return (int)hipGetLastError();
+  }
   if (m->stage_flags & GFK_LB) {        // large batches: the column sums once, then the rows
     if (batch_in_lds(*m)) return -1;
     const int e2 = launch_colstats_lb(m, s, true);
@@ -1203,7 +1239,9 @@ extern "C" int gfk_post_set_smem(size_t bytes) {
                       (const void*)gfk_post_bwd_k<false, true>, (const void*)gfk_post_bwd_k<false, true, true>, (const void*)gfk_post_bwd_k<false, false>, (const void*)gfk_post_bwd_k<false, false, true>,
                       (const void*)gfk_post_fwd_k<false, false, true>, (const void*)gfk_post_fwd_k<false, false, true, 8>,
                       (const void*)gfk_row_bwd_k<8>, (const void*)gfk_post_bwd_k<false, true, false, true>,
-                      (const void*)gfk_post_bwd_k<false, false, false, true>};
+                      (const void*)gfk_post_bwd_k<false, false, false, true>,
+                      (const void*)gfk_post_bwd_k<true, true, true, false, 2>, (const void*)gfk_post_bwd_k<true, false, true, false, 2>,
+                      (const void*)gfk_post_bwd_k<false, true, true, false, 2>, (const void*)gfk_post_bwd_k<false, false, true, false, 2>};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return (int)e;

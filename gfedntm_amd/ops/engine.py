@@ -73,6 +73,7 @@ STAGE_FWD_POSTFOLD = 65536        # bit 16: the strip forward computes post_fwd 
 STAGE_POST_EXTRA_ROWBWD = 131072  # bit 17: post_bwd's batch-level workgroup runs in row_bwd
 STAGE_BWD_KQ1 = 262144            # bit 18: one-k-range backward walking several tiles (K <= 64)
 STAGE_LB = 524288                 # bit 19: the large-batch plan (bmax 256 / 512, csrc/gfk_common.h)
+STAGE_POST_ROWS2 = 1048576        # bit 20: post_bwd two rows per workgroup (batched launches)
 
 
 def engine_bmax(tm) -> int:
@@ -1657,14 +1658,17 @@ class BatchedSteps:
                     and os.environ.get("GFEDNTM_POSTFOLD", "auto") != "0"):
                 mm.stage_flags |= STAGE_FWD_POSTFOLD
             # post_bwd: M clients x (bmax + 1) workgroups of 16 waves with the batch matrices
-            # in LDS (~93 KB: one per CU) run in three rounds at M = 8; with the matrices read
-            # from L2 (stage_flags bit 1, ~42 KB) and the batch-level workgroup moved into
-            # row_bwd, M bmax workgroups fit one round at two per CU -- but the round measured
-            # slower (M = 8, interleaved on one box: 0.1507 / 0.1520 ms without vs 0.1535 /
-            # 0.1527 with, profiles/r5/ab_batch.txt): the L2 reads cost more than the rounds.
-            # Opt-in: GFEDNTM_BATCH_POST=1
-            if (M > 1 and M * (mm.bmax + 1) > self._cu
-                    and os.environ.get("GFEDNTM_BATCH_POST", "0") == "1"):
+            # in LDS (~93 KB: one per CU) run in three rounds at M = 8.  GFEDNTM_BATCH_POST:
+            # "rows2" (the default) -- two rows per workgroup (the matrices, weights and column
+            # sums staged once for both) and the batch-level workgroup moved into row_bwd:
+            # M bmax / 2 workgroups, one round; "l2" -- the round-5a variant, the matrices
+            # read from L2 (~42 KB, two per CU) with the moved batch-level workgroup, measured
+            # slower (0.1507 / 0.1520 ms without vs 0.1535 / 0.1527 with,
+            # profiles/r5/ab_batch.txt); "0" -- neither
+            bpost = os.environ.get("GFEDNTM_BATCH_POST", "rows2")
+            if M > 1 and M * (mm.bmax + 1) > self._cu and bpost == "rows2":
+                mm.stage_flags |= STAGE_POST_EXTRA_ROWBWD | STAGE_POST_ROWS2
+            elif M > 1 and M * (mm.bmax + 1) > self._cu and bpost in ("1", "l2"):
                 mm.stage_flags |= 2 | STAGE_POST_EXTRA_ROWBWD
             # prodlda_bwd at K <= 64: one 16-wave workgroup per tile (~61 KB of LDS, two per
             # CU) -- M clients' tiles beyond two per CU run in a second round (592 on 512

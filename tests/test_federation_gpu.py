@@ -234,7 +234,7 @@ def test_batched_large_round_variants_match_branch_round(monkeypatch, strip):
     from gfedntm_amd.ops.engine import (STAGE_BWD_KQ1, STAGE_FWD_STRIP_PF, STAGE_FWD_STRIP_RING,
                                         STAGE_POST_EXTRA_ROWBWD, STAGE_WIN_BATCH8)
     monkeypatch.setenv("GFEDNTM_BATCH_STRIP", strip)
-    monkeypatch.setenv("GFEDNTM_BATCH_POST", "1")       # the opt-in shapes, covered here
+    monkeypatch.setenv("GFEDNTM_BATCH_POST", "l2")      # the opt-in shapes, covered here
     monkeypatch.setenv("GFEDNTM_BATCH_BWD", "1")
     sc = generate_synthetic(vocab_size=5000, n_topics=50, n_docs=1000, n_nodes=8, frozen_topics=5,
                             nwords=(150, 250), seed=13)
