@@ -485,9 +485,13 @@ extern "C" size_t gfk_row_bwd_smem(const GfkModel* m) { return sizeof(float) * 4
 // last workgroup of PT threads): the priors' gradients -> their grad slots,
 //   d prior_mean = w (nb pm - sum_b mu_b) / pv,
 //   d prior_var  = w / 2 (nb / pv - sum_b exp(ls_b) / pv^2 - sum_b (pm - mu_b)^2 / pv^2),
-// the loss sum_b (w KL_b + RL_b [+ CE_b]) -> loss_hist[step], and the step counter.  Thread k
-// sums topic k's column over the rows (coalesced across threads), in row order.
+// the loss sum_b (w KL_b + RL_b [+ CE_b]) -> loss_hist[step], and the step counter.  Thread
+// (c, g) sums topic column c over rows g, g + NG, ... (CW = 64 / 128 / 256 columns per pass, the
+// smallest covering K, NG = PT / CW row groups; 16 rows' loads in flight per thread), the groups'
+// partials added in group order through LDS -- at K = 50 four groups of 16 rows where one thread
+// per topic walked all 64 rows (the batched round's tail, 9 us).
 __device__ __forceinline__ void post_batch_level(const GfkModel& m, int nb, float* scratch, int tid) {
+  __shared__ float red[3 * PT];
   const int K = m.K;
   const float wk = m.kl_weight;
   const int step0 = *m.step;
@@ -495,19 +499,45 @@ __device__ __forceinline__ void post_batch_level(const GfkModel& m, int nb, floa
   for (int b = tid; b < nb; b += PT)
     lterm += wk * m.ws_kl[b] + m.ws_rl[b] + (m.lab_on ? m.ws_ce[b] : 0.f);
   if (m.learn_priors) {
-    for (int k = tid; k < K; k += PT) {
-      const float pm = m.prior_mean[k], pv = m.prior_var[k];
+    constexpr int RB = 16;
+    const int cw = K <= 64 ? 64 : K <= 128 ? 128 : PT, ng = PT / cw;
+    const int c = tid % cw, g = tid / cw;
+    for (int k0 = 0; k0 < K; k0 += cw) {
+      const int k = k0 + c, kk = min(k, K - 1);
+      const float pm = m.prior_mean[kk];
       float smu = 0.f, svar = 0.f, sdm2 = 0.f;
-#pragma unroll 4
-      for (int b = 0; b < nb; ++b) {
-        const float mu = m.ws_mu[b * K + k], ls = m.ws_ls[b * K + k];
-        smu += mu;
-        svar += expf(ls);
-        const float dm = pm - mu;
-        sdm2 += dm * dm;
+      for (int r0 = g; r0 < nb; r0 += RB * ng) {
+        float mu[RB], ls[RB];
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+          const int r = min(r0 + ng * i, nb - 1);
+          mu[i] = m.ws_mu[r * K + kk];
+          ls[i] = m.ws_ls[r * K + kk];
+        }
+#pragma unroll
+        for (int i = 0; i < RB; ++i)
+          if (r0 + ng * i < nb) {
+            smu += mu[i];
+            svar += expf(ls[i]);
+            const float dm = pm - mu[i];
+            sdm2 += dm * dm;
+          }
       }
-      m.prior_mean[k + m.off_g] = wk * ((float)nb * pm - smu) / pv;
-      m.prior_var[k + m.off_g] = wk * 0.5f * ((float)nb / pv - svar / (pv * pv) - sdm2 / (pv * pv));
+      red[tid] = smu;
+      red[PT + tid] = svar;
+      red[2 * PT + tid] = sdm2;
+      lds_barrier();
+      if (g == 0 && k < K) {
+        for (int j = 1; j < ng; ++j) {
+          smu += red[c + j * cw];
+          svar += red[PT + c + j * cw];
+          sdm2 += red[2 * PT + c + j * cw];
+        }
+        const float pv = m.prior_var[k];
+        m.prior_mean[k + m.off_g] = wk * ((float)nb * pm - smu) / pv;
+        m.prior_var[k + m.off_g] = wk * 0.5f * ((float)nb / pv - svar / (pv * pv) - sdm2 / (pv * pv));
+      }
+      lds_barrier();
     }
   }
   const float l = block_sum_wave0(lterm, scratch);
