@@ -111,7 +111,7 @@ __host__ __device__ inline int enc_weight_floats(const GfkModel& m) {
 #pragma unroll
   for (int l = 0; l + 1 < GFK_MAX_LAYERS; ++l)
     if (l + 1 < m.n_hidden) n += pad4(m.H[l + 1] * m.H[l]) + pad4(m.H[l + 1]);
-  const int Hl = m.H[m.n_hidden - 1];
+  const int Hl = gfk_hlast(m);
   return n + 2 * (pad4(m.K * Hl) + pad4(m.K));
 }
 
@@ -180,8 +180,13 @@ __device__ __forceinline__ void rowvec_gemv(const float* W, const float* x, int 
 // LDS with LDS-only barriers: its global stores are never waited on.
 // Staged (compile-time): the MLP weights are read from LDS (ds_read); a runtime
 // select between the LDS copy and global memory would make every read a flat load.
-template <bool Staged, bool GB = false>
-__global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkArgT<GB> ga) {
+// NQM: the widest H0 class compiled in (outputs per lane, 64 NQM >= H0).  The H0 <= 64
+// instance (NQM = 1) drops the wide paths' registers (87 -> <= 64 VGPRs): two workgroups
+// fit a CU, so a batched launch's M bmax rows (512 at M = 8) run in one round on the 256
+// CUs instead of two.
+template <bool Staged, bool GB = false, int NQM = 8>
+__global__ void __launch_bounds__(ENC_THREADS) __attribute__((amdgpu_waves_per_eu(NQM == 1 ? 8 : 1)))
+gfk_enc_in_k(GfkArgT<GB> ga) {
   const GfkModel& m = gfk_model(ga);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int b = gfk_bx(), tid = threadIdx.x;
@@ -191,7 +196,7 @@ __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkArgT<GB> ga) {
   const float *values = m.values, *w_in = m.w_in, *b_in = m.b_in;
   keep(H0, K, bmax, nh, input, sflags, nxt, indices, stepp, values, w_in, b_in);
   const bool zs = m.ctx_fused == 2;       // ZeroShotTM: dense input layer fused here
-  const int Hl = m.H[nh - 1], hm = enc_hmax(m);
+  const int Hl = gfk_hlast(m), hm = enc_hmax(m);
   float* red = smem;
   float* act0 = red + ENC_WAVES * H0;
   float* act1 = act0 + pad4(hm);
@@ -252,34 +257,40 @@ __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkArgT<GB> ga) {
   GFK_STAMP(m, 5);
   // ---- sparse gather (ZeroShotTM fused: the dense contextual input layer) ----
   if (zs) {
-    float acc[8];
+    float acc[NQM];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+    for (int q = 0; q < NQM; ++q) acc[q] = 0.f;
     const float* xr = m.ctx + (size_t)doc * m.C;
-    if (H0 <= 64) gather_dense<1>(xr, m.C, wave, w_in, H0, lane, acc);
-    else if (H0 <= 128) gather_dense<2>(xr, m.C, wave, w_in, H0, lane, acc);
-    else if (H0 <= 256) gather_dense<4>(xr, m.C, wave, w_in, H0, lane, acc);
-    else gather_dense<8>(xr, m.C, wave, w_in, H0, lane, acc);
+    if constexpr (NQM == 1) gather_dense<1>(xr, m.C, wave, w_in, H0, lane, acc);
+    else {
+      if (H0 <= 64) gather_dense<1>(xr, m.C, wave, w_in, H0, lane, acc);
+      else if (H0 <= 128) gather_dense<2>(xr, m.C, wave, w_in, H0, lane, acc);
+      else if (H0 <= 256) gather_dense<4>(xr, m.C, wave, w_in, H0, lane, acc);
+      else gather_dense<8>(xr, m.C, wave, w_in, H0, lane, acc);
+    }
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
+    for (int q = 0; q < NQM; ++q) {
       const int j = lane + 64 * q;
       if (j < H0) red[wave * H0 + j] = acc[q];
     }
   }
   if (input != GFK_IN_CONTEXTUAL) {
-    float acc[8];
+    float acc[NQM];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+    for (int q = 0; q < NQM; ++q) acc[q] = 0.f;
     const int n = e1 - e0;
-    if (H0 <= 64) gather_slots<1>(sidx, sval, n, gv, gx, wave, w_in, H0, lane, acc);
-    else if (H0 <= 128) gather_slots<2>(sidx, sval, n, gv, gx, wave, w_in, H0, lane, acc);
-    else if (H0 <= 256) gather_slots<4>(sidx, sval, n, gv, gx, wave, w_in, H0, lane, acc);
-    else gather_slots<8>(sidx, sval, n, gv, gx, wave, w_in, H0, lane, acc);
+    if constexpr (NQM == 1) gather_slots<1>(sidx, sval, n, gv, gx, wave, w_in, H0, lane, acc);
+    else {
+      if (H0 <= 64) gather_slots<1>(sidx, sval, n, gv, gx, wave, w_in, H0, lane, acc);
+      else if (H0 <= 128) gather_slots<2>(sidx, sval, n, gv, gx, wave, w_in, H0, lane, acc);
+      else if (H0 <= 256) gather_slots<4>(sidx, sval, n, gv, gx, wave, w_in, H0, lane, acc);
+      else gather_slots<8>(sidx, sval, n, gv, gx, wave, w_in, H0, lane, acc);
+    }
     if (m.ctx_fused) {      // CombinedTM: the row's contextual partials from ctx_fwd (fixed order)
       const int P = m.ctx_parts > 0 ? m.ctx_parts : m.n_tiles;
       const size_t ps = (size_t)bmax * H0;
       const float* hp = m.ws_hpart + (size_t)b * H0;
-      if (H0 <= 64) {
+      if (NQM == 1 || H0 <= 64) {
         // one column per lane: 16 partials in flight per wave (the per-tile partials of a
         // large vocabulary are ~100 per wave: a round trip per 4 of them was most of the
         // kernel), summed in the same order as below
@@ -294,22 +305,22 @@ __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkArgT<GB> ga) {
         }
       } else
       for (int p0 = wave; p0 < P; p0 += 4 * ENC_WAVES) {
-        float hv[4][8];
+        float hv[4][NQM];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int p = min(p0 + u * ENC_WAVES, P - 1);
 #pragma unroll
-          for (int q = 0; q < 8; ++q)
+          for (int q = 0; q < NQM; ++q)
             hv[u][q] = 64 * q < H0 ? hp[(size_t)p * ps + min(lane + 64 * q, H0 - 1)] : 0.f;
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
-          for (int q = 0; q < 8; ++q) acc[q] += p0 + u * ENC_WAVES < P ? hv[u][q] : 0.f;
+          for (int q = 0; q < NQM; ++q) acc[q] += p0 + u * ENC_WAVES < P ? hv[u][q] : 0.f;
       }
     }
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
+    for (int q = 0; q < NQM; ++q) {
       const int j = lane + 64 * q;
       if (j < H0) red[wave * H0 + j] = acc[q];
     }
@@ -424,6 +435,10 @@ __global__ void __launch_bounds__(ENC_THREADS) gfk_enc_in_k(GfkArgT<GB> ga) {
 }
 
 extern "C" int gfk_launch_enc_in(const GfkModel* m, hipStream_t s) {
+  if (m->n_batch > 1 && m->H[0] <= 64 && (m->stage_flags & 1)) {   // batched, narrow, staged: two workgroups per CU
+    hipLaunchKernelGGL((gfk_enc_in_k<true, true, 1>), gfk_grid(dim3(m->bmax), m), dim3(ENC_THREADS), gfk_enc_in_smem(m), s, GfkArgT<true>{gfk_dev(m)});
+    return (int)hipGetLastError();
+  }
   if (m->stage_flags & 1)
     do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_enc_in_k<true, true>), gfk_grid(dim3(m->bmax), m), dim3(ENC_THREADS), gfk_enc_in_smem(m), s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_enc_in_k<true, false>), dim3(m->bmax), dim3(ENC_THREADS), gfk_enc_in_smem(m), s, GfkArgT<false>{*m}); } while (0);
   else
@@ -437,7 +452,8 @@ extern "C" int gfk_enc_in_set_smem(size_t bytes) {
   static size_t cur = 0;
   if (bytes <= cur) return 0;
   cur = bytes;
-  const void* ks[] = {(const void*)gfk_enc_in_k<true>, (const void*)gfk_enc_in_k<true, true>, (const void*)gfk_enc_in_k<false>, (const void*)gfk_enc_in_k<false, true>};
+  const void* ks[] = {(const void*)gfk_enc_in_k<true>, (const void*)gfk_enc_in_k<true, true>, (const void*)gfk_enc_in_k<false>, (const void*)gfk_enc_in_k<false, true>,
+                      (const void*)gfk_enc_in_k<true, true, 1>};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return (int)e;

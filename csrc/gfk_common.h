@@ -219,6 +219,15 @@ constexpr int GFK_LB = 524288;
 // stage_flags bit 20 (GFK_POST_ROWS2): post_bwd takes two rows per workgroup (batched launches)
 constexpr int GFK_POST_ROWS2 = 1048576;
 constexpr int GFK_BMAX_LIMIT = 512;
+// H[n_hidden - 1] without a runtime index into the descriptor (a batched kernel's copy of it
+// is promoted to registers only when every access has a constant offset)
+__host__ __device__ __forceinline__ int gfk_hlast(const GfkModel& m) {
+  int h = m.H[0];
+#pragma unroll
+  for (int l = 1; l < GFK_MAX_LAYERS; ++l)
+    if (l < m.n_hidden) h = m.H[l];
+  return h;
+}
 __host__ __device__ inline bool gfk_postfold(const GfkModel& m) {
   return (m.stage_flags & GFK_FWD_POSTFOLD) && (m.stage_flags & 4) && (m.stage_flags & 256) &&
          m.K <= 64 && m.bmax <= 64 && !m.lab_on && m.kind == GFK_PRODLDA;
@@ -328,7 +337,24 @@ __device__ __forceinline__ int gfk_bx() {
 #endif
 }
 __device__ __forceinline__ const GfkModel& gfk_model(const GfkArgT<false>& a) { return a.m; }
+// (the batched models through the constant address space: the field loads stay scalar
+// (s_load) after the kernel's own stores, as the by-value kernarg model's do)
+#ifndef GFK_BATCHED_COPY
+#define GFK_BATCHED_COPY 0
+#endif
+// Batched kernels: the workgroup's descriptor is COPIED at entry (GFK_BATCHED_COPY, set by
+// the sources whose kernels index it with constant offsets only): the copy's field loads
+// are issued before any store, so they stay scalar and the pointers in it are known global
+// (global_load / global_store with an SGPR base, as the by-value descriptor's) -- through
+// the reference every field read after a store is re-loaded, and its pointers are FLAT
+// (64-bit VGPR addresses): the batched ProdLDA backward needed 80 VGPRs, 64 with the copy.
+// A runtime index into one of its arrays keeps the copy in scratch: those sources keep the
+// reference.
+#if GFK_BATCHED_COPY
+__device__ __forceinline__ GfkModel gfk_model(const GfkArgT<true>& a) { return a.p[gfk_bz()]; }
+#else
 __device__ __forceinline__ const GfkModel& gfk_model(const GfkArgT<true>& a) { return a.p[gfk_bz()]; }
+#endif
 template <bool B> struct GfkUArgT;
 template <> struct GfkUArgT<false> { GfkUpdate u; };
 template <> struct GfkUArgT<true> { const GfkUpdate* p; };

@@ -63,7 +63,7 @@ __host__ __device__ inline int inf_weight_floats(const GfkModel& m) {
   int n = 0;
   for (int l = 0; l + 1 < GFK_MAX_LAYERS; ++l)
     if (l + 1 < m.n_hidden) n += pad4(m.H[l] * m.H[l + 1]) + pad4(m.H[l + 1]);
-  const int Hl = m.H[m.n_hidden - 1];
+  const int Hl = gfk_hlast(m);
   return n + 2 * pad4(Hl * m.K) + 6 * pad4(m.K);
 }
 
@@ -131,7 +131,7 @@ __global__ void __launch_bounds__(INF_THREADS) gfk_theta_infer_k(GfkArgT<GB> ga,
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
   const int H0 = m.H[0], K = m.K, nh = m.n_hidden, act = m.act, input = m.input;
-  const int Hl = m.H[nh - 1], hm = pad4(inf_hmax(m));
+  const int Hl = gfk_hlast(m), hm = pad4(inf_hmax(m));
   const float bn_eps = m.bn_eps;
   float* wst = smem;
   float* abuf = smem + (Staged ? inf_weight_floats(m) : 0) + wave * 2 * hm;

@@ -51,7 +51,7 @@ __host__ __device__ inline int post_hmax(const GfkModel& m) {
 // Floats of the staged backward weights: W_mu, W_s ([K][Hl]), then W_h[l] for
 // l = 0 .. nh-2 ([H[l+1]][H[l]]), each padded to 4.
 __host__ __device__ inline int post_weight_floats(const GfkModel& m) {
-  int n = 2 * pad4(m.K * m.H[m.n_hidden - 1]);
+  int n = 2 * pad4(m.K * gfk_hlast(m));
 #pragma unroll
   for (int l = 0; l + 1 < GFK_MAX_LAYERS; ++l)
     if (l + 1 < m.n_hidden) n += pad4(m.H[l + 1] * m.H[l]);
@@ -655,7 +655,7 @@ __host__ __device__ inline PostLds post_lds(const GfkModel& m) {
 #pragma unroll
   for (int l = 0; l < GFK_MAX_LAYERS; ++l)
     if (l < m.n_hidden) o += pad4(m.H[l]);
-  L.mask = o; o += pad4(m.H[m.n_hidden - 1]);
+  L.mask = o; o += pad4(gfk_hlast(m));
   L.red = o; o += FT / 64;                // block_sum_wave0 scratch, one float per wave
   L.red2 = o; o += 2 * FT;                // column-reduction scratch [2][FT]
   L.w = o;
@@ -798,7 +798,7 @@ __global__ void __launch_bounds__(FT) gfk_post_bwd_k(GfkArgT<GB> ga) {
   int row = r0;
   const bool extra = !(sflags & GFK_POST_EXTRA_ROWBWD) && gfk_bx() == (int)gridDim.x - 1;
   const PostLds L = post_lds(m);
-  const int Hl = m.H[nh - 1];
+  const int Hl = gfk_hlast(m);
   constexpr bool staged = Staged;
   GFK_STAMP(m, 10);
 

@@ -36,6 +36,7 @@
 // the MFMA A-operand reads are bank-conflict free); ws_zn is tiled
 // [n_tiles][bmax][VB] so a tile is one contiguous LDS-DMA copy; ws_row_part is
 // [dec_grid * 4][bmax][2] (one partial per forward wave column strip).
+#define GFK_BATCHED_COPY 1   // batched kernels copy their descriptor (gfk_common.h gfk_model)
 #include "gfk_common.h"
 
 using namespace gfk;

@@ -1670,9 +1670,9 @@ class BatchedSteps:
                 mm.stage_flags |= STAGE_POST_EXTRA_ROWBWD | STAGE_POST_ROWS2
             elif M > 1 and M * (mm.bmax + 1) > self._cu and bpost in ("1", "l2"):
                 mm.stage_flags |= 2 | STAGE_POST_EXTRA_ROWBWD
-            # prodlda_bwd at K <= 64: one 16-wave workgroup per tile (~61 KB of LDS, two per
-            # CU) -- M clients' tiles beyond two per CU run in a second round (592 on 512
-            # slots at M = 8, V = 4.7k); the alternative, each workgroup walking t tiles
+            # prodlda_bwd at K <= 64: one 16-wave workgroup per tile (~61 KB of LDS; 64 VGPRs
+            # with the batched descriptor copied at entry, gfk_common.h gfk_model: two per CU,
+            # where 80 VGPRs fit one); the alternative, each workgroup walking t tiles
             # (n_dpart = n_tiles / t slabs, the persistent one-range shape, t the smallest
             # that fits one round), measured slower: 0.1492 / 0.1484 ms without vs 0.1535 /
             # 0.1527 with (profiles/r5/ab_batch.txt) -- a tile's staging round is not hidden

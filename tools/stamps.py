@@ -50,6 +50,7 @@ def main(argv=None):
     p.add_argument("--docs", type=int, default=1000)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--ctx", type=int, default=0, help="contextual size: CombinedTM when > 0")
+    p.add_argument("--bf16", action="store_true", help="matmul_dtype='bf16' (contextual GEMMs)")
     p.add_argument("--so", default=None, help="a prebuilt -DGFK_STAMPS library (--build-only)")
     p.add_argument("--build-only", action="store_true", help="build it on the host and stop")
     a = p.parse_args(argv)
@@ -67,6 +68,8 @@ def main(argv=None):
     kw = dict(input_size=a.vocab, n_components=a.topics,
               hidden_sizes=tuple(int(h) for h in a.hidden.split(",")), batch_size=a.batch,
               verbose=False, backend="fused", device="cuda")
+    if a.bf16:
+        kw["matmul_dtype"] = "bf16"
     tm = CombinedTM(contextual_size=a.ctx, **kw) if a.ctx else AVITM(**kw)
     X = random_csr(a.docs, a.vocab, a.nnz, seed=0)
     ctx = (np.random.default_rng(1).standard_normal((a.docs, a.ctx)).astype(np.float32)
