@@ -11,6 +11,7 @@
 // on segments flagged for FedAvg, multiplies the result by w_i = n_i / sum n so
 // the following all-reduce(SUM) directly yields the sample-weighted average.
 // float4 vectorised: segment bounds are multiples of 4 floats.
+#define GFK_BATCHED_COPY 1   // batched kernels copy their descriptor (gfk_common.h gfk_model)
 #include "gfk_common.h"
 
 using namespace gfk;

@@ -30,6 +30,7 @@
 // In the backward the C dimension is split across workgroups so the grid covers the
 // chip even for a small vocabulary; that split also spreads the Wa Adam traffic
 // (p / m / v of V x C floats), which is what bounds it.
+#define GFK_BATCHED_COPY 1   // batched kernels copy their descriptor (gfk_common.h gfk_model)
 #include "gfk_common.h"
 
 using namespace gfk;

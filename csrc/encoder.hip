@@ -20,6 +20,8 @@
 // random draws (Philox, keyed by seed/step/element) are produced here, where the
 // VALU is otherwise idle waiting on the gather.  Everything up to the heads is
 // row-local; the batch coupling (batch-norm) starts in post_fwd.
+// (batched descriptor by reference: with the copy (gfk_common.h gfk_model) the narrow
+// instance ran 14.5 -> 20 us at M = 8, profiles/r5/ab_batched_copy2.txt)
 #include "gfk_common.h"
 
 using namespace gfk;

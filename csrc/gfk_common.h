@@ -224,8 +224,16 @@ constexpr int GFK_BMAX_LIMIT = 512;
 __host__ __device__ __forceinline__ int gfk_hlast(const GfkModel& m) {
   int h = m.H[0];
 #pragma unroll
-  for (int l = 1; l < GFK_MAX_LAYERS; ++l)
-    if (l < m.n_hidden) h = m.H[l];
+  for (int l = 1; l < GFK_MAX_LAYERS; ++l) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    // (readfirstlane: each field's load stays its own -- a select of the loaded values would
+    // be folded into one load from a selected offset)
+    const int hl = __builtin_amdgcn_readfirstlane(m.H[l]);
+#else
+    const int hl = m.H[l];
+#endif
+    if (l < m.n_hidden) h = hl;
+  }
   return h;
 }
 __host__ __device__ inline bool gfk_postfold(const GfkModel& m) {
@@ -350,6 +358,10 @@ __device__ __forceinline__ const GfkModel& gfk_model(const GfkArgT<false>& a) { 
 // (64-bit VGPR addresses): the batched ProdLDA backward needed 80 VGPRs, 64 with the copy.
 // A runtime index into one of its arrays keeps the copy in scratch: those sources keep the
 // reference.
+// (a kernel whose copy would not fit the scalar registers -- SGPR spills land in VGPR lanes --
+// takes gfk_model_ref)
+__device__ __forceinline__ const GfkModel& gfk_model_ref(const GfkArgT<false>& a) { return a.m; }
+__device__ __forceinline__ const GfkModel& gfk_model_ref(const GfkArgT<true>& a) { return a.p[gfk_bz()]; }
 #if GFK_BATCHED_COPY
 __device__ __forceinline__ GfkModel gfk_model(const GfkArgT<true>& a) { return a.p[gfk_bz()]; }
 #else

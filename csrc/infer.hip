@@ -25,6 +25,7 @@
 // Philox call (Box-Muller, both branches) and reduces each sample's softmax
 // with wave shuffles.  Draws are keyed by (seed, global document index, topic),
 // so the result does not depend on the grid or on how the corpus is chunked.
+#define GFK_BATCHED_COPY 1   // batched kernels copy their descriptor (gfk_common.h gfk_model)
 #include "gfk_common.h"
 
 using namespace gfk;

@@ -24,6 +24,7 @@
 //   post_bwd  : column sums of dmu, dls (all rows), own row: BN backward ->
 //               d mu_raw, d ls_raw, heads and hidden-layer backward -> dz of every
 //               layer.  Workgroup 0: prior gradients, the loss, the step counter.
+#define GFK_BATCHED_COPY 1   // batched kernels copy their descriptor (gfk_common.h gfk_model)
 #include "gfk_common.h"
 
 using namespace gfk;
@@ -787,7 +788,7 @@ __device__ __forceinline__ void post_prior_sums(int K, int nb, const float* mu, 
 // CUs (one 16-wave workgroup per CU) where bmax + 1 ran in three
 template <bool InLds, bool Staged, bool GB = false, bool PS = false, int R = 1>
 __global__ void __launch_bounds__(FT) gfk_post_bwd_k(GfkArgT<GB> ga) {
-  const GfkModel& m = gfk_model(ga);
+  const GfkModel& m = gfk_model_ref(ga);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   int K = m.K, B = m.bmax, nh = m.n_hidden, sflags = m.stage_flags;
   const float *dmu_g = m.ws_dmu, *dls_g = m.ws_dls, *mu_g = m.ws_mu, *ls_g = m.ws_ls;

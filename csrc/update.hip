@@ -22,6 +22,7 @@
 //     gradient (gradient mode).
 // Deterministic, no atomics, W_in's gradient is never materialised in fused mode.
 // One extra workgroup prepares the next minibatch (gfk_common.h).
+#define GFK_BATCHED_COPY 1   // batched kernels copy their descriptor (gfk_common.h gfk_model)
 #include "gfk_common.h"
 
 using namespace gfk;
