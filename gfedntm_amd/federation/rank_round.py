@@ -174,7 +174,9 @@ class MultiClientRound:
                 c.enable_graph(False)     # the round graph carries every client's step
         if self.fused:
             prepare_local_fedavg(self.shared)
-        self._g = None
+        self._g = None                    # the one-round graph
+        self._gk: Dict[int, object] = {}  # k-round graphs (k > 1)
+        self._bss: Dict[int, object] = {}  # the BatchedSteps each graph was captured with
         self._gens = None
         self._streams = None
         self._side = None
@@ -211,7 +213,18 @@ class MultiClientRound:
             self._reduce_part(part)
         ev_join.record(side)
 
-    def _capture(self):
+    def rounds_per_replay(self) -> int:
+        """Rounds one graph replay may carry (GFEDNTM_ROUNDS_PER_GRAPH, default 16): every
+        round is device-driven (the batch, the step counter, the FedAvg and the in-graph
+        xGMI all-reduce), so k consecutive rounds captured back to back are the same work
+        as k replays of the one-round graph -- without the k - 1 graph-to-graph dispatch
+        gaps (~8 us each between one-round replays at 8 clients, 0.125 ms rounds).  1 when
+        something runs between rounds (RCCL outside the graph, the eager path)."""
+        if not self.graph or (self.colls and not self.coll_in_graph):
+            return 1
+        return max(1, int(os.environ.get("GFEDNTM_ROUNDS_PER_GRAPH", "16")))
+
+    def _capture(self, k: int = 1):
         engines = [c.tm.engine for c in self.clients]
         for e in engines:
             e.prepare_external_capture()
@@ -235,16 +248,18 @@ class MultiClientRound:
                         hooks[at] = (lambda p=part: self._fork(p))
                         forked.add(part)
             with graph_capture(g):
-                bs.launch(after=hooks or None)
-                if self.coll_in_graph or not self.colls:
-                    for part in self.parts:
-                        if part not in forked:
-                            self._reduce_part(part)
-                    if forked:
-                        torch.cuda.current_stream(self.device).wait_event(self._side[1])
-                else:
-                    self._fold("rest", LOCAL_FIRST)
-            self._g, self._batched = g, bs
+                for _ in range(k):
+                    bs.launch(after=hooks or None)
+                    if self.coll_in_graph or not self.colls:
+                        for part in self.parts:
+                            if part not in forked:
+                                self._reduce_part(part)
+                        if forked:
+                            torch.cuda.current_stream(self.device).wait_event(self._side[1])
+                    else:
+                        self._fold("rest", LOCAL_FIRST)
+            self._batched = bs
+            self._bss[k] = bs             # (its device tables are baked into the graph)
         else:
             if self._streams is None:
                 self._streams = [torch.cuda.Stream(self.device) for _ in engines]
@@ -252,29 +267,59 @@ class MultiClientRound:
             with graph_capture(g):
                 main = torch.cuda.current_stream(self.device)
                 fork = torch.cuda.Event()
-                fork.record(main)
-                for e, st, ev in zip(engines, self._streams, joins):
-                    st.wait_event(fork)
-                    with torch.cuda.stream(st):
-                        e.launch_step_phases()
-                    ev.record(st)
-                for ev in joins:
-                    main.wait_event(ev)
-                if self.coll_in_graph or not self.colls:
-                    for part in self.parts:
-                        self._reduce_part(part)
-                else:
-                    self._fold("rest", LOCAL_FIRST)
+                for _ in range(k):
+                    fork.record(main)
+                    for e, st, ev in zip(engines, self._streams, joins):
+                        st.wait_event(fork)
+                        with torch.cuda.stream(st):
+                            e.launch_step_phases()
+                        ev.record(st)
+                    for ev in joins:
+                        main.wait_event(ev)
+                    if self.coll_in_graph or not self.colls:
+                        for part in self.parts:
+                            self._reduce_part(part)
+                    else:
+                        self._fold("rest", LOCAL_FIRST)
+        if k == 1:
             self._g = g
+        else:
+            self._gk[k] = g
         self._gens = tuple(e.graph_gen for e in engines)
 
-    def step(self, it: int, hb=None):
+    def step(self, it: int, hb=None, k: int = 1):
+        """Rounds it .. it + k - 1 (k > 1: one replay of the k-round graph; the caller
+        keeps every round that needs the host between rounds out of such a run)."""
+        if k > 1:
+            if not self.graph or k > self.rounds_per_replay():
+                raise ValueError(f"{k} rounds per replay on this round object")
+            engines = [c.tm.engine for c in self.clients]
+            for e in engines:
+                e.sync_step_counter(it)
+            if self._gens != tuple(e.graph_gen for e in engines):
+                self._g = None
+                self._gk.clear()
+                self._bss.clear()
+            if k not in self._gk:
+                self._capture(k)
+            self._gk[k].replay()
+            for e in engines:
+                e.advance_host_step(it + k - 1)
+            if hb is not None:
+                for r in range(it, it + k):
+                    hb.mark(r, 1)
+            return
+        self._step1(it, hb)
+
+    def _step1(self, it: int, hb=None):
         if self.graph:
             engines = [c.tm.engine for c in self.clients]
             for e in engines:
                 e.sync_step_counter(it)
-            if self._g is not None and self._gens != tuple(e.graph_gen for e in engines):
+            if self._gens != tuple(e.graph_gen for e in engines):
                 self._g = None
+                self._gk.clear()
+                self._bss.clear()
             if self._g is None:
                 self._capture()
             self._g.replay()
@@ -348,6 +393,8 @@ class MultiClientRound:
 
     def close(self):
         self._g = None
+        self._gk.clear()
+        self._bss.clear()
         for c in self.colls.values():
             if c.xgmi is not None:
                 c.xgmi.close()

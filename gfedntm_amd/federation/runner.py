@@ -661,11 +661,45 @@ def _round_loop(rr, clients, client_ids, cmap, world, rank, device, ctrl, hb, lo
     t0 = time.perf_counter()
     timed_from = start
     last = start - 1
+    # several rounds per graph replay (MultiClientRound.rounds_per_replay): a run of rounds
+    # ends at every round after which the host needs the state -- the aligned / epoch-end
+    # rounds, the warmup, poll, digest, metrics and checkpoint boundaries, the last round
+    # (and never with a round hook, an injected corruption or the comm debug log)
+    kmax = getattr(rr, "rounds_per_replay", lambda: 1)()
+    if round_hook is not None or corrupt_from is not None or debug_comm:
+        kmax = 1
+    ends = set(align) | {stop_after}
+    if kmax > 1:
+        for c in clients:
+            ends.update(int(i) for i in np.flatnonzero(c.plan.epoch_end))
+        if timing_warmup:
+            ends.add(start + timing_warmup - 1)
+
+    def run_end(it: int) -> int:
+        r = it
+        while r < it + kmax - 1 and r not in ends:
+            n1 = r + 1
+            if ((poll_every and n1 % poll_every == 0) or (digest_every and n1 % digest_every == 0)
+                    or (metrics_every and n1 % metrics_every == 0)
+                    or (checkpoint_dir and checkpoint_every and n1 % checkpoint_every == 0)):
+                break
+            r += 1
+        return r
+
+    covered = start - 1
     with trace_range("rounds"):
         for it in range(start, stop_after + 1):
             if hb is not None:
                 hb.mark(it, 0)
-            rr.step(it, hb)
+            if it > covered:
+                k = run_end(it) - it + 1 if kmax > 1 else 1
+                if k > 1:
+                    rr.step(it, hb, k)
+                else:
+                    rr.step(it, hb)
+                covered = it + k - 1
+            elif hb is not None:
+                hb.mark(it, 1)
             if corrupt_from is not None and it >= corrupt_from:
                 _flip_word(clients[0].shared)
             if debug_comm and it < start + 16:
