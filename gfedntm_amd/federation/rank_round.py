@@ -72,11 +72,28 @@ class SingleClientRound:
     def xgmi(self) -> bool:
         return bool(self.in_step) and self.in_step.startswith("xgmi")
 
-    def step(self, it: int, hb=None):
-        """Enqueue round ``it``; ``hb`` (parallel/heartbeat.py) is marked in the
-        all-reduce phase once the local step is enqueued (a peer stuck before its step
-        is then behind this rank)."""
+    def rounds_per_replay(self) -> int:
+        """Rounds one replay may carry (MultiClientRound.rounds_per_replay): the fused
+        engine's k-step graph, the all-reduce inside it (or none: one rank)."""
         c = self.client
+        if not (c.fused and self.agg_mode == "params" and c.tm.engine.steps_per_replay_ok()
+                and (self.in_step is not None or self.agg.world == 1)):
+            return 1
+        return max(1, int(os.environ.get("GFEDNTM_ROUNDS_PER_GRAPH", "16")))
+
+    def step(self, it: int, hb=None, k: int = 1):
+        """Enqueue round ``it`` (k > 1: rounds it .. it + k - 1 in one replay); ``hb``
+        (parallel/heartbeat.py) is marked in the all-reduce phase once the local step is
+        enqueued (a peer stuck before its step is then behind this rank)."""
+        c = self.client
+        if k > 1:
+            if k > self.rounds_per_replay():
+                raise ValueError(f"{k} rounds per replay on this round object")
+            c.tm.engine.step_k(it, k)
+            if hb is not None:
+                for r in range(it, it + k):
+                    hb.mark(r, 1)
+            return
         c.local_step(it)
         if hb is not None:
             hb.mark(it, 1)

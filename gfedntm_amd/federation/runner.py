@@ -692,7 +692,9 @@ def _round_loop(rr, clients, client_ids, cmap, world, rank, device, ctrl, hb, lo
             if hb is not None:
                 hb.mark(it, 0)
             if it > covered:
-                k = run_end(it) - it + 1 if kmax > 1 else 1
+                # (a power of two: at most log2(kmax) + 1 graphs are ever captured -- a
+                # capture inside the timed rounds costs milliseconds)
+                k = 1 << ((run_end(it) - it + 1).bit_length() - 1) if kmax > 1 else 1
                 if k > 1:
                     rr.step(it, hb, k)
                 else:

@@ -349,6 +349,7 @@ class FusedEngine(EngineBase):
         self._host_step = 0
         self.graph_enabled = False
         self._graph = None
+        self._graphs_k = {}
         self.graph_gen = 0
         self._graph_key = None
         self._comm = None
@@ -1443,6 +1444,7 @@ class FusedEngine(EngineBase):
         # the generation lets external captures (LocalFederation's round graph) see that
         # the kernel arguments / buffers they baked in are stale
         self._graph = None
+        self._graphs_k = {}
         self.graph_gen += 1
 
     @property
@@ -1468,7 +1470,7 @@ class FusedEngine(EngineBase):
         self.graph_enabled = on
         self._invalidate_graph()
 
-    def _capture(self):
+    def _capture(self, k: int = 1):
         # warm-up on a side stream is not needed: no lazy allocation in gfk_run
         if self.host_gemm_fallback:
             self._warm_host_gemms()
@@ -1477,13 +1479,17 @@ class FusedEngine(EngineBase):
         saved = (self.d_step.clone(), self.adam_t.clone(), self.adam_pow.clone(),
                  self.adam_coef.clone())
         with graph_capture(g):
-            self._launch(self.phases())
+            for _ in range(k):
+                self._launch(self.phases())
         # capture does not execute; restore the device counters defensively
         self.d_step.copy_(saved[0])
         self.adam_t.copy_(saved[1])
         self.adam_pow.copy_(saved[2])
         self.adam_coef.copy_(saved[3])
-        self._graph = g
+        if k == 1:
+            self._graph = g
+        else:
+            self._graphs_k[k] = g
 
     def warm_graph(self):
         """Capture the step graph now (no execution), so the first timed / collective
@@ -1551,6 +1557,30 @@ class FusedEngine(EngineBase):
             agg.allreduce_(buf)
         self._host_step = s + 1
         return self.loss_hist[s]
+
+    def steps_per_replay_ok(self) -> bool:
+        """Several steps may share one graph replay (:meth:`step_k`): the graph is on and
+        nothing runs on the host between steps (no eager all-reduce)."""
+        return self.graph_enabled and not (self._comm is not None and self._comm["mode"] == "eager")
+
+    def step_k(self, s: int, k: int) -> torch.Tensor:
+        """Steps s .. s + k - 1 in one replay of a k-step graph (the step is device-driven:
+        its batch, counter and in-graph all-reduce), the same work as k :meth:`step` calls
+        without the graph-to-graph gaps."""
+        if k <= 1:
+            return self.step(s)
+        if self.plan is None:
+            raise RuntimeError("bind_data() first")
+        if not self.steps_per_replay_ok():
+            raise RuntimeError("step_k needs the step graph and no host-side collective")
+        self.sync_step_counter(s)
+        g = self._graphs_k.get(k)
+        if g is None:
+            self._capture(k)
+            g = self._graphs_k[k]
+        g.replay()
+        self._host_step = s + k
+        return self.loss_hist[s + k - 1]
 
     # ------------------------------------------------------------------ misc
     def optimizer_state_dict(self):
