@@ -81,6 +81,19 @@ class SingleClientRound:
             return 1
         return max(1, int(os.environ.get("GFEDNTM_ROUNDS_PER_GRAPH", "16")))
 
+    def prewarm(self, kmax: int):
+        """Capture the engine's 1, 2, 4, .. kmax-step graphs now (a capture inside the
+        timed rounds costs milliseconds)."""
+        e = self.client.tm.engine
+        if self.rounds_per_replay() <= 1 or e.plan is None:
+            return
+        e.warm_graph()
+        k = 2
+        while k <= kmax:
+            if k not in e._graphs_k:
+                e._capture(k)
+            k *= 2
+
     def step(self, it: int, hb=None, k: int = 1):
         """Enqueue round ``it`` (k > 1: rounds it .. it + k - 1 in one replay); ``hb``
         (parallel/heartbeat.py) is marked in the all-reduce phase once the local step is
@@ -240,6 +253,23 @@ class MultiClientRound:
         if not self.graph or (self.colls and not self.coll_in_graph):
             return 1
         return max(1, int(os.environ.get("GFEDNTM_ROUNDS_PER_GRAPH", "16")))
+
+    def prewarm(self, kmax: int):
+        """Capture the 1, 2, 4, .. kmax-round graphs now (SingleClientRound.prewarm)."""
+        if self.rounds_per_replay() <= 1:
+            return
+        engines = [c.tm.engine for c in self.clients]
+        if self._gens != tuple(e.graph_gen for e in engines):
+            self._g = None
+            self._gk.clear()
+            self._bss.clear()
+        if self._g is None:
+            self._capture()
+        k = 2
+        while k <= kmax:
+            if k not in self._gk:
+                self._capture(k)
+            k *= 2
 
     def _capture(self, k: int = 1):
         engines = [c.tm.engine for c in self.clients]

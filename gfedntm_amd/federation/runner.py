@@ -174,6 +174,8 @@ class LocalFederation:
                               os.environ.get("GFEDNTM_ROUND_BATCHED", "1") == "1")
         self._batched = None
         self._rg = None
+        self._rgk = {}                    # k -> (the k-round graph, the launches it baked in)
+        self._rg_gens = None
         self._stop = False
         if self.round_graph:
             for c in self.clients:
@@ -192,7 +194,7 @@ class LocalFederation:
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
 
-    def _capture_round(self):
+    def _capture_round(self, k: int = 1):
         engines = [c.tm.engine for c in self.clients]
         for e in engines:
             e.prepare_external_capture()
@@ -218,54 +220,92 @@ class LocalFederation:
                 for b in self._batched_parts:
                     b.prepare()
                 with graph_capture(g):
-                    for b in self._batched_parts:
-                        b.launch()
-                    if not self.agg.fused_sum_(shared):
-                        raise RuntimeError("round graph needs the native FedAvg kernel")
-                self._rg = g
-                self._rg_gens = self._engine_gens()
+                    for _ in range(k):
+                        for b in self._batched_parts:
+                            b.launch()
+                        if not self.agg.fused_sum_(shared):
+                            raise RuntimeError("round graph needs the native FedAvg kernel")
+                self._store_round_graph(g, k)
                 return
         if self.round_streams:
             streams = [torch.cuda.Stream(self.device) for _ in engines]
             joins = [torch.cuda.Event() for _ in engines]
         with graph_capture(g):
-            if self.round_streams:
-                main = torch.cuda.current_stream(self.device)
-                fork = torch.cuda.Event()
-                fork.record(main)
-                for e, st, ev in zip(engines, streams, joins):
-                    st.wait_event(fork)
-                    with torch.cuda.stream(st):
+            main = torch.cuda.current_stream(self.device)
+            fork = torch.cuda.Event()
+            for _ in range(k):
+                if self.round_streams:
+                    fork.record(main)
+                    for e, st, ev in zip(engines, streams, joins):
+                        st.wait_event(fork)
+                        with torch.cuda.stream(st):
+                            e.launch_step_phases()
+                        ev.record(st)
+                    for ev in joins:
+                        main.wait_event(ev)
+                else:
+                    for e in engines:
                         e.launch_step_phases()
-                    ev.record(st)
-                for ev in joins:
-                    main.wait_event(ev)
-            else:
-                for e in engines:
-                    e.launch_step_phases()
-            if not self.agg.fused_sum_(shared):
-                raise RuntimeError("round graph needs the native FedAvg kernel")
-        self._rg = g
+                if not self.agg.fused_sum_(shared):
+                    raise RuntimeError("round graph needs the native FedAvg kernel")
+        self._store_round_graph(g, k)
+
+    def _store_round_graph(self, g, k: int):
+        if self._rg_gens != self._engine_gens():
+            self._rgk = {}
+        self._rgk[k] = (g, self._batched_parts if self._batched is not None else None)
+        if k == 1:
+            self._rg = g
         self._rg_gens = self._engine_gens()
 
     def _engine_gens(self):
         return tuple(c.tm.engine.graph_gen for c in self.clients)
 
-    def _round_graph_step(self, it: int):
+    def _round_graph_step(self, it: int, k: int = 1):
         for c in self.clients:
             c.tm.engine.sync_step_counter(it)     # no-op unless resuming / out of sequence
-        if self._rg is not None and self._rg_gens != self._engine_gens():
-            self._rg = None           # an engine was rebound / reconfigured since the capture
-        if self._rg is None:
-            self._capture_round()
-        self._rg.replay()
+        if self._rg_gens != self._engine_gens():
+            self._rg, self._rgk = None, {}  # an engine was rebound / reconfigured since the capture
+        if k not in self._rgk:
+            self._capture_round(k)
+        self._rgk[k][0].replay()
         for c in self.clients:
-            c.tm.engine.advance_host_step(it)
+            c.tm.engine.advance_host_step(it + k - 1)
 
-    def _round(self, it: int):
-        """Every client's local step and the FedAvg of round ``it`` (enqueued)."""
+    def prewarm(self, kmax: int):
+        """Capture the 1, 2, 4, .. kmax-round graphs now: a capture costs milliseconds,
+        which must not land inside timed rounds."""
+        if self._rg_gens != self._engine_gens():
+            self._rg, self._rgk = None, {}
+        k = 1
+        while k <= kmax:
+            if k not in self._rgk:
+                self._capture_round(k)
+            k *= 2
+
+    def rounds_per_replay(self) -> int:
+        """Rounds one replay of the round graph may carry (rank_round.MultiClientRound.
+        rounds_per_replay; GFEDNTM_ROUNDS_PER_GRAPH, default 16)."""
+        if not self.round_graph:
+            return 1
+        return max(1, int(os.environ.get("GFEDNTM_ROUNDS_PER_GRAPH", "16")))
+
+    def _run_end(self, it: int, kmax: int, ends, timed_end: int) -> int:
+        r = it
+        while r < it + kmax - 1 and r not in ends and r != timed_end:
+            n1 = r + 1
+            if ((self.metrics_every and n1 % self.metrics_every == 0)
+                    or (self.checkpoint_dir and self.checkpoint_every
+                        and n1 % self.checkpoint_every == 0)):
+                break
+            r += 1
+        return r
+
+    def _round(self, it: int, k: int = 1):
+        """Every client's local step and the FedAvg of round ``it`` (enqueued; k > 1:
+        rounds it .. it + k - 1 in one replay of the round graph)."""
         if self.round_graph:
-            self._round_graph_step(it)
+            self._round_graph_step(it, k)
             return
         for c in self.clients:
             c.local_step(it)
@@ -291,9 +331,22 @@ class LocalFederation:
         win = RoundWindow(self._sync)
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) \
             if (self.device.type == "cuda" and timing_warmup) else None
+        kmax = self.rounds_per_replay()
+        ends = {self.max_iters - 1}
+        if kmax > 1:
+            self.prewarm(kmax)
+            for c in self.clients:
+                ends.update(int(i) for i in np.flatnonzero(c.plan.epoch_end))
+        timed_end = start + timing_warmup - 1 if timing_warmup else -1
+        covered = start - 1
         with trace_range("rounds"):
             for it in range(self.round, self.max_iters):
-                self._round(it)
+                if it > covered:
+                    k = 1
+                    if kmax > 1:      # (power-of-two runs: few captures, MultiClientRound)
+                        k = 1 << ((self._run_end(it, kmax, ends, timed_end) - it + 1).bit_length() - 1)
+                    self._round(it, k)
+                    covered = it + k - 1
                 done = [c.end_round(it) for c in self.clients]
                 self._after_round(it, win, done)
                 last = it
@@ -686,6 +739,8 @@ def _round_loop(rr, clients, client_ids, cmap, world, rank, device, ctrl, hb, lo
             r += 1
         return r
 
+    if kmax > 1 and hasattr(rr, "prewarm"):
+        rr.prewarm(kmax)              # every k-round graph captured before the first round
     covered = start - 1
     with trace_range("rounds"):
         for it in range(start, stop_after + 1):
