@@ -1671,9 +1671,18 @@ class BatchedSteps:
             # layout: one tile per CU, the fastest for ONE client); "pf" -- the 8-wave
             # prefetching variant, two per CU (round 4); "keep" -- the engines' choice
             # (fill only where it is one round: 16-wave ring workgroups are one per CU)
+            # (the strips are grid-strided: a workgroup's wave group g takes tiles g grid + x,
+            # so any grid works; "fill" takes the FEWEST tiles per workgroup, T in 1..4, whose
+            # M ceil(n_tiles / T) workgroups still fit one round of the CUs -- T = 3 at M = 8,
+            # V = 4.7k: 192 workgroups of 12 busy waves instead of 144 of 16; "fill4": T = 4)
             bstrip = os.environ.get("GFEDNTM_BATCH_STRIP", "fill")
             fill = -(-mm.n_tiles // 4)
-            if (mm.stage_flags & STAGE_FWD_STRIP and M > 1 and bstrip == "fill"
+            if bstrip == "fill":
+                for t in (1, 2, 3, 4):
+                    if M * -(-mm.n_tiles // t) <= self._cu:
+                        fill = -(-mm.n_tiles // t)
+                        break
+            if (mm.stage_flags & STAGE_FWD_STRIP and M > 1 and bstrip in ("fill", "fill4")
                     and mm.stage_flags & STAGE_FWD_STRIP_RING and mm.dec_grid == mm.n_tiles
                     and M * fill <= self._cu):
                 mm.dec_grid = fill

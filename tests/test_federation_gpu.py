@@ -226,7 +226,7 @@ def test_batched_round_matches_branch_round(model_type):
 @pytest.mark.parametrize("strip", ["fill", "pf"])
 def test_batched_large_round_variants_match_branch_round(monkeypatch, strip):
     """8 clients at the headline's vocabulary (~74 tiles each): the batched launch switches
-    the strip forward to 4 tiles per 16-wave workgroup ("fill", the default; "pf": the
+    the strip forward to 3-4 tiles per 16-wave workgroup ("fill", the default; "pf": the
     8-wave prefetching variant), prodlda_bwd to workgroups walking several tiles, post_bwd's
     batch-level workgroup into row_bwd, and win_update to its 8-wave tile shape (all
     clients' tiles exceed two rounds of 16-wave workgroups).  The round must still agree
@@ -253,7 +253,9 @@ def test_batched_large_round_variants_match_branch_round(monkeypatch, strip):
     from gfedntm_amd.ops.engine import STAGE_FWD_POSTFOLD
     if strip == "fill":
         # the ring forward with the posterior folded in (post_fwd not launched)
-        assert host.dec_grid == -(-host.n_tiles // 4) and host.stage_flags & STAGE_FWD_STRIP_RING
+        # (the fewest tiles per workgroup whose 8 clients' workgroups fit one round)
+        t = next(t for t in (1, 2, 3, 4) if 8 * -(-host.n_tiles // t) <= cu)
+        assert host.dec_grid == -(-host.n_tiles // t) and host.stage_flags & STAGE_FWD_STRIP_RING
         assert host.stage_flags & STAGE_FWD_POSTFOLD and abi.PH_POST_FWD not in a._batched._phases
     else:
         # the prefetching variant has no fold: post_fwd runs
