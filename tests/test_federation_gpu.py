@@ -270,3 +270,52 @@ def test_batched_large_round_variants_match_branch_round(monkeypatch, strip):
         assert int((diff > 1e-5).sum()) <= 0.01 * diff.numel()
         torch.testing.assert_close(x.tm.engine.loss_hist[:1], y.tm.engine.loss_hist[:1],
                                    rtol=1e-6, atol=1e-3)
+
+
+@pytest.mark.parametrize("batched", [True, False])
+def test_multi_round_replays_are_bitwise_one_round_replays(monkeypatch, batched):
+    """GFEDNTM_ROUNDS_PER_GRAPH: k rounds captured back to back in one graph (runs ending at
+    the epoch ends, power-of-two lengths, every graph captured before the first round) give
+    the same state and losses, bit for bit, as one replay per round -- and the engine's
+    k-step graph (FusedEngine.step_k) the same as k step() calls."""
+    sc = generate_synthetic(vocab_size=600, n_topics=10, n_docs=200, n_nodes=4, frozen_topics=2,
+                            nwords=(40, 80), seed=9)
+    corpora = [ClientCorpus(synthetic=sc, node=i) for i in range(4)]
+    out = {}
+    for k in ("1", "16"):
+        monkeypatch.setenv("GFEDNTM_ROUNDS_PER_GRAPH", k)
+        fed = LocalFederation(corpora, _params(num_epochs=3), max_iters=37, device="cuda",
+                              backend="fused", seed=3, graph=True, round_batched=batched)
+        assert fed.rounds_per_replay() == int(k)
+        fed.run()
+        torch.cuda.synchronize()
+        out[k] = ([c.shared.clone() for c in fed.clients],
+                  [c.tm.engine.loss_hist[:37].clone() for c in fed.clients])
+        if k == "16":
+            assert 16 in fed._rgk and 1 in fed._rgk
+    for a, b in zip(out["1"][0] + out["1"][1], out["16"][0] + out["16"][1]):
+        assert torch.equal(a, b)
+
+
+def test_engine_step_k_is_bitwise_k_steps():
+    from gfedntm_amd.data.bow import BatchPlan, DeviceCSR
+    from gfedntm_amd.models import AVITM
+    from tests.helpers import random_csr
+    X = random_csr(400, 2000, 40, seed=2)
+    res = []
+    for mode in ("step", "step_k"):
+        torch.manual_seed(0)
+        tm = AVITM(backend="fused", input_size=2000, n_components=20, hidden_sizes=(50, 50),
+                   batch_size=64, verbose=False, device="cuda")
+        e = tm.engine
+        e.bind_data(DeviceCSR(X, "cuda"), BatchPlan.build(400, 64, 24, seed=0))
+        e.enable_graph(True)
+        if mode == "step":
+            for s in range(24):
+                e.step(s)
+        else:
+            e.step_k(0, 8)
+            e.step_k(8, 16)
+        torch.cuda.synchronize()
+        res.append((tm.flat.buffer.clone(), e.loss_hist[:24].clone()))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
