@@ -324,6 +324,9 @@ def run_multi(args, rank, world, device, rehearse):
             + f", {out['allreduce'] or 'no'} all-reduce across ranks)")
         rec["path"] = "run_distributed"
         rec["engine_ran"] = out["clients"][0].tm.engine_info
+        # the in-rank FedAvg of a multi-client rank: inside the update kernels' epilogues
+        # (csrc gfk_bwd_fold_k / gfk_win_fold_k) or the fold kernel after the batched steps
+        rec["fedavg_plan"] = getattr(out["round"], "fold_plan", None)
         rec["digests"] = out.get("digests")
         if fallback:
             rec["allreduce_fallback"] = fallback

@@ -294,6 +294,21 @@ typedef struct GfkAdam {
   uint64_t* dbg;                     // diagnostic stamps (GFK_STAMPS builds)
 } GfkAdam;
 
+// In-epilogue FedAvg of a rank's batched clients (round 6; csrc/prodlda.hip gfk_bwd_fold_k,
+// csrc/update.hip gfk_win_fold_k): the kernels that finish the shared tensors take one tile
+// for ALL M clients of the launch, in client order, and write the client-order sum of the
+// pre-scaled results once -- no per-client post-Adam copies, no fold kernel after the round.
+// left: [n_left][2] (first float, floats) pieces of the shared prefix that no update job owns
+// (batch-norm running statistics): summed in client order by extra workgroups.
+// mode: 0 writes the sum into every client's buffer (one rank: the round's FedAvg is done),
+// 1 into client 0's only (the rank's partial sum, all-reduced over the ranks and broadcast).
+typedef struct GfkFold {
+  const GfkModel* models;        // device array [M] (the batched launch's descriptors)
+  const GfkUpdate* upds;         // device array [M]
+  const int64_t* left;
+  int32_t M, mode, n_left, nj;   // nj: W_in hidden slices of 16 columns (ceil(H0 / 16))
+} GfkFold;
+
 }  // extern "C"
 
 // launch helpers: grid z = the batched models, the kernel argument = the device array

@@ -2028,6 +2028,265 @@ extern "C" size_t gfk_prodlda_fwd_smem(const GfkModel* m) {
   return sizeof(float) * ((size_t)m->bmax * m->kt + KP * LDB_F + 8 * VB);
 }
 
+// ---------------------------------------------------------------------------------------
+// gfk_bwd_fold_k: the ProdLDA backward of M batched clients with their FedAvg fold in the
+// epilogue (csrc/gfk_common.h GfkFold; reference round: server.py:477-521 averages every
+// client's post-step state, federated_model.py:117-131).
+//
+// After a FedAvg every client holds the same beta, so one workgroup takes vocabulary tile t
+// x 16-topic slice q for ALL clients, in client order: stage the client's logit tile,
+// theta_d slice, lse / S / column rstd, rebuild dlogit (the sparse -x p / (p + 1e-10)
+// terms, the dense p S and the column BN backward), d theta_d[:, slice] partial (stored per
+// client: row_bwd sums the slabs as before), dbeta[slice, tile], Adam with that client's
+// m / v, the pre-scale w_c -- and add the result to a register accumulator.  beta is read
+// once (before the loop) and written once, after the last client.  The next client's
+// loads are issued while the current one computes (registers, then LDS at the top of its
+// turn), so the walk costs about one staging round plus M compute phases.
+// Bit-identical to prodlda_bwd_kernel<64, 1, 1, false> per client (the same dlogit
+// expression and thread mapping per column, the same MFMA sequences: d theta_d over c in
+// steps of 8 into two accumulators, dbeta with the R8 row mapping) followed by
+// gfk_local_fedavg's client-order fold -- tests/test_fold_gpu.py.
+// K <= 64, bmax == 64, fp32 operands, one d theta_d slab per tile (ops/engine.py checks).
+// Grid: the 8-aligned tiles x ceil(K / 16) slices, a tile's slices on one XCD (they read
+// the same client tiles: one HBM fetch, three L2 hits).
+// LDS: zt [64][64] (the z tile, then the G tile) + dt [64][66] + th [64][18] + bt [16][66]
+//      + lse, S [64] + rstd [64]: 42.9 KB, two workgroups per CU.
+namespace {
+constexpr int FB_NT = 512;
+constexpr int FB_THS = 18;       // theta_d slice stride: R8 rows r, r + 8 land 16 banks apart
+constexpr size_t FB_SMEM = sizeof(float) * (64 * VB + 64 * LDD + 64 * FB_THS + 16 * LDB_B + 3 * 64);
+typedef const __attribute__((address_space(4))) GfkModel GfkModelC;
+// the batched descriptors through the constant address space: a client's fields are scalar
+// loads wherever the client loop reaches it
+__device__ __forceinline__ GfkModelC& fold_model(const GfkFold& f, int c) {
+  return ((GfkModelC*)(uintptr_t)f.models)[c];
+}
+}  // namespace
+
+extern "C" __global__ void __launch_bounds__(FB_NT, 2) gfk_bwd_fold_k(GfkFold f) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int BM = 64;
+  float* zt = smem;                 // [BM][VB] z tile (swizzled as ws_zn), then G [16][VB]
+  float* dt = zt + BM * VB;         // [BM][LDD] dlogit
+  float* th = dt + BM * LDD;        // [BM][FB_THS] theta_d columns kb .. kb + 15
+  float* bt = th + BM * FB_THS;     // [16][LDB_B] beta rows kb .. kb + 15 of the tile
+  float* lse = bt + 16 * LDB_B;     // [BM]; sb = lse + BM, rs = lse + 2 BM (one 192-float run)
+  float* sb = lse + BM;
+  float* rs = sb + BM;
+  GfkModelC& m0 = fold_model(f, 0);
+  const int K = m0.K, V = m0.V, ldb = m0.ldb, kt = m0.kt, n_tiles = m0.n_tiles;
+  const int ksub = (K + 15) >> 4;
+  const int bx = blockIdx.x, x8 = bx & 7, jj = bx >> 3;
+  const int q = jj % ksub, tile = (jj / ksub) * 8 + x8;
+  if (tile >= n_tiles) return;
+  const int kb = 16 * q, c0 = tile * VB;
+  const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
+  const int M = f.M;
+  const int nrec = K * ldb * 4;
+  // epilogue elements of this thread: column cl, slice rows kl0 and kl0 + 8 (kl0 = wave)
+  const int cl = tid & 63, kl0 = wave;
+  const int vcol = c0 + cl < V ? (c0 + cl) * 4 : 0x7FFF0000;
+  const int cs = cl ^ ((kl0 & 4) << 2);
+  int voff[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) voff[u] = boff(vcol, min(kb + kl0 + 8 * u, K - 1) * ldb * 4);
+  // sparse pass: row tid / 8, sub tid % 8; dense pass: column tid / 16 (+ 32), row group tid % 16
+  const int xrow = tid >> 3, xsub = tid & 7, dg = tid & 15;
+  const int ntp = n_tiles + 1;
+
+  // ---- beta's slice of the tile, once (every client's copy holds these values) ----
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int kl = (tid >> 6) + 8 * u, c = tid & 63;
+    const float b = m0.beta[min(kb + kl, K - 1) * ldb + min(c0 + c, V - 1)];
+    bt[kl * LDB_B + c] = (kb + kl < K && c0 + c < V) ? b : 0.f;
+  }
+
+  // ---- one client's loads (registers; issue order: the tile extents first, so the
+  //      dependent first-non-zero loads wait for them alone) ----
+  struct Pre {
+    int xe0, xe1, xc, nb;
+    float xv, aux, rm[2], rv[2], cf0, cf1;
+    f32x4 z0, z1;
+    float2 th2;
+  };
+  auto issue = [&](int c, Pre& p) {
+    GfkModelC& mc = fold_model(f, c);
+    const int32_t* ts = mc.ws_tstart + (size_t)xrow * ntp + tile;
+    p.xe0 = ts[0];
+    p.xe1 = ts[1];
+    p.nb = *mc.ws_nb;
+    p.cf0 = mc.adam_coef[0];
+    p.cf1 = mc.adam_coef[1];
+    const f32x4* zs = reinterpret_cast<const f32x4*>(mc.ws_zn + (size_t)tile * BM * VB);
+    p.z0 = zs[tid];
+    p.z1 = zs[tid + FB_NT];
+    {
+      const int col = kb + 2 * (tid & 7);
+      const float2 t2 = *reinterpret_cast<const float2*>(mc.ws_thetad + (size_t)xrow * kt + min(col, kt - 2));
+      p.th2 = make_float2(col < K ? t2.x : 0.f, col + 1 < K ? t2.y : 0.f);
+    }
+    const float* ap = tid < 64 ? mc.ws_lse + tid : tid < 128 ? mc.ws_s + (tid - 64)
+                                                             : mc.ws_col_rstd + c0 + min(tid - 128, 63);
+    p.aux = *ap;
+    const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc((void*)(mc.beta + mc.off_m), 0, nrec, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)(mc.beta + mc.off_v), 0, nrec, 0x00020000);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      p.rm[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rm, voff[u], 0, 0));
+      p.rv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rv, voff[u], 0, 0));
+    }
+  };
+  auto issue_nz = [&](int c, Pre& p) {     // depends on the tile extents
+    GfkModelC& mc = fold_model(f, c);
+    const int xe = min(p.xe0 + xsub, max(p.xe1 - 1, 0));
+    p.xc = mc.indices[xe];
+    p.xv = mc.values[xe];
+  };
+
+  Pre nx;
+  issue(0, nx);
+  issue_nz(0, nx);
+  float acc[2] = {0.f, 0.f};
+  for (int c = 0; c < M; ++c) {
+    GfkModelC& mc = fold_model(f, c);
+    const Pre cu = nx;
+    // ---- this client's tiles into LDS; zero dlogit ----
+    reinterpret_cast<f32x4*>(zt)[tid] = cu.z0;
+    reinterpret_cast<f32x4*>(zt)[tid + FB_NT] = cu.z1;
+    *reinterpret_cast<float2*>(th + xrow * FB_THS + 2 * (tid & 7)) = cu.th2;
+    if (tid < 192) lse[tid] = cu.aux;
+    for (int i = tid; i < BM * LDD / 4; i += FB_NT) reinterpret_cast<f32x4*>(dt)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int nb = cu.nb;
+    lds_barrier();
+    if (c + 1 < M) issue(c + 1, nx);        // lands during this client's compute
+    // ---- (3) sparse term at this tile's non-zeros ----
+    if (xrow < nb) {
+      const float l = lse[xrow];
+      for (int i = 0, e = cu.xe0 + xsub; e < cu.xe1; ++i, e += 8) {
+        const int col = (i == 0 ? cu.xc : mc.indices[e]) - c0;
+        const float x = i == 0 ? cu.xv : mc.values[e];
+        const float p = __expf(zt[xrow * VB + (col ^ zswz(xrow))] - l);
+        dt[xrow * LDD + col] = -x * p / (p + RL_EPS);
+      }
+    }
+    lds_barrier();
+    if (c + 1 < M) issue_nz(c + 1, nx);
+    // ---- (4) dense term p S and the column BN backward: 16 lanes per column ----
+    for (int dcol = tid >> 4; dcol < VB; dcol += FB_NT / 16) {
+      const bool valid = c0 + dcol < V;
+      constexpr int NR = BM / 16;
+      float d[NR], z[NR];
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        const int row = dg + 16 * i;
+        z[i] = zt[row * VB + (dcol ^ zswz(row))];
+        const float p = __expf(z[i] - lse[row]);
+        d[i] = (row < nb && valid) ? p * sb[row] + dt[row * LDD + dcol] : 0.f;
+        s1 += d[i];
+        s2 += d[i] * z[i];
+      }
+      s1 = row16_sum(s1) / (float)nb;
+      s2 = row16_sum(s2) / (float)nb;
+      const float r = valid ? rs[dcol] : 0.f;
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        const int row = dg + 16 * i;
+        dt[row * LDD + dcol] = row < nb ? r * (d[i] - s1 - z[i] * s2) : 0.f;
+      }
+    }
+    lds_barrier();
+    // ---- (5) waves 0-3: d theta_d[rows 16 w.., slice]; (6) waves 4-7: dbeta[slice, strip] ----
+    if (wave < 4) {
+      const float* ap = dt + (wave * 16 + (lane & 15)) * LDD + (lane >> 4);
+      const float* bp = bt + (lane & 15) * LDB_B + (lane >> 4);
+      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int cc = 0; cc < VB; cc += 8) {
+        a0 = mfma16x16x4(ap[cc], bp[cc], a0);
+        a1 = mfma16x16x4(ap[cc + 4], bp[cc + 4], a1);
+      }
+      f32x4 dacc = {0.f, 0.f, 0.f, 0.f};
+      dacc += a0 + a1;
+      float* dpart = mc.ws_dthetad + (size_t)tile * mc.bmax * K;
+      const int k = kb + (lane & 15);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = wave * 16 + (lane >> 4) * 4 + e;
+        if (row < nb && k < K) dpart[(size_t)row * K + k] = dacc[e];
+      }
+    } else {
+      const int cst = wave - 4, g = lane >> 4, gr = 8 * g;
+      const float* ap = th + gr * FB_THS + (lane & 15);
+      const float* bp = dt + gr * LDD + cst * 16 + (lane & 15);
+      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < BM / 4; j += 2) {
+        const int r0 = (j & 7) + 32 * (j >> 3);
+        const int r1 = ((j + 1) & 7) + 32 * ((j + 1) >> 3);
+        a0 = mfma16x16x4(ap[r0 * FB_THS], bp[r0 * LDD], a0);
+        a1 = mfma16x16x4(ap[r1 * FB_THS], bp[r1 * LDD], a1);
+      }
+      const int ccl = cst * 16 + (lane & 15);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int kl = g * 4 + e;
+        zt[kl * VB + (ccl ^ ((kl & 4) << 2))] = a0[e] + a1[e];
+      }
+    }
+    lds_barrier();
+    // ---- Adam with this client's moments, its pre-scale, and the client-order sum ----
+    {
+      AdamCoef ac;
+      ac.b1 = mc.beta1; ac.b2 = mc.beta2; ac.eps = mc.adam_eps; ac.wd = mc.weight_decay;
+      ac.step = cu.cf0;
+      ac.ibc2 = cu.cf1;
+      const bool sc = mc.fed_scale_on && (mc.beta - mc.flat_base) < mc.n_shared;
+      const float fs = mc.fed_scale;
+      const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc((void*)(mc.beta + mc.off_m), 0, nrec, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)(mc.beta + mc.off_v), 0, nrec, 0x00020000);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int kl = kl0 + 8 * u;
+        if (kb + kl >= K) continue;           // (wave-uniform)
+        const float g = zt[kl * VB + cs];
+        float mo = cu.rm[u], vo = cu.rv[u];
+        float np = adam_update(bt[kl * LDB_B + cl], g, mo, vo, ac);
+        if (sc) np *= fs;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mo), rm, voff[u], 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vo), rv, voff[u], 0, 0);
+        acc[u] = c == 0 ? np : acc[u] + np;
+      }
+    }
+    lds_barrier();                           // G / th / dt reads done before the next top
+  }
+  // ---- the folded slice: every client's copy (mode 0) or client 0's (mode 1) ----
+  const int nw = f.mode == 1 ? 1 : M;
+  for (int c = 0; c < nw; ++c) {
+    GfkModelC& mc = fold_model(f, c);
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)mc.beta, 0, nrec, 0x00020000);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      if (kb + kl0 + 8 * u < K) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[u]), rb, voff[u], 0, 0);
+  }
+}
+
+extern "C" size_t gfk_bwd_fold_smem() { return FB_SMEM; }
+
+// the shapes gfk_bwd_fold_k is written for (the host plan checks them too)
+extern "C" int gfk_bwd_fold_launch(const GfkModel* m0, const GfkFold* f, hipStream_t s) {
+  if (m0->kind != GFK_PRODLDA || m0->K > 64 || m0->bmax != 64 || m0->vb != VB || m0->mm_bf16 ||
+      m0->update_mode != 1 || m0->beta_split || m0->n_dpart != m0->n_tiles || m0->bwd_pre ||
+      (m0->stage_flags & GFK_LB) || f->M < 1 || !f->models || (int64_t)m0->K * m0->ldb * 4 >= 0x7FFF0000LL ||
+      m0->kt < 2 || (m0->kt & 1))
+    return -1;
+  const int ksub = (m0->K + 15) / 16;
+  const dim3 grid(8 * ksub * ((m0->n_tiles + 7) / 8));
+  hipLaunchKernelGGL(gfk_bwd_fold_k, grid, dim3(FB_NT), FB_SMEM, s, *f);
+  return (int)hipGetLastError();
+}
+
 // k ranges of the backward: 4 when the tiles outnumber the workgroups (n_dpart < n_tiles)
 // and K has at least 4 k tiles, else 1.  (Also splitting the one-tile-per-workgroup
 // headline case, 70 tiles at K=50, was measured: the prologue copy of theta_d's k range

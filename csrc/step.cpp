@@ -137,5 +137,6 @@ int gfk_scale(float* p, int64_t n, float sc, hipStream_t s) { return gfk_launch_
 size_t gfk_model_struct_size() { return sizeof(GfkModel); }
 size_t gfk_adam_struct_size() { return sizeof(GfkAdam); }
 size_t gfk_update_struct_size() { return sizeof(GfkUpdate); }
+size_t gfk_fold_struct_size() { return sizeof(GfkFold); }
 
 }  // extern "C"

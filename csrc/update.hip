@@ -1481,6 +1481,406 @@ extern "C" int gfk_launch_win_update(const GfkModel* m, const GfkUpdate* u, hipS
   return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------
+// gfk_win_fold_k: the encoder update of M batched clients with their FedAvg fold in the
+// epilogue (csrc/gfk_common.h GfkFold; the decoder half is prodlda.hip gfk_bwd_fold_k).
+// Workgroup roles (256 threads), each walking the M clients in order and adding every
+// client's pre-scaled Adam result to a register accumulator, written once at the end:
+//   W_in      (tile, 16-column hidden slice): the x^T tile rebuilt from the client's tile
+//             extents, dz0's slice, the 16x16 MFMA subtiles of gfk_win_update_k (B-step 8,
+//             two accumulators), Adam with the client's m / v;
+//   W         (weight job, 16-row slice): weight_job's products on the slice;
+//   V         (vector job, 16-element pass): vector_job's column sums / the prior gradient;
+//   left      pieces of the shared prefix no job owns (batch-norm running statistics,
+//             already pre-scaled by the forward): the plain client-order sum;
+//   prep      one per client: prepare_next_batch.
+// The next client's loads are in flight while the current one computes; the vector and
+// leftover roles load 8 clients at once.  Per client the arithmetic of the batched
+// gfk_win_update_k<512> (dense x^T tiles: H0 <= 64, bmax == 64, bag-of-words input), then
+// gfk_local_fedavg's client-order sum: bit-identical to that pair (tests/test_fold_gpu.py).
+namespace {
+constexpr int WF_NT = 256;
+constexpr int WF_XS = 66;               // x^T tile stride: stride_a(64)
+constexpr int WF_ZS = 16;               // a 16-column operand slice: rows 16 banks apart
+constexpr int WF_LDJ = 80;
+constexpr int WF_FG = 8;                // clients loaded at once by the vector / leftover roles
+typedef const __attribute__((address_space(4))) GfkModel GfkModelC;
+typedef const __attribute__((address_space(4))) GfkUpdate GfkUpdateC;
+__device__ __forceinline__ GfkModelC& wf_model(const GfkFold& f, int c) {
+  return ((GfkModelC*)(uintptr_t)f.models)[c];
+}
+__device__ __forceinline__ GfkUpdateC& wf_upd(const GfkFold& f, int c) {
+  return ((GfkUpdateC*)(uintptr_t)f.upds)[c];
+}
+__device__ __forceinline__ AdamCoef wf_coef(GfkModelC& m, float c0, float c1) {
+  AdamCoef c;
+  c.b1 = m.beta1; c.b2 = m.beta2; c.eps = m.adam_eps; c.wd = m.weight_decay;
+  c.step = c0;
+  c.ibc2 = c1;
+  return c;
+}
+__device__ __forceinline__ bool wf_scaled(GfkModelC& m, const float* p) {
+  return m.fed_scale_on && (p - m.flat_base) < m.n_shared;
+}
+
+// W_in (tile, hidden slice js)
+__device__ __forceinline__ void wf_win(const GfkFold& f, float* smem, int tile, int js) {
+  float* xt = smem;                       // [64][WF_XS]  x^T tile (zero outside the scatter)
+  float* dzs = xt + 64 * WF_XS;           // [64][WF_ZS]  dz0[:, j0 .. j0 + 15]
+  GfkModelC& m0 = wf_model(f, 0);
+  const int M = f.M, V = m0.V, H0 = m0.H[0], n_tiles = m0.n_tiles, c0 = tile * 64, j0 = 16 * js;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int row = tid >> 2, sub = tid & 3;          // staging: row, 4 threads per row
+  const int i0 = 16 * wave, jc = j0 + (lane & 15);  // MFMA subtile rows (words), output column
+  for (int i = tid; i < 64 * WF_XS / 4; i += WF_NT) reinterpret_cast<f32x4*>(xt)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // the shared values of this thread's 4 outputs (every client's copy holds them)
+  int eo[4];
+  float pp[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int v = c0 + i0 + (lane >> 4) * 4 + r;
+    eo[r] = min(v, V - 1) * H0 + min(jc, H0 - 1);
+    pp[r] = m0.w_in[eo[r]];
+  }
+  struct Pre {
+    int xe0, xe1, nb, xc[2];
+    float xv[2], dz[4], pm[4], pv[4], cf0, cf1;
+  };
+  auto issue = [&](int c, Pre& p) {
+    GfkModelC& mc = wf_model(f, c);
+    const int32_t* ts = mc.ws_tstart + (size_t)row * (n_tiles + 1) + tile;
+    p.xe0 = ts[0];
+    p.xe1 = ts[1];
+    p.nb = *mc.ws_nb;
+    p.cf0 = mc.adam_coef[0];
+    p.cf1 = mc.adam_coef[1];
+    const float* d0 = mc.ws_dz[0] + (size_t)row * H0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) p.dz[i] = d0[min(j0 + 4 * sub + i, H0 - 1)];
+    const float* w = mc.w_in;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      p.pm[r] = w[eo[r] + mc.off_m];
+      p.pv[r] = w[eo[r] + mc.off_v];
+    }
+  };
+  auto issue_nz = [&](int c, Pre& p) {
+    GfkModelC& mc = wf_model(f, c);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = min(p.xe0 + sub + 4 * i, max(p.xe1 - 1, 0));
+      p.xc[i] = mc.indices[e];
+      p.xv[i] = mc.values[e];
+    }
+  };
+  Pre nx;
+  issue(0, nx);
+  issue_nz(0, nx);
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  lds_barrier();                          // the zeroed x^T tile
+  for (int c = 0; c < M; ++c) {
+    GfkModelC& mc = wf_model(f, c);
+    const Pre cu = nx;
+    const int nb = cu.nb;
+    const bool live = row < nb;
+    // ---- stage: dz0's slice (rows >= nb and columns >= H0 zero), the x^T scatter ----
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = j0 + 4 * sub + i;
+      dzs[row * WF_ZS + 4 * sub + i] = (j < H0 && live) ? cu.dz[i] : 0.f;
+    }
+    const int xe1 = live ? cu.xe1 : 0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      if (cu.xe0 + sub + 4 * i < xe1) xt[(cu.xc[i] - c0) * WF_XS + row] = cu.xv[i];
+    for (int e = cu.xe0 + sub + 8; e < xe1; e += 4) xt[(mc.indices[e] - c0) * WF_XS + row] = mc.values[e];
+    lds_barrier();
+    if (c + 1 < M) {
+      issue(c + 1, nx);
+      issue_nz(c + 1, nx);
+    }
+    // ---- G[v, j] = sum_b xt[v, b] dz[b, j] (gfk_win_update_k's subtile sequence) ----
+    const float* ap = xt + (i0 + (lane & 15)) * WF_XS + (lane >> 4);
+    const float* bp = dzs + (lane >> 4) * WF_ZS + (lane & 15);
+    f32x4 c0v = {0.f, 0.f, 0.f, 0.f}, c1v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 64; k += 8) {
+      c0v = mfma16x16x4(ap[k], bp[k * WF_ZS], c0v);
+      c1v = mfma16x16x4(ap[k + 4], bp[(k + 4) * WF_ZS], c1v);
+    }
+    const f32x4 g = c0v + c1v;
+    lds_barrier();                        // every product read its operands
+    // ---- undo the scatter (the next client's tile starts from zeros) ----
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      if (cu.xe0 + sub + 4 * i < xe1) xt[(cu.xc[i] - c0) * WF_XS + row] = 0.f;
+    for (int e = cu.xe0 + sub + 8; e < xe1; e += 4) xt[(mc.indices[e] - c0) * WF_XS + row] = 0.f;
+    // ---- Adam with this client's moments, its pre-scale, the client-order sum ----
+    const AdamCoef ac = wf_coef(mc, cu.cf0, cu.cf1);
+    const bool sc = wf_scaled(mc, mc.w_in);
+    float* w = mc.w_in;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int v = c0 + i0 + (lane >> 4) * 4 + r;
+      if (v >= V || jc >= H0) continue;
+      float mo = cu.pm[r], vo = cu.pv[r];
+      float np = adam_update(pp[r], g[r], mo, vo, ac);
+      if (sc) np *= mc.fed_scale;
+      w[eo[r] + mc.off_m] = mo;
+      w[eo[r] + mc.off_v] = vo;
+      acc[r] = c == 0 ? np : acc[r] + np;
+    }
+    lds_barrier();                        // the undo is done before the next scatter
+  }
+  const int nw = f.mode == 1 ? 1 : M;
+  for (int c = 0; c < nw; ++c) {
+    float* w = wf_model(f, c).w_in;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int v = c0 + i0 + (lane >> 4) * 4 + r;
+      if (v < V && jc < H0) w[eo[r]] = acc[r];
+    }
+  }
+}
+
+// weight job jb, output rows J.j0 + 16 jt ..
+__device__ __forceinline__ void wf_weight(const GfkFold& f, float* smem, int jb, int jt) {
+  float* dzs = smem;                      // [64][WF_ZS] dz[:, row slice]
+  float* as = smem + 64 * WF_ZS;          // [64][WF_LDJ] a[:, i0 .. i0 + 63]
+  GfkModelC& m0 = wf_model(f, 0);
+  GfkUpdateC& u0 = wf_upd(f, 0);
+  const int M = f.M, B = m0.bmax;
+  const int rows = u0.w[jb].rows, cols = u0.w[jb].cols, jr0 = u0.w[jb].j0 + 16 * jt, ic0 = u0.w[jb].i0;
+  if (jr0 >= rows) return;
+  const int tid = threadIdx.x, lane = tid & 63, it = tid >> 6;
+  const int b = tid >> 2, sub = tid & 3;
+  const int ic = ic0 + it * 16 + (lane & 15);
+  int eo[4];
+  float pp[4];
+  {
+    const float* p0 = u0.w[jb].param;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = jr0 + (lane >> 4) * 4 + r;
+      eo[r] = min(j, rows - 1) * cols + min(ic, cols - 1);
+      pp[r] = p0[eo[r]];
+    }
+  }
+  struct Pre {
+    int nb;
+    float dz[4], a[16], pm[4], pv[4], cf0, cf1;
+  };
+  auto issue = [&](int c, Pre& p) {
+    GfkModelC& mc = wf_model(f, c);
+    GfkUpdateC& uc = wf_upd(f, c);
+    p.nb = *mc.ws_nb;
+    p.cf0 = mc.adam_coef[0];
+    p.cf1 = mc.adam_coef[1];
+    const int bb = min(b, B - 1);
+    const float* dz = uc.w[jb].dz + (size_t)bb * rows;
+    const float* a = uc.w[jb].a + (size_t)bb * cols;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) p.dz[i] = dz[min(jr0 + 4 * sub + i, rows - 1)];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) p.a[i] = a[min(ic0 + 16 * sub + i, cols - 1)];
+    const float* pc = uc.w[jb].param;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      p.pm[r] = pc[eo[r] + mc.off_m];
+      p.pv[r] = pc[eo[r] + mc.off_v];
+    }
+  };
+  Pre nx;
+  issue(0, nx);
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int c = 0; c < M; ++c) {
+    GfkModelC& mc = wf_model(f, c);
+    const Pre cu = nx;
+    const bool live = b < cu.nb;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      dzs[b * WF_ZS + 4 * sub + i] = (live && jr0 + 4 * sub + i < rows) ? cu.dz[i] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      as[b * WF_LDJ + 16 * sub + i] = (live && ic0 + 16 * sub + i < cols) ? cu.a[i] : 0.f;
+    lds_barrier();
+    if (c + 1 < M) issue(c + 1, nx);
+    const float* ap = dzs + (lane >> 4) * WF_ZS + (lane & 15);
+    const float* bp = as + (lane >> 4) * WF_LDJ + it * 16 + (lane & 15);
+    f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < B; k += 8) {
+      c0 = mfma16x16x4(ap[k * WF_ZS], bp[k * WF_LDJ], c0);
+      c1 = mfma16x16x4(ap[(k + 4) * WF_ZS], bp[(k + 4) * WF_LDJ], c1);
+    }
+    const f32x4 g = c0 + c1;
+    GfkUpdateC& uc = wf_upd(f, c);
+    float* pc = uc.w[jb].param;
+    const AdamCoef ac = wf_coef(mc, cu.cf0, cu.cf1);
+    const bool sc = wf_scaled(mc, pc);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = jr0 + (lane >> 4) * 4 + r;
+      if (j >= rows || ic >= cols) continue;
+      float mo = cu.pm[r], vo = cu.pv[r];
+      float np = adam_update(pp[r], g[r], mo, vo, ac);
+      if (sc) np *= mc.fed_scale;
+      pc[eo[r] + mc.off_m] = mo;
+      pc[eo[r] + mc.off_v] = vo;
+      acc[r] = c == 0 ? np : acc[r] + np;
+    }
+    lds_barrier();                        // the products read their operands
+  }
+  const int nw = f.mode == 1 ? 1 : M;
+  for (int c = 0; c < nw; ++c) {
+    float* pc = wf_upd(f, c).w[jb].param;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = jr0 + (lane >> 4) * 4 + r;
+      if (j < rows && ic < cols) pc[eo[r]] = acc[r];
+    }
+  }
+}
+
+// vector job jv, elements 16 pass .. 16 pass + 15 (16 lanes each)
+__device__ __forceinline__ void wf_vector(const GfkFold& f, int jv, int pass) {
+  GfkModelC& m0 = wf_model(f, 0);
+  GfkUpdateC& u0 = wf_upd(f, 0);
+  const int M = f.M, B = m0.bmax, n = u0.v[jv].n;
+  const int tid = threadIdx.x, s = tid & 15;
+  const int c = 16 * pass + (tid >> 4);
+  if (16 * pass >= n) return;
+  const int cc = min(c, n - 1);
+  const float pp = u0.v[jv].param[cc];
+  const bool has_src = u0.v[jv].src != nullptr;
+  float acc = 0.f;
+  for (int g0 = 0; g0 < M; g0 += WF_FG) {
+    float v[WF_FG][8], pm[WF_FG], pv[WF_FG], gr[WF_FG], cf0[WF_FG], cf1[WF_FG];
+    int nb[WF_FG];
+#pragma unroll
+    for (int i = 0; i < WF_FG; ++i) {
+      const int ci = min(g0 + i, M - 1);
+      GfkModelC& mc = wf_model(f, ci);
+      GfkUpdateC& uc = wf_upd(f, ci);
+      const float* p = uc.v[jv].param + cc;
+      nb[i] = *mc.ws_nb;
+      cf0[i] = mc.adam_coef[0];
+      cf1[i] = mc.adam_coef[1];
+      pm[i] = p[mc.off_m];
+      pv[i] = p[mc.off_v];
+      gr[i] = 0.f;
+      if (has_src) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[i][u] = uc.v[jv].src[(size_t)min(s + 16 * u, B - 1) * n + cc];
+      } else {
+        gr[i] = p[mc.off_g];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < WF_FG; ++i) {
+      if (g0 + i >= M) break;
+      GfkModelC& mc = wf_model(f, g0 + i);
+      float g = gr[i];
+      if (has_src) {
+        g = 0.f;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) g += s + 16 * u < nb[i] ? v[i][u] : 0.f;
+        g = row16_sum(g);
+      }
+      if (s != 0 || c >= n) continue;
+      float* p = wf_upd(f, g0 + i).v[jv].param + cc;
+      float mo = pm[i], vo = pv[i];
+      float np = adam_update(pp, g, mo, vo, wf_coef(mc, cf0[i], cf1[i]));
+      if (wf_scaled(mc, p)) np *= mc.fed_scale;
+      p[mc.off_m] = mo;
+      p[mc.off_v] = vo;
+      acc = g0 + i == 0 ? np : acc + np;
+    }
+  }
+  if (s != 0 || c >= n) return;
+  const int nw = f.mode == 1 ? 1 : M;
+  for (int ci = 0; ci < nw; ++ci) wf_upd(f, ci).v[jv].param[cc] = acc;
+}
+
+// leftover piece r: f.left[2 r] (first float, a multiple of 4), f.left[2 r + 1] floats (<= 1024)
+__device__ __forceinline__ void wf_left(const GfkFold& f, int r) {
+  const int64_t off = f.left[2 * r];
+  const int len = (int)f.left[2 * r + 1];
+  const int e = 4 * threadIdx.x;
+  if (e >= len) return;
+  const int M = f.M;
+  const bool full = e + 3 < len;
+  f32x4 tot = {0.f, 0.f, 0.f, 0.f};
+  for (int g0 = 0; g0 < M; g0 += WF_FG) {
+    f32x4 v[WF_FG];
+#pragma unroll
+    for (int i = 0; i < WF_FG; ++i) {
+      const float* p = wf_model(f, min(g0 + i, M - 1)).flat_base + off + e;
+      if (full) {
+        v[i] = *reinterpret_cast<const f32x4*>(p);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[i][k] = e + k < len ? p[k] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < WF_FG; ++i) {
+      if (g0 + i >= M) break;
+      tot = g0 + i == 0 ? v[i] : tot + v[i];
+    }
+  }
+  const int nw = f.mode == 1 ? 1 : M;
+  for (int c = 0; c < nw; ++c) {
+    float* p = wf_model(f, c).flat_base + off + e;
+    if (full) {
+      *reinterpret_cast<f32x4*>(p) = tot;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) if (e + k < len) p[k] = tot[k];
+    }
+  }
+}
+}  // namespace
+
+extern "C" __global__ void __launch_bounds__(WF_NT) gfk_win_fold_k(GfkFold f) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  GfkModelC& m0 = wf_model(f, 0);
+  GfkUpdateC& u0 = wf_upd(f, 0);
+  const int n_tiles = m0.n_tiles, nj = f.nj;
+  const int n_win = 8 * nj * ((n_tiles + 7) / 8);
+  int r = blockIdx.x;
+  if (r < n_win) {                  // a tile's nj slices on one XCD (they read the same x^T)
+    const int x8 = r & 7, jj = r >> 3, js = jj % nj, tile = (jj / nj) * 8 + x8;
+    if (tile < n_tiles) wf_win(f, smem, tile, js);
+    return;
+  }
+  r -= n_win;
+  if (r < 4 * u0.n_w) { wf_weight(f, smem, r >> 2, r & 3); return; }
+  r -= 4 * u0.n_w;
+  if (r < 4 * u0.n_v) { wf_vector(f, r >> 2, r & 3); return; }
+  r -= 4 * u0.n_v;
+  if (r < f.n_left) { wf_left(f, r); return; }
+  r -= f.n_left;
+  if (r < f.M) prepare_next_batch(f.models[r], reinterpret_cast<int*>(smem));
+}
+
+extern "C" size_t gfk_win_fold_smem() {
+  const size_t a = 64 * WF_XS + 64 * WF_ZS, b = 64 * WF_ZS + 64 * WF_LDJ, c = 2 * GFK_BMAX_LIMIT;
+  return sizeof(float) * (a > b ? (a > c ? a : c) : (b > c ? b : c));
+}
+
+extern "C" int gfk_win_fold_launch(const GfkModel* m0, const GfkUpdate* u0, const GfkFold* f, hipStream_t s) {
+  if (m0->input != GFK_IN_BOW || m0->H[0] > 64 || m0->bmax != 64 || m0->update_mode != 1 ||
+      (m0->stage_flags & (WIN_SPARSE | GFK_WIN_SPLIT | GFK_LB)) || m0->lab_on || f->M < 1 ||
+      !f->models || !f->upds || f->nj != (m0->H[0] + 15) / 16 || (f->n_left > 0 && !f->left))
+    return -1;
+  for (int j = 0; j < u0->n_v; ++j)
+    if (u0->v[j].n > 64) return -1;
+  const int n_win = 8 * f->nj * ((m0->n_tiles + 7) / 8);
+  const dim3 g(n_win + 4 * u0->n_w + 4 * u0->n_v + f->n_left + f->M);
+  hipLaunchKernelGGL(gfk_win_fold_k, g, dim3(WF_NT), gfk_win_fold_smem(), s, *f);
+  return (int)hipGetLastError();
+}
+
 extern "C" int gfk_win_update_set_smem(size_t bytes) {
   // the attribute is per function and process-wide: only ever raise it, so an engine
   // built earlier with a larger footprint keeps launching after a smaller one is set up

@@ -204,6 +204,7 @@ class MultiClientRound:
                 c.enable_graph(False)     # the round graph carries every client's step
         if self.fused:
             prepare_local_fedavg(self.shared)
+        self.fold_plan: Optional[str] = None   # the in-rank FedAvg of the batched round
         self._g = None                    # the one-round graph
         self._gk: Dict[int, object] = {}  # k-round graphs (k > 1)
         self._bss: Dict[int, object] = {}  # the BatchedSteps each graph was captured with
@@ -214,6 +215,12 @@ class MultiClientRound:
         if logger is not None:
             logger.info("-- -- FedAvg: %d local clients folded in-rank, %s across %d ranks",
                         len(clients), self.method or "no collective", world)
+
+    def _states_equal(self) -> bool:
+        """Every client's shared state is the same (the in-epilogue fold reads client 0's
+        copy for all of them): true after W0's broadcast and after every FedAvg."""
+        s0 = self.shared[0]
+        return all(torch.equal(s0, s) for s in self.shared[1:])
 
     # ---- pieces of the round (enqueued on the current stream) ----
     def _fold(self, part: str, mode: int):
@@ -285,6 +292,19 @@ class MultiClientRound:
         if batched:
             bs = BatchedSteps(engines)
             bs.prepare()
+            # one rank: the round's FedAvg inside the update kernels' epilogues (every client
+            # starts each round from the same averaged state; GFEDNTM_FOLD=0: the fold kernel
+            # after the batched steps)
+            fold = None
+            if not self.colls and os.environ.get("GFEDNTM_FOLD", "1") != "0":
+                why = bs.fold_reason()
+                if why is None and self._states_equal():
+                    from ..ops import kernel_abi as abi
+                    bs.set_fold(abi.FOLD_ALL)
+                    fold = "in-epilogue"
+                else:
+                    fold = None
+                self.fold_plan = fold or ("fold kernel (%s)" % (why or "client states differ"))
             # beta's / adapt_bert's shares on the side stream once the backward has
             # finished them (else reduced with the rest at the end of the round: the same
             # arithmetic)
@@ -297,6 +317,8 @@ class MultiClientRound:
             with graph_capture(g):
                 for _ in range(k):
                     bs.launch(after=hooks or None)
+                    if fold is not None:
+                        continue              # the FedAvg ran in the update epilogues
                     if self.coll_in_graph or not self.colls:
                         for part in self.parts:
                             if part not in forked:

@@ -173,6 +173,7 @@ class LocalFederation:
         self.round_batched = (round_batched if round_batched is not None else
                               os.environ.get("GFEDNTM_ROUND_BATCHED", "1") == "1")
         self._batched = None
+        self.fold_plan: Optional[str] = None    # the batched round's FedAvg (in-epilogue / kernel)
         self._rg = None
         self._rgk = {}                    # k -> (the k-round graph, the launches it baked in)
         self._rg_gens = None
@@ -219,11 +220,20 @@ class LocalFederation:
                 self._batched = self._batched_parts[0]
                 for b in self._batched_parts:
                     b.prepare()
+                # one group: the FedAvg inside the update kernels' epilogues
+                # (rank_round.MultiClientRound; GFEDNTM_FOLD=0: the fold kernel after the steps)
+                fold = (len(self._batched_parts) == 1 and os.environ.get("GFEDNTM_FOLD", "1") != "0"
+                        and self._batched.fold_reason() is None
+                        and all(torch.equal(shared[0], x) for x in shared[1:]))
+                if fold:
+                    from ..ops import kernel_abi as abi
+                    self._batched.set_fold(abi.FOLD_ALL)
+                self.fold_plan = "in-epilogue" if fold else "fold kernel"
                 with graph_capture(g):
                     for _ in range(k):
                         for b in self._batched_parts:
                             b.launch()
-                        if not self.agg.fused_sum_(shared):
+                        if not fold and not self.agg.fused_sum_(shared):
                             raise RuntimeError("round graph needs the native FedAvg kernel")
                 self._store_round_graph(g, k)
                 return
@@ -337,6 +347,9 @@ class LocalFederation:
             self.prewarm(kmax)
             for c in self.clients:
                 ends.update(int(i) for i in np.flatnonzero(c.plan.epoch_end))
+                # rounds whose end_round reads the state on the host (round 0's results when
+                # num_epochs <= 0, ...): a run must end there, as run_distributed's do
+                ends.update(int(i) for i in c.host_heavy_rounds())
         timed_end = start + timing_warmup - 1 if timing_warmup else -1
         covered = start - 1
         with trace_range("rounds"):

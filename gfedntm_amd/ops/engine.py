@@ -1624,6 +1624,8 @@ class BatchedSteps:
         self._phases = e0.phases()
         self._side = (torch.cuda.Stream(self.device), torch.cuda.Event(), torch.cuda.Event())
         self._cu = torch.cuda.get_device_properties(self.device).multi_processor_count
+        self._fold = None                 # abi.GfkFold when the FedAvg runs in the epilogues
+        self._fold_left = None            # its device table of leftover pieces
 
     @staticmethod
     def possible(engines) -> bool:
@@ -1751,6 +1753,116 @@ class BatchedSteps:
         """Upload the descriptors now (before a capture)."""
         self._refresh()
 
+    # ---- the FedAvg in the update epilogues (csrc/prodlda.hip gfk_bwd_fold_k,
+    #      csrc/update.hip gfk_win_fold_k) ----
+    FOLD_PIECE = 1024                     # floats per leftover workgroup (256 threads x float4)
+
+    def _fold_owned(self) -> Dict[int, str]:
+        """Flat offsets of the shared slots the fold kernels' update jobs own (beta, W_in,
+        every weight / vector job's parameter) -> key."""
+        e0 = self.engines[0]
+        base = e0.flat.buffer.data_ptr()
+        by_off = {s.offset: k for k, s in e0.flat.slots.items()}
+        owned = {}
+        ptrs = [int(e0._m.beta), int(e0._m.w_in)]
+        ptrs += [int(e0._u.w[i].param) for i in range(e0._u.n_w)]
+        ptrs += [int(e0._u.v[i].param) for i in range(e0._u.n_v)]
+        for p in ptrs:
+            off = (p - base) // 4
+            if (p - base) % 4 or off not in by_off:
+                raise ValueError("an update job's parameter is not a slot of the flat buffer")
+            owned[off] = by_off[off]
+        return owned
+
+    def fold_reason(self) -> Optional[str]:
+        """Why the in-epilogue FedAvg cannot run this launch (None: it can).  The fold
+        kernels cover the headline plan: ProdLDA, bag of words, fused Adam, fp32, bmax 64,
+        K and every hidden layer <= 64, one d theta_d slab per tile, dense W_in tiles,
+        every parameter in the shared prefix and pre-scaled."""
+        e0 = self.engines[0]
+        m = self._host if self._host is not None else e0._m
+        if not hasattr(e0.lib, "gfk_bwd_fold_launch"):
+            return "kernel library without the fold kernels"
+        checks = [
+            (m.kind == abi.KIND_PRODLDA, "ProdLDA only"),
+            (m.input == abi.IN_BOW and not m.lab_on, "bag-of-words input without a label head"),
+            (e0.update_mode == UPDATE_FUSED, "fused Adam epilogues only"),
+            (not m.mm_bf16, "fp32 GEMM operands only"),
+            (m.K <= 64 and m.bmax == 64, "K <= 64 and batch 64 only"),
+            (max(int(m.H[i]) for i in range(m.n_hidden)) <= 64, "hidden layers <= 64 only"),
+            (not m.beta_split and not m.bwd_pre and m.n_dpart == m.n_tiles,
+             "the one-slab-per-tile backward only"),
+            (not m.stage_flags & (STAGE_WIN_SPARSE | STAGE_WIN_SPLIT | STAGE_LB | STAGE_BWD_KQ1),
+             "dense W_in tiles only"),
+            (m.kt % 2 == 0, "theta_d stride"),
+            (all(e0._u.v[i].n <= 64 for i in range(e0._u.n_v)), "vector jobs <= 64 long"),
+        ]
+        for ok, why in checks:
+            if not ok:
+                return why
+        for e in self.engines:
+            fl = e.flat
+            if any(s.offset + s.numel > fl.n_shared for s in fl.param_slots()):
+                return "a parameter outside the shared prefix"
+            if not e._m.fed_scale_on:
+                return "no FedAvg pre-scale"
+        try:
+            owned = self._fold_owned()
+        except ValueError as exc:
+            return str(exc)
+        fl = e0.flat
+        for k in fl.shared_keys:
+            s = fl.slots[k]
+            if s.offset not in owned and s.is_param:
+                return f"parameter {k} has no fold job"
+        return None
+
+    def set_fold(self, mode: Optional[int]):
+        """mode abi.FOLD_ALL / FOLD_FIRST: replace prodlda_bwd and win_update by the fold
+        kernels (the round's in-rank FedAvg inside their epilogues; every client's state must
+        be the same at the start of each round -- the caller's invariant); None: off."""
+        if mode is None:
+            self._fold = None
+            return
+        why = self.fold_reason()
+        if why is not None:
+            raise ValueError(f"in-epilogue FedAvg not available: {why}")
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("set_fold inside a graph capture")
+        e0 = self.engines[0]
+        owned = self._fold_owned()
+        pieces = []
+        for k in e0.flat.shared_keys:
+            s = e0.flat.slots[k]
+            if s.offset in owned:
+                continue
+            for a in range(0, s.numel, self.FOLD_PIECE):
+                pieces += [s.offset + a, min(self.FOLD_PIECE, s.numel - a)]
+        if any(p % 4 for p in pieces[0::2]):
+            raise ValueError("leftover pieces must start on 16-byte boundaries")
+        self._fold_left = torch.tensor(pieces or [0, 0], dtype=torch.int64, device=self.device)
+        f = abi.GfkFold()
+        f.models, f.upds = self._arr_m.data_ptr(), self._arr_u.data_ptr()
+        f.left = self._fold_left.data_ptr()
+        f.M, f.mode, f.n_left = len(self.engines), int(mode), len(pieces) // 2
+        f.nj = -(-int(e0._m.H[0]) // 16)
+        self._fold = f
+
+    @property
+    def fold_mode(self) -> Optional[int]:
+        return None if self._fold is None else int(self._fold.mode)
+
+    def _run_fold(self, phase: int):
+        e0 = self.engines[0]
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        if phase == abi.PH_FOLD_BWD:
+            rc = e0.lib.gfk_bwd_fold_launch(C.byref(self._host), C.byref(self._fold), stream)
+        else:
+            rc = e0.lib.gfk_win_fold_launch(C.byref(self._host), C.byref(e0._u),
+                                            C.byref(self._fold), stream)
+        if rc:
+            raise RuntimeError(f"fold kernel launch failed: code {rc} (phase {phase})")
+
     def _run(self, phases):
         e0 = self.engines[0]
         arr, n = abi.phase_array(phases)
@@ -1766,16 +1878,24 @@ class BatchedSteps:
         ``after``: {phase: callable} called (on the host, while enqueuing) right after
         that phase's launch -- the multi-client rank round forks beta's FedAvg there."""
         self._refresh()
-        after = after or {}
+        after = dict(after or {})
+        phases = list(self._phases)
+        if self._fold is not None:
+            swap = {abi.PH_PRODLDA_BWD: abi.PH_FOLD_BWD, abi.PH_ENC_BWD: abi.PH_FOLD_WIN}
+            phases = [swap.get(p, p) for p in phases]
+            after = {swap.get(p, p): f for p, f in after.items()}
         run: List[int] = []
-        for p in list(self._phases) + [None]:
-            if p is not None and p not in _BATCH_FORK_PHASES:
+        for p in phases + [None]:
+            if p is not None and p not in _BATCH_FORK_PHASES and p not in (abi.PH_FOLD_BWD,
+                                                                             abi.PH_FOLD_WIN):
                 run.append(p)
                 if p not in after:
                     continue
             if run:
                 self._run(run)
                 run = []
+            if p in (abi.PH_FOLD_BWD, abi.PH_FOLD_WIN):
+                self._run_fold(p)
             if p in after:
                 after[p]()
             elif p == abi.PH_WIN_FORK:

@@ -63,6 +63,11 @@ PH_FEDAVG_WA = 107
 # d theta_d after prodlda_lb_dlogit (PH_PRODLDA_BWD)
 PH_LB_GEMM_FWD = 108
 PH_LB_GEMM_BWD = 109
+# batched clients with the FedAvg in the update epilogues (ops/engine.py BatchedSteps.set_fold):
+# csrc/prodlda.hip gfk_bwd_fold_k in place of PH_PRODLDA_BWD, csrc/update.hip gfk_win_fold_k
+# in place of PH_ENC_BWD (launched by the batched plan, not by gfk_run)
+PH_FOLD_BWD = 110
+PH_FOLD_WIN = 111
 HOST_PHASES = (PH_CTX_FWD, PH_CTX_BWD, PH_FEDAVG_BETA, PH_FEDAVG_END, PH_BETA_ADAM, PH_WIN_FORK,
                PH_WIN_JOIN, PH_FEDAVG_WA, PH_LB_GEMM_FWD, PH_LB_GEMM_BWD)
 
@@ -166,10 +171,22 @@ class GfkInfer(C.Structure):
 
 INFER_POSTPROCESS, INFER_MOMENTS = 1, 2
 
+
+class GfkFold(C.Structure):
+    """The in-epilogue FedAvg of a batched launch (csrc/gfk_common.h GfkFold)."""
+    _fields_ = [("models", P), ("upds", P), ("left", P), ("M", C.c_int32), ("mode", C.c_int32),
+                ("n_left", C.c_int32), ("nj", C.c_int32)]
+
+
+FOLD_ALL, FOLD_FIRST = 0, 1
+
 # optional entry points: name -> (argtypes, restype)
 _EXTRA = {
     "gfk_theta_infer": ([C.POINTER(GfkModel), C.POINTER(GfkInfer), C.c_void_p], C.c_int),
     "gfk_theta_infer_smem": ([C.POINTER(GfkModel)], C.c_size_t),
+    "gfk_bwd_fold_launch": ([C.POINTER(GfkModel), C.POINTER(GfkFold), C.c_void_p], C.c_int),
+    "gfk_win_fold_launch": ([C.POINTER(GfkModel), C.POINTER(GfkUpdate), C.POINTER(GfkFold), C.c_void_p],
+                            C.c_int),
 }
 
 
@@ -199,6 +216,10 @@ def declare(lib: C.CDLL) -> None:
     lib.gfk_infer_struct_size.restype = C.c_size_t
     if lib.gfk_infer_struct_size() != C.sizeof(GfkInfer):
         raise RuntimeError("GfkInfer ABI mismatch")
+    if hasattr(lib, "gfk_fold_struct_size"):
+        lib.gfk_fold_struct_size.restype = C.c_size_t
+        if lib.gfk_fold_struct_size() != C.sizeof(GfkFold):
+            raise RuntimeError("GfkFold ABI mismatch")
     for name, args in _EXTRA.items():
         if hasattr(lib, name):
             f = getattr(lib, name)
