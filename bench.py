@@ -304,9 +304,18 @@ def run_multi(args, rank, world, device, rehearse):
     dist.all_reduce(t, group=_ctrl_group())
     docs = float(t.item())
     eng = out["clients"][0].tm.engine
-    out["round"].close()
     n_rounds = args.warmup + args.steps
     final_loss = float(np.mean(eng.loss_hist[max(0, n_rounds - 20): n_rounds].cpu().numpy()))
+    # round split: the rank's batched local steps alone (no in-rank fold, no collective),
+    # replayed over the same plan steps after the run
+    steps_ms = None
+    rr = out["round"]
+    if hasattr(rr, "time_local_steps") and args.backend == "fused":
+        steps_ms = rr.time_local_steps(args.warmup, min(args.steps, 500))
+    # (every rank joins the reduction, also one that hosts a single client)
+    steps_ms = _max_over_ranks(-1.0 if steps_ms is None else steps_ms, world)
+    steps_ms = None if steps_ms < 0 else steps_ms
+    rr.close()
     # ---- quality: a separate untimed federation of --npmi-steps rounds (all clients) ----
     quality = _quality(args, corpora, ids, sc, n_clients, rank, device, kw)
     if rank == 0:
@@ -327,6 +336,18 @@ def run_multi(args, rank, world, device, rehearse):
         # the in-rank FedAvg of a multi-client rank: inside the update kernels' epilogues
         # (csrc gfk_bwd_fold_k / gfk_win_fold_k) or the fold kernel after the batched steps
         rec["fedavg_plan"] = getattr(out["round"], "fold_plan", None)
+        split = {"round_ms": round(ms, 5)}
+        if rec["device_ms_per_step"] is not None:
+            split["device_ms"] = rec["device_ms_per_step"]
+            split["host_ms"] = round(max(ms - rec["device_ms_per_step"], 0.0), 5)
+            if steps_ms is not None:
+                # the local steps with per-client updates alone, and what the round's FedAvg
+                # (the in-rank fold -- a kernel, or inside the update epilogues -- and the
+                # collective) adds to them on the device (negative: the in-epilogue FedAvg's
+                # kernels beat the per-client update kernels they replace)
+                split["local_steps_device_ms"] = round(steps_ms, 5)
+                split["fedavg_device_ms"] = round(rec["device_ms_per_step"] - steps_ms, 5)
+        rec["round_split_ms"] = split
         rec["digests"] = out.get("digests")
         if fallback:
             rec["allreduce_fallback"] = fallback

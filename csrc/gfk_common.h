@@ -188,6 +188,10 @@ typedef struct GfkModel {
   // computed once per step (csrc/posterior.hip gfk_post_colstats_lb_k): [mean | rstd] of the
   // raw heads, [sum dy | sum dy xhat] of the backward, the priors' sums, 2K floats each ----
   float* ws_colstat;
+  // ---- per-step mean KL and reconstruction terms (metrics, reference federated_avitm.py:109,
+  // SURVEY 5.5): written next to loss_hist by the batch-level workgroup when non-null ----
+  float* kl_hist;
+  float* rl_hist;
 } GfkModel;
 
 constexpr int GFK_WIN_SPLIT = 128;

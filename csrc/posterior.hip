@@ -491,6 +491,26 @@ extern "C" size_t gfk_row_bwd_smem(const GfkModel* m) { return sizeof(float) * 4
 // smallest covering K, NG = PT / CW row groups; 16 rows' loads in flight per thread), the groups'
 // partials added in group order through LDS -- at K = 50 four groups of 16 rows where one thread
 // per topic walked all 64 rows (the batched round's tail, 9 us).
+// metrics (GfkModel kl_hist / rl_hist set): the step's mean KL and reconstruction terms over
+// the batch rows, next to loss_hist (two more block sums behind the loss's; off the
+// training path: only when a metrics window or the per-minibatch log asks for them)
+__device__ __forceinline__ void post_term_hist(const GfkModel& m, int nb, int step0, float* scratch,
+                                               int tid, int nt) {
+  float k = 0.f, r = 0.f;
+  for (int b = tid; b < nb; b += nt) {
+    k += m.ws_kl[b];
+    r += m.ws_rl[b];
+  }
+  lds_barrier();                     // every wave read the loss's partials from scratch
+  const float ks = block_sum_wave0(k, scratch);
+  lds_barrier();
+  const float rs = block_sum_wave0(r, scratch);
+  if (tid == 0) {
+    m.kl_hist[step0] = ks / (float)nb;
+    m.rl_hist[step0] = rs / (float)nb;
+  }
+}
+
 __device__ __forceinline__ void post_batch_level(const GfkModel& m, int nb, float* scratch, int tid) {
   __shared__ float red[3 * PT];
   const int K = m.K;
@@ -546,6 +566,7 @@ __device__ __forceinline__ void post_batch_level(const GfkModel& m, int nb, floa
     m.loss_hist[step0] = l;
     *m.step = step0 + 1;
   }
+  if (m.kl_hist) post_term_hist(m, nb, step0, scratch, tid, PT);
 }
 
 // KQ = ceil(K / 64) topics per lane: only live topics are loaded (K <= 64 -> one
@@ -909,6 +930,7 @@ __global__ void __launch_bounds__(FT) gfk_post_bwd_k(GfkArgT<GB> ga) {
       m.loss_hist[step0] = l;
       *m.step = step0 + 1;
     }
+    if (m.kl_hist) post_term_hist(m, nb, step0, smem + L.red, tid, FT);
     return;
   }
   if constexpr (in_lds) {               // LDS: 16 lanes per column, DPP reductions

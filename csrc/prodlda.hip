@@ -2050,11 +2050,11 @@ extern "C" size_t gfk_prodlda_fwd_smem(const GfkModel* m) {
 // Grid: the 8-aligned tiles x ceil(K / 16) slices, a tile's slices on one XCD (they read
 // the same client tiles: one HBM fetch, three L2 hits).
 // LDS: zt [64][64] (the z tile, then the G tile) + dt [64][66] + th [64][18] + bt [16][66]
-//      + lse, S [64] + rstd [64]: 42.9 KB, two workgroups per CU.
+//      + lse, S [64] + rstd [64] (+ scratch): 44.2 KB, two workgroups per CU.
 namespace {
 constexpr int FB_NT = 512;
 constexpr int FB_THS = 18;       // theta_d slice stride: R8 rows r, r + 8 land 16 banks apart
-constexpr size_t FB_SMEM = sizeof(float) * (64 * VB + 64 * LDD + 64 * FB_THS + 16 * LDB_B + 3 * 64);
+constexpr size_t FB_SMEM = sizeof(float) * (64 * VB + 64 * LDD + 64 * FB_THS + 16 * LDB_B + FB_NT);
 typedef const __attribute__((address_space(4))) GfkModel GfkModelC;
 // the batched descriptors through the constant address space: a client's fields are scalar
 // loads wherever the client loop reaches it
@@ -2063,6 +2063,17 @@ __device__ __forceinline__ GfkModelC& fold_model(const GfkFold& f, int c) {
 }
 }  // namespace
 
+#ifdef GFK_STAMPS
+#define FOLD_STAMP(slot)                                                          \
+  do {                                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                            \
+    if (blockIdx.x == 0 && threadIdx.x == 0 && m0.dbg)                            \
+      m0.dbg[slot] = __builtin_amdgcn_s_memtime();                                \
+    __builtin_amdgcn_sched_barrier(0);                                            \
+  } while (0)
+#else
+#define FOLD_STAMP(slot) do { } while (0)
+#endif
 extern "C" __global__ void __launch_bounds__(FB_NT, 2) gfk_bwd_fold_k(GfkFold f) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int BM = 64;
@@ -2070,7 +2081,7 @@ extern "C" __global__ void __launch_bounds__(FB_NT, 2) gfk_bwd_fold_k(GfkFold f)
   float* dt = zt + BM * VB;         // [BM][LDD] dlogit
   float* th = dt + BM * LDD;        // [BM][FB_THS] theta_d columns kb .. kb + 15
   float* bt = th + BM * FB_THS;     // [16][LDB_B] beta rows kb .. kb + 15 of the tile
-  float* lse = bt + 16 * LDB_B;     // [BM]; sb = lse + BM, rs = lse + 2 BM (one 192-float run)
+  float* lse = bt + 16 * LDB_B;     // [BM]; sb = lse + BM, rs = lse + 2 BM (+ 320 scratch floats)
   float* sb = lse + BM;
   float* rs = sb + BM;
   GfkModelC& m0 = fold_model(f, 0);
@@ -2079,6 +2090,7 @@ extern "C" __global__ void __launch_bounds__(FB_NT, 2) gfk_bwd_fold_k(GfkFold f)
   const int bx = blockIdx.x, x8 = bx & 7, jj = bx >> 3;
   const int q = jj % ksub, tile = (jj / ksub) * 8 + x8;
   if (tile >= n_tiles) return;
+  FOLD_STAMP(98);
   const int kb = 16 * q, c0 = tile * VB;
   const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
   const int M = f.M;
@@ -2102,19 +2114,32 @@ extern "C" __global__ void __launch_bounds__(FB_NT, 2) gfk_bwd_fold_k(GfkFold f)
     bt[kl * LDB_B + c] = (kb + kl < K && c0 + c < V) ? b : 0.f;
   }
 
-  // ---- one client's loads (registers; issue order: the tile extents first, so the
-  //      dependent first-non-zero loads wait for them alone) ----
+  // ---- a client's loads, into registers.  The tile extents run two clients ahead (their
+  //      dependent first-non-zero loads are issued one client ahead, when the extents have
+  //      long arrived); every store of the loop is unconditional (buffer stores, rows / columns
+  //      outside the shapes get an offset past the descriptor and are dropped), so the
+  //      compiler's vmcnt bookkeeping stays exact and the loop top waits for the prefetched
+  //      loads only, never for the previous client's stores ----
   struct Pre {
     int xe0, xe1, xc, nb;
     float xv, aux, rm[2], rv[2], cf0, cf1;
     f32x4 z0, z1;
     float2 th2;
   };
+  auto issue_ts = [&](int c, int& e0, int& e1) {
+    const int32_t* ts = fold_model(f, c).ws_tstart + (size_t)xrow * ntp + tile;
+    e0 = ts[0];
+    e1 = ts[1];
+  };
+  auto issue_nz = [&](int c, Pre& p) {     // depends on the tile extents
+    GfkModelC& mc = fold_model(f, c);
+    const int xe = min(p.xe0 + xsub, max(p.xe1 - 1, 0));
+    p.xc = mc.indices[xe];
+    p.xv = mc.values[xe];
+  };
+  // (lse for wave 0, S for wave 1, the column rstd for wave 2: one wave-uniform pointer)
   auto issue = [&](int c, Pre& p) {
     GfkModelC& mc = fold_model(f, c);
-    const int32_t* ts = mc.ws_tstart + (size_t)xrow * ntp + tile;
-    p.xe0 = ts[0];
-    p.xe1 = ts[1];
     p.nb = *mc.ws_nb;
     p.cf0 = mc.adam_coef[0];
     p.cf1 = mc.adam_coef[1];
@@ -2126,9 +2151,8 @@ extern "C" __global__ void __launch_bounds__(FB_NT, 2) gfk_bwd_fold_k(GfkFold f)
       const float2 t2 = *reinterpret_cast<const float2*>(mc.ws_thetad + (size_t)xrow * kt + min(col, kt - 2));
       p.th2 = make_float2(col < K ? t2.x : 0.f, col + 1 < K ? t2.y : 0.f);
     }
-    const float* ap = tid < 64 ? mc.ws_lse + tid : tid < 128 ? mc.ws_s + (tid - 64)
-                                                             : mc.ws_col_rstd + c0 + min(tid - 128, 63);
-    p.aux = *ap;
+    const float* ap = wave == 0 ? mc.ws_lse : wave == 1 ? mc.ws_s : mc.ws_col_rstd + c0;
+    p.aux = ap[lane];
     const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc((void*)(mc.beta + mc.off_m), 0, nrec, 0x00020000);
     const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)(mc.beta + mc.off_v), 0, nrec, 0x00020000);
 #pragma unroll
@@ -2137,29 +2161,45 @@ extern "C" __global__ void __launch_bounds__(FB_NT, 2) gfk_bwd_fold_k(GfkFold f)
       p.rv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rv, voff[u], 0, 0));
     }
   };
-  auto issue_nz = [&](int c, Pre& p) {     // depends on the tile extents
-    GfkModelC& mc = fold_model(f, c);
-    const int xe = min(p.xe0 + xsub, max(p.xe1 - 1, 0));
-    p.xc = mc.indices[xe];
-    p.xv = mc.values[xe];
+  // store offsets: the slice rows past K dropped (beyond the descriptor)
+  int vst[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) vst[u] = kb + kl0 + 8 * u < K ? voff[u] : 0x7FFF0000;
+  // d theta_d stores (waves 0-3; waves 4-7 issue the same number, all dropped)
+  const int dk = kb + (lane & 15);
+  const int dnrec = 64 * K * 4;
+
+  // a client's tiles into LDS (waits for its loads); zero dlogit.  Runs at the END of the
+  // previous client's turn (and in the prologue), so the wait sits in the straight-line body
+  // right after that client's stores -- the loop top never waits on memory
+  auto stage = [&](const Pre& p) {
+    reinterpret_cast<f32x4*>(zt)[tid] = p.z0;
+    reinterpret_cast<f32x4*>(zt)[tid + FB_NT] = p.z1;
+    *reinterpret_cast<float2*>(th + xrow * FB_THS + 2 * (tid & 7)) = p.th2;
+    lse[tid] = p.aux;                       // (waves 3-7: scratch past rs, no branch)
+    for (int i = tid; i < BM * LDD / 4; i += FB_NT) reinterpret_cast<f32x4*>(dt)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // every other register of the client settles here too (an empty asm use: the wait is
+    // placed now, behind the stores, instead of inside the next turn's sparse pass)
+    asm volatile("" ::"v"(p.xe0), "v"(p.xe1), "v"(p.xc), "v"(p.xv), "v"(p.nb), "v"(p.cf0), "v"(p.cf1));
+    asm volatile("" ::"v"(p.rm[0]), "v"(p.rm[1]), "v"(p.rv[0]), "v"(p.rv[1]));
   };
 
-  Pre nx;
-  issue(0, nx);
-  issue_nz(0, nx);
+  Pre cu, nx;
+  int tn0, tn1, ts2a, ts2b;               // the tile extents of clients c + 1, c + 2
+  issue_ts(0, cu.xe0, cu.xe1);
+  issue(0, cu);
+  issue_nz(0, cu);
+  issue_ts(min(1, M - 1), tn0, tn1);
+  FOLD_STAMP(100);
+  stage(cu);
+  asm volatile("" ::"v"(tn0), "v"(tn1));  // (settled before the loop as at its latch)
+  lds_barrier();
+  FOLD_STAMP(101);
   float acc[2] = {0.f, 0.f};
   for (int c = 0; c < M; ++c) {
     GfkModelC& mc = fold_model(f, c);
-    const Pre cu = nx;
-    // ---- this client's tiles into LDS; zero dlogit ----
-    reinterpret_cast<f32x4*>(zt)[tid] = cu.z0;
-    reinterpret_cast<f32x4*>(zt)[tid + FB_NT] = cu.z1;
-    *reinterpret_cast<float2*>(th + xrow * FB_THS + 2 * (tid & 7)) = cu.th2;
-    if (tid < 192) lse[tid] = cu.aux;
-    for (int i = tid; i < BM * LDD / 4; i += FB_NT) reinterpret_cast<f32x4*>(dt)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int nb = cu.nb;
-    lds_barrier();
-    if (c + 1 < M) issue(c + 1, nx);        // lands during this client's compute
+    FOLD_STAMP(102 + 8 * c);
     // ---- (3) sparse term at this tile's non-zeros ----
     if (xrow < nb) {
       const float l = lse[xrow];
@@ -2170,8 +2210,21 @@ extern "C" __global__ void __launch_bounds__(FB_NT, 2) gfk_bwd_fold_k(GfkFold f)
         dt[xrow * LDD + col] = -x * p / (p + RL_EPS);
       }
     }
+    // ---- the next client's loads, behind the sparse pass's own (rows with more than 8
+    //      entries in the tile load the rest above: no load younger than the prefetch);
+    //      unconditional, client indices clamped (a conditional load merging into a
+    //      loop-carried register is a copy that waits for every load in flight) ----
+    {
+      const int c1 = min(c + 1, M - 1);
+      nx.xe0 = tn0;
+      nx.xe1 = tn1;
+      issue_nz(c1, nx);
+      issue(c1, nx);
+      issue_ts(min(c + 2, M - 1), ts2a, ts2b);
+    }
+    FOLD_STAMP(103 + 8 * c);
     lds_barrier();
-    if (c + 1 < M) issue_nz(c + 1, nx);
+    FOLD_STAMP(104 + 8 * c);
     // ---- (4) dense term p S and the column BN backward: 16 lanes per column ----
     for (int dcol = tid >> 4; dcol < VB; dcol += FB_NT / 16) {
       const bool valid = c0 + dcol < V;
@@ -2197,7 +2250,9 @@ extern "C" __global__ void __launch_bounds__(FB_NT, 2) gfk_bwd_fold_k(GfkFold f)
       }
     }
     lds_barrier();
+    FOLD_STAMP(105 + 8 * c);
     // ---- (5) waves 0-3: d theta_d[rows 16 w.., slice]; (6) waves 4-7: dbeta[slice, strip] ----
+    f32x4 dacc = {0.f, 0.f, 0.f, 0.f};
     if (wave < 4) {
       const float* ap = dt + (wave * 16 + (lane & 15)) * LDD + (lane >> 4);
       const float* bp = bt + (lane & 15) * LDB_B + (lane >> 4);
@@ -2207,15 +2262,7 @@ extern "C" __global__ void __launch_bounds__(FB_NT, 2) gfk_bwd_fold_k(GfkFold f)
         a0 = mfma16x16x4(ap[cc], bp[cc], a0);
         a1 = mfma16x16x4(ap[cc + 4], bp[cc + 4], a1);
       }
-      f32x4 dacc = {0.f, 0.f, 0.f, 0.f};
       dacc += a0 + a1;
-      float* dpart = mc.ws_dthetad + (size_t)tile * mc.bmax * K;
-      const int k = kb + (lane & 15);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = wave * 16 + (lane >> 4) * 4 + e;
-        if (row < nb && k < K) dpart[(size_t)row * K + k] = dacc[e];
-      }
     } else {
       const int cst = wave - 4, g = lane >> 4, gr = 8 * g;
       const float* ap = th + gr * FB_THS + (lane & 15);
@@ -2235,7 +2282,18 @@ extern "C" __global__ void __launch_bounds__(FB_NT, 2) gfk_bwd_fold_k(GfkFold f)
         zt[kl * VB + (ccl ^ ((kl & 4) << 2))] = a0[e] + a1[e];
       }
     }
+    {
+      const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(mc.ws_dthetad + (size_t)tile * 64 * K), 0, dnrec, 0x00020000);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = wave * 16 + (lane >> 4) * 4 + e;
+        const int off = (wave < 4 && row < nb && dk < K) ? (row * K + dk) * 4 : 0x7FFF0000;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(dacc[e]), rd, off, 0, 0);
+      }
+    }
     lds_barrier();
+    FOLD_STAMP(106 + 8 * c);
     // ---- Adam with this client's moments, its pre-scale, and the client-order sum ----
     {
       AdamCoef ac;
@@ -2249,18 +2307,26 @@ extern "C" __global__ void __launch_bounds__(FB_NT, 2) gfk_bwd_fold_k(GfkFold f)
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int kl = kl0 + 8 * u;
-        if (kb + kl >= K) continue;           // (wave-uniform)
         const float g = zt[kl * VB + cs];
         float mo = cu.rm[u], vo = cu.rv[u];
         float np = adam_update(bt[kl * LDB_B + cl], g, mo, vo, ac);
         if (sc) np *= fs;
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mo), rm, voff[u], 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vo), rv, voff[u], 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mo), rm, vst[u], 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vo), rv, vst[u], 0, 0);
         acc[u] = c == 0 ? np : acc[u] + np;
       }
     }
-    lds_barrier();                           // G / th / dt reads done before the next top
+    lds_barrier();                           // G / th / dt reads done
+    FOLD_STAMP(107 + 8 * c);
+    stage(nx);                               // the next client's tiles (a redundant copy of
+    cu = nx;                                 // the last client's after the last turn)
+    tn0 = ts2a;
+    tn1 = ts2b;
+    asm volatile("" ::"v"(tn0), "v"(tn1));
+    FOLD_STAMP(108 + 8 * c);
+    lds_barrier();
   }
+  FOLD_STAMP(99);
   // ---- the folded slice: every client's copy (mode 0) or client 0's (mode 1) ----
   const int nw = f.mode == 1 ? 1 : M;
   for (int c = 0; c < nw; ++c) {

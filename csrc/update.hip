@@ -1523,7 +1523,10 @@ __device__ __forceinline__ bool wf_scaled(GfkModelC& m, const float* p) {
   return m.fed_scale_on && (p - m.flat_base) < m.n_shared;
 }
 
-// W_in (tile, hidden slice js)
+// W_in (tile, hidden slice js).  The tile extents run two clients ahead (the dependent
+// first-non-zero loads one ahead), every store of the loop is an unconditional buffer store
+// (elements outside the shapes get an offset past the descriptor): the loop top waits for the
+// prefetched loads only, not for the previous client's stores.
 __device__ __forceinline__ void wf_win(const GfkFold& f, float* smem, int tile, int js) {
   float* xt = smem;                       // [64][WF_XS]  x^T tile (zero outside the scatter)
   float* dzs = xt + 64 * WF_XS;           // [64][WF_ZS]  dz0[:, j0 .. j0 + 15]
@@ -1532,25 +1535,38 @@ __device__ __forceinline__ void wf_win(const GfkFold& f, float* smem, int tile, 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int row = tid >> 2, sub = tid & 3;          // staging: row, 4 threads per row
   const int i0 = 16 * wave, jc = j0 + (lane & 15);  // MFMA subtile rows (words), output column
+  const int nrec = V * H0 * 4;
   for (int i = tid; i < 64 * WF_XS / 4; i += WF_NT) reinterpret_cast<f32x4*>(xt)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   // the shared values of this thread's 4 outputs (every client's copy holds them)
-  int eo[4];
+  int eo[4], st[4];
   float pp[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int v = c0 + i0 + (lane >> 4) * 4 + r;
     eo[r] = min(v, V - 1) * H0 + min(jc, H0 - 1);
+    st[r] = v < V && jc < H0 ? 4 * eo[r] : 0x7FFF0000;
     pp[r] = m0.w_in[eo[r]];
   }
   struct Pre {
     int xe0, xe1, nb, xc[2];
     float xv[2], dz[4], pm[4], pv[4], cf0, cf1;
   };
+  auto issue_ts = [&](int c, int& e0, int& e1) {
+    const int32_t* ts = wf_model(f, c).ws_tstart + (size_t)row * (n_tiles + 1) + tile;
+    e0 = ts[0];
+    e1 = ts[1];
+  };
+  auto issue_nz = [&](int c, Pre& p) {
+    GfkModelC& mc = wf_model(f, c);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = min(p.xe0 + sub + 4 * i, max(p.xe1 - 1, 0));
+      p.xc[i] = mc.indices[e];
+      p.xv[i] = mc.values[e];
+    }
+  };
   auto issue = [&](int c, Pre& p) {
     GfkModelC& mc = wf_model(f, c);
-    const int32_t* ts = mc.ws_tstart + (size_t)row * (n_tiles + 1) + tile;
-    p.xe0 = ts[0];
-    p.xe1 = ts[1];
     p.nb = *mc.ws_nb;
     p.cf0 = mc.adam_coef[0];
     p.cf1 = mc.adam_coef[1];
@@ -1564,40 +1580,49 @@ __device__ __forceinline__ void wf_win(const GfkFold& f, float* smem, int tile, 
       p.pv[r] = w[eo[r] + mc.off_v];
     }
   };
-  auto issue_nz = [&](int c, Pre& p) {
-    GfkModelC& mc = wf_model(f, c);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int e = min(p.xe0 + sub + 4 * i, max(p.xe1 - 1, 0));
-      p.xc[i] = mc.indices[e];
-      p.xv[i] = mc.values[e];
-    }
-  };
-  Pre nx;
-  issue(0, nx);
-  issue_nz(0, nx);
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  lds_barrier();                          // the zeroed x^T tile
-  for (int c = 0; c < M; ++c) {
-    GfkModelC& mc = wf_model(f, c);
-    const Pre cu = nx;
-    const int nb = cu.nb;
-    const bool live = row < nb;
-    // ---- stage: dz0's slice (rows >= nb and columns >= H0 zero), the x^T scatter ----
+  // a client's operands into LDS: dz0's slice (rows >= nb and columns >= H0 zero) and the
+  // x^T scatter.  Runs at the end of the previous client's turn (and in the prologue): the
+  // wait for its loads sits right behind that client's stores, the loop top never waits
+  auto stage = [&](const Pre& p, int c) {
+    const bool live = row < p.nb;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int j = j0 + 4 * sub + i;
-      dzs[row * WF_ZS + 4 * sub + i] = (j < H0 && live) ? cu.dz[i] : 0.f;
+      dzs[row * WF_ZS + 4 * sub + i] = (j < H0 && live) ? p.dz[i] : 0.f;
     }
-    const int xe1 = live ? cu.xe1 : 0;
+    const int xe1 = live ? p.xe1 : 0;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
-      if (cu.xe0 + sub + 4 * i < xe1) xt[(cu.xc[i] - c0) * WF_XS + row] = cu.xv[i];
-    for (int e = cu.xe0 + sub + 8; e < xe1; e += 4) xt[(mc.indices[e] - c0) * WF_XS + row] = mc.values[e];
-    lds_barrier();
-    if (c + 1 < M) {
-      issue(c + 1, nx);
-      issue_nz(c + 1, nx);
+      if (p.xe0 + sub + 4 * i < xe1) xt[(p.xc[i] - c0) * WF_XS + row] = p.xv[i];
+    GfkModelC& mc = wf_model(f, c);
+    for (int e = p.xe0 + sub + 8; e < xe1; e += 4) xt[(mc.indices[e] - c0) * WF_XS + row] = mc.values[e];
+    // every other register of the client settles here (empty asm uses: the waits land now,
+    // behind the previous client's stores, not inside the next turn)
+    asm volatile("" ::"v"(p.nb), "v"(p.cf0), "v"(p.cf1), "v"(p.pm[0]), "v"(p.pm[1]), "v"(p.pm[2]), "v"(p.pm[3]));
+    asm volatile("" ::"v"(p.pv[0]), "v"(p.pv[1]), "v"(p.pv[2]), "v"(p.pv[3]));
+  };
+  Pre cu, nx;
+  int tn0, tn1, ts2a, ts2b;               // the tile extents of clients c + 1, c + 2
+  issue_ts(0, cu.xe0, cu.xe1);
+  issue(0, cu);
+  issue_nz(0, cu);
+  issue_ts(min(1, M - 1), tn0, tn1);
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  lds_barrier();                          // the zeroed x^T tile
+  stage(cu, 0);
+  asm volatile("" ::"v"(tn0), "v"(tn1));  // (settled before the loop as at its latch)
+  lds_barrier();
+  for (int c = 0; c < M; ++c) {
+    GfkModelC& mc = wf_model(f, c);
+    // ---- the next client's loads (unconditional, client indices clamped: a conditional
+    //      load merging into a loop-carried register is a copy that waits for every load) ----
+    {
+      const int c1 = min(c + 1, M - 1);
+      nx.xe0 = tn0;
+      nx.xe1 = tn1;
+      issue_nz(c1, nx);
+      issue(c1, nx);
+      issue_ts(min(c + 2, M - 1), ts2a, ts2b);
     }
     // ---- G[v, j] = sum_b xt[v, b] dz[b, j] (gfk_win_update_k's subtile sequence) ----
     const float* ap = xt + (i0 + (lane & 15)) * WF_XS + (lane >> 4);
@@ -1610,36 +1635,45 @@ __device__ __forceinline__ void wf_win(const GfkFold& f, float* smem, int tile, 
     }
     const f32x4 g = c0v + c1v;
     lds_barrier();                        // every product read its operands
-    // ---- undo the scatter (the next client's tile starts from zeros) ----
+    // ---- undo the scatter (the next client's tile starts from zeros); a row with more than
+    //      8 entries in the tile clears its whole column instead of re-loading its entries ----
+    {
+      const int xe1 = row < cu.nb ? cu.xe1 : 0;
+      if (xe1 - cu.xe0 > 8) {
+        for (int v = sub; v < 64; v += 4) xt[v * WF_XS + row] = 0.f;
+      } else {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      if (cu.xe0 + sub + 4 * i < xe1) xt[(cu.xc[i] - c0) * WF_XS + row] = 0.f;
-    for (int e = cu.xe0 + sub + 8; e < xe1; e += 4) xt[(mc.indices[e] - c0) * WF_XS + row] = 0.f;
+        for (int i = 0; i < 2; ++i)
+          if (cu.xe0 + sub + 4 * i < xe1) xt[(cu.xc[i] - c0) * WF_XS + row] = 0.f;
+      }
+    }
     // ---- Adam with this client's moments, its pre-scale, the client-order sum ----
     const AdamCoef ac = wf_coef(mc, cu.cf0, cu.cf1);
     const bool sc = wf_scaled(mc, mc.w_in);
-    float* w = mc.w_in;
+    const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc((void*)(mc.w_in + mc.off_m), 0, nrec, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)(mc.w_in + mc.off_v), 0, nrec, 0x00020000);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int v = c0 + i0 + (lane >> 4) * 4 + r;
-      if (v >= V || jc >= H0) continue;
       float mo = cu.pm[r], vo = cu.pv[r];
       float np = adam_update(pp[r], g[r], mo, vo, ac);
       if (sc) np *= mc.fed_scale;
-      w[eo[r] + mc.off_m] = mo;
-      w[eo[r] + mc.off_v] = vo;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mo), rm, st[r], 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vo), rv, st[r], 0, 0);
       acc[r] = c == 0 ? np : acc[r] + np;
     }
     lds_barrier();                        // the undo is done before the next scatter
+    stage(nx, min(c + 1, M - 1));
+    cu = nx;
+    tn0 = ts2a;
+    tn1 = ts2b;
+    asm volatile("" ::"v"(tn0), "v"(tn1));
+    lds_barrier();
   }
   const int nw = f.mode == 1 ? 1 : M;
   for (int c = 0; c < nw; ++c) {
-    float* w = wf_model(f, c).w_in;
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)wf_model(f, c).w_in, 0, nrec, 0x00020000);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int v = c0 + i0 + (lane >> 4) * 4 + r;
-      if (v < V && jc < H0) w[eo[r]] = acc[r];
-    }
+    for (int r = 0; r < 4; ++r) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[r]), rw, st[r], 0, 0);
   }
 }
 
@@ -1655,7 +1689,8 @@ __device__ __forceinline__ void wf_weight(const GfkFold& f, float* smem, int jb,
   const int tid = threadIdx.x, lane = tid & 63, it = tid >> 6;
   const int b = tid >> 2, sub = tid & 3;
   const int ic = ic0 + it * 16 + (lane & 15);
-  int eo[4];
+  const int nrec = rows * cols * 4;
+  int eo[4], st[4];
   float pp[4];
   {
     const float* p0 = u0.w[jb].param;
@@ -1663,6 +1698,7 @@ __device__ __forceinline__ void wf_weight(const GfkFold& f, float* smem, int jb,
     for (int r = 0; r < 4; ++r) {
       const int j = jr0 + (lane >> 4) * 4 + r;
       eo[r] = min(j, rows - 1) * cols + min(ic, cols - 1);
+      st[r] = j < rows && ic < cols ? 4 * eo[r] : 0x7FFF0000;
       pp[r] = p0[eo[r]];
     }
   }
@@ -1704,7 +1740,7 @@ __device__ __forceinline__ void wf_weight(const GfkFold& f, float* smem, int jb,
     for (int i = 0; i < 16; ++i)
       as[b * WF_LDJ + 16 * sub + i] = (live && ic0 + 16 * sub + i < cols) ? cu.a[i] : 0.f;
     lds_barrier();
-    if (c + 1 < M) issue(c + 1, nx);
+    issue(min(c + 1, M - 1), nx);          // (unconditional: see wf_win)
     const float* ap = dzs + (lane >> 4) * WF_ZS + (lane & 15);
     const float* bp = as + (lane >> 4) * WF_LDJ + it * 16 + (lane & 15);
     f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
@@ -1717,27 +1753,24 @@ __device__ __forceinline__ void wf_weight(const GfkFold& f, float* smem, int jb,
     float* pc = uc.w[jb].param;
     const AdamCoef ac = wf_coef(mc, cu.cf0, cu.cf1);
     const bool sc = wf_scaled(mc, pc);
+    const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc((void*)(pc + mc.off_m), 0, nrec, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)(pc + mc.off_v), 0, nrec, 0x00020000);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int j = jr0 + (lane >> 4) * 4 + r;
-      if (j >= rows || ic >= cols) continue;
       float mo = cu.pm[r], vo = cu.pv[r];
       float np = adam_update(pp[r], g[r], mo, vo, ac);
       if (sc) np *= mc.fed_scale;
-      pc[eo[r] + mc.off_m] = mo;
-      pc[eo[r] + mc.off_v] = vo;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mo), rm, st[r], 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vo), rv, st[r], 0, 0);
       acc[r] = c == 0 ? np : acc[r] + np;
     }
     lds_barrier();                        // the products read their operands
   }
   const int nw = f.mode == 1 ? 1 : M;
   for (int c = 0; c < nw; ++c) {
-    float* pc = wf_upd(f, c).w[jb].param;
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)wf_upd(f, c).w[jb].param, 0, nrec, 0x00020000);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int j = jr0 + (lane >> 4) * 4 + r;
-      if (j < rows && ic < cols) pc[eo[r]] = acc[r];
-    }
+    for (int r = 0; r < 4; ++r) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[r]), rw, st[r], 0, 0);
   }
 }
 

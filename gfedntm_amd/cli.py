@@ -59,7 +59,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--log_every", type=int, default=0, help="minibatch loss line every N rounds")
     p.add_argument("--no_graph", action="store_true", help="disable hipGraph replay")
     p.add_argument("--matmul_dtype", type=str, default=None, choices=["fp32", "bf16"],
-                   help="ProdLDA decoder GEMM operands (default: [amd] matmul_dtype of the config)")
+                   help="GEMM operand precision on the matrix cores (bf16: bf16 operands, fp32 "
+                        "accumulation) of the ProdLDA and NeuralLDA decoders and CombinedTM's "
+                        "contextual forward; parameters, Adam state and every other op stay fp32 "
+                        "(default: [amd] matmul_dtype of the config)")
     p.add_argument("--agg", type=str, default="params", choices=["params", "grads"],
                    help="params: FedAvg of the shared state after every local step (reference); "
                         "grads: all-reduce of the sample-weighted gradients before one optimizer "

@@ -159,9 +159,16 @@ class FederatedClient:
         nb = int(self.plan.size[it])
         self.samples_processed += nb
         if self.log_every and it % self.log_every == 0:
-            loss = float(self.tm.engine.loss_hist[it].item())
-            self.logger.info("-- -- Minibatch %d loss %s / samples processes %d", self.current_mb,
-                             loss, self.samples_processed)
+            # the reference line (federated_avitm.py:109), then the loss's KL / RL split
+            e = self.tm.engine
+            loss = float(e.loss_hist[it].item())
+            if e.terms_on:
+                self.logger.info("-- -- Minibatch %d loss %s / samples processes %d / KL %.6g RL %.6g",
+                                 self.current_mb, loss, self.samples_processed,
+                                 float(e.kl_hist[it].item()), float(e.rl_hist[it].item()))
+            else:
+                self.logger.info("-- -- Minibatch %d loss %s / samples processes %d", self.current_mb,
+                                 loss, self.samples_processed)
         self.current_mb += 1
         if bool(self.plan.epoch_end[it]):
             self._queue_epoch_summary(self.epoch_first_step, it)

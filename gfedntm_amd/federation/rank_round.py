@@ -418,6 +418,37 @@ class MultiClientRound:
         for f in self.shared[1:]:
             f.copy_(acc)
 
+    def time_local_steps(self, s0: int, n: int) -> Optional[float]:
+        """Device milliseconds of the rank's batched local steps ALONE -- every client's step
+        kernels with per-client updates, no FedAvg (neither the in-rank fold nor the
+        collective) -- per round, replaying steps s0 .. s0 + n - 1 of the plan: the compute
+        part of bench.py's round split.  The clients' states diverge: call after the run."""
+        if not (self.fused and self.graph):
+            return None
+        from ..ops.engine import BatchedSteps
+        engines = [c.tm.engine for c in self.clients]
+        if not BatchedSteps.possible(engines):
+            return None
+        for e in engines:
+            e.prepare_external_capture()
+        bs = BatchedSteps(engines)
+        bs.prepare()
+        g = torch.cuda.CUDAGraph()
+        with graph_capture(g):
+            bs.launch()
+        for e in engines:
+            e.sync_step_counter(s0)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize(self.device)
+        ev0.record()
+        for _ in range(n):
+            g.replay()
+        ev1.record()
+        torch.cuda.synchronize(self.device)
+        for e in engines:
+            e.advance_host_step(s0 + n - 1)
+        return ev0.elapsed_time(ev1) / max(n, 1)
+
     def resync_reference(self):
         """bf16delta: the (loaded) shared state is the last averaged state."""
         for k, coll in self.colls.items():

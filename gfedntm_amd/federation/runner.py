@@ -95,6 +95,26 @@ def build_dataset(model_type: str, corpus: ClientCorpus, vocab: Dict[str, int], 
     return BOWDataset(X, idx2token)
 
 
+def term_window(clients, it: int, w: Dict) -> Dict:
+    """Mean loss / KL / RL of the window's rounds (ending at round ``it``), averaged over
+    ``clients`` (reference federated_avitm.py:109 logs the minibatch loss)."""
+    n = max(1, int(w.get("rounds") or 1))
+    vals = [c.tm.engine.term_means(max(0, it + 1 - n), it + 1) for c in clients]
+    out = {}
+    for i, k in enumerate(("loss", "kl", "rl")):
+        xs = [v[i] for v in vals if v[i] is not None]
+        if xs:
+            out[k] = float(np.mean(xs))
+    return out
+
+
+def record_terms(clients, on: bool):
+    """KL / RL histories next to the loss (before any graph capture)."""
+    if on:
+        for c in clients:
+            c.tm.engine.record_terms(True)
+
+
 class LocalFederation:
     """N clients in one process; the shared state is averaged exactly after every round."""
 
@@ -153,6 +173,7 @@ class LocalFederation:
         # -- the FedAvg sums each block first, then the block sums, in that run's order
         # fedavg_wire "bf16delta": the in-process golden of the reduced-byte FedAvg (every
         # group -- by default every client -- one rank); eager rounds
+        record_terms(self.clients, bool(self.metrics_every or log_every))
         self.agg = LocalAggregator(n, groups, wire=fedavg_wire)
         self.agg.set_reference(self.clients[0].shared)
         # fused clients on one GPU: every client's step and the FedAvg kernel are
@@ -409,9 +430,7 @@ class LocalFederation:
         w = win.close()
         if w is None:
             return
-        loss = float(np.mean([float(c.tm.engine.loss_hist[max(0, it + 1 - w["rounds"]): it + 1]
-                                    .mean().item()) for c in self.clients]))
-        self.metrics.write(event="window", round=it + 1, loss=loss, **w)
+        self.metrics.write(event="window", round=it + 1, **term_window(self.clients, it, w), **w)
 
     def finish(self):
         for c in self.clients:
@@ -624,6 +643,8 @@ def _round_loop(rr, clients, client_ids, cmap, world, rank, device, ctrl, hb, lo
     import torch.distributed as dist
     from ..parallel.digest import DigestProbe, compare
     start = 0
+    # loss / KL / RL histories for the metrics windows and the per-minibatch log line
+    record_terms(clients, bool(metrics_every or any(c.log_every for c in clients)))
     if checkpoint_dir:
         starts = {ckpt.load_client_checkpoint(checkpoint_dir, c) for c in clients}
         if len(starts) != 1:
@@ -812,7 +833,8 @@ def _round_loop(rr, clients, client_ids, cmap, world, rank, device, ctrl, hb, lo
             if metrics_every and (it + 1) % metrics_every == 0:
                 w = win.close()
                 check_comm(f"metrics window {it + 1}")
-                metrics.write(event="window", rank=rank, round=it + 1, **w)
+                metrics.write(event="window", rank=rank, round=it + 1,
+                              **term_window(clients, it, w or {}), **(w or {}))
             if checkpoint_dir and checkpoint_every and (it + 1) % checkpoint_every == 0:
                 with trace_range("checkpoint"):
                     meet(f"checkpoint {it + 1}")

@@ -51,7 +51,11 @@ class EngineBase:
         self.data: Optional[DeviceCSR] = None
         self.plan: Optional[BatchPlan] = None
         self.loss_hist: Optional[torch.Tensor] = None
+        # per-step mean KL / reconstruction terms (metrics windows, the per-minibatch log):
+        # the fused kernels fill them only while record_terms(True) is set
         self.kl_hist: Optional[torch.Tensor] = None
+        self.rl_hist: Optional[torch.Tensor] = None
+        self.terms_on = False
 
     @property
     def device(self):
@@ -60,6 +64,23 @@ class EngineBase:
     def bind_data(self, data: DeviceCSR, plan: BatchPlan):
         self.data, self.plan = data, plan
         self.loss_hist = torch.zeros(plan.n_steps, dtype=torch.float32, device=self.device)
+        self.kl_hist = torch.zeros(plan.n_steps, dtype=torch.float32, device=self.device)
+        self.rl_hist = torch.zeros(plan.n_steps, dtype=torch.float32, device=self.device)
+
+    def record_terms(self, on: bool = True):
+        """Keep the per-step mean KL and reconstruction terms in ``kl_hist`` / ``rl_hist``
+        (reference federated_avitm.py:109 logs the minibatch loss; SURVEY 5.5 asks for the
+        split).  Host-cheap for the torch engine; a flag of the fused kernels."""
+        self.terms_on = bool(on)
+
+    def term_means(self, s0: int, s1: int):
+        """(loss, KL, RL) means over steps [s0, s1) (None for terms not recorded)."""
+        if self.loss_hist is None or s1 <= s0:
+            return None, None, None
+        loss = float(self.loss_hist[s0:s1].mean())
+        if not self.terms_on:
+            return loss, None, None
+        return loss, float(self.kl_hist[s0:s1].mean()), float(self.rl_hist[s0:s1].mean())
 
     def step(self, s: int) -> torch.Tensor:
         raise NotImplementedError
@@ -151,10 +172,18 @@ class TorchEngine(EngineBase):
             est = None
         kl = kl_terms(pm, pv, mu, var, logvar, m.n_components)
         rl = reconstruction_terms(x, wd)
+        self._terms = (kl.detach(), rl.detach())
         loss = (self.beta_weight * kl + rl).sum()
         if labels is not None and est is not None:
             loss = loss + torch.nn.functional.cross_entropy(est, torch.argmax(labels, 1))
         return loss
+
+    def _record(self, s: int, loss: torch.Tensor):
+        self.loss_hist[s] = loss.detach()
+        if self.terms_on:
+            kl, rl = self._terms
+            self.kl_hist[s] = kl.mean()
+            self.rl_hist[s] = rl.mean()
 
     def step(self, s: int) -> torch.Tensor:
         return self._run_with_rng(lambda: self._step(s))
@@ -166,7 +195,7 @@ class TorchEngine(EngineBase):
         loss = self.loss_on(x, ctx, lab)
         loss.backward()
         self.optimizer.step()
-        self.loss_hist[s] = loss.detach()
+        self._record(s, loss)
         return loss.detach()
 
     @property
@@ -189,7 +218,7 @@ class TorchEngine(EngineBase):
         for k, p in self.model.named_parameters():
             if p.grad is not None:
                 self.flat.view_like(g, k).copy_(p.grad)
-        self.loss_hist[s] = loss.detach()
+        self._record(s, loss)
         return loss.detach()
 
     def apply_grads(self, s: int):

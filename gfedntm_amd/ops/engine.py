@@ -1048,11 +1048,22 @@ class FusedEngine(EngineBase):
         m.plan_start = self._plan_dev["start"].data_ptr()
         m.plan_size = self._plan_dev["size"].data_ptr()
         m.loss_hist = self.loss_hist.data_ptr()
+        m.kl_hist = self.kl_hist.data_ptr() if self.terms_on else None
+        m.rl_hist = self.rl_hist.data_ptr() if self.terms_on else None
         m.n_steps = plan.n_steps
         self.d_step.zero_()
         self._host_step = 0
         self._invalidate_graph()
         self._launch([abi.PH_BATCH_PREP])
+
+    def record_terms(self, on: bool = True):
+        """The batch-level workgroup (csrc/posterior.hip post_term_hist) writes the step's mean
+        KL and RL next to loss_hist while on (two more block sums at the end of the step)."""
+        super().record_terms(on)
+        if self.kl_hist is not None:
+            self._m.kl_hist = self.kl_hist.data_ptr() if self.terms_on else None
+            self._m.rl_hist = self.rl_hist.data_ptr() if self.terms_on else None
+            self._invalidate_graph()
 
     def phases(self) -> List[int]:
         if self._m.kind == abi.KIND_LDA:

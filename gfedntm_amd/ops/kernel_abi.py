@@ -124,6 +124,7 @@ class GfkModel(C.Structure):
         ("lab_in_enc", C.c_int32), ("bwd_pre", C.c_int32), ("ws_dt", P),
         ("dev", P), ("dev_upd", P), ("n_batch", C.c_int32), ("ldb", C.c_int32),
         ("ctx_bgrid", C.c_int32), ("ws_wstamp", P), ("ws_wgen", P), ("ws_colstat", P),
+        ("kl_hist", P), ("rl_hist", P),
     ]
 
 

@@ -89,8 +89,9 @@ class CollectiveAggregator:
             return
         if self.xgmi is not None:
             self.xgmi.set_reference(t)
-        else:
-            self.ref = t.detach().reshape(-1).clone()
+        # (kept for the torch.distributed path as well: a call that falls through to it --
+        # async, or another buffer size -- must start from the same reference on every rank)
+        self.ref = t.detach().reshape(-1).clone()
 
     def _prepare(self, flat: torch.Tensor, inplace: bool = False) -> str:
         if self.world == 1 or self.method == "rccl" or flat.device.type != "cuda":
@@ -212,24 +213,34 @@ class CollectiveAggregator:
         return works
 
     def _delta_allreduce(self, flat: torch.Tensor):
-        """bf16delta over torch.distributed (RCCL / gloo): d = bf16(f - w ref) on the wire
-        (RCCL sums bf16), W = ref + sum, ref = W -- identical on every rank.  A backend
-        without bf16 reductions (gloo builds) sums the bf16-rounded values in fp32 and rounds
-        the sum to bf16 instead (the xGMI kernel's arithmetic)."""
+        """bf16delta over torch.distributed (RCCL / gloo), with the xGMI kernel's arithmetic
+        (csrc/comm.hip gfk_xgmi_allreduce_bf16d, LocalAggregator's golden): every rank's
+        d_r = bf16(f_r - w_r ref) goes on the wire, the d_r are summed in fp32 IN RANK ORDER
+        and the sum rounded once to bf16, S; W = ref + S, ref = W -- identical on every rank
+        for any rank count.  (A native bf16 all-reduce would round after every add / ring
+        hop, and its order depends on the ring.)  The d_r travel by all_gather as int32 pairs
+        of bf16 words (bit-exact on every backend), one bucket at a time."""
         if self.ref is None:
-            self.ref = flat.detach().reshape(-1).clone()
+            raise RuntimeError("bf16delta: no reference state (set_reference / prepare first)")
         ref = self.ref
-        t = ref * torch.tensor(self.weight, dtype=torch.float32, device=ref.device)
-        d = (flat.reshape(-1) - t).to(torch.bfloat16)
-        try:
-            dist.all_reduce(d, op=dist.ReduceOp.SUM, group=self.group)
-            s = d.float()
-        except (RuntimeError, ValueError):
-            s = d.float()
-            dist.all_reduce(s, op=dist.ReduceOp.SUM, group=self.group)
-            s = s.to(torch.bfloat16).float()
-        flat.reshape(-1).copy_(ref + s)
-        ref.copy_(flat.reshape(-1))
+        n = ref.numel()
+        w = torch.tensor(self.weight, dtype=torch.float32, device=ref.device)
+        out = flat.reshape(-1)
+        step = max(2, self.bucket_elems - self.bucket_elems % 2)
+        for a in range(0, n, step):
+            b = min(n, a + step)
+            d = (out[a:b] - ref[a:b] * w).to(torch.bfloat16)
+            if d.numel() % 2:
+                d = torch.cat([d, d.new_zeros(1)])
+            words = d.view(torch.int32)
+            got = [torch.empty_like(words) for _ in range(self.world)]
+            dist.all_gather(got, words, group=self.group)
+            s = got[0].view(torch.bfloat16).float()
+            for g in got[1:]:
+                s = s + g.view(torch.bfloat16).float()
+            s = s.to(torch.bfloat16).float()[: b - a]
+            out[a:b].copy_(ref[a:b] + s)
+        ref.copy_(out)
 
     def average_(self, flat: torch.Tensor, weight: float):
         """Weighted average without a prior pre-scale (generic path)."""

@@ -135,6 +135,17 @@ def test_gloo_bf16delta_matches_golden_and_tracks_fp32():
     assert abs(l_bf - l_fp) / l_fp < 1e-3, (l_bf, l_fp)
 
 
+def test_gloo_bf16delta_three_ranks_is_bitwise_golden():
+    """3 ranks: the torch.distributed path sums the bf16 departures in fp32 in
+    rank order and rounds once (all_gather of the bf16 words), as the xGMI kernel and the
+    golden do -- a native bf16 all-reduce would round after every add, which 2 ranks cannot
+    tell apart from this arithmetic but 3 can."""
+    res = _run(3, 25, "bf16delta")
+    for r in res[1:]:
+        np.testing.assert_array_equal(res[0][1], r[1])
+    np.testing.assert_array_equal(res[0][1], _golden(3, 25, "bf16delta"))
+
+
 @pytest.mark.gpu
 def test_xgmi_bf16delta_rehearsal_is_bitwise_and_reproducible():
     res1 = _run(3, 12, "bf16delta", gpu=True)
