@@ -306,11 +306,36 @@ typedef struct GfkAdam {
 // (batch-norm running statistics): summed in client order by extra workgroups.
 // mode: 0 writes the sum into every client's buffer (one rank: the round's FedAvg is done),
 // 1 into client 0's only (the rank's partial sum, all-reduced over the ranks and broadcast).
+// One client's pointers for the fold kernels, packed by the host (ops/engine.py
+// BatchedSteps.set_fold): a client's turn reads them with a few batched scalar loads from
+// one base (the GfkModel / GfkUpdate fields, read one by one between dependent address
+// computations, cost ~1.5 us of scalar-load round trips per client turn).  *_m / *_v: the
+// Adam moments of the tensor (parameter pointer + off_m / off_v); *_sc: the FedAvg
+// pre-scale of the tensor (fed_scale, or 1 where it is not shared -- x * 1 = x exactly).
+#define GFK_FOLD_W 8
+#define GFK_FOLD_V 16
+typedef struct GfkFoldClient {
+  const int32_t *tstart, *indices;
+  const float* values;
+  const int32_t* nb;
+  const float *coef, *zn, *thetad, *lse, *s, *rstd;
+  float *beta, *beta_m, *beta_v, *dthetad;
+  const float* dz0;
+  float *w_in, *w_in_m, *w_in_v, *flat;
+  float beta_sc, win_sc, b1, b2, eps, wd;
+  const float *wdz[GFK_FOLD_W], *wa[GFK_FOLD_W];
+  float *wp[GFK_FOLD_W], *wm[GFK_FOLD_W], *wv[GFK_FOLD_W];
+  const float* vsrc[GFK_FOLD_V];
+  float *vp[GFK_FOLD_V], *vm[GFK_FOLD_V], *vv[GFK_FOLD_V], *vg[GFK_FOLD_V];
+  float wsc[GFK_FOLD_W], vsc[GFK_FOLD_V];
+} GfkFoldClient;
+
 typedef struct GfkFold {
   const GfkModel* models;        // device array [M] (the batched launch's descriptors)
   const GfkUpdate* upds;         // device array [M]
   const int64_t* left;
   int32_t M, mode, n_left, nj;   // nj: W_in hidden slices of 16 columns (ceil(H0 / 16))
+  const GfkFoldClient* cl;       // device array [M]
 } GfkFold;
 
 }  // extern "C"
@@ -617,6 +642,16 @@ __device__ __forceinline__ float adam_update(float p, float g, float& mo, float&
   vo = __builtin_fmaf(c.b2, vo, (1.f - c.b2) * g * g);
   const float den = __builtin_fmaf(__builtin_amdgcn_sqrtf(vo), c.ibc2, c.eps);
   return __builtin_fmaf(-(c.step * mo), __builtin_amdgcn_rcpf(den), p);
+}
+
+// The in-epilogue FedAvg's client-order sum (csrc/prodlda.hip gfk_bwd_fold_k, csrc/update.hip
+// gfk_win_fold_k): the client's pre-scaled value w_c p_c rounded on its own, then added --
+// contraction off, or acc + p * w would become one fma (one rounding) and differ from the
+// per-client epilogue + gfk_local_fedavg in the last bit wherever w_c is not a power of two.
+__device__ __forceinline__ float fold_add(float acc, float p, float w, bool first) {
+#pragma clang fp contract(off)
+  const float x = p * w;
+  return first ? x : acc + x;
 }
 
 // Final value of a parameter element: fused mode applies Adam (and the FedAvg

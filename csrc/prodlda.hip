@@ -2056,10 +2056,15 @@ constexpr int FB_NT = 512;
 constexpr int FB_THS = 18;       // theta_d slice stride: R8 rows r, r + 8 land 16 banks apart
 constexpr size_t FB_SMEM = sizeof(float) * (64 * VB + 64 * LDD + 64 * FB_THS + 16 * LDB_B + FB_NT);
 typedef const __attribute__((address_space(4))) GfkModel GfkModelC;
+typedef const __attribute__((address_space(4))) GfkFoldClient GfkFoldClientC;
 // the batched descriptors through the constant address space: a client's fields are scalar
 // loads wherever the client loop reaches it
 __device__ __forceinline__ GfkModelC& fold_model(const GfkFold& f, int c) {
   return ((GfkModelC*)(uintptr_t)f.models)[c];
+}
+// a client's packed pointers (csrc/gfk_common.h GfkFoldClient): a few batched scalar loads
+__device__ __forceinline__ GfkFoldClientC& fold_cl(const GfkFold& f, int c) {
+  return ((GfkFoldClientC*)(uintptr_t)f.cl)[c];
 }
 }  // namespace
 
@@ -2127,34 +2132,38 @@ extern "C" __global__ void __launch_bounds__(FB_NT, 2) gfk_bwd_fold_k(GfkFold f)
     float2 th2;
   };
   auto issue_ts = [&](int c, int& e0, int& e1) {
-    const int32_t* ts = fold_model(f, c).ws_tstart + (size_t)xrow * ntp + tile;
+    const int32_t* ts = fold_cl(f, c).tstart + (size_t)xrow * ntp + tile;
     e0 = ts[0];
     e1 = ts[1];
   };
   auto issue_nz = [&](int c, Pre& p) {     // depends on the tile extents
-    GfkModelC& mc = fold_model(f, c);
+    GfkFoldClientC& P = fold_cl(f, c);
     const int xe = min(p.xe0 + xsub, max(p.xe1 - 1, 0));
-    p.xc = mc.indices[xe];
-    p.xv = mc.values[xe];
+    p.xc = P.indices[xe];
+    p.xv = P.values[xe];
   };
   // (lse for wave 0, S for wave 1, the column rstd for wave 2: one wave-uniform pointer)
   auto issue = [&](int c, Pre& p) {
-    GfkModelC& mc = fold_model(f, c);
-    p.nb = *mc.ws_nb;
-    p.cf0 = mc.adam_coef[0];
-    p.cf1 = mc.adam_coef[1];
-    const f32x4* zs = reinterpret_cast<const f32x4*>(mc.ws_zn + (size_t)tile * BM * VB);
+    GfkFoldClientC& P = fold_cl(f, c);
+    // (the pointers first, together: one batch of scalar loads)
+    const int32_t* nbp = P.nb;
+    const float *coef = P.coef, *zn = P.zn, *thd = P.thetad, *lsep = P.lse, *sp = P.s, *rsp = P.rstd;
+    float *bm = P.beta_m, *bv = P.beta_v;
+    p.nb = *nbp;
+    p.cf0 = coef[0];
+    p.cf1 = coef[1];
+    const f32x4* zs = reinterpret_cast<const f32x4*>(zn + (size_t)tile * BM * VB);
     p.z0 = zs[tid];
     p.z1 = zs[tid + FB_NT];
     {
       const int col = kb + 2 * (tid & 7);
-      const float2 t2 = *reinterpret_cast<const float2*>(mc.ws_thetad + (size_t)xrow * kt + min(col, kt - 2));
+      const float2 t2 = *reinterpret_cast<const float2*>(thd + (size_t)xrow * kt + min(col, kt - 2));
       p.th2 = make_float2(col < K ? t2.x : 0.f, col + 1 < K ? t2.y : 0.f);
     }
-    const float* ap = wave == 0 ? mc.ws_lse : wave == 1 ? mc.ws_s : mc.ws_col_rstd + c0;
+    const float* ap = wave == 0 ? lsep : wave == 1 ? sp : rsp + c0;
     p.aux = ap[lane];
-    const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc((void*)(mc.beta + mc.off_m), 0, nrec, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)(mc.beta + mc.off_v), 0, nrec, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc((void*)bm, 0, nrec, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)bv, 0, nrec, 0x00020000);
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       p.rm[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rm, voff[u], 0, 0));
@@ -2197,15 +2206,17 @@ extern "C" __global__ void __launch_bounds__(FB_NT, 2) gfk_bwd_fold_k(GfkFold f)
   FOLD_STAMP(101);
   float acc[2] = {0.f, 0.f};
   for (int c = 0; c < M; ++c) {
-    GfkModelC& mc = fold_model(f, c);
+    GfkFoldClientC& P = fold_cl(f, c);
+    const int32_t* indices = P.indices;
+    const float* values = P.values;
     const int nb = cu.nb;
     FOLD_STAMP(102 + 8 * c);
     // ---- (3) sparse term at this tile's non-zeros ----
     if (xrow < nb) {
       const float l = lse[xrow];
       for (int i = 0, e = cu.xe0 + xsub; e < cu.xe1; ++i, e += 8) {
-        const int col = (i == 0 ? cu.xc : mc.indices[e]) - c0;
-        const float x = i == 0 ? cu.xv : mc.values[e];
+        const int col = (i == 0 ? cu.xc : indices[e]) - c0;
+        const float x = i == 0 ? cu.xv : values[e];
         const float p = __expf(zt[xrow * VB + (col ^ zswz(xrow))] - l);
         dt[xrow * LDD + col] = -x * p / (p + RL_EPS);
       }
@@ -2225,28 +2236,50 @@ extern "C" __global__ void __launch_bounds__(FB_NT, 2) gfk_bwd_fold_k(GfkFold f)
     FOLD_STAMP(103 + 8 * c);
     lds_barrier();
     FOLD_STAMP(104 + 8 * c);
-    // ---- (4) dense term p S and the column BN backward: 16 lanes per column ----
-    for (int dcol = tid >> 4; dcol < VB; dcol += FB_NT / 16) {
-      const bool valid = c0 + dcol < V;
-      constexpr int NR = BM / 16;
-      float d[NR], z[NR];
-      float s1 = 0.f, s2 = 0.f;
+    // ---- (4) dense term p S and the column BN backward: 16 lanes per column, columns
+    //      tid / 16 and tid / 16 + 32 -- every LDS operand of both columns read first (one
+    //      wait instead of a round trip per row), then prodlda_bwd's arithmetic ----
+    {
+      constexpr int NR = BM / 16, NP = VB / (FB_NT / 16);
+      float lr[NR], sr[NR], z[NP][NR], dd[NP][NR], rr[NP];
 #pragma unroll
       for (int i = 0; i < NR; ++i) {
-        const int row = dg + 16 * i;
-        z[i] = zt[row * VB + (dcol ^ zswz(row))];
-        const float p = __expf(z[i] - lse[row]);
-        d[i] = (row < nb && valid) ? p * sb[row] + dt[row * LDD + dcol] : 0.f;
-        s1 += d[i];
-        s2 += d[i] * z[i];
+        lr[i] = lse[dg + 16 * i];
+        sr[i] = sb[dg + 16 * i];
       }
-      s1 = row16_sum(s1) / (float)nb;
-      s2 = row16_sum(s2) / (float)nb;
-      const float r = valid ? rs[dcol] : 0.f;
 #pragma unroll
-      for (int i = 0; i < NR; ++i) {
-        const int row = dg + 16 * i;
-        dt[row * LDD + dcol] = row < nb ? r * (d[i] - s1 - z[i] * s2) : 0.f;
+      for (int h = 0; h < NP; ++h) {
+        const int dcol = (tid >> 4) + h * (FB_NT / 16);
+        rr[h] = rs[dcol];
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          const int row = dg + 16 * i;
+          z[h][i] = zt[row * VB + (dcol ^ zswz(row))];
+          dd[h][i] = dt[row * LDD + dcol];
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < NP; ++h) {
+        const int dcol = (tid >> 4) + h * (FB_NT / 16);
+        const bool valid = c0 + dcol < V;
+        float d[NR];
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          const int row = dg + 16 * i;
+          const float p = __expf(z[h][i] - lr[i]);
+          d[i] = (row < nb && valid) ? p * sr[i] + dd[h][i] : 0.f;
+          s1 += d[i];
+          s2 += d[i] * z[h][i];
+        }
+        s1 = row16_sum(s1) / (float)nb;
+        s2 = row16_sum(s2) / (float)nb;
+        const float r = valid ? rr[h] : 0.f;
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          const int row = dg + 16 * i;
+          dt[row * LDD + dcol] = row < nb ? r * (d[i] - s1 - z[h][i] * s2) : 0.f;
+        }
       }
     }
     lds_barrier();
@@ -2284,7 +2317,7 @@ extern "C" __global__ void __launch_bounds__(FB_NT, 2) gfk_bwd_fold_k(GfkFold f)
     }
     {
       const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(mc.ws_dthetad + (size_t)tile * 64 * K), 0, dnrec, 0x00020000);
+          (void*)(P.dthetad + (size_t)tile * 64 * K), 0, dnrec, 0x00020000);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int row = wave * 16 + (lane >> 4) * 4 + e;
@@ -2297,23 +2330,21 @@ extern "C" __global__ void __launch_bounds__(FB_NT, 2) gfk_bwd_fold_k(GfkFold f)
     // ---- Adam with this client's moments, its pre-scale, and the client-order sum ----
     {
       AdamCoef ac;
-      ac.b1 = mc.beta1; ac.b2 = mc.beta2; ac.eps = mc.adam_eps; ac.wd = mc.weight_decay;
+      ac.b1 = P.b1; ac.b2 = P.b2; ac.eps = P.eps; ac.wd = P.wd;
       ac.step = cu.cf0;
       ac.ibc2 = cu.cf1;
-      const bool sc = mc.fed_scale_on && (mc.beta - mc.flat_base) < mc.n_shared;
-      const float fs = mc.fed_scale;
-      const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc((void*)(mc.beta + mc.off_m), 0, nrec, 0x00020000);
-      const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)(mc.beta + mc.off_v), 0, nrec, 0x00020000);
+      const float fs = P.beta_sc;           // (1 where beta is not shared: x * 1 = x)
+      const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc((void*)P.beta_m, 0, nrec, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)P.beta_v, 0, nrec, 0x00020000);
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int kl = kl0 + 8 * u;
         const float g = zt[kl * VB + cs];
         float mo = cu.rm[u], vo = cu.rv[u];
-        float np = adam_update(bt[kl * LDB_B + cl], g, mo, vo, ac);
-        if (sc) np *= fs;
+        const float np = adam_update(bt[kl * LDB_B + cl], g, mo, vo, ac);
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mo), rm, vst[u], 0, 0);
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vo), rv, vst[u], 0, 0);
-        acc[u] = c == 0 ? np : acc[u] + np;
+        acc[u] = fold_add(acc[u], np, fs, c == 0);
       }
     }
     lds_barrier();                           // G / th / dt reads done
@@ -2330,8 +2361,7 @@ extern "C" __global__ void __launch_bounds__(FB_NT, 2) gfk_bwd_fold_k(GfkFold f)
   // ---- the folded slice: every client's copy (mode 0) or client 0's (mode 1) ----
   const int nw = f.mode == 1 ? 1 : M;
   for (int c = 0; c < nw; ++c) {
-    GfkModelC& mc = fold_model(f, c);
-    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)mc.beta, 0, nrec, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)fold_cl(f, c).beta, 0, nrec, 0x00020000);
 #pragma unroll
     for (int u = 0; u < 2; ++u)
       if (kb + kl0 + 8 * u < K) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[u]), rb, voff[u], 0, 0);

@@ -138,5 +138,6 @@ size_t gfk_model_struct_size() { return sizeof(GfkModel); }
 size_t gfk_adam_struct_size() { return sizeof(GfkAdam); }
 size_t gfk_update_struct_size() { return sizeof(GfkUpdate); }
 size_t gfk_fold_struct_size() { return sizeof(GfkFold); }
+size_t gfk_fold_client_struct_size() { return sizeof(GfkFoldClient); }
 
 }  // extern "C"

@@ -1512,17 +1512,30 @@ __device__ __forceinline__ GfkModelC& wf_model(const GfkFold& f, int c) {
 __device__ __forceinline__ GfkUpdateC& wf_upd(const GfkFold& f, int c) {
   return ((GfkUpdateC*)(uintptr_t)f.upds)[c];
 }
-__device__ __forceinline__ AdamCoef wf_coef(GfkModelC& m, float c0, float c1) {
+typedef const __attribute__((address_space(4))) GfkFoldClient GfkFoldClientC;
+// a client's packed pointers (csrc/gfk_common.h GfkFoldClient): a few batched scalar loads
+__device__ __forceinline__ GfkFoldClientC& wf_cl(const GfkFold& f, int c) {
+  return ((GfkFoldClientC*)(uintptr_t)f.cl)[c];
+}
+__device__ __forceinline__ AdamCoef wf_coefp(GfkFoldClientC& P, float c0, float c1) {
   AdamCoef c;
-  c.b1 = m.beta1; c.b2 = m.beta2; c.eps = m.adam_eps; c.wd = m.weight_decay;
+  c.b1 = P.b1; c.b2 = P.b2; c.eps = P.eps; c.wd = P.wd;
   c.step = c0;
   c.ibc2 = c1;
   return c;
 }
-__device__ __forceinline__ bool wf_scaled(GfkModelC& m, const float* p) {
-  return m.fed_scale_on && (p - m.flat_base) < m.n_shared;
-}
 
+#ifdef GFK_STAMPS
+#define WF_STAMP(slot)                                                            \
+  do {                                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                            \
+    if (blockIdx.x == 0 && threadIdx.x == 0 && wf_model(f, 0).dbg)               \
+      wf_model(f, 0).dbg[slot] = __builtin_amdgcn_s_memtime();                    \
+    __builtin_amdgcn_sched_barrier(0);                                            \
+  } while (0)
+#else
+#define WF_STAMP(slot) do { } while (0)
+#endif
 // W_in (tile, hidden slice js).  The tile extents run two clients ahead (the dependent
 // first-non-zero loads one ahead), every store of the loop is an unconditional buffer store
 // (elements outside the shapes get an offset past the descriptor): the loop top waits for the
@@ -1552,32 +1565,35 @@ __device__ __forceinline__ void wf_win(const GfkFold& f, float* smem, int tile, 
     float xv[2], dz[4], pm[4], pv[4], cf0, cf1;
   };
   auto issue_ts = [&](int c, int& e0, int& e1) {
-    const int32_t* ts = wf_model(f, c).ws_tstart + (size_t)row * (n_tiles + 1) + tile;
+    const int32_t* ts = wf_cl(f, c).tstart + (size_t)row * (n_tiles + 1) + tile;
     e0 = ts[0];
     e1 = ts[1];
   };
   auto issue_nz = [&](int c, Pre& p) {
-    GfkModelC& mc = wf_model(f, c);
+    GfkFoldClientC& P = wf_cl(f, c);
+    const int32_t* indices = P.indices;
+    const float* values = P.values;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int e = min(p.xe0 + sub + 4 * i, max(p.xe1 - 1, 0));
-      p.xc[i] = mc.indices[e];
-      p.xv[i] = mc.values[e];
+      p.xc[i] = indices[e];
+      p.xv[i] = values[e];
     }
   };
   auto issue = [&](int c, Pre& p) {
-    GfkModelC& mc = wf_model(f, c);
-    p.nb = *mc.ws_nb;
-    p.cf0 = mc.adam_coef[0];
-    p.cf1 = mc.adam_coef[1];
-    const float* d0 = mc.ws_dz[0] + (size_t)row * H0;
+    GfkFoldClientC& P = wf_cl(f, c);
+    const int32_t* nbp = P.nb;
+    const float *coef = P.coef, *dz0 = P.dz0, *wm = P.w_in_m, *wv = P.w_in_v;
+    p.nb = *nbp;
+    p.cf0 = coef[0];
+    p.cf1 = coef[1];
+    const float* d0 = dz0 + (size_t)row * H0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) p.dz[i] = d0[min(j0 + 4 * sub + i, H0 - 1)];
-    const float* w = mc.w_in;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      p.pm[r] = w[eo[r] + mc.off_m];
-      p.pv[r] = w[eo[r] + mc.off_v];
+      p.pm[r] = wm[eo[r]];
+      p.pv[r] = wv[eo[r]];
     }
   };
   // a client's operands into LDS: dz0's slice (rows >= nb and columns >= H0 zero) and the
@@ -1594,8 +1610,8 @@ __device__ __forceinline__ void wf_win(const GfkFold& f, float* smem, int tile, 
 #pragma unroll
     for (int i = 0; i < 2; ++i)
       if (p.xe0 + sub + 4 * i < xe1) xt[(p.xc[i] - c0) * WF_XS + row] = p.xv[i];
-    GfkModelC& mc = wf_model(f, c);
-    for (int e = p.xe0 + sub + 8; e < xe1; e += 4) xt[(mc.indices[e] - c0) * WF_XS + row] = mc.values[e];
+    GfkFoldClientC& P = wf_cl(f, c);
+    for (int e = p.xe0 + sub + 8; e < xe1; e += 4) xt[(P.indices[e] - c0) * WF_XS + row] = P.values[e];
     // every other register of the client settles here (empty asm uses: the waits land now,
     // behind the previous client's stores, not inside the next turn)
     asm volatile("" ::"v"(p.nb), "v"(p.cf0), "v"(p.cf1), "v"(p.pm[0]), "v"(p.pm[1]), "v"(p.pm[2]), "v"(p.pm[3]));
@@ -1608,11 +1624,14 @@ __device__ __forceinline__ void wf_win(const GfkFold& f, float* smem, int tile, 
   issue_nz(0, cu);
   issue_ts(min(1, M - 1), tn0, tn1);
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  WF_STAMP(300);
   lds_barrier();                          // the zeroed x^T tile
   stage(cu, 0);
   asm volatile("" ::"v"(tn0), "v"(tn1));  // (settled before the loop as at its latch)
   lds_barrier();
+  WF_STAMP(301);
   for (int c = 0; c < M; ++c) {
+    WF_STAMP(302 + 8 * c);
     GfkModelC& mc = wf_model(f, c);
     // ---- the next client's loads (unconditional, client indices clamped: a conditional
     //      load merging into a loop-carried register is a copy that waits for every load) ----
@@ -1624,6 +1643,7 @@ __device__ __forceinline__ void wf_win(const GfkFold& f, float* smem, int tile, 
       issue(c1, nx);
       issue_ts(min(c + 2, M - 1), ts2a, ts2b);
     }
+    WF_STAMP(303 + 8 * c);
     // ---- G[v, j] = sum_b xt[v, b] dz[b, j] (gfk_win_update_k's subtile sequence) ----
     const float* ap = xt + (i0 + (lane & 15)) * WF_XS + (lane >> 4);
     const float* bp = dzs + (lane >> 4) * WF_ZS + (lane & 15);
@@ -1634,7 +1654,9 @@ __device__ __forceinline__ void wf_win(const GfkFold& f, float* smem, int tile, 
       c1v = mfma16x16x4(ap[k + 4], bp[(k + 4) * WF_ZS], c1v);
     }
     const f32x4 g = c0v + c1v;
+    WF_STAMP(304 + 8 * c);
     lds_barrier();                        // every product read its operands
+    WF_STAMP(305 + 8 * c);
     // ---- undo the scatter (the next client's tile starts from zeros); a row with more than
     //      8 entries in the tile clears its whole column instead of re-loading its entries ----
     {
@@ -1648,30 +1670,34 @@ __device__ __forceinline__ void wf_win(const GfkFold& f, float* smem, int tile, 
       }
     }
     // ---- Adam with this client's moments, its pre-scale, the client-order sum ----
-    const AdamCoef ac = wf_coef(mc, cu.cf0, cu.cf1);
-    const bool sc = wf_scaled(mc, mc.w_in);
-    const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc((void*)(mc.w_in + mc.off_m), 0, nrec, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)(mc.w_in + mc.off_v), 0, nrec, 0x00020000);
+    GfkFoldClientC& P = wf_cl(f, c);
+    const AdamCoef ac = wf_coefp(P, cu.cf0, cu.cf1);
+    const float fs = P.win_sc;            // (1 where W_in is not shared: x * 1 = x)
+    const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc((void*)P.w_in_m, 0, nrec, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)P.w_in_v, 0, nrec, 0x00020000);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float mo = cu.pm[r], vo = cu.pv[r];
-      float np = adam_update(pp[r], g[r], mo, vo, ac);
-      if (sc) np *= mc.fed_scale;
+      const float np = adam_update(pp[r], g[r], mo, vo, ac);
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mo), rm, st[r], 0, 0);
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vo), rv, st[r], 0, 0);
-      acc[r] = c == 0 ? np : acc[r] + np;
+      acc[r] = fold_add(acc[r], np, fs, c == 0);
     }
+    WF_STAMP(306 + 8 * c);
     lds_barrier();                        // the undo is done before the next scatter
+    WF_STAMP(307 + 8 * c);
     stage(nx, min(c + 1, M - 1));
     cu = nx;
     tn0 = ts2a;
     tn1 = ts2b;
     asm volatile("" ::"v"(tn0), "v"(tn1));
+    WF_STAMP(308 + 8 * c);
     lds_barrier();
   }
+  WF_STAMP(299);
   const int nw = f.mode == 1 ? 1 : M;
   for (int c = 0; c < nw; ++c) {
-    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)wf_model(f, c).w_in, 0, nrec, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)wf_cl(f, c).w_in, 0, nrec, 0x00020000);
 #pragma unroll
     for (int r = 0; r < 4; ++r) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[r]), rw, st[r], 0, 0);
   }
@@ -1707,23 +1733,23 @@ __device__ __forceinline__ void wf_weight(const GfkFold& f, float* smem, int jb,
     float dz[4], a[16], pm[4], pv[4], cf0, cf1;
   };
   auto issue = [&](int c, Pre& p) {
-    GfkModelC& mc = wf_model(f, c);
-    GfkUpdateC& uc = wf_upd(f, c);
-    p.nb = *mc.ws_nb;
-    p.cf0 = mc.adam_coef[0];
-    p.cf1 = mc.adam_coef[1];
+    GfkFoldClientC& P = wf_cl(f, c);
+    const int32_t* nbp = P.nb;
+    const float *coef = P.coef, *dzp = P.wdz[jb], *ap0 = P.wa[jb], *pm0 = P.wm[jb], *pv0 = P.wv[jb];
+    p.nb = *nbp;
+    p.cf0 = coef[0];
+    p.cf1 = coef[1];
     const int bb = min(b, B - 1);
-    const float* dz = uc.w[jb].dz + (size_t)bb * rows;
-    const float* a = uc.w[jb].a + (size_t)bb * cols;
+    const float* dz = dzp + (size_t)bb * rows;
+    const float* a = ap0 + (size_t)bb * cols;
 #pragma unroll
     for (int i = 0; i < 4; ++i) p.dz[i] = dz[min(jr0 + 4 * sub + i, rows - 1)];
 #pragma unroll
     for (int i = 0; i < 16; ++i) p.a[i] = a[min(ic0 + 16 * sub + i, cols - 1)];
-    const float* pc = uc.w[jb].param;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      p.pm[r] = pc[eo[r] + mc.off_m];
-      p.pv[r] = pc[eo[r] + mc.off_v];
+      p.pm[r] = pm0[eo[r]];
+      p.pv[r] = pv0[eo[r]];
     }
   };
   Pre nx;
@@ -1749,26 +1775,24 @@ __device__ __forceinline__ void wf_weight(const GfkFold& f, float* smem, int jb,
       c1 = mfma16x16x4(ap[(k + 4) * WF_ZS], bp[(k + 4) * WF_LDJ], c1);
     }
     const f32x4 g = c0 + c1;
-    GfkUpdateC& uc = wf_upd(f, c);
-    float* pc = uc.w[jb].param;
-    const AdamCoef ac = wf_coef(mc, cu.cf0, cu.cf1);
-    const bool sc = wf_scaled(mc, pc);
-    const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc((void*)(pc + mc.off_m), 0, nrec, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)(pc + mc.off_v), 0, nrec, 0x00020000);
+    GfkFoldClientC& P = wf_cl(f, c);
+    const AdamCoef ac = wf_coefp(P, cu.cf0, cu.cf1);
+    const float fs = P.wsc[jb];
+    const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc((void*)P.wm[jb], 0, nrec, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)P.wv[jb], 0, nrec, 0x00020000);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float mo = cu.pm[r], vo = cu.pv[r];
-      float np = adam_update(pp[r], g[r], mo, vo, ac);
-      if (sc) np *= mc.fed_scale;
+      const float np = adam_update(pp[r], g[r], mo, vo, ac);
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mo), rm, st[r], 0, 0);
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vo), rv, st[r], 0, 0);
-      acc[r] = c == 0 ? np : acc[r] + np;
+      acc[r] = fold_add(acc[r], np, fs, c == 0);
     }
     lds_barrier();                        // the products read their operands
   }
   const int nw = f.mode == 1 ? 1 : M;
   for (int c = 0; c < nw; ++c) {
-    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)wf_upd(f, c).w[jb].param, 0, nrec, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)wf_cl(f, c).wp[jb], 0, nrec, 0x00020000);
 #pragma unroll
     for (int r = 0; r < 4; ++r) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[r]), rw, st[r], 0, 0);
   }
@@ -1792,26 +1816,26 @@ __device__ __forceinline__ void wf_vector(const GfkFold& f, int jv, int pass) {
 #pragma unroll
     for (int i = 0; i < WF_FG; ++i) {
       const int ci = min(g0 + i, M - 1);
-      GfkModelC& mc = wf_model(f, ci);
-      GfkUpdateC& uc = wf_upd(f, ci);
-      const float* p = uc.v[jv].param + cc;
-      nb[i] = *mc.ws_nb;
-      cf0[i] = mc.adam_coef[0];
-      cf1[i] = mc.adam_coef[1];
-      pm[i] = p[mc.off_m];
-      pv[i] = p[mc.off_v];
+      GfkFoldClientC& P = wf_cl(f, ci);
+      const int32_t* nbp = P.nb;
+      const float *coef = P.coef, *vm = P.vm[jv], *vv = P.vv[jv], *vg = P.vg[jv], *src = P.vsrc[jv];
+      nb[i] = *nbp;
+      cf0[i] = coef[0];
+      cf1[i] = coef[1];
+      pm[i] = vm[cc];
+      pv[i] = vv[cc];
       gr[i] = 0.f;
       if (has_src) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[i][u] = uc.v[jv].src[(size_t)min(s + 16 * u, B - 1) * n + cc];
+        for (int u = 0; u < 8; ++u) v[i][u] = src[(size_t)min(s + 16 * u, B - 1) * n + cc];
       } else {
-        gr[i] = p[mc.off_g];
+        gr[i] = vg[cc];
       }
     }
 #pragma unroll
     for (int i = 0; i < WF_FG; ++i) {
       if (g0 + i >= M) break;
-      GfkModelC& mc = wf_model(f, g0 + i);
+      GfkFoldClientC& P = wf_cl(f, g0 + i);
       float g = gr[i];
       if (has_src) {
         g = 0.f;
@@ -1820,18 +1844,16 @@ __device__ __forceinline__ void wf_vector(const GfkFold& f, int jv, int pass) {
         g = row16_sum(g);
       }
       if (s != 0 || c >= n) continue;
-      float* p = wf_upd(f, g0 + i).v[jv].param + cc;
       float mo = pm[i], vo = pv[i];
-      float np = adam_update(pp, g, mo, vo, wf_coef(mc, cf0[i], cf1[i]));
-      if (wf_scaled(mc, p)) np *= mc.fed_scale;
-      p[mc.off_m] = mo;
-      p[mc.off_v] = vo;
-      acc = g0 + i == 0 ? np : acc + np;
+      const float np = adam_update(pp, g, mo, vo, wf_coefp(P, cf0[i], cf1[i]));
+      P.vm[jv][cc] = mo;
+      P.vv[jv][cc] = vo;
+      acc = fold_add(acc, np, P.vsc[jv], g0 + i == 0);
     }
   }
   if (s != 0 || c >= n) return;
   const int nw = f.mode == 1 ? 1 : M;
-  for (int ci = 0; ci < nw; ++ci) wf_upd(f, ci).v[jv].param[cc] = acc;
+  for (int ci = 0; ci < nw; ++ci) wf_cl(f, ci).vp[jv][cc] = acc;
 }
 
 // leftover piece r: f.left[2 r] (first float, a multiple of 4), f.left[2 r + 1] floats (<= 1024)
@@ -1847,7 +1869,7 @@ __device__ __forceinline__ void wf_left(const GfkFold& f, int r) {
     f32x4 v[WF_FG];
 #pragma unroll
     for (int i = 0; i < WF_FG; ++i) {
-      const float* p = wf_model(f, min(g0 + i, M - 1)).flat_base + off + e;
+      const float* p = wf_cl(f, min(g0 + i, M - 1)).flat + off + e;
       if (full) {
         v[i] = *reinterpret_cast<const f32x4*>(p);
       } else {
@@ -1863,7 +1885,7 @@ __device__ __forceinline__ void wf_left(const GfkFold& f, int r) {
   }
   const int nw = f.mode == 1 ? 1 : M;
   for (int c = 0; c < nw; ++c) {
-    float* p = wf_model(f, c).flat_base + off + e;
+    float* p = wf_cl(f, c).flat + off + e;
     if (full) {
       *reinterpret_cast<f32x4*>(p) = tot;
     } else {
@@ -1881,6 +1903,7 @@ extern "C" __global__ void __launch_bounds__(WF_NT) gfk_win_fold_k(GfkFold f) {
   const int n_tiles = m0.n_tiles, nj = f.nj;
   const int n_win = 8 * nj * ((n_tiles + 7) / 8);
   int r = blockIdx.x;
+  WF_STAMP(298);
   if (r < n_win) {                  // a tile's nj slices on one XCD (they read the same x^T)
     const int x8 = r & 7, jj = r >> 3, js = jj % nj, tile = (jj / nj) * 8 + x8;
     if (tile < n_tiles) wf_win(f, smem, tile, js);
@@ -1904,7 +1927,7 @@ extern "C" size_t gfk_win_fold_smem() {
 extern "C" int gfk_win_fold_launch(const GfkModel* m0, const GfkUpdate* u0, const GfkFold* f, hipStream_t s) {
   if (m0->input != GFK_IN_BOW || m0->H[0] > 64 || m0->bmax != 64 || m0->update_mode != 1 ||
       (m0->stage_flags & (WIN_SPARSE | GFK_WIN_SPLIT | GFK_LB)) || m0->lab_on || f->M < 1 ||
-      !f->models || !f->upds || f->nj != (m0->H[0] + 15) / 16 || (f->n_left > 0 && !f->left))
+      !f->models || !f->upds || !f->cl || f->nj != (m0->H[0] + 15) / 16 || (f->n_left > 0 && !f->left))
     return -1;
   for (int j = 0; j < u0->n_v; ++j)
     if (u0->v[j].n > 64) return -1;

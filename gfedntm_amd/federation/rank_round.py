@@ -292,19 +292,21 @@ class MultiClientRound:
         if batched:
             bs = BatchedSteps(engines)
             bs.prepare()
-            # one rank: the round's FedAvg inside the update kernels' epilogues (every client
-            # starts each round from the same averaged state; GFEDNTM_FOLD=0: the fold kernel
-            # after the batched steps)
+            # one rank, GFEDNTM_FOLD=1: the round's FedAvg inside the update kernels' epilogues
+            # (every client starts each round from the same averaged state) -- bit-identical
+            # to the default, the batched steps + the fold kernel, but measured slower at the
+            # headline (0.1355 vs 0.1174 ms per round, profiles/r6/README.md): opt-in
             fold = None
-            if not self.colls and os.environ.get("GFEDNTM_FOLD", "1") != "0":
+            self.fold_plan = "fold kernel" + (" + all-reduce" if self.colls else "")
+            if not self.colls and os.environ.get("GFEDNTM_FOLD", "0") == "1":
                 why = bs.fold_reason()
                 if why is None and self._states_equal():
                     from ..ops import kernel_abi as abi
                     bs.set_fold(abi.FOLD_ALL)
                     fold = "in-epilogue"
+                    self.fold_plan = fold
                 else:
-                    fold = None
-                self.fold_plan = fold or ("fold kernel (%s)" % (why or "client states differ"))
+                    self.fold_plan = "fold kernel (%s)" % (why or "client states differ")
             # beta's / adapt_bert's shares on the side stream once the backward has
             # finished them (else reduced with the rest at the end of the round: the same
             # arithmetic)
@@ -330,6 +332,7 @@ class MultiClientRound:
             self._batched = bs
             self._bss[k] = bs             # (its device tables are baked into the graph)
         else:
+            self.fold_plan = "per-client graph branches + fold kernel"
             if self._streams is None:
                 self._streams = [torch.cuda.Stream(self.device) for _ in engines]
             joins = [torch.cuda.Event() for _ in engines]

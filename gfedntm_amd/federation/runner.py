@@ -241,9 +241,9 @@ class LocalFederation:
                 self._batched = self._batched_parts[0]
                 for b in self._batched_parts:
                     b.prepare()
-                # one group: the FedAvg inside the update kernels' epilogues
-                # (rank_round.MultiClientRound; GFEDNTM_FOLD=0: the fold kernel after the steps)
-                fold = (len(self._batched_parts) == 1 and os.environ.get("GFEDNTM_FOLD", "1") != "0"
+                # one group, GFEDNTM_FOLD=1: the FedAvg inside the update kernels' epilogues
+                # (rank_round.MultiClientRound: opt-in, measured slower than the fold kernel)
+                fold = (len(self._batched_parts) == 1 and os.environ.get("GFEDNTM_FOLD", "0") == "1"
                         and self._batched.fold_reason() is None
                         and all(torch.equal(shared[0], x) for x in shared[1:]))
                 if fold:

@@ -1700,6 +1700,11 @@ class BatchedSteps:
                     and M * fill <= self._cu):
                 mm.dec_grid = fill
             elif (mm.stage_flags & STAGE_FWD_STRIP and M * mm.dec_grid > self._cu
+                    and bstrip != "keep" and mm.mm_bf16):
+                # bf16 GEMM operands exist only in the ring variant: keep it, M clients' grids
+                # sharing one round of the CUs (the strips are grid-strided, any grid works)
+                mm.dec_grid = max(1, self._cu // M)
+            elif (mm.stage_flags & STAGE_FWD_STRIP and M * mm.dec_grid > self._cu
                     and bstrip != "keep"):
                 # (the prefetching variant has no folded posterior: post_fwd runs again)
                 mm.stage_flags = (mm.stage_flags & ~(STAGE_FWD_STRIP_ROLL | STAGE_FWD_STRIP_RING
@@ -1759,6 +1764,8 @@ class BatchedSteps:
             self._arr_u.copy_(torch.frombuffer(bytearray(b"".join(us)), dtype=torch.uint8))
             self._blob = blob
         self._host = abi.GfkModel.from_buffer_copy(ms[0])
+        if self._fold is not None:
+            self._upload_fold_table()
 
     def prepare(self):
         """Upload the descriptors now (before a capture)."""
@@ -1807,6 +1814,7 @@ class BatchedSteps:
              "dense W_in tiles only"),
             (m.kt % 2 == 0, "theta_d stride"),
             (all(e0._u.v[i].n <= 64 for i in range(e0._u.n_v)), "vector jobs <= 64 long"),
+            (e0._u.n_w <= abi.FOLD_W and e0._u.n_v <= abi.FOLD_V, "too many update jobs"),
         ]
         for ok, why in checks:
             if not ok:
@@ -1852,12 +1860,62 @@ class BatchedSteps:
         if any(p % 4 for p in pieces[0::2]):
             raise ValueError("leftover pieces must start on 16-byte boundaries")
         self._fold_left = torch.tensor(pieces or [0, 0], dtype=torch.int64, device=self.device)
+        M = len(self.engines)
+        self._fold_cl = torch.zeros(M * C.sizeof(abi.GfkFoldClient), dtype=torch.uint8,
+                                    device=self.device)
+        self._fold_cl_bytes = None
         f = abi.GfkFold()
         f.models, f.upds = self._arr_m.data_ptr(), self._arr_u.data_ptr()
         f.left = self._fold_left.data_ptr()
-        f.M, f.mode, f.n_left = len(self.engines), int(mode), len(pieces) // 2
+        f.M, f.mode, f.n_left = M, int(mode), len(pieces) // 2
         f.nj = -(-int(e0._m.H[0]) // 16)
+        f.cl = self._fold_cl.data_ptr()
         self._fold = f
+        self._upload_fold_table()
+
+    @staticmethod
+    def _fold_client(e) -> "abi.GfkFoldClient":
+        """One client's pointer table for the fold kernels (csrc GfkFoldClient)."""
+        m, u = e._m, e._u
+        c = abi.GfkFoldClient()
+        base = int(m.flat_base)
+
+        def moments(p):
+            p = int(p)
+            return p, p + 4 * int(m.off_m), p + 4 * int(m.off_v)
+
+        def scale(p):
+            return float(m.fed_scale) if (m.fed_scale_on and (int(p) - base) // 4 < int(m.n_shared)) else 1.0
+
+        c.tstart, c.indices, c.values, c.nb = m.ws_tstart, m.indices, m.values, m.ws_nb
+        c.coef, c.zn, c.thetad, c.lse, c.s, c.rstd = (m.adam_coef, m.ws_zn, m.ws_thetad, m.ws_lse,
+                                                       m.ws_s, m.ws_col_rstd)
+        c.beta, c.beta_m, c.beta_v = moments(m.beta)
+        c.dthetad, c.dz0 = m.ws_dthetad, m.ws_dz[0]
+        c.w_in, c.w_in_m, c.w_in_v = moments(m.w_in)
+        c.flat = base
+        c.beta_sc, c.win_sc = scale(m.beta), scale(m.w_in)
+        c.b1, c.b2, c.eps, c.wd = m.beta1, m.beta2, m.adam_eps, m.weight_decay
+        for j in range(u.n_w):
+            J = u.w[j]
+            c.wdz[j], c.wa[j] = J.dz, J.a
+            c.wp[j], c.wm[j], c.wv[j] = moments(J.param)
+            c.wsc[j] = scale(J.param)
+        for j in range(u.n_v):
+            J = u.v[j]
+            c.vsrc[j] = J.src
+            c.vp[j], c.vm[j], c.vv[j] = moments(J.param)
+            c.vg[j] = int(J.param) + 4 * int(m.off_g)
+            c.vsc[j] = scale(J.param)
+        return c
+
+    def _upload_fold_table(self):
+        blob = b"".join(bytes(self._fold_client(e)) for e in self.engines)
+        if blob != self._fold_cl_bytes:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("fold client table changed inside a graph capture")
+            self._fold_cl.copy_(torch.frombuffer(bytearray(blob), dtype=torch.uint8))
+            self._fold_cl_bytes = blob
 
     @property
     def fold_mode(self) -> Optional[int]:

@@ -173,10 +173,27 @@ class GfkInfer(C.Structure):
 INFER_POSTPROCESS, INFER_MOMENTS = 1, 2
 
 
+FOLD_W, FOLD_V = 8, 16
+
+
+class GfkFoldClient(C.Structure):
+    """One client's pointers for the fold kernels (csrc/gfk_common.h GfkFoldClient)."""
+    _fields_ = [("tstart", P), ("indices", P), ("values", P), ("nb", P),
+                ("coef", P), ("zn", P), ("thetad", P), ("lse", P), ("s", P), ("rstd", P),
+                ("beta", P), ("beta_m", P), ("beta_v", P), ("dthetad", P), ("dz0", P),
+                ("w_in", P), ("w_in_m", P), ("w_in_v", P), ("flat", P),
+                ("beta_sc", C.c_float), ("win_sc", C.c_float), ("b1", C.c_float), ("b2", C.c_float),
+                ("eps", C.c_float), ("wd", C.c_float),
+                ("wdz", P * FOLD_W), ("wa", P * FOLD_W), ("wp", P * FOLD_W), ("wm", P * FOLD_W),
+                ("wv", P * FOLD_W), ("vsrc", P * FOLD_V), ("vp", P * FOLD_V), ("vm", P * FOLD_V),
+                ("vv", P * FOLD_V), ("vg", P * FOLD_V),
+                ("wsc", C.c_float * FOLD_W), ("vsc", C.c_float * FOLD_V)]
+
+
 class GfkFold(C.Structure):
     """The in-epilogue FedAvg of a batched launch (csrc/gfk_common.h GfkFold)."""
     _fields_ = [("models", P), ("upds", P), ("left", P), ("M", C.c_int32), ("mode", C.c_int32),
-                ("n_left", C.c_int32), ("nj", C.c_int32)]
+                ("n_left", C.c_int32), ("nj", C.c_int32), ("cl", P)]
 
 
 FOLD_ALL, FOLD_FIRST = 0, 1
@@ -219,7 +236,9 @@ def declare(lib: C.CDLL) -> None:
         raise RuntimeError("GfkInfer ABI mismatch")
     if hasattr(lib, "gfk_fold_struct_size"):
         lib.gfk_fold_struct_size.restype = C.c_size_t
-        if lib.gfk_fold_struct_size() != C.sizeof(GfkFold):
+        lib.gfk_fold_client_struct_size.restype = C.c_size_t
+        if (lib.gfk_fold_struct_size() != C.sizeof(GfkFold)
+                or lib.gfk_fold_client_struct_size() != C.sizeof(GfkFoldClient)):
             raise RuntimeError("GfkFold ABI mismatch")
     for name, args in _EXTRA.items():
         if hasattr(lib, name):

@@ -319,3 +319,29 @@ def test_engine_step_k_is_bitwise_k_steps():
         torch.cuda.synchronize()
         res.append((tm.flat.buffer.clone(), e.loss_hist[:24].clone()))
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+
+
+def test_batched_bf16_large_vocab_keeps_ring_forward():
+    """bf16 GEMM operands live only in the ring strip forward: with more clients' grids than
+    the CUs hold (V > 64 x CUs) the batched plan keeps the ring variant on a shared grid
+    instead of switching to the fp32-only prefetching one (round 5's launcher refused it:
+    CombinedTM K=100 V=99k bf16, 8 clients).  Agrees with the per-client branch round."""
+    from gfedntm_amd.ops.engine import STAGE_FWD_STRIP_PF, STAGE_FWD_STRIP_RING
+    sc = generate_synthetic(vocab_size=60000, n_topics=20, n_docs=1200, n_nodes=2, frozen_topics=2,
+                            nwords=(150, 250), seed=17)
+    corpora = [ClientCorpus(synthetic=sc, node=i) for i in range(2)]
+    kw = dict(device="cuda", backend="fused", seed=4)
+    p = _params(batch_size=64, n_components=20, matmul_dtype="bf16")
+    a = LocalFederation(corpora, p, max_iters=3, round_batched=True, **kw)
+    b = LocalFederation(corpora, p, max_iters=3, round_batched=False, **kw)
+    a.run()
+    b.run()
+    host = a._batched._host
+    cu = torch.cuda.get_device_properties(0).multi_processor_count
+    assert host.n_tiles > cu and host.mm_bf16
+    assert host.stage_flags & STAGE_FWD_STRIP_RING and not host.stage_flags & STAGE_FWD_STRIP_PF
+    assert 2 * host.dec_grid <= cu
+    for x, y in zip(a.clients, b.clients):
+        assert torch.isfinite(x.tm.flat.buffer).all()
+        torch.testing.assert_close(x.tm.engine.loss_hist[:3], y.tm.engine.loss_hist[:3],
+                                   rtol=1e-5, atol=1e-2)

@@ -49,6 +49,25 @@ def _state(fed):
     return out
 
 
+def _assert_same(a, b):
+    """Bitwise equality of two runs' states; on a mismatch, name the client, buffer and
+    flat-layout slot of the first differing element."""
+    sa, sb = _state(a), _state(b)
+    for i, (x, y) in enumerate(zip(sa, sb)):
+        if torch.equal(x, y):
+            continue
+        c, kind = divmod(i, 4)
+        j = int(torch.nonzero(x != y)[0])
+        slot = None
+        if kind < 3:
+            for k, s in a.clients[c].tm.flat.slots.items():
+                if s.offset <= j < s.offset + s.numel:
+                    slot = (k, j - s.offset)
+        n = int((x != y).sum())
+        raise AssertionError(f"client {c} {['param', 'exp_avg', 'exp_avg_sq', 'loss'][kind]}: "
+                             f"{n} elements differ, first {j} {slot}: {float(x[j])!r} vs {float(y[j])!r}")
+
+
 @pytest.mark.parametrize("n_clients,iters", [(8, 40), (3, 25)])
 def test_fold_in_epilogue_is_bitwise_fold_kernel(monkeypatch, n_clients, iters):
     """Several epochs (partial last batches, uneven weights): the in-epilogue FedAvg gives
@@ -58,8 +77,7 @@ def test_fold_in_epilogue_is_bitwise_fold_kernel(monkeypatch, n_clients, iters):
     a = _run(monkeypatch, corpora, "1", iters)
     b = _run(monkeypatch, corpora, "0", iters)
     assert a.fold_plan == "in-epilogue" and b.fold_plan == "fold kernel"
-    for x, y in zip(_state(a), _state(b)):
-        assert torch.equal(x, y)
+    _assert_same(a, b)
     s0 = a.clients[0].shared
     for c in a.clients[1:]:
         assert torch.equal(c.shared, s0)
@@ -74,8 +92,7 @@ def test_fold_learn_priors_and_leftover_pieces(monkeypatch):
     b = _run(monkeypatch, corpora, "0", 12, learn_priors=True)
     assert a.fold_plan == "in-epilogue"
     assert a._batched._fold.n_left >= 3
-    for x, y in zip(_state(a), _state(b)):
-        assert torch.equal(x, y)
+    _assert_same(a, b)
 
 
 def test_fold_reason_refuses_other_plans():

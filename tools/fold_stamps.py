@@ -43,7 +43,12 @@ def main():
     print("fold plan:", fed.fold_plan)
     t0 = d[98]
     print("start->prologue issued", d[100] - t0, " prologue staged", d[101] - t0, " end", d[99] - t0)
-    names = ["sparse", "barrier1", "dense", "mfma", "adam", "stage", ]
+    w0 = d[298]
+    print("win: start->prologue", d[300] - w0, d[301] - w0, " end", d[299] - w0)
+    for c in range(M):
+        s = [d[302 + 8 * c + i] for i in range(7)]
+        print(f"win client {c}: top {s[0] - w0:6d} | issue {s[1] - s[0]:5d} mfma {s[2] - s[1]:5d} "
+              f"barrier {s[3] - s[2]:5d} adam {s[4] - s[3]:5d} barrier {s[5] - s[4]:5d} stage {s[6] - s[5]:5d}")
     for c in range(M):
         s = [d[102 + 8 * c + i] for i in range(7)]
         print(f"client {c}: top {s[0] - t0:6d} | issue+sparse {s[1] - s[0]:5d} barrier {s[2] - s[1]:5d} "
