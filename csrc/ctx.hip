@@ -363,372 +363,10 @@ __global__ void __launch_bounds__(FT) gfk_ctx_fwd_full_k(GfkArgT<GB> ga) {
   (void)nb;
 }
 
-// Balanced persistent shape of the CombinedTM forward (stage_flags bit 11, B <= 64,
-// H0 <= 64).  gridDim.x = ctx_parts workgroups (the resident slots); workgroup w owns the
-// contiguous columns of 16-column units [w U / G, (w + 1) U / G), U = ceil(V / 16), walked
-// in chunks of up to 64 columns.  One workgroup per 64-column tile left the last round of a
-// vocabulary mostly empty (V = 99k: 1553 tiles on 512 slots ran as 4 rounds for 3.03);
-// here every slot gets the same columns to within one unit.
-//
-// Per chunk, A [64 rows, 64 cols] = x_ctx Wa_chunk^T + ba over C in slices of 64 floats.
-// A slice (64 x_ctx rows + 64 Wa rows, 32 KB) goes global -> LDS by buffer_load ... lds
-// (no VGPRs, no ds_write), double-buffered: slice s + 1 is in flight while slice s is
-// multiplied, continuously across chunks.  The DMA writes a wave's 64 lanes to 1 KB of
-// consecutive LDS, so rows are unpadded (256 B) and XOR-swizzled instead: LDS quad p of
-// row r holds the row's quad p ^ (r & 15) (256-B rows = the 64 banks of a ds_read_b128).  The MFMA operands are read as ds_read_b128 --
-// lane (row l & 15, group g) takes quad 4 s + g of the 16-float block s and feeds its 4
-// floats to 4 successive 16x16x4 MFMAs (the reduction index permuted identically in both
-// roles); each 16-lane bank group of a read ({0-3,12-15,20-27}, ...: rows r, groups g = 0,
-// 1) covers 16 distinct quads: conflict-free (a swizzle by r mod 8 left every group 2-way).
-// Out-of-range quads (k >= C, Wa rows past the chunk) come from an offset past the buffer:
-// zeros.  After a chunk's last slice its buffer holds A (swizzled, for the P product) and
-// Wc^T of the chunk, P [64, H0] += A Wc accumulates in registers, and A goes to ws_actx;
-// the workgroup leaves ONE partial of the contextual z0 terms (ctx_parts for enc_in).
-constexpr int CTX_BAL = 2048;
-constexpr int CTX_BAL3 = 8192;          // stage_flags bit 13: the 16-wave 3-deep variant
-constexpr int FD = 64;                  // slice width (floats); one slice buffer: 128 rows x 64
-template <bool GB = false>
-__global__ void __launch_bounds__(FT, 4) gfk_ctx_fwd_bal_k(GfkArgT<GB> ga) {
-  const GfkModel& m = gfk_model(ga);
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
-  const int r = lane & 15, g = lane >> 4;
-  const int V = m.V, C = m.C, H0 = m.H[0];
-  const int G = (int)gridDim.x, w = (int)gfk_bx();
-  const int U = (V + 15) / 16;
-  const int cs = (int)((int64_t)w * U / G) * 16;
-  const int ce = min(V, (int)((int64_t)(w + 1) * U / G) * 16);
-  const int NSL = (C + FD - 1) / FD;
-  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
-  const __amdgpu_buffer_rsrc_t rs_x = __builtin_amdgcn_make_buffer_rsrc((void*)m.ctx, 0, 0x7FFFFFFF, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rs_w =
-      __builtin_amdgcn_make_buffer_rsrc((void*)m.w_a, 0, (int)((uint32_t)V * (uint32_t)C * 4u), 0x00020000);
-  constexpr uint32_t OOB = 0x80000000u;
-  // ---- DMA lanes: instruction j of wave w moves quads Q = 512 j + 64 w + lane, i.e. LDS row
-  //      R = Q >> 4 (j < 2: x_ctx row R, j >= 2: Wa row R - 64), LDS quad p = lane & 15,
-  //      global quad q = p ^ (R & 15) ----
-  uint32_t xoff[2];
-  int wrow[2], wq[2];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int R = 32 * j + 4 * wave + (lane >> 4), q = (lane & 15) ^ (R & 15);
-    if (j < 2) {
-      const int doc = m.ws_next[1 + min(R, m.bmax - 1)];
-      xoff[j] = ((uint32_t)doc * (uint32_t)C + 4u * q) * 4u;
-    } else {
-      wrow[j - 2] = R - 64;
-      wq[j - 2] = q;
-    }
-  }
-  const int xq0 = 4 * ((lane & 15) ^ ((4 * wave + (lane >> 4)) & 15));  // this lane's k within a slice
-  // (rows 32 j + 4 wave + lane >> 4: the swizzle (R & 15) is the same for j = 0..3)
-  float* buf0 = smem;                   // [2][128][64]
-  auto dma = [&](int sl, int c0c, int nvvc, float* buf) {   // slice sl of chunk c0c into buf
-    const int k0 = sl * FD;
-    const int so = uniform(k0 * 4);
-    const bool kin = k0 + xq0 < C;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float* dst = buf + (512 * j + 64 * wave) * 4;
-      uint32_t vo;
-      if (j < 2) {
-        vo = kin ? xoff[j] : OOB;
-      } else {
-        const int vv = wrow[j - 2];
-        vo = (kin && vv < nvvc) ? ((uint32_t)(c0c + vv) * (uint32_t)C + 4u * wq[j - 2]) * 4u : OOB;
-      }
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(j < 2 ? rs_x : rs_w, (lds_void_ptr)dst, 16, vo, so, 0, 0);
-    }
-  };
-  // ---- MFMA operand addresses (floats) within a slice buffer: wave (rt, cs0) = (w >> 1, 2 (w & 1)) ----
-  const int rt = wave >> 1, cs0 = 2 * (wave & 1);
-  const int ra_row = rt * 16 + r, rb0 = 64 + cs0 * 16 + r, rb1 = rb0 + 16;
-  auto qaddr = [&](int row, int quad) { return row * FD + 4 * (quad ^ (row & 15)); };
-  const int NJT = (H0 + 15) / 16;
-  f32x4 pacc[2] = {z4, z4};
-  int s = 0;                            // global slice counter (buffer s & 1)
-  if (cs < ce) dma(0, cs, min(64, ce - cs), buf0);
-  for (int c0 = cs; c0 < ce; c0 += 64) {
-    const int nvv = min(64, ce - c0);
-    // the chunk's Wc rows (for the epilogue), issued with the first slice
-    float wcr[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int i = tid + FT * u, vv = i / H0, h = i - vv * H0;
-      wcr[u] = (i < 64 * H0 && vv < nvv) ? m.w_in[(size_t)(V + c0 + min(vv, nvv - 1)) * H0 + h] : 0.f;
-    }
-    const int bv = tid & 63;
-    const float bias = bv < nvv ? m.b_a[c0 + bv] : 0.f;
-    f32x4 acc0 = z4, acc1 = z4;
-    for (int sl = 0; sl < NSL; ++sl, ++s) {
-      vm_barrier();                     // slice s landed (every wave's DMA), mma(s - 1) done
-      float* cur = buf0 + (s & 1) * 128 * FD;
-      float* nxt = buf0 + ((s + 1) & 1) * 128 * FD;
-      if (sl + 1 < NSL) dma(sl + 1, c0, nvv, nxt);
-      else if (c0 + 64 < ce) dma(0, c0 + 64, min(64, ce - c0 - 64), nxt);
-#pragma unroll
-      for (int b = 0; b < FD / 16; ++b) {
-        const f32x4 a4 = *reinterpret_cast<const f32x4*>(cur + qaddr(ra_row, 4 * b + g));
-        const f32x4 b4 = *reinterpret_cast<const f32x4*>(cur + qaddr(rb0, 4 * b + g));
-        const f32x4 c4 = *reinterpret_cast<const f32x4*>(cur + qaddr(rb1, 4 * b + g));
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          acc0 = mfma16x16x4(a4[j], b4[j], acc0);
-          acc1 = mfma16x16x4(a4[j], c4[j], acc1);
-        }
-      }
-    }
-    // ---- epilogue in the last slice's buffer: A (swizzled rows, for P) + Wc^T ----
-    float* eb = buf0 + ((s - 1) & 1) * 128 * FD;
-    float* as = eb;                     // [64 rows b][64 cols v]
-    float* wt = eb + 64 * FD;           // [64 rows h][64 cols v]
-    lds_barrier();                      // every wave done reading the last slice
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const f32x4& a4 = h ? acc1 : acc0;
-      const int col = (cs0 + h) * 16 + r;
-      const float bb = __shfl(bias, col, 64);
-      const int gc = c0 + col;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = rt * 16 + g * 4 + i;
-        const float a = col < nvv ? a4[i] + bb : 0.f;
-        as[qaddr(row, col >> 2) + (col & 3)] = a;
-        if (row < m.bmax && col < nvv)
-          m.ws_actx[((size_t)(gc >> 6) * m.bmax + row) * 64 + (gc & 63)] = a;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int i = tid + FT * u, vv = i / H0, h = i - vv * H0;
-      if (i < 64 * H0) wt[qaddr(h, vv >> 2) + (vv & 3)] = wcr[u];
-    }
-    if (H0 < 64) {                      // Wc^T rows h in [H0, 64): zero (their P columns are discarded,
-      for (int i = tid; i < (64 - H0) * 64; i += FT) wt[H0 * 64 + i] = 0.f;   // but stay finite)
-    }
-    lds_barrier();
-    // ---- P [64, H0] += A Wc: subtiles (row tile, h tile) t = wave, wave + 8 ----
-#pragma unroll
-    for (int k2 = 0; k2 < 2; ++k2) {
-      const int t = wave + (FT / 64) * k2;
-      if (t >= 4 * NJT) break;
-      const int prt = t / NJT, jt = t % NJT;
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const f32x4 a4 = *reinterpret_cast<const f32x4*>(as + qaddr(prt * 16 + r, 4 * b + g));
-        const f32x4 b4 = *reinterpret_cast<const f32x4*>(wt + qaddr(jt * 16 + r, 4 * b + g));
-#pragma unroll
-        for (int j = 0; j < 4; ++j) pacc[k2] = mfma16x16x4(a4[j], b4[j], pacc[k2]);
-      }
-    }
-  }
-  vm_barrier();                         // nothing in flight when the workgroup retires
-  // ---- this workgroup's partial of the contextual z0 terms ----
-  float* hg = m.ws_hpart + (size_t)w * m.bmax * H0;
-#pragma unroll
-  for (int k2 = 0; k2 < 2; ++k2) {
-    const int t = wave + (FT / 64) * k2;
-    if (t >= 4 * NJT) break;
-    const int prt = t / NJT, jt = t % NJT, j = jt * 16 + r;
-    if (j < H0) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = prt * 16 + g * 4 + i;
-        if (row < m.bmax) hg[(size_t)row * H0 + j] = pacc[k2][i];
-      }
-    }
-  }
-}
-
-__host__ __device__ inline int fwd_bal_lds_floats() { return 2 * 128 * FD; }
-
-// The 16-wave, 3-deep variant (ctx_parts = one workgroup per CU, H0 <= 63): slice s + 2 is in
-// flight while slice s is multiplied (a 3-buffer ring, 96 KB), the waits counted per slice
-// (s_waitcnt vmcnt(2) / (3): only the newer slice's 2 DMA instructions -- and the next
-// chunk's Wc block -- may still be outstanding; a full drain once per chunk, after the
-// epilogue's stores).  The 16 waves split each slice's 4 16-float blocks in two halves
-// (kh = wave >> 3) over the same 8 (row tile, column pair) subtiles; the halves are summed
-// through LDS in the epilogue.  The chunk's Wc rows and bias come by DMA as well (double-
-// buffered), so the epilogue never waits on a global load issued before the slices'.
-constexpr int FT3 = 1024;
-__host__ __device__ inline int bal3_wcb_floats() { return 4096 + 64; }
-__host__ __device__ inline int fwd_bal3_lds_floats() { return 3 * 128 * FD + 2 * bal3_wcb_floats() + 64 * FD; }
-template <bool GB = false>
-__global__ void __launch_bounds__(FT3) gfk_ctx_fwd_bal3_k(GfkArgT<GB> ga) {
-  const GfkModel& m = gfk_model(ga);
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
-  const int r = lane & 15, g = lane >> 4;
-  const int V = m.V, C = m.C, H0 = m.H[0];
-  const int G = (int)gridDim.x, w = (int)gfk_bx();
-  const int U = (V + 15) / 16;
-  const int cs = (int)((int64_t)w * U / G) * 16;
-  const int ce = min(V, (int)((int64_t)(w + 1) * U / G) * 16);
-  const int NSL = (C + FD - 1) / FD;
-  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
-  const __amdgpu_buffer_rsrc_t rs_x = __builtin_amdgcn_make_buffer_rsrc((void*)m.ctx, 0, 0x7FFFFFFF, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rs_w =
-      __builtin_amdgcn_make_buffer_rsrc((void*)m.w_a, 0, (int)((uint32_t)V * (uint32_t)C * 4u), 0x00020000);
-  // Wc and ba through one resource on the flat parameter buffer (offsets < 2 GB: host check)
-  const __amdgpu_buffer_rsrc_t rs_f = __builtin_amdgcn_make_buffer_rsrc((void*)m.flat_base, 0, 0x7FFFFFFF, 0x00020000);
-  const uint32_t wc_off = (uint32_t)((m.w_in + (size_t)V * H0) - m.flat_base) * 4u;
-  const uint32_t ba_off = (uint32_t)(m.b_a - m.flat_base) * 4u;
-  constexpr uint32_t OOB = 0x80000000u;
-  float* ring = smem;                               // [3][128][64]
-  float* wcb0 = smem + 3 * 128 * FD;                // [2][Wc block (64 H0, at most 4032) | bias (64 at 4032)]
-  float* ar = wcb0 + 2 * bal3_wcb_floats();         // [64][64] A (swizzled rows) / kh partials
-  // ---- slice DMA: instruction j (0: x_ctx, 1: Wa) of wave w moves quads 1024 j + 64 w + lane,
-  //      LDS row R = 64 j + 4 w + lane >> 4, LDS quad p = lane & 15, global quad p ^ (R & 15) ----
-  const int R0 = 4 * wave + (lane >> 4);
-  const int q = (lane & 15) ^ (R0 & 15);
-  const uint32_t xoff = ((uint32_t)m.ws_next[1 + min(R0, m.bmax - 1)] * (uint32_t)C + 4u * q) * 4u;
-  auto dma = [&](int sl, int c0c, int nvvc, float* buf) {
-    const int k0 = sl * FD;
-    const int so = uniform(k0 * 4);
-    const bool kin = k0 + 4 * q < C;
-    const uint32_t vw = (kin && R0 < nvvc) ? ((uint32_t)(c0c + R0) * (uint32_t)C + 4u * q) * 4u : OOB;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_x, (lds_void_ptr)(buf + 64 * wave * 4), 16, kin ? xoff : OOB, so, 0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_w, (lds_void_ptr)(buf + (1024 + 64 * wave) * 4), 16, vw, so, 0, 0);
-  };
-  // ---- the chunk's Wc rows (quads 64 w + lane < 16 H0) and bias (quads 1008..1023): one
-  //      instruction per wave, one (flat) resource ----
-  auto aux = [&](int c0c, int nvvc, float* wb) {
-    const int Q = 64 * wave + lane;
-    uint32_t vo;
-    if (Q >= 1008) {
-      const int cb = c0c + 4 * (Q - 1008);
-      vo = cb < V ? ba_off + (uint32_t)cb * 4u : OOB;
-    } else {
-      const int e = 4 * Q;
-      vo = e < nvvc * H0 ? wc_off + ((uint32_t)c0c * (uint32_t)H0 + (uint32_t)e) * 4u : OOB;
-    }
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_f, (lds_void_ptr)(wb + 64 * wave * 4), 16, vo, 0, 0, 0);
-  };
-  const int kh = wave >> 3, w8 = wave & 7;
-  const int rt = w8 >> 1, cs0 = 2 * (w8 & 1);
-  const int ra_row = rt * 16 + r, rb0 = 64 + cs0 * 16 + r, rb1 = rb0 + 16;
-  auto qaddr = [&](int row, int quad) { return row * FD + 4 * (quad ^ (row & 15)); };
-  const int NJT = (H0 + 15) / 16;
-  f32x4 pacc = z4;
-  // the slice wait: everything a wave issued after slice s's DMA is what it issued at the top
-  // of slice s - 1 (`newer`: 0, 2 or 3 instructions) -- except at a chunk's first slice, after
-  // the epilogue's stores: drain
-  int newer = 0;
-  auto wait_slice = [&](int sl) {
-    if (sl == 0) { vm_barrier(); return; }
-    if (sl == 1) { lds_barrier(); return; }               // drained at sl == 0
-    if (newer == 3) asm volatile("s_waitcnt vmcnt(3)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else if (newer == 2) asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    else vm_barrier();
-  };
-  int s = 0, j = 0;
-  if (cs < ce) {
-    const int nvv0 = min(64, ce - cs);
-    dma(0, cs, nvv0, ring);
-    aux(cs, nvv0, wcb0);
-    if (NSL > 1) dma(1, cs, nvv0, ring + 128 * FD);
-    else if (cs + 64 < ce) dma(0, cs + 64, min(64, ce - cs - 64), ring + 128 * FD);
-  }
-  for (int c0 = cs; c0 < ce; c0 += 64, ++j) {
-    const int nvv = min(64, ce - c0);
-    f32x4 acc0 = z4, acc1 = z4;
-    for (int sl = 0; sl < NSL; ++sl, ++s) {
-      wait_slice(sl);
-      __builtin_amdgcn_sched_barrier(0);
-      float* cur = ring + (s % 3) * 128 * FD;
-      float* nx2 = ring + ((s + 2) % 3) * 128 * FD;
-      // slice s + 2: this chunk's, or the next chunk's first (with its Wc block / bias: NSL >= 4)
-      newer = 0;
-      {
-        const int sl2 = sl + 2 < NSL ? sl + 2 : sl + 2 - NSL;
-        const int c2 = sl + 2 < NSL ? c0 : c0 + 64;
-        if (c2 < ce) {
-          const int nv2 = min(64, ce - c2);
-          dma(sl2, c2, nv2, nx2);
-          newer = 2;
-          if (sl2 == 0) {
-            aux(c2, nv2, wcb0 + ((j + 1) & 1) * bal3_wcb_floats());
-            newer = 3;
-          }
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      // this wave's two 16-float blocks (2 kh, 2 kh + 1): all 6 operand reads, then 16 MFMAs
-      f32x4 a4[2], b4[2], c4[2];
-#pragma unroll
-      for (int bb = 0; bb < 2; ++bb) {
-        const int b = 2 * kh + bb;
-        a4[bb] = *reinterpret_cast<const f32x4*>(cur + qaddr(ra_row, 4 * b + g));
-        b4[bb] = *reinterpret_cast<const f32x4*>(cur + qaddr(rb0, 4 * b + g));
-        c4[bb] = *reinterpret_cast<const f32x4*>(cur + qaddr(rb1, 4 * b + g));
-      }
-#pragma unroll
-      for (int bb = 0; bb < 2; ++bb)
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          acc0 = mfma16x16x4(a4[bb][jj], b4[bb][jj], acc0);
-          acc1 = mfma16x16x4(a4[bb][jj], c4[bb][jj], acc1);
-        }
-    }
-    // ---- epilogue: the k-halves summed in ar, + bias, -> ar (swizzled) and ws_actx; P += A Wc ----
-    const float* wb = wcb0 + (j & 1) * bal3_wcb_floats();
-    if (kh == 1) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const f32x4& a4v = h ? acc1 : acc0;
-        const int col = (cs0 + h) * 16 + r;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) ar[qaddr(rt * 16 + g * 4 + i, col >> 2) + (col & 3)] = a4v[i];
-      }
-    }
-    lds_barrier();
-    if (kh == 0) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const f32x4& a4v = h ? acc1 : acc0;
-        const int col = (cs0 + h) * 16 + r;
-        const float bb = wb[4032 + col];
-        const int gc = c0 + col;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = rt * 16 + g * 4 + i;
-          const int ad = qaddr(row, col >> 2) + (col & 3);
-          const float a = col < nvv ? a4v[i] + ar[ad] + bb : 0.f;
-          ar[ad] = a;
-          if (row < m.bmax && col < nvv)
-            m.ws_actx[((size_t)(gc >> 6) * m.bmax + row) * 64 + (gc & 63)] = a;
-        }
-      }
-    }
-    lds_barrier();
-    if (wave < 4 * NJT) {                 // P subtile (row tile, h tile) = (wave / NJT, wave % NJT)
-      const int prt = wave / NJT, jt = wave % NJT;
-      const int hh = min(jt * 16 + r, H0 - 1);
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const f32x4 av = *reinterpret_cast<const f32x4*>(ar + qaddr(prt * 16 + r, 4 * b + g));
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) pacc = mfma16x16x4(av[jj], wb[(16 * b + 4 * g + jj) * H0 + hh], pacc);
-      }
-    }
-  }
-  vm_barrier();                         // nothing in flight when the workgroup retires
-  float* hg = m.ws_hpart + (size_t)w * m.bmax * H0;
-  if (wave < 4 * NJT) {
-    const int prt = wave / NJT, jt = wave % NJT, jh = jt * 16 + r;
-    if (jh < H0) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = prt * 16 + g * 4 + i;
-        if (row < m.bmax) hg[(size_t)row * H0 + jh] = pacc[i];
-      }
-    }
-  }
-}
-
-// Register-streamed forward (stage_flags bit 15, GFEDNTM_CTX_BAL=4; B <= 64, H0 <= 64, at
-// most 32 16-column units per workgroup).  The DMA-staged variants above move every Wa slice
-// AND the matching x_ctx slice through LDS once per 64-column chunk (x_ctx re-staged per
+// Register-streamed forward (stage_flags bit 15; B <= 64, H0 <= 64, at most 32 16-column
+// units per workgroup).  The DMA-staged balanced variants of rounds 3-4 (removed in round 6;
+// profiles/r4/ab_s8) moved every Wa slice AND the matching x_ctx slice through LDS once per
+// 64-column chunk (x_ctx re-staged per
 // chunk, a barrier per slice, and at most two slices = 1.7 us of Wa in flight per CU).  Here
 // one 16-wave workgroup per CU owns a contiguous range of nu 16-column units; wave w owns
 // units w and w + 16 of it, and computes A^T[v, b] = sum_k Wa[v, k] x[b, k] with Wa as the
@@ -753,16 +391,11 @@ __global__ void __launch_bounds__(FT3) gfk_ctx_fwd_bal3_k(GfkArgT<GB> ga) {
 // Wc from global in chunks of 8 k steps, the next chunk in flight): ONE z0 partial per
 // workgroup in ws_hpart (ctx_parts = the grid), as the balanced kernels leave it.
 constexpr int CTX_RS = 32768;
-// GFK_RS_RING: ring blocks per wave.  Interleaved at V = 99k (profiles/r4/ab_s9): 4 blocks
+// RS_R: ring blocks per wave.  Interleaved at V = 99k (profiles/r4/ab_s9): 4 blocks
 // 121.4 us, 8 blocks 124.9 us; 4 + the next block's x operands read before this block's
 // MFMAs 121.1 us (not kept) -- the ring's depth and the LDS reads are not the limit: the
 // busiest SIMD's MFMAs (main + P) are ~75 % of the kernel's cycles
-#ifndef GFK_RS_RING
-#define GFK_RS_RING 4
-#endif
-#define GFK_STR2(x) #x
-#define GFK_STR(x) GFK_STR2(x)
-constexpr int RS_T = 1024, RS_KP = 256, RS_R = GFK_RS_RING, RS_AL = 512;
+constexpr int RS_T = 1024, RS_KP = 256, RS_R = 4, RS_AL = 512;
 static_assert((RS_KP / 16) % RS_R == 0, "a segment's blocks cycle the ring whole");
 // x phases / A [64][RS_AL] (the same 128 KB), + 3 split-unit partials [64][16]
 __host__ __device__ inline int fwd_rs_lds_floats() { return 2 * 64 * RS_KP + 3 * 64 * 16; }
@@ -858,7 +491,7 @@ __global__ void __launch_bounds__(RS_T) gfk_ctx_fwd_rs_k(GfkArgT<GB> ga) {
   for (int p = 0; p < NPH; ++p) {
     // phase p's x: issued before every ring load still in flight (RS_R of them, issued
     // after it by any wave with a segment since; a wave without one may have issued none)
-    if (has0 || helper) asm volatile("s_waitcnt vmcnt(" GFK_STR(GFK_RS_RING) ")\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (has0 || helper) asm volatile("s_waitcnt vmcnt(4)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     else vm_barrier();
     // (4 j + g) ^ r = 16 (j >> 2) + 4 ((j & 3) ^ (r >> 2)) + (g ^ (r & 3)): four lane
     // offsets, the rest immediates
@@ -1395,8 +1028,6 @@ __host__ __device__ inline int fwd_full_lds_floats(const GfkModel& m) {
 extern "C" size_t gfk_ctx_smem(const GfkModel* m) {
   size_t a = fwd_lds_floats(*m), b = bwd_lds(*m).total;
   if ((m->stage_flags & CTX_FULL) && (size_t)fwd_full_lds_floats(*m) > a) a = fwd_full_lds_floats(*m);
-  if ((m->stage_flags & CTX_BAL) && (size_t)fwd_bal_lds_floats() > a) a = fwd_bal_lds_floats();
-  if ((m->stage_flags & CTX_BAL3) && (size_t)fwd_bal3_lds_floats() > a) a = fwd_bal3_lds_floats();
   if ((m->stage_flags & CTX_RS) && (size_t)fwd_rs_lds_floats() > a) a = fwd_rs_lds_floats();
   if ((m->stage_flags & CTX_BWDPP) && (size_t)pp_lds(*m).total > b) b = pp_lds(*m).total;
   return sizeof(float) * (a > b ? a : b);
@@ -1413,9 +1044,7 @@ extern "C" int gfk_ctx_set_smem(size_t bytes) {
                       (const void*)gfk_ctx_bwd_k<16>, (const void*)gfk_ctx_bwd_k<16, true>, (const void*)gfk_ctx_bwd_k<32>, (const void*)gfk_ctx_bwd_k<32, true>,
                       (const void*)gfk_ctx_bwd_k<64>, (const void*)gfk_ctx_bwd_k<64, true>, (const void*)gfk_ctx_bwd_k<128>, (const void*)gfk_ctx_bwd_k<128, true>,
                       (const void*)gfk_ctx_fwd_full_k<false>, (const void*)gfk_ctx_fwd_full_k<true>,
-                      (const void*)gfk_ctx_fwd_bal_k<false>, (const void*)gfk_ctx_fwd_bal_k<true>,
                       (const void*)gfk_ctx_bwd_pp_k<false>, (const void*)gfk_ctx_bwd_pp_k<true>,
-                      (const void*)gfk_ctx_fwd_bal3_k<false>, (const void*)gfk_ctx_fwd_bal3_k<true>,
                       (const void*)gfk_ctx_fwd_rs_k<false>, (const void*)gfk_ctx_fwd_rs_k<true>,
                       (const void*)gfk_ctx_fwd_rs_k<false, true>, (const void*)gfk_ctx_fwd_rs_k<true, true>};
   for (const void* k : ks) {
@@ -1448,20 +1077,6 @@ extern "C" int gfk_launch_ctx_fwd(const GfkModel* m, hipStream_t s) {
       do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_ctx_fwd_rs_k<true, true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_ctx_fwd_rs_k<false, true>), g, t, sm, s, GfkArgT<false>{*m}); } while (0);
     else
       do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_ctx_fwd_rs_k<true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_ctx_fwd_rs_k<false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0);
-    return (int)hipGetLastError();
-  }
-  if ((m->stage_flags & CTX_FULL) && (m->stage_flags & CTX_BAL3) && m->bmax <= 64 && m->H[0] <= 63 && m->C > 3 * FD &&
-      m->ctx_parts > 0 && m->ctx_parts <= m->n_tiles) {
-    const dim3 g(m->ctx_parts), t(FT3);
-    const size_t sm = sizeof(float) * fwd_bal3_lds_floats();
-    do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_ctx_fwd_bal3_k<true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_ctx_fwd_bal3_k<false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0);
-    return (int)hipGetLastError();
-  }
-  if ((m->stage_flags & CTX_FULL) && (m->stage_flags & CTX_BAL) && m->bmax <= 64 && m->H[0] <= 64 &&
-      m->ctx_parts > 0 && m->ctx_parts <= m->n_tiles) {
-    const dim3 g(m->ctx_parts), t(FT);
-    const size_t sm = sizeof(float) * fwd_bal_lds_floats();
-    do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_ctx_fwd_bal_k<true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_ctx_fwd_bal_k<false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0);
     return (int)hipGetLastError();
   }
   if ((m->stage_flags & CTX_FULL) && m->bmax <= 64) {

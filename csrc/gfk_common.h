@@ -54,8 +54,6 @@ typedef struct GfkModel {
   float drop_enc, drop_theta;
   float bn_momentum, bn_eps;
   float kl_weight;       // CTM loss_weights["beta"], 1 for AVITM
-  int32_t beta_split;    // 1: prodlda_bwd writes beta's gradient (fused mode otherwise) and
-                         //    the generic optimizer kernel updates beta in one float4 pass
   uint64_t seed;
 
   // ---- parameters (views into the flat fp32 buffer) and their gradients ----
@@ -178,12 +176,6 @@ typedef struct GfkModel {
   // CombinedTM backward, persistent pipelined shape (stage_flags bit 12): workgroups
   // (one per CU) of csrc/ctx.hip gfk_ctx_bwd_pp_k (0: the (tile, chunk) grid)
   int32_t ctx_bgrid;
-  // ---- split W_in update (stage_flags bit 7, GFK_WIN_SPLIT): prepare_next_batch stamps
-  // every word of the next batch with a fresh generation (ws_wstamp[V], ws_wgen[1]); the
-  // words NOT in the batch get their zero-gradient Adam step from gfk_win_dense_k on a side
-  // stream while the decoder runs, and the sparse W_in tiles update only the batch's words
-  int32_t* ws_wstamp;
-  int32_t* ws_wgen;
   // ---- the large-batch plan (stage_flags GFK_LB): the posterior's column statistics,
   // computed once per step (csrc/posterior.hip gfk_post_colstats_lb_k): [mean | rstd] of the
   // raw heads, [sum dy | sum dy xhat] of the backward, the priors' sums, 2K floats each ----
@@ -194,22 +186,10 @@ typedef struct GfkModel {
   float* rl_hist;
 } GfkModel;
 
-constexpr int GFK_WIN_SPLIT = 128;
-
 // stage_flags bit 16 (GFK_FWD_POSTFOLD): the ProdLDA strip forward's ring variant computes
 // the batch-coupled posterior itself (csrc/prodlda.hip, FP) and post_fwd is not launched --
 // where it applies: strip ring forward (bit 2 + bit 8), K <= 64, B <= 64, no label head
 constexpr int GFK_FWD_POSTFOLD = 65536;
-// stage_flags bit 17 (GFK_POST_EXTRA_ROWBWD): post_bwd's batch-level workgroup (prior
-// gradients, the loss, the step counter) runs as an extra workgroup of row_bwd instead, so
-// post_bwd is exactly bmax workgroups (batched launches: M clients' post_bwd then fits one
-// round of the CUs' slots; its inputs -- mu, log sigma^2, KL, RL -- are final before row_bwd)
-constexpr int GFK_POST_EXTRA_ROWBWD = 131072;
-// stage_flags bit 18 (GFK_BWD_KQ1): the ProdLDA backward keeps the one-k-range shape with
-// fewer slabs than vocabulary tiles (n_dpart < n_tiles: each 16-wave workgroup walks
-// several tiles), K <= 64 -- batched launches, where M clients' one-workgroup-per-tile grid
-// would run in two rounds
-constexpr int GFK_BWD_KQ1 = 262144;
 // stage_flags bit 19 (GFK_LB): the large-batch plan, 128 < bmax <= GFK_BMAX_LIMIT.  The
 // ProdLDA decoder's three products (logits = theta_d beta, dbeta = theta_d^T dlogit,
 // d theta_d = dlogit beta^T) are library GEMMs issued by the engine on the step's stream
@@ -220,7 +200,10 @@ constexpr int GFK_BWD_KQ1 = 262144;
 // beta backward builds its x^T tile per 128-row chunk; gradient mode + the generic
 // optimizer kernel
 constexpr int GFK_LB = 524288;
-// stage_flags bit 20 (GFK_POST_ROWS2): post_bwd takes two rows per workgroup (batched launches)
+// stage_flags bit 20 (GFK_POST_ROWS2, batched launches): post_bwd takes two rows per
+// workgroup, and its batch-level workgroup (prior gradients, the loss, the step counter)
+// runs as an extra workgroup of row_bwd instead (its inputs -- mu, log sigma^2, KL, RL --
+// are final before row_bwd): M clients' post_bwd is M bmax / 2 workgroups, one round
 constexpr int GFK_POST_ROWS2 = 1048576;
 constexpr int GFK_BMAX_LIMIT = 512;
 // H[n_hidden - 1] without a runtime index into the descriptor (a batched kernel's copy of it
@@ -241,7 +224,7 @@ __host__ __device__ __forceinline__ int gfk_hlast(const GfkModel& m) {
   return h;
 }
 __host__ __device__ inline bool gfk_postfold(const GfkModel& m) {
-  return (m.stage_flags & GFK_FWD_POSTFOLD) && (m.stage_flags & 4) && (m.stage_flags & 256) &&
+  return (m.stage_flags & GFK_FWD_POSTFOLD) && (m.stage_flags & 4) && !(m.stage_flags & 8) &&
          m.K <= 64 && m.bmax <= 64 && !m.lab_on && m.kind == GFK_PRODLDA;
 }
 
@@ -366,27 +349,18 @@ template <> struct GfkArgT<true> { const GfkModel* p; };
 // client's previous outputs (heads, theta_d, logit tiles, ...) and parameters in its own
 // XCD's L2 instead of another die's.  Indices b and b + 8 of a client still share an XCD
 // (their L differ by 8 M), which the pipelined backward's tile grouping relies on.
-// (-DGFK_NO_XCD_MAP: the plain (blockIdx.z, blockIdx.x), for A/B builds.)
 // (power-of-two client counts only -- shifts and masks on scalar registers; a division here
 // would run on the VALU and cost the 64-VGPR kernels spills -- other counts keep the plain
 // placement)
 __device__ __forceinline__ int gfk_bz() {
-#ifdef GFK_NO_XCD_MAP
-  return (int)blockIdx.z;
-#else
   const unsigned M = gridDim.z;
   if (M & (M - 1)) return (int)blockIdx.z;
   return (int)((blockIdx.x + gridDim.x * blockIdx.z) & (M - 1));
-#endif
 }
 __device__ __forceinline__ int gfk_bx() {
-#ifdef GFK_NO_XCD_MAP
-  return (int)blockIdx.x;
-#else
   const unsigned M = gridDim.z;
   if (M & (M - 1)) return (int)blockIdx.x;
   return (int)((blockIdx.x + gridDim.x * blockIdx.z) >> __builtin_ctz(M));
-#endif
 }
 __device__ __forceinline__ const GfkModel& gfk_model(const GfkArgT<false>& a) { return a.m; }
 // (the batched models through the constant address space: the field loads stay scalar
@@ -424,20 +398,6 @@ namespace gfk {
 
 // In-kernel phase timestamps for diagnostic builds (-DGFK_STAMPS): lane 0 of
 // workgroup 0 writes s_memtime into dbg[slot].  Compiled out otherwise.
-#ifndef GFK_POST_PLAIN_LDS
-// posterior batch matrices staged contiguously (the default): the padded 2 x odd row stride
-// removes the K = 100 column reductions' bank conflicts (31 % -> 0 %) but its per-row dword
-// LDS-DMA costs more than they did -- CombinedTM K = 100 V = 99k, interleaved on one box:
-// 0.7296 / 0.7355 ms contiguous vs 0.7369 / 0.7432 padded (profiles/r5/ab_post_stride.txt).
-// -DGFK_POST_PLAIN_LDS=0 builds the padded layout
-#define GFK_POST_PLAIN_LDS 1
-#endif
-#ifndef GFK_STRIP_OLDEST_LIGHT
-#define GFK_STRIP_OLDEST_LIGHT 0   // strip forward: wave groups in reverse order (A/B builds)
-#endif
-#ifndef GFK_DIAG_BWD
-#define GFK_DIAG_BWD 0      // diagnostic variants of prodlda_bwd_pipe_kernel (tools/ab_libs.py AB_DEFS)
-#endif
 #ifdef GFK_STAMPS
 #define GFK_STAMP(m, slot)                                                        \
   do {                                                                            \
@@ -616,8 +576,8 @@ __device__ __forceinline__ AdamCoef adam_coef(const GfkModel& m) {
 }
 
 // One optimizer step's advance of the running powers and the bias-correction coefficients
-// (post_fwd; and gfk_win_dense_k from prepare_next_batch's snapshot of the powers, which
-// must produce the same bits: contraction off, every operation explicit).
+// (post_fwd, the strip forward's folded posterior and the large-batch plan, which must
+// produce the same bits: contraction off, every operation explicit).
 __device__ __forceinline__ void adam_advance(const GfkModel& m, double pw0, double pw1, double& p1,
                                              double& p2, float& c0, float& c1) {
 #pragma clang fp contract(off)
@@ -632,9 +592,9 @@ __device__ __forceinline__ void adam_advance(const GfkModel& m, double pw0, doub
 // with their denormal scaling): the optimizer epilogues of the large-vocabulary
 // kernels are VALU-heavy, and the step's relative error stays ~1e-7 of an lr-sized term.
 // Every fused multiply-add is explicit and contraction is off, so the update rounds the
-// same way in every kernel it is inlined into (the split W_in update's two halves must
-// agree bit for bit with the one-kernel update; the compiler's own contraction choices
-// differ between kernels).
+// same way in every kernel it is inlined into (the in-epilogue FedAvg kernels must agree
+// bit for bit with the per-client updates; the compiler's own contraction choices differ
+// between kernels).
 __device__ __forceinline__ float adam_update(float p, float g, float& mo, float& vo, const AdamCoef& c) {
 #pragma clang fp contract(off)
   if (c.wd != 0.f) g = __builtin_fmaf(c.wd, p, g);
@@ -859,20 +819,7 @@ __device__ __forceinline__ void prepare_next_batch(const GfkModel& m, int* pnb_e
   if (threadIdx.x == 0) nxt[0] = nb;
   const int cap = m.slot_cap;
   if (cap <= 0) return;
-  // split W_in update: the next batch's words get generation gen (read by every thread
-  // before thread 0 publishes it after the barrier; a generation, not the step index, so
-  // a stamp left from an earlier epoch never matches)
-  const bool split = m.stage_flags & GFK_WIN_SPLIT;
-  const int gen = split ? *m.ws_wgen + 1 : 0;
   __syncthreads();
-  if (split && threadIdx.x == 0) {
-    *m.ws_wgen = gen;
-    // the running powers the next step's post_fwd advances: gfk_win_dense_k, forked at the
-    // start of that step, derives the step's Adam coefficients from them (adam_advance)
-    double* snap = reinterpret_cast<double*>(m.ws_wgen + 2);
-    snap[0] = m.adam_pow[0];
-    snap[1] = m.adam_pow[1];
-  }
   // the rows' non-zeros into their slots: G threads per row, U loads in flight each
   constexpr int U = 8;
   const int G = max(1, (int)blockDim.x / bmax);
@@ -895,7 +842,6 @@ __device__ __forceinline__ void prepare_next_batch(const GfkModel& m, int* pnb_e
         if (j < n) {
           si[j] = ci[u];
           sv[j] = xv[u];
-          if (split) m.ws_wstamp[ci[u]] = gen;
         }
       }
     }

@@ -68,21 +68,12 @@ __host__ __device__ inline int post_weight_floats(const GfkModel& m) {
 // four of them would not fit the 160 KiB.
 __host__ __device__ inline bool batch_in_lds(const GfkModel& m) { return !(m.stage_flags & 2); }
 
-// Row stride of the LDS-staged [B][K] batch matrices (GFK_POST_PLAIN_LDS=0 builds): K rounded
-// up to 2 x odd.  The column reductions read 16 rows x 2 columns per half-wave (ds_read_b32,
-// bank = dword mod 32); a stride of 2 x odd puts those 16 rows on 16 distinct even bank
-// offsets (the two columns fill the odd ones) -- at K = 100 (4 mod 32) rows r and r + 8
-// share a bank, half of the kernels' LDS cycles are conflicts (CombinedTM K = 100: 31 %,
-// profiles/r4; the model: tools/lds_bank_model.py).  Measured slower overall (the per-row
-// staging, gfk_common.h GFK_POST_PLAIN_LDS), so the default build keeps the contiguous rows.
-__host__ __device__ inline int post_lds_ld(int K) {
-#if GFK_POST_PLAIN_LDS                  // (A/B builds: the contiguous staging of round 4)
-  return K;
-#else
-  const int k2 = (K + 1) / 2 * 2;
-  return (k2 / 2) % 2 ? k2 : k2 + 2;
-#endif
-}
+// Row stride of the LDS-staged [B][K] batch matrices: K (contiguous rows, one LDS-DMA copy).
+// A padded 2 x odd stride removed the K = 100 column reductions' bank conflicts (31 % -> 0 %)
+// but its per-row dword staging cost more than they did (CombinedTM K = 100 V = 99k: 0.7296 /
+// 0.7355 ms contiguous vs 0.7369 / 0.7432 padded, profiles/r5/ab_post_stride.txt; removed in
+// round 6).
+__host__ __device__ inline int post_lds_ld(int K) { return K; }
 
 // Rows of a row-major [rows][cols] global matrix into LDS rows of stride ld (LDS-DMA, one
 // dword per lane: 64 columns of a row per wave instruction; ld == cols: one contiguous copy)
@@ -478,7 +469,7 @@ __global__ void __launch_bounds__(FT) gfk_post_fwd_k(GfkArgT<GB> ga) {
 // backward, part 1 (own row): d theta_d from the decoder partials, softmax /
 // reparameterisation / KL backward
 // ---------------------------------------------------------------------------
-// grid: bmax workgroups (+ the batch-level one, stage_flags GFK_POST_EXTRA_ROWBWD).
+// grid: bmax workgroups (+ the batch-level one, stage_flags GFK_POST_ROWS2).
 // dynamic LDS: part[4][K]
 extern "C" size_t gfk_row_bwd_smem(const GfkModel* m) { return sizeof(float) * 4 * (size_t)pad4(m->K); }
 
@@ -583,7 +574,7 @@ __global__ void __launch_bounds__(PT) gfk_row_bwd_k(GfkArgT<GB> ga) {
   const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
   const int row = gfk_bx();
   const int nb = *nbp;
-  if ((m.stage_flags & GFK_POST_EXTRA_ROWBWD) && row == B) {
+  if ((m.stage_flags & GFK_POST_ROWS2) && row == B) {
     post_batch_level(m, nb, part, tid);    // the batch-level workgroup (grid = bmax + 1)
     return;
   }
@@ -818,7 +809,7 @@ __global__ void __launch_bounds__(FT) gfk_post_bwd_k(GfkArgT<GB> ga) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int r0 = gfk_bx() * R;          // this workgroup's first row
   int row = r0;
-  const bool extra = !(sflags & GFK_POST_EXTRA_ROWBWD) && gfk_bx() == (int)gridDim.x - 1;
+  const bool extra = !(sflags & GFK_POST_ROWS2) && gfk_bx() == (int)gridDim.x - 1;
   const PostLds L = post_lds(m);
   const int Hl = gfk_hlast(m);
   constexpr bool staged = Staged;
@@ -1222,7 +1213,9 @@ extern "C" int gfk_launch_post_fwd(const GfkModel* m, hipStream_t s) {
 
 extern "C" int gfk_launch_post_bwd(const GfkModel* m, hipStream_t s) {
   const int kq = (m->K + 63) / 64;
-  const bool moved = m->stage_flags & GFK_POST_EXTRA_ROWBWD;
+  // GFK_POST_ROWS2 (batched launches only): the batch-level workgroup runs in row_bwd
+  const bool moved = m->stage_flags & GFK_POST_ROWS2;
+  if (moved && (m->n_batch < 2 || (m->stage_flags & GFK_LB))) return -1;
   const dim3 g(m->bmax + (moved ? 1 : 0)), t(PT);
   const size_t sm = gfk_row_bwd_smem(m);
   if (kq <= 1) do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_row_bwd_k<1, true>), gfk_grid(g, m), t, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_row_bwd_k<1, false>), g, t, sm, s, GfkArgT<false>{*m}); } while (0);
@@ -1238,7 +1231,7 @@ extern "C" int gfk_launch_post_bwd(const GfkModel* m, hipStream_t s) {
   const dim3 gb(m->bmax + (moved ? 0 : 1)), tb(FT);   // + the prior / loss / step workgroup
   const size_t sb = gfk_post_bwd_smem(m);
   const bool st = m->stage_flags & 1;
-  if ((m->stage_flags & GFK_POST_ROWS2) && m->n_batch > 1 && !(m->stage_flags & GFK_LB)) {
+  if (moved) {
     // two rows per workgroup (batched launches)
     const dim3 g2((m->bmax + 1) / 2 + (moved ? 0 : 1));
     const GfkArgT<true> a{gfk_dev(m)};

@@ -322,20 +322,18 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkArgT<GB> ga
 // global rounds overlap.  Measured (profiles/r2/ab_strip_forward.txt): K=50 headline
 // round 0.0589 -> 0.0583 ms, K=50 V=28k 0.101 -> 0.092, K=200 V=112k 0.349 -> 0.342.
 // NP: k pairs held in registers (compile-time, the launcher's smallest instance >= K / 8).
-// PF = 2 (stage_flags bit 6, the default): ROLLING prefetch at 16 waves of <= 128 VGPRs:
-// right after the MFMAs that consume a k pair of this strip's beta block, the same pair of
-// the wave's NEXT strip is loaded into those registers, so each pair has a whole strip of
-// compute to arrive, with no second register block (PF = 1 holds two: 190 VGPRs, 2 waves
-// per SIMD, the MFMA pipe ~40 % busy at K = 200).
-// (PF = 2 with more than 13 k pairs: 12 waves of <= 168 VGPRs, 3 per SIMD -- the 50-register
-// beta block + accumulators + A operands spill at 128)
-// PF = 3 (stage_flags bit 8): the rolling prefetch through a RING of strip_ring(NP) <= 13
+// PF = 3 (stage_flags bit 8, the default): ROLLING prefetch at 16 waves of <= 128 VGPRs:
+// right after the MFMAs that consume a k pair of this strip's beta block, the next pair is
+// loaded into those registers, so each pair has many MFMAs of time to arrive, with no second
+// register block (PF = 1, the 8-wave variant the batched plan takes at large V, holds two:
+// 190 VGPRs, 2 waves per SIMD).  The pairs go through a RING of strip_ring(NP) <= 13
 // pairs instead of the whole strip's NP: pair t's registers receive pair t + R -- of this
 // strip while t + R < NP, else of the next one -- so a load still has R pairs of MFMAs
 // (x 4 waves per SIMD) to arrive, and K = 200 (25 pairs) fits 128 VGPRs: 16 waves per CU
 // instead of 12, and 7004 strips over 4096 waves (at most 2 each; 76 -> 85 % of the last
-// round's slots busy) instead of 3072 (at most 3).
-__host__ __device__ constexpr int strip_threads(int pf, int np) { return pf == 1 ? 512 : pf == 2 && np > 13 ? 768 : 1024; }
+// round's slots busy) instead of 3072 (at most 3).  (Round 6 removed the whole-strip rolling
+// variant PF = 2 and the non-prefetching PF = 0, both measured slower: profiles/r3, r4.)
+__host__ __device__ constexpr int strip_threads(int pf, int np) { return pf == 1 ? 512 : 1024; }
 // The ring must divide NP: the next strip's pair p is written into the slot of pair
 // p + NP - R of this one, and read back from slot p % R.  (A 13-pair ring with NP = 25
 // -- K = 200 until round 4 -- shifted every later strip's beta pairs by one slot: wrong
@@ -379,6 +377,7 @@ __host__ __device__ constexpr int strip_ring(int pf, int np) {
 // 82-83 + decoder_network.py:102-118 + avitm.py:207-220).
 template <int BM, int NP, int PF, bool GB = false, bool BF = false, bool FP = false>
 __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kernel(GfkArgT<GB> ga) {
+  static_assert(PF == 1 || PF == 3, "strip variants: 8-wave prefetching (1), ring (3)");
   static_assert(!BF || (PF == 3 && NP % 4 == 0), "bf16 strips: ring variant, whole 32-k steps");
   static_assert(!FP || (PF == 3 && NP == 8), "fused posterior: ring variant, K <= 64");
   const GfkModel& m = gfk_model(ga);
@@ -451,14 +450,7 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
   // 4 strips of a tile stay on one CU (their beta rows share cache lines), and the
   // tiles of the last, partial round are spread over every CU's wave group 0 instead
   // of all 8 waves of the first CUs, so no SIMD gets more than ceil(strips / SIMDs) + 1
-#if GFK_STRIP_OLDEST_LIGHT
-  // (A/B build: the wave groups in reverse order, so the groups with one tile fewer are the
-  // OLDEST waves -- served first by the SIMD's oldest-first issue, done early -- and the last
-  // round of strips runs with three waves per SIMD instead of a lone youngest one)
-  int s = 4 * ((NW / 4 - 1 - (wave >> 2)) * (int)gridDim.x + (int)gfk_bx()) + (wave & 3);
-#else
   int s = 4 * ((wave >> 2) * (int)gridDim.x + (int)gfk_bx()) + (wave & 3);
-#endif
   if constexpr (FP) {
     // ---- fused posterior: one round of loads (heads, the rows' noise / masks, priors,
     // workgroup 0's running statistics and counters), the first beta block behind them ----
@@ -640,19 +632,17 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
   }
 #pragma unroll 1
   for (; s < nstrips; s += stride) {
-    // PF = 2: the next strip's per-lane buffer offset (its pairs are loaded in the MFMA loop)
+    // PF = 3: the next strip's per-lane buffer offset (its pairs are loaded in the MFMA loop)
     int voffn = 0, v4n = LDB * 4;
     if (PF == 1) {
       issue(min(s + stride, nstrips - 1), bn, rmn, rvn);   // (the last one re-reads a strip)
-    } else if (PF == 2 || PF == 3) {
+    } else {
       const int sn = min(s + stride, nstrips - 1);
       const int vcn = min((sn >> 2) * VB + 16 * (sn & 3) + (lane & 15), V - 1);
       asm volatile("" : "+s"(v4n));
       voffn = gb * v4n + vcn * 4;
       rmn = m.beta_rm[vcn];
       rvn = m.beta_rv[vcn];
-    } else {
-      issue(s, b, rm0, rv0);
     }
     const int tile = s >> 2, cs = s & 3;
     const int col = 16 * cs + (lane & 15);
@@ -710,11 +700,7 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
       for (int i = 0; i < RT; ++i) acc[i] = mfma16x16x4(a[t & 1][i].x, b[2 * (t % NR)], acc[i]);
 #pragma unroll
       for (int i = 0; i < RT; ++i) acc[i] = mfma16x16x4(a[t & 1][i].y, b[2 * (t % NR) + 1], acc[i]);
-      if (PF == 2) {                  // the next strip's pair t into the registers just read
-        b[2 * t] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bres, voffn, 0, 0));
-        b[2 * t + 1] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bres, voffn, v4n, 0));
-        voffn += 8 * v4n;
-      } else if (PF == 3) {           // pair t + NR (this strip's, else the next one's)
+      if (PF == 3) {                  // pair t + NR (this strip's, else the next one's)
         const int pn = t + NR;
         const int vo = pn < NP ? voffc + pn * 8 * v4n : voffn + (pn - NP) * 8 * v4n;
         b[2 * (t % NR)] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bres, vo, 0, 0));
@@ -1258,7 +1244,7 @@ __device__ __forceinline__ void prodlda_bwd_body(const GfkModel& m) {
   float* rs = Sb + BM;
   const int NB_T = nks * 4;                    // dbeta subtiles (k tile, column strip)
   const int NDT_T = (BM / 16) * nks;           // d theta_d subtiles (row tile, k tile)
-  const bool fused = m.update_mode == 1 && !m.beta_split;
+  const bool fused = m.update_mode == 1;
   const int nb = *m.ws_nb;
   const AdamCoef ac = adam_coef(m);
   const bool beta_shared = is_shared(m, m.beta);
@@ -1371,7 +1357,7 @@ __device__ __forceinline__ void prodlda_bwd_body(const GfkModel& m) {
     // one staging round per tile: every global read is issued before the barrier
     issue_tile(tile);
     if (!PRE) issue_first_nz();
-    if (fused) {                               // (beta_split: no Adam state here)
+    if (fused) {
       if constexpr (RW) issue_state_rw(tile);
       else issue_state(tile);
     }
@@ -1669,15 +1655,8 @@ prodlda_bwd_kernel(GfkArgT<GB> ga) {
   prodlda_bwd_body<BM, MAXU, KQ, BF, false>(m);
 }
 
-// the precomputed-dlogit shape: bwd_pre = 1: <= 80 VGPRs (6 waves per SIMD), so three
-// 8-wave workgroups share a CU; bwd_pre = 2: the compiler's register budget (two per CU)
-template <int BM, int MAXU, bool BF, bool GB = false>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(6)))
-prodlda_bwd_pre_kernel(GfkArgT<GB> ga) {
-  const GfkModel& m = gfk_model(ga);
-  prodlda_bwd_body<BM, MAXU, 4, BF, true>(m);
-}
-
+// the precomputed-dlogit shape (bwd_pre = 2): the compiler's register budget, two 8-wave
+// workgroups per CU (round 6 removed the 80-VGPR three-per-CU shape, measured slower)
 template <int BM, int MAXU, bool BF, bool GB = false>
 __global__ void __launch_bounds__(512, 2) prodlda_bwd_pre2_kernel(GfkArgT<GB> ga) {
   const GfkModel& m = gfk_model(ga);
@@ -1874,10 +1853,8 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
       for (int j = 0; j < DU; ++j) {           // dense [BM][64] -> dt [b][c] and dtT [c][b]
         const int i = tid + NTH * j, r = i >> 4, c4 = (i & 15) * 4;
         *reinterpret_cast<f32x4*>(dt + __mul24(r, LDP) + c4) = dr[j];
-#if GFK_DIAG_BWD != 2                          // (diagnostic builds: no transposed stores)
 #pragma unroll
         for (int e = 0; e < 4; ++e) dtT[__mul24(c4 + e, LDP) + (r ^ dtt_swz(c4 + e))] = dr[j][e];
-#endif
       }
     }
     // (KEEP: the beta quads stay in registers for the Adam epilogue -- read back from bt
@@ -1897,9 +1874,6 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
 
     const int r = lane & 15, g4 = 4 * (lane >> 4);
     // d theta_d[b, k] += sum_c dt[b][c] bt[k][c]
-#if GFK_DIAG_BWD == 1                          // (diagnostic builds: no MFMA phase)
-    if (nb < 0)
-#endif
 #pragma unroll
     for (int j = 0; j < NDT; ++j) {
       const int t = wave + NW * j;
@@ -1913,10 +1887,6 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
     for (int u = 0; u < MU; ++u) {
       const int t = wave + NW * u;
       if (t >= NB_T) break;
-#if GFK_DIAG_BWD == 1
-      for (int e = 0; e < 4; ++e) gr[u][e] = 0.f;
-      continue;
-#endif
       const int ks = t >> 2, cst = t & 3;
       const int cr = cst * 16 + r;
       const f32x4 a = mm64(thT + __mul24(ks * 16 + r, LDP), dtT + __mul24(cr, LDP), g4, dtt_swz(cr));
@@ -1949,11 +1919,7 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
       if constexpr (FUSED) {
         f32x4 pv;
         if constexpr (KEEP) pv = bkeep[u];
-#if GFK_DIAG_BWD == 3                          // (diagnostic builds: no beta read-back)
-        else pv = f32x4{0.f, 0.f, 0.f, 0.f};
-#else
         else pv = *reinterpret_cast<const f32x4*>(bt + __mul24(kl, LDP) + c4);
-#endif
         f32x4 mo = rm[u], vo = rv[u], np;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -2000,7 +1966,6 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
 // per-wave row partials only
 constexpr int FWD_STRIP = 4;
 constexpr int FWD_STRIP_PF = 8;   // bit 3: its prefetching 8-wave variant
-constexpr int FWD_STRIP_ROLL = 64;  // bit 6: its rolling-prefetch 16-wave variant (PF = 2)
 constexpr int FWD_STRIP_RING = 256; // bit 8: the rolling prefetch through a 13-pair ring (PF = 3)
 __host__ __device__ inline bool strip_postfold(const GfkModel& m) { return gfk_postfold(m); }
 __host__ __device__ inline int strip_pairs(int K) { return (K + 7) / 8; }
@@ -2373,7 +2338,7 @@ extern "C" size_t gfk_bwd_fold_smem() { return FB_SMEM; }
 // the shapes gfk_bwd_fold_k is written for (the host plan checks them too)
 extern "C" int gfk_bwd_fold_launch(const GfkModel* m0, const GfkFold* f, hipStream_t s) {
   if (m0->kind != GFK_PRODLDA || m0->K > 64 || m0->bmax != 64 || m0->vb != VB || m0->mm_bf16 ||
-      m0->update_mode != 1 || m0->beta_split || m0->n_dpart != m0->n_tiles || m0->bwd_pre ||
+      m0->update_mode != 1 || m0->n_dpart != m0->n_tiles || m0->bwd_pre ||
       (m0->stage_flags & GFK_LB) || f->M < 1 || !f->models || (int64_t)m0->K * m0->ldb * 4 >= 0x7FFF0000LL ||
       m0->kt < 2 || (m0->kt & 1))
     return -1;
@@ -2389,7 +2354,6 @@ extern "C" int gfk_bwd_fold_launch(const GfkModel* m0, const GfkFold* f, hipStre
 // and the 8-wave dense pass cost more than the quartered MFMA work saved, 0.0652 vs 0.0615
 // ms per round.)
 __host__ __device__ inline int bwd_kq(const GfkModel& m) {
-  if ((m.stage_flags & GFK_BWD_KQ1) && m.K <= 64) return 1;      // persistent one-range tiles
   return (m.n_dpart < m.n_tiles && round_up(m.K, 16) / 16 >= 4) ? 4 : 1;
 }
 
@@ -2454,14 +2418,10 @@ extern "C" int gfk_launch_prodlda_fwd(const GfkModel* m, hipStream_t s) {
     do {                                                                                       \
       if (NP == 8 && fp)                                                                       \
         do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, 8, 3, true, false, true>), gfk_grid(g, m), dim3(1024), sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, 8, 3, false, false, true>), g, dim3(1024), sm, s, GfkArgT<false>{*m}); } while (0); \
-      else if (m->stage_flags & FWD_STRIP_RING)                                                \
-        do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 3, true>), gfk_grid(g, m), dim3(strip_threads(3, NP)), sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 3, false>), g, dim3(strip_threads(3, NP)), sm, s, GfkArgT<false>{*m}); } while (0); \
-      else if (m->stage_flags & FWD_STRIP_ROLL)                                                \
-        do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 2, true>), gfk_grid(g, m), dim3(strip_threads(2, NP)), sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 2, false>), g, dim3(strip_threads(2, NP)), sm, s, GfkArgT<false>{*m}); } while (0); \
       else if (m->stage_flags & FWD_STRIP_PF)                                                  \
         do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 1, true>), gfk_grid(g, m), dim3(512), sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 1, false>), g, dim3(512), sm, s, GfkArgT<false>{*m}); } while (0); \
       else                                                                                     \
-        do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 0, true>), gfk_grid(g, m), dim3(1024), sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 0, false>), g, dim3(1024), sm, s, GfkArgT<false>{*m}); } while (0); \
+        do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 3, true>), gfk_grid(g, m), dim3(strip_threads(3, NP)), sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 3, false>), g, dim3(strip_threads(3, NP)), sm, s, GfkArgT<false>{*m}); } while (0); \
     } while (0)
 #define GFK_FWS_B(BM)                                                      \
     if (np == 8) GFK_FWS(BM, 8);                                           \
@@ -2500,7 +2460,7 @@ static void launch_bwd_p(const GfkModel* m, dim3 g, size_t sm, hipStream_t s) {
   // kernel is bound by its beta / Adam-state HBM traffic, not by the matrix cores)
   if constexpr (PRE) {
     if (bwd_pipe(*m)) {
-      if (m->update_mode == 1 && !m->beta_split) {
+      if (m->update_mode == 1) {
         if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_bwd_pipe_kernel<64, MAXU, true, true>), gfk_grid(g, m), blk, sm, s, GfkArgT<true>{gfk_dev(m)});
         else hipLaunchKernelGGL((prodlda_bwd_pipe_kernel<64, MAXU, true, false>), g, blk, sm, s, GfkArgT<false>{*m});
       } else {
@@ -2510,19 +2470,11 @@ static void launch_bwd_p(const GfkModel* m, dim3 g, size_t sm, hipStream_t s) {
       return;
     }
   }
-  if (PRE && m->bwd_pre >= 2) {
+  if (PRE) {
     switch (m->bmax) {
       case 16: do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_bwd_pre2_kernel<16, MAXU, BF, true>), gfk_grid(g, m), blk, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_bwd_pre2_kernel<16, MAXU, BF, false>), g, blk, sm, s, GfkArgT<false>{*m}); } while (0); break;
       case 32: do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_bwd_pre2_kernel<32, MAXU, BF, true>), gfk_grid(g, m), blk, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_bwd_pre2_kernel<32, MAXU, BF, false>), g, blk, sm, s, GfkArgT<false>{*m}); } while (0); break;
       default: do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_bwd_pre2_kernel<64, MAXU, BF, true>), gfk_grid(g, m), blk, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_bwd_pre2_kernel<64, MAXU, BF, false>), g, blk, sm, s, GfkArgT<false>{*m}); } while (0); break;
-    }
-    return;
-  }
-  if (PRE) {
-    switch (m->bmax) {
-      case 16: do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_bwd_pre_kernel<16, MAXU, BF, true>), gfk_grid(g, m), blk, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_bwd_pre_kernel<16, MAXU, BF, false>), g, blk, sm, s, GfkArgT<false>{*m}); } while (0); break;
-      case 32: do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_bwd_pre_kernel<32, MAXU, BF, true>), gfk_grid(g, m), blk, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_bwd_pre_kernel<32, MAXU, BF, false>), g, blk, sm, s, GfkArgT<false>{*m}); } while (0); break;
-      default: do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_bwd_pre_kernel<64, MAXU, BF, true>), gfk_grid(g, m), blk, sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_bwd_pre_kernel<64, MAXU, BF, false>), g, blk, sm, s, GfkArgT<false>{*m}); } while (0); break;
     }
     return;
   }
@@ -2601,7 +2553,7 @@ extern "C" int gfk_prodlda_set_smem(size_t bytes) {
     (const void*)prodlda_fwd_strip_kernel<BM, 32, 3, false, true>, (const void*)prodlda_fwd_strip_kernel<BM, 32, 3, true, true>
 #define GFK_FWS_PTRSF(BM) (const void*)prodlda_fwd_strip_kernel<BM, 8, 3, false, false, true>, (const void*)prodlda_fwd_strip_kernel<BM, 8, 3, true, false, true>, \
     (const void*)prodlda_fwd_strip_kernel<BM, 8, 3, false, true, true>, (const void*)prodlda_fwd_strip_kernel<BM, 8, 3, true, true, true>
-#define GFK_FWS_PTRS(BM) GFK_FWS_PTRS1(BM, 0), GFK_FWS_PTRS1(BM, 1), GFK_FWS_PTRS1(BM, 2), GFK_FWS_PTRS1(BM, 3), GFK_FWS_PTRSB(BM), GFK_FWS_PTRSF(BM)
+#define GFK_FWS_PTRS(BM) GFK_FWS_PTRS1(BM, 1), GFK_FWS_PTRS1(BM, 3), GFK_FWS_PTRSB(BM), GFK_FWS_PTRSF(BM)
                       GFK_FWS_PTRS(16), GFK_FWS_PTRS(32), GFK_FWS_PTRS(64),
 #undef GFK_FWS_PTRS
 #undef GFK_FWS_PTRSF
@@ -2611,9 +2563,7 @@ extern "C" int gfk_prodlda_set_smem(size_t bytes) {
     (const void*)prodlda_bwd_kernel<32, U, T, F>, (const void*)prodlda_bwd_kernel<32, U, T, F, true>, (const void*)prodlda_bwd_kernel<64, U, T, F>, (const void*)prodlda_bwd_kernel<64, U, T, F, true>, \
     (const void*)prodlda_bwd_kernel<128, U, T, F>, (const void*)prodlda_bwd_kernel<128, U, T, F, true>
 #define GFK_BWD_PTRS1(U, T) GFK_BWD_PTRS2(U, T, false), GFK_BWD_PTRS2(U, T, true)
-#define GFK_BWD_PTRS3(U, F) (const void*)prodlda_bwd_pre_kernel<16, U, F>, (const void*)prodlda_bwd_pre_kernel<16, U, F, true>, \
-    (const void*)prodlda_bwd_pre_kernel<32, U, F>, (const void*)prodlda_bwd_pre_kernel<32, U, F, true>, (const void*)prodlda_bwd_pre_kernel<64, U, F>, (const void*)prodlda_bwd_pre_kernel<64, U, F, true>, \
-    (const void*)prodlda_bwd_pre2_kernel<16, U, F>, (const void*)prodlda_bwd_pre2_kernel<16, U, F, true>, (const void*)prodlda_bwd_pre2_kernel<32, U, F>, (const void*)prodlda_bwd_pre2_kernel<32, U, F, true>, \
+#define GFK_BWD_PTRS3(U, F) (const void*)prodlda_bwd_pre2_kernel<16, U, F>, (const void*)prodlda_bwd_pre2_kernel<16, U, F, true>, (const void*)prodlda_bwd_pre2_kernel<32, U, F>, (const void*)prodlda_bwd_pre2_kernel<32, U, F, true>, \
     (const void*)prodlda_bwd_pre2_kernel<64, U, F>, (const void*)prodlda_bwd_pre2_kernel<64, U, F, true>
 #define GFK_BWD_PTRS(U) GFK_BWD_PTRS1(U, 1), GFK_BWD_PTRS1(U, 4), GFK_BWD_PTRS3(U, false), \
     GFK_BWD_PTRS3(U, true), (const void*)prodlda_bwd_pipe_kernel<64, U, false>, (const void*)prodlda_bwd_pipe_kernel<64, U, false, true>, \

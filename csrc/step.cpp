@@ -29,7 +29,6 @@ int gfk_launch_adam(const GfkAdam*, int, hipStream_t);
 int gfk_launch_scale(float*, int64_t, float, hipStream_t);
 int gfk_launch_ctx_fwd(const GfkModel*, hipStream_t);
 int gfk_launch_ctx_bwd(const GfkModel*, hipStream_t);
-int gfk_launch_win_dense(const GfkModel*, hipStream_t);
 size_t gfk_ctx_smem(const GfkModel*);
 int gfk_ctx_set_smem(size_t);
 size_t gfk_prodlda_fwd_smem(const GfkModel*);
@@ -62,7 +61,7 @@ enum GfkPhase {
   GFK_PH_BATCH_PREP = 12,
   GFK_PH_CTXF_FWD = 13,
   GFK_PH_CTXF_BWD = 14,
-  GFK_PH_WIN_DENSE = 15,
+  // (15: the split W_in update's dense half, removed in round 6)
 };
 
 
@@ -124,7 +123,6 @@ int gfk_run(const GfkModel* m, const GfkAdam* a, int adam_grid, const GfkUpdate*
       case GFK_PH_BATCH_PREP: e = gfk_launch_batch_prep(m, s); break;
       case GFK_PH_CTXF_FWD: e = gfk_launch_ctx_fwd(m, s); break;
       case GFK_PH_CTXF_BWD: e = gfk_launch_ctx_bwd(m, s); break;
-      case GFK_PH_WIN_DENSE: e = gfk_launch_win_dense(m, s); break;
       default: e = -2;
     }
     if (e) return e * 100 + phases[i];

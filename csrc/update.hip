@@ -589,407 +589,6 @@ __device__ __forceinline__ void win_tile_ctx(const GfkModel& m, float* smem, int
   }
 }
 
-// CombinedTM's contextual input-layer half as a persistent kernel (stage_flags bit 14,
-// launched after the sparse bag-of-words tiles): ctx_bgrid x 2 workgroups own contiguous
-// ranges of 16-word units of Wc (rows V..2V-1 of the transposed input layer), walked in
-// blocks of up to 64 words, so every slot moves the same p / m / v bytes to within a unit
-// (one short-lived workgroup per 64-word tile spent most of its time starting up and
-// waiting), with block i + 1's adapted columns and Adam state in flight in a second
-// register set while block i's gradient G[v, h] = sum_{b < nb} A[b, v] dz0[b, h] runs on the
-// matrix cores and its update is stored.  p / m / v go through buffer loads / stores at
-// 4-byte granularity (a block's [words, H0] run need not be 16-byte aligned).
-constexpr int WIN_CTXPP = 16384;
-constexpr int WCT = 512;
-__host__ __device__ inline int win_ctxpp_lds_floats(const GfkModel& m) {
-  return ((m.bmax * m.H[0] + 3) & ~3) + 64 * 80 + 64 * 64;
-}
-template <bool GB = false>
-__global__ void __launch_bounds__(WCT, 4) gfk_win_ctx_pp_k(GfkArgT<GB> ga) {
-  const GfkModel& m = gfk_model(ga);
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = uniform(tid >> 6);
-  const int V = m.V, H0 = m.H[0], B = m.bmax, nb = *m.ws_nb;
-  const int G = (int)gridDim.x, w = (int)gfk_bx();
-  const int U = (V + 15) / 16;
-  const int cs = (int)((int64_t)w * U / G) * 16;
-  const int ce = min(V, (int)((int64_t)(w + 1) * U / G) * 16);
-  float* dz = smem;                                   // [B][H0]
-  float* at = smem + ((B * H0 + 3) & ~3);             // [64 b][80] the block's adapted columns
-  float* gt = at + 64 * 80;                           // [64 words][H0] gradient, flat
-  const bool fused = m.update_mode == 1;
-  const AdamCoef ac = adam_coef(m);
-  const bool sh = is_shared(m, m.w_in);
-  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
-  const __amdgpu_buffer_rsrc_t rs_p = __builtin_amdgcn_make_buffer_rsrc((void*)m.flat_base, 0, 0x7FFFFFFF, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rs_m =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(m.flat_base + (fused ? m.off_m : m.off_g)), 0, 0x7FFFFFFF, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rs_v = __builtin_amdgcn_make_buffer_rsrc((void*)(m.flat_base + m.off_v), 0, 0x7FFFFFFF, 0x00020000);
-  const uint32_t wc0 = (uint32_t)((m.w_in + (size_t)V * H0) - m.flat_base) * 4u;   // Wc's first byte
-  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-  glds_copy(dz, m.ws_dz[0], B * H0, tid, WCT);
-  // per-thread quads of a block's flat [words, H0] run: e = 4 (tid + WCT u), u < 2
-  // A columns: (b, q) = ((tid + WCT u) >> 4, (tid + WCT u) & 15): 4 consecutive words of row b
-  auto ld_blk = [&](int v0, int nw, f32x4 (&P)[6], f32x4 (&A)[2]) {
-    const int nel = nw * H0;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int e = 4 * (tid + WCT * u);
-      // the thread's own quad, at the offset do_blk stores it to: whole quads as 128-bit
-      // loads, the block's partial last quad (nel % 4 != 0: odd word counts at H0 = 50)
-      // element by element, nothing past the block's run
-      const uint32_t off = wc0 + ((uint32_t)v0 * (uint32_t)H0 + (uint32_t)e) * 4u;
-      if (e + 3 < nel) {
-        P[3 * u] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_p, off, 0, 0));
-        P[3 * u + 1] = fused ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_m, off, 0, 0)) : z4;
-        P[3 * u + 2] = fused ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_v, off, 0, 0)) : z4;
-      } else {
-        P[3 * u] = P[3 * u + 1] = P[3 * u + 2] = z4;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          if (e + i < nel) {
-            P[3 * u][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_p, off + 4 * i, 0, 0));
-            if (fused) {
-              P[3 * u + 1][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_m, off + 4 * i, 0, 0));
-              P[3 * u + 2][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_v, off + 4 * i, 0, 0));
-            }
-          }
-        }
-      }
-      const int i = tid + WCT * u, b = i >> 4, q = i & 15, v = v0 + 4 * q;
-      A[u] = (b < B && 4 * q < nw)
-                 ? *reinterpret_cast<const f32x4*>(m.ws_actx + ((size_t)(v >> 6) * B + b) * 64 + (v & 63))
-                 : z4;
-    }
-  };
-  const int NT = (H0 + 15) / 16;
-  auto do_blk = [&](int v0, int nw, const f32x4 (&P)[6], const f32x4 (&A)[2]) {
-    const int nel = nw * H0;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int i = tid + WCT * u, b = i >> 4, q = i & 15;
-      *reinterpret_cast<f32x4*>(at + b * 80 + 4 * q) = b < nb ? A[u] : z4;
-    }
-    vm_barrier();                                     // (first block: dz0's LDS-DMA too)
-    // G subtiles (word tile, h tile) = t = wave + 8 u: A-role at[b][v] (b = k + lane >> 4),
-    // B-role dz[b][h] (columns >= H0 read the next row: discarded)
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int t = wave + (WCT / 64) * u;
-      if (t >= 4 * NT) break;
-      const int i0 = (t / NT) * 16, j0 = (t % NT) * 16;
-      f32x4 acc = z4;
-      const float* ap = at + (lane >> 4) * 80 + i0 + (lane & 15);
-      const float* bp = dz + (lane >> 4) * H0 + j0 + (lane & 15);
-      for (int k = 0; k < B; k += 4) acc = mfma16x16x4(ap[k * 80], bp[k * H0], acc);
-      const int j = j0 + (lane & 15);
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (j < H0) gt[(i0 + (lane >> 4) * 4 + r) * H0 + j] = acc[r];
-    }
-    lds_barrier();
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int e = 4 * (tid + WCT * u);
-      if (e >= nel) break;
-      const uint32_t off = wc0 + ((uint32_t)v0 * (uint32_t)H0 + (uint32_t)e) * 4u;
-      f32x4 g4 = *reinterpret_cast<const f32x4*>(gt + e);
-      f32x4 np, mo, vo;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float a = P[3 * u + 1][i], b2 = P[3 * u + 2][i];
-        const float x = fused ? adam_update(P[3 * u][i], g4[i], a, b2, ac) : g4[i];
-        np[i] = sh && m.fed_scale_on && fused ? x * m.fed_scale : x;
-        mo[i] = a;
-        vo[i] = b2;
-      }
-      if (e + 3 < nel) {
-        if (fused) {
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, mo), rs_m, off, 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, vo), rs_v, off, 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, np), rs_p, off, 0, 0);
-        } else {
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, np), rs_m, off, 0, 0);   // (rs_m = grad)
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          if (e + i >= nel) break;
-          if (fused) {
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mo[i]), rs_m, off + 4 * i, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vo[i]), rs_v, off + 4 * i, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(np[i]), rs_p, off + 4 * i, 0, 0);
-          } else {
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(np[i]), rs_m, off + 4 * i, 0, 0);
-          }
-        }
-      }
-    }
-    lds_barrier();                                    // before the next block's A columns / G
-  };
-  f32x4 PA[6], AA[2], PB[6], AB[2];
-  if (cs < ce) ld_blk(cs, min(64, ce - cs), PA, AA);
-  for (int v0 = cs; v0 < ce; v0 += 128) {
-    const int n0 = min(64, ce - v0);
-    if (v0 + 64 < ce) ld_blk(v0 + 64, min(64, ce - v0 - 64), PB, AB);
-    do_blk(v0, n0, PA, AA);
-    if (v0 + 64 >= ce) break;
-    if (v0 + 128 < ce) ld_blk(v0 + 128, min(64, ce - v0 - 128), PA, AA);
-    do_blk(v0 + 64, min(64, ce - v0 - 64), PB, AB);
-  }
-}
-
-// Split W_in update (stage_flags GFK_WIN_SPLIT, fused mode): the sparse tile updates only
-// the words of the batch -- the words stamped with this batch's generation by
-// prepare_next_batch, which are exactly the words with entries in the tiles' lists --
-// and gfk_win_dense_k gives every other word its zero-gradient Adam step, earlier in the
-// step on a side stream.  The tile's words come from its entry list (a word mask in LDS,
-// compacted by one ballot); thread t owns elements t, t + UT, .. of the [n_words, H0]
-// block, loads its p / m / v rows (contiguous 4 H0-byte runs), and sums its gradient
-// over the list in the same order as win_tile_sparse: the update is bit-identical to the
-// unsplit kernel's, at ~1/9 of its bytes at V = 112k (~7 words per 64-word tile).
-template <int UT>
-__device__ __forceinline__ void win_tile_sparse_rows(const GfkModel& m, float* smem, int tile) {
-  constexpr int CAP = 512;
-  constexpr int TPR = UT / 64;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int B = m.bmax, H0 = m.H[0], c0 = tile * 64;
-  const int nb = *m.ws_nb;
-  float* dz = smem;                            // [B][H0]
-  int* ecol = reinterpret_cast<int*>(dz + B * H0);   // [CAP] (row << 8) | local column
-  float* ex = reinterpret_cast<float*>(ecol + CAP);  // [CAP]
-  int* offs = reinterpret_cast<int*>(ex + CAP);      // [129] rows' first slots, total
-  int* wmark = offs + 129;                           // [64] word present / word list
-  __shared__ int s_nw;
-  const int32_t* tst = m.ws_tstart;
-  const int ntp = m.n_tiles + 1;
-  const int sub = tid % TPR;
-  int xe0[2], xe1[2], cnt[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int r = min(tid / TPR + 64 * i, B - 1);
-    xe0[i] = tst[(size_t)r * ntp + tile];
-    xe1[i] = tst[(size_t)r * ntp + tile + 1];
-  }
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int r = min(lane + 64 * i, B - 1);
-    cnt[i] = wave == 0 ? tst[(size_t)r * ntp + tile + 1] - tst[(size_t)r * ntp + tile] : 0;
-  }
-  glds_copy(dz, m.ws_dz[0], B * H0, tid, UT);
-  if (tid < 64) wmark[tid] = 0;
-  int fi[2];
-  float fv[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int e = min(xe0[i] + sub, max(xe1[i] - 1, 0));
-    fi[i] = m.indices[e];
-    fv[i] = m.values[e];
-  }
-  if (wave == 0) {             // row counts -> slots, rows in order
-    int base = 0;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = lane + 64 * i < nb ? cnt[i] : 0;
-      int x = c;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const int y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
-      }
-      offs[lane + 64 * i] = base + x - c;
-      base += __shfl(x, 63, 64);
-    }
-    if (lane == 0) offs[128] = base;
-  }
-  vm_barrier();
-  // the words with entries (every entry of the thread's rows, not only this pass's)
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int r = tid / TPR + 64 * i;
-    if (r >= nb) continue;
-    int e = xe0[i] + sub;
-    if (e < xe1[i]) wmark[fi[i] - c0] = 1;
-    for (e += TPR; e < xe1[i]; e += TPR) wmark[m.indices[e] - c0] = 1;
-  }
-  __syncthreads();
-  if (wave == 0) {             // compact: wmark[0 .. nw) = the tile's words, ascending
-    const uint64_t mask = __ballot(wmark[lane] != 0);
-    const int pos = __popcll(mask & ((1ull << lane) - 1));
-    if ((mask >> lane) & 1) offs[129 + 64 + pos] = lane;   // (the word list after wmark)
-    if (lane == 0) s_nw = __popcll(mask);
-  }
-  __syncthreads();
-  const int nw = s_nw, nel = nw * H0;
-  const int* wl = offs + 129 + 64;
-  const int total = offs[128];
-  const AdamCoef ac = adam_coef(m);
-  const bool sh = is_shared(m, m.w_in);
-  // element groups of EG per thread (one group for a typical tile: ~7 words x H0 <= 512);
-  // the entry list is built once when it fits CAP, else once per pass of each group
-  constexpr int EG = 2;
-  for (int base = 0; base < nel; base += EG * UT) {
-    int ew[EG], eh[EG];
-    float pp[EG], pm[EG], pv[EG], g[EG];
-#pragma unroll
-    for (int u = 0; u < EG; ++u) {
-      const int el = min(base + tid + UT * u, nel - 1);
-      const int wi = el / H0;
-      eh[u] = el - wi * H0;
-      ew[u] = wl[wi];
-      const float* p = m.w_in + (size_t)(c0 + ew[u]) * H0 + eh[u];
-      pp[u] = *p;
-      pm[u] = p[m.off_m];
-      pv[u] = p[m.off_v];
-      g[u] = 0.f;
-    }
-    for (int p0 = 0; p0 < total; p0 += CAP) {
-      if (!(total <= CAP && base > 0)) {         // (uniform) build this pass's list
-        if (p0 || base) __syncthreads();         // the previous list's reads are done
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const int r = tid / TPR + 64 * i;
-          if (r >= nb) continue;
-          const int o = offs[r] - xe0[i];
-          int e = xe0[i] + sub;
-          if (e < xe1[i]) {
-            const int s = o + e - p0;
-            if (s >= 0 && s < CAP) {
-              ecol[s] = (r << 8) | (fi[i] - c0);
-              ex[s] = fv[i];
-            }
-          }
-          for (e += TPR; e < xe1[i]; e += TPR) {
-            const int s = o + e - p0;
-            if (s >= 0 && s < CAP) {
-              ecol[s] = (r << 8) | (m.indices[e] - c0);
-              ex[s] = m.values[e];
-            }
-          }
-        }
-        __syncthreads();
-      }
-      const int n = min(CAP, total - p0);
-      for (int j = 0; j < n; ++j) {
-        const int cb = ecol[j];
-        const float x = ex[j];
-        const int col = cb & 255;
-        const float* dr = dz + (cb >> 8) * H0;
-#pragma unroll
-        for (int u = 0; u < EG; ++u)
-          if (col == ew[u]) g[u] = __builtin_fmaf(x, dr[eh[u]], g[u]);   // (as win_tile_sparse)
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < EG; ++u) {
-      if (base + tid + UT * u >= nel) break;
-      float* p = m.w_in + (size_t)(c0 + ew[u]) * H0 + eh[u];
-      float a = pm[u], b = pv[u];
-      float x = adam_update(pp[u], g[u], a, b, ac);
-      if (sh && m.fed_scale_on) x *= m.fed_scale;
-      p[m.off_m] = a;
-      p[m.off_v] = b;
-      *p = x;
-    }
-  }
-}
-
-// The zero-gradient Adam step of every input-layer word NOT in the batch (split W_in
-// update): flat float4 quads of the [V, H0] block, QU per thread in one round (the
-// stamps of the quads' words first, then p / m / v unconditionally -- the batch's words
-// are only read here; their writer, the sparse tile, runs after this kernel); an element
-// is stored iff its word's stamp differs from the batch's generation.  adam_update with
-// g = 0 is exactly what the unsplit tile computes for a word without entries.
-// It runs at the START of the step, on a side stream next to enc_in / post_fwd (latency-
-// bound, ~64 CUs busy), so its coefficients cannot come from adam_coef (post_fwd writes
-// them): they are derived from the powers snapshotted by prepare_next_batch.
-// grid: ceil(V H0 / 4 / (256 QU)) workgroups of 256 threads (short-lived, so the kernels
-// this overlaps keep getting CUs).
-constexpr int WD_QU = 4;
-template <bool GB = false>
-__global__ void __launch_bounds__(256) gfk_win_dense_k(GfkArgT<GB> ga) {
-  const GfkModel& m = gfk_model(ga);
-  const int H0 = m.H[0];
-  const int64_t n = (int64_t)m.V * H0;
-  const int64_t q0 = ((int64_t)gfk_bx() * 256 * WD_QU) + threadIdx.x;
-  const int32_t* st = m.ws_wstamp;
-  const int tag = *m.ws_wgen;
-  int sa[WD_QU], sb[WD_QU];
-#pragma unroll
-  for (int u = 0; u < WD_QU; ++u) {
-    const int64_t e = min(4 * (q0 + 256 * u), n - 1);
-    sa[u] = st[e / H0];
-    sb[u] = st[min(e + 3, n - 1) / H0];
-  }
-  f32x4 pp[WD_QU], pm[WD_QU], pv[WD_QU];
-#pragma unroll
-  for (int u = 0; u < WD_QU; ++u) {
-    const int64_t e = 4 * (q0 + 256 * u);
-    if (e + 3 < n) {
-      pp[u] = *reinterpret_cast<const f32x4*>(m.w_in + e);
-      pm[u] = *reinterpret_cast<const f32x4*>(m.w_in + m.off_m + e);
-      pv[u] = *reinterpret_cast<const f32x4*>(m.w_in + m.off_v + e);
-    } else {                                   // the partial last quad / past the end
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const bool in = e + i < n;
-        pp[u][i] = in ? m.w_in[e + i] : 0.f;
-        pm[u][i] = in ? m.w_in[m.off_m + e + i] : 0.f;
-        pv[u][i] = in ? m.w_in[m.off_v + e + i] : 0.f;
-      }
-    }
-  }
-  // this step's coefficients, from the powers prepare_next_batch saw (post_fwd advances the
-  // same powers concurrently: adam_advance reproduces its bits)
-  AdamCoef ac = adam_coef(m);
-  {
-    const double* snap = reinterpret_cast<const double*>(m.ws_wgen + 2);
-    double p1, p2;
-    adam_advance(m, snap[0], snap[1], p1, p2, ac.step, ac.ibc2);
-  }
-  const bool sh = is_shared(m, m.w_in);
-  // a zero the compiler cannot fold: the same Adam instruction sequence as the sparse
-  // tile's (whose g is a runtime sum), so both halves round identically
-  float gz = 0.f;
-  asm volatile("" : "+v"(gz));
-#pragma unroll
-  for (int u = 0; u < WD_QU; ++u) {
-    const int64_t e = 4 * (q0 + 256 * u);
-    if (e >= n) break;
-    const int64_t wa = e / H0;
-    bool ok[4];
-    bool all = e + 3 < n;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int64_t w = (e + i) / H0;
-      ok[i] = e + i < n && (w == wa ? sa[u] : sb[u]) != tag;
-      all = all && ok[i];
-    }
-    f32x4 np, mo, vo;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float a = pm[u][i], b = pv[u][i];
-      float x = adam_update(pp[u][i], gz, a, b, ac);
-      np[i] = sh && m.fed_scale_on ? x * m.fed_scale : x;
-      mo[i] = a;
-      vo[i] = b;
-    }
-    float* p = m.w_in + e;
-    if (all) {
-      *reinterpret_cast<f32x4*>(p + m.off_m) = mo;
-      *reinterpret_cast<f32x4*>(p + m.off_v) = vo;
-      *reinterpret_cast<f32x4*>(p) = np;
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if (!ok[i]) continue;
-        p[m.off_m + i] = mo[i];
-        p[m.off_v + i] = vo[i];
-        p[i] = np[i];
-      }
-    }
-  }
-}
-
 // grid: n_tiles + n_w + n_v + 1 (+ n_tiles for fused CombinedTM, + ceil(C / 64) for fused
 // ZeroShotTM) workgroups of 1024 threads.  The trailing tiles are the contextual input
 // layer: CombinedTM's Wc = rows V..2V-1 of the transposed W_in with the dense adapted
@@ -1357,38 +956,11 @@ __global__ void __launch_bounds__(UT, VL ? 4096 / UT : 1) gfk_win_sparse_k(GfkAr
   win_tile_sparse<UT, VL, RS>(m, smem, t);
 }
 
-// the split update's sparse half: the same job workgroups, then the batch words' tiles (its
-// own kernel, so neither tile body inflates the other's register budget)
-template <int UT, bool GB = false>
-__global__ void __launch_bounds__(UT) gfk_win_rows_k(GfkArgT<GB> ga, GfkUArgT<GB> gua) {
-  const GfkModel& m = gfk_model(ga);
-  const GfkUpdate& U = gfk_upd(gua);
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int r = (int)gfk_bx();
-  if (r < U.n_w) { weight_job<UT>(m, U.w[r], smem); return; }
-  if (r < U.n_w + U.n_v) { vector_job<UT>(m, U.v[r - U.n_w]); return; }
-  if (r == U.n_w + U.n_v) { prepare_next_batch(m, reinterpret_cast<int*>(smem)); return; }
-  win_tile_sparse_rows<UT>(m, smem, r - (U.n_w + U.n_v + 1));
-}
-
-// the zero-gradient half of the split W_in update (fused mode, sparse tiles, float4-aligned
-// W_in / m / v: checked by the engine before it sets GFK_WIN_SPLIT)
-extern "C" int gfk_launch_win_dense(const GfkModel* m, hipStream_t s) {
-  if (!(m->stage_flags & GFK_WIN_SPLIT) || !(m->stage_flags & WIN_SPARSE) || m->update_mode != 1 ||
-      m->H[0] < 4 || ((uintptr_t)m->w_in & 15) || (m->off_m & 3) || (m->off_v & 3))
-    return -1;
-  const int64_t quads = ((int64_t)m->V * m->H[0] + 3) / 4;
-  const dim3 g((unsigned)((quads + 256 * WD_QU - 1) / (256 * WD_QU)));
-  do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_win_dense_k<true>), gfk_grid(g, m), dim3(256), 0, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_win_dense_k<false>), g, dim3(256), 0, s, GfkArgT<false>{*m}); } while (0);
-  return (int)hipGetLastError();
-}
-
 // the sparse tile's LDS second-moment variant: fused mode, and the block fits the LDS the
-// kernel is given anyway (gfk_win_update_smem: no occupancy lost to LDS).  stage_flags
-// bit 10 (GFEDNTM_WIN_VL=0) keeps the register variant.
-constexpr int WIN_VREG = 1024;
+// kernel is given anyway (gfk_win_update_smem: no occupancy lost to LDS); gradient mode and
+// the large-batch plan keep the second moment in registers
 static bool win_sparse_vl(const GfkModel* m) {
-  if ((m->stage_flags & WIN_VREG) || m->update_mode != 1) return false;
+  if (m->update_mode != 1) return false;
   if (m->bmax > 128) return false;      // (the large-batch instance keeps it in registers)
   const size_t need = sizeof(float) * ((((size_t)m->bmax * m->H[0] + 2 * 512 + 129 + 3) & ~(size_t)3) +
                                        (size_t)64 * m->H[0]);
@@ -1418,42 +990,17 @@ static bool win_sparse_vl(const GfkModel* m) {
                          gfk_win_update_smem(m), s, GfkArgT<false>{*m}, GfkUArgT<false>{*u});    \
   } while (0)
 
-static int launch_win_sparse_bow(const GfkModel* m, const GfkUpdate* u, hipStream_t s) {
-  const dim3 gs(u->n_w + u->n_v + 1 + m->n_tiles);
-  if (m->bmax > 128)
-    GFK_WIN_SPARSE_LB_LAUNCH();
-  else if (win_sparse_vl(m))
-    GFK_WIN_SPARSE_LAUNCH(true, false);
-  else
-    GFK_WIN_SPARSE_LAUNCH(false, false);
-  return (int)hipGetLastError();
-}
-
 extern "C" int gfk_launch_win_update(const GfkModel* m, const GfkUpdate* u, hipStream_t s) {
   const int extra = m->ctx_fused == 1 ? m->n_tiles : (m->ctx_fused == 2 ? (m->C + 63) / 64 : 0);
   if (m->stage_flags & WIN_SPARSE) {
     // bag-of-words inputs, or fused CombinedTM (its contextual half as dense tiles after
     // the sparse ones: B <= 64 so the operand blocks fit the kernel's LDS)
     const bool comb = m->input == GFK_IN_COMBINED && m->ctx_fused == 1;
-    if (m->H[0] > 64 || m->bmax > (comb ? 64 : GFK_BMAX_LIMIT) || !(m->input == GFK_IN_BOW || comb) ||
-        (comb && (m->stage_flags & GFK_WIN_SPLIT)) ||
-        (m->bmax > 128 && (m->stage_flags & GFK_WIN_SPLIT)))
+    if (m->H[0] > 64 || m->bmax > (comb ? 64 : GFK_BMAX_LIMIT) || !(m->input == GFK_IN_BOW || comb))
       return -1;
-    // the contextual half: dense tiles of this launch, or the persistent kernel after it
-    const bool ctxpp = comb && (m->stage_flags & WIN_CTXPP) && m->ctx_bgrid > 0;
-    if (ctxpp) {
-      const int e = launch_win_sparse_bow(m, u, s);
-      if (e) return e;
-      const dim3 gp(2 * m->ctx_bgrid);
-      const size_t sp = sizeof(float) * win_ctxpp_lds_floats(*m);
-      do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_win_ctx_pp_k<true>), gfk_grid(gp, m), dim3(WCT), sp, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_win_ctx_pp_k<false>), gp, dim3(WCT), sp, s, GfkArgT<false>{*m}); } while (0);
-      return (int)hipGetLastError();
-    }
     const dim3 gs(u->n_w + u->n_v + 1 + m->n_tiles * (comb ? 2 : 1));
     if (m->bmax > 128)
       GFK_WIN_SPARSE_LB_LAUNCH();
-    else if (m->stage_flags & GFK_WIN_SPLIT)
-      do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_win_rows_k<512, true>), gfk_grid(gs, m), dim3(512), gfk_win_update_smem(m), s, GfkArgT<true>{gfk_dev(m)}, GfkUArgT<true>{reinterpret_cast<const GfkUpdate*>(m->dev_upd)}); else hipLaunchKernelGGL((gfk_win_rows_k<512, false>), gs, dim3(512), gfk_win_update_smem(m), s, GfkArgT<false>{*m}, GfkUArgT<false>{*u}); } while (0);
     else if (comb && win_sparse_vl(m))
       GFK_WIN_SPARSE_LAUNCH(true, true);
     else if (comb)
@@ -1926,7 +1473,7 @@ extern "C" size_t gfk_win_fold_smem() {
 
 extern "C" int gfk_win_fold_launch(const GfkModel* m0, const GfkUpdate* u0, const GfkFold* f, hipStream_t s) {
   if (m0->input != GFK_IN_BOW || m0->H[0] > 64 || m0->bmax != 64 || m0->update_mode != 1 ||
-      (m0->stage_flags & (WIN_SPARSE | GFK_WIN_SPLIT | GFK_LB)) || m0->lab_on || f->M < 1 ||
+      (m0->stage_flags & (WIN_SPARSE | GFK_LB)) || m0->lab_on || f->M < 1 ||
       !f->models || !f->upds || !f->cl || f->nj != (m0->H[0] + 15) / 16 || (f->n_left > 0 && !f->left))
     return -1;
   for (int j = 0; j < u0->n_v; ++j)
@@ -1949,7 +1496,6 @@ extern "C" int gfk_win_update_set_smem(size_t bytes) {
                       (const void*)gfk_win_sparse_k<512, false, true>, (const void*)gfk_win_sparse_k<512, true, true>,
                       (const void*)gfk_win_sparse_k<512, false, false, true>, (const void*)gfk_win_sparse_k<512, true, false, true>,
                       (const void*)gfk_win_sparse_k<512, false, true, true>, (const void*)gfk_win_sparse_k<512, true, true, true>,
-                      (const void*)gfk_win_rows_k<512, false>, (const void*)gfk_win_rows_k<512, true>,
                       (const void*)gfk_win_sparse_k<512, false, false, false, GFK_BMAX_LIMIT / 64>,
                       (const void*)gfk_win_sparse_k<512, true, false, false, GFK_BMAX_LIMIT / 64>,
                       (const void*)gfk_win_lb_k<1024>};

@@ -59,21 +59,18 @@ STAGE_FWD_STRIP = 4               # bit 2: ProdLDA strip forward (csrc/prodlda.h
 STAGE_FWD_STRIP_PF = 8            # bit 3: its prefetching 8-wave variant
 STAGE_WIN_SPARSE = 16             # bit 4: sparse W_in tiles (csrc/update.hip win_tile_sparse)
 STAGE_CTX_FULL = 32               # bit 5: CombinedTM forward, one workgroup per tile (csrc/ctx.hip)
-STAGE_FWD_STRIP_ROLL = 64         # bit 6: the strip forward's rolling-prefetch variant
-STAGE_WIN_SPLIT = 128             # bit 7: split W_in update (csrc/update.hip gfk_win_dense_k)
 STAGE_FWD_STRIP_RING = 256        # bit 8: the strip forward's ring-prefetch variant (PF = 3)
 STAGE_WIN_BATCH8 = 512            # bit 9: batched launches: win_update's 8-wave tile shape
-STAGE_WIN_VREG = 1024             # bit 10: sparse W_in tiles keep the second moment in registers
-STAGE_CTX_BAL = 2048              # bit 11: CombinedTM forward, balanced persistent shape (csrc/ctx.hip)
 STAGE_CTX_BWDPP = 4096            # bit 12: CombinedTM backward, persistent pipelined shape (csrc/ctx.hip)
-STAGE_CTX_BAL3 = 8192             # bit 13: the balanced forward's 16-wave 3-deep variant (csrc/ctx.hip)
-STAGE_WIN_CTXPP = 16384           # bit 14: CombinedTM's contextual W_in half as a persistent kernel
 STAGE_CTX_RS = 32768              # bit 15: CombinedTM forward, Wa register-streamed (csrc/ctx.hip)
 STAGE_FWD_POSTFOLD = 65536        # bit 16: the strip forward computes post_fwd (csrc/prodlda.hip FP)
-STAGE_POST_EXTRA_ROWBWD = 131072  # bit 17: post_bwd's batch-level workgroup runs in row_bwd
-STAGE_BWD_KQ1 = 262144            # bit 18: one-k-range backward walking several tiles (K <= 64)
 STAGE_LB = 524288                 # bit 19: the large-batch plan (bmax 256 / 512, csrc/gfk_common.h)
-STAGE_POST_ROWS2 = 1048576        # bit 20: post_bwd two rows per workgroup (batched launches)
+STAGE_POST_ROWS2 = 1048576        # bit 20: batched post_bwd, two rows per workgroup; its batch-level
+                                  #         workgroup in row_bwd (csrc/posterior.hip)
+# (removed in round 6, measured not faster and the default nowhere: bit 6 the strip forward's
+# plain rolling prefetch, 7 the split W_in update, 10 the sparse tile's register second moment
+# as a knob, 11 / 13 the LDS-DMA balanced CombinedTM forwards, 14 the persistent Wc update,
+# 17 the moved batch-level workgroup on its own, 18 the one-range backward walking tiles)
 
 
 def engine_bmax(tm) -> int:
@@ -392,16 +389,7 @@ class FusedEngine(EngineBase):
             raise ValueError(f"the fused update mode is Adam only (solver {self.solver})")
         self.update_mode = mode
         self._m.update_mode = mode
-        was = self.win_split
-        if getattr(self, "_win_split_ok", False):     # the split W_in update is fused-mode only
-            if mode == UPDATE_FUSED:
-                self._m.stage_flags |= STAGE_WIN_SPLIT
-            else:
-                self._m.stage_flags &= ~STAGE_WIN_SPLIT
         self._rebuild_adam()
-        if self.win_split and not was and self.plan is not None:
-            # the bound batch was prepared without word stamps: prepare it again
-            self._launch([abi.PH_BATCH_PREP])
 
     def set_adam_t(self, t: int):
         """Set the optimizer step count and the device bias-correction state."""
@@ -411,9 +399,6 @@ class FusedEngine(EngineBase):
         if t > 0:
             self.adam_coef.copy_(torch.tensor([self.lr / (1.0 - p1), 1.0 / np.sqrt(1.0 - p2)],
                                               dtype=torch.float32))
-        if self.win_split and getattr(self, "plan", None) is not None:
-            # the split W_in update snapshots the powers when it prepares a batch
-            self._launch([abi.PH_BATCH_PREP])
 
     def _ptr(self, buf, key):
         if key not in self.flat.slots:
@@ -546,18 +531,16 @@ class FusedEngine(EngineBase):
                 # per SIMD, ~190 VGPRs) measured ahead of 16 non-prefetching waves per CU
                 # (K=200: V=112k 0.341 vs 0.346 ms, V=74k 0.251 vs 0.260 ms; the tile
                 # kernel 0.346 / 0.255); GFEDNTM_FWD_STRIP_PF=0 selects the 16-wave one
-                # 2, the default: the rolling prefetch (the next strip's k pair loaded into
-                # the registers its MFMAs just consumed; 12-16 waves per CU, no second
-                # register block)
-                # 3, the default since g26: the same rolling prefetch through a 13-pair ring
-                # (K > 104: 128 VGPRs, 16 waves per CU instead of 12; K = 200 V = 112k forward
-                # 39.7 -> 36.5 us, round 0.2794 -> 0.2751 ms; identical code for K <= 104)
+                # 3, the default since g26: the rolling prefetch (the next strip's k pair loaded
+                # into the registers its MFMAs just consumed) through a 13-pair ring (K > 104:
+                # 128 VGPRs, 16 waves per CU instead of 12; K = 200 V = 112k forward 39.7 ->
+                # 36.5 us, round 0.2794 -> 0.2751 ms).  Round 6 removed the plain rolling
+                # variant (2) and the non-prefetching one (0), both measured slower; "1" keeps
+                # the 8-wave prefetching variant the batched plan uses at large V
                 pf = "3" if m.mm_bf16 else os.environ.get("GFEDNTM_FWD_STRIP_PF", "3")
                 if pf == "1":
                     m.stage_flags |= STAGE_FWD_STRIP_PF
-                elif pf == "2":
-                    m.stage_flags |= STAGE_FWD_STRIP_ROLL
-                elif pf == "3":
+                else:
                     m.stage_flags |= STAGE_FWD_STRIP_RING
                 m.dec_grid = int(min(m.n_tiles, cu))
                 # the batch-coupled posterior (BN of the heads, reparameterisation, softmax,
@@ -591,28 +574,17 @@ class FusedEngine(EngineBase):
             # recomputing them in each range workgroup; GFEDNTM_BWD_PRE=0 selects the
             # recomputing variant
             kq4 = m.n_dpart < m.n_tiles and -(-m.K // 16) >= 4
-            # (1: <= 80 VGPRs, three per CU; 2: two per CU; 3, the default: two per CU,
-            # software-pipelined -- the next tile's loads in flight during this tile's
-            # compute and stores -- where it applies: fp32, B = 64)
+            # (2: two per CU; 3, the default: two per CU, software-pipelined -- the next
+            # tile's loads in flight during this tile's compute and stores -- where it
+            # applies: fp32, B = 64.  Round 6 removed the 80-VGPR three-per-CU shape and the
+            # split beta Adam pass, both measured slower: profiles/r2, profiles/r4)
             pre = os.environ.get("GFEDNTM_BWD_PRE", "3")
-            m.bwd_pre = int(pre) if kq4 and m.bmax <= 64 and pre in ("1", "2", "3") else 0
-            if m.bwd_pre == 1 and 3 * self.lib.gfk_smem_required(C.byref(m), 1) <= LDS_LIMIT:
-                # its smaller LDS plan (no logit tile, G aliases dt) and <= 80 VGPRs fit
-                # THREE range workgroups per CU: 3/4 of a CU's slots per slab of 4
-                m.n_dpart = min(3 * cu // 4, m.n_tiles - 1)
-            elif (m.bwd_pre == 3 and m.bmax == 64 and m.ldb % 64 == 0
-                  and m.K * m.ldb * 4 < 0x7FFF0000):
+            m.bwd_pre = int(pre) if kq4 and m.bmax <= 64 and pre in ("2", "3") else 0
+            if (m.bwd_pre == 3 and m.bmax == 64 and m.ldb % 64 == 0
+                    and m.K * m.ldb * 4 < 0x7FFF0000):
                 pass
             elif m.bwd_pre:
                 m.bwd_pre = 2            # two per CU, no register cap
-            # GFEDNTM_BETA_SPLIT=1: beta's Adam as one streaming float4 pass after
-            # prodlda_bwd (which then only writes the gradient) instead of the epilogue.
-            # The pass alone runs at 5.7-6.7 TB/s vs 4.2 for the epilogue's layout
-            # (profiles/r2/adam_rmw_bandwidth.jsonl), but the round is slower (K=200,
-            # V=112k: 0.446 vs 0.406 ms): prodlda_bwd's own staging / MFMA time does not
-            # shrink without the Adam work, so the extra pass is added, not overlapped
-            m.beta_split = int(os.environ.get("GFEDNTM_BETA_SPLIT", "0") == "1"
-                               and self.update_mode == UPDATE_FUSED)
         # W_in tiles as entry lists instead of dense x^T MFMA tiles where a 64-word tile
         # holds few non-zeros (large vocabularies, the 8-wave update shape: more tiles than
         # two rounds of workgroups); GFEDNTM_WIN_SPARSE=0 keeps the dense tiles
@@ -625,31 +597,20 @@ class FusedEngine(EngineBase):
         if m.ctx_fused == 1 and m.bmax <= 64 and (
                 cf_env == "1" or (cf_env == "auto" and (m.n_tiles > 2 * cu_n or m.mm_bf16))):
             m.stage_flags |= STAGE_CTX_FULL
-            # ... as the balanced persistent kernel: ctx_parts workgroups (two per CU) own
-            # equal column ranges instead of one workgroup per tile (whose last round runs
-            # mostly empty) and leave one contextual z0 partial each; slices staged by DMA.
-            # GFEDNTM_CTX_BAL=0 keeps the one-workgroup-per-tile kernel
-            bal = os.environ.get("GFEDNTM_CTX_BAL", "4")
-            if bal != "0" and int(m.H[0]) <= 64 and m.V * m.C * 4 < (1 << 31):
-                m.stage_flags |= STAGE_CTX_BAL
-                m.ctx_parts = int(min(m.n_tiles, 2 * cu_n))
-                # "3": one 16-wave workgroup per CU, slices three deep (counted waits), the
-                # Wc rows / bias by DMA too; needs C > 192, H0 <= 63 and the flat buffer
-                # under 2 GB (32-bit buffer offsets)
-                if (bal in ("3", "4") and int(m.H[0]) <= 63 and m.C > 192
-                        and 4 * self.flat.n_total < (1 << 31)):
-                    m.stage_flags |= STAGE_CTX_BAL3
-                    m.ctx_parts = int(min(m.n_tiles, cu_n))
-                # "4" (the default; "3" where it does not apply): Wa streamed from global
-                # memory into registers as the MFMA A operand, x_ctx staged once per
-                # workgroup in 256-float phases (at most 32 16-column units per CU: V <= 131k
-                # on 256 CUs).  V = 99k, interleaved: ctx_fwd 134 -> 122 us, round 0.7386 /
-                # 0.7396 -> 0.7287 / 0.7304 ms (profiles/r4/ab_s8)
-                n_units = -(-int(m.V) // 16)
-                if (bal == "4" and -(-n_units // min(m.n_tiles, cu_n)) <= 32
-                        and 4 * self.flat.n_total < (1 << 31)):
-                    m.stage_flags |= STAGE_CTX_RS
-                    m.ctx_parts = int(min(m.n_tiles, cu_n))
+            # ... as the register-streamed persistent kernel: one 16-wave workgroup per CU
+            # owns an equal range of 16-column units (at most 32: V <= 131k on 256 CUs), Wa
+            # streamed from global memory into registers as the MFMA A operand, x_ctx staged
+            # once per workgroup in 256-float phases; each workgroup leaves one contextual z0
+            # partial (ctx_parts for enc_in).  V = 99k, interleaved: ctx_fwd 134 -> 122 us,
+            # round 0.7386 -> 0.7287 ms (profiles/r4/ab_s8).  GFEDNTM_CTX_RS=0 keeps the
+            # one-workgroup-per-tile kernel.  (Round 6 removed the LDS-DMA balanced shapes,
+            # bits 11 / 13, measured slower than this one.)
+            n_units = -(-int(m.V) // 16)
+            if (os.environ.get("GFEDNTM_CTX_RS", "1") != "0" and int(m.H[0]) <= 64
+                    and -(-n_units // min(m.n_tiles, cu_n)) <= 32
+                    and m.V * m.C * 4 < (1 << 31) and 4 * self.flat.n_total < (1 << 31)):
+                m.stage_flags |= STAGE_CTX_RS
+                m.ctx_parts = int(min(m.n_tiles, cu_n))
         # CombinedTM backward as one persistent workgroup per CU walking equal ranges of the
         # (tile, C chunk) items with the next item's Wa state in flight (csrc/ctx.hip
         # gfk_ctx_bwd_pp_k); GFEDNTM_CTX_BWDPP=0 keeps the (tile, chunk) grid
@@ -665,34 +626,12 @@ class FusedEngine(EngineBase):
         if (m.input == abi.IN_BOW or comb) and int(m.H[0]) <= 64 and m.bmax <= 128 and (
                 ws_env == "1" or (ws_env == "auto" and m.n_tiles > 4 * cu_n)):
             m.stage_flags |= STAGE_WIN_SPARSE
-            # fused CombinedTM: the contextual half (Wc) as dense tiles of the same launch, or
-            # (GFEDNTM_WIN_CTXPP=1) as a persistent kernel after the sparse tiles (csrc/
-            # update.hip gfk_win_ctx_pp_k: equal word ranges per slot, the next block's state
-            # in flight).  Not the default: V = 99k, interleaved on one box, round 0.7309 /
-            # 0.7415 ms with the tiles vs 0.7389 / 0.7389 (the kernel moves Wc's 120 MB at
-            # 2.4 TB/s: Wc's rows start V H0 floats into W_in, not 16-byte aligned at odd V)
-            if (comb and os.environ.get("GFEDNTM_WIN_CTXPP", "0") == "1"
-                    and 4 * self.flat.n_total < (1 << 31)):
-                m.stage_flags |= STAGE_WIN_CTXPP
-                m.ctx_bgrid = int(cu_n)
-            # fused mode: the tile's second moment goes through LDS (64 VGPRs, 4 workgroups
-            # per CU; profiles/r3/win_vl/); GFEDNTM_WIN_VL=0 keeps it in registers
-            if os.environ.get("GFEDNTM_WIN_VL", "1") == "0":
-                m.stage_flags |= STAGE_WIN_VREG
-            # split W_in update (GFEDNTM_WIN_SPLIT=1, fused mode): the words not in the batch
-            # (~89 % at V = 112k) get their zero-gradient Adam step from gfk_win_dense_k on a
-            # side stream from the start of the step; the sparse tiles then move only the
-            # batch's words.  Bit-identical to the one-kernel update (tests/test_win_split.py)
-            # but slower, so not the default: K=200 V=112k 0.320 vs 0.294 ms per round
-            # (profiles/r3/win_split.md) -- the 134 MB streaming kernel does not hide
-            # behind enc_in / post_fwd (enc_in 14 -> 29 us) and its sparse half still pays
-            # three dependent rounds per tile (28 us)
-            win_al = (int(m.w_in or 0) % 16 == 0
-                      and m.off_m % 4 == 0 and m.off_v % 4 == 0)
-            self._win_split_ok = (os.environ.get("GFEDNTM_WIN_SPLIT", "0") == "1" and win_al
-                                  and m.input == abi.IN_BOW)
-            if self._win_split_ok and self.update_mode == UPDATE_FUSED:
-                m.stage_flags |= STAGE_WIN_SPLIT
+            # fused CombinedTM: the contextual half (Wc) as dense tiles of the same launch.
+            # (Round 6 removed three opt-in variants measured slower: Wc as a persistent
+            # kernel -- V = 99k, 0.7389 vs 0.7309 ms; the sparse tile's second moment in
+            # registers instead of LDS -- profiles/r3/win_vl/; the split W_in update, the
+            # words outside the batch on a side stream -- K=200 V=112k 0.320 vs 0.294 ms,
+            # profiles/r3/win_split.md)
         self._alloc_workspace()
         rc = self.lib.gfk_setup(C.byref(m))
         if rc:
@@ -718,8 +657,6 @@ class FusedEngine(EngineBase):
         m.dec_grid = int(min(m.n_tiles, 2 * cu))
         m.n_dpart = 1
         m.bwd_pre = 0
-        m.beta_split = 0
-        self._win_split_ok = False
         which = (0, 1) if m.kind == abi.KIND_PRODLDA else (2, 3)
         need = max(self.lib.gfk_smem_required(C.byref(m), w) for w in which + (4, 5, 7))
         if need > LDS_LIMIT:
@@ -821,11 +758,6 @@ class FusedEngine(EngineBase):
             # (the large-batch plan: the [B, ldb] logit / logit-gradient matrix)
             "dt": f(B * int(m.ldb) if m.stage_flags & STAGE_LB else
                     m.n_tiles * B * 66 + 64 * (4 * m.n_dpart + 32) if m.bwd_pre else 1),
-            # split W_in update: per-word generation stamps of the batch's words + the
-            # current generation (prepare_next_batch -> gfk_win_dense_k)
-            "wstamp": torch.zeros((V if getattr(self, "_win_split_ok", False) else 1) + 16,
-                                  dtype=torch.int32, device=dev),
-            "wgen": torch.zeros(16, dtype=torch.int32, device=dev),
             # the large-batch plan's posterior column statistics (6 x 2K floats)
             "colstat": f(12 * K if m.stage_flags & STAGE_LB else 1),
         }
@@ -838,10 +770,6 @@ class FusedEngine(EngineBase):
         for i, h in enumerate(hs):
             ws[f"dz{i}"] = f(B, h)
         self.ws = ws
-        # the split W_in update's side stream and fork / join events (created here, never
-        # inside a graph capture)
-        self._win_side = ((torch.cuda.Stream(dev), torch.cuda.Event(), torch.cuda.Event())
-                          if getattr(self, "_win_split_ok", False) else None)
         self._alloc_ctx()
         for k, t in ws.items():
             if k[0] in "za" and k[1:].isdigit():
@@ -948,9 +876,6 @@ class FusedEngine(EngineBase):
     def _rebuild_adam(self):
         self._sync_opt_fields()
         self.adam_grid = int(max(1, self._fill_adam(self._a)))
-        self._a_beta = abi.GfkAdam()
-        self.beta_adam_grid = int(max(1, self._fill_adam(self._a_beta, keys=["beta"],
-                                                         keep_grad=True)))
         self._invalidate_graph()
 
     @property
@@ -971,33 +896,6 @@ class FusedEngine(EngineBase):
             return ("large-batch: hipBLASLt decoder GEMMs + HIP kernels, gradient mode"
                     if self._m.kind == abi.KIND_PRODLDA else "large-batch: HIP kernels, gradient mode")
         return "fused kernels" + (" (fused optimizer epilogues)" if self.update_mode == UPDATE_FUSED else "")
-
-    @property
-    def beta_split(self) -> bool:
-        """Beta's update runs as a separate streaming optimizer pass (large V)."""
-        return bool(self._m.beta_split) and self.update_mode == UPDATE_FUSED
-
-    @property
-    def win_split(self) -> bool:
-        """W_in's update is split: the words not in the batch on a side stream."""
-        return bool(self._m.stage_flags & STAGE_WIN_SPLIT)
-
-    def _win_fork(self):
-        side, ev_fork, ev_join = self._win_side
-        ev_fork.record(torch.cuda.current_stream(self.device))
-        side.wait_event(ev_fork)
-        with torch.cuda.stream(side):
-            self._launch_native([abi.PH_WIN_DENSE])
-        ev_join.record(side)
-
-    def _win_join(self):
-        torch.cuda.current_stream(self.device).wait_event(self._win_side[2])
-
-    def _beta_adam(self):
-        stream = torch.cuda.current_stream(self.device).cuda_stream
-        rc = self.lib.gfk_launch_adam(C.byref(self._a_beta), self.beta_adam_grid, stream)
-        if rc:
-            raise RuntimeError(f"gfk_launch_adam failed ({rc})")
 
     def set_fedavg_scale(self, w: Optional[float]):
         """Pre-scale the shared state by w after the update (None disables)."""
@@ -1027,10 +925,10 @@ class FusedEngine(EngineBase):
                 self.ws["dbsm"] = torch.zeros(nnz + 16, dtype=torch.float32, device=dev)
             m.ws_dbsm = self.ws["dbsm"].data_ptr()
         m.ctx = data.contextual.data_ptr() if data.contextual is not None else None
-        if m.stage_flags & STAGE_CTX_BAL and data.contextual is not None \
+        if m.stage_flags & STAGE_CTX_RS and data.contextual is not None \
                 and 4 * data.contextual.numel() >= (1 << 31):
-            # the balanced forward addresses x_ctx with 32-bit buffer offsets
-            m.stage_flags &= ~(STAGE_CTX_BAL | STAGE_CTX_BAL3 | STAGE_CTX_RS)
+            # the register-streamed forward addresses x_ctx with 32-bit buffer offsets
+            m.stage_flags &= ~STAGE_CTX_RS
             m.ctx_parts = 0
         if m.lab_on:
             if data.labels is None or data.labels.shape[1] != m.L:
@@ -1076,11 +974,6 @@ class FusedEngine(EngineBase):
                 ph.insert(ph.index(abi.PH_PRODLDA_BWD) + 1, abi.PH_LB_GEMM_BWD)
             if self._m.stage_flags & STAGE_FWD_POSTFOLD:
                 ph.remove(abi.PH_POST_FWD)          # computed by the strip forward
-            if self.beta_split:
-                ph.insert(ph.index(abi.PH_PRODLDA_BWD) + 1, abi.PH_BETA_ADAM)
-        if self.win_split:
-            ph.insert(0, abi.PH_WIN_FORK)
-            ph.insert(ph.index(abi.PH_ENC_BWD), abi.PH_WIN_JOIN)
         if self.ctx_fused:
             if self._m.ctx_fused == 1:
                 ph.insert(ph.index(abi.PH_ENC_FWD), abi.PH_CTXF_FWD)
@@ -1091,8 +984,6 @@ class FusedEngine(EngineBase):
         if self._comm is not None and self._comm["mode"] == "graph":
             if "beta" in self._comm:
                 last = abi.PH_PRODLDA_BWD if abi.PH_PRODLDA_BWD in ph else abi.PH_LDA_BETA_BWD
-                if abi.PH_BETA_ADAM in ph:
-                    last = abi.PH_BETA_ADAM
                 ph.insert(ph.index(last) + 1, abi.PH_FEDAVG_BETA)
             if "wa" in self._comm:
                 ph.insert(ph.index(abi.PH_CTXF_BWD) + 1, abi.PH_FEDAVG_WA)
@@ -1405,18 +1296,12 @@ class FusedEngine(EngineBase):
                         self._ctx_fwd()
                     elif p == abi.PH_CTX_BWD:
                         self._ctx_bwd()
-                    elif p == abi.PH_BETA_ADAM:
-                        self._beta_adam()
                     elif p == abi.PH_FEDAVG_BETA:
                         self._fedavg_beta()
                     elif p == abi.PH_FEDAVG_WA:
                         self._fedavg_wa()
                     elif p == abi.PH_FEDAVG_END:
                         self._fedavg_end()
-                    elif p == abi.PH_WIN_FORK:
-                        self._win_fork()
-                    elif p == abi.PH_WIN_JOIN:
-                        self._win_join()
                     elif p == abi.PH_LB_GEMM_FWD:
                         self._lb_gemm_fwd()
                     elif p == abi.PH_LB_GEMM_BWD:
@@ -1605,11 +1490,8 @@ class FusedEngine(EngineBase):
 # launch per phase must agree on all of them (their pointers and per-client values differ)
 _BATCH_SHAPE_FIELDS = ("bmax", "V", "ldb", "K", "n_hidden", "act", "kind", "input", "C", "L", "vb", "ctx_parts",
                        "n_tiles", "dec_grid", "learn_priors", "stage_flags", "kt", "n_dpart",
-                       "beta_split", "update_mode", "ctx_fused", "ctx_kb", "ctx_ckb", "mm_bf16",
+                       "update_mode", "ctx_fused", "ctx_kb", "ctx_ckb", "mm_bf16",
                        "lab_on", "lab_off", "lab_in_enc", "bwd_pre")
-
-
-_BATCH_FORK_PHASES = (abi.PH_WIN_FORK, abi.PH_WIN_JOIN)
 
 
 class BatchedSteps:
@@ -1633,7 +1515,6 @@ class BatchedSteps:
         self._blob = None
         self._host = None
         self._phases = e0.phases()
-        self._side = (torch.cuda.Stream(self.device), torch.cuda.Event(), torch.cuda.Event())
         self._cu = torch.cuda.get_device_properties(self.device).multi_processor_count
         self._fold = None                 # abi.GfkFold when the FedAvg runs in the epilogues
         self._fold_left = None            # its device table of leftover pieces
@@ -1659,7 +1540,7 @@ class BatchedSteps:
                 raise ValueError("batched engines must share a device")
             if e.phases() != ph:
                 raise ValueError("batched engines must run the same phases")
-            if any(p in abi.HOST_PHASES and p not in _BATCH_FORK_PHASES for p in ph) \
+            if any(p in abi.HOST_PHASES for p in ph) \
                     or e._comm is not None:
                 raise ValueError("batched launches need native phases only")
             for f in _BATCH_SHAPE_FIELDS:
@@ -1700,14 +1581,14 @@ class BatchedSteps:
                     and M * fill <= self._cu):
                 mm.dec_grid = fill
             elif (mm.stage_flags & STAGE_FWD_STRIP and M * mm.dec_grid > self._cu
-                    and bstrip != "keep" and mm.mm_bf16):
+                    and bstrip != "keep" and (mm.mm_bf16 or bstrip == "ring")):
                 # bf16 GEMM operands exist only in the ring variant: keep it, M clients' grids
                 # sharing one round of the CUs (the strips are grid-strided, any grid works)
                 mm.dec_grid = max(1, self._cu // M)
             elif (mm.stage_flags & STAGE_FWD_STRIP and M * mm.dec_grid > self._cu
                     and bstrip != "keep"):
                 # (the prefetching variant has no folded posterior: post_fwd runs again)
-                mm.stage_flags = (mm.stage_flags & ~(STAGE_FWD_STRIP_ROLL | STAGE_FWD_STRIP_RING
+                mm.stage_flags = (mm.stage_flags & ~(STAGE_FWD_STRIP_RING
                                                      | STAGE_FWD_POSTFOLD)) | STAGE_FWD_STRIP_PF
             # the posterior folded into the ring forward for M > 1 clients (the engines' own
             # plan keeps post_fwd for one client; GFEDNTM_POSTFOLD=0: never)
@@ -1715,31 +1596,15 @@ class BatchedSteps:
                     and os.environ.get("GFEDNTM_POSTFOLD", "auto") != "0"):
                 mm.stage_flags |= STAGE_FWD_POSTFOLD
             # post_bwd: M clients x (bmax + 1) workgroups of 16 waves with the batch matrices
-            # in LDS (~93 KB: one per CU) run in three rounds at M = 8.  GFEDNTM_BATCH_POST:
-            # "rows2" (the default) -- two rows per workgroup (the matrices, weights and column
-            # sums staged once for both) and the batch-level workgroup moved into row_bwd:
-            # M bmax / 2 workgroups, one round; "l2" -- the round-5a variant, the matrices
-            # read from L2 (~42 KB, two per CU) with the moved batch-level workgroup, measured
-            # slower (0.1507 / 0.1520 ms without vs 0.1535 / 0.1527 with,
-            # profiles/r5/ab_batch.txt); "0" -- neither
-            bpost = os.environ.get("GFEDNTM_BATCH_POST", "rows2")
-            if M > 1 and M * (mm.bmax + 1) > self._cu and bpost == "rows2":
-                mm.stage_flags |= STAGE_POST_EXTRA_ROWBWD | STAGE_POST_ROWS2
-            elif M > 1 and M * (mm.bmax + 1) > self._cu and bpost in ("1", "l2"):
-                mm.stage_flags |= 2 | STAGE_POST_EXTRA_ROWBWD
-            # prodlda_bwd at K <= 64: one 16-wave workgroup per tile (~61 KB of LDS; 64 VGPRs
-            # with the batched descriptor copied at entry, gfk_common.h gfk_model: two per CU,
-            # where 80 VGPRs fit one); the alternative, each workgroup walking t tiles
-            # (n_dpart = n_tiles / t slabs, the persistent one-range shape, t the smallest
-            # that fits one round), measured slower: 0.1492 / 0.1484 ms without vs 0.1535 /
-            # 0.1527 with (profiles/r5/ab_batch.txt) -- a tile's staging round is not hidden
-            # when one workgroup walks several.  Opt-in: GFEDNTM_BATCH_BWD=1
-            if (M > 1 and mm.kind == abi.KIND_PRODLDA and mm.K <= 64 and mm.n_dpart == mm.n_tiles
-                    and M * mm.n_tiles > 2 * self._cu
-                    and os.environ.get("GFEDNTM_BATCH_BWD", "0") == "1"):
-                t = -(-(M * mm.n_tiles) // (2 * self._cu))
-                mm.n_dpart = -(-mm.n_tiles // t)
-                mm.stage_flags |= STAGE_BWD_KQ1
+            # in LDS (~93 KB: one per CU) run in three rounds at M = 8.  Two rows per
+            # workgroup (the matrices, weights and column sums staged once for both) and the
+            # batch-level workgroup moved into row_bwd: M bmax / 2 workgroups, one round
+            # (GFEDNTM_BATCH_POST=0: off).  (Round 6 removed the opt-in variants measured
+            # slower: the matrices read from L2, and the persistent one-range backward
+            # walking several tiles -- profiles/r5/ab_batch.txt.)
+            if (M > 1 and M * (mm.bmax + 1) > self._cu
+                    and os.environ.get("GFEDNTM_BATCH_POST", "rows2") != "0"):
+                mm.stage_flags |= STAGE_POST_ROWS2
             # win_update: all clients' W_in tiles in one launch -> the 8-wave tile shape once
             # they exceed two rounds of 16-wave workgroups (GFEDNTM_BATCH_WIN8=0: off)
             if (M * (mm.n_tiles + 8) > 2 * self._cu
@@ -1808,9 +1673,9 @@ class BatchedSteps:
             (not m.mm_bf16, "fp32 GEMM operands only"),
             (m.K <= 64 and m.bmax == 64, "K <= 64 and batch 64 only"),
             (max(int(m.H[i]) for i in range(m.n_hidden)) <= 64, "hidden layers <= 64 only"),
-            (not m.beta_split and not m.bwd_pre and m.n_dpart == m.n_tiles,
+            (not m.bwd_pre and m.n_dpart == m.n_tiles,
              "the one-slab-per-tile backward only"),
-            (not m.stage_flags & (STAGE_WIN_SPARSE | STAGE_WIN_SPLIT | STAGE_LB | STAGE_BWD_KQ1),
+            (not m.stage_flags & (STAGE_WIN_SPARSE | STAGE_LB),
              "dense W_in tiles only"),
             (m.kt % 2 == 0, "theta_d stride"),
             (all(e0._u.v[i].n <= 64 for i in range(e0._u.n_v)), "vector jobs <= 64 long"),
@@ -1942,10 +1807,9 @@ class BatchedSteps:
             raise RuntimeError(f"gfk_run (batched) failed: code {rc}")
 
     def launch(self, after=None):
-        """Enqueue one local step of every engine on the current stream (the split W_in
-        update's dense half forked onto a side stream, as in a single engine's step).
-        ``after``: {phase: callable} called (on the host, while enqueuing) right after
-        that phase's launch -- the multi-client rank round forks beta's FedAvg there."""
+        """Enqueue one local step of every engine on the current stream.  ``after``:
+        {phase: callable} called (on the host, while enqueuing) right after that phase's
+        launch -- the multi-client rank round forks beta's FedAvg there."""
         self._refresh()
         after = dict(after or {})
         phases = list(self._phases)
@@ -1955,8 +1819,7 @@ class BatchedSteps:
             after = {swap.get(p, p): f for p, f in after.items()}
         run: List[int] = []
         for p in phases + [None]:
-            if p is not None and p not in _BATCH_FORK_PHASES and p not in (abi.PH_FOLD_BWD,
-                                                                             abi.PH_FOLD_WIN):
+            if p is not None and p not in (abi.PH_FOLD_BWD, abi.PH_FOLD_WIN):
                 run.append(p)
                 if p not in after:
                     continue
@@ -1967,15 +1830,6 @@ class BatchedSteps:
                 self._run_fold(p)
             if p in after:
                 after[p]()
-            elif p == abi.PH_WIN_FORK:
-                side, ev_fork, ev_join = self._side
-                ev_fork.record(torch.cuda.current_stream(self.device))
-                side.wait_event(ev_fork)
-                with torch.cuda.stream(side):
-                    self._run([abi.PH_WIN_DENSE])
-                ev_join.record(side)
-            elif p == abi.PH_WIN_JOIN:
-                torch.cuda.current_stream(self.device).wait_event(self._side[2])
 
     def wa_final_phase(self) -> Optional[int]:
         """The phase after which every client's adapt_bert (CombinedTM) is final in the

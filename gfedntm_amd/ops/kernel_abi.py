@@ -33,7 +33,6 @@ PH_ADAM = 11
 PH_BATCH_PREP = 12
 PH_CTXF_FWD = 13      # CombinedTM contextual forward on the fused kernels (ctx_fwd)
 PH_CTXF_BWD = 14      # ... and its backward + adapt_bert updates (ctx_bwd)
-PH_WIN_DENSE = 15     # split W_in update: the zero-gradient Adam of the words not in the batch
 
 # PH_ENC_FWD = enc_in (sparse gather, MLP, heads, random draws), PH_POST_FWD =
 # post_fwd (batch-norm, reparameterisation, softmax, KL), PH_POST_BWD = row_bwd +
@@ -48,13 +47,7 @@ PH_CTX_BWD = 101
 # overlapping the encoder backward) and of the rest of the shared state
 PH_FEDAVG_BETA = 102
 PH_FEDAVG_END = 103
-# large-vocabulary ProdLDA (beta_split): prodlda_bwd leaves beta's gradient in the grad
-# slot and the generic float4 optimizer kernel updates beta (one streaming pass)
-PH_BETA_ADAM = 104
-# split W_in update (large vocabularies): PH_WIN_DENSE forked onto a side stream at the
-# start of the step, joined before win_update
-PH_WIN_FORK = 105
-PH_WIN_JOIN = 106
+# (104 - 106: round 5's split beta / W_in update phases, removed in round 6)
 # CombinedTM (fused): adapt_bert's share of the FedAvg forked onto the side stream once
 # ctx_bwd has finished it (overlapping win_update), behind beta's
 PH_FEDAVG_WA = 107
@@ -68,8 +61,8 @@ PH_LB_GEMM_BWD = 109
 # in place of PH_ENC_BWD (launched by the batched plan, not by gfk_run)
 PH_FOLD_BWD = 110
 PH_FOLD_WIN = 111
-HOST_PHASES = (PH_CTX_FWD, PH_CTX_BWD, PH_FEDAVG_BETA, PH_FEDAVG_END, PH_BETA_ADAM, PH_WIN_FORK,
-               PH_WIN_JOIN, PH_FEDAVG_WA, PH_LB_GEMM_FWD, PH_LB_GEMM_BWD)
+HOST_PHASES = (PH_CTX_FWD, PH_CTX_BWD, PH_FEDAVG_BETA, PH_FEDAVG_END, PH_FEDAVG_WA, PH_LB_GEMM_FWD,
+               PH_LB_GEMM_BWD)
 
 PRODLDA_STEP = [PH_ENC_FWD, PH_POST_FWD, PH_PRODLDA_FWD, PH_PRODLDA_LOSS, PH_PRODLDA_BWD,
                 PH_POST_BWD, PH_ENC_BWD]
@@ -88,7 +81,7 @@ class GfkModel(C.Structure):
         ("learn_priors", C.c_int32), ("stage_flags", C.c_int32), ("kt", C.c_int32),
         ("scatter_chunks", C.c_int32), ("n_dpart", C.c_int32), ("n_steps", C.c_int32),
         ("drop_enc", C.c_float), ("drop_theta", C.c_float), ("bn_momentum", C.c_float),
-        ("bn_eps", C.c_float), ("kl_weight", C.c_float), ("beta_split", C.c_int32),
+        ("bn_eps", C.c_float), ("kl_weight", C.c_float),
         ("seed", C.c_uint64),
         ("prior_mean", P), ("prior_var", P), ("beta", P), ("w_in", P), ("b_in", P),
         ("w_h", P * MAX_LAYERS), ("b_h", P * MAX_LAYERS),
@@ -123,7 +116,7 @@ class GfkModel(C.Structure):
         ("ws_lab", P), ("ws_dlab", P), ("ws_ce", P), ("ws_thd", P),
         ("lab_in_enc", C.c_int32), ("bwd_pre", C.c_int32), ("ws_dt", P),
         ("dev", P), ("dev_upd", P), ("n_batch", C.c_int32), ("ldb", C.c_int32),
-        ("ctx_bgrid", C.c_int32), ("ws_wstamp", P), ("ws_wgen", P), ("ws_colstat", P),
+        ("ctx_bgrid", C.c_int32), ("ws_colstat", P),
         ("kl_hist", P), ("rl_hist", P),
     ]
 

@@ -227,15 +227,13 @@ def test_batched_round_matches_branch_round(model_type):
 def test_batched_large_round_variants_match_branch_round(monkeypatch, strip):
     """8 clients at the headline's vocabulary (~74 tiles each): the batched launch switches
     the strip forward to 3-4 tiles per 16-wave workgroup ("fill", the default; "pf": the
-    8-wave prefetching variant), prodlda_bwd to workgroups walking several tiles, post_bwd's
-    batch-level workgroup into row_bwd, and win_update to its 8-wave tile shape (all
-    clients' tiles exceed two rounds of 16-wave workgroups).  The round must still agree
-    with the per-client branch round within fp32 rounding."""
-    from gfedntm_amd.ops.engine import (STAGE_BWD_KQ1, STAGE_FWD_STRIP_PF, STAGE_FWD_STRIP_RING,
-                                        STAGE_POST_EXTRA_ROWBWD, STAGE_WIN_BATCH8)
+    8-wave prefetching variant), post_bwd to two rows per workgroup with its batch-level
+    workgroup in row_bwd (bit 20), and win_update to its 8-wave tile shape (bit 9: all
+    clients' tiles exceed two rounds of 16-wave workgroups), all in the fused update mode.
+    The round must still agree with the per-client branch round within fp32 rounding."""
+    from gfedntm_amd.ops.engine import (STAGE_FWD_STRIP_PF, STAGE_FWD_STRIP_RING, STAGE_POST_ROWS2,
+                                        STAGE_WIN_BATCH8, UPDATE_FUSED)
     monkeypatch.setenv("GFEDNTM_BATCH_STRIP", strip)
-    monkeypatch.setenv("GFEDNTM_BATCH_POST", "l2")      # the opt-in shapes, covered here
-    monkeypatch.setenv("GFEDNTM_BATCH_BWD", "1")
     sc = generate_synthetic(vocab_size=5000, n_topics=50, n_docs=1000, n_nodes=8, frozen_topics=5,
                             nwords=(150, 250), seed=13)
     corpora = [ClientCorpus(synthetic=sc, node=i) for i in range(8)]
@@ -261,8 +259,8 @@ def test_batched_large_round_variants_match_branch_round(monkeypatch, strip):
         # the prefetching variant has no fold: post_fwd runs
         assert 8 * host.dec_grid > cu and host.stage_flags & STAGE_FWD_STRIP_PF
         assert not host.stage_flags & STAGE_FWD_POSTFOLD and abi.PH_POST_FWD in a._batched._phases
-    assert host.stage_flags & STAGE_POST_EXTRA_ROWBWD and host.stage_flags & 2
-    assert host.stage_flags & STAGE_BWD_KQ1 and host.n_dpart < host.n_tiles, host.n_dpart
+    assert host.stage_flags & STAGE_POST_ROWS2 and host.n_dpart == host.n_tiles
+    assert all(c.tm.engine.update_mode == UPDATE_FUSED for c in a.clients)
     lr = a.clients[0].tm.engine.lr
     for x, y in zip(a.clients, b.clients):
         diff = (x.tm.flat.buffer - y.tm.flat.buffer).abs()

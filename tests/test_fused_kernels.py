@@ -93,27 +93,30 @@ def test_step_matches_oracle(model_type, B, n_docs, K, H, V):
                                             (64, 80, 204, (50,), 80000),      # NP = 26, ring 13
                                             (64, 80, 120, (50,), 80000),      # NP = 16, ring 8
                                             (64, 80, 250, (50,), 80000)])     # NP = 32, ring 8
-@pytest.mark.parametrize("pf", ["2", "3"])
+@pytest.mark.parametrize("pf", ["1", "3"])
 def test_strip_forward_matches_oracle(monkeypatch, pf, B, n_docs, K, H, V):
     """prodlda_fwd_strip_kernel (GFEDNTM_FWD_STRIP=1 forces it): per-wave column strips,
     beta by buffer loads straight into the MFMA B registers, k paired for ds_read_b64;
-    pf = 2 rolls the next strip's whole beta block through the registers, pf = 3 a
-    13-pair ring (more than 13 pairs: the current strip's later pairs, then the next's)."""
+    pf = 1 the 8-wave variant prefetching the next strip's beta block (bit 3), pf = 3 a
+    13-pair ring (bit 8; more than 13 pairs: the current strip's later pairs, then the
+    next's)."""
     monkeypatch.setenv("GFEDNTM_FWD_STRIP", "1")
     monkeypatch.setenv("GFEDNTM_FWD_STRIP_PF", pf)
-    from gfedntm_amd.ops.engine import STAGE_FWD_STRIP
+    from gfedntm_amd.ops.engine import STAGE_FWD_STRIP, STAGE_FWD_STRIP_PF, STAGE_FWD_STRIP_RING
     fused, _ = _pair("prodLDA", V=V, K=K, H=H, B=B)
-    assert fused.engine._m.stage_flags & STAGE_FWD_STRIP
+    sf = fused.engine._m.stage_flags
+    assert sf & STAGE_FWD_STRIP
+    assert bool(sf & STAGE_FWD_STRIP_PF) == (pf == "1") and bool(sf & STAGE_FWD_STRIP_RING) == (pf == "3")
     _oracle_step("prodLDA", B, n_docs, K, H, V)
 
 
-@pytest.mark.parametrize("pre", ["3", "1", "2", "0"])
+@pytest.mark.parametrize("pre", ["3", "2", "0"])
 @pytest.mark.parametrize("B,n_docs,K,V", [(64, 80, 200, 40000), (32, 60, 64, 40000),
                                           (64, 100, 64, 40000), (64, 70, 100, 30011)])
 def test_bwd_precomputed_dlogit_matches_oracle(monkeypatch, pre, B, n_docs, K, V):
     """Persistent 4-k-range backward: the logit-gradient tiles precomputed once per tile
     by prodlda_dlogit -- software-pipelined (GFEDNTM_BWD_PRE=3, the default at B = 64;
-    B = 32 runs the =2 kernel), two or three workgroups per CU (=2 / =1) -- or recomputed
+    B = 32 runs the =2 kernel), two workgroups per CU (=2) -- or recomputed
     by every range workgroup (=0): all match the oracle (K = 100: a partial last k tile;
     V = 30011: a partial last vocabulary tile)."""
     monkeypatch.setenv("GFEDNTM_BWD_PRE", pre)
@@ -250,47 +253,6 @@ def test_graph_replay_matches_eager():
     torch.cuda.synchronize()
     torch.testing.assert_close(a.engine.loss_hist, b.engine.loss_hist, rtol=1e-5, atol=1e-4)
     torch.testing.assert_close(a.flat.buffer, b.flat.buffer, rtol=1e-5, atol=1e-6)
-
-
-@pytest.mark.parametrize("V,K", [(900, 50), (40000, 200), (40000, 20)])
-def test_beta_split_update_matches_fused(V, K, monkeypatch):
-    """Large-vocabulary beta update (prodlda_bwd writes the gradient, one streaming
-    optimizer pass applies it, GFEDNTM_BETA_SPLIT) vs Adam fused into prodlda_bwd: same
-    parameters, moments and losses, with the FedAvg pre-scale, over graph replays."""
-    tms = []
-    for split in ("0", "1"):
-        monkeypatch.setenv("GFEDNTM_BETA_SPLIT", split)
-        torch.manual_seed(0)
-        tms.append(AVITM(input_size=V, n_components=K, hidden_sizes=(50, 50), batch_size=64,
-                         verbose=False, device="cuda", backend="fused"))
-    a, b = tms
-    b.model.load_state_dict(a.model.state_dict())
-    b.engine.seed = b.engine._m.seed = a.engine.seed
-    assert not a.engine.beta_split and b.engine.beta_split
-    assert abi.PH_BETA_ADAM in b.engine.phases()
-    X = random_csr(200, V, 60, seed=2)
-    for tm in (a, b):
-        tm.engine.set_fedavg_scale(0.75)
-        _bind(tm, X, n_steps=6)
-        tm.engine.enable_graph(True)
-        for s in range(6):
-            tm.engine.step(s)
-    torch.cuda.synchronize()
-    torch.testing.assert_close(a.engine.loss_hist, b.engine.loss_hist, rtol=1e-5, atol=1e-2)
-    # the same Adam arithmetic inlined into two kernels may differ by an ulp (FP
-    # contraction); tensors whose true gradient is 0 (rounding noise, _NOISE_KEYS) then
-    # drift by up to lr per step after Adam's normalisation
-    sa, sb = a.model.state_dict(), b.model.state_dict()
-    lr_steps = 2 * a.engine.lr * 6
-    for k in sb:
-        if not sb[k].is_floating_point():
-            assert torch.equal(sa[k], sb[k]), k
-            continue
-        noisy = k in _NOISE_KEYS or "batchnorm.running_mean" in k
-        torch.testing.assert_close(sa[k], sb[k], rtol=1e-4, atol=lr_steps if noisy else 1e-5,
-                                   msg=lambda m: f"{k}: {m}")
-    fa, fb = a.engine.view_like(a.engine.exp_avg, "beta"), b.engine.view_like(b.engine.exp_avg, "beta")
-    torch.testing.assert_close(fa, fb, rtol=1e-2, atol=1e-4)
 
 
 @pytest.mark.parametrize("model_type", ["prodLDA", "LDA"])
@@ -744,20 +706,25 @@ def test_sparse_win_tiles_match_oracle(monkeypatch, model_type, B, n_docs, K, H,
     _oracle_step(model_type, B, n_docs, K, H, V)
 
 
-@pytest.mark.parametrize("bal", ["4", "3", "1", "0"])
+@pytest.mark.parametrize("rs", ["1", "0"])
 @pytest.mark.parametrize("Cdim,V", [(96, 600), (768, 9000), (100, 5000), (260, 3000), (768, 40000),
                                     (96, 69600), (260, 69600)])
-def test_ctm_full_tile_forward_matches_oracle(monkeypatch, Cdim, V, bal):
+def test_ctm_full_tile_forward_matches_oracle(monkeypatch, Cdim, V, rs):
     """ctx_fwd with all batch rows per vocab tile (stage_flags bit 5, the large-V shape;
-    GFEDNTM_CTX_FULL=1 forces it at small V): the balanced persistent kernel (bit 11,
-    DMA-staged slices, column ranges of 16-column units not aligned to the 64-column
-    tiles, a partial last C slice at C = 96 / 100 / 260), its 16-wave 3-deep variant (bal = 3,
-    C > 192: the counted slice waits across chunk boundaries), the register-streamed
-    kernel (bal = 4: a partial last 256-float phase at C = 96 / 100 / 260; V = 69.6k: 17
-    units in some workgroups, the last split over the helper waves' phases, one or two
-    phases) or one workgroup per tile (bal = 0)."""
+    GFEDNTM_CTX_FULL=1 forces it at small V): the register-streamed kernel (bit 15, rs = 1:
+    column ranges of 16-column units not aligned to the 64-column tiles, a partial last
+    256-float phase at C = 96 / 100 / 260; V = 69.6k: 17 units in some workgroups, the last
+    split over the helper waves' phases, one or two phases) or one workgroup per tile
+    (rs = 0)."""
+    from gfedntm_amd.ops.engine import STAGE_CTX_FULL, STAGE_CTX_RS
     monkeypatch.setenv("GFEDNTM_CTX_FULL", "1")
-    monkeypatch.setenv("GFEDNTM_CTX_BAL", bal)
+    monkeypatch.setenv("GFEDNTM_CTX_RS", rs)
+    from gfedntm_amd.models import CombinedTM
+    torch.manual_seed(0)
+    tm = CombinedTM(input_size=V, contextual_size=Cdim, n_components=20, hidden_sizes=(32, 24),
+                    batch_size=64, verbose=False, device="cuda", backend="fused")
+    sf = tm.engine._m.stage_flags
+    assert sf & STAGE_CTX_FULL and bool(sf & STAGE_CTX_RS) == (rs == "1")
     test_ctm_step_matches_oracle("combined", Cdim, V, 20, "prodLDA")
 
 
@@ -767,16 +734,13 @@ def test_ctm_v99k_step_matches_oracle():
     test_ctm_step_matches_oracle("combined", 768, 99000, 100, "prodLDA")
 
 
-@pytest.mark.parametrize("ctxpp", ["1", "0"])
 @pytest.mark.parametrize("Cdim,V", [(96, 600), (768, 9000)])
-def test_ctm_sparse_win_tiles_match_oracle(monkeypatch, Cdim, V, ctxpp):
+def test_ctm_sparse_win_tiles_match_oracle(monkeypatch, Cdim, V):
     """CombinedTM with the sparse W_in tiles (GFEDNTM_WIN_SPARSE=1 forces the large-V
     path): the bag-of-words half as entry-list tiles and the contextual half as dense
     A^T dz0 tiles of the same launch (csrc/update.hip win_tile_ctx) give the oracle's
-    input-layer gradient (both halves); ctxpp = 1: the contextual half by the persistent
-    kernel after the sparse launch (csrc/update.hip gfk_win_ctx_pp_k)."""
+    input-layer gradient (both halves)."""
     monkeypatch.setenv("GFEDNTM_WIN_SPARSE", "1")
-    monkeypatch.setenv("GFEDNTM_WIN_CTXPP", ctxpp)
     test_ctm_step_matches_oracle("combined", Cdim, V, 20, "prodLDA")
 
 

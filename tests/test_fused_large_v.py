@@ -9,8 +9,8 @@ large configurations:
 * ``prodlda_bwd_pipe_kernel`` (bwd_pre = 3: buffer-descriptor pipelined backward, Adam +
   the FedAvg pre-scale fused, beta row padding, dropped out-of-range rows / stores);
 * ``bwd_pre = 2`` at B = 32;
-* the sparse W_in tiles (STAGE_WIN_SPARSE) with the second moment in LDS (default) or in
-  registers (STAGE_WIN_VREG);
+* the sparse W_in tiles (STAGE_WIN_SPARSE; fused mode: the second moment in LDS, gradient
+  mode: in registers);
 * odd K and V % 64 != 0 (padding columns and a partial last vocabulary tile);
 * CombinedTM K = 100, C = 768, V = 74k (ctx_fwd full tiles, ctx_bwd Adam epilogue).
 
@@ -25,7 +25,7 @@ import torch
 
 from gfedntm_amd.data.bow import BatchPlan, DeviceCSR
 from gfedntm_amd.models import AVITM
-from gfedntm_amd.ops.engine import (STAGE_WIN_SPARSE, STAGE_WIN_VREG, UPDATE_FUSED, UPDATE_GRAD)
+from gfedntm_amd.ops.engine import STAGE_WIN_SPARSE, UPDATE_FUSED, UPDATE_GRAD
 from tests.helpers import random_csr
 
 pytestmark = pytest.mark.gpu
@@ -96,16 +96,14 @@ def _assert_beta_padding_zero(tm):
 @pytest.mark.parametrize("B,K,V,win", [
     (64, 200, 40000, "dense"),       # bwd_pre = 3, dense W_in tiles (the auto choice here)
     (64, 200, 112000, "auto"),       # the BASELINE large config: sparse W_in tiles (LDS v)
-    (64, 200, 40000, "vreg"),        # sparse W_in tiles, second moment in registers
     (32, 200, 40000, "sparse"),      # B = 32: bwd_pre = 2
     (64, 199, 40001, "sparse"),      # odd K, V % 64 != 0: padded rows, partial last tile
 ])
 def test_large_v_fused_matches_gradient_mode(monkeypatch, B, K, V, win):
     if win == "dense":
         monkeypatch.setenv("GFEDNTM_WIN_SPARSE", "0")
-    elif win in ("sparse", "vreg"):
+    elif win == "sparse":
         monkeypatch.setenv("GFEDNTM_WIN_SPARSE", "1")
-    monkeypatch.setenv("GFEDNTM_WIN_VL", "0" if win == "vreg" else "1")
     kw = dict(input_size=V, n_components=K, hidden_sizes=(50, 50), batch_size=B,
               verbose=False, device="cuda")
     a, b = _twins(AVITM, kw)
@@ -115,8 +113,6 @@ def test_large_v_fused_matches_gradient_mode(monkeypatch, B, K, V, win):
         assert m.bwd_pre == (3 if B == 64 else 2), m.bwd_pre
         sparse = bool(m.stage_flags & STAGE_WIN_SPARSE)
         assert sparse == (win != "dense"), win
-        if sparse:
-            assert bool(m.stage_flags & STAGE_WIN_VREG) == (win == "vreg")
     n_docs = 3 * B + 7
     X = random_csr(n_docs, V, 60, seed=2)
     data = DeviceCSR(X, "cuda")
@@ -128,21 +124,22 @@ def test_large_v_fused_matches_gradient_mode(monkeypatch, B, K, V, win):
     _assert_beta_padding_zero(b)
 
 
-@pytest.mark.parametrize("bal,V", [("3", 74000), ("4", 74000), ("4", 69600)])
-def test_ctm_large_v_fused_matches_gradient_mode(monkeypatch, bal, V):
+@pytest.mark.parametrize("rs,V", [("0", 74000), ("1", 74000), ("1", 69600)])
+def test_ctm_large_v_fused_matches_gradient_mode(monkeypatch, rs, V):
     """CombinedTM K = 100, C = 768, V = 74k (the BASELINE CTM class): ctx_fwd full tiles,
     Adam in ctx_bwd (adapt_bert) and win_update (both input-layer halves) vs gradient mode;
-    bal = 4: the register-streamed forward (18-19 units per workgroup on 256 CUs: waves with
-    two; V = 69.6k: 16-17, the 17th unit split by phase over three helper waves)."""
+    rs = 1: the register-streamed forward (18-19 units per workgroup on 256 CUs: waves with
+    two; V = 69.6k: 16-17, the 17th unit split by phase over three helper waves); rs = 0: one
+    workgroup per tile."""
     from gfedntm_amd.models import CombinedTM
     from gfedntm_amd.ops.engine import STAGE_CTX_FULL, STAGE_CTX_RS
-    monkeypatch.setenv("GFEDNTM_CTX_BAL", bal)
+    monkeypatch.setenv("GFEDNTM_CTX_RS", rs)
     K, Cdim, B = 100, 768, 64
     kw = dict(input_size=V, contextual_size=Cdim, n_components=K, hidden_sizes=(50, 50),
               batch_size=B, verbose=False, device="cuda")
     a, b = _twins(CombinedTM, kw)
     assert a.engine._m.ctx_fused == 1 and a.engine._m.stage_flags & STAGE_CTX_FULL
-    assert bool(a.engine._m.stage_flags & STAGE_CTX_RS) == (bal == "4")
+    assert bool(a.engine._m.stage_flags & STAGE_CTX_RS) == (rs == "1")
     n_docs = 2 * B + 5
     X = random_csr(n_docs, V, 60, seed=3)
     ctx = np.random.default_rng(4).standard_normal((n_docs, Cdim)).astype(np.float32)
@@ -154,29 +151,3 @@ def test_ctm_large_v_fused_matches_gradient_mode(monkeypatch, bal, V):
     fb = b.engine.view_like(b.engine.exp_avg, "inf_net.adapt_bert.weight")
     torch.testing.assert_close(fa, fb, rtol=1e-2, atol=1e-4 * (float(fb.abs().max()) + 1e-12))
     _assert_beta_padding_zero(a)
-
-
-@pytest.mark.parametrize("V", [9001, 12347])
-def test_ctm_win_ctxpp_fused_update_odd_vocab(monkeypatch, V):
-    """CombinedTM's contextual W_in half as the persistent kernel (GFEDNTM_WIN_CTXPP=1) in
-    the FUSED update mode at H0 = 50 and an odd vocabulary: a block's last quad of its
-    [words, H0] run is partial (odd word count x 50 floats), and its Adam update must use
-    the parameter / moments of the elements it stores (csrc/update.hip gfk_win_ctx_pp_k;
-    the clamped 128-bit load shifted them by 1-3 elements)."""
-    from gfedntm_amd.models import CombinedTM
-    from gfedntm_amd.ops.engine import STAGE_WIN_CTXPP
-    monkeypatch.setenv("GFEDNTM_WIN_SPARSE", "1")
-    monkeypatch.setenv("GFEDNTM_WIN_CTXPP", "1")
-    K, Cdim, B = 20, 64, 64
-    kw = dict(input_size=V, contextual_size=Cdim, n_components=K, hidden_sizes=(50, 50),
-              batch_size=B, verbose=False, device="cuda")
-    a, b = _twins(CombinedTM, kw)
-    for tm in (a, b):
-        assert tm.engine._m.stage_flags & STAGE_WIN_CTXPP, "expected the persistent Wc kernel"
-    n_docs = 2 * B + 5
-    X = random_csr(n_docs, V, 60, seed=5)
-    ctx = np.random.default_rng(6).standard_normal((n_docs, Cdim)).astype(np.float32)
-    data = DeviceCSR(X, "cuda", contextual=ctx)
-    plan = BatchPlan.build(n_docs, B, 4, seed=0)
-    _run((a, b), data, plan)
-    _compare(a, b, 4)
