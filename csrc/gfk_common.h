@@ -188,7 +188,7 @@ typedef struct GfkModel {
 
 // stage_flags bit 16 (GFK_FWD_POSTFOLD): the ProdLDA strip forward's ring variant computes
 // the batch-coupled posterior itself (csrc/prodlda.hip, FP) and post_fwd is not launched --
-// where it applies: strip ring forward (bit 2 + bit 8), K <= 64, B <= 64, no label head
+// where it applies: strip forward (bit 2), K <= 64, B <= 64, no label head
 constexpr int GFK_FWD_POSTFOLD = 65536;
 // stage_flags bit 19 (GFK_LB): the large-batch plan, 128 < bmax <= GFK_BMAX_LIMIT.  The
 // ProdLDA decoder's three products (logits = theta_d beta, dbeta = theta_d^T dlogit,
@@ -224,7 +224,7 @@ __host__ __device__ __forceinline__ int gfk_hlast(const GfkModel& m) {
   return h;
 }
 __host__ __device__ inline bool gfk_postfold(const GfkModel& m) {
-  return (m.stage_flags & GFK_FWD_POSTFOLD) && (m.stage_flags & 4) && !(m.stage_flags & 8) &&
+  return (m.stage_flags & GFK_FWD_POSTFOLD) && (m.stage_flags & 4) &&
          m.K <= 64 && m.bmax <= 64 && !m.lab_on && m.kind == GFK_PRODLDA;
 }
 

@@ -308,9 +308,7 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkArgT<GB> ga
 //  * the column batch-norm statistics are a reduction over the wave's own rows: register
 //    sums + two lane-group shuffles, no LDS, no barrier;
 //  * after theta_d is staged there is no barrier between the waves;
-//  * PF (stage_flags bit 3, the default): 8 waves of ~190 VGPRs (2 per SIMD), the next
-//    strip's beta block in flight while this one runs its MFMAs / batch norm / stores;
-//    PF = false: 16 waves of <= 128 VGPRs overlapping each other's loads instead.
+//  * the next strip's beta pairs in flight while this one runs its MFMAs (PF below).
 // k pairing: MFMA steps 2t and 2t + 1 take k = 8t + 2g and 8t + 2g + 1 for lane group
 // g = lane >> 4 (any bijection of k works if A and B agree), so a lane's two A operands
 // are one ds_read_b64, read one pair ahead of the MFMAs.  Strips s = tile * 4 + cs are
@@ -322,18 +320,19 @@ __global__ void __launch_bounds__(DEC_THREADS) prodlda_fwd_kernel(GfkArgT<GB> ga
 // global rounds overlap.  Measured (profiles/r2/ab_strip_forward.txt): K=50 headline
 // round 0.0589 -> 0.0583 ms, K=50 V=28k 0.101 -> 0.092, K=200 V=112k 0.349 -> 0.342.
 // NP: k pairs held in registers (compile-time, the launcher's smallest instance >= K / 8).
-// PF = 3 (stage_flags bit 8, the default): ROLLING prefetch at 16 waves of <= 128 VGPRs:
+// PF = 3 (the only variant since round 6): ROLLING prefetch at 16 waves of <= 128 VGPRs:
 // right after the MFMAs that consume a k pair of this strip's beta block, the next pair is
 // loaded into those registers, so each pair has many MFMAs of time to arrive, with no second
-// register block (PF = 1, the 8-wave variant the batched plan takes at large V, holds two:
-// 190 VGPRs, 2 waves per SIMD).  The pairs go through a RING of strip_ring(NP) <= 13
+// register block.  The pairs go through a RING of strip_ring(NP) <= 13
 // pairs instead of the whole strip's NP: pair t's registers receive pair t + R -- of this
 // strip while t + R < NP, else of the next one -- so a load still has R pairs of MFMAs
 // (x 4 waves per SIMD) to arrive, and K = 200 (25 pairs) fits 128 VGPRs: 16 waves per CU
 // instead of 12, and 7004 strips over 4096 waves (at most 2 each; 76 -> 85 % of the last
 // round's slots busy) instead of 3072 (at most 3).  (Round 6 removed the whole-strip rolling
-// variant PF = 2 and the non-prefetching PF = 0, both measured slower: profiles/r3, r4.)
-__host__ __device__ constexpr int strip_threads(int pf, int np) { return pf == 1 ? 512 : 1024; }
+// variant PF = 2 and the non-prefetching PF = 0, both measured slower: profiles/r3, r4; and
+// the 8-wave variant prefetching the whole next block, PF = 1 (190 VGPRs, 2 waves per SIMD),
+// the batched plan's large-V choice until then: profiles/r6/ab_strip_pf_vs_ring.txt.)
+__host__ __device__ constexpr int strip_threads(int pf, int np) { return 1024; }
 // The ring must divide NP: the next strip's pair p is written into the slot of pair
 // p + NP - R of this one, and read back from slot p % R.  (A 13-pair ring with NP = 25
 // -- K = 200 until round 4 -- shifted every later strip's beta pairs by one slot: wrong
@@ -377,7 +376,7 @@ __host__ __device__ constexpr int strip_ring(int pf, int np) {
 // 82-83 + decoder_network.py:102-118 + avitm.py:207-220).
 template <int BM, int NP, int PF, bool GB = false, bool BF = false, bool FP = false>
 __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kernel(GfkArgT<GB> ga) {
-  static_assert(PF == 1 || PF == 3, "strip variants: 8-wave prefetching (1), ring (3)");
+  static_assert(PF == 3, "strip variant: the ring (3)");
   static_assert(!BF || (PF == 3 && NP % 4 == 0), "bf16 strips: ring variant, whole 32-k steps");
   static_assert(!FP || (PF == 3 && NP == 8), "fused posterior: ring variant, K <= 64");
   const GfkModel& m = gfk_model(ga);
@@ -439,13 +438,11 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
     rm = m.beta_rm[vc];
     rv = m.beta_rv[vc];
   };
-  // software pipeline over the wave's strips: the NEXT strip's beta block is in flight
-  // while this one runs its MFMAs / batch norm / stores (2 waves per SIMD, ~190 VGPRs)
-  // PF = false: no prefetch, 16 waves per CU at <= 128 VGPRs (the waves overlap each
-  // other's loads instead)
+  // software pipeline over the wave's strips: the NEXT strip's first beta pairs are in
+  // flight while this one runs its last MFMAs / batch norm / stores
   constexpr int NR = strip_ring(PF, NP);       // pairs held in registers
   static_assert(NP % NR == 0, "the ring's slots must repeat whole strips");
-  float b[2 * NR], bn[2 * (PF == 1 ? NP : 1)], rm0 = 0.f, rv0 = 0.f, rmn = 0.f, rvn = 0.f;
+  float b[2 * NR], rm0 = 0.f, rv0 = 0.f, rmn = 0.f, rvn = 0.f;
   // wave group gq = wave >> 2 takes whole tiles gq * grid + g, + NW / 4 * grid, ...: the
   // 4 strips of a tile stay on one CU (their beta rows share cache lines), and the
   // tiles of the last, partial round are spread over every CU's wave group 0 instead
@@ -634,9 +631,7 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
   for (; s < nstrips; s += stride) {
     // PF = 3: the next strip's per-lane buffer offset (its pairs are loaded in the MFMA loop)
     int voffn = 0, v4n = LDB * 4;
-    if (PF == 1) {
-      issue(min(s + stride, nstrips - 1), bn, rmn, rvn);   // (the last one re-reads a strip)
-    } else {
+    {
       const int sn = min(s + stride, nstrips - 1);
       const int vcn = min((sn >> 2) * VB + 16 * (sn & 3) + (lane & 15), V - 1);
       asm volatile("" : "+s"(v4n));
@@ -762,14 +757,8 @@ __global__ void __launch_bounds__(strip_threads(PF, NP)) prodlda_fwd_strip_kerne
         if (i * 16 + e < lim) zt[row * VB + (col ^ zswz(row))] = z;
         rs_[i][e] += valid ? __expf(z) : 0.f;
       }
-    if (PF == 1) {
-#pragma unroll
-      for (int j = 0; j < 2 * NP; ++j) b[j] = bn[j];
-    }
-    if (PF != 0) {
-      rm0 = rmn;
-      rv0 = rvn;
-    }
+    rm0 = rmn;
+    rv0 = rvn;
 #ifdef GFK_STAMPS
     if (it_ < 2) STRIP_STAMP(4 + 2 * it_, false);
     ++it_;
@@ -1965,8 +1954,6 @@ prodlda_bwd_pipe_kernel(GfkArgT<GB> ga) {
 // stage_flags bit 2: the strip forward (prodlda_fwd_strip_kernel) -- theta_d + the
 // per-wave row partials only
 constexpr int FWD_STRIP = 4;
-constexpr int FWD_STRIP_PF = 8;   // bit 3: its prefetching 8-wave variant
-constexpr int FWD_STRIP_RING = 256; // bit 8: the rolling prefetch through a 13-pair ring (PF = 3)
 __host__ __device__ inline bool strip_postfold(const GfkModel& m) { return gfk_postfold(m); }
 __host__ __device__ inline int strip_pairs(int K) { return (K + 7) / 8; }
 // the kernel instance (k pairs in registers) for K
@@ -2396,8 +2383,7 @@ extern "C" int gfk_launch_prodlda_fwd(const GfkModel* m, hipStream_t s) {
     if (m->bmax > 64 || m->K > 256 || m->dec_grid > m->n_tiles ||
         (int64_t)m->K * m->ldb >= (1LL << 29)) return -1;
     const bool fp = strip_postfold(*m);
-    if (m->mm_bf16) {                   // bf16: the ring variant only
-      if (!(m->stage_flags & FWD_STRIP_RING)) return -1;
+    if (m->mm_bf16) {
       const int nb = strip_np_bf(m->K);
 #define GFK_FWSB(BM, NP)                                                                       \
       do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 3, true, true>), gfk_grid(g, m), dim3(strip_threads(3, NP)), sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 3, false, true>), g, dim3(strip_threads(3, NP)), sm, s, GfkArgT<false>{*m}); } while (0)
@@ -2418,8 +2404,6 @@ extern "C" int gfk_launch_prodlda_fwd(const GfkModel* m, hipStream_t s) {
     do {                                                                                       \
       if (NP == 8 && fp)                                                                       \
         do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, 8, 3, true, false, true>), gfk_grid(g, m), dim3(1024), sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, 8, 3, false, false, true>), g, dim3(1024), sm, s, GfkArgT<false>{*m}); } while (0); \
-      else if (m->stage_flags & FWD_STRIP_PF)                                                  \
-        do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 1, true>), gfk_grid(g, m), dim3(512), sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 1, false>), g, dim3(512), sm, s, GfkArgT<false>{*m}); } while (0); \
       else                                                                                     \
         do { if (m->n_batch > 1) hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 3, true>), gfk_grid(g, m), dim3(strip_threads(3, NP)), sm, s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((prodlda_fwd_strip_kernel<BM, NP, 3, false>), g, dim3(strip_threads(3, NP)), sm, s, GfkArgT<false>{*m}); } while (0); \
     } while (0)
@@ -2553,7 +2537,7 @@ extern "C" int gfk_prodlda_set_smem(size_t bytes) {
     (const void*)prodlda_fwd_strip_kernel<BM, 32, 3, false, true>, (const void*)prodlda_fwd_strip_kernel<BM, 32, 3, true, true>
 #define GFK_FWS_PTRSF(BM) (const void*)prodlda_fwd_strip_kernel<BM, 8, 3, false, false, true>, (const void*)prodlda_fwd_strip_kernel<BM, 8, 3, true, false, true>, \
     (const void*)prodlda_fwd_strip_kernel<BM, 8, 3, false, true, true>, (const void*)prodlda_fwd_strip_kernel<BM, 8, 3, true, true, true>
-#define GFK_FWS_PTRS(BM) GFK_FWS_PTRS1(BM, 1), GFK_FWS_PTRS1(BM, 3), GFK_FWS_PTRSB(BM), GFK_FWS_PTRSF(BM)
+#define GFK_FWS_PTRS(BM) GFK_FWS_PTRS1(BM, 3), GFK_FWS_PTRSB(BM), GFK_FWS_PTRSF(BM)
                       GFK_FWS_PTRS(16), GFK_FWS_PTRS(32), GFK_FWS_PTRS(64),
 #undef GFK_FWS_PTRS
 #undef GFK_FWS_PTRSF

@@ -56,10 +56,8 @@ VB = 64
 # of one dependent L2 round trip per pass
 STAGE_PLANS = (1, 0, 3, 2)
 STAGE_FWD_STRIP = 4               # bit 2: ProdLDA strip forward (csrc/prodlda.hip)
-STAGE_FWD_STRIP_PF = 8            # bit 3: its prefetching 8-wave variant
 STAGE_WIN_SPARSE = 16             # bit 4: sparse W_in tiles (csrc/update.hip win_tile_sparse)
 STAGE_CTX_FULL = 32               # bit 5: CombinedTM forward, one workgroup per tile (csrc/ctx.hip)
-STAGE_FWD_STRIP_RING = 256        # bit 8: the strip forward's ring-prefetch variant (PF = 3)
 STAGE_WIN_BATCH8 = 512            # bit 9: batched launches: win_update's 8-wave tile shape
 STAGE_CTX_BWDPP = 4096            # bit 12: CombinedTM backward, persistent pipelined shape (csrc/ctx.hip)
 STAGE_CTX_RS = 32768              # bit 15: CombinedTM forward, Wa register-streamed (csrc/ctx.hip)
@@ -67,8 +65,8 @@ STAGE_FWD_POSTFOLD = 65536        # bit 16: the strip forward computes post_fwd 
 STAGE_LB = 524288                 # bit 19: the large-batch plan (bmax 256 / 512, csrc/gfk_common.h)
 STAGE_POST_ROWS2 = 1048576        # bit 20: batched post_bwd, two rows per workgroup; its batch-level
                                   #         workgroup in row_bwd (csrc/posterior.hip)
-# (removed in round 6, measured not faster and the default nowhere: bit 6 the strip forward's
-# plain rolling prefetch, 7 the split W_in update, 10 the sparse tile's register second moment
+# (removed in round 6, measured not faster: bits 3 / 8 the strip forward's 8-wave whole-block
+# prefetch vs its ring (now the only variant), bit 6 the plain rolling prefetch, 7 the split W_in update, 10 the sparse tile's register second moment
 # as a knob, 11 / 13 the LDS-DMA balanced CombinedTM forwards, 14 the persistent Wc update,
 # 17 the moved batch-level workgroup on its own, 18 the one-range backward walking tiles)
 
@@ -527,21 +525,12 @@ class FusedEngine(EngineBase):
             fits = (m.bmax <= 64 and m.K <= 256 and m.K * m.ldb < (1 << 29))
             if fits and strip in ("1", "auto"):
                 m.stage_flags |= STAGE_FWD_STRIP
-                # the 8-wave variant that prefetches the next strip's beta block (2 waves
-                # per SIMD, ~190 VGPRs) measured ahead of 16 non-prefetching waves per CU
-                # (K=200: V=112k 0.341 vs 0.346 ms, V=74k 0.251 vs 0.260 ms; the tile
-                # kernel 0.346 / 0.255); GFEDNTM_FWD_STRIP_PF=0 selects the 16-wave one
-                # 3, the default since g26: the rolling prefetch (the next strip's k pair loaded
-                # into the registers its MFMAs just consumed) through a 13-pair ring (K > 104:
-                # 128 VGPRs, 16 waves per CU instead of 12; K = 200 V = 112k forward 39.7 ->
-                # 36.5 us, round 0.2794 -> 0.2751 ms).  Round 6 removed the plain rolling
-                # variant (2) and the non-prefetching one (0), both measured slower; "1" keeps
-                # the 8-wave prefetching variant the batched plan uses at large V
-                pf = "3" if m.mm_bf16 else os.environ.get("GFEDNTM_FWD_STRIP_PF", "3")
-                if pf == "1":
-                    m.stage_flags |= STAGE_FWD_STRIP_PF
-                else:
-                    m.stage_flags |= STAGE_FWD_STRIP_RING
+                # the rolling prefetch: the next strip's k pair loaded into the registers
+                # its MFMAs just consumed, through a ring of <= 13 pairs (K > 104: 128 VGPRs,
+                # 16 waves per CU; K = 200 V = 112k forward 39.7 -> 36.5 us, round 0.2794 ->
+                # 0.2751 ms).  Rounds 5-6 removed the other strip variants: the plain rolling
+                # one, the non-prefetching one and the 8-wave whole-block prefetch, measured
+                # slower (profiles/r3, r4, r6/ab_strip_pf_vs_ring.txt)
                 m.dec_grid = int(min(m.n_tiles, cu))
                 # the batch-coupled posterior (BN of the heads, reparameterisation, softmax,
                 # dropout, KL) inside the ring forward's theta_d staging: post_fwd is not
@@ -551,8 +540,7 @@ class FusedEngine(EngineBase):
                 # statistics lengthen the forward's critical path more than the launch they
                 # save (interleaved, one box: 0.0601 vs 0.0597 ms per round,
                 # profiles/r5/ab_fold.txt).  GFEDNTM_POSTFOLD=1 forces it here, =0 everywhere
-                self._fold_ok = bool(m.stage_flags & STAGE_FWD_STRIP_RING and m.K <= 64
-                                     and not m.lab_on)
+                self._fold_ok = bool(m.K <= 64 and not m.lab_on)
                 if self._fold_ok and os.environ.get("GFEDNTM_POSTFOLD", "auto") == "1":
                     m.stage_flags |= STAGE_FWD_POSTFOLD
             # backward: one workgroup per tile while the tiles fit the resident slots;
@@ -1556,43 +1544,21 @@ class BatchedSteps:
         for e in self.engines:
             mm = abi.GfkModel.from_buffer_copy(bytes(e._m))
             mm.dev, mm.dev_upd, mm.n_batch = self._arr_m.data_ptr(), self._arr_u.data_ptr(), M
-            # the strip forward: with M clients' tiles in one launch the 16-wave variant (one
-            # workgroup per CU) runs M dec_grid workgroups in rounds; the 8-wave prefetching
-            # variant fits two per CU (GFEDNTM_BATCH_STRIP_PF=0 keeps the engines' choice)
-            # GFEDNTM_BATCH_STRIP: "fill" -- every 16-wave workgroup of the ring variant takes
-            # 4 whole tiles (one strip per wave), so M clients' strips need M n_tiles / 4
-            # workgroups instead of M n_tiles with 12 of 16 waves idle (a single client's
-            # layout: one tile per CU, the fastest for ONE client); "pf" -- the 8-wave
-            # prefetching variant, two per CU (round 4); "keep" -- the engines' choice
-            # (fill only where it is one round: 16-wave ring workgroups are one per CU)
-            # (the strips are grid-strided: a workgroup's wave group g takes tiles g grid + x,
-            # so any grid works; "fill" takes the FEWEST tiles per workgroup, T in 1..4, whose
-            # M ceil(n_tiles / T) workgroups still fit one round of the CUs -- T = 3 at M = 8,
-            # V = 4.7k: 192 workgroups of 12 busy waves instead of 144 of 16; "fill4": T = 4)
-            bstrip = os.environ.get("GFEDNTM_BATCH_STRIP", "fill")
-            fill = -(-mm.n_tiles // 4)
-            if bstrip == "fill":
-                for t in (1, 2, 3, 4):
-                    if M * -(-mm.n_tiles // t) <= self._cu:
-                        fill = -(-mm.n_tiles // t)
-                        break
-            if (mm.stage_flags & STAGE_FWD_STRIP and M > 1 and bstrip in ("fill", "fill4")
-                    and mm.stage_flags & STAGE_FWD_STRIP_RING and mm.dec_grid == mm.n_tiles
-                    and M * fill <= self._cu):
-                mm.dec_grid = fill
-            elif (mm.stage_flags & STAGE_FWD_STRIP and M * mm.dec_grid > self._cu
-                    and bstrip != "keep" and (mm.mm_bf16 or bstrip == "ring")):
-                # bf16 GEMM operands exist only in the ring variant: keep it, M clients' grids
-                # sharing one round of the CUs (the strips are grid-strided, any grid works)
-                mm.dec_grid = max(1, self._cu // M)
-            elif (mm.stage_flags & STAGE_FWD_STRIP and M * mm.dec_grid > self._cu
-                    and bstrip != "keep"):
-                # (the prefetching variant has no folded posterior: post_fwd runs again)
-                mm.stage_flags = (mm.stage_flags & ~(STAGE_FWD_STRIP_RING
-                                                     | STAGE_FWD_POSTFOLD)) | STAGE_FWD_STRIP_PF
-            # the posterior folded into the ring forward for M > 1 clients (the engines' own
+            # the strip forward: M clients' tiles in one launch of 16-wave workgroups (one per
+            # CU).  The strips are grid-strided (a workgroup's wave group g takes tiles
+            # g grid + x, so any grid works): where M clients' one-tile-per-workgroup grids
+            # exceed one round of the CUs, each workgroup takes T whole tiles (one strip per
+            # wave), T the FEWEST in 1..4 whose M ceil(n_tiles / T) workgroups still fit one
+            # round -- T = 3 at M = 8, V = 4.7k: 192 workgroups of 12 busy waves instead of
+            # 144 of 16; past 4 tiles the M clients share one round (dec_grid = CUs / M).
+            # GFEDNTM_BATCH_STRIP=keep: the engines' own grids (rounds of the CUs).
+            if (mm.stage_flags & STAGE_FWD_STRIP and M > 1 and M * mm.dec_grid > self._cu
+                    and os.environ.get("GFEDNTM_BATCH_STRIP", "fill") != "keep"):
+                t = next((t for t in (1, 2, 3, 4) if M * -(-mm.n_tiles // t) <= self._cu), None)
+                mm.dec_grid = -(-mm.n_tiles // t) if t else max(1, self._cu // M)
+            # the posterior folded into the strip forward for M > 1 clients (the engines' own
             # plan keeps post_fwd for one client; GFEDNTM_POSTFOLD=0: never)
-            if (M > 1 and getattr(e, "_fold_ok", False) and mm.stage_flags & STAGE_FWD_STRIP_RING
+            if (M > 1 and getattr(e, "_fold_ok", False) and mm.stage_flags & STAGE_FWD_STRIP
                     and os.environ.get("GFEDNTM_POSTFOLD", "auto") != "0"):
                 mm.stage_flags |= STAGE_FWD_POSTFOLD
             # post_bwd: M clients x (bmax + 1) workgroups of 16 waves with the batch matrices

@@ -223,16 +223,16 @@ def test_batched_round_matches_branch_round(model_type):
         assert torch.equal(x.tm.flat.buffer, y.tm.flat.buffer)
 
 
-@pytest.mark.parametrize("strip", ["fill", "pf"])
+@pytest.mark.parametrize("strip", ["fill", "keep"])
 def test_batched_large_round_variants_match_branch_round(monkeypatch, strip):
     """8 clients at the headline's vocabulary (~74 tiles each): the batched launch switches
-    the strip forward to 3-4 tiles per 16-wave workgroup ("fill", the default; "pf": the
-    8-wave prefetching variant), post_bwd to two rows per workgroup with its batch-level
+    the strip forward to 3-4 tiles per 16-wave workgroup ("fill", the default; "keep": the
+    engines' one-tile-per-workgroup grids in rounds of the CUs), post_bwd to two rows per workgroup with its batch-level
     workgroup in row_bwd (bit 20), and win_update to its 8-wave tile shape (bit 9: all
     clients' tiles exceed two rounds of 16-wave workgroups), all in the fused update mode.
     The round must still agree with the per-client branch round within fp32 rounding."""
-    from gfedntm_amd.ops.engine import (STAGE_FWD_STRIP_PF, STAGE_FWD_STRIP_RING, STAGE_POST_ROWS2,
-                                        STAGE_WIN_BATCH8, UPDATE_FUSED)
+    from gfedntm_amd.ops.engine import (STAGE_FWD_STRIP, STAGE_POST_ROWS2, STAGE_WIN_BATCH8,
+                                        UPDATE_FUSED)
     monkeypatch.setenv("GFEDNTM_BATCH_STRIP", strip)
     sc = generate_synthetic(vocab_size=5000, n_topics=50, n_docs=1000, n_nodes=8, frozen_topics=5,
                             nwords=(150, 250), seed=13)
@@ -249,16 +249,15 @@ def test_batched_large_round_variants_match_branch_round(monkeypatch, strip):
     assert 8 * (host.n_tiles + 8) > 2 * cu and host.stage_flags & STAGE_WIN_BATCH8, host.n_tiles
     from gfedntm_amd.ops import kernel_abi as abi
     from gfedntm_amd.ops.engine import STAGE_FWD_POSTFOLD
+    # the strip forward with the posterior folded in (post_fwd not launched)
+    assert host.stage_flags & STAGE_FWD_STRIP
+    assert host.stage_flags & STAGE_FWD_POSTFOLD and abi.PH_POST_FWD not in a._batched._phases
     if strip == "fill":
-        # the ring forward with the posterior folded in (post_fwd not launched)
         # (the fewest tiles per workgroup whose 8 clients' workgroups fit one round)
         t = next(t for t in (1, 2, 3, 4) if 8 * -(-host.n_tiles // t) <= cu)
-        assert host.dec_grid == -(-host.n_tiles // t) and host.stage_flags & STAGE_FWD_STRIP_RING
-        assert host.stage_flags & STAGE_FWD_POSTFOLD and abi.PH_POST_FWD not in a._batched._phases
+        assert host.dec_grid == -(-host.n_tiles // t)
     else:
-        # the prefetching variant has no fold: post_fwd runs
-        assert 8 * host.dec_grid > cu and host.stage_flags & STAGE_FWD_STRIP_PF
-        assert not host.stage_flags & STAGE_FWD_POSTFOLD and abi.PH_POST_FWD in a._batched._phases
+        assert host.dec_grid == host.n_tiles and 8 * host.dec_grid > cu
     assert host.stage_flags & STAGE_POST_ROWS2 and host.n_dpart == host.n_tiles
     assert all(c.tm.engine.update_mode == UPDATE_FUSED for c in a.clients)
     lr = a.clients[0].tm.engine.lr
@@ -320,11 +319,11 @@ def test_engine_step_k_is_bitwise_k_steps():
 
 
 def test_batched_bf16_large_vocab_keeps_ring_forward():
-    """bf16 GEMM operands live only in the ring strip forward: with more clients' grids than
-    the CUs hold (V > 64 x CUs) the batched plan keeps the ring variant on a shared grid
-    instead of switching to the fp32-only prefetching one (round 5's launcher refused it:
-    CombinedTM K=100 V=99k bf16, 8 clients).  Agrees with the per-client branch round."""
-    from gfedntm_amd.ops.engine import STAGE_FWD_STRIP_PF, STAGE_FWD_STRIP_RING
+    """bf16 strip forward at a vocabulary past 4 tiles per workgroup (V > 64 x CUs): the
+    batched plan shares one round of the CUs between the clients' grids (round 5 switched to
+    an fp32-only variant here, which the launcher refused: CombinedTM K=100 V=99k bf16, 8
+    clients).  Agrees with the per-client branch round."""
+    from gfedntm_amd.ops.engine import STAGE_FWD_STRIP
     sc = generate_synthetic(vocab_size=60000, n_topics=20, n_docs=1200, n_nodes=2, frozen_topics=2,
                             nwords=(150, 250), seed=17)
     corpora = [ClientCorpus(synthetic=sc, node=i) for i in range(2)]
@@ -337,7 +336,7 @@ def test_batched_bf16_large_vocab_keeps_ring_forward():
     host = a._batched._host
     cu = torch.cuda.get_device_properties(0).multi_processor_count
     assert host.n_tiles > cu and host.mm_bf16
-    assert host.stage_flags & STAGE_FWD_STRIP_RING and not host.stage_flags & STAGE_FWD_STRIP_PF
+    assert host.stage_flags & STAGE_FWD_STRIP
     assert 2 * host.dec_grid <= cu
     for x, y in zip(a.clients, b.clients):
         assert torch.isfinite(x.tm.flat.buffer).all()

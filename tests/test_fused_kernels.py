@@ -93,20 +93,15 @@ def test_step_matches_oracle(model_type, B, n_docs, K, H, V):
                                             (64, 80, 204, (50,), 80000),      # NP = 26, ring 13
                                             (64, 80, 120, (50,), 80000),      # NP = 16, ring 8
                                             (64, 80, 250, (50,), 80000)])     # NP = 32, ring 8
-@pytest.mark.parametrize("pf", ["1", "3"])
-def test_strip_forward_matches_oracle(monkeypatch, pf, B, n_docs, K, H, V):
+def test_strip_forward_matches_oracle(monkeypatch, B, n_docs, K, H, V):
     """prodlda_fwd_strip_kernel (GFEDNTM_FWD_STRIP=1 forces it): per-wave column strips,
-    beta by buffer loads straight into the MFMA B registers, k paired for ds_read_b64;
-    pf = 1 the 8-wave variant prefetching the next strip's beta block (bit 3), pf = 3 a
-    13-pair ring (bit 8; more than 13 pairs: the current strip's later pairs, then the
-    next's)."""
+    beta by buffer loads straight into the MFMA B registers, k paired for ds_read_b64,
+    the next pairs through a <= 13-pair ring (more than 13 pairs: the current strip's
+    later pairs, then the next's)."""
     monkeypatch.setenv("GFEDNTM_FWD_STRIP", "1")
-    monkeypatch.setenv("GFEDNTM_FWD_STRIP_PF", pf)
-    from gfedntm_amd.ops.engine import STAGE_FWD_STRIP, STAGE_FWD_STRIP_PF, STAGE_FWD_STRIP_RING
+    from gfedntm_amd.ops.engine import STAGE_FWD_STRIP
     fused, _ = _pair("prodLDA", V=V, K=K, H=H, B=B)
-    sf = fused.engine._m.stage_flags
-    assert sf & STAGE_FWD_STRIP
-    assert bool(sf & STAGE_FWD_STRIP_PF) == (pf == "1") and bool(sf & STAGE_FWD_STRIP_RING) == (pf == "3")
+    assert fused.engine._m.stage_flags & STAGE_FWD_STRIP
     _oracle_step("prodLDA", B, n_docs, K, H, V)
 
 

@@ -4,7 +4,7 @@
 # run prints one line: variant, repetition, ms_per_step, device_ms_per_step, final_loss.
 # usage: tools/ab_env.sh <out_dir> <reps> "<bench args>" "NAME=ENV1=v1,ENV2=v2" "NAME2=..." ...
 #   e.g. tools/ab_env.sh gpurun_out/ab1 2 "--steps 1000 --warmup 100 --no-npmi" \
-#          "fill=GFEDNTM_BATCH_STRIP=fill" "pf=GFEDNTM_BATCH_STRIP=pf"
+#          "fill=GFEDNTM_BATCH_STRIP=fill" "keep=GFEDNTM_BATCH_STRIP=keep"
 # Every bench run has its own time limit; a failing run stops the script.
 set -o pipefail
 out="$1"; reps="$2"; args="$3"; shift 3
