@@ -1565,16 +1565,14 @@ class BatchedSteps:
             # in LDS (~93 KB: one per CU) run in three rounds at M = 8.  Two rows per
             # workgroup (the matrices, weights and column sums staged once for both) and the
             # batch-level workgroup moved into row_bwd: M bmax / 2 workgroups, one round
-            # (GFEDNTM_BATCH_POST=0: off).  (Round 6 removed the opt-in variants measured
-            # slower: the matrices read from L2, and the persistent one-range backward
-            # walking several tiles -- profiles/r5/ab_batch.txt.)
-            if (M > 1 and M * (mm.bmax + 1) > self._cu
-                    and os.environ.get("GFEDNTM_BATCH_POST", "rows2") != "0"):
+            # (M (bmax + 1) <= CUs: the one-row shape).  Round 6 removed the opt-in variants
+            # measured slower: the matrices read from L2, and the persistent one-range
+            # backward walking several tiles (profiles/r5/ab_batch.txt).
+            if M > 1 and M * (mm.bmax + 1) > self._cu:
                 mm.stage_flags |= STAGE_POST_ROWS2
             # win_update: all clients' W_in tiles in one launch -> the 8-wave tile shape once
-            # they exceed two rounds of 16-wave workgroups (GFEDNTM_BATCH_WIN8=0: off)
-            if (M * (mm.n_tiles + 8) > 2 * self._cu
-                    and os.environ.get("GFEDNTM_BATCH_WIN8", "1") != "0"):
+            # they exceed two rounds of 16-wave workgroups
+            if M * (mm.n_tiles + 8) > 2 * self._cu:
                 mm.stage_flags |= STAGE_WIN_BATCH8
             ms.append(bytes(mm))
             us.append(bytes(e._u))
