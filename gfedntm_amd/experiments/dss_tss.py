@@ -226,6 +226,9 @@ def _federated(cfg, sc, train, inf_counts, inf_thetas, device, seed, rounds=None
     fed = LocalFederation(corpora, params, max_iters=rounds, device=device,
                           backend=cfg["backend"], seed=seed, agg=agg, fedavg_wire=wire)
     fed.run()
+    logging.getLogger("gfedntm_amd.dss_tss").info(
+        "  federated round: %s, FedAvg %s", "batched launches" if fed._batched is not None
+        else "per-client steps", fed.fold_plan or fed.agg.__class__.__name__)
     tm = fed.clients[0].tm                     # every client holds the averaged state
     id2token = dict(enumerate(fed.terms))
     return _score(tm, id2token, fed.vocab, cfg, inf_counts, sc.topic_vectors, inf_thetas)

@@ -640,8 +640,11 @@ class FusedEngine(EngineBase):
         m = self._m
         # W_in's gradient: the sparse entry-list tiles where a 64-word tile holds few of the
         # batch's non-zeros (more tiles than 4 rounds of the CUs, as for small batches), else
-        # the dense tiles in 128-row chunks (csrc/update.hip win_tile_dense_ch)
-        m.stage_flags = 2 | STAGE_LB | (STAGE_WIN_SPARSE if m.n_tiles > 4 * cu else 0)
+        # the dense tiles in 128-row chunks (csrc/update.hip win_tile_dense_ch);
+        # GFEDNTM_WIN_SPARSE=1 / 0 forces either
+        ws_env = os.environ.get("GFEDNTM_WIN_SPARSE", "auto")
+        sparse = ws_env == "1" or (ws_env == "auto" and m.n_tiles > 4 * cu)
+        m.stage_flags = 2 | STAGE_LB | (STAGE_WIN_SPARSE if sparse else 0)
         m.dec_grid = int(min(m.n_tiles, 2 * cu))
         m.n_dpart = 1
         m.bwd_pre = 0
