@@ -54,6 +54,8 @@ typedef struct GfkModel {
   float drop_enc, drop_theta;
   float bn_momentum, bn_eps;
   float kl_weight;       // CTM loss_weights["beta"], 1 for AVITM
+  int32_t lb_fused;      // the large-batch plan's decoder on the matrix cores: bit 0 forward,
+                         //   bit 1 backward (csrc/prodlda.hip prodlda_lb_fwd / _bwd)
   uint64_t seed;
 
   // ---- parameters (views into the flat fp32 buffer) and their gradients ----

@@ -1059,6 +1059,352 @@ __global__ void __launch_bounds__(LB_THREADS) prodlda_lb_dlogit_kernel(GfkArgT<G
   }
 }
 
+// Large batches on the matrix cores (GfkModel.lb_fused; round 6).  The library GEMMs above
+// read and write the whole [bmax][ldb] logit matrix and run the skinny products (K = 50 inner
+// or outer dimension) on tiles built for square ones; these two kernels keep each 64-column
+// tile's work inside one workgroup (16 waves, persistent over the tiles, one per CU):
+//  * prodlda_lb_fwd (bit 0, bmax 256 / 512, K <= 256): the logits of the tile on the fp32
+//    matrix cores -- A = theta_d rows straight from L2 (one float per lane per 4-k step),
+//    B = beta through a buffer resource of K rows (rows >= K and columns past ldb read 0),
+//    both one chunk of 4 k steps ahead of the MFMAs -- in accumulators (wave w: row tiles
+//    w + 16 j x the tile's 4 column strips); then prodlda_lb_colbn's work on the registers:
+//    column statistics (the wave's rows + two lane shuffles, the 16 waves through LDS in a
+//    fixed order), running statistics / rstd, the BN'ed tile into ws_zn, the per-row sum-exp
+//    partials (slot 0 of the workgroup's 4).
+//  * prodlda_lb_bwd (bit 1, bmax 256, K <= 256, gradient mode): prodlda_lb_dlogit's logit
+//    gradient into LDS (D [256][68]), beta's tile by LDS-DMA (Bt [16 KT][68], rows >= K zero),
+//    then dbeta[k][c] = sum_b theta_d[b][k] D[b][c] (subtiles (k tile, column strip) over the
+//    waves, theta_d from L2) into beta's gradient slot, and d theta_d[b][k] += sum_c D[b][c]
+//    beta[k][c] (wave w: row tile w x every k tile, accumulated in registers over the
+//    workgroup's tiles; one slab per workgroup, n_dpart = the grid, summed by row_bwd).
+// Reference: decoder_network.py:121-126 (ProdLDA decoder), avitm.py:84-85 (any batch_size).
+constexpr int LBB_LD = 68;                   // LDS row stride of D / Bt (conflict-free A reads)
+template <int BM>
+__global__ void __launch_bounds__(LB_THREADS) prodlda_lb_fwd_kernel(GfkArgT<false> ga) {
+  const GfkModel& m = gfk_model(ga);
+  constexpr int RTW = BM / 256;              // row tiles per wave
+  constexpr int LBF_KC = BM == 256 ? 4 : 2;  // 4-k MFMA steps per prefetched chunk
+  __shared__ float red[2][16][VB];
+  const int tid = threadIdx.x, lane = tid & 63, w = uniform(tid >> 6);
+  const int r16 = lane & 15, g = lane >> 4;
+  const int K = m.K, V = m.V, ldb = m.ldb, kt = m.kt, nb = *m.ws_nb;
+  const float inv_nb = 1.f / (float)nb;
+  const int nch = (K + 4 * LBF_KC - 1) / (4 * LBF_KC);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)m.beta, 0, K * ldb * 4, 0x00020000);
+  if (gfk_bx() == 0 && tid == 0) *m.nbt_beta += 1;
+  const float* tha[RTW];
+#pragma unroll
+  for (int j = 0; j < RTW; ++j) tha[j] = m.ws_thetad + (size_t)(16 * (w + 16 * j) + r16) * kt;
+  float rs[RTW][4];
+#pragma unroll
+  for (int j = 0; j < RTW; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) rs[j][e] = 0.f;
+#pragma unroll 1
+  for (int tile = gfk_bx(); tile < m.n_tiles; tile += gridDim.x) {
+    const int c0 = tile * VB;
+    int cb[4];
+#pragma unroll
+    for (int cs = 0; cs < 4; ++cs) {
+      const int c = c0 + 16 * cs + r16;
+      cb[cs] = c < ldb ? c * 4 : 0x7FFF0000;
+    }
+    float rm0[4], rv0[4];
+    if (w == 0) {
+#pragma unroll
+      for (int cs = 0; cs < 4; ++cs) {
+        const int vc = min(c0 + 16 * cs + r16, V - 1);
+        rm0[cs] = m.beta_rm[vc];
+        rv0[cs] = m.beta_rv[vc];
+      }
+    }
+    f32x4 acc[RTW][4];
+#pragma unroll
+    for (int j = 0; j < RTW; ++j)
+#pragma unroll
+      for (int cs = 0; cs < 4; ++cs) acc[j][cs] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // A[i][kk] = theta_d[row0 + i][k0 + kk], B[kk][jj] = beta[k0 + kk][col0 + jj]
+    auto load = [&](int ch, float (&a)[LBF_KC][RTW], float (&b)[LBF_KC][4]) {
+#pragma unroll
+      for (int q = 0; q < LBF_KC; ++q) {
+        const int k = 4 * (ch * LBF_KC + q) + g, kc = min(k, K - 1);
+#pragma unroll
+        for (int j = 0; j < RTW; ++j) a[q][j] = tha[j][kc];
+        const int ko = k * ldb * 4;
+#pragma unroll
+        for (int cs = 0; cs < 4; ++cs)
+          b[q][cs] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rb, boff(cb[cs], ko), 0, 0));
+      }
+    };
+    auto mma = [&](const float (&a)[LBF_KC][RTW], const float (&b)[LBF_KC][4]) {
+#pragma unroll
+      for (int q = 0; q < LBF_KC; ++q)
+#pragma unroll
+        for (int j = 0; j < RTW; ++j)
+#pragma unroll
+          for (int cs = 0; cs < 4; ++cs) acc[j][cs] = mfma16x16x4(a[q][j], b[q][cs], acc[j][cs]);
+    };
+    float a0[LBF_KC][RTW], b0[LBF_KC][4], a1[LBF_KC][RTW], b1[LBF_KC][4];
+    load(0, a0, b0);
+#pragma unroll 1
+    for (int ch = 0; ch < nch; ch += 2) {    // (chunks past K load zeros for beta)
+      load(ch + 1, a1, b1);
+      mma(a0, b0);
+      load(ch + 2, a0, b0);
+      mma(a1, b1);
+    }
+    // ---- column statistics over the batch rows (rows >= nb excluded), two-pass variance ----
+    float mean[4], rstd[4], sv[4];
+#pragma unroll
+    for (int cs = 0; cs < 4; ++cs) {
+      float v = 0.f;
+#pragma unroll
+      for (int j = 0; j < RTW; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v += 16 * (w + 16 * j) + 4 * g + e < nb ? acc[j][cs][e] : 0.f;
+      v += __shfl_xor(v, 16);
+      sv[cs] = v + __shfl_xor(v, 32);
+    }
+    if (g == 0) {
+#pragma unroll
+      for (int cs = 0; cs < 4; ++cs) red[0][w][16 * cs + r16] = sv[cs];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int cs = 0; cs < 4; ++cs) {
+      float mu = 0.f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) mu += red[0][q][16 * cs + r16];
+      mean[cs] = mu * inv_nb;
+      float v = 0.f;
+#pragma unroll
+      for (int j = 0; j < RTW; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = acc[j][cs][e] - mean[cs];
+          v += 16 * (w + 16 * j) + 4 * g + e < nb ? d * d : 0.f;
+        }
+      v += __shfl_xor(v, 16);
+      sv[cs] = v + __shfl_xor(v, 32);
+    }
+    if (g == 0) {
+#pragma unroll
+      for (int cs = 0; cs < 4; ++cs) red[1][w][16 * cs + r16] = sv[cs];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int cs = 0; cs < 4; ++cs) {
+      float var = 0.f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) var += red[1][q][16 * cs + r16];
+      var *= inv_nb;
+      rstd[cs] = rsqrtf(var + m.bn_eps);
+      const int v = c0 + 16 * cs + r16;
+      if (w == 0 && g == 0 && v < V) {
+        const float mom = m.bn_momentum;
+        const float unb = nb > 1 ? var * (float)nb / (float)(nb - 1) : var;
+        float nm = (1.f - mom) * rm0[cs] + mom * mean[cs], nv = (1.f - mom) * rv0[cs] + mom * unb;
+        if (m.fed_scale_on && is_shared(m, m.beta_rm)) { nm *= m.fed_scale; nv *= m.fed_scale; }
+        m.beta_rm[v] = nm;
+        m.beta_rv[v] = nv;
+        m.ws_col_rstd[v] = rstd[cs];
+      }
+    }
+    // ---- the BN'ed tile into ws_zn (row_loss's layout), the rows' sum-exp ----
+    const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(m.ws_zn + (size_t)tile * BM * VB), 0, BM * VB * 4, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < RTW; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = 16 * (w + 16 * j) + 4 * g + e;
+#pragma unroll
+        for (int cs = 0; cs < 4; ++cs) {
+          const int col = 16 * cs + r16;
+          const float z = (acc[j][cs][e] - mean[cs]) * rstd[cs];
+          const int zo = row < nb ? (row * VB + (col ^ zswz(row))) * 4 : 0x7FFF0000;
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(z), rz, zo, 0, 0);
+          rs[j][e] += (row < nb && c0 + col < V) ? __expf(z) : 0.f;
+        }
+      }
+    // (red[0] is rewritten next tile only after every wave passed the second barrier, which
+    // follows its reads; red[1]'s reads precede the next tile's first barrier)
+  }
+  float* part = m.ws_row_part + (size_t)gfk_bx() * 4 * m.bmax * 2;
+#pragma unroll
+  for (int j = 0; j < RTW; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float se = row16_sum(rs[j][e]);
+      const int row = 16 * (w + 16 * j) + 4 * g + e;
+      if (r16 < 4 && row < nb) {
+        float* p = part + ((size_t)r16 * m.bmax + row) * 2;
+        p[0] = 0.f;                     // (max, sum-exp) with max 0: |z| <= sqrt(nb - 1)
+        p[1] = r16 == 0 ? se : 0.f;
+      }
+    }
+}
+
+__host__ __device__ inline int lb_bwd_lds_floats(int K) { return (256 + 16 * ((K + 15) / 16)) * LBB_LD; }
+
+template <int KTM>
+__global__ void __launch_bounds__(LB_THREADS) prodlda_lb_bwd_kernel(GfkArgT<false> ga) {
+  constexpr int BM = 256, NR = BM / 16;
+  constexpr int RB = KTM >= 16 ? 4 : 8;      // rows per sparse-entry round (registers)
+  constexpr int AV = KTM >= 16 ? 8 : 16;     // theta_d operands in flight per dbeta chunk
+  const GfkModel& m = gfk_model(ga);
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* D = smem;                           // [BM][LBB_LD] the logit gradient
+  float* Bt = D + BM * LBB_LD;               // [16 KT][LBB_LD] beta's tile (rows >= K: 0)
+  __shared__ float red[2][16][VB];
+  __shared__ float sx[16][VB];               // per wave: the current row's sparse x by column
+  const int tid = threadIdx.x, lane = tid & 63, w = uniform(tid >> 6);
+  const int r16 = lane & 15, g = lane >> 4;
+  const int K = m.K, V = m.V, ldb = m.ldb, kt = m.kt, nb = *m.ws_nb, ntp = m.n_tiles + 1;
+  const int KT = (K + 15) / 16;
+  const float inv_nb = 1.f / (float)nb;
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)m.beta, 0, K * ldb * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rgr = __builtin_amdgcn_make_buffer_rsrc((void*)(m.beta + m.off_g), 0, K * ldb * 4, 0x00020000);
+  const int zc = (lane ^ zswz(w)) * 4;       // (zswz(w + 16 i) == zswz(w))
+  sx[w][lane] = 0.f;
+  f32x4 dacc[KTM];                           // d theta_d [row tile w][k tile]
+#pragma unroll
+  for (int q = 0; q < KTM; ++q) dacc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int tile = gfk_bx(); tile < m.n_tiles; tile += gridDim.x) {
+    const int c0 = tile * VB, v = c0 + lane;
+    const bool valid = v < V;
+    // beta's tile -> Bt by LDS-DMA: wave w copies rows w + 16 u (64 columns each)
+    {
+      const int vb = v < ldb ? v * 4 : 0x7FFF0000;
+#pragma unroll
+      for (int u = 0; u < KTM; ++u) {
+        const int k = w + 16 * u;
+        if (u < KT)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void_ptr)(Bt + k * LBB_LD), 4, boff(vb, k * ldb * 4), 0, 0, 0);
+      }
+    }
+    const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(m.ws_zn + (size_t)tile * BM * VB), 0, BM * VB * 4, 0x00020000);
+    const float rsd = m.ws_col_rstd[min(v, V - 1)];
+    int ex0 = 0, ex1 = 0;                    // lane i: row w + 16 i's extent in this tile
+    if (lane < NR && w + 16 * lane < nb) {
+      const int32_t* ts = m.ws_tstart + (size_t)(w + 16 * lane) * ntp + tile;
+      ex0 = ts[0];
+      ex1 = ts[1];
+    }
+    // ---- the logit gradient (prodlda_lb_dlogit): d = p S - x p / (p + eps), then the
+    //      column BN backward; d parked in D, z kept in registers ----
+    float z[NR], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i0 = 0; i0 < NR; i0 += RB) {
+      int ci[RB];
+      float xi[RB];
+#pragma unroll
+      for (int i = 0; i < RB; ++i) {
+        const int e0 = __builtin_amdgcn_readlane(ex0, i0 + i), n = __builtin_amdgcn_readlane(ex1, i0 + i) - e0;
+        ci[i] = -1;
+        xi[i] = 0.f;
+        if (lane < n) {
+          ci[i] = m.indices[e0 + lane] - c0;
+          xi[i] = m.values[e0 + lane];
+        }
+        z[i0 + i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rz, zc, (w + 16 * (i0 + i)) * VB * 4, 0));
+      }
+#pragma unroll
+      for (int i = 0; i < RB; ++i) {
+        const int r = w + 16 * (i0 + i);
+        float d = 0.f;
+        if (r < nb) {                        // (wave-uniform)
+          const float p = __expf(z[i0 + i] - m.ws_lse[r]);
+          if (ci[i] >= 0) sx[w][ci[i]] = xi[i];
+          const float xs = sx[w][lane];
+          sx[w][lane] = 0.f;
+          const float dd = p * m.ws_s[r] - xs * p / (p + RL_EPS);
+          d = valid ? dd : 0.f;
+          s1 += d;
+          s2 += d * z[i0 + i];
+        } else {
+          z[i0 + i] = 0.f;
+        }
+        D[r * LBB_LD + lane] = d;
+      }
+    }
+    red[0][w][lane] = s1;
+    red[1][w][lane] = s2;
+    vm_barrier();                            // (+ beta's tile in LDS)
+    float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      a1 += red[0][q][lane];
+      a2 += red[1][q][lane];
+    }
+    a1 *= inv_nb;
+    a2 *= inv_nb;
+    const float rr = valid ? rsd : 0.f;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int r = w + 16 * i;
+      float* dp = D + r * LBB_LD + lane;
+      *dp = r < nb ? rr * (*dp - a1 - z[i] * a2) : 0.f;
+    }
+    lds_barrier();
+    // ---- dbeta[k][c] = sum_b theta_d[b][k] D[b][c] -> beta's gradient slot ----
+    // (A[i][kk] = theta_d[b0 + kk][k0 + i], B[kk][jj] = D[b0 + kk][c0' + jj])
+#pragma unroll 1
+    for (int sidx = w; sidx < 4 * KT; sidx += 16) {
+      const int ktile = sidx >> 2, cs = sidx & 3;
+      const float* ta = m.ws_thetad + min(16 * ktile + r16, K - 1);
+      const float* db = D + 16 * cs + r16;
+      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+      for (int b0 = 0; b0 < BM; b0 += 4 * AV) {
+        float av[AV];
+#pragma unroll
+        for (int q = 0; q < AV; ++q) av[q] = ta[(size_t)(b0 + 4 * q + g) * kt];
+#pragma unroll
+        for (int q = 0; q < AV; q += 2) {
+          acc0 = mfma16x16x4(av[q], db[(b0 + 4 * q + g) * LBB_LD], acc0);
+          acc1 = mfma16x16x4(av[q + 1], db[(b0 + 4 * q + 4 + g) * LBB_LD], acc1);
+        }
+      }
+      const int c = c0 + 16 * cs + r16;
+      const int vo = c < ldb ? c * 4 : 0x7FFF0000;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = 16 * ktile + 4 * g + e;
+        if (k < K)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc0[e] + acc1[e]), rgr, boff(vo, k * ldb * 4), 0, 0);
+      }
+    }
+    // ---- d theta_d[b][k] += sum_c D[b][c] beta[k][c]: row tile w x every k tile ----
+    // (A[i][kk] = D[16 w + i][c + kk], B[kk][jj] = beta[16 kt + jj][c + kk])
+    {
+      const float* da = D + (16 * w + r16) * LBB_LD + g;
+      const float* bb = Bt + r16 * LBB_LD + g;
+#pragma unroll
+      for (int c = 0; c < VB; c += 4) {
+        const float a = da[c];
+#pragma unroll
+        for (int q = 0; q < KTM; ++q)
+          if (q < KT) dacc[q] = mfma16x16x4(a, bb[q * 16 * LBB_LD + c], dacc[q]);
+      }
+    }
+    __syncthreads();                         // D / Bt / red / sx are rewritten by the next tile
+  }
+  // ---- this workgroup's d theta_d partial (slab gfk_bx(); row_bwd sums the slabs in order) ----
+  float* dpart = m.ws_dthetad + (size_t)gfk_bx() * m.bmax * K;
+#pragma unroll
+  for (int q = 0; q < KTM; ++q) {
+    const int k = 16 * q + r16;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = 16 * w + 4 * g + e;
+      if (q < KT && k < K && row < nb) dpart[(size_t)row * K + k] = dacc[q][e];
+    }
+  }
+}
+
 // Backward.  Two launch shapes of one kernel:
 //  * KQ = 1 (every vocab tile has its own workgroup of 16 waves -- the K=50 headline --
 //    or K <= 48): workgroup g owns tiles g, g + grid, ...;
@@ -2355,13 +2701,31 @@ static size_t bwd_smem(const GfkModel* m, int kq) {
 
 // the LDS of the launch shape this model uses (the k-range split when it applies)
 extern "C" size_t gfk_prodlda_bwd_smem(const GfkModel* m) {
-  return (m->stage_flags & GFK_LB) ? 0 : bwd_smem(m, bwd_kq(*m));
+  if (m->stage_flags & GFK_LB)
+    return (m->lb_fused & 2) ? sizeof(float) * lb_bwd_lds_floats(m->K) : 0;
+  return bwd_smem(m, bwd_kq(*m));
 }
 
 // the large-batch kernels (stage_flags GFK_LB): bmax 256 or 512, ws_dt the [bmax][ldb] matrix
 #define GFK_LB_LAUNCH(KERN, BM)                                                                      do { if (m->n_batch > 1) hipLaunchKernelGGL((KERN<BM, true>), gfk_grid(dim3(m->dec_grid), m), dim3(LB_THREADS), 0, s, GfkArgT<true>{gfk_dev(m)});        else hipLaunchKernelGGL((KERN<BM, false>), dim3(m->dec_grid), dim3(LB_THREADS), 0, s, GfkArgT<false>{*m}); } while (0)
 static int launch_lb(const GfkModel* m, hipStream_t s, bool fwd) {
-  if ((m->bmax != 256 && m->bmax != 512) || m->dec_grid < 1 || !m->ws_dt || m->ldb < m->V) return -1;
+  if ((m->bmax != 256 && m->bmax != 512) || m->dec_grid < 1 || m->ldb < m->V || m->n_batch > 1) return -1;
+  if ((int64_t)(m->K + 16) * m->ldb * 4 >= 0x7FFF0000LL) return -1;     // 32-bit buffer offsets
+  if (fwd && (m->lb_fused & 1)) {
+    if (m->bmax != 256 || m->K > 256 || m->kind != GFK_PRODLDA) return -1;
+    hipLaunchKernelGGL((prodlda_lb_fwd_kernel<256>), dim3(m->dec_grid), dim3(LB_THREADS), 0, s, GfkArgT<false>{*m});
+    return (int)hipGetLastError();
+  }
+  if (!fwd && (m->lb_fused & 2)) {
+    if (m->bmax != 256 || m->K > 256 || m->update_mode != 0 || m->n_dpart != m->dec_grid) return -1;
+    const size_t sm = sizeof(float) * lb_bwd_lds_floats(m->K);
+    if (m->K <= 64) hipLaunchKernelGGL((prodlda_lb_bwd_kernel<4>), dim3(m->dec_grid), dim3(LB_THREADS), sm, s, GfkArgT<false>{*m});
+    else if (m->K <= 128) hipLaunchKernelGGL((prodlda_lb_bwd_kernel<8>), dim3(m->dec_grid), dim3(LB_THREADS), sm, s, GfkArgT<false>{*m});
+    else if (m->K <= 208) hipLaunchKernelGGL((prodlda_lb_bwd_kernel<13>), dim3(m->dec_grid), dim3(LB_THREADS), sm, s, GfkArgT<false>{*m});
+    else hipLaunchKernelGGL((prodlda_lb_bwd_kernel<16>), dim3(m->dec_grid), dim3(LB_THREADS), sm, s, GfkArgT<false>{*m});
+    return (int)hipGetLastError();
+  }
+  if (!m->ws_dt) return -1;
   if (fwd) {
     if (m->bmax == 256) GFK_LB_LAUNCH(prodlda_lb_colbn_kernel, 256);
     else GFK_LB_LAUNCH(prodlda_lb_colbn_kernel, 512);
@@ -2552,7 +2916,9 @@ extern "C" int gfk_prodlda_set_smem(size_t bytes) {
 #define GFK_BWD_PTRS(U) GFK_BWD_PTRS1(U, 1), GFK_BWD_PTRS1(U, 4), GFK_BWD_PTRS3(U, false), \
     GFK_BWD_PTRS3(U, true), (const void*)prodlda_bwd_pipe_kernel<64, U, false>, (const void*)prodlda_bwd_pipe_kernel<64, U, false, true>, \
     (const void*)prodlda_bwd_pipe_kernel<64, U, true>, (const void*)prodlda_bwd_pipe_kernel<64, U, true, true>
-                      GFK_BWD_PTRS(1), GFK_BWD_PTRS(2), GFK_BWD_PTRS(3), GFK_BWD_PTRS(4)};
+                      GFK_BWD_PTRS(1), GFK_BWD_PTRS(2), GFK_BWD_PTRS(3), GFK_BWD_PTRS(4),
+                      (const void*)prodlda_lb_bwd_kernel<4>, (const void*)prodlda_lb_bwd_kernel<8>,
+                      (const void*)prodlda_lb_bwd_kernel<13>, (const void*)prodlda_lb_bwd_kernel<16>};
 #undef GFK_BWD_PTRS
 #undef GFK_BWD_PTRS3
 #undef GFK_BWD_PTRS1

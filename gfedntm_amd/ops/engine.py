@@ -648,6 +648,17 @@ class FusedEngine(EngineBase):
         m.dec_grid = int(min(m.n_tiles, 2 * cu))
         m.n_dpart = 1
         m.bwd_pre = 0
+        # ProdLDA's decoder on the matrix cores (csrc/prodlda.hip prodlda_lb_fwd / _bwd) at
+        # bmax 256, K <= 256: one 16-wave workgroup per CU, persistent over the tiles, the
+        # backward's d theta_d in one slab per workgroup.  Elsewhere (bmax 512, K > 256) and
+        # with GFEDNTM_LB_GEMM=1: the library GEMMs around the HIP kernels.
+        m.lb_fused = 0
+        if (m.kind == abi.KIND_PRODLDA and int(m.K) <= 256 and self.bmax == 256
+                and os.environ.get("GFEDNTM_LB_GEMM", "0") != "1"):
+            m.lb_fused = 3
+            m.dec_grid = int(min(m.n_tiles, cu))
+            if m.lb_fused & 2:
+                m.n_dpart = m.dec_grid
         which = (0, 1) if m.kind == abi.KIND_PRODLDA else (2, 3)
         need = max(self.lib.gfk_smem_required(C.byref(m), w) for w in which + (4, 5, 7))
         if need > LDS_LIMIT:
@@ -747,7 +758,7 @@ class FusedEngine(EngineBase):
             # precomputed logit-gradient tiles [n_tiles][B][66] (bwd_pre; + the pipelined
             # backward's store sinks, 64 floats per workgroup)
             # (the large-batch plan: the [B, ldb] logit / logit-gradient matrix)
-            "dt": f(B * int(m.ldb) if m.stage_flags & STAGE_LB else
+            "dt": f(B * int(m.ldb) if m.stage_flags & STAGE_LB and m.lb_fused != 3 else
                     m.n_tiles * B * 66 + 64 * (4 * m.n_dpart + 32) if m.bwd_pre else 1),
             # the large-batch plan's posterior column statistics (6 x 2K floats)
             "colstat": f(12 * K if m.stage_flags & STAGE_LB else 1),
@@ -884,8 +895,10 @@ class FusedEngine(EngineBase):
     def launch_plan(self) -> str:
         """The launch plan in one phrase (recorded in bench / metrics records)."""
         if self.large_batch:
-            return ("large-batch: hipBLASLt decoder GEMMs + HIP kernels, gradient mode"
-                    if self._m.kind == abi.KIND_PRODLDA else "large-batch: HIP kernels, gradient mode")
+            if self._m.kind == abi.KIND_PRODLDA and self._m.lb_fused != 3:
+                return ("large-batch: HIP kernels + hipBLASLt decoder GEMMs"
+                        + (" (backward)" if self._m.lb_fused else "") + ", gradient mode")
+            return "large-batch: HIP kernels, gradient mode"
         return "fused kernels" + (" (fused optimizer epilogues)" if self.update_mode == UPDATE_FUSED else "")
 
     def set_fedavg_scale(self, w: Optional[float]):
@@ -961,8 +974,10 @@ class FusedEngine(EngineBase):
         else:
             ph = abi.PRODLDA_STEP + ([abi.PH_ADAM] if self.update_mode == UPDATE_GRAD else [])
             if self.large_batch:                    # the decoder's GEMMs around its kernels
-                ph.insert(ph.index(abi.PH_PRODLDA_FWD), abi.PH_LB_GEMM_FWD)
-                ph.insert(ph.index(abi.PH_PRODLDA_BWD) + 1, abi.PH_LB_GEMM_BWD)
+                if not self._m.lb_fused & 1:
+                    ph.insert(ph.index(abi.PH_PRODLDA_FWD), abi.PH_LB_GEMM_FWD)
+                if not self._m.lb_fused & 2:
+                    ph.insert(ph.index(abi.PH_PRODLDA_BWD) + 1, abi.PH_LB_GEMM_BWD)
             if self._m.stage_flags & STAGE_FWD_POSTFOLD:
                 ph.remove(abi.PH_POST_FWD)          # computed by the strip forward
         if self.ctx_fused:
@@ -1349,8 +1364,10 @@ class FusedEngine(EngineBase):
             self._ctx_fwd()
             self._ctx_bwd()
         if self.large_batch and self._m.kind == abi.KIND_PRODLDA:
-            self._lb_gemm_fwd()
-            self._lb_gemm_bwd()
+            if not self._m.lb_fused & 1:
+                self._lb_gemm_fwd()
+            if not self._m.lb_fused & 2:
+                self._lb_gemm_bwd()
         torch.cuda.synchronize(self.device)
 
     def enable_graph(self, on: bool = True):

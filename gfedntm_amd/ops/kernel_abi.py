@@ -81,7 +81,7 @@ class GfkModel(C.Structure):
         ("learn_priors", C.c_int32), ("stage_flags", C.c_int32), ("kt", C.c_int32),
         ("scatter_chunks", C.c_int32), ("n_dpart", C.c_int32), ("n_steps", C.c_int32),
         ("drop_enc", C.c_float), ("drop_theta", C.c_float), ("bn_momentum", C.c_float),
-        ("bn_eps", C.c_float), ("kl_weight", C.c_float),
+        ("bn_eps", C.c_float), ("kl_weight", C.c_float), ("lb_fused", C.c_int32),
         ("seed", C.c_uint64),
         ("prior_mean", P), ("prior_var", P), ("beta", P), ("w_in", P), ("b_in", P),
         ("w_h", P * MAX_LAYERS), ("b_h", P * MAX_LAYERS),

@@ -2,8 +2,11 @@
 ops/engine.py FusedEngine._plan_large_batch).  The reference takes any batch_size
 (avitm.py:84-85, SURVEY.md item 4 of round 4's verdict); up to 128 rows the fused kernels keep
 the batch in LDS, above it the row-parallel kernels read the batch matrices from L2, the weight
-jobs and NeuralLDA's beta backward stage 128-row chunks, and ProdLDA's decoder products are
-hipBLASLt GEMMs around two HIP kernels (column batch-norm / logit gradient).
+jobs and NeuralLDA's beta backward stage 128-row chunks.  ProdLDA's decoder at B = 256, K <= 256
+runs on two hand-written MFMA kernels (csrc/prodlda.hip prodlda_lb_fwd / prodlda_lb_bwd: the
+logits GEMM + column batch-norm; the logit gradient + dbeta + d theta_d); elsewhere (B = 512,
+K > 256, or GFEDNTM_LB_GEMM=1) its products are hipBLASLt GEMMs around two HIP kernels (column
+batch-norm / logit gradient).
 
 Oracle: the same PyTorch fp32 functional step as tests/test_fused_kernels.py (loss, KL, RL,
 every gradient, BN running statistics, the optimizer step) at B in {256, 512} x K in {50, 200}
@@ -32,6 +35,17 @@ def test_large_batch_step_matches_oracle(model_type, B, K, V):
     _oracle_step(model_type, B, B + 37, K, (50, 50), V)
 
 
+@pytest.mark.parametrize("K,V", [(50, 5000), (200, 40000)])
+def test_large_batch_gemm_path_matches_oracle(monkeypatch, K, V):
+    """B = 256 with the library-GEMM decoder forced (GFEDNTM_LB_GEMM=1): the same oracle."""
+    monkeypatch.setenv("GFEDNTM_LB_GEMM", "1")
+    torch.manual_seed(0)
+    tm = AVITM(backend="fused", input_size=V, n_components=K, hidden_sizes=(50, 50),
+               batch_size=256, verbose=False, device="cuda")
+    assert tm.engine._m.lb_fused == 0 and abi.PH_LB_GEMM_FWD in tm.engine.phases()
+    _oracle_step("prodLDA", 256, 256 + 37, K, (50, 50), V)
+
+
 @pytest.mark.parametrize("model_type", ["prodLDA", "LDA"])
 def test_large_batch_partial_batch_matches_oracle(model_type):
     """Fewer documents than bmax: rows >= nb are masked out of every column statistic and
@@ -45,11 +59,21 @@ def test_large_batch_plan_and_record():
                batch_size=256, verbose=False, device="cuda")
     e = tm.engine
     assert e.large_batch and e.bmax == 256 and e._m.stage_flags & STAGE_LB
-    assert e.update_mode != UPDATE_FUSED and e.host_gemm_fallback
+    assert e.update_mode != UPDATE_FUSED
+    # B = 256, K = 50: the decoder on the MFMA kernels, no library GEMM phase, one d theta_d
+    # slab per persistent workgroup
     ph = e.phases()
+    assert e._m.lb_fused == 3 and abi.PH_LB_GEMM_FWD not in ph and abi.PH_LB_GEMM_BWD not in ph
+    assert e._m.n_dpart == e._m.dec_grid
+    assert tm.engine_info["engine"] == "fused" and "large-batch" in tm.engine_info["plan"]
+    assert "hipBLASLt" not in tm.engine_info["plan"]
+    # B = 512: the library GEMMs around the HIP kernels
+    tm2 = AVITM(backend="fused", input_size=5000, n_components=50, hidden_sizes=(50, 50),
+                batch_size=512, verbose=False, device="cuda")
+    ph = tm2.engine.phases()
+    assert tm2.engine._m.lb_fused == 0 and tm2.engine.host_gemm_fallback
     assert ph.index(abi.PH_LB_GEMM_FWD) < ph.index(abi.PH_PRODLDA_FWD)
     assert ph.index(abi.PH_PRODLDA_BWD) < ph.index(abi.PH_LB_GEMM_BWD) < ph.index(abi.PH_POST_BWD)
-    assert tm.engine_info["engine"] == "fused" and "large-batch" in tm.engine_info["plan"]
     with pytest.raises(ValueError):
         e.set_update_mode(UPDATE_FUSED)
 
