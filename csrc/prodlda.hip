@@ -1063,15 +1063,15 @@ __global__ void __launch_bounds__(LB_THREADS) prodlda_lb_dlogit_kernel(GfkArgT<G
 // read and write the whole [bmax][ldb] logit matrix and run the skinny products (K = 50 inner
 // or outer dimension) on tiles built for square ones; these two kernels keep each 64-column
 // tile's work inside one workgroup (16 waves, persistent over the tiles, one per CU):
-//  * prodlda_lb_fwd (bit 0, bmax 256 / 512, K <= 256): the logits of the tile on the fp32
-//    matrix cores -- A = theta_d rows straight from L2 (one float per lane per 4-k step),
-//    B = beta through a buffer resource of K rows (rows >= K and columns past ldb read 0),
-//    both one chunk of 4 k steps ahead of the MFMAs -- in accumulators (wave w: row tiles
-//    w + 16 j x the tile's 4 column strips); then prodlda_lb_colbn's work on the registers:
+//  * prodlda_lb_fwd (bit 0, bmax 256, K <= 208): the logits of the tile on the fp32
+//    matrix cores -- A = theta_d's row tile of the wave, held in registers for the whole
+//    persistent loop, B = the tile's beta rows by LDS-DMA (double-buffered; rows >= K and
+//    columns past ldb read 0) -- in accumulators (wave w: row tile w x the tile's 4 column
+//    strips); then prodlda_lb_colbn's work on the registers:
 //    column statistics (the wave's rows + two lane shuffles, the 16 waves through LDS in a
 //    fixed order), running statistics / rstd, the BN'ed tile into ws_zn, the per-row sum-exp
 //    partials (slot 0 of the workgroup's 4).
-//  * prodlda_lb_bwd (bit 1, bmax 256, K <= 256, gradient mode): prodlda_lb_dlogit's logit
+//  * prodlda_lb_bwd (bit 1, bmax 256, K <= 208, gradient mode): prodlda_lb_dlogit's logit
 //    gradient into LDS (D [256][68]), beta's tile by LDS-DMA (Bt [16 KT][68], rows >= K zero),
 //    then dbeta[k][c] = sum_b theta_d[b][k] D[b][c] (subtiles (k tile, column strip) over the
 //    waves, theta_d from L2) into beta's gradient slot, and d theta_d[b][k] += sum_c D[b][c]
@@ -1079,36 +1079,56 @@ __global__ void __launch_bounds__(LB_THREADS) prodlda_lb_dlogit_kernel(GfkArgT<G
 //    workgroup's tiles; one slab per workgroup, n_dpart = the grid, summed by row_bwd).
 // Reference: decoder_network.py:121-126 (ProdLDA decoder), avitm.py:84-85 (any batch_size).
 constexpr int LBB_LD = 68;                   // LDS row stride of D / Bt (conflict-free A reads)
-template <int BM>
-__global__ void __launch_bounds__(LB_THREADS) prodlda_lb_fwd_kernel(GfkArgT<false> ga) {
+// Forward: wave w of 8 owns row tiles w and w + 8 (16 rows each) of the 256, their theta_d
+// A operands for every k step held in registers for the whole persistent loop (2 KS per lane,
+// KS = ceil(K / 4); theta_d is the same for every tile; 8 waves so that K = 200's 104 of them
+// fit without spills), and the tile's beta rows come by LDS-DMA into one of two
+// buffers (Bs [K][LBF_LD]: the next tile's rows land while this one multiplies), read as the
+// MFMA B operand (4 rows x 16 columns per instruction at stride 80: 64 distinct banks).
+constexpr int LBF_LD = 80;
+constexpr int LBF_NT = 512;                  // 8 waves (one workgroup per CU: up to 256 VGPRs)
+__host__ __device__ inline int lb_fwd_lds_floats(int K) { return 2 * K * LBF_LD; }
+template <int KS>
+__global__ void __launch_bounds__(LBF_NT) prodlda_lb_fwd_kernel(GfkArgT<false> ga) {
+  constexpr int BM = 256, NW = LBF_NT / 64, RTW = BM / 16 / NW;
   const GfkModel& m = gfk_model(ga);
-  constexpr int RTW = BM / 256;              // row tiles per wave
-  constexpr int LBF_KC = BM == 256 ? 4 : 2;  // 4-k MFMA steps per prefetched chunk
-  __shared__ float red[2][16][VB];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ float red[2][NW][VB];
   const int tid = threadIdx.x, lane = tid & 63, w = uniform(tid >> 6);
   const int r16 = lane & 15, g = lane >> 4;
   const int K = m.K, V = m.V, ldb = m.ldb, kt = m.kt, nb = *m.ws_nb;
+  const int nks = (K + 3) / 4;
   const float inv_nb = 1.f / (float)nb;
-  const int nch = (K + 4 * LBF_KC - 1) / (4 * LBF_KC);
+  float* bs0 = smem;
+  float* bs1 = smem + K * LBF_LD;
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)m.beta, 0, K * ldb * 4, 0x00020000);
   if (gfk_bx() == 0 && tid == 0) *m.nbt_beta += 1;
-  const float* tha[RTW];
+  // beta's rows of a tile -> LDS: wave w copies rows w + NW u (64 columns; past ldb: zeros)
+  auto dma = [&](int tile, float* buf) {
+    const int c = tile * VB + lane;
+    const int vb = c < ldb ? c * 4 : 0x7FFF0000;
+    for (int k = w; k < K; k += NW)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void_ptr)(buf + k * LBF_LD), 4, boff(vb, k * ldb * 4), 0, 0, 0);
+  };
+  if (gfk_bx() < m.n_tiles) dma(gfk_bx(), bs0);
+  // A[i][kk] = theta_d[16 (w + NW j) + i][4 s + kk]: lane (r16, g) holds it in th[j][s]
+  float th[RTW][KS];
 #pragma unroll
-  for (int j = 0; j < RTW; ++j) tha[j] = m.ws_thetad + (size_t)(16 * (w + 16 * j) + r16) * kt;
+  for (int j = 0; j < RTW; ++j) {
+    const float* tr = m.ws_thetad + (size_t)(16 * (w + NW * j) + r16) * kt;
+#pragma unroll
+    for (int q = 0; q < KS; ++q) th[j][q] = tr[min(4 * q + g, K - 1)] * (4 * q + g < K ? 1.f : 0.f);
+  }
   float rs[RTW][4];
 #pragma unroll
   for (int j = 0; j < RTW; ++j)
 #pragma unroll
     for (int e = 0; e < 4; ++e) rs[j][e] = 0.f;
+  int it = 0;
 #pragma unroll 1
-  for (int tile = gfk_bx(); tile < m.n_tiles; tile += gridDim.x) {
+  for (int tile = gfk_bx(); tile < m.n_tiles; tile += gridDim.x, ++it) {
     const int c0 = tile * VB;
-    int cb[4];
-#pragma unroll
-    for (int cs = 0; cs < 4; ++cs) {
-      const int c = c0 + 16 * cs + r16;
-      cb[cs] = c < ldb ? c * 4 : 0x7FFF0000;
-    }
+    float* bcur = (it & 1) ? bs1 : bs0;
     float rm0[4], rv0[4];
     if (w == 0) {
 #pragma unroll
@@ -1118,40 +1138,27 @@ __global__ void __launch_bounds__(LB_THREADS) prodlda_lb_fwd_kernel(GfkArgT<fals
         rv0[cs] = m.beta_rv[vc];
       }
     }
+    vm_barrier();                            // this tile's beta rows (and every older access)
+    if (tile + (int)gridDim.x < m.n_tiles) dma(tile + gridDim.x, (it & 1) ? bs0 : bs1);
     f32x4 acc[RTW][4];
 #pragma unroll
     for (int j = 0; j < RTW; ++j)
 #pragma unroll
       for (int cs = 0; cs < 4; ++cs) acc[j][cs] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // A[i][kk] = theta_d[row0 + i][k0 + kk], B[kk][jj] = beta[k0 + kk][col0 + jj]
-    auto load = [&](int ch, float (&a)[LBF_KC][RTW], float (&b)[LBF_KC][4]) {
+    const float* bp = bcur + g * LBF_LD + r16;
 #pragma unroll
-      for (int q = 0; q < LBF_KC; ++q) {
-        const int k = 4 * (ch * LBF_KC + q) + g, kc = min(k, K - 1);
+    for (int q = 0; q < KS; ++q) {
+      if (q < nks) {
 #pragma unroll
-        for (int j = 0; j < RTW; ++j) a[q][j] = tha[j][kc];
-        const int ko = k * ldb * 4;
+        for (int cs = 0; cs < 4; ++cs) {
+          const float bv = bp[4 * q * LBF_LD + 16 * cs];
 #pragma unroll
-        for (int cs = 0; cs < 4; ++cs)
-          b[q][cs] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rb, boff(cb[cs], ko), 0, 0));
+          for (int j = 0; j < RTW; ++j) acc[j][cs] = mfma16x16x4(th[j][q], bv, acc[j][cs]);
+        }
       }
-    };
-    auto mma = [&](const float (&a)[LBF_KC][RTW], const float (&b)[LBF_KC][4]) {
-#pragma unroll
-      for (int q = 0; q < LBF_KC; ++q)
-#pragma unroll
-        for (int j = 0; j < RTW; ++j)
-#pragma unroll
-          for (int cs = 0; cs < 4; ++cs) acc[j][cs] = mfma16x16x4(a[q][j], b[q][cs], acc[j][cs]);
-    };
-    float a0[LBF_KC][RTW], b0[LBF_KC][4], a1[LBF_KC][RTW], b1[LBF_KC][4];
-    load(0, a0, b0);
-#pragma unroll 1
-    for (int ch = 0; ch < nch; ch += 2) {    // (chunks past K load zeros for beta)
-      load(ch + 1, a1, b1);
-      mma(a0, b0);
-      load(ch + 2, a0, b0);
-      mma(a1, b1);
+      // (a scheduling fence every 4 steps: the B reads stay near their MFMAs instead of all
+      // being hoisted into registers next to the resident theta_d operands)
+      if ((q & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
     // ---- column statistics over the batch rows (rows >= nb excluded), two-pass variance ----
     float mean[4], rstd[4], sv[4];
@@ -1161,7 +1168,7 @@ __global__ void __launch_bounds__(LB_THREADS) prodlda_lb_fwd_kernel(GfkArgT<fals
 #pragma unroll
       for (int j = 0; j < RTW; ++j)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v += 16 * (w + 16 * j) + 4 * g + e < nb ? acc[j][cs][e] : 0.f;
+        for (int e = 0; e < 4; ++e) v += 16 * (w + NW * j) + 4 * g + e < nb ? acc[j][cs][e] : 0.f;
       v += __shfl_xor(v, 16);
       sv[cs] = v + __shfl_xor(v, 32);
     }
@@ -1174,7 +1181,7 @@ __global__ void __launch_bounds__(LB_THREADS) prodlda_lb_fwd_kernel(GfkArgT<fals
     for (int cs = 0; cs < 4; ++cs) {
       float mu = 0.f;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) mu += red[0][q][16 * cs + r16];
+      for (int q = 0; q < NW; ++q) mu += red[0][q][16 * cs + r16];
       mean[cs] = mu * inv_nb;
       float v = 0.f;
 #pragma unroll
@@ -1182,7 +1189,7 @@ __global__ void __launch_bounds__(LB_THREADS) prodlda_lb_fwd_kernel(GfkArgT<fals
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float d = acc[j][cs][e] - mean[cs];
-          v += 16 * (w + 16 * j) + 4 * g + e < nb ? d * d : 0.f;
+          v += 16 * (w + NW * j) + 4 * g + e < nb ? d * d : 0.f;
         }
       v += __shfl_xor(v, 16);
       sv[cs] = v + __shfl_xor(v, 32);
@@ -1196,7 +1203,7 @@ __global__ void __launch_bounds__(LB_THREADS) prodlda_lb_fwd_kernel(GfkArgT<fals
     for (int cs = 0; cs < 4; ++cs) {
       float var = 0.f;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) var += red[1][q][16 * cs + r16];
+      for (int q = 0; q < NW; ++q) var += red[1][q][16 * cs + r16];
       var *= inv_nb;
       rstd[cs] = rsqrtf(var + m.bn_eps);
       const int v = c0 + 16 * cs + r16;
@@ -1217,7 +1224,7 @@ __global__ void __launch_bounds__(LB_THREADS) prodlda_lb_fwd_kernel(GfkArgT<fals
     for (int j = 0; j < RTW; ++j)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int row = 16 * (w + 16 * j) + 4 * g + e;
+        const int row = 16 * (w + NW * j) + 4 * g + e;
 #pragma unroll
         for (int cs = 0; cs < 4; ++cs) {
           const int col = 16 * cs + r16;
@@ -1236,7 +1243,7 @@ __global__ void __launch_bounds__(LB_THREADS) prodlda_lb_fwd_kernel(GfkArgT<fals
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const float se = row16_sum(rs[j][e]);
-      const int row = 16 * (w + 16 * j) + 4 * g + e;
+      const int row = 16 * (w + NW * j) + 4 * g + e;
       if (r16 < 4 && row < nb) {
         float* p = part + ((size_t)r16 * m.bmax + row) * 2;
         p[0] = 0.f;                     // (max, sum-exp) with max 0: |z| <= sqrt(nb - 1)
@@ -1247,17 +1254,20 @@ __global__ void __launch_bounds__(LB_THREADS) prodlda_lb_fwd_kernel(GfkArgT<fals
 
 __host__ __device__ inline int lb_bwd_lds_floats(int K) { return (256 + 16 * ((K + 15) / 16)) * LBB_LD; }
 
-template <int KTM>
-__global__ void __launch_bounds__(LB_THREADS) prodlda_lb_bwd_kernel(GfkArgT<false> ga) {
-  constexpr int BM = 256, NR = BM / 16;
-  constexpr int RB = KTM >= 16 ? 4 : 8;      // rows per sparse-entry round (registers)
-  constexpr int AV = KTM >= 16 ? 8 : 16;     // theta_d operands in flight per dbeta chunk
+template <int KTM, int NW>
+__global__ void __launch_bounds__(64 * NW) prodlda_lb_bwd_kernel(GfkArgT<false> ga) {
+  // NW waves (16: every wave's row tile of d theta_d in registers, 4-13 k tiles).  8 waves
+  // with two row tiles each (256 VGPRs, no spills at K = 200) measured slower: 413 vs 359 us
+  // per step at K = 200, V = 112k (the 16-wave instance spills 24 bytes outside its loops)
+  constexpr int BM = 256, NR = BM / NW, RTW = 16 / NW;
+  constexpr int RB = NW == 8 ? 4 : 8;        // rows per sparse-entry round (registers)
+  constexpr int AV = KTM >= 13 ? 8 : 16;     // theta_d operands in flight per dbeta chunk
   const GfkModel& m = gfk_model(ga);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* D = smem;                           // [BM][LBB_LD] the logit gradient
   float* Bt = D + BM * LBB_LD;               // [16 KT][LBB_LD] beta's tile (rows >= K: 0)
-  __shared__ float red[2][16][VB];
-  __shared__ float sx[16][VB];               // per wave: the current row's sparse x by column
+  __shared__ float red[2][NW][VB];
+  __shared__ float sx[NW][VB];               // per wave: the current row's sparse x by column
   const int tid = threadIdx.x, lane = tid & 63, w = uniform(tid >> 6);
   const int r16 = lane & 15, g = lane >> 4;
   const int K = m.K, V = m.V, ldb = m.ldb, kt = m.kt, nb = *m.ws_nb, ntp = m.n_tiles + 1;
@@ -1265,31 +1275,28 @@ __global__ void __launch_bounds__(LB_THREADS) prodlda_lb_bwd_kernel(GfkArgT<fals
   const float inv_nb = 1.f / (float)nb;
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)m.beta, 0, K * ldb * 4, 0x00020000);
   const __amdgpu_buffer_rsrc_t rgr = __builtin_amdgcn_make_buffer_rsrc((void*)(m.beta + m.off_g), 0, K * ldb * 4, 0x00020000);
-  const int zc = (lane ^ zswz(w)) * 4;       // (zswz(w + 16 i) == zswz(w))
   sx[w][lane] = 0.f;
-  f32x4 dacc[KTM];                           // d theta_d [row tile w][k tile]
+  f32x4 dacc[RTW][KTM];                      // d theta_d [row tile w + NW j][k tile]
 #pragma unroll
-  for (int q = 0; q < KTM; ++q) dacc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < RTW; ++j)
+#pragma unroll
+    for (int q = 0; q < KTM; ++q) dacc[j][q] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
   for (int tile = gfk_bx(); tile < m.n_tiles; tile += gridDim.x) {
     const int c0 = tile * VB, v = c0 + lane;
     const bool valid = v < V;
-    // beta's tile -> Bt by LDS-DMA: wave w copies rows w + 16 u (64 columns each)
+    // beta's tile -> Bt by LDS-DMA: wave w copies rows w + NW u (64 columns each)
     {
       const int vb = v < ldb ? v * 4 : 0x7FFF0000;
-#pragma unroll
-      for (int u = 0; u < KTM; ++u) {
-        const int k = w + 16 * u;
-        if (u < KT)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void_ptr)(Bt + k * LBB_LD), 4, boff(vb, k * ldb * 4), 0, 0, 0);
-      }
+      for (int k = w; k < 16 * KT; k += NW)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void_ptr)(Bt + k * LBB_LD), 4, boff(vb, k * ldb * 4), 0, 0, 0);
     }
     const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(m.ws_zn + (size_t)tile * BM * VB), 0, BM * VB * 4, 0x00020000);
     const float rsd = m.ws_col_rstd[min(v, V - 1)];
-    int ex0 = 0, ex1 = 0;                    // lane i: row w + 16 i's extent in this tile
-    if (lane < NR && w + 16 * lane < nb) {
-      const int32_t* ts = m.ws_tstart + (size_t)(w + 16 * lane) * ntp + tile;
+    int ex0 = 0, ex1 = 0;                    // lane i: row w + NW i's extent in this tile
+    if (lane < NR && w + NW * lane < nb) {
+      const int32_t* ts = m.ws_tstart + (size_t)(w + NW * lane) * ntp + tile;
       ex0 = ts[0];
       ex1 = ts[1];
     }
@@ -1302,6 +1309,7 @@ __global__ void __launch_bounds__(LB_THREADS) prodlda_lb_bwd_kernel(GfkArgT<fals
       float xi[RB];
 #pragma unroll
       for (int i = 0; i < RB; ++i) {
+        const int r = w + NW * (i0 + i);
         const int e0 = __builtin_amdgcn_readlane(ex0, i0 + i), n = __builtin_amdgcn_readlane(ex1, i0 + i) - e0;
         ci[i] = -1;
         xi[i] = 0.f;
@@ -1309,11 +1317,11 @@ __global__ void __launch_bounds__(LB_THREADS) prodlda_lb_bwd_kernel(GfkArgT<fals
           ci[i] = m.indices[e0 + lane] - c0;
           xi[i] = m.values[e0 + lane];
         }
-        z[i0 + i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rz, zc, (w + 16 * (i0 + i)) * VB * 4, 0));
+        z[i0 + i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rz, (lane ^ zswz(r)) * 4, r * VB * 4, 0));
       }
 #pragma unroll
       for (int i = 0; i < RB; ++i) {
-        const int r = w + 16 * (i0 + i);
+        const int r = w + NW * (i0 + i);
         float d = 0.f;
         if (r < nb) {                        // (wave-uniform)
           const float p = __expf(z[i0 + i] - m.ws_lse[r]);
@@ -1335,7 +1343,7 @@ __global__ void __launch_bounds__(LB_THREADS) prodlda_lb_bwd_kernel(GfkArgT<fals
     vm_barrier();                            // (+ beta's tile in LDS)
     float a1 = 0.f, a2 = 0.f;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
+    for (int q = 0; q < NW; ++q) {
       a1 += red[0][q][lane];
       a2 += red[1][q][lane];
     }
@@ -1344,50 +1352,83 @@ __global__ void __launch_bounds__(LB_THREADS) prodlda_lb_bwd_kernel(GfkArgT<fals
     const float rr = valid ? rsd : 0.f;
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
-      const int r = w + 16 * i;
+      const int r = w + NW * i;
       float* dp = D + r * LBB_LD + lane;
       *dp = r < nb ? rr * (*dp - a1 - z[i] * a2) : 0.f;
     }
     lds_barrier();
     // ---- dbeta[k][c] = sum_b theta_d[b][k] D[b][c] -> beta's gradient slot ----
     // (A[i][kk] = theta_d[b0 + kk][k0 + i], B[kk][jj] = D[b0 + kk][c0' + jj])
-#pragma unroll 1
-    for (int sidx = w; sidx < 4 * KT; sidx += 16) {
-      const int ktile = sidx >> 2, cs = sidx & 3;
-      const float* ta = m.ws_thetad + min(16 * ktile + r16, K - 1);
-      const float* db = D + 16 * cs + r16;
-      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-      for (int b0 = 0; b0 < BM; b0 += 4 * AV) {
-        float av[AV];
-#pragma unroll
-        for (int q = 0; q < AV; ++q) av[q] = ta[(size_t)(b0 + 4 * q + g) * kt];
-#pragma unroll
-        for (int q = 0; q < AV; q += 2) {
-          acc0 = mfma16x16x4(av[q], db[(b0 + 4 * q + g) * LBB_LD], acc0);
-          acc1 = mfma16x16x4(av[q + 1], db[(b0 + 4 * q + 4 + g) * LBB_LD], acc1);
-        }
-      }
+    // KTM >= 13 (K > 128): a wave takes whole k tiles with all 4 column strips, so each
+    // theta_d operand is loaded once per tile (the (k tile, strip) round-robin loaded it 4
+    // times: 0.8 MB of L2 reads per tile at K = 200); smaller K keeps the round-robin (16
+    // subtiles at K = 50: one per wave)
+    auto store_g = [&](int ktile, int cs, const f32x4& v4) {
       const int c = c0 + 16 * cs + r16;
       const int vo = c < ldb ? c * 4 : 0x7FFF0000;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int k = 16 * ktile + 4 * g + e;
         if (k < K)
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc0[e] + acc1[e]), rgr, boff(vo, k * ldb * 4), 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v4[e]), rgr, boff(vo, k * ldb * 4), 0, 0);
+      }
+    };
+    if constexpr (KTM >= 13) {
+#pragma unroll 1
+      for (int ktile = w; ktile < KT; ktile += NW) {
+        const float* ta = m.ws_thetad + min(16 * ktile + r16, K - 1);
+        const float* db = D + r16;
+        f32x4 acc[4];
+#pragma unroll
+        for (int cs = 0; cs < 4; ++cs) acc[cs] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+        for (int b0 = 0; b0 < BM; b0 += 4 * AV) {
+          float av[AV];
+#pragma unroll
+          for (int q = 0; q < AV; ++q) av[q] = ta[(size_t)(b0 + 4 * q + g) * kt];
+#pragma unroll
+          for (int q = 0; q < AV; ++q)
+#pragma unroll
+            for (int cs = 0; cs < 4; ++cs)
+              acc[cs] = mfma16x16x4(av[q], db[(b0 + 4 * q + g) * LBB_LD + 16 * cs], acc[cs]);
+        }
+#pragma unroll
+        for (int cs = 0; cs < 4; ++cs) store_g(ktile, cs, acc[cs]);
+      }
+    } else {
+#pragma unroll 1
+      for (int sidx = w; sidx < 4 * KT; sidx += NW) {
+        const int ktile = sidx >> 2, cs = sidx & 3;
+        const float* ta = m.ws_thetad + min(16 * ktile + r16, K - 1);
+        const float* db = D + 16 * cs + r16;
+        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+        for (int b0 = 0; b0 < BM; b0 += 4 * AV) {
+          float av[AV];
+#pragma unroll
+          for (int q = 0; q < AV; ++q) av[q] = ta[(size_t)(b0 + 4 * q + g) * kt];
+#pragma unroll
+          for (int q = 0; q < AV; q += 2) {
+            acc0 = mfma16x16x4(av[q], db[(b0 + 4 * q + g) * LBB_LD], acc0);
+            acc1 = mfma16x16x4(av[q + 1], db[(b0 + 4 * q + 4 + g) * LBB_LD], acc1);
+          }
+        }
+        store_g(ktile, cs, acc0 + acc1);
       }
     }
-    // ---- d theta_d[b][k] += sum_c D[b][c] beta[k][c]: row tile w x every k tile ----
-    // (A[i][kk] = D[16 w + i][c + kk], B[kk][jj] = beta[16 kt + jj][c + kk])
+    // ---- d theta_d[b][k] += sum_c D[b][c] beta[k][c]: row tiles w + NW j x every k tile ----
+    // (A[i][kk] = D[16 rt + i][c + kk], B[kk][jj] = beta[16 kt + jj][c + kk])
     {
-      const float* da = D + (16 * w + r16) * LBB_LD + g;
       const float* bb = Bt + r16 * LBB_LD + g;
 #pragma unroll
       for (int c = 0; c < VB; c += 4) {
-        const float a = da[c];
 #pragma unroll
-        for (int q = 0; q < KTM; ++q)
-          if (q < KT) dacc[q] = mfma16x16x4(a, bb[q * 16 * LBB_LD + c], dacc[q]);
+        for (int j = 0; j < RTW; ++j) {
+          const float a = D[(16 * (w + NW * j) + r16) * LBB_LD + g + c];
+#pragma unroll
+          for (int q = 0; q < KTM; ++q)
+            if (q < KT) dacc[j][q] = mfma16x16x4(a, bb[q * 16 * LBB_LD + c], dacc[j][q]);
+        }
       }
     }
     __syncthreads();                         // D / Bt / red / sx are rewritten by the next tile
@@ -1395,14 +1436,16 @@ __global__ void __launch_bounds__(LB_THREADS) prodlda_lb_bwd_kernel(GfkArgT<fals
   // ---- this workgroup's d theta_d partial (slab gfk_bx(); row_bwd sums the slabs in order) ----
   float* dpart = m.ws_dthetad + (size_t)gfk_bx() * m.bmax * K;
 #pragma unroll
-  for (int q = 0; q < KTM; ++q) {
-    const int k = 16 * q + r16;
+  for (int j = 0; j < RTW; ++j)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int row = 16 * w + 4 * g + e;
-      if (q < KT && k < K && row < nb) dpart[(size_t)row * K + k] = dacc[q][e];
+    for (int q = 0; q < KTM; ++q) {
+      const int k = 16 * q + r16;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = 16 * (w + NW * j) + 4 * g + e;
+        if (q < KT && k < K && row < nb) dpart[(size_t)row * K + k] = dacc[j][q][e];
+      }
     }
-  }
 }
 
 // Backward.  Two launch shapes of one kernel:
@@ -2315,7 +2358,8 @@ __host__ __device__ inline int strip_np(int K) {
 __host__ __device__ inline int strip_np_bf(int K) { return K <= 64 ? 8 : K <= 128 ? 16 : 32; }
 
 extern "C" size_t gfk_prodlda_fwd_smem(const GfkModel* m) {
-  if (m->stage_flags & GFK_LB) return 0;           // (static LDS only)
+  if (m->stage_flags & GFK_LB)                     // (else static LDS only)
+    return (m->lb_fused & 1) ? sizeof(float) * lb_fwd_lds_floats(m->K) : 0;
   if (m->stage_flags & FWD_STRIP) {
     const int np = m->mm_bf16 ? strip_np_bf(m->K) : strip_np(m->K);
     // (+ the fused posterior's raw heads [2][B][64] and column statistics [2][128])
@@ -2712,17 +2756,20 @@ static int launch_lb(const GfkModel* m, hipStream_t s, bool fwd) {
   if ((m->bmax != 256 && m->bmax != 512) || m->dec_grid < 1 || m->ldb < m->V || m->n_batch > 1) return -1;
   if ((int64_t)(m->K + 16) * m->ldb * 4 >= 0x7FFF0000LL) return -1;     // 32-bit buffer offsets
   if (fwd && (m->lb_fused & 1)) {
-    if (m->bmax != 256 || m->K > 256 || m->kind != GFK_PRODLDA) return -1;
-    hipLaunchKernelGGL((prodlda_lb_fwd_kernel<256>), dim3(m->dec_grid), dim3(LB_THREADS), 0, s, GfkArgT<false>{*m});
+    if (m->bmax != 256 || m->K > 208 || m->kind != GFK_PRODLDA) return -1;
+    const size_t sm = sizeof(float) * lb_fwd_lds_floats(m->K);
+    const dim3 g(m->dec_grid), b(LBF_NT);
+    if (m->K <= 64) hipLaunchKernelGGL((prodlda_lb_fwd_kernel<16>), g, b, sm, s, GfkArgT<false>{*m});
+    else if (m->K <= 128) hipLaunchKernelGGL((prodlda_lb_fwd_kernel<32>), g, b, sm, s, GfkArgT<false>{*m});
+    else hipLaunchKernelGGL((prodlda_lb_fwd_kernel<52>), g, b, sm, s, GfkArgT<false>{*m});
     return (int)hipGetLastError();
   }
   if (!fwd && (m->lb_fused & 2)) {
-    if (m->bmax != 256 || m->K > 256 || m->update_mode != 0 || m->n_dpart != m->dec_grid) return -1;
+    if (m->bmax != 256 || m->K > 208 || m->update_mode != 0 || m->n_dpart != m->dec_grid) return -1;
     const size_t sm = sizeof(float) * lb_bwd_lds_floats(m->K);
-    if (m->K <= 64) hipLaunchKernelGGL((prodlda_lb_bwd_kernel<4>), dim3(m->dec_grid), dim3(LB_THREADS), sm, s, GfkArgT<false>{*m});
-    else if (m->K <= 128) hipLaunchKernelGGL((prodlda_lb_bwd_kernel<8>), dim3(m->dec_grid), dim3(LB_THREADS), sm, s, GfkArgT<false>{*m});
-    else if (m->K <= 208) hipLaunchKernelGGL((prodlda_lb_bwd_kernel<13>), dim3(m->dec_grid), dim3(LB_THREADS), sm, s, GfkArgT<false>{*m});
-    else hipLaunchKernelGGL((prodlda_lb_bwd_kernel<16>), dim3(m->dec_grid), dim3(LB_THREADS), sm, s, GfkArgT<false>{*m});
+    if (m->K <= 64) hipLaunchKernelGGL((prodlda_lb_bwd_kernel<4, 16>), dim3(m->dec_grid), dim3(1024), sm, s, GfkArgT<false>{*m});
+    else if (m->K <= 128) hipLaunchKernelGGL((prodlda_lb_bwd_kernel<8, 16>), dim3(m->dec_grid), dim3(1024), sm, s, GfkArgT<false>{*m});
+    else hipLaunchKernelGGL((prodlda_lb_bwd_kernel<13, 16>), dim3(m->dec_grid), dim3(1024), sm, s, GfkArgT<false>{*m});
     return (int)hipGetLastError();
   }
   if (!m->ws_dt) return -1;
@@ -2917,8 +2964,10 @@ extern "C" int gfk_prodlda_set_smem(size_t bytes) {
     GFK_BWD_PTRS3(U, true), (const void*)prodlda_bwd_pipe_kernel<64, U, false>, (const void*)prodlda_bwd_pipe_kernel<64, U, false, true>, \
     (const void*)prodlda_bwd_pipe_kernel<64, U, true>, (const void*)prodlda_bwd_pipe_kernel<64, U, true, true>
                       GFK_BWD_PTRS(1), GFK_BWD_PTRS(2), GFK_BWD_PTRS(3), GFK_BWD_PTRS(4),
-                      (const void*)prodlda_lb_bwd_kernel<4>, (const void*)prodlda_lb_bwd_kernel<8>,
-                      (const void*)prodlda_lb_bwd_kernel<13>, (const void*)prodlda_lb_bwd_kernel<16>};
+                      (const void*)prodlda_lb_bwd_kernel<4, 16>, (const void*)prodlda_lb_bwd_kernel<8, 16>,
+                      (const void*)prodlda_lb_bwd_kernel<13, 16>,
+                      (const void*)prodlda_lb_fwd_kernel<16>, (const void*)prodlda_lb_fwd_kernel<32>,
+                      (const void*)prodlda_lb_fwd_kernel<52>};
 #undef GFK_BWD_PTRS
 #undef GFK_BWD_PTRS3
 #undef GFK_BWD_PTRS1

@@ -35,6 +35,17 @@ def test_large_batch_step_matches_oracle(model_type, B, K, V):
     _oracle_step(model_type, B, B + 37, K, (50, 50), V)
 
 
+@pytest.mark.parametrize("K,V", [(100, 9000), (128, 5000), (7, 3001)])
+def test_large_batch_mfma_decoder_shapes_match_oracle(K, V):
+    """The MFMA decoder kernels' other instances: K in (64, 128] (16 waves, 8 k tiles), a
+    partial last k tile and vocabulary tile (K = 7, V = 3001)."""
+    torch.manual_seed(0)
+    tm = AVITM(backend="fused", input_size=V, n_components=K, hidden_sizes=(50, 50),
+               batch_size=256, verbose=False, device="cuda")
+    assert tm.engine._m.lb_fused == 3
+    _oracle_step("prodLDA", 256, 256 + 37, K, (50, 50), V)
+
+
 @pytest.mark.parametrize("K,V", [(50, 5000), (200, 40000)])
 def test_large_batch_gemm_path_matches_oracle(monkeypatch, K, V):
     """B = 256 with the library-GEMM decoder forced (GFEDNTM_LB_GEMM=1): the same oracle."""
