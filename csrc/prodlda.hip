@@ -976,7 +976,7 @@ __global__ void __launch_bounds__(LB_THREADS) prodlda_lb_colbn_kernel(GfkArgT<GB
 template <int BM, bool GB = false>
 __global__ void __launch_bounds__(LB_THREADS) prodlda_lb_dlogit_kernel(GfkArgT<GB> ga) {
   const GfkModel& m = gfk_model(ga);
-  constexpr int NR = BM / 16, RB = 8;        // rows per thread; rows per load block
+  constexpr int NR = BM / 16, RB = NR < 8 ? NR : 8;   // rows per thread; rows per load block
   __shared__ float red[2][16][VB];
   __shared__ float sx[16][VB];               // per wave: the current row's sparse x by column
   const int tid = threadIdx.x, lane = tid & 63, w = uniform(tid >> 6);
@@ -2753,7 +2753,9 @@ extern "C" size_t gfk_prodlda_bwd_smem(const GfkModel* m) {
 // the large-batch kernels (stage_flags GFK_LB): bmax 256 or 512, ws_dt the [bmax][ldb] matrix
 #define GFK_LB_LAUNCH(KERN, BM)                                                                      do { if (m->n_batch > 1) hipLaunchKernelGGL((KERN<BM, true>), gfk_grid(dim3(m->dec_grid), m), dim3(LB_THREADS), 0, s, GfkArgT<true>{gfk_dev(m)});        else hipLaunchKernelGGL((KERN<BM, false>), dim3(m->dec_grid), dim3(LB_THREADS), 0, s, GfkArgT<false>{*m}); } while (0)
 static int launch_lb(const GfkModel* m, hipStream_t s, bool fwd) {
-  if ((m->bmax != 256 && m->bmax != 512) || m->dec_grid < 1 || m->ldb < m->V || m->n_batch > 1) return -1;
+  if (m->bmax < 16 || m->bmax > 512 || (m->bmax & (m->bmax - 1)) || m->dec_grid < 1 || m->ldb < m->V ||
+      m->n_batch > 1)
+    return -1;
   if ((int64_t)(m->K + 16) * m->ldb * 4 >= 0x7FFF0000LL) return -1;     // 32-bit buffer offsets
   if (fwd && (m->lb_fused & 1)) {
     if (m->bmax != 256 || m->K > 208 || m->kind != GFK_PRODLDA) return -1;
@@ -2774,11 +2776,23 @@ static int launch_lb(const GfkModel* m, hipStream_t s, bool fwd) {
   }
   if (!m->ws_dt) return -1;
   if (fwd) {
-    if (m->bmax == 256) GFK_LB_LAUNCH(prodlda_lb_colbn_kernel, 256);
-    else GFK_LB_LAUNCH(prodlda_lb_colbn_kernel, 512);
+    switch (m->bmax) {               // (below 256: K > 256 at the batch's own size)
+      case 16: GFK_LB_LAUNCH(prodlda_lb_colbn_kernel, 16); break;
+      case 32: GFK_LB_LAUNCH(prodlda_lb_colbn_kernel, 32); break;
+      case 64: GFK_LB_LAUNCH(prodlda_lb_colbn_kernel, 64); break;
+      case 128: GFK_LB_LAUNCH(prodlda_lb_colbn_kernel, 128); break;
+      case 256: GFK_LB_LAUNCH(prodlda_lb_colbn_kernel, 256); break;
+      default: GFK_LB_LAUNCH(prodlda_lb_colbn_kernel, 512); break;
+    }
   } else {
-    if (m->bmax == 256) GFK_LB_LAUNCH(prodlda_lb_dlogit_kernel, 256);
-    else GFK_LB_LAUNCH(prodlda_lb_dlogit_kernel, 512);
+    switch (m->bmax) {
+      case 16: GFK_LB_LAUNCH(prodlda_lb_dlogit_kernel, 16); break;
+      case 32: GFK_LB_LAUNCH(prodlda_lb_dlogit_kernel, 32); break;
+      case 64: GFK_LB_LAUNCH(prodlda_lb_dlogit_kernel, 64); break;
+      case 128: GFK_LB_LAUNCH(prodlda_lb_dlogit_kernel, 128); break;
+      case 256: GFK_LB_LAUNCH(prodlda_lb_dlogit_kernel, 256); break;
+      default: GFK_LB_LAUNCH(prodlda_lb_dlogit_kernel, 512); break;
+    }
   }
   return (int)hipGetLastError();
 }

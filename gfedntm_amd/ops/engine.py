@@ -73,11 +73,15 @@ STAGE_POST_ROWS2 = 1048576        # bit 20: batched post_bwd, two rows per workg
 
 def engine_bmax(tm) -> int:
     """Rows the engine's workspaces are sized for: the batch size rounded up to a kernel
-    instance; K > 256 runs the large-batch plan (its posterior / decoder shapes take
-    K <= 512), so such a model's batch is padded to 256 rows (rows >= the batch are
-    masked everywhere, as a short last batch)."""
-    b = next(x for x in BMAX_CHOICES if x >= tm.batch_size)
-    return max(b, LB_MIN_BMAX) if tm.n_components > 256 else b
+    instance.  (K > 256 runs the large-batch plan at the batch's own size since round 6;
+    round 5 padded it to 256 rows.)"""
+    return next(x for x in BMAX_CHOICES if x >= tm.batch_size)
+
+
+def uses_large_batch_plan(tm, bmax: int) -> bool:
+    """The large-batch plan (csrc/gfk_common.h GFK_LB): 256 / 512 rows, or K > 256 (its
+    posterior / decoder shapes take K <= 512) at any batch size."""
+    return bmax >= LB_MIN_BMAX or tm.n_components > 256
 
 
 def _explain(ok: bool, why: str, explain: bool) -> bool:
@@ -109,7 +113,7 @@ def supports(tm, explain: bool = False) -> bool:
     if tm.n_components > 256 and (tm.kind == "ctm" or tm.model_type.lower() != "prodlda"):
         return _explain(False, "n_components > 256 needs the large-batch plan: ProdLDA, bag-of-words",
                         explain)
-    if bmax >= LB_MIN_BMAX:
+    if uses_large_batch_plan(tm, bmax):
         # the large-batch plan: bag-of-words AVITM, the sparse W_in tiles (H0 <= 64), the
         # [bmax, ldb] logit matrix addressed with 32-bit buffer offsets
         lb = [(tm.kind != "ctm", "batch_size > 128 needs a bag-of-words AVITM model"),
@@ -190,7 +194,7 @@ def lds_required(tm, bmax: int) -> int:
     m.n_dpart = m.n_tiles if m.kind == abi.KIND_PRODLDA else 1
     lib = native.kernels()
     which = (0, 1) if m.kind == abi.KIND_PRODLDA else (2, 3)
-    if bmax >= LB_MIN_BMAX:
+    if uses_large_batch_plan(tm, bmax):
         need = 0
         for win in (0, STAGE_WIN_SPARSE):        # (either W_in tile shape)
             m.stage_flags, m.n_dpart = 2 | STAGE_LB | win, 1
@@ -335,7 +339,7 @@ class FusedEngine(EngineBase):
         self.bmax = engine_bmax(tm)
         # the large-batch plan (bmax 256 / 512): library GEMMs for the decoder products,
         # gradient mode (the kernels write gradients; the generic optimizer kernel follows)
-        self.large_batch = self.bmax >= LB_MIN_BMAX
+        self.large_batch = uses_large_batch_plan(tm, self.bmax)
         if self.large_batch:
             self.update_mode = UPDATE_GRAD
         self.param_order: List[Tuple[str, torch.nn.Parameter]] = list(self.model.named_parameters())
@@ -649,11 +653,11 @@ class FusedEngine(EngineBase):
         m.n_dpart = 1
         m.bwd_pre = 0
         # ProdLDA's decoder on the matrix cores (csrc/prodlda.hip prodlda_lb_fwd / _bwd) at
-        # bmax 256, K <= 256: one 16-wave workgroup per CU, persistent over the tiles, the
-        # backward's d theta_d in one slab per workgroup.  Elsewhere (bmax 512, K > 256) and
+        # bmax 256, K <= 208: one 16-wave workgroup per CU, persistent over the tiles, the
+        # backward's d theta_d in one slab per workgroup.  Elsewhere (bmax 512, K > 208) and
         # with GFEDNTM_LB_GEMM=1: the library GEMMs around the HIP kernels.
         m.lb_fused = 0
-        if (m.kind == abi.KIND_PRODLDA and int(m.K) <= 256 and self.bmax == 256
+        if (m.kind == abi.KIND_PRODLDA and int(m.K) <= 208 and self.bmax == 256
                 and os.environ.get("GFEDNTM_LB_GEMM", "0") != "1"):
             m.lb_fused = 3
             m.dec_grid = int(min(m.n_tiles, cu))

@@ -11,7 +11,7 @@ batch-norm / logit gradient).
 Oracle: the same PyTorch fp32 functional step as tests/test_fused_kernels.py (loss, KL, RL,
 every gradient, BN running statistics, the optimizer step) at B in {256, 512} x K in {50, 200}
 x V in {5k, 112k}, ProdLDA and NeuralLDA, plus a partial batch, a graph-replayed run, and
-K in (256, 512] (ProdLDA: the same plan, the batch padded to 256 rows) with θ inference.
+K in (256, 512] (ProdLDA: the same plan at the batch's own size) with θ inference.
 """
 import numpy as np
 import pytest
@@ -123,13 +123,13 @@ def test_large_batch_graph_training_tracks_torch(model_type):
 
 @pytest.mark.parametrize("B,K", [(64, 300), (256, 512), (100, 512)])
 def test_large_k_matches_oracle(B, K):
-    """K in (256, 512] (ProdLDA, bag of words) runs the large-batch plan, the batch padded to
-    256 rows when smaller (rows >= the batch masked everywhere): same oracle."""
-    from gfedntm_amd.ops.engine import engine_bmax
+    """K in (256, 512] (ProdLDA, bag of words) runs the large-batch plan at the batch's own
+    row count (round 5 padded a smaller batch to 256 rows): same oracle."""
+    from gfedntm_amd.ops.engine import BMAX_CHOICES
     torch.manual_seed(0)
     tm = AVITM(backend="fused", input_size=5000, n_components=K, hidden_sizes=(50, 50),
                batch_size=B, verbose=False, device="cuda")
-    assert tm.engine.large_batch and tm.engine.bmax == engine_bmax(tm) >= 256
+    assert tm.engine.large_batch and tm.engine.bmax == next(x for x in BMAX_CHOICES if x >= B)
     _oracle_step("prodLDA", B, B + 37, K, (50, 50), 5000)
 
 
