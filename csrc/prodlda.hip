@@ -1071,7 +1071,8 @@ __global__ void __launch_bounds__(LB_THREADS) prodlda_lb_dlogit_kernel(GfkArgT<G
 //    column statistics (the wave's rows + two lane shuffles, the 16 waves through LDS in a
 //    fixed order), running statistics / rstd, the BN'ed tile into ws_zn, the per-row sum-exp
 //    partials (slot 0 of the workgroup's 4).
-//  * prodlda_lb_bwd (bit 1, bmax 256, K <= 208, gradient mode): prodlda_lb_dlogit's logit
+//  * prodlda_lb_bwd (bit 1, bmax 256, K <= 208; bit 2: beta's Adam step in its epilogue, the
+//    rest of the model in gradient mode + the generic optimizer): prodlda_lb_dlogit's logit
 //    gradient into LDS (D [256][68]), beta's tile by LDS-DMA (Bt [16 KT][68], rows >= K zero),
 //    then dbeta[k][c] = sum_b theta_d[b][k] D[b][c] (subtiles (k tile, column strip) over the
 //    waves, theta_d from L2) into beta's gradient slot, and d theta_d[b][k] += sum_c D[b][c]
@@ -1275,6 +1276,14 @@ __global__ void __launch_bounds__(64 * NW) prodlda_lb_bwd_kernel(GfkArgT<false> 
   const float inv_nb = 1.f / (float)nb;
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)m.beta, 0, K * ldb * 4, 0x00020000);
   const __amdgpu_buffer_rsrc_t rgr = __builtin_amdgcn_make_buffer_rsrc((void*)(m.beta + m.off_g), 0, K * ldb * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rmo = __builtin_amdgcn_make_buffer_rsrc((void*)(m.beta + m.off_m), 0, K * ldb * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rvo = __builtin_amdgcn_make_buffer_rsrc((void*)(m.beta + m.off_v), 0, K * ldb * 4, 0x00020000);
+  // lb_fused bit 2: beta's Adam step (+ the FedAvg pre-scale) in this kernel's dbeta epilogue
+  // -- p from the staged tile, m / v loaded next to it; the generic optimizer pass skips beta
+  const bool adam_here = m.lb_fused & 4;
+  const AdamCoef ac = adam_coef(m);
+  const bool pre_scale = m.fed_scale_on && is_shared(m, m.beta);
+  const float fscale = m.fed_scale;
   sx[w][lane] = 0.f;
   f32x4 dacc[RTW][KTM];                      // d theta_d [row tile w + NW j][k tile]
 #pragma unroll
@@ -1364,7 +1373,29 @@ __global__ void __launch_bounds__(64 * NW) prodlda_lb_bwd_kernel(GfkArgT<false> 
     // times: 0.8 MB of L2 reads per tile at K = 200); smaller K keeps the round-robin (16
     // subtiles at K = 50: one per wave)
     auto store_g = [&](int ktile, int cs, const f32x4& v4) {
-      const int c = c0 + 16 * cs + r16;
+      const int cl = 16 * cs + r16, c = c0 + cl;
+      if (adam_here) {                       // (columns >= V keep their zeros)
+        const int vo = c < V ? c * 4 : 0x7FFF0000;
+        float mo[4], vv[4];
+        int off[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int k = 16 * ktile + 4 * g + e;
+          off[e] = k < K ? boff(vo, k * ldb * 4) : 0x7FFF0000;
+          mo[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rmo, off[e], 0, 0));
+          vv[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rvo, off[e], 0, 0));
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int k = 16 * ktile + 4 * g + e;
+          float np = adam_update(Bt[k * LBB_LD + cl], v4[e], mo[e], vv[e], ac);
+          if (pre_scale) np *= fscale;
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mo[e]), rmo, off[e], 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vv[e]), rvo, off[e], 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(np), rb, off[e], 0, 0);
+        }
+        return;
+      }
       const int vo = c < ldb ? c * 4 : 0x7FFF0000;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {

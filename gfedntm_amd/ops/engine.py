@@ -391,6 +391,10 @@ class FusedEngine(EngineBase):
             raise ValueError(f"the fused update mode is Adam only (solver {self.solver})")
         self.update_mode = mode
         self._m.update_mode = mode
+        if self.large_batch and mode == UPDATE_GRAD:
+            # an explicit gradient mode materialises every gradient, beta's included (the
+            # oracle tests, --agg grads): beta's Adam leaves the large-batch backward
+            self._m.lb_fused &= ~4
         self._rebuild_adam()
 
     def set_adam_t(self, t: int):
@@ -659,7 +663,9 @@ class FusedEngine(EngineBase):
         m.lb_fused = 0
         if (m.kind == abi.KIND_PRODLDA and int(m.K) <= 208 and self.bmax == 256
                 and os.environ.get("GFEDNTM_LB_GEMM", "0") != "1"):
-            m.lb_fused = 3
+            # (+ bit 2: beta's Adam step in prodlda_lb_bwd's epilogue -- the generic optimizer
+            # pass then skips beta, 80 % of the parameters at K = 200, V = 112k)
+            m.lb_fused = 3 | (4 if self.solver == "adam" else 0)
             m.dec_grid = int(min(m.n_tiles, cu))
             if m.lb_fused & 2:
                 m.n_dpart = m.dec_grid
@@ -762,7 +768,7 @@ class FusedEngine(EngineBase):
             # precomputed logit-gradient tiles [n_tiles][B][66] (bwd_pre; + the pipelined
             # backward's store sinks, 64 floats per workgroup)
             # (the large-batch plan: the [B, ldb] logit / logit-gradient matrix)
-            "dt": f(B * int(m.ldb) if m.stage_flags & STAGE_LB and m.lb_fused != 3 else
+            "dt": f(B * int(m.ldb) if m.stage_flags & STAGE_LB and (m.lb_fused & 3) != 3 else
                     m.n_tiles * B * 66 + 64 * (4 * m.n_dpart + 32) if m.bwd_pre else 1),
             # the large-batch plan's posterior column statistics (6 x 2K floats)
             "colstat": f(12 * K if m.stage_flags & STAGE_LB else 1),
@@ -853,6 +859,10 @@ class FusedEngine(EngineBase):
         up = lambda x: -(-x // ALIGN) * ALIGN  # noqa: E731
         n_total = self.flat.n_total
         shared_end = up(self.flat.n_shared) if self.fedavg_scale is not None else 0
+        if keys is None and getattr(self, "large_batch", False) and self._m.lb_fused & 4:
+            # beta's Adam runs in the large-batch backward's epilogue (csrc/prodlda.hip)
+            keys = [k for k in self.flat.slots if k != "beta"
+                    and any(k == n for n, _ in self.param_order)]
         if keys is None:
             pr = [(s0, up(s1)) for s0, s1 in self.flat.param_ranges()]
         else:
@@ -899,7 +909,7 @@ class FusedEngine(EngineBase):
     def launch_plan(self) -> str:
         """The launch plan in one phrase (recorded in bench / metrics records)."""
         if self.large_batch:
-            if self._m.kind == abi.KIND_PRODLDA and self._m.lb_fused != 3:
+            if self._m.kind == abi.KIND_PRODLDA and (self._m.lb_fused & 3) != 3:
                 return ("large-batch: HIP kernels + hipBLASLt decoder GEMMs"
                         + (" (backward)" if self._m.lb_fused else "") + ", gradient mode")
             return "large-batch: HIP kernels, gradient mode"

@@ -42,8 +42,31 @@ def test_large_batch_mfma_decoder_shapes_match_oracle(K, V):
     torch.manual_seed(0)
     tm = AVITM(backend="fused", input_size=V, n_components=K, hidden_sizes=(50, 50),
                batch_size=256, verbose=False, device="cuda")
-    assert tm.engine._m.lb_fused == 3
+    assert tm.engine._m.lb_fused & 3 == 3
     _oracle_step("prodLDA", 256, 256 + 37, K, (50, 50), V)
+
+
+@pytest.mark.parametrize("K,V", [(50, 5000), (200, 40000)])
+def test_large_batch_fused_beta_adam_matches_gradient_mode(K, V):
+    """B = 256 by default runs beta's Adam step (+ the FedAvg pre-scale) in prodlda_lb_bwd's
+    epilogue and the rest in the generic optimizer pass (GfkModel.lb_fused bit 2); an explicit
+    gradient mode materialises beta's gradient too.  Several graph-replayed steps: the same
+    parameters, moments and losses."""
+    from tests.test_fused_large_v import _compare, _run
+    from gfedntm_amd.ops.engine import UPDATE_GRAD
+    torch.manual_seed(0)
+    kw = dict(input_size=V, n_components=K, hidden_sizes=(50, 50), batch_size=256,
+              verbose=False, device="cuda")
+    a, b = AVITM(backend="fused", **kw), AVITM(backend="fused", **kw)
+    b.model.load_state_dict(a.model.state_dict())
+    b.engine.seed = b.engine._m.seed = a.engine.seed
+    b.engine.set_update_mode(UPDATE_GRAD)
+    assert a.engine._m.lb_fused == 7 and b.engine._m.lb_fused == 3
+    n_docs = 2 * 256 + 37
+    X = random_csr(n_docs, V, 60, seed=4)
+    data = DeviceCSR(X, "cuda")
+    _run((a, b), data, BatchPlan.build(n_docs, 256, 4, seed=0))
+    _compare(a, b, 4)
 
 
 @pytest.mark.parametrize("K,V", [(50, 5000), (200, 40000)])
@@ -74,7 +97,7 @@ def test_large_batch_plan_and_record():
     # B = 256, K = 50: the decoder on the MFMA kernels, no library GEMM phase, one d theta_d
     # slab per persistent workgroup
     ph = e.phases()
-    assert e._m.lb_fused == 3 and abi.PH_LB_GEMM_FWD not in ph and abi.PH_LB_GEMM_BWD not in ph
+    assert e._m.lb_fused == 7 and abi.PH_LB_GEMM_FWD not in ph and abi.PH_LB_GEMM_BWD not in ph
     assert e._m.n_dpart == e._m.dec_grid
     assert tm.engine_info["engine"] == "fused" and "large-batch" in tm.engine_info["plan"]
     assert "hipBLASLt" not in tm.engine_info["plan"]
