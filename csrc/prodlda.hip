@@ -1139,7 +1139,9 @@ __global__ void __launch_bounds__(LBF_NT) prodlda_lb_fwd_kernel(GfkArgT<false> g
         rv0[cs] = m.beta_rv[vc];
       }
     }
+    GFK_STAMP(m, 130);
     vm_barrier();                            // this tile's beta rows (and every older access)
+    GFK_STAMP(m, 131);
     if (tile + (int)gridDim.x < m.n_tiles) dma(tile + gridDim.x, (it & 1) ? bs0 : bs1);
     f32x4 acc[RTW][4];
 #pragma unroll
@@ -1161,6 +1163,7 @@ __global__ void __launch_bounds__(LBF_NT) prodlda_lb_fwd_kernel(GfkArgT<false> g
       // being hoisted into registers next to the resident theta_d operands)
       if ((q & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
+    GFK_STAMP(m, 132);
     // ---- column statistics over the batch rows (rows >= nb excluded), two-pass variance ----
     float mean[4], rstd[4], sv[4];
 #pragma unroll
@@ -1218,6 +1221,7 @@ __global__ void __launch_bounds__(LBF_NT) prodlda_lb_fwd_kernel(GfkArgT<false> g
         m.ws_col_rstd[v] = rstd[cs];
       }
     }
+    GFK_STAMP(m, 133);
     // ---- the BN'ed tile into ws_zn (row_loss's layout), the rows' sum-exp ----
     const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(m.ws_zn + (size_t)tile * BM * VB), 0, BM * VB * 4, 0x00020000);
@@ -1292,6 +1296,7 @@ __global__ void __launch_bounds__(64 * NW) prodlda_lb_bwd_kernel(GfkArgT<false> 
     for (int q = 0; q < KTM; ++q) dacc[j][q] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
   for (int tile = gfk_bx(); tile < m.n_tiles; tile += gridDim.x) {
+    GFK_STAMP(m, 120);
     const int c0 = tile * VB, v = c0 + lane;
     const bool valid = v < V;
     // beta's tile -> Bt by LDS-DMA: wave w copies rows w + NW u (64 columns each)
@@ -1347,9 +1352,11 @@ __global__ void __launch_bounds__(64 * NW) prodlda_lb_bwd_kernel(GfkArgT<false> 
         D[r * LBB_LD + lane] = d;
       }
     }
+    GFK_STAMP(m, 121);
     red[0][w][lane] = s1;
     red[1][w][lane] = s2;
     vm_barrier();                            // (+ beta's tile in LDS)
+    GFK_STAMP(m, 122);
     float a1 = 0.f, a2 = 0.f;
 #pragma unroll
     for (int q = 0; q < NW; ++q) {
@@ -1366,6 +1373,7 @@ __global__ void __launch_bounds__(64 * NW) prodlda_lb_bwd_kernel(GfkArgT<false> 
       *dp = r < nb ? rr * (*dp - a1 - z[i] * a2) : 0.f;
     }
     lds_barrier();
+    GFK_STAMP(m, 123);
     // ---- dbeta[k][c] = sum_b theta_d[b][k] D[b][c] -> beta's gradient slot ----
     // (A[i][kk] = theta_d[b0 + kk][k0 + i], B[kk][jj] = D[b0 + kk][c0' + jj])
     // KTM >= 13 (K > 128): a wave takes whole k tiles with all 4 column strips, so each
@@ -1447,6 +1455,7 @@ __global__ void __launch_bounds__(64 * NW) prodlda_lb_bwd_kernel(GfkArgT<false> 
         store_g(ktile, cs, acc0 + acc1);
       }
     }
+    GFK_STAMP(m, 124);
     // ---- d theta_d[b][k] += sum_c D[b][c] beta[k][c]: row tiles w + NW j x every k tile ----
     // (A[i][kk] = D[16 rt + i][c + kk], B[kk][jj] = beta[16 kt + jj][c + kk])
     {
@@ -1462,7 +1471,9 @@ __global__ void __launch_bounds__(64 * NW) prodlda_lb_bwd_kernel(GfkArgT<false> 
         }
       }
     }
+    GFK_STAMP(m, 125);
     __syncthreads();                         // D / Bt / red / sx are rewritten by the next tile
+    GFK_STAMP(m, 126);
   }
   // ---- this workgroup's d theta_d partial (slab gfk_bx(); row_bwd sums the slabs in order) ----
   float* dpart = m.ws_dthetad + (size_t)gfk_bx() * m.bmax * K;

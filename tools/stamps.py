@@ -109,6 +109,15 @@ def main(argv=None):
         print("ctx_bwd (wg 0) cycles: staging", int(d[35] - d[34]), "| dA", int(d[36] - d[35]),
               "| g_ba + g_Wa", int(d[37] - d[36]), "| update", int(d[38] - d[37]))
     print("win_update (W_in tile 0) cycles: staging", int(d[41] - d[40]), "| mfma+update", int(d[42] - d[41]))
+    if m.stage_flags & (1 << 19) and m.lb_fused:
+        # the large-batch MFMA decoder (csrc/prodlda.hip prodlda_lb_fwd / _bwd), the last tile
+        # of workgroup 0
+        print("lb_fwd cycles: beta rows wait", int(d[131] - d[130]), "| mfma", int(d[132] - d[131]),
+              "| column stats", int(d[133] - d[132]))
+        print("lb_bwd cycles: logit gradient (loads + sparse)", int(d[121] - d[120]),
+              "| barrier", int(d[122] - d[121]), "| bn bwd", int(d[123] - d[122]),
+              "| dbeta (+ adam)", int(d[124] - d[123]), "| dtheta", int(d[125] - d[124]),
+              "| end barrier", int(d[126] - d[125]))
     # strip forward (stage_flags bit 2): per-wave timelines of workgroups 0 and grid - 1,
     # memtime cycles from the earliest wave's entry; clock = memtime / memrealtime (100 MHz)
     for wg, base in (("0", 64), ("last", 320)):
