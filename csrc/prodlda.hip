@@ -1308,22 +1308,33 @@ __global__ void __launch_bounds__(64 * NW) prodlda_lb_bwd_kernel(GfkArgT<false> 
     const __amdgpu_buffer_rsrc_t rz = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(m.ws_zn + (size_t)tile * BM * VB), 0, BM * VB * 4, 0x00020000);
     const float rsd = m.ws_col_rstd[min(v, V - 1)];
-    int ex0 = 0, ex1 = 0;                    // lane i: row w + NW i's extent in this tile
+    // one round of independent loads: lane i holds row w + NW i's extent in this tile, lse
+    // and S; every z of the thread's rows (kept in registers); then the rows' non-zeros
+    // (their addresses depend on the extents: the second round) in blocks of RB rows
+    int ex0 = 0, ex1 = 0;
+    float lse_l = 0.f, s_l = 0.f;
     if (lane < NR && w + NW * lane < nb) {
-      const int32_t* ts = m.ws_tstart + (size_t)(w + NW * lane) * ntp + tile;
+      const int rl = w + NW * lane;
+      const int32_t* ts = m.ws_tstart + (size_t)rl * ntp + tile;
       ex0 = ts[0];
       ex1 = ts[1];
+      lse_l = m.ws_lse[rl];
+      s_l = m.ws_s[rl];
+    }
+    float z[NR], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int r = w + NW * i;
+      z[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rz, (lane ^ zswz(r)) * 4, r * VB * 4, 0));
     }
     // ---- the logit gradient (prodlda_lb_dlogit): d = p S - x p / (p + eps), then the
     //      column BN backward; d parked in D, z kept in registers ----
-    float z[NR], s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i0 = 0; i0 < NR; i0 += RB) {
       int ci[RB];
       float xi[RB];
 #pragma unroll
       for (int i = 0; i < RB; ++i) {
-        const int r = w + NW * (i0 + i);
         const int e0 = __builtin_amdgcn_readlane(ex0, i0 + i), n = __builtin_amdgcn_readlane(ex1, i0 + i) - e0;
         ci[i] = -1;
         xi[i] = 0.f;
@@ -1331,18 +1342,19 @@ __global__ void __launch_bounds__(64 * NW) prodlda_lb_bwd_kernel(GfkArgT<false> 
           ci[i] = m.indices[e0 + lane] - c0;
           xi[i] = m.values[e0 + lane];
         }
-        z[i0 + i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rz, (lane ^ zswz(r)) * 4, r * VB * 4, 0));
       }
 #pragma unroll
       for (int i = 0; i < RB; ++i) {
         const int r = w + NW * (i0 + i);
         float d = 0.f;
         if (r < nb) {                        // (wave-uniform)
-          const float p = __expf(z[i0 + i] - m.ws_lse[r]);
+          const float lse_r = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lse_l), i0 + i));
+          const float s_r = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s_l), i0 + i));
+          const float p = __expf(z[i0 + i] - lse_r);
           if (ci[i] >= 0) sx[w][ci[i]] = xi[i];
           const float xs = sx[w][lane];
           sx[w][lane] = 0.f;
-          const float dd = p * m.ws_s[r] - xs * p / (p + RL_EPS);
+          const float dd = p * s_r - xs * p / (p + RL_EPS);
           d = valid ? dd : 0.f;
           s1 += d;
           s2 += d * z[i0 + i];
