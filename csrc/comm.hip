@@ -396,25 +396,30 @@ __device__ __forceinline__ T fold(const GfkLocalAvg& a, int64_t i) {
 }
 }  // namespace
 
-// Up to FV clients: every client's float4 is loaded before the first add (one round trip
-// instead of a dependent load per client), then folded in the same group order as fold()
-// -- the same bits.
+// FV clients at a time: every client's float4 of a chunk is loaded before the first add (one
+// round trip per 8 clients instead of a dependent load per client), then folded in the same
+// group order as fold() -- the same bits.  (17 clients on one GPU: the per-client loop was a
+// chain of 17 dependent round trips.)
 constexpr int FV = 8;
 __device__ __forceinline__ float4 fold_regs(const GfkLocalAvg& a, int64_t i) {
-  float4 v[FV];
+  const int n = a.n_clients;
+  float4 tot = {0.f, 0.f, 0.f, 0.f}, s = tot;
+  int g = 0, gs = 0, e = a.gend[0];
+  for (int j0 = 0; j0 < n; j0 += FV) {
+    float4 v[FV];
 #pragma unroll
-  for (int j = 0; j < FV; ++j)
-    v[j] = lptr<const float4>(a, j < a.n_clients ? j : 0)[i];
-  float4 tot = v[0], s = v[0];
-  int g = 0, e = a.gend[0];
+    for (int j = 0; j < FV; ++j) v[j] = lptr<const float4>(a, j0 + j < n ? j0 + j : 0)[i];
 #pragma unroll
-  for (int j = 0; j < FV; ++j) {
-    if (j >= a.n_clients) break;
-    if (j > 0) s = j == (g == 0 ? 0 : a.gend[g - 1]) ? v[j] : s + v[j];
-    if (j == e - 1) {
-      tot = g == 0 ? s : tot + s;
-      ++g;
-      if (g < a.n_groups) e = a.gend[g];
+    for (int j = 0; j < FV; ++j) {
+      const int jj = j0 + j;
+      if (jj >= n) break;
+      s = jj == gs ? v[j] : s + v[j];
+      if (jj == e - 1) {
+        tot = g == 0 ? s : tot + s;
+        ++g;
+        gs = e;
+        if (g < a.n_groups) e = a.gend[g];
+      }
     }
   }
   return tot;
@@ -426,9 +431,8 @@ extern "C" __global__ void __launch_bounds__(256) gfk_local_fedavg(GfkLocalAvg a
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int w1 = a.mode == 1 ? 1 : a.n_clients;     // buffers written
   const int w0 = a.mode == 2 ? 1 : 0;
-  const bool regs = a.mode != 2 && a.n_clients <= FV;
   for (int64_t i = g; i < n4; i += stride) {
-    const float4 acc = a.mode == 2 ? lptr<const float4>(a, 0)[i] : regs ? fold_regs(a, i) : fold<float4>(a, i);
+    const float4 acc = a.mode == 2 ? lptr<const float4>(a, 0)[i] : fold_regs(a, i);
     for (int j = w0; j < w1; ++j) lptr<float4>(a, j)[i] = acc;
   }
   if (g < (a.n & 3)) {           // the partial float4 at the end: nothing past n is touched
