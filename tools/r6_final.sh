@@ -19,6 +19,13 @@ if [ "$1" = 1 ]; then
   run lda1 200 --model LDA --clients 1 --steps 2000 --warmup 200 --no-npmi
   run lb256 200 --clients 1 --batch 256 --steps 1000 --warmup 100 --no-npmi
   run lb512 200 --clients 1 --batch 512 --steps 500 --warmup 50 --no-npmi
+elif [ "$1" = 3 ]; then
+  run lb256 200 --clients 1 --batch 256 --steps 1000 --warmup 100 --no-npmi
+  run lb256k200 240 --clients 1 --batch 256 --topics 200 --vocab 150000 --docs 1500 --steps 100 --warmup 10 --no-npmi
+  run k300b64 200 --clients 1 --topics 300 --steps 1000 --warmup 100 --no-npmi
+  run multi17 240 --clients-per-gpu 17 --steps 300 --warmup 30 --no-npmi
+  run k50 240 --steps 2000 --warmup 200
+  run driver_default 200 --steps 20 --warmup 5
 else
   run b112 200 --clients 1 --topics 200 --vocab 150000 --docs 1500 --steps 300 --warmup 30 --no-npmi
   run lb256k200 240 --clients 1 --batch 256 --topics 200 --vocab 150000 --docs 1500 --steps 100 --warmup 10 --no-npmi
