@@ -437,8 +437,11 @@ gfk_enc_in_k(GfkArgT<GB> ga) {
 }
 
 extern "C" int gfk_launch_enc_in(const GfkModel* m, hipStream_t s) {
-  if (m->n_batch > 1 && m->H[0] <= 64 && (m->stage_flags & 1)) {   // batched, narrow, staged: two workgroups per CU
-    hipLaunchKernelGGL((gfk_enc_in_k<true, true, 1>), gfk_grid(dim3(m->bmax), m), dim3(ENC_THREADS), gfk_enc_in_smem(m), s, GfkArgT<true>{gfk_dev(m)});
+  if (m->H[0] <= 64 && (m->stage_flags & 1)) {   // narrow, staged: two workgroups per CU
+    if (m->n_batch > 1)
+      hipLaunchKernelGGL((gfk_enc_in_k<true, true, 1>), gfk_grid(dim3(m->bmax), m), dim3(ENC_THREADS), gfk_enc_in_smem(m), s, GfkArgT<true>{gfk_dev(m)});
+    else
+      hipLaunchKernelGGL((gfk_enc_in_k<true, false, 1>), dim3(m->bmax), dim3(ENC_THREADS), gfk_enc_in_smem(m), s, GfkArgT<false>{*m});
     return (int)hipGetLastError();
   }
   if (m->stage_flags & 1)
@@ -455,6 +458,7 @@ extern "C" int gfk_enc_in_set_smem(size_t bytes) {
   if (bytes <= cur) return 0;
   cur = bytes;
   const void* ks[] = {(const void*)gfk_enc_in_k<true>, (const void*)gfk_enc_in_k<true, true>, (const void*)gfk_enc_in_k<false>, (const void*)gfk_enc_in_k<false, true>,
+                      (const void*)gfk_enc_in_k<true, false, 1>,
                       (const void*)gfk_enc_in_k<true, true, 1>};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
