@@ -496,6 +496,7 @@ __global__ void __launch_bounds__(RS_T) gfk_ctx_fwd_rs_k(GfkArgT<GB> ga) {
     // (4 j + g) ^ r = 16 (j >> 2) + 4 ((j & 3) ^ (r >> 2)) + (g ^ (r & 3)): four lane
     // offsets, the rest immediates
     if (p == 0) GFK_STAMP(m, 31);
+    if (p == NPH - 1) GFK_STAMP(m, 143);
     const float* xc = smem + (p & 1) * 64 * RS_KP + r * RS_KP + (g ^ (r & 3)) * 4;
     if (p + 1 < NPH) dma_x(p + 1, smem + ((p + 1) & 1) * 64 * RS_KP);
 #pragma unroll
@@ -571,6 +572,7 @@ __global__ void __launch_bounds__(RS_T) gfk_ctx_fwd_rs_k(GfkArgT<GB> ga) {
       bias[t][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_f, on && v < V ? ba_off + (uint32_t)v * 4u : OOB, 0, 0));
     }
   lds_barrier();                        // every wave done with the last phase's x
+  GFK_STAMP(m, 140);
   float* al = smem;                     // [64 b][RS_AL v], quads XOR (b & 15)
   float* sp = smem + 2 * 64 * RS_KP;    // [3][64 b][16 v] split-unit partials
   // A of unit ul (+ bias) into LDS and ws_actx
@@ -613,7 +615,9 @@ __global__ void __launch_bounds__(RS_T) gfk_ctx_fwd_rs_k(GfkArgT<GB> ga) {
     }
     put_a(nuf, a4, bias[1]);
   }
+  GFK_STAMP(m, 141);
   if (split) lds_barrier();
+  GFK_STAMP(m, 142);
   // ---- P^T[h, b] over the workgroup's 16 nu words: k steps v = 16 s + 4 g + i ----
   f32x4 pacc = z4;
   if (ht < NJT) {

@@ -106,6 +106,9 @@ def main(argv=None):
         # ring fill, C loop = the phases' MFMAs, A + P = the epilogue, of wave 0 of wg 0)
         print("ctx_fwd (wg 0) cycles: prologue", int(d[31] - d[30]), "| C loop", int(d[32] - d[31]),
               "| A + P", int(d[33] - d[32]))
+        print("ctx_fwd (wg 0) last phase", int(d[32] - d[143]), "| epilogue: first barrier",
+              int(d[140] - d[32]), "| A stores + barrier", int(d[141] - d[140]),
+              "| split sum", int(d[142] - d[141]), "| P", int(d[33] - d[142]))
         print("ctx_bwd (wg 0) cycles: staging", int(d[35] - d[34]), "| dA", int(d[36] - d[35]),
               "| g_ba + g_Wa", int(d[37] - d[36]), "| update", int(d[38] - d[37]))
     print("win_update (W_in tile 0) cycles: staging", int(d[41] - d[40]), "| mfma+update", int(d[42] - d[41]))
