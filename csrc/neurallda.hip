@@ -30,8 +30,11 @@ constexpr float RL_EPS = 1e-10f;
 constexpr int LBT = 1024;
 constexpr int LBW = LBT / 64;
 
-template <bool GB = false>
-__global__ void __launch_bounds__(LBT) gfk_lda_beta_fwd(GfkArgT<GB> ga) {
+// KM: the largest K compiled in (the beta tile's registers); the K <= 64 instance fits 64
+// VGPRs, so two workgroups share a CU (a batched launch of M clients' tiles in fewer rounds)
+template <bool GB = false, int KM = 256>
+__global__ void __launch_bounds__(LBT) __attribute__((amdgpu_waves_per_eu(KM <= 64 ? 8 : 1)))
+gfk_lda_beta_fwd(GfkArgT<GB> ga) {
   const GfkModel& m = gfk_model(ga);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int K = m.K, V = m.V, tid = threadIdx.x;
@@ -40,7 +43,7 @@ __global__ void __launch_bounds__(LBT) gfk_lda_beta_fwd(GfkArgT<GB> ga) {
   float* rows = rowm + K;
   for (int k = tid; k < K; k += LBT) { rowm[k] = -INFINITY; rows[k] = 0.f; }
   if (gfk_bx() == 0 && tid == 0) *m.nbt_beta += 1;
-  constexpr int BU = (256 * VB + LBT - 1) / LBT;      // K <= 256
+  constexpr int BU = (KM * VB + LBT - 1) / LBT;       // K <= KM
   const int c = tid >> 4, sub = tid & 15;             // BN: 16 lanes per column
   for (int tile = gfk_bx(); tile < m.n_tiles; tile += gridDim.x) {
     const int c0 = tile * VB, nv = min(VB, V - c0);
@@ -464,7 +467,10 @@ extern "C" size_t gfk_lda_bwd_smem(const GfkModel* m) {
 }
 
 extern "C" int gfk_launch_lda_beta_fwd(const GfkModel* m, hipStream_t s) {
-  do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_lda_beta_fwd<true>), gfk_grid(dim3(m->dec_grid), m), dim3(LBT), gfk_lda_fwd_smem(m->K), s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_lda_beta_fwd<false>), dim3(m->dec_grid), dim3(LBT), gfk_lda_fwd_smem(m->K), s, GfkArgT<false>{*m}); } while (0);
+  if (m->K <= 64)
+    do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_lda_beta_fwd<true, 64>), gfk_grid(dim3(m->dec_grid), m), dim3(LBT), gfk_lda_fwd_smem(m->K), s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_lda_beta_fwd<false, 64>), dim3(m->dec_grid), dim3(LBT), gfk_lda_fwd_smem(m->K), s, GfkArgT<false>{*m}); } while (0);
+  else
+    do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_lda_beta_fwd<true>), gfk_grid(dim3(m->dec_grid), m), dim3(LBT), gfk_lda_fwd_smem(m->K), s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_lda_beta_fwd<false>), dim3(m->dec_grid), dim3(LBT), gfk_lda_fwd_smem(m->K), s, GfkArgT<false>{*m}); } while (0);
   return (int)hipGetLastError();
 }
 
@@ -496,7 +502,8 @@ extern "C" int gfk_lda_set_smem(size_t bytes) {
   static size_t cur = 0;
   if (bytes <= cur) return 0;
   cur = bytes;
-  const void* ks[] = {(const void*)gfk_lda_beta_fwd<false>, (const void*)gfk_lda_beta_fwd<true>, (const void*)gfk_lda_beta_bwd_k<true>, (const void*)gfk_lda_beta_bwd_k<true, true>,
+  const void* ks[] = {(const void*)gfk_lda_beta_fwd<false>, (const void*)gfk_lda_beta_fwd<true>,
+                      (const void*)gfk_lda_beta_fwd<false, 64>, (const void*)gfk_lda_beta_fwd<true, 64>, (const void*)gfk_lda_beta_bwd_k<true>, (const void*)gfk_lda_beta_bwd_k<true, true>,
                       (const void*)gfk_lda_beta_bwd_k<false>, (const void*)gfk_lda_beta_bwd_k<false, true>,
                       (const void*)gfk_lda_beta_bwd_k<false, false, true>, (const void*)gfk_lda_beta_bwd_k<false, true, true>};
   for (const void* k : ks) {
