@@ -1604,6 +1604,29 @@ class BatchedSteps:
             # backward walking several tiles (profiles/r5/ab_batch.txt).
             if M > 1 and M * (mm.bmax + 1) > self._cu:
                 mm.stage_flags |= STAGE_POST_ROWS2
+            # CombinedTM: M clients' vocabulary tiles in one launch fill the CUs the way one
+            # client's do at a large vocabulary, so the batched launch takes that plan -- the
+            # forward with all batch rows per tile (each Wa block staged once) and the
+            # persistent pipelined backward -- once M n_tiles > 2 CUs (V = 5k, 8 clients:
+            # 0.5296 -> 0.5175 / 0.5137 ms each, profiles/r6/ctm_batched/).  The z0 partials
+            # keep the per-tile layout (no register-streamed forward here).
+            # GFEDNTM_CTX_FULL / GFEDNTM_CTX_BWDPP = 0: the engines' own plan.
+            if (M > 1 and mm.ctx_fused == 1 and mm.bmax <= 64 and int(mm.H[0]) <= 64
+                    and M * mm.n_tiles > 2 * self._cu):
+                ctx_new = False
+                if (not mm.stage_flags & STAGE_CTX_FULL
+                        and os.environ.get("GFEDNTM_CTX_FULL", "auto") == "auto"):
+                    mm.stage_flags |= STAGE_CTX_FULL
+                    ctx_new = True
+                if (not mm.stage_flags & STAGE_CTX_BWDPP
+                        and os.environ.get("GFEDNTM_CTX_BWDPP", "auto") == "auto"):
+                    mm.stage_flags |= STAGE_CTX_BWDPP
+                    mm.ctx_bgrid = int(self._cu)
+                    ctx_new = True
+                if ctx_new:                  # (the new kernels' dynamic-LDS limit)
+                    rc = e.lib.gfk_setup(C.byref(mm))
+                    if rc:
+                        raise RuntimeError(f"gfk_setup failed ({rc})")
             # win_update: all clients' W_in tiles in one launch -> the 8-wave tile shape once
             # they exceed two rounds of 16-wave workgroups
             if M * (mm.n_tiles + 8) > 2 * self._cu:

@@ -269,6 +269,42 @@ def test_batched_large_round_variants_match_branch_round(monkeypatch, strip):
                                    rtol=1e-6, atol=1e-3)
 
 
+def test_batched_ctm_takes_the_large_vocabulary_plan():
+    """CombinedTM, 8 clients at V ~ 5-10k (> 64 tiles each): the batched launch's 8 x n_tiles
+    vocabulary tiles exceed two rounds of the CUs, so it runs the large-vocabulary shapes
+    (stage bits 5 and 12: the forward with all batch rows per tile, the persistent
+    pipelined backward) that one client of this size does not use.  The round must agree
+    with the per-client branch round (the engines' own plan) within fp32 rounding."""
+    from gfedntm_amd.ops.engine import STAGE_CTX_BWDPP, STAGE_CTX_FULL, STAGE_CTX_RS
+    C = 64
+    sc = generate_synthetic(vocab_size=10000, n_topics=50, n_docs=1000, n_nodes=8, frozen_topics=2,
+                            nwords=(150, 250), seed=17)
+    rng = np.random.default_rng(17)
+    corpora = [ClientCorpus(synthetic=sc, node=i,
+                            embeddings=rng.standard_normal((sc.counts[i].shape[0], C)).astype(np.float32))
+               for i in range(8)]
+    kw = dict(model_type="ctm", device="cuda", backend="fused", seed=4)
+    p = _params(batch_size=64, n_components=20, contextual_size=C)
+    a = LocalFederation(corpora, p, max_iters=1, round_batched=True, **kw)
+    b = LocalFederation(corpora, p, max_iters=1, round_batched=False, **kw)
+    e = b.clients[0].tm.engine
+    assert not e._m.stage_flags & (STAGE_CTX_FULL | STAGE_CTX_BWDPP)    # one client's plan
+    a.run()
+    b.run()
+    host = a._batched._host
+    cu = torch.cuda.get_device_properties(0).multi_processor_count
+    assert 8 * host.n_tiles > 2 * cu, host.n_tiles
+    assert host.stage_flags & STAGE_CTX_FULL and host.stage_flags & STAGE_CTX_BWDPP
+    assert not host.stage_flags & STAGE_CTX_RS and host.ctx_bgrid == cu
+    lr = a.clients[0].tm.engine.lr
+    for x, y in zip(a.clients, b.clients):
+        diff = (x.tm.flat.buffer - y.tm.flat.buffer).abs()
+        assert float(diff.max()) <= 2.5 * lr
+        assert int((diff > 1e-5).sum()) <= 0.01 * diff.numel()
+        torch.testing.assert_close(x.tm.engine.loss_hist[:1], y.tm.engine.loss_hist[:1],
+                                   rtol=1e-5, atol=1e-2)
+
+
 @pytest.mark.parametrize("batched", [True, False])
 def test_multi_round_replays_are_bitwise_one_round_replays(monkeypatch, batched):
     """GFEDNTM_ROUNDS_PER_GRAPH: k rounds captured back to back in one graph (runs ending at
