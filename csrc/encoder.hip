@@ -444,6 +444,13 @@ extern "C" int gfk_launch_enc_in(const GfkModel* m, hipStream_t s) {
       hipLaunchKernelGGL((gfk_enc_in_k<true, false, 1>), dim3(m->bmax), dim3(ENC_THREADS), gfk_enc_in_smem(m), s, GfkArgT<false>{*m});
     return (int)hipGetLastError();
   }
+  if (m->H[0] <= 64) {                           // narrow, weights from L2 (large K plans)
+    if (m->n_batch > 1)
+      hipLaunchKernelGGL((gfk_enc_in_k<false, true, 1>), gfk_grid(dim3(m->bmax), m), dim3(ENC_THREADS), gfk_enc_in_smem(m), s, GfkArgT<true>{gfk_dev(m)});
+    else
+      hipLaunchKernelGGL((gfk_enc_in_k<false, false, 1>), dim3(m->bmax), dim3(ENC_THREADS), gfk_enc_in_smem(m), s, GfkArgT<false>{*m});
+    return (int)hipGetLastError();
+  }
   if (m->stage_flags & 1)
     do { if (m->n_batch > 1) hipLaunchKernelGGL((gfk_enc_in_k<true, true>), gfk_grid(dim3(m->bmax), m), dim3(ENC_THREADS), gfk_enc_in_smem(m), s, GfkArgT<true>{gfk_dev(m)}); else hipLaunchKernelGGL((gfk_enc_in_k<true, false>), dim3(m->bmax), dim3(ENC_THREADS), gfk_enc_in_smem(m), s, GfkArgT<false>{*m}); } while (0);
   else
@@ -459,7 +466,8 @@ extern "C" int gfk_enc_in_set_smem(size_t bytes) {
   cur = bytes;
   const void* ks[] = {(const void*)gfk_enc_in_k<true>, (const void*)gfk_enc_in_k<true, true>, (const void*)gfk_enc_in_k<false>, (const void*)gfk_enc_in_k<false, true>,
                       (const void*)gfk_enc_in_k<true, false, 1>,
-                      (const void*)gfk_enc_in_k<true, true, 1>};
+                      (const void*)gfk_enc_in_k<true, true, 1>, (const void*)gfk_enc_in_k<false, false, 1>,
+                      (const void*)gfk_enc_in_k<false, true, 1>};
   for (const void* k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e != hipSuccess) return (int)e;
