@@ -1590,6 +1590,16 @@ class BatchedSteps:
                     and os.environ.get("GFEDNTM_BATCH_STRIP", "fill") != "keep"):
                 t = next((t for t in (1, 2, 3, 4) if M * -(-mm.n_tiles // t) <= self._cu), None)
                 mm.dec_grid = -(-mm.n_tiles // t) if t else max(1, self._cu // M)
+            # NeuralLDA's decoder kernels (beta forward / backward, grid-strided over the
+            # tiles) likewise: T tiles per workgroup so the M clients' workgroups fit one
+            # round of the CUs -- the backward's theta_d staging is then paid once per T
+            # tiles (8 clients, V = 4.7k: 0.1426 -> 0.1407 ms, same bits; one round of two
+            # workgroups per CU measured 0.1497, profiles/r6/lda/ab_batch_fill.txt).
+            # GFEDNTM_BATCH_STRIP=keep: the engines' own grids here too.
+            if (mm.kind == abi.KIND_LDA and M > 1 and M * mm.dec_grid > self._cu
+                    and os.environ.get("GFEDNTM_BATCH_STRIP", "fill") != "keep"):
+                t = next((t for t in (1, 2, 3, 4) if M * -(-mm.n_tiles // t) <= self._cu), None)
+                mm.dec_grid = -(-mm.n_tiles // t) if t else max(1, self._cu // M)
             # the posterior folded into the strip forward for M > 1 clients (the engines' own
             # plan keeps post_fwd for one client; GFEDNTM_POSTFOLD=0: never)
             if (M > 1 and getattr(e, "_fold_ok", False) and mm.stage_flags & STAGE_FWD_STRIP

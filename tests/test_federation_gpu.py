@@ -305,6 +305,39 @@ def test_batched_ctm_takes_the_large_vocabulary_plan():
                                    rtol=1e-5, atol=1e-2)
 
 
+@pytest.mark.parametrize("strip", ["fill", "keep"])
+def test_batched_lda_decoder_grid_fill(monkeypatch, strip):
+    """NeuralLDA, 8 clients at the headline's vocabulary: the batched launch gives each
+    decoder workgroup T tiles so the 8 clients' workgroups fit one round of the CUs ("fill",
+    the default; "keep": the engines' own grids).  Either way the round agrees with the
+    per-client branch round within fp32 rounding."""
+    monkeypatch.setenv("GFEDNTM_BATCH_STRIP", strip)
+    sc = generate_synthetic(vocab_size=5000, n_topics=50, n_docs=1000, n_nodes=8, frozen_topics=5,
+                            nwords=(150, 250), seed=13)
+    corpora = [ClientCorpus(synthetic=sc, node=i) for i in range(8)]
+    kw = dict(device="cuda", backend="fused", seed=4)
+    p = _params(model_type="LDA", batch_size=64, n_components=50)
+    a = LocalFederation(corpora, p, max_iters=1, round_batched=True, **kw)
+    b = LocalFederation(corpora, p, max_iters=1, round_batched=False, **kw)
+    a.run()
+    b.run()
+    host = a._batched._host
+    own = b.clients[0].tm.engine._m.dec_grid
+    cu = torch.cuda.get_device_properties(0).multi_processor_count
+    if strip == "fill" and 8 * own > cu:
+        t = next((t for t in (1, 2, 3, 4) if 8 * -(-host.n_tiles // t) <= cu), None)
+        assert host.dec_grid == (-(-host.n_tiles // t) if t else max(1, cu // 8))
+    else:
+        assert host.dec_grid == own
+    lr = a.clients[0].tm.engine.lr
+    for x, y in zip(a.clients, b.clients):
+        diff = (x.tm.flat.buffer - y.tm.flat.buffer).abs()
+        assert float(diff.max()) <= 2.5 * lr
+        assert int((diff > 1e-5).sum()) <= 0.01 * diff.numel()
+        torch.testing.assert_close(x.tm.engine.loss_hist[:1], y.tm.engine.loss_hist[:1],
+                                   rtol=1e-6, atol=1e-3)
+
+
 @pytest.mark.parametrize("batched", [True, False])
 def test_multi_round_replays_are_bitwise_one_round_replays(monkeypatch, batched):
     """GFEDNTM_ROUNDS_PER_GRAPH: k rounds captured back to back in one graph (runs ending at
